@@ -1,0 +1,44 @@
+# Build for MI355X (gfx950).  `make` builds the product library and the CPU
+# oracle; __graft_entry__.build() runs it.  Outputs stay in-tree (git-ignored)
+# so they travel to the GPU box with the snapshot.
+HIPCC     ?= /opt/rocm/bin/hipcc
+ARCH      ?= gfx950
+CXX       ?= g++
+CC        ?= gcc
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -Wall -Wno-unused-result
+CXXFLAGS  := -O3 -std=c++17 -fPIC -fopenmp -Iinclude -Wall
+CFLAGS    := -O2 -std=c11 -fPIC -fopenmp -Wall -D_GNU_SOURCE
+
+PKG       := dag_rider_amd
+LIB       := $(PKG)/libdagrider_gpu.so
+ORACLE    := oracle/liboracle.so
+BUILD     := build
+
+.PHONY: all lib oracle clean tests-cpp
+all: lib oracle tests-cpp
+
+lib: $(LIB)
+oracle: $(ORACLE)
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+$(BUILD)/dag_gen.o: $(PKG)/csrc/dag_gen.cpp include/dagrider_gen.h | $(BUILD)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp include/dagrider_gpu.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/engine.o $(BUILD)/dag_gen.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -Wl,-soname,libdagrider_gpu.so
+
+$(ORACLE): oracle/ref_literal.c oracle/ref_bitset.c oracle/oracle.h
+	$(CC) $(CFLAGS) -shared -o $@ oracle/ref_literal.c oracle/ref_bitset.c
+
+# C++ host mirror of process.Process over the C ABI + its TestPath port
+tests-cpp: $(BUILD)/process_internal_test
+$(BUILD)/process_internal_test: tests/cpp/process_internal_test.cpp $(PKG)/host/process.hpp include/dagrider_gpu.h $(LIB) | $(BUILD)
+	$(CXX) -O2 -std=c++17 -Iinclude -I$(PKG)/host $< -o $@ -L$(PKG) -ldagrider_gpu -Wl,-rpath,'$$ORIGIN/../$(PKG)'
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(ORACLE)

@@ -1,0 +1,90 @@
+"""ctypes binding of libdagrider_gpu.so (C ABI: include/dagrider_gpu.h, include/dagrider_gen.h).
+
+The library is built in-tree by ``make`` / ``__graft_entry__.build()``.  There is no
+fallback: if it is missing, importing anything that needs it raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdagrider_gpu.so")
+
+DR_OK, DR_E_INVAL, DR_E_CAPACITY, DR_E_HIP, DR_E_RCCL, DR_E_CONTRACT, DR_E_STATE = 0, -1, -2, -3, -4, -5, -6
+DR_CHAIN_LITERAL, DR_CHAIN_PERSISTENT = 0, 1
+DR_DELIVER_REF, DR_DELIVER_PAPER = 0, 1
+
+P = C.c_void_p
+i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float
+
+
+class GenParams(C.Structure):
+    _fields_ = [("n", i32), ("last_round", i32), ("seed", u64), ("p_present", C.c_double),
+                ("p_late", C.c_double), ("p_w", C.c_double), ("p_la", C.c_double),
+                ("weak_depth", i32), ("nthreads", i32)]
+
+
+class ReplayOut(C.Structure):
+    _fields_ = [("commit", P), ("vcount", P), ("push_off", P), ("push_wave", P), ("push_cap", i64),
+                ("pop_count", P), ("pop_digest", P), ("pop_edges", P), ("ids", P), ("ids_cap", i64),
+                ("n_push", i64), ("n_ids", i64), ("commit_edges", u64), ("chain_edges", u64),
+                ("deliver_edges", u64), ("ms_commit", f32), ("ms_chain", f32), ("ms_deliver", f32),
+                ("ms_emit", f32), ("sweep_weak_edges", u64), ("sweep_count", u64), ("sweep_rounds", u64),
+                ("sweep_vertices", u64)]
+
+
+# symbol -> (restype, argtypes); every symbol declared in include/*.h
+SIGNATURES = {
+    "dr_abi_version": (C.c_int, []),
+    "dr_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)]),
+    "dr_destroy": (None, [P]),
+    "dr_last_error": (C.c_char_p, [P]),
+    "dr_num_rounds": (C.c_int, [P]),
+    "dr_append_rounds_lists": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
+    "dr_append_rounds_packed": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
+    "dr_path_batch": (C.c_int, [P, C.c_int, P, P, C.c_int, P]),
+    "dr_reach_sets": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "dr_wave_commit": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "dr_wave_ready": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, C.POINTER(C.c_int)]),
+    "dr_order_vertices": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, C.c_size_t,
+                                    C.POINTER(C.c_size_t), P, P]),
+    "dr_replay": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
+    "dr_gen_create": (C.c_int, [C.POINTER(GenParams), C.POINTER(P)]),
+    "dr_gen_free": (None, [P]),
+    "dr_gen_info": (C.c_int, [P, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(u64),
+                              C.POINTER(u64)]),
+    "dr_gen_slot_off": (P, [P]),
+    "dr_gen_slot_src": (P, [P]),
+    "dr_gen_strong": (P, [P]),
+    "dr_gen_weak_off": (P, [P]),
+    "dr_gen_weak_tgt": (P, [P]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
+                               "there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class DrError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def ptr(a):
+    """numpy array -> void* (None passes NULL)."""
+    return None if a is None else a.ctypes.data_as(P)

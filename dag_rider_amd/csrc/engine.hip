@@ -1,0 +1,1013 @@
+// engine.hip -- host side of the C ABI (include/dagrider_gpu.h): the device
+// mirror of Process.dag, validation, kernel orchestration.
+//
+// One dr_ctx per reference Process.  The DAG lives in HBM in the packed layout
+// of kernels.hpp; host keeps only slot lists, presence bits and per-round
+// degree sums (for leader lookups, emission bounds and edge accounting).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dagrider_gpu.h"
+#include "kernels.hpp"
+
+using dr::u64;
+
+namespace {
+
+thread_local std::string g_create_err;
+
+int next_pow2(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t c = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipMalloc(&p, c);
+    if (e == hipSuccess) cap = c;
+    return e;
+  }
+  // grow keeping the first `keep` bytes
+  hipError_t grow(size_t bytes, size_t keep, hipStream_t s) {
+    if (bytes <= cap) return hipSuccess;
+    size_t c = std::max<size_t>({bytes, cap * 2, 4096});
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, c);
+    if (e != hipSuccess) return e;
+    if (p && keep) {
+      e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) { (void)hipFree(q); return e; }
+    }
+    if (p) (void)hipFree(p);
+    p = q;
+    cap = c;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+}  // namespace
+
+struct dr_ctx {
+  int n = 0, f = 0, W = 0, WS = 0, max_rounds = 0, dev = 0;
+  int nrounds = 0;
+  int dmax_near = 1;  // largest weak delta stored in the near format
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+  // device DAG
+  DevBuf strong, present, slot_off, slot_src, weak, weak_roff, far, far_roff;
+  size_t nweak = 0, nfar = 0;
+  // host mirrors
+  std::vector<uint32_t> h_slot_off{0};
+  std::vector<uint16_t> h_slot_src;
+  std::vector<u64> h_present;
+  std::vector<uint64_t> h_deg;  // total strong degree per round
+  std::vector<uint32_t> h_weak_roff{0}, h_far_roff{0};
+  // scratch
+  DevBuf q_buf, masks, dlv, push_out, push_n, edges, wedges, hits, commit, vcount, popdesc, rbase, counts,
+      digest, pop_pos, ids;
+  std::string err;
+  int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+  dr::DagView view() const {
+    dr::DagView v;
+    v.strong = strong.as<u64>();
+    v.present = present.as<u64>();
+    v.weak = weak.as<uint32_t>();
+    v.weak_roff = weak_roff.as<uint32_t>();
+    v.far = far.as<u64>();
+    v.far_roff = far_roff.as<uint32_t>();
+    v.n = n;
+    v.nrounds = nrounds;
+    return v;
+  }
+  bool is_present(int r, int s /*1-based*/) const {
+    if (r < 0 || r >= nrounds || s < 1 || s > n) return false;
+    return (h_present[(size_t)r * WS + ((s - 1) >> 6)] >> ((s - 1) & 63)) & 1ULL;
+  }
+  int depth_log2() const {
+    int need = next_pow2(std::max(2, dmax_near + 1));
+    int cap_words = (65536 - 64) / 8 - 2 * WS;
+    int cap = 1;
+    while (cap * 2 * WS <= cap_words) cap *= 2;
+    int d = std::min(need, cap);
+    int l = 0;
+    while ((1 << l) < d) l++;
+    return l;
+  }
+  size_t sweep_lds(int dl) const { return (size_t)(2 * WS + (1 << dl) * WS) * 8 + 32; }
+};
+
+#define HIPCHK(ctx, call)                                                                   \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return (ctx)->fail(DR_E_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),   \
+                         __FILE__, __LINE__);                                               \
+  } while (0)
+
+namespace {
+
+template <int WS>
+constexpr int block_for() {
+  return WS == 1 ? 64 : WS == 2 ? 128 : WS == 4 ? 256 : WS == 8 ? 512 : 1024;
+}
+
+// ---- kernel launch dispatch over the row stride ----
+template <int WS>
+hipError_t launch_commit_t(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc) {
+  constexpr int NT = block_for<WS>();
+  hipLaunchKernelGGL((dr::k_commit<WS, NT>), dim3(nw), dim3(NT), 0, c->stream, c->view(), w0, nw,
+                     2 * c->f + 1, cm, vc);
+  return hipGetLastError();
+}
+hipError_t launch_commit(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc) {
+  switch (c->WS) {
+    case 1: return launch_commit_t<1>(c, w0, nw, cm, vc);
+    case 2: return launch_commit_t<2>(c, w0, nw, cm, vc);
+    case 4: return launch_commit_t<4>(c, w0, nw, cm, vc);
+    case 8: return launch_commit_t<8>(c, w0, nw, cm, vc);
+    case 16: return launch_commit_t<16>(c, w0, nw, cm, vc);
+    case 32: return launch_commit_t<32>(c, w0, nw, cm, vc);
+  }
+  return hipErrorInvalidValue;
+}
+
+struct SweepArgs {
+  const dr::SweepQuery *q;
+  int nq, seq;
+  u64 *masks, *dlv;
+  int32_t *push_out, *push_n;
+  u64 *edges, *wedges;
+  uint8_t *hits;
+};
+
+template <int WS>
+hipError_t launch_sweep_t(dr_ctx *c, const SweepArgs &a) {
+  constexpr int NT = block_for<WS>();
+  const int dl = c->depth_log2();
+  const size_t lds = c->sweep_lds(dl);
+  hipError_t e = hipFuncSetAttribute((const void *)dr::k_sweep<WS, NT>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_sweep<WS, NT>), dim3(a.seq ? 1 : a.nq), dim3(NT), lds, c->stream,
+                     c->view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out, a.push_n,
+                     a.edges, a.wedges, a.hits);
+  return hipGetLastError();
+}
+hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a) {
+  if (a.nq <= 0) return hipSuccess;
+  switch (c->WS) {
+    case 1: return launch_sweep_t<1>(c, a);
+    case 2: return launch_sweep_t<2>(c, a);
+    case 4: return launch_sweep_t<4>(c, a);
+    case 8: return launch_sweep_t<8>(c, a);
+    case 16: return launch_sweep_t<16>(c, a);
+    case 32: return launch_sweep_t<32>(c, a);
+  }
+  return hipErrorInvalidValue;
+}
+
+constexpr int kEmitRPB = 16;
+
+template <int WS>
+hipError_t launch_emit_t(dr_ctx *c, int npop, int max_rounds_span, const dr::PopDesc *pd,
+                         u64 *cnt, u64 *dg, const int64_t *pos, int32_t *ids, int64_t cap,
+                         bool count_phase) {
+  if (count_phase) {
+    hipLaunchKernelGGL((dr::k_emit_count<WS, 256>), dim3(npop), dim3(256), 0, c->stream, c->view(),
+                       pd, c->masks.as<u64>(), c->rbase.as<uint32_t>(), cnt);
+  } else {
+    const int bx = std::max(1, (max_rounds_span + kEmitRPB - 1) / kEmitRPB);
+    hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(bx, npop), dim3(256), 0, c->stream,
+                       c->view(), c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd,
+                       c->masks.as<u64>(), c->rbase.as<uint32_t>(), pos, dg, ids, cap);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_emit(dr_ctx *c, int npop, int span, const dr::PopDesc *pd, u64 *cnt, u64 *dg,
+                       const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase) {
+  if (npop <= 0) return hipSuccess;
+  switch (c->WS) {
+    case 1: return launch_emit_t<1>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
+    case 2: return launch_emit_t<2>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
+    case 4: return launch_emit_t<4>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
+    case 8: return launch_emit_t<8>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
+    case 16: return launch_emit_t<16>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
+    case 32: return launch_emit_t<32>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
+  }
+  return hipErrorInvalidValue;
+}
+
+int set_device(dr_ctx *c) {
+  hipError_t e = hipSetDevice(c->dev);
+  if (e != hipSuccess) return c->fail(DR_E_HIP, "hipSetDevice(%d): %s", c->dev, hipGetErrorString(e));
+  return DR_OK;
+}
+
+template <class T>
+int h2d(dr_ctx *c, DevBuf &b, const std::vector<T> &v) {
+  HIPCHK(c, b.ensure(std::max<size_t>(v.size(), 1) * sizeof(T)));
+  if (!v.empty())
+    HIPCHK(c, hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return DR_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// lifecycle
+// ===========================================================================
+extern "C" int dr_abi_version(void) { return DR_ABI_VERSION; }
+
+extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx **out) {
+  if (!out) return DR_E_INVAL;
+  *out = nullptr;
+  if (n < 1 || n > 2048 || faulty < 0 || max_rounds < 1 || max_rounds > (1 << 20) || device < 0) {
+    g_create_err = "dr_create: n must be in [1,2048], faulty >= 0, max_rounds in [1,2^20], device >= 0";
+    return DR_E_INVAL;
+  }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || device >= ndev) {
+    g_create_err = std::string("dr_create: no usable HIP device (") +
+                   (e != hipSuccess ? hipGetErrorString(e) : "ordinal out of range") +
+                   "); this library has no CPU fallback";
+    return DR_E_HIP;
+  }
+  dr_ctx *c = new dr_ctx();
+  c->n = n;
+  c->f = faulty;
+  c->W = (n + 63) / 64;
+  c->WS = next_pow2(c->W);
+  c->max_rounds = max_rounds;
+  c->dev = device;
+  if (set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    g_create_err = "dr_create: stream creation failed";
+    delete c;
+    return DR_E_HIP;
+  }
+  for (auto &ev : c->ev) (void)hipEventCreate(&ev);
+  const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64);
+  if (c->strong.ensure(rows) != hipSuccess ||
+      c->present.ensure((size_t)max_rounds * c->WS * sizeof(u64)) != hipSuccess ||
+      c->slot_off.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
+      c->weak_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
+      c->far_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
+      c->weak.ensure(4096) != hipSuccess || c->far.ensure(4096) != hipSuccess ||
+      c->slot_src.ensure(4096) != hipSuccess) {
+    g_create_err = "dr_create: device allocation failed";
+    dr_destroy(c);
+    return DR_E_HIP;
+  }
+  uint32_t zero = 0;
+  (void)hipMemcpy(c->slot_off.p, &zero, 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(c->weak_roff.p, &zero, 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(c->far_roff.p, &zero, 4, hipMemcpyHostToDevice);
+  *out = c;
+  return DR_OK;
+}
+
+extern "C" void dr_destroy(dr_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->dev);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  DevBuf *bufs[] = {&c->strong,  &c->present, &c->slot_off, &c->slot_src, &c->weak,
+                    &c->weak_roff, &c->far,   &c->far_roff, &c->q_buf,    &c->masks,
+                    &c->dlv,     &c->push_out, &c->push_n,  &c->edges,    &c->hits, &c->wedges,
+                    &c->commit,  &c->vcount,  &c->popdesc,  &c->rbase,    &c->counts,
+                    &c->digest,  &c->pop_pos, &c->ids};
+  for (DevBuf *b : bufs) b->release();
+  for (auto &ev : c->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" const char *dr_last_error(const dr_ctx *c) {
+  return c ? c->err.c_str() : g_create_err.c_str();
+}
+
+extern "C" int dr_num_rounds(const dr_ctx *c) { return c ? c->nrounds : -1; }
+
+// ===========================================================================
+// DAG append (validation + packing)
+// ===========================================================================
+extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t *slot_off,
+                                       const uint16_t *slot_src, const uint64_t *strong,
+                                       const uint32_t *weak_off, const uint32_t *weak_tgt) {
+  if (!c) return DR_E_INVAL;
+  if (int rc = set_device(c)) return rc;
+  if (r0 != c->nrounds) return c->fail(DR_E_STATE, "append at round %d but %d rounds mirrored", r0, c->nrounds);
+  if (k < 0 || r0 + k > c->max_rounds) return c->fail(DR_E_INVAL, "append of %d rounds exceeds max_rounds %d", k, c->max_rounds);
+  if (k == 0) return DR_OK;
+  if (!slot_off || !slot_src || !strong || !weak_off) return c->fail(DR_E_INVAL, "null array");
+  const int n = c->n, W = c->W, WS = c->WS;
+  std::vector<u64> pres((size_t)k * WS, 0);
+  std::vector<uint64_t> deg(k, 0);
+  std::vector<uint32_t> wdev, wroff(k);
+  std::vector<u64> fdev;
+  std::vector<uint32_t> froff(k);
+  int dmax = c->dmax_near;
+  const u64 lastmask = (n % 64) ? ((1ULL << (n % 64)) - 1ULL) : ~0ULL;
+  for (int i = 0; i < k; i++) {
+    const int r = r0 + i;
+    u64 *P = &pres[(size_t)i * WS];
+    for (uint32_t sl = slot_off[i]; sl < slot_off[i + 1]; sl++) {
+      const int s = slot_src[sl];
+      if (s > n) return c->fail(DR_E_CONTRACT, "round %d slot %u: source %d > n=%d", r, sl - slot_off[i], s, n);
+      if (s == 0) continue;  // ghost slot {0,0}
+      u64 &wd = P[(s - 1) >> 6];
+      const u64 bit = 1ULL << ((s - 1) & 63);
+      if ((wd & bit) && r >= 1) return c->fail(DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, s);
+      wd |= bit;
+    }
+    wroff[i] = (uint32_t)wdev.size();
+    froff[i] = (uint32_t)fdev.size();
+    for (int s0 = 0; s0 < n; s0++) {
+      const bool here = (P[s0 >> 6] >> (s0 & 63)) & 1ULL;
+      const uint64_t *row = strong + ((size_t)i * n + s0) * W;
+      uint64_t d = 0;
+      bool nz = false;
+      for (int w = 0; w < W; w++) { d += (uint64_t)__builtin_popcountll(row[w]); nz |= row[w] != 0; }
+      if (nz && !here) return c->fail(DR_E_CONTRACT, "round %d: strong edges on absent vertex (%d,%d)", r, r, s0 + 1);
+      if (nz && r == 0) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", s0 + 1);
+      if (row[W - 1] & ~lastmask) return c->fail(DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
+      deg[i] += d;
+      const uint32_t ea = weak_off[(size_t)i * n + s0], eb = weak_off[(size_t)i * n + s0 + 1];
+      if (eb < ea) return c->fail(DR_E_INVAL, "weak_off not monotone at round %d", r);
+      if (eb > ea && !here) return c->fail(DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1);
+      for (uint32_t e = ea; e < eb; e++) {
+        const uint32_t t = weak_tgt[e];
+        const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
+        if (ts >= n) return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): source > n", r, s0 + 1, tr, ts + 1);
+        if (tr > r - 2) return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target a round < r-1", r, s0 + 1, tr, ts + 1);
+        const int delta = r - tr;
+        if (delta <= 1023) {
+          wdev.push_back(((uint32_t)delta << 22) | ((uint32_t)s0 << 11) | (uint32_t)ts);
+          dmax = std::max(dmax, delta);
+        } else {
+          fdev.push_back(((u64)s0 << 32) | t);
+        }
+      }
+    }
+  }
+  // ---- commit to device ----
+  const size_t row_words = (size_t)n * WS;
+  if (WS == W) {
+    HIPCHK(c, hipMemcpyAsync(c->strong.as<u64>() + (size_t)r0 * row_words, strong,
+                             (size_t)k * row_words * 8, hipMemcpyHostToDevice, c->stream));
+  } else {
+    std::vector<u64> pad((size_t)k * row_words, 0);
+    for (size_t v = 0; v < (size_t)k * n; v++)
+      std::memcpy(&pad[v * WS], strong + v * W, (size_t)W * 8);
+    HIPCHK(c, hipMemcpyAsync(c->strong.as<u64>() + (size_t)r0 * row_words, pad.data(), pad.size() * 8,
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  HIPCHK(c, hipMemcpyAsync(c->present.as<u64>() + (size_t)r0 * WS, pres.data(), pres.size() * 8,
+                           hipMemcpyHostToDevice, c->stream));
+  // slots
+  const size_t old_slots = c->h_slot_src.size();
+  const uint32_t add_slots = slot_off[k] - slot_off[0];
+  HIPCHK(c, c->slot_src.grow((old_slots + add_slots) * 2 + 64, old_slots * 2, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->slot_src.as<uint16_t>() + old_slots, slot_src + slot_off[0],
+                           (size_t)add_slots * 2, hipMemcpyHostToDevice, c->stream));
+  // weak
+  HIPCHK(c, c->weak.grow((c->nweak + wdev.size()) * 4 + 64, c->nweak * 4, c->stream));
+  if (!wdev.empty())
+    HIPCHK(c, hipMemcpyAsync(c->weak.as<uint32_t>() + c->nweak, wdev.data(), wdev.size() * 4,
+                             hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, c->far.grow((c->nfar + fdev.size()) * 8 + 64, c->nfar * 8, c->stream));
+  if (!fdev.empty())
+    HIPCHK(c, hipMemcpyAsync(c->far.as<u64>() + c->nfar, fdev.data(), fdev.size() * 8,
+                             hipMemcpyHostToDevice, c->stream));
+  // host mirrors + offsets
+  for (int i = 0; i < k; i++) {
+    c->h_slot_off.push_back(c->h_slot_off.back() + (slot_off[i + 1] - slot_off[i]));
+    c->h_weak_roff.push_back((uint32_t)(c->nweak + (i + 1 < k ? wroff[i + 1] : wdev.size())));
+    c->h_far_roff.push_back((uint32_t)(c->nfar + (i + 1 < k ? froff[i + 1] : fdev.size())));
+  }
+  c->h_slot_src.insert(c->h_slot_src.end(), slot_src + slot_off[0], slot_src + slot_off[k]);
+  c->h_present.insert(c->h_present.end(), pres.begin(), pres.end());
+  c->h_deg.insert(c->h_deg.end(), deg.begin(), deg.end());
+  HIPCHK(c, hipMemcpyAsync(c->slot_off.as<uint32_t>() + r0 + 1, &c->h_slot_off[r0 + 1], (size_t)k * 4,
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->weak_roff.as<uint32_t>() + r0 + 1, &c->h_weak_roff[r0 + 1], (size_t)k * 4,
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->far_roff.as<uint32_t>() + r0 + 1, &c->h_far_roff[r0 + 1], (size_t)k * 4,
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->nweak += wdev.size();
+  c->nfar += fdev.size();
+  c->dmax_near = dmax;
+  c->nrounds += k;
+  return DR_OK;
+}
+
+extern "C" int dr_append_rounds_lists(dr_ctx *c, int r0, int k, const uint32_t *slot_off,
+                                      const int32_t *slot_id, const uint32_t *strong_off,
+                                      const int32_t *strong_ids, const uint32_t *weak_off,
+                                      const int32_t *weak_ids) {
+  if (!c) return DR_E_INVAL;
+  if (k < 0) return c->fail(DR_E_INVAL, "negative round count");
+  if (k == 0) return DR_OK;
+  if (!slot_off || !slot_id || !strong_off || !weak_off) return c->fail(DR_E_INVAL, "null array");
+  const int n = c->n, W = c->W;
+  const uint32_t S0 = slot_off[0], S1 = slot_off[k];
+  std::vector<uint32_t> so(k + 1);
+  std::vector<uint16_t> src(S1 - S0);
+  std::vector<uint64_t> rows((size_t)k * n * W, 0);
+  std::vector<std::vector<uint32_t>> wl((size_t)k * n);
+  for (int i = 0; i <= k; i++) so[i] = slot_off[i] - S0;
+  for (int i = 0; i < k; i++) {
+    const int r = r0 + i;
+    for (uint32_t sl = slot_off[i]; sl < slot_off[i + 1]; sl++) {
+      const int vr = slot_id[2 * sl], vs = slot_id[2 * sl + 1];
+      const uint32_t sa = strong_off[sl], sb = strong_off[sl + 1];
+      const uint32_t wa = weak_off[sl], wb = weak_off[sl + 1];
+      if (vr == 0 && vs == 0) {  // ghost slot: zero vertexID (process_internal_test.go:89-100)
+        if (sb != sa || wb != wa) return c->fail(DR_E_CONTRACT, "round %d: ghost slot {0,0} with edges", r);
+        src[sl - S0] = 0;
+        continue;
+      }
+      if (vr != r || vs < 1 || vs > n)
+        return c->fail(DR_E_CONTRACT, "round %d slot %u: id (%d,%d) outside the mirrored contract", r, sl - slot_off[i], vr, vs);
+      src[sl - S0] = (uint16_t)vs;
+      uint64_t *row = &rows[((size_t)i * n + (vs - 1)) * W];
+      for (uint32_t e = sa; e < sb; e++) {
+        const int tr = strong_ids[2 * e], ts = strong_ids[2 * e + 1];
+        if (tr != r - 1 || ts < 1 || ts > n)
+          return c->fail(DR_E_CONTRACT, "strong edge (%d,%d)->(%d,%d) must target round r-1, source in [1,n]", r, vs, tr, ts);
+        row[(ts - 1) >> 6] |= 1ULL << ((ts - 1) & 63);
+      }
+      std::vector<uint32_t> &L = wl[(size_t)i * n + (vs - 1)];
+      if (!L.empty() || (wb > wa && false)) {}
+      for (uint32_t e = wa; e < wb; e++) {
+        const int tr = weak_ids[2 * e], ts = weak_ids[2 * e + 1];
+        if (tr < 0 || tr > r - 2 || ts < 1 || ts > n)
+          return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target round < r-1, source in [1,n]", r, vs, tr, ts);
+        L.push_back(((uint32_t)tr << 11) | (uint32_t)(ts - 1));
+      }
+    }
+  }
+  std::vector<uint32_t> woff((size_t)k * n + 1, 0);
+  std::vector<uint32_t> wt;
+  for (size_t v = 0; v < (size_t)k * n; v++) {
+    woff[v] = (uint32_t)wt.size();
+    wt.insert(wt.end(), wl[v].begin(), wl[v].end());
+  }
+  woff[(size_t)k * n] = (uint32_t)wt.size();
+  return dr_append_rounds_packed(c, r0, k, so.data(), src.data(), rows.data(), woff.data(), wt.data());
+}
+
+// ===========================================================================
+// queries
+// ===========================================================================
+namespace {
+
+// Run sweep queries in batches bounded by the mask budget.  qv: queries with
+// mask_off left relative (filled here per batch when Q_MASKS).  On return the
+// per-query edges / hits / pushes are in host arrays.  If keep_masks, each
+// batch's masks are handed to `on_batch` before the next batch overwrites them.
+template <class OnBatch>
+int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector<uint64_t> *edges,
+               std::vector<uint64_t> *wedges, std::vector<uint8_t> *hits, std::vector<int32_t> *push_n, int32_t *push_out_dev,
+               OnBatch on_batch, float *ms) {
+  const size_t budget_words = (size_t)1 << 29;  // 4 GiB of frontier masks per batch
+  const int WS = c->WS;
+  if (edges) edges->assign(qv.size(), 0);
+  if (wedges) wedges->assign(qv.size(), 0);
+  if (hits) hits->assign(qv.size(), 0);
+  if (push_n) push_n->assign(qv.size(), 0);
+  size_t i0 = 0;
+  float total_ms = 0;
+  while (i0 < qv.size()) {
+    // batch [i0, i1): as many queries as the mask budget allows (sequential
+    // mode keeps its order across batches: the delivered set persists)
+    size_t i1 = i0, words = 0;
+    while (i1 < qv.size()) {
+      const size_t w = (qv[i1].flags & dr::Q_MASKS) ? (size_t)(qv[i1].top - qv[i1].bottom + 1) * WS : 0;
+      if (i1 > i0 && words + w > budget_words) break;
+      qv[i1].mask_off = (int64_t)words;
+      words += w;
+      i1++;
+    }
+    const int nq = (int)(i1 - i0);
+    HIPCHK(c, c->masks.ensure(std::max<size_t>(words, 1) * 8));
+    if (words) HIPCHK(c, hipMemsetAsync(c->masks.p, 0, words * 8, c->stream));
+    HIPCHK(c, c->q_buf.ensure((size_t)nq * sizeof(dr::SweepQuery)));
+    HIPCHK(c, hipMemcpyAsync(c->q_buf.p, qv.data() + i0, (size_t)nq * sizeof(dr::SweepQuery),
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->edges.ensure((size_t)nq * 8));
+    HIPCHK(c, c->wedges.ensure((size_t)nq * 8));
+    HIPCHK(c, c->hits.ensure((size_t)nq));
+    HIPCHK(c, c->push_n.ensure((size_t)nq * 4));
+    SweepArgs a;
+    a.q = c->q_buf.as<dr::SweepQuery>();
+    a.nq = nq;
+    a.seq = seq ? 1 : 0;
+    a.masks = c->masks.as<u64>();
+    a.dlv = c->dlv.as<u64>();
+    a.push_out = push_out_dev;
+    a.push_n = c->push_n.as<int32_t>();
+    a.edges = c->edges.as<u64>();
+    a.wedges = c->wedges.as<u64>();
+    a.hits = c->hits.as<uint8_t>();
+    HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(c, launch_sweep(c, a));
+    HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    if (edges) HIPCHK(c, hipMemcpyAsync(edges->data() + i0, c->edges.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    if (wedges) HIPCHK(c, hipMemcpyAsync(wedges->data() + i0, c->wedges.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    if (hits) HIPCHK(c, hipMemcpyAsync(hits->data() + i0, c->hits.p, (size_t)nq, hipMemcpyDeviceToHost, c->stream));
+    if (push_n) HIPCHK(c, hipMemcpyAsync(push_n->data() + i0, c->push_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float t = 0;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[1]));
+    total_ms += t;
+    if (int rc = on_batch(i0, i1)) return rc;
+    i0 = i1;
+  }
+  if (ms) *ms = total_ms;
+  return DR_OK;
+}
+
+// Emission for pops whose masks (round 0 at pd[i].mask_off) are resident.
+// counts/digests per pop to host; ids (optional) at global positions pos0 + ...
+int run_emit(dr_ctx *c, const std::vector<dr::PopDesc> &pd, uint64_t *count_out, uint64_t *digest_out,
+             int32_t *ids_host, int64_t ids_cap, int64_t ids_base, int64_t *ids_total, float *ms) {
+  const int np = (int)pd.size();
+  if (np == 0) return DR_OK;
+  int64_t rb_words = 0;
+  int span = 0;
+  for (const auto &d : pd) {
+    rb_words = std::max<int64_t>(rb_words, d.rbase_off + d.last + 1);
+    span = std::max(span, d.last - d.first + 1);
+  }
+  HIPCHK(c, c->rbase.ensure((size_t)std::max<int64_t>(rb_words, 1) * 4));
+  HIPCHK(c, c->popdesc.ensure((size_t)np * sizeof(dr::PopDesc)));
+  HIPCHK(c, c->counts.ensure((size_t)np * 8));
+  HIPCHK(c, c->digest.ensure((size_t)np * 8));
+  HIPCHK(c, hipMemcpyAsync(c->popdesc.p, pd.data(), (size_t)np * sizeof(dr::PopDesc), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->digest.p, 0, (size_t)np * 8, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  HIPCHK(c, launch_emit(c, np, span, c->popdesc.as<dr::PopDesc>(), c->counts.as<u64>(), nullptr, nullptr,
+                        nullptr, 0, true));
+  std::vector<uint64_t> cnt(np);
+  HIPCHK(c, hipMemcpyAsync(cnt.data(), c->counts.p, (size_t)np * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int32_t *ids_dev = nullptr;
+  int64_t cap_here = 0;
+  int64_t tot = 0;
+  for (int i = 0; i < np; i++) tot += (int64_t)cnt[i];
+  if (ids_host && ids_base < ids_cap) {
+    cap_here = std::min<int64_t>(tot, ids_cap - ids_base);
+    std::vector<int64_t> pos(np);
+    int64_t run = 0;
+    for (int i = 0; i < np; i++) { pos[i] = run; run += (int64_t)cnt[i]; }
+    HIPCHK(c, c->pop_pos.ensure((size_t)np * 8));
+    HIPCHK(c, hipMemcpyAsync(c->pop_pos.p, pos.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->ids.ensure((size_t)std::max<int64_t>(cap_here, 1) * 8));
+    ids_dev = c->ids.as<int32_t>();
+  }
+  HIPCHK(c, launch_emit(c, np, span, c->popdesc.as<dr::PopDesc>(), nullptr, c->digest.as<u64>(),
+                        ids_dev ? c->pop_pos.as<int64_t>() : nullptr, ids_dev, cap_here, false));
+  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  HIPCHK(c, hipMemcpyAsync(digest_out, c->digest.p, (size_t)np * 8, hipMemcpyDeviceToHost, c->stream));
+  if (ids_dev && cap_here > 0)
+    HIPCHK(c, hipMemcpyAsync(ids_host + 2 * ids_base, ids_dev, (size_t)cap_here * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memcpy(count_out, cnt.data(), (size_t)np * 8);
+  if (ids_total) *ids_total = tot;
+  if (ms) {
+    float t = 0;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev[2], c->ev[3]));
+    *ms += t;
+  }
+  return DR_OK;
+}
+
+}  // namespace
+
+extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_t *to, int strong_only,
+                             uint8_t *out) {
+  if (!c) return DR_E_INVAL;
+  if (q < 0 || (q > 0 && (!from || !to || !out))) return c->fail(DR_E_INVAL, "bad query arrays");
+  if (int rc = set_device(c)) return rc;
+  std::vector<dr::SweepQuery> qv;
+  std::vector<int> idx;
+  for (int i = 0; i < q; i++) {
+    const int fr = from[2 * i], fs = from[2 * i + 1], tr = to[2 * i], ts = to[2 * i + 1];
+    if (fr == tr && fs == ts) { out[i] = 1; continue; }  // process.go:91-93
+    if (fr < 0 || fr >= c->nrounds)
+      return c->fail(DR_E_INVAL, "query %d: from round %d outside the DAG (Go: index out of range)", i, fr);
+    out[i] = 0;
+    if (tr < 0 || tr >= fr || ts < 1 || ts > c->n) continue;  // unreachable by construction
+    if (fs < 1 || fs > c->n) continue;                         // unknown `from`: no edges
+    dr::SweepQuery sq{};
+    sq.top = fr;
+    sq.bottom = tr;
+    sq.src0 = fs - 1;
+    sq.flags = strong_only ? dr::Q_STRONG_ONLY : dr::Q_MASKS;
+    sq.tgt0 = ts - 1;
+    sq.out_off = 0;
+    sq.cur_round = 0;
+    qv.push_back(sq);
+    idx.push_back(i);
+  }
+  std::vector<uint8_t> hits;
+  int rc = run_sweeps(c, qv, false, nullptr, nullptr, &hits, nullptr, nullptr,
+                      [](size_t, size_t) { return 0; }, nullptr);
+  if (rc) return rc;
+  for (size_t k = 0; k < idx.size(); k++) out[idx[k]] = hits[k];
+  return DR_OK;
+}
+
+extern "C" int dr_reach_sets(dr_ctx *c, int q, const int32_t *from, const int32_t *bottom, int strong_only,
+                             uint64_t *out, size_t cap_words, size_t *out_words) {
+  if (!c) return DR_E_INVAL;
+  if (int rc = set_device(c)) return rc;
+  size_t need = 0;
+  for (int i = 0; i < q; i++) {
+    const int fr = from[2 * i], b = bottom[i];
+    if (fr < 0 || fr >= c->nrounds || b < 0 || b > fr)
+      return c->fail(DR_E_INVAL, "query %d: rounds [%d,%d] outside the DAG", i, b, fr);
+    need += (size_t)(fr - b + 1) * c->W;
+  }
+  if (out_words) *out_words = need;
+  if (need > cap_words || (!out && need)) return c->fail(DR_E_CAPACITY, "reach sets need %zu words", need);
+  std::vector<dr::SweepQuery> qv(q);
+  std::vector<size_t> obase(q);
+  size_t acc = 0;
+  for (int i = 0; i < q; i++) {
+    dr::SweepQuery &s = qv[i];
+    s = dr::SweepQuery{};
+    s.top = from[2 * i];
+    s.bottom = bottom[i];
+    const int fs = from[2 * i + 1];
+    s.src0 = (fs >= 1 && fs <= c->n) ? fs - 1 : -1;
+    s.flags = dr::Q_MASKS | (strong_only ? dr::Q_STRONG_ONLY : 0);
+    s.tgt0 = -1;
+    obase[i] = acc;
+    acc += (size_t)(s.top - s.bottom + 1) * c->W;
+  }
+  const int W = c->W, WS = c->WS;
+  std::vector<u64> tmp;
+  return run_sweeps(c, qv, false, nullptr, nullptr, nullptr, nullptr, nullptr,
+                    [&](size_t i0, size_t i1) -> int {
+                      size_t words = 0;
+                      for (size_t i = i0; i < i1; i++) words += (size_t)(qv[i].top - qv[i].bottom + 1) * WS;
+                      tmp.resize(words);
+                      HIPCHK(c, hipMemcpy(tmp.data(), c->masks.p, words * 8, hipMemcpyDeviceToHost));
+                      for (size_t i = i0; i < i1; i++) {
+                        const int nr = qv[i].top - qv[i].bottom + 1;
+                        for (int r = 0; r < nr; r++)
+                          std::memcpy(out + obase[i] + (size_t)r * W, &tmp[qv[i].mask_off + (size_t)r * WS], (size_t)W * 8);
+                      }
+                      return 0;
+                    },
+                    nullptr);
+}
+
+namespace {
+
+// Commit decisions for waves [w0, w1] (host handles waves whose round(w,4) is
+// not mirrored: legal only when their leader is bottom).
+int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, float *ms) {
+  if (w0 < 1 || w1 < w0) return c->fail(DR_E_INVAL, "wave range [%d,%d] invalid (waves are 1-based)", w0, w1);
+  int wk = w0 - 1;  // last wave the kernel can evaluate
+  while (wk + 1 <= w1 && 4 * (wk + 1) < c->nrounds) wk++;
+  for (int w = wk + 1; w <= w1; w++) {
+    const int r1 = 4 * (w - 1) + 1;
+    if (r1 >= c->nrounds) return c->fail(DR_E_INVAL, "wave %d: leader round %d not in the DAG (Go: index out of range)", w, r1);
+    if (c->is_present(r1, 1)) return c->fail(DR_E_INVAL, "wave %d: round %d not in the DAG (Go: index out of range)", w, 4 * w);
+    commit[w - w0] = 0;
+    vcount[w - w0] = -1;
+  }
+  const int nw = wk - w0 + 1;
+  if (nw <= 0) return DR_OK;
+  HIPCHK(c, c->commit.ensure((size_t)nw));
+  HIPCHK(c, c->vcount.ensure((size_t)nw * 4));
+  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  HIPCHK(c, launch_commit(c, w0, nw, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));
+  HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+  HIPCHK(c, hipMemcpyAsync(commit, c->commit.p, (size_t)nw, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(vcount, c->vcount.p, (size_t)nw * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (ms) HIPCHK(c, hipEventElapsedTime(ms, c->ev[4], c->ev[5]));
+  return DR_OK;
+}
+
+struct ChainTask { int wave, floor; };
+
+// Leader chains of commits (process.go:341-350).  pushes[i] receives the waves
+// pushed by task i in push order (task wave first).
+int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::vector<int32_t>> &pushes,
+               uint64_t *edges_total, float *ms) {
+  pushes.assign(tasks.size(), {});
+  std::vector<dr::SweepQuery> qv;
+  std::vector<int> qi;
+  int64_t off = 0;
+  for (size_t i = 0; i < tasks.size(); i++) {
+    pushes[i].push_back(tasks[i].wave);
+    if (tasks[i].wave - 1 < tasks[i].floor + 1) continue;
+    if (tasks[i].floor < 0) return c->fail(DR_E_INVAL, "decidedWave %d < 0 (Go: waveRound(0,1) index out of range)", tasks[i].floor);
+    dr::SweepQuery s{};
+    s.top = 4 * (tasks[i].wave - 1) + 1;
+    s.bottom = 4 * tasks[i].floor + 1;
+    s.src0 = 0;
+    s.flags = dr::Q_CHAIN | dr::Q_STRONG_ONLY;
+    s.out_off = (int32_t)off;
+    s.tgt0 = -1;
+    off += tasks[i].wave - tasks[i].floor - 1;
+    qv.push_back(s);
+    qi.push_back((int)i);
+  }
+  if (edges_total) *edges_total = 0;
+  if (ms) *ms = 0;
+  if (qv.empty()) return DR_OK;
+  if (off > INT32_MAX) return c->fail(DR_E_INVAL, "chain output too large");
+  HIPCHK(c, c->push_out.ensure((size_t)std::max<int64_t>(off, 1) * 4));
+  std::vector<uint64_t> edges;
+  std::vector<int32_t> pn;
+  int rc = run_sweeps(c, qv, false, &edges, nullptr, nullptr, &pn, c->push_out.as<int32_t>(),
+                      [](size_t, size_t) { return 0; }, ms);
+  if (rc) return rc;
+  std::vector<int32_t> po((size_t)off);
+  HIPCHK(c, hipMemcpy(po.data(), c->push_out.p, (size_t)off * 4, hipMemcpyDeviceToHost));
+  uint64_t et = 0;
+  for (size_t k = 0; k < qv.size(); k++) {
+    et += edges[k];
+    auto &P = pushes[qi[k]];
+    for (int j = 0; j < pn[k]; j++) P.push_back(po[qv[k].out_off + j]);
+  }
+  if (edges_total) *edges_total = et;
+  return DR_OK;
+}
+
+struct Pop { int32_t round, source, cur_round; };
+
+// Deliver pops (in pop order).  REF: every pop's cone independently (identical
+// leaders share one sweep); PAPER: one workgroup walks the pops in order,
+// pruning at delivered vertices.
+struct SweepStats { uint64_t weak_edges = 0, sweeps = 0, rounds = 0, vertices = 0; };
+
+int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pcount, uint64_t *pdigest,
+                uint64_t *pedges, SweepStats *stats, int32_t *ids, int64_t ids_cap, int64_t *ids_total, float *ms_sweep,
+                float *ms_emit) {
+  const int WS = c->WS;
+  if (ms_sweep) *ms_sweep = 0;
+  if (ms_emit) *ms_emit = 0;
+  int64_t id_run = 0;
+  if (pops.empty()) { if (ids_total) *ids_total = 0; return DR_OK; }
+  std::vector<dr::SweepQuery> qv;
+  std::vector<int> pop2q(pops.size());
+  const bool want_ids = ids && ids_cap > 0;
+  if (mode == DR_DELIVER_REF && !want_ids) {
+    // unique leaders, longest first
+    std::vector<int> order(pops.size());
+    for (size_t i = 0; i < pops.size(); i++) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      if (pops[a].round != pops[b].round) return pops[a].round > pops[b].round;
+      return pops[a].source < pops[b].source;
+    });
+    for (size_t k = 0; k < order.size(); k++) {
+      const Pop &p = pops[order[k]];
+      if (k > 0 && pops[order[k - 1]].round == p.round && pops[order[k - 1]].source == p.source) {
+        pop2q[order[k]] = (int)qv.size() - 1;
+        continue;
+      }
+      dr::SweepQuery s{};
+      s.top = p.round;
+      s.bottom = 0;
+      s.src0 = (p.source >= 1 && p.source <= c->n) ? p.source - 1 : -1;
+      s.flags = dr::Q_MASKS;
+      s.tgt0 = -1;
+      qv.push_back(s);
+      pop2q[order[k]] = (int)qv.size() - 1;
+    }
+  } else {
+    // pop order, one sweep per pop (paper mode's dedup and the id list need it)
+    const bool paper = mode == DR_DELIVER_PAPER;
+    if (paper) {
+      HIPCHK(c, c->dlv.ensure((size_t)c->nrounds * WS * 8));
+      HIPCHK(c, hipMemsetAsync(c->dlv.p, 0, (size_t)c->nrounds * WS * 8, c->stream));
+    }
+    for (size_t i = 0; i < pops.size(); i++) {
+      dr::SweepQuery s{};
+      s.top = pops[i].round;
+      s.bottom = 0;
+      s.src0 = (pops[i].source >= 1 && pops[i].source <= c->n) ? pops[i].source - 1 : -1;
+      s.flags = dr::Q_MASKS | (paper ? dr::Q_PRUNE : 0);
+      s.tgt0 = -1;
+      s.cur_round = pops[i].cur_round;
+      qv.push_back(s);
+      pop2q[i] = (int)i;
+    }
+  }
+  // q -> pops that use it
+  std::vector<std::vector<int>> q2pop(qv.size());
+  for (size_t i = 0; i < pops.size(); i++) q2pop[pop2q[i]].push_back((int)i);
+  std::vector<uint64_t> qedges, qwedges;
+  // ids need pop order: emission per batch is in q order, so collect (count,
+  // digest) per pop and, for ids, run a second emission pass in pop order below.
+  std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
+  float ms_e = 0;
+  int rc = run_sweeps(
+      c, qv, mode == DR_DELIVER_PAPER, &qedges, &qwedges, nullptr, nullptr, nullptr,
+      [&](size_t i0, size_t i1) -> int {
+        // pops served by this batch, in pop order
+        std::vector<int> pl;
+        for (size_t k = i0; k < i1; k++) pl.insert(pl.end(), q2pop[k].begin(), q2pop[k].end());
+        std::sort(pl.begin(), pl.end());
+        std::vector<dr::PopDesc> pd(pl.size());
+        int64_t rb = 0;
+        for (size_t t = 0; t < pl.size(); t++) {
+          const Pop &p = pops[pl[t]];
+          const dr::SweepQuery &s = qv[pop2q[pl[t]]];
+          pd[t].mask_off = s.mask_off;
+          pd[t].rbase_off = rb;
+          pd[t].first = 1;
+          pd[t].last = std::min(p.cur_round, s.top);
+          rb += s.top + 1;
+        }
+        std::vector<uint64_t> bc(pl.size()), bd(pl.size());
+        int64_t tot = 0;
+        // with ids requested, queries are in pop order, one per pop, so a
+        // batch's pops are a contiguous run and its ids start at id_run
+        int r2 = run_emit(c, pd, bc.data(), bd.data(), want_ids ? ids : nullptr, ids_cap, id_run, &tot, &ms_e);
+        if (r2) return r2;
+        id_run += tot;
+        for (size_t t = 0; t < pl.size(); t++) { cnt[pl[t]] = bc[t]; dg[pl[t]] = bd[t]; }
+        return 0;
+      },
+      ms_sweep);
+  if (rc) return rc;
+  if (stats) {  // per distinct sweep: the work actually done
+    *stats = SweepStats{};
+    for (size_t k = 0; k < qv.size(); k++) {
+      stats->weak_edges += qwedges[k];
+      stats->sweeps++;
+      stats->rounds += (uint64_t)(qv[k].top - qv[k].bottom + 1);
+      stats->vertices += cnt[q2pop[k][0]];
+    }
+  }
+  for (size_t i = 0; i < pops.size(); i++) {
+    pcount[i] = cnt[i];
+    pdigest[i] = dg[i];
+    if (pedges) pedges[i] = qedges[pop2q[i]];
+  }
+  if (ids_total) *ids_total = id_run;
+  if (ms_emit) *ms_emit = ms_e;
+  return DR_OK;
+}
+
+}  // namespace
+
+extern "C" int dr_wave_commit(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount) {
+  if (!c) return DR_E_INVAL;
+  if (!commit || !vcount) return c->fail(DR_E_INVAL, "null output");
+  if (int rc = set_device(c)) return rc;
+  return commit_range(c, w0, w1, commit, vcount, nullptr);
+}
+
+extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *commit, int32_t *vcount,
+                             int32_t *pushed_waves, int cap, int *n_pushed) {
+  if (!c) return DR_E_INVAL;
+  if (!commit || !vcount || !n_pushed) return c->fail(DR_E_INVAL, "null output");
+  if (int rc = set_device(c)) return rc;
+  *n_pushed = 0;
+  if (int rc = commit_range(c, wave, wave, commit, vcount, nullptr)) return rc;
+  if (!*commit) return DR_OK;
+  std::vector<std::vector<int32_t>> pushes;
+  if (int rc = run_chains(c, {ChainTask{wave, decided_wave}}, pushes, nullptr, nullptr)) return rc;
+  *n_pushed = (int)pushes[0].size();
+  if ((int)pushes[0].size() > cap || (!pushed_waves && !pushes[0].empty()))
+    return c->fail(DR_E_CAPACITY, "%zu pushed leaders, capacity %d", pushes[0].size(), cap);
+  std::copy(pushes[0].begin(), pushes[0].end(), pushed_waves);
+  return DR_OK;
+}
+
+extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack, int cur_round, int mode,
+                                 int32_t *out_ids, size_t cap, size_t *out_n, uint64_t *pop_count,
+                                 uint64_t *pop_digest) {
+  if (!c) return DR_E_INVAL;
+  if (nstack < 0 || (nstack > 0 && !stack_rs)) return c->fail(DR_E_INVAL, "bad stack");
+  if (mode != DR_DELIVER_REF && mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad mode %d", mode);
+  if (int rc = set_device(c)) return rc;
+  if (out_n) *out_n = 0;
+  if (nstack == 0) return DR_OK;
+  if (cur_round >= c->nrounds) return c->fail(DR_E_INVAL, "p.round %d beyond the DAG (Go: index out of range)", cur_round);
+  std::vector<Pop> pops;
+  for (int t = nstack - 1; t >= 0; t--) {  // LIFO (stack/stack.go:23-28)
+    Pop p{stack_rs[2 * t], stack_rs[2 * t + 1], cur_round};
+    if (cur_round >= 1 && (p.round < 0 || p.round >= c->nrounds))
+      return c->fail(DR_E_INVAL, "popped vertex round %d outside the DAG (Go: index out of range)", p.round);
+    if (p.source < 1 || p.source > c->n)
+      return c->fail(DR_E_CONTRACT, "popped vertex (%d,%d): source outside [1,n]", p.round, p.source);
+    if (cur_round < 1) p.round = std::max(0, std::min(p.round, c->nrounds - 1));
+    pops.push_back(p);
+  }
+  std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
+  int64_t tot = 0;
+  int rc = run_deliver(c, pops, mode, cnt.data(), dg.data(), nullptr, nullptr, out_ids, (int64_t)cap, &tot,
+                       nullptr, nullptr);
+  if (rc) return rc;
+  if (out_n) *out_n = (size_t)tot;
+  if (pop_count) std::copy(cnt.begin(), cnt.end(), pop_count);
+  if (pop_digest) std::copy(dg.begin(), dg.end(), pop_digest);
+  if (out_ids && (size_t)tot > cap) return c->fail(DR_E_CAPACITY, "%lld delivered ids, capacity %zu", (long long)tot, cap);
+  return DR_OK;
+}
+
+extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
+  if (!c) return DR_E_INVAL;
+  if (!o || !o->commit || !o->vcount || !o->push_off) return c->fail(DR_E_INVAL, "null output");
+  if (nwaves < 1 || 4 * nwaves >= c->nrounds) return c->fail(DR_E_INVAL, "nwaves %d needs rounds 0..%d mirrored", nwaves, 4 * nwaves);
+  if (chain_mode != DR_CHAIN_LITERAL && chain_mode != DR_CHAIN_PERSISTENT) return c->fail(DR_E_INVAL, "bad chain mode");
+  if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad deliver mode");
+  if (int rc = set_device(c)) return rc;
+  o->ms_commit = o->ms_chain = o->ms_deliver = o->ms_emit = 0;
+  o->sweep_weak_edges = o->sweep_count = o->sweep_rounds = o->sweep_vertices = 0;
+  o->n_ids = 0;
+  // 1. commit decisions, all waves at once
+  if (int rc = commit_range(c, 1, nwaves, o->commit, o->vcount, &o->ms_commit)) return rc;
+  uint64_t ce = 0;
+  for (int w = 1; w <= nwaves; w++)
+    if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
+  o->commit_edges = ce;
+  // 2. chains
+  std::vector<ChainTask> tasks;
+  int last = 0;
+  for (int w = 1; w <= nwaves; w++)
+    if (o->commit[w - 1]) {
+      tasks.push_back(ChainTask{w, chain_mode == DR_CHAIN_PERSISTENT ? last : 0});
+      last = w;
+    }
+  std::vector<std::vector<int32_t>> pushes;
+  if (int rc = run_chains(c, tasks, pushes, &o->chain_edges, &o->ms_chain)) return rc;
+  int64_t np = 0;
+  for (auto &p : pushes) np += (int64_t)p.size();
+  o->n_push = np;
+  if (np > o->push_cap || !o->push_wave || !o->pop_count || !o->pop_digest)
+    return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)np, (long long)o->push_cap);
+  // 3. pops
+  std::vector<Pop> pops;
+  int64_t at = 0;
+  size_t t = 0;
+  for (int w = 1; w <= nwaves; w++) {
+    o->push_off[w - 1] = (uint32_t)at;
+    if (t < tasks.size() && tasks[t].wave == w) {
+      for (int32_t pw : pushes[t]) o->push_wave[at++] = pw;
+      for (auto it = pushes[t].rbegin(); it != pushes[t].rend(); ++it)
+        pops.push_back(Pop{4 * (*it - 1) + 1, 1, 4 * w});
+      t++;
+    }
+  }
+  o->push_off[nwaves] = (uint32_t)at;
+  int64_t tot = 0;
+  std::vector<uint64_t> pe(pops.size());
+  SweepStats st;
+  int rc = run_deliver(c, pops, deliver_mode, o->pop_count, o->pop_digest, pe.data(), &st, o->ids, o->ids_cap,
+                       &tot, &o->ms_deliver, &o->ms_emit);
+  o->sweep_weak_edges = st.weak_edges;
+  o->sweep_count = st.sweeps;
+  o->sweep_rounds = st.rounds;
+  o->sweep_vertices = st.vertices;
+  if (rc) return rc;
+  uint64_t de = 0;
+  for (size_t i = 0; i < pops.size(); i++) {
+    de += pe[i];
+    if (o->pop_edges) o->pop_edges[i] = pe[i];
+  }
+  o->deliver_edges = de;
+  o->n_ids = tot;
+  return DR_OK;
+}

@@ -1,0 +1,448 @@
+// kernels.hpp -- CDNA4 (gfx950) kernels of the causal-history reachability engine.
+//
+// Device layout, WS = row stride in u64 words = next_pow2(ceil(n/64)):
+//   strong  [rounds][n][WS]  bit t of row (r,s) <=> strong edge (r,s) -> (r-1,t+1)
+//   present [rounds][WS]     bit s-1 <=> source s has a vertex in round r
+//   weak    u32 per edge, grouped by round (weak_roff[r]..weak_roff[r+1]):
+//           bits 0-10 target source-1, 11-21 own source-1, 22-31 delta = r - r'
+//   far     u64 per edge with delta > 1023: (own source-1) << 32 | (r' << 11 | t-1)
+//
+// Kernels (all integer/boolean; HBM-bound, no MFMA):
+//   k_commit  waveReady's commit decision (process.go:326-339) for a range of
+//             waves, one workgroup per wave: backward strong sweep from the leader
+//             over rounds 4w-2..4w with ballot-compacted "row AND S != 0" tests.
+//   k_sweep   forward reachability (path(), process.go:89-148) from one vertex per
+//             workgroup, round by round: OR of the rows in the frontier (coalesced
+//             16-B row chunks, wave64 xor-shuffle OR reduction, LDS 64-bit atomic OR
+//             into a ring of future-round frontiers) plus weak-edge scatter into that
+//             ring.  Variants: chain (waveReady's leader chain, :341-350), prune
+//             (paper-mode orderVertices dedup), masks (reach sets for delivery).
+//   k_emit_*  orderVertices emission (process.go:417-441): per (pop, round) counts,
+//             scan, then (round asc, slot asc) positions via ballot ranks, the
+//             order-sensitive digest and optional id list.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dr {
+
+typedef unsigned long long u64;
+
+enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8 };
+
+struct SweepQuery {
+  int32_t top;       // start round (the `from` vertex's round)
+  int32_t bottom;    // last round of the sweep (not expanded)
+  int32_t src0;      // 0-based source of `from`; -1 = nothing to expand
+  int32_t flags;     // Q_*
+  int64_t mask_off;  // word offset of round `bottom` in masks (Q_MASKS)
+  int32_t out_off;   // Q_CHAIN: first entry in push_out
+  int32_t tgt0;      // path: 0-based target source tested at round `bottom`, -1 none
+  int32_t cur_round; // Q_PRUNE: rounds 1..cur_round enter the delivered set
+  int32_t pad;
+};
+
+struct DagView {
+  const u64 *strong;
+  const u64 *present;
+  const uint32_t *weak;
+  const uint32_t *weak_roff;
+  const u64 *far;
+  const uint32_t *far_roff;
+  int32_t n;
+  int32_t nrounds;
+};
+
+__device__ __forceinline__ int popc64(u64 x) { return __popcll(x); }
+
+__device__ __forceinline__ u64 ld_agent(const u64 *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ u64 mix64(u64 z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ u64 digest_term(uint32_t round, uint32_t source, u64 k) {
+  u64 key = ((u64)round << 32) | source;
+  return mix64(key ^ mix64(k + 0x9E3779B97F4A7C15ULL));
+}
+
+// Geometry per row stride: chunks are 16 B (two words) for WS >= 2, one word for WS == 1.
+template <int WS, int NT>
+struct Geo {
+  static constexpr int CW = WS >= 2 ? 2 : 1;    // words per chunk
+  static constexpr int CPR = WS / CW;           // chunks per row
+  static constexpr int RPP = NT / CPR;          // rows per pass
+  static constexpr int NMAX = 64 * WS;          // max n for this stride
+  static constexpr int CPT = (NMAX + RPP - 1) / RPP;  // passes (chunks per thread)
+  static_assert(NT % 64 == 0 && NT % CPR == 0, "block must tile rows");
+};
+
+// ---------------------------------------------------------------------------
+// k_commit: one workgroup per wave.  S0 = {leader}; S_{k+1} = {v in round
+// r1+k+1 : row(v) & S_k != 0}; vcount = |S_3|.  Row loads of round r1+1 are
+// restricted to the chunk holding the leader's bit; rounds r1+2, r1+3 are
+// prefetched whole (they do not depend on S) when the registers allow.
+// ---------------------------------------------------------------------------
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int quorum,
+                                               uint8_t *__restrict__ commit,
+                                               int32_t *__restrict__ vcount) {
+  using G = Geo<WS, NT>;
+  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  __shared__ u64 S[WS];
+  __shared__ u64 T[WS];
+  __shared__ u64 P[3][WS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int bi = blockIdx.x;
+  if (bi >= nw) return;
+  const int w = w0 + bi;
+  const int r1 = 4 * (w - 1) + 1;
+  const int n = g.n;
+  if (!(g.present[(size_t)r1 * WS] & 1ULL)) {  // leader is bottom (process.go:327-329)
+    if (tid == 0) { commit[bi] = 0; vcount[bi] = -1; }
+    return;
+  }
+  if (tid < WS) {
+    S[tid] = tid == 0 ? 1ULL : 0ULL;
+    T[tid] = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) P[k][tid] = g.present[(size_t)(r1 + 1 + k) * WS + tid];
+  }
+  __syncthreads();
+  const int j = tid % CPR;  // this thread's chunk column
+#pragma unroll
+  for (int k = 1; k <= 3; k++) {
+    const int r = r1 + k;
+    const u64 *rows = g.strong + (size_t)r * n * WS;
+    const u64 *pres = P[k - 1];
+    // S chunk this thread ANDs with
+    u64 s0 = S[j * CW], s1 = CW == 2 ? S[j * CW + 1] : 0ULL;
+    const bool need = (s0 | s1) != 0ULL;
+    u64 v0[CPT], v1[CPT];
+#pragma unroll
+    for (int p = 0; p < CPT; p++) {
+      const int s = tid / CPR + p * RPP;
+      v0[p] = 0;
+      v1[p] = 0;
+      if (need && s < n && ((pres[s >> 6] >> (s & 63)) & 1ULL)) {
+        if constexpr (CW == 2) {
+          const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(rows + (size_t)s * WS + 2 * j);
+          v0[p] = x.x;
+          v1[p] = x.y;
+        } else {
+          v0[p] = rows[s];
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < CPT; p++) {
+      const int rowbase = (wid * 64) / CPR + p * RPP;  // first row of this wave's pass
+      if (rowbase >= n) break;                         // wave-uniform
+      const bool hit = ((v0[p] & s0) | (v1[p] & s1)) != 0ULL;
+      u64 m = __ballot(hit);
+      if (lane == 0 && m) {
+        u64 bits;
+        if constexpr (CPR == 1) {
+          bits = m;
+        } else {
+#pragma unroll
+          for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
+          bits = 0;
+#pragma unroll
+          for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
+        }
+        atomicOr(&T[rowbase >> 6], bits << (rowbase & 63));
+      }
+    }
+    __syncthreads();
+    if (tid < WS) { S[tid] = T[tid]; T[tid] = 0; }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int vc = 0;
+#pragma unroll
+    for (int i = 0; i < WS; i++) vc += popc64(S[i]);
+    vcount[bi] = vc;
+    commit[bi] = vc >= quorum ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_sweep: one workgroup per query (or, with seq != 0, one workgroup walking all
+// queries in order -- paper-mode dedup needs that order).
+//
+// Per round r (top .. bottom):
+//   phase A (wave 0, lane w < WS): F[w] = ring[r][w] (| far-scatter mask word)
+//           (& ~delivered); chain restart; masks/delivered writes; ring slot freed.
+//   phase B (all): strong rows of F -> ring[r-1]; weak edges of F -> ring[r'].
+// LDS: F[WS] | FE[WS] | ring[depth][WS] | ctl (int[4]) | edges (u64).
+// ---------------------------------------------------------------------------
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_sweep(DagView g, const SweepQuery *__restrict__ qs,
+                                              int nq, int seq, int depth_log2,
+                                              u64 *__restrict__ masks, u64 *__restrict__ dlv,
+                                              int32_t *__restrict__ push_out,
+                                              int32_t *__restrict__ push_n,
+                                              u64 *__restrict__ edges_out,
+                                              u64 *__restrict__ wedges_out,
+                                              uint8_t *__restrict__ hit_out) {
+  using G = Geo<WS, NT>;
+  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  extern __shared__ __attribute__((aligned(16))) u64 smem[];
+  u64 *F = smem;                // WS: frontier (reached ids, dangling included)
+  u64 *FE = smem + WS;          // WS: F & present (the vertices that expand)
+  u64 *ring = smem + 2 * WS;    // depth * WS
+  const int depth = 1 << depth_log2, dmask = depth - 1;
+  int *s_ctl = reinterpret_cast<int *>(ring + (size_t)depth * WS);  // [0]=low water [1]=nonzero
+  u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 4);  // [0] all edges, [1] weak edges
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int n = g.n;
+  const int j = tid % CPR;
+
+  const int qa = seq ? 0 : blockIdx.x;
+  const int qb = seq ? nq : blockIdx.x + 1;
+  for (int qi = qa; qi < qb; qi++) {
+    const SweepQuery q = qs[qi];
+    const bool strong_only = q.flags & Q_STRONG_ONLY;
+    const bool chain = q.flags & Q_CHAIN;
+    const bool has_masks = q.flags & Q_MASKS;
+    const bool prune = q.flags & Q_PRUNE;
+    for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
+    if (tid == 0) { s_ctl[0] = q.top; s_ctl[1] = 0; s_edges[0] = 0; s_edges[1] = 0; }
+    __syncthreads();
+    if (tid == 0 && q.src0 >= 0)
+      ring[(size_t)(q.top & dmask) * WS + (q.src0 >> 6)] = 1ULL << (q.src0 & 63);
+    int npush = 0;  // thread 0
+    u64 my_edges = 0, my_wedges = 0;
+    __syncthreads();
+    for (int r = q.top;; --r) {
+      // ---------------- phase A ----------------
+      if (tid < WS) {
+        const int slot = (r & dmask) * WS + tid;
+        u64 f = ring[slot];
+        ring[slot] = 0;
+        u64 *mrow = has_masks ? masks + q.mask_off + (int64_t)(r - q.bottom) * WS : nullptr;
+        if (has_masks && !strong_only) f |= ld_agent(mrow + tid);  // far weak scatters
+        if (prune) f &= ~ld_agent(dlv + (size_t)r * WS + tid);
+        if (chain && r < q.top && ((r - 1) & 3) == 0) {
+          const u64 f0 = __shfl(f, 0);
+          const bool pres = g.present[(size_t)r * WS] & 1ULL;
+          if ((f0 & 1ULL) && pres) {  // strong_path(leader, v') holds: push v' (process.go:344-349)
+            f = tid == 0 ? 1ULL : 0ULL;
+            if (tid == 0) push_out[q.out_off + npush++] = (r - 1) / 4 + 1;
+          }
+        }
+        F[tid] = f;
+        FE[tid] = f & g.present[(size_t)r * WS + tid];
+        if (has_masks) mrow[tid] = f;
+        if (prune && r >= 1 && r <= q.cur_round) {
+          const u64 add = f & g.present[(size_t)r * WS + tid];
+          if (add) atomicOr(dlv + (size_t)r * WS + tid, add);
+        }
+        const bool nz = __any(f != 0ULL);
+        if (tid == 0) {
+          s_ctl[1] = nz;
+          if (nz && r - 1 < s_ctl[0]) s_ctl[0] = r - 1;
+        }
+      }
+      __syncthreads();
+      if (r <= q.bottom) break;
+      if (!s_ctl[1] && s_ctl[0] >= r) break;  // frontier and every pending round empty
+      // ---------------- phase B: strong rows ----------------
+      if (s_ctl[1]) {
+        const u64 *rows = g.strong + (size_t)r * n * WS;
+        u64 v0[CPT], v1[CPT];
+#pragma unroll
+        for (int p = 0; p < CPT; p++) {
+          const int s = tid / CPR + p * RPP;
+          v0[p] = 0;
+          v1[p] = 0;
+          if (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
+            if constexpr (CW == 2) {
+              const ulonglong2 x =
+                  *reinterpret_cast<const ulonglong2 *>(rows + (size_t)s * WS + 2 * j);
+              v0[p] = x.x;
+              v1[p] = x.y;
+            } else {
+              v0[p] = rows[s];
+            }
+          }
+        }
+        u64 a0 = 0, a1 = 0;
+#pragma unroll
+        for (int p = 0; p < CPT; p++) {
+          a0 |= v0[p];
+          a1 |= v1[p];
+          my_edges += (u64)(popc64(v0[p]) + popc64(v1[p]));
+        }
+#pragma unroll
+        for (int off = CPR; off < 64; off <<= 1) {
+          a0 |= __shfl_xor(a0, off);
+          if constexpr (CW == 2) a1 |= __shfl_xor(a1, off);
+        }
+        if (lane < CPR) {
+          u64 *dst = ring + (size_t)((r - 1) & dmask) * WS + lane * CW;
+          if (a0) atomicOr(dst, a0);
+          if (CW == 2 && a1) atomicOr(dst + 1, a1);
+        }
+      }
+      // ---------------- phase B: weak edges ----------------
+      if (!strong_only) {
+        int lowmin = 0x7fffffff;
+        const uint32_t e0 = g.weak_roff[r], e1 = g.weak_roff[r + 1];
+        for (uint32_t e = e0 + tid; e < e1; e += NT) {
+          const uint32_t x = g.weak[e];
+          const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
+          if (!((FE[own >> 6] >> (own & 63)) & 1ULL)) continue;
+          my_wedges++;
+          const int tr = r - delta;
+          if (tr < q.bottom) continue;
+          const u64 bit = 1ULL << (ts & 63);
+          if (delta < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
+          else atomicOr(masks + q.mask_off + (int64_t)(tr - q.bottom) * WS + (ts >> 6), bit);
+          lowmin = min(lowmin, tr);
+        }
+        const uint32_t f0 = g.far_roff[r], f1 = g.far_roff[r + 1];
+        for (uint32_t e = f0 + tid; e < f1; e += NT) {
+          const u64 y = g.far[e];
+          const int own = (int)(y >> 32);
+          const uint32_t t = (uint32_t)y;
+          if (!((FE[own >> 6] >> (own & 63)) & 1ULL)) continue;
+          my_wedges++;
+          const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
+          if (tr < q.bottom) continue;
+          const u64 bit = 1ULL << (ts & 63);
+          if (r - tr < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
+          else atomicOr(masks + q.mask_off + (int64_t)(tr - q.bottom) * WS + (ts >> 6), bit);
+          lowmin = min(lowmin, tr);
+        }
+        if (lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
+      }
+      __syncthreads();
+    }
+    // results
+    my_edges += my_wedges;
+    if (my_edges) atomicAdd(&s_edges[0], my_edges);
+    if (my_wedges) atomicAdd(&s_edges[1], my_wedges);
+    __syncthreads();
+    if (tid == 0) {
+      if (edges_out) edges_out[qi] = s_edges[0];
+      if (wedges_out) wedges_out[qi] = s_edges[1];
+      if (hit_out) hit_out[qi] = q.tgt0 >= 0 ? (uint8_t)((F[q.tgt0 >> 6] >> (q.tgt0 & 63)) & 1ULL) : 0;
+      if (push_n) push_n[qi] = npush;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Emission, part 1: one workgroup per pop.  Per round r in 1..last:
+// c_r = |mask_r & present_r|; exclusive scan -> rbase; total -> count.
+// ---------------------------------------------------------------------------
+struct PopDesc {
+  int64_t mask_off;   // word offset of round 0
+  int64_t rbase_off;  // int offset of round 0 in rbase
+  int32_t last;       // last delivered round = min(cur_round, top)
+  int32_t first;      // first delivered round (1)
+};
+
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_emit_count(DagView g, const PopDesc *__restrict__ pd,
+                                                   const u64 *__restrict__ masks,
+                                                   uint32_t *__restrict__ rbase,
+                                                   u64 *__restrict__ count) {
+  __shared__ uint32_t part[NT];
+  const PopDesc d = pd[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int nr = d.last - d.first + 1;
+  const int per = nr > 0 ? (nr + NT - 1) / NT : 0;
+  const int ra = d.first + tid * per, rb = min(d.last + 1, ra + per);
+  uint32_t loc = 0;
+  for (int r = ra; r < rb; r++) {
+    const u64 *m = masks + d.mask_off + (int64_t)r * WS;
+    const u64 *p = g.present + (size_t)r * WS;
+#pragma unroll
+    for (int w = 0; w < WS; w++) loc += popc64(m[w] & p[w]);
+  }
+  part[tid] = loc;
+  __syncthreads();
+  // inclusive scan (Hillis-Steele) over NT partials
+  for (int off = 1; off < NT; off <<= 1) {
+    uint32_t v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - loc;
+  for (int r = ra; r < rb; r++) {
+    rbase[d.rbase_off + r] = run;
+    const u64 *m = masks + d.mask_off + (int64_t)r * WS;
+    const u64 *p = g.present + (size_t)r * WS;
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < WS; w++) c += popc64(m[w] & p[w]);
+    run += c;
+  }
+  if (tid == NT - 1) count[blockIdx.x] = part[NT - 1];
+}
+
+// ---------------------------------------------------------------------------
+// Emission, part 2: grid (round blocks, pops).  Each wave walks one round's slots
+// in order, 64 at a time: ballot of "slot's source in mask" gives ranks, so the
+// k-th delivered vertex of the pop gets position rbase + rank.
+// ---------------------------------------------------------------------------
+template <int WS, int NT, int RPB>
+__global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__restrict__ slot_off,
+                                                 const uint16_t *__restrict__ slot_src,
+                                                 const PopDesc *__restrict__ pd,
+                                                 const u64 *__restrict__ masks,
+                                                 const uint32_t *__restrict__ rbase,
+                                                 const int64_t *__restrict__ pop_pos,
+                                                 u64 *__restrict__ digest,
+                                                 int32_t *__restrict__ ids, int64_t ids_cap) {
+  __shared__ u64 s_dg;
+  const PopDesc d = pd[blockIdx.y];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int NWAVE = NT / 64;
+  if (tid == 0) s_dg = 0;
+  __syncthreads();
+  u64 dg = 0;
+  const int ra = d.first + blockIdx.x * RPB;
+  const int rb = min(d.last + 1, ra + RPB);
+  const int64_t pbase = pop_pos ? pop_pos[blockIdx.y] : 0;
+  for (int r = ra + wid; r < rb; r += NWAVE) {
+    const u64 *m = masks + d.mask_off + (int64_t)r * WS;
+    uint32_t pos = rbase[d.rbase_off + r];
+    const uint32_t sa = slot_off[r], sb = slot_off[r + 1];
+    for (uint32_t i0 = sa; i0 < sb; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      int src = i < sb ? (int)slot_src[i] : 0;
+      bool in = false;
+      if (src > 0) {
+        const int s = src - 1;
+        in = (m[s >> 6] >> (s & 63)) & 1ULL;
+      }
+      const u64 b = __ballot(in);
+      if (in) {
+        const uint32_t k = pos + (uint32_t)__popcll(b & ((1ULL << lane) - 1ULL));
+        dg += digest_term((uint32_t)r, (uint32_t)src, k);
+        if (ids) {
+          const int64_t at = pbase + k;
+          if (at < ids_cap) { ids[2 * at] = r; ids[2 * at + 1] = src; }
+        }
+      }
+      pos += (uint32_t)__popcll(b);
+    }
+  }
+  // block reduce
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) dg += __shfl_xor(dg, off);
+  if (lane == 0 && dg) atomicAdd(&s_dg, dg);
+  __syncthreads();
+  if (tid == 0 && s_dg) atomicAdd(digest + blockIdx.y, s_dg);
+}
+
+}  // namespace dr

@@ -1,0 +1,179 @@
+"""Python handle on one device mirror (dr_ctx) -- a thin veneer over the C ABI.
+
+Each method names the reference function it stands in for; semantics are those of
+``include/dagrider_gpu.h``.  All compute happens in the HIP library: there is no
+Python or CPU implementation of any query here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from .dag import PackedDag, Vertex, flatten_lists
+
+
+@dataclass
+class ReplayResult:
+    commit: np.ndarray  # uint8 [nwaves]
+    vcount: np.ndarray  # int32 [nwaves]
+    push_off: np.ndarray  # uint32 [nwaves+1]
+    push_wave: np.ndarray  # int32 [n_push]
+    pop_count: np.ndarray  # uint64 [n_push]
+    pop_digest: np.ndarray  # uint64 [n_push]
+    pop_edges: np.ndarray  # uint64 [n_push]
+    ids: Optional[np.ndarray]  # int32 [n_ids, 2]
+    commit_edges: int
+    chain_edges: int
+    deliver_edges: int
+    ms: dict
+    sweep: dict
+
+    @property
+    def total_edges(self) -> int:
+        return self.commit_edges + self.chain_edges + self.deliver_edges
+
+
+class Engine:
+    """One Process.dag mirror on a GPU (dr_create ... dr_destroy)."""
+
+    def __init__(self, n: int, faulty: int, max_rounds: int, device: int = 0):
+        self._L = L.lib()
+        h = L.P()
+        rc = self._L.dr_create(n, faulty, max_rounds, device, C.byref(h))
+        if rc != L.DR_OK:
+            raise L.DrError(rc, self._L.dr_last_error(None).decode())
+        self._h = h
+        self.n, self.faulty, self.max_rounds, self.device = n, faulty, max_rounds, device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.dr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != L.DR_OK:
+            raise L.DrError(rc, self._L.dr_last_error(self._h).decode())
+
+    @property
+    def num_rounds(self) -> int:
+        return self._L.dr_num_rounds(self._h)
+
+    # ---- p.dag[r] = append(...)  (process.go:229) ----
+    def append_lists(self, dag: Sequence[Sequence[Vertex]], r0: Optional[int] = None, r1: Optional[int] = None):
+        r0 = self.num_rounds if r0 is None else r0
+        r1 = len(dag) if r1 is None else r1
+        a = flatten_lists(dag, r0, r1)
+        self._check(self._L.dr_append_rounds_lists(self._h, r0, r1 - r0, *[L.ptr(x) for x in a]))
+
+    def append_packed(self, d: PackedDag, r0: Optional[int] = None, r1: Optional[int] = None):
+        r0 = self.num_rounds if r0 is None else r0
+        r1 = d.nrounds if r1 is None else r1
+        n, W = d.n, d.W
+        so = np.ascontiguousarray(d.slot_off[r0:r1 + 1])
+        st = np.ascontiguousarray(d.strong[r0 * n * W:r1 * n * W])
+        wo = np.ascontiguousarray(d.weak_off[r0 * n:r1 * n + 1])
+        self._check(self._L.dr_append_rounds_packed(self._h, r0, r1 - r0, L.ptr(so), L.ptr(d.slot_src), L.ptr(st),
+                                                    L.ptr(wo), L.ptr(d.weak_tgt if len(d.weak_tgt) else
+                                                                     np.zeros(1, np.uint32))))
+
+    # ---- path(from, to, strongPath)  (process.go:89-148), batched ----
+    def path_batch(self, pairs: Sequence[Tuple[Tuple[int, int], Tuple[int, int]]], strong_only: bool) -> np.ndarray:
+        q = len(pairs)
+        fr = np.asarray([p[0] for p in pairs], dtype=np.int32).reshape(-1)
+        to = np.asarray([p[1] for p in pairs], dtype=np.int32).reshape(-1)
+        out = np.zeros(max(q, 1), dtype=np.uint8)
+        self._check(self._L.dr_path_batch(self._h, q, L.ptr(fr), L.ptr(to), int(strong_only), L.ptr(out)))
+        return out[:q]
+
+    def reach_sets(self, froms: Sequence[Tuple[int, int]], bottoms: Sequence[int], strong_only: bool) -> List[np.ndarray]:
+        q = len(froms)
+        fr = np.asarray(froms, dtype=np.int32).reshape(-1)
+        bt = np.asarray(bottoms, dtype=np.int32)
+        W = (self.n + 63) // 64
+        need = sum((f[0] - b + 1) * W for f, b in zip(froms, bottoms))
+        out = np.zeros(max(need, 1), dtype=np.uint64)
+        nw = C.c_size_t()
+        self._check(self._L.dr_reach_sets(self._h, q, L.ptr(fr), L.ptr(bt), int(strong_only), L.ptr(out), need,
+                                          C.byref(nw)))
+        res, o = [], 0
+        for f, b in zip(froms, bottoms):
+            k = (f[0] - b + 1) * W
+            res.append(out[o:o + k].reshape(-1, W))
+            o += k
+        return res
+
+    # ---- waveReady (process.go:314-354) ----
+    def wave_commit(self, w0: int, w1: int):
+        nw = w1 - w0 + 1
+        cm = np.zeros(max(nw, 1), np.uint8)
+        vc = np.zeros(max(nw, 1), np.int32)
+        self._check(self._L.dr_wave_commit(self._h, w0, w1, L.ptr(cm), L.ptr(vc)))
+        return cm[:nw], vc[:nw]
+
+    def wave_ready(self, wave: int, decided_wave: int):
+        cm = np.zeros(1, np.uint8)
+        vc = np.zeros(1, np.int32)
+        cap = max(wave + 1, 1)
+        pw = np.zeros(cap, np.int32)
+        npush = C.c_int()
+        self._check(self._L.dr_wave_ready(self._h, wave, decided_wave, L.ptr(cm), L.ptr(vc), L.ptr(pw), cap,
+                                          C.byref(npush)))
+        return bool(cm[0]), int(vc[0]), [int(x) for x in pw[:npush.value]]
+
+    # ---- orderVertices (process.go:404-443) ----
+    def order_vertices(self, stack: Sequence[Tuple[int, int]], cur_round: int, mode: int = L.DR_DELIVER_REF,
+                       cap: int = 1 << 20):
+        ns = len(stack)
+        st = np.asarray(stack if ns else [(0, 0)], dtype=np.int32).reshape(-1)
+        ids = np.zeros(max(cap, 1) * 2, np.int32)
+        out_n = C.c_size_t()
+        pc = np.zeros(max(ns, 1), np.uint64)
+        pd = np.zeros(max(ns, 1), np.uint64)
+        self._check(self._L.dr_order_vertices(self._h, L.ptr(st), ns, cur_round, mode, L.ptr(ids), cap,
+                                              C.byref(out_n), L.ptr(pc), L.ptr(pd)))
+        k = out_n.value
+        return ids[:2 * k].reshape(-1, 2), pc[:ns], pd[:ns]
+
+    # ---- whole replay ----
+    def replay(self, nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT, deliver_mode: int = L.DR_DELIVER_REF,
+               ids_cap: int = 0, push_cap: Optional[int] = None) -> ReplayResult:
+        push_cap = push_cap if push_cap is not None else (
+            nwaves * (nwaves + 1) // 2 if chain_mode == L.DR_CHAIN_LITERAL else 2 * nwaves + 1)
+        cm = np.zeros(nwaves, np.uint8)
+        vc = np.zeros(nwaves, np.int32)
+        po = np.zeros(nwaves + 1, np.uint32)
+        pw = np.zeros(max(push_cap, 1), np.int32)
+        pc = np.zeros(max(push_cap, 1), np.uint64)
+        pdg = np.zeros(max(push_cap, 1), np.uint64)
+        pe = np.zeros(max(push_cap, 1), np.uint64)
+        ids = np.zeros(max(ids_cap, 1) * 2, np.int32) if ids_cap else None
+        o = L.ReplayOut()
+        o.commit, o.vcount, o.push_off, o.push_wave = L.ptr(cm), L.ptr(vc), L.ptr(po), L.ptr(pw)
+        o.push_cap = push_cap
+        o.pop_count, o.pop_digest, o.pop_edges = L.ptr(pc), L.ptr(pdg), L.ptr(pe)
+        o.ids = L.ptr(ids)
+        o.ids_cap = ids_cap
+        self._check(self._L.dr_replay(self._h, nwaves, chain_mode, deliver_mode, C.byref(o)))
+        k = o.n_push
+        return ReplayResult(cm, vc, po, pw[:k], pc[:k], pdg[:k], pe[:k],
+                            None if ids is None else ids[:2 * min(o.n_ids, ids_cap)].reshape(-1, 2),
+                            o.commit_edges, o.chain_edges, o.deliver_edges,
+                            dict(commit=o.ms_commit, chain=o.ms_chain, deliver=o.ms_deliver, emit=o.ms_emit),
+                            dict(weak_edges=o.sweep_weak_edges, count=o.sweep_count, rounds=o.sweep_rounds,
+                                 vertices=o.sweep_vertices))

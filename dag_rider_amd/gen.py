@@ -1,0 +1,85 @@
+"""Synthetic DAG workloads (generator spec: include/dagrider_gen.h) and the five configs.
+
+CONFIGS pins SURVEY.md s8(d)'s proposed parameters.  The generator is host C++
+(deterministic splitmix64 streams), so the same DAG is produced here and on the
+GPU box without shipping data.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+from .dag import PackedDag
+
+
+@dataclass(frozen=True)
+class GenConfig:
+    name: str
+    n: int
+    last_round: int  # R: rounds 0..R
+    seed: int
+    p_present: float
+    p_late: float
+    p_w: float
+    weak_depth: int
+    p_la: float = 0.0
+
+    @property
+    def faulty(self) -> int:
+        return (self.n - 1) // 3
+
+    @property
+    def nwaves(self) -> int:
+        return self.last_round // 4
+
+
+CONFIGS = {
+    # C1: seeded n=4 companion of the Figure-1 fixture (4 waves)
+    "c1": GenConfig("c1", 4, 16, 1, 1.0, 0.25, 1.0, 4, 0.0),
+    "c2": GenConfig("c2", 64, 1000, 2, 0.95, 0.05, 0.5, 8, 0.05),
+    "c3": GenConfig("c3", 256, 10000, 3, 1.0, 0.3, 0.25, 4, 0.0),
+    "c4": GenConfig("c4", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0),
+    # C5: one of the 4096 independent n=128 replays (seed 5000+i)
+    "c5": GenConfig("c5", 128, 128, 5000, 0.9, 0.1, 0.5, 4, 0.05),
+}
+
+
+def generate(cfg: GenConfig, nthreads: int = 0) -> PackedDag:
+    lib = L.lib()
+    p = L.GenParams(cfg.n, cfg.last_round, cfg.seed, cfg.p_present, cfg.p_late, cfg.p_w, cfg.p_la,
+                    cfg.weak_depth, nthreads)
+    h = L.P()
+    rc = lib.dr_gen_create(C.byref(p), C.byref(h))
+    if rc != 0:
+        raise ValueError(f"generator rejected {cfg}")
+    try:
+        n, W, nr = L.i32(), L.i32(), L.i32()
+        ns, nw = L.u64(), L.u64()
+        lib.dr_gen_info(h, C.byref(n), C.byref(W), C.byref(nr), C.byref(ns), C.byref(nw))
+        n, W, nr, ns, nw = n.value, W.value, nr.value, ns.value, nw.value
+
+        def view(fn, dtype, count):
+            if count == 0:
+                return np.zeros(0, dtype)
+            addr = fn(h)
+            buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(addr)
+            return np.frombuffer(buf, dtype=dtype, count=count).copy()
+
+        return PackedDag(n, nr,
+                         view(lib.dr_gen_slot_off, np.uint32, nr + 1),
+                         view(lib.dr_gen_slot_src, np.uint16, ns),
+                         view(lib.dr_gen_strong, np.uint64, nr * n * W),
+                         view(lib.dr_gen_weak_off, np.uint32, nr * n + 1),
+                         view(lib.dr_gen_weak_tgt, np.uint32, nw))
+    finally:
+        lib.dr_gen_free(h)
+
+
+def small_config(n: int, last_round: int, seed: int, **kw) -> GenConfig:
+    """Seeded small DAGs for cross-checks (parameters randomised per seed by the caller)."""
+    base = dict(p_present=0.9, p_late=0.2, p_w=0.5, weak_depth=4, p_la=0.1)
+    base.update(kw)
+    return GenConfig(f"small-{n}-{last_round}-{seed}", n, last_round, seed, **base)

@@ -1,0 +1,161 @@
+/*
+ * dagrider_gpu.h -- C ABI of the MI355X causal-history reachability engine.
+ *
+ * Drop-in boundary for xenowits/dag-rider's hot path (process/process.go).
+ * The reference has no FFI; its hot path is unexported methods of
+ * process.Process.  Each entry point below names the Go function it replaces;
+ * INTEGRATION.md shows the cgo binding a maintainer would add.
+ *
+ * Contract (cgo rules): only C scalars and flat caller-owned arrays cross the
+ * boundary; the library keeps no host pointer after a call returns; calls on one
+ * context are not thread-safe (the caller serialises them, as the reference's
+ * single Start goroutine does); every call selects the context's device itself,
+ * so goroutine/OS-thread migration is harmless.  Calls are synchronous.
+ * Errors are negative status codes, never exceptions or aborts; the reference's
+ * panics (index out of range, empty Pop) map to DR_E_INVAL.  dr_last_error()
+ * describes the last failure.
+ *
+ * There is no CPU fallback: dr_create fails with DR_E_HIP when no gfx950
+ * device is usable.
+ *
+ * Vertex ids travel as int32 pairs {round, source} (vertexID,
+ * process/process.go:20-23).  Waves are 1-based; round(w, k) = 4(w-1)+k
+ * (waveRound, process.go:400-402); the leader of every wave is source 1
+ * (chooseLeader, process.go:390-392).
+ */
+#ifndef DAGRIDER_GPU_H
+#define DAGRIDER_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DR_ABI_VERSION 1
+
+enum {
+  DR_OK = 0,
+  DR_E_INVAL = -1,    /* bad argument / reference would panic */
+  DR_E_CAPACITY = -2, /* output buffer too small; required size reported */
+  DR_E_HIP = -3,      /* device / runtime failure */
+  DR_E_RCCL = -4,     /* collective failure */
+  DR_E_CONTRACT = -5, /* DAG outside the mirrored contract (see dr_append_rounds_lists) */
+  DR_E_STATE = -6     /* call order violated (e.g. append not contiguous) */
+};
+enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
+enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
+
+typedef struct dr_ctx dr_ctx;
+
+int dr_abi_version(void);
+
+/* New(index, faulty, tp) (process.go:34-60) minus the protocol state: one
+ * device mirror of Process.dag (process.go:79) for n processes (sources
+ * 1..n, n <= 2048), faulty = f (2f+1 thresholds, process.go:337).
+ * max_rounds bounds the rounds that may be appended (device memory is sized
+ * from it).  device >= 0 is a HIP ordinal. */
+int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx **out);
+void dr_destroy(dr_ctx *ctx);
+const char *dr_last_error(const dr_ctx *ctx);
+/* number of rounds currently mirrored (len(p.dag)) */
+int dr_num_rounds(const dr_ctx *ctx);
+
+/* p.dag[r] = append(p.dag[r], v) (process.go:229) for whole rounds
+ * [r0, r0+k), r0 == dr_num_rounds(ctx): the flattened [][]vertex.
+ *   slot_off   [k+1]   slots of round r0+i: [slot_off[i], slot_off[i+1])
+ *   slot_id    [2*S]   vertex id per slot, in insertion order
+ *   strong_off [S+1], strong_ids [2*E]   strongEdges per slot
+ *   weak_off   [S+1], weak_ids   [2*E']  weakEdges per slot
+ * Contract (else DR_E_CONTRACT): a slot's id is (r, s), 1 <= s <= n, unique in
+ * its round (round 0 may repeat ids), or the zero id {0,0} with no edges (the
+ * Figure-1 ghost slot, process_internal_test.go:91); strong edges target
+ * (r-1, t), weak edges (r', t) with r' < r-1; 1 <= t <= n.  Targets need not
+ * exist (a dangling target counts as reached, process.go:123,136). */
+int dr_append_rounds_lists(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off,
+                           const int32_t *slot_id, const uint32_t *strong_off,
+                           const int32_t *strong_ids, const uint32_t *weak_off,
+                           const int32_t *weak_ids);
+
+/* Same, pre-packed (the layout of dagrider_gen.h; W = ceil(n/64)):
+ *   slot_src [slot_off[k]] source per slot (0 = ghost)
+ *   strong   [k*n*W]  row of (r0+i, s) at (i*n + s-1)*W, zero for absent s
+ *   weak_off [k*n+1]  relative offsets into weak_tgt (weak_off[0] may be != 0)
+ *   weak_tgt          (round << 11) | (source-1) */
+int dr_append_rounds_packed(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off,
+                            const uint16_t *slot_src, const uint64_t *strong,
+                            const uint32_t *weak_off, const uint32_t *weak_tgt);
+
+/* path(from, to, strongPath) (process.go:89-148) for q queries at once.
+ * out[i] = 1 iff to_i is reachable from from_i (self-path included).
+ * from.round outside the mirrored rounds (Go: index out of range) -> DR_E_INVAL. */
+int dr_path_batch(dr_ctx *ctx, int q, const int32_t *from, const int32_t *to, int strong_only,
+                  uint8_t *out);
+
+/* Reach sets: for each query i, the set of ids reachable from from_i in rounds
+ * [bottom_i, from_i.round], as W-word bitsets per round, round-major from
+ * bottom_i, concatenated over queries (words_needed written to *out_words). */
+int dr_reach_sets(dr_ctx *ctx, int q, const int32_t *from, const int32_t *bottom, int strong_only,
+                  uint64_t *out, size_t cap_words, size_t *out_words);
+
+/* The commit decision of waveReady (process.go:326-339) for waves w0..w1:
+ * commit[i] = leader exists && vcount >= 2f+1; vcount[i] = number of slots of
+ * round(w,4) with a strong path to the leader, -1 when the leader is bottom. */
+int dr_wave_commit(dr_ctx *ctx, int w0, int w1, uint8_t *commit, int32_t *vcount);
+
+/* waveReady(wave) (process.go:314-354) given decidedWave: commit decision and,
+ * on commit, the leaders pushed onto leadersStack in push order (as waves),
+ * leader first, then each w' in wave-1..decided_wave+1 strongly reachable from
+ * the last pushed leader. */
+int dr_wave_ready(dr_ctx *ctx, int wave, int decided_wave, uint8_t *commit, int32_t *vcount,
+                  int32_t *pushed_waves, int cap, int *n_pushed);
+
+/* orderVertices() (process.go:404-443) with leadersStack = stack_rs (bottom to
+ * top, ids) and p.round = cur_round.  Pops run top first; each delivers, in
+ * (round asc, slot asc) order over rounds 1..cur_round, every vertex reachable
+ * from the popped leader -- all of them in DR_DELIVER_REF (the reference's
+ * no-op filter, :423-427) or only those not delivered by an earlier pop of
+ * this call in DR_DELIVER_PAPER (Alg. 3 line 54).  out_ids (may be NULL)
+ * receives up to cap ids; *out_n = total delivered.  pop_count / pop_digest
+ * (length nstack, may be NULL): per pop count and order-sensitive digest
+ * sum_k mix(id_k, k). */
+int dr_order_vertices(dr_ctx *ctx, const int32_t *stack_rs, int nstack, int cur_round, int mode,
+                      int32_t *out_ids, size_t cap, size_t *out_n, uint64_t *pop_count,
+                      uint64_t *pop_digest);
+
+/* Whole replay (the wiring the reference omits): for
+ * w = 1..nwaves, waveReady(w) and on commit orderVertices with
+ * p.round = round(w,4); decidedWave stays 0 (DR_CHAIN_LITERAL, Q1) or becomes
+ * the committed wave (DR_CHAIN_PERSISTENT). */
+typedef struct {
+  /* per wave (length nwaves) */
+  uint8_t *commit;
+  int32_t *vcount;
+  /* pushed leaders, push order; wave w's are push_wave[push_off[w-1] .. push_off[w]) */
+  uint32_t *push_off; /* nwaves + 1 */
+  int32_t *push_wave;
+  int64_t push_cap;
+  /* per pop, global pop order (length >= total pushes) */
+  uint64_t *pop_count;
+  uint64_t *pop_digest;
+  uint64_t *pop_edges;
+  /* optional delivered ids (2 int32 each), may be NULL */
+  int32_t *ids;
+  int64_t ids_cap;
+  /* results */
+  int64_t n_push;
+  int64_t n_ids;
+  uint64_t commit_edges, chain_edges, deliver_edges;
+  /* device time (ms) of each phase of the last call, HIP events */
+  float ms_commit, ms_chain, ms_deliver, ms_emit;
+  /* work actually done by the delivery sweeps (identical leaders share one
+   * sweep): weak edges expanded, distinct sweeps, rounds swept, vertices expanded */
+  uint64_t sweep_weak_edges, sweep_count, sweep_rounds, sweep_vertices;
+} dr_replay_out;
+
+int dr_replay(dr_ctx *ctx, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

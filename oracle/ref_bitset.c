@@ -1,0 +1,325 @@
+/*
+ * ref_bitset.c -- packed-bitset CPU restatement of the same hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Same outputs as ref_literal.c on
+ * contract DAGs (strong edges target round r-1, weak edges rounds < r-1,
+ * no duplicate ids in a round >= 1), computed by round sweeps:
+ *   path(from,to)   process.go:89-148  -> forward sweep from `from`, bit test
+ *   waveReady       process.go:314-354 -> backward strong sweep from the
+ *                   leader over rounds 4w-2..4w; chain = one forward strong
+ *                   sweep that restarts at every pushed leader
+ *   orderVertices   process.go:404-443 -> forward strong+weak cone sweep per
+ *                   pop, then (round asc, slot asc) emission
+ * OpenMP parallelises over independent waves / chains / pops.
+ */
+#include "oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static inline const uint64_t *row_of(const or_pdag *p, int r, int s0) {
+  return p->strong + ((size_t)r * p->n + s0) * p->W;
+}
+static inline int present(const or_pdag *p, int r, int src) {
+  for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++)
+    if (p->slot_src[i] == src) return 1;
+  return 0;
+}
+static inline int popc(uint64_t x) { return __builtin_popcountll(x); }
+
+/* Forward sweep from (top, src0) down to `bottom`.  masks: (top-bottom+1)*W
+ * words, round r at (r-bottom)*W, caller-zeroed, bit src0 seeded by caller.
+ * Rows of rounds > bottom are expanded; `prune` (paper mode) holds the
+ * delivered set per round (same indexing, NULL = none): pruned bits are
+ * removed from the frontier before expansion.  Returns edges traversed. */
+static uint64_t sweep(const or_pdag *p, int top, int bottom, int strong_only, uint64_t *masks,
+                      const uint64_t *prune_base) {
+  const int W = p->W, n = p->n;
+  uint64_t edges = 0;
+  for (int r = top; r > bottom; r--) {
+    uint64_t *F = masks + (size_t)(r - bottom) * W;
+    if (prune_base) {
+      const uint64_t *D = prune_base + (size_t)r * W;
+      for (int w = 0; w < W; w++) F[w] &= ~D[w];
+    }
+    uint64_t *N = F - W;
+    for (int w = 0; w < W; w++) {
+      uint64_t x = F[w];
+      while (x) {
+        int b = __builtin_ctzll(x);
+        x &= x - 1;
+        int s0 = w * 64 + b;
+        if (s0 >= n) continue;
+        const uint64_t *row = row_of(p, r, s0);
+        for (int k = 0; k < W; k++) { N[k] |= row[k]; edges += (uint64_t)popc(row[k]); }
+        if (!strong_only) {
+          size_t g = (size_t)r * n + s0;
+          for (uint32_t e = p->weak_off[g]; e < p->weak_off[g + 1]; e++) {
+            uint32_t t = p->weak_tgt[e];
+            int tr = (int)(t >> 11), ts = (int)(t & 2047u);
+            edges++;
+            if (tr < bottom) continue;
+            masks[(size_t)(tr - bottom) * W + (ts >> 6)] |= 1ULL << (ts & 63);
+          }
+        }
+      }
+    }
+  }
+  if (prune_base && top >= bottom) {
+    uint64_t *F = masks;
+    const uint64_t *D = prune_base + (size_t)bottom * W;
+    for (int w = 0; w < W; w++) F[w] &= ~D[w];
+  }
+  return edges;
+}
+
+int or_bs_cone(const or_pdag *p, or_vid from, int bottom, int strong_only, uint64_t *masks,
+               uint64_t *edges) {
+  if (from.round < 0 || from.round >= p->nrounds || bottom < 0 || bottom > from.round) return OR_PANIC;
+  size_t nw = (size_t)(from.round - bottom + 1) * p->W;
+  memset(masks, 0, nw * sizeof(uint64_t));
+  uint64_t e = 0;
+  if (from.source >= 1 && from.source <= p->n) {
+    masks[(size_t)(from.round - bottom) * p->W + ((from.source - 1) >> 6)] |= 1ULL << ((from.source - 1) & 63);
+    e = sweep(p, from.round, bottom, strong_only, masks, NULL);
+  }
+  if (edges) *edges = e;
+  return 0;
+}
+
+/* process.go:89-148 path() by bitset reachability */
+int or_bs_path(const or_pdag *p, or_vid from, or_vid to, int strong_path) {
+  if (from.round == to.round && from.source == to.source) return 1;
+  if (from.round < 0 || from.round >= p->nrounds) return OR_PANIC;
+  if (to.round < 0 || to.round >= from.round || to.source < 1 || to.source > p->n) return 0;
+  uint64_t *m = (uint64_t *)calloc((size_t)(from.round - to.round + 1) * p->W, sizeof(uint64_t));
+  or_bs_cone(p, from, to.round, strong_path, m, NULL);
+  int hit = (int)((m[(to.source - 1) >> 6] >> ((to.source - 1) & 63)) & 1);
+  free(m);
+  return hit;
+}
+
+/* waveReady commit decision for one wave: backward strong sweep from the
+ * leader (source 1 of round 4w-3).  vcount = #slots of round 4w with a strong
+ * path to the leader (process.go:331-336).  -1 when the leader is absent. */
+static int commit_one(const or_pdag *p, int faulty, int w, uint8_t *commit, int32_t *vcount,
+                      uint64_t *edges) {
+  const int W = p->W, n = p->n;
+  int r1 = 4 * (w - 1) + 1;
+  if (w < 1 || r1 + 3 >= p->nrounds) return OR_PANIC;
+  *edges = 0;
+  if (!present(p, r1, 1)) { *commit = 0; *vcount = -1; return 0; }
+  uint64_t S[64], T[64]; /* W <= 32 */
+  memset(S, 0, sizeof S);
+  S[0] = 1;
+  for (int r = r1 + 1; r <= r1 + 3; r++) {
+    memset(T, 0, sizeof T);
+    for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++) {
+      int src = p->slot_src[i];
+      if (src == 0) continue;
+      const uint64_t *row = row_of(p, r, src - 1);
+      int hit = 0;
+      for (int k = 0; k < W; k++) { hit |= (row[k] & S[k]) != 0; *edges += (uint64_t)popc(row[k]); }
+      if (hit) T[(src - 1) >> 6] |= 1ULL << ((src - 1) & 63);
+    }
+    memcpy(S, T, sizeof S);
+  }
+  (void)n;
+  int vc = 0;
+  for (int k = 0; k < W; k++) vc += popc(S[k]);
+  *vcount = vc;
+  *commit = vc >= 2 * faulty + 1;
+  return 0;
+}
+
+int or_bs_commit_sweep(const or_pdag *p, int faulty, int w0, int w1, uint8_t *commit,
+                       int32_t *vcount, uint64_t *edges) {
+  int bad = 0;
+  uint64_t tot = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : tot) reduction(| : bad)
+  for (int w = w0; w <= w1; w++) {
+    uint64_t e = 0;
+    if (commit_one(p, faulty, w, &commit[w - w0], &vcount[w - w0], &e) < 0) bad = 1;
+    tot += e;
+  }
+  if (edges) *edges = tot;
+  return bad ? OR_PANIC : 0;
+}
+
+/* Leader chain of a commit at wave w (process.go:341-350): one forward strong
+ * sweep from round 4w-3 down to round(floor+1, 1), restarting the frontier at
+ * every leader it reaches.  Writes pushed waves (push order) to out. */
+static int chain_one(const or_pdag *p, int w, int floor_w, int32_t *out, uint64_t *edges) {
+  const int W = p->W, n = p->n;
+  int top = 4 * (w - 1) + 1, bottom = 4 * floor_w + 1;
+  int np = 0;
+  out[np++] = w;
+  uint64_t F[64], N[64];
+  memset(F, 0, sizeof F);
+  F[0] = 1;
+  uint64_t e = 0;
+  for (int r = top;; r--) {
+    if (r < top && ((r - 1) & 3) == 0) {
+      int w2 = (r - 1) / 4 + 1;
+      if ((F[0] & 1) && present(p, r, 1)) {
+        out[np++] = w2;
+        memset(F, 0, sizeof F);
+        F[0] = 1;
+      }
+    }
+    if (r <= bottom) break;
+    memset(N, 0, sizeof N);
+    int any = 0;
+    for (int k = 0; k < W; k++) {
+      uint64_t x = F[k];
+      while (x) {
+        int b = __builtin_ctzll(x);
+        x &= x - 1;
+        int s0 = k * 64 + b;
+        if (s0 >= n) continue;
+        const uint64_t *row = row_of(p, r, s0);
+        for (int j = 0; j < W; j++) { N[j] |= row[j]; e += (uint64_t)popc(row[j]); }
+      }
+    }
+    for (int k = 0; k < W; k++) { F[k] = N[k]; any |= N[k] != 0; }
+    if (!any) break;
+  }
+  *edges = e;
+  return np;
+}
+
+typedef struct { int leader_wave, cur_round, pop_index; } pop_t;
+
+static void emit_pop(const or_pdag *p, const uint64_t *masks, int bottom, int top, int cur_round,
+                     uint64_t *count, uint64_t *digest, or_vid *ids, int64_t ids_cap, int64_t *ids_n) {
+  const int W = p->W;
+  uint64_t k = 0, dg = 0;
+  int last = cur_round < top ? cur_round : top;
+  for (int r = 1; r <= last; r++) {
+    if (r < bottom) continue;
+    const uint64_t *F = masks + (size_t)(r - bottom) * W;
+    for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++) {
+      int s = p->slot_src[i];
+      if (s == 0) continue; /* ghost {0,0}: never reachable (no edge targets source 0) */
+      if (!((F[(s - 1) >> 6] >> ((s - 1) & 63)) & 1)) continue;
+      dg += or_digest_term(r, s, k);
+      if (ids) {
+        if (*ids_n < ids_cap) { ids[*ids_n].round = r; ids[*ids_n].source = s; }
+        (*ids_n)++;
+      }
+      k++;
+    }
+  }
+  *count = k;
+  *digest = dg;
+}
+
+int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode, int deliver_mode,
+                 int nthreads, or_replay_out *o) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+  (void)nthreads;
+#endif
+  const int W = p->W;
+  o->n_ids = 0;
+  o->commit_edges = o->chain_edges = o->deliver_edges = 0;
+  int rc = or_bs_commit_sweep(p, faulty, 1, nwaves, o->commit, o->vcount, &o->commit_edges);
+  if (rc) return rc;
+  /* chains: independent given the commit bits */
+  int *cw = (int *)malloc((size_t)(nwaves + 1) * sizeof(int));
+  int *cfloor = (int *)malloc((size_t)(nwaves + 1) * sizeof(int));
+  int nc = 0, last = 0;
+  for (int w = 1; w <= nwaves; w++)
+    if (o->commit[w - 1]) {
+      cw[nc] = w;
+      cfloor[nc] = chain_mode == OR_CHAIN_PERSISTENT ? last : 0;
+      nc++;
+      last = w;
+    }
+  int32_t *pushbuf = (int32_t *)malloc((size_t)nc * (nwaves + 1) * sizeof(int32_t) + 4);
+  int *npush = (int *)calloc((size_t)nc + 1, sizeof(int));
+  uint64_t chain_e = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : chain_e)
+  for (int c = 0; c < nc; c++) {
+    uint64_t e = 0;
+    npush[c] = chain_one(p, cw[c], cfloor[c], pushbuf + (size_t)c * (nwaves + 1), &e);
+    chain_e += e;
+  }
+  o->chain_edges = chain_e;
+  /* push lists + pop schedule */
+  int64_t tot = 0;
+  for (int c = 0; c < nc; c++) tot += npush[c];
+  if (tot > o->push_cap) { free(cw); free(cfloor); free(pushbuf); free(npush); return OR_PANIC; }
+  pop_t *pops = (pop_t *)malloc((size_t)(tot + 1) * sizeof(pop_t));
+  int64_t np = 0, npop = 0;
+  for (int w = 1, c = 0; w <= nwaves; w++) {
+    o->push_off[w - 1] = (uint32_t)np;
+    if (c < nc && cw[c] == w) {
+      const int32_t *pb = pushbuf + (size_t)c * (nwaves + 1);
+      for (int i = 0; i < npush[c]; i++) o->push_wave[np++] = pb[i];
+      for (int i = npush[c] - 1; i >= 0; i--) {
+        pops[npop].leader_wave = pb[i];
+        pops[npop].cur_round = 4 * w;
+        pops[npop].pop_index = (int)npop;
+        npop++;
+      }
+      c++;
+    }
+  }
+  o->push_off[nwaves] = (uint32_t)np;
+  o->n_push = np;
+  uint64_t del_e = 0;
+  if (deliver_mode == OR_DELIVER_REF && !o->ids) {
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : del_e)
+    for (int64_t j = 0; j < npop; j++) {
+      int top = 4 * (pops[j].leader_wave - 1) + 1;
+      uint64_t *m = (uint64_t *)calloc((size_t)(top + 1) * W, sizeof(uint64_t));
+      or_vid from = {top, 1};
+      uint64_t e = 0;
+      or_bs_cone(p, from, 0, 0, m, &e);
+      emit_pop(p, m, 0, top, pops[j].cur_round, &o->pop_count[j], &o->pop_digest[j], NULL, 0, NULL);
+      o->pop_edges[j] = e;
+      del_e += e;
+      free(m);
+    }
+  } else {
+    /* sequential: needed for the ids list order and for paper-mode dedup */
+    uint64_t *D = NULL;
+    if (deliver_mode == OR_DELIVER_PAPER) D = (uint64_t *)calloc((size_t)p->nrounds * W, sizeof(uint64_t));
+    for (int64_t j = 0; j < npop; j++) {
+      int top = 4 * (pops[j].leader_wave - 1) + 1;
+      uint64_t *m = (uint64_t *)calloc((size_t)(top + 1) * W, sizeof(uint64_t));
+      m[(size_t)top * W] |= 1ULL;
+      uint64_t e = sweep(p, top, 0, 0, m, D);
+      emit_pop(p, m, 0, top, pops[j].cur_round, &o->pop_count[j], &o->pop_digest[j], o->ids,
+               o->ids_cap, &o->n_ids);
+      if (D) { /* delivered := delivered U (new cone restricted to present, rounds 1..cur) */
+        int lastr = pops[j].cur_round < top ? pops[j].cur_round : top;
+        for (int r = 1; r <= lastr; r++)
+          for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++) {
+            int s = p->slot_src[i];
+            if (s == 0) continue;
+            uint64_t bit = 1ULL << ((s - 1) & 63);
+            if (m[(size_t)r * W + ((s - 1) >> 6)] & bit) D[(size_t)r * W + ((s - 1) >> 6)] |= bit;
+          }
+        /* edges: only the expanded (new) vertices of rounds >= 1 count, which
+         * sweep() already restricted by pruning; round-0 bits expand nothing */
+      }
+      o->pop_edges[j] = e;
+      del_e += e;
+      free(m);
+    }
+    free(D);
+  }
+  o->deliver_edges = del_e;
+  free(pops);
+  free(cw);
+  free(cfloor);
+  free(pushbuf);
+  free(npush);
+  return 0;
+}

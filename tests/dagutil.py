@@ -1,0 +1,74 @@
+"""Test-side DAG builders.
+
+``random_dag`` draws *unconstrained* contract DAGs (any strong-edge density, so
+partial quorums, non-commits and leader-chain pushes are common; dangling strong
+targets; ghost {0,0} slots; weak edges of any depth).  The product's generator
+(dag_rider_amd.gen) only emits quorum-shaped DAGs, where every present leader
+commits and chains are empty.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+from dag_rider_amd.dag import PackedDag, Vertex, VertexID
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def random_dag(rng: np.random.Generator, n: int, R: int, p_present=0.8, p_s=0.5, p_w=0.1, max_depth=6,
+               dangling=0.05, ghosts=0.1, leader_p=0.85) -> PackedDag:
+    W = (n + 63) // 64
+    NR = R + 1
+    slot_off = [0]
+    slot_src = []
+    strong = np.zeros(NR * n * W, dtype=np.uint64)
+    pres = np.zeros((NR, n), dtype=bool)
+    weak_lists = [[] for _ in range(NR * n)]
+    for r in range(NR):
+        if r == 0:
+            p = np.ones(n, dtype=bool)
+        else:
+            p = rng.random(n) < p_present
+            if (r - 1) % 4 == 0:
+                p[0] = rng.random() < leader_p
+        pres[r] = p
+        srcs = [s + 1 for s in range(n) if p[s]]
+        rng.shuffle(srcs)
+        if ghosts and rng.random() < ghosts:
+            srcs.insert(int(rng.integers(0, len(srcs) + 1)), 0)
+        slot_src += srcs
+        slot_off.append(len(slot_src))
+        if r == 0:
+            continue
+        for s in range(n):
+            if not p[s]:
+                continue
+            for t in range(n):
+                if (pres[r - 1][t] and rng.random() < p_s) or (not pres[r - 1][t] and rng.random() < dangling):
+                    o = (r * n + s) * W + t // 64
+                    strong[o] |= np.uint64(1 << (t % 64))
+            if r >= 2 and p_w > 0:
+                for r2 in range(max(0, r - max_depth), r - 1):
+                    for t in range(n):
+                        if rng.random() < p_w / n * 2:
+                            weak_lists[r * n + s].append((r2 << 11) | t)
+    weak_off = np.zeros(NR * n + 1, dtype=np.uint32)
+    acc = 0
+    for i, l in enumerate(weak_lists):
+        weak_off[i] = acc
+        acc += len(l)
+    weak_off[-1] = acc
+    weak_tgt = np.asarray([t for l in weak_lists for t in l], dtype=np.uint32)
+    return PackedDag(n, NR, np.asarray(slot_off, np.uint32), np.asarray(slot_src, np.uint16), strong, weak_off,
+                     weak_tgt)
+
+
+def figure1():
+    with open(os.path.join(GOLDEN, "figure1.json")) as f:
+        g = json.load(f)
+    dag = [[Vertex(VertexID(*v["id"]), b"", [VertexID(*e) for e in v["strong"]],
+                   [VertexID(*e) for e in v["weak"]]) for v in rnd] for rnd in g["rounds"]]
+    return g, dag

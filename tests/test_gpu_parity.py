@@ -1,0 +1,203 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bar: bit-exact for every output (commit bits, vote counts, pushed leaders, delivered
+order via full id lists or count+digest, edges traversed, reach sets).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from dag_rider_amd import _lib as L
+from dag_rider_amd.dag import pack_lists
+from dag_rider_amd.engine import Engine
+from dag_rider_amd.gen import CONFIGS, generate
+from dagutil import figure1, random_dag
+
+pytestmark = pytest.mark.gpu
+
+
+# --------------------------------------------------------------------------- Figure-1
+def test_figure1_testpath(gpu_device):
+    """TestPath (process_internal_test.go:8-84) through dr_append_rounds_lists + dr_path_batch."""
+    g, dag = figure1()
+    with Engine(g["n"], g["faulty"], 8, gpu_device) as e:
+        e.append_lists(dag)
+        for t in g["test_path"]:
+            got = e.path_batch([(tuple(t["from"]), tuple(t["to"]))], t["strong"])[0]
+            assert bool(got) == t["want"], t
+
+
+def test_figure1_allpairs(gpu_device):
+    g, dag = figure1()
+    ids = [tuple(x) for x in g["allpairs_ids"]]
+    pairs = [(a, b) for a in ids for b in ids]
+    with Engine(g["n"], g["faulty"], 8, gpu_device) as e:
+        e.append_lists(dag)
+        for key, strong in (("strong", True), ("any", False)):
+            got = e.path_batch(pairs, strong).reshape(len(ids), len(ids))
+            assert (got == np.asarray(g["allpairs"][key], dtype=np.uint8)).all(), key
+
+
+def test_figure1_wave_ready_and_order(gpu_device):
+    g, dag = figure1()
+    d = g["derived"]
+    with Engine(g["n"], g["faulty"], 8, gpu_device) as e:
+        e.append_lists(dag)
+        commit, vcount, pushed = e.wave_ready(1, 0)
+        assert (commit, vcount) == (d["wave_ready_1"]["commit"], d["wave_ready_1"]["vcount"])
+        assert pushed == []
+        for case in d["order_vertices"]:
+            ids, cnt, dg = e.order_vertices([tuple(x) for x in case["stack"]], case["p_round"])
+            assert ids.tolist() == case["want"]
+            assert int(cnt[0]) == len(case["want"])
+            assert int(dg[0]) == oracle.digest([tuple(x) for x in case["want"]])
+        # strong reach set of (4,1) down to round 0
+        (m,) = e.reach_sets([(4, 1)], [0], True)
+        got = [[r, s] for r in range(5) for s in range(1, 5) if (int(m[r][0]) >> (s - 1)) & 1]
+        assert got == d["strong_reach_4_1"]
+
+
+def test_figure1_multi_pop_stack(gpu_device):
+    """LIFO pops (stack/stack.go:23-28), ref (no dedup, Q2) vs paper (dedup) modes."""
+    g, dag = figure1()
+    ld = oracle.LDag(arrays=__import__("dag_rider_amd").flatten_lists(dag))
+    stack = [(1, 1), (3, 3), (4, 1)]
+    with Engine(g["n"], g["faulty"], 8, gpu_device) as e:
+        e.append_lists(dag)
+        for mode in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+            ids, cnt, dg = e.order_vertices(stack, 4, mode)
+            rc, want, wc, wd = ld.order_vertices(stack, 4, mode)
+            assert rc == 0
+            assert ids.tolist() == want.tolist()
+            assert cnt.tolist() == wc.tolist() and dg.tolist() == wd.tolist()
+
+
+# --------------------------------------------------------------------------- random DAGs
+def _compare_replay(a, b, ids=True):
+    assert (a.commit == b.commit).all()
+    assert (a.vcount == b.vcount).all()
+    assert (a.push_off == b.push_off).all()
+    assert (a.push_wave == b.push_wave).all()
+    assert (a.pop_count == b.pop_count).all()
+    assert (a.pop_digest == b.pop_digest).all()
+    assert (a.pop_edges == b.pop_edges).all()
+    assert a.commit_edges == b.commit_edges
+    assert a.deliver_edges == b.deliver_edges
+    if ids:
+        assert (a.ids == b.ids).all()
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_dag_replay(gpu_device, seed):
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.choice([1, 3, 4, 7, 10, 63, 64, 65, 100, 130, 200, 257, 300]))
+    R = int(rng.integers(4, 41))
+    d = random_dag(rng, n, R, p_present=rng.uniform(0.5, 1), p_s=rng.uniform(0.05, 0.9), p_w=rng.uniform(0, 1),
+                   max_depth=int(rng.integers(2, 40)))
+    f = int(rng.integers(0, (n - 1) // 3 + 2))
+    nw = R // 4
+    bs = oracle.PDag(d)
+    with Engine(n, f, R + 1, gpu_device) as e:
+        # append in two chunks: exercises the append-only mirror
+        cut = int(rng.integers(1, R + 1))
+        e.append_packed(d, 0, cut)
+        e.append_packed(d, cut, d.nrounds)
+        for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+            for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+                want = bs.replay(f, nw, cm, dm, ids_cap=1 << 20)
+                assert want.rc == 0
+                got = e.replay(nw, cm, dm, ids_cap=1 << 20)
+                _compare_replay(got, want)
+                assert got.chain_edges == want.chain_edges
+                got2 = e.replay(nw, cm, dm)  # no ids: REF mode dedups identical leaders
+                _compare_replay(got2, want, ids=False)
+        # path(): all pairs over a sample
+        ids = [(r, s) for r in range(R + 1) for s in range(0, n + 1)]
+        samp = [ids[i] for i in rng.choice(len(ids), size=min(len(ids), 40), replace=False)]
+        pairs = [(a, b) for a in samp for b in samp]
+        for strong in (True, False):
+            got = e.path_batch(pairs, strong)
+            want = np.asarray([bs.path(a, b, strong) for a, b in pairs], dtype=np.uint8)
+            assert (got == want).all()
+        # reach sets
+        froms = [samp[i] for i in range(min(8, len(samp))) if samp[i][1] >= 1]
+        if froms:
+            bottoms = [int(rng.integers(0, fr[0] + 1)) for fr in froms]
+            for strong in (True, False):
+                got = e.reach_sets(froms, bottoms, strong)
+                for fr, bt, m in zip(froms, bottoms, got):
+                    want, _ = bs.cone(fr, bt, strong)
+                    assert (m == want).all()
+
+
+def test_list_and_packed_append_agree(gpu_device):
+    rng = np.random.default_rng(7)
+    d = random_dag(rng, 9, 20, ghosts=0.3)
+    lists = d.to_lists()
+    d2 = pack_lists(lists, 9)
+    with Engine(9, 2, 21, gpu_device) as a, Engine(9, 2, 21, gpu_device) as b:
+        a.append_packed(d)
+        b.append_lists(lists)
+        ra, rb = a.replay(5, ids_cap=1 << 16), b.replay(5, ids_cap=1 << 16)
+        _compare_replay(ra, rb)
+    assert (d2.strong == d.strong).all() and (d2.slot_src == d.slot_src).all()
+
+
+# --------------------------------------------------------------------------- configs
+@pytest.mark.parametrize("name", ["c1", "c2", "c5"])
+def test_config_replay(gpu_device, name):
+    cfg = CONFIGS[name]
+    d = generate(cfg)
+    bs = oracle.PDag(d)
+    with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
+        e.append_packed(d)
+        for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+            want = bs.replay(cfg.faulty, cfg.nwaves, cm, L.DR_DELIVER_REF)
+            got = e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF)
+            _compare_replay(got, want, ids=False)
+            assert got.chain_edges == want.chain_edges
+        want = bs.replay(cfg.faulty, cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_PAPER)
+        got = e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_PAPER)
+        _compare_replay(got, want, ids=False)
+
+
+def test_c1_literal_ids(gpu_device):
+    """C1 seeded n=4: full delivered sequence against the literal restatement."""
+    cfg = CONFIGS["c1"]
+    d = generate(cfg)
+    lit = oracle.LDag(packed=d)
+    with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
+        e.append_packed(d)
+        for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+            for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+                want = lit.replay(cfg.faulty, cfg.nwaves, cm, dm, ids_cap=1 << 16)
+                got = e.replay(cfg.nwaves, cm, dm, ids_cap=1 << 16)
+                _compare_replay(got, want)
+
+
+# --------------------------------------------------------------------------- errors
+def test_errors(gpu_device):
+    g, dag = figure1()
+    with Engine(4, 1, 8, gpu_device) as e:
+        e.append_lists(dag)
+        with pytest.raises(L.DrError) as ei:
+            e.path_batch([((9, 1), (1, 1))], True)  # Go: index out of range
+        assert ei.value.code == L.DR_E_INVAL
+        assert e.path_batch([((9, 1), (9, 1))], True)[0] == 1  # self path returns before the lookup
+        with pytest.raises(L.DrError):
+            e.wave_commit(2, 2)  # round(2,1)=5 is not mirrored
+        with pytest.raises(L.DrError) as ei:
+            e.order_vertices([(4, 1)], 5)
+        assert ei.value.code == L.DR_E_INVAL
+    with Engine(4, 1, 8, gpu_device) as e:
+        bad = [list(r) for r in dag]
+        from dag_rider_amd.dag import Vertex, VertexID
+        bad[2] = bad[2] + [Vertex(VertexID(2, 1))]  # duplicate id in a round
+        with pytest.raises(L.DrError) as ei:
+            e.append_lists(bad)
+        assert ei.value.code == L.DR_E_CONTRACT
+        bad = [list(r) for r in dag]
+        bad[3][1] = Vertex(VertexID(3, 1), b"", [VertexID(1, 1)])  # strong edge skipping a round
+        with pytest.raises(L.DrError) as ei:
+            e.append_lists(bad)
+        assert ei.value.code == L.DR_E_CONTRACT
