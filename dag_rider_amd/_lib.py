@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libdagrider_gpu.so")
 DR_OK, DR_E_INVAL, DR_E_CAPACITY, DR_E_HIP, DR_E_RCCL, DR_E_CONTRACT, DR_E_STATE = 0, -1, -2, -3, -4, -5, -6
 DR_CHAIN_LITERAL, DR_CHAIN_PERSISTENT = 0, 1
 DR_DELIVER_REF, DR_DELIVER_PAPER = 0, 1
+DR_OPT_MEMO = 1
 
 P = C.c_void_p
 i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float
@@ -30,7 +31,7 @@ class ReplayOut(C.Structure):
                 ("pop_count", P), ("pop_digest", P), ("pop_edges", P), ("ids", P), ("ids_cap", i64),
                 ("n_push", i64), ("n_ids", i64), ("commit_edges", u64), ("chain_edges", u64),
                 ("deliver_edges", u64), ("ms_commit", f32), ("ms_chain", f32), ("ms_deliver", f32),
-                ("ms_emit", f32), ("sweep_weak_edges", u64), ("sweep_count", u64), ("sweep_rounds", u64),
+                ("ms_emit", f32), ("ms_summary", f32), ("canon_segments", i32), ("sweep_weak_edges", u64), ("sweep_count", u64), ("sweep_rounds", u64),
                 ("sweep_vertices", u64)]
 
 
@@ -41,6 +42,7 @@ SIGNATURES = {
     "dr_destroy": (None, [P]),
     "dr_last_error": (C.c_char_p, [P]),
     "dr_num_rounds": (C.c_int, [P]),
+    "dr_set_option": (C.c_int, [P, C.c_int, C.c_int]),
     "dr_append_rounds_lists": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
     "dr_append_rounds_packed": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "dr_path_batch": (C.c_int, [P, C.c_int, P, P, C.c_int, P]),

@@ -83,6 +83,15 @@ struct dr_ctx {
   std::vector<u64> h_present;
   std::vector<uint64_t> h_deg;  // total strong degree per round
   std::vector<uint32_t> h_weak_roff{0}, h_far_roff{0};
+  // round summaries + canonical cone (memo path), valid for rounds 0..summary_T
+  bool use_memo = true;
+  int summary_T = -1;
+  int32_t canon_segments = 0;
+  DevBuf U, WU, SD, K, good, CE, RD, Cc, Gc, Ec, crbase, ccount, nseg, stops;
+  std::vector<uint64_t> hC, hG, hE;
+  // memo needs every weak edge in the dense summary window
+  bool memo_ok() const { return nfar == 0 && dmax_near <= 17; }
+  int memo_dd() const { return std::max(0, dmax_near - 1); }
   // scratch
   DevBuf q_buf, masks, dlv, push_out, push_n, edges, wedges, hits, commit, vcount, popdesc, rbase, counts,
       digest, pop_pos, ids;
@@ -95,6 +104,16 @@ struct dr_ctx {
     va_end(ap);
     err = buf;
     return code;
+  }
+  dr::MemoView memo_view() const {
+    dr::MemoView m;
+    m.U = U.as<u64>();
+    m.WU = WU.as<u64>();
+    m.SD = SD.as<u64>();
+    m.K = K.as<u64>();
+    m.dd = memo_dd();
+    m.dmax = std::max(1, dmax_near);
+    return m;
   }
   dr::DagView view() const {
     dr::DagView v;
@@ -122,7 +141,7 @@ struct dr_ctx {
     while ((1 << l) < d) l++;
     return l;
   }
-  size_t sweep_lds(int dl) const { return (size_t)(2 * WS + (1 << dl) * WS) * 8 + 32; }
+  size_t sweep_lds(int dl) const { return (size_t)(2 * WS + (1 << dl) * WS) * 8 + 64; }
 };
 
 #define HIPCHK(ctx, call)                                                                   \
@@ -167,6 +186,7 @@ struct SweepArgs {
   int32_t *push_out, *push_n;
   u64 *edges, *wedges;
   uint8_t *hits;
+  int32_t *stops;
 };
 
 template <int WS>
@@ -178,8 +198,8 @@ hipError_t launch_sweep_t(dr_ctx *c, const SweepArgs &a) {
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((dr::k_sweep<WS, NT>), dim3(a.seq ? 1 : a.nq), dim3(NT), lds, c->stream,
-                     c->view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out, a.push_n,
-                     a.edges, a.wedges, a.hits);
+                     c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops);
   return hipGetLastError();
 }
 hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a) {
@@ -198,30 +218,61 @@ hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a) {
 constexpr int kEmitRPB = 16;
 
 template <int WS>
-hipError_t launch_emit_t(dr_ctx *c, int npop, int max_rounds_span, const dr::PopDesc *pd,
-                         u64 *cnt, u64 *dg, const int64_t *pos, int32_t *ids, int64_t cap,
-                         bool count_phase) {
+hipError_t launch_emit_t(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
+                         u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase) {
   if (count_phase) {
-    hipLaunchKernelGGL((dr::k_emit_count<WS, 256>), dim3(npop), dim3(256), 0, c->stream, c->view(),
-                       pd, c->masks.as<u64>(), c->rbase.as<uint32_t>(), cnt);
+    hipLaunchKernelGGL((dr::k_emit_count<WS, 256>), dim3(ndesc), dim3(256), 0, c->stream, c->view(), pd,
+                       c->masks.as<u64>(), c->K.as<u64>(), rbase, cnt);
   } else {
-    const int bx = std::max(1, (max_rounds_span + kEmitRPB - 1) / kEmitRPB);
-    hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(bx, npop), dim3(256), 0, c->stream,
-                       c->view(), c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd,
-                       c->masks.as<u64>(), c->rbase.as<uint32_t>(), pos, dg, ids, cap);
+    const int bx = std::max(1, (span + kEmitRPB - 1) / kEmitRPB);
+    hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(bx, ndesc), dim3(256), 0, c->stream, c->view(),
+                       c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, c->masks.as<u64>(),
+                       c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap);
   }
   return hipGetLastError();
 }
-hipError_t launch_emit(dr_ctx *c, int npop, int span, const dr::PopDesc *pd, u64 *cnt, u64 *dg,
-                       const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase) {
-  if (npop <= 0) return hipSuccess;
+hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
+                       u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase) {
+  if (ndesc <= 0) return hipSuccess;
   switch (c->WS) {
-    case 1: return launch_emit_t<1>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
-    case 2: return launch_emit_t<2>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
-    case 4: return launch_emit_t<4>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
-    case 8: return launch_emit_t<8>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
-    case 16: return launch_emit_t<16>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
-    case 32: return launch_emit_t<32>(c, npop, span, pd, cnt, dg, pos, ids, cap, count_phase);
+    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
+    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
+    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
+    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
+    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
+    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int WS>
+hipError_t launch_summary_t(dr_ctx *c, int T) {
+  constexpr int NT = block_for<WS>();
+  const dr::MemoView mv = c->memo_view();
+  hipLaunchKernelGGL((dr::k_summary<WS, NT>), dim3(T), dim3(NT), 0, c->stream, c->view(), 1, mv.dd,
+                     c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>());
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 255) / 256), dim3(256), 0, c->stream, c->view(), mv, T,
+                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>());
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int dl = c->depth_log2();
+  const size_t lds = c->sweep_lds(dl);
+  e = hipFuncSetAttribute((const void *)dr::k_canon<WS, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_canon<WS, NT>), dim3(1), dim3(NT), lds, c->stream, c->view(), mv, T, dl,
+                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>());
+  return hipGetLastError();
+}
+hipError_t launch_summary(dr_ctx *c, int T) {
+  switch (c->WS) {
+    case 1: return launch_summary_t<1>(c, T);
+    case 2: return launch_summary_t<2>(c, T);
+    case 4: return launch_summary_t<4>(c, T);
+    case 8: return launch_summary_t<8>(c, T);
+    case 16: return launch_summary_t<16>(c, T);
+    case 32: return launch_summary_t<32>(c, T);
   }
   return hipErrorInvalidValue;
 }
@@ -303,7 +354,10 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->weak_roff, &c->far,   &c->far_roff, &c->q_buf,    &c->masks,
                     &c->dlv,     &c->push_out, &c->push_n,  &c->edges,    &c->hits, &c->wedges,
                     &c->commit,  &c->vcount,  &c->popdesc,  &c->rbase,    &c->counts,
-                    &c->digest,  &c->pop_pos, &c->ids};
+                    &c->digest,  &c->pop_pos, &c->ids,      &c->U,        &c->WU,
+                    &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
+                    &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
+                    &c->nseg,    &c->stops};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -429,6 +483,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   c->nfar += fdev.size();
   c->dmax_near = dmax;
   c->nrounds += k;
+  c->summary_T = -1;  // summaries describe the old DAG
   return DR_OK;
 }
 
@@ -494,35 +549,40 @@ extern "C" int dr_append_rounds_lists(dr_ctx *c, int r0, int k, const uint32_t *
 namespace {
 
 // Run sweep queries in batches bounded by the mask budget.  qv: queries with
-// mask_off left relative (filled here per batch when Q_MASKS).  On return the
-// per-query edges / hits / pushes are in host arrays.  If keep_masks, each
-// batch's masks are handed to `on_batch` before the next batch overwrites them.
+// mask_off filled here per batch (Q_MASKS).  On return the per-query edges /
+// hits / pushes / stop rounds are in host arrays.  Each batch's masks are
+// handed to `on_batch` before the next batch overwrites them.  Masks are
+// zeroed unless every query of the batch is a merge sweep (those write every
+// round they report).
 template <class OnBatch>
 int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector<uint64_t> *edges,
-               std::vector<uint64_t> *wedges, std::vector<uint8_t> *hits, std::vector<int32_t> *push_n, int32_t *push_out_dev,
-               OnBatch on_batch, float *ms) {
+               std::vector<uint64_t> *wedges, std::vector<uint8_t> *hits, std::vector<int32_t> *push_n,
+               int32_t *push_out_dev, std::vector<int32_t> *stops, OnBatch on_batch, float *ms) {
   const size_t budget_words = (size_t)1 << 29;  // 4 GiB of frontier masks per batch
   const int WS = c->WS;
   if (edges) edges->assign(qv.size(), 0);
   if (wedges) wedges->assign(qv.size(), 0);
   if (hits) hits->assign(qv.size(), 0);
   if (push_n) push_n->assign(qv.size(), 0);
+  if (stops) stops->assign(qv.size(), 0);
   size_t i0 = 0;
   float total_ms = 0;
   while (i0 < qv.size()) {
     // batch [i0, i1): as many queries as the mask budget allows (sequential
     // mode keeps its order across batches: the delivered set persists)
     size_t i1 = i0, words = 0;
+    bool all_merge = true;
     while (i1 < qv.size()) {
       const size_t w = (qv[i1].flags & dr::Q_MASKS) ? (size_t)(qv[i1].top - qv[i1].bottom + 1) * WS : 0;
       if (i1 > i0 && words + w > budget_words) break;
       qv[i1].mask_off = (int64_t)words;
+      all_merge &= (qv[i1].flags & dr::Q_MERGE) != 0;
       words += w;
       i1++;
     }
     const int nq = (int)(i1 - i0);
     HIPCHK(c, c->masks.ensure(std::max<size_t>(words, 1) * 8));
-    if (words) HIPCHK(c, hipMemsetAsync(c->masks.p, 0, words * 8, c->stream));
+    if (words && !all_merge) HIPCHK(c, hipMemsetAsync(c->masks.p, 0, words * 8, c->stream));
     HIPCHK(c, c->q_buf.ensure((size_t)nq * sizeof(dr::SweepQuery)));
     HIPCHK(c, hipMemcpyAsync(c->q_buf.p, qv.data() + i0, (size_t)nq * sizeof(dr::SweepQuery),
                              hipMemcpyHostToDevice, c->stream));
@@ -530,6 +590,7 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     HIPCHK(c, c->wedges.ensure((size_t)nq * 8));
     HIPCHK(c, c->hits.ensure((size_t)nq));
     HIPCHK(c, c->push_n.ensure((size_t)nq * 4));
+    HIPCHK(c, c->stops.ensure((size_t)nq * 4));
     SweepArgs a;
     a.q = c->q_buf.as<dr::SweepQuery>();
     a.nq = nq;
@@ -541,6 +602,7 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     a.edges = c->edges.as<u64>();
     a.wedges = c->wedges.as<u64>();
     a.hits = c->hits.as<uint8_t>();
+    a.stops = c->stops.as<int32_t>();
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_sweep(c, a));
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
@@ -548,6 +610,7 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     if (wedges) HIPCHK(c, hipMemcpyAsync(wedges->data() + i0, c->wedges.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
     if (hits) HIPCHK(c, hipMemcpyAsync(hits->data() + i0, c->hits.p, (size_t)nq, hipMemcpyDeviceToHost, c->stream));
     if (push_n) HIPCHK(c, hipMemcpyAsync(push_n->data() + i0, c->push_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
+    if (stops) HIPCHK(c, hipMemcpyAsync(stops->data() + i0, c->stops.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float t = 0;
     HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[1]));
@@ -559,53 +622,73 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
   return DR_OK;
 }
 
-// Emission for pops whose masks (round 0 at pd[i].mask_off) are resident.
-// counts/digests per pop to host; ids (optional) at global positions pos0 + ...
-int run_emit(dr_ctx *c, const std::vector<dr::PopDesc> &pd, uint64_t *count_out, uint64_t *digest_out,
-             int32_t *ids_host, int64_t ids_cap, int64_t ids_base, int64_t *ids_total, float *ms) {
-  const int np = (int)pd.size();
-  if (np == 0) return DR_OK;
+// Emission of npop pops from their segments pd (pd[i].out in [0, npop),
+// rbase_off assigned here).  count_out[p] = extra[p] (vertices the caller
+// accounts for, may be null) + the segments' vertices; digest_out[p] = the
+// segments' digest sum.  ids (optional): pop p's vertices at ids_base + the
+// pops before it (then every vertex must be in a segment).
+int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *extra, uint64_t *count_out,
+             uint64_t *digest_out, int32_t *ids_host, int64_t ids_cap, int64_t ids_base, int64_t *ids_total,
+             float *ms) {
+  const int nd = (int)pd.size();
+  std::vector<uint64_t> cnt(npop, 0);
+  if (extra) std::copy(extra, extra + npop, cnt.begin());
+  std::fill(digest_out, digest_out + npop, 0);
+  if (nd == 0) {
+    std::copy(cnt.begin(), cnt.end(), count_out);
+    if (ids_total) { *ids_total = 0; for (auto x : cnt) *ids_total += (int64_t)x; }
+    return DR_OK;
+  }
   int64_t rb_words = 0;
   int span = 0;
-  for (const auto &d : pd) {
-    rb_words = std::max<int64_t>(rb_words, d.rbase_off + d.last + 1);
+  for (auto &d : pd) {
+    d.rbase_off = rb_words;
+    rb_words += d.last + 1;
     span = std::max(span, d.last - d.first + 1);
   }
   HIPCHK(c, c->rbase.ensure((size_t)std::max<int64_t>(rb_words, 1) * 4));
-  HIPCHK(c, c->popdesc.ensure((size_t)np * sizeof(dr::PopDesc)));
-  HIPCHK(c, c->counts.ensure((size_t)np * 8));
-  HIPCHK(c, c->digest.ensure((size_t)np * 8));
-  HIPCHK(c, hipMemcpyAsync(c->popdesc.p, pd.data(), (size_t)np * sizeof(dr::PopDesc), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->digest.p, 0, (size_t)np * 8, c->stream));
+  HIPCHK(c, c->popdesc.ensure((size_t)nd * sizeof(dr::PopDesc)));
+  HIPCHK(c, c->counts.ensure((size_t)nd * 8));
+  HIPCHK(c, c->digest.ensure((size_t)npop * 8));
+  HIPCHK(c, hipMemcpyAsync(c->popdesc.p, pd.data(), (size_t)nd * sizeof(dr::PopDesc), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->digest.p, 0, (size_t)npop * 8, c->stream));
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
-  HIPCHK(c, launch_emit(c, np, span, c->popdesc.as<dr::PopDesc>(), c->counts.as<u64>(), nullptr, nullptr,
-                        nullptr, 0, true));
-  std::vector<uint64_t> cnt(np);
-  HIPCHK(c, hipMemcpyAsync(cnt.data(), c->counts.p, (size_t)np * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, launch_emit(c, nd, span, c->popdesc.as<dr::PopDesc>(), c->rbase.as<uint32_t>(), c->counts.as<u64>(),
+                        nullptr, nullptr, nullptr, nullptr, 0, true));
   int32_t *ids_dev = nullptr;
-  int64_t cap_here = 0;
-  int64_t tot = 0;
-  for (int i = 0; i < np; i++) tot += (int64_t)cnt[i];
+  int64_t cap_here = 0, tot = 0;
   if (ids_host && ids_base < ids_cap) {
+    std::vector<uint64_t> dc(nd);
+    HIPCHK(c, hipMemcpyAsync(dc.data(), c->counts.p, (size_t)nd * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> pc(cnt);
+    for (int i = 0; i < nd; i++) pc[pd[i].out] += dc[i];
+    for (int p = 0; p < npop; p++) tot += (int64_t)pc[p];
     cap_here = std::min<int64_t>(tot, ids_cap - ids_base);
-    std::vector<int64_t> pos(np);
+    std::vector<int64_t> pos(npop);
     int64_t run = 0;
-    for (int i = 0; i < np; i++) { pos[i] = run; run += (int64_t)cnt[i]; }
-    HIPCHK(c, c->pop_pos.ensure((size_t)np * 8));
-    HIPCHK(c, hipMemcpyAsync(c->pop_pos.p, pos.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
+    for (int p = 0; p < npop; p++) { pos[p] = run; run += (int64_t)pc[p]; }
+    HIPCHK(c, c->pop_pos.ensure((size_t)npop * 8));
+    HIPCHK(c, hipMemcpyAsync(c->pop_pos.p, pos.data(), (size_t)npop * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, c->ids.ensure((size_t)std::max<int64_t>(cap_here, 1) * 8));
     ids_dev = c->ids.as<int32_t>();
   }
-  HIPCHK(c, launch_emit(c, np, span, c->popdesc.as<dr::PopDesc>(), nullptr, c->digest.as<u64>(),
-                        ids_dev ? c->pop_pos.as<int64_t>() : nullptr, ids_dev, cap_here, false));
+  HIPCHK(c, launch_emit(c, nd, span, c->popdesc.as<dr::PopDesc>(), c->rbase.as<uint32_t>(), nullptr,
+                        c->digest.as<u64>(), nullptr, ids_dev ? c->pop_pos.as<int64_t>() : nullptr, ids_dev,
+                        cap_here, false));
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
-  HIPCHK(c, hipMemcpyAsync(digest_out, c->digest.p, (size_t)np * 8, hipMemcpyDeviceToHost, c->stream));
+  std::vector<uint64_t> dc(nd);
+  HIPCHK(c, hipMemcpyAsync(dc.data(), c->counts.p, (size_t)nd * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(digest_out, c->digest.p, (size_t)npop * 8, hipMemcpyDeviceToHost, c->stream));
   if (ids_dev && cap_here > 0)
     HIPCHK(c, hipMemcpyAsync(ids_host + 2 * ids_base, ids_dev, (size_t)cap_here * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  std::memcpy(count_out, cnt.data(), (size_t)np * 8);
-  if (ids_total) *ids_total = tot;
+  for (int i = 0; i < nd; i++) cnt[pd[i].out] += dc[i];
+  std::copy(cnt.begin(), cnt.end(), count_out);
+  if (ids_total) {
+    *ids_total = 0;
+    for (auto x : cnt) *ids_total += (int64_t)x;
+  }
   if (ms) {
     float t = 0;
     HIPCHK(c, hipEventElapsedTime(&t, c->ev[2], c->ev[3]));
@@ -614,7 +697,77 @@ int run_emit(dr_ctx *c, const std::vector<dr::PopDesc> &pd, uint64_t *count_out,
   return DR_OK;
 }
 
+// Round summaries + canonical cone + canonical prefixes for rounds 0..T
+// (T = last mirrored round).  Reads every strong row and weak edge once.
+int build_summary(dr_ctx *c, float *ms_summary) {
+  const int T = c->nrounds - 1;
+  const int WS = c->WS, dd = c->memo_dd();
+  const size_t R = (size_t)T + 1;
+  if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
+  HIPCHK(c, c->U.ensure(R * WS * 8));
+  HIPCHK(c, c->WU.ensure(std::max<size_t>(R * dd * WS, 1) * 8));
+  HIPCHK(c, c->SD.ensure(R * 8));
+  HIPCHK(c, c->K.ensure(R * WS * 8));
+  HIPCHK(c, c->good.ensure(R));
+  HIPCHK(c, c->CE.ensure(R * 8));
+  HIPCHK(c, c->RD.ensure(R * 8));
+  HIPCHK(c, c->Cc.ensure(R * 8));
+  HIPCHK(c, c->Gc.ensure(R * 8));
+  HIPCHK(c, c->Ec.ensure(R * 8));
+  HIPCHK(c, c->crbase.ensure((R + 1) * 4));
+  HIPCHK(c, c->ccount.ensure(8));
+  HIPCHK(c, c->nseg.ensure(4));
+  HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+  HIPCHK(c, launch_summary(c, T));
+  HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+  // canonical emission: one segment, rounds 1..T of K; per-round digests
+  dr::PopDesc d{};
+  d.mask_off = 0;
+  d.rbase_off = 0;
+  d.pos0 = 0;
+  d.first = 1;
+  d.last = T;
+  d.out = 0;
+  d.use_k = 1;
+  HIPCHK(c, c->popdesc.ensure(sizeof(dr::PopDesc)));
+  HIPCHK(c, hipMemcpyAsync(c->popdesc.p, &d, sizeof d, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, launch_emit(c, 1, T, c->popdesc.as<dr::PopDesc>(), c->crbase.as<uint32_t>(), c->ccount.as<u64>(),
+                        nullptr, nullptr, nullptr, nullptr, 0, true));
+  HIPCHK(c, launch_emit(c, 1, T, c->popdesc.as<dr::PopDesc>(), c->crbase.as<uint32_t>(), nullptr, nullptr,
+                        c->RD.as<u64>(), nullptr, nullptr, 0, false));
+  hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->crbase.as<uint32_t>(),
+                     c->ccount.as<u64>(), c->RD.as<u64>(), c->CE.as<u64>(), c->Cc.as<u64>(), c->Gc.as<u64>(),
+                     c->Ec.as<u64>());
+  HIPCHK(c, hipGetLastError());
+  c->hC.resize(R);
+  c->hG.resize(R);
+  c->hE.resize(R);
+  HIPCHK(c, hipMemcpyAsync(c->hC.data(), c->Cc.p, R * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->hG.data(), c->Gc.p, R * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->hE.data(), c->Ec.p, R * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&c->canon_segments, c->nseg.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (ms_summary) HIPCHK(c, hipEventElapsedTime(ms_summary, c->ev[6], c->ev[7]));
+  c->summary_T = T;
+  return DR_OK;
+}
+
 }  // namespace
+
+namespace {
+// Summaries usable for this context's current DAG (built lazily / per replay).
+bool summary_fresh(const dr_ctx *c) { return c->use_memo && c->memo_ok() && c->summary_T == c->nrounds - 1; }
+int shortcut_flag(const dr_ctx *c) { return summary_fresh(c) ? dr::Q_SHORTCUT : 0; }
+}  // namespace
+
+extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
+  if (!c) return DR_E_INVAL;
+  if (option == DR_OPT_MEMO) {
+    c->use_memo = value != 0;
+    return DR_OK;
+  }
+  return c->fail(DR_E_INVAL, "unknown option %d", option);
+}
 
 extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_t *to, int strong_only,
                              uint8_t *out) {
@@ -635,15 +788,13 @@ extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_
     sq.top = fr;
     sq.bottom = tr;
     sq.src0 = fs - 1;
-    sq.flags = strong_only ? dr::Q_STRONG_ONLY : dr::Q_MASKS;
+    sq.flags = (strong_only ? dr::Q_STRONG_ONLY : dr::Q_MASKS) | shortcut_flag(c);
     sq.tgt0 = ts - 1;
-    sq.out_off = 0;
-    sq.cur_round = 0;
     qv.push_back(sq);
     idx.push_back(i);
   }
   std::vector<uint8_t> hits;
-  int rc = run_sweeps(c, qv, false, nullptr, nullptr, &hits, nullptr, nullptr,
+  int rc = run_sweeps(c, qv, false, nullptr, nullptr, &hits, nullptr, nullptr, nullptr,
                       [](size_t, size_t) { return 0; }, nullptr);
   if (rc) return rc;
   for (size_t k = 0; k < idx.size(); k++) out[idx[k]] = hits[k];
@@ -673,14 +824,14 @@ extern "C" int dr_reach_sets(dr_ctx *c, int q, const int32_t *from, const int32_
     s.bottom = bottom[i];
     const int fs = from[2 * i + 1];
     s.src0 = (fs >= 1 && fs <= c->n) ? fs - 1 : -1;
-    s.flags = dr::Q_MASKS | (strong_only ? dr::Q_STRONG_ONLY : 0);
+    s.flags = dr::Q_MASKS | (strong_only ? dr::Q_STRONG_ONLY : 0) | shortcut_flag(c);
     s.tgt0 = -1;
     obase[i] = acc;
     acc += (size_t)(s.top - s.bottom + 1) * c->W;
   }
   const int W = c->W, WS = c->WS;
   std::vector<u64> tmp;
-  return run_sweeps(c, qv, false, nullptr, nullptr, nullptr, nullptr, nullptr,
+  return run_sweeps(c, qv, false, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                     [&](size_t i0, size_t i1) -> int {
                       size_t words = 0;
                       for (size_t i = i0; i < i1; i++) words += (size_t)(qv[i].top - qv[i].bottom + 1) * WS;
@@ -743,7 +894,7 @@ int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::
     s.top = 4 * (tasks[i].wave - 1) + 1;
     s.bottom = 4 * tasks[i].floor + 1;
     s.src0 = 0;
-    s.flags = dr::Q_CHAIN | dr::Q_STRONG_ONLY;
+    s.flags = dr::Q_CHAIN | dr::Q_STRONG_ONLY | shortcut_flag(c);
     s.out_off = (int32_t)off;
     s.tgt0 = -1;
     off += tasks[i].wave - tasks[i].floor - 1;
@@ -757,7 +908,7 @@ int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::
   HIPCHK(c, c->push_out.ensure((size_t)std::max<int64_t>(off, 1) * 4));
   std::vector<uint64_t> edges;
   std::vector<int32_t> pn;
-  int rc = run_sweeps(c, qv, false, &edges, nullptr, nullptr, &pn, c->push_out.as<int32_t>(),
+  int rc = run_sweeps(c, qv, false, &edges, nullptr, nullptr, &pn, c->push_out.as<int32_t>(), nullptr,
                       [](size_t, size_t) { return 0; }, ms);
   if (rc) return rc;
   std::vector<int32_t> po((size_t)off);
@@ -773,25 +924,30 @@ int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::
 }
 
 struct Pop { int32_t round, source, cur_round; };
-
-// Deliver pops (in pop order).  REF: every pop's cone independently (identical
-// leaders share one sweep); PAPER: one workgroup walks the pops in order,
-// pruning at delivered vertices.
 struct SweepStats { uint64_t weak_edges = 0, sweeps = 0, rounds = 0, vertices = 0; };
 
+// Deliver pops (in pop order).
+//  REF + fresh summaries: one merge sweep per distinct leader; the cone below
+//    the merge round is the canonical K, counted from the canonical prefixes.
+//  REF otherwise: every distinct leader's cone swept to round 0.
+//  PAPER: one workgroup walks the pops in order, pruning at delivered vertices.
+// With ids requested, sweeps run one per pop in pop order.
 int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pcount, uint64_t *pdigest,
-                uint64_t *pedges, SweepStats *stats, int32_t *ids, int64_t ids_cap, int64_t *ids_total, float *ms_sweep,
-                float *ms_emit) {
+                uint64_t *pedges, SweepStats *stats, int32_t *ids, int64_t ids_cap, int64_t *ids_total,
+                float *ms_sweep, float *ms_emit) {
   const int WS = c->WS;
   if (ms_sweep) *ms_sweep = 0;
   if (ms_emit) *ms_emit = 0;
-  int64_t id_run = 0;
-  if (pops.empty()) { if (ids_total) *ids_total = 0; return DR_OK; }
+  if (stats) *stats = SweepStats{};
+  if (ids_total) *ids_total = 0;
+  if (pops.empty()) return DR_OK;
+  const bool want_ids = ids && ids_cap > 0;
+  const bool paper = mode == DR_DELIVER_PAPER;
+  const bool memo = !paper && summary_fresh(c);
   std::vector<dr::SweepQuery> qv;
   std::vector<int> pop2q(pops.size());
-  const bool want_ids = ids && ids_cap > 0;
-  if (mode == DR_DELIVER_REF && !want_ids) {
-    // unique leaders, longest first
+  if (!paper && !want_ids) {
+    // distinct leaders, longest first
     std::vector<int> order(pops.size());
     for (size_t i = 0; i < pops.size(); i++) order[i] = (int)i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
@@ -806,16 +962,11 @@ int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pco
       }
       dr::SweepQuery s{};
       s.top = p.round;
-      s.bottom = 0;
       s.src0 = (p.source >= 1 && p.source <= c->n) ? p.source - 1 : -1;
-      s.flags = dr::Q_MASKS;
-      s.tgt0 = -1;
       qv.push_back(s);
       pop2q[order[k]] = (int)qv.size() - 1;
     }
   } else {
-    // pop order, one sweep per pop (paper mode's dedup and the id list need it)
-    const bool paper = mode == DR_DELIVER_PAPER;
     if (paper) {
       HIPCHK(c, c->dlv.ensure((size_t)c->nrounds * WS * 8));
       HIPCHK(c, hipMemsetAsync(c->dlv.p, 0, (size_t)c->nrounds * WS * 8, c->stream));
@@ -823,66 +974,105 @@ int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pco
     for (size_t i = 0; i < pops.size(); i++) {
       dr::SweepQuery s{};
       s.top = pops[i].round;
-      s.bottom = 0;
       s.src0 = (pops[i].source >= 1 && pops[i].source <= c->n) ? pops[i].source - 1 : -1;
-      s.flags = dr::Q_MASKS | (paper ? dr::Q_PRUNE : 0);
-      s.tgt0 = -1;
       s.cur_round = pops[i].cur_round;
       qv.push_back(s);
       pop2q[i] = (int)i;
     }
   }
-  // q -> pops that use it
+  for (auto &s : qv) {
+    s.bottom = 0;
+    s.tgt0 = -1;
+    s.flags = dr::Q_MASKS | (paper ? dr::Q_PRUNE : 0) | (memo ? (dr::Q_SHORTCUT | dr::Q_MERGE) : 0);
+  }
   std::vector<std::vector<int>> q2pop(qv.size());
   for (size_t i = 0; i < pops.size(); i++) q2pop[pop2q[i]].push_back((int)i);
   std::vector<uint64_t> qedges, qwedges;
-  // ids need pop order: emission per batch is in q order, so collect (count,
-  // digest) per pop and, for ids, run a second emission pass in pop order below.
+  std::vector<int32_t> qstop;
   std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
   float ms_e = 0;
+  int64_t id_run = 0;
   int rc = run_sweeps(
-      c, qv, mode == DR_DELIVER_PAPER, &qedges, &qwedges, nullptr, nullptr, nullptr,
+      c, qv, paper, &qedges, &qwedges, nullptr, nullptr, nullptr, &qstop,
       [&](size_t i0, size_t i1) -> int {
-        // pops served by this batch, in pop order
+        // pops served by this batch, in pop order (contiguous when ids are wanted)
         std::vector<int> pl;
         for (size_t k = i0; k < i1; k++) pl.insert(pl.end(), q2pop[k].begin(), q2pop[k].end());
         std::sort(pl.begin(), pl.end());
-        std::vector<dr::PopDesc> pd(pl.size());
-        int64_t rb = 0;
+        std::vector<dr::PopDesc> pd;
+        std::vector<uint64_t> extra(pl.size(), 0), extra_dg(pl.size(), 0);
         for (size_t t = 0; t < pl.size(); t++) {
           const Pop &p = pops[pl[t]];
           const dr::SweepQuery &s = qv[pop2q[pl[t]]];
-          pd[t].mask_off = s.mask_off;
-          pd[t].rbase_off = rb;
-          pd[t].first = 1;
-          pd[t].last = std::min(p.cur_round, s.top);
-          rb += s.top + 1;
+          const int stop = memo ? qstop[pop2q[pl[t]]] : -1;
+          const int last = std::min(p.cur_round, s.top);
+          int own_first = 1;
+          uint64_t pos0 = 0;
+          if (memo) {
+            if (stop >= 0) {  // merged at m = stop: rounds 1..min(m, cur) are canonical
+              const int cm = std::min(stop, p.cur_round);
+              if (want_ids) {
+                if (cm >= 1) {
+                  dr::PopDesc d{};
+                  d.mask_off = 0;
+                  d.pos0 = 0;
+                  d.first = 1;
+                  d.last = cm;
+                  d.out = (int32_t)t;
+                  d.use_k = 1;
+                  pd.push_back(d);
+                }
+              } else {
+                extra[t] = c->hC[cm];
+                extra_dg[t] = c->hG[cm];
+              }
+              pos0 = c->hC[cm];
+              own_first = stop + 1;
+            } else {
+              own_first = std::max(1, -1 - stop);  // swept to (-1-stop); rounds below it are empty
+            }
+          }
+          if (own_first <= last) {
+            dr::PopDesc d{};
+            d.mask_off = s.mask_off;  // bottom = 0: the image starts at round 0
+            d.pos0 = (int64_t)pos0;
+            d.first = own_first;
+            d.last = last;
+            d.out = (int32_t)t;
+            d.use_k = 0;
+            pd.push_back(d);
+          }
         }
         std::vector<uint64_t> bc(pl.size()), bd(pl.size());
         int64_t tot = 0;
-        // with ids requested, queries are in pop order, one per pop, so a
-        // batch's pops are a contiguous run and its ids start at id_run
-        int r2 = run_emit(c, pd, bc.data(), bd.data(), want_ids ? ids : nullptr, ids_cap, id_run, &tot, &ms_e);
+        int r2 = run_emit(c, pd, (int)pl.size(), extra.data(), bc.data(), bd.data(), want_ids ? ids : nullptr,
+                          ids_cap, id_run, &tot, &ms_e);
         if (r2) return r2;
         id_run += tot;
-        for (size_t t = 0; t < pl.size(); t++) { cnt[pl[t]] = bc[t]; dg[pl[t]] = bd[t]; }
+        for (size_t t = 0; t < pl.size(); t++) { cnt[pl[t]] = bc[t]; dg[pl[t]] = bd[t] + extra_dg[t]; }
         return 0;
       },
       ms_sweep);
   if (rc) return rc;
-  if (stats) {  // per distinct sweep: the work actually done
-    *stats = SweepStats{};
-    for (size_t k = 0; k < qv.size(); k++) {
+  for (size_t k = 0; k < qv.size(); k++) {
+    const int stop = memo ? qstop[k] : -1;
+    const uint64_t canon_e = (memo && stop >= 0) ? c->hE[stop] : 0;
+    if (stats) {
       stats->weak_edges += qwedges[k];
       stats->sweeps++;
-      stats->rounds += (uint64_t)(qv[k].top - qv[k].bottom + 1);
-      stats->vertices += cnt[q2pop[k][0]];
+      stats->rounds += (uint64_t)(qv[k].top - (memo && stop >= 0 ? stop : (stop >= 0 ? 0 : -1 - stop)) + 1);
     }
-  }
-  for (size_t i = 0; i < pops.size(); i++) {
-    pcount[i] = cnt[i];
-    pdigest[i] = dg[i];
-    if (pedges) pedges[i] = qedges[pop2q[i]];
+    for (int p : q2pop[k]) {
+      pcount[p] = cnt[p];
+      pdigest[p] = dg[p];
+      if (pedges) pedges[p] = qedges[k] + canon_e;
+    }
+    if (stats && !q2pop[k].empty()) {
+      // vertices actually expanded by this sweep (own rounds)
+      const int p = q2pop[k][0];
+      const uint64_t canon_v = (memo && stop >= 0) ? c->hC[std::min(stop, pops[p].cur_round)] : 0;
+      stats->vertices += cnt[p] - canon_v;
+    }
   }
   if (ids_total) *ids_total = id_run;
   if (ms_emit) *ms_emit = ms_e;
@@ -935,11 +1125,17 @@ extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack,
     if (cur_round < 1) p.round = std::max(0, std::min(p.round, c->nrounds - 1));
     pops.push_back(p);
   }
+  if (mode == DR_DELIVER_REF && c->use_memo && c->memo_ok() && !summary_fresh(c) && c->nrounds >= 2)
+    if (int rc = build_summary(c, nullptr)) return rc;
   std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
   int64_t tot = 0;
-  int rc = run_deliver(c, pops, mode, cnt.data(), dg.data(), nullptr, nullptr, out_ids, (int64_t)cap, &tot,
-                       nullptr, nullptr);
+  int rc = run_deliver(c, pops, mode, cnt.data(), dg.data(), nullptr, nullptr, out_ids, (int64_t)cap, &tot, nullptr,
+                       nullptr);
   if (rc) return rc;
+  if (!out_ids) {
+    tot = 0;
+    for (auto x : cnt) tot += (int64_t)x;
+  }
   if (out_n) *out_n = (size_t)tot;
   if (pop_count) std::copy(cnt.begin(), cnt.end(), pop_count);
   if (pop_digest) std::copy(dg.begin(), dg.end(), pop_digest);
@@ -954,9 +1150,15 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   if (chain_mode != DR_CHAIN_LITERAL && chain_mode != DR_CHAIN_PERSISTENT) return c->fail(DR_E_INVAL, "bad chain mode");
   if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad deliver mode");
   if (int rc = set_device(c)) return rc;
-  o->ms_commit = o->ms_chain = o->ms_deliver = o->ms_emit = 0;
+  o->ms_commit = o->ms_chain = o->ms_deliver = o->ms_emit = o->ms_summary = 0;
   o->sweep_weak_edges = o->sweep_count = o->sweep_rounds = o->sweep_vertices = 0;
   o->n_ids = 0;
+  o->canon_segments = -1;
+  // 0. round summaries + canonical cone (every replay re-reads the whole DAG)
+  if (c->use_memo && c->memo_ok()) {
+    if (int rc = build_summary(c, &o->ms_summary)) return rc;
+    o->canon_segments = c->canon_segments;
+  }
   // 1. commit decisions, all waves at once
   if (int rc = commit_range(c, 1, nwaves, o->commit, o->vcount, &o->ms_commit)) return rc;
   uint64_t ce = 0;
@@ -997,11 +1199,11 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   SweepStats st;
   int rc = run_deliver(c, pops, deliver_mode, o->pop_count, o->pop_digest, pe.data(), &st, o->ids, o->ids_cap,
                        &tot, &o->ms_deliver, &o->ms_emit);
+  if (rc) return rc;
   o->sweep_weak_edges = st.weak_edges;
   o->sweep_count = st.sweeps;
   o->sweep_rounds = st.rounds;
   o->sweep_vertices = st.vertices;
-  if (rc) return rc;
   uint64_t de = 0;
   for (size_t i = 0; i < pops.size(); i++) {
     de += pe[i];

@@ -27,8 +27,9 @@
 namespace dr {
 
 typedef unsigned long long u64;
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
-enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8 };
+enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8, Q_SHORTCUT = 16, Q_MERGE = 32 };
 
 struct SweepQuery {
   int32_t top;       // start round (the `from` vertex's round)
@@ -171,36 +172,148 @@ __global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int qu
 }
 
 // ---------------------------------------------------------------------------
+// Round summaries (memo): per round r, U_r = OR of every strong row, WU_r[d] =
+// union of the weak targets at delta d+2, SD_r = total strong degree.  A sweep
+// whose frontier covers every present vertex of r (a "full" round) expands it
+// as U_r / WU_r -- the same bits the rows would give -- without reading rows.
+// K is the canonical cone: the reach sets of "every vertex of the top round";
+// once a sweep's frontier equals K on dmax consecutive rounds, the rest of its
+// cone is K.
+// ---------------------------------------------------------------------------
+struct MemoView {
+  const u64 *U;
+  const u64 *WU;
+  const u64 *SD;
+  const u64 *K;
+  int32_t dd;    // dense weak slots (deltas 2 .. dd+1); 0 with no weak edges
+  int32_t dmax;  // merge window = max(1, largest weak delta)
+};
+
+// strong rows of the vertices in FE (round r) -> ring slot of round r-1
+template <int WS, int NT>
+__device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *FE, u64 *ring, int dmask,
+                                            u64 &my_edges) {
+  using G = Geo<WS, NT>;
+  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
+  const u64 *rows = g.strong + (size_t)r * n * WS;
+  u64 v0[CPT], v1[CPT];
+#pragma unroll
+  for (int p = 0; p < CPT; p++) {
+    const int s = tid / CPR + p * RPP;
+    v0[p] = 0;
+    v1[p] = 0;
+    if (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
+      if constexpr (CW == 2) {
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(rows + (size_t)s * WS + 2 * j);
+        v0[p] = x.x;
+        v1[p] = x.y;
+      } else {
+        v0[p] = rows[s];
+      }
+    }
+  }
+  u64 a0 = 0, a1 = 0;
+#pragma unroll
+  for (int p = 0; p < CPT; p++) {
+    a0 |= v0[p];
+    a1 |= v1[p];
+    my_edges += (u64)(popc64(v0[p]) + popc64(v1[p]));
+  }
+#pragma unroll
+  for (int off = CPR; off < 64; off <<= 1) {
+    a0 |= __shfl_xor(a0, off);
+    if constexpr (CW == 2) a1 |= __shfl_xor(a1, off);
+  }
+  if (lane < CPR) {
+    u64 *dst = ring + (size_t)((r - 1) & dmask) * WS + lane * CW;
+    if (a0) atomicOr(dst, a0);
+    if (CW == 2 && a1) atomicOr(dst + 1, a1);
+  }
+}
+
+// weak edges of the vertices in FE (round r) -> ring (or far mask rows); returns lowest target round
+template <int WS, int NT>
+__device__ __forceinline__ int expand_weak(const DagView &g, int r, int bottom, const u64 *FE, u64 *ring,
+                                           int depth, u64 *mask_bottom, u64 &my_wedges) {
+  const int tid = threadIdx.x, dmask = depth - 1;
+  int lowmin = 0x7fffffff;
+  const uint32_t e0 = g.weak_roff[r], e1 = g.weak_roff[r + 1];
+  for (uint32_t e = e0 + tid; e < e1; e += NT) {
+    const uint32_t x = g.weak[e];
+    const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
+    if (!((FE[own >> 6] >> (own & 63)) & 1ULL)) continue;
+    my_wedges++;
+    const int tr = r - delta;
+    if (tr < bottom) continue;
+    const u64 bit = 1ULL << (ts & 63);
+    if (delta < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
+    else atomicOr(mask_bottom + (int64_t)(tr - bottom) * WS + (ts >> 6), bit);
+    lowmin = min(lowmin, tr);
+  }
+  const uint32_t f0 = g.far_roff[r], f1 = g.far_roff[r + 1];
+  for (uint32_t e = f0 + tid; e < f1; e += NT) {
+    const u64 y = g.far[e];
+    const int own = (int)(y >> 32);
+    const uint32_t t = (uint32_t)y;
+    if (!((FE[own >> 6] >> (own & 63)) & 1ULL)) continue;
+    my_wedges++;
+    const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
+    if (tr < bottom) continue;
+    const u64 bit = 1ULL << (ts & 63);
+    if (r - tr < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
+    else atomicOr(mask_bottom + (int64_t)(tr - bottom) * WS + (ts >> 6), bit);
+    lowmin = min(lowmin, tr);
+  }
+  return lowmin;
+}
+
+// full round r: ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d] (wave 0, lane w < WS owns word w)
+template <int WS>
+__device__ __forceinline__ void expand_summary(const MemoView &m, int r, int bottom, bool strong_only, u64 *ring,
+                                               int dmask) {
+  const int w = threadIdx.x;
+  if (w >= WS) return;
+  ring[(size_t)((r - 1) & dmask) * WS + w] |= m.U[(size_t)r * WS + w];
+  if (strong_only) return;
+  for (int d = 0; d < m.dd; d++) {
+    const int tr = r - d - 2;
+    if (tr < bottom) break;
+    ring[(size_t)(tr & dmask) * WS + w] |= m.WU[((size_t)r * m.dd + d) * WS + w];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_sweep: one workgroup per query (or, with seq != 0, one workgroup walking all
 // queries in order -- paper-mode dedup needs that order).
 //
 // Per round r (top .. bottom):
 //   phase A (wave 0, lane w < WS): F[w] = ring[r][w] (| far-scatter mask word)
-//           (& ~delivered); chain restart; masks/delivered writes; ring slot freed.
-//   phase B (all): strong rows of F -> ring[r-1]; weak edges of F -> ring[r'].
-// LDS: F[WS] | FE[WS] | ring[depth][WS] | ctl (int[4]) | edges (u64).
+//           (& ~delivered); chain restart; masks/delivered writes; ring slot freed;
+//           full / merge tests.
+//   phase B (all): full round with Q_SHORTCUT -> summaries; else strong rows of
+//           F -> ring[r-1] and weak edges of F -> ring[r'].
+// LDS: F[WS] | FE[WS] | ring[depth][WS] | ctl (int[8]) | edges (u64[2]).
 // ---------------------------------------------------------------------------
 template <int WS, int NT>
-__global__ __launch_bounds__(NT) void k_sweep(DagView g, const SweepQuery *__restrict__ qs,
+__global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
                                               int nq, int seq, int depth_log2,
                                               u64 *__restrict__ masks, u64 *__restrict__ dlv,
                                               int32_t *__restrict__ push_out,
                                               int32_t *__restrict__ push_n,
                                               u64 *__restrict__ edges_out,
                                               u64 *__restrict__ wedges_out,
-                                              uint8_t *__restrict__ hit_out) {
-  using G = Geo<WS, NT>;
-  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+                                              uint8_t *__restrict__ hit_out,
+                                              int32_t *__restrict__ stop_out) {
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
   u64 *F = smem;                // WS: frontier (reached ids, dangling included)
   u64 *FE = smem + WS;          // WS: F & present (the vertices that expand)
   u64 *ring = smem + 2 * WS;    // depth * WS
   const int depth = 1 << depth_log2, dmask = depth - 1;
-  int *s_ctl = reinterpret_cast<int *>(ring + (size_t)depth * WS);  // [0]=low water [1]=nonzero
-  u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 4);  // [0] all edges, [1] weak edges
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int n = g.n;
-  const int j = tid % CPR;
+  // ctl: [0] low water [1] nonzero [2] full [3] merged
+  int *s_ctl = reinterpret_cast<int *>(ring + (size_t)depth * WS);
+  u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 8);  // [0] all edges, [1] weak edges
+  const int tid = threadIdx.x;
 
   const int qa = seq ? 0 : blockIdx.x;
   const int qb = seq ? nq : blockIdx.x + 1;
@@ -210,12 +323,19 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, const SweepQuery *__res
     const bool chain = q.flags & Q_CHAIN;
     const bool has_masks = q.flags & Q_MASKS;
     const bool prune = q.flags & Q_PRUNE;
+    const bool shortcut = q.flags & Q_SHORTCUT;
+    const bool merge = q.flags & Q_MERGE;
     for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
-    if (tid == 0) { s_ctl[0] = q.top; s_ctl[1] = 0; s_edges[0] = 0; s_edges[1] = 0; }
+    if (tid == 0) {
+      s_ctl[0] = q.top; s_ctl[1] = 0; s_ctl[2] = 0; s_ctl[3] = 0;
+      s_edges[0] = 0; s_edges[1] = 0;
+    }
     __syncthreads();
     if (tid == 0 && q.src0 >= 0)
       ring[(size_t)(q.top & dmask) * WS + (q.src0 >> 6)] = 1ULL << (q.src0 & 63);
     int npush = 0;  // thread 0
+    int run = 0;    // wave 0: consecutive rounds equal to K
+    int stop = q.bottom;
     u64 my_edges = 0, my_wedges = 0;
     __syncthreads();
     for (int r = q.top;; --r) {
@@ -225,7 +345,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, const SweepQuery *__res
         u64 f = ring[slot];
         ring[slot] = 0;
         u64 *mrow = has_masks ? masks + q.mask_off + (int64_t)(r - q.bottom) * WS : nullptr;
-        if (has_masks && !strong_only) f |= ld_agent(mrow + tid);  // far weak scatters
+        if (has_masks && !strong_only && !merge) f |= ld_agent(mrow + tid);  // far weak scatters
         if (prune) f &= ~ld_agent(dlv + (size_t)r * WS + tid);
         if (chain && r < q.top && ((r - 1) & 3) == 0) {
           const u64 f0 = __shfl(f, 0);
@@ -235,91 +355,47 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, const SweepQuery *__res
             if (tid == 0) push_out[q.out_off + npush++] = (r - 1) / 4 + 1;
           }
         }
+        const u64 p = g.present[(size_t)r * WS + tid];
         F[tid] = f;
-        FE[tid] = f & g.present[(size_t)r * WS + tid];
+        FE[tid] = f & p;
         if (has_masks) mrow[tid] = f;
         if (prune && r >= 1 && r <= q.cur_round) {
-          const u64 add = f & g.present[(size_t)r * WS + tid];
+          const u64 add = f & p;
           if (add) atomicOr(dlv + (size_t)r * WS + tid, add);
         }
         const bool nz = __any(f != 0ULL);
+        const bool full = __all((f & p) == p);
+        if (merge) {
+          const bool eq = __all(f == mv.K[(size_t)r * WS + tid]);
+          run = eq ? run + 1 : 0;
+        }
         if (tid == 0) {
           s_ctl[1] = nz;
+          s_ctl[2] = full;
+          s_ctl[3] = merge && run >= mv.dmax;
           if (nz && r - 1 < s_ctl[0]) s_ctl[0] = r - 1;
         }
       }
       __syncthreads();
+      if (s_ctl[3]) { stop = r; break; }      // state == canonical: the cone below is K
       if (r <= q.bottom) break;
-      if (!s_ctl[1] && s_ctl[0] >= r) break;  // frontier and every pending round empty
-      // ---------------- phase B: strong rows ----------------
-      if (s_ctl[1]) {
-        const u64 *rows = g.strong + (size_t)r * n * WS;
-        u64 v0[CPT], v1[CPT];
-#pragma unroll
-        for (int p = 0; p < CPT; p++) {
-          const int s = tid / CPR + p * RPP;
-          v0[p] = 0;
-          v1[p] = 0;
-          if (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
-            if constexpr (CW == 2) {
-              const ulonglong2 x =
-                  *reinterpret_cast<const ulonglong2 *>(rows + (size_t)s * WS + 2 * j);
-              v0[p] = x.x;
-              v1[p] = x.y;
-            } else {
-              v0[p] = rows[s];
-            }
-          }
+      if (!s_ctl[1] && s_ctl[0] >= r) { stop = r; break; }  // frontier and every pending round empty
+      // ---------------- phase B ----------------
+      if (shortcut && s_ctl[2]) {
+        expand_summary<WS>(mv, r, q.bottom, strong_only, ring, dmask);
+        if (tid == 0) {
+          my_edges += mv.SD[r];
+          if (!strong_only) my_wedges += g.weak_roff[r + 1] - g.weak_roff[r];
+          const int lo = strong_only ? r - 1 : r - 1 - mv.dd;
+          if (lo < s_ctl[0]) s_ctl[0] = lo;
         }
-        u64 a0 = 0, a1 = 0;
-#pragma unroll
-        for (int p = 0; p < CPT; p++) {
-          a0 |= v0[p];
-          a1 |= v1[p];
-          my_edges += (u64)(popc64(v0[p]) + popc64(v1[p]));
+      } else {
+        if (s_ctl[1]) expand_rows<WS, NT>(g, r, FE, ring, dmask, my_edges);
+        if (!strong_only) {
+          const int lowmin = expand_weak<WS, NT>(g, r, q.bottom, FE, ring, depth,
+                                                 masks + q.mask_off, my_wedges);
+          if (lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
         }
-#pragma unroll
-        for (int off = CPR; off < 64; off <<= 1) {
-          a0 |= __shfl_xor(a0, off);
-          if constexpr (CW == 2) a1 |= __shfl_xor(a1, off);
-        }
-        if (lane < CPR) {
-          u64 *dst = ring + (size_t)((r - 1) & dmask) * WS + lane * CW;
-          if (a0) atomicOr(dst, a0);
-          if (CW == 2 && a1) atomicOr(dst + 1, a1);
-        }
-      }
-      // ---------------- phase B: weak edges ----------------
-      if (!strong_only) {
-        int lowmin = 0x7fffffff;
-        const uint32_t e0 = g.weak_roff[r], e1 = g.weak_roff[r + 1];
-        for (uint32_t e = e0 + tid; e < e1; e += NT) {
-          const uint32_t x = g.weak[e];
-          const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
-          if (!((FE[own >> 6] >> (own & 63)) & 1ULL)) continue;
-          my_wedges++;
-          const int tr = r - delta;
-          if (tr < q.bottom) continue;
-          const u64 bit = 1ULL << (ts & 63);
-          if (delta < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
-          else atomicOr(masks + q.mask_off + (int64_t)(tr - q.bottom) * WS + (ts >> 6), bit);
-          lowmin = min(lowmin, tr);
-        }
-        const uint32_t f0 = g.far_roff[r], f1 = g.far_roff[r + 1];
-        for (uint32_t e = f0 + tid; e < f1; e += NT) {
-          const u64 y = g.far[e];
-          const int own = (int)(y >> 32);
-          const uint32_t t = (uint32_t)y;
-          if (!((FE[own >> 6] >> (own & 63)) & 1ULL)) continue;
-          my_wedges++;
-          const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
-          if (tr < q.bottom) continue;
-          const u64 bit = 1ULL << (ts & 63);
-          if (r - tr < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
-          else atomicOr(masks + q.mask_off + (int64_t)(tr - q.bottom) * WS + (ts >> 6), bit);
-          lowmin = min(lowmin, tr);
-        }
-        if (lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
       }
       __syncthreads();
     }
@@ -333,44 +409,226 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, const SweepQuery *__res
       if (wedges_out) wedges_out[qi] = s_edges[1];
       if (hit_out) hit_out[qi] = q.tgt0 >= 0 ? (uint8_t)((F[q.tgt0 >> 6] >> (q.tgt0 & 63)) & 1ULL) : 0;
       if (push_n) push_n[qi] = npush;
+      if (stop_out) stop_out[qi] = s_ctl[3] ? stop : -1 - stop;  // >= 0 merged at stop; < 0 ended at -1-x
     }
     __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------------------
-// Emission, part 1: one workgroup per pop.  Per round r in 1..last:
-// c_r = |mask_r & present_r|; exclusive scan -> rbase; total -> count.
+// k_summary: one workgroup per round: U_r, WU_r, SD_r from one streaming pass
+// over the round's strong rows and weak edges (every byte of the DAG is read
+// once per replay; HBM-bound).
+// ---------------------------------------------------------------------------
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_summary(DagView g, int r0, int dd, u64 *__restrict__ U,
+                                                u64 *__restrict__ WU, u64 *__restrict__ SD) {
+  using G = Geo<WS, NT>;
+  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  __shared__ u64 sU[WS];
+  __shared__ u64 sWU[16 * WS];
+  __shared__ u64 sSD;
+  const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
+  const int r = r0 + blockIdx.x;
+  for (int i = tid; i < WS * (dd + 1); i += NT) {
+    if (i < WS) sU[i] = 0;
+    else sWU[i - WS] = 0;
+  }
+  if (tid == 0) sSD = 0;
+  __syncthreads();
+  const u64 *rows = g.strong + (size_t)r * n * WS;
+  u64 v0[CPT], v1[CPT];
+#pragma unroll
+  for (int p = 0; p < CPT; p++) {
+    const int s = tid / CPR + p * RPP;
+    v0[p] = 0;
+    v1[p] = 0;
+    if (s < n) {
+      if constexpr (CW == 2) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j));
+        v0[p] = x.x;
+        v1[p] = x.y;
+      } else {
+        v0[p] = __builtin_nontemporal_load(rows + s);
+      }
+    }
+  }
+  // weak edges of the round (coalesced u32 stream)
+  const uint32_t e0 = g.weak_roff[r], e1 = g.weak_roff[r + 1];
+  for (uint32_t e = e0 + tid; e < e1; e += NT) {
+    const uint32_t x = __builtin_nontemporal_load(g.weak + e);
+    const int ts = x & 2047, d = (int)(x >> 22) - 2;
+    atomicOr(&sWU[d * WS + (ts >> 6)], 1ULL << (ts & 63));
+  }
+  u64 a0 = 0, a1 = 0, deg = 0;
+#pragma unroll
+  for (int p = 0; p < CPT; p++) {
+    a0 |= v0[p];
+    a1 |= v1[p];
+    deg += (u64)(popc64(v0[p]) + popc64(v1[p]));
+  }
+#pragma unroll
+  for (int off = CPR; off < 64; off <<= 1) {
+    a0 |= __shfl_xor(a0, off);
+    if constexpr (CW == 2) a1 |= __shfl_xor(a1, off);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) deg += __shfl_xor(deg, off);
+  if (lane < CPR) {
+    if (a0) atomicOr(&sU[lane * CW], a0);
+    if (CW == 2 && a1) atomicOr(&sU[lane * CW + 1], a1);
+  }
+  if (lane == 0 && deg) atomicAdd(&sSD, deg);
+  __syncthreads();
+  for (int i = tid; i < WS * (dd + 1); i += NT) {
+    if (i < WS) U[(size_t)r * WS + i] = sU[i];
+    else WU[(size_t)r * dd * WS + (i - WS)] = sWU[i - WS];
+  }
+  if (tid == 0) SD[r] = sSD;
+}
+
+// K^cand_r = U_{r+1} | OR_d WU_{r+d+2}[d] (the cone of round r when every round
+// above it is full); K^cand_T = P_T.  good_r = K^cand_r covers P_r.  CE_r (the
+// canonical round's edges) defaults to the full-round total.
+template <int WS>
+__global__ void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K, uint8_t *__restrict__ good,
+                        u64 *__restrict__ CE) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > T) return;
+  bool ok = true;
+  for (int w = 0; w < WS; w++) {
+    const u64 p = g.present[(size_t)r * WS + w];
+    u64 k;
+    if (r == T) {
+      k = p;
+    } else {
+      k = mv.U[(size_t)(r + 1) * WS + w];
+      for (int d = 0; d < mv.dd && r + d + 2 <= T; d++) k |= mv.WU[((size_t)(r + d + 2) * mv.dd + d) * WS + w];
+    }
+    K[(size_t)r * WS + w] = k;
+    ok &= (k & p) == p;
+  }
+  good[r] = ok;
+  CE[r] = r == 0 ? 0 : mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
+}
+
+// ---------------------------------------------------------------------------
+// k_canon: one workgroup walks the canonical cone from the top.  Rounds whose
+// K^cand covers the round (good) and whose dmax-window above is full are exact
+// already; at each bad round b a segment sweep (rows where partial, summaries
+// where full) runs until dmax consecutive full rounds restore the regime.
+// ---------------------------------------------------------------------------
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int depth_log2,
+                                              u64 *__restrict__ K, const uint8_t *__restrict__ good,
+                                              u64 *__restrict__ CE, int32_t *__restrict__ nseg) {
+  extern __shared__ __attribute__((aligned(16))) u64 smem[];
+  u64 *F = smem, *FE = smem + WS, *ring = smem + 2 * WS;
+  const int depth = 1 << depth_log2, dmask = depth - 1;
+  int *s_ctl = reinterpret_cast<int *>(ring + (size_t)depth * WS);  // [0] next bad [1] full [2] done
+  u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 8);
+  const int tid = threadIdx.x;
+  int pos = T;  // rounds >= pos are final; the regime holds below pos until the next bad round
+  int segs = 0;
+  while (true) {
+    // next bad round below pos
+    if (tid == 0) s_ctl[0] = -1;
+    __syncthreads();
+    for (int base = pos - 1; base >= 0; base -= NT) {
+      const int idx = base - tid;
+      if (idx >= 0 && !good[idx]) atomicMax(&s_ctl[0], idx);
+      __syncthreads();
+      if (s_ctl[0] >= 0) break;
+      __syncthreads();
+    }
+    const int b = s_ctl[0];
+    __syncthreads();
+    if (b < 0) break;
+    segs++;
+    // state at b: F_b = K^cand_b; pending for rounds below from the full rounds above b
+    for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
+    __syncthreads();
+    if (tid < WS) {
+      ring[(size_t)(b & dmask) * WS + tid] = K[(size_t)b * WS + tid];
+      for (int x = b - 1; x >= 0 && x >= b - mv.dd; x--)
+        for (int y = max(b + 1, x + 2); y <= T && y <= x + mv.dd + 1; y++)
+          ring[(size_t)(x & dmask) * WS + tid] |= mv.WU[((size_t)y * mv.dd + (y - x - 2)) * WS + tid];
+    }
+    __syncthreads();
+    int run = 0;
+    int r = b;
+    for (;; --r) {
+      if (tid < WS) {
+        const int slot = (r & dmask) * WS + tid;
+        const u64 f = ring[slot];
+        ring[slot] = 0;
+        const u64 p = g.present[(size_t)r * WS + tid];
+        F[tid] = f;
+        FE[tid] = f & p;
+        K[(size_t)r * WS + tid] = f;
+        const bool full = __all((f & p) == p);
+        run = full ? run + 1 : 0;
+        if (tid == 0) { s_ctl[1] = full; s_ctl[2] = (run >= mv.dmax) || r == 0; s_edges[0] = 0; }
+      }
+      __syncthreads();
+      if (s_ctl[2]) break;  // regime restored at r (or bottom reached): CE_r stays the full total
+      u64 e = 0, we = 0;
+      if (s_ctl[1]) {
+        expand_summary<WS>(mv, r, 0, false, ring, dmask);
+        if (tid == 0) e = mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
+      } else {
+        expand_rows<WS, NT>(g, r, FE, ring, dmask, e);
+        expand_weak<WS, NT>(g, r, 0, FE, ring, depth, K, we);
+      }
+      e += we;
+      if (e) atomicAdd(&s_edges[0], e);
+      __syncthreads();
+      if (tid == 0) CE[r] = s_edges[0];
+      __syncthreads();
+    }
+    pos = r;
+  }
+  if (tid == 0 && nseg) *nseg = segs;
+}
+
+// ---------------------------------------------------------------------------
+// Emission.  A pop's delivered sequence is the concatenation, in round order,
+// of segments; each segment is a PopDesc: rounds [first, last] read from a
+// mask image (the pop's own masks, or the canonical cone K), positions starting
+// at pos0 within the pop.
 // ---------------------------------------------------------------------------
 struct PopDesc {
-  int64_t mask_off;   // word offset of round 0
+  int64_t mask_off;   // word offset of round 0 in its image
   int64_t rbase_off;  // int offset of round 0 in rbase
-  int32_t last;       // last delivered round = min(cur_round, top)
-  int32_t first;      // first delivered round (1)
+  int64_t pos0;       // position of the segment's first vertex within its pop
+  int32_t first, last;
+  int32_t out;        // pop index (count / digest / ids slot)
+  int32_t use_k;      // mask image: 0 = masks, 1 = canonical K
 };
 
+// part 1: one workgroup per segment: c_r = |mask_r & present_r|, exclusive scan
+// over the segment's rounds -> rbase, total -> count[seg]
 template <int WS, int NT>
 __global__ __launch_bounds__(NT) void k_emit_count(DagView g, const PopDesc *__restrict__ pd,
-                                                   const u64 *__restrict__ masks,
-                                                   uint32_t *__restrict__ rbase,
-                                                   u64 *__restrict__ count) {
+                                                   const u64 *__restrict__ masks, const u64 *__restrict__ K,
+                                                   uint32_t *__restrict__ rbase, u64 *__restrict__ count) {
   __shared__ uint32_t part[NT];
   const PopDesc d = pd[blockIdx.x];
+  const u64 *img = (d.use_k ? K : masks) + d.mask_off;
   const int tid = threadIdx.x;
   const int nr = d.last - d.first + 1;
   const int per = nr > 0 ? (nr + NT - 1) / NT : 0;
   const int ra = d.first + tid * per, rb = min(d.last + 1, ra + per);
   uint32_t loc = 0;
   for (int r = ra; r < rb; r++) {
-    const u64 *m = masks + d.mask_off + (int64_t)r * WS;
+    const u64 *m = img + (int64_t)r * WS;
     const u64 *p = g.present + (size_t)r * WS;
 #pragma unroll
     for (int w = 0; w < WS; w++) loc += popc64(m[w] & p[w]);
   }
   part[tid] = loc;
   __syncthreads();
-  // inclusive scan (Hillis-Steele) over NT partials
-  for (int off = 1; off < NT; off <<= 1) {
+  for (int off = 1; off < NT; off <<= 1) {  // inclusive scan over NT partials
     uint32_t v = tid >= off ? part[tid - off] : 0;
     __syncthreads();
     part[tid] += v;
@@ -379,32 +637,33 @@ __global__ __launch_bounds__(NT) void k_emit_count(DagView g, const PopDesc *__r
   uint32_t run = part[tid] - loc;
   for (int r = ra; r < rb; r++) {
     rbase[d.rbase_off + r] = run;
-    const u64 *m = masks + d.mask_off + (int64_t)r * WS;
+    const u64 *m = img + (int64_t)r * WS;
     const u64 *p = g.present + (size_t)r * WS;
     uint32_t c = 0;
 #pragma unroll
     for (int w = 0; w < WS; w++) c += popc64(m[w] & p[w]);
     run += c;
   }
-  if (tid == NT - 1) count[blockIdx.x] = part[NT - 1];
+  if (tid == NT - 1) count[blockIdx.x] = nr > 0 ? part[NT - 1] : 0;
 }
 
-// ---------------------------------------------------------------------------
-// Emission, part 2: grid (round blocks, pops).  Each wave walks one round's slots
-// in order, 64 at a time: ballot of "slot's source in mask" gives ranks, so the
-// k-th delivered vertex of the pop gets position rbase + rank.
-// ---------------------------------------------------------------------------
+// part 2: grid (round blocks, segments).  Each wave walks one round's slots in
+// order, 64 at a time: the ballot of "slot's source in mask" ranks the round's
+// delivered vertices, so vertex k of the pop (k = pos0 + rbase + rank) adds
+// digest_term(round, source, k); ids land at pop_pos[out] + k.  With
+// round_out != nullptr the per-round digest sums are written instead.
 template <int WS, int NT, int RPB>
 __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__restrict__ slot_off,
                                                  const uint16_t *__restrict__ slot_src,
                                                  const PopDesc *__restrict__ pd,
-                                                 const u64 *__restrict__ masks,
+                                                 const u64 *__restrict__ masks, const u64 *__restrict__ K,
                                                  const uint32_t *__restrict__ rbase,
                                                  const int64_t *__restrict__ pop_pos,
-                                                 u64 *__restrict__ digest,
+                                                 u64 *__restrict__ digest, u64 *__restrict__ round_out,
                                                  int32_t *__restrict__ ids, int64_t ids_cap) {
   __shared__ u64 s_dg;
   const PopDesc d = pd[blockIdx.y];
+  const u64 *img = (d.use_k ? K : masks) + d.mask_off;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int NWAVE = NT / 64;
   if (tid == 0) s_dg = 0;
@@ -412,14 +671,15 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
   u64 dg = 0;
   const int ra = d.first + blockIdx.x * RPB;
   const int rb = min(d.last + 1, ra + RPB);
-  const int64_t pbase = pop_pos ? pop_pos[blockIdx.y] : 0;
+  const int64_t pbase = pop_pos ? pop_pos[d.out] : 0;
   for (int r = ra + wid; r < rb; r += NWAVE) {
-    const u64 *m = masks + d.mask_off + (int64_t)r * WS;
-    uint32_t pos = rbase[d.rbase_off + r];
+    const u64 *m = img + (int64_t)r * WS;
+    u64 pos = (u64)d.pos0 + rbase[d.rbase_off + r];
+    u64 rdg = 0;
     const uint32_t sa = slot_off[r], sb = slot_off[r + 1];
     for (uint32_t i0 = sa; i0 < sb; i0 += 64) {
       const uint32_t i = i0 + lane;
-      int src = i < sb ? (int)slot_src[i] : 0;
+      const int src = i < sb ? (int)slot_src[i] : 0;
       bool in = false;
       if (src > 0) {
         const int s = src - 1;
@@ -427,22 +687,63 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
       }
       const u64 b = __ballot(in);
       if (in) {
-        const uint32_t k = pos + (uint32_t)__popcll(b & ((1ULL << lane) - 1ULL));
-        dg += digest_term((uint32_t)r, (uint32_t)src, k);
+        const u64 k = pos + (u64)__popcll(b & ((1ULL << lane) - 1ULL));
+        rdg += digest_term((uint32_t)r, (uint32_t)src, k);
         if (ids) {
-          const int64_t at = pbase + k;
+          const int64_t at = pbase + (int64_t)k;
           if (at < ids_cap) { ids[2 * at] = r; ids[2 * at + 1] = src; }
         }
       }
-      pos += (uint32_t)__popcll(b);
+      pos += (u64)__popcll(b);
+    }
+    if (round_out) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) rdg += __shfl_xor(rdg, off);
+      if (lane == 0) round_out[r] = rdg;
+    } else {
+      dg += rdg;
     }
   }
-  // block reduce
+  if (round_out) return;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) dg += __shfl_xor(dg, off);
   if (lane == 0 && dg) atomicAdd(&s_dg, dg);
   __syncthreads();
-  if (tid == 0 && s_dg) atomicAdd(digest + blockIdx.y, s_dg);
+  if (tid == 0 && s_dg) atomicAdd(digest + d.out, s_dg);
+}
+
+// Canonical prefixes over rounds 0..T (one workgroup): C[r] = vertices of K in
+// rounds 1..r, G[r] = their digest (positions from 0), E[r] = their edges.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_canon_prefix(int T, const uint32_t *__restrict__ rbase,
+                                                     const u64 *__restrict__ ccount,
+                                                     const u64 *__restrict__ RD, const u64 *__restrict__ CE,
+                                                     u64 *__restrict__ C, u64 *__restrict__ G,
+                                                     u64 *__restrict__ E) {
+  __shared__ u64 pg[NT], pe[NT];
+  const int tid = threadIdx.x;
+  const int n = T + 1, per = (n + NT - 1) / NT;
+  const int ra = tid * per, rb = min(n, ra + per);
+  u64 sg = 0, se = 0;
+  for (int r = max(ra, 1); r < rb; r++) { sg += RD[r]; se += CE[r]; }
+  pg[tid] = sg;
+  pe[tid] = se;
+  __syncthreads();
+  for (int off = 1; off < NT; off <<= 1) {
+    u64 a = tid >= off ? pg[tid - off] : 0, b = tid >= off ? pe[tid - off] : 0;
+    __syncthreads();
+    pg[tid] += a;
+    pe[tid] += b;
+    __syncthreads();
+  }
+  u64 rg = pg[tid] - sg, re = pe[tid] - se;
+  for (int r = ra; r < rb; r++) {
+    if (r >= 1) { rg += RD[r]; re += CE[r]; }
+    G[r] = rg;
+    E[r] = re;
+    // rbase[r] = delivered in rounds 1..r-1; inclusive count through r
+    C[r] = r == 0 ? 0 : (r < T ? rbase[r + 1] : *ccount);
+  }
 }
 
 }  // namespace dr

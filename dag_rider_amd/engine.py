@@ -70,6 +70,10 @@ class Engine:
         if rc != L.DR_OK:
             raise L.DrError(rc, self._L.dr_last_error(self._h).decode())
 
+    def set_memo(self, on: bool):
+        """DR_OPT_MEMO: round summaries + canonical cone (identical results either way)."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_MEMO, int(on)))
+
     @property
     def num_rounds(self) -> int:
         return self._L.dr_num_rounds(self._h)
@@ -174,6 +178,7 @@ class Engine:
         return ReplayResult(cm, vc, po, pw[:k], pc[:k], pdg[:k], pe[:k],
                             None if ids is None else ids[:2 * min(o.n_ids, ids_cap)].reshape(-1, 2),
                             o.commit_edges, o.chain_edges, o.deliver_edges,
-                            dict(commit=o.ms_commit, chain=o.ms_chain, deliver=o.ms_deliver, emit=o.ms_emit),
+                            dict(commit=o.ms_commit, chain=o.ms_chain, deliver=o.ms_deliver, emit=o.ms_emit,
+                                 summary=o.ms_summary),
                             dict(weak_edges=o.sweep_weak_edges, count=o.sweep_count, rounds=o.sweep_rounds,
-                                 vertices=o.sweep_vertices))
+                                 vertices=o.sweep_vertices, canon_segments=o.canon_segments))

@@ -44,6 +44,7 @@ enum {
   DR_E_STATE = -6     /* call order violated (e.g. append not contiguous) */
 };
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
+enum { DR_OPT_MEMO = 1 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
 
 typedef struct dr_ctx dr_ctx;
@@ -60,6 +61,9 @@ void dr_destroy(dr_ctx *ctx);
 const char *dr_last_error(const dr_ctx *ctx);
 /* number of rounds currently mirrored (len(p.dag)) */
 int dr_num_rounds(const dr_ctx *ctx);
+/* DR_OPT_MEMO (default 1): use round summaries + the canonical cone for
+ * orderVertices / path sweeps (identical results; 0 = sweep every cone). */
+int dr_set_option(dr_ctx *ctx, int option, int value);
 
 /* p.dag[r] = append(p.dag[r], v) (process.go:229) for whole rounds
  * [r0, r0+k), r0 == dr_num_rounds(ctx): the flattened [][]vertex.
@@ -147,7 +151,8 @@ typedef struct {
   int64_t n_ids;
   uint64_t commit_edges, chain_edges, deliver_edges;
   /* device time (ms) of each phase of the last call, HIP events */
-  float ms_commit, ms_chain, ms_deliver, ms_emit;
+  float ms_commit, ms_chain, ms_deliver, ms_emit, ms_summary;
+  int32_t canon_segments; /* partial-round segments of the canonical cone (-1: summaries off) */
   /* work actually done by the delivery sweeps (identical leaders share one
    * sweep): weak edges expanded, distinct sweeps, rounds swept, vertices expanded */
   uint64_t sweep_weak_edges, sweep_count, sweep_rounds, sweep_vertices;

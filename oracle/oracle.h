@@ -112,6 +112,9 @@ int or_bs_cone(const or_pdag *p, or_vid from, int bottom, int strong_only,
                uint64_t *edges);
 int or_bs_commit_sweep(const or_pdag *p, int faulty, int w0, int w1,
                        uint8_t *commit, int32_t *vcount, uint64_t *edges);
+int or_bs_order_vertices(const or_pdag *p, const or_vid *stack, int stack_len, int cur_round, int mode,
+                         or_vid *out, int64_t out_cap, int64_t *out_n, uint64_t *pop_count,
+                         uint64_t *pop_digest);
 int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode,
                  int deliver_mode, int nthreads, or_replay_out *o);
 

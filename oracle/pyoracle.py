@@ -63,6 +63,8 @@ def lib():
             "or_bs_path": (C.c_int, [C.POINTER(PDagS), Vid, Vid, C.c_int]),
             "or_bs_cone": (C.c_int, [C.POINTER(PDagS), Vid, C.c_int, C.c_int, P, P]),
             "or_bs_commit_sweep": (C.c_int, [C.POINTER(PDagS), C.c_int, C.c_int, C.c_int, P, P, P]),
+            "or_bs_order_vertices": (C.c_int, [C.POINTER(PDagS), P, C.c_int, C.c_int, C.c_int, P, C.c_int64,
+                                               C.POINTER(C.c_int64), P, P]),
             "or_bs_replay": (C.c_int, [C.POINTER(PDagS), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                        C.POINTER(ReplayOutS)]),
         }
@@ -162,6 +164,17 @@ class PDag:
         rc = lib().or_bs_cone(C.byref(self.s), Vid(*fr), bottom, int(strong), _p(m), C.byref(e))
         assert rc == 0
         return m.reshape(-1, W), e.value
+
+    def order_vertices(self, stack, cur_round: int, mode: int = DELIVER_REF, cap: int = 1 << 20):
+        ns = len(stack)
+        st = np.asarray(stack if ns else [(0, 0)], np.int32).reshape(-1)
+        out = np.zeros(2 * cap, np.int32)
+        on = C.c_int64(0)
+        pc = np.zeros(max(ns, 1), np.uint64)
+        pd = np.zeros(max(ns, 1), np.uint64)
+        rc = lib().or_bs_order_vertices(C.byref(self.s), _p(st), ns, cur_round, mode, _p(out), cap, C.byref(on),
+                                        _p(pc), _p(pd))
+        return rc, out[:2 * min(on.value, cap)].reshape(-1, 2), pc[:ns], pd[:ns]
 
     def commit_sweep(self, faulty: int, w0: int, w1: int):
         nw = w1 - w0 + 1

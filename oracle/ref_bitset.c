@@ -323,3 +323,41 @@ int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode, int d
   free(npush);
   return 0;
 }
+
+/* orderVertices (process.go:404-443) for an arbitrary stack: pops top first,
+ * delivering in (round asc, slot asc) order over rounds 1..cur_round.  PAPER
+ * skips vertices delivered by an earlier pop of this call. */
+int or_bs_order_vertices(const or_pdag *p, const or_vid *stack, int stack_len, int cur_round, int mode,
+                         or_vid *out, int64_t out_cap, int64_t *out_n, uint64_t *pop_count,
+                         uint64_t *pop_digest) {
+  const int W = p->W;
+  *out_n = 0;
+  if (stack_len == 0) return 0;
+  if (cur_round >= p->nrounds) return OR_PANIC;
+  uint64_t *D = NULL;
+  if (mode == OR_DELIVER_PAPER) D = (uint64_t *)calloc((size_t)p->nrounds * W, sizeof(uint64_t));
+  int j = 0;
+  for (int t = stack_len - 1; t >= 0; t--, j++) {
+    or_vid v = stack[t];
+    if (cur_round >= 1 && (v.round < 0 || v.round >= p->nrounds)) { free(D); return OR_PANIC; }
+    int top = v.round < 0 ? 0 : (v.round >= p->nrounds ? p->nrounds - 1 : v.round);
+    uint64_t *m = (uint64_t *)calloc((size_t)(top + 1) * W, sizeof(uint64_t));
+    if (v.source >= 1 && v.source <= p->n)
+      m[(size_t)top * W + ((v.source - 1) >> 6)] |= 1ULL << ((v.source - 1) & 63);
+    sweep(p, top, 0, 0, m, D);
+    emit_pop(p, m, 0, top, cur_round, &pop_count[j], &pop_digest[j], out, out_cap, out_n);
+    if (D) {
+      int lastr = cur_round < top ? cur_round : top;
+      for (int r = 1; r <= lastr; r++)
+        for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++) {
+          int s = p->slot_src[i];
+          if (s == 0) continue;
+          uint64_t bit = 1ULL << ((s - 1) & 63);
+          if (m[(size_t)r * W + ((s - 1) >> 6)] & bit) D[(size_t)r * W + ((s - 1) >> 6)] |= bit;
+        }
+    }
+    free(m);
+  }
+  free(D);
+  return 0;
+}

@@ -43,18 +43,20 @@ def random_dag(rng: np.random.Generator, n: int, R: int, p_present=0.8, p_s=0.5,
         slot_off.append(len(slot_src))
         if r == 0:
             continue
+        prev = pres[r - 1]
         for s in range(n):
             if not p[s]:
                 continue
-            for t in range(n):
-                if (pres[r - 1][t] and rng.random() < p_s) or (not pres[r - 1][t] and rng.random() < dangling):
-                    o = (r * n + s) * W + t // 64
-                    strong[o] |= np.uint64(1 << (t % 64))
-            if r >= 2 and p_w > 0:
-                for r2 in range(max(0, r - max_depth), r - 1):
-                    for t in range(n):
-                        if rng.random() < p_w / n * 2:
-                            weak_lists[r * n + s].append((r2 << 11) | t)
+            u = rng.random(n)
+            hit = np.where(prev, u < p_s, u < dangling)
+            for t in np.nonzero(hit)[0]:
+                o = (r * n + s) * W + t // 64
+                strong[o] |= np.uint64(1 << (int(t) % 64))
+            lo = max(0, r - max_depth)
+            if r >= 2 and p_w > 0 and r - 1 > lo:
+                cand = rng.random((r - 1 - lo, n)) < p_w / n * 2
+                for r2, t in zip(*np.nonzero(cand)):
+                    weak_lists[r * n + s].append(((lo + int(r2)) << 11) | int(t))
     weak_off = np.zeros(NR * n + 1, dtype=np.uint32)
     acc = 0
     for i, l in enumerate(weak_lists):

@@ -87,13 +87,15 @@ def _compare_replay(a, b, ids=True):
         assert (a.ids == b.ids).all()
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(48))
 def test_random_dag_replay(gpu_device, seed):
     rng = np.random.default_rng(1000 + seed)
-    n = int(rng.choice([1, 3, 4, 7, 10, 63, 64, 65, 100, 130, 200, 257, 300]))
+    n = int(rng.choice([1, 3, 4, 7, 10, 63, 64, 65, 100, 130, 200, 257, 300, 513]))
     R = int(rng.integers(4, 41))
+    # mostly shallow weak edges (round summaries apply), sometimes deep ones (they do not)
+    depth = int(rng.integers(2, 12)) if seed % 4 else int(rng.integers(12, 40))
     d = random_dag(rng, n, R, p_present=rng.uniform(0.5, 1), p_s=rng.uniform(0.05, 0.9), p_w=rng.uniform(0, 1),
-                   max_depth=int(rng.integers(2, 40)))
+                   max_depth=depth)
     f = int(rng.integers(0, (n - 1) // 3 + 2))
     nw = R // 4
     bs = oracle.PDag(d)
@@ -102,15 +104,29 @@ def test_random_dag_replay(gpu_device, seed):
         cut = int(rng.integers(1, R + 1))
         e.append_packed(d, 0, cut)
         e.append_packed(d, cut, d.nrounds)
-        for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
-            for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
-                want = bs.replay(f, nw, cm, dm, ids_cap=1 << 20)
-                assert want.rc == 0
-                got = e.replay(nw, cm, dm, ids_cap=1 << 20)
-                _compare_replay(got, want)
-                assert got.chain_edges == want.chain_edges
-                got2 = e.replay(nw, cm, dm)  # no ids: REF mode dedups identical leaders
-                _compare_replay(got2, want, ids=False)
+        for memo in (True, False):
+            e.set_memo(memo)
+            for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+                for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+                    want = bs.replay(f, nw, cm, dm, ids_cap=1 << 20)
+                    assert want.rc == 0
+                    got = e.replay(nw, cm, dm, ids_cap=1 << 20)
+                    _compare_replay(got, want)
+                    assert got.chain_edges == want.chain_edges
+                    got2 = e.replay(nw, cm, dm)  # no ids: REF mode dedups identical leaders
+                    _compare_replay(got2, want, ids=False)
+            # orderVertices with arbitrary stacks and p.round below the leaders
+            stack = [(int(rng.integers(0, R + 1)), int(rng.integers(1, n + 1))) for _ in range(3)]
+            cur = int(rng.integers(0, R + 1))
+            # literal BFS oracle (O(n^3 R^2)) for small n, the bitset oracle otherwise
+            ov = oracle.LDag(packed=d) if n <= 16 else bs
+            for mode in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+                ids_, cnt_, dg_ = e.order_vertices(stack, cur, mode)
+                rc, want_ids, wc, wd = ov.order_vertices(stack, cur, mode)
+                assert rc == 0
+                assert ids_.tolist() == want_ids.tolist()
+                assert cnt_.tolist() == wc.tolist() and dg_.tolist() == wd.tolist()
+        e.set_memo(True)
         # path(): all pairs over a sample
         ids = [(r, s) for r in range(R + 1) for s in range(0, n + 1)]
         samp = [ids[i] for i in rng.choice(len(ids), size=min(len(ids), 40), replace=False)]
@@ -130,6 +146,37 @@ def test_random_dag_replay(gpu_device, seed):
                     assert (m == want).all()
 
 
+def test_far_weak_edges(gpu_device):
+    """Weak edges spanning > 1023 rounds use the far format and global frontier rows."""
+    rng = np.random.default_rng(77)
+    n, R = 5, 1200
+    d = random_dag(rng, n, R, p_present=0.9, p_s=0.6, p_w=0.002, max_depth=1150, ghosts=0.0)
+    assert any(((r := int(t) >> 11) < 200) for t in d.weak_tgt)
+    bs = oracle.PDag(d)
+    with Engine(n, 1, R + 1, gpu_device) as e:
+        e.append_packed(d)
+        for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+            want = bs.replay(1, R // 4, cm, L.DR_DELIVER_REF)
+            _compare_replay(e.replay(R // 4, cm, L.DR_DELIVER_REF), want, ids=False)
+        pairs = [((R, s), (r, t)) for s in range(1, n + 1) for r in (0, 1, 5, 100, 600) for t in range(1, n + 1)]
+        got = e.path_batch(pairs, False)
+        assert (got == np.asarray([bs.path(a, b, False) for a, b in pairs], dtype=np.uint8)).all()
+
+
+def test_memo_on_off_large_n(gpu_device):
+    """n=2048 (row stride 32 words) and n=1024 with shallow weak edges: memo == full sweeps."""
+    for n, R in ((2048, 24), (1024, 40)):
+        rng = np.random.default_rng(n)
+        d = random_dag(rng, n, R, p_present=0.97, p_s=0.7, p_w=0.02, max_depth=5, dangling=0.001, ghosts=0.0)
+        f = (n - 1) // 3
+        want = oracle.PDag(d).replay(f, R // 4, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+        with Engine(n, f, R + 1, gpu_device) as e:
+            e.append_packed(d)
+            for memo in (True, False):
+                e.set_memo(memo)
+                _compare_replay(e.replay(R // 4, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), want, ids=False)
+
+
 def test_list_and_packed_append_agree(gpu_device):
     rng = np.random.default_rng(7)
     d = random_dag(rng, 9, 20, ghosts=0.3)
@@ -144,13 +191,14 @@ def test_list_and_packed_append_agree(gpu_device):
 
 
 # --------------------------------------------------------------------------- configs
-@pytest.mark.parametrize("name", ["c1", "c2", "c5"])
-def test_config_replay(gpu_device, name):
+@pytest.mark.parametrize("name,memo", [(c, m) for c in ("c1", "c2", "c5") for m in (True, False)])
+def test_config_replay(gpu_device, name, memo):
     cfg = CONFIGS[name]
     d = generate(cfg)
     bs = oracle.PDag(d)
     with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
         e.append_packed(d)
+        e.set_memo(memo)
         for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
             want = bs.replay(cfg.faulty, cfg.nwaves, cm, L.DR_DELIVER_REF)
             got = e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF)

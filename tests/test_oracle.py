@@ -98,6 +98,12 @@ def test_literal_vs_bitset_random(seed):
     for cm in (oracle.CHAIN_LITERAL, oracle.CHAIN_PERSISTENT):
         for dm in (oracle.DELIVER_REF, oracle.DELIVER_PAPER):
             _same(lit.replay(f, R // 4, cm, dm, ids_cap=1 << 16), bs.replay(f, R // 4, cm, dm, ids_cap=1 << 16))
+    stack = [(int(rng.integers(0, R + 1)), int(rng.integers(1, n + 1))) for _ in range(3)]
+    cur = int(rng.integers(0, R + 1))
+    for mode in (oracle.DELIVER_REF, oracle.DELIVER_PAPER):
+        a, b = lit.order_vertices(stack, cur, mode), bs.order_vertices(stack, cur, mode)
+        assert a[0] == b[0] == 0
+        assert a[1].tolist() == b[1].tolist() and a[2].tolist() == b[2].tolist() and a[3].tolist() == b[3].tolist()
     ids = [(r, s) for r in range(R + 1) for s in range(0, n + 1)]
     for strong in (0, 1):
         for a in ids[::3]:
