@@ -70,6 +70,40 @@ def cpu_bitset(cfg, d, nthreads: int, budget_s: float):
                 sample=f"C4 waves 1..{k} bitset replay (oracle/ref_bitset.c, OpenMP): {e} edges in {dt:.2f} s")
 
 
+def kernel_bytes(cfg, d, res):
+    """Algorithmic bytes per launch of each replay phase."""
+    n, W, T = cfg.n, (cfg.n + 63) // 64, d.nrounds - 1
+    nweak = int(d.weak_off[-1])
+    leaders = int((res.vcount >= 0).sum())
+    dd = max(0, weak_depth(d) - 1)
+    sw = res.sweep
+    out = {
+        # every strong row and weak edge of rounds 1..T read once; U, WU, SD written
+        "summary": dict(kernel="k_summary (round summaries)", ms=res.ms["summary"],
+                        bytes=T * n * W * 8 + nweak * 4 + T * (1 + dd) * W * 8 + T * 8),
+        # round 4w-2: the word holding the leader bit; rounds 4w-1, 4w: whole rows
+        "commit": dict(kernel="k_commit (waveReady commit rule)", ms=res.ms["commit"],
+                       bytes=leaders * (n * 8 + 2 * n * W * 8)),
+        # partial rounds: rows of the frontier + the round's weak list; summary
+        # rounds: U + WU; every round: presence, K and the reach mask written
+        "sweep": dict(kernel="k_sweep (orderVertices cones, merge with canonical)", ms=res.ms["deliver"],
+                      bytes=sw["rows"] * W * 8 + sw["weak_scanned"] * 4 + sw["shortcut"] * (1 + dd) * W * 8
+                      + (sw["partial"] + sw["shortcut"]) * 3 * W * 8),
+    }
+    return out
+
+
+def weak_depth(d):
+    """largest weak-edge delta of the DAG (the summary window)."""
+    import numpy as np
+
+    n = d.n
+    g = np.repeat(np.arange(d.nrounds * n, dtype=np.int64), np.diff(d.weak_off.astype(np.int64)))
+    if len(g) == 0:
+        return 1
+    return int((g // n - (d.weak_tgt.astype(np.int64) >> 11)).max())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -154,17 +188,10 @@ def main():
         return
 
     W = (cfg.n + 63) // 64
-    sw = res.sweep
-    # dominant kernel: k_sweep (delivery cones).  Algorithmic bytes per launch:
-    # cone rows (W*8 per expanded vertex) + weak edges of cone vertices (4 B) +
-    # presence read and reach mask written per swept round (2 * W*8).
-    sweep_bytes = sw["vertices"] * W * 8 + sw["weak_edges"] * 4 + sw["rounds"] * W * 8 * 2
-    sweep_s = res.ms["deliver"] / 1e3
-    achieved = sweep_bytes / sweep_s / 1e9 if sweep_s > 0 else 0.0
-    leaders = int((res.vcount >= 0).sum())
-    commit_bytes = leaders * (cfg.n * 8 + 2 * cfg.n * W * 8)
-    commit_gbs = commit_bytes / (res.ms["commit"] / 1e3) / 1e9 if res.ms["commit"] > 0 else 0.0
-
+    kb = kernel_bytes(cfg, d, res)
+    # dominant kernel = the phase with the largest device time (HIP events)
+    dom = max(kb, key=lambda k: kb[k]["ms"])
+    ach = kb[dom]["bytes"] / (kb[dom]["ms"] / 1e3) / 1e9 if kb[dom]["ms"] > 0 else 0.0
     cpu = None
     cpu2 = None
     if not args.no_cpu and world == 1:
@@ -189,17 +216,18 @@ def main():
                                "waveReady (persistent decidedWave) + orderVertices (ref, full cones) per commit",
                    "n": cfg.n, "rounds": cfg.last_round, "waves": cfg.nwaves,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_sweep<16,1024> (delivery cones)", "bytes_per_launch": sweep_bytes,
-                     "ms_per_launch": res.ms["deliver"]},
+        "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": kb[dom]["kernel"], "bytes_per_launch": kb[dom]["bytes"],
+                     "ms_per_launch": kb[dom]["ms"]},
         "cpu_baseline": cpu,
         "cpu_bitset": cpu2,
         "detail": {"edges_per_step": res.total_edges, "commit_edges": res.commit_edges,
                    "chain_edges": res.chain_edges, "deliver_edges": res.deliver_edges,
                    "commits": int(res.commit.sum()), "pops": int(len(res.pop_count)),
-                   "ms": res.ms, "sweep": sw, "commit_sweep_GBps": commit_gbs,
-                   "commit_sweep_bytes": commit_bytes, "verify_vs_oracle": verify},
+                   "ms": res.ms, "sweep": res.sweep, "verify_vs_oracle": verify,
+                   "kernels": {k: dict(v, GBps=(v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None))
+                               for k, v in kb.items()}},
     }
     print(json.dumps(out), flush=True)
     if dist:

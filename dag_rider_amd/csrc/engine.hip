@@ -87,7 +87,7 @@ struct dr_ctx {
   bool use_memo = true;
   int summary_T = -1;
   int32_t canon_segments = 0;
-  DevBuf U, WU, SD, K, good, CE, RD, Cc, Gc, Ec, crbase, ccount, nseg, stops;
+  DevBuf U, WU, SD, K, good, CE, RD, Cc, Gc, Ec, crbase, ccount, nseg, stops, qstats;
   std::vector<uint64_t> hC, hG, hE;
   // memo needs every weak edge in the dense summary window
   bool memo_ok() const { return nfar == 0 && dmax_near <= 17; }
@@ -158,6 +158,12 @@ template <int WS>
 constexpr int block_for() {
   return WS == 1 ? 64 : WS == 2 ? 128 : WS == 4 ? 256 : WS == 8 ? 512 : 1024;
 }
+// sweeps keep more state live across a round: cap the block at 512 threads
+// (256 VGPRs per lane) so nothing spills
+template <int WS>
+constexpr int sweep_block() {
+  return WS == 1 ? 64 : WS == 2 ? 128 : WS == 4 ? 256 : 512;
+}
 
 // ---- kernel launch dispatch over the row stride ----
 template <int WS>
@@ -187,30 +193,51 @@ struct SweepArgs {
   u64 *edges, *wedges;
   uint8_t *hits;
   int32_t *stops;
+  u64 *stats;
 };
 
-template <int WS>
-hipError_t launch_sweep_t(dr_ctx *c, const SweepArgs &a) {
-  constexpr int NT = block_for<WS>();
+template <int WS, int MODE>
+hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
+  constexpr int NT = sweep_block<WS>();
   const int dl = c->depth_log2();
   const size_t lds = c->sweep_lds(dl);
-  hipError_t e = hipFuncSetAttribute((const void *)dr::k_sweep<WS, NT>,
+  hipError_t e = hipFuncSetAttribute((const void *)dr::k_sweep<WS, NT, MODE>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_sweep<WS, NT>), dim3(a.seq ? 1 : a.nq), dim3(NT), lds, c->stream,
+  hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(a.seq ? 1 : a.nq), dim3(NT), lds, c->stream,
                      c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
-                     a.push_n, a.edges, a.wedges, a.hits, a.stops);
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats);
   return hipGetLastError();
 }
-hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a) {
+template <int WS>
+hipError_t launch_sweep_t(dr_ctx *c, const SweepArgs &a, int mode) {
+  switch (mode) {
+    case 0: return launch_sweep_m<WS, 0>(c, a);
+    case dr::SW_WEAK: return launch_sweep_m<WS, dr::SW_WEAK>(c, a);
+    case dr::SW_CHAIN: return launch_sweep_m<WS, dr::SW_CHAIN>(c, a);
+    case dr::SW_WEAK | dr::SW_PRUNE: return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_PRUNE>(c, a);
+    case dr::SW_WEAK | dr::SW_MERGE: return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_MERGE>(c, a);
+  }
+  return hipErrorInvalidValue;
+}
+// the compile-time mode of a query (every query of one launch shares it)
+int sweep_mode(const dr::SweepQuery &q) {
+  int m = 0;
+  if (!(q.flags & dr::Q_STRONG_ONLY)) m |= dr::SW_WEAK;
+  if (q.flags & dr::Q_CHAIN) m |= dr::SW_CHAIN;
+  if (q.flags & dr::Q_PRUNE) m |= dr::SW_PRUNE;
+  if (q.flags & dr::Q_MERGE) m |= dr::SW_MERGE;
+  return m;
+}
+hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode) {
   if (a.nq <= 0) return hipSuccess;
   switch (c->WS) {
-    case 1: return launch_sweep_t<1>(c, a);
-    case 2: return launch_sweep_t<2>(c, a);
-    case 4: return launch_sweep_t<4>(c, a);
-    case 8: return launch_sweep_t<8>(c, a);
-    case 16: return launch_sweep_t<16>(c, a);
-    case 32: return launch_sweep_t<32>(c, a);
+    case 1: return launch_sweep_t<1>(c, a, mode);
+    case 2: return launch_sweep_t<2>(c, a, mode);
+    case 4: return launch_sweep_t<4>(c, a, mode);
+    case 8: return launch_sweep_t<8>(c, a, mode);
+    case 16: return launch_sweep_t<16>(c, a, mode);
+    case 32: return launch_sweep_t<32>(c, a, mode);
   }
   return hipErrorInvalidValue;
 }
@@ -246,33 +273,51 @@ hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, ui
 }
 
 template <int WS>
-hipError_t launch_summary_t(dr_ctx *c, int T) {
+hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
   constexpr int NT = block_for<WS>();
   const dr::MemoView mv = c->memo_view();
-  hipLaunchKernelGGL((dr::k_summary<WS, NT>), dim3(T), dim3(NT), 0, c->stream, c->view(), 1, mv.dd,
-                     c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>());
+  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T, nwc,
+                     mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(), cm, vc);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 255) / 256), dim3(256), 0, c->stream, c->view(), mv, T,
+  hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
                      c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>());
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int dl = c->depth_log2();
   const size_t lds = c->sweep_lds(dl);
-  e = hipFuncSetAttribute((const void *)dr::k_canon<WS, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  constexpr int NTS = sweep_block<WS>();
+  e = hipFuncSetAttribute((const void *)dr::k_canon<WS, NTS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_canon<WS, NT>), dim3(1), dim3(NT), lds, c->stream, c->view(), mv, T, dl,
+  hipLaunchKernelGGL((dr::k_canon<WS, NTS>), dim3(1), dim3(NTS), lds, c->stream, c->view(), mv, T, dl,
                      c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>());
   return hipGetLastError();
 }
-hipError_t launch_summary(dr_ctx *c, int T) {
+template <int WS>
+hipError_t launch_canon_count_t(dr_ctx *c, int T) {
+  hipLaunchKernelGGL((dr::k_canon_count<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), T,
+                     c->K.as<u64>(), c->RD.as<u64>());
+  return hipGetLastError();
+}
+hipError_t launch_canon_count(dr_ctx *c, int T) {
   switch (c->WS) {
-    case 1: return launch_summary_t<1>(c, T);
-    case 2: return launch_summary_t<2>(c, T);
-    case 4: return launch_summary_t<4>(c, T);
-    case 8: return launch_summary_t<8>(c, T);
-    case 16: return launch_summary_t<16>(c, T);
-    case 32: return launch_summary_t<32>(c, T);
+    case 1: return launch_canon_count_t<1>(c, T);
+    case 2: return launch_canon_count_t<2>(c, T);
+    case 4: return launch_canon_count_t<4>(c, T);
+    case 8: return launch_canon_count_t<8>(c, T);
+    case 16: return launch_canon_count_t<16>(c, T);
+    case 32: return launch_canon_count_t<32>(c, T);
+  }
+  return hipErrorInvalidValue;
+}
+hipError_t launch_summary(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
+  switch (c->WS) {
+    case 1: return launch_summary_t<1>(c, T, nwc, cm, vc);
+    case 2: return launch_summary_t<2>(c, T, nwc, cm, vc);
+    case 4: return launch_summary_t<4>(c, T, nwc, cm, vc);
+    case 8: return launch_summary_t<8>(c, T, nwc, cm, vc);
+    case 16: return launch_summary_t<16>(c, T, nwc, cm, vc);
+    case 32: return launch_summary_t<32>(c, T, nwc, cm, vc);
   }
   return hipErrorInvalidValue;
 }
@@ -357,7 +402,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->digest,  &c->pop_pos, &c->ids,      &c->U,        &c->WU,
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
-                    &c->nseg,    &c->stops};
+                    &c->nseg,    &c->stops,   &c->qstats};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -431,6 +476,29 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
           fdev.push_back(((u64)s0 << 32) | t);
         }
       }
+    }
+  }
+  // device weak edges of each round sorted by (delta, target): the kernels'
+  // wave-uniform OR path (kernels.hpp walk_weak) needs equal destinations
+  // adjacent; edge order is irrelevant to every result.  2-pass LSD radix.
+  {
+    std::vector<uint32_t> tmp;
+    std::vector<uint32_t> cnt(2048);
+    for (int i = 0; i < k; i++) {
+      const size_t a = wroff[i], b = (i + 1 < k) ? wroff[i + 1] : wdev.size();
+      if (b - a < 2) continue;
+      tmp.resize(b - a);
+      uint32_t *src = wdev.data() + a, *dst = tmp.data();
+      for (int pass = 0; pass < 2; pass++) {
+        const int sh = pass == 0 ? 0 : 22, nb = pass == 0 ? 2048 : 1024;
+        std::fill(cnt.begin(), cnt.begin() + nb, 0);
+        for (size_t e = 0; e < b - a; e++) cnt[(src[e] >> sh) & (nb - 1)]++;
+        uint32_t run = 0;
+        for (int t = 0; t < nb; t++) { const uint32_t c2 = cnt[t]; cnt[t] = run; run += c2; }
+        for (size_t e = 0; e < b - a; e++) dst[cnt[(src[e] >> sh) & (nb - 1)]++] = src[e];
+        std::swap(src, dst);
+      }
+      // after two passes the sorted data is back in wdev
     }
   }
   // ---- commit to device ----
@@ -557,7 +625,8 @@ namespace {
 template <class OnBatch>
 int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector<uint64_t> *edges,
                std::vector<uint64_t> *wedges, std::vector<uint8_t> *hits, std::vector<int32_t> *push_n,
-               int32_t *push_out_dev, std::vector<int32_t> *stops, OnBatch on_batch, float *ms) {
+               int32_t *push_out_dev, std::vector<int32_t> *stops, OnBatch on_batch, float *ms,
+               std::vector<uint64_t> *qstats = nullptr) {
   const size_t budget_words = (size_t)1 << 29;  // 4 GiB of frontier masks per batch
   const int WS = c->WS;
   if (edges) edges->assign(qv.size(), 0);
@@ -565,6 +634,7 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
   if (hits) hits->assign(qv.size(), 0);
   if (push_n) push_n->assign(qv.size(), 0);
   if (stops) stops->assign(qv.size(), 0);
+  if (qstats) qstats->assign(qv.size() * 4, 0);
   size_t i0 = 0;
   float total_ms = 0;
   while (i0 < qv.size()) {
@@ -574,7 +644,7 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     bool all_merge = true;
     while (i1 < qv.size()) {
       const size_t w = (qv[i1].flags & dr::Q_MASKS) ? (size_t)(qv[i1].top - qv[i1].bottom + 1) * WS : 0;
-      if (i1 > i0 && words + w > budget_words) break;
+      if (i1 > i0 && (words + w > budget_words || sweep_mode(qv[i1]) != sweep_mode(qv[i0]))) break;
       qv[i1].mask_off = (int64_t)words;
       all_merge &= (qv[i1].flags & dr::Q_MERGE) != 0;
       words += w;
@@ -591,6 +661,7 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     HIPCHK(c, c->hits.ensure((size_t)nq));
     HIPCHK(c, c->push_n.ensure((size_t)nq * 4));
     HIPCHK(c, c->stops.ensure((size_t)nq * 4));
+    HIPCHK(c, c->qstats.ensure((size_t)nq * 32));
     SweepArgs a;
     a.q = c->q_buf.as<dr::SweepQuery>();
     a.nq = nq;
@@ -603,14 +674,16 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     a.wedges = c->wedges.as<u64>();
     a.hits = c->hits.as<uint8_t>();
     a.stops = c->stops.as<int32_t>();
+    a.stats = qstats ? c->qstats.as<u64>() : nullptr;
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-    HIPCHK(c, launch_sweep(c, a));
+    HIPCHK(c, launch_sweep(c, a, sweep_mode(qv[i0])));
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
     if (edges) HIPCHK(c, hipMemcpyAsync(edges->data() + i0, c->edges.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
     if (wedges) HIPCHK(c, hipMemcpyAsync(wedges->data() + i0, c->wedges.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
     if (hits) HIPCHK(c, hipMemcpyAsync(hits->data() + i0, c->hits.p, (size_t)nq, hipMemcpyDeviceToHost, c->stream));
     if (push_n) HIPCHK(c, hipMemcpyAsync(push_n->data() + i0, c->push_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
     if (stops) HIPCHK(c, hipMemcpyAsync(stops->data() + i0, c->stops.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
+    if (qstats) HIPCHK(c, hipMemcpyAsync(qstats->data() + 4 * i0, c->qstats.p, (size_t)nq * 32, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float t = 0;
     HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[1]));
@@ -698,8 +771,9 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
 }
 
 // Round summaries + canonical cone + canonical prefixes for rounds 0..T
-// (T = last mirrored round).  Reads every strong row and weak edge once.
-int build_summary(dr_ctx *c, float *ms_summary) {
+// (T = last mirrored round).  Reads every strong row and weak edge once; with
+// nwc > 0 the same pass decides the commits of waves 1..nwc (host arrays).
+int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr) {
   const int T = c->nrounds - 1;
   const int WS = c->WS, dd = c->memo_dd();
   const size_t R = (size_t)T + 1;
@@ -717,10 +791,16 @@ int build_summary(dr_ctx *c, float *ms_summary) {
   HIPCHK(c, c->crbase.ensure((R + 1) * 4));
   HIPCHK(c, c->ccount.ensure(8));
   HIPCHK(c, c->nseg.ensure(4));
+  HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
+  HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
-  HIPCHK(c, launch_summary(c, T));
+  HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
-  // canonical emission: one segment, rounds 1..T of K; per-round digests
+  // canonical emission: per-round counts -> positions -> per-round digests -> prefixes
+  HIPCHK(c, launch_canon_count(c, T));
+  hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
+                     (const u64 *)nullptr, c->Cc.as<u64>(), (u64 *)nullptr, c->crbase.as<uint32_t>());
+  HIPCHK(c, hipGetLastError());
   dr::PopDesc d{};
   d.mask_off = 0;
   d.rbase_off = 0;
@@ -731,13 +811,10 @@ int build_summary(dr_ctx *c, float *ms_summary) {
   d.use_k = 1;
   HIPCHK(c, c->popdesc.ensure(sizeof(dr::PopDesc)));
   HIPCHK(c, hipMemcpyAsync(c->popdesc.p, &d, sizeof d, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, launch_emit(c, 1, T, c->popdesc.as<dr::PopDesc>(), c->crbase.as<uint32_t>(), c->ccount.as<u64>(),
-                        nullptr, nullptr, nullptr, nullptr, 0, true));
   HIPCHK(c, launch_emit(c, 1, T, c->popdesc.as<dr::PopDesc>(), c->crbase.as<uint32_t>(), nullptr, nullptr,
                         c->RD.as<u64>(), nullptr, nullptr, 0, false));
-  hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->crbase.as<uint32_t>(),
-                     c->ccount.as<u64>(), c->RD.as<u64>(), c->CE.as<u64>(), c->Cc.as<u64>(), c->Gc.as<u64>(),
-                     c->Ec.as<u64>());
+  hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
+                     c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
   c->hC.resize(R);
   c->hG.resize(R);
@@ -746,6 +823,10 @@ int build_summary(dr_ctx *c, float *ms_summary) {
   HIPCHK(c, hipMemcpyAsync(c->hG.data(), c->Gc.p, R * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->hE.data(), c->Ec.p, R * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(&c->canon_segments, c->nseg.p, 4, hipMemcpyDeviceToHost, c->stream));
+  if (nwc > 0) {
+    HIPCHK(c, hipMemcpyAsync(commit, c->commit.p, (size_t)nwc, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(vcount, c->vcount.p, (size_t)nwc * 4, hipMemcpyDeviceToHost, c->stream));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (ms_summary) HIPCHK(c, hipEventElapsedTime(ms_summary, c->ev[6], c->ev[7]));
   c->summary_T = T;
@@ -924,7 +1005,7 @@ int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::
 }
 
 struct Pop { int32_t round, source, cur_round; };
-struct SweepStats { uint64_t weak_edges = 0, sweeps = 0, rounds = 0, vertices = 0; };
+struct SweepStats { uint64_t sweeps = 0, partial = 0, rows = 0, weak_scanned = 0, shortcut = 0; };
 
 // Deliver pops (in pop order).
 //  REF + fresh summaries: one merge sweep per distinct leader; the cone below
@@ -987,7 +1068,7 @@ int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pco
   }
   std::vector<std::vector<int>> q2pop(qv.size());
   for (size_t i = 0; i < pops.size(); i++) q2pop[pop2q[i]].push_back((int)i);
-  std::vector<uint64_t> qedges, qwedges;
+  std::vector<uint64_t> qedges, qwedges, qst;
   std::vector<int32_t> qstop;
   std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
   float ms_e = 0;
@@ -1052,26 +1133,22 @@ int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pco
         for (size_t t = 0; t < pl.size(); t++) { cnt[pl[t]] = bc[t]; dg[pl[t]] = bd[t] + extra_dg[t]; }
         return 0;
       },
-      ms_sweep);
+      ms_sweep, &qst);
   if (rc) return rc;
   for (size_t k = 0; k < qv.size(); k++) {
     const int stop = memo ? qstop[k] : -1;
     const uint64_t canon_e = (memo && stop >= 0) ? c->hE[stop] : 0;
     if (stats) {
-      stats->weak_edges += qwedges[k];
       stats->sweeps++;
-      stats->rounds += (uint64_t)(qv[k].top - (memo && stop >= 0 ? stop : (stop >= 0 ? 0 : -1 - stop)) + 1);
+      stats->partial += qst[4 * k + 0];
+      stats->rows += qst[4 * k + 1];
+      stats->weak_scanned += qst[4 * k + 2];
+      stats->shortcut += qst[4 * k + 3];
     }
     for (int p : q2pop[k]) {
       pcount[p] = cnt[p];
       pdigest[p] = dg[p];
       if (pedges) pedges[p] = qedges[k] + canon_e;
-    }
-    if (stats && !q2pop[k].empty()) {
-      // vertices actually expanded by this sweep (own rounds)
-      const int p = q2pop[k][0];
-      const uint64_t canon_v = (memo && stop >= 0) ? c->hC[std::min(stop, pops[p].cur_round)] : 0;
-      stats->vertices += cnt[p] - canon_v;
     }
   }
   if (ids_total) *ids_total = id_run;
@@ -1151,16 +1228,17 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad deliver mode");
   if (int rc = set_device(c)) return rc;
   o->ms_commit = o->ms_chain = o->ms_deliver = o->ms_emit = o->ms_summary = 0;
-  o->sweep_weak_edges = o->sweep_count = o->sweep_rounds = o->sweep_vertices = 0;
+  o->sweep_count = o->sweep_partial = o->sweep_rows = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;
   o->canon_segments = -1;
-  // 0. round summaries + canonical cone (every replay re-reads the whole DAG)
+  // 0+1. round summaries + canonical cone, fused with the commit decisions of
+  // every wave (one pass over the DAG per replay); without summaries, k_commit
   if (c->use_memo && c->memo_ok()) {
-    if (int rc = build_summary(c, &o->ms_summary)) return rc;
+    if (int rc = build_summary(c, &o->ms_summary, nwaves, o->commit, o->vcount)) return rc;
     o->canon_segments = c->canon_segments;
+  } else if (int rc = commit_range(c, 1, nwaves, o->commit, o->vcount, &o->ms_commit)) {
+    return rc;
   }
-  // 1. commit decisions, all waves at once
-  if (int rc = commit_range(c, 1, nwaves, o->commit, o->vcount, &o->ms_commit)) return rc;
   uint64_t ce = 0;
   for (int w = 1; w <= nwaves; w++)
     if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
@@ -1200,10 +1278,11 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   int rc = run_deliver(c, pops, deliver_mode, o->pop_count, o->pop_digest, pe.data(), &st, o->ids, o->ids_cap,
                        &tot, &o->ms_deliver, &o->ms_emit);
   if (rc) return rc;
-  o->sweep_weak_edges = st.weak_edges;
   o->sweep_count = st.sweeps;
-  o->sweep_rounds = st.rounds;
-  o->sweep_vertices = st.vertices;
+  o->sweep_partial = st.partial;
+  o->sweep_rows = st.rows;
+  o->sweep_weak_scanned = st.weak_scanned;
+  o->sweep_shortcut = st.shortcut;
   uint64_t de = 0;
   for (size_t i = 0; i < pops.size(); i++) {
     de += pe[i];

@@ -28,6 +28,7 @@ namespace dr {
 
 typedef unsigned long long u64;
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8, Q_SHORTCUT = 16, Q_MERGE = 32 };
 
@@ -189,36 +190,102 @@ struct MemoView {
   int32_t dmax;  // merge window = max(1, largest weak delta)
 };
 
-// strong rows of the vertices in FE (round r) -> ring slot of round r-1
+// Walk the weak edges of round r, 16 B (4 edges) per lane, UNR loads in flight
+// per thread.  Edges are stored sorted by (delta, target) (engine.hip, append),
+// so a wave's 256 edges usually hit one destination word: then one wave-wide
+// OR and a single LDS atomic replace 256 of them.  keep(own) filters by source;
+// dest(delta, ts) returns the word index in lds (-1 = not in LDS) and
+// far(delta, ts, bit) handles the rest.  Returns #edges kept.
+template <int NT, int UNR, class Keep, class Dest, class Far>
+__device__ __forceinline__ uint32_t walk_weak(const uint32_t *__restrict__ weak, uint32_t e0, uint32_t e1,
+                                              u64 *lds, Keep keep, Dest dest, Far far) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t a0 = e0 & ~3u;
+  const int nvec = (int)((e1 - a0 + 3) >> 2);
+  const u32x4 *vp = reinterpret_cast<const u32x4 *>(weak + a0);
+  uint32_t kept = 0;
+  for (int v0 = tid; v0 - tid < nvec; v0 += NT * UNR) {  // uniform trip count per workgroup
+    u32x4 q[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; k++) {
+      const int vi = v0 + k * NT;
+      q[k] = vi < nvec ? __builtin_nontemporal_load(vp + vi) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; k++) {
+      const int vi = v0 + k * NT;
+      if (v0 - tid + k * NT >= nvec) break;  // wave-uniform: no lane of this wave has work left
+      const uint32_t xs[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+      int w0 = -1;
+      u64 acc = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t e = a0 + 4u * (uint32_t)vi + (uint32_t)j;
+        if (vi >= nvec || e < e0 || e >= e1) continue;
+        const uint32_t x = xs[j];
+        const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
+        if (!keep(own)) continue;
+        kept++;
+        const u64 bit = 1ULL << (ts & 63);
+        const int dw = dest(delta, ts);
+        if (dw < 0) { far(delta, ts, bit); continue; }
+        if (w0 < 0) { w0 = dw; acc = bit; }
+        else if (dw == w0) acc |= bit;
+        else atomicOr(&lds[dw], bit);
+      }
+      // wave-uniform destination: one OR-reduction + one atomic
+      const u64 nzm = __ballot(w0 >= 0);
+      if (!nzm) continue;
+      const int lead = __shfl(w0, __builtin_ctzll(nzm));
+      if (__all(w0 < 0 || w0 == lead)) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc |= __shfl_xor(acc, off);
+        if (lane == 0 && acc) atomicOr(&lds[lead], acc);
+      } else if (w0 >= 0) {
+        atomicOr(&lds[w0], acc);
+      }
+    }
+  }
+  return kept;
+}
+
+// strong rows of the vertices in FE (round r) -> ring slot of round r-1.
+// Loads go out in groups of 8 passes (16 B each), so register use does not grow
+// with the rows per thread.
 template <int WS, int NT>
 __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *FE, u64 *ring, int dmask,
                                             u64 &my_edges) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  constexpr int GRP = CPT < 8 ? CPT : 8;
   const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
   const u64 *rows = g.strong + (size_t)r * n * WS;
-  u64 v0[CPT], v1[CPT];
+  u64 a0 = 0, a1 = 0;
+#pragma unroll 1
+  for (int p0 = 0; p0 < CPT; p0 += GRP) {
+    if ((tid / CPR) + p0 * RPP - (tid & ~63) / CPR >= n) break;  // wave-uniform: rows of this wave done
+    u64 v0[GRP], v1[GRP];
 #pragma unroll
-  for (int p = 0; p < CPT; p++) {
-    const int s = tid / CPR + p * RPP;
-    v0[p] = 0;
-    v1[p] = 0;
-    if (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
-      if constexpr (CW == 2) {
-        const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(rows + (size_t)s * WS + 2 * j);
-        v0[p] = x.x;
-        v1[p] = x.y;
-      } else {
-        v0[p] = rows[s];
+    for (int p = 0; p < GRP; p++) {
+      const int s = tid / CPR + (p0 + p) * RPP;
+      v0[p] = 0;
+      v1[p] = 0;
+      if (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
+        if constexpr (CW == 2) {
+          const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(rows + (size_t)s * WS + 2 * j);
+          v0[p] = x.x;
+          v1[p] = x.y;
+        } else {
+          v0[p] = rows[s];
+        }
       }
     }
-  }
-  u64 a0 = 0, a1 = 0;
 #pragma unroll
-  for (int p = 0; p < CPT; p++) {
-    a0 |= v0[p];
-    a1 |= v1[p];
-    my_edges += (u64)(popc64(v0[p]) + popc64(v1[p]));
+    for (int p = 0; p < GRP; p++) {
+      a0 |= v0[p];
+      a1 |= v1[p];
+      my_edges += (u64)(popc64(v0[p]) + popc64(v1[p]));
+    }
   }
 #pragma unroll
   for (int off = CPR; off < 64; off <<= 1) {
@@ -239,18 +306,20 @@ __device__ __forceinline__ int expand_weak(const DagView &g, int r, int bottom, 
   const int tid = threadIdx.x, dmask = depth - 1;
   int lowmin = 0x7fffffff;
   const uint32_t e0 = g.weak_roff[r], e1 = g.weak_roff[r + 1];
-  for (uint32_t e = e0 + tid; e < e1; e += NT) {
-    const uint32_t x = g.weak[e];
-    const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
-    if (!((FE[own >> 6] >> (own & 63)) & 1ULL)) continue;
-    my_wedges++;
-    const int tr = r - delta;
-    if (tr < bottom) continue;
-    const u64 bit = 1ULL << (ts & 63);
-    if (delta < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
-    else atomicOr(mask_bottom + (int64_t)(tr - bottom) * WS + (ts >> 6), bit);
-    lowmin = min(lowmin, tr);
-  }
+  my_wedges += walk_weak<NT, 4>(
+      g.weak, e0, e1, ring, [&](int own) { return ((FE[own >> 6] >> (own & 63)) & 1ULL) != 0; },
+      [&](int delta, int ts) -> int {
+        const int tr = r - delta;
+        if (tr < bottom || delta >= depth) return -1;
+        lowmin = min(lowmin, tr);
+        return (tr & dmask) * WS + (ts >> 6);
+      },
+      [&](int delta, int ts, u64 bit) {
+        const int tr = r - delta;
+        if (tr < bottom) return;
+        lowmin = min(lowmin, tr);
+        atomicOr(mask_bottom + (int64_t)(tr - bottom) * WS + (ts >> 6), bit);
+      });
   const uint32_t f0 = g.far_roff[r], f1 = g.far_roff[r + 1];
   for (uint32_t e = f0 + tid; e < f1; e += NT) {
     const u64 y = g.far[e];
@@ -268,34 +337,67 @@ __device__ __forceinline__ int expand_weak(const DagView &g, int r, int bottom, 
   return lowmin;
 }
 
-// full round r: ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d] (wave 0, lane w < WS owns word w)
-template <int WS>
-__device__ __forceinline__ void expand_summary(const MemoView &m, int r, int bottom, bool strong_only, u64 *ring,
-                                               int dmask) {
+// Per-round data that does not depend on the frontier, prefetched one round
+// ahead by lane w < WS (word w): presence, canonical word, U and the first
+// DDR weak-summary slots (later slots are read when used).
+constexpr int DDR = 3;
+struct RoundWords {
+  u64 P, K, U, WU[DDR];
+};
+
+template <int WS, bool MERGE, bool SUMMARY, bool WEAK>
+__device__ __forceinline__ void load_round(const DagView &g, const MemoView &mv, int r, RoundWords &x) {
   const int w = threadIdx.x;
-  if (w >= WS) return;
-  ring[(size_t)((r - 1) & dmask) * WS + w] |= m.U[(size_t)r * WS + w];
-  if (strong_only) return;
-  for (int d = 0; d < m.dd; d++) {
+  x.P = g.present[(size_t)r * WS + w];
+  if constexpr (MERGE) x.K = mv.K[(size_t)r * WS + w];
+  if constexpr (SUMMARY) {
+    x.U = mv.U[(size_t)r * WS + w];
+    if constexpr (WEAK) {
+#pragma unroll
+      for (int d = 0; d < DDR; d++) x.WU[d] = d < mv.dd ? mv.WU[((size_t)r * mv.dd + d) * WS + w] : 0ULL;
+    }
+  }
+}
+
+// full round r: ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d] (lane w < WS owns word w)
+template <int WS, bool WEAK>
+__device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWords &x, int r, int bottom,
+                                               u64 *ring, int dmask) {
+  const int w = threadIdx.x;
+  ring[(size_t)((r - 1) & dmask) * WS + w] |= x.U;
+  if constexpr (!WEAK) return;
+#pragma unroll
+  for (int d = 0; d < DDR; d++) {
+    const int tr = r - d - 2;
+    if (d < mv.dd && tr >= bottom) ring[(size_t)(tr & dmask) * WS + w] |= x.WU[d];
+  }
+  for (int d = DDR; d < mv.dd; d++) {
     const int tr = r - d - 2;
     if (tr < bottom) break;
-    ring[(size_t)(tr & dmask) * WS + w] |= m.WU[((size_t)r * m.dd + d) * WS + w];
+    ring[(size_t)(tr & dmask) * WS + w] |= mv.WU[((size_t)r * mv.dd + d) * WS + w];
   }
 }
 
 // ---------------------------------------------------------------------------
 // k_sweep: one workgroup per query (or, with seq != 0, one workgroup walking all
-// queries in order -- paper-mode dedup needs that order).
-//
+// queries in order -- paper-mode dedup needs that order).  MODE (compile time):
+//   SW_WEAK   follow weak edges too (path(.., false), orderVertices)
+//   SW_CHAIN  waveReady's leader chain: restart at every reachable leader
+//   SW_PRUNE  paper-mode orderVertices: skip delivered vertices
+//   SW_MERGE  stop once the frontier equals the canonical cone K on dmax
+//             consecutive rounds (the cone below is K)
 // Per round r (top .. bottom):
 //   phase A (wave 0, lane w < WS): F[w] = ring[r][w] (| far-scatter mask word)
 //           (& ~delivered); chain restart; masks/delivered writes; ring slot freed;
-//           full / merge tests.
+//           full / merge tests.  Round r-1's frontier-independent words are
+//           prefetched meanwhile.
 //   phase B (all): full round with Q_SHORTCUT -> summaries; else strong rows of
 //           F -> ring[r-1] and weak edges of F -> ring[r'].
 // LDS: F[WS] | FE[WS] | ring[depth][WS] | ctl (int[8]) | edges (u64[2]).
 // ---------------------------------------------------------------------------
-template <int WS, int NT>
+enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8 };
+
+template <int WS, int NT, int MODE>
 __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
                                               int nq, int seq, int depth_log2,
                                               u64 *__restrict__ masks, u64 *__restrict__ dlv,
@@ -304,100 +406,145 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
                                               u64 *__restrict__ edges_out,
                                               u64 *__restrict__ wedges_out,
                                               uint8_t *__restrict__ hit_out,
-                                              int32_t *__restrict__ stop_out) {
+                                              int32_t *__restrict__ stop_out,
+                                              u64 *__restrict__ stats_out) {
+  constexpr bool WEAK = MODE & SW_WEAK, CHAIN = MODE & SW_CHAIN, PRUNE = MODE & SW_PRUNE,
+                 MERGE = MODE & SW_MERGE;
+  constexpr u64 WMASK = WS >= 64 ? ~0ULL : ((1ULL << WS) - 1ULL);  // lanes owning a frontier word
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
   u64 *F = smem;                // WS: frontier (reached ids, dangling included)
   u64 *FE = smem + WS;          // WS: F & present (the vertices that expand)
   u64 *ring = smem + 2 * WS;    // depth * WS
   const int depth = 1 << depth_log2, dmask = depth - 1;
-  // ctl: [0] low water [1] nonzero [2] full [3] merged
+  // ctl: [0] low water [1] round [2] status (0 partial, 1 stop) [3] merged [4] stop round
   int *s_ctl = reinterpret_cast<int *>(ring + (size_t)depth * WS);
   u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 8);  // [0] all edges, [1] weak edges
   const int tid = threadIdx.x;
+  const bool w0 = tid < 64;     // wave 0 runs phase A and every summary round
+  const bool act = tid < WS;    // lane w owns frontier word w
 
   const int qa = seq ? 0 : blockIdx.x;
   const int qb = seq ? nq : blockIdx.x + 1;
   for (int qi = qa; qi < qb; qi++) {
     const SweepQuery q = qs[qi];
-    const bool strong_only = q.flags & Q_STRONG_ONLY;
-    const bool chain = q.flags & Q_CHAIN;
     const bool has_masks = q.flags & Q_MASKS;
-    const bool prune = q.flags & Q_PRUNE;
     const bool shortcut = q.flags & Q_SHORTCUT;
-    const bool merge = q.flags & Q_MERGE;
     for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
     if (tid == 0) {
-      s_ctl[0] = q.top; s_ctl[1] = 0; s_ctl[2] = 0; s_ctl[3] = 0;
+      s_ctl[0] = q.top; s_ctl[1] = q.top; s_ctl[2] = 0; s_ctl[3] = 0; s_ctl[4] = q.bottom;
       s_edges[0] = 0; s_edges[1] = 0;
     }
     __syncthreads();
     if (tid == 0 && q.src0 >= 0)
       ring[(size_t)(q.top & dmask) * WS + (q.src0 >> 6)] = 1ULL << (q.src0 & 63);
     int npush = 0;  // thread 0
+    u64 st_partial = 0, st_rows = 0, st_scan = 0, st_short = 0;  // thread 0: work counters
     int run = 0;    // wave 0: consecutive rounds equal to K
-    int stop = q.bottom;
     u64 my_edges = 0, my_wedges = 0;
+    RoundWords cur{}, nxt{};
+    if (act) {
+      if (shortcut) load_round<WS, MERGE, true, WEAK>(g, mv, q.top, cur);
+      else load_round<WS, MERGE, false, WEAK>(g, mv, q.top, cur);
+    }
     __syncthreads();
-    for (int r = q.top;; --r) {
-      // ---------------- phase A ----------------
-      if (tid < WS) {
-        const int slot = (r & dmask) * WS + tid;
-        u64 f = ring[slot];
-        ring[slot] = 0;
-        u64 *mrow = has_masks ? masks + q.mask_off + (int64_t)(r - q.bottom) * WS : nullptr;
-        if (has_masks && !strong_only && !merge) f |= ld_agent(mrow + tid);  // far weak scatters
-        if (prune) f &= ~ld_agent(dlv + (size_t)r * WS + tid);
-        if (chain && r < q.top && ((r - 1) & 3) == 0) {
-          const u64 f0 = __shfl(f, 0);
-          const bool pres = g.present[(size_t)r * WS] & 1ULL;
-          if ((f0 & 1ULL) && pres) {  // strong_path(leader, v') holds: push v' (process.go:344-349)
-            f = tid == 0 ? 1ULL : 0ULL;
-            if (tid == 0) push_out[q.out_off + npush++] = (r - 1) / 4 + 1;
+    int r = q.top;
+    for (;;) {
+      // ---------- wave 0: phase A of round r; summary rounds end here ----------
+      if (w0) {
+        for (;;) {
+          if (act && r > q.bottom) {  // prefetch round r-1 (frontier-independent)
+            if (shortcut) load_round<WS, MERGE, true, WEAK>(g, mv, r - 1, nxt);
+            else load_round<WS, MERGE, false, WEAK>(g, mv, r - 1, nxt);
           }
-        }
-        const u64 p = g.present[(size_t)r * WS + tid];
-        F[tid] = f;
-        FE[tid] = f & p;
-        if (has_masks) mrow[tid] = f;
-        if (prune && r >= 1 && r <= q.cur_round) {
-          const u64 add = f & p;
-          if (add) atomicOr(dlv + (size_t)r * WS + tid, add);
-        }
-        const bool nz = __any(f != 0ULL);
-        const bool full = __all((f & p) == p);
-        if (merge) {
-          const bool eq = __all(f == mv.K[(size_t)r * WS + tid]);
-          run = eq ? run + 1 : 0;
-        }
-        if (tid == 0) {
-          s_ctl[1] = nz;
-          s_ctl[2] = full;
-          s_ctl[3] = merge && run >= mv.dmax;
-          if (nz && r - 1 < s_ctl[0]) s_ctl[0] = r - 1;
+          u64 f = 0, p = 0;
+          if (act) {
+            const int slot = (r & dmask) * WS + tid;
+            f = ring[slot];
+            ring[slot] = 0;
+            u64 *mrow = has_masks ? masks + q.mask_off + (int64_t)(r - q.bottom) * WS : nullptr;
+            if constexpr (WEAK && !MERGE) {
+              if (has_masks) f |= ld_agent(mrow + tid);  // far weak scatters
+            }
+            if constexpr (PRUNE) f &= ~ld_agent(dlv + (size_t)r * WS + tid);
+            p = cur.P;
+          }
+          if constexpr (CHAIN) {
+            if (r < q.top && ((r - 1) & 3) == 0) {
+              const u64 f0 = __shfl(f, 0);
+              const u64 p0 = __shfl(p, 0);
+              if ((f0 & 1ULL) && (p0 & 1ULL)) {  // strong_path(leader, v') holds: push v' (process.go:344-349)
+                f = tid == 0 ? 1ULL : 0ULL;
+                if (tid == 0) push_out[q.out_off + npush++] = (r - 1) / 4 + 1;
+              }
+            }
+          }
+          if (act) {
+            F[tid] = f;
+            FE[tid] = f & p;
+            if (has_masks) masks[q.mask_off + (int64_t)(r - q.bottom) * WS + tid] = f;
+            if constexpr (PRUNE) {
+              if (r >= 1 && r <= q.cur_round) {
+                const u64 add = f & p;
+                if (add) atomicOr(dlv + (size_t)r * WS + tid, add);
+              }
+            }
+          }
+          const bool nz = (__ballot(act && f != 0ULL) & WMASK) != 0;
+          const bool full = (__ballot(act && (f & p) != p) & WMASK) == 0;
+          if constexpr (MERGE) {
+            const bool eq = (__ballot(act && f != cur.K) & WMASK) == 0;
+            run = eq ? run + 1 : 0;
+          }
+          const bool merged = MERGE && run >= mv.dmax;
+          int low = s_ctl[0];
+          if (nz && r - 1 < low) low = r - 1;
+          const bool stop = merged || r <= q.bottom || (!nz && low >= r);
+          const bool summary = !stop && shortcut && full;
+          if (stats_out) {
+            int pc = act ? popc64(f & p) : 0;
+#pragma unroll
+            for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
+            if (tid == 0 && !stop) {
+              if (summary) st_short++;
+              else { st_partial++; st_rows += (u64)pc; if (WEAK) st_scan += g.weak_roff[r + 1] - g.weak_roff[r]; }
+            }
+          }
+          if (summary) {  // the round is the union of its rows: apply the summaries, stay in wave 0
+            if (act) expand_summary<WS, WEAK>(mv, cur, r, q.bottom, ring, dmask);
+            if (tid == 0) {
+              my_edges += mv.SD[r];
+              if (WEAK) my_wedges += g.weak_roff[r + 1] - g.weak_roff[r];
+            }
+            low = min(low, WEAK ? r - 1 - mv.dd : r - 1);
+            if (tid == 0) s_ctl[0] = low;
+            cur = nxt;
+            --r;
+            continue;
+          }
+          if (tid == 0) {
+            s_ctl[0] = low;
+            s_ctl[1] = r;
+            s_ctl[2] = stop ? 1 : 0;
+            s_ctl[3] = merged ? 1 : 0;
+            if (stop && (merged || r > q.bottom)) s_ctl[4] = r;
+          }
+          break;
         }
       }
       __syncthreads();
-      if (s_ctl[3]) { stop = r; break; }      // state == canonical: the cone below is K
-      if (r <= q.bottom) break;
-      if (!s_ctl[1] && s_ctl[0] >= r) { stop = r; break; }  // frontier and every pending round empty
-      // ---------------- phase B ----------------
-      if (shortcut && s_ctl[2]) {
-        expand_summary<WS>(mv, r, q.bottom, strong_only, ring, dmask);
-        if (tid == 0) {
-          my_edges += mv.SD[r];
-          if (!strong_only) my_wedges += g.weak_roff[r + 1] - g.weak_roff[r];
-          const int lo = strong_only ? r - 1 : r - 1 - mv.dd;
-          if (lo < s_ctl[0]) s_ctl[0] = lo;
-        }
-      } else {
-        if (s_ctl[1]) expand_rows<WS, NT>(g, r, FE, ring, dmask, my_edges);
-        if (!strong_only) {
-          const int lowmin = expand_weak<WS, NT>(g, r, q.bottom, FE, ring, depth,
-                                                 masks + q.mask_off, my_wedges);
+      r = s_ctl[1];
+      if (s_ctl[2]) break;
+      // ---------- all threads: rows and weak edges of partial round r ----------
+      if (s_ctl[0] < r || true) {
+        expand_rows<WS, NT>(g, r, FE, ring, dmask, my_edges);
+        if constexpr (WEAK) {
+          const int lowmin = expand_weak<WS, NT>(g, r, q.bottom, FE, ring, depth, masks + q.mask_off, my_wedges);
           if (lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
         }
       }
       __syncthreads();
+      cur = nxt;
+      --r;
     }
     // results
     my_edges += my_wedges;
@@ -409,94 +556,162 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       if (wedges_out) wedges_out[qi] = s_edges[1];
       if (hit_out) hit_out[qi] = q.tgt0 >= 0 ? (uint8_t)((F[q.tgt0 >> 6] >> (q.tgt0 & 63)) & 1ULL) : 0;
       if (push_n) push_n[qi] = npush;
-      if (stop_out) stop_out[qi] = s_ctl[3] ? stop : -1 - stop;  // >= 0 merged at stop; < 0 ended at -1-x
+      if (stop_out) stop_out[qi] = s_ctl[3] ? s_ctl[4] : -1 - s_ctl[4];  // >= 0 merged there; < 0 ended at -1-x
+      if (stats_out) {
+        stats_out[4 * qi + 0] = st_partial;
+        stats_out[4 * qi + 1] = st_rows;
+        stats_out[4 * qi + 2] = st_scan;
+        stats_out[4 * qi + 3] = st_short;
+      }
     }
     __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------------------
-// k_summary: one workgroup per round: U_r, WU_r, SD_r from one streaming pass
-// over the round's strong rows and weak edges (every byte of the DAG is read
-// once per replay; HBM-bound).
+// k_summary_commit: one workgroup per wave w (rounds 4w-3 .. 4w, clipped to T):
+// the round summaries of k_summary AND waveReady's commit decision of k_commit
+// from one read of each strong row.  The next round's rows are prefetched while
+// the current round's weak edges are walked.  Commit: S_0 = {leader}; for the
+// wave's rounds 2..4, S_k = {v : row(v) & S_{k-1} != 0} by ballot; vcount = |S_3|
+// (process.go:326-339).  Waves past nwc get summaries only.
 // ---------------------------------------------------------------------------
 template <int WS, int NT>
-__global__ __launch_bounds__(NT) void k_summary(DagView g, int r0, int dd, u64 *__restrict__ U,
-                                                u64 *__restrict__ WU, u64 *__restrict__ SD) {
+__global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc, int dd, int quorum,
+                                                       u64 *__restrict__ U, u64 *__restrict__ WU,
+                                                       u64 *__restrict__ SD, uint8_t *__restrict__ commit,
+                                                       int32_t *__restrict__ vcount) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  constexpr int GRP = CPT < 8 ? CPT : 8;  // row chunks in flight per thread
   __shared__ u64 sU[WS];
   __shared__ u64 sWU[16 * WS];
+  __shared__ u64 S[WS], Tn[WS], P[WS];
   __shared__ u64 sSD;
-  const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
-  const int r = r0 + blockIdx.x;
-  for (int i = tid; i < WS * (dd + 1); i += NT) {
-    if (i < WS) sU[i] = 0;
-    else sWU[i - WS] = 0;
-  }
-  if (tid == 0) sSD = 0;
-  __syncthreads();
-  const u64 *rows = g.strong + (size_t)r * n * WS;
-  u64 v0[CPT], v1[CPT];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, j = tid % CPR, n = g.n;
+  const int w = blockIdx.x + 1;
+  const int r1 = 4 * (w - 1) + 1;
+  const int rl = min(T, r1 + 3);
+  const bool do_commit = w <= nwc;
+  const bool leader = do_commit && (g.present[(size_t)r1 * WS] & 1ULL);
+  if (tid < WS) { S[tid] = tid == 0 ? 1ULL : 0ULL; Tn[tid] = 0; }
+  for (int r = r1; r <= rl; r++) {
+    const int k = r - r1;
+    for (int i = tid; i < WS * (dd + 1); i += NT) {
+      if (i < WS) sU[i] = 0;
+      else sWU[i - WS] = 0;
+    }
+    if (tid == 0) sSD = 0;
+    if (tid < WS) P[tid] = g.present[(size_t)r * WS + tid];
+    __syncthreads();
+    const u64 *rows = g.strong + (size_t)r * n * WS;
+    const bool test = leader && k >= 1;
+    const u64 s0 = test ? S[j * CW] : 0ULL, s1 = (test && CW == 2) ? S[j * CW + 1] : 0ULL;
+    u64 a0 = 0, a1 = 0, deg = 0;
+#pragma unroll 1
+    for (int p0 = 0; p0 < CPT; p0 += GRP) {
+      if ((wid * 64) / CPR + p0 * RPP >= n) break;  // wave-uniform: this wave's rows are done
+      u64 v0[GRP], v1[GRP];
 #pragma unroll
-  for (int p = 0; p < CPT; p++) {
-    const int s = tid / CPR + p * RPP;
-    v0[p] = 0;
-    v1[p] = 0;
-    if (s < n) {
-      if constexpr (CW == 2) {
-        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j));
-        v0[p] = x.x;
-        v1[p] = x.y;
-      } else {
-        v0[p] = __builtin_nontemporal_load(rows + s);
+      for (int p = 0; p < GRP; p++) {
+        const int s = tid / CPR + (p0 + p) * RPP;
+        v0[p] = 0;
+        v1[p] = 0;
+        if (s < n) {
+          if constexpr (CW == 2) {
+            const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j));
+            v0[p] = x.x;
+            v1[p] = x.y;
+          } else {
+            v0[p] = __builtin_nontemporal_load(rows + s);
+          }
+        }
+      }
+      if (p0 == 0)  // this round's weak edges while the first row group is in flight
+        walk_weak<NT, 4>(
+            g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
+            [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
+#pragma unroll
+      for (int p = 0; p < GRP; p++) {
+        a0 |= v0[p];
+        a1 |= v1[p];
+        deg += (u64)(popc64(v0[p]) + popc64(v1[p]));
+      }
+      if (test) {  // commit: rows of round r that reach S (wave rounds 2..4)
+#pragma unroll
+        for (int p = 0; p < GRP; p++) {
+          const int rowbase = (wid * 64) / CPR + (p0 + p) * RPP;
+          if (rowbase >= n) break;  // wave-uniform
+          const int s = tid / CPR + (p0 + p) * RPP;
+          const bool pres = s < n && ((P[s >> 6] >> (s & 63)) & 1ULL);
+          const bool hit = pres && ((v0[p] & s0) | (v1[p] & s1)) != 0ULL;
+          u64 m = __ballot(hit);
+          if (lane == 0 && m) {
+            u64 bits;
+            if constexpr (CPR == 1) {
+              bits = m;
+            } else {
+#pragma unroll
+              for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
+              bits = 0;
+#pragma unroll
+              for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
+            }
+            atomicOr(&Tn[rowbase >> 6], bits << (rowbase & 63));
+          }
+        }
       }
     }
-  }
-  // weak edges of the round (coalesced u32 stream)
-  const uint32_t e0 = g.weak_roff[r], e1 = g.weak_roff[r + 1];
-  for (uint32_t e = e0 + tid; e < e1; e += NT) {
-    const uint32_t x = __builtin_nontemporal_load(g.weak + e);
-    const int ts = x & 2047, d = (int)(x >> 22) - 2;
-    atomicOr(&sWU[d * WS + (ts >> 6)], 1ULL << (ts & 63));
-  }
-  u64 a0 = 0, a1 = 0, deg = 0;
+    if ((wid * 64) / CPR >= n)  // waves with no rows still walk the weak edges
+      walk_weak<NT, 4>(
+          g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
+          [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
 #pragma unroll
-  for (int p = 0; p < CPT; p++) {
-    a0 |= v0[p];
-    a1 |= v1[p];
-    deg += (u64)(popc64(v0[p]) + popc64(v1[p]));
-  }
+    for (int off = CPR; off < 64; off <<= 1) {
+      a0 |= __shfl_xor(a0, off);
+      if constexpr (CW == 2) a1 |= __shfl_xor(a1, off);
+    }
 #pragma unroll
-  for (int off = CPR; off < 64; off <<= 1) {
-    a0 |= __shfl_xor(a0, off);
-    if constexpr (CW == 2) a1 |= __shfl_xor(a1, off);
+    for (int off = 32; off > 0; off >>= 1) deg += __shfl_xor(deg, off);
+    if (lane < CPR) {
+      if (a0) atomicOr(&sU[lane * CW], a0);
+      if (CW == 2 && a1) atomicOr(&sU[lane * CW + 1], a1);
+    }
+    if (lane == 0 && deg) atomicAdd(&sSD, deg);
+    __syncthreads();
+    for (int i = tid; i < WS * (dd + 1); i += NT) {
+      if (i < WS) U[(size_t)r * WS + i] = sU[i];
+      else WU[(size_t)r * dd * WS + (i - WS)] = sWU[i - WS];
+    }
+    if (tid == 0) SD[r] = sSD;
+    if (test && tid < WS) { S[tid] = Tn[tid]; Tn[tid] = 0; }
+    __syncthreads();
   }
+  if (do_commit && tid == 0) {
+    if (!leader) {  // leader is bottom (process.go:327-329)
+      commit[w - 1] = 0;
+      vcount[w - 1] = -1;
+    } else {
+      int vc = 0;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) deg += __shfl_xor(deg, off);
-  if (lane < CPR) {
-    if (a0) atomicOr(&sU[lane * CW], a0);
-    if (CW == 2 && a1) atomicOr(&sU[lane * CW + 1], a1);
+      for (int i = 0; i < WS; i++) vc += popc64(S[i]);
+      vcount[w - 1] = vc;
+      commit[w - 1] = vc >= quorum ? 1 : 0;
+    }
   }
-  if (lane == 0 && deg) atomicAdd(&sSD, deg);
-  __syncthreads();
-  for (int i = tid; i < WS * (dd + 1); i += NT) {
-    if (i < WS) U[(size_t)r * WS + i] = sU[i];
-    else WU[(size_t)r * dd * WS + (i - WS)] = sWU[i - WS];
-  }
-  if (tid == 0) SD[r] = sSD;
 }
 
 // K^cand_r = U_{r+1} | OR_d WU_{r+d+2}[d] (the cone of round r when every round
 // above it is full); K^cand_T = P_T.  good_r = K^cand_r covers P_r.  CE_r (the
-// canonical round's edges) defaults to the full-round total.
+// canonical round's edges) defaults to the full-round total.  One wave per
+// round, lane w < WS owns word w.
 template <int WS>
-__global__ void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K, uint8_t *__restrict__ good,
-                        u64 *__restrict__ CE) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K,
+                                               uint8_t *__restrict__ good, u64 *__restrict__ CE) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
   if (r > T) return;
-  bool ok = true;
-  for (int w = 0; w < WS; w++) {
+  bool bad = false;
+  if (w < WS) {
     const u64 p = g.present[(size_t)r * WS + w];
     u64 k;
     if (r == T) {
@@ -506,10 +721,13 @@ __global__ void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K, uint
       for (int d = 0; d < mv.dd && r + d + 2 <= T; d++) k |= mv.WU[((size_t)(r + d + 2) * mv.dd + d) * WS + w];
     }
     K[(size_t)r * WS + w] = k;
-    ok &= (k & p) == p;
+    bad = (k & p) != p;
   }
-  good[r] = ok;
-  CE[r] = r == 0 ? 0 : mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
+  const bool ok = __ballot(bad) == 0ULL;
+  if (w == 0) {
+    good[r] = ok;
+    CE[r] = r == 0 ? 0 : mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -548,21 +766,24 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     // state at b: F_b = K^cand_b; pending for rounds below from the full rounds above b
     for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
     __syncthreads();
+    RoundWords cur{}, nxt{};
     if (tid < WS) {
       ring[(size_t)(b & dmask) * WS + tid] = K[(size_t)b * WS + tid];
       for (int x = b - 1; x >= 0 && x >= b - mv.dd; x--)
         for (int y = max(b + 1, x + 2); y <= T && y <= x + mv.dd + 1; y++)
           ring[(size_t)(x & dmask) * WS + tid] |= mv.WU[((size_t)y * mv.dd + (y - x - 2)) * WS + tid];
+      load_round<WS, false, true, true>(g, mv, b, cur);
     }
     __syncthreads();
     int run = 0;
     int r = b;
     for (;; --r) {
       if (tid < WS) {
+        if (r > 0) load_round<WS, false, true, true>(g, mv, r - 1, nxt);
         const int slot = (r & dmask) * WS + tid;
         const u64 f = ring[slot];
         ring[slot] = 0;
-        const u64 p = g.present[(size_t)r * WS + tid];
+        const u64 p = cur.P;
         F[tid] = f;
         FE[tid] = f & p;
         K[(size_t)r * WS + tid] = f;
@@ -574,7 +795,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
       if (s_ctl[2]) break;  // regime restored at r (or bottom reached): CE_r stays the full total
       u64 e = 0, we = 0;
       if (s_ctl[1]) {
-        expand_summary<WS>(mv, r, 0, false, ring, dmask);
+        if (tid < WS) expand_summary<WS, true>(mv, cur, r, 0, ring, dmask);
         if (tid == 0) e = mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
       } else {
         expand_rows<WS, NT>(g, r, FE, ring, dmask, e);
@@ -584,6 +805,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
       if (e) atomicAdd(&s_edges[0], e);
       __syncthreads();
       if (tid == 0) CE[r] = s_edges[0];
+      cur = nxt;
       __syncthreads();
     }
     pos = r;
@@ -712,37 +934,47 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
   if (tid == 0 && s_dg) atomicAdd(digest + d.out, s_dg);
 }
 
-// Canonical prefixes over rounds 0..T (one workgroup): C[r] = vertices of K in
-// rounds 1..r, G[r] = their digest (positions from 0), E[r] = their edges.
+// Canonical per-round delivered counts c_r = |K_r & P_r| (one wave per round).
+template <int WS>
+__global__ __launch_bounds__(256) void k_canon_count(DagView g, int T, const u64 *__restrict__ K,
+                                                     u64 *__restrict__ cnt) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
+  if (r > T) return;
+  int c = (w < WS && r >= 1) ? popc64(K[(size_t)r * WS + w] & g.present[(size_t)r * WS + w]) : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if (w == 0) cnt[r] = (u64)c;
+}
+
+// Inclusive prefix over rounds 0..T of up to three per-round arrays (one
+// workgroup; rounds >= 1 only).  With rbase != nullptr, also the exclusive
+// prefix of a (positions of round r's first canonical vertex).
 template <int NT>
-__global__ __launch_bounds__(NT) void k_canon_prefix(int T, const uint32_t *__restrict__ rbase,
-                                                     const u64 *__restrict__ ccount,
-                                                     const u64 *__restrict__ RD, const u64 *__restrict__ CE,
-                                                     u64 *__restrict__ C, u64 *__restrict__ G,
-                                                     u64 *__restrict__ E) {
-  __shared__ u64 pg[NT], pe[NT];
+__global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                     u64 *__restrict__ A, u64 *__restrict__ B,
+                                                     uint32_t *__restrict__ rbase) {
+  __shared__ u64 pa[NT], pb[NT];
   const int tid = threadIdx.x;
   const int n = T + 1, per = (n + NT - 1) / NT;
   const int ra = tid * per, rb = min(n, ra + per);
-  u64 sg = 0, se = 0;
-  for (int r = max(ra, 1); r < rb; r++) { sg += RD[r]; se += CE[r]; }
-  pg[tid] = sg;
-  pe[tid] = se;
+  u64 sa = 0, sb = 0;
+  for (int r = max(ra, 1); r < rb; r++) { sa += a[r]; if (b) sb += b[r]; }
+  pa[tid] = sa;
+  pb[tid] = sb;
   __syncthreads();
   for (int off = 1; off < NT; off <<= 1) {
-    u64 a = tid >= off ? pg[tid - off] : 0, b = tid >= off ? pe[tid - off] : 0;
+    const u64 x = tid >= off ? pa[tid - off] : 0, y = tid >= off ? pb[tid - off] : 0;
     __syncthreads();
-    pg[tid] += a;
-    pe[tid] += b;
+    pa[tid] += x;
+    pb[tid] += y;
     __syncthreads();
   }
-  u64 rg = pg[tid] - sg, re = pe[tid] - se;
+  u64 ra_ = pa[tid] - sa, rb_ = pb[tid] - sb;
   for (int r = ra; r < rb; r++) {
-    if (r >= 1) { rg += RD[r]; re += CE[r]; }
-    G[r] = rg;
-    E[r] = re;
-    // rbase[r] = delivered in rounds 1..r-1; inclusive count through r
-    C[r] = r == 0 ? 0 : (r < T ? rbase[r + 1] : *ccount);
+    if (rbase) rbase[r] = (uint32_t)ra_;
+    if (r >= 1) { ra_ += a[r]; if (b) rb_ += b[r]; }
+    A[r] = ra_;
+    if (b) B[r] = rb_;
   }
 }
 

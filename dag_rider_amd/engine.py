@@ -180,5 +180,6 @@ class Engine:
                             o.commit_edges, o.chain_edges, o.deliver_edges,
                             dict(commit=o.ms_commit, chain=o.ms_chain, deliver=o.ms_deliver, emit=o.ms_emit,
                                  summary=o.ms_summary),
-                            dict(weak_edges=o.sweep_weak_edges, count=o.sweep_count, rounds=o.sweep_rounds,
-                                 vertices=o.sweep_vertices, canon_segments=o.canon_segments))
+                            dict(count=o.sweep_count, partial=o.sweep_partial, rows=o.sweep_rows,
+                                 weak_scanned=o.sweep_weak_scanned, shortcut=o.sweep_shortcut,
+                                 canon_segments=o.canon_segments))

@@ -153,9 +153,10 @@ typedef struct {
   /* device time (ms) of each phase of the last call, HIP events */
   float ms_commit, ms_chain, ms_deliver, ms_emit, ms_summary;
   int32_t canon_segments; /* partial-round segments of the canonical cone (-1: summaries off) */
-  /* work actually done by the delivery sweeps (identical leaders share one
-   * sweep): weak edges expanded, distinct sweeps, rounds swept, vertices expanded */
-  uint64_t sweep_weak_edges, sweep_count, sweep_rounds, sweep_vertices;
+  /* work done by the delivery sweeps (identical leaders share one sweep):
+   * sweeps, rounds expanded from rows (+ weak lists), rows read there, weak
+   * edges scanned there, rounds expanded from the round summaries */
+  uint64_t sweep_count, sweep_partial, sweep_rows, sweep_weak_scanned, sweep_shortcut;
 } dr_replay_out;
 
 int dr_replay(dr_ctx *ctx, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o);
