@@ -95,7 +95,56 @@ struct dr_ctx {
   // scratch
   DevBuf q_buf, masks, dlv, push_out, push_n, edges, wedges, hits, commit, vcount, popdesc, rbase, counts,
       digest, pop_pos, ids;
+  // pinned staging for the small per-call transfers: H2D copies are staged
+  // immediately, D2H copies land in pinned memory and are copied out at sync()
+  char *pin = nullptr;
+  size_t pin_cap = 0, pin_used = 0;
+  struct Pending { void *dst; const void *src; size_t n; };
+  std::vector<Pending> pend;
   std::string err;
+  hipError_t sync() {
+    hipError_t e = hipStreamSynchronize(stream);
+    for (auto &p : pend) std::memcpy(p.dst, p.src, p.n);
+    pend.clear();
+    pin_used = 0;
+    return e;
+  }
+  hipError_t stage(size_t n, void **out) {
+    n = (n + 63) & ~(size_t)63;
+    if (pin_used + n > pin_cap) {
+      hipError_t e = sync();
+      if (e != hipSuccess) return e;
+      if (n > pin_cap) {
+        if (pin) (void)hipHostFree(pin);
+        pin = nullptr;
+        pin_cap = 0;
+        const size_t cap = std::max<size_t>(n, (size_t)8 << 20);
+        e = hipHostMalloc((void **)&pin, cap, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        pin_cap = cap;
+      }
+    }
+    *out = pin + pin_used;
+    pin_used += n;
+    return hipSuccess;
+  }
+  hipError_t d2h(void *host, const void *dev, size_t n) {
+    if (!n) return hipSuccess;
+    void *p = nullptr;
+    hipError_t e = stage(n, &p);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(p, dev, n, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) pend.push_back(Pending{host, p, n});
+    return e;
+  }
+  hipError_t h2d(void *dev, const void *host, size_t n) {
+    if (!n) return hipSuccess;
+    void *p = nullptr;
+    hipError_t e = stage(n, &p);
+    if (e != hipSuccess) return e;
+    std::memcpy(p, host, n);
+    return hipMemcpyAsync(dev, p, n, hipMemcpyHostToDevice, stream);
+  }
   int fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
@@ -394,7 +443,8 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
 extern "C" void dr_destroy(dr_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->dev);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->stream) (void)c->sync();
+  if (c->pin) (void)hipHostFree(c->pin);
   DevBuf *bufs[] = {&c->strong,  &c->present, &c->slot_off, &c->slot_src, &c->weak,
                     &c->weak_roff, &c->far,   &c->far_roff, &c->q_buf,    &c->masks,
                     &c->dlv,     &c->push_out, &c->push_n,  &c->edges,    &c->hits, &c->wedges,
@@ -654,8 +704,7 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     HIPCHK(c, c->masks.ensure(std::max<size_t>(words, 1) * 8));
     if (words && !all_merge) HIPCHK(c, hipMemsetAsync(c->masks.p, 0, words * 8, c->stream));
     HIPCHK(c, c->q_buf.ensure((size_t)nq * sizeof(dr::SweepQuery)));
-    HIPCHK(c, hipMemcpyAsync(c->q_buf.p, qv.data() + i0, (size_t)nq * sizeof(dr::SweepQuery),
-                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->h2d(c->q_buf.p, qv.data() + i0, (size_t)nq * sizeof(dr::SweepQuery)));
     HIPCHK(c, c->edges.ensure((size_t)nq * 8));
     HIPCHK(c, c->wedges.ensure((size_t)nq * 8));
     HIPCHK(c, c->hits.ensure((size_t)nq));
@@ -678,13 +727,13 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
     HIPCHK(c, launch_sweep(c, a, sweep_mode(qv[i0])));
     HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
-    if (edges) HIPCHK(c, hipMemcpyAsync(edges->data() + i0, c->edges.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
-    if (wedges) HIPCHK(c, hipMemcpyAsync(wedges->data() + i0, c->wedges.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
-    if (hits) HIPCHK(c, hipMemcpyAsync(hits->data() + i0, c->hits.p, (size_t)nq, hipMemcpyDeviceToHost, c->stream));
-    if (push_n) HIPCHK(c, hipMemcpyAsync(push_n->data() + i0, c->push_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
-    if (stops) HIPCHK(c, hipMemcpyAsync(stops->data() + i0, c->stops.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
-    if (qstats) HIPCHK(c, hipMemcpyAsync(qstats->data() + 4 * i0, c->qstats.p, (size_t)nq * 32, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (edges) HIPCHK(c, c->d2h(edges->data() + i0, c->edges.p, (size_t)nq * 8));
+    if (wedges) HIPCHK(c, c->d2h(wedges->data() + i0, c->wedges.p, (size_t)nq * 8));
+    if (hits) HIPCHK(c, c->d2h(hits->data() + i0, c->hits.p, (size_t)nq));
+    if (push_n) HIPCHK(c, c->d2h(push_n->data() + i0, c->push_n.p, (size_t)nq * 4));
+    if (stops) HIPCHK(c, c->d2h(stops->data() + i0, c->stops.p, (size_t)nq * 4));
+    if (qstats) HIPCHK(c, c->d2h(qstats->data() + 4 * i0, c->qstats.p, (size_t)nq * 32));
+    HIPCHK(c, c->sync());
     float t = 0;
     HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[1]));
     total_ms += t;
@@ -723,7 +772,7 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
   HIPCHK(c, c->popdesc.ensure((size_t)nd * sizeof(dr::PopDesc)));
   HIPCHK(c, c->counts.ensure((size_t)nd * 8));
   HIPCHK(c, c->digest.ensure((size_t)npop * 8));
-  HIPCHK(c, hipMemcpyAsync(c->popdesc.p, pd.data(), (size_t)nd * sizeof(dr::PopDesc), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, c->h2d(c->popdesc.p, pd.data(), (size_t)nd * sizeof(dr::PopDesc)));
   HIPCHK(c, hipMemsetAsync(c->digest.p, 0, (size_t)npop * 8, c->stream));
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   HIPCHK(c, launch_emit(c, nd, span, c->popdesc.as<dr::PopDesc>(), c->rbase.as<uint32_t>(), c->counts.as<u64>(),
@@ -732,8 +781,8 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
   int64_t cap_here = 0, tot = 0;
   if (ids_host && ids_base < ids_cap) {
     std::vector<uint64_t> dc(nd);
-    HIPCHK(c, hipMemcpyAsync(dc.data(), c->counts.p, (size_t)nd * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, c->d2h(dc.data(), c->counts.p, (size_t)nd * 8));
+    HIPCHK(c, c->sync());
     std::vector<uint64_t> pc(cnt);
     for (int i = 0; i < nd; i++) pc[pd[i].out] += dc[i];
     for (int p = 0; p < npop; p++) tot += (int64_t)pc[p];
@@ -742,7 +791,7 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
     int64_t run = 0;
     for (int p = 0; p < npop; p++) { pos[p] = run; run += (int64_t)pc[p]; }
     HIPCHK(c, c->pop_pos.ensure((size_t)npop * 8));
-    HIPCHK(c, hipMemcpyAsync(c->pop_pos.p, pos.data(), (size_t)npop * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->h2d(c->pop_pos.p, pos.data(), (size_t)npop * 8));
     HIPCHK(c, c->ids.ensure((size_t)std::max<int64_t>(cap_here, 1) * 8));
     ids_dev = c->ids.as<int32_t>();
   }
@@ -751,11 +800,11 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
                         cap_here, false));
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
   std::vector<uint64_t> dc(nd);
-  HIPCHK(c, hipMemcpyAsync(dc.data(), c->counts.p, (size_t)nd * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(digest_out, c->digest.p, (size_t)npop * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, c->d2h(dc.data(), c->counts.p, (size_t)nd * 8));
+  HIPCHK(c, c->d2h(digest_out, c->digest.p, (size_t)npop * 8));
   if (ids_dev && cap_here > 0)
-    HIPCHK(c, hipMemcpyAsync(ids_host + 2 * ids_base, ids_dev, (size_t)cap_here * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, c->d2h(ids_host + 2 * ids_base, ids_dev, (size_t)cap_here * 8));
+  HIPCHK(c, c->sync());
   for (int i = 0; i < nd; i++) cnt[pd[i].out] += dc[i];
   std::copy(cnt.begin(), cnt.end(), count_out);
   if (ids_total) {
@@ -810,7 +859,7 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   d.out = 0;
   d.use_k = 1;
   HIPCHK(c, c->popdesc.ensure(sizeof(dr::PopDesc)));
-  HIPCHK(c, hipMemcpyAsync(c->popdesc.p, &d, sizeof d, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, c->h2d(c->popdesc.p, &d, sizeof d));
   HIPCHK(c, launch_emit(c, 1, T, c->popdesc.as<dr::PopDesc>(), c->crbase.as<uint32_t>(), nullptr, nullptr,
                         c->RD.as<u64>(), nullptr, nullptr, 0, false));
   hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
@@ -819,15 +868,15 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   c->hC.resize(R);
   c->hG.resize(R);
   c->hE.resize(R);
-  HIPCHK(c, hipMemcpyAsync(c->hC.data(), c->Cc.p, R * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->hG.data(), c->Gc.p, R * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->hE.data(), c->Ec.p, R * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(&c->canon_segments, c->nseg.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, c->d2h(c->hC.data(), c->Cc.p, R * 8));
+  HIPCHK(c, c->d2h(c->hG.data(), c->Gc.p, R * 8));
+  HIPCHK(c, c->d2h(c->hE.data(), c->Ec.p, R * 8));
+  HIPCHK(c, c->d2h(&c->canon_segments, c->nseg.p, 4));
   if (nwc > 0) {
-    HIPCHK(c, hipMemcpyAsync(commit, c->commit.p, (size_t)nwc, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(vcount, c->vcount.p, (size_t)nwc * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nwc));
+    HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nwc * 4));
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, c->sync());
   if (ms_summary) HIPCHK(c, hipEventElapsedTime(ms_summary, c->ev[6], c->ev[7]));
   c->summary_T = T;
   return DR_OK;
@@ -848,6 +897,90 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     return DR_OK;
   }
   return c->fail(DR_E_INVAL, "unknown option %d", option);
+}
+
+namespace {
+template <int WS, int SV>
+hipError_t launch_sv(dr_ctx *c, int T) {
+  constexpr int NT = block_for<WS>();
+  const dr::MemoView mv = c->memo_view();
+  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, SV>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T,
+                     T / 4, mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(),
+                     c->commit.as<uint8_t>(), c->vcount.as<int32_t>());
+  return hipGetLastError();
+}
+template <int WS>
+hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
+  switch (variant) {
+    case 0: return launch_sv<WS, 0>(c, T);
+    case 1: return launch_sv<WS, dr::SV_NO_WEAK>(c, T);
+    case 2: return launch_sv<WS, dr::SV_NO_ROWS>(c, T);
+    case 3: return launch_sv<WS, dr::SV_UNR8>(c, T);
+  }
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
+// Tuning hook: average device time (HIP events) of `iters` launches of one
+// kernel variant on the resident DAG.  kernel 0: k_summary_commit (variant 0
+// shipped, 1 rows only, 2 weak only, 3 weak unroll 8); kernel 1: streaming read
+// of the strong rows (variant 0) or rows + weak edges (variant 1); kernel 2:
+// the whole dr_replay summary phase (k_summary_commit + canonical cone).
+extern "C" int dr_profile_kernel(dr_ctx *c, int kernel, int variant, int iters, float *avg_ms) {
+  if (!c || !avg_ms || iters < 1) return DR_E_INVAL;
+  if (int rc = set_device(c)) return rc;
+  const int T = c->nrounds - 1;
+  if (T < 4) return c->fail(DR_E_STATE, "profiling needs a DAG");
+  const size_t R = (size_t)T + 1;
+  HIPCHK(c, c->U.ensure(R * c->WS * 8));
+  HIPCHK(c, c->WU.ensure(std::max<size_t>(R * c->memo_dd() * c->WS, 1) * 8));
+  HIPCHK(c, c->SD.ensure(R * 8));
+  HIPCHK(c, c->commit.ensure(R));
+  HIPCHK(c, c->vcount.ensure(R * 4));
+  HIPCHK(c, c->edges.ensure(64));
+  auto one = [&]() -> hipError_t {
+    if (kernel == 0) {
+      if (!c->memo_ok()) return hipErrorInvalidValue;
+      switch (c->WS) {
+        case 1: return launch_sv_t<1>(c, T, variant);
+        case 2: return launch_sv_t<2>(c, T, variant);
+        case 4: return launch_sv_t<4>(c, T, variant);
+        case 8: return launch_sv_t<8>(c, T, variant);
+        case 16: return launch_sv_t<16>(c, T, variant);
+        case 32: return launch_sv_t<32>(c, T, variant);
+      }
+      return hipErrorInvalidValue;
+    }
+    if (kernel == 1) {
+      const size_t a16 = (size_t)c->nrounds * c->n * c->WS / 2;
+      hipLaunchKernelGGL((dr::k_stream_read<256>), dim3(2048), dim3(256), 0, c->stream,
+                         reinterpret_cast<const dr::u64x2 *>(c->strong.p), a16, c->edges.as<u64>());
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess || variant == 0) return e;
+      hipLaunchKernelGGL((dr::k_stream_read<256>), dim3(2048), dim3(256), 0, c->stream,
+                         reinterpret_cast<const dr::u64x2 *>(c->weak.p), c->nweak / 4, c->edges.as<u64>());
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  };
+  if (kernel == 2) {
+    float t = 0, tot = 0;
+    for (int i = 0; i < iters; i++) {
+      if (int rc = build_summary(c, &t)) return rc;
+      tot += t;
+    }
+    *avg_ms = tot / iters;
+    return DR_OK;
+  }
+  HIPCHK(c, one());  // warm
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  for (int i = 0; i < iters; i++) HIPCHK(c, one());
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(c, c->sync());
+  float ms = 0;
+  HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+  *avg_ms = ms / iters;
+  return DR_OK;
 }
 
 extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_t *to, int strong_only,
@@ -950,9 +1083,9 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   HIPCHK(c, launch_commit(c, w0, nw, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
-  HIPCHK(c, hipMemcpyAsync(commit, c->commit.p, (size_t)nw, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(vcount, c->vcount.p, (size_t)nw * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nw));
+  HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nw * 4));
+  HIPCHK(c, c->sync());
   if (ms) HIPCHK(c, hipEventElapsedTime(ms, c->ev[4], c->ev[5]));
   return DR_OK;
 }
@@ -993,7 +1126,8 @@ int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::
                       [](size_t, size_t) { return 0; }, ms);
   if (rc) return rc;
   std::vector<int32_t> po((size_t)off);
-  HIPCHK(c, hipMemcpy(po.data(), c->push_out.p, (size_t)off * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, c->d2h(po.data(), c->push_out.p, (size_t)off * 4));
+  HIPCHK(c, c->sync());
   uint64_t et = 0;
   for (size_t k = 0; k < qv.size(); k++) {
     et += edges[k];

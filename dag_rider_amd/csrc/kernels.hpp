@@ -576,7 +576,9 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
 // wave's rounds 2..4, S_k = {v : row(v) & S_{k-1} != 0} by ballot; vcount = |S_3|
 // (process.go:326-339).  Waves past nwc get summaries only.
 // ---------------------------------------------------------------------------
-template <int WS, int NT>
+enum : int { SV_NO_WEAK = 1, SV_NO_ROWS = 2, SV_UNR8 = 4 };  // tuning variants (dr_profile_kernel)
+
+template <int WS, int NT, int SV = 0>
 __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc, int dd, int quorum,
                                                        u64 *__restrict__ U, u64 *__restrict__ WU,
                                                        u64 *__restrict__ SD, uint8_t *__restrict__ commit,
@@ -611,6 +613,10 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
 #pragma unroll 1
     for (int p0 = 0; p0 < CPT; p0 += GRP) {
       if ((wid * 64) / CPR + p0 * RPP >= n) break;  // wave-uniform: this wave's rows are done
+      if (SV & SV_NO_ROWS) { if (p0 == 0 && !(SV & SV_NO_WEAK)) walk_weak<NT, (SV & SV_UNR8) ? 8 : 4>(
+            g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
+            [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
+        break; }
       u64 v0[GRP], v1[GRP];
 #pragma unroll
       for (int p = 0; p < GRP; p++) {
@@ -627,8 +633,8 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
           }
         }
       }
-      if (p0 == 0)  // this round's weak edges while the first row group is in flight
-        walk_weak<NT, 4>(
+      if (p0 == 0 && !(SV & SV_NO_WEAK))  // this round's weak edges while the first row group is in flight
+        walk_weak<NT, (SV & SV_UNR8) ? 8 : 4>(
             g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
             [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
 #pragma unroll
@@ -662,8 +668,8 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
         }
       }
     }
-    if ((wid * 64) / CPR >= n)  // waves with no rows still walk the weak edges
-      walk_weak<NT, 4>(
+    if ((wid * 64) / CPR >= n && !(SV & SV_NO_WEAK))  // waves with no rows still walk the weak edges
+      walk_weak<NT, (SV & SV_UNR8) ? 8 : 4>(
           g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
           [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
 #pragma unroll
@@ -976,6 +982,23 @@ __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restric
     A[r] = ra_;
     if (b) B[r] = rb_;
   }
+}
+
+// Calibration: read n16 16-B words (grid-stride, 4 in flight per thread) and
+// fold them so nothing is dead-code eliminated.  The practical ceiling for the
+// streaming kernels (dr_profile_kernel).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_stream_read(const u64x2 *__restrict__ p, size_t n16, u64 *__restrict__ out) {
+  u64 acc = 0;
+  const size_t stride = (size_t)gridDim.x * NT;
+  size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u64x2 a = __builtin_nontemporal_load(p + i), b = __builtin_nontemporal_load(p + i + stride);
+    const u64x2 c = __builtin_nontemporal_load(p + i + 2 * stride), d = __builtin_nontemporal_load(p + i + 3 * stride);
+    acc ^= a.x ^ a.y ^ b.x ^ b.y ^ c.x ^ c.y ^ d.x ^ d.y;
+  }
+  for (; i < n16; i += stride) { const u64x2 a = __builtin_nontemporal_load(p + i); acc ^= a.x ^ a.y; }
+  if (acc == 0x9E3779B97F4A7C15ULL) out[0] = acc;  // practically never taken
 }
 
 }  // namespace dr

@@ -74,6 +74,12 @@ class Engine:
         """DR_OPT_MEMO: round summaries + canonical cone (identical results either way)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_MEMO, int(on)))
 
+    def profile_kernel(self, kernel: int, variant: int = 0, iters: int = 20) -> float:
+        """dr_profile_kernel: average device ms of one kernel variant (tuning hook)."""
+        ms = L.f32()
+        self._check(self._L.dr_profile_kernel(self._h, kernel, variant, iters, C.byref(ms)))
+        return ms.value
+
     @property
     def num_rounds(self) -> int:
         return self._L.dr_num_rounds(self._h)
