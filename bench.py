@@ -104,6 +104,27 @@ def weak_depth(d):
     return int((g // n - (d.weak_tgt.astype(np.int64) >> 11)).max())
 
 
+def rank_config(cfg, rank: int, world: int):
+    """Weak scaling: rank r replays its own independent DAG of the same shape (seed + r)."""
+    import dataclasses
+
+    return dataclasses.replace(cfg, seed=cfg.seed + rank) if world > 1 else cfg
+
+
+def reduce_over_ranks(dist, dt: float, edges: int, device: str):
+    """Whole-job numbers: the slowest rank's time (MAX) and all ranks' edges (SUM).
+    device is "cuda" under RCCL ("nccl"), "cpu" under gloo (tests/test_dist_gloo.py)."""
+    import torch
+
+    if dist is None:
+        return dt, float(edges)
+    t = torch.tensor([dt], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    e = torch.tensor([float(edges)], device=device, dtype=torch.float64)
+    dist.all_reduce(e)
+    return float(t.item()), float(e.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,11 +152,8 @@ def main():
     from dag_rider_amd import _lib as L
     from dag_rider_amd.engine import Engine
     from dag_rider_amd.gen import CONFIGS, generate
-    import dataclasses
 
-    cfg = CONFIGS[args.config]
-    if world > 1:
-        cfg = dataclasses.replace(cfg, seed=cfg.seed + rank)
+    cfg = rank_config(CONFIGS[args.config], rank, world)
     t0 = time.perf_counter()
     d = generate(cfg, nthreads=16)
     log(f"[rank {rank}] generated {cfg} in {time.perf_counter() - t0:.1f} s")
@@ -161,16 +179,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        e = torch.tensor([float(res.total_edges)], device="cuda", dtype=torch.float64)
-        dist.all_reduce(e)
-        total_edges = float(e.item())
-    else:
-        total_edges = float(res.total_edges)
+    dt, total_edges = reduce_over_ranks(dist, time.perf_counter() - t0, res.total_edges, "cuda")
 
     verify = None
     if args.verify and rank == 0:

@@ -1,0 +1,59 @@
+"""bench.py's multi-rank path (one process per GPU, weak scaling) on CPU: world_size 2
+over gloo.  Each rank derives its own workload (distinct seed, same shape), the job's
+time is the slowest rank's and its edge total the sum over ranks."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    import bench
+    from dag_rider_amd.gen import CONFIGS, generate, small_config
+
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    try:
+        cfg = bench.rank_config(CONFIGS["c4"], rank, world)
+        small = bench.rank_config(small_config(16, 12, 5), rank, world)
+        d = generate(small)
+        edges = int(d.weak_off[-1]) + 1000 * (rank + 1)  # any per-rank count
+        dt, tot = bench.reduce_over_ranks(dist, 0.5 + rank, edges, "cpu")
+        out[rank] = (cfg.seed, cfg.n, cfg.last_round, small.seed, int(d.strong.sum() % (1 << 32)), edges, dt, tot)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_weak_scaling_two_ranks_gloo():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    r0, r1 = out[0], out[1]
+    # same shape, independent units
+    assert r0[1:3] == r1[1:3] and r0[0] != r1[0] and r0[3] != r1[3]
+    # max time, summed edges, identical on every rank
+    assert r0[6] == r1[6] == 1.5
+    assert r0[7] == r1[7] == float(r0[5] + r1[5])
+
+
+def test_single_rank_passthrough():
+    sys.path.insert(0, ROOT)
+    import bench
+    from dag_rider_amd.gen import CONFIGS
+
+    assert bench.rank_config(CONFIGS["c4"], 0, 1) == CONFIGS["c4"]
+    assert bench.reduce_over_ranks(None, 2.0, 7, "cpu") == (2.0, 7.0)
