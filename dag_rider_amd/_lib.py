@@ -15,6 +15,7 @@ DR_OK, DR_E_INVAL, DR_E_CAPACITY, DR_E_HIP, DR_E_RCCL, DR_E_CONTRACT, DR_E_STATE
 DR_CHAIN_LITERAL, DR_CHAIN_PERSISTENT = 0, 1
 DR_DELIVER_REF, DR_DELIVER_PAPER = 0, 1
 DR_OPT_MEMO = 1
+DR_OPT_DEVICE_PLAN = 2
 
 P = C.c_void_p
 i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float

@@ -11,10 +11,12 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "dagrider_gpu.h"
 #include "kernels.hpp"
+#include "replay_plan.hpp"
 
 using dr::u64;
 
@@ -89,22 +91,58 @@ struct dr_ctx {
   int32_t canon_segments = 0;
   DevBuf U, WU, SD, K, good, CE, RD, Cc, Gc, Ec, crbase, ccount, nseg, stops, qstats;
   std::vector<uint64_t> hC, hG, hE;
+  bool canon_host = false;
+  int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies  // hC/hG/hE mirror Cc/Gc/Ec (fetched lazily after a planned replay)
+  DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
   // memo needs every weak edge in the dense summary window
   bool memo_ok() const { return nfar == 0 && dmax_near <= 17; }
   int memo_dd() const { return std::max(0, dmax_near - 1); }
   // scratch
   DevBuf q_buf, masks, dlv, push_out, push_n, edges, wedges, hits, commit, vcount, popdesc, rbase, counts,
       digest, pop_pos, ids;
-  // pinned staging for the small per-call transfers: H2D copies are staged
-  // immediately, D2H copies land in pinned memory and are copied out at sync()
+  // pinned, device-mapped staging for the per-call transfers.  H2D: staged and
+  // copied by k_copy at once.  D2H: deferred to sync(), where one k_copy launch
+  // moves every pending small array into pinned memory (callers sync before
+  // launching anything that overwrites a pending source).  sync() spins on an
+  // event: the host waits microseconds, not an interrupt round trip.
   char *pin = nullptr;
   size_t pin_cap = 0, pin_used = 0;
-  struct Pending { void *dst; const void *src; size_t n; };
+  struct Pending { void *dst; void *stage; const void *src; size_t n; };
   std::vector<Pending> pend;
-  std::string err;
+  hipEvent_t ev_sync = nullptr;
+  hipError_t launch_copies(const dr::CopySeg *sg, int k) {
+    for (int i0 = 0; i0 < k; i0 += dr::kCopySegs) {
+      dr::CopyList L{};
+      const int m = std::min(dr::kCopySegs, k - i0);
+      uint64_t mx = 1;
+      for (int i = 0; i < m; i++) { L.s[i] = sg[i0 + i]; mx = std::max<uint64_t>(mx, sg[i0 + i].n); }
+      const unsigned bx = (unsigned)std::min<uint64_t>(256, (mx + 4095) / 4096);
+      hipLaunchKernelGGL(dr::k_copy, dim3(bx, m), dim3(256), 0, stream, L);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   hipError_t sync() {
-    hipError_t e = hipStreamSynchronize(stream);
-    for (auto &p : pend) std::memcpy(p.dst, p.src, p.n);
+    hipError_t e = hipSuccess;
+    if (!pend.empty()) {
+      std::vector<dr::CopySeg> small;
+      for (auto &p : pend) {
+        if (p.n >= ((size_t)1 << 22))  // bulk: DMA engine
+          e = hipMemcpyAsync(p.stage, p.src, p.n, hipMemcpyDeviceToHost, stream);
+        else
+          small.push_back(dr::CopySeg{static_cast<const uint8_t *>(p.src), static_cast<uint8_t *>(p.stage), p.n});
+        if (e != hipSuccess) break;
+      }
+      if (e == hipSuccess && !small.empty()) e = launch_copies(small.data(), (int)small.size());
+    }
+    if (e == hipSuccess) e = hipEventRecord(ev_sync, stream);
+    if (e == hipSuccess) {
+      while ((e = hipEventQuery(ev_sync)) == hipErrorNotReady) {
+      }
+    }
+    if (e == hipSuccess)
+      for (auto &p : pend) std::memcpy(p.dst, p.stage, p.n);
     pend.clear();
     pin_used = 0;
     return e;
@@ -119,7 +157,7 @@ struct dr_ctx {
         pin = nullptr;
         pin_cap = 0;
         const size_t cap = std::max<size_t>(n, (size_t)8 << 20);
-        e = hipHostMalloc((void **)&pin, cap, hipHostMallocDefault);
+        e = hipHostMalloc((void **)&pin, cap, hipHostMallocMapped);
         if (e != hipSuccess) return e;
         pin_cap = cap;
       }
@@ -132,9 +170,7 @@ struct dr_ctx {
     if (!n) return hipSuccess;
     void *p = nullptr;
     hipError_t e = stage(n, &p);
-    if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(p, dev, n, hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) pend.push_back(Pending{host, p, n});
+    if (e == hipSuccess) pend.push_back(Pending{host, p, dev, n});
     return e;
   }
   hipError_t h2d(void *dev, const void *host, size_t n) {
@@ -143,8 +179,11 @@ struct dr_ctx {
     hipError_t e = stage(n, &p);
     if (e != hipSuccess) return e;
     std::memcpy(p, host, n);
-    return hipMemcpyAsync(dev, p, n, hipMemcpyHostToDevice, stream);
+    if (n >= ((size_t)1 << 22)) return hipMemcpyAsync(dev, p, n, hipMemcpyHostToDevice, stream);
+    const dr::CopySeg sg{static_cast<const uint8_t *>(p), static_cast<uint8_t *>(dev), n};
+    return launch_copies(&sg, 1);
   }
+  std::string err;
   int fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
@@ -243,6 +282,7 @@ struct SweepArgs {
   uint8_t *hits;
   int32_t *stops;
   u64 *stats;
+  const int *nq_dev = nullptr;  // planned replay: query count on the device, nq = grid upper bound
 };
 
 template <int WS, int MODE>
@@ -255,7 +295,7 @@ hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(a.seq ? 1 : a.nq), dim3(NT), lds, c->stream,
                      c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
-                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats);
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev);
   return hipGetLastError();
 }
 template <int WS>
@@ -294,29 +334,39 @@ hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode) {
 constexpr int kEmitRPB = 16;
 
 template <int WS>
+// Planned mode (plan != nullptr, device-planned replay): the count pass runs
+// ndesc = an upper bound of workgroups and reads the true count from plan[0];
+// the digest pass strides a fixed grid over the work items item_pref describes.
 hipError_t launch_emit_t(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
-                         u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase) {
+                         u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase,
+                         const int *plan, const int64_t *item_pref) {
   if (count_phase) {
     hipLaunchKernelGGL((dr::k_emit_count<WS, 256>), dim3(ndesc), dim3(256), 0, c->stream, c->view(), pd,
-                       c->masks.as<u64>(), c->K.as<u64>(), rbase, cnt);
+                       c->masks.as<u64>(), c->K.as<u64>(), rbase, cnt, plan);
+  } else if (plan) {
+    hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(2048), dim3(256), 0, c->stream, c->view(),
+                       c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, c->masks.as<u64>(),
+                       c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, item_pref, plan);
   } else {
     const int bx = std::max(1, (span + kEmitRPB - 1) / kEmitRPB);
     hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(bx, ndesc), dim3(256), 0, c->stream, c->view(),
                        c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, c->masks.as<u64>(),
-                       c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap);
+                       c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, (const int64_t *)nullptr,
+                       (const int *)nullptr);
   }
   return hipGetLastError();
 }
 hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
-                       u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase) {
+                       u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase,
+                       const int *plan = nullptr, const int64_t *item_pref = nullptr) {
   if (ndesc <= 0) return hipSuccess;
   switch (c->WS) {
-    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
-    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
-    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
-    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
-    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
-    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase);
+    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
+    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
+    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
+    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
+    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
+    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
   }
   return hipErrorInvalidValue;
 }
@@ -420,6 +470,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
     return DR_E_HIP;
   }
   for (auto &ev : c->ev) (void)hipEventCreate(&ev);
+  (void)hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming);
   const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64);
   if (c->strong.ensure(rows) != hipSuccess ||
       c->present.ensure((size_t)max_rounds * c->WS * sizeof(u64)) != hipSuccess ||
@@ -456,6 +507,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
+  if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -676,7 +728,7 @@ template <class OnBatch>
 int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector<uint64_t> *edges,
                std::vector<uint64_t> *wedges, std::vector<uint8_t> *hits, std::vector<int32_t> *push_n,
                int32_t *push_out_dev, std::vector<int32_t> *stops, OnBatch on_batch, float *ms,
-               std::vector<uint64_t> *qstats = nullptr) {
+               std::vector<uint64_t> *qstats = nullptr, const std::function<int()> &pre_sync = {}) {
   const size_t budget_words = (size_t)1 << 29;  // 4 GiB of frontier masks per batch
   const int WS = c->WS;
   if (edges) edges->assign(qv.size(), 0);
@@ -733,6 +785,8 @@ int run_sweeps(dr_ctx *c, std::vector<dr::SweepQuery> &qv, bool seq, std::vector
     if (push_n) HIPCHK(c, c->d2h(push_n->data() + i0, c->push_n.p, (size_t)nq * 4));
     if (stops) HIPCHK(c, c->d2h(stops->data() + i0, c->stops.p, (size_t)nq * 4));
     if (qstats) HIPCHK(c, c->d2h(qstats->data() + 4 * i0, c->qstats.p, (size_t)nq * 32));
+    if (pre_sync && i1 == qv.size())
+      if (int rc = pre_sync()) return rc;
     HIPCHK(c, c->sync());
     float t = 0;
     HIPCHK(c, hipEventElapsedTime(&t, c->ev[0], c->ev[1]));
@@ -765,7 +819,7 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
   int span = 0;
   for (auto &d : pd) {
     d.rbase_off = rb_words;
-    rb_words += d.last + 1;
+    rb_words += d.last - d.first + 1;
     span = std::max(span, d.last - d.first + 1);
   }
   HIPCHK(c, c->rbase.ensure((size_t)std::max<int64_t>(rb_words, 1) * 4));
@@ -822,7 +876,8 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
 // Round summaries + canonical cone + canonical prefixes for rounds 0..T
 // (T = last mirrored round).  Reads every strong row and weak edge once; with
 // nwc > 0 the same pass decides the commits of waves 1..nwc (host arrays).
-int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr) {
+int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
+                  bool host_out = true) {
   const int T = c->nrounds - 1;
   const int WS = c->WS, dd = c->memo_dd();
   const size_t R = (size_t)T + 1;
@@ -852,7 +907,7 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   HIPCHK(c, hipGetLastError());
   dr::PopDesc d{};
   d.mask_off = 0;
-  d.rbase_off = 0;
+  d.rbase_off = 1;  // crbase is indexed by round; rbase_off addresses round `first`
   d.pos0 = 0;
   d.first = 1;
   d.last = T;
@@ -865,6 +920,9 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
                      c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
+  c->summary_T = T;
+  c->canon_host = false;
+  if (!host_out) return DR_OK;  // planned replay: results stay on the device
   c->hC.resize(R);
   c->hG.resize(R);
   c->hE.resize(R);
@@ -878,7 +936,23 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   }
   HIPCHK(c, c->sync());
   if (ms_summary) HIPCHK(c, hipEventElapsedTime(ms_summary, c->ev[6], c->ev[7]));
-  c->summary_T = T;
+  c->canon_host = true;
+  return DR_OK;
+}
+
+// host copies of the canonical prefixes (after a planned replay left them on the device)
+int fetch_canon(dr_ctx *c) {
+  if (c->canon_host) return DR_OK;
+  const size_t R = (size_t)c->summary_T + 1;
+  c->hC.resize(R);
+  c->hG.resize(R);
+  c->hE.resize(R);
+  HIPCHK(c, c->d2h(c->hC.data(), c->Cc.p, R * 8));
+  HIPCHK(c, c->d2h(c->hG.data(), c->Gc.p, R * 8));
+  HIPCHK(c, c->d2h(c->hE.data(), c->Ec.p, R * 8));
+  HIPCHK(c, c->d2h(&c->canon_segments, c->nseg.p, 4));
+  HIPCHK(c, c->sync());
+  c->canon_host = true;
   return DR_OK;
 }
 
@@ -896,13 +970,17 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     c->use_memo = value != 0;
     return DR_OK;
   }
+  if (option == DR_OPT_DEVICE_PLAN) {
+    c->plan_mode = value != 0;
+    return DR_OK;
+  }
   return c->fail(DR_E_INVAL, "unknown option %d", option);
 }
 
 namespace {
-template <int WS, int SV>
+template <int WS, int SV, int NTO = 0>
 hipError_t launch_sv(dr_ctx *c, int T) {
-  constexpr int NT = block_for<WS>();
+  constexpr int NT = NTO ? (NTO < 64 * (WS / (WS >= 2 ? 2 : 1)) ? block_for<WS>() : NTO) : block_for<WS>();
   const dr::MemoView mv = c->memo_view();
   hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, SV>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T,
                      T / 4, mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(),
@@ -916,6 +994,8 @@ hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
     case 1: return launch_sv<WS, dr::SV_NO_WEAK>(c, T);
     case 2: return launch_sv<WS, dr::SV_NO_ROWS>(c, T);
     case 3: return launch_sv<WS, dr::SV_UNR8>(c, T);
+    case 4: return launch_sv<WS, 0, 512>(c, T);
+    case 5: return launch_sv<WS, 0, 256>(c, T);
   }
   return hipErrorInvalidValue;
 }
@@ -953,6 +1033,11 @@ extern "C" int dr_profile_kernel(dr_ctx *c, int kernel, int variant, int iters, 
     }
     if (kernel == 1) {
       const size_t a16 = (size_t)c->nrounds * c->n * c->WS / 2;
+      if (variant == 2) {  // blocked pattern: one workgroup per 4-round wave's worth of rows
+        hipLaunchKernelGGL((dr::k_stream_read_blocked<1024>), dim3(1000), dim3(1024), 0, c->stream,
+                           reinterpret_cast<const dr::u64x2 *>(c->strong.p), a16, c->edges.as<u64>());
+        return hipGetLastError();
+      }
       hipLaunchKernelGGL((dr::k_stream_read<256>), dim3(2048), dim3(256), 0, c->stream,
                          reinterpret_cast<const dr::u64x2 *>(c->strong.p), a16, c->edges.as<u64>());
       hipError_t e = hipGetLastError();
@@ -1122,12 +1207,14 @@ int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::
   HIPCHK(c, c->push_out.ensure((size_t)std::max<int64_t>(off, 1) * 4));
   std::vector<uint64_t> edges;
   std::vector<int32_t> pn;
-  int rc = run_sweeps(c, qv, false, &edges, nullptr, nullptr, &pn, c->push_out.as<int32_t>(), nullptr,
-                      [](size_t, size_t) { return 0; }, ms);
-  if (rc) return rc;
   std::vector<int32_t> po((size_t)off);
-  HIPCHK(c, c->d2h(po.data(), c->push_out.p, (size_t)off * 4));
-  HIPCHK(c, c->sync());
+  // chain queries carry no masks: one batch, whose sync also brings push_out
+  int rc = run_sweeps(c, qv, false, &edges, nullptr, nullptr, &pn, c->push_out.as<int32_t>(), nullptr,
+                      [](size_t, size_t) { return 0; }, ms, nullptr, [&]() -> int {
+                        HIPCHK(c, c->d2h(po.data(), c->push_out.p, (size_t)off * 4));
+                        return 0;
+                      });
+  if (rc) return rc;
   uint64_t et = 0;
   for (size_t k = 0; k < qv.size(); k++) {
     et += edges[k];
@@ -1159,6 +1246,8 @@ int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pco
   const bool want_ids = ids && ids_cap > 0;
   const bool paper = mode == DR_DELIVER_PAPER;
   const bool memo = !paper && summary_fresh(c);
+  if (memo)
+    if (int rc = fetch_canon(c)) return rc;
   std::vector<dr::SweepQuery> qv;
   std::vector<int> pop2q(pops.size());
   if (!paper && !want_ids) {
@@ -1354,6 +1443,192 @@ extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack,
   return DR_OK;
 }
 
+namespace {
+// bump allocator over one device buffer (sizing pass with base == nullptr)
+struct Carve {
+  char *base = nullptr;
+  size_t off = 0;
+  template <class T> T *take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T *p = reinterpret_cast<T *>(base + off);
+    off += std::max<size_t>(n, 1) * sizeof(T);
+    return p;
+  }
+};
+
+// Device-planned replay (memo summaries, DR_DELIVER_REF, no ids): the same
+// phases as the host-planned path below, planned by replay_plan.hpp's kernels,
+// with one host synchronisation.  Returns 1 when the bounds do not fit (the
+// caller then takes the host-planned path), else a DR_* status.
+int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
+  const int WS = c->WS, T = c->nrounds - 1;
+  const bool persistent = chain_mode == DR_CHAIN_PERSISTENT;
+  const int64_t pbound = persistent ? 2 * (int64_t)nw + 1 : (int64_t)nw * (nw + 1) / 2;
+  const int64_t pcap = std::max<int64_t>(1, std::min<int64_t>(o->push_cap, pbound));
+  const int64_t chain_slots = persistent ? nw : (int64_t)nw * (nw - 1) / 2;
+  const int64_t rb_cap = pcap * (int64_t)(T + 1);
+  size_t mask_words = 0;  // every wave's leader a distinct query: rounds 0..4(w-1)+1
+  for (int w = 1; w <= nw; w++) mask_words += (size_t)(4 * (w - 1) + 2) * WS;
+  if (mask_words > ((size_t)1 << 29) || rb_cap > ((int64_t)1 << 28) || chain_slots > INT32_MAX) return 1;
+  // device arena
+  Carve cv;
+  int32_t *plan = nullptr, *task_wave, *task_q, *cpush_n, *push_out, *push_wave, *pop_wave, *pop_cur, *pop_q,
+          *desc_of_pop, *qidx, *dstops;
+  int64_t *task_pos, *item_pref;
+  uint32_t *push_off, *rbase;
+  uint8_t *seen, *hits;
+  dr::SweepQuery *cq, *dq;
+  dr::PopDesc *pd;
+  u64 *cedges, *cwedges, *dedges, *dwedges, *dstats, *extra_c, *extra_g, *pedges, *counts, *digest;
+  int32_t *cstops;
+  for (int pass = 0; pass < 2; pass++) {
+    cv.off = 0;
+    plan = cv.take<int32_t>(dr::PL_N);
+    task_wave = cv.take<int32_t>(nw);
+    task_q = cv.take<int32_t>(nw);
+    task_pos = cv.take<int64_t>(nw);
+    cq = cv.take<dr::SweepQuery>(nw);
+    dq = cv.take<dr::SweepQuery>(nw);
+    cpush_n = cv.take<int32_t>(nw);
+    cedges = cv.take<u64>(nw);
+    cwedges = cv.take<u64>(nw);
+    cstops = cv.take<int32_t>(nw);
+    hits = cv.take<uint8_t>(nw);
+    push_out = cv.take<int32_t>((size_t)chain_slots);
+    dedges = cv.take<u64>(nw);
+    dwedges = cv.take<u64>(nw);
+    dstops = cv.take<int32_t>(nw);
+    dstats = cv.take<u64>(4 * (size_t)nw);
+    seen = cv.take<uint8_t>(nw + 1);
+    qidx = cv.take<int32_t>(nw + 1);
+    push_off = cv.take<uint32_t>(nw + 1);
+    push_wave = cv.take<int32_t>(pcap);
+    pop_wave = cv.take<int32_t>(pcap);
+    pop_cur = cv.take<int32_t>(pcap);
+    pop_q = cv.take<int32_t>(pcap);
+    desc_of_pop = cv.take<int32_t>(pcap);
+    extra_c = cv.take<u64>(pcap);
+    extra_g = cv.take<u64>(pcap);
+    pedges = cv.take<u64>(pcap);
+    counts = cv.take<u64>(pcap);
+    digest = cv.take<u64>(pcap);
+    item_pref = cv.take<int64_t>(pcap + 1);
+    pd = cv.take<dr::PopDesc>(pcap);
+    rbase = cv.take<uint32_t>((size_t)rb_cap);
+    if (pass == 0) {
+      HIPCHK(c, c->plan_arena.ensure(cv.off));
+      cv.base = static_cast<char *>(c->plan_arena.p);
+    }
+  }
+  HIPCHK(c, c->masks.ensure(mask_words * 8));
+  // host-visible outputs (pinned, written by k_plan_final)
+  void *hp = nullptr;
+  const size_t h_bytes = 16 * 8 + (size_t)nw + 4 * (size_t)nw + 4 * ((size_t)nw + 1) + 4 * (size_t)pcap +
+                         3 * 8 * (size_t)pcap + 5 * 64;
+  HIPCHK(c, c->stage(h_bytes, &hp));
+  Carve hv;
+  hv.base = static_cast<char *>(hp);
+  u64 *h_hdr = hv.take<u64>(dr::PH_N);
+  uint8_t *h_commit = hv.take<uint8_t>(nw);
+  int32_t *h_vcount = hv.take<int32_t>(nw);
+  uint32_t *h_push_off = hv.take<uint32_t>(nw + 1);
+  int32_t *h_push_wave = hv.take<int32_t>(pcap);
+  u64 *h_pc = hv.take<u64>(pcap), *h_pd = hv.take<u64>(pcap), *h_pe = hv.take<u64>(pcap);
+  if (hv.off > c->pin_cap - (static_cast<char *>(hp) - c->pin)) return c->fail(DR_E_STATE, "staging overflow");
+
+  // 0+1. summaries + canonical cone + commits (no host copies)
+  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false)) return rc;
+  const int sc = dr::Q_SHORTCUT;
+  // 2. leader chains
+  hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(), nw,
+                     persistent ? 1 : 0, dr::Q_CHAIN | dr::Q_STRONG_ONLY | sc, task_wave, task_q, cq, plan);
+  HIPCHK(c, hipGetLastError());
+  SweepArgs a;
+  a.q = cq;
+  a.nq = nw;
+  a.seq = 0;
+  a.masks = c->masks.as<u64>();
+  a.dlv = nullptr;
+  a.push_out = push_out;
+  a.push_n = cpush_n;
+  a.edges = cedges;
+  a.wedges = cwedges;
+  a.hits = hits;
+  a.stops = cstops;
+  a.stats = nullptr;
+  a.nq_dev = plan + dr::PL_NQC;
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(c, launch_sweep(c, a, dr::SW_CHAIN));
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  // 3. pops + delivery sweeps
+  hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
+                     dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, task_wave, task_q, cq, cpush_n, push_out, pcap,
+                     task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
+  HIPCHK(c, hipGetLastError());
+  a.q = dq;
+  a.push_out = nullptr;
+  a.edges = dedges;
+  a.wedges = dwedges;
+  a.stops = dstops;
+  a.stats = dstats;
+  a.nq_dev = plan + dr::PL_NQD;
+  dr::SweepQuery probe{};
+  probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
+  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
+  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  // 4. emission
+  hipLaunchKernelGGL((dr::k_plan_emit<1024>), dim3(1), dim3(1024), 0, c->stream, pop_cur, pop_q, dq, dstops,
+                     c->Cc.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), dedges, kEmitRPB, rb_cap, pd, desc_of_pop,
+                     extra_c, extra_g, pedges, digest, item_pref, plan);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, counts, nullptr, nullptr, nullptr, nullptr, 0, true,
+                        plan + dr::PL_NDESC, nullptr));
+  HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, nullptr, digest, nullptr, nullptr, nullptr, 0, false,
+                        plan + dr::PL_NDESC, item_pref));
+  HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+  hipLaunchKernelGGL((dr::k_plan_final<1024>), dim3(1), dim3(1024), 0, c->stream, nw, c->commit.as<uint8_t>(),
+                     c->vcount.as<int32_t>(), push_off, push_wave, desc_of_pop, extra_c, extra_g, pedges, counts,
+                     digest, cedges, dstats, c->nseg.as<int32_t>(), plan, h_commit, h_vcount, h_push_off,
+                     h_push_wave, h_pc, h_pd, h_pe, h_hdr);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, c->sync());
+  // outputs
+  HIPCHK(c, hipEventElapsedTime(&o->ms_summary, c->ev[6], c->ev[7]));
+  HIPCHK(c, hipEventElapsedTime(&o->ms_chain, c->ev[0], c->ev[1]));
+  HIPCHK(c, hipEventElapsedTime(&o->ms_deliver, c->ev[2], c->ev[3]));
+  HIPCHK(c, hipEventElapsedTime(&o->ms_emit, c->ev[4], c->ev[5]));
+  std::memcpy(o->commit, h_commit, (size_t)nw);
+  std::memcpy(o->vcount, h_vcount, (size_t)nw * 4);
+  c->canon_segments = (int32_t)(int64_t)h_hdr[dr::PH_NSEG];
+  o->canon_segments = c->canon_segments;
+  uint64_t ce = 0;
+  for (int w = 1; w <= nw; w++)
+    if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
+  o->commit_edges = ce;
+  o->chain_edges = h_hdr[dr::PH_CHAIN_E];
+  const int64_t np = (int64_t)h_hdr[dr::PH_NPUSH];
+  o->n_push = np;
+  if (h_hdr[dr::PH_CAPERR] == 2) return c->fail(DR_E_STATE, "replay planner: segment bound exceeded");
+  if (h_hdr[dr::PH_CAPERR] || np > o->push_cap)
+    return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)np, (long long)o->push_cap);
+  std::memcpy(o->push_off, h_push_off, ((size_t)nw + 1) * 4);
+  std::memcpy(o->push_wave, h_push_wave, (size_t)np * 4);
+  std::memcpy(o->pop_count, h_pc, (size_t)np * 8);
+  std::memcpy(o->pop_digest, h_pd, (size_t)np * 8);
+  if (o->pop_edges) std::memcpy(o->pop_edges, h_pe, (size_t)np * 8);
+  o->deliver_edges = h_hdr[dr::PH_DELIVER_E];
+  o->sweep_count = h_hdr[dr::PH_NQD];
+  o->sweep_partial = h_hdr[dr::PH_PARTIAL];
+  o->sweep_rows = h_hdr[dr::PH_ROWS];
+  o->sweep_weak_scanned = h_hdr[dr::PH_WEAK];
+  o->sweep_shortcut = h_hdr[dr::PH_SHORT];
+  o->n_ids = 0;
+  return DR_OK;
+}
+}  // namespace
+
 extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
   if (!c) return DR_E_INVAL;
   if (!o || !o->commit || !o->vcount || !o->push_off) return c->fail(DR_E_INVAL, "null output");
@@ -1365,6 +1640,11 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   o->sweep_count = o->sweep_partial = o->sweep_rows = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;
   o->canon_segments = -1;
+  if (c->plan_mode != 0 && c->use_memo && c->memo_ok() && deliver_mode == DR_DELIVER_REF &&
+      !(o->ids && o->ids_cap > 0) && o->push_wave && o->pop_count && o->pop_digest) {
+    const int rc = replay_planned(c, nwaves, chain_mode, o);
+    if (rc != 1) return rc;
+  }
   // 0+1. round summaries + canonical cone, fused with the commit decisions of
   // every wave (one pass over the DAG per replay); without summaries, k_commit
   if (c->use_memo && c->memo_ok()) {

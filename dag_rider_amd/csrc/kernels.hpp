@@ -407,7 +407,12 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
                                               u64 *__restrict__ wedges_out,
                                               uint8_t *__restrict__ hit_out,
                                               int32_t *__restrict__ stop_out,
-                                              u64 *__restrict__ stats_out) {
+                                              u64 *__restrict__ stats_out, const int *__restrict__ nq_dev) {
+  if (nq_dev) {  // grid sized by an upper bound, count on the device (planned replay)
+    const int m = *nq_dev;
+    if (seq) nq = m;
+    else if ((int)blockIdx.x >= m) return;
+  }
   constexpr bool WEAK = MODE & SW_WEAK, CHAIN = MODE & SW_CHAIN, PRUNE = MODE & SW_PRUNE,
                  MERGE = MODE & SW_MERGE;
   constexpr u64 WMASK = WS >= 64 ? ~0ULL : ((1ULL << WS) - 1ULL);  // lanes owning a frontier word
@@ -827,7 +832,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
 // ---------------------------------------------------------------------------
 struct PopDesc {
   int64_t mask_off;   // word offset of round 0 in its image
-  int64_t rbase_off;  // int offset of round 0 in rbase
+  int64_t rbase_off;  // int offset of round `first` in rbase
   int64_t pos0;       // position of the segment's first vertex within its pop
   int32_t first, last;
   int32_t out;        // pop index (count / digest / ids slot)
@@ -839,8 +844,10 @@ struct PopDesc {
 template <int WS, int NT>
 __global__ __launch_bounds__(NT) void k_emit_count(DagView g, const PopDesc *__restrict__ pd,
                                                    const u64 *__restrict__ masks, const u64 *__restrict__ K,
-                                                   uint32_t *__restrict__ rbase, u64 *__restrict__ count) {
+                                                   uint32_t *__restrict__ rbase, u64 *__restrict__ count,
+                                                   const int *__restrict__ nd_dev) {
   __shared__ uint32_t part[NT];
+  if (nd_dev && (int)blockIdx.x >= *nd_dev) return;  // grid sized by an upper bound
   const PopDesc d = pd[blockIdx.x];
   const u64 *img = (d.use_k ? K : masks) + d.mask_off;
   const int tid = threadIdx.x;
@@ -864,7 +871,7 @@ __global__ __launch_bounds__(NT) void k_emit_count(DagView g, const PopDesc *__r
   }
   uint32_t run = part[tid] - loc;
   for (int r = ra; r < rb; r++) {
-    rbase[d.rbase_off + r] = run;
+    rbase[d.rbase_off + (r - d.first)] = run;
     const u64 *m = img + (int64_t)r * WS;
     const u64 *p = g.present + (size_t)r * WS;
     uint32_t c = 0;
@@ -881,28 +888,24 @@ __global__ __launch_bounds__(NT) void k_emit_count(DagView g, const PopDesc *__r
 // digest_term(round, source, k); ids land at pop_pos[out] + k.  With
 // round_out != nullptr the per-round digest sums are written instead.
 template <int WS, int NT, int RPB>
-__global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__restrict__ slot_off,
-                                                 const uint16_t *__restrict__ slot_src,
-                                                 const PopDesc *__restrict__ pd,
-                                                 const u64 *__restrict__ masks, const u64 *__restrict__ K,
-                                                 const uint32_t *__restrict__ rbase,
-                                                 const int64_t *__restrict__ pop_pos,
-                                                 u64 *__restrict__ digest, u64 *__restrict__ round_out,
-                                                 int32_t *__restrict__ ids, int64_t ids_cap) {
-  __shared__ u64 s_dg;
-  const PopDesc d = pd[blockIdx.y];
+__device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__restrict__ slot_off,
+                                           const uint16_t *__restrict__ slot_src, const PopDesc &d, int blk,
+                                           const u64 *__restrict__ masks, const u64 *__restrict__ K,
+                                           const uint32_t *__restrict__ rbase, const int64_t *__restrict__ pop_pos,
+                                           u64 *__restrict__ digest, u64 *__restrict__ round_out,
+                                           int32_t *__restrict__ ids, int64_t ids_cap, u64 *s_dg) {
   const u64 *img = (d.use_k ? K : masks) + d.mask_off;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int NWAVE = NT / 64;
-  if (tid == 0) s_dg = 0;
+  if (tid == 0) *s_dg = 0;
   __syncthreads();
   u64 dg = 0;
-  const int ra = d.first + blockIdx.x * RPB;
+  const int ra = d.first + blk * RPB;
   const int rb = min(d.last + 1, ra + RPB);
   const int64_t pbase = pop_pos ? pop_pos[d.out] : 0;
   for (int r = ra + wid; r < rb; r += NWAVE) {
     const u64 *m = img + (int64_t)r * WS;
-    u64 pos = (u64)d.pos0 + rbase[d.rbase_off + r];
+    u64 pos = (u64)d.pos0 + rbase[d.rbase_off + (r - d.first)];
     u64 rdg = 0;
     const uint32_t sa = slot_off[r], sb = slot_off[r + 1];
     for (uint32_t i0 = sa; i0 < sb; i0 += 64) {
@@ -932,12 +935,45 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
       dg += rdg;
     }
   }
-  if (round_out) return;
+  if (round_out) return;  // uniform: no barrier follows
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) dg += __shfl_xor(dg, off);
-  if (lane == 0 && dg) atomicAdd(&s_dg, dg);
+  if (lane == 0 && dg) atomicAdd(s_dg, dg);
   __syncthreads();
-  if (tid == 0 && s_dg) atomicAdd(digest + d.out, s_dg);
+  if (tid == 0 && *s_dg) atomicAdd(digest + d.out, *s_dg);
+}
+
+// Two launch shapes: grid (round blocks, segments) when item_pref is null; else
+// a fixed grid striding over the work items [0, ctl[1]) of ctl[0] segments,
+// segment i owning items [item_pref[i], item_pref[i+1]) (device-planned replay).
+template <int WS, int NT, int RPB>
+__global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__restrict__ slot_off,
+                                                 const uint16_t *__restrict__ slot_src,
+                                                 const PopDesc *__restrict__ pd,
+                                                 const u64 *__restrict__ masks, const u64 *__restrict__ K,
+                                                 const uint32_t *__restrict__ rbase,
+                                                 const int64_t *__restrict__ pop_pos,
+                                                 u64 *__restrict__ digest, u64 *__restrict__ round_out,
+                                                 int32_t *__restrict__ ids, int64_t ids_cap,
+                                                 const int64_t *__restrict__ item_pref, const int *__restrict__ ctl) {
+  __shared__ u64 s_dg;
+  if (!item_pref) {
+    emit_block<WS, NT, RPB>(g, slot_off, slot_src, pd[blockIdx.y], blockIdx.x, masks, K, rbase, pop_pos, digest,
+                            round_out, ids, ids_cap, &s_dg);
+    return;
+  }
+  const int nd = ctl[0];
+  const int64_t nit = item_pref[nd];
+  for (int64_t it = blockIdx.x; it < nit; it += gridDim.x) {
+    int lo = 0, hi = nd - 1;  // last segment with item_pref <= it
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (item_pref[mid] <= it) lo = mid; else hi = mid - 1;
+    }
+    emit_block<WS, NT, RPB>(g, slot_off, slot_src, pd[lo], (int)(it - item_pref[lo]), masks, K, rbase, pop_pos,
+                            digest, round_out, ids, ids_cap, &s_dg);
+    __syncthreads();
+  }
 }
 
 // Canonical per-round delivered counts c_r = |K_r & P_r| (one wave per round).
@@ -984,6 +1020,26 @@ __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restric
   }
 }
 
+// Multi-segment copy between device memory and pinned (device-mapped) host
+// memory: one launch moves every small result of a call, instead of one blit
+// (and one queue round trip) per array.  blockIdx.y = segment.
+struct CopySeg { const uint8_t *src; uint8_t *dst; uint64_t n; };
+constexpr int kCopySegs = 16;
+struct CopyList { CopySeg s[kCopySegs]; };
+
+__global__ __launch_bounds__(256) void k_copy(CopyList L) {
+  const CopySeg sg = L.s[blockIdx.y];
+  const size_t stride = (size_t)gridDim.x * 256, t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  size_t head = 0;
+  if ((((uintptr_t)sg.src | (uintptr_t)sg.dst) & 15) == 0) {
+    head = sg.n & ~(uint64_t)15;
+    const u32x4 *a = reinterpret_cast<const u32x4 *>(sg.src);
+    u32x4 *b = reinterpret_cast<u32x4 *>(sg.dst);
+    for (size_t i = t; i < head / 16; i += stride) b[i] = a[i];
+  }
+  for (size_t i = head + t; i < sg.n; i += stride) sg.dst[i] = sg.src[i];
+}
+
 // Calibration: read n16 16-B words (grid-stride, 4 in flight per thread) and
 // fold them so nothing is dead-code eliminated.  The practical ceiling for the
 // streaming kernels (dr_profile_kernel).
@@ -999,6 +1055,24 @@ __global__ __launch_bounds__(NT) void k_stream_read(const u64x2 *__restrict__ p,
   }
   for (; i < n16; i += stride) { const u64x2 a = __builtin_nontemporal_load(p + i); acc ^= a.x ^ a.y; }
   if (acc == 0x9E3779B97F4A7C15ULL) out[0] = acc;  // practically never taken
+}
+
+// Calibration, blocked pattern: workgroup b reads its own contiguous chunk
+// (the access shape of one-workgroup-per-wave kernels).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_stream_read_blocked(const u64x2 *__restrict__ p, size_t n16,
+                                                            u64 *__restrict__ out) {
+  u64 acc = 0;
+  const size_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const size_t a = (size_t)blockIdx.x * per, b = min(n16, a + per);
+  size_t i = a + threadIdx.x;
+  for (; i + 3 * NT < b; i += 4 * NT) {
+    const u64x2 x = __builtin_nontemporal_load(p + i), y = __builtin_nontemporal_load(p + i + NT);
+    const u64x2 z = __builtin_nontemporal_load(p + i + 2 * NT), w = __builtin_nontemporal_load(p + i + 3 * NT);
+    acc ^= x.x ^ x.y ^ y.x ^ y.y ^ z.x ^ z.y ^ w.x ^ w.y;
+  }
+  for (; i < b; i += NT) { const u64x2 x = __builtin_nontemporal_load(p + i); acc ^= x.x ^ x.y; }
+  if (acc == 0x9E3779B97F4A7C15ULL) out[0] = acc;
 }
 
 }  // namespace dr

@@ -74,6 +74,10 @@ class Engine:
         """DR_OPT_MEMO: round summaries + canonical cone (identical results either way)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_MEMO, int(on)))
 
+    def set_device_plan(self, on: bool):
+        """DR_OPT_DEVICE_PLAN: plan dr_replay's phases on the device (identical results either way)."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_DEVICE_PLAN, int(on)))
+
     def profile_kernel(self, kernel: int, variant: int = 0, iters: int = 20) -> float:
         """dr_profile_kernel: average device ms of one kernel variant (tuning hook)."""
         ms = L.f32()

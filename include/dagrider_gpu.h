@@ -44,7 +44,7 @@ enum {
   DR_E_STATE = -6     /* call order violated (e.g. append not contiguous) */
 };
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
-enum { DR_OPT_MEMO = 1 };
+enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
 
 typedef struct dr_ctx dr_ctx;
@@ -62,7 +62,11 @@ const char *dr_last_error(const dr_ctx *ctx);
 /* number of rounds currently mirrored (len(p.dag)) */
 int dr_num_rounds(const dr_ctx *ctx);
 /* DR_OPT_MEMO (default 1): use round summaries + the canonical cone for
- * orderVertices / path sweeps (identical results; 0 = sweep every cone). */
+ * orderVertices / path sweeps (identical results; 0 = sweep every cone).
+ * DR_OPT_DEVICE_PLAN (default 1): dr_replay plans its chain, pop and emission
+ * phases on the device (one host synchronisation per replay) when summaries
+ * are on, deliver_mode is DR_DELIVER_REF and no ids are requested; 0 = plan
+ * on the host between phases (identical results). */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 
 /* p.dag[r] = append(p.dag[r], v) (process.go:229) for whole rounds

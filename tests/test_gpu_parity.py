@@ -209,6 +209,31 @@ def test_config_replay(gpu_device, name, memo):
         _compare_replay(got, want, ids=False)
 
 
+@pytest.mark.parametrize("name", ["c1", "c2", "c5"])
+def test_device_planned_replay_matches_host_planned(gpu_device, name):
+    """DR_OPT_DEVICE_PLAN on/off: the device planner restates run_chains/run_deliver exactly
+    (pushes, pops, per-pop counts/digests/edges, sweep statistics, timings aside)."""
+    cfg = CONFIGS[name]
+    d = generate(cfg)
+    with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
+        e.append_packed(d)
+        for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+            e.set_device_plan(True)
+            a = e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF)
+            e.set_device_plan(False)
+            b = e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF)
+            _compare_replay(a, b, ids=False)
+            assert a.chain_edges == b.chain_edges
+            assert a.sweep == b.sweep
+            # twice in a row (arena reuse), then with a push capacity that is too small
+            e.set_device_plan(True)
+            _compare_replay(e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF), b, ids=False)
+            if len(b.push_wave) > 1:
+                with pytest.raises(L.DrError) as ei:
+                    e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF, push_cap=len(b.push_wave) - 1)
+                assert ei.value.code == L.DR_E_CAPACITY
+
+
 def test_c1_literal_ids(gpu_device):
     """C1 seeded n=4: full delivered sequence against the literal restatement."""
     cfg = CONFIGS["c1"]
