@@ -109,7 +109,8 @@ struct dr_ctx {
   size_t pin_cap = 0, pin_used = 0;
   struct Pending { void *dst; void *stage; const void *src; size_t n; };
   std::vector<Pending> pend;
-  hipEvent_t ev_sync = nullptr;
+  hipEvent_t ev_sync = nullptr, ev_sync2 = nullptr, ev_fork = nullptr, ev_join = nullptr;
+  hipStream_t stream2 = nullptr;  // second queue: canonical cone beside the leader chains
   hipError_t launch_copies(const dr::CopySeg *sg, int k) {
     for (int i0 = 0; i0 < k; i0 += dr::kCopySegs) {
       dr::CopyList L{};
@@ -137,8 +138,13 @@ struct dr_ctx {
       if (e == hipSuccess && !small.empty()) e = launch_copies(small.data(), (int)small.size());
     }
     if (e == hipSuccess) e = hipEventRecord(ev_sync, stream);
+    if (e == hipSuccess && stream2) e = hipEventRecord(ev_sync2, stream2);
     if (e == hipSuccess) {
       while ((e = hipEventQuery(ev_sync)) == hipErrorNotReady) {
+      }
+    }
+    if (e == hipSuccess && stream2) {
+      while ((e = hipEventQuery(ev_sync2)) == hipErrorNotReady) {
       }
     }
     if (e == hipSuccess)
@@ -246,6 +252,12 @@ template <int WS>
 constexpr int block_for() {
   return WS == 1 ? 64 : WS == 2 ? 128 : WS == 4 ? 256 : WS == 8 ? 512 : 1024;
 }
+// k_summary_commit: 512 threads at WS 16 (two workgroups per CU overlap each
+// other's per-round barriers: 274 vs 291 us on C4, profiles/r01/v4_tune.txt)
+template <int WS>
+constexpr int summary_block() {
+  return WS == 16 ? 512 : block_for<WS>();
+}
 // sweeps keep more state live across a round: cap the block at 512 threads
 // (256 VGPRs per lane) so nothing spills
 template <int WS>
@@ -331,7 +343,7 @@ hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode) {
   return hipErrorInvalidValue;
 }
 
-constexpr int kEmitRPB = 16;
+constexpr int kEmitRPB = 4;  // rounds per emit workgroup: one per wave
 
 template <int WS>
 // Planned mode (plan != nullptr, device-planned replay): the count pass runs
@@ -373,15 +385,27 @@ hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, ui
 
 template <int WS>
 hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
-  constexpr int NT = block_for<WS>();
+  // rows + commit decisions (U, SD), then the weak-edge unions (WU): two
+  // back-to-back streaming passes beat the fused one (profiles/r01/v5_tune.txt)
+  constexpr int NT = summary_block<WS>();
   const dr::MemoView mv = c->memo_view();
-  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T, nwc,
-                     mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(), cm, vc);
+  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, dr::SV_NO_WEAK>), dim3((T + 3) / 4), dim3(NT), 0, c->stream,
+                     c->view(), T, nwc, mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(), cm,
+                     vc);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || mv.dd == 0) return e;
+  hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, c->stream, c->view(), T, mv.dd,
+                     c->WU.as<u64>());
+  return hipGetLastError();
+}
+
+// canonical cone: K^cand per round, then the exact cone at the bad rounds
+template <int WS>
+hipError_t launch_canon_cone_t(dr_ctx *c, int T) {
+  const dr::MemoView mv = c->memo_view();
   hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
                      c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>());
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int dl = c->depth_log2();
   const size_t lds = c->sweep_lds(dl);
@@ -409,6 +433,18 @@ hipError_t launch_canon_count(dr_ctx *c, int T) {
   }
   return hipErrorInvalidValue;
 }
+hipError_t launch_canon_cone(dr_ctx *c, int T) {
+  switch (c->WS) {
+    case 1: return launch_canon_cone_t<1>(c, T);
+    case 2: return launch_canon_cone_t<2>(c, T);
+    case 4: return launch_canon_cone_t<4>(c, T);
+    case 8: return launch_canon_cone_t<8>(c, T);
+    case 16: return launch_canon_cone_t<16>(c, T);
+    case 32: return launch_canon_cone_t<32>(c, T);
+  }
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_summary(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
   switch (c->WS) {
     case 1: return launch_summary_t<1>(c, T, nwc, cm, vc);
@@ -464,13 +500,15 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   c->WS = next_pow2(c->W);
   c->max_rounds = max_rounds;
   c->dev = device;
-  if (set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     g_create_err = "dr_create: stream creation failed";
     delete c;
     return DR_E_HIP;
   }
   for (auto &ev : c->ev) (void)hipEventCreate(&ev);
-  (void)hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming);
+  for (hipEvent_t *e : {&c->ev_sync, &c->ev_sync2, &c->ev_fork, &c->ev_join})
+    (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
   const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64);
   if (c->strong.ensure(rows) != hipSuccess ||
       c->present.ensure((size_t)max_rounds * c->WS * sizeof(u64)) != hipSuccess ||
@@ -507,7 +545,9 @@ extern "C" void dr_destroy(dr_ctx *c) {
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
-  if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
+  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join})
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -876,8 +916,10 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
 // Round summaries + canonical cone + canonical prefixes for rounds 0..T
 // (T = last mirrored round).  Reads every strong row and weak edge once; with
 // nwc > 0 the same pass decides the commits of waves 1..nwc (host arrays).
+// fork: the canonical cone and its prefixes run on stream2 (joined by the
+// caller through ev_join) while the caller's next phases use stream.
 int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
-                  bool host_out = true) {
+                  bool host_out = true, bool fork = false) {
   const int T = c->nrounds - 1;
   const int WS = c->WS, dd = c->memo_dd();
   const size_t R = (size_t)T + 1;
@@ -900,6 +942,19 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
   HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+  struct Swap {  // launch helpers use c->stream: point it at stream2 for the canonical chain
+    dr_ctx *c;
+    bool on;
+    Swap(dr_ctx *c_, bool on_) : c(c_), on(on_) { if (on) std::swap(c->stream, c->stream2); }
+    ~Swap() { if (on) std::swap(c->stream, c->stream2); }
+  };
+  if (fork) {
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+  }
+  {
+  Swap sw(c, fork);
+  HIPCHK(c, launch_canon_cone(c, T));
   // canonical emission: per-round counts -> positions -> per-round digests -> prefixes
   HIPCHK(c, launch_canon_count(c, T));
   hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
@@ -920,6 +975,8 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
                      c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
+  if (fork) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
+  }
   c->summary_T = T;
   c->canon_host = false;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
@@ -980,7 +1037,7 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
 namespace {
 template <int WS, int SV, int NTO = 0>
 hipError_t launch_sv(dr_ctx *c, int T) {
-  constexpr int NT = NTO ? (NTO < 64 * (WS / (WS >= 2 ? 2 : 1)) ? block_for<WS>() : NTO) : block_for<WS>();
+  constexpr int NT = NTO ? (NTO < 64 * (WS / (WS >= 2 ? 2 : 1)) ? summary_block<WS>() : NTO) : summary_block<WS>();
   const dr::MemoView mv = c->memo_view();
   hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, SV>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T,
                      T / 4, mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(),
@@ -996,6 +1053,26 @@ hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
     case 3: return launch_sv<WS, dr::SV_UNR8>(c, T);
     case 4: return launch_sv<WS, 0, 512>(c, T);
     case 5: return launch_sv<WS, 0, 256>(c, T);
+    case 9: return launch_sv<WS, dr::SV_NO_WEAK, 256>(c, T);
+    case 10: return launch_sv<WS, dr::SV_NO_WEAK, 1024>(c, T);
+    case 6: case 7: case 8: {  // split: rows + commit beside k_weak_union (6: two streams, 7: one, 8: weak alone)
+      hipError_t e = hipSuccess;
+      if (variant != 8) e = launch_sv<WS, dr::SV_NO_WEAK>(c, T);
+      if (e != hipSuccess) return e;
+      if (variant == 6) {
+        if ((e = hipEventRecord(c->ev_fork, c->stream)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(c->stream2, c->ev_fork, 0)) != hipSuccess) return e;
+      }
+      hipStream_t s2 = variant == 6 ? c->stream2 : c->stream;
+      hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, s2, c->view(), T, c->memo_dd(),
+                         c->WU.as<u64>());
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      if (variant == 6) {
+        if ((e = hipEventRecord(c->ev_join, c->stream2)) != hipSuccess) return e;
+        e = hipStreamWaitEvent(c->stream, c->ev_join, 0);
+      }
+      return e;
+    }
   }
   return hipErrorInvalidValue;
 }
@@ -1537,7 +1614,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   if (hv.off > c->pin_cap - (static_cast<char *>(hp) - c->pin)) return c->fail(DR_E_STATE, "staging overflow");
 
   // 0+1. summaries + canonical cone + commits (no host copies)
-  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false)) return rc;
+  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true)) return rc;
   const int sc = dr::Q_SHORTCUT;
   // 2. leader chains
   hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(), nw,
@@ -1574,6 +1651,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   a.nq_dev = plan + dr::PL_NQD;
   dr::SweepQuery probe{};
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // merge sweeps read the canonical cone K
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
@@ -1588,7 +1666,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, nullptr, digest, nullptr, nullptr, nullptr, 0, false,
                         plan + dr::PL_NDESC, item_pref));
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
-  hipLaunchKernelGGL((dr::k_plan_final<1024>), dim3(1), dim3(1024), 0, c->stream, nw, c->commit.as<uint8_t>(),
+  hipLaunchKernelGGL((dr::k_plan_final<256>), dim3(16), dim3(256), 0, c->stream, nw, c->commit.as<uint8_t>(),
                      c->vcount.as<int32_t>(), push_off, push_wave, desc_of_pop, extra_c, extra_g, pedges, counts,
                      digest, cedges, dstats, c->nseg.as<int32_t>(), plan, h_commit, h_vcount, h_push_off,
                      h_push_wave, h_pc, h_pd, h_pe, h_hdr);

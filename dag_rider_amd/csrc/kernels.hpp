@@ -71,6 +71,51 @@ __device__ __forceinline__ u64 digest_term(uint32_t round, uint32_t source, u64 
   return mix64(key ^ mix64(k + 0x9E3779B97F4A7C15ULL));
 }
 
+// ---------------------------------------------------------------------------
+// Wave reductions on DPP row operations (rows of 16 lanes) + readlane: no LDS
+// traffic, no ds_bpermute latency chain.  Every lane of the wave must be active.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ u64 dpp64(u64 x) {
+  return ((u64)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | (u64)dpp32<CTRL>((uint32_t)x);
+}
+enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141,
+             DPP_ROW_ROR = 0x120 };
+__device__ __forceinline__ u64 readlane64(u64 x, int l) {
+  return ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+}
+// OR of all 64 lanes (wave-uniform result)
+__device__ __forceinline__ u64 wave_or(u64 x) {
+  x |= dpp64<DPP_QP_1032>(x);
+  x |= dpp64<DPP_QP_2301>(x);
+  x |= dpp64<DPP_ROW_HALF_MIRROR>(x);
+  x |= dpp64<DPP_ROW_MIRROR>(x);
+  return readlane64(x, 0) | readlane64(x, 16) | readlane64(x, 32) | readlane64(x, 48);
+}
+// sum of all 64 lanes (wave-uniform result)
+__device__ __forceinline__ u64 wave_sum(u64 x) {
+  x += dpp64<DPP_QP_1032>(x);
+  x += dpp64<DPP_QP_2301>(x);
+  x += dpp64<DPP_ROW_HALF_MIRROR>(x);
+  x += dpp64<DPP_ROW_MIRROR>(x);
+  return readlane64(x, 0) + readlane64(x, 16) + readlane64(x, 32) + readlane64(x, 48);
+}
+// OR over the lanes of a row with equal (lane mod C), C a power of two < 16:
+// afterwards lane l of every row holds the OR of its row's class l mod C.
+template <int C>
+__device__ __forceinline__ u64 row_or_stride(u64 x) {
+  if constexpr (C <= 1) x |= dpp64<DPP_ROW_ROR + 1>(x);
+  if constexpr (C <= 2) x |= dpp64<DPP_ROW_ROR + 2>(x);
+  if constexpr (C <= 4) x |= dpp64<DPP_ROW_ROR + 4>(x);
+  if constexpr (C <= 8) x |= dpp64<DPP_ROW_ROR + 8>(x);
+  return x;
+}
+
 // Geometry per row stride: chunks are 16 B (two words) for WS >= 2, one word for WS == 1.
 template <int WS, int NT>
 struct Geo {
@@ -219,27 +264,27 @@ __device__ __forceinline__ uint32_t walk_weak(const uint32_t *__restrict__ weak,
       int w0 = -1;
       u64 acc = 0;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+      for (int j = 0; j < 4; j++) {  // selects, not branches: the common case is one word per lane
         const uint32_t e = a0 + 4u * (uint32_t)vi + (uint32_t)j;
-        if (vi >= nvec || e < e0 || e >= e1) continue;
         const uint32_t x = xs[j];
         const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
-        if (!keep(own)) continue;
-        kept++;
+        const bool valid = vi < nvec && e >= e0 && e < e1 && keep(own);
+        kept += valid ? 1u : 0u;
         const u64 bit = 1ULL << (ts & 63);
-        const int dw = dest(delta, ts);
-        if (dw < 0) { far(delta, ts, bit); continue; }
-        if (w0 < 0) { w0 = dw; acc = bit; }
-        else if (dw == w0) acc |= bit;
-        else atomicOr(&lds[dw], bit);
+        const int dw = valid ? dest(delta, ts) : -2;
+        if (dw == -1) far(delta, ts, bit);  // rare
+        const bool first = dw >= 0 && w0 < 0;
+        const bool same = dw >= 0 && dw == w0;
+        w0 = first ? dw : w0;
+        acc |= (first || same) ? bit : 0ULL;
+        if (dw >= 0 && !first && !same) atomicOr(&lds[dw], bit);  // rare: a second word in one lane
       }
       // wave-uniform destination: one OR-reduction + one atomic
       const u64 nzm = __ballot(w0 >= 0);
       if (!nzm) continue;
-      const int lead = __shfl(w0, __builtin_ctzll(nzm));
+      const int lead = __builtin_amdgcn_readlane(w0, __builtin_ctzll(nzm));
       if (__all(w0 < 0 || w0 == lead)) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) acc |= __shfl_xor(acc, off);
+        acc = wave_or(acc);  // lanes without a kept edge hold acc = 0
         if (lane == 0 && acc) atomicOr(&lds[lead], acc);
       } else if (w0 >= 0) {
         atomicOr(&lds[w0], acc);
@@ -287,13 +332,13 @@ __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *
       my_edges += (u64)(popc64(v0[p]) + popc64(v1[p]));
     }
   }
-#pragma unroll
-  for (int off = CPR; off < 64; off <<= 1) {
-    a0 |= __shfl_xor(a0, off);
-    if constexpr (CW == 2) a1 |= __shfl_xor(a1, off);
+  // chunk j = lane mod CPR: fold each row's lanes of class j, then one LDS OR per row
+  if constexpr (CPR < 16) {
+    a0 = row_or_stride<CPR>(a0);
+    if constexpr (CW == 2) a1 = row_or_stride<CPR>(a1);
   }
-  if (lane < CPR) {
-    u64 *dst = ring + (size_t)((r - 1) & dmask) * WS + lane * CW;
+  if ((lane & 15) < CPR) {
+    u64 *dst = ring + (size_t)((r - 1) & dmask) * WS + (lane & 15) * CW;
     if (a0) atomicOr(dst, a0);
     if (CW == 2 && a1) atomicOr(dst + 1, a1);
   }
@@ -677,22 +722,20 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
       walk_weak<NT, (SV & SV_UNR8) ? 8 : 4>(
           g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
           [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
-#pragma unroll
-    for (int off = CPR; off < 64; off <<= 1) {
-      a0 |= __shfl_xor(a0, off);
-      if constexpr (CW == 2) a1 |= __shfl_xor(a1, off);
+    if constexpr (CPR < 16) {
+      a0 = row_or_stride<CPR>(a0);
+      if constexpr (CW == 2) a1 = row_or_stride<CPR>(a1);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) deg += __shfl_xor(deg, off);
-    if (lane < CPR) {
-      if (a0) atomicOr(&sU[lane * CW], a0);
-      if (CW == 2 && a1) atomicOr(&sU[lane * CW + 1], a1);
+    deg = wave_sum(deg);
+    if ((lane & 15) < CPR) {
+      if (a0) atomicOr(&sU[(lane & 15) * CW], a0);
+      if (CW == 2 && a1) atomicOr(&sU[(lane & 15) * CW + 1], a1);
     }
     if (lane == 0 && deg) atomicAdd(&sSD, deg);
     __syncthreads();
     for (int i = tid; i < WS * (dd + 1); i += NT) {
       if (i < WS) U[(size_t)r * WS + i] = sU[i];
-      else WU[(size_t)r * dd * WS + (i - WS)] = sWU[i - WS];
+      else if (!(SV & SV_NO_WEAK)) WU[(size_t)r * dd * WS + (i - WS)] = sWU[i - WS];
     }
     if (tid == 0) SD[r] = sSD;
     if (test && tid < WS) { S[tid] = Tn[tid]; Tn[tid] = 0; }
@@ -710,6 +753,22 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
       commit[w - 1] = vc >= quorum ? 1 : 0;
     }
   }
+}
+
+// WU_r[delta] = the union of round r's weak targets at distance delta, one
+// workgroup per round (the weak half of k_summary_commit as a separate stream:
+// it runs beside the rows + commit pass, k_summary_commit<SV_NO_WEAK>).
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64 *__restrict__ WU) {
+  __shared__ u64 sWU[16 * WS];
+  const int r = blockIdx.x + 1, tid = threadIdx.x;
+  if (r > T) return;
+  for (int i = tid; i < dd * WS; i += NT) sWU[i] = 0;
+  __syncthreads();
+  walk_weak<NT, 8>(g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
+                   [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
+  __syncthreads();
+  for (int i = tid; i < dd * WS; i += NT) WU[(size_t)r * dd * WS + i] = sWU[i];
 }
 
 // K^cand_r = U_{r+1} | OR_d WU_{r+d+2}[d] (the cone of round r when every round
@@ -894,6 +953,7 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
                                            const uint32_t *__restrict__ rbase, const int64_t *__restrict__ pop_pos,
                                            u64 *__restrict__ digest, u64 *__restrict__ round_out,
                                            int32_t *__restrict__ ids, int64_t ids_cap, u64 *s_dg) {
+  constexpr int SPL = 16;  // slots per lane per pass: one wave covers 1024 slots with one load latency
   const u64 *img = (d.use_k ? K : masks) + d.mask_off;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int NWAVE = NT / 64;
@@ -904,40 +964,52 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
   const int rb = min(d.last + 1, ra + RPB);
   const int64_t pbase = pop_pos ? pop_pos[d.out] : 0;
   for (int r = ra + wid; r < rb; r += NWAVE) {
-    const u64 *m = img + (int64_t)r * WS;
+    const u64 mw = lane < WS ? img[(int64_t)r * WS + lane] : 0ULL;  // lane w holds mask word w
     u64 pos = (u64)d.pos0 + rbase[d.rbase_off + (r - d.first)];
     u64 rdg = 0;
     const uint32_t sa = slot_off[r], sb = slot_off[r + 1];
-    for (uint32_t i0 = sa; i0 < sb; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      const int src = i < sb ? (int)slot_src[i] : 0;
-      bool in = false;
-      if (src > 0) {
-        const int s = src - 1;
-        in = (m[s >> 6] >> (s & 63)) & 1ULL;
+    for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPL) {
+      const uint32_t i0 = c0 + (uint32_t)lane * SPL;  // this lane's slots, in slot order
+      int src[SPL];
+#pragma unroll
+      for (int j = 0; j < SPL; j++) src[j] = i0 + j < sb ? (int)slot_src[i0 + j] : 0;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int j = 0; j < SPL; j++) {
+        const int s = src[j] - 1;
+        const u64 w = __shfl(mw, s >= 0 ? (s >> 6) : 0);
+        if (s >= 0 && ((w >> (s & 63)) & 1ULL)) bits |= 1u << j;
       }
-      const u64 b = __ballot(in);
-      if (in) {
-        const u64 k = pos + (u64)__popcll(b & ((1ULL << lane) - 1ULL));
-        rdg += digest_term((uint32_t)r, (uint32_t)src, k);
+      const int cnt = __popc(bits);
+      int x = cnt;  // inclusive scan of the lanes' counts = ranks in slot order
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+      }
+      const int total = __shfl(x, 63);
+      u64 k = pos + (u64)(x - cnt);
+#pragma unroll
+      for (int j = 0; j < SPL; j++) {
+        if (!((bits >> j) & 1u)) continue;
+        rdg += digest_term((uint32_t)r, (uint32_t)src[j], k);
         if (ids) {
           const int64_t at = pbase + (int64_t)k;
-          if (at < ids_cap) { ids[2 * at] = r; ids[2 * at + 1] = src; }
+          if (at < ids_cap) { ids[2 * at] = r; ids[2 * at + 1] = src[j]; }
         }
+        k++;
       }
-      pos += (u64)__popcll(b);
+      pos += (u64)total;
     }
     if (round_out) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) rdg += __shfl_xor(rdg, off);
+      rdg = wave_sum(rdg);
       if (lane == 0) round_out[r] = rdg;
     } else {
       dg += rdg;
     }
   }
   if (round_out) return;  // uniform: no barrier follows
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) dg += __shfl_xor(dg, off);
+  dg = wave_sum(dg);
   if (lane == 0 && dg) atomicAdd(s_dg, dg);
   __syncthreads();
   if (tid == 0 && *s_dg) atomicAdd(digest + d.out, *s_dg);

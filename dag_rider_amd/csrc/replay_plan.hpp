@@ -294,7 +294,7 @@ __global__ __launch_bounds__(NT) void k_plan_emit(const int32_t *__restrict__ po
   }
 }
 
-// Outputs -> pinned host memory (h_*), totals -> hdr.
+// Outputs -> pinned host memory (h_*, every workgroup a share), totals -> hdr (workgroup 0).
 template <int NT>
 __global__ __launch_bounds__(NT) void k_plan_final(int nw, const uint8_t *__restrict__ commit,
                                                    const int32_t *__restrict__ vcount,
@@ -310,26 +310,28 @@ __global__ __launch_bounds__(NT) void k_plan_final(int nw, const uint8_t *__rest
                                                    u64 *h_pc, u64 *h_pd, u64 *h_pe, u64 *h_hdr) {
   __shared__ u64 acc[8];
   const int tid = threadIdx.x;
+  const int gt = blockIdx.x * NT + tid, gs = gridDim.x * NT;
   if (tid < 8) acc[tid] = 0;
   __syncthreads();
   const int caperr = plan[PL_CAPERR];
   const int64_t np = caperr ? 0 : plan[PL_NPUSH];
   const int nqc = plan[PL_NQC], nqd = plan[PL_NQD];
-  for (int w = tid; w < nw; w += NT) {
+  for (int w = gt; w < nw; w += gs) {
     h_commit[w] = commit[w];
     h_vcount[w] = vcount[w];
   }
   if (!caperr)
-    for (int w = tid; w <= nw; w += NT) h_push_off[w] = push_off[w];
-  u64 de = 0, ce = 0, st[4] = {0, 0, 0, 0};
-  for (int64_t p = tid; p < np; p += NT) {
+    for (int w = gt; w <= nw; w += gs) h_push_off[w] = push_off[w];
+  for (int64_t p = gt; p < np; p += gs) {
     const int di = desc_of_pop[p];
     h_push_wave[p] = push_wave[p];
     h_pc[p] = extra_c[p] + (di >= 0 ? counts[di] : 0);
     h_pd[p] = extra_g[p] + digest[p];
     h_pe[p] = pedges[p];
-    de += pedges[p];
   }
+  if (blockIdx.x != 0) return;  // totals: workgroup 0 (device-memory reads only)
+  u64 de = 0, ce = 0, st[4] = {0, 0, 0, 0};
+  for (int64_t p = tid; p < np; p += NT) de += pedges[p];
   for (int q = tid; q < nqc; q += NT) ce += cedges[q];
   for (int q = tid; q < nqd; q += NT)
 #pragma unroll

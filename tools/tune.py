@@ -16,7 +16,9 @@ weak_b = int(d.weak_off[-1]) * 4
 cases = [("summary_commit shipped", 0, 0, rows_b + weak_b), ("rows only", 0, 1, rows_b), ("weak only", 0, 2, weak_b),
          ("weak unroll 8", 0, 3, rows_b + weak_b), ("stream rows", 1, 0, rows_b), ("stream rows+weak", 1, 1, rows_b + weak_b),
          ("stream rows blocked", 1, 2, rows_b), ("summary_commit NT=512", 0, 4, rows_b + weak_b),
-         ("summary_commit NT=256", 0, 5, rows_b + weak_b), ("summary phase (all)", 2, 0, rows_b + weak_b)]
+         ("summary_commit NT=256", 0, 5, rows_b + weak_b),
+         ("split 2 streams", 0, 6, rows_b + weak_b), ("split 1 stream", 0, 7, rows_b + weak_b),
+         ("weak_union alone", 0, 8, weak_b), ("rows only NT=256", 0, 9, rows_b), ("rows only NT=1024", 0, 10, rows_b), ("summary phase (all)", 2, 0, rows_b + weak_b)]
 res = {name: [] for name, *_ in cases}
 for rep in range(5):
     for name, k, v, b in cases:
