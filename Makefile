@@ -26,7 +26,7 @@ $(BUILD):
 $(BUILD)/dag_gen.o: $(PKG)/csrc/dag_gen.cpp include/dagrider_gen.h | $(BUILD)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp include/dagrider_gpu.h | $(BUILD)
+$(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp include/dagrider_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(BUILD)/engine.o $(BUILD)/dag_gen.o

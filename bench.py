@@ -25,6 +25,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950
+# correction of MI355X_MICROARCH.md) on this bench: tools/pmc_traffic.py output
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "traffic.json")
+# replay phase -> the kernels it launches (names as rocprofv3 reports them)
+PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 512, 1>", "dr::k_weak_union<16, 256>"],
+                 "sweep": ["dr::k_sweep<16, 512, 9>"],
+                 "batch": ["dr::k_replay_small<8>"]}
+
+
+def measured_traffic(phase):
+    """PMC-measured HBM bytes per launch of a phase's kernels, or None if not profiled."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+        return sum(t[k]["traffic_bytes"] for k in PHASE_KERNELS[phase])
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def log(*a):
@@ -226,7 +243,8 @@ def main():
                    "n": cfg.n, "rounds": cfg.last_round, "waves": cfg.nwaves,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                     "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic(dom),
+                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r01/traffic.json)",
                      "kernel": kb[dom]["kernel"], "bytes_per_launch": kb[dom]["bytes"],
                      "ms_per_launch": kb[dom]["ms"]},
         "cpu_baseline": cpu,

@@ -53,6 +53,7 @@ SIGNATURES = {
     "dr_order_vertices": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, C.c_size_t,
                                     C.POINTER(C.c_size_t), P, P]),
     "dr_replay": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
+    "dr_replay_batch": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
     "dr_profile_kernel": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(f32)]),
     "dr_gen_create": (C.c_int, [C.POINTER(GenParams), C.POINTER(P)]),
     "dr_gen_free": (None, [P]),

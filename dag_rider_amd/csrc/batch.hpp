@@ -1,0 +1,343 @@
+// batch.hpp -- fused replay of many small DAGs: one wavefront per DAG.
+//
+// thousands of independent replays (one Process mirror
+// each, n <= 128, up to 64 waves).  A per-DAG dr_replay would spend its time in
+// launches and host round trips; here one kernel replays every DAG of a batch,
+// a wavefront per DAG, everything between the DAG in HBM and the per-pop
+// results on the device.
+//
+// Per DAG (T = 4*(nw-1)+1, the highest leader round):
+//   1. commits (waveReady's rule, process.go:326-339), wave by wave: S0 =
+//      {leader}; S_k = ballot(row(v) & S_{k-1} != 0) over rounds 4w-2..4w.
+//   2. one top-down pass over rounds T..1 computing, for every vertex v, the
+//      set of leader waves whose cone contains v: Qs (strong edges only, the
+//      chains' strong_path) and Qf (strong + weak, orderVertices' path(.., false)).
+//      Strong: lane u of round r-1 ORs Q(v) of every v of round r whose row has
+//      bit u (rows broadcast by readlane).  Weak: LDS atomics into a ring of
+//      pending rounds.  Q and degrees go to a per-DAG scratch.
+//   3. chains (process.go:341-350) from the leaders' Qs: wave w' is pushed
+//      after leader L iff L's bit is in Qs(leader(w')); pops = reverse pushes.
+//   4. bottom-up emission, lane b = leader wave b+1: for each round's slots in
+//      order, vertex v is delivered by b (REF) iff b in Qf(v), or (PAPER) iff
+//      additionally no leader popped before b's first pop is in Qf(v); position
+//      counters give the order-sensitive digest.  Chain edges
+//      come from per-leader prefix sums of strong degrees over Qs at the leader
+//      rounds.
+// Supported: n <= 128, nw <= 64, weak deltas < ring depth (<= 32), no far edges.
+#pragma once
+#include "kernels.hpp"
+
+namespace dr {
+
+struct SmallJob {
+  const u64 *strong;
+  const u64 *present;
+  const uint32_t *weak;
+  const uint32_t *weak_roff;
+  const uint32_t *slot_off;
+  const uint16_t *slot_src;
+  // scratch, rounds 0..T: Qf, Qs, (deg << 16 | strong deg)
+  u64 *qf;
+  u64 *qs;
+  uint32_t *deg;
+  // outputs
+  uint8_t *commit;      // [nw]
+  int32_t *vcount;      // [nw]
+  uint32_t *push_off;   // [nw + 1]
+  int32_t *push_wave;   // [push_cap]
+  u64 *pop_count;       // [push_cap]
+  u64 *pop_digest;      // [push_cap]
+  u64 *pop_edges;       // [push_cap]
+  u64 *totals;          // [4]: commit edges, chain edges, deliver edges, n_push
+  int32_t n, WS, push_cap, quorum;  // quorum = 2f+1 (process.go:337)
+};
+
+constexpr int kSmallMaxPops = 64 * 65 / 2;  // literal chains: wave w pushes up to w leaders
+
+template <int DEPTH>
+__global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict__ jobs, int njobs, int nw,
+                                                     int chain_persistent, int paper) {
+  constexpr int DM = DEPTH - 1;
+  __shared__ u64 ring[DEPTH * 128];
+  __shared__ u64 QF[128], QS[128];
+  __shared__ uint32_t DG[128];
+  __shared__ uint32_t wcnt[128];
+  __shared__ u64 QL[64];
+  __shared__ int32_t vc_s[64];
+  __shared__ int8_t coef[64 * 65];
+  __shared__ uint8_t pop_lead[kSmallMaxPops];
+  __shared__ int16_t first_pop[64];
+  __shared__ int8_t lst[64];
+  __shared__ uint16_t SL[128];
+  __shared__ u64 res[64 * 6];  // per leader: REF count, digest, edges; PAPER count, digest, edges
+  const int lane = threadIdx.x;
+  const int jb = blockIdx.x;
+  if (jb >= njobs) return;
+  const SmallJob J = jobs[jb];
+  const int n = J.n, WS = J.WS;
+  const int q = J.quorum;
+  const int T = 4 * (nw - 1) + 1;
+  auto row = [&](int r, int v, u64 &a, u64 &b) {  // row of (r, v+1); zero for v >= n
+    a = 0;
+    b = 0;
+    if (v < n) {
+      const u64 *p = J.strong + ((size_t)r * n + v) * WS;
+      if (WS == 2) {
+        const u64x2 x = *reinterpret_cast<const u64x2 *>(p);
+        a = x.x;
+        b = x.y;
+      } else {
+        a = p[0];
+      }
+    }
+  };
+  auto pres_word = [&](int r, int w) -> u64 { return w < WS ? J.present[(size_t)r * WS + w] : 0ULL; };
+
+  // ---------------- 1. commits ----------------
+  u64 commit_mask = 0, lead_mask = 0, commit_edges = 0;
+  for (int w = 1; w <= nw; w++) {
+    const int r1 = 4 * (w - 1) + 1;
+    const bool lead = pres_word(r1, 0) & 1ULL;
+    if (!lead) {
+      if (lane == 0) vc_s[w - 1] = -1;
+      continue;
+    }
+    lead_mask |= 1ULL << (w - 1);
+    u64 a[3][2], b[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      row(r1 + 1 + k, lane, a[k][0], b[k][0]);
+      row(r1 + 1 + k, lane + 64, a[k][1], b[k][1]);
+    }
+    u64 s0 = 1, s1 = 0, deg = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int r = r1 + 1 + k;
+      const u64 p0 = pres_word(r, 0), p1 = pres_word(r, 1);
+      const bool h0 = ((p0 >> lane) & 1ULL) && (((a[k][0] & s0) | (b[k][0] & s1)) != 0ULL);
+      const bool h1 = ((p1 >> lane) & 1ULL) && (((a[k][1] & s0) | (b[k][1] & s1)) != 0ULL);
+      s0 = __ballot(h0);
+      s1 = __ballot(h1);
+      deg += (u64)(__popcll(a[k][0]) + __popcll(b[k][0]) + __popcll(a[k][1]) + __popcll(b[k][1]));
+    }
+    commit_edges += wave_sum(deg);
+    const int vc = __popcll(s0) + __popcll(s1);
+    if (lane == 0) vc_s[w - 1] = vc;
+    if (vc >= q) commit_mask |= 1ULL << (w - 1);
+  }
+
+  // ---------------- 2. top-down Q pass ----------------
+  for (int i = lane; i < DEPTH * 128; i += 64) ring[i] = 0;
+  u64 qf[2] = {0, 0}, qs[2] = {0, 0};
+  __syncthreads();
+  for (int r = T; r >= 1; r--) {
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int v = lane + 64 * i;
+      qf[i] |= ring[(r & DM) * 128 + v];
+      ring[(r & DM) * 128 + v] = 0;
+    }
+    if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its bit at source 1
+      const int w = (r - 1) / 4 + 1;
+      if ((lead_mask >> (w - 1)) & 1ULL) {
+        if (lane == 0) {
+          qf[0] |= 1ULL << (w - 1);
+          qs[0] |= 1ULL << (w - 1);
+          QL[w - 1] = qs[0];
+        }
+      } else if (lane == 0) {
+        QL[w - 1] = 0;
+      }
+    }
+    u64 ra[2], rb[2];
+    row(r, lane, ra[0], rb[0]);
+    row(r, lane + 64, ra[1], rb[1]);
+    QF[lane] = qf[0];
+    QF[lane + 64] = qf[1];
+    wcnt[lane] = 0;
+    wcnt[lane + 64] = 0;
+    __syncthreads();
+    // weak edges of round r: degree per source, Qf into the pending rounds
+    const uint32_t e0 = J.weak_roff[r], e1 = J.weak_roff[r + 1];
+    for (uint32_t e = e0 + lane; e < e1; e += 64) {
+      const uint32_t x = J.weak[e];
+      const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
+      atomicAdd(&wcnt[own], 1u);
+      const u64 f = QF[own];
+      if (f && r - delta >= 1) atomicOr(&ring[((r - delta) & DM) * 128 + ts], f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int v = lane + 64 * i;
+      if (v < n) {
+        const uint32_t sd = (uint32_t)(__popcll(ra[i]) + __popcll(rb[i]));
+        const size_t at = (size_t)r * n + v;
+        J.qf[at] = qf[i];
+        J.qs[at] = qs[i];
+        J.deg[at] = ((sd + wcnt[v]) << 16) | sd;
+      }
+    }
+    // strong edges: Q of round r-1, lane u owns targets u and u+64
+    u64 nf0 = 0, nf1 = 0, ns0 = 0, ns1 = 0;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      u64 m = __ballot((qf[i] | qs[i]) != 0ULL);
+      while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        const u64 a = readlane64(ra[i], l), b = readlane64(rb[i], l);
+        const u64 f = readlane64(qf[i], l), s = readlane64(qs[i], l);
+        const bool ha = (a >> lane) & 1ULL, hb = (b >> lane) & 1ULL;
+        nf0 |= ha ? f : 0ULL;
+        ns0 |= ha ? s : 0ULL;
+        nf1 |= hb ? f : 0ULL;
+        ns1 |= hb ? s : 0ULL;
+      }
+    }
+    qf[0] = nf0;
+    qf[1] = nf1;
+    qs[0] = ns0;
+    qs[1] = ns1;
+    __syncthreads();
+  }
+
+  // ---------------- 3. chains and pops (wave-uniform scalar code) ----------------
+  for (int i = lane; i < 64 * 65; i += 64) coef[i] = 0;
+  if (lane < 64) first_pop[lane] = -1;
+  __syncthreads();
+  int npush = 0, npop = 0, last = 0;
+  for (int w = 1; w <= nw; w++) {
+    if (lane == 0) J.push_off[w - 1] = (uint32_t)npush;
+    if (!((commit_mask >> (w - 1)) & 1ULL)) continue;
+    const int floor_w = chain_persistent ? last : 0;
+    // pushed leaders of this commit, push order (every lane writes the same
+    // values to lst: the list stays in LDS, not in per-lane scratch)
+    int k = 0;
+    lst[k++] = (int8_t)w;
+    int L = w;
+    for (int w2 = w - 1; w2 >= floor_w + 1; w2--) {
+      if (((lead_mask >> (w2 - 1)) & 1ULL) && ((QL[w2 - 1] >> (L - 1)) & 1ULL)) {
+        lst[k++] = (int8_t)w2;
+        L = w2;
+      }
+    }
+    __syncthreads();
+    // chain edges: segment i expands leader list[i]'s strong cone over rounds
+    // (round(list[i+1]), round(list[i])], the last one down to round(floor+1)
+    if (lane == 0) {
+      for (int i = 0; i < k; i++) {
+        const int hi = lst[i], lo = i + 1 < k ? lst[i + 1] : floor_w + 1;
+        coef[(lst[i] - 1) * 65 + hi] += 1;
+        coef[(lst[i] - 1) * 65 + lo] -= 1;
+        if (npush + i < J.push_cap) J.push_wave[npush + i] = lst[i];
+      }
+      for (int i = k - 1; i >= 0; i--) {  // pops: reverse push order (stack/stack.go:23-28)
+        const int j = npop + (k - 1 - i);
+        pop_lead[j] = (uint8_t)lst[i];
+        if (first_pop[lst[i] - 1] < 0) first_pop[lst[i] - 1] = (int16_t)j;
+      }
+    }
+    npush += k;
+    npop += k;
+    last = w;
+    __syncthreads();
+  }
+  if (lane == 0) J.push_off[nw] = (uint32_t)npush;
+  __syncthreads();
+
+  // ---------------- 4. bottom-up emission, lane b = leader wave b+1 ----------------
+  const int b = lane;
+  const int myfirst = first_pop[b];
+  u64 before = 0;  // leaders first popped before b (PAPER: they own shared vertices)
+  for (int x = 0; x < 64; x++) {
+    const int fp = first_pop[x];
+    if (fp >= 0 && myfirst >= 0 && fp < myfirst) before |= 1ULL << x;
+  }
+  u64 kr = 0, dr_ = 0, er = 0, kp = 0, dp = 0, ep = 0, cs = 0, chain = 0;
+  for (int r = 1; r <= T; r++) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int v = lane + 64 * i;
+      if (v < n) {
+        const size_t at = (size_t)r * n + v;
+        QF[v] = J.qf[at];
+        QS[v] = J.qs[at];
+        DG[v] = J.deg[at];
+      }
+    }
+    __syncthreads();
+    const uint32_t sa = J.slot_off[r], sb = J.slot_off[r + 1];
+    for (uint32_t c0 = sa; c0 < sb; c0 += 128) {  // slots staged in LDS, 128 at a time
+      const uint32_t m = min(128u, sb - c0);
+      __syncthreads();
+      if ((uint32_t)lane < m) SL[lane] = J.slot_src[c0 + lane];
+      if ((uint32_t)lane + 64 < m) SL[lane + 64] = J.slot_src[c0 + lane + 64];
+      __syncthreads();
+      for (uint32_t i = 0; i < m; i++) {
+        const int s = SL[i];
+        if (s == 0) continue;  // ghost slot {0,0}: never reached
+        const u64 f = QF[s - 1], g = QS[s - 1];
+        const uint32_t d = DG[s - 1];
+        if ((g >> b) & 1ULL) cs += d & 0xFFFFu;
+        if ((f >> b) & 1ULL) {
+          const u64 full = d >> 16;
+          dr_ += digest_term((uint32_t)r, (uint32_t)s, kr);
+          kr++;
+          er += full;
+          if (!(f & before)) {
+            dp += digest_term((uint32_t)r, (uint32_t)s, kp);
+            kp++;
+            ep += full;
+          }
+        }
+      }
+    }
+    if (((r - 1) & 3) == 0) {
+      const int x = (r - 1) / 4 + 1;
+      const int c = coef[b * 65 + x];
+      if (c) chain += (u64)(int64_t)c * cs;
+    }
+  }
+  res[b * 6 + 0] = kr;
+  res[b * 6 + 1] = dr_;
+  res[b * 6 + 2] = er;
+  res[b * 6 + 3] = kp;
+  res[b * 6 + 4] = dp;
+  res[b * 6 + 5] = ep;
+  chain = wave_sum(chain);
+  __syncthreads();
+
+  // ---------------- 5. outputs ----------------
+  u64 dsum = 0;
+  const int np = min(npop, min(J.push_cap, kSmallMaxPops));
+  for (int j = lane; j < np; j += 64) {
+    const int lb = pop_lead[j] - 1;
+    u64 c, d, e;
+    if (!paper) {
+      c = res[lb * 6 + 0]; d = res[lb * 6 + 1]; e = res[lb * 6 + 2];
+    } else if (first_pop[lb] == j) {
+      c = res[lb * 6 + 3]; d = res[lb * 6 + 4]; e = res[lb * 6 + 5];
+    } else {
+      c = 0; d = 0; e = 0;  // the leader's cone was delivered by its first pop
+    }
+    J.pop_count[j] = c;
+    J.pop_digest[j] = d;
+    J.pop_edges[j] = e;
+    dsum += e;
+  }
+  dsum = wave_sum(dsum);
+  if (lane < nw) {
+    J.vcount[lane] = vc_s[lane];
+    J.commit[lane] = (uint8_t)((commit_mask >> lane) & 1ULL);
+  }
+  if (lane == 0) {
+    J.totals[0] = commit_edges;
+    J.totals[1] = chain;
+    J.totals[2] = dsum;
+    J.totals[3] = (u64)npush;
+  }
+}
+
+}  // namespace dr

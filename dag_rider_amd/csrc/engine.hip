@@ -17,6 +17,7 @@
 #include "dagrider_gpu.h"
 #include "kernels.hpp"
 #include "replay_plan.hpp"
+#include "batch.hpp"
 
 using dr::u64;
 
@@ -94,6 +95,7 @@ struct dr_ctx {
   bool canon_host = false;
   int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies  // hC/hG/hE mirror Cc/Gc/Ec (fetched lazily after a planned replay)
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
+  DevBuf batch_arena;       // dr_replay_batch scratch + outputs (batch.hpp)
   // memo needs every weak edge in the dense summary window
   bool memo_ok() const { return nfar == 0 && dmax_near <= 17; }
   int memo_dd() const { return std::max(0, dmax_near - 1); }
@@ -541,7 +543,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->digest,  &c->pop_pos, &c->ids,      &c->U,        &c->WU,
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
-                    &c->nseg,    &c->stops,   &c->qstats};
+                    &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1782,5 +1784,143 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   }
   o->deliver_edges = de;
   o->n_ids = tot;
+  return DR_OK;
+}
+
+// ===========================================================================
+// batch of independent replays
+// ===========================================================================
+namespace {
+// the fused small-DAG path (batch.hpp) covers this context's DAG
+bool small_ok(const dr_ctx *c, int nwaves) {
+  return c->n <= 128 && nwaves <= 64 && c->nfar == 0 && c->dmax_near < 32;
+}
+
+template <int DEPTH>
+hipError_t launch_small(hipStream_t s, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper) {
+  hipLaunchKernelGGL((dr::k_replay_small<DEPTH>), dim3(nj), dim3(64), 0, s, jobs, nj, nw, persistent, paper);
+  return hipGetLastError();
+}
+}  // namespace
+
+extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
+                               dr_replay_out *outs) {
+  if (!ctxs || nctx < 1 || !outs) return DR_E_INVAL;
+  for (int i = 0; i < nctx; i++)
+    if (!ctxs[i]) return DR_E_INVAL;
+  dr_ctx *c0 = ctxs[0];
+  bool fused = true;
+  int dmax = 1;
+  for (int i = 0; i < nctx; i++) {
+    dr_ctx *c = ctxs[i];
+    dr_replay_out *o = &outs[i];
+    if (c->dev != c0->dev) return c0->fail(DR_E_INVAL, "batch contexts on devices %d and %d", c0->dev, c->dev);
+    if (!o->commit || !o->vcount || !o->push_off) return c0->fail(DR_E_INVAL, "null output (context %d)", i);
+    if (nwaves < 1 || 4 * nwaves >= c->nrounds)
+      return c0->fail(DR_E_INVAL, "context %d: nwaves %d needs rounds 0..%d mirrored", i, nwaves, 4 * nwaves);
+    for (int j = 0; j < i && nctx <= 64; j++)
+      if (ctxs[j] == c) return c0->fail(DR_E_INVAL, "context %d repeated in the batch", i);
+    if (!small_ok(c, nwaves) || (o->ids && o->ids_cap > 0)) fused = false;
+    dmax = std::max(dmax, c->dmax_near);
+  }
+  if (chain_mode != DR_CHAIN_LITERAL && chain_mode != DR_CHAIN_PERSISTENT) return c0->fail(DR_E_INVAL, "bad chain mode");
+  if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER) return c0->fail(DR_E_INVAL, "bad deliver mode");
+  if (!fused) {  // general shapes: one dr_replay per context (all on the GPU)
+    for (int i = 0; i < nctx; i++)
+      if (int rc = dr_replay(ctxs[i], nwaves, chain_mode, deliver_mode, &outs[i])) {
+        if (ctxs[i] != c0) c0->err = "context " + std::to_string(i) + ": " + ctxs[i]->err;
+        return rc;
+      }
+    return DR_OK;
+  }
+  if (int rc = set_device(c0)) return rc;
+  const int nw = nwaves, T = 4 * (nw - 1) + 1;
+  const int64_t pbound = chain_mode == DR_CHAIN_PERSISTENT ? nw : (int64_t)nw * (nw + 1) / 2;
+  // device arena: per job scratch + outputs, then the job table
+  Carve cv;
+  std::vector<dr::SmallJob> jobs(nctx);
+  std::vector<int64_t> pcap(nctx);
+  for (int pass = 0; pass < 2; pass++) {
+    cv.off = 0;
+    for (int i = 0; i < nctx; i++) {
+      dr_ctx *c = ctxs[i];
+      dr::SmallJob &J = jobs[i];
+      pcap[i] = std::max<int64_t>(1, std::min<int64_t>(outs[i].push_wave ? outs[i].push_cap : 0, pbound));
+      const size_t nv = (size_t)(T + 1) * c->n;
+      J.qf = cv.take<u64>(nv);
+      J.qs = cv.take<u64>(nv);
+      J.deg = cv.take<uint32_t>(nv);
+      J.commit = cv.take<uint8_t>(nw);
+      J.vcount = cv.take<int32_t>(nw);
+      J.push_off = cv.take<uint32_t>(nw + 1);
+      J.push_wave = cv.take<int32_t>(pcap[i]);
+      J.pop_count = cv.take<u64>(pcap[i]);
+      J.pop_digest = cv.take<u64>(pcap[i]);
+      J.pop_edges = cv.take<u64>(pcap[i]);
+      J.totals = cv.take<u64>(4);
+    }
+    dr::SmallJob *jt = cv.take<dr::SmallJob>(nctx);
+    if (pass == 0) {
+      HIPCHK(c0, c0->batch_arena.ensure(cv.off));
+      cv.base = c0->batch_arena.as<char>();
+      continue;
+    }
+    for (int i = 0; i < nctx; i++) {
+      dr_ctx *c = ctxs[i];
+      dr::SmallJob &J = jobs[i];
+      J.strong = c->strong.as<u64>();
+      J.present = c->present.as<u64>();
+      J.weak = c->weak.as<uint32_t>();
+      J.weak_roff = c->weak_roff.as<uint32_t>();
+      J.slot_off = c->slot_off.as<uint32_t>();
+      J.slot_src = c->slot_src.as<uint16_t>();
+      J.n = c->n;
+      J.WS = c->WS;
+      J.push_cap = (int32_t)pcap[i];
+      J.quorum = 2 * c->f + 1;
+    }
+    // appends are synchronous (dr_append_rounds_*), so every DAG is resident
+    HIPCHK(c0, c0->h2d(jt, jobs.data(), jobs.size() * sizeof(dr::SmallJob)));
+    const int persistent = chain_mode == DR_CHAIN_PERSISTENT, paper = deliver_mode == DR_DELIVER_PAPER;
+    HIPCHK(c0, hipEventRecord(c0->ev[0], c0->stream));
+    const int need = next_pow2(dmax + 1);
+    hipError_t e = need <= 8    ? launch_small<8>(c0->stream, jt, nctx, nw, persistent, paper)
+                   : need <= 16 ? launch_small<16>(c0->stream, jt, nctx, nw, persistent, paper)
+                                : launch_small<32>(c0->stream, jt, nctx, nw, persistent, paper);
+    HIPCHK(c0, e);
+    HIPCHK(c0, hipEventRecord(c0->ev[1], c0->stream));
+  }
+  // results: one bulk copy of the output region of the arena
+  std::vector<char> host(cv.off);
+  HIPCHK(c0, hipMemcpyAsync(host.data(), c0->batch_arena.p, cv.off, hipMemcpyDeviceToHost, c0->stream));
+  HIPCHK(c0, hipStreamSynchronize(c0->stream));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c0->ev[0], c0->ev[1]);
+  auto at = [&](const void *dev) { return host.data() + (reinterpret_cast<const char *>(dev) - c0->batch_arena.as<char>()); };
+  for (int i = 0; i < nctx; i++) {
+    const dr::SmallJob &J = jobs[i];
+    dr_replay_out *o = &outs[i];
+    const u64 *tot = reinterpret_cast<const u64 *>(at(J.totals));
+    const int64_t np = (int64_t)tot[3];
+    std::memcpy(o->commit, at(J.commit), nw);
+    std::memcpy(o->vcount, at(J.vcount), 4 * (size_t)nw);
+    std::memcpy(o->push_off, at(J.push_off), 4 * (size_t)(nw + 1));
+    o->n_push = np;
+    o->n_ids = 0;
+    o->commit_edges = tot[0];
+    o->chain_edges = tot[1];
+    o->deliver_edges = tot[2];
+    o->ms_commit = o->ms_chain = o->ms_emit = o->ms_summary = 0;
+    o->ms_deliver = ms;  // the whole fused replay kernel
+    o->canon_segments = -1;
+    o->sweep_count = o->sweep_partial = o->sweep_rows = o->sweep_weak_scanned = o->sweep_shortcut = 0;
+    if (np > o->push_cap || !o->push_wave || !o->pop_count || !o->pop_digest)
+      return c0->fail(DR_E_CAPACITY, "context %d: %lld pushed leaders, capacity %lld", i, (long long)np,
+                      (long long)o->push_cap);
+    std::memcpy(o->push_wave, at(J.push_wave), 4 * (size_t)np);
+    std::memcpy(o->pop_count, at(J.pop_count), 8 * (size_t)np);
+    std::memcpy(o->pop_digest, at(J.pop_digest), 8 * (size_t)np);
+    if (o->pop_edges) std::memcpy(o->pop_edges, at(J.pop_edges), 8 * (size_t)np);
+  }
   return DR_OK;
 }

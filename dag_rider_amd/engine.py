@@ -167,29 +167,75 @@ class Engine:
     # ---- whole replay ----
     def replay(self, nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT, deliver_mode: int = L.DR_DELIVER_REF,
                ids_cap: int = 0, push_cap: Optional[int] = None) -> ReplayResult:
-        push_cap = push_cap if push_cap is not None else (
-            nwaves * (nwaves + 1) // 2 if chain_mode == L.DR_CHAIN_LITERAL else 2 * nwaves + 1)
-        cm = np.zeros(nwaves, np.uint8)
-        vc = np.zeros(nwaves, np.int32)
-        po = np.zeros(nwaves + 1, np.uint32)
-        pw = np.zeros(max(push_cap, 1), np.int32)
-        pc = np.zeros(max(push_cap, 1), np.uint64)
-        pdg = np.zeros(max(push_cap, 1), np.uint64)
-        pe = np.zeros(max(push_cap, 1), np.uint64)
-        ids = np.zeros(max(ids_cap, 1) * 2, np.int32) if ids_cap else None
-        o = L.ReplayOut()
-        o.commit, o.vcount, o.push_off, o.push_wave = L.ptr(cm), L.ptr(vc), L.ptr(po), L.ptr(pw)
-        o.push_cap = push_cap
-        o.pop_count, o.pop_digest, o.pop_edges = L.ptr(pc), L.ptr(pdg), L.ptr(pe)
-        o.ids = L.ptr(ids)
-        o.ids_cap = ids_cap
+        """The Alg. 3 wiring the reference lacks: waveReady(w) for w = 1..nwaves, orderVertices on commit."""
+        o, keep = _replay_out(nwaves, chain_mode, ids_cap, push_cap)
         self._check(self._L.dr_replay(self._h, nwaves, chain_mode, deliver_mode, C.byref(o)))
-        k = o.n_push
-        return ReplayResult(cm, vc, po, pw[:k], pc[:k], pdg[:k], pe[:k],
-                            None if ids is None else ids[:2 * min(o.n_ids, ids_cap)].reshape(-1, 2),
-                            o.commit_edges, o.chain_edges, o.deliver_edges,
-                            dict(commit=o.ms_commit, chain=o.ms_chain, deliver=o.ms_deliver, emit=o.ms_emit,
-                                 summary=o.ms_summary),
-                            dict(count=o.sweep_count, partial=o.sweep_partial, rows=o.sweep_rows,
-                                 weak_scanned=o.sweep_weak_scanned, shortcut=o.sweep_shortcut,
-                                 canon_segments=o.canon_segments))
+        return _replay_result(o, keep, ids_cap)
+
+
+def _replay_out(nwaves: int, chain_mode: int, ids_cap: int = 0, push_cap: Optional[int] = None):
+    push_cap = push_cap if push_cap is not None else (
+        nwaves * (nwaves + 1) // 2 if chain_mode == L.DR_CHAIN_LITERAL else 2 * nwaves + 1)
+    keep = dict(cm=np.zeros(nwaves, np.uint8), vc=np.zeros(nwaves, np.int32), po=np.zeros(nwaves + 1, np.uint32),
+                pw=np.zeros(max(push_cap, 1), np.int32), pc=np.zeros(max(push_cap, 1), np.uint64),
+                pdg=np.zeros(max(push_cap, 1), np.uint64), pe=np.zeros(max(push_cap, 1), np.uint64),
+                ids=np.zeros(max(ids_cap, 1) * 2, np.int32) if ids_cap else None)
+    o = L.ReplayOut()
+    o.commit, o.vcount, o.push_off, o.push_wave = L.ptr(keep["cm"]), L.ptr(keep["vc"]), L.ptr(keep["po"]), \
+        L.ptr(keep["pw"])
+    o.push_cap = push_cap
+    o.pop_count, o.pop_digest, o.pop_edges = L.ptr(keep["pc"]), L.ptr(keep["pdg"]), L.ptr(keep["pe"])
+    o.ids = L.ptr(keep["ids"])
+    o.ids_cap = ids_cap
+    return o, keep
+
+
+def _replay_result(o, keep, ids_cap: int = 0) -> ReplayResult:
+    k = o.n_push
+    ids = keep["ids"]
+    return ReplayResult(keep["cm"], keep["vc"], keep["po"], keep["pw"][:k], keep["pc"][:k], keep["pdg"][:k],
+                        keep["pe"][:k], None if ids is None else ids[:2 * min(o.n_ids, ids_cap)].reshape(-1, 2),
+                        o.commit_edges, o.chain_edges, o.deliver_edges,
+                        dict(commit=o.ms_commit, chain=o.ms_chain, deliver=o.ms_deliver, emit=o.ms_emit,
+                             summary=o.ms_summary),
+                        dict(count=o.sweep_count, partial=o.sweep_partial, rows=o.sweep_rows,
+                             weak_scanned=o.sweep_weak_scanned, shortcut=o.sweep_shortcut,
+                             canon_segments=o.canon_segments))
+
+
+class ReplayBatch:
+    """dr_replay_batch over a fixed list of engines: output buffers are allocated once and
+    reused by every call (the C5 bench replays the same batch many times)."""
+
+    def __init__(self, engines: Sequence["Engine"], nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT,
+                 deliver_mode: int = L.DR_DELIVER_REF):
+        self.engines = list(engines)
+        self.nwaves, self.chain_mode, self.deliver_mode = nwaves, chain_mode, deliver_mode
+        n = len(self.engines)
+        self._ctxs = (L.P * n)(*[e._h for e in self.engines])
+        self._outs = (L.ReplayOut * n)()
+        self._keep = []
+        for i in range(n):
+            o, keep = _replay_out(nwaves, chain_mode)
+            self._outs[i] = o
+            self._keep.append(keep)
+
+    def run(self) -> None:
+        L0 = L.lib()
+        rc = L0.dr_replay_batch(self._ctxs, len(self.engines), self.nwaves, self.chain_mode, self.deliver_mode,
+                                self._outs)
+        if rc != L.DR_OK:
+            raise L.DrError(rc, L0.dr_last_error(self.engines[0]._h).decode())
+
+    def results(self) -> List[ReplayResult]:
+        return [_replay_result(self._outs[i], self._keep[i]) for i in range(len(self.engines))]
+
+    def __call__(self) -> List[ReplayResult]:
+        self.run()
+        return self.results()
+
+
+def replay_batch(engines: Sequence["Engine"], nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT,
+                 deliver_mode: int = L.DR_DELIVER_REF) -> List[ReplayResult]:
+    """dr_replay_batch: every engine's dr_replay, as one fused launch when the DAGs are small."""
+    return ReplayBatch(engines, nwaves, chain_mode, deliver_mode)()

@@ -78,6 +78,13 @@ def generate(cfg: GenConfig, nthreads: int = 0) -> PackedDag:
         lib.dr_gen_free(h)
 
 
+def c5_config(i: int) -> GenConfig:
+    """DAG i of C5's batch of 4096 independent n=128 replays (seed 5000+i)."""
+    import dataclasses
+
+    return dataclasses.replace(CONFIGS["c5"], name=f"c5-{i}", seed=CONFIGS["c5"].seed + i)
+
+
 def small_config(n: int, last_round: int, seed: int, **kw) -> GenConfig:
     """Seeded small DAGs for cross-checks (parameters randomised per seed by the caller)."""
     base = dict(p_present=0.9, p_late=0.2, p_w=0.5, weak_depth=4, p_la=0.1)

@@ -165,6 +165,18 @@ typedef struct {
 
 int dr_replay(dr_ctx *ctx, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o);
 
+/* A batch of independent replays: dr_replay(ctxs[i], nwaves, chain_mode,
+ * deliver_mode, &outs[i]) for i in [0, nctx), each context a separate
+ * Process mirror (thousands of n=128 replays on one GPU).
+ * Contexts must be distinct and on one device; errors name the context.
+ * Outputs, semantics and capacities are exactly dr_replay's.  When every
+ * context has n <= 128, nwaves <= 64, weak deltas < 32 and no ids are
+ * requested, the whole batch runs as one fused kernel (one wavefront per DAG,
+ * dag_rider_amd/csrc/batch.hpp; outs[i].ms_deliver = its device time);
+ * otherwise the contexts replay one after another through dr_replay. */
+int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
+                    dr_replay_out *outs);
+
 /* Tuning hook (not part of the reference's surface): average device time of
  * `iters` launches of one kernel variant on the resident DAG.  kernel 0 =
  * round-summary + commit pass (variant 0 shipped, 1 rows only, 2 weak edges

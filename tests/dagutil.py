@@ -8,6 +8,7 @@ commits and chains are empty.
 """
 from __future__ import annotations
 
+import hashlib
 import json
 import os
 
@@ -74,3 +75,30 @@ def figure1():
     dag = [[Vertex(VertexID(*v["id"]), b"", [VertexID(*e) for e in v["strong"]],
                    [VertexID(*e) for e in v["weak"]]) for v in rnd] for rnd in g["rounds"]]
     return g, dag
+
+
+def dag_fingerprint(d: PackedDag) -> str:
+    """Hash of a packed DAG's arrays: pins the generator's output across machines."""
+    h = hashlib.blake2b(digest_size=16)
+    h.update(np.asarray([d.n, d.nrounds], np.int64).tobytes())
+    for a, t in ((d.slot_off, np.uint32), (d.slot_src, np.uint16), (d.strong, np.uint64), (d.weak_off, np.uint32),
+                 (d.weak_tgt, np.uint32)):
+        h.update(np.ascontiguousarray(a, dtype=t).tobytes())
+    return h.hexdigest()
+
+
+def replay_fingerprint(r) -> str:
+    """Hash of every output of one replay (engine ReplayResult or oracle OracleReplay)."""
+    h = hashlib.blake2b(digest_size=16)
+    for a, t in ((r.commit, np.uint8), (r.vcount, np.int32), (r.push_off, np.uint32), (r.push_wave, np.int32),
+                 (r.pop_count, np.uint64), (r.pop_digest, np.uint64), (r.pop_edges, np.uint64)):
+        h.update(np.ascontiguousarray(a, dtype=t).tobytes())
+    h.update(np.asarray([r.commit_edges, r.chain_edges, r.deliver_edges], np.uint64).tobytes())
+    return h.hexdigest()
+
+
+def load_large():
+    import gzip
+
+    with gzip.open(os.path.join(GOLDEN, "large_replay.json.gz"), "rt") as f:
+        return json.load(f)

@@ -1,0 +1,149 @@
+"""GPU parity of dr_replay_batch: the fused one-wavefront-per-DAG
+replay (dag_rider_amd/csrc/batch.hpp) against the oracle, against per-context
+dr_replay, and against the C5 golden fingerprints (tests/golden/large_replay.json.gz).
+
+random_dag draws unconstrained DAGs (partial quorums, failed commits, leader chains,
+dangling targets, ghost slots), which the quorum-shaped generator never produces.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from dag_rider_amd import _lib as L
+from dag_rider_amd.engine import Engine, ReplayBatch, replay_batch
+from dag_rider_amd.gen import CONFIGS, c5_config, generate
+from dagutil import dag_fingerprint, load_large, random_dag, replay_fingerprint
+
+pytestmark = pytest.mark.gpu
+
+MODES = [(cm, dm) for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT) for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER)]
+
+
+def _same(a, b):
+    assert (a.commit == b.commit).all()
+    assert (a.vcount == b.vcount).all()
+    assert (a.push_off == b.push_off).all()
+    assert (a.push_wave == b.push_wave).all()
+    assert (a.pop_count == b.pop_count).all()
+    assert (a.pop_digest == b.pop_digest).all()
+    assert (a.pop_edges == b.pop_edges).all()
+    assert (a.commit_edges, a.chain_edges, a.deliver_edges) == (b.commit_edges, b.chain_edges, b.deliver_edges)
+
+
+def _random_batch(dev, seed, count, nw, ns=(1, 4, 7, 33, 64, 65, 100, 128), depth=(2, 12)):
+    rng = np.random.default_rng(seed)
+    items = []
+    for _ in range(count):
+        n = int(rng.choice(ns))
+        R = 4 * nw + int(rng.integers(0, 6))
+        d = random_dag(rng, n, R, p_present=rng.uniform(0.5, 1), p_s=rng.uniform(0.05, 0.9),
+                       p_w=rng.uniform(0, 1), max_depth=int(rng.integers(*depth)))
+        f = int(rng.integers(0, (n - 1) // 3 + 2))
+        e = Engine(n, f, d.nrounds, dev)
+        e.append_packed(d)
+        items.append((d, f, e))
+    return items
+
+
+@pytest.mark.parametrize("cm,dm", MODES)
+def test_batch_random_vs_oracle(gpu_device, cm, dm):
+    nw = 10
+    items = _random_batch(gpu_device, 77 + 4 * cm + dm, 24, nw)
+    got = replay_batch([e for _, _, e in items], nw, cm, dm)
+    for (d, f, e), g in zip(items, got):
+        want = oracle.PDag(d).replay(f, nw, cm, dm)
+        assert want.rc == 0
+        _same(g, want)
+        assert g.ms["deliver"] > 0  # the fused kernel ran
+    for _, _, e in items:
+        e.close()
+
+
+def test_batch_max_waves(gpu_device):
+    """nw = 64 (the fused path's limit) at n = 128: long literal chains, up to 2080 pops."""
+    nw = 64
+    items = _random_batch(gpu_device, 5, 3, nw, ns=(128, 100, 64))
+    for cm, dm in MODES:
+        got = replay_batch([e for _, _, e in items], nw, cm, dm)
+        for (d, f, e), g in zip(items, got):
+            _same(g, oracle.PDag(d).replay(f, nw, cm, dm))
+    for _, _, e in items:
+        e.close()
+
+
+def test_batch_matches_single_replay(gpu_device):
+    """The fused batch and dr_replay context by context agree on everything."""
+    nw = 12
+    items = _random_batch(gpu_device, 9, 16, nw)
+    for cm, dm in MODES:
+        got = replay_batch([e for _, _, e in items], nw, cm, dm)
+        for (_, _, e), g in zip(items, got):
+            _same(g, e.replay(nw, cm, dm))
+    for _, _, e in items:
+        e.close()
+
+
+def test_batch_general_shapes_fall_back(gpu_device):
+    """n > 128 or weak deltas >= 32 in any context: the batch replays context by context."""
+    nw = 6
+    items = _random_batch(gpu_device, 11, 3, nw) + _random_batch(gpu_device, 12, 1, nw, ns=(200,)) + \
+        _random_batch(gpu_device, 13, 1, nw, depth=(33, 40))
+    for cm, dm in MODES:
+        got = replay_batch([e for _, _, e in items], nw, cm, dm)
+        for (d, f, e), g in zip(items, got):
+            _same(g, oracle.PDag(d).replay(f, nw, cm, dm))
+    for _, _, e in items:
+        e.close()
+
+
+def test_batch_errors(gpu_device):
+    cfg = CONFIGS["c1"]  # 4 waves, commits (and so pushes) on every present leader
+    d = generate(cfg)
+    es = []
+    for _ in range(2):
+        es.append(Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device))
+        es[-1].append_packed(d)
+    with pytest.raises(L.DrError) as ei:
+        replay_batch([es[0], es[0]], 4)
+    assert ei.value.code == L.DR_E_INVAL
+    with pytest.raises(L.DrError) as ei:
+        replay_batch(es, 50)  # rounds of wave 50 are not mirrored
+    assert ei.value.code == L.DR_E_INVAL
+    # capacity: a batch whose first context pushes more leaders than its buffers hold
+    b = ReplayBatch(es, 4, L.DR_CHAIN_LITERAL)
+    for i in range(len(es)):
+        b._outs[i].push_cap = 0
+    with pytest.raises(L.DrError) as ei:
+        b.run()
+    assert ei.value.code == L.DR_E_CAPACITY
+    for e in es:
+        e.close()
+
+
+def test_c5_batch_golden(gpu_device):
+    """C5: 4096 independent n=128 x 128-round replays (seeds 5000+i) in one batch,
+    bit-exact against the committed fingerprints (PERSISTENT/REF for all, LITERAL/REF and
+    PERSISTENT/PAPER for the first 64)."""
+    g = load_large()["c5"]
+    count = g["count"]
+    engines = []
+    try:
+        for i in range(count):
+            cfg = c5_config(i)
+            d = generate(cfg)
+            assert dag_fingerprint(d) == g["dag"][i], f"generator drift at C5 DAG {i}"
+            e = Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device)
+            e.append_packed(d)
+            engines.append(e)
+        nw = c5_config(0).nwaves
+        got = replay_batch(engines, nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+        bad = [i for i, r in enumerate(got) if replay_fingerprint(r) != g["persistent_ref"][i]]
+        assert not bad, f"{len(bad)} C5 replays differ, first {bad[:8]}"
+        detail = engines[:len(g["literal_ref"])]
+        for key, cm, dm in (("literal_ref", L.DR_CHAIN_LITERAL, L.DR_DELIVER_REF),
+                            ("persistent_paper", L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_PAPER)):
+            got = replay_batch(detail, nw, cm, dm)
+            assert [replay_fingerprint(r) for r in got] == g[key], key
+    finally:
+        for e in engines:
+            e.close()

@@ -164,3 +164,27 @@ def test_golden_c2_replay():
                                                           oracle.DELIVER_REF)
     npop = int(lit.push_off[k])
     assert lit.pop_digest.tolist() == r.pop_digest[:npop].tolist()
+
+
+def test_large_golden_pins_generator_and_oracle():
+    """The committed C3/C4/C5 golden vectors: the generator reproduces the C5 DAGs (and the
+    C3/C4 configs they were made from), and the oracle reproduces the first C5 replays in
+    every recorded mode (the full C3/C4 replays take a minute each; the GPU tests compare them)."""
+    from dag_rider_amd.gen import CONFIGS, c5_config, generate
+    from dagutil import dag_fingerprint, load_large, replay_fingerprint
+
+    g = load_large()
+    for name in ("c3", "c4"):
+        assert g[name]["config"] == CONFIGS[name].__dict__
+        assert len(g[name]["persistent_ref"]["pop_digest"]) == len(g[name]["persistent_ref"]["push_wave"])
+    c5 = g["c5"]
+    assert c5["count"] == 4096 and len(c5["persistent_ref"]) == 4096
+    for i in range(6):
+        cfg = c5_config(i)
+        d = generate(cfg)
+        assert dag_fingerprint(d) == c5["dag"][i]
+        bs = oracle.PDag(d)
+        for key, cm, dm in (("persistent_ref", oracle.CHAIN_PERSISTENT, oracle.DELIVER_REF),
+                            ("literal_ref", oracle.CHAIN_LITERAL, oracle.DELIVER_REF),
+                            ("persistent_paper", oracle.CHAIN_PERSISTENT, oracle.DELIVER_PAPER)):
+            assert replay_fingerprint(bs.replay(cfg.faulty, cfg.nwaves, cm, dm, nthreads=1)) == c5[key][i]
