@@ -29,8 +29,11 @@ $(BUILD)/dag_gen.o: $(PKG)/csrc/dag_gen.cpp include/dagrider_gen.h | $(BUILD)
 $(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp include/dagrider_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/engine.o $(BUILD)/dag_gen.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -Wl,-soname,libdagrider_gpu.so
+$(BUILD)/shard.o: $(PKG)/csrc/shard.hip include/dagrider_shard.h include/dagrider_gpu.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/engine.o $(BUILD)/shard.o $(BUILD)/dag_gen.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdagrider_gpu.so
 
 $(ORACLE): oracle/ref_literal.c oracle/ref_bitset.c oracle/oracle.h
 	$(CC) $(CFLAGS) -shared -o $@ oracle/ref_literal.c oracle/ref_bitset.c

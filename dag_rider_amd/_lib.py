@@ -16,6 +16,7 @@ DR_CHAIN_LITERAL, DR_CHAIN_PERSISTENT = 0, 1
 DR_DELIVER_REF, DR_DELIVER_PAPER = 0, 1
 DR_OPT_MEMO = 1
 DR_OPT_DEVICE_PLAN = 2
+DR_SHARD_ID_BYTES = 128
 
 P = C.c_void_p
 i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float
@@ -55,6 +56,18 @@ SIGNATURES = {
     "dr_replay": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
     "dr_replay_batch": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
     "dr_profile_kernel": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(f32)]),
+    # include/dagrider_shard.h
+    "dr_shard_unique_id": (C.c_int, [P]),
+    "dr_shard_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.POINTER(P)]),
+    "dr_shard_destroy": (None, [P]),
+    "dr_shard_last_error": (C.c_char_p, [P]),
+    "dr_shard_num_rounds": (C.c_int, [P]),
+    "dr_shard_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "dr_shard_append_rounds_packed": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
+    "dr_shard_reach_sets": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "dr_shard_path_batch": (C.c_int, [P, C.c_int, P, P, C.c_int, P]),
+    "dr_shard_stats": (C.c_int, [P, C.POINTER(f32), C.POINTER(u64), C.POINTER(u64)]),
     "dr_gen_create": (C.c_int, [C.POINTER(GenParams), C.POINTER(P)]),
     "dr_gen_free": (None, [P]),
     "dr_gen_info": (C.c_int, [P, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(u64),

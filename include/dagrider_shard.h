@@ -1,0 +1,78 @@
+/*
+ * dagrider_shard.h -- process-column sharded reachability.
+ *
+ * The same path()/reach-set queries as dagrider_gpu.h (process/process.go:89-148),
+ * for a DAG whose edge rows are split by TARGET column across G shards: shard g
+ * stores, for every vertex (r, s), the words [g*C, (g+1)*C) of its strong row
+ * (C = 64 * ceil(ceil(n/64) / G) target sources per shard) and the weak edges whose
+ * target source lies in those columns.  A sweep keeps the whole frontier of the
+ * current round on every shard (one u64 query mask per source: bit b <=> query b
+ * reached it), expands it into its own columns of the rounds below, and the shards'
+ * columns of the next frontier are all-gathered (one RCCL all-gather over xGMI per
+ * round, in a batch of up to 64 queries).  Results are bit-identical to
+ * dr_reach_sets / dr_path_batch on the unsharded DAG.
+ *
+ * Two exchange modes, chosen at creation:
+ *   - RCCL: one process per GPU; the nshards ranks build a communicator from a
+ *     unique id (dr_shard_unique_id on rank 0, broadcast by the caller).
+ *   - local (id == NULL): one context holds all nshards column shards on one
+ *     device and the exchange is the shared frontier buffer.  Same kernels, same
+ *     column split; it is how the decomposition is tested on a 1-GPU box.
+ *
+ * Contract as dagrider_gpu.h: C scalars and caller-owned flat arrays, no host
+ * pointer kept after a call, synchronous calls, negative status codes
+ * (DR_E_* of dagrider_gpu.h), one caller thread per context.  In RCCL mode every
+ * rank must make the same calls with the same arguments (the collective runs
+ * inside them); every rank receives the full results.
+ */
+#ifndef DAGRIDER_SHARD_H
+#define DAGRIDER_SHARD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DR_SHARD_ID_BYTES 128
+
+typedef struct dr_shard dr_shard;
+
+/* RCCL unique id for a new shard group (ncclGetUniqueId); rank 0 makes it and the
+ * caller hands the bytes to every rank (e.g. torch.distributed broadcast). */
+int dr_shard_unique_id(uint8_t *id);
+
+/* dr_create (dagrider_gpu.h) for one column shard group.  nshards in [1, 64];
+ * id != NULL: this process is shard `rank` of an RCCL group of nshards ranks;
+ * id == NULL: local mode, this context holds every shard (rank must be 0). */
+int dr_shard_create(int n, int faulty, int max_rounds, int device, int nshards, int rank, const uint8_t *id,
+                    dr_shard **out);
+void dr_shard_destroy(dr_shard *ctx);
+const char *dr_shard_last_error(const dr_shard *ctx);
+int dr_shard_num_rounds(const dr_shard *ctx);
+/* this context's shards [*shard0, *shard0 + *nlocal) and the target sources
+ * [*col0, *col1) (1-based, half-open) it stores */
+int dr_shard_info(const dr_shard *ctx, int *nshards, int *shard0, int *nlocal, int *col0, int *col1);
+
+/* p.dag[r] = append(...) (process.go:229): dr_append_rounds_packed's arguments and
+ * contract; the context keeps only its columns.  Weak edges must satisfy
+ * r - r' <= 1023 (else DR_E_CONTRACT). */
+int dr_shard_append_rounds_packed(dr_shard *ctx, int r0, int k, const uint32_t *slot_off, const uint16_t *slot_src,
+                                  const uint64_t *strong, const uint32_t *weak_off, const uint32_t *weak_tgt);
+
+/* dr_reach_sets (dagrider_gpu.h) on the sharded DAG: same arguments and output layout. */
+int dr_shard_reach_sets(dr_shard *ctx, int q, const int32_t *from, const int32_t *bottom, int strong_only,
+                        uint64_t *out, size_t cap_words, size_t *out_words);
+
+/* dr_path_batch (path(), process.go:89-148) on the sharded DAG. */
+int dr_shard_path_batch(dr_shard *ctx, int q, const int32_t *from, const int32_t *to, int strong_only,
+                        uint8_t *out);
+
+/* Last query call: device time (ms, HIP events around the sweeps, exchange
+ * included), rounds stepped, and bytes this rank sent through the exchange. */
+int dr_shard_stats(const dr_shard *ctx, float *ms, uint64_t *rounds, uint64_t *exchange_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -57,3 +57,51 @@ def test_single_rank_passthrough():
 
     assert bench.rank_config(CONFIGS["c4"], 0, 1) == CONFIGS["c4"]
     assert bench.reduce_over_ranks(None, 2.0, 7, "cpu") == (2.0, 7.0)
+
+
+def _id_worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from dag_rider_amd.shard import exchange_unique_id
+
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    try:
+        made = []
+
+        def make():  # stands in for ncclGetUniqueId, which needs a GPU
+            made.append(rank)
+            return bytes((7 * i + 3) % 256 for i in range(128))
+
+        out[rank] = (exchange_unique_id(dist, make), tuple(made))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_unique_id_exchange_gloo():
+    """The column-sharded path's RCCL bootstrap: rank 0 makes the unique id, every rank gets it."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_id_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert out[0][0] == out[1][0] and len(out[0][0]) == 128
+    assert out[0][1] == (0,) and out[1][1] == ()
+
+
+def test_shard_no_cpu_fallback():
+    """dr_shard_create fails loudly without a HIP device."""
+    sys.path.insert(0, ROOT)
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is visible")
+    except Exception:
+        pass
+    from dag_rider_amd import _lib as L
+    from dag_rider_amd.shard import ShardEngine
+
+    with pytest.raises(L.DrError) as ei:
+        ShardEngine(16, 5, 8, 0, nshards=2)
+    assert ei.value.code == L.DR_E_HIP

@@ -1,0 +1,138 @@
+"""GPU parity of the process-column sharded path (include/dagrider_shard.h).
+
+The sharded sweep splits every strong row and the weak edges by target column
+across G shards and exchanges the per-round frontier (local mode: shared buffer;
+RCCL mode: ncclAllGather).  Bar: reach sets and path() answers bit-identical to the
+oracle (oracle/ref_bitset.c cones, pinned to TestPath and the literal restatement)
+and to the unsharded engine, for every shard count.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from dag_rider_amd.dag import pack_lists
+from dag_rider_amd.engine import Engine
+from dag_rider_amd.gen import generate, small_config
+from dag_rider_amd.shard import ShardEngine, shard_unique_id
+from dagutil import figure1, random_dag
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_reach(se, bs, froms, bottoms):
+    for strong in (True, False):
+        got = se.reach_sets(froms, bottoms, strong)
+        for fr, bt, m in zip(froms, bottoms, got):
+            want, _ = bs.cone(fr, bt, strong)
+            assert (m == want).all(), (fr, bt, strong)
+
+
+def test_shard_figure1_testpath(gpu_device):
+    """TestPath (process_internal_test.go:8-84) through the sharded path, G = 1..4."""
+    g, dag = figure1()
+    d = pack_lists(dag, g["n"])
+    for G in (1, 2, 4):
+        with ShardEngine(g["n"], g["faulty"], 8, gpu_device, nshards=G) as se:
+            se.append_packed(d)
+            for t in g["test_path"]:
+                got = se.path_batch([(tuple(t["from"]), tuple(t["to"]))], t["strong"])[0]
+                assert bool(got) == t["want"], (G, t)
+            ids = [tuple(x) for x in g["allpairs_ids"]]
+            pairs = [(a, b) for a in ids for b in ids]
+            for key, strong in (("strong", True), ("any", False)):
+                got = se.path_batch(pairs, strong).reshape(len(ids), len(ids))
+                assert (got == np.asarray(g["allpairs"][key], dtype=np.uint8)).all(), (G, key)
+
+
+@pytest.mark.parametrize("seed,n,R", [(1, 5, 24), (2, 70, 30), (3, 130, 20), (4, 300, 12)])
+def test_shard_random_dags(gpu_device, seed, n, R):
+    """Unconstrained random DAGs (dangling targets, ghosts, deep weak edges) at G = 1, 2, 3, 8."""
+    rng = np.random.default_rng(1000 + seed)
+    d = random_dag(rng, n, R, p_present=0.8, p_s=0.3, p_w=0.2, max_depth=7)
+    bs = oracle.PDag(d)
+    froms = [(int(rng.integers(1, R + 1)), int(rng.integers(1, n + 1))) for _ in range(70)]  # > one batch of 64
+    bottoms = [int(rng.integers(0, fr[0] + 1)) for fr in froms]
+    ids = [(r, s) for r in range(R + 1) for s in range(0, n + 1)]
+    samp = [ids[i] for i in rng.choice(len(ids), size=min(len(ids), 24), replace=False)]
+    pairs = [(a, b) for a in samp for b in samp]
+    for G in (1, 2, 3, 8):
+        with ShardEngine(n, (n - 1) // 3, R + 1, gpu_device, nshards=G) as se:
+            se.append_packed(d)
+            _check_reach(se, bs, froms, bottoms)
+            for strong in (True, False):
+                want = np.asarray([bs.path(a, b, strong) for a, b in pairs], dtype=np.uint8)
+                assert (se.path_batch(pairs, strong) == want).all(), (G, strong)
+
+
+def test_shard_incremental_append_and_edge_queries(gpu_device):
+    """Round-by-round appends; bottom == top; absent/unknown sources agree with dr_reach_sets."""
+    rng = np.random.default_rng(9)
+    n, R = 90, 16
+    d = random_dag(rng, n, R, p_present=0.7, p_s=0.4, p_w=0.3, max_depth=5)
+    bs = oracle.PDag(d)
+    with ShardEngine(n, 29, R + 1, gpu_device, nshards=2) as se, Engine(n, 29, R + 1, gpu_device) as e:
+        for r in range(R + 1):
+            se.append_packed(d, r, r + 1)
+        e.append_packed(d)
+        assert se.num_rounds == R + 1
+        froms = [(R, 1), (R, n), (7, 3), (5, 5), (R, 0), (3, n)]
+        bottoms = [R, 0, 7, 0, 2, 1]
+        for strong in (True, False):
+            got = se.reach_sets(froms, bottoms, strong)
+            ref = e.reach_sets(froms, bottoms, strong)
+            for a, b in zip(got, ref):
+                assert (a == b).all()
+        _check_reach(se, bs, [f for f in froms if f[1] >= 1], [b for f, b in zip(froms, bottoms) if f[1] >= 1])
+
+
+def test_shard_generated_n1024(gpu_device):
+    """C4 parameters (n=1024, weak delta 2..4) on 120 rounds: G = 1, 2, 4, 8 agree with the oracle."""
+    cfg = small_config(1024, 120, 4, p_present=1.0, p_late=0.02, p_w=0.5, weak_depth=4)
+    d = generate(cfg)
+    bs = oracle.PDag(d)
+    rng = np.random.default_rng(5)
+    froms = [(120, 1), (117, 512)] + [(int(rng.integers(60, 121)), int(rng.integers(1, 1025))) for _ in range(10)]
+    bottoms = [0, 30] + [int(rng.integers(0, 50)) for _ in range(10)]
+    for G in (1, 2, 4, 8):
+        with ShardEngine(1024, 341, 121, gpu_device, nshards=G) as se:
+            se.append_packed(d)
+            info = se.info()
+            assert info["nshards"] == G and info["nlocal"] == G and (info["col0"], info["col1"]) == (1, 1025)
+            _check_reach(se, bs, froms, bottoms)
+            st = se.stats()
+            assert st["rounds"] > 0 and st["exchange_bytes"] == 0  # local mode: no collective
+
+
+def test_shard_rccl_single_rank(gpu_device):
+    """RCCL mode with a one-rank communicator: the all-gather path runs and agrees."""
+    rng = np.random.default_rng(11)
+    n, R = 200, 20
+    d = random_dag(rng, n, R, p_present=0.8, p_s=0.3, p_w=0.2, max_depth=6)
+    bs = oracle.PDag(d)
+    uid = shard_unique_id()
+    with ShardEngine(n, 66, R + 1, gpu_device, nshards=1, rank=0, unique_id=uid) as se:
+        se.append_packed(d)
+        froms = [(R, s) for s in range(1, 40)]
+        bottoms = [0] * len(froms)
+        _check_reach(se, bs, froms, bottoms)
+        st = se.stats()
+        assert st["exchange_bytes"] > 0
+
+
+def test_shard_errors(gpu_device):
+    from dag_rider_amd import _lib as L
+
+    with pytest.raises(L.DrError):
+        ShardEngine(10, 3, 8, gpu_device, nshards=0)
+    with pytest.raises(L.DrError):
+        ShardEngine(10, 3, 8, gpu_device, nshards=2, rank=1)  # local mode is rank 0
+    g, dag = figure1()
+    d = pack_lists(dag, g["n"])
+    with ShardEngine(g["n"], g["faulty"], 8, gpu_device, nshards=2) as se:
+        se.append_packed(d)
+        with pytest.raises(L.DrError) as ei:
+            se.reach_sets([(9, 1)], [0], True)
+        assert ei.value.code == L.DR_E_INVAL
+        with pytest.raises(L.DrError) as ei:
+            se.append_packed(d, 2, 3)  # not contiguous
+        assert ei.value.code == L.DR_E_STATE
