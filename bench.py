@@ -10,6 +10,8 @@ counted by SURVEY.md s8(d)'s formula (the same numbers the CPU oracle reports).
 
 N>1 (torchrun, one rank per GPU): each rank replays its own independent C4 DAG
 (seed 4+rank): independent units, no data-path collective ("scaling": "weak").
+After the timed region, N>1 also runs the process-column sharded sweep of one C4
+DAG across all ranks (RCCL all-gather of the frontier per round; detail.colshard).
 
 Prints ONE JSON line on rank 0.
 """
@@ -142,6 +144,76 @@ def reduce_over_ranks(dist, dt: float, edges: int, device: str):
     return float(t.item()), float(e.item())
 
 
+def colshard_child(args):
+    """One rank of the process-column sharded sweep: every rank
+    holds 1/N of the target columns; the frontier is all-gathered over RCCL each round.
+    Workload: the full causal-history reach sets (strong + weak, rounds 0..leader) of
+    the 64 newest wave leaders of the C4 DAG -- the sets orderVertices delivers."""
+    import numpy as np
+
+    from dag_rider_amd.gen import CONFIGS, generate
+    from dag_rider_amd.shard import ShardEngine
+
+    cfg = CONFIGS["c4"]
+    d = generate(cfg, nthreads=16)
+    se = ShardEngine(cfg.n, cfg.faulty, d.nrounds, args.cs_device, args.cs_world, args.cs_rank,
+                     bytes.fromhex(args.cs_uid))
+    se.append_packed(d)
+    froms = [(4 * w - 3, 1) for w in range(cfg.nwaves, cfg.nwaves - 64, -1)]
+    bottoms = [0] * len(froms)
+    got = se.reach_sets(froms, bottoms, False)  # warm-up
+    runs = []
+    for _ in range(3):
+        got = se.reach_sets(froms, bottoms, False)
+        runs.append(se.stats())
+    st = min(runs, key=lambda x: x["ms"])
+    out = dict(st, nshards=args.cs_world, queries=len(froms), info=se.info())
+    se.close()
+    if args.cs_rank == 0:
+        from dag_rider_amd.engine import Engine
+
+        with Engine(cfg.n, cfg.faulty, d.nrounds, args.cs_device) as e:
+            e.append_packed(d)
+            ref = e.reach_sets(froms, bottoms, False)
+        out["verify_vs_unsharded"] = bool(all((a == b).all() for a, b in zip(got, ref)))
+        out["reach_bits"] = int(sum(int(np.unpackbits(a.view(np.uint8)).sum()) for a in got))
+    print(json.dumps(out), flush=True)
+
+
+def colshard_check(dist, rank: int, world: int, local: int, timeout_s: float = 240.0):
+    """Run colshard_child in one child process per rank (a hung collective can then be
+    killed without losing the headline line); returns rank 0's result + max time."""
+    import subprocess
+
+    from dag_rider_amd.shard import exchange_unique_id
+
+    if dist is not None:
+        uid = exchange_unique_id(dist)
+    else:
+        from dag_rider_amd.shard import shard_unique_id
+
+        uid = shard_unique_id()
+    cmd = [sys.executable, os.path.abspath(__file__), "--colshard-child", "--cs-uid", uid.hex(),
+           "--cs-rank", str(rank), "--cs-world", str(world), "--cs-device", str(local)]
+    res = None
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+        lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+        res = json.loads(lines[-1]) if p.returncode == 0 and lines else dict(error=(p.stderr or "")[-400:])
+    except subprocess.TimeoutExpired:
+        res = dict(error=f"timed out after {timeout_s} s")
+    if dist is not None:
+        allr = [None] * world
+        dist.all_gather_object(allr, res)
+    else:
+        allr = [res]
+    ms = [r.get("ms") for r in allr if r and "ms" in r]
+    if rank == 0 and res is not None:
+        res["ms_max_over_ranks"] = max(ms) if len(ms) == world else None
+        res["errors"] = [r.get("error") for r in allr if r and "error" in r] or None
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,7 +223,17 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check the replay against the bitset oracle")
+    ap.add_argument("--colshard", action="store_true",
+                    help="also run the process-column sharded C4 sweep (default on when N>1)")
+    ap.add_argument("--no-colshard", action="store_true")
+    ap.add_argument("--colshard-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cs-uid", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--cs-rank", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--cs-world", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--cs-device", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.colshard_child:
+        return colshard_child(args)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -208,6 +290,12 @@ def main():
                       and (want.pop_count == res.pop_count).all() and want.deliver_edges == res.deliver_edges
                       and want.chain_edges == res.chain_edges and want.commit_edges == res.commit_edges)
 
+    colshard = None
+    if (world > 1 or args.colshard) and not args.no_colshard:
+        colshard = colshard_check(dist, rank, world, local)
+        if rank == 0:
+            log(f"[colshard] {colshard}")
+
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -253,6 +341,7 @@ def main():
                    "chain_edges": res.chain_edges, "deliver_edges": res.deliver_edges,
                    "commits": int(res.commit.sum()), "pops": int(len(res.pop_count)),
                    "ms": res.ms, "sweep": res.sweep, "verify_vs_oracle": verify,
+                   "colshard": colshard,
                    "kernels": {k: dict(v, GBps=(v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None))
                                for k, v in kb.items()}},
     }

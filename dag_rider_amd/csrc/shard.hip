@@ -105,11 +105,15 @@ __global__ void __launch_bounds__(SH_NT) k_shard_round(ShardArgs a, int r, u64 e
   const int C = a.C;
   u64 *pend = a.pend + (size_t)l * a.depth * C;
 
-  // 1 + 2: reach rows of round r and strong expansion into round r-1
-  for (int s0 = gw * 64; s0 < a.n; s0 += nwv * 64) {
+  // 1 + 2: reach rows of round r and strong expansion into round r-1.  A wave's
+  // work item is (64-source chunk, target word): nchunks * WSs items spread over
+  // every wave of the grid; the chunk's first word also writes the reach rows.
+  const int nchunks = (a.n + 63) >> 6;
+  for (int it = gw; it < nchunks * a.WSs; it += nwv) {
+    const int s0 = (it / a.WSs) * 64, tw = it % a.WSs;
     const int s = s0 + lane;
     const u64 m = s < a.n ? a.ft[s] : 0ULL;
-    if (l == 0 && outmask) {
+    if (l == 0 && tw == 0 && outmask) {
       u64 mine = 0;
       for (u64 om = outmask; om; om &= om - 1) {
         const int b = __builtin_ctzll(om);
@@ -123,19 +127,18 @@ __global__ void __launch_bounds__(SH_NT) k_shard_round(ShardArgs a, int r, u64 e
     }
     const u64 me = m & expmask;
     if (r < 1 || __ballot(me != 0ULL) == 0ULL) continue;
-    const u64 *rows = a.strong + (size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.WSs;
-    for (int tw = 0; tw < a.WSs; tw++) {
-      const u64 row = (me != 0ULL) ? rows[tw] : 0ULL;
-      u64 act = __ballot(row != 0ULL);
-      u64 acc = 0;
-      while (act) {  // wave-uniform loop over the sources that contribute
-        const int src = __builtin_ctzll(act);
-        act &= act - 1;
-        const u64 rs = rdlane64(row, src), ms = rdlane64(me, src);
-        if ((rs >> lane) & 1ULL) acc |= ms;
-      }
-      if (acc) atomicOr(&pend[(size_t)((r - 1) & (a.depth - 1)) * C + tw * 64 + lane], acc);
+    const u64 row = (me != 0ULL)
+                        ? a.strong[(size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.WSs + tw]
+                        : 0ULL;
+    u64 act = __ballot(row != 0ULL);
+    u64 acc = 0;
+    while (act) {  // wave-uniform loop over the sources that contribute
+      const int src = __builtin_ctzll(act);
+      act &= act - 1;
+      const u64 rs = rdlane64(row, src), ms = rdlane64(me, src);
+      if ((rs >> lane) & 1ULL) acc |= ms;
     }
+    if (acc) atomicOr(&pend[(size_t)((r - 1) & (a.depth - 1)) * C + tw * 64 + lane], acc);
   }
 
   // 3: weak expansion
@@ -299,9 +302,9 @@ int sweep_batch(dr_shard *c, const std::vector<QInfo> &qs, const std::vector<siz
   a.nq = nq;
   a.strong_only = strong_only;
   a.strong_shard_stride = (int64_t)c->max_rounds * c->n * c->WSs;
-  const int src_waves = (c->n + 63) / 64;
-  const size_t weak_waves = strong_only ? 0 : (c->max_weak_round + 1023) / 1024;
-  const int gx = (int)std::max<size_t>((src_waves + 3) / 4, std::min<size_t>(64, (weak_waves + 3) / 4));
+  const int item_waves = (c->n + 63) / 64 * c->WSs;  // (source chunk, target word) items
+  const size_t weak_waves = strong_only ? 0 : (c->max_weak_round + 511) / 512;
+  const int gx = (int)std::max<size_t>((item_waves + 3) / 4, std::min<size_t>(128, (weak_waves + 3) / 4));
   const dim3 grid(gx, c->nlocal), block(SH_NT);
   for (int r = T; r >= Bm; r--) {
     u64 expm = 0, outm = 0, injm = 0;
