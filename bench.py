@@ -92,24 +92,40 @@ def cpu_bitset(cfg, d, nthreads: int, budget_s: float):
 def kernel_bytes(cfg, d, res):
     """Algorithmic bytes per launch of each replay phase."""
     n, W, T = cfg.n, (cfg.n + 63) // 64, d.nrounds - 1
-    nweak = int(d.weak_off[-1])
+    nwc = weak_columns(d)
     leaders = int((res.vcount >= 0).sum())
     dd = max(0, weak_depth(d) - 1)
     sw = res.sweep
     out = {
-        # every strong row and weak edge of rounds 1..T read once; U, WU, SD written
+        # every strong row of rounds 1..T and every weak-column key read once; U, WU, SD written
         "summary": dict(kernel="k_summary (round summaries)", ms=res.ms["summary"],
-                        bytes=T * n * W * 8 + nweak * 4 + T * (1 + dd) * W * 8 + T * 8),
+                        bytes=T * n * W * 8 + nwc * 4 + T * (1 + dd) * W * 8 + T * 8),
         # round 4w-2: the word holding the leader bit; rounds 4w-1, 4w: whole rows
         "commit": dict(kernel="k_commit (waveReady commit rule)", ms=res.ms["commit"],
                        bytes=leaders * (n * 8 + 2 * n * W * 8)),
-        # partial rounds: rows of the frontier + the round's weak list; summary
+        # partial rounds: rows of the frontier + the round's weak columns (key + row); summary
         # rounds: U + WU; every round: presence, K and the reach mask written
         "sweep": dict(kernel="k_sweep (orderVertices cones, merge with canonical)", ms=res.ms["deliver"],
-                      bytes=sw["rows"] * W * 8 + sw["weak_scanned"] * 4 + sw["shortcut"] * (1 + dd) * W * 8
+                      bytes=sw["rows"] * W * 8 + sw["weak_scanned"] * (W * 8 + 4) + sw["shortcut"] * (1 + dd) * W * 8
                       + (sw["partial"] + sw["shortcut"]) * 3 * W * 8),
     }
     return out
+
+
+def weak_columns(d):
+    """weak-column entries of the device mirror: distinct (round, delta, target) over
+    the near weak edges (delta <= 1023), kernels.hpp DagView::wc_*."""
+    import numpy as np
+
+    n = d.n
+    g = np.repeat(np.arange(d.nrounds * n, dtype=np.int64), np.diff(d.weak_off.astype(np.int64)))
+    if len(g) == 0:
+        return 0
+    r = g // n
+    t = d.weak_tgt.astype(np.int64)
+    delta = r - (t >> 11)
+    near = delta <= 1023
+    return int(len(np.unique((r[near] << 22) | (delta[near] << 11) | (t[near] & 2047))))
 
 
 def weak_depth(d):

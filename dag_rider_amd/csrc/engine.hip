@@ -80,6 +80,11 @@ struct dr_ctx {
   // device DAG
   DevBuf strong, present, slot_off, slot_src, weak, weak_roff, far, far_roff;
   size_t nweak = 0, nfar = 0;
+  // weak columns (kernels.hpp DagView::wc_*): one entry per distinct near weak
+  // target (delta, t) of a round + the bitset of the round's sources pointing at it
+  DevBuf wc_key, wc_rows, wc_roff;
+  size_t nwc = 0;
+  std::vector<uint32_t> h_wc_roff{0};
   // host mirrors
   std::vector<uint32_t> h_slot_off{0};
   std::vector<uint16_t> h_slot_src;
@@ -219,6 +224,9 @@ struct dr_ctx {
     v.weak_roff = weak_roff.as<uint32_t>();
     v.far = far.as<u64>();
     v.far_roff = far_roff.as<uint32_t>();
+    v.wc_key = wc_key.as<uint32_t>();
+    v.wc_rows = wc_rows.as<u64>();
+    v.wc_roff = wc_roff.as<uint32_t>();
     v.n = n;
     v.nrounds = nrounds;
     return v;
@@ -518,6 +526,8 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
       c->weak_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->far_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->weak.ensure(4096) != hipSuccess || c->far.ensure(4096) != hipSuccess ||
+      c->wc_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
+      c->wc_key.ensure(4096) != hipSuccess || c->wc_rows.ensure(4096) != hipSuccess ||
       c->slot_src.ensure(4096) != hipSuccess) {
     g_create_err = "dr_create: device allocation failed";
     dr_destroy(c);
@@ -527,6 +537,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   (void)hipMemcpy(c->slot_off.p, &zero, 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(c->weak_roff.p, &zero, 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(c->far_roff.p, &zero, 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(c->wc_roff.p, &zero, 4, hipMemcpyHostToDevice);
   *out = c;
   return DR_OK;
 }
@@ -543,7 +554,8 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->digest,  &c->pop_pos, &c->ids,      &c->U,        &c->WU,
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
-                    &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena};
+                    &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena,
+                    &c->wc_key,  &c->wc_rows, &c->wc_roff};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -645,6 +657,24 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
       // after two passes the sorted data is back in wdev
     }
   }
+  // weak columns: each run of equal (delta, target) in the sorted round is one
+  // entry; its row holds the sources of the run (bit s-1, WS-word stride)
+  std::vector<uint32_t> wck, wcroff(k + 1);
+  std::vector<u64> wcrows;
+  for (int i = 0; i < k; i++) {
+    wcroff[i] = (uint32_t)wck.size();
+    const size_t a = wroff[i], b = (i + 1 < k) ? wroff[i + 1] : wdev.size();
+    for (size_t e = a; e < b; e++) {
+      const uint32_t x = wdev[e], key = ((x >> 22) << 11) | (x & 2047u);
+      if (e == a || key != wck.back()) {
+        wck.push_back(key);
+        wcrows.resize(wcrows.size() + WS, 0ULL);
+      }
+      const uint32_t own = (x >> 11) & 2047u;
+      wcrows[wcrows.size() - WS + (own >> 6)] |= 1ULL << (own & 63);
+    }
+  }
+  wcroff[k] = (uint32_t)wck.size();
   // ---- commit to device ----
   const size_t row_words = (size_t)n * WS;
   if (WS == W) {
@@ -671,6 +701,14 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   if (!wdev.empty())
     HIPCHK(c, hipMemcpyAsync(c->weak.as<uint32_t>() + c->nweak, wdev.data(), wdev.size() * 4,
                              hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, c->wc_key.grow((c->nwc + wck.size()) * 4 + 64, c->nwc * 4, c->stream));
+  HIPCHK(c, c->wc_rows.grow((c->nwc + wck.size()) * WS * 8 + 64, c->nwc * WS * 8, c->stream));
+  if (!wck.empty()) {
+    HIPCHK(c, hipMemcpyAsync(c->wc_key.as<uint32_t>() + c->nwc, wck.data(), wck.size() * 4,
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->wc_rows.as<u64>() + c->nwc * WS, wcrows.data(), wcrows.size() * 8,
+                             hipMemcpyHostToDevice, c->stream));
+  }
   HIPCHK(c, c->far.grow((c->nfar + fdev.size()) * 8 + 64, c->nfar * 8, c->stream));
   if (!fdev.empty())
     HIPCHK(c, hipMemcpyAsync(c->far.as<u64>() + c->nfar, fdev.data(), fdev.size() * 8,
@@ -680,6 +718,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
     c->h_slot_off.push_back(c->h_slot_off.back() + (slot_off[i + 1] - slot_off[i]));
     c->h_weak_roff.push_back((uint32_t)(c->nweak + (i + 1 < k ? wroff[i + 1] : wdev.size())));
     c->h_far_roff.push_back((uint32_t)(c->nfar + (i + 1 < k ? froff[i + 1] : fdev.size())));
+    c->h_wc_roff.push_back((uint32_t)(c->nwc + wcroff[i + 1]));
   }
   c->h_slot_src.insert(c->h_slot_src.end(), slot_src + slot_off[0], slot_src + slot_off[k]);
   c->h_present.insert(c->h_present.end(), pres.begin(), pres.end());
@@ -690,9 +729,12 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
                            hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->far_roff.as<uint32_t>() + r0 + 1, &c->h_far_roff[r0 + 1], (size_t)k * 4,
                            hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->wc_roff.as<uint32_t>() + r0 + 1, &c->h_wc_roff[r0 + 1], (size_t)k * 4,
+                           hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->nweak += wdev.size();
   c->nfar += fdev.size();
+  c->nwc += wck.size();
   c->dmax_near = dmax;
   c->nrounds += k;
   c->summary_T = -1;  // summaries describe the old DAG

@@ -6,6 +6,11 @@
 //   weak    u32 per edge, grouped by round (weak_roff[r]..weak_roff[r+1]):
 //           bits 0-10 target source-1, 11-21 own source-1, 22-31 delta = r - r'
 //   far     u64 per edge with delta > 1023: (own source-1) << 32 | (r' << 11 | t-1)
+//   wc      weak columns, grouped by round (wc_roff[r]..wc_roff[r+1]): one entry per
+//           distinct near weak target of the round, key (delta << 11 | t-1), and a
+//           WS-word row of the round's sources with that edge.  A late vertex
+//           collects hundreds of weak edges, so the columns are ~1/16 of the edge
+//           list at C4; the sweeps and the weak union read them instead.
 //
 // Kernels (all integer/boolean; HBM-bound, no MFMA):
 //   k_commit  waveReady's commit decision (process.go:326-339) for a range of
@@ -51,6 +56,9 @@ struct DagView {
   const uint32_t *weak_roff;
   const u64 *far;
   const uint32_t *far_roff;
+  const uint32_t *wc_key;
+  const u64 *wc_rows;
+  const uint32_t *wc_roff;
   int32_t n;
   int32_t nrounds;
 };
@@ -350,21 +358,31 @@ __device__ __forceinline__ int expand_weak(const DagView &g, int r, int bottom, 
                                            int depth, u64 *mask_bottom, u64 &my_wedges) {
   const int tid = threadIdx.x, dmask = depth - 1;
   int lowmin = 0x7fffffff;
-  const uint32_t e0 = g.weak_roff[r], e1 = g.weak_roff[r + 1];
-  my_wedges += walk_weak<NT, 4>(
-      g.weak, e0, e1, ring, [&](int own) { return ((FE[own >> 6] >> (own & 63)) & 1ULL) != 0; },
-      [&](int delta, int ts) -> int {
-        const int tr = r - delta;
-        if (tr < bottom || delta >= depth) return -1;
+  // weak columns of round r: lane group j (WS lanes, lane w owns word w) tests
+  // entry j's source row against FE; a hit sets the target bit (one atomic per
+  // entry), the popcount is the number of weak edges followed.
+  static_assert(WS <= 64 && (64 % WS) == 0, "WS lanes per column entry");
+  constexpr int EPP = NT / WS;  // entries per pass
+  const int w = tid % WS, lane = tid & 63, gbase = lane & ~(WS - 1);
+  const uint32_t c0 = g.wc_roff[r], c1 = g.wc_roff[r + 1];
+  const u64 fe = FE[w];
+  for (uint32_t j0 = c0; j0 < c1; j0 += EPP) {
+    const uint32_t j = j0 + (uint32_t)(tid / WS);
+    const u64 v = j < c1 ? g.wc_rows[(size_t)j * WS + w] & fe : 0ULL;
+    my_wedges += (u64)popc64(v);
+    const u64 bal = __ballot(v != 0ULL);
+    const u64 gm = WS >= 64 ? ~0ULL : (((1ULL << WS) - 1ULL) << gbase);
+    if (w == 0 && (bal & gm)) {
+      const uint32_t key = g.wc_key[j];
+      const int delta = (int)(key >> 11), ts = (int)(key & 2047u), tr = r - delta;
+      if (tr >= bottom) {
+        const u64 bit = 1ULL << (ts & 63);
         lowmin = min(lowmin, tr);
-        return (tr & dmask) * WS + (ts >> 6);
-      },
-      [&](int delta, int ts, u64 bit) {
-        const int tr = r - delta;
-        if (tr < bottom) return;
-        lowmin = min(lowmin, tr);
-        atomicOr(mask_bottom + (int64_t)(tr - bottom) * WS + (ts >> 6), bit);
-      });
+        if (delta < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
+        else atomicOr(mask_bottom + (int64_t)(tr - bottom) * WS + (ts >> 6), bit);
+      }
+    }
+  }
   const uint32_t f0 = g.far_roff[r], f1 = g.far_roff[r + 1];
   for (uint32_t e = f0 + tid; e < f1; e += NT) {
     const u64 y = g.far[e];
@@ -556,7 +574,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
             for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
             if (tid == 0 && !stop) {
               if (summary) st_short++;
-              else { st_partial++; st_rows += (u64)pc; if (WEAK) st_scan += g.weak_roff[r + 1] - g.weak_roff[r]; }
+              else { st_partial++; st_rows += (u64)pc; if (WEAK) st_scan += g.wc_roff[r + 1] - g.wc_roff[r]; }
             }
           }
           if (summary) {  // the round is the union of its rows: apply the summaries, stay in wave 0
@@ -765,8 +783,11 @@ __global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64
   if (r > T) return;
   for (int i = tid; i < dd * WS; i += NT) sWU[i] = 0;
   __syncthreads();
-  walk_weak<NT, 8>(g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
-                   [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
+  // every weak-column entry has at least one source: its key alone is the union
+  for (uint32_t j = g.wc_roff[r] + tid; j < g.wc_roff[r + 1]; j += NT) {
+    const uint32_t key = g.wc_key[j];
+    atomicOr(&sWU[((key >> 11) - 2) * WS + ((key & 2047u) >> 6)], 1ULL << (key & 63u));
+  }
   __syncthreads();
   for (int i = tid; i < dd * WS; i += NT) WU[(size_t)r * dd * WS + i] = sWU[i];
 }
