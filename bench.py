@@ -106,7 +106,7 @@ def kernel_bytes(cfg, d, res):
         # partial rounds: rows of the frontier + the round's weak columns (key + row); summary
         # rounds: U + WU; every round: presence, K and the reach mask written
         "sweep": dict(kernel="k_sweep (orderVertices cones, merge with canonical)", ms=res.ms["deliver"],
-                      bytes=sw["rows"] * W * 8 + sw["weak_scanned"] * (W * 8 + 4) + sw["shortcut"] * (1 + dd) * W * 8
+                      bytes=sw["row_bytes"] + sw["weak_scanned"] * (W * 8 + 4) + sw["shortcut"] * (1 + dd) * W * 8
                       + (sw["partial"] + sw["shortcut"]) * 3 * W * 8),
     }
     return out

@@ -34,7 +34,7 @@ class ReplayOut(C.Structure):
                 ("n_push", i64), ("n_ids", i64), ("commit_edges", u64), ("chain_edges", u64),
                 ("deliver_edges", u64), ("ms_commit", f32), ("ms_chain", f32), ("ms_deliver", f32),
                 ("ms_emit", f32), ("ms_summary", f32), ("canon_segments", i32), ("sweep_count", u64),
-                ("sweep_partial", u64), ("sweep_rows", u64), ("sweep_weak_scanned", u64), ("sweep_shortcut", u64)]
+                ("sweep_partial", u64), ("sweep_row_bytes", u64), ("sweep_weak_scanned", u64), ("sweep_shortcut", u64)]
 
 
 # symbol -> (restype, argtypes); every symbol declared in include/*.h

@@ -84,6 +84,7 @@ struct dr_ctx {
   // target (delta, t) of a round + the bitset of the round's sources pointing at it
   DevBuf wc_key, wc_rows, wc_roff;
   size_t nwc = 0;
+  DevBuf sdeg;  // [max_rounds][n] u16 strong degree per vertex (kernels.hpp expand_rows)
   std::vector<uint32_t> h_wc_roff{0};
   // host mirrors
   std::vector<uint32_t> h_slot_off{0};
@@ -227,6 +228,7 @@ struct dr_ctx {
     v.wc_key = wc_key.as<uint32_t>();
     v.wc_rows = wc_rows.as<u64>();
     v.wc_roff = wc_roff.as<uint32_t>();
+    v.sdeg = sdeg.as<uint16_t>();
     v.n = n;
     v.nrounds = nrounds;
     return v;
@@ -528,6 +530,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
       c->weak.ensure(4096) != hipSuccess || c->far.ensure(4096) != hipSuccess ||
       c->wc_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->wc_key.ensure(4096) != hipSuccess || c->wc_rows.ensure(4096) != hipSuccess ||
+      c->sdeg.ensure((size_t)max_rounds * n * sizeof(uint16_t)) != hipSuccess ||
       c->slot_src.ensure(4096) != hipSuccess) {
     g_create_err = "dr_create: device allocation failed";
     dr_destroy(c);
@@ -555,7 +558,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena,
-                    &c->wc_key,  &c->wc_rows, &c->wc_roff};
+                    &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -587,6 +590,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   const int n = c->n, W = c->W, WS = c->WS;
   std::vector<u64> pres((size_t)k * WS, 0);
   std::vector<uint64_t> deg(k, 0);
+  std::vector<uint16_t> vdeg((size_t)k * n, 0);
   std::vector<uint32_t> wdev, wroff(k);
   std::vector<u64> fdev;
   std::vector<uint32_t> froff(k);
@@ -616,6 +620,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
       if (nz && r == 0) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", s0 + 1);
       if (row[W - 1] & ~lastmask) return c->fail(DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
       deg[i] += d;
+      vdeg[(size_t)i * n + s0] = (uint16_t)d;
       const uint32_t ea = weak_off[(size_t)i * n + s0], eb = weak_off[(size_t)i * n + s0 + 1];
       if (eb < ea) return c->fail(DR_E_INVAL, "weak_off not monotone at round %d", r);
       if (eb > ea && !here) return c->fail(DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1);
@@ -689,6 +694,8 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   HIPCHK(c, hipMemcpyAsync(c->present.as<u64>() + (size_t)r0 * WS, pres.data(), pres.size() * 8,
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->sdeg.as<uint16_t>() + (size_t)r0 * n, vdeg.data(), vdeg.size() * 2,
                            hipMemcpyHostToDevice, c->stream));
   // slots
   const size_t old_slots = c->h_slot_src.size();
@@ -1743,7 +1750,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   o->deliver_edges = h_hdr[dr::PH_DELIVER_E];
   o->sweep_count = h_hdr[dr::PH_NQD];
   o->sweep_partial = h_hdr[dr::PH_PARTIAL];
-  o->sweep_rows = h_hdr[dr::PH_ROWS];
+  o->sweep_row_bytes = h_hdr[dr::PH_ROWS];
   o->sweep_weak_scanned = h_hdr[dr::PH_WEAK];
   o->sweep_shortcut = h_hdr[dr::PH_SHORT];
   o->n_ids = 0;
@@ -1759,7 +1766,7 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad deliver mode");
   if (int rc = set_device(c)) return rc;
   o->ms_commit = o->ms_chain = o->ms_deliver = o->ms_emit = o->ms_summary = 0;
-  o->sweep_count = o->sweep_partial = o->sweep_rows = o->sweep_weak_scanned = o->sweep_shortcut = 0;
+  o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;
   o->canon_segments = -1;
   if (c->plan_mode != 0 && c->use_memo && c->memo_ok() && deliver_mode == DR_DELIVER_REF &&
@@ -1816,7 +1823,7 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   if (rc) return rc;
   o->sweep_count = st.sweeps;
   o->sweep_partial = st.partial;
-  o->sweep_rows = st.rows;
+  o->sweep_row_bytes = st.rows;
   o->sweep_weak_scanned = st.weak_scanned;
   o->sweep_shortcut = st.shortcut;
   uint64_t de = 0;
@@ -1955,7 +1962,7 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     o->ms_commit = o->ms_chain = o->ms_emit = o->ms_summary = 0;
     o->ms_deliver = ms;  // the whole fused replay kernel
     o->canon_segments = -1;
-    o->sweep_count = o->sweep_partial = o->sweep_rows = o->sweep_weak_scanned = o->sweep_shortcut = 0;
+    o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
     if (np > o->push_cap || !o->push_wave || !o->pop_count || !o->pop_digest)
       return c0->fail(DR_E_CAPACITY, "context %d: %lld pushed leaders, capacity %lld", i, (long long)np,
                       (long long)o->push_cap);

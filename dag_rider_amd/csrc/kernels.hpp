@@ -59,6 +59,7 @@ struct DagView {
   const uint32_t *wc_key;
   const u64 *wc_rows;
   const uint32_t *wc_roff;
+  const uint16_t *sdeg;  // [rounds][n] strong degree per vertex
   int32_t n;
   int32_t nrounds;
 };
@@ -303,20 +304,42 @@ __device__ __forceinline__ uint32_t walk_weak(const uint32_t *__restrict__ weak,
 }
 
 // strong rows of the vertices in FE (round r) -> ring slot of round r-1.
-// Loads go out in groups of 8 passes (16 B each), so register use does not grow
-// with the rows per thread.
+// Loads go out in groups of GRP passes (16 B each), so register use does not grow
+// with the rows per thread.  With Ur (round r's union of rows, from the round
+// summaries) a wave stops loading rows once the OR of the rows it has read equals
+// Ur -- no further row can add a bit -- and takes the remaining frontier vertices'
+// strong degrees from sdeg (2 B instead of a W*8-B row) for the edge count.  The
+// result is exact either way.  row_bytes counts the bytes actually read.
 template <int WS, int NT>
 __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *FE, u64 *ring, int dmask,
-                                            u64 &my_edges) {
+                                            u64 &my_edges, const u64 *Ur, u64 &row_bytes) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
-  constexpr int GRP = CPT < 8 ? CPT : 8;
+  constexpr int GRP = CPT < 2 ? CPT : 2;
   const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
   const u64 *rows = g.strong + (size_t)r * n * WS;
+  const uint16_t *deg = g.sdeg + (size_t)r * n;
   u64 a0 = 0, a1 = 0;
+  u64 u0 = ~0ULL, u1 = ~0ULL;  // never equal to a partial OR when Ur is absent
+  if (Ur) {
+    u0 = Ur[CW * j];
+    u1 = CW == 2 ? Ur[CW * j + 1] : 0ULL;
+  }
+  bool sat = false;
 #pragma unroll 1
   for (int p0 = 0; p0 < CPT; p0 += GRP) {
     if ((tid / CPR) + p0 * RPP - (tid & ~63) / CPR >= n) break;  // wave-uniform: rows of this wave done
+    if (sat) {  // rows cannot add bits: degrees only
+#pragma unroll
+      for (int p = 0; p < GRP; p++) {
+        const int s = tid / CPR + (p0 + p) * RPP;
+        if (j == 0 && s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
+          my_edges += deg[s];
+          row_bytes += 2;
+        }
+      }
+      continue;
+    }
     u64 v0[GRP], v1[GRP];
 #pragma unroll
     for (int p = 0; p < GRP; p++) {
@@ -331,6 +354,7 @@ __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *
         } else {
           v0[p] = rows[s];
         }
+        row_bytes += CW * 8;
       }
     }
 #pragma unroll
@@ -338,6 +362,15 @@ __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *
       a0 |= v0[p];
       a1 |= v1[p];
       my_edges += (u64)(popc64(v0[p]) + popc64(v1[p]));
+    }
+    if (Ur) {  // the wave's OR so far (lanes of one chunk class j) against U_r
+      u64 r0 = a0, r1 = a1;
+#pragma unroll
+      for (int off = CPR; off < 64; off <<= 1) {
+        r0 |= __shfl_xor(r0, off);
+        if (CW == 2) r1 |= __shfl_xor(r1, off);
+      }
+      sat = __ballot(r0 != u0 || r1 != u1) == 0ULL;
     }
   }
   // chunk j = lane mod CPR: fold each row's lanes of class j, then one LDS OR per row
@@ -486,7 +519,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
   const int depth = 1 << depth_log2, dmask = depth - 1;
   // ctl: [0] low water [1] round [2] status (0 partial, 1 stop) [3] merged [4] stop round
   int *s_ctl = reinterpret_cast<int *>(ring + (size_t)depth * WS);
-  u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 8);  // [0] all edges, [1] weak edges
+  u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 8);  // [0] all edges, [1] weak edges, [2] row bytes
   const int tid = threadIdx.x;
   const bool w0 = tid < 64;     // wave 0 runs phase A and every summary round
   const bool act = tid < WS;    // lane w owns frontier word w
@@ -500,15 +533,15 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
     for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
     if (tid == 0) {
       s_ctl[0] = q.top; s_ctl[1] = q.top; s_ctl[2] = 0; s_ctl[3] = 0; s_ctl[4] = q.bottom;
-      s_edges[0] = 0; s_edges[1] = 0;
+      s_edges[0] = 0; s_edges[1] = 0; s_edges[2] = 0;
     }
     __syncthreads();
     if (tid == 0 && q.src0 >= 0)
       ring[(size_t)(q.top & dmask) * WS + (q.src0 >> 6)] = 1ULL << (q.src0 & 63);
     int npush = 0;  // thread 0
-    u64 st_partial = 0, st_rows = 0, st_scan = 0, st_short = 0;  // thread 0: work counters
+    u64 st_partial = 0, st_scan = 0, st_short = 0;  // thread 0: work counters
     int run = 0;    // wave 0: consecutive rounds equal to K
-    u64 my_edges = 0, my_wedges = 0;
+    u64 my_edges = 0, my_wedges = 0, my_rowb = 0;
     RoundWords cur{}, nxt{};
     if (act) {
       if (shortcut) load_round<WS, MERGE, true, WEAK>(g, mv, q.top, cur);
@@ -574,7 +607,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
             for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
             if (tid == 0 && !stop) {
               if (summary) st_short++;
-              else { st_partial++; st_rows += (u64)pc; if (WEAK) st_scan += g.wc_roff[r + 1] - g.wc_roff[r]; }
+              else { st_partial++; (void)pc; if (WEAK) st_scan += g.wc_roff[r + 1] - g.wc_roff[r]; }
             }
           }
           if (summary) {  // the round is the union of its rows: apply the summaries, stay in wave 0
@@ -604,7 +637,8 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       if (s_ctl[2]) break;
       // ---------- all threads: rows and weak edges of partial round r ----------
       if (s_ctl[0] < r || true) {
-        expand_rows<WS, NT>(g, r, FE, ring, dmask, my_edges);
+        expand_rows<WS, NT>(g, r, FE, ring, dmask, my_edges, shortcut ? mv.U + (size_t)r * WS : nullptr,
+                            my_rowb);
         if constexpr (WEAK) {
           const int lowmin = expand_weak<WS, NT>(g, r, q.bottom, FE, ring, depth, masks + q.mask_off, my_wedges);
           if (lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
@@ -618,6 +652,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
     my_edges += my_wedges;
     if (my_edges) atomicAdd(&s_edges[0], my_edges);
     if (my_wedges) atomicAdd(&s_edges[1], my_wedges);
+    if (my_rowb) atomicAdd(&s_edges[2], my_rowb);
     __syncthreads();
     if (tid == 0) {
       if (edges_out) edges_out[qi] = s_edges[0];
@@ -627,7 +662,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       if (stop_out) stop_out[qi] = s_ctl[3] ? s_ctl[4] : -1 - s_ctl[4];  // >= 0 merged there; < 0 ended at -1-x
       if (stats_out) {
         stats_out[4 * qi + 0] = st_partial;
-        stats_out[4 * qi + 1] = st_rows;
+        stats_out[4 * qi + 1] = s_edges[2];  // strong-row bytes read
         stats_out[4 * qi + 2] = st_scan;
         stats_out[4 * qi + 3] = st_short;
       }
@@ -889,7 +924,8 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
         if (tid < WS) expand_summary<WS, true>(mv, cur, r, 0, ring, dmask);
         if (tid == 0) e = mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
       } else {
-        expand_rows<WS, NT>(g, r, FE, ring, dmask, e);
+        u64 rb = 0;
+        expand_rows<WS, NT>(g, r, FE, ring, dmask, e, mv.U + (size_t)r * WS, rb);
         expand_weak<WS, NT>(g, r, 0, FE, ring, depth, K, we);
       }
       e += we;

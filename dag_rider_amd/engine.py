@@ -198,7 +198,7 @@ def _replay_result(o, keep, ids_cap: int = 0) -> ReplayResult:
                         o.commit_edges, o.chain_edges, o.deliver_edges,
                         dict(commit=o.ms_commit, chain=o.ms_chain, deliver=o.ms_deliver, emit=o.ms_emit,
                              summary=o.ms_summary),
-                        dict(count=o.sweep_count, partial=o.sweep_partial, rows=o.sweep_rows,
+                        dict(count=o.sweep_count, partial=o.sweep_partial, row_bytes=o.sweep_row_bytes,
                              weak_scanned=o.sweep_weak_scanned, shortcut=o.sweep_shortcut,
                              canon_segments=o.canon_segments))
 

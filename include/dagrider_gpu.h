@@ -158,9 +158,10 @@ typedef struct {
   float ms_commit, ms_chain, ms_deliver, ms_emit, ms_summary;
   int32_t canon_segments; /* partial-round segments of the canonical cone (-1: summaries off) */
   /* work done by the delivery sweeps (identical leaders share one sweep):
-   * sweeps, rounds expanded from rows (+ weak lists), rows read there, weak
-   * edges scanned there, rounds expanded from the round summaries */
-  uint64_t sweep_count, sweep_partial, sweep_rows, sweep_weak_scanned, sweep_shortcut;
+   * sweeps, rounds expanded from rows (+ weak columns), strong-row bytes read
+   * there (rows, plus 2-B degrees of rows skipped once the OR saturated), weak
+   * columns scanned there, rounds expanded from the round summaries */
+  uint64_t sweep_count, sweep_partial, sweep_row_bytes, sweep_weak_scanned, sweep_shortcut;
 } dr_replay_out;
 
 int dr_replay(dr_ctx *ctx, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o);
