@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libdagrider_gpu.so")
 DR_OK, DR_E_INVAL, DR_E_CAPACITY, DR_E_HIP, DR_E_RCCL, DR_E_CONTRACT, DR_E_STATE = 0, -1, -2, -3, -4, -5, -6
 DR_CHAIN_LITERAL, DR_CHAIN_PERSISTENT = 0, 1
 DR_DELIVER_REF, DR_DELIVER_PAPER = 0, 1
+DR_WEAK_LITERAL, DR_WEAK_PAPER = 0, 1
 DR_OPT_MEMO = 1
 DR_OPT_DEVICE_PLAN = 2
 DR_SHARD_ID_BYTES = 128
@@ -50,6 +51,7 @@ SIGNATURES = {
     "dr_path_batch": (C.c_int, [P, C.c_int, P, P, C.c_int, P]),
     "dr_reach_sets": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dr_wave_commit": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "dr_set_weak_edges": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dr_wave_ready": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, C.POINTER(C.c_int)]),
     "dr_order_vertices": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, C.c_size_t,
                                     C.POINTER(C.c_size_t), P, P]),

@@ -85,6 +85,7 @@ struct dr_ctx {
   DevBuf wc_key, wc_rows, wc_roff;
   size_t nwc = 0;
   DevBuf sdeg;  // [max_rounds][n] u16 strong degree per vertex (kernels.hpp expand_rows)
+  DevBuf setweak;  // dr_set_weak_edges scratch
   std::vector<uint32_t> h_wc_roff{0};
   // host mirrors
   std::vector<uint32_t> h_slot_off{0};
@@ -566,7 +567,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena,
-                    &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg};
+                    &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1113,6 +1114,20 @@ hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
     case 4: return launch_sv<WS, 0, 512>(c, T);
     case 5: return launch_sv<WS, 0, 256>(c, T);
     case 9: return launch_sv<WS, dr::SV_NO_WEAK, 256>(c, T);
+    case 11: case 12: {  // software-pipelined rows + commit (11: __syncthreads, 12: bare s_barrier)
+      constexpr int NT = summary_block<WS>();
+      const dr::MemoView mv = c->memo_view();
+      (void)mv;
+      if (variant == 11)
+        hipLaunchKernelGGL((dr::k_summary_rows<WS, NT, 0>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T,
+                           T / 4, 2 * c->f + 1, c->U.as<u64>(), c->SD.as<u64>(), c->commit.as<uint8_t>(),
+                           c->vcount.as<int32_t>());
+      else
+        hipLaunchKernelGGL((dr::k_summary_rows<WS, NT, 1>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T,
+                           T / 4, 2 * c->f + 1, c->U.as<u64>(), c->SD.as<u64>(), c->commit.as<uint8_t>(),
+                           c->vcount.as<int32_t>());
+      return hipGetLastError();
+    }
     case 10: return launch_sv<WS, dr::SV_NO_WEAK, 1024>(c, T);
     case 6: case 7: case 8: {  // split: rows + commit beside k_weak_union (6: two streams, 7: one, 8: weak alone)
       hipError_t e = hipSuccess;
@@ -1516,6 +1531,84 @@ int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pco
 }
 
 }  // namespace
+
+namespace {
+template <int WS>
+hipError_t launch_set_weak_t(dr_ctx *c, int r0, const u64 *srow, u64 *out, u64 *far) {
+  constexpr int NT = sweep_block<WS>();
+  const int dl = c->depth_log2();
+  const size_t lds = c->sweep_lds(dl);
+  hipError_t e = hipFuncSetAttribute((const void *)dr::k_set_weak<WS, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_set_weak<WS, NT>), dim3(1), dim3(NT), lds, c->stream, c->view(), r0, dl, srow, out, far);
+  return hipGetLastError();
+}
+hipError_t launch_set_weak(dr_ctx *c, int r0, const u64 *srow, u64 *out, u64 *far) {
+  switch (c->WS) {
+    case 1: return launch_set_weak_t<1>(c, r0, srow, out, far);
+    case 2: return launch_set_weak_t<2>(c, r0, srow, out, far);
+    case 4: return launch_set_weak_t<4>(c, r0, srow, out, far);
+    case 8: return launch_set_weak_t<8>(c, r0, srow, out, far);
+    case 16: return launch_set_weak_t<16>(c, r0, srow, out, far);
+    case 32: return launch_set_weak_t<32>(c, r0, srow, out, far);
+  }
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
+extern "C" int dr_set_weak_edges(dr_ctx *c, int round, int nstrong, const int32_t *strong_ids, int mode,
+                                 int32_t *out_ids, size_t cap, size_t *out_n) {
+  if (!c) return DR_E_INVAL;
+  if (out_n) *out_n = 0;
+  if (round < 1 || round > c->nrounds)
+    return c->fail(DR_E_INVAL, "setWeakEdges: round %d outside [1, %d] (Go: index out of range)", round, c->nrounds);
+  if (mode != DR_WEAK_LITERAL && mode != DR_WEAK_PAPER) return c->fail(DR_E_INVAL, "unknown mode %d", mode);
+  if (nstrong < 0 || (nstrong > 0 && !strong_ids)) return c->fail(DR_E_INVAL, "bad strong edge array");
+  if (int rc = set_device(c)) return rc;
+  const int WS = c->WS;
+  std::vector<u64> srow(WS, 0);
+  for (int i = 0; i < nstrong; i++) {
+    const int tr = strong_ids[2 * i], ts = strong_ids[2 * i + 1];
+    if (tr != round - 1 || ts < 1 || ts > c->n)
+      return c->fail(DR_E_CONTRACT, "strong edge %d -> (%d,%d) must target (round-1, 1..n)", i, tr, ts);
+    srow[(ts - 1) >> 6] |= 1ULL << ((ts - 1) & 63);
+  }
+  const int lo = 1, hi = round - 2;  // process.go:304: r = round-2 down to 1
+  std::vector<u64> add;
+  if (mode == DR_WEAK_PAPER && hi >= lo) {
+    const size_t rows = (size_t)round + 1;
+    HIPCHK(c, c->setweak.ensure((WS + 2 * rows * WS) * 8));
+    u64 *d_srow = c->setweak.as<u64>(), *d_out = d_srow + WS, *d_far = d_out + rows * WS;
+    HIPCHK(c, hipMemsetAsync(d_out, 0, 2 * rows * WS * 8, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d_srow, srow.data(), WS * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_set_weak(c, round, d_srow, d_out, d_far));
+    add.resize(rows * WS);
+    HIPCHK(c, hipMemcpyAsync(add.data(), d_out, rows * WS * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  // emission in the reference's order: rounds hi..lo, slots in insertion order
+  size_t k = 0;
+  bool ghost_edge = false;  // paper: once v has a weak edge to {0,0}, path(v, {0,0}) holds
+  for (int r = hi; r >= lo; r--) {
+    for (uint32_t sl = c->h_slot_off[r]; sl < c->h_slot_off[r + 1]; sl++) {
+      const int s = c->h_slot_src[sl];
+      bool take;
+      if (mode == DR_WEAK_LITERAL) take = s != 0;  // v.id == {0,0}: path() reaches nothing but itself
+      else if (s == 0) { take = !ghost_edge; ghost_edge = true; }  // no DAG edge targets {0,0}
+      else take = (add[(size_t)r * WS + ((s - 1) >> 6)] >> ((s - 1) & 63)) & 1ULL;
+      if (!take) continue;
+      if (out_ids && k < cap) {
+        out_ids[2 * k] = s == 0 ? 0 : r;
+        out_ids[2 * k + 1] = s;
+      }
+      k++;
+    }
+  }
+  if (out_n) *out_n = k;
+  if (k > cap && out_ids) return c->fail(DR_E_CAPACITY, "setWeakEdges: %zu ids, capacity %zu", k, cap);
+  return DR_OK;
+}
 
 extern "C" int dr_wave_commit(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount) {
   if (!c) return DR_E_INVAL;

@@ -132,6 +132,20 @@ class Engine:
             o += k
         return res
 
+    # ---- setWeakEdges (process.go:298-310) ----
+    def set_weak_edges(self, round_: int, strong: Sequence[Tuple[int, int]], mode: int = L.DR_WEAK_PAPER,
+                       cap: Optional[int] = None) -> np.ndarray:
+        """The weak edges of a vertex of round `round_` with these strong edges, in the
+        reference's order (rounds round-2 .. 1, slot order); ids as an [k, 2] int32 array."""
+        ns = len(strong)
+        st = np.asarray(strong if ns else [(0, 0)], dtype=np.int32).reshape(-1)
+        out_n = C.c_size_t()
+        self._check(self._L.dr_set_weak_edges(self._h, round_, ns, L.ptr(st), mode, None, 0, C.byref(out_n)))
+        k = out_n.value
+        ids = np.zeros(max(k, 1) * 2, np.int32)
+        self._check(self._L.dr_set_weak_edges(self._h, round_, ns, L.ptr(st), mode, L.ptr(ids), k, C.byref(out_n)))
+        return ids[:2 * k].reshape(-1, 2)
+
     # ---- waveReady (process.go:314-354) ----
     def wave_commit(self, w0: int, w1: int):
         nw = w1 - w0 + 1

@@ -46,6 +46,7 @@ enum {
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
 enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
+enum { DR_WEAK_LITERAL = 0, DR_WEAK_PAPER = 1 };
 
 typedef struct dr_ctx dr_ctx;
 
@@ -105,6 +106,23 @@ int dr_path_batch(dr_ctx *ctx, int q, const int32_t *from, const int32_t *to, in
  * bottom_i, concatenated over queries (words_needed written to *out_words). */
 int dr_reach_sets(dr_ctx *ctx, int q, const int32_t *from, const int32_t *bottom, int strong_only,
                   uint64_t *out, size_t cap_words, size_t *out_words);
+
+/* setWeakEdges(v, round) (process.go:298-310) for a vertex v of round `round`
+ * (1 <= round <= dr_num_rounds: v may belong to the next, not yet appended
+ * round) whose strong edges are strong_ids (nstrong ids (round-1, t)).  Writes,
+ * in the reference's order -- rounds round-2 down to 1, slots in insertion
+ * order -- the ids that become v's weak edges:
+ *   DR_WEAK_LITERAL  the code as written: v.id is still {0,0} when it runs
+ *                    (SURVEY.md App. A Q5), so path() reaches nothing and
+ *                    every slot except the zero id becomes a weak edge;
+ *   DR_WEAK_PAPER    Alg. 2 lines 29-31: u is added iff no path from v, over
+ *                    v's strong edges and the weak edges added so far, reaches
+ *                    u (no DAG edge targets a ghost slot {0,0}: the first one
+ *                    becomes a weak edge, which then reaches the others).
+ * out_ids (may be NULL): 2 int32 per id, up to cap; *out_n = total (an
+ * undersized out_ids gives DR_E_CAPACITY with *out_n set). */
+int dr_set_weak_edges(dr_ctx *ctx, int round, int nstrong, const int32_t *strong_ids, int mode,
+                      int32_t *out_ids, size_t cap, size_t *out_n);
 
 /* The commit decision of waveReady (process.go:326-339) for waves w0..w1:
  * commit[i] = leader exists && vcount >= 2f+1; vcount[i] = number of slots of

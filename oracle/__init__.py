@@ -10,3 +10,4 @@ of :86-283) plus SURVEY.md s4's hand-derived answers, both committed in
 tests/golden/figure1.json.
 """
 from .pyoracle import *  # noqa: F401,F403
+from . import setweak  # noqa: F401,E402  (setWeakEdges, process.go:298-310)
