@@ -250,7 +250,7 @@ def run_c5(args, rank: int, world: int, local: int, dist):
         e = Engine(cfg.n, cfg.faulty, d.nrounds, local)
         e.append_packed(d)
         engines.append(e)
-        dag_bytes += d.nrounds * cfg.n * d.W * 8 + int(d.weak_off[-1]) * 4
+        dag_bytes += d.nrounds * cfg.n * d.W * 8 + weak_columns(d) * (4 + d.W * 8)
     log(f"[rank {rank}] C5 DAGs {lo}..{hi - 1} loaded in {time.perf_counter() - t0:.1f} s")
     nw = c5_config(0).nwaves
     b = ReplayBatch(engines, nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
@@ -293,7 +293,7 @@ def run_c5(args, rank: int, world: int, local: int, dist):
                      "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic("batch"),
                      "kernel": "k_replay_small (one wavefront per DAG)",
                      "bytes_per_launch": dag_bytes, "ms_per_launch": kms,
-                     "note": "unique DAG bytes (strong rows + weak edges) once per launch"},
+                     "note": "unique DAG bytes (strong rows + weak columns) once per launch"},
         "cpu_baseline": None,
         "detail": {"edges_per_step": edges, "commits": int(sum(int(r.commit.sum()) for r in res)),
                    "pops": int(sum(len(r.pop_count) for r in res))},

@@ -13,8 +13,10 @@
 //      set of leader waves whose cone contains v: Qs (strong edges only, the
 //      chains' strong_path) and Qf (strong + weak, orderVertices' path(.., false)).
 //      Strong: lane u of round r-1 ORs Q(v) of every v of round r whose row has
-//      bit u (rows broadcast by readlane).  Weak: LDS atomics into a ring of
-//      pending rounds.  Q and degrees go to a per-DAG scratch.
+//      bit u (rows broadcast by readlane).  Weak: per weak column (one distinct
+//      weak target of the round), the wave-OR of Qf over the column's sources
+//      goes into a ring of pending rounds (one LDS atomic per column).  Q and
+//      degrees go to a per-DAG scratch.
 //   3. chains (process.go:341-350) from the leaders' Qs: wave w' is pushed
 //      after leader L iff L's bit is in Qs(leader(w')); pops = reverse pushes.
 //   4. bottom-up emission, lane b = leader wave b+1: for each round's slots in
@@ -32,8 +34,10 @@ namespace dr {
 struct SmallJob {
   const u64 *strong;
   const u64 *present;
-  const uint32_t *weak;
-  const uint32_t *weak_roff;
+  const uint32_t *wc_key;   // weak columns (kernels.hpp DagView::wc_*)
+  const u64 *wc_rows;
+  const uint32_t *wc_roff;
+  const uint16_t *wdeg;     // [rounds][n] weak degree per vertex
   const uint32_t *slot_off;
   const uint16_t *slot_src;
   // scratch, rounds 0..T: Qf, Qs, (deg << 16 | strong deg)
@@ -61,7 +65,6 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   __shared__ u64 ring[DEPTH * 128];
   __shared__ u64 QF[128], QS[128];
   __shared__ uint32_t DG[128];
-  __shared__ uint32_t wcnt[128];
   __shared__ u64 QL[64];
   __shared__ int32_t vc_s[64];
   __shared__ int8_t coef[64 * 65];
@@ -154,17 +157,20 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
     row(r, lane + 64, ra[1], rb[1]);
     QF[lane] = qf[0];
     QF[lane + 64] = qf[1];
-    wcnt[lane] = 0;
-    wcnt[lane + 64] = 0;
     __syncthreads();
-    // weak edges of round r: degree per source, Qf into the pending rounds
-    const uint32_t e0 = J.weak_roff[r], e1 = J.weak_roff[r + 1];
-    for (uint32_t e = e0 + lane; e < e1; e += 64) {
-      const uint32_t x = J.weak[e];
-      const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
-      atomicAdd(&wcnt[own], 1u);
-      const u64 f = QF[own];
-      if (f && r - delta >= 1) atomicOr(&ring[((r - delta) & DM) * 128 + ts], f);
+    // weak columns of round r: Qf of the column's sources into the pending round
+    {
+      const uint32_t c0 = J.wc_roff[r], c1 = J.wc_roff[r + 1];
+      const int WSJ = J.WS;
+      for (uint32_t jc = c0; jc < c1; jc++) {  // wave-uniform
+        const uint32_t key = J.wc_key[jc];
+        const u64 w0 = J.wc_rows[(size_t)jc * WSJ], w1 = WSJ > 1 ? J.wc_rows[(size_t)jc * WSJ + 1] : 0ULL;
+        u64 v = ((w0 >> lane) & 1ULL) ? qf[0] : 0ULL;
+        v |= ((w1 >> lane) & 1ULL) ? qf[1] : 0ULL;
+        v = wave_or(v);
+        const int delta = (int)(key >> 11), ts = (int)(key & 2047u);
+        if (lane == 0 && v && r - delta >= 1) atomicOr(&ring[((r - delta) & DM) * 128 + ts], v);
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -175,7 +181,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
         const size_t at = (size_t)r * n + v;
         J.qf[at] = qf[i];
         J.qs[at] = qs[i];
-        J.deg[at] = ((sd + wcnt[v]) << 16) | sd;
+        J.deg[at] = ((sd + J.wdeg[at]) << 16) | sd;
       }
     }
     // strong edges: Q of round r-1, lane u owns targets u and u+64

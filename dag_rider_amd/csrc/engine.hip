@@ -86,6 +86,7 @@ struct dr_ctx {
   size_t nwc = 0;
   DevBuf sdeg;  // [max_rounds][n] u16 strong degree per vertex (kernels.hpp expand_rows)
   DevBuf setweak;  // dr_set_weak_edges scratch
+  DevBuf wdeg;     // [max_rounds][n] u16 weak degree per vertex (batch.hpp)
   std::vector<uint32_t> h_wc_roff{0};
   // host mirrors
   std::vector<uint32_t> h_slot_off{0};
@@ -541,6 +542,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
       c->wc_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->wc_key.ensure(4096) != hipSuccess || c->wc_rows.ensure(4096) != hipSuccess ||
       c->sdeg.ensure((size_t)max_rounds * n * sizeof(uint16_t)) != hipSuccess ||
+      c->wdeg.ensure((size_t)max_rounds * n * sizeof(uint16_t)) != hipSuccess ||
       c->slot_src.ensure(4096) != hipSuccess) {
     g_create_err = "dr_create: device allocation failed";
     dr_destroy(c);
@@ -568,7 +570,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena,
-                    &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak};
+                    &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -600,7 +602,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   const int n = c->n, W = c->W, WS = c->WS;
   std::vector<u64> pres((size_t)k * WS, 0);
   std::vector<uint64_t> deg(k, 0);
-  std::vector<uint16_t> vdeg((size_t)k * n, 0);
+  std::vector<uint16_t> vdeg((size_t)k * n, 0), vwdeg((size_t)k * n, 0);
   std::vector<uint32_t> wdev, wroff(k);
   std::vector<u64> fdev;
   std::vector<uint32_t> froff(k);
@@ -634,6 +636,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
       const uint32_t ea = weak_off[(size_t)i * n + s0], eb = weak_off[(size_t)i * n + s0 + 1];
       if (eb < ea) return c->fail(DR_E_INVAL, "weak_off not monotone at round %d", r);
       if (eb > ea && !here) return c->fail(DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1);
+      vwdeg[(size_t)i * n + s0] = (uint16_t)std::min<uint32_t>(eb - ea, 65535u);
       for (uint32_t e = ea; e < eb; e++) {
         const uint32_t t = weak_tgt[e];
         const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
@@ -706,6 +709,8 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   HIPCHK(c, hipMemcpyAsync(c->present.as<u64>() + (size_t)r0 * WS, pres.data(), pres.size() * 8,
                            hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->sdeg.as<uint16_t>() + (size_t)r0 * n, vdeg.data(), vdeg.size() * 2,
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->wdeg.as<uint16_t>() + (size_t)r0 * n, vwdeg.data(), vwdeg.size() * 2,
                            hipMemcpyHostToDevice, c->stream));
   // slots
   const size_t old_slots = c->h_slot_src.size();
@@ -2030,8 +2035,10 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
       dr::SmallJob &J = jobs[i];
       J.strong = c->strong.as<u64>();
       J.present = c->present.as<u64>();
-      J.weak = c->weak.as<uint32_t>();
-      J.weak_roff = c->weak_roff.as<uint32_t>();
+      J.wc_key = c->wc_key.as<uint32_t>();
+      J.wc_rows = c->wc_rows.as<u64>();
+      J.wc_roff = c->wc_roff.as<uint32_t>();
+      J.wdeg = c->wdeg.as<uint16_t>();
       J.slot_off = c->slot_off.as<uint32_t>();
       J.slot_src = c->slot_src.as<uint16_t>();
       J.n = c->n;
