@@ -1120,6 +1120,9 @@ hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
     case 4: return launch_sv<WS, 0, 512>(c, T);
     case 5: return launch_sv<WS, 0, 256>(c, T);
     case 9: return launch_sv<WS, dr::SV_NO_WEAK, 256>(c, T);
+    case 13: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_GRP16>(c, T);
+    case 14: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_TEMPORAL>(c, T);
+    case 15: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_GRP16, 1024>(c, T);
     case 11: case 12: {  // software-pipelined rows + commit (11: __syncthreads, 12: bare s_barrier)
       constexpr int NT = summary_block<WS>();
       const dr::MemoView mv = c->memo_view();

@@ -679,7 +679,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
 // wave's rounds 2..4, S_k = {v : row(v) & S_{k-1} != 0} by ballot; vcount = |S_3|
 // (process.go:326-339).  Waves past nwc get summaries only.
 // ---------------------------------------------------------------------------
-enum : int { SV_NO_WEAK = 1, SV_NO_ROWS = 2, SV_UNR8 = 4 };  // tuning variants (dr_profile_kernel)
+enum : int { SV_NO_WEAK = 1, SV_NO_ROWS = 2, SV_UNR8 = 4, SV_GRP16 = 8, SV_TEMPORAL = 16 };  // tuning variants (dr_profile_kernel)
 
 template <int WS, int NT, int SV = 0>
 __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc, int dd, int quorum,
@@ -688,7 +688,8 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
                                                        int32_t *__restrict__ vcount) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
-  constexpr int GRP = CPT < 8 ? CPT : 8;  // row chunks in flight per thread
+  constexpr int GMAX = (SV & SV_GRP16) ? 16 : 8;
+  constexpr int GRP = CPT < GMAX ? CPT : GMAX;  // row chunks in flight per thread
   __shared__ u64 sU[WS];
   __shared__ u64 sWU[16 * WS];
   __shared__ u64 S[WS], Tn[WS], P[WS];
@@ -728,11 +729,12 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
         v1[p] = 0;
         if (s < n) {
           if constexpr (CW == 2) {
-            const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j));
+            const u64x2 *src = reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j);
+            const u64x2 x = (SV & SV_TEMPORAL) ? *src : __builtin_nontemporal_load(src);
             v0[p] = x.x;
             v1[p] = x.y;
           } else {
-            v0[p] = __builtin_nontemporal_load(rows + s);
+            v0[p] = (SV & SV_TEMPORAL) ? rows[s] : __builtin_nontemporal_load(rows + s);
           }
         }
       }
