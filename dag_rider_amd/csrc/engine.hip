@@ -1123,21 +1123,6 @@ hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
     case 13: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_GRP16>(c, T);
     case 14: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_TEMPORAL>(c, T);
     case 15: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_GRP16, 1024>(c, T);
-    case 11: case 12: {  // software-pipelined rows + commit (11: __syncthreads, 12: bare s_barrier)
-      constexpr int NT = summary_block<WS>();
-      const dr::MemoView mv = c->memo_view();
-      (void)mv;
-      if (variant == 11)
-        hipLaunchKernelGGL((dr::k_summary_rows<WS, NT, 0>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T,
-                           T / 4, 2 * c->f + 1, c->U.as<u64>(), c->SD.as<u64>(), c->commit.as<uint8_t>(),
-                           c->vcount.as<int32_t>());
-      else
-        hipLaunchKernelGGL((dr::k_summary_rows<WS, NT, 1>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T,
-                           T / 4, 2 * c->f + 1, c->U.as<u64>(), c->SD.as<u64>(), c->commit.as<uint8_t>(),
-                           c->vcount.as<int32_t>());
-      return hipGetLastError();
-    }
-    case 10: return launch_sv<WS, dr::SV_NO_WEAK, 1024>(c, T);
     case 6: case 7: case 8: {  // split: rows + commit beside k_weak_union (6: two streams, 7: one, 8: weak alone)
       hipError_t e = hipSuccess;
       if (variant != 8) e = launch_sv<WS, dr::SV_NO_WEAK>(c, T);

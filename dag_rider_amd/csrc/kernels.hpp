@@ -859,138 +859,6 @@ __global__ __launch_bounds__(NT) void k_set_weak(DagView g, int r0, int depth_lo
   }
 }
 
-// k_summary_rows: k_summary_commit<SV_NO_WEAK> (rows + commit, one workgroup per
-// wave) software-pipelined across the wave's rounds: the loads of the next row
-// group -- the next round's first group included -- are issued before the
-// current group is folded, so the per-round reduction, the barriers and the S
-// update run while HBM keeps streaming.  BAR = 1 uses bare s_barrier (LDS
-// traffic ordered by explicit lgkmcnt waits) so no barrier waits on the
-// prefetched loads.
-template <int WS, int NT, int BAR>
-__global__ __launch_bounds__(NT) void k_summary_rows(DagView g, int T, int nwc, int quorum, u64 *__restrict__ U,
-                                                     u64 *__restrict__ SD, uint8_t *__restrict__ commit,
-                                                     int32_t *__restrict__ vcount) {
-  using G = Geo<WS, NT>;
-  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
-  constexpr int GRP = CPT < 8 ? CPT : 8;
-  constexpr int NG = (CPT + GRP - 1) / GRP;  // row groups per round
-  __shared__ u64 sU[WS];
-  __shared__ u64 S[WS], Tn[WS], P[WS];
-  __shared__ u64 sSD;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, j = tid % CPR, n = g.n;
-  const int w = blockIdx.x + 1;
-  const int r1 = 4 * (w - 1) + 1;
-  const int rl = min(T, r1 + 3);
-  const bool do_commit = w <= nwc;
-  const bool leader = do_commit && (g.present[(size_t)r1 * WS] & 1ULL);
-  auto sync = [&]() {
-    if constexpr (BAR) {
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS ops done
-      __builtin_amdgcn_s_barrier();
-    } else {
-      __syncthreads();
-    }
-  };
-  auto load = [&](int r, int gi, u64 *b0, u64 *b1) {
-    const u64 *rows = g.strong + (size_t)r * n * WS;
-#pragma unroll
-    for (int p = 0; p < GRP; p++) {
-      const int s = tid / CPR + (gi * GRP + p) * RPP;
-      b0[p] = 0;
-      b1[p] = 0;
-      if (gi * GRP + p < CPT && s < n) {
-        if constexpr (CW == 2) {
-          const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j));
-          b0[p] = x.x;
-          b1[p] = x.y;
-        } else {
-          b0[p] = __builtin_nontemporal_load(rows + s);
-        }
-      }
-    }
-  };
-  if (tid < WS) { S[tid] = tid == 0 ? 1ULL : 0ULL; Tn[tid] = 0; sU[tid] = 0; }
-  if (tid == 0) sSD = 0;
-  u64 c0[GRP], c1[GRP], n0[GRP], n1[GRP];
-  load(r1, 0, c0, c1);
-  for (int r = r1; r <= rl; r++) {
-    const int k = r - r1;
-    if (tid < WS) P[tid] = g.present[(size_t)r * WS + tid];
-    sync();
-    const bool test = leader && k >= 1;
-    const u64 s0 = test ? S[j * CW] : 0ULL, s1 = (test && CW == 2) ? S[j * CW + 1] : 0ULL;
-    u64 a0 = 0, a1 = 0, deg = 0;
-#pragma unroll 1
-    for (int gi = 0; gi < NG; gi++) {
-      // next group: this round's next, or the next round's first
-      if (gi + 1 < NG) load(r, gi + 1, n0, n1);
-      else if (r < rl) load(r + 1, 0, n0, n1);
-#pragma unroll
-      for (int p = 0; p < GRP; p++) {
-        a0 |= c0[p];
-        a1 |= c1[p];
-        deg += (u64)(popc64(c0[p]) + popc64(c1[p]));
-      }
-      if (test) {
-#pragma unroll
-        for (int p = 0; p < GRP; p++) {
-          const int rowbase = (wid * 64) / CPR + (gi * GRP + p) * RPP;
-          if (gi * GRP + p >= CPT || rowbase >= n) break;  // wave-uniform
-          const int s = tid / CPR + (gi * GRP + p) * RPP;
-          const bool pres = s < n && ((P[s >> 6] >> (s & 63)) & 1ULL);
-          const bool hit = pres && ((c0[p] & s0) | (c1[p] & s1)) != 0ULL;
-          u64 m = __ballot(hit);
-          if (lane == 0 && m) {
-            u64 bits;
-            if constexpr (CPR == 1) {
-              bits = m;
-            } else {
-#pragma unroll
-              for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
-              bits = 0;
-#pragma unroll
-              for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
-            }
-            atomicOr(&Tn[rowbase >> 6], bits << (rowbase & 63));
-          }
-        }
-      }
-#pragma unroll
-      for (int p = 0; p < GRP; p++) { c0[p] = n0[p]; c1[p] = n1[p]; }
-    }
-    if constexpr (CPR < 16) {
-      a0 = row_or_stride<CPR>(a0);
-      if constexpr (CW == 2) a1 = row_or_stride<CPR>(a1);
-    }
-    deg = wave_sum(deg);
-    if ((lane & 15) < CPR) {
-      if (a0) atomicOr(&sU[(lane & 15) * CW], a0);
-      if (CW == 2 && a1) atomicOr(&sU[(lane & 15) * CW + 1], a1);
-    }
-    if (lane == 0 && deg) atomicAdd(&sSD, deg);
-    sync();
-    if (tid < WS) {
-      U[(size_t)r * WS + tid] = sU[tid];
-      sU[tid] = 0;
-      if (test) { S[tid] = Tn[tid]; Tn[tid] = 0; }
-    }
-    if (tid == 0) { SD[r] = sSD; sSD = 0; }
-  }
-  sync();
-  if (do_commit && tid == 0) {
-    if (!leader) {  // leader is bottom (process.go:327-329)
-      commit[w - 1] = 0;
-      vcount[w - 1] = -1;
-    } else {
-      int vc = 0;
-#pragma unroll
-      for (int i = 0; i < WS; i++) vc += popc64(S[i]);
-      vcount[w - 1] = vc;
-      commit[w - 1] = vc >= quorum ? 1 : 0;
-    }
-  }
-}
-
 // WU_r[delta] = the union of round r's weak targets at distance delta, one
 // workgroup per round (the weak half of k_summary_commit as a separate stream:
 // it runs beside the rows + commit pass, k_summary_commit<SV_NO_WEAK>).

@@ -19,7 +19,6 @@ cases = [("summary_commit shipped", 0, 0, rows_b + weak_b), ("rows only", 0, 1, 
          ("summary_commit NT=256", 0, 5, rows_b + weak_b),
          ("split 2 streams", 0, 6, rows_b + weak_b), ("split 1 stream", 0, 7, rows_b + weak_b),
          ("weak_union alone", 0, 8, weak_b), ("rows only NT=256", 0, 9, rows_b), ("rows only NT=1024", 0, 10, rows_b),
-         ("rows pipelined", 0, 11, rows_b), ("rows pipelined s_barrier", 0, 12, rows_b),
          ("rows GRP16", 0, 13, rows_b), ("rows temporal loads", 0, 14, rows_b), ("rows GRP16 NT=1024", 0, 15, rows_b), ("summary phase (all)", 2, 0, rows_b + weak_b)]
 res = {name: [] for name, *_ in cases}
 for rep in range(5):
