@@ -58,9 +58,10 @@ struct SmallJob {
 
 constexpr int kSmallMaxPops = 64 * 65 / 2;  // literal chains: wave w pushes up to w leaders
 
-template <int DEPTH>
+template <int DEPTH, bool PAPER>
 __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict__ jobs, int njobs, int nw,
-                                                     int chain_persistent, int paper) {
+                                                     int chain_persistent) {
+  constexpr bool paper = PAPER;  // REF mode skips the paper-mode digests entirely
   constexpr int DM = DEPTH - 1;
   __shared__ u64 ring[DEPTH * 128];
   __shared__ u64 QF[128], QS[128];
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
           dr_ += digest_term((uint32_t)r, (uint32_t)s, kr);
           kr++;
           er += full;
-          if (!(f & before)) {
+          if (PAPER && !(f & before)) {
             dp += digest_term((uint32_t)r, (uint32_t)s, kp);
             kp++;
             ep += full;

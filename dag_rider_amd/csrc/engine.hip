@@ -1942,7 +1942,8 @@ bool small_ok(const dr_ctx *c, int nwaves) {
 
 template <int DEPTH>
 hipError_t launch_small(hipStream_t s, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper) {
-  hipLaunchKernelGGL((dr::k_replay_small<DEPTH>), dim3(nj), dim3(64), 0, s, jobs, nj, nw, persistent, paper);
+  if (paper) hipLaunchKernelGGL((dr::k_replay_small<DEPTH, true>), dim3(nj), dim3(64), 0, s, jobs, nj, nw, persistent);
+  else hipLaunchKernelGGL((dr::k_replay_small<DEPTH, false>), dim3(nj), dim3(64), 0, s, jobs, nj, nw, persistent);
   return hipGetLastError();
 }
 }  // namespace
