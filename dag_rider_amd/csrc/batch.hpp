@@ -63,17 +63,24 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
                                                      int chain_persistent) {
   constexpr bool paper = PAPER;  // REF mode skips the paper-mode digests entirely
   constexpr int DM = DEPTH - 1;
-  __shared__ u64 ring[DEPTH * 128];
+  // LDS is what limits DAGs per CU: the weak ring (phase 2 only) shares its
+  // bytes with the chain coefficients, pop list and per-leader results (phases
+  // 3-5, which start after phase 2's last barrier).
+  constexpr int kCoefB = 64 * 65, kPopB = (kSmallMaxPops + 255) & ~255, kResB = 64 * 6 * 8;
+  constexpr int kLateB = kCoefB + kPopB + kResB;
+  constexpr int kArenaB = DEPTH * 128 * 8 > kLateB ? DEPTH * 128 * 8 : kLateB;
+  __shared__ __attribute__((aligned(16))) u64 arena[(kArenaB + 7) / 8];
+  u64 *ring = arena;                                                            // [DEPTH * 128], phase 2
+  int8_t *coef = reinterpret_cast<int8_t *>(arena);                             // [64 * 65], phases 3-4
+  uint8_t *pop_lead = reinterpret_cast<uint8_t *>(arena) + kCoefB;              // [kSmallMaxPops], 3-5
+  u64 *res = reinterpret_cast<u64 *>(reinterpret_cast<char *>(arena) + ((kCoefB + kPopB + 7) & ~7));  // 4-5
   __shared__ u64 QF[128], QS[128];
   __shared__ uint32_t DG[128];
   __shared__ u64 QL[64];
   __shared__ int32_t vc_s[64];
-  __shared__ int8_t coef[64 * 65];
-  __shared__ uint8_t pop_lead[kSmallMaxPops];
   __shared__ int16_t first_pop[64];
   __shared__ int8_t lst[64];
   __shared__ uint16_t SL[128];
-  __shared__ u64 res[64 * 6];  // per leader: REF count, digest, edges; PAPER count, digest, edges
   const int lane = threadIdx.x;
   const int jb = blockIdx.x;
   if (jb >= njobs) return;
