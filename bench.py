@@ -33,7 +33,7 @@ TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "traffic.json")
 # replay phase -> the kernels it launches (names as rocprofv3 reports them)
 PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 512, 1>", "dr::k_weak_union<16, 256>"],
                  "sweep": ["dr::k_sweep<16, 256, 9>"],
-                 "batch": ["dr::k_replay_small<8, false>"]}
+                 "batch": ["dr::k_replay_small<8, false, true>"]}
 
 
 def measured_traffic(phase):

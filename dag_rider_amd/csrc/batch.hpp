@@ -58,19 +58,34 @@ struct SmallJob {
 
 constexpr int kSmallMaxPops = 64 * 65 / 2;  // literal chains: wave w pushes up to w leaders
 
-template <int DEPTH, bool PAPER>
-__global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict__ jobs, int njobs, int nw,
-                                                     int chain_persistent) {
+// dynamic LDS of k_replay_small: the weak ring (rsl slots of 128 u64) or the
+// later phases' arrays, whichever is larger
+template <bool PAPER, bool PERSIST>
+constexpr int small_late_bytes() {
+  return 64 * 65 + (((PERSIST ? 64 : kSmallMaxPops) + 255) & ~255) + 64 * (PAPER ? 6 : 3) * 8;
+}
+template <bool PAPER, bool PERSIST>
+inline size_t small_lds_bytes(int rsl) {
+  const size_t ring = (size_t)rsl * 128 * 8, late = (size_t)small_late_bytes<PAPER, PERSIST>();
+  return ring > late ? ring : late;
+}
+
+// rsl = ring slots = largest weak delta + 1 (round x's slot is reused by round
+// x + rsl, which is drained before any contribution to x arrives)
+template <int DEPTH, bool PAPER, bool PERSIST>
+__global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict__ jobs, int njobs, int nw, int rsl) {
   constexpr bool paper = PAPER;  // REF mode skips the paper-mode digests entirely
-  constexpr int DM = DEPTH - 1;
+  constexpr bool chain_persistent = PERSIST;  // persistent chains push every wave at most once: <= 64 pops
   // LDS is what limits DAGs per CU: the weak ring (phase 2 only) shares its
   // bytes with the chain coefficients, pop list and per-leader results (phases
   // 3-5, which start after phase 2's last barrier).
-  constexpr int kCoefB = 64 * 65, kPopB = (kSmallMaxPops + 255) & ~255, kResB = 64 * 6 * 8;
-  constexpr int kLateB = kCoefB + kPopB + kResB;
-  constexpr int kArenaB = DEPTH * 128 * 8 > kLateB ? DEPTH * 128 * 8 : kLateB;
-  __shared__ __attribute__((aligned(16))) u64 arena[(kArenaB + 7) / 8];
-  u64 *ring = arena;                                                            // [DEPTH * 128], phase 2
+  constexpr int kMaxPops = PERSIST ? 64 : kSmallMaxPops;
+  constexpr int RS = PAPER ? 6 : 3;  // per-leader results kept
+  constexpr int kCoefB = 64 * 65, kPopB = (kMaxPops + 255) & ~255, kResB = 64 * RS * 8;
+  static_assert(kCoefB + kPopB + kResB == small_late_bytes<PAPER, PERSIST>(), "LDS layout");
+  (void)kResB;
+  extern __shared__ __attribute__((aligned(16))) u64 arena[];                  // small_lds_bytes(rsl)
+  u64 *ring = arena;                                                            // [rsl * 128], phase 2
   int8_t *coef = reinterpret_cast<int8_t *>(arena);                             // [64 * 65], phases 3-4
   uint8_t *pop_lead = reinterpret_cast<uint8_t *>(arena) + kCoefB;              // [kSmallMaxPops], 3-5
   u64 *res = reinterpret_cast<u64 *>(reinterpret_cast<char *>(arena) + ((kCoefB + kPopB + 7) & ~7));  // 4-5
@@ -138,15 +153,15 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   }
 
   // ---------------- 2. top-down Q pass ----------------
-  for (int i = lane; i < DEPTH * 128; i += 64) ring[i] = 0;
+  for (int i = lane; i < rsl * 128; i += 64) ring[i] = 0;
   u64 qf[2] = {0, 0}, qs[2] = {0, 0};
   __syncthreads();
   for (int r = T; r >= 1; r--) {
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
-      qf[i] |= ring[(r & DM) * 128 + v];
-      ring[(r & DM) * 128 + v] = 0;
+      qf[i] |= ring[(r % rsl) * 128 + v];
+      ring[(r % rsl) * 128 + v] = 0;
     }
     if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its bit at source 1
       const int w = (r - 1) / 4 + 1;
@@ -177,7 +192,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
         v |= ((w1 >> lane) & 1ULL) ? qf[1] : 0ULL;
         v = wave_or(v);
         const int delta = (int)(key >> 11), ts = (int)(key & 2047u);
-        if (lane == 0 && v && r - delta >= 1) atomicOr(&ring[((r - delta) & DM) * 128 + ts], v);
+        if (lane == 0 && v && r - delta >= 1) atomicOr(&ring[((r - delta) % rsl) * 128 + ts], v);
       }
     }
     __syncthreads();
@@ -314,25 +329,27 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
       if (c) chain += (u64)(int64_t)c * cs;
     }
   }
-  res[b * 6 + 0] = kr;
-  res[b * 6 + 1] = dr_;
-  res[b * 6 + 2] = er;
-  res[b * 6 + 3] = kp;
-  res[b * 6 + 4] = dp;
-  res[b * 6 + 5] = ep;
+  res[b * RS + 0] = kr;
+  res[b * RS + 1] = dr_;
+  res[b * RS + 2] = er;
+  if (PAPER) {
+    res[b * RS + 3] = kp;
+    res[b * RS + 4] = dp;
+    res[b * RS + 5] = ep;
+  }
   chain = wave_sum(chain);
   __syncthreads();
 
   // ---------------- 5. outputs ----------------
   u64 dsum = 0;
-  const int np = min(npop, min(J.push_cap, kSmallMaxPops));
+  const int np = min(npop, min(J.push_cap, kMaxPops));
   for (int j = lane; j < np; j += 64) {
     const int lb = pop_lead[j] - 1;
     u64 c, d, e;
     if (!paper) {
-      c = res[lb * 6 + 0]; d = res[lb * 6 + 1]; e = res[lb * 6 + 2];
+      c = res[lb * RS + 0]; d = res[lb * RS + 1]; e = res[lb * RS + 2];
     } else if (first_pop[lb] == j) {
-      c = res[lb * 6 + 3]; d = res[lb * 6 + 4]; e = res[lb * 6 + 5];
+      c = res[lb * RS + (RS - 3)]; d = res[lb * RS + (RS - 2)]; e = res[lb * RS + (RS - 1)];
     } else {
       c = 0; d = 0; e = 0;  // the leader's cone was delivered by its first pop
     }

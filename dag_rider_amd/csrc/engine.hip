@@ -1941,9 +1941,23 @@ bool small_ok(const dr_ctx *c, int nwaves) {
 }
 
 template <int DEPTH>
-hipError_t launch_small(hipStream_t s, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper) {
-  if (paper) hipLaunchKernelGGL((dr::k_replay_small<DEPTH, true>), dim3(nj), dim3(64), 0, s, jobs, nj, nw, persistent);
-  else hipLaunchKernelGGL((dr::k_replay_small<DEPTH, false>), dim3(nj), dim3(64), 0, s, jobs, nj, nw, persistent);
+hipError_t launch_small(hipStream_t s, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper,
+                        int rsl) {
+  const dim3 g(nj), b(64);
+  const size_t lds_tt = dr::small_lds_bytes<true, true>(rsl), lds_tf = dr::small_lds_bytes<true, false>(rsl);
+  const size_t lds_ft = dr::small_lds_bytes<false, true>(rsl), lds_ff = dr::small_lds_bytes<false, false>(rsl);
+  if (paper && persistent)
+    hipLaunchKernelGGL((dr::k_replay_small<DEPTH, true, true>), g, b, lds_tt, s, jobs,
+                       nj, nw, rsl);
+  else if (paper)
+    hipLaunchKernelGGL((dr::k_replay_small<DEPTH, true, false>), g, b, lds_tf, s,
+                       jobs, nj, nw, rsl);
+  else if (persistent)
+    hipLaunchKernelGGL((dr::k_replay_small<DEPTH, false, true>), g, b, lds_ft, s,
+                       jobs, nj, nw, rsl);
+  else
+    hipLaunchKernelGGL((dr::k_replay_small<DEPTH, false, false>), g, b, lds_ff, s,
+                       jobs, nj, nw, rsl);
   return hipGetLastError();
 }
 }  // namespace
@@ -2040,9 +2054,10 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     const int persistent = chain_mode == DR_CHAIN_PERSISTENT, paper = deliver_mode == DR_DELIVER_PAPER;
     HIPCHK(c0, hipEventRecord(c0->ev[0], c0->stream));
     const int need = next_pow2(dmax + 1);
-    hipError_t e = need <= 8    ? launch_small<8>(c0->stream, jt, nctx, nw, persistent, paper)
-                   : need <= 16 ? launch_small<16>(c0->stream, jt, nctx, nw, persistent, paper)
-                                : launch_small<32>(c0->stream, jt, nctx, nw, persistent, paper);
+    const int rsl = dmax + 1;  // ring slots (batch.hpp k_replay_small)
+    hipError_t e = need <= 8    ? launch_small<8>(c0->stream, jt, nctx, nw, persistent, paper, rsl)
+                   : need <= 16 ? launch_small<16>(c0->stream, jt, nctx, nw, persistent, paper, rsl)
+                                : launch_small<32>(c0->stream, jt, nctx, nw, persistent, paper, rsl);
     HIPCHK(c0, e);
     HIPCHK(c0, hipEventRecord(c0->ev[1], c0->stream));
   }
