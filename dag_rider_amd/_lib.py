@@ -17,6 +17,7 @@ DR_DELIVER_REF, DR_DELIVER_PAPER = 0, 1
 DR_WEAK_LITERAL, DR_WEAK_PAPER = 0, 1
 DR_OPT_MEMO = 1
 DR_OPT_DEVICE_PLAN = 2
+DR_OPT_PHASE_TIMING = 3
 DR_SHARD_ID_BYTES = 128
 
 P = C.c_void_p

@@ -101,6 +101,12 @@ struct dr_ctx {
   DevBuf U, WU, SD, K, good, CE, RD, Cc, Gc, Ec, crbase, ccount, nseg, stops, qstats;
   std::vector<uint64_t> hC, hG, hE;
   bool canon_host = false;
+  // DR_OPT_PHASE_TIMING: 2 = HIP events around every replay phase, 1 = around the
+  // summary pass only (ev[6], ev[7]), 0 = none.  Each timed event record costs the
+  // stream a few microseconds.
+  int phase_timing = 2;
+  bool timed(int i) const { return phase_timing >= 2 || (phase_timing == 1 && (i == 6 || i == 7)); }
+  hipError_t rec(int i) { return timed(i) ? hipEventRecord(ev[i], stream) : hipSuccess; }
   int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies  // hC/hG/hE mirror Cc/Gc/Ec (fetched lazily after a planned replay)
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
   DevBuf batch_arena;       // dr_replay_batch scratch + outputs (batch.hpp)
@@ -1005,9 +1011,9 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   HIPCHK(c, c->nseg.ensure(4));
   HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
   HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
-  HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+  HIPCHK(c, c->rec(6));
   HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));
-  HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+  HIPCHK(c, c->rec(7));
   struct Swap {  // launch helpers use c->stream: point it at stream2 for the canonical chain
     dr_ctx *c;
     bool on;
@@ -1058,7 +1064,10 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
     HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nwc * 4));
   }
   HIPCHK(c, c->sync());
-  if (ms_summary) HIPCHK(c, hipEventElapsedTime(ms_summary, c->ev[6], c->ev[7]));
+  if (ms_summary) {
+    *ms_summary = 0;
+    if (c->timed(6)) HIPCHK(c, hipEventElapsedTime(ms_summary, c->ev[6], c->ev[7]));
+  }
   c->canon_host = true;
   return DR_OK;
 }
@@ -1095,6 +1104,11 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
   }
   if (option == DR_OPT_DEVICE_PLAN) {
     c->plan_mode = value != 0;
+    return DR_OK;
+  }
+  if (option == DR_OPT_PHASE_TIMING) {
+    if (value < 0 || value > 2) return c->fail(DR_E_INVAL, "DR_OPT_PHASE_TIMING is 0, 1 or 2");
+    c->phase_timing = value;
     return DR_OK;
   }
   return c->fail(DR_E_INVAL, "unknown option %d", option);
@@ -1780,9 +1794,9 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   a.stops = cstops;
   a.stats = nullptr;
   a.nq_dev = plan + dr::PL_NQC;
-  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(c, c->rec(0));
   HIPCHK(c, launch_sweep(c, a, dr::SW_CHAIN));
-  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(c, c->rec(1));
   // 3. pops + delivery sweeps
   hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
                      dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, task_wave, task_q, cq, cpush_n, push_out, pcap,
@@ -1798,20 +1812,20 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   dr::SweepQuery probe{};
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
   HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // merge sweeps read the canonical cone K
-  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  HIPCHK(c, c->rec(2));
   HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
-  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  HIPCHK(c, c->rec(3));
   // 4. emission
   hipLaunchKernelGGL((dr::k_plan_emit<1024>), dim3(1), dim3(1024), 0, c->stream, pop_cur, pop_q, dq, dstops,
                      c->Cc.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), dedges, kEmitRPB, rb_cap, pd, desc_of_pop,
                      extra_c, extra_g, pedges, digest, item_pref, plan);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  HIPCHK(c, c->rec(4));
   HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, counts, nullptr, nullptr, nullptr, nullptr, 0, true,
                         plan + dr::PL_NDESC, nullptr));
   HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, nullptr, digest, nullptr, nullptr, nullptr, 0, false,
                         plan + dr::PL_NDESC, item_pref));
-  HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+  HIPCHK(c, c->rec(5));
   hipLaunchKernelGGL((dr::k_plan_final<256>), dim3(16), dim3(256), 0, c->stream, nw, c->commit.as<uint8_t>(),
                      c->vcount.as<int32_t>(), push_off, push_wave, desc_of_pop, extra_c, extra_g, pedges, counts,
                      digest, cedges, dstats, c->nseg.as<int32_t>(), plan, h_commit, h_vcount, h_push_off,
@@ -1819,10 +1833,13 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, c->sync());
   // outputs
-  HIPCHK(c, hipEventElapsedTime(&o->ms_summary, c->ev[6], c->ev[7]));
-  HIPCHK(c, hipEventElapsedTime(&o->ms_chain, c->ev[0], c->ev[1]));
-  HIPCHK(c, hipEventElapsedTime(&o->ms_deliver, c->ev[2], c->ev[3]));
-  HIPCHK(c, hipEventElapsedTime(&o->ms_emit, c->ev[4], c->ev[5]));
+  o->ms_summary = o->ms_chain = o->ms_deliver = o->ms_emit = 0;
+  if (c->timed(6)) HIPCHK(c, hipEventElapsedTime(&o->ms_summary, c->ev[6], c->ev[7]));
+  if (c->timed(0)) {
+    HIPCHK(c, hipEventElapsedTime(&o->ms_chain, c->ev[0], c->ev[1]));
+    HIPCHK(c, hipEventElapsedTime(&o->ms_deliver, c->ev[2], c->ev[3]));
+    HIPCHK(c, hipEventElapsedTime(&o->ms_emit, c->ev[4], c->ev[5]));
+  }
   std::memcpy(o->commit, h_commit, (size_t)nw);
   std::memcpy(o->vcount, h_vcount, (size_t)nw * 4);
   c->canon_segments = (int32_t)(int64_t)h_hdr[dr::PH_NSEG];

@@ -74,6 +74,10 @@ class Engine:
         """DR_OPT_MEMO: round summaries + canonical cone (identical results either way)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_MEMO, int(on)))
 
+    def set_phase_timing(self, level: int):
+        """DR_OPT_PHASE_TIMING: 2 = every replay phase timed, 1 = summary pass only, 0 = none."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_PHASE_TIMING, int(level)))
+
     def set_device_plan(self, on: bool):
         """DR_OPT_DEVICE_PLAN: plan dr_replay's phases on the device (identical results either way)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_DEVICE_PLAN, int(on)))

@@ -44,7 +44,7 @@ enum {
   DR_E_STATE = -6     /* call order violated (e.g. append not contiguous) */
 };
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
-enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2 };
+enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
 enum { DR_WEAK_LITERAL = 0, DR_WEAK_PAPER = 1 };
 
@@ -67,7 +67,10 @@ int dr_num_rounds(const dr_ctx *ctx);
  * DR_OPT_DEVICE_PLAN (default 1): dr_replay plans its chain, pop and emission
  * phases on the device (one host synchronisation per replay) when summaries
  * are on, deliver_mode is DR_DELIVER_REF and no ids are requested; 0 = plan
- * on the host between phases (identical results). */
+ * on the host between phases (identical results).
+ * DR_OPT_PHASE_TIMING (default 2): HIP events time every phase of a
+ * device-planned dr_replay (ms_* outputs); 1 = the summary pass only, 0 = none
+ * (untimed ms_* are 0).  Each timed event costs the stream a few microseconds. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 
 /* p.dag[r] = append(p.dag[r], v) (process.go:229) for whole rounds
