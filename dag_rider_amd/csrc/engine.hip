@@ -990,8 +990,11 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
 // nwc > 0 the same pass decides the commits of waves 1..nwc (host arrays).
 // fork: the canonical cone and its prefixes run on stream2 (joined by the
 // caller through ev_join) while the caller's next phases use stream.
+// side (optional, with fork): work launched on stream2 right after the summary
+// pass, beside the canonical chain, which then stays on the main stream; ev_join
+// marks its end.  Without side, fork puts the canonical chain on stream2.
 int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
-                  bool host_out = true, bool fork = false) {
+                  bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr) {
   const int T = c->nrounds - 1;
   const int WS = c->WS, dd = c->memo_dd();
   const size_t R = (size_t)T + 1;
@@ -1024,8 +1027,13 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
   }
+  if (fork && side) {
+    Swap sw(c, true);
+    if (int rc = (*side)()) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
+  }
   {
-  Swap sw(c, fork);
+  Swap sw(c, fork && !side);
   HIPCHK(c, launch_canon_cone(c, T));
   // canonical emission: per-round counts -> positions -> per-round digests -> prefixes
   HIPCHK(c, launch_canon_count(c, T));
@@ -1047,7 +1055,7 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
                      c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
-  if (fork) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
+  if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   }
   c->summary_T = T;
   c->canon_host = false;
@@ -1773,35 +1781,41 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   u64 *h_pc = hv.take<u64>(pcap), *h_pd = hv.take<u64>(pcap), *h_pe = hv.take<u64>(pcap);
   if (hv.off > c->pin_cap - (static_cast<char *>(hp) - c->pin)) return c->fail(DR_E_STATE, "staging overflow");
 
-  // 0+1. summaries + canonical cone + commits (no host copies)
-  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true)) return rc;
+  // 0+1. summaries + commits; then the leader chains and pop planning on stream2
+  // beside the canonical cone on the main stream (the cone takes longer, so the
+  // join before the delivery sweeps finds stream2 done)
   const int sc = dr::Q_SHORTCUT;
-  // 2. leader chains
-  hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(), nw,
-                     persistent ? 1 : 0, dr::Q_CHAIN | dr::Q_STRONG_ONLY | sc, task_wave, task_q, cq, plan);
-  HIPCHK(c, hipGetLastError());
   SweepArgs a;
-  a.q = cq;
-  a.nq = nw;
-  a.seq = 0;
-  a.masks = c->masks.as<u64>();
-  a.dlv = nullptr;
-  a.push_out = push_out;
-  a.push_n = cpush_n;
-  a.edges = cedges;
-  a.wedges = cwedges;
-  a.hits = hits;
-  a.stops = cstops;
-  a.stats = nullptr;
-  a.nq_dev = plan + dr::PL_NQC;
-  HIPCHK(c, c->rec(0));
-  HIPCHK(c, launch_sweep(c, a, dr::SW_CHAIN));
-  HIPCHK(c, c->rec(1));
-  // 3. pops + delivery sweeps
-  hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
-                     dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, task_wave, task_q, cq, cpush_n, push_out, pcap,
-                     task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
-  HIPCHK(c, hipGetLastError());
+  std::function<int()> side = [&]() -> int {
+    // 2. leader chains
+    hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(), nw,
+                       persistent ? 1 : 0, dr::Q_CHAIN | dr::Q_STRONG_ONLY | sc, task_wave, task_q, cq, plan);
+    HIPCHK(c, hipGetLastError());
+    a.q = cq;
+    a.nq = nw;
+    a.seq = 0;
+    a.masks = c->masks.as<u64>();
+    a.dlv = nullptr;
+    a.push_out = push_out;
+    a.push_n = cpush_n;
+    a.edges = cedges;
+    a.wedges = cwedges;
+    a.hits = hits;
+    a.stops = cstops;
+    a.stats = nullptr;
+    a.nq_dev = plan + dr::PL_NQC;
+    HIPCHK(c, c->rec(0));
+    HIPCHK(c, launch_sweep(c, a, dr::SW_CHAIN));
+    HIPCHK(c, c->rec(1));
+    // 3. pops
+    hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
+                       dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, task_wave, task_q, cq, cpush_n, push_out, pcap,
+                       task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
+    HIPCHK(c, hipGetLastError());
+    return 0;
+  };
+  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side)) return rc;
+  // 3. delivery sweeps
   a.q = dq;
   a.push_out = nullptr;
   a.edges = dedges;
@@ -1811,7 +1825,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   a.nq_dev = plan + dr::PL_NQD;
   dr::SweepQuery probe{};
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // merge sweeps read the canonical cone K
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
   HIPCHK(c, c->rec(2));
   HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
   HIPCHK(c, c->rec(3));
