@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 # correction of MI355X_MICROARCH.md) on this bench: tools/pmc_traffic.py output
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "traffic.json")
 # replay phase -> the kernels it launches (names as rocprofv3 reports them)
-PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 512, 1>", "dr::k_weak_union<16, 256>"],
+PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 512, 1>"],
                  "sweep": ["dr::k_sweep<16, 256, 9>"],
                  "batch": ["dr::k_replay_small<8, false, true>"]}
 
@@ -92,14 +92,14 @@ def cpu_bitset(cfg, d, nthreads: int, budget_s: float):
 def kernel_bytes(cfg, d, res):
     """Algorithmic bytes per launch of each replay phase."""
     n, W, T = cfg.n, (cfg.n + 63) // 64, d.nrounds - 1
-    nwc = weak_columns(d)
     leaders = int((res.vcount >= 0).sum())
     dd = max(0, weak_depth(d) - 1)
     sw = res.sweep
     out = {
-        # every strong row of rounds 1..T and every weak-column key read once; U, WU, SD written
-        "summary": dict(kernel="k_summary (round summaries)", ms=res.ms["summary"],
-                        bytes=T * n * W * 8 + nwc * 4 + T * (1 + dd) * W * 8 + T * 8),
+        # k_summary_commit: every strong row of rounds 1..T read once; U and SD written
+        # (the weak-column keys -> WU pass, k_weak_union, runs after it, ~4 us, untimed here)
+        "summary": dict(kernel="k_summary_commit (rows -> U, SD + waveReady commit rule)", ms=res.ms["summary"],
+                        bytes=T * n * W * 8 + T * W * 8 + T * 8),
         # round 4w-2: the word holding the leader bit; rounds 4w-1, 4w: whole rows
         "commit": dict(kernel="k_commit (waveReady commit rule)", ms=res.ms["commit"],
                        bytes=leaders * (n * 8 + 2 * n * W * 8)),

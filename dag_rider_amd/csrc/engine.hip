@@ -422,6 +422,7 @@ hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc)
                      c->view(), T, nwc, mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(), cm,
                      vc);
   hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = c->rec(7);  // ms_summary times k_summary_commit alone (the roofline kernel)
   if (e != hipSuccess || mv.dd == 0) return e;
   hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, c->stream, c->view(), T, mv.dd,
                      c->WU.as<u64>());
@@ -1015,8 +1016,7 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
   HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
   HIPCHK(c, c->rec(6));
-  HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));
-  HIPCHK(c, c->rec(7));
+  HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
   struct Swap {  // launch helpers use c->stream: point it at stream2 for the canonical chain
     dr_ctx *c;
     bool on;

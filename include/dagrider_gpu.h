@@ -175,7 +175,9 @@ typedef struct {
   int64_t n_push;
   int64_t n_ids;
   uint64_t commit_edges, chain_edges, deliver_edges;
-  /* device time (ms) of each phase of the last call, HIP events */
+  /* device time (ms) of each phase of the last call, HIP events (ms_summary: the
+   * rows + commit pass k_summary_commit; the weak union that follows it is not
+   * included) */
   float ms_commit, ms_chain, ms_deliver, ms_emit, ms_summary;
   int32_t canon_segments; /* partial-round segments of the canonical cone (-1: summaries off) */
   /* work done by the delivery sweeps (identical leaders share one sweep):
