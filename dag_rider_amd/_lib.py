@@ -53,6 +53,7 @@ SIGNATURES = {
     "dr_reach_sets": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dr_wave_commit": (C.c_int, [P, C.c_int, C.c_int, P, P]),
     "dr_set_weak_edges": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "dr_buffer_admit": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P]),
     "dr_wave_ready": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, C.POINTER(C.c_int)]),
     "dr_order_vertices": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, C.c_size_t,
                                     C.POINTER(C.c_size_t), P, P]),

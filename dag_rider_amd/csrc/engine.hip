@@ -86,6 +86,7 @@ struct dr_ctx {
   size_t nwc = 0;
   DevBuf sdeg;  // [max_rounds][n] u16 strong degree per vertex (kernels.hpp expand_rows)
   DevBuf setweak;  // dr_set_weak_edges scratch
+  DevBuf admit_buf;  // dr_buffer_admit scratch
   DevBuf wdeg;     // [max_rounds][n] u16 weak degree per vertex (batch.hpp)
   std::vector<uint32_t> h_wc_roff{0};
   // host mirrors
@@ -577,7 +578,8 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena,
-                    &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg};
+                    &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
+                    &c->admit_buf};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1571,7 +1573,96 @@ hipError_t launch_set_weak(dr_ctx *c, int r0, const u64 *srow, u64 *out, u64 *fa
   }
   return hipErrorInvalidValue;
 }
+
+// One sweep of the buffer pass (process.go:200-234): thread i admits buffered
+// vertex i once every predecessor is present (process.go:374-384) in the
+// mirrored rounds <= cur, or was admitted earlier in the same pass by a
+// buffered vertex j < i (first[] = least admitted buffer index per id of the
+// buffered round span).  first[] only falls, so repeated sweeps reach the
+// sequential pass's unique fixed point.
+__global__ void __launch_bounds__(256) k_buffer_admit(const u64 *__restrict__ present, int WS, int n, int lim,
+                                                      int cur, int ghost_round, int rlo, int rhi, int q,
+                                                      const int32_t *__restrict__ ids, const uint32_t *__restrict__ poff,
+                                                      const int32_t *__restrict__ preds, uint32_t *first,
+                                                      uint8_t *admit, uint32_t *changed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q || admit[i]) return;
+  const int vr = ids[2 * i], vs = ids[2 * i + 1];
+  if (vr > cur) return;  // process.go:203: stays buffered
+  bool ok = true;
+  for (uint32_t e = poff[i]; ok && e < poff[i + 1]; e++) {
+    const int pr = preds[2 * e], ps = preds[2 * e + 1];
+    bool here = false;
+    if (pr == 0 && ps == 0) here = ghost_round <= cur;  // a ghost slot {0,0} in rounds 0..cur
+    else if (pr >= 0 && pr <= lim && ps >= 1 && ps <= n)
+      here = (present[(size_t)pr * WS + ((ps - 1) >> 6)] >> ((ps - 1) & 63)) & 1ULL;
+    if (!here && pr >= rlo && pr <= rhi && ps >= 0 && ps <= n)
+      here = __atomic_load_n(&first[(size_t)(pr - rlo) * (n + 1) + ps], __ATOMIC_RELAXED) < (uint32_t)i;
+    ok = here;
+  }
+  if (!ok) return;
+  admit[i] = 1;
+  atomicMin(&first[(size_t)(vr - rlo) * (n + 1) + vs], (uint32_t)i);
+  atomicOr(changed, 1u);
+}
 }  // namespace
+
+extern "C" int dr_buffer_admit(dr_ctx *c, int cur_round, int q, const int32_t *ids, const uint32_t *pred_off,
+                               const int32_t *preds, uint8_t *admit) {
+  if (!c) return DR_E_INVAL;
+  if (q < 0 || (q > 0 && (!ids || !pred_off || !admit))) return c->fail(DR_E_INVAL, "bad buffer arrays");
+  if (q == 0) return DR_OK;
+  const uint32_t ne = pred_off[q];
+  if (pred_off[0] != 0 || (ne > 0 && !preds)) return c->fail(DR_E_INVAL, "bad pred_off/preds");
+  for (int i = 0; i < q; i++)
+    if (pred_off[i + 1] < pred_off[i]) return c->fail(DR_E_INVAL, "pred_off not monotone at %d", i);
+  int rlo = INT32_MAX, rhi = -1;
+  for (int i = 0; i < q; i++) {
+    const int r = ids[2 * i], s = ids[2 * i + 1];
+    if (r < 0 || s < 0 || s > c->n)
+      return c->fail(DR_E_CONTRACT, "buffered vertex %d: id (%d,%d) outside rounds >= 0, sources 0..n", i, r, s);
+    if (r <= cur_round) { rlo = std::min(rlo, r); rhi = std::max(rhi, r); }
+  }
+  std::fill(admit, admit + q, 0);
+  if (rhi < 0) return DR_OK;  // every buffered vertex is ahead of the current round
+  if (int rc = set_device(c)) return rc;
+  int ghost_round = INT32_MAX;
+  for (int r = 0; r < c->nrounds && ghost_round == INT32_MAX; r++)
+    for (uint32_t sl = c->h_slot_off[r]; sl < c->h_slot_off[r + 1]; sl++)
+      if (c->h_slot_src[sl] == 0) { ghost_round = r; break; }
+  const int lim = std::min(cur_round, c->nrounds - 1);
+  const size_t nfirst = (size_t)(rhi - rlo + 1) * (c->n + 1);
+  const size_t b_ids = (size_t)q * 8, b_off = (size_t)(q + 1) * 4, b_pr = (size_t)std::max<uint32_t>(ne, 1) * 8;
+  const size_t o_off = (b_ids + 15) & ~15ull, o_pr = (o_off + b_off + 15) & ~15ull,
+               o_first = (o_pr + b_pr + 15) & ~15ull, o_adm = (o_first + nfirst * 4 + 15) & ~15ull,
+               o_chg = (o_adm + q + 15) & ~15ull, total = o_chg + 16;
+  HIPCHK(c, c->admit_buf.ensure(total));
+  char *base = static_cast<char *>(c->admit_buf.p);
+  int32_t *d_ids = reinterpret_cast<int32_t *>(base);
+  uint32_t *d_off = reinterpret_cast<uint32_t *>(base + o_off);
+  int32_t *d_pr = reinterpret_cast<int32_t *>(base + o_pr);
+  uint32_t *d_first = reinterpret_cast<uint32_t *>(base + o_first), *d_chg = reinterpret_cast<uint32_t *>(base + o_chg);
+  uint8_t *d_adm = reinterpret_cast<uint8_t *>(base + o_adm);
+  HIPCHK(c, hipMemcpyAsync(d_ids, ids, b_ids, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_off, pred_off, b_off, hipMemcpyHostToDevice, c->stream));
+  if (ne) HIPCHK(c, hipMemcpyAsync(d_pr, preds, (size_t)ne * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(d_first, 0xff, nfirst * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(d_adm, 0, q, c->stream));
+  // dependency chains inside one pass are at most q long: at most q+1 sweeps
+  for (int sweep = 0; sweep <= q; sweep++) {
+    uint32_t chg = 0;
+    HIPCHK(c, hipMemsetAsync(d_chg, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_buffer_admit, dim3((q + 255) / 256), dim3(256), 0, c->stream, c->present.as<u64>(), c->WS,
+                       c->n, lim, cur_round, ghost_round, rlo, rhi, q, d_ids, d_off, d_pr, d_first, d_adm, d_chg);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(&chg, d_chg, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!chg) break;
+  }
+  HIPCHK(c, hipMemcpyAsync(admit, d_adm, q, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return DR_OK;
+}
 
 extern "C" int dr_set_weak_edges(dr_ctx *c, int round, int nstrong, const int32_t *strong_ids, int mode,
                                  int32_t *out_ids, size_t cap, size_t *out_n) {

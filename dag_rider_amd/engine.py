@@ -150,6 +150,24 @@ class Engine:
         self._check(self._L.dr_set_weak_edges(self._h, round_, ns, L.ptr(st), mode, L.ptr(ids), k, C.byref(out_n)))
         return ids[:2 * k].reshape(-1, 2)
 
+    # ---- buffer loop + present() (process.go:200-234, :374-384) ----
+    def buffer_admit(self, cur_round: int, buffer: Sequence[Tuple[Tuple[int, int], Sequence[Tuple[int, int]]]]
+                     ) -> np.ndarray:
+        """One pass of the buffer loop: buffer = [(id, predecessors)] in buffer order.
+        Returns admit[i] (uint8): 1 where the reference appends vertex i to the DAG."""
+        q = len(buffer)
+        ids = np.asarray([v for v, _ in buffer] if q else [(0, 0)], dtype=np.int32).reshape(-1)
+        off = np.zeros(q + 1, np.uint32)
+        flat = []
+        for i, (_, pr) in enumerate(buffer):
+            flat.extend(pr)
+            off[i + 1] = len(flat)
+        preds = np.asarray(flat if flat else [(0, 0)], dtype=np.int32).reshape(-1)
+        admit = np.zeros(max(q, 1), np.uint8)
+        self._check(self._L.dr_buffer_admit(self._h, cur_round, q, L.ptr(ids), L.ptr(off), L.ptr(preds),
+                                            L.ptr(admit)))
+        return admit[:q]
+
     # ---- waveReady (process.go:314-354) ----
     def wave_commit(self, w0: int, w1: int):
         nw = w1 - w0 + 1

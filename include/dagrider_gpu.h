@@ -127,6 +127,19 @@ int dr_reach_sets(dr_ctx *ctx, int q, const int32_t *from, const int32_t *bottom
 int dr_set_weak_edges(dr_ctx *ctx, int round, int nstrong, const int32_t *strong_ids, int mode,
                       int32_t *out_ids, size_t cap, size_t *out_n);
 
+/* One pass of the buffer loop (process.go:200-234) with present()
+ * (process.go:374-384) as a presence-bitset test on the device, replacing the
+ * reference's O(R*n) scan per predecessor.  The q buffered vertices, in buffer
+ * order, have ids ids[2i], ids[2i+1] (round, source; 0 <= source <= n, else
+ * DR_E_CONTRACT) and predecessors (strong then weak edges, any order)
+ * preds[2e..] for e in [pred_off[i], pred_off[i+1]).  admit[i] = 1 iff
+ * round_i <= cur_round and every predecessor is present in the mirrored rounds
+ * 0..cur_round or is the id of a vertex j < i admitted earlier in the same
+ * pass -- exactly the sequential pass.  The caller appends the admitted
+ * vertices (buffer order) to the DAG; the rest form the new buffer. */
+int dr_buffer_admit(dr_ctx *ctx, int cur_round, int q, const int32_t *ids, const uint32_t *pred_off,
+                    const int32_t *preds, uint8_t *admit);
+
 /* The commit decision of waveReady (process.go:326-339) for waves w0..w1:
  * commit[i] = leader exists && vcount >= 2f+1; vcount[i] = number of slots of
  * round(w,4) with a strong path to the leader, -1 when the leader is bottom. */

@@ -11,3 +11,4 @@ tests/golden/figure1.json.
 """
 from .pyoracle import *  # noqa: F401,F403
 from . import setweak  # noqa: F401,E402  (setWeakEdges, process.go:298-310)
+from . import buffer  # noqa: F401,E402  (buffer loop + present(), process.go:200-234, :374-384)
