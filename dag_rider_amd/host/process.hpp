@@ -9,6 +9,7 @@
 //   waveReady(wave)                    process/process.go:312-354
 //   getWaveVertexLeader(w)             process/process.go:356-371
 //   orderVertices()                    process/process.go:404-443
+//   buffer / processBuffer()           process/process.go:200-234 (one pass; present() :374-384)
 //   chooseLeader / waveRound           process/process.go:386-402
 //   Stack<T>                           stack/stack.go:3-28 (Pop on empty panics)
 //   Transport / bcastMsg               process/transport.go:6-32 (delivery sink)
@@ -18,6 +19,7 @@
 // receivers drop them); the DAG must satisfy the mirrored contract
 // (dr_append_rounds_lists).  All reachability runs on the GPU.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -188,6 +190,38 @@ class Process {
     }
   }
 
+  // One pass of the buffer loop (process.go:200-234): vertices of rounds <= round
+  // whose predecessors are all present() (process.go:374-384) -- in the DAG or
+  // appended earlier in this pass -- go to dag[v.id.round] in buffer order; the
+  // rest stay buffered.  present() is a device presence-bitset test.
+  void processBuffer() {
+    if (buffer.empty()) return;
+    int ms = 1;  // the mirror's n must cover the buffered ids' sources
+    for (const vertex &v : buffer) ms = std::max(ms, v.id.source);
+    sync(ms);
+    std::vector<int32_t> ids, preds;
+    std::vector<uint32_t> off{0};
+    for (const vertex &v : buffer) {
+      ids.push_back(v.id.round);
+      ids.push_back(v.id.source);
+      for (const auto *es : {&v.strongEdges, &v.weakEdges})
+        for (const auto &e : *es) { preds.push_back(e.round); preds.push_back(e.source); }
+      off.push_back((uint32_t)preds.size() / 2);
+    }
+    preds.push_back(0);
+    std::vector<uint8_t> admit(buffer.size());
+    check(dr_buffer_admit(ctx_, round, (int)buffer.size(), ids.data(), off.data(), preds.data(), admit.data()));
+    std::vector<vertex> next;
+    for (size_t i = 0; i < buffer.size(); i++) {
+      if (!admit[i]) { next.push_back(std::move(buffer[i])); continue; }
+      const int r = buffer[i].id.round;
+      if (r >= (int)dag.size()) throw panic_error("runtime error: index out of range");  // p.dag[r]
+      dag[r].push_back(std::move(buffer[i]));
+    }
+    buffer = std::move(next);
+  }
+
+  std::vector<vertex> buffer;
   int lastVoteCount = -1;
 
  private:
@@ -233,13 +267,13 @@ class Process {
   }
 
   // Mirror p.dag onto the device when it changed (the reference mutates it in place).
-  void sync() {
+  void sync(int need_n = 0) {
     int ms = 1;
     const uint64_t fp = fingerprint(&ms);
-    if (ctx_ && fp == fp_) return;
+    if (ctx_ && fp == fp_ && need_n <= n_) return;
     if (ctx_) dr_destroy(ctx_);
     ctx_ = nullptr;
-    n_ = std::max(ms, 3 * faulty + 1);
+    n_ = std::max({ms, 3 * faulty + 1, need_n});
     int rc = dr_create(n_, faulty, (int)std::max<size_t>(dag.size(), 1), device_, &ctx_);
     if (rc != DR_OK) throw std::runtime_error(std::string("dagrider: ") + dr_last_error(nullptr));
     std::vector<uint32_t> so{0}, sto{0}, wo{0};

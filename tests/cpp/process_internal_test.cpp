@@ -20,6 +20,12 @@ static int failures = 0;
     if (!ok_) failures++;                                          \
   } while (0)
 
+static std::vector<vertexID> E(std::initializer_list<std::pair<int, int>> l) {
+  std::vector<vertexID> v;
+  for (auto &x : l) v.push_back(vertexID{x.first, x.second});
+  return v;
+}
+
 // createDag: rounds 0..4, 5 slots each, slot 0 left zero-valued.
 static std::vector<std::vector<vertex>> createDag(int rounds, int numprocs) {
   std::vector<std::vector<vertex>> dag(rounds);
@@ -27,11 +33,6 @@ static std::vector<std::vector<vertex>> createDag(int rounds, int numprocs) {
     dag[r].resize(numprocs);
     for (int p = 1; p <= 4; p++) dag[r][p].id = vertexID{r, p};
   }
-  auto E = [](std::initializer_list<std::pair<int, int>> l) {
-    std::vector<vertexID> v;
-    for (auto &x : l) v.push_back(vertexID{x.first, x.second});
-    return v;
-  };
   for (int p = 1; p <= 4; p++) dag[1][p].strongEdges = E({{0, 1}, {0, 2}, {0, 3}});
   dag[2][1].strongEdges = E({{1, 1}, {1, 2}, {1, 4}});
   dag[2][2].strongEdges = E({{1, 1}, {1, 2}, {1, 4}});
@@ -95,8 +96,23 @@ int main() {
     same = sunk[i].round == want[i].first && sunk[i].sender == want[i].second;
   REQUIRE(same && p->deliveredVertices.size() == 12 && p->leadersStack.IsEmpty(), "orderVertices/stack[(4,1)]");
 
-  // panics: path from a round beyond the DAG; getWaveVertexLeader(0)
+  // buffer pass (process.go:200-234) at p.round = 4
+  const size_t d4 = p->dag[4].size();
+  p->buffer = {vertex{{4, 5}, {}, E({{3, 1}, {3, 2}}), {}},   // all present -> dag[4]
+               vertex{{5, 1}, {}, E({{4, 1}}), {}},           // round 5 > p.round: stays
+               vertex{{4, 3}, {}, E({{2, 1}}), E({{1, 9}})}};  // (1,9) absent: stays
+  p->processBuffer();
+  REQUIRE(p->dag[4].size() == d4 + 1 && p->buffer.size() == 2 && p->buffer[0].id == (vertexID{5, 1}),
+          "processBuffer/admit-one");
+  // at p.round = 5, (5,1) is admitted into p.dag[5], beyond the DAG: Go panics
+  p->round = 5;
   bool panicked = false;
+  try { p->processBuffer(); } catch (const panic_error &) { panicked = true; }
+  REQUIRE(panicked, "processBuffer/dag-index-panics");
+  p->round = 4;
+
+  // panics: path from a round beyond the DAG; getWaveVertexLeader(0)
+  panicked = false;
   try { p->path({7, 1}, {1, 1}, true); } catch (const panic_error &) { panicked = true; }
   REQUIRE(panicked, "path/out-of-range-panics");
   panicked = false;
