@@ -1574,23 +1574,25 @@ hipError_t launch_set_weak(dr_ctx *c, int r0, const u64 *srow, u64 *out, u64 *fa
   return hipErrorInvalidValue;
 }
 
-// One sweep of the buffer pass (process.go:200-234): thread i admits buffered
-// vertex i once every predecessor is present (process.go:374-384) in the
-// mirrored rounds <= cur, or was admitted earlier in the same pass by a
+// One sweep of the buffer pass (process.go:200-234): wavefront i admits
+// buffered vertex i once every predecessor is present (process.go:374-384) in
+// the mirrored rounds <= cur, or was admitted earlier in the same pass by a
 // buffered vertex j < i (first[] = least admitted buffer index per id of the
-// buffered round span).  first[] only falls, so repeated sweeps reach the
-// sequential pass's unique fixed point.
+// buffered round span).  The 64 lanes stride the predecessor list (a vertex
+// has ~2f+1 of them) and vote with __all.  first[] only falls, so repeated
+// sweeps reach the sequential pass's unique fixed point.
 __global__ void __launch_bounds__(256) k_buffer_admit(const u64 *__restrict__ present, int WS, int n, int lim,
                                                       int cur, int ghost_round, int rlo, int rhi, int q,
                                                       const int32_t *__restrict__ ids, const uint32_t *__restrict__ poff,
                                                       const int32_t *__restrict__ preds, uint32_t *first,
                                                       uint8_t *admit, uint32_t *changed) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);  // wave-uniform
+  const int lane = threadIdx.x & 63;
   if (i >= q || admit[i]) return;
   const int vr = ids[2 * i], vs = ids[2 * i + 1];
   if (vr > cur) return;  // process.go:203: stays buffered
   bool ok = true;
-  for (uint32_t e = poff[i]; ok && e < poff[i + 1]; e++) {
+  for (uint32_t e = poff[i] + lane; ok && e < poff[i + 1]; e += 64) {
     const int pr = preds[2 * e], ps = preds[2 * e + 1];
     bool here = false;
     if (pr == 0 && ps == 0) here = ghost_round <= cur;  // a ghost slot {0,0} in rounds 0..cur
@@ -1600,10 +1602,12 @@ __global__ void __launch_bounds__(256) k_buffer_admit(const u64 *__restrict__ pr
       here = __atomic_load_n(&first[(size_t)(pr - rlo) * (n + 1) + ps], __ATOMIC_RELAXED) < (uint32_t)i;
     ok = here;
   }
-  if (!ok) return;
-  admit[i] = 1;
-  atomicMin(&first[(size_t)(vr - rlo) * (n + 1) + vs], (uint32_t)i);
-  atomicOr(changed, 1u);
+  if (!__all(ok)) return;
+  if (lane == 0) {
+    admit[i] = 1;
+    atomicMin(&first[(size_t)(vr - rlo) * (n + 1) + vs], (uint32_t)i);
+    atomicOr(changed, 1u);
+  }
 }
 }  // namespace
 
@@ -1652,7 +1656,7 @@ extern "C" int dr_buffer_admit(dr_ctx *c, int cur_round, int q, const int32_t *i
   for (int sweep = 0; sweep <= q; sweep++) {
     uint32_t chg = 0;
     HIPCHK(c, hipMemsetAsync(d_chg, 0, 4, c->stream));
-    hipLaunchKernelGGL(k_buffer_admit, dim3((q + 255) / 256), dim3(256), 0, c->stream, c->present.as<u64>(), c->WS,
+    hipLaunchKernelGGL(k_buffer_admit, dim3((q + 3) / 4), dim3(256), 0, c->stream, c->present.as<u64>(), c->WS,
                        c->n, lim, cur_round, ghost_round, rlo, rhi, q, d_ids, d_off, d_pr, d_first, d_adm, d_chg);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(&chg, d_chg, 4, hipMemcpyDeviceToHost, c->stream));
