@@ -49,6 +49,7 @@ SIGNATURES = {
     "dr_set_option": (C.c_int, [P, C.c_int, C.c_int]),
     "dr_append_rounds_lists": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
     "dr_append_rounds_packed": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
+    "dr_append_vertices": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),
     "dr_path_batch": (C.c_int, [P, C.c_int, P, P, C.c_int, P]),
     "dr_reach_sets": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dr_wave_commit": (C.c_int, [P, C.c_int, C.c_int, P, P]),

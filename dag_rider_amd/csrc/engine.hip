@@ -12,6 +12,7 @@
 #include <cstring>
 #include <string>
 #include <functional>
+#include <unordered_set>
 #include <vector>
 
 #include "dagrider_gpu.h"
@@ -69,6 +70,20 @@ struct DevBuf {
   template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// Host copy of one round of Process.dag (process.go:79): what the kernels need
+// beyond the fixed-stride device arrays.  Variable-size per-round data lives
+// here and is flattened to the device from the lowest changed round on
+// (dr_ctx::upload_suffix), so a vertex appended to an old round
+// (process.go:229) rewrites only the rounds from there to the top.
+struct HostRound {
+  std::vector<uint16_t> slots;   // source per slot, insertion order (0 = ghost {0,0})
+  uint64_t deg = 0;              // total strong degree
+  uint64_t nweak = 0;            // weak edges (near + far)
+  std::vector<uint32_t> wc_key;  // weak columns: distinct near targets (delta << 11 | t-1), sorted
+  std::vector<u64> wc_rows;      // [key][WS]: the round's sources with that weak edge
+  std::vector<u64> far;          // weak edges with delta > 1023: (own s-1) << 32 | (r' << 11 | t-1)
+};
+
 }  // namespace
 
 struct dr_ctx {
@@ -78,28 +93,32 @@ struct dr_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
   // device DAG
-  DevBuf strong, present, slot_off, slot_src, weak, weak_roff, far, far_roff;
-  size_t nweak = 0, nfar = 0;
+  DevBuf strong, present, slot_off, slot_src, weak_roff, far, far_roff;
+  size_t nfar = 0;
   // weak columns (kernels.hpp DagView::wc_*): one entry per distinct near weak
   // target (delta, t) of a round + the bitset of the round's sources pointing at it
   DevBuf wc_key, wc_rows, wc_roff;
-  size_t nwc = 0;
   DevBuf sdeg;  // [max_rounds][n] u16 strong degree per vertex (kernels.hpp expand_rows)
   DevBuf setweak;  // dr_set_weak_edges scratch
   DevBuf admit_buf;  // dr_buffer_admit scratch
   DevBuf wdeg;     // [max_rounds][n] u16 weak degree per vertex (batch.hpp)
-  std::vector<uint32_t> h_wc_roff{0};
-  // host mirrors
-  std::vector<uint32_t> h_slot_off{0};
-  std::vector<uint16_t> h_slot_src;
+  DevBuf put_buf;  // dr_append_vertices staging on the device
+  // host mirror: per-round data, presence [rounds][WS], and the prefix offsets
+  // of the flattened device arrays (valid for rounds < up_lo)
+  std::vector<HostRound> hr;
   std::vector<u64> h_present;
-  std::vector<uint64_t> h_deg;  // total strong degree per round
-  std::vector<uint32_t> h_weak_roff{0}, h_far_roff{0};
-  // round summaries + canonical cone (memo path), valid for rounds 0..summary_T
+  std::vector<uint32_t> h_slot_off{0}, h_wc_roff{0}, h_far_roff{0}, h_weak_roff{0};
+  int up_lo = 0;  // lowest round whose flattened device arrays are stale
+  // round summaries (U, SD, WU) per round: sdirty[r] = stale; the canonical cone
+  // and its prefixes (K, C, G, E) describe the DAG as of the last canon build
   bool use_memo = true;
-  int summary_T = -1;
+  std::vector<uint8_t> sdirty;
+  int sum_dd = -1;            // WU layout the summaries were built with (memo_dd())
+  bool canon_ok = false;      // K/C/G/E describe the current DAG
   int32_t canon_segments = 0;
-  DevBuf U, WU, SD, K, good, CE, RD, Cc, Gc, Ec, crbase, ccount, nseg, stops, qstats;
+  DevBuf U, WU, SD, K, good, CE, RD, Cc, Gc, Ec, crbase, ccount, nseg, stops, qstats, srounds;
+  int ndirty = 0;     // rounds with sdirty set
+  int canon_T = -1;   // top round of the last canonical build
   std::vector<uint64_t> hC, hG, hE;
   bool canon_host = false;
   // DR_OPT_PHASE_TIMING: 2 = HIP events around every replay phase, 1 = around the
@@ -231,7 +250,6 @@ struct dr_ctx {
     dr::DagView v;
     v.strong = strong.as<u64>();
     v.present = present.as<u64>();
-    v.weak = weak.as<uint32_t>();
     v.weak_roff = weak_roff.as<uint32_t>();
     v.far = far.as<u64>();
     v.far_roff = far_roff.as<uint32_t>();
@@ -258,6 +276,71 @@ struct dr_ctx {
     return l;
   }
   size_t sweep_lds(int dl) const { return (size_t)(2 * WS + (1 << dl) * WS) * 8 + 64; }
+  uint64_t round_deg(int r) const { return hr[r].deg; }
+  bool has_ghost(int r) const {
+    for (uint16_t s : hr[r].slots)
+      if (s == 0) return true;
+    return false;
+  }
+  // a round changed: its summaries are stale, and so is every canonical prefix
+  void touch(int r) {
+    while ((int)sdirty.size() <= r) { sdirty.push_back(1); ndirty++; }
+    if (!sdirty[r]) { sdirty[r] = 1; ndirty++; }
+    canon_ok = false;
+    up_lo = std::min(up_lo, r);
+  }
+  // Flatten rounds [up_lo, nrounds) of the variable-size per-round arrays
+  // (slots, weak columns, far edges, weak counts, presence) and copy them to
+  // the device after the unchanged prefix.  One staged copy per array.
+  hipError_t upload_suffix() {
+    const int R = nrounds, lo = up_lo;
+    if (lo >= R) { up_lo = R; return hipSuccess; }
+    h_slot_off.resize(R + 1);
+    h_wc_roff.resize(R + 1);
+    h_far_roff.resize(R + 1);
+    h_weak_roff.resize(R + 1);
+    for (int r = lo; r < R; r++) {
+      const HostRound &h = hr[r];
+      h_slot_off[r + 1] = h_slot_off[r] + (uint32_t)h.slots.size();
+      h_wc_roff[r + 1] = h_wc_roff[r] + (uint32_t)h.wc_key.size();
+      h_far_roff[r + 1] = h_far_roff[r] + (uint32_t)h.far.size();
+      h_weak_roff[r + 1] = h_weak_roff[r] + (uint32_t)h.nweak;
+    }
+    const size_t s0 = h_slot_off[lo], s1 = h_slot_off[R], k0 = h_wc_roff[lo], k1 = h_wc_roff[R];
+    const size_t f0 = h_far_roff[lo], f1 = h_far_roff[R];
+    hipError_t e;
+    if ((e = slot_src.grow(s1 * 2 + 64, s0 * 2, stream)) != hipSuccess) return e;
+    if ((e = wc_key.grow(k1 * 4 + 64, k0 * 4, stream)) != hipSuccess) return e;
+    if ((e = wc_rows.grow(k1 * WS * 8 + 64, k0 * WS * 8, stream)) != hipSuccess) return e;
+    if ((e = far.grow(f1 * 8 + 64, f0 * 8, stream)) != hipSuccess) return e;
+    std::vector<uint16_t> sl;
+    sl.reserve(s1 - s0);
+    std::vector<uint32_t> kk;
+    kk.reserve(k1 - k0);
+    std::vector<u64> rows, ff;
+    rows.reserve((k1 - k0) * WS);
+    ff.reserve(f1 - f0);
+    for (int r = lo; r < R; r++) {
+      const HostRound &h = hr[r];
+      sl.insert(sl.end(), h.slots.begin(), h.slots.end());
+      kk.insert(kk.end(), h.wc_key.begin(), h.wc_key.end());
+      rows.insert(rows.end(), h.wc_rows.begin(), h.wc_rows.end());
+      ff.insert(ff.end(), h.far.begin(), h.far.end());
+    }
+    const size_t nr = (size_t)(R - lo);
+    if ((e = h2d(slot_src.as<uint16_t>() + s0, sl.data(), sl.size() * 2)) != hipSuccess) return e;
+    if ((e = h2d(wc_key.as<uint32_t>() + k0, kk.data(), kk.size() * 4)) != hipSuccess) return e;
+    if ((e = h2d(wc_rows.as<u64>() + k0 * WS, rows.data(), rows.size() * 8)) != hipSuccess) return e;
+    if ((e = h2d(far.as<u64>() + f0, ff.data(), ff.size() * 8)) != hipSuccess) return e;
+    if ((e = h2d(slot_off.as<uint32_t>() + lo + 1, &h_slot_off[lo + 1], nr * 4)) != hipSuccess) return e;
+    if ((e = h2d(wc_roff.as<uint32_t>() + lo + 1, &h_wc_roff[lo + 1], nr * 4)) != hipSuccess) return e;
+    if ((e = h2d(far_roff.as<uint32_t>() + lo + 1, &h_far_roff[lo + 1], nr * 4)) != hipSuccess) return e;
+    if ((e = h2d(weak_roff.as<uint32_t>() + lo + 1, &h_weak_roff[lo + 1], nr * 4)) != hipSuccess) return e;
+    if ((e = h2d(present.as<u64>() + (size_t)lo * WS, &h_present[(size_t)lo * WS], nr * WS * 8)) != hipSuccess)
+      return e;
+    up_lo = R;
+    return hipSuccess;
+  }
 };
 
 #define HIPCHK(ctx, call)                                                                   \
@@ -413,21 +496,55 @@ hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, ui
   return hipErrorInvalidValue;
 }
 
+// k_summary_commit geometry (block, chunks in flight per thread, software
+// pipelining); dr_profile_kernel's variants time the alternatives.
+template <int WS, int NT, int GRP, bool PIPE>
+hipError_t launch_sc(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
+  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, GRP, PIPE>), dim3((T + 3) / 4), dim3(NT), 0, c->stream,
+                     c->view(), T, nwc, 2 * c->f + 1, c->U.as<u64>(), c->SD.as<u64>(), cm, vc);
+  return hipGetLastError();
+}
+template <int WS>
+hipError_t launch_sc_shipped(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
+  return launch_sc<WS, summary_block<WS>(), 8, false>(c, T, nwc, cm, vc);
+}
+
 template <int WS>
 hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
-  // rows + commit decisions (U, SD), then the weak-edge unions (WU): two
-  // back-to-back streaming passes beat the fused one (profiles/r01/v5_tune.txt)
-  constexpr int NT = summary_block<WS>();
+  // rows + commit decisions (U, SD), then the weak-edge unions (WU) from the
+  // weak-column keys: two back-to-back passes (profiles/r01/v5_tune.txt)
   const dr::MemoView mv = c->memo_view();
-  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, dr::SV_NO_WEAK>), dim3((T + 3) / 4), dim3(NT), 0, c->stream,
-                     c->view(), T, nwc, mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(), cm,
-                     vc);
-  hipError_t e = hipGetLastError();
+  hipError_t e = launch_sc_shipped<WS>(c, T, nwc, cm, vc);
   if (e == hipSuccess) e = c->rec(7);  // ms_summary times k_summary_commit alone (the roofline kernel)
   if (e != hipSuccess || mv.dd == 0) return e;
   hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, c->stream, c->view(), T, mv.dd,
-                     c->WU.as<u64>());
+                     c->WU.as<u64>(), (const int32_t *)nullptr);
   return hipGetLastError();
+}
+
+// incremental summaries of the listed rounds (device list of nr rounds)
+template <int WS>
+hipError_t launch_round_summary_t(dr_ctx *c, const int32_t *rounds, int nr) {
+  constexpr int NT = block_for<WS>() < 256 ? 256 : block_for<WS>();
+  const dr::MemoView mv = c->memo_view();
+  hipLaunchKernelGGL((dr::k_round_summary<WS, NT>), dim3(nr), dim3(NT), 0, c->stream, c->view(), rounds,
+                     c->U.as<u64>(), c->SD.as<u64>());
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || mv.dd == 0) return e;
+  hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(nr), dim3(256), 0, c->stream, c->view(), c->nrounds - 1,
+                     mv.dd, c->WU.as<u64>(), rounds);
+  return hipGetLastError();
+}
+hipError_t launch_round_summary(dr_ctx *c, const int32_t *rounds, int nr) {
+  switch (c->WS) {
+    case 1: return launch_round_summary_t<1>(c, rounds, nr);
+    case 2: return launch_round_summary_t<2>(c, rounds, nr);
+    case 4: return launch_round_summary_t<4>(c, rounds, nr);
+    case 8: return launch_round_summary_t<8>(c, rounds, nr);
+    case 16: return launch_round_summary_t<16>(c, rounds, nr);
+    case 32: return launch_round_summary_t<32>(c, rounds, nr);
+  }
+  return hipErrorInvalidValue;
 }
 
 // canonical cone: K^cand per round, then the exact cone at the bad rounds
@@ -546,7 +663,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
       c->slot_off.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->weak_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->far_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
-      c->weak.ensure(4096) != hipSuccess || c->far.ensure(4096) != hipSuccess ||
+      c->far.ensure(4096) != hipSuccess ||
       c->wc_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->wc_key.ensure(4096) != hipSuccess || c->wc_rows.ensure(4096) != hipSuccess ||
       c->sdeg.ensure((size_t)max_rounds * n * sizeof(uint16_t)) != hipSuccess ||
@@ -570,14 +687,14 @@ extern "C" void dr_destroy(dr_ctx *c) {
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)c->sync();
   if (c->pin) (void)hipHostFree(c->pin);
-  DevBuf *bufs[] = {&c->strong,  &c->present, &c->slot_off, &c->slot_src, &c->weak,
+  DevBuf *bufs[] = {&c->strong,  &c->present, &c->slot_off, &c->slot_src, &c->put_buf,
                     &c->weak_roff, &c->far,   &c->far_roff, &c->q_buf,    &c->masks,
                     &c->dlv,     &c->push_out, &c->push_n,  &c->edges,    &c->hits, &c->wedges,
                     &c->commit,  &c->vcount,  &c->popdesc,  &c->rbase,    &c->counts,
                     &c->digest,  &c->pop_pos, &c->ids,      &c->U,        &c->WU,
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
-                    &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena,
+                    &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
                     &c->admit_buf};
   for (DevBuf *b : bufs) b->release();
@@ -599,6 +716,37 @@ extern "C" int dr_num_rounds(const dr_ctx *c) { return c ? c->nrounds : -1; }
 // ===========================================================================
 // DAG append (validation + packing)
 // ===========================================================================
+namespace {
+// Set bit `own` (0-based source) of the weak column `key` of round h, keeping
+// the keys sorted (the order the bulk path produces; no kernel depends on it).
+void wc_add(HostRound &h, int WS, uint32_t key, int own) {
+  auto it = std::lower_bound(h.wc_key.begin(), h.wc_key.end(), key);
+  const size_t j = (size_t)(it - h.wc_key.begin());
+  if (it == h.wc_key.end() || *it != key) {
+    h.wc_key.insert(it, key);
+    h.wc_rows.insert(h.wc_rows.begin() + (ptrdiff_t)(j * WS), (size_t)WS, 0ULL);
+  }
+  h.wc_rows[j * WS + (own >> 6)] |= 1ULL << (own & 63);
+}
+
+// rows, strong and weak degrees of individually appended vertices (vidx = r*n + s-1)
+__global__ __launch_bounds__(256) void k_put_vertices(const u64 *__restrict__ rows, const uint32_t *__restrict__ vidx,
+                                                      const uint16_t *__restrict__ sd,
+                                                      const uint16_t *__restrict__ wd, int nv, int WS,
+                                                      u64 *__restrict__ strong, uint16_t *__restrict__ sdeg,
+                                                      uint16_t *__restrict__ wdeg) {
+  const int64_t total = (int64_t)nv * WS;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t v = t / WS, w = t - v * WS;
+    strong[(size_t)vidx[v] * WS + w] = rows[t];
+    if (w == 0) {
+      sdeg[vidx[v]] = sd[v];
+      wdeg[vidx[v]] = wd[v];
+    }
+  }
+}
+}  // namespace
+
 extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t *slot_off,
                                        const uint16_t *slot_src, const uint64_t *strong,
                                        const uint32_t *weak_off, const uint32_t *weak_tgt) {
@@ -610,27 +758,28 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   if (!slot_off || !slot_src || !strong || !weak_off) return c->fail(DR_E_INVAL, "null array");
   const int n = c->n, W = c->W, WS = c->WS;
   std::vector<u64> pres((size_t)k * WS, 0);
-  std::vector<uint64_t> deg(k, 0);
+  std::vector<HostRound> nh(k);
   std::vector<uint16_t> vdeg((size_t)k * n, 0), vwdeg((size_t)k * n, 0);
-  std::vector<uint32_t> wdev, wroff(k);
-  std::vector<u64> fdev;
-  std::vector<uint32_t> froff(k);
+  size_t nfar = 0;
   int dmax = c->dmax_near;
   const u64 lastmask = (n % 64) ? ((1ULL << (n % 64)) - 1ULL) : ~0ULL;
+  std::vector<uint32_t> wl, tmp;  // one round's near weak edges: delta << 22 | own << 11 | t
+  std::vector<uint32_t> cnt(2048);
   for (int i = 0; i < k; i++) {
     const int r = r0 + i;
     u64 *P = &pres[(size_t)i * WS];
+    HostRound &h = nh[i];
     for (uint32_t sl = slot_off[i]; sl < slot_off[i + 1]; sl++) {
       const int s = slot_src[sl];
       if (s > n) return c->fail(DR_E_CONTRACT, "round %d slot %u: source %d > n=%d", r, sl - slot_off[i], s, n);
+      h.slots.push_back((uint16_t)s);
       if (s == 0) continue;  // ghost slot {0,0}
       u64 &wd = P[(s - 1) >> 6];
       const u64 bit = 1ULL << ((s - 1) & 63);
       if ((wd & bit) && r >= 1) return c->fail(DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, s);
       wd |= bit;
     }
-    wroff[i] = (uint32_t)wdev.size();
-    froff[i] = (uint32_t)fdev.size();
+    wl.clear();
     for (int s0 = 0; s0 < n; s0++) {
       const bool here = (P[s0 >> 6] >> (s0 & 63)) & 1ULL;
       const uint64_t *row = strong + ((size_t)i * n + s0) * W;
@@ -640,12 +789,13 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
       if (nz && !here) return c->fail(DR_E_CONTRACT, "round %d: strong edges on absent vertex (%d,%d)", r, r, s0 + 1);
       if (nz && r == 0) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", s0 + 1);
       if (row[W - 1] & ~lastmask) return c->fail(DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
-      deg[i] += d;
+      h.deg += d;
       vdeg[(size_t)i * n + s0] = (uint16_t)d;
       const uint32_t ea = weak_off[(size_t)i * n + s0], eb = weak_off[(size_t)i * n + s0 + 1];
       if (eb < ea) return c->fail(DR_E_INVAL, "weak_off not monotone at round %d", r);
       if (eb > ea && !here) return c->fail(DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1);
       vwdeg[(size_t)i * n + s0] = (uint16_t)std::min<uint32_t>(eb - ea, 65535u);
+      h.nweak += eb - ea;
       for (uint32_t e = ea; e < eb; e++) {
         const uint32_t t = weak_tgt[e];
         const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
@@ -653,56 +803,41 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
         if (tr > r - 2) return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target a round < r-1", r, s0 + 1, tr, ts + 1);
         const int delta = r - tr;
         if (delta <= 1023) {
-          wdev.push_back(((uint32_t)delta << 22) | ((uint32_t)s0 << 11) | (uint32_t)ts);
+          wl.push_back(((uint32_t)delta << 22) | ((uint32_t)s0 << 11) | (uint32_t)ts);
           dmax = std::max(dmax, delta);
         } else {
-          fdev.push_back(((u64)s0 << 32) | t);
+          h.far.push_back(((u64)s0 << 32) | t);
+          nfar++;
         }
       }
     }
-  }
-  // device weak edges of each round sorted by (delta, target): the kernels'
-  // wave-uniform OR path (kernels.hpp walk_weak) needs equal destinations
-  // adjacent; edge order is irrelevant to every result.  2-pass LSD radix.
-  {
-    std::vector<uint32_t> tmp;
-    std::vector<uint32_t> cnt(2048);
-    for (int i = 0; i < k; i++) {
-      const size_t a = wroff[i], b = (i + 1 < k) ? wroff[i + 1] : wdev.size();
-      if (b - a < 2) continue;
-      tmp.resize(b - a);
-      uint32_t *src = wdev.data() + a, *dst = tmp.data();
+    // weak columns: sort the round's edges by (delta, target) (2-pass LSD radix);
+    // each run of equal keys is one column, its row the run's sources
+    if (wl.size() >= 2) {
+      tmp.resize(wl.size());
+      uint32_t *src = wl.data(), *dst = tmp.data();
       for (int pass = 0; pass < 2; pass++) {
         const int sh = pass == 0 ? 0 : 22, nb = pass == 0 ? 2048 : 1024;
         std::fill(cnt.begin(), cnt.begin() + nb, 0);
-        for (size_t e = 0; e < b - a; e++) cnt[(src[e] >> sh) & (nb - 1)]++;
+        for (size_t e = 0; e < wl.size(); e++) cnt[(src[e] >> sh) & (nb - 1)]++;
         uint32_t run = 0;
         for (int t = 0; t < nb; t++) { const uint32_t c2 = cnt[t]; cnt[t] = run; run += c2; }
-        for (size_t e = 0; e < b - a; e++) dst[cnt[(src[e] >> sh) & (nb - 1)]++] = src[e];
+        for (size_t e = 0; e < wl.size(); e++) dst[cnt[(src[e] >> sh) & (nb - 1)]++] = src[e];
         std::swap(src, dst);
       }
-      // after two passes the sorted data is back in wdev
+      // after two passes the sorted data is back in wl
     }
-  }
-  // weak columns: each run of equal (delta, target) in the sorted round is one
-  // entry; its row holds the sources of the run (bit s-1, WS-word stride)
-  std::vector<uint32_t> wck, wcroff(k + 1);
-  std::vector<u64> wcrows;
-  for (int i = 0; i < k; i++) {
-    wcroff[i] = (uint32_t)wck.size();
-    const size_t a = wroff[i], b = (i + 1 < k) ? wroff[i + 1] : wdev.size();
-    for (size_t e = a; e < b; e++) {
-      const uint32_t x = wdev[e], key = ((x >> 22) << 11) | (x & 2047u);
-      if (e == a || key != wck.back()) {
-        wck.push_back(key);
-        wcrows.resize(wcrows.size() + WS, 0ULL);
+    for (size_t e = 0; e < wl.size(); e++) {
+      const uint32_t x = wl[e], key = ((x >> 22) << 11) | (x & 2047u);
+      if (h.wc_key.empty() || key != h.wc_key.back()) {
+        h.wc_key.push_back(key);
+        h.wc_rows.resize(h.wc_rows.size() + WS, 0ULL);
       }
       const uint32_t own = (x >> 11) & 2047u;
-      wcrows[wcrows.size() - WS + (own >> 6)] |= 1ULL << (own & 63);
+      h.wc_rows[h.wc_rows.size() - WS + (own >> 6)] |= 1ULL << (own & 63);
     }
   }
-  wcroff[k] = (uint32_t)wck.size();
-  // ---- commit to device ----
+  // ---- commit: rows and per-vertex degrees, then the flattened per-round arrays ----
   const size_t row_words = (size_t)n * WS;
   if (WS == W) {
     HIPCHK(c, hipMemcpyAsync(c->strong.as<u64>() + (size_t)r0 * row_words, strong,
@@ -715,60 +850,134 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  HIPCHK(c, hipMemcpyAsync(c->present.as<u64>() + (size_t)r0 * WS, pres.data(), pres.size() * 8,
-                           hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->sdeg.as<uint16_t>() + (size_t)r0 * n, vdeg.data(), vdeg.size() * 2,
                            hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->wdeg.as<uint16_t>() + (size_t)r0 * n, vwdeg.data(), vwdeg.size() * 2,
                            hipMemcpyHostToDevice, c->stream));
-  // slots
-  const size_t old_slots = c->h_slot_src.size();
-  const uint32_t add_slots = slot_off[k] - slot_off[0];
-  HIPCHK(c, c->slot_src.grow((old_slots + add_slots) * 2 + 64, old_slots * 2, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->slot_src.as<uint16_t>() + old_slots, slot_src + slot_off[0],
-                           (size_t)add_slots * 2, hipMemcpyHostToDevice, c->stream));
-  // weak
-  HIPCHK(c, c->weak.grow((c->nweak + wdev.size()) * 4 + 64, c->nweak * 4, c->stream));
-  if (!wdev.empty())
-    HIPCHK(c, hipMemcpyAsync(c->weak.as<uint32_t>() + c->nweak, wdev.data(), wdev.size() * 4,
-                             hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, c->wc_key.grow((c->nwc + wck.size()) * 4 + 64, c->nwc * 4, c->stream));
-  HIPCHK(c, c->wc_rows.grow((c->nwc + wck.size()) * WS * 8 + 64, c->nwc * WS * 8, c->stream));
-  if (!wck.empty()) {
-    HIPCHK(c, hipMemcpyAsync(c->wc_key.as<uint32_t>() + c->nwc, wck.data(), wck.size() * 4,
-                             hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->wc_rows.as<u64>() + c->nwc * WS, wcrows.data(), wcrows.size() * 8,
-                             hipMemcpyHostToDevice, c->stream));
-  }
-  HIPCHK(c, c->far.grow((c->nfar + fdev.size()) * 8 + 64, c->nfar * 8, c->stream));
-  if (!fdev.empty())
-    HIPCHK(c, hipMemcpyAsync(c->far.as<u64>() + c->nfar, fdev.data(), fdev.size() * 8,
-                             hipMemcpyHostToDevice, c->stream));
-  // host mirrors + offsets
-  for (int i = 0; i < k; i++) {
-    c->h_slot_off.push_back(c->h_slot_off.back() + (slot_off[i + 1] - slot_off[i]));
-    c->h_weak_roff.push_back((uint32_t)(c->nweak + (i + 1 < k ? wroff[i + 1] : wdev.size())));
-    c->h_far_roff.push_back((uint32_t)(c->nfar + (i + 1 < k ? froff[i + 1] : fdev.size())));
-    c->h_wc_roff.push_back((uint32_t)(c->nwc + wcroff[i + 1]));
-  }
-  c->h_slot_src.insert(c->h_slot_src.end(), slot_src + slot_off[0], slot_src + slot_off[k]);
+  for (auto &h : nh) c->hr.push_back(std::move(h));
   c->h_present.insert(c->h_present.end(), pres.begin(), pres.end());
-  c->h_deg.insert(c->h_deg.end(), deg.begin(), deg.end());
-  HIPCHK(c, hipMemcpyAsync(c->slot_off.as<uint32_t>() + r0 + 1, &c->h_slot_off[r0 + 1], (size_t)k * 4,
-                           hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->weak_roff.as<uint32_t>() + r0 + 1, &c->h_weak_roff[r0 + 1], (size_t)k * 4,
-                           hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->far_roff.as<uint32_t>() + r0 + 1, &c->h_far_roff[r0 + 1], (size_t)k * 4,
-                           hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->wc_roff.as<uint32_t>() + r0 + 1, &c->h_wc_roff[r0 + 1], (size_t)k * 4,
-                           hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->nweak += wdev.size();
-  c->nfar += fdev.size();
-  c->nwc += wck.size();
+  c->nfar += nfar;
   c->dmax_near = dmax;
   c->nrounds += k;
-  c->summary_T = -1;  // summaries describe the old DAG
+  for (int r = r0; r < r0 + k; r++) c->touch(r);
+  HIPCHK(c, c->upload_suffix());
+  HIPCHK(c, c->sync());
+  return DR_OK;
+}
+
+extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, const int32_t *ids,
+                                  const uint32_t *strong_off, const int32_t *strong_ids, const uint32_t *weak_off,
+                                  const int32_t *weak_ids) {
+  if (!c) return DR_E_INVAL;
+  if (k < 0) return c->fail(DR_E_INVAL, "negative vertex count");
+  if (k == 0) return DR_OK;
+  if (!ids || !strong_off || !weak_off) return c->fail(DR_E_INVAL, "null array");
+  if (int rc = set_device(c)) return rc;
+  const int n = c->n, WS = c->WS, R0 = c->nrounds;
+  // pass 1: validate every vertex against the mirror plus the vertices before it
+  // in this call; nothing changes unless all of them are inside the contract
+  int R = R0;
+  std::unordered_set<uint64_t> added;
+  for (int i = 0; i < k; i++) {
+    const int vr = ids[2 * i], vs = ids[2 * i + 1];
+    const int r = slot_round ? slot_round[i] : vr;
+    if (r < 0 || r > R)
+      return c->fail(DR_E_INVAL, "vertex %d: p.dag[%d] with %d rounds (Go: index out of range)", i, r, R);
+    if (r == R) {
+      if (R >= c->max_rounds) return c->fail(DR_E_INVAL, "vertex %d opens round %d beyond max_rounds %d", i, r, c->max_rounds);
+      R++;
+    }
+    const uint32_t sa = strong_off[i], sb = strong_off[i + 1], wa = weak_off[i], wb = weak_off[i + 1];
+    if (sb < sa || wb < wa) return c->fail(DR_E_INVAL, "vertex %d: edge offsets not monotone", i);
+    if ((sb > sa && !strong_ids) || (wb > wa && !weak_ids)) return c->fail(DR_E_INVAL, "null edge array");
+    if (vr == 0 && vs == 0) {  // ghost slot: zero vertexID (process_internal_test.go:89-100)
+      if (sb != sa || wb != wa) return c->fail(DR_E_CONTRACT, "p.dag[%d]: ghost slot {0,0} with edges", r);
+      continue;
+    }
+    if (vr != r || vs < 1 || vs > n)
+      return c->fail(DR_E_CONTRACT, "p.dag[%d]: id (%d,%d) outside the mirrored contract", r, vr, vs);
+    if (r >= 1 && ((r < R0 && c->is_present(r, vs)) || !added.insert(((uint64_t)r << 32) | (uint32_t)vs).second))
+      return c->fail(DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, vs);
+    if (r == 0 && sb > sa) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", vs);
+    for (uint32_t e = sa; e < sb; e++) {
+      const int tr = strong_ids[2 * e], ts = strong_ids[2 * e + 1];
+      if (tr != r - 1 || ts < 1 || ts > n)
+        return c->fail(DR_E_CONTRACT, "strong edge (%d,%d)->(%d,%d) must target round r-1, source in [1,n]", r, vs, tr, ts);
+    }
+    for (uint32_t e = wa; e < wb; e++) {
+      const int tr = weak_ids[2 * e], ts = weak_ids[2 * e + 1];
+      if (tr < 0 || tr > r - 2 || ts < 1 || ts > n)
+        return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target round < r-1, source in [1,n]", r, vs, tr, ts);
+    }
+  }
+  // pass 2: apply
+  if (R > R0) {  // opened rounds start empty: zero rows and degrees
+    const size_t a = (size_t)R0 * n, b = (size_t)R * n;
+    HIPCHK(c, hipMemsetAsync(c->strong.as<u64>() + a * WS, 0, (b - a) * WS * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sdeg.as<uint16_t>() + a, 0, (b - a) * 2, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->wdeg.as<uint16_t>() + a, 0, (b - a) * 2, c->stream));
+    c->hr.resize(R);
+    c->h_present.resize((size_t)R * WS, 0);
+    c->nrounds = R;
+  }
+  std::vector<u64> rows((size_t)k * WS, 0);
+  std::vector<uint32_t> vidx(k);
+  std::vector<uint16_t> sd(k), wd(k);
+  int nv = 0, dmax = c->dmax_near;
+  for (int i = 0; i < k; i++) {
+    const int vr = ids[2 * i], vs = ids[2 * i + 1];
+    const int r = slot_round ? slot_round[i] : vr;
+    HostRound &h = c->hr[r];
+    c->touch(r);
+    if (vr == 0 && vs == 0) {
+      h.slots.push_back(0);
+      continue;
+    }
+    h.slots.push_back((uint16_t)vs);
+    c->h_present[(size_t)r * WS + ((vs - 1) >> 6)] |= 1ULL << ((vs - 1) & 63);
+    u64 *row = &rows[(size_t)nv * WS];
+    for (uint32_t e = strong_off[i]; e < strong_off[i + 1]; e++) {
+      const int ts = strong_ids[2 * e + 1] - 1;
+      row[ts >> 6] |= 1ULL << (ts & 63);
+    }
+    uint64_t d = 0;
+    for (int w = 0; w < WS; w++) d += (uint64_t)__builtin_popcountll(row[w]);
+    h.deg += d;
+    const uint32_t wa = weak_off[i], wb = weak_off[i + 1];
+    for (uint32_t e = wa; e < wb; e++) {
+      const int tr = weak_ids[2 * e], ts = weak_ids[2 * e + 1] - 1, delta = r - tr;
+      if (delta <= 1023) {
+        wc_add(h, WS, ((uint32_t)delta << 11) | (uint32_t)ts, vs - 1);
+        dmax = std::max(dmax, delta);
+      } else {
+        h.far.push_back(((u64)(vs - 1) << 32) | ((uint32_t)tr << 11) | (uint32_t)ts);
+        c->nfar++;
+      }
+    }
+    h.nweak += wb - wa;
+    vidx[nv] = (uint32_t)((size_t)r * n + vs - 1);
+    sd[nv] = (uint16_t)d;
+    wd[nv] = (uint16_t)std::min<uint32_t>(wb - wa, 65535u);
+    nv++;
+  }
+  c->dmax_near = dmax;
+  if (nv) {
+    const size_t o_idx = (size_t)nv * WS * 8, o_sd = o_idx + (size_t)nv * 4, o_wd = o_sd + (size_t)nv * 2;
+    HIPCHK(c, c->put_buf.ensure(o_wd + (size_t)nv * 2));
+    char *b = c->put_buf.as<char>();
+    HIPCHK(c, c->h2d(b, rows.data(), o_idx));
+    HIPCHK(c, c->h2d(b + o_idx, vidx.data(), (size_t)nv * 4));
+    HIPCHK(c, c->h2d(b + o_sd, sd.data(), (size_t)nv * 2));
+    HIPCHK(c, c->h2d(b + o_wd, wd.data(), (size_t)nv * 2));
+    const int blocks = (int)std::min<int64_t>(1024, ((int64_t)nv * WS + 255) / 256);
+    hipLaunchKernelGGL(k_put_vertices, dim3(blocks), dim3(256), 0, c->stream, reinterpret_cast<const u64 *>(b),
+                       reinterpret_cast<const uint32_t *>(b + o_idx), reinterpret_cast<const uint16_t *>(b + o_sd),
+                       reinterpret_cast<const uint16_t *>(b + o_wd), nv, WS, c->strong.as<u64>(),
+                       c->sdeg.as<uint16_t>(), c->wdeg.as<uint16_t>());
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, c->upload_suffix());
+  HIPCHK(c, c->sync());
   return DR_OK;
 }
 
@@ -988,20 +1197,10 @@ int run_emit(dr_ctx *c, std::vector<dr::PopDesc> &pd, int npop, const uint64_t *
   return DR_OK;
 }
 
-// Round summaries + canonical cone + canonical prefixes for rounds 0..T
-// (T = last mirrored round).  Reads every strong row and weak edge once; with
-// nwc > 0 the same pass decides the commits of waves 1..nwc (host arrays).
-// fork: the canonical cone and its prefixes run on stream2 (joined by the
-// caller through ev_join) while the caller's next phases use stream.
-// side (optional, with fork): work launched on stream2 right after the summary
-// pass, beside the canonical chain, which then stays on the main stream; ev_join
-// marks its end.  Without side, fork puts the canonical chain on stream2.
-int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
-                  bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr) {
-  const int T = c->nrounds - 1;
-  const int WS = c->WS, dd = c->memo_dd();
-  const size_t R = (size_t)T + 1;
-  if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
+// Summary and canonical-cone buffers, sized once for max_rounds (WU for the
+// current weak window; a wider window reallocates it and rebuilds every round).
+int ensure_summary_bufs(dr_ctx *c) {
+  const size_t R = (size_t)c->max_rounds + 1, WS = c->WS, dd = (size_t)c->memo_dd();
   HIPCHK(c, c->U.ensure(R * WS * 8));
   HIPCHK(c, c->WU.ensure(std::max<size_t>(R * dd * WS, 1) * 8));
   HIPCHK(c, c->SD.ensure(R * 8));
@@ -1015,10 +1214,46 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   HIPCHK(c, c->crbase.ensure((R + 1) * 4));
   HIPCHK(c, c->ccount.ensure(8));
   HIPCHK(c, c->nseg.ensure(4));
-  HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
-  HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
-  HIPCHK(c, c->rec(6));
-  HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
+  HIPCHK(c, c->srounds.ensure(R * 4));
+  return DR_OK;
+}
+
+void mark_rounds_clean(dr_ctx *c) {
+  std::fill(c->sdirty.begin(), c->sdirty.end(), 0);
+  c->ndirty = 0;
+  c->sum_dd = c->memo_dd();
+}
+
+// Incremental round summaries (U, SD, WU) of the rounds appended or changed
+// since they were last built: one workgroup per stale round.  A DAG that left
+// the memo contract (far weak edges, deltas > 17) keeps none.
+int refresh_rounds(dr_ctx *c) {
+  if (!(c->use_memo && c->memo_ok())) return DR_OK;
+  const int T = c->nrounds - 1;
+  if (T < 1) return DR_OK;
+  const int dd = c->memo_dd();
+  const bool all = dd != c->sum_dd;
+  if (!all && c->ndirty == 0) return DR_OK;
+  if (int rc = ensure_summary_bufs(c)) return rc;
+  std::vector<int32_t> list;
+  for (int r = 1; r <= T; r++)
+    if (all || c->sdirty[r]) list.push_back(r);
+  if (!list.empty()) {
+    HIPCHK(c, c->h2d(c->srounds.p, list.data(), list.size() * 4));
+    HIPCHK(c, launch_round_summary(c, c->srounds.as<int32_t>(), (int)list.size()));
+  }
+  mark_rounds_clean(c);
+  return DR_OK;
+}
+
+// Canonical cone K of the current top round + canonical prefixes C, G, E
+// (DESIGN.md s3.2), from fresh round summaries.
+// fork: the canonical chain runs on stream2 (joined by the caller through
+// ev_join) while the caller's next phases use stream.  side (optional, with
+// fork): work launched on stream2 first, beside the canonical chain, which then
+// stays on the main stream; ev_join marks its end.
+int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side) {
+  const int T = c->nrounds - 1;
   struct Swap {  // launch helpers use c->stream: point it at stream2 for the canonical chain
     dr_ctx *c;
     bool on;
@@ -1034,7 +1269,6 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
     if (int rc = (*side)()) return rc;
     HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   }
-  {
   Swap sw(c, fork && !side);
   HIPCHK(c, launch_canon_cone(c, T));
   // canonical emission: per-round counts -> positions -> per-round digests -> prefixes
@@ -1058,34 +1292,16 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
                      c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
   if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
-  }
-  c->summary_T = T;
+  c->canon_T = T;
+  c->canon_ok = true;
   c->canon_host = false;
-  if (!host_out) return DR_OK;  // planned replay: results stay on the device
-  c->hC.resize(R);
-  c->hG.resize(R);
-  c->hE.resize(R);
-  HIPCHK(c, c->d2h(c->hC.data(), c->Cc.p, R * 8));
-  HIPCHK(c, c->d2h(c->hG.data(), c->Gc.p, R * 8));
-  HIPCHK(c, c->d2h(c->hE.data(), c->Ec.p, R * 8));
-  HIPCHK(c, c->d2h(&c->canon_segments, c->nseg.p, 4));
-  if (nwc > 0) {
-    HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nwc));
-    HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nwc * 4));
-  }
-  HIPCHK(c, c->sync());
-  if (ms_summary) {
-    *ms_summary = 0;
-    if (c->timed(6)) HIPCHK(c, hipEventElapsedTime(ms_summary, c->ev[6], c->ev[7]));
-  }
-  c->canon_host = true;
   return DR_OK;
 }
 
 // host copies of the canonical prefixes (after a planned replay left them on the device)
 int fetch_canon(dr_ctx *c) {
   if (c->canon_host) return DR_OK;
-  const size_t R = (size_t)c->summary_T + 1;
+  const size_t R = (size_t)c->canon_T + 1;
   c->hC.resize(R);
   c->hG.resize(R);
   c->hE.resize(R);
@@ -1098,12 +1314,56 @@ int fetch_canon(dr_ctx *c) {
   return DR_OK;
 }
 
+// Bring the round summaries and the canonical cone up to date with the DAG
+// (the per-call path: only stale rounds are re-read).
+int refresh_canon(dr_ctx *c) {
+  if (!(c->use_memo && c->memo_ok()) || c->nrounds < 2) return DR_OK;
+  if (int rc = refresh_rounds(c)) return rc;
+  if (!c->canon_ok) {
+    if (int rc = ensure_summary_bufs(c)) return rc;
+    if (int rc = launch_canon(c, false, nullptr)) return rc;
+  }
+  return fetch_canon(c);
+}
+
+// Full summary pass (dr_replay): every strong row of rounds 1..T read once by
+// k_summary_commit, which with nwc > 0 also decides the commits of waves
+// 1..nwc (host arrays), then the canonical cone and prefixes.  Every replay
+// re-reads the whole DAG; nothing carries over from earlier calls.
+int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
+                  bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr) {
+  const int T = c->nrounds - 1;
+  if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
+  if (int rc = ensure_summary_bufs(c)) return rc;
+  HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
+  HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
+  HIPCHK(c, c->rec(6));
+  HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
+  mark_rounds_clean(c);
+  if (int rc = launch_canon(c, fork, side)) return rc;
+  if (!host_out) return DR_OK;  // planned replay: results stay on the device
+  if (nwc > 0) {
+    HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nwc));
+    HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nwc * 4));
+  }
+  if (int rc = fetch_canon(c)) return rc;  // syncs
+  if (ms_summary) {
+    *ms_summary = 0;
+    if (c->timed(6)) HIPCHK(c, hipEventElapsedTime(ms_summary, c->ev[6], c->ev[7]));
+  }
+  return DR_OK;
+}
+
 }  // namespace
 
 namespace {
-// Summaries usable for this context's current DAG (built lazily / per replay).
-bool summary_fresh(const dr_ctx *c) { return c->use_memo && c->memo_ok() && c->summary_T == c->nrounds - 1; }
-int shortcut_flag(const dr_ctx *c) { return summary_fresh(c) ? dr::Q_SHORTCUT : 0; }
+// Round summaries usable for this context's current DAG (Q_SHORTCUT), and the
+// canonical cone too (Q_MERGE).
+bool rounds_fresh(const dr_ctx *c) {
+  return c->use_memo && c->memo_ok() && c->ndirty == 0 && c->sum_dd == c->memo_dd() && c->nrounds >= 2;
+}
+bool summary_fresh(const dr_ctx *c) { return rounds_fresh(c) && c->canon_ok && c->canon_T == c->nrounds - 1; }
+int shortcut_flag(const dr_ctx *c) { return rounds_fresh(c) ? dr::Q_SHORTCUT : 0; }
 }  // namespace
 
 extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
@@ -1125,55 +1385,34 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
 }
 
 namespace {
-template <int WS, int SV, int NTO = 0>
-hipError_t launch_sv(dr_ctx *c, int T) {
-  constexpr int NT = NTO ? (NTO < 64 * (WS / (WS >= 2 ? 2 : 1)) ? summary_block<WS>() : NTO) : summary_block<WS>();
-  const dr::MemoView mv = c->memo_view();
-  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, SV>), dim3((T + 3) / 4), dim3(NT), 0, c->stream, c->view(), T,
-                     T / 4, mv.dd, 2 * c->f + 1, c->U.as<u64>(), c->WU.as<u64>(), c->SD.as<u64>(),
-                     c->commit.as<uint8_t>(), c->vcount.as<int32_t>());
-  return hipGetLastError();
-}
+// dr_profile_kernel variants of k_summary_commit (WS = 16 geometries; other
+// strides run the shipped one)
 template <int WS>
 hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
-  switch (variant) {
-    case 0: return launch_sv<WS, 0>(c, T);
-    case 1: return launch_sv<WS, dr::SV_NO_WEAK>(c, T);
-    case 2: return launch_sv<WS, dr::SV_NO_ROWS>(c, T);
-    case 3: return launch_sv<WS, dr::SV_UNR8>(c, T);
-    case 4: return launch_sv<WS, 0, 512>(c, T);
-    case 5: return launch_sv<WS, 0, 256>(c, T);
-    case 9: return launch_sv<WS, dr::SV_NO_WEAK, 256>(c, T);
-    case 13: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_GRP16>(c, T);
-    case 14: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_TEMPORAL>(c, T);
-    case 15: return launch_sv<WS, dr::SV_NO_WEAK | dr::SV_GRP16, 1024>(c, T);
-    case 6: case 7: case 8: {  // split: rows + commit beside k_weak_union (6: two streams, 7: one, 8: weak alone)
-      hipError_t e = hipSuccess;
-      if (variant != 8) e = launch_sv<WS, dr::SV_NO_WEAK>(c, T);
-      if (e != hipSuccess) return e;
-      if (variant == 6) {
-        if ((e = hipEventRecord(c->ev_fork, c->stream)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(c->stream2, c->ev_fork, 0)) != hipSuccess) return e;
-      }
-      hipStream_t s2 = variant == 6 ? c->stream2 : c->stream;
-      hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, s2, c->view(), T, c->memo_dd(),
-                         c->WU.as<u64>());
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      if (variant == 6) {
-        if ((e = hipEventRecord(c->ev_join, c->stream2)) != hipSuccess) return e;
-        e = hipStreamWaitEvent(c->stream, c->ev_join, 0);
-      }
-      return e;
+  uint8_t *cm = c->commit.as<uint8_t>();
+  int32_t *vc = c->vcount.as<int32_t>();
+  const int nwc = T / 4;
+  if constexpr (WS == 16) {
+    switch (variant) {
+      case 1: return launch_sc<WS, 512, 8, false>(c, T, nwc, cm, vc);
+      case 2: return launch_sc<WS, 512, 8, true>(c, T, nwc, cm, vc);
+      case 3: return launch_sc<WS, 512, 4, true>(c, T, nwc, cm, vc);
+      case 4: return launch_sc<WS, 1024, 4, true>(c, T, nwc, cm, vc);
+      case 5: return launch_sc<WS, 1024, 8, false>(c, T, nwc, cm, vc);
+      case 6: return launch_sc<WS, 256, 8, true>(c, T, nwc, cm, vc);
+      case 7: return launch_sc<WS, 1024, 2, true>(c, T, nwc, cm, vc);
+      case 8: return launch_sc<WS, 512, 16, false>(c, T, nwc, cm, vc);
+      case 9: return launch_sc<WS, 256, 16, false>(c, T, nwc, cm, vc);
     }
   }
-  return hipErrorInvalidValue;
+  return launch_sc_shipped<WS>(c, T, nwc, cm, vc);
 }
 }  // namespace
 
 // Tuning hook: average device time (HIP events) of `iters` launches of one
 // kernel variant on the resident DAG.  kernel 0: k_summary_commit (variant 0
-// shipped, 1 rows only, 2 weak only, 3 weak unroll 8); kernel 1: streaming read
-// of the strong rows (variant 0) or rows + weak edges (variant 1); kernel 2:
+// shipped, 1-9 the geometries of launch_sv_t); kernel 1: streaming read of the
+// strong rows (variant 0 grid-stride, 2 one block per wave's rows); kernel 2:
 // the whole dr_replay summary phase (k_summary_commit + canonical cone).
 extern "C" int dr_profile_kernel(dr_ctx *c, int kernel, int variant, int iters, float *avg_ms) {
   if (!c || !avg_ms || iters < 1) return DR_E_INVAL;
@@ -1181,9 +1420,7 @@ extern "C" int dr_profile_kernel(dr_ctx *c, int kernel, int variant, int iters, 
   const int T = c->nrounds - 1;
   if (T < 4) return c->fail(DR_E_STATE, "profiling needs a DAG");
   const size_t R = (size_t)T + 1;
-  HIPCHK(c, c->U.ensure(R * c->WS * 8));
-  HIPCHK(c, c->WU.ensure(std::max<size_t>(R * c->memo_dd() * c->WS, 1) * 8));
-  HIPCHK(c, c->SD.ensure(R * 8));
+  if (int rc = ensure_summary_bufs(c)) return rc;
   HIPCHK(c, c->commit.ensure(R));
   HIPCHK(c, c->vcount.ensure(R * 4));
   HIPCHK(c, c->edges.ensure(64));
@@ -1209,10 +1446,6 @@ extern "C" int dr_profile_kernel(dr_ctx *c, int kernel, int variant, int iters, 
       }
       hipLaunchKernelGGL((dr::k_stream_read<256>), dim3(2048), dim3(256), 0, c->stream,
                          reinterpret_cast<const dr::u64x2 *>(c->strong.p), a16, c->edges.as<u64>());
-      hipError_t e = hipGetLastError();
-      if (e != hipSuccess || variant == 0) return e;
-      hipLaunchKernelGGL((dr::k_stream_read<256>), dim3(2048), dim3(256), 0, c->stream,
-                         reinterpret_cast<const dr::u64x2 *>(c->weak.p), c->nweak / 4, c->edges.as<u64>());
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
@@ -1242,6 +1475,7 @@ extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_
   if (!c) return DR_E_INVAL;
   if (q < 0 || (q > 0 && (!from || !to || !out))) return c->fail(DR_E_INVAL, "bad query arrays");
   if (int rc = set_device(c)) return rc;
+  if (int rc = refresh_rounds(c)) return rc;
   std::vector<dr::SweepQuery> qv;
   std::vector<int> idx;
   for (int i = 0; i < q; i++) {
@@ -1273,6 +1507,7 @@ extern "C" int dr_reach_sets(dr_ctx *c, int q, const int32_t *from, const int32_
                              uint64_t *out, size_t cap_words, size_t *out_words) {
   if (!c) return DR_E_INVAL;
   if (int rc = set_device(c)) return rc;
+  if (int rc = refresh_rounds(c)) return rc;
   size_t need = 0;
   for (int i = 0; i < q; i++) {
     const int fr = from[2 * i], b = bottom[i];
@@ -1632,8 +1867,7 @@ extern "C" int dr_buffer_admit(dr_ctx *c, int cur_round, int q, const int32_t *i
   if (int rc = set_device(c)) return rc;
   int ghost_round = INT32_MAX;
   for (int r = 0; r < c->nrounds && ghost_round == INT32_MAX; r++)
-    for (uint32_t sl = c->h_slot_off[r]; sl < c->h_slot_off[r + 1]; sl++)
-      if (c->h_slot_src[sl] == 0) { ghost_round = r; break; }
+    if (c->has_ghost(r)) ghost_round = r;
   const int lim = std::min(cur_round, c->nrounds - 1);
   const size_t nfirst = (size_t)(rhi - rlo + 1) * (c->n + 1);
   const size_t b_ids = (size_t)q * 8, b_off = (size_t)(q + 1) * 4, b_pr = (size_t)std::max<uint32_t>(ne, 1) * 8;
@@ -1665,6 +1899,20 @@ extern "C" int dr_buffer_admit(dr_ctx *c, int cur_round, int q, const int32_t *i
   }
   HIPCHK(c, hipMemcpyAsync(admit, d_adm, q, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  // Go panics.  present() scans p.dag[0..p.round] (process.go:375-376): with
+  // p.round >= len(p.dag) each absent predecessor it evaluates runs off the end,
+  // and a vertex of a round <= p.round that stays buffered evaluated one.  An
+  // admitted vertex of a round >= len(p.dag) panics at p.dag[v.id.round] (:229).
+  for (int i = 0; i < q; i++) {
+    const int r = ids[2 * i];
+    if (r > cur_round) continue;
+    if (!admit[i] && cur_round >= c->nrounds)
+      return c->fail(DR_E_INVAL, "buffered vertex %d (%d,%d): present() scans p.dag[%d] of %d rounds (Go: index out of range)",
+                     i, r, ids[2 * i + 1], cur_round, c->nrounds);
+    if (admit[i] && r >= c->nrounds)
+      return c->fail(DR_E_INVAL, "admitted vertex %d: p.dag[%d] of %d rounds (Go: index out of range)", i, r,
+                     c->nrounds);
+  }
   return DR_OK;
 }
 
@@ -1702,8 +1950,7 @@ extern "C" int dr_set_weak_edges(dr_ctx *c, int round, int nstrong, const int32_
   size_t k = 0;
   bool ghost_edge = false;  // paper: once v has a weak edge to {0,0}, path(v, {0,0}) holds
   for (int r = hi; r >= lo; r--) {
-    for (uint32_t sl = c->h_slot_off[r]; sl < c->h_slot_off[r + 1]; sl++) {
-      const int s = c->h_slot_src[sl];
+    for (const uint16_t s : c->hr[r].slots) {
       bool take;
       if (mode == DR_WEAK_LITERAL) take = s != 0;  // v.id == {0,0}: path() reaches nothing but itself
       else if (s == 0) { take = !ghost_edge; ghost_edge = true; }  // no DAG edge targets {0,0}
@@ -1733,6 +1980,7 @@ extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *com
   if (!c) return DR_E_INVAL;
   if (!commit || !vcount || !n_pushed) return c->fail(DR_E_INVAL, "null output");
   if (int rc = set_device(c)) return rc;
+  if (int rc = refresh_rounds(c)) return rc;
   *n_pushed = 0;
   if (int rc = commit_range(c, wave, wave, commit, vcount, nullptr)) return rc;
   if (!*commit) return DR_OK;
@@ -1765,8 +2013,8 @@ extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack,
     if (cur_round < 1) p.round = std::max(0, std::min(p.round, c->nrounds - 1));
     pops.push_back(p);
   }
-  if (mode == DR_DELIVER_REF && c->use_memo && c->memo_ok() && !summary_fresh(c) && c->nrounds >= 2)
-    if (int rc = build_summary(c, nullptr)) return rc;
+  if (mode == DR_DELIVER_REF)  // stale rounds' summaries + the canonical cone of the current top
+    if (int rc = refresh_canon(c)) return rc;
   std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
   int64_t tot = 0;
   int rc = run_deliver(c, pops, mode, cnt.data(), dg.data(), nullptr, nullptr, out_ids, (int64_t)cap, &tot, nullptr,
@@ -1955,7 +2203,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   o->canon_segments = c->canon_segments;
   uint64_t ce = 0;
   for (int w = 1; w <= nw; w++)
-    if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
+    if (o->vcount[w - 1] >= 0) ce += c->round_deg(4 * w - 2) + c->round_deg(4 * w - 1) + c->round_deg(4 * w);
   o->commit_edges = ce;
   o->chain_edges = h_hdr[dr::PH_CHAIN_E];
   const int64_t np = (int64_t)h_hdr[dr::PH_NPUSH];
@@ -2005,7 +2253,7 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   }
   uint64_t ce = 0;
   for (int w = 1; w <= nwaves; w++)
-    if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
+    if (o->vcount[w - 1] >= 0) ce += c->round_deg(4 * w - 2) + c->round_deg(4 * w - 1) + c->round_deg(4 * w);
   o->commit_edges = ce;
   // 2. chains
   std::vector<ChainTask> tasks;

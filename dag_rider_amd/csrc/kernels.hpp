@@ -3,8 +3,8 @@
 // Device layout, WS = row stride in u64 words = next_pow2(ceil(n/64)):
 //   strong  [rounds][n][WS]  bit t of row (r,s) <=> strong edge (r,s) -> (r-1,t+1)
 //   present [rounds][WS]     bit s-1 <=> source s has a vertex in round r
-//   weak    u32 per edge, grouped by round (weak_roff[r]..weak_roff[r+1]):
-//           bits 0-10 target source-1, 11-21 own source-1, 22-31 delta = r - r'
+//   weak_roff  prefix of each round's weak-edge count (the edges themselves live
+//           in the weak columns below; only counts are needed per edge)
 //   far     u64 per edge with delta > 1023: (own source-1) << 32 | (r' << 11 | t-1)
 //   wc      weak columns, grouped by round (wc_roff[r]..wc_roff[r+1]): one entry per
 //           distinct near weak target of the round, key (delta << 11 | t-1), and a
@@ -52,8 +52,7 @@ struct SweepQuery {
 struct DagView {
   const u64 *strong;
   const u64 *present;
-  const uint32_t *weak;
-  const uint32_t *weak_roff;
+  const uint32_t *weak_roff;  // prefix of weak-edge counts per round (edge accounting)
   const u64 *far;
   const uint32_t *far_roff;
   const uint32_t *wc_key;
@@ -243,65 +242,6 @@ struct MemoView {
   int32_t dd;    // dense weak slots (deltas 2 .. dd+1); 0 with no weak edges
   int32_t dmax;  // merge window = max(1, largest weak delta)
 };
-
-// Walk the weak edges of round r, 16 B (4 edges) per lane, UNR loads in flight
-// per thread.  Edges are stored sorted by (delta, target) (engine.hip, append),
-// so a wave's 256 edges usually hit one destination word: then one wave-wide
-// OR and a single LDS atomic replace 256 of them.  keep(own) filters by source;
-// dest(delta, ts) returns the word index in lds (-1 = not in LDS) and
-// far(delta, ts, bit) handles the rest.  Returns #edges kept.
-template <int NT, int UNR, class Keep, class Dest, class Far>
-__device__ __forceinline__ uint32_t walk_weak(const uint32_t *__restrict__ weak, uint32_t e0, uint32_t e1,
-                                              u64 *lds, Keep keep, Dest dest, Far far) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t a0 = e0 & ~3u;
-  const int nvec = (int)((e1 - a0 + 3) >> 2);
-  const u32x4 *vp = reinterpret_cast<const u32x4 *>(weak + a0);
-  uint32_t kept = 0;
-  for (int v0 = tid; v0 - tid < nvec; v0 += NT * UNR) {  // uniform trip count per workgroup
-    u32x4 q[UNR];
-#pragma unroll
-    for (int k = 0; k < UNR; k++) {
-      const int vi = v0 + k * NT;
-      q[k] = vi < nvec ? __builtin_nontemporal_load(vp + vi) : u32x4{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int k = 0; k < UNR; k++) {
-      const int vi = v0 + k * NT;
-      if (v0 - tid + k * NT >= nvec) break;  // wave-uniform: no lane of this wave has work left
-      const uint32_t xs[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
-      int w0 = -1;
-      u64 acc = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {  // selects, not branches: the common case is one word per lane
-        const uint32_t e = a0 + 4u * (uint32_t)vi + (uint32_t)j;
-        const uint32_t x = xs[j];
-        const int own = (x >> 11) & 2047, ts = x & 2047, delta = (int)(x >> 22);
-        const bool valid = vi < nvec && e >= e0 && e < e1 && keep(own);
-        kept += valid ? 1u : 0u;
-        const u64 bit = 1ULL << (ts & 63);
-        const int dw = valid ? dest(delta, ts) : -2;
-        if (dw == -1) far(delta, ts, bit);  // rare
-        const bool first = dw >= 0 && w0 < 0;
-        const bool same = dw >= 0 && dw == w0;
-        w0 = first ? dw : w0;
-        acc |= (first || same) ? bit : 0ULL;
-        if (dw >= 0 && !first && !same) atomicOr(&lds[dw], bit);  // rare: a second word in one lane
-      }
-      // wave-uniform destination: one OR-reduction + one atomic
-      const u64 nzm = __ballot(w0 >= 0);
-      if (!nzm) continue;
-      const int lead = __builtin_amdgcn_readlane(w0, __builtin_ctzll(nzm));
-      if (__all(w0 < 0 || w0 == lead)) {
-        acc = wave_or(acc);  // lanes without a kept edge hold acc = 0
-        if (lane == 0 && acc) atomicOr(&lds[lead], acc);
-      } else if (w0 >= 0) {
-        atomicOr(&lds[w0], acc);
-      }
-    }
-  }
-  return kept;
-}
 
 // strong rows of the vertices in FE (round r) -> ring slot of round r-1.
 // Loads go out in groups of GRP passes (16 B each), so register use does not grow
@@ -673,110 +613,103 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
 
 // ---------------------------------------------------------------------------
 // k_summary_commit: one workgroup per wave w (rounds 4w-3 .. 4w, clipped to T):
-// the round summaries of k_summary AND waveReady's commit decision of k_commit
-// from one read of each strong row.  The next round's rows are prefetched while
-// the current round's weak edges are walked.  Commit: S_0 = {leader}; for the
-// wave's rounds 2..4, S_k = {v : row(v) & S_{k-1} != 0} by ballot; vcount = |S_3|
-// (process.go:326-339).  Waves past nwc get summaries only.
+// the round summaries U_r (OR of every strong row) and SD_r (strong degree sum)
+// AND waveReady's commit decision from one read of each strong row.  Commit:
+// S_0 = {leader}; for the wave's rounds 2..4, S_k = {v : row(v) & S_{k-1} != 0}
+// by ballot; vcount = |S_3| (process.go:326-339).  Waves past nwc get
+// summaries only.  Each thread owns 16-B chunk column j of rows tid/CPR + p*RPP;
+// loads go out GRP chunks at a time (nontemporal: every row is read once).
+// PIPE: the next group's loads -- the next round's first group at a round end
+// -- are issued before the current group is consumed, so the two barriers that
+// publish a round's U, SD and S overlap the next round's loads.
 // ---------------------------------------------------------------------------
-enum : int { SV_NO_WEAK = 1, SV_NO_ROWS = 2, SV_UNR8 = 4, SV_GRP16 = 8, SV_TEMPORAL = 16 };  // tuning variants (dr_profile_kernel)
-
-template <int WS, int NT, int SV = 0>
-__global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc, int dd, int quorum,
-                                                       u64 *__restrict__ U, u64 *__restrict__ WU,
+template <int WS, int NT, int GRP, bool PIPE>
+__global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc, int quorum, u64 *__restrict__ U,
                                                        u64 *__restrict__ SD, uint8_t *__restrict__ commit,
                                                        int32_t *__restrict__ vcount) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
-  constexpr int GMAX = (SV & SV_GRP16) ? 16 : 8;
-  constexpr int GRP = CPT < GMAX ? CPT : GMAX;  // row chunks in flight per thread
-  __shared__ u64 sU[WS];
-  __shared__ u64 sWU[16 * WS];
-  __shared__ u64 S[WS], Tn[WS], P[WS];
+  constexpr int GR = CPT < GRP ? CPT : GRP;  // chunks per group
+  constexpr int NGR = (CPT + GR - 1) / GR;   // groups per round
+  __shared__ u64 sU[WS], S[WS], Tn[WS], P[WS];
   __shared__ u64 sSD;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, j = tid % CPR, n = g.n;
   const int w = blockIdx.x + 1;
   const int r1 = 4 * (w - 1) + 1;
-  const int rl = min(T, r1 + 3);
+  const int nr = min(T, r1 + 3) - r1 + 1;
   const bool do_commit = w <= nwc;
   const bool leader = do_commit && (g.present[(size_t)r1 * WS] & 1ULL);
-  if (tid < WS) { S[tid] = tid == 0 ? 1ULL : 0ULL; Tn[tid] = 0; }
-  for (int r = r1; r <= rl; r++) {
-    const int k = r - r1;
-    for (int i = tid; i < WS * (dd + 1); i += NT) {
-      if (i < WS) sU[i] = 0;
-      else sWU[i - WS] = 0;
-    }
-    if (tid == 0) sSD = 0;
-    if (tid < WS) P[tid] = g.present[(size_t)r * WS + tid];
-    __syncthreads();
-    const u64 *rows = g.strong + (size_t)r * n * WS;
-    const bool test = leader && k >= 1;
-    const u64 s0 = test ? S[j * CW] : 0ULL, s1 = (test && CW == 2) ? S[j * CW + 1] : 0ULL;
-    u64 a0 = 0, a1 = 0, deg = 0;
-#pragma unroll 1
-    for (int p0 = 0; p0 < CPT; p0 += GRP) {
-      if ((wid * 64) / CPR + p0 * RPP >= n) break;  // wave-uniform: this wave's rows are done
-      if (SV & SV_NO_ROWS) { if (p0 == 0 && !(SV & SV_NO_WEAK)) walk_weak<NT, (SV & SV_UNR8) ? 8 : 4>(
-            g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
-            [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
-        break; }
-      u64 v0[GRP], v1[GRP];
+  if (tid < WS) {
+    sU[tid] = 0;
+    S[tid] = tid == 0 ? 1ULL : 0ULL;
+    Tn[tid] = 0;
+    P[tid] = g.present[(size_t)r1 * WS + tid];
+  }
+  if (tid == 0) sSD = 0;
+  __syncthreads();
+  const int NG = nr * NGR;
+  u64 A0[GR], A1[GR], B0[GR], B1[GR];
+  u64 a0 = 0, a1 = 0, deg = 0, s0 = 0, s1 = 0;
+  bool test = false;
+  auto load = [&](u64 *x0, u64 *x1, int gi) {
+    const int k = gi / NGR, p0 = (gi - k * NGR) * GR;
+    const u64 *rows = g.strong + (size_t)(r1 + k) * n * WS;
 #pragma unroll
-      for (int p = 0; p < GRP; p++) {
+    for (int p = 0; p < GR; p++) {
+      const int s = tid / CPR + (p0 + p) * RPP;
+      x0[p] = 0;
+      x1[p] = 0;
+      if (p0 + p < CPT && s < n) {
+        if constexpr (CW == 2) {
+          const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j));
+          x0[p] = x.x;
+          x1[p] = x.y;
+        } else {
+          x0[p] = __builtin_nontemporal_load(rows + s);
+        }
+      }
+    }
+  };
+  auto round_begin = [&](int k) {  // S_{k-1} is published: the chunk of it this thread tests
+    test = leader && k >= 1;
+    s0 = test ? S[j * CW] : 0ULL;
+    s1 = (test && CW == 2) ? S[j * CW + 1] : 0ULL;
+  };
+  auto consume = [&](const u64 *x0, const u64 *x1, int gi) {
+    const int k = gi / NGR, p0 = (gi - k * NGR) * GR;
+#pragma unroll
+    for (int p = 0; p < GR; p++) {
+      a0 |= x0[p];
+      a1 |= x1[p];
+      deg += (u64)(popc64(x0[p]) + popc64(x1[p]));
+    }
+    if (test) {  // commit: rows of round r that reach S (wave rounds 2..4)
+#pragma unroll
+      for (int p = 0; p < GR; p++) {
+        const int rowbase = (wid * 64) / CPR + (p0 + p) * RPP;
+        if (p0 + p >= CPT || rowbase >= n) break;  // wave-uniform
         const int s = tid / CPR + (p0 + p) * RPP;
-        v0[p] = 0;
-        v1[p] = 0;
-        if (s < n) {
-          if constexpr (CW == 2) {
-            const u64x2 *src = reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j);
-            const u64x2 x = (SV & SV_TEMPORAL) ? *src : __builtin_nontemporal_load(src);
-            v0[p] = x.x;
-            v1[p] = x.y;
+        const bool pres = s < n && ((P[s >> 6] >> (s & 63)) & 1ULL);
+        const bool hit = pres && ((x0[p] & s0) | (x1[p] & s1)) != 0ULL;
+        u64 m = __ballot(hit);
+        if (lane == 0 && m) {
+          u64 bits;
+          if constexpr (CPR == 1) {
+            bits = m;
           } else {
-            v0[p] = (SV & SV_TEMPORAL) ? rows[s] : __builtin_nontemporal_load(rows + s);
+#pragma unroll
+            for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
+            bits = 0;
+#pragma unroll
+            for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
           }
-        }
-      }
-      if (p0 == 0 && !(SV & SV_NO_WEAK))  // this round's weak edges while the first row group is in flight
-        walk_weak<NT, (SV & SV_UNR8) ? 8 : 4>(
-            g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
-            [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
-#pragma unroll
-      for (int p = 0; p < GRP; p++) {
-        a0 |= v0[p];
-        a1 |= v1[p];
-        deg += (u64)(popc64(v0[p]) + popc64(v1[p]));
-      }
-      if (test) {  // commit: rows of round r that reach S (wave rounds 2..4)
-#pragma unroll
-        for (int p = 0; p < GRP; p++) {
-          const int rowbase = (wid * 64) / CPR + (p0 + p) * RPP;
-          if (rowbase >= n) break;  // wave-uniform
-          const int s = tid / CPR + (p0 + p) * RPP;
-          const bool pres = s < n && ((P[s >> 6] >> (s & 63)) & 1ULL);
-          const bool hit = pres && ((v0[p] & s0) | (v1[p] & s1)) != 0ULL;
-          u64 m = __ballot(hit);
-          if (lane == 0 && m) {
-            u64 bits;
-            if constexpr (CPR == 1) {
-              bits = m;
-            } else {
-#pragma unroll
-              for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
-              bits = 0;
-#pragma unroll
-              for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
-            }
-            atomicOr(&Tn[rowbase >> 6], bits << (rowbase & 63));
-          }
+          atomicOr(&Tn[rowbase >> 6], bits << (rowbase & 63));
         }
       }
     }
-    if ((wid * 64) / CPR >= n && !(SV & SV_NO_WEAK))  // waves with no rows still walk the weak edges
-      walk_weak<NT, (SV & SV_UNR8) ? 8 : 4>(
-          g.weak, g.weak_roff[r], g.weak_roff[r + 1], sWU, [](int) { return true; },
-          [&](int delta, int ts) -> int { return (delta - 2) * WS + (ts >> 6); }, [](int, int, u64) {});
+  };
+  auto round_end = [&](int k) {  // publish U_r, SD_r, S_k; load the next round's presence
+    const int r = r1 + k;
     if constexpr (CPR < 16) {
       a0 = row_or_stride<CPR>(a0);
       if constexpr (CW == 2) a1 = row_or_stride<CPR>(a1);
@@ -787,14 +720,38 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
       if (CW == 2 && a1) atomicOr(&sU[(lane & 15) * CW + 1], a1);
     }
     if (lane == 0 && deg) atomicAdd(&sSD, deg);
+    a0 = a1 = deg = 0;
     __syncthreads();
-    for (int i = tid; i < WS * (dd + 1); i += NT) {
-      if (i < WS) U[(size_t)r * WS + i] = sU[i];
-      else if (!(SV & SV_NO_WEAK)) WU[(size_t)r * dd * WS + (i - WS)] = sWU[i - WS];
+    if (tid < WS) {
+      U[(size_t)r * WS + tid] = sU[tid];
+      sU[tid] = 0;
+      if (test) { S[tid] = Tn[tid]; Tn[tid] = 0; }
+      if (k + 1 < nr) P[tid] = g.present[(size_t)(r + 1) * WS + tid];
     }
-    if (tid == 0) SD[r] = sSD;
-    if (test && tid < WS) { S[tid] = Tn[tid]; Tn[tid] = 0; }
+    if (tid == 0) { SD[r] = sSD; sSD = 0; }
     __syncthreads();
+    round_begin(k + 1);
+  };
+  round_begin(0);
+  if constexpr (PIPE) {
+    load(A0, A1, 0);
+    for (int gi = 0; gi < NG; gi += 2) {
+      if (gi + 1 < NG) load(B0, B1, gi + 1);
+      consume(A0, A1, gi);
+      if (gi % NGR == NGR - 1) round_end(gi / NGR);
+      if (gi + 1 >= NG) break;
+      if (gi + 2 < NG) load(A0, A1, gi + 2);
+      consume(B0, B1, gi + 1);
+      if ((gi + 1) % NGR == NGR - 1) round_end((gi + 1) / NGR);
+    }
+  } else {
+    (void)B0;
+    (void)B1;
+    for (int gi = 0; gi < NG; gi++) {
+      load(A0, A1, gi);
+      consume(A0, A1, gi);
+      if (gi % NGR == NGR - 1) round_end(gi / NGR);
+    }
   }
   if (do_commit && tid == 0) {
     if (!leader) {  // leader is bottom (process.go:327-329)
@@ -808,6 +765,54 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
       commit[w - 1] = vc >= quorum ? 1 : 0;
     }
   }
+}
+
+// U_r and SD_r of the listed rounds (the incremental summaries of rounds an
+// append touched): one workgroup per round, the row stream of k_summary_commit
+// without the commit rule.
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_round_summary(DagView g, const int32_t *__restrict__ rounds,
+                                                      u64 *__restrict__ U, u64 *__restrict__ SD) {
+  using G = Geo<WS, NT>;
+  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  __shared__ u64 sU[WS];
+  __shared__ u64 sSD;
+  const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
+  const int r = rounds[blockIdx.x];
+  if (tid < WS) sU[tid] = 0;
+  if (tid == 0) sSD = 0;
+  __syncthreads();
+  const u64 *rows = g.strong + (size_t)r * n * WS;
+  u64 a0 = 0, a1 = 0, deg = 0;
+#pragma unroll 4
+  for (int p = 0; p < CPT; p++) {
+    const int s = tid / CPR + p * RPP;
+    if (s >= n) break;
+    u64 x0, x1 = 0;
+    if constexpr (CW == 2) {
+      const u64x2 x = *reinterpret_cast<const u64x2 *>(rows + (size_t)s * WS + 2 * j);
+      x0 = x.x;
+      x1 = x.y;
+    } else {
+      x0 = rows[s];
+    }
+    a0 |= x0;
+    a1 |= x1;
+    deg += (u64)(popc64(x0) + popc64(x1));
+  }
+  if constexpr (CPR < 16) {
+    a0 = row_or_stride<CPR>(a0);
+    if constexpr (CW == 2) a1 = row_or_stride<CPR>(a1);
+  }
+  deg = wave_sum(deg);
+  if ((lane & 15) < CPR) {
+    if (a0) atomicOr(&sU[(lane & 15) * CW], a0);
+    if (CW == 2 && a1) atomicOr(&sU[(lane & 15) * CW + 1], a1);
+  }
+  if (lane == 0 && deg) atomicAdd(&sSD, deg);
+  __syncthreads();
+  if (tid < WS) U[(size_t)r * WS + tid] = sU[tid];
+  if (tid == 0) SD[r] = sSD;
 }
 
 // ---------------------------------------------------------------------------
@@ -860,12 +865,12 @@ __global__ __launch_bounds__(NT) void k_set_weak(DagView g, int r0, int depth_lo
 }
 
 // WU_r[delta] = the union of round r's weak targets at distance delta, one
-// workgroup per round (the weak half of k_summary_commit as a separate stream:
-// it runs beside the rows + commit pass, k_summary_commit<SV_NO_WEAK>).
+// workgroup per round r = blockIdx.x + 1 (or rounds[blockIdx.x]: incremental).
 template <int WS, int NT>
-__global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64 *__restrict__ WU) {
+__global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64 *__restrict__ WU,
+                                                   const int32_t *__restrict__ rounds) {
   __shared__ u64 sWU[16 * WS];
-  const int r = blockIdx.x + 1, tid = threadIdx.x;
+  const int r = rounds ? rounds[blockIdx.x] : blockIdx.x + 1, tid = threadIdx.x;
   if (r > T) return;
   for (int i = tid; i < dd * WS; i += NT) sWU[i] = 0;
   __syncthreads();

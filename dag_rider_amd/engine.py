@@ -110,6 +110,30 @@ class Engine:
                                                     L.ptr(wo), L.ptr(d.weak_tgt if len(d.weak_tgt) else
                                                                      np.zeros(1, np.uint32))))
 
+    def append_vertices(self, verts: Sequence[Vertex], rounds: Optional[Sequence[int]] = None):
+        """p.dag[v.id.round] = append(p.dag[v.id.round], v) (process.go:229) per vertex, in
+        order; rounds[i] (default v.id.round) is the dag index, == num_rounds opens it."""
+        k = len(verts)
+        if k == 0:
+            return
+        ids = np.asarray([(v.id.round, v.id.source) for v in verts], np.int32).reshape(-1)
+        so = np.zeros(k + 1, np.uint32)
+        wo = np.zeros(k + 1, np.uint32)
+        st: List[int] = []
+        wk: List[int] = []
+        for i, v in enumerate(verts):
+            for e in v.strong_edges:
+                st += [e.round, e.source]
+            for e in v.weak_edges:
+                wk += [e.round, e.source]
+            so[i + 1] = len(st) // 2
+            wo[i + 1] = len(wk) // 2
+        sti = np.asarray(st if st else [0], np.int32)
+        wki = np.asarray(wk if wk else [0], np.int32)
+        rr = None if rounds is None else np.asarray(rounds, np.int32)
+        self._check(self._L.dr_append_vertices(self._h, k, L.ptr(rr), L.ptr(ids), L.ptr(so), L.ptr(sti), L.ptr(wo),
+                                               L.ptr(wki)))
+
     # ---- path(from, to, strongPath)  (process.go:89-148), batched ----
     def path_batch(self, pairs: Sequence[Tuple[Tuple[int, int], Tuple[int, int]]], strong_only: bool) -> np.ndarray:
         q = len(pairs)

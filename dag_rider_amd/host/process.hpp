@@ -5,6 +5,7 @@
 //   vertexID / vertex / block          process/process.go:14-31
 //   New / NewForT                      process/process.go:33-70 (index < 1 -> error)
 //   Process::dag (assign, then query)  process/process.go:79, process_internal_test.go:18
+//   dag.append(r, v)                   p.dag[r] = append(p.dag[r], v), process.go:229
 //   path(from, to, strongPath)         process/process.go:87-148
 //   waveReady(wave)                    process/process.go:312-354
 //   getWaveVertexLeader(w)             process/process.go:356-371
@@ -18,6 +19,10 @@
 // (decidedWave / leadersStack / deliveredVertices persist; the reference's value
 // receivers drop them); the DAG must satisfy the mirrored contract
 // (dr_append_rounds_lists).  All reachability runs on the GPU.
+// The device mirror follows p.dag incrementally: Dag records every append, and
+// the next query streams the new vertices through dr_append_vertices (late
+// vertices into old rounds included); only assigning a whole new DAG
+// re-uploads it.
 #pragma once
 #include <algorithm>
 #include <cstdint>
@@ -93,6 +98,42 @@ class Transport {
   std::vector<std::function<void(const bcastMsg &)>> subs_;
 };
 
+// Process.dag (process.go:79): [][]vertex whose mutations are the reference's
+// two -- assignment (p.dag = dag, process_internal_test.go:18) and append into
+// a round (p.dag[r] = append(p.dag[r], v), process.go:229) -- plus growing by
+// empty rounds.  Existing vertices are read-only, so the log of appends is the
+// whole difference to the device mirror.
+class Dag {
+ public:
+  using Rounds = std::vector<std::vector<vertex>>;
+  Dag() = default;
+  Dag(Rounds d) : r_(std::move(d)) {}
+  Dag &operator=(Rounds d) {
+    r_ = std::move(d);
+    reset_ = true;
+    log_.clear();
+    return *this;
+  }
+  size_t size() const { return r_.size(); }
+  bool empty() const { return r_.empty(); }
+  const std::vector<vertex> &operator[](size_t r) const { return r_[r]; }
+  const Rounds &rounds() const { return r_; }
+  // p.dag[r] = append(p.dag[r], v)
+  void append(size_t r, vertex v) {
+    if (r >= r_.size()) throw panic_error("runtime error: index out of range");
+    r_[r].push_back(std::move(v));
+    log_.emplace_back((int)r, (int)r_[r].size() - 1);
+  }
+  // p.dag = append(p.dag, make([][]vertex, k)...): k more (empty) rounds
+  void grow(size_t k = 1) { r_.resize(r_.size() + k); }
+
+ private:
+  friend class Process;
+  Rounds r_;
+  bool reset_ = true;                     // whole DAG replaced since the last mirror sync
+  std::vector<std::pair<int, int>> log_;  // (round, slot) appended since then
+};
+
 inline int chooseLeader(int) { return 1; }
 inline int waveRound(int w, int k) { return 4 * (w - 1) + k; }
 
@@ -111,8 +152,9 @@ class Process {
     p->tp = tp;
     p->device_ = device;
     // 2f+1 genesis vertices {0, index} (process.go:42-49)
-    p->dag.resize(1);
-    for (int i = 0; i < 2 * faulty + 1; i++) p->dag[0].push_back(vertex{vertexID{0, index}, {}, {}, {}});
+    Dag::Rounds g(1);
+    for (int i = 0; i < 2 * faulty + 1; i++) g[0].push_back(vertex{vertexID{0, index}, {}, {}, {}});
+    p->dag = std::move(g);
     if (err) err->clear();
     return p;
   }
@@ -125,7 +167,7 @@ class Process {
   int index = 0;
   int round = 0;
   int faulty = 0;
-  std::vector<std::vector<vertex>> dag;
+  Dag dag;
   int decidedWave = 0;
   std::vector<vertex> deliveredVertices;
   Stack<vertex> leadersStack = Stack<vertex>::New();
@@ -211,12 +253,28 @@ class Process {
     preds.push_back(0);
     std::vector<uint8_t> admit(buffer.size());
     check(dr_buffer_admit(ctx_, round, (int)buffer.size(), ids.data(), off.data(), preds.data(), admit.data()));
+    // validate every admission before anything moves (Go replaces p.buffer only
+    // after the loop): p.dag[r] in range, and an id the mirror can hold -- Go
+    // would append a second vertex with an id already in the round (path() then
+    // sees the last one), which is outside the mirrored contract
+    std::vector<std::pair<int, int>> seen;
+    for (size_t i = 0; i < buffer.size(); i++) {
+      if (!admit[i]) continue;
+      const vertexID id = buffer[i].id;
+      if (id.round >= (int)dag.size()) throw panic_error("runtime error: index out of range");  // p.dag[r]
+      if (id.round == 0) continue;  // round 0 may repeat ids (genesis)
+      bool dup = std::find(seen.begin(), seen.end(), std::make_pair(id.round, id.source)) != seen.end();
+      for (const vertex &u : dag[id.round]) dup |= u.id == id;
+      if (dup)
+        throw std::runtime_error("dagrider: buffered vertex (" + std::to_string(id.round) + "," +
+                                 std::to_string(id.source) + ") duplicates an id in p.dag[" +
+                                 std::to_string(id.round) + "] (outside the mirrored contract)");
+      seen.emplace_back(id.round, id.source);
+    }
     std::vector<vertex> next;
     for (size_t i = 0; i < buffer.size(); i++) {
-      if (!admit[i]) { next.push_back(std::move(buffer[i])); continue; }
-      const int r = buffer[i].id.round;
-      if (r >= (int)dag.size()) throw panic_error("runtime error: index out of range");  // p.dag[r]
-      dag[r].push_back(std::move(buffer[i]));
+      if (admit[i]) dag.append(buffer[i].id.round, std::move(buffer[i]));
+      else next.push_back(std::move(buffer[i]));
     }
     buffer = std::move(next);
   }
@@ -229,7 +287,7 @@ class Process {
   dr_ctx *ctx_ = nullptr;
   int device_ = 0;
   int n_ = 0;
-  uint64_t fp_ = 0;
+  int cap_rounds_ = 0;
 
   void check(int rc) {
     if (rc == DR_OK) return;
@@ -246,39 +304,28 @@ class Process {
     return *hit;
   }
 
-  uint64_t fingerprint(int *maxsrc) const {
-    uint64_t h = 1469598103934665603ULL;
-    auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ULL; };
-    int ms = 1;
-    mix(dag.size());
-    for (const auto &rnd : dag) {
-      mix(rnd.size());
-      for (const vertex &v : rnd) {
-        mix((uint64_t)(uint32_t)v.id.round << 32 | (uint32_t)v.id.source);
-        mix(v.strongEdges.size());
-        mix(v.weakEdges.size());
-        ms = std::max(ms, v.id.source);
-        for (const auto &e : v.strongEdges) { mix((uint64_t)(uint32_t)e.round << 32 | (uint32_t)e.source); ms = std::max(ms, e.source); }
-        for (const auto &e : v.weakEdges) { mix((uint64_t)(uint32_t)e.round << 32 | (uint32_t)e.source); ms = std::max(ms, e.source); }
-      }
-    }
-    *maxsrc = ms;
-    return h;
+  static int max_source(const vertex &v) {
+    int ms = v.id.source;
+    for (const auto &e : v.strongEdges) ms = std::max(ms, e.source);
+    for (const auto &e : v.weakEdges) ms = std::max(ms, e.source);
+    return ms;
   }
 
-  // Mirror p.dag onto the device when it changed (the reference mutates it in place).
-  void sync(int need_n = 0) {
-    int ms = 1;
-    const uint64_t fp = fingerprint(&ms);
-    if (ctx_ && fp == fp_ && need_n <= n_) return;
+  // Whole-DAG upload into a fresh context (p.dag was assigned, or the mirror
+  // ran out of rounds or sources); room for growth is reserved.
+  void rebuild(int need_n) {
+    int ms = need_n;
+    for (const auto &rnd : dag.r_)
+      for (const vertex &v : rnd) ms = std::max(ms, max_source(v));
     if (ctx_) dr_destroy(ctx_);
     ctx_ = nullptr;
-    n_ = std::max({ms, 3 * faulty + 1, need_n});
-    int rc = dr_create(n_, faulty, (int)std::max<size_t>(dag.size(), 1), device_, &ctx_);
+    n_ = std::max({ms, 3 * faulty + 1, 1});
+    cap_rounds_ = std::max<int>(64, 2 * (int)dag.size());
+    int rc = dr_create(n_, faulty, cap_rounds_, device_, &ctx_);
     if (rc != DR_OK) throw std::runtime_error(std::string("dagrider: ") + dr_last_error(nullptr));
     std::vector<uint32_t> so{0}, sto{0}, wo{0};
     std::vector<int32_t> sid, sti, wi;
-    for (const auto &rnd : dag) {
+    for (const auto &rnd : dag.r_) {
       for (const vertex &v : rnd) {
         sid.push_back(v.id.round);
         sid.push_back(v.id.source);
@@ -293,7 +340,42 @@ class Process {
     wi.push_back(0);
     check(dr_append_rounds_lists(ctx_, 0, (int)dag.size(), so.data(), sid.data(), sto.data(), sti.data(),
                                  wo.data(), wi.data()));
-    fp_ = fp;
+    dag.reset_ = false;
+    dag.log_.clear();
+  }
+
+  // Bring the device mirror up to p.dag: empty rounds opened since, then the
+  // logged appends in order (dr_append_vertices, all or nothing).
+  void sync(int need_n = 0) {
+    bool full = !ctx_ || dag.reset_ || need_n > n_ || (int)dag.size() > cap_rounds_;
+    for (size_t i = 0; !full && i < dag.log_.size(); i++)
+      full = max_source(dag.r_[dag.log_[i].first][dag.log_[i].second]) > n_;
+    if (full) return rebuild(need_n);
+    const int have = dr_num_rounds(ctx_);
+    if ((int)dag.size() > have) {
+      const int k = (int)dag.size() - have;
+      std::vector<uint32_t> so(k + 1, 0), off{0};
+      int32_t zero = 0;
+      check(dr_append_rounds_lists(ctx_, have, k, so.data(), &zero, off.data(), &zero, off.data(), &zero));
+    }
+    if (dag.log_.empty()) return;
+    std::vector<int32_t> sr, sid, sti, wi;
+    std::vector<uint32_t> sto{0}, wo{0};
+    for (const auto &rs : dag.log_) {
+      const vertex &v = dag.r_[rs.first][rs.second];
+      sr.push_back(rs.first);
+      sid.push_back(v.id.round);
+      sid.push_back(v.id.source);
+      for (const auto &e : v.strongEdges) { sti.push_back(e.round); sti.push_back(e.source); }
+      for (const auto &e : v.weakEdges) { wi.push_back(e.round); wi.push_back(e.source); }
+      sto.push_back((uint32_t)sti.size() / 2);
+      wo.push_back((uint32_t)wi.size() / 2);
+    }
+    sti.push_back(0);
+    wi.push_back(0);
+    check(dr_append_vertices(ctx_, (int)sr.size(), sr.data(), sid.data(), sto.data(), sti.data(), wo.data(),
+                             wi.data()));
+    dag.log_.clear();
   }
 };
 

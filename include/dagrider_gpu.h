@@ -98,6 +98,22 @@ int dr_append_rounds_packed(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off
                             const uint16_t *slot_src, const uint64_t *strong,
                             const uint32_t *weak_off, const uint32_t *weak_tgt);
 
+/* p.dag[v.id.round] = append(p.dag[v.id.round], v) (process.go:229), one
+ * vertex at a time, for k vertices in order -- the buffer loop's append, into
+ * any mirrored round, not only new ones.  Vertex i goes to p.dag[r_i], r_i =
+ * slot_round[i] (slot_round may be NULL: r_i = ids[2i], the Go index);
+ * r_i == dr_num_rounds() opens that round, as growing p.dag by one would (a
+ * larger r_i: DR_E_INVAL, Go's index out of range).  Its slot follows the
+ * round's existing slots.  ids[2i], ids[2i+1] = (round, source); strong edges
+ * strong_ids[2e..] for e in [strong_off[i], strong_off[i+1]), weak likewise.
+ * Same contract as dr_append_rounds_lists (else DR_E_CONTRACT): id (r_i, s)
+ * unique in its round, or the ghost {0,0} with no edges.  All or nothing: on
+ * any error the mirror is unchanged.  Only the rounds touched are re-read when
+ * round summaries or the canonical cone are next needed. */
+int dr_append_vertices(dr_ctx *ctx, int k, const int32_t *slot_round, const int32_t *ids,
+                       const uint32_t *strong_off, const int32_t *strong_ids, const uint32_t *weak_off,
+                       const int32_t *weak_ids);
+
 /* path(from, to, strongPath) (process.go:89-148) for q queries at once.
  * out[i] = 1 iff to_i is reachable from from_i (self-path included).
  * from.round outside the mirrored rounds (Go: index out of range) -> DR_E_INVAL. */
@@ -136,7 +152,11 @@ int dr_set_weak_edges(dr_ctx *ctx, int round, int nstrong, const int32_t *strong
  * round_i <= cur_round and every predecessor is present in the mirrored rounds
  * 0..cur_round or is the id of a vertex j < i admitted earlier in the same
  * pass -- exactly the sequential pass.  The caller appends the admitted
- * vertices (buffer order) to the DAG; the rest form the new buffer. */
+ * vertices (buffer order) to the DAG (dr_append_vertices); the rest form the
+ * new buffer.  The pass's Go panics return DR_E_INVAL: with cur_round >=
+ * dr_num_rounds, present() runs off p.dag for any vertex of a round <=
+ * cur_round that stays buffered (process.go:375-376); an admitted vertex of a
+ * round >= dr_num_rounds panics at p.dag[v.id.round] (:229). */
 int dr_buffer_admit(dr_ctx *ctx, int cur_round, int q, const int32_t *ids, const uint32_t *pred_off,
                     const int32_t *preds, uint8_t *admit);
 

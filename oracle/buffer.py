@@ -21,11 +21,16 @@ from typing import List, Sequence, Tuple
 Id = Tuple[int, int]
 
 
+class GoPanic(IndexError):
+    """The reference panics here (runtime error: index out of range)."""
+
+
 def present(dag, cur_round: int, vid: Id) -> bool:
-    """process.go:374-384; dag in oracle.setweak.to_plain() form."""
+    """process.go:374-384; dag in oracle.setweak.to_plain() form.  The scan runs over
+    p.dag[0..p.round]; an id not found before len(p.dag) indexes past it (:376)."""
     for r in range(0, cur_round + 1):
         if r >= len(dag):
-            break  # rounds not mirrored hold no slots
+            raise GoPanic(f"present({vid}): p.dag[{r}] with len {len(dag)}")
         for v in dag[r]:
             if v[0] == vid:
                 return True
@@ -34,7 +39,11 @@ def present(dag, cur_round: int, vid: Id) -> bool:
 
 def admit_pass(dag, cur_round: int, buffer: Sequence[Tuple[Id, Sequence[Id]]]) -> List[int]:
     """One pass of process.go:200-234; buffer = [(id, preds)], preds = strong + weak.
-    Returns admit flags; dag is copied, not modified."""
+    Returns admit flags; dag is copied, not modified.  Raises GoPanic where Go panics:
+    in present() (above) or at p.dag[v.id.round] for an admitted vertex past the DAG.
+    all() stops at the first absent predecessor; Go evaluates strong edges to the
+    first absent one, then weak edges to the first absent one -- either way the first
+    absent predecessor evaluated is the one that panics."""
     dag = [list(rnd) for rnd in dag]
     out = []
     for vid, preds in buffer:
@@ -42,8 +51,8 @@ def admit_pass(dag, cur_round: int, buffer: Sequence[Tuple[Id, Sequence[Id]]]) -
             out.append(0)
             continue
         if all(present(dag, cur_round, p) for p in preds):
-            while len(dag) <= vid[0]:
-                dag.append([])
+            if vid[0] >= len(dag):
+                raise GoPanic(f"p.dag[{vid[0]}] = append(...) with len {len(dag)}")
             dag[vid[0]].append((tuple(vid), [], []))
             out.append(1)
         else:

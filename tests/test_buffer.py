@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import oracle
+from dag_rider_amd import _lib as L
 from dag_rider_amd.engine import Engine
 from dagutil import figure1, random_dag
 
@@ -23,14 +24,24 @@ def test_oracle_figure1_pass():
     assert B.present(plain, 4, (4, 1)) and B.present(plain, 4, (0, 0))
     assert not B.present(plain, 3, (4, 1))  # present() scans rounds 0..p.round only
     assert not B.present(plain, 4, (2, 5))
+    with pytest.raises(B.GoPanic):  # absent id with p.round >= len(p.dag): the scan runs off the end
+        B.present(plain, 5, (2, 5))
+    assert B.present(plain, 7, (4, 1))  # found before the end: no panic
+    grown = plain + [[], [], []]  # p.dag with rounds 5..7 opened
     buf = [((5, 1), [(4, 1), (4, 2)]),          # present preds -> admitted
            ((6, 1), [(5, 1), (5, 2)]),          # (5,2) arrives later in the pass -> stays
            ((5, 2), [(4, 3), (0, 0)]),          # ghost id is present -> admitted
            ((6, 2), [(5, 1), (5, 2)]),          # both admitted earlier in this pass
            ((7, 1), []),                        # ahead of p.round -> stays
            ((5, 3), [(4, 9)])]                  # unknown predecessor -> stays
-    assert B.admit_pass(plain, 6, buf) == [1, 0, 1, 1, 0, 0]
-    assert B.admit_pass(plain, 5, buf) == [1, 0, 1, 0, 0, 0]  # round 6 > p.round
+    assert B.admit_pass(grown, 6, buf) == [1, 0, 1, 1, 0, 0]
+    assert B.admit_pass(grown, 5, buf) == [1, 0, 1, 0, 0, 0]  # round 6 > p.round
+    assert B.admit_pass(plain, 4, buf) == [0, 0, 0, 0, 0, 0]
+    for cur in (5, 6):  # (5,1) admitted into p.dag[5] of a 5-round DAG
+        with pytest.raises(B.GoPanic):
+            B.admit_pass(plain, cur, buf)
+    with pytest.raises(B.GoPanic):  # (5,3)'s absent predecessor scanned past p.dag[7]
+        B.admit_pass(grown, 8, buf)
 
 
 def _random_buffer(rng, plain, n, R, q):
@@ -58,6 +69,19 @@ def _random_buffer(rng, plain, n, R, q):
     return buf
 
 
+def _expect(e, cur, buf, plain):
+    """GPU admit flags == the oracle's, or DR_E_INVAL where the oracle panics."""
+    try:
+        want = B.admit_pass(plain, cur, buf)
+    except B.GoPanic:
+        with pytest.raises(L.DrError) as ei:
+            e.buffer_admit(cur, buf)
+        assert ei.value.code == L.DR_E_INVAL, cur
+        return "panic"
+    assert e.buffer_admit(cur, buf).tolist() == want, cur
+    return want
+
+
 @pytest.mark.gpu
 def test_gpu_buffer_figure1(gpu_device):
     g, dag = figure1()
@@ -66,9 +90,13 @@ def test_gpu_buffer_figure1(gpu_device):
            ((6, 2), [(5, 1), (5, 2)]), ((7, 1), []), ((5, 3), [(4, 9)])]
     with Engine(g["n"], g["faulty"], 8, gpu_device) as e:
         e.append_lists(dag)
-        for cur in (3, 4, 5, 6, 7):
-            assert e.buffer_admit(cur, buf).tolist() == B.admit_pass(plain, cur, buf), cur
+        got = {cur: _expect(e, cur, buf, plain) for cur in (3, 4, 5, 6, 7)}
+        assert got[5] == got[6] == got[7] == "panic"
         assert e.buffer_admit(4, []).tolist() == []
+        e.append_lists(dag + [[], [], []])  # open rounds 5..7 (p.dag grown)
+        grown = plain + [[], [], []]
+        got = {cur: _expect(e, cur, buf, grown) for cur in (3, 4, 5, 6, 7, 8)}
+        assert got[6] == [1, 0, 1, 1, 0, 0] and got[8] == "panic"
 
 
 @pytest.mark.gpu
@@ -77,10 +105,15 @@ def test_gpu_buffer_random(gpu_device, seed, n, R, q):
     rng = np.random.default_rng(500 + seed)
     d = random_dag(rng, n, R, p_present=0.8, p_s=0.35, p_w=0.15, max_depth=6)
     plain = oracle.setweak.to_plain(d.to_lists())
+    grown = plain + [[], []]
     with Engine(n, (n - 1) // 3, R + 4, gpu_device) as e:
         e.append_packed(d)
         for _ in range(3):
             buf = _random_buffer(rng, plain, n, R, q)
             for cur in (R - 2, R - 1, R + 1):
-                got = e.buffer_admit(cur, buf).tolist()
-                assert got == B.admit_pass(plain, cur, buf), (seed, cur)
+                _expect(e, cur, buf, plain)
+        e.append_lists(d.to_lists() + [[], []])  # rounds R+1, R+2 opened
+        for _ in range(2):
+            buf = _random_buffer(rng, plain, n, R, q)
+            for cur in (R - 1, R + 1, R + 2, R + 3):
+                _expect(e, cur, buf, grown)
