@@ -1,17 +1,26 @@
-"""Benchmark: DAG edges traversed/sec (commit + delivery) on MI355X.
+"""Benchmark: DAG edges traversed/sec (commit+delivery) on MI355X.
 
-Workload (BASELINE.json configs[3], the metric's n=1024 case; fits one GPU): the
-synthetic C4 DAG, n=1024 processes x 4000 rounds, replayed end to end through the
-C ABI: waveReady for all 1000 waves (commit sweep + leader chains,
-decidedWave persistent) and orderVertices for every committed leader
-(DR_DELIVER_REF: each pop delivers its full causal history, as the reference's
-no-op dedup does).  One step = one dr_replay of the resident DAG.  Edges are
-counted by SURVEY.md s8(d)'s formula (the same numbers the CPU oracle reports).
+Default workload (BASELINE.json configs[3], the metric's n=1024 case; fits one GPU):
+the synthetic C4 DAG, n=1024 processes x 4000 rounds, replayed end to end through
+the C ABI: waveReady for all 1000 waves (commit sweep + leader chains, decidedWave
+persistent) and orderVertices for every committed leader (DR_DELIVER_REF: each pop
+delivers its full causal history, as the reference's no-op dedup does).  One step =
+one dr_replay of the resident DAG.  Edges are counted by SURVEY.md s8(d)'s formula
+(the same numbers the CPU oracle reports).
 
-N>1 (torchrun, one rank per GPU): each rank replays its own independent C4 DAG
-(seed 4+rank): independent units, no data-path collective ("scaling": "weak").
-After the timed region, N>1 also runs the process-column sharded sweep of one C4
-DAG across all ranks (RCCL all-gather of the frontier per round; detail.colshard).
+Other lines (--config): c3 (n=256 x 10k rounds, weak-heavy: the metric's other
+half), c2, c5 (4096 independent n=128 replays, split across ranks), c4-deep (weak
+edges past the memo window: every pop sweeps its cone), c4-loop (the drop-in call
+pattern: per wave append 4 rounds -> dr_wave_ready -> dr_order_vertices, per-wave
+latency), --deliver paper (dedup across pops).
+
+--gpus N without torchrun: spawns N ranks (torch.distributed.run) before anything
+touches a GPU; under torchrun WORLD_SIZE must equal N.  Each rank replays its own
+independent C4 DAG (seed 4+rank): independent units, no data-path collective
+("scaling": "weak").  After the timed region N>1 also runs (a) the all-waves commit
+sweep of ONE C4 DAG split into wave ranges, one per GPU (detail.commit_split), and
+(b) the process-column sharded reach sweep with an RCCL all-gather per round
+(detail.colshard).
 
 Prints ONE JSON line on rank 0.
 """
@@ -20,6 +29,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -29,11 +39,12 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950
 # correction of MI355X_MICROARCH.md) on this bench: tools/pmc_traffic.py output
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02", "traffic.json")
 # replay phase -> the kernels it launches (names as rocprofv3 reports them)
-PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 512, 1>"],
+PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 1024, 2, true>"],
                  "sweep": ["dr::k_sweep<16, 256, 9>"],
                  "batch": ["dr::k_replay_small<8, false, true>"]}
+CPU_THREADS = 16  # the GPU box's host share for one GPU (OMP_NUM_THREADS there)
 
 
 def measured_traffic(phase):
@@ -50,43 +61,97 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg, d, budget_s: float):
-    """Time the oracle's literal restatement of process.go (the reference algorithm:
-    BFS + hash-set visited + linear id scans, one BFS per delivery candidate) on a
-    bounded sample: a full replay of the first k waves, k grown until the budget."""
+def cpu_info():
+    """Host CPU model and the cores this process may use (recorded with every baseline)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return dict(model=model, nproc=os.cpu_count(), affinity=aff, omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
+
+
+def _median_runs(fn, runs):
+    ts, out = [], None
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), ts, out
+
+
+def cpu_literal(cfg, d, budget_s: float, full_edges: int, deliver_mode: int):
+    """The oracle's literal restatement of process.go (the reference's algorithm: BFS +
+    hash-set visited + linear id scans, one BFS per orderVertices candidate) on a bounded
+    sample: a replay of waves 1..k.  Single thread (the reference is one goroutine) and
+    one thread per core (candidates' BFSs in parallel); median of 5 runs each.  The
+    literal cost grows ~ w^2 per wave, so two extrapolations to the full replay are
+    given: per edge at the sample's rate (a lower bound) and by a power law fitted to
+    the per-wave times of waves 1..k."""
     import oracle
 
-    best = None
-    k = 1
-    while k <= cfg.nwaves:
+    nt = min(CPU_THREADS, cpu_info()["affinity"] or 1)
+    # multi-thread: grow k until one replay takes ~budget/12
+    k, per_wave, prev = 1, [], 0.0
+    while True:
         ld = oracle.LDag(packed=d, nrounds=4 * k + 1)
         t0 = time.perf_counter()
-        r = ld.replay(cfg.faulty, k, oracle.CHAIN_PERSISTENT, oracle.DELIVER_REF)
+        r = ld.replay(cfg.faulty, k, oracle.CHAIN_PERSISTENT, deliver_mode, nthreads=nt)
         dt = time.perf_counter() - t0
         assert r.rc == 0
-        edges = r.commit_edges + r.deliver_edges  # literal restatement does not count chain edges
-        best = dict(value=edges / dt, unit="edges/s", cores=1, kind="port",
-                    sample=f"C4 waves 1..{k} (rounds 0..{4 * k}) literal replay: {edges} edges in {dt:.2f} s, "
-                           f"single thread, oracle/ref_literal.c")
-        if dt * 6 > budget_s:  # the next wave costs several times more (cone grows)
+        per_wave.append(max(dt - prev, 1e-9))
+        prev = dt
+        if dt * 3 > budget_s / 12 or k >= min(cfg.nwaves, 8):
             break
         k += 1
-    return best
+    ld = oracle.LDag(packed=d, nrounds=4 * k + 1)
+    mt_med, mt_ts, r = _median_runs(
+        lambda: ld.replay(cfg.faulty, k, oracle.CHAIN_PERSISTENT, deliver_mode, nthreads=nt), 5)
+    edges = r.commit_edges + r.deliver_edges  # the literal restatement does not count chain edges
+    # single thread on the first wave only (its cost is known from the multi-thread run)
+    ld1 = oracle.LDag(packed=d, nrounds=5)
+    st_med, st_ts, r1 = _median_runs(lambda: ld1.replay(cfg.faulty, 1, oracle.CHAIN_PERSISTENT, deliver_mode), 5)
+    e1 = r1.commit_edges + r1.deliver_edges
+    # power-law fit t(w) = a w^b over the multi-thread per-wave times
+    import math
+
+    if len(per_wave) >= 2:
+        b = math.log(per_wave[-1] / per_wave[0]) / math.log(len(per_wave))
+    else:
+        b = 2.0
+    a = per_wave[0]
+    fit_full = sum(a * (w ** b) for w in range(1, cfg.nwaves + 1)) * (st_med / max(per_wave[0], 1e-9))
+    return dict(value=e1 / st_med, unit="edges/s", cores=1, kind="port",
+                sample=f"{cfg.name} waves 1..1 (rounds 0..4) literal replay (oracle/ref_literal.c, the reference's "
+                       f"algorithm), single thread: {e1} edges, median {st_med:.2f} s of 5 runs",
+                runs_s=st_ts,
+                all_cores=dict(value=edges / mt_med, cores=nt, waves=k, edges=edges, median_s=mt_med, runs_s=mt_ts,
+                               per_wave_s=per_wave),
+                extrapolated_full_s_per_edge=full_edges / (e1 / st_med),
+                extrapolated_full_s_fit=fit_full, fit_exponent=b, host=cpu_info())
 
 
-def cpu_bitset(cfg, d, nthreads: int, budget_s: float):
-    """The optimized CPU restatement (packed bitsets, OpenMP) on a bounded sample of pops."""
+def cpu_bitset(cfg, d, nthreads: int, full_runs: int, deliver_mode: int):
+    """The optimized CPU restatement (packed bitsets, OpenMP): the full replay, median of runs."""
     import oracle
 
     bs = oracle.PDag(d)
-    k = max(1, cfg.nwaves // 16)
-    t0 = time.perf_counter()
-    r = bs.replay(cfg.faulty, k, oracle.CHAIN_PERSISTENT, oracle.DELIVER_REF, nthreads=nthreads)
-    dt = time.perf_counter() - t0
+    med, ts, r = _median_runs(lambda: bs.replay(cfg.faulty, cfg.nwaves, oracle.CHAIN_PERSISTENT, deliver_mode,
+                                                nthreads=nthreads), full_runs)
     assert r.rc == 0
     e = r.commit_edges + r.chain_edges + r.deliver_edges
-    return dict(value=e / dt, unit="edges/s", cores=nthreads, kind="port",
-                sample=f"C4 waves 1..{k} bitset replay (oracle/ref_bitset.c, OpenMP): {e} edges in {dt:.2f} s")
+    return dict(value=e / med, unit="edges/s", cores=nthreads, kind="port",
+                sample=f"{cfg.name} full replay ({cfg.nwaves} waves) bitset restatement (oracle/ref_bitset.c, "
+                       f"OpenMP {nthreads} threads): {e} edges, median {med:.3f} s of {full_runs} runs",
+                runs_s=ts), r
 
 
 def kernel_bytes(cfg, d, res):
@@ -95,7 +160,7 @@ def kernel_bytes(cfg, d, res):
     leaders = int((res.vcount >= 0).sum())
     dd = max(0, weak_depth(d) - 1)
     sw = res.sweep
-    out = {
+    return {
         # k_summary_commit: every strong row of rounds 1..T read once; U and SD written
         # (the weak-column keys -> WU pass, k_weak_union, runs after it, ~4 us, untimed here)
         "summary": dict(kernel="k_summary_commit (rows -> U, SD + waveReady commit rule)", ms=res.ms["summary"],
@@ -109,7 +174,6 @@ def kernel_bytes(cfg, d, res):
                       bytes=sw["row_bytes"] + sw["weak_scanned"] * (W * 8 + 4) + sw["shortcut"] * (1 + dd) * W * 8
                       + (sw["partial"] + sw["shortcut"]) * 3 * W * 8),
     }
-    return out
 
 
 def weak_columns(d):
@@ -160,6 +224,73 @@ def reduce_over_ranks(dist, dt: float, edges: int, device: str):
     return float(t.item()), float(e.item())
 
 
+def wave_slice(d, w0: int, w1: int):
+    """The rounds waves w0..w1 read for their commit decisions, as a DAG of its own:
+    round 4(w0-1) .. 4 w1 shifted to 0 .. 4(w1-w0+1) (round 0 keeps presence only; weak
+    edges dropped: the commit rule follows strong edges inside the wave)."""
+    import numpy as np
+
+    from dag_rider_amd.dag import PackedDag
+
+    n, W = d.n, d.W
+    lo, hi = 4 * (w0 - 1), 4 * w1
+    so = d.slot_off[lo:hi + 2].astype(np.int64)
+    strong = d.strong[lo * n * W:(hi + 1) * n * W].copy()
+    strong[:n * W] = 0
+    k = hi - lo + 1
+    return PackedDag(n, k, (so - so[0]).astype(np.uint32), d.slot_src[so[0]:so[-1]].copy(), strong,
+                     np.zeros(k * n + 1, np.uint32), np.zeros(0, np.uint32))
+
+
+def commit_split(dist, rank: int, world: int, local: int, want_commit=None, want_vcount=None, iters: int = 20):
+    """the all-waves commit sweep of ONE C4 DAG (seed 4), waves
+    split into contiguous ranges, one per GPU, each GPU holding only its rounds; no
+    exchange.  Returns rank 0's view: max time over ranks, bit-exact check of the
+    gathered commits against the full replay on rank 0."""
+    import numpy as np
+    import torch
+
+    from dag_rider_amd.engine import Engine
+    from dag_rider_amd.gen import CONFIGS, generate
+
+    cfg = CONFIGS["c4"]
+    d = generate(cfg, nthreads=CPU_THREADS)
+    nw = cfg.nwaves
+    w0, w1 = rank * nw // world + 1, (rank + 1) * nw // world
+    sub = wave_slice(d, w0, w1)
+    with Engine(cfg.n, cfg.faulty, sub.nrounds, local) as e:
+        e.append_packed(sub)
+        cm, vc = e.wave_commit(1, w1 - w0 + 1)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            cm, vc = e.wave_commit(1, w1 - w0 + 1)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
+    mine = dict(rank=rank, w0=w0, w1=w1, commit=cm.tolist(), vcount=vc.tolist(), ms=dt * 1e3)
+    allr = [None] * world
+    if dist:
+        dist.all_gather_object(allr, mine)
+    else:
+        allr = [mine]
+    if rank != 0:
+        return None
+    cmt = np.concatenate([np.asarray(r["commit"], np.uint8) for r in allr])
+    vct = np.concatenate([np.asarray(r["vcount"], np.int32) for r in allr])
+    ok = None
+    if want_commit is not None:
+        ok = bool((cmt == want_commit).all() and (vct == want_vcount).all())
+    ms = max(r["ms"] for r in allr)
+    n, W = cfg.n, (cfg.n + 63) // 64
+    leaders = int((vct >= 0).sum())
+    alg = leaders * (n * 16 + 2 * n * W * 8)  # k_commit: the leader's chunk of round 4w-2, rounds 4w-1, 4w whole
+    return dict(waves=nw, ranges=[(r["w0"], r["w1"]) for r in allr], ms_max_over_ranks=ms,
+                waves_per_s=nw / (ms / 1e3), algorithmic_bytes=alg, GBps=alg / (ms / 1e3) / 1e9,
+                verify_vs_full_replay=ok, note="dr_wave_commit (k_commit) per rank, wall clock incl. D2H")
+
+
 def colshard_child(args):
     """One rank of the process-column sharded sweep: every rank
     holds 1/N of the target columns; the frontier is all-gathered over RCCL each round.
@@ -171,7 +302,7 @@ def colshard_child(args):
     from dag_rider_amd.shard import ShardEngine
 
     cfg = CONFIGS["c4"]
-    d = generate(cfg, nthreads=16)
+    d = generate(cfg, nthreads=CPU_THREADS)
     se = ShardEngine(cfg.n, cfg.faulty, d.nrounds, args.cs_device, args.cs_world, args.cs_rank,
                      bytes.fromhex(args.cs_uid))
     se.append_packed(d)
@@ -233,7 +364,7 @@ def colshard_check(dist, rank: int, world: int, local: int, timeout_s: float = 2
 def run_c5(args, rank: int, world: int, local: int, dist):
     """C5 (BASELINE.json configs[4]): the fixed batch of 4096 independent n=128 x 128-round
     replays (seeds 5000+i), split across ranks (strong scaling); each rank replays its
-    DAGs as one fused dr_replay_batch launch (one wavefront per DAG, batch.hpp)."""
+    DAGs as one fused dr_replay_batch launch (batch.hpp)."""
     import torch
 
     from dag_rider_amd import _lib as L
@@ -243,17 +374,18 @@ def run_c5(args, rank: int, world: int, local: int, dist):
     total = 4096
     lo, hi = rank * total // world, (rank + 1) * total // world
     t0 = time.perf_counter()
-    engines, dag_bytes = [], 0
+    engines, dags, dag_bytes = [], [], 0
     for i in range(lo, hi):
         cfg = c5_config(i)
         d = generate(cfg)
         e = Engine(cfg.n, cfg.faulty, d.nrounds, local)
         e.append_packed(d)
         engines.append(e)
+        dags.append(d)
         dag_bytes += d.nrounds * cfg.n * d.W * 8 + weak_columns(d) * (4 + d.W * 8)
     log(f"[rank {rank}] C5 DAGs {lo}..{hi - 1} loaded in {time.perf_counter() - t0:.1f} s")
     nw = c5_config(0).nwaves
-    b = ReplayBatch(engines, nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+    b = ReplayBatch(engines, nw, L.DR_CHAIN_PERSISTENT, args.deliver_mode)
     for _ in range(args.warmup):
         b.run()
     if dist:
@@ -271,6 +403,9 @@ def run_c5(args, rank: int, world: int, local: int, dist):
     dt, total_edges = reduce_over_ranks(dist, time.perf_counter() - t0, edges, "cuda")
     if rank != 0:
         return None
+    cpu = None
+    if not args.no_cpu and world == 1:
+        cpu = cpu_c5(dags, args.deliver_mode, res)
     ach = dag_bytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
     return {
         "metric": "DAG edges traversed/sec (commit+delivery)",
@@ -285,33 +420,194 @@ def run_c5(args, rank: int, world: int, local: int, dist):
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (seeded generator, SURVEY.md s8(d) C5 parameters, seeds 5000+i)",
-        "config": {"workload": "C5: 4096 independent n=128 x 128-round replays (waveReady + orderVertices ref, "
-                               "persistent decidedWave), split across ranks",
+        "config": {"workload": "C5: 4096 independent n=128 x 128-round replays (waveReady + orderVertices "
+                               f"{'paper' if args.deliver_mode else 'ref'}, persistent decidedWave), split across ranks",
                    "dags": total, "dags_per_rank": hi - lo, "n": 128, "rounds": 128, "waves": nw,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "roofline": {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic("batch"),
-                     "kernel": "k_replay_small (one wavefront per DAG)",
+                     "kernel": "k_replay_small (batch.hpp)",
                      "bytes_per_launch": dag_bytes, "ms_per_launch": kms,
                      "note": "unique DAG bytes (strong rows + weak columns) once per launch"},
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
         "detail": {"edges_per_step": edges, "commits": int(sum(int(r.commit.sum()) for r in res)),
                    "pops": int(sum(len(r.pop_count) for r in res))},
     }
 
 
-def main():
+def cpu_c5(dags, deliver_mode, gpu_res, sample: int = 64):
+    """C5 on the host: the literal restatement on the first `sample` DAGs, one DAG per
+    thread (independent replays, all cores), and the bitset restatement on all 4096
+    DAGs likewise; both checked against the GPU's per-DAG outputs."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import oracle
+
+    nt = min(CPU_THREADS, cpu_info()["affinity"] or 1)
+    f = (dags[0].n - 1) // 3
+    nw = (dags[0].nrounds - 1) // 4
+
+    def lit(i):
+        return oracle.LDag(packed=dags[i]).replay(f, nw, oracle.CHAIN_PERSISTENT, deliver_mode)
+
+    def bit(i):
+        return oracle.PDag(dags[i]).replay(f, nw, oracle.CHAIN_PERSISTENT, deliver_mode, nthreads=1)
+
+    out = {}
+    for name, fn, k in (("literal", lit, min(sample, len(dags))), ("bitset", bit, len(dags))):
+        ts = []
+        for _ in range(3 if name == "literal" else 5):
+            t0 = time.perf_counter()
+            with ThreadPoolExecutor(nt) as ex:
+                rs = list(ex.map(fn, range(k)))
+            ts.append(time.perf_counter() - t0)
+        med = statistics.median(ts)
+        e = sum(r.commit_edges + (r.chain_edges if name == "bitset" else 0) + r.deliver_edges for r in rs)
+        same = all((r.pop_digest == g.pop_digest).all() and (r.commit == g.commit).all()
+                   for r, g in zip(rs, gpu_res[:k]))
+        out[name] = dict(value=e / med, unit="edges/s", cores=nt, kind="port", dags=k, median_s=med, runs_s=ts,
+                         matches_gpu=bool(same))
+    lt = out["literal"]
+    return dict(value=lt["value"], unit="edges/s", cores=nt, kind="port",
+                sample=f"C5 DAGs 0..{lt['dags'] - 1} literal replay (oracle/ref_literal.c), one DAG per thread on "
+                       f"{nt} threads, median of 3 runs",
+                bitset_all_dags=out["bitset"], literal=lt, host=cpu_info())
+
+
+def run_loop(args, local: int):
+    """The drop-in call pattern on C4 (the reference's Start loop wired as Alg. 3): for
+    each wave w the 4 new rounds are appended (dr_append_rounds_packed), waveReady(w)
+    runs (dr_wave_ready: incremental round summaries, commit rule, leader chain) and
+    on commit orderVertices delivers the pushed leaders (dr_order_vertices: the
+    canonical cone of the new top, per-pop counts and digests).  Per-wave latency;
+    outputs checked against one dr_replay of the whole DAG."""
+    import numpy as np
+    import torch
+
+    from dag_rider_amd import _lib as L
+    from dag_rider_amd.engine import Engine
+    from dag_rider_amd.gen import CONFIGS, generate
+
+    cfg = CONFIGS["c4"]
+    d = generate(cfg, nthreads=CPU_THREADS)
+    nw = cfg.nwaves if args.loop_waves <= 0 else min(args.loop_waves, cfg.nwaves)
+
+    def one_pass(e):
+        e.append_packed(d, 0, 1)
+        decided = 0
+        lat = {"append": [], "wave_ready": [], "order_vertices": [], "wave": []}
+        commit, vcount, pushes, pc, pdg = [], [], [], [], []
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        for w in range(1, nw + 1):
+            t0 = time.perf_counter()
+            e.append_packed(d, 4 * w - 3, 4 * w + 1)
+            t1 = time.perf_counter()
+            cm, vc, pushed = e.wave_ready(w, decided)
+            t2 = time.perf_counter()
+            commit.append(cm)
+            vcount.append(vc)
+            if cm:
+                pushes += pushed
+                _, cnt, dg = e.order_vertices([(4 * (x - 1) + 1, 1) for x in pushed], 4 * w, L.DR_DELIVER_REF,
+                                              cap=0)
+                pc += cnt.tolist()
+                pdg += dg.tolist()
+                decided = w
+            t3 = time.perf_counter()
+            lat["append"].append(t1 - t0)
+            lat["wave_ready"].append(t2 - t1)
+            lat["order_vertices"].append(t3 - t2)
+            lat["wave"].append(t3 - t0)
+        total = time.perf_counter() - t_start
+        return total, lat, (np.asarray(commit, np.uint8), np.asarray(vcount, np.int32), pushes, pc, pdg)
+
+    # warm-up pass (first-call costs), then the measured pass on a fresh mirror
+    with Engine(cfg.n, cfg.faulty, 4 * nw + 1, local) as e:
+        one_pass(e)
+    with Engine(cfg.n, cfg.faulty, 4 * nw + 1, local) as e:
+        total, lat, (cm, vc, pushes, pc, pdg) = one_pass(e)
+        ref = e.replay(nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+    ok = bool((cm == ref.commit).all() and (vc == ref.vcount).all() and pushes == ref.push_wave.tolist()
+              and pc == ref.pop_count.tolist() and pdg == ref.pop_digest.tolist())
+
+    def pct(x):
+        a = np.asarray(x) * 1e6
+        return dict(p50=float(np.percentile(a, 50)), p90=float(np.percentile(a, 90)),
+                    p99=float(np.percentile(a, 99)), mean=float(a.mean()), max=float(a.max()))
+
+    edges = ref.total_edges
+    return {
+        "metric": "DAG edges traversed/sec (commit+delivery)",
+        "value": edges / total,
+        "unit": "edges/s",
+        "n_gpus": 1,
+        "steps": 1,
+        "warmup": 1,
+        "ms_per_step": total * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded generator, SURVEY.md s8(d) C4 parameters)",
+        "config": {"workload": f"C4 per-wave drop-in loop, waves 1..{nw}: append 4 rounds -> dr_wave_ready -> "
+                               "dr_order_vertices (ref, counts + digests), host wall clock per call",
+                   "n": cfg.n, "rounds": 4 * nw, "waves": nw, "parallelism": "single"},
+        "roofline": None,
+        "cpu_baseline": None,
+        "detail": {"latency_us": {k: pct(v) for k, v in lat.items()}, "verify_vs_replay": ok,
+                   "edges": edges, "commits": int(cm.sum()), "pops": len(pc)},
+    }
+
+
+def spawn_ranks(args) -> int:
+    """bench.py --gpus N outside torchrun: N ranks via torch.distributed.run, started
+    before this process touches a GPU; their exit status is ours."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] spawning {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd)
+
+
+def dist_selftest(rank: int, world: int, local: int) -> int:
+    """The multi-rank plumbing without a GPU (gloo): every rank reports in, the job's
+    line is reduced exactly as the GPU path reduces it (tests/test_dist_gloo.py)."""
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method="env://")
+    try:
+        dt, tot = reduce_over_ranks(dist, 0.25 * (rank + 1), 1000 * (rank + 1), "cpu")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, dict(rank=rank, local_rank=local, pid=os.getpid()))
+        if rank == 0:
+            print(json.dumps({"metric": "dist selftest", "value": tot / dt, "n_gpus": world, "ms_per_step": dt * 1e3,
+                              "ranks": ranks}), flush=True)
+    finally:
+        dist.destroy_process_group()
+    return 0
+
+
+def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c4")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c4-deep", "c5", "c4-loop"])
+    ap.add_argument("--deliver", default="ref", choices=["ref", "paper"])
+    ap.add_argument("--cpu-budget", type=float, default=40.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--loop-waves", type=int, default=0, help="c4-loop: waves to run (0 = all)")
     ap.add_argument("--verify", action="store_true", help="check the replay against the bitset oracle")
     ap.add_argument("--colshard", action="store_true",
                     help="also run the process-column sharded C4 sweep (default on when N>1)")
     ap.add_argument("--no-colshard", action="store_true")
+    ap.add_argument("--dist-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--colshard-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cs-uid", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cs-rank", type=int, default=0, help=argparse.SUPPRESS)
@@ -319,12 +615,22 @@ def main():
     ap.add_argument("--cs-device", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.colshard_child:
-        return colshard_child(args)
-
+        colshard_child(args)
+        return 0
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        log(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a mislabelled line")
+        return 2
+    if args.dist_selftest:
+        return dist_selftest(rank, world, local)
 
+    from dag_rider_amd import _lib as L
+
+    args.deliver_mode = L.DR_DELIVER_PAPER if args.deliver == "paper" else L.DR_DELIVER_REF
     import torch
 
     dist = None
@@ -334,7 +640,6 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
 
-    from dag_rider_amd import _lib as L
     from dag_rider_amd.engine import Engine
     from dag_rider_amd.gen import CONFIGS, generate
 
@@ -344,11 +649,17 @@ def main():
             print(json.dumps(out), flush=True)
         if dist:
             dist.destroy_process_group()
-        return
+        return 0
+    if args.config == "c4-loop":
+        if world > 1:
+            log("[bench] c4-loop is a single-GPU latency line")
+            return 2
+        print(json.dumps(run_loop(args, local)), flush=True)
+        return 0
 
     cfg = rank_config(CONFIGS[args.config], rank, world)
     t0 = time.perf_counter()
-    d = generate(cfg, nthreads=16)
+    d = generate(cfg, nthreads=CPU_THREADS)
     log(f"[rank {rank}] generated {cfg} in {time.perf_counter() - t0:.1f} s")
     eng = Engine(cfg.n, cfg.faulty, d.nrounds, local)
     t0 = time.perf_counter()
@@ -356,7 +667,7 @@ def main():
     log(f"[rank {rank}] loaded DAG into HBM in {time.perf_counter() - t0:.1f} s")
 
     def step():
-        return eng.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+        return eng.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, args.deliver_mode)
 
     # timed steps: HIP events around the summary pass only (the dominant kernel);
     # every other phase is timed by one extra, untimed-by-the-clock replay below
@@ -380,37 +691,42 @@ def main():
     res.ms = dict(prof.ms, summary=ms_summary / args.steps)
 
     verify = None
-    if args.verify and rank == 0:
-        import oracle
-
-        want = oracle.PDag(d).replay(cfg.faulty, cfg.nwaves, oracle.CHAIN_PERSISTENT, oracle.DELIVER_REF,
-                                     nthreads=16)
+    cpu = cpu2 = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        runs = 5 if cfg.n * cfg.last_round <= 1024 * 4000 else 3
+        cpu2, want = cpu_bitset(cfg, d, CPU_THREADS, runs, args.deliver_mode)
         verify = bool((want.commit == res.commit).all() and (want.pop_digest == res.pop_digest).all()
                       and (want.pop_count == res.pop_count).all() and want.deliver_edges == res.deliver_edges
                       and want.chain_edges == res.chain_edges and want.commit_edges == res.commit_edges)
+        cpu = cpu_literal(cfg, d, args.cpu_budget, res.total_edges, args.deliver_mode)
+    elif args.verify and rank == 0:
+        import oracle
 
-    colshard = None
-    if (world > 1 or args.colshard) and not args.no_colshard:
+        want = oracle.PDag(d).replay(cfg.faulty, cfg.nwaves, oracle.CHAIN_PERSISTENT, args.deliver_mode,
+                                     nthreads=CPU_THREADS)
+        verify = bool((want.commit == res.commit).all() and (want.pop_digest == res.pop_digest).all()
+                      and (want.pop_count == res.pop_count).all() and want.deliver_edges == res.deliver_edges)
+
+    split = colshard = None
+    if world > 1 and args.config == "c4":
+        split = commit_split(dist, rank, world, local, res.commit if rank == 0 else None,
+                             res.vcount if rank == 0 else None)
+        if not args.no_colshard:
+            colshard = colshard_check(dist, rank, world, local)
+    elif args.colshard and args.config == "c4":
         colshard = colshard_check(dist, rank, world, local)
-        if rank == 0:
-            log(f"[colshard] {colshard}")
+    if rank == 0 and colshard is not None:
+        log(f"[colshard] {colshard}")
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
-        return
+        return 0
 
-    W = (cfg.n + 63) // 64
     kb = kernel_bytes(cfg, d, res)
     # dominant kernel = the phase with the largest device time (HIP events)
     dom = max(kb, key=lambda k: kb[k]["ms"])
     ach = kb[dom]["bytes"] / (kb[dom]["ms"] / 1e3) / 1e9 if kb[dom]["ms"] > 0 else 0.0
-    cpu = None
-    cpu2 = None
-    if not args.no_cpu and world == 1:
-        cpu = cpu_baseline(cfg, d, args.cpu_budget)
-        cpu2 = cpu_bitset(cfg, d, 16, args.cpu_budget)
-
     ms_per_step = dt / args.steps * 1e3
     out = {
         "metric": "DAG edges traversed/sec (commit+delivery)",
@@ -424,14 +740,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic (seeded generator, SURVEY.md s8(d) C4 parameters)",
-        "config": {"workload": f"C4 full replay: n={cfg.n} x {cfg.last_round} rounds, {cfg.nwaves} waves, "
-                               "waveReady (persistent decidedWave) + orderVertices (ref, full cones) per commit",
+        "data": f"synthetic (seeded generator, SURVEY.md s8(d) {cfg.name.upper()} parameters)",
+        "config": {"workload": f"{cfg.name.upper()} full replay: n={cfg.n} x {cfg.last_round} rounds, {cfg.nwaves} "
+                               f"waves, waveReady (persistent decidedWave) + orderVertices ({args.deliver}"
+                               f"{', full cones' if args.deliver == 'ref' else ', dedup'}) per commit",
                    "n": cfg.n, "rounds": cfg.last_round, "waves": cfg.nwaves,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic(dom),
-                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r01/traffic.json)",
+                     "frac": ach / HBM_PEAK_GBS,
+                     "traffic": measured_traffic(dom) if args.config == "c4" and args.deliver == "ref" else None,
+                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r02/traffic.json)",
                      "kernel": kb[dom]["kernel"], "bytes_per_launch": kb[dom]["bytes"],
                      "ms_per_launch": kb[dom]["ms"]},
         "cpu_baseline": cpu,
@@ -442,14 +760,15 @@ def main():
                    "ms": res.ms, "ms_note": "summary: mean over the timed steps; other phases: one "
                    "profiling replay after them (DR_OPT_PHASE_TIMING=2)",
                    "sweep": res.sweep, "verify_vs_oracle": verify,
-                   "colshard": colshard,
+                   "commit_split": split, "colshard": colshard,
                    "kernels": {k: dict(v, GBps=(v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None))
                                for k, v in kb.items()}},
     }
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

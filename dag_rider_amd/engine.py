@@ -213,16 +213,17 @@ class Engine:
     # ---- orderVertices (process.go:404-443) ----
     def order_vertices(self, stack: Sequence[Tuple[int, int]], cur_round: int, mode: int = L.DR_DELIVER_REF,
                        cap: int = 1 << 20):
+        """Delivered ids [k, 2] (None with cap=0: counts and digests only), per-pop counts, digests."""
         ns = len(stack)
         st = np.asarray(stack if ns else [(0, 0)], dtype=np.int32).reshape(-1)
-        ids = np.zeros(max(cap, 1) * 2, np.int32)
+        ids = np.zeros(max(cap, 1) * 2, np.int32) if cap else None
         out_n = C.c_size_t()
         pc = np.zeros(max(ns, 1), np.uint64)
         pd = np.zeros(max(ns, 1), np.uint64)
         self._check(self._L.dr_order_vertices(self._h, L.ptr(st), ns, cur_round, mode, L.ptr(ids), cap,
                                               C.byref(out_n), L.ptr(pc), L.ptr(pd)))
         k = out_n.value
-        return ids[:2 * k].reshape(-1, 2), pc[:ns], pd[:ns]
+        return (ids[:2 * k].reshape(-1, 2) if cap else None), pc[:ns], pd[:ns]
 
     # ---- whole replay ----
     def replay(self, nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT, deliver_mode: int = L.DR_DELIVER_REF,

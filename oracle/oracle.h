@@ -99,6 +99,8 @@ int or_lit_order_vertices(const or_ldag *d, const or_vid *stack, int stack_len,
                           uint64_t *pop_count, uint64_t *pop_digest);
 int or_lit_replay(const or_ldag *d, int faulty, int nwaves, int chain_mode,
                   int deliver_mode, or_replay_out *o);
+int or_lit_replay_mt(const or_ldag *d, int faulty, int nwaves, int chain_mode, int deliver_mode, int nthreads,
+                     or_replay_out *o);
 
 /* expand a packed DAG (rounds [0, nrounds)) to list form; buffers malloc'd,
  * release with or_ldag_free */

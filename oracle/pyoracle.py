@@ -58,6 +58,8 @@ def lib():
                                                 C.POINTER(C.c_int64), P, P]),
             "or_lit_replay": (C.c_int, [C.POINTER(LDagS), C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.POINTER(ReplayOutS)]),
+            "or_lit_replay_mt": (C.c_int, [C.POINTER(LDagS), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.POINTER(ReplayOutS)]),
             "or_ldag_from_packed": (C.c_int, [C.POINTER(PDagS), C.c_int, C.POINTER(LDagS)]),
             "or_ldag_free": (None, [C.POINTER(LDagS)]),
             "or_bs_path": (C.c_int, [C.POINTER(PDagS), Vid, Vid, C.c_int]),
@@ -140,9 +142,9 @@ class LDag:
         return rc, out[:2 * min(on.value, cap)].reshape(-1, 2), pc[:ns], pd[:ns]
 
     def replay(self, faulty: int, nwaves: int, chain_mode=CHAIN_PERSISTENT, deliver_mode=DELIVER_REF,
-               ids_cap: int = 0):
-        return _replay(lambda o: lib().or_lit_replay(C.byref(self.s), faulty, nwaves, chain_mode, deliver_mode,
-                                                     C.byref(o)), nwaves, chain_mode, ids_cap)
+               ids_cap: int = 0, nthreads: int = 1):
+        return _replay(lambda o: lib().or_lit_replay_mt(C.byref(self.s), faulty, nwaves, chain_mode, deliver_mode,
+                                                        nthreads, C.byref(o)), nwaves, chain_mode, ids_cap)
 
 
 class PDag:

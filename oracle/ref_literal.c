@@ -195,16 +195,28 @@ static uint64_t slot_degree(const or_ldag *d, uint32_t i) {
  * mode REF: the delivered filter is a no-op (Q2, :423-427), so each pop
  * delivers its full causal history in rounds 1..cur_round.  mode PAPER:
  * skip ids already in `delivered` (Alg.3 line 54), which persists. */
+/* nthreads > 1: the candidates' path() calls (independent BFSs) run on that
+ * many OpenMP threads first; emission then walks them in order as above. */
 static int order_pop(const or_ldag *d, or_vid popped, int cur_round, int mode, hset *delivered,
                      or_vid *out, int64_t out_cap, int64_t *out_n, uint64_t *count,
-                     uint64_t *digest, uint64_t *edges) {
+                     uint64_t *digest, uint64_t *edges, int nthreads) {
   uint64_t k = 0, dg = 0, ed = 0;
+  int8_t *hit = NULL;
+  uint32_t base = 0;
+  if (nthreads > 1 && cur_round >= 1) {
+    if (cur_round >= d->nrounds) return OR_PANIC;
+    base = d->slot_off[1];
+    const int64_t m = (int64_t)d->slot_off[cur_round + 1] - base;
+    hit = (int8_t *)malloc((size_t)(m > 0 ? m : 1));
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads)
+    for (int64_t i = 0; i < m; i++) hit[i] = (int8_t)or_lit_path(d, popped, d->slot_id[base + i], 0);
+  }
   for (int r = 1; r <= cur_round; r++) { /* :417 */
-    if (r >= d->nrounds) return OR_PANIC;
+    if (r >= d->nrounds) { free(hit); return OR_PANIC; }
     for (uint32_t i = d->slot_off[r]; i < d->slot_off[r + 1]; i++) { /* :418 */
       or_vid t = d->slot_id[i];
-      int p = or_lit_path(d, popped, t, 0); /* :419 */
-      if (p < 0) return OR_PANIC;
+      int p = hit ? hit[i - base] : or_lit_path(d, popped, t, 0); /* :419 */
+      if (p < 0) { free(hit); return OR_PANIC; }
       if (!p) continue;
       if (mode == OR_DELIVER_PAPER) {
         if (hs_has(delivered, vid_key(t))) continue;
@@ -218,6 +230,7 @@ static int order_pop(const or_ldag *d, or_vid popped, int cur_round, int mode, h
       k++;
     }
   }
+  free(hit);
   *count = k;
   *digest = dg;
   if (edges) *edges = ed;
@@ -234,7 +247,7 @@ int or_lit_order_vertices(const or_ldag *d, const or_vid *stack, int stack_len, 
   int j = 0;
   for (int top = stack_len - 1; top >= 0; top--, j++) { /* :412-413 LIFO pops */
     int rc = order_pop(d, stack[top], cur_round, mode, &del, out, out_cap, out_n,
-                       &pop_count[j], &pop_digest[j], NULL);
+                       &pop_count[j], &pop_digest[j], NULL, 1);
     if (rc < 0) { hs_free(&del); return rc; }
   }
   hs_free(&del);
@@ -247,6 +260,14 @@ int or_lit_order_vertices(const or_ldag *d, const or_vid *stack, int stack_len, 
  * CHAIN_PERSISTENT. */
 int or_lit_replay(const or_ldag *d, int faulty, int nwaves, int chain_mode, int deliver_mode,
                   or_replay_out *o) {
+  return or_lit_replay_mt(d, faulty, nwaves, chain_mode, deliver_mode, 1, o);
+}
+
+/* The same replay with orderVertices' candidate path() calls spread over
+ * nthreads OpenMP threads (the reference's algorithm and cost, one BFS per
+ * candidate, on every core; results identical). */
+int or_lit_replay_mt(const or_ldag *d, int faulty, int nwaves, int chain_mode, int deliver_mode, int nthreads,
+                     or_replay_out *o) {
   hset del;
   hs_init(&del, 1 << 10);
   int decided = 0;
@@ -275,7 +296,7 @@ int or_lit_replay(const or_ldag *d, int faulty, int nwaves, int chain_mode, int 
     for (int top = slen - 1; top >= 0; top--, npop++) {
       uint64_t ed = 0;
       rc = order_pop(d, stack[top], wave_round(w, 4), deliver_mode, &del, o->ids, o->ids_cap,
-                     &o->n_ids, &o->pop_count[npop], &o->pop_digest[npop], &ed);
+                     &o->n_ids, &o->pop_count[npop], &o->pop_digest[npop], &ed, nthreads);
       if (rc < 0) break;
       o->pop_edges[npop] = ed;
       o->deliver_edges += ed;

@@ -59,6 +59,35 @@ def test_single_rank_passthrough():
     assert bench.reduce_over_ranks(None, 2.0, 7, "cpu") == (2.0, 7.0)
 
 
+def test_bench_gpus_spawns_ranks():
+    """bench.py --gpus 2 outside torchrun really starts 2 ranks (torch.distributed.run)
+    and rank 0 prints one line reduced over both: max time, summed work."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-selftest"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert sorted(r["rank"] for r in out["ranks"]) == [0, 1]
+    assert len({r["pid"] for r in out["ranks"]}) == 2
+    assert out["ms_per_step"] == 500.0 and out["value"] == 3000 / 0.5
+
+
+def test_bench_world_mismatch_refused():
+    """Under torchrun a WORLD_SIZE that disagrees with --gpus exits non-zero, prints nothing."""
+    import subprocess
+
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-selftest"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 2 and not p.stdout.strip()
+
+
 def _id_worker(rank, world, port, out):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

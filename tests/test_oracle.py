@@ -125,6 +125,19 @@ def test_literal_vs_bitset_generator(seed):
               bs.replay(cfg.faulty, cfg.nwaves, cm, oracle.DELIVER_REF, ids_cap=1 << 16))
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_literal_multithreaded_identical(seed):
+    """or_lit_replay_mt (the CPU baseline on every core) == the single-thread literal replay."""
+    rng = np.random.default_rng(300 + seed)
+    d = random_dag(rng, int(rng.integers(3, 12)), int(rng.integers(8, 25)), p_s=0.5, p_w=0.3)
+    f = (d.n - 1) // 3
+    lit = oracle.LDag(packed=d)
+    for cm in (oracle.CHAIN_LITERAL, oracle.CHAIN_PERSISTENT):
+        for dm in (oracle.DELIVER_REF, oracle.DELIVER_PAPER):
+            _same(lit.replay(f, (d.nrounds - 1) // 4, cm, dm, ids_cap=1 << 16),
+                  lit.replay(f, (d.nrounds - 1) // 4, cm, dm, ids_cap=1 << 16, nthreads=4))
+
+
 def test_generator_deterministic_and_thread_independent():
     cfg = CONFIGS["c2"]
     a, b = generate(cfg, nthreads=1), generate(cfg, nthreads=4)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, smoke, bench, rocprof kernel trace and the PMC
 # traffic passes for the dominant kernel.  Every GPU step has its own time limit and
-# the chain stops at the first failure.
+# the chain stops at the first failure.  usage: tools/gpu_check.sh <tag> [quick]
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-run}
@@ -9,12 +9,10 @@ mkdir -p $OUT
 step() { local t=$1; shift; echo "[step] $*" >&2; timeout -k 10 $t "$@"; }
 step 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 &&
 step 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
-step 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err &&
-step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python bench.py --no-cpu --no-colshard --steps 5 --warmup 2 > $OUT/bench_prof.json 2> $OUT/prof.err &&
+step 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err &&
+step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python bench.py --no-cpu --steps 5 --warmup 2 > $OUT/bench_prof.json 2> $OUT/prof.err &&
 step 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_fetch -o fetch -- python bench.py --no-cpu --steps 2 --warmup 1 > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err &&
-step 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o write -- python bench.py --no-cpu --steps 2 --warmup 1 > $OUT/pmc_write.json 2> $OUT/pmc_write.err &&
-step 300 python bench.py --config c5 > $OUT/bench_c5.json 2> $OUT/bench_c5.err &&
-step 200 python tools/shard_bench.py > $OUT/shard_local.jsonl 2> $OUT/shard_local.err
+step 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o write -- python bench.py --no-cpu --steps 2 --warmup 1 > $OUT/pmc_write.json 2> $OUT/pmc_write.err
 rc=$?
 echo "exit $rc" > $OUT/status.txt
 exit $rc
