@@ -90,45 +90,45 @@ def _median_runs(fn, runs):
 
 def cpu_literal(cfg, d, budget_s: float, full_edges: int, deliver_mode: int):
     """The oracle's literal restatement of process.go (the reference's algorithm: BFS +
-    hash-set visited + linear id scans, one BFS per orderVertices candidate) on a bounded
-    sample: a replay of waves 1..k.  Single thread (the reference is one goroutine) and
-    one thread per core (candidates' BFSs in parallel); median of 5 runs each.  The
-    literal cost grows ~ w^2 per wave, so two extrapolations to the full replay are
-    given: per edge at the sample's rate (a lower bound) and by a power law fitted to
-    the per-wave times of waves 1..k."""
+    hash-set visited + linear id scans, one BFS per voter and per orderVertices
+    candidate) on a bounded sample: a replay of waves 1..k.  Single thread (the
+    reference is one goroutine) and one thread per core (the independent BFSs of the
+    voter loop and of a pop's candidates in parallel); median of 5 runs each.  The
+    literal cost per wave grows ~ w^2 (every pop BFSes a cone of ~4w rounds for each
+    of 4w*n candidates), so the full replay is extrapolated two ways: per edge at the
+    sample's rate (a lower bound) and by fitting t(w) = a + b w^2 to the measured
+    per-wave times."""
     import oracle
 
     nt = min(CPU_THREADS, cpu_info()["affinity"] or 1)
-    # multi-thread: grow k until one replay takes ~budget/12
-    k, per_wave, prev = 1, [], 0.0
-    while True:
+    k, cum = 0, []
+    while k < min(cfg.nwaves, 6):
+        k += 1
         ld = oracle.LDag(packed=d, nrounds=4 * k + 1)
         t0 = time.perf_counter()
         r = ld.replay(cfg.faulty, k, oracle.CHAIN_PERSISTENT, deliver_mode, nthreads=nt)
-        dt = time.perf_counter() - t0
+        cum.append(time.perf_counter() - t0)
         assert r.rc == 0
-        per_wave.append(max(dt - prev, 1e-9))
-        prev = dt
-        if dt * 3 > budget_s / 12 or k >= min(cfg.nwaves, 8):
+        if cum[-1] * 4 > budget_s / 4:
             break
-        k += 1
+    per_wave = [cum[0]] + [max(cum[i] - cum[i - 1], 1e-9) for i in range(1, len(cum))]
     ld = oracle.LDag(packed=d, nrounds=4 * k + 1)
     mt_med, mt_ts, r = _median_runs(
         lambda: ld.replay(cfg.faulty, k, oracle.CHAIN_PERSISTENT, deliver_mode, nthreads=nt), 5)
     edges = r.commit_edges + r.deliver_edges  # the literal restatement does not count chain edges
-    # single thread on the first wave only (its cost is known from the multi-thread run)
     ld1 = oracle.LDag(packed=d, nrounds=5)
     st_med, st_ts, r1 = _median_runs(lambda: ld1.replay(cfg.faulty, 1, oracle.CHAIN_PERSISTENT, deliver_mode), 5)
     e1 = r1.commit_edges + r1.deliver_edges
-    # power-law fit t(w) = a w^b over the multi-thread per-wave times
-    import math
+    import numpy as np
 
+    w = np.arange(1, len(per_wave) + 1, dtype=np.float64)
     if len(per_wave) >= 2:
-        b = math.log(per_wave[-1] / per_wave[0]) / math.log(len(per_wave))
+        (fa, fb), *_ = np.linalg.lstsq(np.stack([np.ones_like(w), w * w], 1), np.asarray(per_wave), rcond=None)
+        fa, fb = max(float(fa), 0.0), max(float(fb), 0.0)
     else:
-        b = 2.0
-    a = per_wave[0]
-    fit_full = sum(a * (w ** b) for w in range(1, cfg.nwaves + 1)) * (st_med / max(per_wave[0], 1e-9))
+        fa, fb = per_wave[0], 0.0
+    N = cfg.nwaves
+    full_mt = fa * N + fb * N * (N + 1) * (2 * N + 1) / 6
     return dict(value=e1 / st_med, unit="edges/s", cores=1, kind="port",
                 sample=f"{cfg.name} waves 1..1 (rounds 0..4) literal replay (oracle/ref_literal.c, the reference's "
                        f"algorithm), single thread: {e1} edges, median {st_med:.2f} s of 5 runs",
@@ -136,7 +136,9 @@ def cpu_literal(cfg, d, budget_s: float, full_edges: int, deliver_mode: int):
                 all_cores=dict(value=edges / mt_med, cores=nt, waves=k, edges=edges, median_s=mt_med, runs_s=mt_ts,
                                per_wave_s=per_wave),
                 extrapolated_full_s_per_edge=full_edges / (e1 / st_med),
-                extrapolated_full_s_fit=fit_full, fit_exponent=b, host=cpu_info())
+                extrapolated_full_s_fit_all_cores=full_mt,
+                extrapolated_full_s_fit_single=full_mt * st_med / max(cum[0], 1e-9),
+                fit=dict(model="t(w) = a + b w^2 (all cores)", a=fa, b=fb), host=cpu_info())
 
 
 def cpu_bitset(cfg, d, nthreads: int, full_runs: int, deliver_mode: int):

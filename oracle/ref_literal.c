@@ -153,8 +153,8 @@ int or_lit_leader(const or_ldag *d, int wave, or_vid *leader) {
 
 /* process.go:314-354 waveReady (without the decidedWave write, which the caller
  * owns: Q1, value receiver). Returns 1 commit, 0 no commit, -1 panic. */
-int or_lit_wave_ready(const or_ldag *d, int faulty, int wave, int decided_wave,
-                      or_vid *stack, int *stack_len, int stack_cap, int *vcount) {
+static int wave_ready_impl(const or_ldag *d, int faulty, int wave, int decided_wave, or_vid *stack,
+                           int *stack_len, int stack_cap, int *vcount, int nthreads) {
   or_vid leader;
   *vcount = -1;
   int rc = or_lit_leader(d, wave, &leader);
@@ -162,12 +162,15 @@ int or_lit_wave_ready(const or_ldag *d, int faulty, int wave, int decided_wave,
   if (rc == 0) return 0; /* :327-329 */
   int r4 = wave_round(wave, 4);
   if (r4 < 0 || r4 >= d->nrounds) return OR_PANIC;
-  int vc = 0; /* :331-336 voter loop over every SLOT of dag[round(w,4)] */
-  for (uint32_t i = d->slot_off[r4]; i < d->slot_off[r4 + 1]; i++) {
+  int vc = 0, panic = 0; /* :331-336 voter loop over every SLOT of dag[round(w,4)] (independent BFSs) */
+  const int64_t a = d->slot_off[r4], b = d->slot_off[r4 + 1];
+#pragma omp parallel for schedule(dynamic, 8) num_threads(nthreads > 1 ? nthreads : 1) reduction(+ : vc, panic)
+  for (int64_t i = a; i < b; i++) {
     int p = or_lit_path(d, d->slot_id[i], leader, 1);
-    if (p < 0) return OR_PANIC;
-    vc += p;
+    if (p < 0) panic++;
+    else vc += p;
   }
+  if (panic) return OR_PANIC;
   *vcount = vc;
   if (vc < 2 * faulty + 1) return 0; /* :337-339 */
   if (*stack_len >= stack_cap) return OR_PANIC;
@@ -185,6 +188,11 @@ int or_lit_wave_ready(const or_ldag *d, int faulty, int wave, int decided_wave,
     leader = v;
   }
   return 1;
+}
+
+int or_lit_wave_ready(const or_ldag *d, int faulty, int wave, int decided_wave,
+                      or_vid *stack, int *stack_len, int stack_cap, int *vcount) {
+  return wave_ready_impl(d, faulty, wave, decided_wave, stack, stack_len, stack_cap, vcount, 1);
 }
 
 static uint64_t slot_degree(const or_ldag *d, uint32_t i) {
@@ -278,8 +286,8 @@ int or_lit_replay_mt(const or_ldag *d, int faulty, int nwaves, int chain_mode, i
   int rc = 0;
   for (int w = 1; w <= nwaves && rc == 0; w++) {
     int slen = 0, vc = -1;
-    int c = or_lit_wave_ready(d, faulty, w, chain_mode == OR_CHAIN_PERSISTENT ? decided : 0, stack,
-                              &slen, nwaves + 1, &vc);
+    int c = wave_ready_impl(d, faulty, w, chain_mode == OR_CHAIN_PERSISTENT ? decided : 0, stack, &slen,
+                            nwaves + 1, &vc, nthreads);
     if (c < 0) { rc = c; break; }
     o->commit[w - 1] = (uint8_t)c;
     o->vcount[w - 1] = vc;
