@@ -18,6 +18,7 @@ DR_WEAK_LITERAL, DR_WEAK_PAPER = 0, 1
 DR_OPT_MEMO = 1
 DR_OPT_DEVICE_PLAN = 2
 DR_OPT_PHASE_TIMING = 3
+DR_LEADER_CONST1, DR_LEADER_SEEDED, DR_LEADER_TABLE = 0, 1, 2
 DR_SHARD_ID_BYTES = 128
 
 P = C.c_void_p
@@ -47,6 +48,9 @@ SIGNATURES = {
     "dr_last_error": (C.c_char_p, [P]),
     "dr_num_rounds": (C.c_int, [P]),
     "dr_set_option": (C.c_int, [P, C.c_int, C.c_int]),
+    "dr_set_leader_coin": (C.c_int, [P, C.c_int, C.c_uint64, C.c_int, P]),
+    "dr_coin_leader": (C.c_int, [C.c_uint64, C.c_int, C.c_int]),
+    "dr_wave_leader": (C.c_int, [P, C.c_int]),
     "dr_append_rounds_lists": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
     "dr_append_rounds_packed": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "dr_append_vertices": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),

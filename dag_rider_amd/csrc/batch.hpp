@@ -40,6 +40,7 @@ struct SmallJob {
   const uint16_t *wdeg;     // [rounds][n] weak degree per vertex
   const uint32_t *slot_off;
   const uint16_t *slot_src;
+  const uint16_t *lead;     // [wave] chooseLeader(w), 1-based source
   // scratch, rounds 0..T: Qf, Qs, (deg << 16 | strong deg)
   u64 *qf;
   u64 *qs;
@@ -123,7 +124,8 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   u64 commit_mask = 0, lead_mask = 0, commit_edges = 0;
   for (int w = 1; w <= nw; w++) {
     const int r1 = 4 * (w - 1) + 1;
-    const bool lead = pres_word(r1, 0) & 1ULL;
+    const int l = J.lead[w] - 1;  // chooseLeader(w), 0-based (< 128)
+    const bool lead = (pres_word(r1, l >> 6) >> (l & 63)) & 1ULL;
     if (!lead) {
       if (lane == 0) vc_s[w - 1] = -1;
       continue;
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
       row(r1 + 1 + k, lane, a[k][0], b[k][0]);
       row(r1 + 1 + k, lane + 64, a[k][1], b[k][1]);
     }
-    u64 s0 = 1, s1 = 0, deg = 0;
+    u64 s0 = l < 64 ? 1ULL << l : 0ULL, s1 = l >= 64 ? 1ULL << (l - 64) : 0ULL, deg = 0;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       const int r = r1 + 1 + k;
@@ -163,13 +165,20 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
       qf[i] |= ring[(r % rsl) * 128 + v];
       ring[(r % rsl) * 128 + v] = 0;
     }
-    if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its bit at source 1
+    if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its bit at the leader's source
       const int w = (r - 1) / 4 + 1;
+      const int l = J.lead[w] - 1;
       if ((lead_mask >> (w - 1)) & 1ULL) {
-        if (lane == 0) {
-          qf[0] |= 1ULL << (w - 1);
-          qs[0] |= 1ULL << (w - 1);
-          QL[w - 1] = qs[0];
+        if (lane == (l & 63)) {  // register arrays: constant indices only
+          if (l < 64) {
+            qf[0] |= 1ULL << (w - 1);
+            qs[0] |= 1ULL << (w - 1);
+            QL[w - 1] = qs[0];
+          } else {
+            qf[1] |= 1ULL << (w - 1);
+            qs[1] |= 1ULL << (w - 1);
+            QL[w - 1] = qs[1];
+          }
         }
       } else if (lane == 0) {
         QL[w - 1] = 0;

@@ -103,6 +103,11 @@ struct dr_ctx {
   DevBuf admit_buf;  // dr_buffer_admit scratch
   DevBuf wdeg;     // [max_rounds][n] u16 weak degree per vertex (batch.hpp)
   DevBuf put_buf;  // dr_append_vertices staging on the device
+  // chooseLeader (process.go:386-392): leader source of every wave, index w
+  // (DR_LEADER_CONST1: 1, the reference's constant), mirrored on the device
+  DevBuf lead;
+  std::vector<uint16_t> h_lead;
+  int lead_src(int w) const { return (w >= 0 && w < (int)h_lead.size()) ? h_lead[w] : 1; }
   // host mirror: per-round data, presence [rounds][WS], and the prefix offsets
   // of the flattened device arrays (valid for rounds < up_lo)
   std::vector<HostRound> hr;
@@ -257,6 +262,7 @@ struct dr_ctx {
     v.wc_rows = wc_rows.as<u64>();
     v.wc_roff = wc_roff.as<uint32_t>();
     v.sdeg = sdeg.as<uint16_t>();
+    v.lead = lead.as<uint16_t>();
     v.n = n;
     v.nrounds = nrounds;
     return v;
@@ -672,7 +678,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
       c->wc_key.ensure(4096) != hipSuccess || c->wc_rows.ensure(4096) != hipSuccess ||
       c->sdeg.ensure((size_t)max_rounds * n * sizeof(uint16_t)) != hipSuccess ||
       c->wdeg.ensure((size_t)max_rounds * n * sizeof(uint16_t)) != hipSuccess ||
-      c->slot_src.ensure(4096) != hipSuccess) {
+      c->slot_src.ensure(4096) != hipSuccess || c->lead.ensure(((size_t)max_rounds / 4 + 2) * 2) != hipSuccess) {
     g_create_err = "dr_create: device allocation failed";
     dr_destroy(c);
     return DR_E_HIP;
@@ -682,6 +688,8 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   (void)hipMemcpy(c->weak_roff.p, &zero, 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(c->far_roff.p, &zero, 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(c->wc_roff.p, &zero, 4, hipMemcpyHostToDevice);
+  c->h_lead.assign((size_t)max_rounds / 4 + 2, 1);  // chooseLeader(w) = 1 (process.go:390-392)
+  (void)hipMemcpy(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice);
   *out = c;
   return DR_OK;
 }
@@ -700,7 +708,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
-                    &c->admit_buf};
+                    &c->admit_buf, &c->lead};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1371,6 +1379,39 @@ bool summary_fresh(const dr_ctx *c) { return rounds_fresh(c) && c->canon_ok && c
 int shortcut_flag(const dr_ctx *c) { return rounds_fresh(c) ? dr::Q_SHORTCUT : 0; }
 }  // namespace
 
+extern "C" int dr_set_leader_coin(dr_ctx *c, int mode, uint64_t seed, int k, const int32_t *table) {
+  if (!c) return DR_E_INVAL;
+  if (int rc = set_device(c)) return rc;
+  std::vector<uint16_t> L(c->h_lead.size(), 1);
+  if (mode == DR_LEADER_SEEDED) {
+    for (size_t w = 1; w < L.size(); w++) L[w] = (uint16_t)dr_coin_leader(seed, (int)w, c->n);
+  } else if (mode == DR_LEADER_TABLE) {
+    if (k < 0 || (k > 0 && !table)) return c->fail(DR_E_INVAL, "bad leader table");
+    for (int w = 1; w <= k && w < (int)L.size(); w++) {
+      if (table[w - 1] < 1 || table[w - 1] > c->n)
+        return c->fail(DR_E_INVAL, "leader of wave %d: source %d outside [1, %d]", w, table[w - 1], c->n);
+      L[w] = (uint16_t)table[w - 1];
+    }
+  } else if (mode != DR_LEADER_CONST1) {
+    return c->fail(DR_E_INVAL, "unknown leader coin mode %d", mode);
+  }
+  c->h_lead = std::move(L);
+  HIPCHK(c, c->h2d(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2));
+  HIPCHK(c, c->sync());
+  return DR_OK;
+}
+
+extern "C" int dr_wave_leader(const dr_ctx *c, int wave) { return c ? c->lead_src(wave) : -1; }
+
+extern "C" int dr_coin_leader(uint64_t seed, int wave, int n) {
+  if (n < 1) return 1;
+  uint64_t z = seed + (uint64_t)(uint32_t)wave * 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  z ^= z >> 31;
+  return 1 + (int)(z % (uint64_t)n);
+}
+
 extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
   if (!c) return DR_E_INVAL;
   if (option == DR_OPT_MEMO) {
@@ -1571,7 +1612,7 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   for (int w = wk + 1; w <= w1; w++) {
     const int r1 = 4 * (w - 1) + 1;
     if (r1 >= c->nrounds) return c->fail(DR_E_INVAL, "wave %d: leader round %d not in the DAG (Go: index out of range)", w, r1);
-    if (c->is_present(r1, 1)) return c->fail(DR_E_INVAL, "wave %d: round %d not in the DAG (Go: index out of range)", w, 4 * w);
+    if (c->is_present(r1, c->lead_src(w))) return c->fail(DR_E_INVAL, "wave %d: round %d not in the DAG (Go: index out of range)", w, 4 * w);
     commit[w - w0] = 0;
     vcount[w - w0] = -1;
   }
@@ -1606,7 +1647,7 @@ int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::
     dr::SweepQuery s{};
     s.top = 4 * (tasks[i].wave - 1) + 1;
     s.bottom = 4 * tasks[i].floor + 1;
-    s.src0 = 0;
+    s.src0 = c->lead_src(tasks[i].wave) - 1;
     s.flags = dr::Q_CHAIN | dr::Q_STRONG_ONLY | shortcut_flag(c);
     s.out_off = (int32_t)off;
     s.tgt0 = -1;
@@ -2141,7 +2182,8 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   SweepArgs a;
   std::function<int()> side = [&]() -> int {
     // 2. leader chains
-    hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(), nw,
+    hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(),
+                       c->lead.as<uint16_t>(), nw,
                        persistent ? 1 : 0, dr::Q_CHAIN | dr::Q_STRONG_ONLY | sc, task_wave, task_q, cq, plan);
     HIPCHK(c, hipGetLastError());
     a.q = cq;
@@ -2162,7 +2204,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     HIPCHK(c, c->rec(1));
     // 3. pops
     hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
-                       dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, task_wave, task_q, cq, cpush_n, push_out, pcap,
+                       dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave, task_q, cq, cpush_n, push_out, pcap,
                        task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
     HIPCHK(c, hipGetLastError());
     return 0;
@@ -2289,7 +2331,7 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
     if (t < tasks.size() && tasks[t].wave == w) {
       for (int32_t pw : pushes[t]) o->push_wave[at++] = pw;
       for (auto it = pushes[t].rbegin(); it != pushes[t].rend(); ++it)
-        pops.push_back(Pop{4 * (*it - 1) + 1, 1, 4 * w});
+        pops.push_back(Pop{4 * (*it - 1) + 1, c->lead_src(*it), 4 * w});
       t++;
     }
   }
@@ -2428,6 +2470,7 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
       J.wdeg = c->wdeg.as<uint16_t>();
       J.slot_off = c->slot_off.as<uint32_t>();
       J.slot_src = c->slot_src.as<uint16_t>();
+      J.lead = c->lead.as<uint16_t>();
       J.n = c->n;
       J.WS = c->WS;
       J.push_cap = (int32_t)pcap[i];

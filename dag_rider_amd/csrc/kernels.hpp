@@ -59,6 +59,7 @@ struct DagView {
   const u64 *wc_rows;
   const uint32_t *wc_roff;
   const uint16_t *sdeg;  // [rounds][n] strong degree per vertex
+  const uint16_t *lead;  // [wave] chooseLeader(w) (process.go:386-392), 1-based source
   int32_t n;
   int32_t nrounds;
 };
@@ -156,12 +157,13 @@ __global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int qu
   const int w = w0 + bi;
   const int r1 = 4 * (w - 1) + 1;
   const int n = g.n;
-  if (!(g.present[(size_t)r1 * WS] & 1ULL)) {  // leader is bottom (process.go:327-329)
+  const int l = g.lead[w] - 1;  // chooseLeader(w), 0-based
+  if (!((g.present[(size_t)r1 * WS + (l >> 6)] >> (l & 63)) & 1ULL)) {  // leader is bottom (process.go:327-329)
     if (tid == 0) { commit[bi] = 0; vcount[bi] = -1; }
     return;
   }
   if (tid < WS) {
-    S[tid] = tid == 0 ? 1ULL : 0ULL;
+    S[tid] = tid == (l >> 6) ? 1ULL << (l & 63) : 0ULL;
     T[tid] = 0;
 #pragma unroll
     for (int k = 0; k < 3; k++) P[k][tid] = g.present[(size_t)(r1 + 1 + k) * WS + tid];
@@ -511,11 +513,11 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
           }
           if constexpr (CHAIN) {
             if (r < q.top && ((r - 1) & 3) == 0) {
-              const u64 f0 = __shfl(f, 0);
-              const u64 p0 = __shfl(p, 0);
-              if ((f0 & 1ULL) && (p0 & 1ULL)) {  // strong_path(leader, v') holds: push v' (process.go:344-349)
-                f = tid == 0 ? 1ULL : 0ULL;
-                if (tid == 0) push_out[q.out_off + npush++] = (r - 1) / 4 + 1;
+              const int wv = (r - 1) / 4 + 1, l = g.lead[wv] - 1;  // leader of wave wv, 0-based
+              const u64 fl = __shfl(f, l >> 6), pl = __shfl(p, l >> 6);
+              if (((fl & pl) >> (l & 63)) & 1ULL) {  // v' present, strong_path(leader, v'): push v' (process.go:344-349)
+                f = tid == (l >> 6) ? 1ULL << (l & 63) : 0ULL;
+                if (tid == 0) push_out[q.out_off + npush++] = wv;
               }
             }
           }
@@ -638,10 +640,11 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
   const int r1 = 4 * (w - 1) + 1;
   const int nr = min(T, r1 + 3) - r1 + 1;
   const bool do_commit = w <= nwc;
-  const bool leader = do_commit && (g.present[(size_t)r1 * WS] & 1ULL);
+  const int l = do_commit ? g.lead[w] - 1 : 0;  // chooseLeader(w), 0-based
+  const bool leader = do_commit && ((g.present[(size_t)r1 * WS + (l >> 6)] >> (l & 63)) & 1ULL);
   if (tid < WS) {
     sU[tid] = 0;
-    S[tid] = tid == 0 ? 1ULL : 0ULL;
+    S[tid] = tid == (l >> 6) ? 1ULL << (l & 63) : 0ULL;
     Tn[tid] = 0;
     P[tid] = g.present[(size_t)r1 * WS + tid];
   }

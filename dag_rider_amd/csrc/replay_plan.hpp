@@ -66,8 +66,8 @@ __device__ __forceinline__ T block_scan_excl(T v, T *s, T &total) {
 // wave - floor >= 2 walks rounds 4(w-1)+1 .. 4 floor + 1 and may push up to
 // wave - floor - 1 leaders at out_off.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ commit, int nw, int persistent,
-                                                    int qflags, int32_t *__restrict__ task_wave,
+__global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ commit, const uint16_t *__restrict__ lead,
+                                                    int nw, int persistent, int qflags, int32_t *__restrict__ task_wave,
                                                     int32_t *__restrict__ task_q, SweepQuery *__restrict__ cq,
                                                     int32_t *__restrict__ plan) {
   __shared__ int64_t s[NT / 64];
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ 
       SweepQuery q{};
       q.top = 4 * (w - 1) + 1;
       q.bottom = 4 * fl + 1;
-      q.src0 = 0;
+      q.src0 = lead[w] - 1;
       q.flags = qflags;
       q.mask_off = 0;
       q.out_off = (int32_t)(c2 + off);
@@ -129,7 +129,8 @@ __global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ 
 // and one delivery query per distinct leader, highest round first, with
 // cumulative mask images (rounds 0..top).
 template <int NT>
-__global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, const int32_t *__restrict__ task_wave,
+__global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, const uint16_t *__restrict__ lead,
+                                                  const int32_t *__restrict__ task_wave,
                                                   const int32_t *__restrict__ task_q,
                                                   const SweepQuery *__restrict__ cq,
                                                   const int32_t *__restrict__ push_n,
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
       SweepQuery q{};
       q.top = top;
       q.bottom = 0;
-      q.src0 = 0;
+      q.src0 = lead[w] - 1;
       q.flags = qflags;
       q.mask_off = c1 + mo;
       q.tgt0 = -1;

@@ -74,6 +74,17 @@ class Engine:
         """DR_OPT_MEMO: round summaries + canonical cone (identical results either way)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_MEMO, int(on)))
 
+    def set_leader_coin(self, mode: int = L.DR_LEADER_CONST1, seed: int = 0,
+                        table: Optional[Sequence[int]] = None):
+        """chooseLeader (process.go:386-392): constant 1 (the reference), a seeded coin, or a table."""
+        t = np.asarray(table if table is not None else [1], np.int32)
+        k = len(table) if table is not None else 0
+        self._check(self._L.dr_set_leader_coin(self._h, mode, seed, k, L.ptr(t)))
+
+    def wave_leader(self, wave: int) -> int:
+        """chooseLeader(wave) under the current coin (1-based source)."""
+        return int(self._L.dr_wave_leader(self._h, wave))
+
     def set_phase_timing(self, level: int):
         """DR_OPT_PHASE_TIMING: 2 = every replay phase timed, 1 = summary pass only, 0 = none."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_PHASE_TIMING, int(level)))

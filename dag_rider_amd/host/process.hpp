@@ -182,9 +182,20 @@ class Process {
     return out != 0;
   }
 
+  // The global coin behind chooseLeader (process.go:386-392): the reference's
+  // constant 1 (DR_LEADER_CONST1, default), a seeded coin, or a caller's table
+  // (dagrider_gpu.h dr_set_leader_coin); kept across mirror rebuilds.
+  void setLeaderCoin(int mode, uint64_t seed = 0, std::vector<int32_t> table = {}) {
+    coinMode_ = mode;
+    coinSeed_ = seed;
+    coinTable_ = std::move(table);
+    if (ctx_) applyCoin();
+  }
+
   // getWaveVertexLeader (process.go:357-371): FIRST slot with source == leader.
   std::pair<vertex, bool> getWaveVertexLeader(int w) {
-    const int leader = chooseLeader(w);
+    sync();
+    const int leader = dr_wave_leader(ctx_, w);
     const int r = waveRound(w, 1);
     if (r < 0 || r >= (int)dag.size()) throw panic_error("runtime error: index out of range");
     for (const vertex &v : dag[r])
@@ -288,6 +299,14 @@ class Process {
   int device_ = 0;
   int n_ = 0;
   int cap_rounds_ = 0;
+  int coinMode_ = DR_LEADER_CONST1;
+  uint64_t coinSeed_ = 0;
+  std::vector<int32_t> coinTable_;
+
+  void applyCoin() {
+    check(dr_set_leader_coin(ctx_, coinMode_, coinSeed_, (int)coinTable_.size(),
+                             coinTable_.empty() ? nullptr : coinTable_.data()));
+  }
 
   void check(int rc) {
     if (rc == DR_OK) return;
@@ -323,6 +342,7 @@ class Process {
     cap_rounds_ = std::max<int>(64, 2 * (int)dag.size());
     int rc = dr_create(n_, faulty, cap_rounds_, device_, &ctx_);
     if (rc != DR_OK) throw std::runtime_error(std::string("dagrider: ") + dr_last_error(nullptr));
+    if (coinMode_ != DR_LEADER_CONST1) applyCoin();
     std::vector<uint32_t> so{0}, sto{0}, wo{0};
     std::vector<int32_t> sid, sti, wi;
     for (const auto &rnd : dag.r_) {

@@ -20,8 +20,8 @@
  *
  * Vertex ids travel as int32 pairs {round, source} (vertexID,
  * process/process.go:20-23).  Waves are 1-based; round(w, k) = 4(w-1)+k
- * (waveRound, process.go:400-402); the leader of every wave is source 1
- * (chooseLeader, process.go:390-392).
+ * (waveRound, process.go:400-402); the leader of wave w is chooseLeader(w)
+ * (process.go:390-392): source 1 unless dr_set_leader_coin says otherwise.
  */
 #ifndef DAGRIDER_GPU_H
 #define DAGRIDER_GPU_H
@@ -62,6 +62,22 @@ void dr_destroy(dr_ctx *ctx);
 const char *dr_last_error(const dr_ctx *ctx);
 /* number of rounds currently mirrored (len(p.dag)) */
 int dr_num_rounds(const dr_ctx *ctx);
+/* chooseLeader(w) (process.go:386-392): "a global perfect coin"; the
+ * reference returns process 1 for every wave.
+ *   DR_LEADER_CONST1  leader(w) = 1 (the default: parity with the code)
+ *   DR_LEADER_SEEDED  leader(w) = dr_coin_leader(seed, w, n): a seeded coin
+ *                     every process computes alike (agreement, fairness)
+ *   DR_LEADER_TABLE   leader(w) = table[w-1] for w <= k (the caller's coin,
+ *                     e.g. an (f+1)-of-n threshold signature), 1 beyond
+ * Applies to every later waveReady / getWaveVertexLeader / replay. */
+enum { DR_LEADER_CONST1 = 0, DR_LEADER_SEEDED = 1, DR_LEADER_TABLE = 2 };
+int dr_set_leader_coin(dr_ctx *ctx, int mode, uint64_t seed, int k, const int32_t *table);
+/* The seeded coin: 1 + splitmix64(seed + wave * 0x9E3779B97F4A7C15) mod n
+ * (n = the context's process count). */
+int dr_coin_leader(uint64_t seed, int wave, int n);
+/* chooseLeader(wave) as the context currently decides it (1-based source). */
+int dr_wave_leader(const dr_ctx *ctx, int wave);
+
 /* DR_OPT_MEMO (default 1): use round summaries + the canonical cone for
  * orderVertices / path sweeps (identical results; 0 = sweep every cone).
  * DR_OPT_DEVICE_PLAN (default 1): dr_replay plans its chain, pop and emission

@@ -43,6 +43,8 @@ typedef struct {
   const or_vid *strong_ids;
   const uint32_t *weak_off;
   const or_vid *weak_ids;
+  const int32_t *leader; /* chooseLeader(w) = leader[w-1] for w <= nleader, else 1 (NULL: always 1) */
+  int32_t nleader;
 } or_ldag;
 
 /* Packed DAG: strong rows indexed by (round, source-1), W = ceil(n/64) u64
@@ -56,7 +58,15 @@ typedef struct {
   const uint64_t *strong;
   const uint32_t *weak_off;
   const uint32_t *weak_tgt;
+  const int32_t *leader; /* as or_ldag */
+  int32_t nleader;
 } or_pdag;
+
+/* chooseLeader (process.go:386-392): the reference's constant 1, or the
+ * caller's coin table (the engine's DR_LEADER_* modes) */
+static inline int or_leader(const int32_t *leader, int32_t nleader, int w) {
+  return (leader && w >= 1 && w <= nleader) ? leader[w - 1] : 1;
+}
 
 enum { OR_CHAIN_LITERAL = 0, OR_CHAIN_PERSISTENT = 1 };
 enum { OR_DELIVER_REF = 0, OR_DELIVER_PAPER = 1 };

@@ -24,12 +24,12 @@ class Vid(C.Structure):
 
 class LDagS(C.Structure):
     _fields_ = [("nrounds", C.c_int32), ("slot_off", P), ("slot_id", P), ("strong_off", P), ("strong_ids", P),
-                ("weak_off", P), ("weak_ids", P)]
+                ("weak_off", P), ("weak_ids", P), ("leader", P), ("nleader", C.c_int32)]
 
 
 class PDagS(C.Structure):
     _fields_ = [("n", C.c_int32), ("W", C.c_int32), ("nrounds", C.c_int32), ("slot_off", P), ("slot_src", P),
-                ("strong", P), ("weak_off", P), ("weak_tgt", P)]
+                ("strong", P), ("weak_off", P), ("weak_tgt", P), ("leader", P), ("nleader", C.c_int32)]
 
 
 class ReplayOutS(C.Structure):
@@ -89,10 +89,33 @@ def digest(seq: Sequence[Tuple[int, int]]) -> int:
     return sum(digest_term(r, s, k) for k, (r, s) in enumerate(seq)) & ((1 << 64) - 1)
 
 
+def coin_leaders(seed: int, n: int, nwaves: int):
+    """The engine's seeded coin (DR_LEADER_SEEDED) restated: leader(w) = 1 +
+    splitmix64(seed + w * 0x9E3779B97F4A7C15) mod n, for w = 1..nwaves."""
+    M = (1 << 64) - 1
+    out = []
+    for w in range(1, nwaves + 1):
+        z = (seed + w * 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        out.append(1 + z % n)
+    return out
+
+
+def _set_leaders(obj, leaders):
+    """chooseLeader(w) = leaders[w-1] (None: the reference's constant 1)."""
+    if leaders is None:
+        obj.s.leader, obj.s.nleader = None, 0
+        return
+    obj._lead = np.ascontiguousarray(np.asarray(leaders, np.int32))
+    obj.s.leader, obj.s.nleader = _p(obj._lead), len(obj._lead)
+
+
 class LDag:
     """List-form DAG (the literal [][]vertex), from flatten_lists-style arrays or a packed prefix."""
 
-    def __init__(self, arrays=None, packed=None, nrounds: Optional[int] = None):
+    def __init__(self, arrays=None, packed=None, nrounds: Optional[int] = None, leaders=None):
         self._owned = False
         self.s = LDagS()
         if arrays is not None:
@@ -108,6 +131,7 @@ class LDag:
                                            C.byref(self.s))
             assert rc == 0
             self._owned = True
+        _set_leaders(self, leaders)
 
     def __del__(self):
         if getattr(self, "_owned", False):
@@ -150,11 +174,12 @@ class LDag:
 class PDag:
     """Packed DAG view (dag_rider_amd.dag.PackedDag duck type)."""
 
-    def __init__(self, d):
+    def __init__(self, d, leaders=None):
         self.d = d
         self._keep = [np.ascontiguousarray(x) for x in (d.slot_off, d.slot_src, d.strong, d.weak_off,
                                                          d.weak_tgt if len(d.weak_tgt) else np.zeros(1, np.uint32))]
-        self.s = PDagS(d.n, (d.n + 63) // 64, d.nrounds, *[_p(x) for x in self._keep])
+        self.s = PDagS(d.n, (d.n + 63) // 64, d.nrounds, *[_p(x) for x in self._keep], None, 0)
+        _set_leaders(self, leaders)
 
     def path(self, fr, to, strong: bool) -> int:
         return lib().or_bs_path(C.byref(self.s), Vid(*fr), Vid(*to), int(strong))

@@ -111,10 +111,11 @@ static int commit_one(const or_pdag *p, int faulty, int w, uint8_t *commit, int3
   int r1 = 4 * (w - 1) + 1;
   if (w < 1 || r1 + 3 >= p->nrounds) return OR_PANIC;
   *edges = 0;
-  if (!present(p, r1, 1)) { *commit = 0; *vcount = -1; return 0; }
+  const int L = or_leader(p->leader, p->nleader, w) - 1; /* chooseLeader(w), 0-based */
+  if (!present(p, r1, L + 1)) { *commit = 0; *vcount = -1; return 0; }
   uint64_t S[64], T[64]; /* W <= 32 */
   memset(S, 0, sizeof S);
-  S[0] = 1;
+  S[L >> 6] = 1ULL << (L & 63);
   for (int r = r1 + 1; r <= r1 + 3; r++) {
     memset(T, 0, sizeof T);
     for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++) {
@@ -159,15 +160,17 @@ static int chain_one(const or_pdag *p, int w, int floor_w, int32_t *out, uint64_
   out[np++] = w;
   uint64_t F[64], N[64];
   memset(F, 0, sizeof F);
-  F[0] = 1;
+  const int L0 = or_leader(p->leader, p->nleader, w) - 1;
+  F[L0 >> 6] = 1ULL << (L0 & 63);
   uint64_t e = 0;
   for (int r = top;; r--) {
     if (r < top && ((r - 1) & 3) == 0) {
       int w2 = (r - 1) / 4 + 1;
-      if ((F[0] & 1) && present(p, r, 1)) {
+      const int L2 = or_leader(p->leader, p->nleader, w2) - 1;
+      if (((F[L2 >> 6] >> (L2 & 63)) & 1) && present(p, r, L2 + 1)) {
         out[np++] = w2;
         memset(F, 0, sizeof F);
-        F[0] = 1;
+        F[L2 >> 6] = 1ULL << (L2 & 63);
       }
     }
     if (r <= bottom) break;
@@ -278,7 +281,7 @@ int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode, int d
     for (int64_t j = 0; j < npop; j++) {
       int top = 4 * (pops[j].leader_wave - 1) + 1;
       uint64_t *m = (uint64_t *)calloc((size_t)(top + 1) * W, sizeof(uint64_t));
-      or_vid from = {top, 1};
+      or_vid from = {top, or_leader(p->leader, p->nleader, pops[j].leader_wave)};
       uint64_t e = 0;
       or_bs_cone(p, from, 0, 0, m, &e);
       emit_pop(p, m, 0, top, pops[j].cur_round, &o->pop_count[j], &o->pop_digest[j], NULL, 0, NULL);
@@ -293,7 +296,8 @@ int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode, int d
     for (int64_t j = 0; j < npop; j++) {
       int top = 4 * (pops[j].leader_wave - 1) + 1;
       uint64_t *m = (uint64_t *)calloc((size_t)(top + 1) * W, sizeof(uint64_t));
-      m[(size_t)top * W] |= 1ULL;
+      const int L = or_leader(p->leader, p->nleader, pops[j].leader_wave) - 1;
+      m[(size_t)top * W + (L >> 6)] |= 1ULL << (L & 63);
       uint64_t e = sweep(p, top, 0, 0, m, D);
       emit_pop(p, m, 0, top, pops[j].cur_round, &o->pop_count[j], &o->pop_digest[j], o->ids,
                o->ids_cap, &o->n_ids);

@@ -139,11 +139,11 @@ int or_lit_path(const or_ldag *d, or_vid from, or_vid to, int strong_path) {
 }
 
 static inline int wave_round(int w, int k) { return 4 * (w - 1) + k; } /* process.go:400-402 */
-static inline int choose_leader(int w) { (void)w; return 1; }         /* process.go:390-392 */
+static inline int choose_leader(const or_ldag *d, int w) { return or_leader(d->leader, d->nleader, w); } /* :390-392 */
 
 /* process.go:357-371 getWaveVertexLeader: FIRST slot with source == leader */
 int or_lit_leader(const or_ldag *d, int wave, or_vid *leader) {
-  int src = choose_leader(wave);
+  int src = choose_leader(d, wave);
   int r = wave_round(wave, 1);
   if (r < 0 || r >= d->nrounds) return OR_PANIC;
   for (uint32_t i = d->slot_off[r]; i < d->slot_off[r + 1]; i++)
@@ -377,6 +377,8 @@ int or_ldag_from_packed(const or_pdag *p, int nrounds, or_ldag *out) {
   out->strong_ids = sid;
   out->weak_off = wo;
   out->weak_ids = wid;
+  out->leader = p->leader;
+  out->nleader = p->nleader;
   return 0;
 }
 
