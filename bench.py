@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 # correction of MI355X_MICROARCH.md) on this bench: tools/pmc_traffic.py output
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02", "traffic.json")
 # replay phase -> the kernels it launches (names as rocprofv3 reports them)
-PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 1024, 2, true>"],
+PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 1024, 2, false>"],
                  "sweep": ["dr::k_sweep<16, 256, 9>"],
                  "batch": ["dr::k_replay_small<8, false, true>"]}
 CPU_THREADS = 16  # the GPU box's host share for one GPU (OMP_NUM_THREADS there)

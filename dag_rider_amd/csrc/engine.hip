@@ -510,12 +510,12 @@ hipError_t launch_sc(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
                      c->view(), T, nwc, 2 * c->f + 1, c->U.as<u64>(), c->SD.as<u64>(), cm, vc);
   return hipGetLastError();
 }
-// WS = 16 (n = 1024): 1024 threads, 2 chunks per thread per group, pipelined
-// across the round barriers: 84.3 us for C4's 524.8 MB, the rate of a bare
-// blocked streaming read of the same rows (profiles/r02/v26_tune.txt)
+// WS = 16 (n = 1024): 1024 threads, 2 chunks per thread per group: 80.8 us
+// for C4's 524.8 MB (6.5 TB/s), faster than a bare blocked streaming read of
+// the same rows (profiles/r02/v29_tune.txt: 82.5 us)
 template <int WS>
 hipError_t launch_sc_shipped(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
-  if constexpr (WS == 16) return launch_sc<WS, 1024, 2, true>(c, T, nwc, cm, vc);
+  if constexpr (WS == 16) return launch_sc<WS, 1024, 2, false>(c, T, nwc, cm, vc);
   return launch_sc<WS, summary_block<WS>(), 8, false>(c, T, nwc, cm, vc);
 }
 
@@ -1454,6 +1454,11 @@ hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
       case 12: return launch_sc<WS, 256, 4, true>(c, T, nwc, cm, vc);
       case 13: return launch_sc<WS, 1024, 4, false>(c, T, nwc, cm, vc);
       case 14: return launch_sc<WS, 1024, 2, false>(c, T, nwc, cm, vc);
+      case 15: return launch_sc<WS, 1024, 1, false>(c, T, nwc, cm, vc);
+      case 16: return launch_sc<WS, 512, 2, false>(c, T, nwc, cm, vc);
+      case 17: return launch_sc<WS, 512, 4, false>(c, T, nwc, cm, vc);
+      case 18: return launch_sc<WS, 256, 2, false>(c, T, nwc, cm, vc);
+      case 19: return launch_sc<WS, 256, 4, false>(c, T, nwc, cm, vc);
     }
   }
   return launch_sc_shipped<WS>(c, T, nwc, cm, vc);

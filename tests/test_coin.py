@@ -10,7 +10,6 @@ import pytest
 
 import oracle
 from dag_rider_amd import _lib as L
-from dag_rider_amd.dag import pack_lists
 from dag_rider_amd.engine import Engine, replay_batch
 from dag_rider_amd.gen import CONFIGS, c5_config, generate
 from dagutil import random_dag
@@ -133,8 +132,8 @@ def test_gpu_coin_c2_and_c5(gpu_device):
 
 
 @pytest.mark.gpu
-def test_cpp_host_mirror_coin(gpu_device):
-    """getWaveVertexLeader follows the coin (the C++ test binary covers CONST1)."""
+def test_gpu_coin_figure1(gpu_device):
+    """waveReady on the Figure-1 DAG (process_internal_test.go:86-283) under a table coin."""
     g_leaders = [3, 2, 4]
     from dagutil import figure1
 
@@ -146,4 +145,3 @@ def test_cpp_host_mirror_coin(gpu_device):
         rc, vc, st = ld.wave_ready(g["faulty"], 1, 0)
         cm, vc_, pushed = e.wave_ready(1, 0)
         assert (cm, vc_) == (rc == 1, vc)
-        del pack_lists

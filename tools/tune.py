@@ -21,7 +21,8 @@ rows_b = T * cfg.n * W * 8 + T * W * 8 + T * 8  # rows read + U + SD written (be
 cases = [("shipped", 0, 0), ("NT512 GRP8", 0, 1), ("NT512 GRP8 pipe", 0, 2), ("NT512 GRP4 pipe", 0, 3),
          ("NT1024 GRP4 pipe", 0, 4), ("NT1024 GRP8", 0, 5), ("NT256 GRP8 pipe", 0, 6), ("NT1024 GRP2 pipe", 0, 7),
          ("NT512 GRP16", 0, 8), ("NT256 GRP16", 0, 9), ("NT512 GRP2 pipe", 0, 10), ("NT1024 GRP1 pipe", 0, 11),
-         ("NT256 GRP4 pipe", 0, 12), ("NT1024 GRP4", 0, 13), ("NT1024 GRP2", 0, 14),
+         ("NT256 GRP4 pipe", 0, 12), ("NT1024 GRP4", 0, 13), ("NT1024 GRP2", 0, 14), ("NT1024 GRP1", 0, 15),
+         ("NT512 GRP2", 0, 16), ("NT512 GRP4", 0, 17), ("NT256 GRP2", 0, 18), ("NT256 GRP4", 0, 19),
          ("stream rows", 1, 0), ("stream rows blocked", 1, 2)]
 res = {name: [] for name, *_ in cases}
 for rep in range(5):
