@@ -112,6 +112,7 @@ struct dr_ctx {
   // of the flattened device arrays (valid for rounds < up_lo)
   std::vector<HostRound> hr;
   std::vector<u64> h_present;
+  std::vector<int32_t> wc_tab;  // append scratch: weak column of (delta, target) in the round being built
   std::vector<uint32_t> h_slot_off{0}, h_wc_roff{0}, h_far_roff{0}, h_weak_roff{0};
   int up_lo = 0;  // lowest round whose flattened device arrays are stale
   // round summaries (U, SD, WU) per round: sdirty[r] = stale; the canonical cone
@@ -134,6 +135,8 @@ struct dr_ctx {
   hipError_t rec(int i) { return timed(i) ? hipEventRecord(ev[i], stream) : hipSuccess; }
   int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies  // hC/hG/hE mirror Cc/Gc/Ec (fetched lazily after a planned replay)
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
+  DevBuf plan_out;          // its outputs, packed for one copy back
+  std::vector<char> plan_host;
   DevBuf batch_arena;       // dr_replay_batch scratch + outputs (batch.hpp)
   std::vector<char> batch_host;  // dr_replay_batch output region, host side
   // memo needs every weak edge in the dense summary window
@@ -151,7 +154,8 @@ struct dr_ctx {
   size_t pin_cap = 0, pin_used = 0;
   struct Pending { void *dst; void *stage; const void *src; size_t n; };
   std::vector<Pending> pend;
-  hipEvent_t ev_sync = nullptr, ev_sync2 = nullptr, ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_sync = nullptr, ev_sync2 = nullptr, ev_fork = nullptr, ev_join = nullptr, ev_start = nullptr,
+            ev_wu = nullptr;
   hipStream_t stream2 = nullptr;  // second queue: canonical cone beside the leader chains
   hipError_t launch_copies(const dr::CopySeg *sg, int k) {
     for (int i0 = 0; i0 < k; i0 += dr::kCopySegs) {
@@ -464,24 +468,25 @@ hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode) {
 
 constexpr int kEmitRPB = 4;  // rounds per emit workgroup: one per wave
 
-template <int WS>
 // Planned mode (plan != nullptr, device-planned replay): the count pass runs
 // ndesc = an upper bound of workgroups and reads the true count from plan[0];
 // the digest pass strides a fixed grid over the work items item_pref describes.
+// pd == nullptr: one segment, described by d1 (passed by value).
+template <int WS>
 hipError_t launch_emit_t(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
                          u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase,
-                         const int *plan, const int64_t *item_pref) {
+                         const int *plan, const int64_t *item_pref, const dr::PopDesc &d1) {
   if (count_phase) {
     hipLaunchKernelGGL((dr::k_emit_count<WS, 256>), dim3(ndesc), dim3(256), 0, c->stream, c->view(), pd,
                        c->masks.as<u64>(), c->K.as<u64>(), rbase, cnt, plan);
   } else if (plan) {
     hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(2048), dim3(256), 0, c->stream, c->view(),
-                       c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, c->masks.as<u64>(),
+                       c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, d1, c->masks.as<u64>(),
                        c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, item_pref, plan);
   } else {
     const int bx = std::max(1, (span + kEmitRPB - 1) / kEmitRPB);
     hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(bx, ndesc), dim3(256), 0, c->stream, c->view(),
-                       c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, c->masks.as<u64>(),
+                       c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, d1, c->masks.as<u64>(),
                        c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, (const int64_t *)nullptr,
                        (const int *)nullptr);
   }
@@ -489,15 +494,16 @@ hipError_t launch_emit_t(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, 
 }
 hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
                        u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase,
-                       const int *plan = nullptr, const int64_t *item_pref = nullptr) {
+                       const int *plan = nullptr, const int64_t *item_pref = nullptr,
+                       const dr::PopDesc &d1 = dr::PopDesc{}) {
   if (ndesc <= 0) return hipSuccess;
   switch (c->WS) {
-    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
-    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
-    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
-    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
-    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
-    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref);
+    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
+    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
+    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
+    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
+    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
+    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
   }
   return hipErrorInvalidValue;
 }
@@ -519,17 +525,32 @@ hipError_t launch_sc_shipped(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc
   return launch_sc<WS, summary_block<WS>(), 8, false>(c, T, nwc, cm, vc);
 }
 
+// rows + commit decisions (U, SD); the weak-edge unions (WU) come from the
+// weak-column keys alone (launch_weak_union), beside it or after it
 template <int WS>
 hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
-  // rows + commit decisions (U, SD), then the weak-edge unions (WU) from the
-  // weak-column keys: two back-to-back passes (profiles/r01/v5_tune.txt)
-  const dr::MemoView mv = c->memo_view();
   hipError_t e = launch_sc_shipped<WS>(c, T, nwc, cm, vc);
   if (e == hipSuccess) e = c->rec(7);  // ms_summary times k_summary_commit alone (the roofline kernel)
-  if (e != hipSuccess || mv.dd == 0) return e;
-  hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, c->stream, c->view(), T, mv.dd,
-                     c->WU.as<u64>(), (const int32_t *)nullptr);
+  return e;
+}
+template <int WS>
+hipError_t launch_weak_union_t(dr_ctx *c, int T, hipStream_t st) {
+  const int dd = c->memo_dd();
+  if (dd == 0) return hipSuccess;
+  hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, st, c->view(), T, dd, c->WU.as<u64>(),
+                     (const int32_t *)nullptr);
   return hipGetLastError();
+}
+hipError_t launch_weak_union(dr_ctx *c, int T, hipStream_t st) {
+  switch (c->WS) {
+    case 1: return launch_weak_union_t<1>(c, T, st);
+    case 2: return launch_weak_union_t<2>(c, T, st);
+    case 4: return launch_weak_union_t<4>(c, T, st);
+    case 8: return launch_weak_union_t<8>(c, T, st);
+    case 16: return launch_weak_union_t<16>(c, T, st);
+    case 32: return launch_weak_union_t<32>(c, T, st);
+  }
+  return hipErrorInvalidValue;
 }
 
 // incremental summaries of the listed rounds (device list of nr rounds)
@@ -562,7 +583,7 @@ template <int WS>
 hipError_t launch_canon_cone_t(dr_ctx *c, int T) {
   const dr::MemoView mv = c->memo_view();
   hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
-                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>());
+                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int dl = c->depth_log2();
@@ -571,25 +592,9 @@ hipError_t launch_canon_cone_t(dr_ctx *c, int T) {
   e = hipFuncSetAttribute((const void *)dr::k_canon<WS, NTS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((dr::k_canon<WS, NTS>), dim3(1), dim3(NTS), lds, c->stream, c->view(), mv, T, dl,
-                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>());
+                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>(), c->RD.as<u64>(),
+                     c->Cc.as<u64>(), c->crbase.as<uint32_t>());
   return hipGetLastError();
-}
-template <int WS>
-hipError_t launch_canon_count_t(dr_ctx *c, int T) {
-  hipLaunchKernelGGL((dr::k_canon_count<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), T,
-                     c->K.as<u64>(), c->RD.as<u64>());
-  return hipGetLastError();
-}
-hipError_t launch_canon_count(dr_ctx *c, int T) {
-  switch (c->WS) {
-    case 1: return launch_canon_count_t<1>(c, T);
-    case 2: return launch_canon_count_t<2>(c, T);
-    case 4: return launch_canon_count_t<4>(c, T);
-    case 8: return launch_canon_count_t<8>(c, T);
-    case 16: return launch_canon_count_t<16>(c, T);
-    case 32: return launch_canon_count_t<32>(c, T);
-  }
-  return hipErrorInvalidValue;
 }
 hipError_t launch_canon_cone(dr_ctx *c, int T) {
   switch (c->WS) {
@@ -665,7 +670,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
     return DR_E_HIP;
   }
   for (auto &ev : c->ev) (void)hipEventCreate(&ev);
-  for (hipEvent_t *e : {&c->ev_sync, &c->ev_sync2, &c->ev_fork, &c->ev_join})
+  for (hipEvent_t *e : {&c->ev_sync, &c->ev_sync2, &c->ev_fork, &c->ev_join, &c->ev_start, &c->ev_wu})
     (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
   const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64);
   if (c->strong.ensure(rows) != hipSuccess ||
@@ -706,13 +711,13 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->digest,  &c->pop_pos, &c->ids,      &c->U,        &c->WU,
                     &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
-                    &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds,
+                    &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds, &c->plan_out,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
                     &c->admit_buf, &c->lead};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
-  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join})
+  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join, c->ev_start, c->ev_wu})
     if (e) (void)hipEventDestroy(e);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -776,8 +781,12 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   size_t nfar = 0;
   int dmax = c->dmax_near;
   const u64 lastmask = (n % 64) ? ((1ULL << (n % 64)) - 1ULL) : ~0ULL;
-  std::vector<uint32_t> wl, tmp;  // one round's near weak edges: delta << 22 | own << 11 | t
-  std::vector<uint32_t> cnt(2048);
+  // weak columns of a round: tab[delta * n + t] = column index of (delta, t)
+  // (-1 = none yet); touched entries are reset after each round
+  if (c->wc_tab.empty()) c->wc_tab.assign((size_t)1024 * n, -1);
+  std::vector<int32_t> &tab = c->wc_tab;
+  std::vector<uint32_t> touched, order;
+  std::vector<u64> rows_tmp;
   for (int i = 0; i < k; i++) {
     const int r = r0 + i;
     u64 *P = &pres[(size_t)i * WS];
@@ -792,7 +801,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
       if ((wd & bit) && r >= 1) return c->fail(DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, s);
       wd |= bit;
     }
-    wl.clear();
+    touched.clear();
     for (int s0 = 0; s0 < n; s0++) {
       const bool here = (P[s0 >> 6] >> (s0 & 63)) & 1ULL;
       const uint64_t *row = strong + ((size_t)i * n + s0) * W;
@@ -816,7 +825,15 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
         if (tr > r - 2) return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target a round < r-1", r, s0 + 1, tr, ts + 1);
         const int delta = r - tr;
         if (delta <= 1023) {
-          wl.push_back(((uint32_t)delta << 22) | ((uint32_t)s0 << 11) | (uint32_t)ts);
+          const size_t at = (size_t)delta * n + ts;
+          int32_t col = tab[at];
+          if (col < 0) {
+            col = tab[at] = (int32_t)h.wc_key.size();
+            touched.push_back((uint32_t)at);
+            h.wc_key.push_back(((uint32_t)delta << 11) | (uint32_t)ts);
+            h.wc_rows.resize(h.wc_rows.size() + WS, 0ULL);
+          }
+          h.wc_rows[(size_t)col * WS + (s0 >> 6)] |= 1ULL << (s0 & 63);
           dmax = std::max(dmax, delta);
         } else {
           h.far.push_back(((u64)s0 << 32) | t);
@@ -824,35 +841,30 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
         }
       }
     }
-    // weak columns: sort the round's edges by (delta, target) (2-pass LSD radix);
-    // each run of equal keys is one column, its row the run's sources
-    if (wl.size() >= 2) {
-      tmp.resize(wl.size());
-      uint32_t *src = wl.data(), *dst = tmp.data();
-      for (int pass = 0; pass < 2; pass++) {
-        const int sh = pass == 0 ? 0 : 22, nb = pass == 0 ? 2048 : 1024;
-        std::fill(cnt.begin(), cnt.begin() + nb, 0);
-        for (size_t e = 0; e < wl.size(); e++) cnt[(src[e] >> sh) & (nb - 1)]++;
-        uint32_t run = 0;
-        for (int t = 0; t < nb; t++) { const uint32_t c2 = cnt[t]; cnt[t] = run; run += c2; }
-        for (size_t e = 0; e < wl.size(); e++) dst[cnt[(src[e] >> sh) & (nb - 1)]++] = src[e];
-        std::swap(src, dst);
+    for (uint32_t at : touched) tab[at] = -1;
+    // columns sorted by key (wc_add's binary search relies on it; no kernel does)
+    const size_t nk = h.wc_key.size();
+    bool sorted = true;
+    for (size_t x = 1; x < nk && sorted; x++) sorted = h.wc_key[x - 1] < h.wc_key[x];
+    if (!sorted) {
+      order.resize(nk);
+      for (size_t x = 0; x < nk; x++) order[x] = (uint32_t)x;
+      std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return h.wc_key[a] < h.wc_key[b]; });
+      std::vector<uint32_t> keys(nk);
+      rows_tmp.resize(nk * WS);
+      for (size_t x = 0; x < nk; x++) {
+        keys[x] = h.wc_key[order[x]];
+        std::memcpy(&rows_tmp[x * WS], &h.wc_rows[(size_t)order[x] * WS], (size_t)WS * 8);
       }
-      // after two passes the sorted data is back in wl
-    }
-    for (size_t e = 0; e < wl.size(); e++) {
-      const uint32_t x = wl[e], key = ((x >> 22) << 11) | (x & 2047u);
-      if (h.wc_key.empty() || key != h.wc_key.back()) {
-        h.wc_key.push_back(key);
-        h.wc_rows.resize(h.wc_rows.size() + WS, 0ULL);
-      }
-      const uint32_t own = (x >> 11) & 2047u;
-      h.wc_rows[h.wc_rows.size() - WS + (own >> 6)] |= 1ULL << (own & 63);
+      h.wc_key.swap(keys);
+      h.wc_rows.swap(rows_tmp);
     }
   }
   // ---- commit: rows and per-vertex degrees, then the flattened per-round arrays ----
   const size_t row_words = (size_t)n * WS;
-  if (WS == W) {
+  if (WS == W && (size_t)k * row_words * 8 <= ((size_t)16 << 20)) {  // per-round appends: pinned staging
+    HIPCHK(c, c->h2d(c->strong.as<u64>() + (size_t)r0 * row_words, strong, (size_t)k * row_words * 8));
+  } else if (WS == W) {  // bulk loads: straight from the caller's memory
     HIPCHK(c, hipMemcpyAsync(c->strong.as<u64>() + (size_t)r0 * row_words, strong,
                              (size_t)k * row_words * 8, hipMemcpyHostToDevice, c->stream));
   } else {
@@ -863,10 +875,8 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  HIPCHK(c, hipMemcpyAsync(c->sdeg.as<uint16_t>() + (size_t)r0 * n, vdeg.data(), vdeg.size() * 2,
-                           hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->wdeg.as<uint16_t>() + (size_t)r0 * n, vwdeg.data(), vwdeg.size() * 2,
-                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, c->h2d(c->sdeg.as<uint16_t>() + (size_t)r0 * n, vdeg.data(), vdeg.size() * 2));
+  HIPCHK(c, c->h2d(c->wdeg.as<uint16_t>() + (size_t)r0 * n, vwdeg.data(), vwdeg.size() * 2));
   for (auto &h : nh) c->hr.push_back(std::move(h));
   c->h_present.insert(c->h_present.end(), pres.begin(), pres.end());
   c->nfar += nfar;
@@ -1218,7 +1228,7 @@ int ensure_summary_bufs(dr_ctx *c) {
   HIPCHK(c, c->WU.ensure(std::max<size_t>(R * dd * WS, 1) * 8));
   HIPCHK(c, c->SD.ensure(R * 8));
   HIPCHK(c, c->K.ensure(R * WS * 8));
-  HIPCHK(c, c->good.ensure(R));
+  HIPCHK(c, c->good.ensure(R + 8));  // k_canon reads good[] 8 rounds at a time
   HIPCHK(c, c->CE.ensure(R * 8));
   HIPCHK(c, c->RD.ensure(R * 8));
   HIPCHK(c, c->Cc.ensure(R * 8));
@@ -1283,12 +1293,9 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side) {
     HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   }
   Swap sw(c, fork && !side);
+  // canonical cone, per-round counts and positions (k_kcand + k_canon), then the
+  // per-round digests (emission) and their prefixes
   HIPCHK(c, launch_canon_cone(c, T));
-  // canonical emission: per-round counts -> positions -> per-round digests -> prefixes
-  HIPCHK(c, launch_canon_count(c, T));
-  hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
-                     (const u64 *)nullptr, c->Cc.as<u64>(), (u64 *)nullptr, c->crbase.as<uint32_t>());
-  HIPCHK(c, hipGetLastError());
   dr::PopDesc d{};
   d.mask_off = 0;
   d.rbase_off = 1;  // crbase is indexed by round; rbase_off addresses round `first`
@@ -1297,10 +1304,8 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side) {
   d.last = T;
   d.out = 0;
   d.use_k = 1;
-  HIPCHK(c, c->popdesc.ensure(sizeof(dr::PopDesc)));
-  HIPCHK(c, c->h2d(c->popdesc.p, &d, sizeof d));
-  HIPCHK(c, launch_emit(c, 1, T, c->popdesc.as<dr::PopDesc>(), c->crbase.as<uint32_t>(), nullptr, nullptr,
-                        c->RD.as<u64>(), nullptr, nullptr, 0, false));
+  HIPCHK(c, launch_emit(c, 1, T, nullptr, c->crbase.as<uint32_t>(), nullptr, nullptr, c->RD.as<u64>(), nullptr,
+                        nullptr, 0, false, nullptr, nullptr, d));  // the descriptor travels by value
   hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
                      c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
@@ -1350,8 +1355,16 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   if (int rc = ensure_summary_bufs(c)) return rc;
   HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
   HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
+  if (fork) {  // the weak unions on stream2, beside the row pass
+    HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+    HIPCHK(c, launch_weak_union(c, T, c->stream2));
+    HIPCHK(c, hipEventRecord(c->ev_wu, c->stream2));
+  }
   HIPCHK(c, c->rec(6));
   HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
+  if (fork) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_wu, 0));
+  else HIPCHK(c, launch_weak_union(c, T, c->stream));
   mark_rounds_clean(c);
   if (int rc = launch_canon(c, fork, side)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
@@ -2165,20 +2178,21 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     }
   }
   HIPCHK(c, c->masks.ensure(mask_words * 8));
-  // host-visible outputs (pinned, written by k_plan_final)
-  void *hp = nullptr;
+  // outputs: k_plan_final packs them into one device region, which comes back
+  // in one copy (writing them straight into pinned host memory from the kernel
+  // took 19.5 us, profiles/r02/v27_timeline.txt)
   const size_t h_bytes = 16 * 8 + (size_t)nw + 4 * (size_t)nw + 4 * ((size_t)nw + 1) + 4 * (size_t)pcap +
-                         3 * 8 * (size_t)pcap + 5 * 64;
-  HIPCHK(c, c->stage(h_bytes, &hp));
+                         3 * 8 * (size_t)pcap + 8 * 256;
+  HIPCHK(c, c->plan_out.ensure(h_bytes));
   Carve hv;
-  hv.base = static_cast<char *>(hp);
+  hv.base = c->plan_out.as<char>();
   u64 *h_hdr = hv.take<u64>(dr::PH_N);
   uint8_t *h_commit = hv.take<uint8_t>(nw);
   int32_t *h_vcount = hv.take<int32_t>(nw);
   uint32_t *h_push_off = hv.take<uint32_t>(nw + 1);
   int32_t *h_push_wave = hv.take<int32_t>(pcap);
   u64 *h_pc = hv.take<u64>(pcap), *h_pd = hv.take<u64>(pcap), *h_pe = hv.take<u64>(pcap);
-  if (hv.off > c->pin_cap - (static_cast<char *>(hp) - c->pin)) return c->fail(DR_E_STATE, "staging overflow");
+  const size_t out_bytes = hv.off;
 
   // 0+1. summaries + commits; then the leader chains and pop planning on stream2
   // beside the canonical cone on the main stream (the cone takes longer, so the
@@ -2245,7 +2259,21 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
                      digest, cedges, dstats, c->nseg.as<int32_t>(), plan, h_commit, h_vcount, h_push_off,
                      h_push_wave, h_pc, h_pd, h_pe, h_hdr);
   HIPCHK(c, hipGetLastError());
+  c->plan_host.resize(out_bytes);
+  HIPCHK(c, c->d2h(c->plan_host.data(), c->plan_out.p, out_bytes));
   HIPCHK(c, c->sync());
+  {  // device addresses -> the same offsets in the host copy
+    char *hb = c->plan_host.data(), *db = c->plan_out.as<char>();
+    auto H = [&](auto *p) { return reinterpret_cast<decltype(p)>(hb + (reinterpret_cast<char *>(p) - db)); };
+    h_hdr = H(h_hdr);
+    h_commit = H(h_commit);
+    h_vcount = H(h_vcount);
+    h_push_off = H(h_push_off);
+    h_push_wave = H(h_push_wave);
+    h_pc = H(h_pc);
+    h_pd = H(h_pd);
+    h_pe = H(h_pe);
+  }
   // outputs
   o->ms_summary = o->ms_chain = o->ms_deliver = o->ms_emit = 0;
   if (c->timed(6)) HIPCHK(c, hipEventElapsedTime(&o->ms_summary, c->ev[6], c->ev[7]));

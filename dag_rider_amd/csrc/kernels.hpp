@@ -246,42 +246,45 @@ struct MemoView {
 };
 
 // strong rows of the vertices in FE (round r) -> ring slot of round r-1.
-// Loads go out in groups of GRP passes (16 B each), so register use does not grow
-// with the rows per thread.  With Ur (round r's union of rows, from the round
-// summaries) a wave stops loading rows once the OR of the rows it has read equals
-// Ur -- no further row can add a bit -- and takes the remaining frontier vertices'
-// strong degrees from sdeg (2 B instead of a W*8-B row) for the edge count.  The
-// result is exact either way.  row_bytes counts the bytes actually read.
+// Edges: the frontier's strong degrees from sdeg, every thread summing a
+// contiguous run of sources with independent loads (2 B per vertex instead of a
+// W*8-B row; sdeg is the rows' popcount, so the count is exact).  Rows: loads go
+// out in groups of GRP passes (16 B each), so register use does not grow with
+// the rows per thread.  With Ur (round r's union of rows, from the round
+// summaries) a wave stops loading rows once the OR of the rows it has read
+// equals Ur -- no further row can add a bit.  row_bytes counts the bytes read.
 template <int WS, int NT>
 __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *FE, u64 *ring, int dmask,
                                             u64 &my_edges, const u64 *Ur, u64 &row_bytes) {
   using G = Geo<WS, NT>;
-  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT, NMAX = G::NMAX;
   constexpr int GRP = CPT < 2 ? CPT : 2;
+  constexpr int SPT = (NMAX + NT - 1) / NT;  // sources per thread for the degree sum
   const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
   const u64 *rows = g.strong + (size_t)r * n * WS;
   const uint16_t *deg = g.sdeg + (size_t)r * n;
+  {
+    uint32_t dsum = 0, cnt = 0;
+#pragma unroll
+    for (int k = 0; k < SPT; k++) {
+      const int s = tid * SPT + k;
+      if (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
+        dsum += deg[s];
+        cnt++;
+      }
+    }
+    my_edges += dsum;
+    row_bytes += 2 * cnt;
+  }
   u64 a0 = 0, a1 = 0;
   u64 u0 = ~0ULL, u1 = ~0ULL;  // never equal to a partial OR when Ur is absent
   if (Ur) {
     u0 = Ur[CW * j];
     u1 = CW == 2 ? Ur[CW * j + 1] : 0ULL;
   }
-  bool sat = false;
 #pragma unroll 1
   for (int p0 = 0; p0 < CPT; p0 += GRP) {
     if ((tid / CPR) + p0 * RPP - (tid & ~63) / CPR >= n) break;  // wave-uniform: rows of this wave done
-    if (sat) {  // rows cannot add bits: degrees only
-#pragma unroll
-      for (int p = 0; p < GRP; p++) {
-        const int s = tid / CPR + (p0 + p) * RPP;
-        if (j == 0 && s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
-          my_edges += deg[s];
-          row_bytes += 2;
-        }
-      }
-      continue;
-    }
     u64 v0[GRP], v1[GRP];
 #pragma unroll
     for (int p = 0; p < GRP; p++) {
@@ -303,7 +306,6 @@ __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *
     for (int p = 0; p < GRP; p++) {
       a0 |= v0[p];
       a1 |= v1[p];
-      my_edges += (u64)(popc64(v0[p]) + popc64(v1[p]));
     }
     if (Ur) {  // the wave's OR so far (lanes of one chunk class j) against U_r
       u64 r0 = a0, r1 = a1;
@@ -312,7 +314,7 @@ __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *
         r0 |= __shfl_xor(r0, off);
         if (CW == 2) r1 |= __shfl_xor(r1, off);
       }
-      sat = __ballot(r0 != u0 || r1 != u1) == 0ULL;
+      if (__ballot(r0 != u0 || r1 != u1) == 0ULL) break;  // saturated: no row can add a bit
     }
   }
   // chunk j = lane mod CPR: fold each row's lanes of class j, then one LDS OR per row
@@ -888,14 +890,16 @@ __global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64
 
 // K^cand_r = U_{r+1} | OR_d WU_{r+d+2}[d] (the cone of round r when every round
 // above it is full); K^cand_T = P_T.  good_r = K^cand_r covers P_r.  CE_r (the
-// canonical round's edges) defaults to the full-round total.  One wave per
-// round, lane w < WS owns word w.
+// canonical round's edges) defaults to the full-round total, RD_r (its vertex
+// count |K_r & P_r|) to K^cand's.  One wave per round, lane w < WS owns word w.
 template <int WS>
 __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K,
-                                               uint8_t *__restrict__ good, u64 *__restrict__ CE) {
+                                               uint8_t *__restrict__ good, u64 *__restrict__ CE,
+                                               u64 *__restrict__ RD) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
   if (r > T) return;
   bool bad = false;
+  int cnt = 0;
   if (w < WS) {
     const u64 p = g.present[(size_t)r * WS + w];
     u64 k;
@@ -907,11 +911,15 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
     }
     K[(size_t)r * WS + w] = k;
     bad = (k & p) != p;
+    cnt = popc64(k & p);
   }
   const bool ok = __ballot(bad) == 0ULL;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
   if (w == 0) {
     good[r] = ok;
     CE[r] = r == 0 ? 0 : mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
+    RD[r] = r == 0 ? 0 : (u64)cnt;
   }
 }
 
@@ -919,12 +927,17 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
 // k_canon: one workgroup walks the canonical cone from the top.  Rounds whose
 // K^cand covers the round (good) and whose dmax-window above is full are exact
 // already; at each bad round b a segment sweep (rows where partial, summaries
-// where full) runs until dmax consecutive full rounds restore the regime.
+// where full) runs until dmax consecutive full rounds restore the regime.  The
+// next bad round below is found 8 rounds per thread (one 8-B load of good[]).
+// Then the canonical positions: C_r = sum of RD over rounds 1..r, crbase_r =
+// C_{r-1} (k_kcand's counts, rewritten here for the segment rounds).
 // ---------------------------------------------------------------------------
 template <int WS, int NT>
 __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int depth_log2,
                                               u64 *__restrict__ K, const uint8_t *__restrict__ good,
-                                              u64 *__restrict__ CE, int32_t *__restrict__ nseg) {
+                                              u64 *__restrict__ CE, int32_t *__restrict__ nseg,
+                                              u64 *__restrict__ RD, u64 *__restrict__ Cc,
+                                              uint32_t *__restrict__ crbase) {
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
   u64 *F = smem, *FE = smem + WS, *ring = smem + 2 * WS;
   const int depth = 1 << depth_log2, dmask = depth - 1;
@@ -934,12 +947,22 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
   int pos = T;  // rounds >= pos are final; the regime holds below pos until the next bad round
   int segs = 0;
   while (true) {
-    // next bad round below pos
+    // next bad round below pos: thread t looks at the 8 rounds of block (pos-1)/8 - t - i*NT
     if (tid == 0) s_ctl[0] = -1;
     __syncthreads();
-    for (int base = pos - 1; base >= 0; base -= NT) {
-      const int idx = base - tid;
-      if (idx >= 0 && !good[idx]) atomicMax(&s_ctl[0], idx);
+    for (int b0 = (pos - 1) >> 3; b0 >= 0; b0 -= NT) {
+      const int b = b0 - tid;
+      if (b >= 0) {
+        const u64 v = *reinterpret_cast<const u64 *>(good + 8 * (size_t)b);
+#pragma unroll
+        for (int k = 7; k >= 0; k--) {
+          const int x = 8 * b + k;
+          if (x < pos && !((v >> (8 * k)) & 0xffULL)) {
+            atomicMax(&s_ctl[0], x);
+            break;
+          }
+        }
+      }
       __syncthreads();
       if (s_ctl[0] >= 0) break;
       __syncthreads();
@@ -963,18 +986,31 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     int run = 0;
     int r = b;
     for (;; --r) {
-      if (tid < WS) {
-        if (r > 0) load_round<WS, false, true, true>(g, mv, r - 1, nxt);
-        const int slot = (r & dmask) * WS + tid;
-        const u64 f = ring[slot];
-        ring[slot] = 0;
-        const u64 p = cur.P;
-        F[tid] = f;
-        FE[tid] = f & p;
-        K[(size_t)r * WS + tid] = f;
-        const bool full = __all((f & p) == p);
+      if (tid < 64) {
+        int cnt = 0;
+        bool full = true;
+        if (tid < WS) {
+          if (r > 0) load_round<WS, false, true, true>(g, mv, r - 1, nxt);
+          const int slot = (r & dmask) * WS + tid;
+          const u64 f = ring[slot];
+          ring[slot] = 0;
+          const u64 p = cur.P;
+          F[tid] = f;
+          FE[tid] = f & p;
+          K[(size_t)r * WS + tid] = f;
+          full = (f & p) == p;
+          cnt = popc64(f & p);
+        }
+        full = __all(full);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
         run = full ? run + 1 : 0;
-        if (tid == 0) { s_ctl[1] = full; s_ctl[2] = (run >= mv.dmax) || r == 0; s_edges[0] = 0; }
+        if (tid == 0) {
+          s_ctl[1] = full;
+          s_ctl[2] = (run >= mv.dmax) || r == 0;
+          s_edges[0] = 0;
+          RD[r] = r == 0 ? 0 : (u64)cnt;
+        }
       }
       __syncthreads();
       if (s_ctl[2]) break;  // regime restored at r (or bottom reached): CE_r stays the full total
@@ -997,6 +1033,27 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     pos = r;
   }
   if (tid == 0 && nseg) *nseg = segs;
+  // canonical positions (the RD writes above are this workgroup's own: visible after the barrier)
+  __syncthreads();
+  __shared__ u64 part[NT];
+  const int per = (T + 1 + NT - 1) / NT;
+  const int ra = tid * per, rb = min(T + 1, ra + per);
+  u64 loc = 0;
+  for (int x = ra; x < rb; x++) loc += RD[x];
+  part[tid] = loc;
+  __syncthreads();
+  for (int off = 1; off < NT; off <<= 1) {
+    const u64 v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  u64 run = part[tid] - loc;
+  for (int x = ra; x < rb; x++) {
+    crbase[x] = (uint32_t)run;
+    run += RD[x];
+    Cc[x] = run;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1137,7 +1194,7 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
 template <int WS, int NT, int RPB>
 __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__restrict__ slot_off,
                                                  const uint16_t *__restrict__ slot_src,
-                                                 const PopDesc *__restrict__ pd,
+                                                 const PopDesc *__restrict__ pd, const PopDesc d1,
                                                  const u64 *__restrict__ masks, const u64 *__restrict__ K,
                                                  const uint32_t *__restrict__ rbase,
                                                  const int64_t *__restrict__ pop_pos,
@@ -1146,8 +1203,8 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
                                                  const int64_t *__restrict__ item_pref, const int *__restrict__ ctl) {
   __shared__ u64 s_dg;
   if (!item_pref) {
-    emit_block<WS, NT, RPB>(g, slot_off, slot_src, pd[blockIdx.y], blockIdx.x, masks, K, rbase, pop_pos, digest,
-                            round_out, ids, ids_cap, &s_dg);
+    emit_block<WS, NT, RPB>(g, slot_off, slot_src, pd ? pd[blockIdx.y] : d1, blockIdx.x, masks, K, rbase, pop_pos,
+                            digest, round_out, ids, ids_cap, &s_dg);
     return;
   }
   const int nd = ctl[0];
@@ -1162,18 +1219,6 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
                             digest, round_out, ids, ids_cap, &s_dg);
     __syncthreads();
   }
-}
-
-// Canonical per-round delivered counts c_r = |K_r & P_r| (one wave per round).
-template <int WS>
-__global__ __launch_bounds__(256) void k_canon_count(DagView g, int T, const u64 *__restrict__ K,
-                                                     u64 *__restrict__ cnt) {
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
-  if (r > T) return;
-  int c = (w < WS && r >= 1) ? popc64(K[(size_t)r * WS + w] & g.present[(size_t)r * WS + w]) : 0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-  if (w == 0) cnt[r] = (u64)c;
 }
 
 // Inclusive prefix over rounds 0..T of up to three per-round arrays (one
