@@ -1355,16 +1355,12 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   if (int rc = ensure_summary_bufs(c)) return rc;
   HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
   HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
-  if (fork) {  // the weak unions on stream2, beside the row pass
-    HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_start, 0));
-    HIPCHK(c, launch_weak_union(c, T, c->stream2));
-    HIPCHK(c, hipEventRecord(c->ev_wu, c->stream2));
-  }
+  // rows + commits, then the weak unions from the weak-column keys (on a second
+  // stream beside the row pass they only queued behind its workgroups and paid a
+  // cross-stream join: profiles/r02/v30_timeline.txt)
   HIPCHK(c, c->rec(6));
   HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
-  if (fork) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_wu, 0));
-  else HIPCHK(c, launch_weak_union(c, T, c->stream));
+  HIPCHK(c, launch_weak_union(c, T, c->stream));
   mark_rounds_clean(c);
   if (int rc = launch_canon(c, fork, side)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
@@ -2169,7 +2165,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     pedges = cv.take<u64>(pcap);
     counts = cv.take<u64>(pcap);
     digest = cv.take<u64>(pcap);
-    item_pref = cv.take<int64_t>(pcap + 1);
+    item_pref = cv.take<int64_t>(pcap + 1 + (size_t)rb_cap / kEmitRPB + pcap);  // prefix, then item -> segment
     pd = cv.take<dr::PopDesc>(pcap);
     rbase = cv.take<uint32_t>((size_t)rb_cap);
     if (pass == 0) {

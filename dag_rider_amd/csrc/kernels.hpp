@@ -245,43 +245,61 @@ struct MemoView {
   int32_t dmax;  // merge window = max(1, largest weak delta)
 };
 
-// strong rows of the vertices in FE (round r) -> ring slot of round r-1.
-// Edges: the frontier's strong degrees from sdeg, every thread summing a
-// contiguous run of sources with independent loads (2 B per vertex instead of a
-// W*8-B row; sdeg is the rows' popcount, so the count is exact).  Rows: loads go
-// out in groups of GRP passes (16 B each), so register use does not grow with
-// the rows per thread.  With Ur (round r's union of rows, from the round
-// summaries) a wave stops loading rows once the OR of the rows it has read
-// equals Ur -- no further row can add a bit.  row_bytes counts the bytes read.
-template <int WS, int NT>
-__device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *FE, u64 *ring, int dmask,
-                                            u64 &my_edges, const u64 *Ur, u64 &row_bytes) {
+// One partial round r of a sweep: the frontier FE's strong rows -> ring slot of
+// round r-1, and (WEAK) its weak columns -> the ring slots (or far mask rows,
+// mask_bottom) of their target rounds.  Returns the lowest target round.
+// Every load that does not depend on another goes out first -- the round's weak
+// columns (WPF passes of WS-lane entries), the frontier's strong degrees and the
+// first group of rows -- so a round costs a few memory latencies, not one per
+// loop step.  Edges: the frontier's strong degrees from sdeg (2 B per vertex, the
+// rows' exact popcount) plus one per followed weak edge.  Rows: GRP 16-B chunks
+// per thread in flight; with Ur (round r's union of rows, from the round
+// summaries) a wave stops loading rows once the OR of what it has read equals Ur
+// -- no further row can add a bit.  wc0/wc1: the round's weak-column range when
+// the caller prefetched it (-1: read it here).  row_bytes counts bytes read.
+template <int WS, int NT, bool WEAK>
+__device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom, const u64 *FE, u64 *ring, int depth,
+                                            u64 *mask_bottom, const u64 *Ur, u64 &my_edges, u64 &my_wedges,
+                                            u64 &row_bytes, int64_t wc0 = -1, int64_t wc1 = -1) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT, NMAX = G::NMAX;
   constexpr int GRP = CPT < 2 ? CPT : 2;
   constexpr int SPT = (NMAX + NT - 1) / NT;  // sources per thread for the degree sum
-  const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
-  const u64 *rows = g.strong + (size_t)r * n * WS;
-  const uint16_t *deg = g.sdeg + (size_t)r * n;
-  {
-    uint32_t dsum = 0, cnt = 0;
+  static_assert(WS <= 64 && (64 % WS) == 0, "WS lanes per weak-column entry");
+  constexpr int EPP = NT / WS;  // weak-column entries per pass
+  constexpr int WPF = 4;        // weak passes loaded up front
+  const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n, dmask = depth - 1;
+  const int w = tid % WS, gbase = lane & ~(WS - 1);
+  int lowmin = 0x7fffffff;
+  // ---- independent loads first ----
+  uint32_t c0 = 0, c1 = 0;
+  u64 wv[WPF];
+  uint32_t wk[WPF];
+  if constexpr (WEAK) {
+    c0 = wc0 >= 0 ? (uint32_t)wc0 : g.wc_roff[r];
+    c1 = wc1 >= 0 ? (uint32_t)wc1 : g.wc_roff[r + 1];
 #pragma unroll
-    for (int k = 0; k < SPT; k++) {
-      const int s = tid * SPT + k;
-      if (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) {
-        dsum += deg[s];
-        cnt++;
-      }
+    for (int p = 0; p < WPF; p++) {
+      const uint32_t jj = c0 + (uint32_t)(p * EPP + tid / WS);
+      wv[p] = jj < c1 ? g.wc_rows[(size_t)jj * WS + w] : 0ULL;
+      wk[p] = jj < c1 ? g.wc_key[jj] : 0u;
     }
-    my_edges += dsum;
-    row_bytes += 2 * cnt;
   }
+  const uint16_t *deg = g.sdeg + (size_t)r * n;
+  uint32_t dg[SPT];
+#pragma unroll
+  for (int k = 0; k < SPT; k++) {
+    const int s = tid * SPT + k;
+    dg[k] = (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) ? (uint32_t)deg[s] + 0x10000u : 0u;  // bit 16: counted
+  }
+  const u64 *rows = g.strong + (size_t)r * n * WS;
   u64 a0 = 0, a1 = 0;
   u64 u0 = ~0ULL, u1 = ~0ULL;  // never equal to a partial OR when Ur is absent
   if (Ur) {
     u0 = Ur[CW * j];
     u1 = CW == 2 ? Ur[CW * j + 1] : 0ULL;
   }
+  // ---- strong rows until the OR saturates ----
 #pragma unroll 1
   for (int p0 = 0; p0 < CPT; p0 += GRP) {
     if ((tid / CPR) + p0 * RPP - (tid & ~63) / CPR >= n) break;  // wave-uniform: rows of this wave done
@@ -327,30 +345,22 @@ __device__ __forceinline__ void expand_rows(const DagView &g, int r, const u64 *
     if (a0) atomicOr(dst, a0);
     if (CW == 2 && a1) atomicOr(dst + 1, a1);
   }
-}
-
-// weak edges of the vertices in FE (round r) -> ring (or far mask rows); returns lowest target round
-template <int WS, int NT>
-__device__ __forceinline__ int expand_weak(const DagView &g, int r, int bottom, const u64 *FE, u64 *ring,
-                                           int depth, u64 *mask_bottom, u64 &my_wedges) {
-  const int tid = threadIdx.x, dmask = depth - 1;
-  int lowmin = 0x7fffffff;
-  // weak columns of round r: lane group j (WS lanes, lane w owns word w) tests
-  // entry j's source row against FE; a hit sets the target bit (one atomic per
-  // entry), the popcount is the number of weak edges followed.
-  static_assert(WS <= 64 && (64 % WS) == 0, "WS lanes per column entry");
-  constexpr int EPP = NT / WS;  // entries per pass
-  const int w = tid % WS, lane = tid & 63, gbase = lane & ~(WS - 1);
-  const uint32_t c0 = g.wc_roff[r], c1 = g.wc_roff[r + 1];
+#pragma unroll
+  for (int k = 0; k < SPT; k++) {
+    my_edges += dg[k] & 0xffffu;
+    row_bytes += (dg[k] >> 16) * 2;
+  }
+  if constexpr (!WEAK) return lowmin;
+  // ---- weak columns: lane group of entry jj (WS lanes, lane w owns word w)
+  // ANDs the entry's source row with the frontier; a hit sets the target bit
+  // (one atomic per entry); the popcount is the number of weak edges followed
   const u64 fe = FE[w];
-  for (uint32_t j0 = c0; j0 < c1; j0 += EPP) {
-    const uint32_t j = j0 + (uint32_t)(tid / WS);
-    const u64 v = j < c1 ? g.wc_rows[(size_t)j * WS + w] & fe : 0ULL;
+  const u64 gm = WS >= 64 ? ~0ULL : (((1ULL << WS) - 1ULL) << gbase);
+  auto column = [&](u64 row, uint32_t key) {
+    const u64 v = row & fe;
     my_wedges += (u64)popc64(v);
     const u64 bal = __ballot(v != 0ULL);
-    const u64 gm = WS >= 64 ? ~0ULL : (((1ULL << WS) - 1ULL) << gbase);
     if (w == 0 && (bal & gm)) {
-      const uint32_t key = g.wc_key[j];
       const int delta = (int)(key >> 11), ts = (int)(key & 2047u), tr = r - delta;
       if (tr >= bottom) {
         const u64 bit = 1ULL << (ts & 63);
@@ -359,6 +369,13 @@ __device__ __forceinline__ int expand_weak(const DagView &g, int r, int bottom, 
         else atomicOr(mask_bottom + (int64_t)(tr - bottom) * WS + (ts >> 6), bit);
       }
     }
+  };
+#pragma unroll
+  for (int p = 0; p < WPF; p++)
+    if (c0 + (uint32_t)(p * EPP) < c1) column(wv[p], wk[p]);  // wave-uniform
+  for (uint32_t j0 = c0 + (uint32_t)(WPF * EPP); j0 < c1; j0 += EPP) {
+    const uint32_t jj = j0 + (uint32_t)(tid / WS);
+    column(jj < c1 ? g.wc_rows[(size_t)jj * WS + w] : 0ULL, jj < c1 ? g.wc_key[jj] : 0u);
   }
   const uint32_t f0 = g.far_roff[r], f1 = g.far_roff[r + 1];
   for (uint32_t e = f0 + tid; e < f1; e += NT) {
@@ -383,12 +400,17 @@ __device__ __forceinline__ int expand_weak(const DagView &g, int r, int bottom, 
 constexpr int DDR = 3;
 struct RoundWords {
   u64 P, K, U, WU[DDR];
+  uint32_t C0, C1;  // the round's weak-column range
 };
 
 template <int WS, bool MERGE, bool SUMMARY, bool WEAK>
 __device__ __forceinline__ void load_round(const DagView &g, const MemoView &mv, int r, RoundWords &x) {
   const int w = threadIdx.x;
   x.P = g.present[(size_t)r * WS + w];
+  if constexpr (WEAK) {
+    x.C0 = g.wc_roff[r];
+    x.C1 = g.wc_roff[r + 1];
+  }
   if constexpr (MERGE) x.K = mv.K[(size_t)r * WS + w];
   if constexpr (SUMMARY) {
     x.U = mv.U[(size_t)r * WS + w];
@@ -462,6 +484,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
   u64 *ring = smem + 2 * WS;    // depth * WS
   const int depth = 1 << depth_log2, dmask = depth - 1;
   // ctl: [0] low water [1] round [2] status (0 partial, 1 stop) [3] merged [4] stop round
+  //      [5] [6] the partial round's weak-column range
   int *s_ctl = reinterpret_cast<int *>(ring + (size_t)depth * WS);
   u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 8);  // [0] all edges, [1] weak edges, [2] row bytes
   const int tid = threadIdx.x;
@@ -572,6 +595,10 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
             s_ctl[2] = stop ? 1 : 0;
             s_ctl[3] = merged ? 1 : 0;
             if (stop && (merged || r > q.bottom)) s_ctl[4] = r;
+            if constexpr (WEAK) {  // the round's weak-column range, prefetched with its words
+              s_ctl[5] = (int)cur.C0;
+              s_ctl[6] = (int)cur.C1;
+            }
           }
           break;
         }
@@ -581,12 +608,10 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       if (s_ctl[2]) break;
       // ---------- all threads: rows and weak edges of partial round r ----------
       if (s_ctl[0] < r || true) {
-        expand_rows<WS, NT>(g, r, FE, ring, dmask, my_edges, shortcut ? mv.U + (size_t)r * WS : nullptr,
-                            my_rowb);
-        if constexpr (WEAK) {
-          const int lowmin = expand_weak<WS, NT>(g, r, q.bottom, FE, ring, depth, masks + q.mask_off, my_wedges);
-          if (lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
-        }
+        const int lowmin = expand_round<WS, NT, WEAK>(g, r, q.bottom, FE, ring, depth, masks + q.mask_off,
+                                                      shortcut ? mv.U + (size_t)r * WS : nullptr, my_edges,
+                                                      my_wedges, my_rowb, WEAK ? s_ctl[5] : -1, WEAK ? s_ctl[6] : -1);
+        if (WEAK && lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
       }
       __syncthreads();
       cur = nxt;
@@ -862,8 +887,7 @@ __global__ __launch_bounds__(NT) void k_set_weak(DagView g, int r0, int depth_lo
     }
     __syncthreads();
     if (s_nz) {
-      expand_rows<WS, NT>(g, r, FE, ring, dmask, e_dummy, nullptr, rb_dummy);
-      expand_weak<WS, NT>(g, r, 1, FE, ring, depth, far + WS, we_dummy);
+      expand_round<WS, NT, true>(g, r, 1, FE, ring, depth, far + WS, nullptr, e_dummy, we_dummy, rb_dummy);
     }
     __syncthreads();
   }
@@ -1020,8 +1044,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
         if (tid == 0) e = mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
       } else {
         u64 rb = 0;
-        expand_rows<WS, NT>(g, r, FE, ring, dmask, e, mv.U + (size_t)r * WS, rb);
-        expand_weak<WS, NT>(g, r, 0, FE, ring, depth, K, we);
+        expand_round<WS, NT, true>(g, r, 0, FE, ring, depth, K, mv.U + (size_t)r * WS, e, we, rb);
       }
       e += we;
       if (e) atomicAdd(&s_edges[0], e);
@@ -1189,8 +1212,8 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
 }
 
 // Two launch shapes: grid (round blocks, segments) when item_pref is null; else
-// a fixed grid striding over the work items [0, ctl[1]) of ctl[0] segments,
-// segment i owning items [item_pref[i], item_pref[i+1]) (device-planned replay).
+// a fixed grid striding over the work items of ctl[0] segments, segment i owning
+// items [item_pref[i], item_pref[i+1]) (device-planned replay).
 template <int WS, int NT, int RPB>
 __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__restrict__ slot_off,
                                                  const uint16_t *__restrict__ slot_src,
@@ -1207,14 +1230,11 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
                             digest, round_out, ids, ids_cap, &s_dg);
     return;
   }
+  // item_pref[nd] = item count; item_pref[nd + 1 + it] = the segment owning item it
   const int nd = ctl[0];
   const int64_t nit = item_pref[nd];
   for (int64_t it = blockIdx.x; it < nit; it += gridDim.x) {
-    int lo = 0, hi = nd - 1;  // last segment with item_pref <= it
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (item_pref[mid] <= it) lo = mid; else hi = mid - 1;
-    }
+    const int lo = (int)item_pref[nd + 1 + it];
     emit_block<WS, NT, RPB>(g, slot_off, slot_src, pd[lo], (int)(it - item_pref[lo]), masks, K, rbase, pop_pos,
                             digest, round_out, ids, ids_cap, &s_dg);
     __syncthreads();

@@ -293,6 +293,11 @@ __global__ __launch_bounds__(NT) void k_plan_emit(const int32_t *__restrict__ po
     plan[PL_NDESC] = over ? 0 : (int32_t)c0;
     if (over) plan[PL_CAPERR] = 2;
   }
+  __syncthreads();
+  // item -> segment map after the prefix (k_emit_ids looks its segment up in one load)
+  const int nd = plan[PL_NDESC];
+  for (int i = tid; i < nd; i += NT)
+    for (int64_t it = item_pref[i]; it < item_pref[i + 1]; it++) item_pref[nd + 1 + it] = i;
 }
 
 // Outputs -> pinned host memory (h_*, every workgroup a share), totals -> hdr (workgroup 0).
@@ -337,10 +342,17 @@ __global__ __launch_bounds__(NT) void k_plan_final(int nw, const uint8_t *__rest
   for (int q = tid; q < nqd; q += NT)
 #pragma unroll
     for (int k = 0; k < 4; k++) st[k] += dstats[4 * q + k];
-  atomicAdd(&acc[0], de);
-  atomicAdd(&acc[1], ce);
+  // one LDS atomic per wave and counter (256 same-address atomics serialise)
+  de = wave_sum(de);
+  ce = wave_sum(ce);
 #pragma unroll
-  for (int k = 0; k < 4; k++) atomicAdd(&acc[2 + k], st[k]);
+  for (int k = 0; k < 4; k++) st[k] = wave_sum(st[k]);
+  if ((tid & 63) == 0) {
+    atomicAdd(&acc[0], de);
+    atomicAdd(&acc[1], ce);
+#pragma unroll
+    for (int k = 0; k < 4; k++) atomicAdd(&acc[2 + k], st[k]);
+  }
   __syncthreads();
   if (tid == 0) {
     h_hdr[PH_NPUSH] = (u64)plan[PL_NPUSH];
