@@ -11,11 +11,14 @@ CFLAGS    := -O2 -std=c11 -fPIC -fopenmp -Wall -D_GNU_SOURCE
 
 PKG       := dag_rider_amd
 LIB       := $(PKG)/libdagrider_gpu.so
+# profiling build (per-query sweep phase timings, tools/sweep_timing.py); never loaded by tests or the bench
+LIBT      := $(PKG)/libdagrider_gpu_timing.so
 ORACLE    := oracle/liboracle.so
 BUILD     := build
 
-.PHONY: all lib oracle clean tests-cpp
-all: lib oracle tests-cpp
+.PHONY: all lib oracle clean tests-cpp timing
+all: lib oracle tests-cpp timing
+timing: $(LIBT)
 
 lib: $(LIB)
 oracle: $(ORACLE)
@@ -28,6 +31,12 @@ $(BUILD)/dag_gen.o: $(PKG)/csrc/dag_gen.cpp include/dagrider_gen.h | $(BUILD)
 
 $(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp include/dagrider_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/engine_timing.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp include/dagrider_gpu.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DDR_SWEEP_TIMING -c $< -o $@
+
+$(LIBT): $(BUILD)/engine_timing.o $(BUILD)/shard.o $(BUILD)/dag_gen.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdagrider_gpu_timing.so
 
 $(BUILD)/shard.o: $(PKG)/csrc/shard.hip include/dagrider_shard.h include/dagrider_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -44,4 +53,4 @@ $(BUILD)/process_internal_test: tests/cpp/process_internal_test.cpp $(PKG)/host/
 	$(CXX) -O2 -std=c++17 -Iinclude -I$(PKG)/host $< -o $@ -L$(PKG) -ldagrider_gpu -Wl,-rpath,'$$ORIGIN/../$(PKG)'
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(ORACLE)
+	rm -rf $(BUILD) $(LIB) $(LIBT) $(ORACLE)

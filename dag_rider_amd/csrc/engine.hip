@@ -1412,6 +1412,16 @@ extern "C" int dr_set_leader_coin(dr_ctx *c, int mode, uint64_t seed, int k, con
 
 extern "C" int dr_wave_leader(const dr_ctx *c, int wave) { return c ? c->lead_src(wave) : -1; }
 
+#ifdef DR_SWEEP_TIMING
+// profiling build only: the per-query phase timings of the last k_sweep launch
+// (kernels.hpp g_sweep_timing; 8 u64 per query, wall-clock ticks)
+extern "C" int dr_debug_sweep_timing(uint64_t *out, int nq) {
+  if (nq < 0 || nq > dr::kSweepTimingQ) return DR_E_INVAL;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dr::g_sweep_timing), (size_t)nq * 64, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess ? DR_OK : DR_E_HIP;
+}
+#endif
+
 extern "C" int dr_coin_leader(uint64_t seed, int wave, int n) {
   if (n < 1) return 1;
   uint64_t z = seed + (uint64_t)(uint32_t)wave * 0x9E3779B97F4A7C15ULL;

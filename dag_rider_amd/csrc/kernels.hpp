@@ -401,6 +401,8 @@ constexpr int DDR = 3;
 struct RoundWords {
   u64 P, K, U, WU[DDR];
   uint32_t C0, C1;  // the round's weak-column range
+  u64 SD;           // the round's strong-degree sum (summary rounds' edge count)
+  uint32_t NW;      // the round's weak edges
 };
 
 template <int WS, bool MERGE, bool SUMMARY, bool WEAK>
@@ -413,6 +415,10 @@ __device__ __forceinline__ void load_round(const DagView &g, const MemoView &mv,
   }
   if constexpr (MERGE) x.K = mv.K[(size_t)r * WS + w];
   if constexpr (SUMMARY) {
+    if (w == 0) {
+      x.SD = mv.SD[r];
+      if constexpr (WEAK) x.NW = g.weak_roff[r + 1] - g.weak_roff[r];
+    }
     x.U = mv.U[(size_t)r * WS + w];
     if constexpr (WEAK) {
 #pragma unroll
@@ -458,6 +464,17 @@ __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWo
 // LDS: F[WS] | FE[WS] | ring[depth][WS] | ctl (int[8]) | edges (u64[2]).
 // ---------------------------------------------------------------------------
 enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8 };
+
+#ifdef DR_SWEEP_TIMING
+// profiling build only (libdagrider_gpu_timing.so, tools/sweep_timing.py): per
+// query, wall-clock ticks of the prologue, wave 0's phase A (summary rounds
+// included), the partial rounds' expansion, the total, and the round counts
+constexpr int kSweepTimingQ = 8192;
+__device__ u64 g_sweep_timing[8 * kSweepTimingQ];
+#define DR_TT(...) __VA_ARGS__
+#else
+#define DR_TT(...)
+#endif
 
 template <int WS, int NT, int MODE>
 __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
@@ -507,6 +524,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       ring[(size_t)(q.top & dmask) * WS + (q.src0 >> 6)] = 1ULL << (q.src0 & 63);
     int npush = 0;  // thread 0
     u64 st_partial = 0, st_scan = 0, st_short = 0;  // thread 0: work counters
+    DR_TT(u64 tt0 = wall_clock64(); u64 tt_a = 0, tt_b = 0, tt_pro = 0, tt_ns = 0, tt_np = 0;)
     int run = 0;    // wave 0: consecutive rounds equal to K
     u64 my_edges = 0, my_wedges = 0, my_rowb = 0;
     RoundWords cur{}, nxt{};
@@ -516,8 +534,10 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
     }
     __syncthreads();
     int r = q.top;
+    DR_TT(tt_pro = wall_clock64() - tt0;)
     for (;;) {
       // ---------- wave 0: phase A of round r; summary rounds end here ----------
+      DR_TT(const u64 tta = wall_clock64();)
       if (w0) {
         for (;;) {
           if (act && r > q.bottom) {  // prefetch round r-1 (frontier-independent)
@@ -574,17 +594,18 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
             for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
             if (tid == 0 && !stop) {
               if (summary) st_short++;
-              else { st_partial++; (void)pc; if (WEAK) st_scan += g.wc_roff[r + 1] - g.wc_roff[r]; }
+              else { st_partial++; (void)pc; if (WEAK) st_scan += cur.C1 - cur.C0; }
             }
           }
           if (summary) {  // the round is the union of its rows: apply the summaries, stay in wave 0
             if (act) expand_summary<WS, WEAK>(mv, cur, r, q.bottom, ring, dmask);
             if (tid == 0) {
-              my_edges += mv.SD[r];
-              if (WEAK) my_wedges += g.weak_roff[r + 1] - g.weak_roff[r];
+              my_edges += cur.SD;
+              if (WEAK) my_wedges += cur.NW;
             }
             low = min(low, WEAK ? r - 1 - mv.dd : r - 1);
             if (tid == 0) s_ctl[0] = low;
+            DR_TT(tt_ns++;)
             cur = nxt;
             --r;
             continue;
@@ -604,6 +625,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
         }
       }
       __syncthreads();
+      DR_TT(const u64 ttb = wall_clock64(); tt_a += ttb - tta;)
       r = s_ctl[1];
       if (s_ctl[2]) break;
       // ---------- all threads: rows and weak edges of partial round r ----------
@@ -614,6 +636,7 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
         if (WEAK && lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
       }
       __syncthreads();
+      DR_TT(tt_b += wall_clock64() - ttb; tt_np++;)
       cur = nxt;
       --r;
     }
@@ -629,6 +652,13 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       if (hit_out) hit_out[qi] = q.tgt0 >= 0 ? (uint8_t)((F[q.tgt0 >> 6] >> (q.tgt0 & 63)) & 1ULL) : 0;
       if (push_n) push_n[qi] = npush;
       if (stop_out) stop_out[qi] = s_ctl[3] ? s_ctl[4] : -1 - s_ctl[4];  // >= 0 merged there; < 0 ended at -1-x
+#ifdef DR_SWEEP_TIMING
+      if (qi < kSweepTimingQ) {
+        u64 *t = g_sweep_timing + 8 * (size_t)qi;
+        t[0] = tt_pro; t[1] = tt_a; t[2] = tt_b; t[3] = wall_clock64() - tt0; t[4] = tt_ns; t[5] = tt_np;
+        t[6] = (u64)q.top; t[7] = (u64)(int64_t)s_ctl[4];
+      }
+#endif
       if (stats_out) {
         stats_out[4 * qi + 0] = st_partial;
         stats_out[4 * qi + 1] = s_edges[2];  // strong-row bytes read

@@ -1,0 +1,43 @@
+"""Where a delivery sweep's time goes: per-query phase timings from the profiling
+build (libdagrider_gpu_timing.so, kernels.hpp DR_SWEEP_TIMING) of one C4 replay.
+
+usage: DR_LIB_VARIANT=timing python tools/sweep_timing.py [config]
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+os.environ["DR_LIB_VARIANT"] = "timing"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from dag_rider_amd import _lib as L  # noqa: E402
+from dag_rider_amd.engine import Engine  # noqa: E402
+from dag_rider_amd.gen import CONFIGS, generate  # noqa: E402
+
+cfg = CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c4"]
+d = generate(cfg, nthreads=16)
+lib = L.lib()
+lib.dr_debug_sweep_timing.restype = C.c_int
+lib.dr_debug_sweep_timing.argtypes = [C.c_void_p, C.c_int]
+import torch  # noqa: E402
+
+rate = torch.cuda.get_device_properties(0).__dict__.get("clock_rate", None)
+with Engine(cfg.n, cfg.faulty, d.nrounds, 0) as e:
+    e.append_packed(d)
+    for _ in range(3):
+        res = e.replay(cfg.nwaves)
+    nq = int(res.sweep["count"])
+    buf = np.zeros(8 * nq, np.uint64)
+    assert lib.dr_debug_sweep_timing(L.ptr(buf), nq) == 0
+t = buf.reshape(nq, 8).astype(np.float64)
+tick_us = 0.01  # wall_clock64 runs at 100 MHz on gfx950
+out = {}
+for k, name in enumerate(["prologue", "phaseA", "expansion", "total"]):
+    v = t[:, k] * tick_us
+    out[name + "_us"] = dict(mean=float(v.mean()), p50=float(np.median(v)), max=float(v.max()))
+out["summary_rounds"] = float(t[:, 4].mean())
+out["partial_rounds"] = float(t[:, 5].mean())
+out["queries"] = nq
+print(json.dumps(out, indent=1))
