@@ -79,6 +79,10 @@ SIGNATURES = {
     "dr_shard_reach_sets": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dr_shard_path_batch": (C.c_int, [P, C.c_int, P, P, C.c_int, P]),
     "dr_shard_stats": (C.c_int, [P, C.POINTER(f32), C.POINTER(u64), C.POINTER(u64)]),
+    # include/dagrider_wire.h
+    "dr_wire_check": (C.c_int, [P, C.c_size_t, C.POINTER(i32), C.POINTER(i32)]),
+    "dr_wire_append": (C.c_int, [P, P, C.c_size_t]),
+    "dr_wire_block": (C.c_int, [P, C.c_size_t, i64, C.POINTER(P), C.POINTER(C.c_size_t)]),
     "dr_gen_create": (C.c_int, [C.POINTER(GenParams), C.POINTER(P)]),
     "dr_gen_free": (None, [P]),
     "dr_gen_info": (C.c_int, [P, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(u64),

@@ -145,6 +145,11 @@ class Engine:
         self._check(self._L.dr_append_vertices(self._h, k, L.ptr(rr), L.ptr(ids), L.ptr(so), L.ptr(sti), L.ptr(wo),
                                                L.ptr(wki)))
 
+    def append_capture(self, buf: bytes):
+        """Replay a DRW1 capture (dag_rider_amd/wire.py) through the C reader (dr_wire_append)."""
+        b = C.create_string_buffer(bytes(buf), len(buf))
+        self._check(self._L.dr_wire_append(self._h, b, len(buf)))
+
     # ---- path(from, to, strongPath)  (process.go:89-148), batched ----
     def path_batch(self, pairs: Sequence[Tuple[Tuple[int, int], Tuple[int, int]]], strong_only: bool) -> np.ndarray:
         q = len(pairs)

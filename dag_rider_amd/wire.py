@@ -46,22 +46,46 @@ def encode(dag: Sequence[Sequence[Vertex]]) -> bytes:
     return b"".join(out)
 
 
+def _offsets(name: str, off: np.ndarray, n: int, total: int):
+    """An offset array: n+1 entries, starting at 0, non-decreasing, ending at total."""
+    if off.size != n + 1:
+        raise ValueError(f"corrupt DRW1 capture: {name} has {off.size} entries, want {n + 1}")
+    if int(off[0]) != 0 or int(off[-1]) != total or (off.size > 1 and (np.diff(off.astype(np.int64)) < 0).any()):
+        raise ValueError(f"corrupt DRW1 capture: {name} is not a 0-based non-decreasing prefix ending at {total}")
+
+
 def _parse(buf: bytes):
-    if buf[:4] != MAGIC:
+    """Header and arrays of a capture, every size and offset checked: arrays() feeds
+    dr_append_rounds_lists, which trusts them as raw pointers and lengths."""
+    if len(buf) < 12 or buf[:4] != MAGIC:
         raise ValueError("not a DRW1 DAG capture")
     nrounds, nslots = struct.unpack_from("<II", buf, 4)
     pos = 12
     arrs = []
     for dt in _DT:
+        if pos + 8 > len(buf):
+            raise ValueError("corrupt DRW1 capture: truncated array header")
         (k,) = struct.unpack_from("<Q", buf, pos)
         pos += 8
+        if k > (len(buf) - pos) // 4:
+            raise ValueError("corrupt DRW1 capture: array runs past the end")
         a = np.frombuffer(buf, dtype=dt, count=k, offset=pos)
         pos += 4 * k
         arrs.append(a)
-    if arrs[0].size != nrounds + 1 or arrs[1].size != 2 * nslots:
+    so, sid, sto, sti, wo, wi = arrs
+    if sid.size != 2 * nslots:
         raise ValueError("corrupt DRW1 capture: round/slot counts disagree")
+    _offsets("slot_off", so, nrounds, nslots)
+    if sti.size % 2 or wi.size % 2:
+        raise ValueError("corrupt DRW1 capture: odd id array")
+    _offsets("strong_off", sto, nslots, sti.size // 2)
+    _offsets("weak_off", wo, nslots, wi.size // 2)
+    if pos + 8 * (nslots + 1) > len(buf):
+        raise ValueError("corrupt DRW1 capture: block offsets truncated")
     boff = np.frombuffer(buf, dtype=np.uint64, count=nslots + 1, offset=pos)
     pos += 8 * (nslots + 1)
+    if int(boff[0]) != 0 or (boff.size > 1 and (boff[1:] < boff[:-1]).any()):
+        raise ValueError("corrupt DRW1 capture: block offsets not a 0-based non-decreasing prefix")
     if pos + int(boff[-1]) != len(buf):
         raise ValueError("corrupt DRW1 capture: block bytes truncated or trailing data")
     return nrounds, arrs, boff, pos

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     syms = set()
-    for h in ("dagrider_gpu.h", "dagrider_gen.h", "dagrider_shard.h"):
+    for h in ("dagrider_gpu.h", "dagrider_gen.h", "dagrider_shard.h", "dagrider_wire.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         syms |= set(re.findall(r"\b(dr_[a-z_]+)\s*\(", txt))

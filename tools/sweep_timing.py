@@ -23,7 +23,7 @@ lib.dr_debug_sweep_timing.restype = C.c_int
 lib.dr_debug_sweep_timing.argtypes = [C.c_void_p, C.c_int]
 import torch  # noqa: E402
 
-rate = torch.cuda.get_device_properties(0).__dict__.get("clock_rate", None)
+torch.cuda.init()
 with Engine(cfg.n, cfg.faulty, d.nrounds, 0) as e:
     e.append_packed(d)
     for _ in range(3):
