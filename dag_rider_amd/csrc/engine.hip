@@ -1414,10 +1414,10 @@ extern "C" int dr_wave_leader(const dr_ctx *c, int wave) { return c ? c->lead_sr
 
 #ifdef DR_SWEEP_TIMING
 // profiling build only: the per-query phase timings of the last k_sweep launch
-// (kernels.hpp g_sweep_timing; 8 u64 per query, wall-clock ticks)
+// (kernels.hpp g_sweep_timing; 16 u64 per query, wall-clock ticks)
 extern "C" int dr_debug_sweep_timing(uint64_t *out, int nq) {
   if (nq < 0 || nq > dr::kSweepTimingQ) return DR_E_INVAL;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dr::g_sweep_timing), (size_t)nq * 64, 0, hipMemcpyDeviceToHost) ==
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dr::g_sweep_timing), (size_t)nq * 128, 0, hipMemcpyDeviceToHost) ==
                  hipSuccess ? DR_OK : DR_E_HIP;
 }
 #endif

@@ -31,9 +31,22 @@
 
 namespace dr {
 
+
+
 typedef unsigned long long u64;
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#ifdef DR_SWEEP_TIMING
+// profiling build only (libdagrider_gpu_timing.so, tools/sweep_timing.py): per
+// query, wall-clock ticks of the prologue, wave 0's phase A (summary rounds
+// included), the partial rounds' expansion, the total, and the round counts
+constexpr int kSweepTimingQ = 8192;
+__device__ u64 g_sweep_timing[16 * kSweepTimingQ];
+#define DR_TT(...) __VA_ARGS__
+#else
+#define DR_TT(...)
+#endif
 
 enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8, Q_SHORTCUT = 16, Q_MERGE = 32 };
 
@@ -260,10 +273,10 @@ struct MemoView {
 template <int WS, int NT, bool WEAK>
 __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom, const u64 *FE, u64 *ring, int depth,
                                             u64 *mask_bottom, const u64 *Ur, u64 &my_edges, u64 &my_wedges,
-                                            u64 &row_bytes, int64_t wc0 = -1, int64_t wc1 = -1) {
+                                            u64 &row_bytes, int64_t wc0 = -1, int64_t wc1 = -1, u64 *tsub = nullptr) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT, NMAX = G::NMAX;
-  constexpr int GRP = CPT < 2 ? CPT : 2;
+  constexpr int GRP = CPT < 4 ? CPT : 4;  // 4 x RPP rows per step: a C4 frontier saturates in one
   constexpr int SPT = (NMAX + NT - 1) / NT;  // sources per thread for the degree sum
   static_assert(WS <= 64 && (64 % WS) == 0, "WS lanes per weak-column entry");
   constexpr int EPP = NT / WS;  // weak-column entries per pass
@@ -271,6 +284,7 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
   const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n, dmask = depth - 1;
   const int w = tid % WS, gbase = lane & ~(WS - 1);
   int lowmin = 0x7fffffff;
+  DR_TT(u64 t0 = wall_clock64(); (void)t0;)
   // ---- independent loads first ----
   uint32_t c0 = 0, c1 = 0;
   u64 wv[WPF];
@@ -286,11 +300,14 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
     }
   }
   const uint16_t *deg = g.sdeg + (size_t)r * n;
-  uint32_t dg[SPT];
+  uint16_t dg[SPT];  // loaded now, used after the rows: no wait here
+  uint32_t din = 0;  // bit k: source tid*SPT+k is in the frontier
 #pragma unroll
   for (int k = 0; k < SPT; k++) {
     const int s = tid * SPT + k;
-    dg[k] = (s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL)) ? (uint32_t)deg[s] + 0x10000u : 0u;  // bit 16: counted
+    const bool in = s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL);
+    din |= (in ? 1u : 0u) << k;
+    dg[k] = in ? deg[s] : (uint16_t)0;
   }
   const u64 *rows = g.strong + (size_t)r * n * WS;
   u64 a0 = 0, a1 = 0;
@@ -299,6 +316,7 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
     u0 = Ur[CW * j];
     u1 = CW == 2 ? Ur[CW * j + 1] : 0ULL;
   }
+  DR_TT(if (tsub && tid == 0) { const u64 t = wall_clock64(); tsub[0] += t - t0; t0 = t; })
   // ---- strong rows until the OR saturates ----
 #pragma unroll 1
   for (int p0 = 0; p0 < CPT; p0 += GRP) {
@@ -335,6 +353,7 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
       if (__ballot(r0 != u0 || r1 != u1) == 0ULL) break;  // saturated: no row can add a bit
     }
   }
+  DR_TT(if (tsub && tid == 0) { const u64 t = wall_clock64(); tsub[1] += t - t0; t0 = t; })
   // chunk j = lane mod CPR: fold each row's lanes of class j, then one LDS OR per row
   if constexpr (CPR < 16) {
     a0 = row_or_stride<CPR>(a0);
@@ -346,10 +365,9 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
     if (CW == 2 && a1) atomicOr(dst + 1, a1);
   }
 #pragma unroll
-  for (int k = 0; k < SPT; k++) {
-    my_edges += dg[k] & 0xffffu;
-    row_bytes += (dg[k] >> 16) * 2;
-  }
+  for (int k = 0; k < SPT; k++) my_edges += dg[k];
+  row_bytes += 2 * (u64)__popc(din);
+  DR_TT(if (tsub && tid == 0) { const u64 t = wall_clock64(); tsub[2] += t - t0; t0 = t; })
   if constexpr (!WEAK) return lowmin;
   // ---- weak columns: lane group of entry jj (WS lanes, lane w owns word w)
   // ANDs the entry's source row with the frontier; a hit sets the target bit
@@ -391,6 +409,7 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
     else atomicOr(mask_bottom + (int64_t)(tr - bottom) * WS + (ts >> 6), bit);
     lowmin = min(lowmin, tr);
   }
+  DR_TT(if (tsub && tid == 0) { const u64 t = wall_clock64(); tsub[3] += t - t0; t0 = t; })
   return lowmin;
 }
 
@@ -465,16 +484,7 @@ __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWo
 // ---------------------------------------------------------------------------
 enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8 };
 
-#ifdef DR_SWEEP_TIMING
-// profiling build only (libdagrider_gpu_timing.so, tools/sweep_timing.py): per
-// query, wall-clock ticks of the prologue, wave 0's phase A (summary rounds
-// included), the partial rounds' expansion, the total, and the round counts
-constexpr int kSweepTimingQ = 8192;
-__device__ u64 g_sweep_timing[8 * kSweepTimingQ];
-#define DR_TT(...) __VA_ARGS__
-#else
-#define DR_TT(...)
-#endif
+
 
 template <int WS, int NT, int MODE>
 __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
@@ -524,7 +534,8 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       ring[(size_t)(q.top & dmask) * WS + (q.src0 >> 6)] = 1ULL << (q.src0 & 63);
     int npush = 0;  // thread 0
     u64 st_partial = 0, st_scan = 0, st_short = 0;  // thread 0: work counters
-    DR_TT(u64 tt0 = wall_clock64(); u64 tt_a = 0, tt_b = 0, tt_pro = 0, tt_ns = 0, tt_np = 0;)
+    DR_TT(u64 tt0 = wall_clock64(); u64 tt_a = 0, tt_b = 0, tt_pro = 0, tt_ns = 0, tt_np = 0, tt_end = 0;
+          u64 tt_sub[4] = {0, 0, 0, 0};)
     int run = 0;    // wave 0: consecutive rounds equal to K
     u64 my_edges = 0, my_wedges = 0, my_rowb = 0;
     RoundWords cur{}, nxt{};
@@ -632,7 +643,11 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       if (s_ctl[0] < r || true) {
         const int lowmin = expand_round<WS, NT, WEAK>(g, r, q.bottom, FE, ring, depth, masks + q.mask_off,
                                                       shortcut ? mv.U + (size_t)r * WS : nullptr, my_edges,
-                                                      my_wedges, my_rowb, WEAK ? s_ctl[5] : -1, WEAK ? s_ctl[6] : -1);
+                                                      my_wedges, my_rowb, WEAK ? s_ctl[5] : -1, WEAK ? s_ctl[6] : -1
+#ifdef DR_SWEEP_TIMING
+                                                      , tt_sub
+#endif
+        );
         if (WEAK && lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
       }
       __syncthreads();
@@ -641,10 +656,17 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       --r;
     }
     // results
+    DR_TT(tt_end = wall_clock64();)
     my_edges += my_wedges;
-    if (my_edges) atomicAdd(&s_edges[0], my_edges);
-    if (my_wedges) atomicAdd(&s_edges[1], my_wedges);
-    if (my_rowb) atomicAdd(&s_edges[2], my_rowb);
+    // one LDS atomic per wave and counter (a workgroup of same-address atomics serialises)
+    my_edges = wave_sum(my_edges);
+    my_wedges = wave_sum(my_wedges);
+    my_rowb = wave_sum(my_rowb);
+    if ((tid & 63) == 0) {
+      if (my_edges) atomicAdd(&s_edges[0], my_edges);
+      if (my_wedges) atomicAdd(&s_edges[1], my_wedges);
+      if (my_rowb) atomicAdd(&s_edges[2], my_rowb);
+    }
     __syncthreads();
     if (tid == 0) {
       if (edges_out) edges_out[qi] = s_edges[0];
@@ -654,9 +676,10 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       if (stop_out) stop_out[qi] = s_ctl[3] ? s_ctl[4] : -1 - s_ctl[4];  // >= 0 merged there; < 0 ended at -1-x
 #ifdef DR_SWEEP_TIMING
       if (qi < kSweepTimingQ) {
-        u64 *t = g_sweep_timing + 8 * (size_t)qi;
+        u64 *t = g_sweep_timing + 16 * (size_t)qi;
         t[0] = tt_pro; t[1] = tt_a; t[2] = tt_b; t[3] = wall_clock64() - tt0; t[4] = tt_ns; t[5] = tt_np;
         t[6] = (u64)q.top; t[7] = (u64)(int64_t)s_ctl[4];
+        t[8] = tt_sub[0]; t[9] = tt_sub[1]; t[10] = tt_sub[2]; t[11] = tt_sub[3]; t[12] = wall_clock64() - tt_end;
       }
 #endif
       if (stats_out) {

@@ -21,20 +21,20 @@ d = generate(cfg, nthreads=16)
 lib = L.lib()
 lib.dr_debug_sweep_timing.restype = C.c_int
 lib.dr_debug_sweep_timing.argtypes = [C.c_void_p, C.c_int]
-import torch  # noqa: E402
-
-torch.cuda.init()
 with Engine(cfg.n, cfg.faulty, d.nrounds, 0) as e:
     e.append_packed(d)
     for _ in range(3):
         res = e.replay(cfg.nwaves)
     nq = int(res.sweep["count"])
-    buf = np.zeros(8 * nq, np.uint64)
+    buf = np.zeros(16 * nq, np.uint64)
     assert lib.dr_debug_sweep_timing(L.ptr(buf), nq) == 0
-t = buf.reshape(nq, 8).astype(np.float64)
+t = buf.reshape(nq, 16).astype(np.float64)
 tick_us = 0.01  # wall_clock64 runs at 100 MHz on gfx950
 out = {}
 for k, name in enumerate(["prologue", "phaseA", "expansion", "total"]):
+    v = t[:, k] * tick_us
+    out[name + "_us"] = dict(mean=float(v.mean()), p50=float(np.median(v)), max=float(v.max()))
+for k, name in ((8, "exp_issue"), (9, "exp_rows"), (10, "exp_fold"), (11, "exp_weak"), (12, "results")):
     v = t[:, k] * tick_us
     out[name + "_us"] = dict(mean=float(v.mean()), p50=float(np.median(v)), max=float(v.max()))
 out["summary_rounds"] = float(t[:, 4].mean())
