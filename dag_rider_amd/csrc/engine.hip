@@ -1274,8 +1274,9 @@ int refresh_rounds(dr_ctx *c) {
 // fork: the canonical chain runs on stream2 (joined by the caller through
 // ev_join) while the caller's next phases use stream.  side (optional, with
 // fork): work launched on stream2 first, beside the canonical chain, which then
-// stays on the main stream; ev_join marks its end.
-int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side) {
+// stays on the main stream; ev_join marks its end.  forked: stream2 already
+// waits on an event of the main stream (build_summary's).
+int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool forked = false) {
   const int T = c->nrounds - 1;
   struct Swap {  // launch helpers use c->stream: point it at stream2 for the canonical chain
     dr_ctx *c;
@@ -1283,7 +1284,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side) {
     Swap(dr_ctx *c_, bool on_) : c(c_), on(on_) { if (on) std::swap(c->stream, c->stream2); }
     ~Swap() { if (on) std::swap(c->stream, c->stream2); }
   };
-  if (fork) {
+  if (fork && !forked) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
   }
@@ -1360,9 +1361,20 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   // cross-stream join: profiles/r02/v30_timeline.txt)
   HIPCHK(c, c->rec(6));
   HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
+  const bool early = fork && side;
+  if (early) {  // stream2's work (side) needs only the rows' summaries and commits: fork here,
+    // on the summary's end event when it is recorded anyway (each event costs the
+    // stream ~7 us: profiles/r02/v34_timeline.txt)
+    hipEvent_t fe = c->ev_fork;
+    if (c->timed(7))
+      fe = c->ev[7];
+    else
+      HIPCHK(c, hipEventRecord(fe, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, fe, 0));
+  }
   HIPCHK(c, launch_weak_union(c, T, c->stream));
   mark_rounds_clean(c);
-  if (int rc = launch_canon(c, fork, side)) return rc;
+  if (int rc = launch_canon(c, fork, side, early)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
   if (nwc > 0) {
     HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nwc));

@@ -7,6 +7,7 @@ Python or CPU implementation of any query here.
 from __future__ import annotations
 
 import ctypes as C
+import functools
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -250,20 +251,38 @@ class Engine:
         return _replay_result(o, keep, ids_cap)
 
 
+@functools.lru_cache(maxsize=64)
+def _out_layout(nwaves: int, push_cap: int, ids_cap: int):
+    """(name, dtype, byte offset, byte size) of every dr_replay output inside one buffer,
+    ordered so each array is aligned to its itemsize."""
+    pc = max(push_cap, 1)
+    spec = (("pc", np.uint64, pc), ("pdg", np.uint64, pc), ("pe", np.uint64, pc), ("vc", np.int32, nwaves),
+            ("po", np.uint32, nwaves + 1), ("pw", np.int32, pc), ("ids", np.int32, 2 * ids_cap),
+            ("cm", np.uint8, nwaves))
+    out, off = [], 0
+    for name, t, k in spec:
+        nb = np.dtype(t).itemsize * k
+        out.append((name, t, off, nb))
+        off += nb
+    return tuple(out), off + 8
+
+
 def _replay_out(nwaves: int, chain_mode: int, ids_cap: int = 0, push_cap: Optional[int] = None):
+    """Output arrays of one dr_replay, carved from a single allocation: a C4 step is
+    ~0.25 ms on the GPU, and nine separate arrays plus nine ctypes pointer conversions
+    cost ~45 us of Python per call."""
     push_cap = push_cap if push_cap is not None else (
         nwaves * (nwaves + 1) // 2 if chain_mode == L.DR_CHAIN_LITERAL else 2 * nwaves + 1)
-    keep = dict(cm=np.zeros(nwaves, np.uint8), vc=np.zeros(nwaves, np.int32), po=np.zeros(nwaves + 1, np.uint32),
-                pw=np.zeros(max(push_cap, 1), np.int32), pc=np.zeros(max(push_cap, 1), np.uint64),
-                pdg=np.zeros(max(push_cap, 1), np.uint64), pe=np.zeros(max(push_cap, 1), np.uint64),
-                ids=np.zeros(max(ids_cap, 1) * 2, np.int32) if ids_cap else None)
-    o = L.ReplayOut()
-    o.commit, o.vcount, o.push_off, o.push_wave = L.ptr(keep["cm"]), L.ptr(keep["vc"]), L.ptr(keep["po"]), \
-        L.ptr(keep["pw"])
-    o.push_cap = push_cap
-    o.pop_count, o.pop_digest, o.pop_edges = L.ptr(keep["pc"]), L.ptr(keep["pdg"]), L.ptr(keep["pe"])
-    o.ids = L.ptr(keep["ids"])
-    o.ids_cap = ids_cap
+    layout, total = _out_layout(nwaves, push_cap, ids_cap)
+    buf = np.zeros(total, np.uint8)
+    base = buf.ctypes.data
+    keep, a = {"_buf": buf}, {}
+    for name, t, off, nb in layout:
+        keep[name] = buf[off:off + nb].view(t)
+        a[name] = base + off
+    if not ids_cap:
+        keep["ids"], a["ids"] = None, None
+    o = L.ReplayOut(a["cm"], a["vc"], a["po"], a["pw"], push_cap, a["pc"], a["pdg"], a["pe"], a["ids"], ids_cap)
     return o, keep
 
 
@@ -278,6 +297,30 @@ def _replay_result(o, keep, ids_cap: int = 0) -> ReplayResult:
                         dict(count=o.sweep_count, partial=o.sweep_partial, row_bytes=o.sweep_row_bytes,
                              weak_scanned=o.sweep_weak_scanned, shortcut=o.sweep_shortcut,
                              canon_segments=o.canon_segments))
+
+
+class Replayer:
+    """dr_replay of one engine into output buffers allocated once (Engine.replay allocates
+    per call, ~20-45 us of Python that a 0.25 ms C4 step cannot hide).  result() returns
+    views of those buffers: the next call overwrites them."""
+
+    def __init__(self, eng: "Engine", nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT,
+                 deliver_mode: int = L.DR_DELIVER_REF, ids_cap: int = 0):
+        self._eng, self._ids_cap = eng, ids_cap
+        self._o, self._keep = _replay_out(nwaves, chain_mode, ids_cap)
+        self._fn, self._args = eng._L.dr_replay, (eng._h, nwaves, chain_mode, deliver_mode, C.byref(self._o))
+
+    def __call__(self) -> None:
+        rc = self._fn(*self._args)
+        if rc != L.DR_OK:
+            self._eng._check(rc)
+
+    @property
+    def ms_summary(self) -> float:
+        return self._o.ms_summary
+
+    def result(self) -> ReplayResult:
+        return _replay_result(self._o, self._keep, self._ids_cap)
 
 
 class ReplayBatch:
