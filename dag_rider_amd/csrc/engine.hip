@@ -418,6 +418,7 @@ struct SweepArgs {
   int32_t *stops;
   u64 *stats;
   const int *nq_dev = nullptr;  // planned replay: query count on the device, nq = grid upper bound
+  uint32_t *rcnt = nullptr;     // planned delivery: per-mask-row vertex counts for the emission
 };
 
 template <int WS, int MODE>
@@ -430,7 +431,7 @@ hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(a.seq ? 1 : a.nq), dim3(NT), lds, c->stream,
                      c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
-                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev);
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt);
   return hipGetLastError();
 }
 template <int WS>
@@ -475,35 +476,35 @@ constexpr int kEmitRPB = 4;  // rounds per emit workgroup: one per wave
 template <int WS>
 hipError_t launch_emit_t(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
                          u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase,
-                         const int *plan, const int64_t *item_pref, const dr::PopDesc &d1) {
+                         const int *plan, const int64_t *item_pref, const dr::PopDesc &d1, const uint32_t *rcnt) {
   if (count_phase) {
     hipLaunchKernelGGL((dr::k_emit_count<WS, 256>), dim3(ndesc), dim3(256), 0, c->stream, c->view(), pd,
                        c->masks.as<u64>(), c->K.as<u64>(), rbase, cnt, plan);
   } else if (plan) {
     hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(2048), dim3(256), 0, c->stream, c->view(),
                        c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, d1, c->masks.as<u64>(),
-                       c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, item_pref, plan);
+                       c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, item_pref, plan, rcnt, cnt);
   } else {
     const int bx = std::max(1, (span + kEmitRPB - 1) / kEmitRPB);
     hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(bx, ndesc), dim3(256), 0, c->stream, c->view(),
                        c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, d1, c->masks.as<u64>(),
                        c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, (const int64_t *)nullptr,
-                       (const int *)nullptr);
+                       (const int *)nullptr, (const uint32_t *)nullptr, (u64 *)nullptr);
   }
   return hipGetLastError();
 }
 hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
                        u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase,
                        const int *plan = nullptr, const int64_t *item_pref = nullptr,
-                       const dr::PopDesc &d1 = dr::PopDesc{}) {
+                       const dr::PopDesc &d1 = dr::PopDesc{}, const uint32_t *rcnt = nullptr) {
   if (ndesc <= 0) return hipSuccess;
   switch (c->WS) {
-    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
-    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
-    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
-    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
-    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
-    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1);
+    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
+    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
+    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
+    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
+    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
+    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
   }
   return hipErrorInvalidValue;
 }
@@ -2150,7 +2151,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   int32_t *plan = nullptr, *task_wave, *task_q, *cpush_n, *push_out, *push_wave, *pop_wave, *pop_cur, *pop_q,
           *desc_of_pop, *qidx, *dstops;
   int64_t *task_pos, *item_pref;
-  uint32_t *push_off, *rbase;
+  uint32_t *push_off, *rbase, *rcnt;
   uint8_t *seen, *hits;
   dr::SweepQuery *cq, *dq;
   dr::PopDesc *pd;
@@ -2190,6 +2191,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     item_pref = cv.take<int64_t>(pcap + 1 + (size_t)rb_cap / kEmitRPB + pcap);  // prefix, then item -> segment
     pd = cv.take<dr::PopDesc>(pcap);
     rbase = cv.take<uint32_t>((size_t)rb_cap);
+    rcnt = cv.take<uint32_t>(mask_words / WS);  // one per mask row
     if (pass == 0) {
       HIPCHK(c, c->plan_arena.ensure(cv.off));
       cv.base = static_cast<char *>(c->plan_arena.p);
@@ -2255,6 +2257,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   a.stops = dstops;
   a.stats = dstats;
   a.nq_dev = plan + dr::PL_NQD;
+  a.rcnt = rcnt;
   dr::SweepQuery probe{};
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
   HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
@@ -2264,13 +2267,12 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   // 4. emission
   hipLaunchKernelGGL((dr::k_plan_emit<1024>), dim3(1), dim3(1024), 0, c->stream, pop_cur, pop_q, dq, dstops,
                      c->Cc.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), dedges, kEmitRPB, rb_cap, pd, desc_of_pop,
-                     extra_c, extra_g, pedges, digest, item_pref, plan);
+                     extra_c, extra_g, pedges, digest, counts, item_pref, plan);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, c->rec(4));
-  HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, counts, nullptr, nullptr, nullptr, nullptr, 0, true,
-                        plan + dr::PL_NDESC, nullptr));
-  HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, nullptr, digest, nullptr, nullptr, nullptr, 0, false,
-                        plan + dr::PL_NDESC, item_pref));
+  // positions and pop totals from the sweep's per-round counts (no count pass)
+  HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, counts, digest, nullptr, nullptr, nullptr, 0, false,
+                        plan + dr::PL_NDESC, item_pref, dr::PopDesc{}, rcnt));
   HIPCHK(c, c->rec(5));
   hipLaunchKernelGGL((dr::k_plan_final<256>), dim3(16), dim3(256), 0, c->stream, nw, c->commit.as<uint8_t>(),
                      c->vcount.as<int32_t>(), push_off, push_wave, desc_of_pop, extra_c, extra_g, pedges, counts,

@@ -496,7 +496,8 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
                                               u64 *__restrict__ wedges_out,
                                               uint8_t *__restrict__ hit_out,
                                               int32_t *__restrict__ stop_out,
-                                              u64 *__restrict__ stats_out, const int *__restrict__ nq_dev) {
+                                              u64 *__restrict__ stats_out, const int *__restrict__ nq_dev,
+                                              uint32_t *__restrict__ rcnt) {
   if (nq_dev) {  // grid sized by an upper bound, count on the device (planned replay)
     const int m = *nq_dev;
     if (seq) nq = m;
@@ -599,14 +600,15 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
           if (nz && r - 1 < low) low = r - 1;
           const bool stop = merged || r <= q.bottom || (!nz && low >= r);
           const bool summary = !stop && shortcut && full;
-          if (stats_out) {
+          if (rcnt && has_masks) {  // |mask_r & P_r|: the emission's per-round counts
             int pc = act ? popc64(f & p) : 0;
 #pragma unroll
             for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
-            if (tid == 0 && !stop) {
-              if (summary) st_short++;
-              else { st_partial++; (void)pc; if (WEAK) st_scan += cur.C1 - cur.C0; }
-            }
+            if (tid == 0) rcnt[q.mask_off / WS + (r - q.bottom)] = (uint32_t)pc;
+          }
+          if (stats_out && tid == 0 && !stop) {
+            if (summary) st_short++;
+            else { st_partial++; if (WEAK) st_scan += cur.C1 - cur.C0; }
           }
           if (summary) {  // the round is the union of its rows: apply the summaries, stay in wave 0
             if (act) expand_summary<WS, WEAK>(mv, cur, r, q.bottom, ring, dmask);
@@ -1201,7 +1203,8 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
                                            const u64 *__restrict__ masks, const u64 *__restrict__ K,
                                            const uint32_t *__restrict__ rbase, const int64_t *__restrict__ pop_pos,
                                            u64 *__restrict__ digest, u64 *__restrict__ round_out,
-                                           int32_t *__restrict__ ids, int64_t ids_cap, u64 *s_dg) {
+                                           int32_t *__restrict__ ids, int64_t ids_cap, u64 *s_dg,
+                                           const uint32_t *__restrict__ rcnt, u64 *__restrict__ pcount) {
   constexpr int SPL = 16;  // slots per lane per pass: one wave covers 1024 slots with one load latency
   const u64 *img = (d.use_k ? K : masks) + d.mask_off;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1214,7 +1217,16 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
   const int64_t pbase = pop_pos ? pop_pos[d.out] : 0;
   for (int r = ra + wid; r < rb; r += NWAVE) {
     const u64 mw = lane < WS ? img[(int64_t)r * WS + lane] : 0ULL;  // lane w holds mask word w
-    u64 pos = (u64)d.pos0 + rbase[d.rbase_off + (r - d.first)];
+    u64 pos;
+    if (rcnt) {  // the sweep's per-round counts: position = pos0 + counts of rounds first..r-1
+      const uint32_t *rc = rcnt + d.mask_off / WS;
+      u64 below = 0;
+      for (int x = d.first + lane; x < r; x += 64) below += rc[x];
+      pos = (u64)d.pos0 + wave_sum(below);
+      if (lane == 0 && rc[r]) atomicAdd(pcount + d.out, (u64)rc[r]);
+    } else {
+      pos = (u64)d.pos0 + rbase[d.rbase_off + (r - d.first)];
+    }
     u64 rdg = 0;
     const uint32_t sa = slot_off[r], sb = slot_off[r + 1];
     for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPL) {
@@ -1266,7 +1278,9 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
 
 // Two launch shapes: grid (round blocks, segments) when item_pref is null; else
 // a fixed grid striding over the work items of ctl[0] segments, segment i owning
-// items [item_pref[i], item_pref[i+1]) (device-planned replay).
+// items [item_pref[i], item_pref[i+1]) (device-planned replay).  There, with rcnt
+// (the delivery sweep's per-round counts, indexed like the mask rows), positions
+// come from rcnt and the pop totals accumulate in pcount[out]: no count pass.
 template <int WS, int NT, int RPB>
 __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__restrict__ slot_off,
                                                  const uint16_t *__restrict__ slot_src,
@@ -1276,11 +1290,12 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
                                                  const int64_t *__restrict__ pop_pos,
                                                  u64 *__restrict__ digest, u64 *__restrict__ round_out,
                                                  int32_t *__restrict__ ids, int64_t ids_cap,
-                                                 const int64_t *__restrict__ item_pref, const int *__restrict__ ctl) {
+                                                 const int64_t *__restrict__ item_pref, const int *__restrict__ ctl,
+                                                 const uint32_t *__restrict__ rcnt, u64 *__restrict__ pcount) {
   __shared__ u64 s_dg;
   if (!item_pref) {
     emit_block<WS, NT, RPB>(g, slot_off, slot_src, pd ? pd[blockIdx.y] : d1, blockIdx.x, masks, K, rbase, pop_pos,
-                            digest, round_out, ids, ids_cap, &s_dg);
+                            digest, round_out, ids, ids_cap, &s_dg, nullptr, nullptr);
     return;
   }
   // item_pref[nd] = item count; item_pref[nd + 1 + it] = the segment owning item it
@@ -1289,7 +1304,7 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
   for (int64_t it = blockIdx.x; it < nit; it += gridDim.x) {
     const int lo = (int)item_pref[nd + 1 + it];
     emit_block<WS, NT, RPB>(g, slot_off, slot_src, pd[lo], (int)(it - item_pref[lo]), masks, K, rbase, pop_pos,
-                            digest, round_out, ids, ids_cap, &s_dg);
+                            digest, round_out, ids, ids_cap, &s_dg, rcnt, pcount);
     __syncthreads();
   }
 }

@@ -231,7 +231,8 @@ __global__ __launch_bounds__(NT) void k_plan_emit(const int32_t *__restrict__ po
                                                   PopDesc *__restrict__ pd, int32_t *__restrict__ desc_of_pop,
                                                   u64 *__restrict__ extra_c, u64 *__restrict__ extra_g,
                                                   u64 *__restrict__ pedges, u64 *__restrict__ digest,
-                                                  int64_t *__restrict__ item_pref, int32_t *__restrict__ plan) {
+                                                  u64 *__restrict__ counts, int64_t *__restrict__ item_pref,
+                                                  int32_t *__restrict__ plan) {
   __shared__ int64_t s[NT / 64];
   __shared__ int64_t c0, c1, c2;
   const int tid = threadIdx.x;
@@ -262,6 +263,7 @@ __global__ __launch_bounds__(NT) void k_plan_emit(const int32_t *__restrict__ po
       extra_g[p] = eg;
       pedges[p] = pe;
       digest[p] = 0;
+      counts[p] = 0;  // k_emit_ids accumulates the pop's delivered-vertex count here
       has = first <= last ? 1 : 0;
       nr = has ? last - first + 1 : 0;
       items = has ? (nr + rpb - 1) / rpb : 0;
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(NT) void k_plan_final(int nw, const uint8_t *__rest
   for (int64_t p = gt; p < np; p += gs) {
     const int di = desc_of_pop[p];
     h_push_wave[p] = push_wave[p];
-    h_pc[p] = extra_c[p] + (di >= 0 ? counts[di] : 0);
+    h_pc[p] = extra_c[p] + (di >= 0 ? counts[p] : 0);
     h_pd[p] = extra_g[p] + digest[p];
     h_pe[p] = pedges[p];
   }
