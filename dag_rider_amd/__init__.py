@@ -3,8 +3,9 @@
 Drop-in for the hot path of xenowits/dag-rider (process/process.go: path,
 waveReady, orderVertices) behind a C ABI (include/dagrider_gpu.h) implemented
 by hand-written HIP kernels for gfx950 (csrc/).  Python here is orchestration:
-ctypes handles (engine.py), the reference-shaped Process mirror (process.py),
-workload generation (gen.py).
+ctypes handles (engine.py, shard.py), the DRW1 capture format (wire.py) and
+workload generation (gen.py).  The reference-shaped Process mirror is C++
+(host/process.hpp); the Go binding is go/dagridergpu.
 """
 from .dag import PackedDag, Vertex, VertexID, flatten_lists, pack_lists  # noqa: F401
 

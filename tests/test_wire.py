@@ -142,3 +142,16 @@ def test_gpu_replay_from_capture(gpu_device):
             e.append_lists(d)
             res.append([e.path_batch(qs, strong).tolist() for strong in (False, True)])
     assert res[0] == res[1]
+
+
+def test_go_fixture_current():
+    """tests/golden/figure1.drw1 (read by go/dagridergpu's tests, which re-encode it byte
+    for byte) is what wire.py writes for the fixture DAG."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_wire_fixture import fixture_dag
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "figure1.drw1"), "rb") as f:
+        assert f.read() == wire.encode(fixture_dag())
