@@ -32,19 +32,22 @@ $(BUILD)/dag_gen.o: $(PKG)/csrc/dag_gen.cpp include/dagrider_gen.h | $(BUILD)
 $(BUILD)/wire.o: $(PKG)/csrc/wire.cpp include/dagrider_wire.h include/dagrider_gpu.h | $(BUILD)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp include/dagrider_gpu.h | $(BUILD)
+$(BUILD)/host_rounds.o: $(PKG)/csrc/host_rounds.cpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h | $(BUILD)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/engine_timing.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp include/dagrider_gpu.h | $(BUILD)
+$(BUILD)/engine_timing.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DDR_SWEEP_TIMING -c $< -o $@
 
-$(LIBT): $(BUILD)/engine_timing.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o
+$(LIBT): $(BUILD)/engine_timing.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdagrider_gpu_timing.so
 
 $(BUILD)/shard.o: $(PKG)/csrc/shard.hip include/dagrider_shard.h include/dagrider_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/engine.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o
+$(LIB): $(BUILD)/engine.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdagrider_gpu.so
 
 $(ORACLE): oracle/ref_literal.c oracle/ref_bitset.c oracle/oracle.h

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -16,6 +17,7 @@
 #include <vector>
 
 #include "dagrider_gpu.h"
+#include "host_rounds.hpp"
 #include "kernels.hpp"
 #include "replay_plan.hpp"
 #include "batch.hpp"
@@ -75,14 +77,7 @@ struct DevBuf {
 // here and is flattened to the device from the lowest changed round on
 // (dr_ctx::upload_suffix), so a vertex appended to an old round
 // (process.go:229) rewrites only the rounds from there to the top.
-struct HostRound {
-  std::vector<uint16_t> slots;   // source per slot, insertion order (0 = ghost {0,0})
-  uint64_t deg = 0;              // total strong degree
-  uint64_t nweak = 0;            // weak edges (near + far)
-  std::vector<uint32_t> wc_key;  // weak columns: distinct near targets (delta << 11 | t-1), sorted
-  std::vector<u64> wc_rows;      // [key][WS]: the round's sources with that weak edge
-  std::vector<u64> far;          // weak edges with delta > 1023: (own s-1) << 32 | (r' << 11 | t-1)
-};
+using dr_host::HostRound;
 
 }  // namespace
 
@@ -112,7 +107,6 @@ struct dr_ctx {
   // of the flattened device arrays (valid for rounds < up_lo)
   std::vector<HostRound> hr;
   std::vector<u64> h_present;
-  std::vector<int32_t> wc_tab;  // append scratch: weak column of (delta, target) in the round being built
   std::vector<uint32_t> h_slot_off{0}, h_wc_roff{0}, h_far_roff{0}, h_weak_roff{0};
   int up_lo = 0;  // lowest round whose flattened device arrays are stale
   // round summaries (U, SD, WU) per round: sdirty[r] = stale; the canonical cone
@@ -123,6 +117,12 @@ struct dr_ctx {
   bool canon_ok = false;      // K/C/G/E describe the current DAG
   int32_t canon_segments = 0;
   DevBuf U, WU, SD, K, good, CE, RD, Cc, Gc, Ec, crbase, ccount, nseg, stops, qstats, srounds;
+  // incremental canonical cone: the previous cone, per-round
+  // canonical digests, the lowest round to re-emit; canon_lo = lowest round
+  // touched since the last cone
+  DevBuf Kprev, RG, rlo;
+  int canon_lo = 0, canon_dd = -1;
+  bool kprev_ok = false;
   int ndirty = 0;     // rounds with sdirty set
   int canon_T = -1;   // top round of the last canonical build
   std::vector<uint64_t> hC, hG, hE;
@@ -297,6 +297,7 @@ struct dr_ctx {
     while ((int)sdirty.size() <= r) { sdirty.push_back(1); ndirty++; }
     if (!sdirty[r]) { sdirty[r] = 1; ndirty++; }
     canon_ok = false;
+    canon_lo = std::min(canon_lo, r);
     up_lo = std::min(up_lo, r);
   }
   // Flatten rounds [up_lo, nrounds) of the variable-size per-round arrays
@@ -476,35 +477,38 @@ constexpr int kEmitRPB = 4;  // rounds per emit workgroup: one per wave
 template <int WS>
 hipError_t launch_emit_t(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
                          u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase,
-                         const int *plan, const int64_t *item_pref, const dr::PopDesc &d1, const uint32_t *rcnt) {
+                         const int *plan, const int64_t *item_pref, const dr::PopDesc &d1, const uint32_t *rcnt,
+                         const int *skip) {
   if (count_phase) {
     hipLaunchKernelGGL((dr::k_emit_count<WS, 256>), dim3(ndesc), dim3(256), 0, c->stream, c->view(), pd,
                        c->masks.as<u64>(), c->K.as<u64>(), rbase, cnt, plan);
   } else if (plan) {
     hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(2048), dim3(256), 0, c->stream, c->view(),
                        c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, d1, c->masks.as<u64>(),
-                       c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, item_pref, plan, rcnt, cnt);
+                       c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, item_pref, plan, rcnt, cnt,
+                       (const int *)nullptr);
   } else {
     const int bx = std::max(1, (span + kEmitRPB - 1) / kEmitRPB);
     hipLaunchKernelGGL((dr::k_emit_ids<WS, 256, kEmitRPB>), dim3(bx, ndesc), dim3(256), 0, c->stream, c->view(),
                        c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), pd, d1, c->masks.as<u64>(),
                        c->K.as<u64>(), rbase, pos, dg, round_out, ids, cap, (const int64_t *)nullptr,
-                       (const int *)nullptr, (const uint32_t *)nullptr, (u64 *)nullptr);
+                       (const int *)nullptr, (const uint32_t *)nullptr, (u64 *)nullptr, skip);
   }
   return hipGetLastError();
 }
 hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, uint32_t *rbase, u64 *cnt, u64 *dg,
                        u64 *round_out, const int64_t *pos, int32_t *ids, int64_t cap, bool count_phase,
                        const int *plan = nullptr, const int64_t *item_pref = nullptr,
-                       const dr::PopDesc &d1 = dr::PopDesc{}, const uint32_t *rcnt = nullptr) {
+                       const dr::PopDesc &d1 = dr::PopDesc{}, const uint32_t *rcnt = nullptr,
+                       const int *skip = nullptr) {
   if (ndesc <= 0) return hipSuccess;
   switch (c->WS) {
-    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
-    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
-    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
-    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
-    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
-    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt);
+    case 1: return launch_emit_t<1>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt, skip);
+    case 2: return launch_emit_t<2>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt, skip);
+    case 4: return launch_emit_t<4>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt, skip);
+    case 8: return launch_emit_t<8>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt, skip);
+    case 16: return launch_emit_t<16>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt, skip);
+    case 32: return launch_emit_t<32>(c, ndesc, span, pd, rbase, cnt, dg, round_out, pos, ids, cap, count_phase, plan, item_pref, d1, rcnt, skip);
   }
   return hipErrorInvalidValue;
 }
@@ -581,10 +585,10 @@ hipError_t launch_round_summary(dr_ctx *c, const int32_t *rounds, int nr) {
 
 // canonical cone: K^cand per round, then the exact cone at the bad rounds
 template <int WS>
-hipError_t launch_canon_cone_t(dr_ctx *c, int T) {
+hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo) {
   const dr::MemoView mv = c->memo_view();
   hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
-                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>());
+                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>(), c->rlo.as<int>(), lo);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int dl = c->depth_log2();
@@ -595,16 +599,20 @@ hipError_t launch_canon_cone_t(dr_ctx *c, int T) {
   hipLaunchKernelGGL((dr::k_canon<WS, NTS>), dim3(1), dim3(NTS), lds, c->stream, c->view(), mv, T, dl,
                      c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>(), c->RD.as<u64>(),
                      c->Cc.as<u64>(), c->crbase.as<uint32_t>());
+  e = hipGetLastError();
+  if (e != hipSuccess || lo <= 1) return e;
+  hipLaunchKernelGGL((dr::k_canon_diff<WS>), dim3((lo - 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), lo,
+                     c->K.as<u64>(), c->Kprev.as<u64>(), c->rlo.as<int>());
   return hipGetLastError();
 }
-hipError_t launch_canon_cone(dr_ctx *c, int T) {
+hipError_t launch_canon_cone(dr_ctx *c, int T, int lo) {
   switch (c->WS) {
-    case 1: return launch_canon_cone_t<1>(c, T);
-    case 2: return launch_canon_cone_t<2>(c, T);
-    case 4: return launch_canon_cone_t<4>(c, T);
-    case 8: return launch_canon_cone_t<8>(c, T);
-    case 16: return launch_canon_cone_t<16>(c, T);
-    case 32: return launch_canon_cone_t<32>(c, T);
+    case 1: return launch_canon_cone_t<1>(c, T, lo);
+    case 2: return launch_canon_cone_t<2>(c, T, lo);
+    case 4: return launch_canon_cone_t<4>(c, T, lo);
+    case 8: return launch_canon_cone_t<8>(c, T, lo);
+    case 16: return launch_canon_cone_t<16>(c, T, lo);
+    case 32: return launch_canon_cone_t<32>(c, T, lo);
   }
   return hipErrorInvalidValue;
 }
@@ -710,7 +718,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->dlv,     &c->push_out, &c->push_n,  &c->edges,    &c->hits, &c->wedges,
                     &c->commit,  &c->vcount,  &c->popdesc,  &c->rbase,    &c->counts,
                     &c->digest,  &c->pop_pos, &c->ids,      &c->U,        &c->WU,
-                    &c->SD,      &c->K,       &c->good,     &c->CE,       &c->RD,
+                    &c->SD,      &c->K,       &c->Kprev,    &c->RG,       &c->rlo,      &c->good,     &c->CE,       &c->RD,
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds, &c->plan_out,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
@@ -776,91 +784,22 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   if (!slot_off || (!slot_src && slot_off[k] > slot_off[0]) || !strong || !weak_off)
     return c->fail(DR_E_INVAL, "null array");
   const int n = c->n, W = c->W, WS = c->WS;
-  std::vector<u64> pres((size_t)k * WS, 0);
-  std::vector<HostRound> nh(k);
-  std::vector<uint16_t> vdeg((size_t)k * n, 0), vwdeg((size_t)k * n, 0);
-  size_t nfar = 0;
-  int dmax = c->dmax_near;
-  const u64 lastmask = (n % 64) ? ((1ULL << (n % 64)) - 1ULL) : ~0ULL;
-  // weak columns of a round: tab[delta * n + t] = column index of (delta, t)
-  // (-1 = none yet); touched entries are reset after each round
-  if (c->wc_tab.empty()) c->wc_tab.assign((size_t)1024 * n, -1);
-  std::vector<int32_t> &tab = c->wc_tab;
-  std::vector<uint32_t> touched, order;
-  std::vector<u64> rows_tmp;
-  for (int i = 0; i < k; i++) {
-    const int r = r0 + i;
-    u64 *P = &pres[(size_t)i * WS];
-    HostRound &h = nh[i];
-    for (uint32_t sl = slot_off[i]; sl < slot_off[i + 1]; sl++) {
-      const int s = slot_src[sl];
-      if (s > n) return c->fail(DR_E_CONTRACT, "round %d slot %u: source %d > n=%d", r, sl - slot_off[i], s, n);
-      h.slots.push_back((uint16_t)s);
-      if (s == 0) continue;  // ghost slot {0,0}
-      u64 &wd = P[(s - 1) >> 6];
-      const u64 bit = 1ULL << ((s - 1) & 63);
-      if ((wd & bit) && r >= 1) return c->fail(DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, s);
-      wd |= bit;
-    }
-    touched.clear();
-    for (int s0 = 0; s0 < n; s0++) {
-      const bool here = (P[s0 >> 6] >> (s0 & 63)) & 1ULL;
-      const uint64_t *row = strong + ((size_t)i * n + s0) * W;
-      uint64_t d = 0;
-      bool nz = false;
-      for (int w = 0; w < W; w++) { d += (uint64_t)__builtin_popcountll(row[w]); nz |= row[w] != 0; }
-      if (nz && !here) return c->fail(DR_E_CONTRACT, "round %d: strong edges on absent vertex (%d,%d)", r, r, s0 + 1);
-      if (nz && r == 0) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", s0 + 1);
-      if (row[W - 1] & ~lastmask) return c->fail(DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
-      h.deg += d;
-      vdeg[(size_t)i * n + s0] = (uint16_t)d;
-      const uint32_t ea = weak_off[(size_t)i * n + s0], eb = weak_off[(size_t)i * n + s0 + 1];
-      if (eb < ea) return c->fail(DR_E_INVAL, "weak_off not monotone at round %d", r);
-      if (eb > ea && !here) return c->fail(DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1);
-      vwdeg[(size_t)i * n + s0] = (uint16_t)std::min<uint32_t>(eb - ea, 65535u);
-      h.nweak += eb - ea;
-      for (uint32_t e = ea; e < eb; e++) {
-        const uint32_t t = weak_tgt[e];
-        const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
-        if (ts >= n) return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): source > n", r, s0 + 1, tr, ts + 1);
-        if (tr > r - 2) return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target a round < r-1", r, s0 + 1, tr, ts + 1);
-        const int delta = r - tr;
-        if (delta <= 1023) {
-          const size_t at = (size_t)delta * n + ts;
-          int32_t col = tab[at];
-          if (col < 0) {
-            col = tab[at] = (int32_t)h.wc_key.size();
-            touched.push_back((uint32_t)at);
-            h.wc_key.push_back(((uint32_t)delta << 11) | (uint32_t)ts);
-            h.wc_rows.resize(h.wc_rows.size() + WS, 0ULL);
-          }
-          h.wc_rows[(size_t)col * WS + (s0 >> 6)] |= 1ULL << (s0 & 63);
-          dmax = std::max(dmax, delta);
-        } else {
-          h.far.push_back(((u64)s0 << 32) | t);
-          nfar++;
-        }
-      }
-    }
-    for (uint32_t at : touched) tab[at] = -1;
-    // columns sorted by key (wc_add's binary search relies on it; no kernel does)
-    const size_t nk = h.wc_key.size();
-    bool sorted = true;
-    for (size_t x = 1; x < nk && sorted; x++) sorted = h.wc_key[x - 1] < h.wc_key[x];
-    if (!sorted) {
-      order.resize(nk);
-      for (size_t x = 0; x < nk; x++) order[x] = (uint32_t)x;
-      std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return h.wc_key[a] < h.wc_key[b]; });
-      std::vector<uint32_t> keys(nk);
-      rows_tmp.resize(nk * WS);
-      for (size_t x = 0; x < nk; x++) {
-        keys[x] = h.wc_key[order[x]];
-        std::memcpy(&rows_tmp[x * WS], &h.wc_rows[(size_t)order[x] * WS], (size_t)WS * 8);
-      }
-      h.wc_key.swap(keys);
-      h.wc_rows.swap(rows_tmp);
-    }
-  }
+  dr_host::PackedRounds in;
+  in.n = n;
+  in.W = W;
+  in.WS = WS;
+  in.r0 = r0;
+  in.k = k;
+  in.slot_off = slot_off;
+  in.slot_src = slot_src;
+  in.strong = strong;
+  in.weak_off = weak_off;
+  in.weak_tgt = weak_tgt;
+  dr_host::BuiltRounds built;
+  if (int rc = dr_host::build_packed_rounds(in, c->dmax_near, built, c->err)) return rc;
+  std::vector<HostRound> &nh = built.rounds;
+  const size_t nfar = built.nfar;
+  const int dmax = built.dmax;
   // ---- commit: rows and per-vertex degrees, then the flattened per-round arrays ----
   const size_t row_words = (size_t)n * WS;
   if (WS == W && (size_t)k * row_words * 8 <= ((size_t)16 << 20)) {  // per-round appends: pinned staging
@@ -876,10 +815,10 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  HIPCHK(c, c->h2d(c->sdeg.as<uint16_t>() + (size_t)r0 * n, vdeg.data(), vdeg.size() * 2));
-  HIPCHK(c, c->h2d(c->wdeg.as<uint16_t>() + (size_t)r0 * n, vwdeg.data(), vwdeg.size() * 2));
+  HIPCHK(c, c->h2d(c->sdeg.as<uint16_t>() + (size_t)r0 * n, built.sdeg.data(), built.sdeg.size() * 2));
+  HIPCHK(c, c->h2d(c->wdeg.as<uint16_t>() + (size_t)r0 * n, built.wdeg.data(), built.wdeg.size() * 2));
   for (auto &h : nh) c->hr.push_back(std::move(h));
-  c->h_present.insert(c->h_present.end(), pres.begin(), pres.end());
+  c->h_present.insert(c->h_present.end(), built.pres.begin(), built.pres.end());
   c->nfar += nfar;
   c->dmax_near = dmax;
   c->nrounds += k;
@@ -1232,6 +1171,9 @@ int ensure_summary_bufs(dr_ctx *c) {
   HIPCHK(c, c->good.ensure(R + 8));  // k_canon reads good[] 8 rounds at a time
   HIPCHK(c, c->CE.ensure(R * 8));
   HIPCHK(c, c->RD.ensure(R * 8));
+  HIPCHK(c, c->Kprev.ensure(R * WS * 8));
+  HIPCHK(c, c->RG.ensure(R * 8));
+  HIPCHK(c, c->rlo.ensure(8));
   HIPCHK(c, c->Cc.ensure(R * 8));
   HIPCHK(c, c->Gc.ensure(R * 8));
   HIPCHK(c, c->Ec.ensure(R * 8));
@@ -1277,8 +1219,15 @@ int refresh_rounds(dr_ctx *c) {
 // fork): work launched on stream2 first, beside the canonical chain, which then
 // stays on the main stream; ev_join marks its end.  forked: stream2 already
 // waits on an event of the main stream (build_summary's).
-int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool forked = false) {
+int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool forked = false,
+                 bool incremental = false) {
   const int T = c->nrounds - 1;
+  // incremental (the per-call path): rounds below the lowest one that changed
+  // since the last cone, and whose canonical vertices are unchanged, keep their
+  // per-round digests (RG); a replay recomputes every round
+  const bool inc = incremental && c->kprev_ok && c->canon_dd == c->memo_dd();
+  const int lo = inc ? std::max(1, std::min(c->canon_lo, c->canon_T + 1)) : 1;
+  if (c->kprev_ok) std::swap(c->K, c->Kprev);  // Kprev: the last cone (every round of K is rewritten)
   struct Swap {  // launch helpers use c->stream: point it at stream2 for the canonical chain
     dr_ctx *c;
     bool on;
@@ -1297,7 +1246,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
   Swap sw(c, fork && !side);
   // canonical cone, per-round counts and positions (k_kcand + k_canon), then the
   // per-round digests (emission) and their prefixes
-  HIPCHK(c, launch_canon_cone(c, T));
+  HIPCHK(c, launch_canon_cone(c, T, lo));  // *rlo = the lowest round to re-emit
   dr::PopDesc d{};
   d.mask_off = 0;
   d.rbase_off = 1;  // crbase is indexed by round; rbase_off addresses round `first`
@@ -1306,12 +1255,16 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
   d.last = T;
   d.out = 0;
   d.use_k = 1;
-  HIPCHK(c, launch_emit(c, 1, T, nullptr, c->crbase.as<uint32_t>(), nullptr, nullptr, c->RD.as<u64>(), nullptr,
-                        nullptr, 0, false, nullptr, nullptr, d));  // the descriptor travels by value
-  hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RD.as<u64>(),
+  HIPCHK(c, launch_emit(c, 1, T, nullptr, c->crbase.as<uint32_t>(), nullptr, nullptr, c->RG.as<u64>(), nullptr,
+                        nullptr, 0, false, nullptr, nullptr, d, nullptr,
+                        lo > 1 ? c->rlo.as<int>() : nullptr));  // the descriptor travels by value
+  hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
                      c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
   if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
+  c->kprev_ok = true;
+  c->canon_dd = c->memo_dd();
+  c->canon_lo = INT_MAX;
   c->canon_T = T;
   c->canon_ok = true;
   c->canon_host = false;
@@ -1341,9 +1294,9 @@ int refresh_canon(dr_ctx *c) {
   if (int rc = refresh_rounds(c)) return rc;
   if (!c->canon_ok) {
     if (int rc = ensure_summary_bufs(c)) return rc;
-    if (int rc = launch_canon(c, false, nullptr)) return rc;
+    if (int rc = launch_canon(c, false, nullptr, false, true)) return rc;
   }
-  return fetch_canon(c);
+  return DR_OK;  // host copies of the prefixes: fetch_canon, when a host-planned path needs them
 }
 
 // Full summary pass (dr_replay): every strong row of rounds 1..T read once by
@@ -2081,6 +2034,10 @@ extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *com
   return DR_OK;
 }
 
+namespace {
+int deliver_planned(dr_ctx *c, const std::vector<Pop> &pops, uint64_t *pcount, uint64_t *pdigest);
+}
+
 extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack, int cur_round, int mode,
                                  int32_t *out_ids, size_t cap, size_t *out_n, uint64_t *pop_count,
                                  uint64_t *pop_digest) {
@@ -2105,8 +2062,13 @@ extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack,
     if (int rc = refresh_canon(c)) return rc;
   std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
   int64_t tot = 0;
-  int rc = run_deliver(c, pops, mode, cnt.data(), dg.data(), nullptr, nullptr, out_ids, (int64_t)cap, &tot, nullptr,
-                       nullptr);
+  // REF mode on fresh summaries without ids: planned on the device, one copy back
+  int rc = 1;
+  if (mode == DR_DELIVER_REF && !out_ids && c->plan_mode != 0 && summary_fresh(c))
+    rc = deliver_planned(c, pops, cnt.data(), dg.data());
+  if (rc == 1)
+    rc = run_deliver(c, pops, mode, cnt.data(), dg.data(), nullptr, nullptr, out_ids, (int64_t)cap, &tot, nullptr,
+                     nullptr);
   if (rc) return rc;
   if (!out_ids) {
     tot = 0;
@@ -2131,6 +2093,113 @@ struct Carve {
     return p;
   }
 };
+
+// orderVertices (DR_DELIVER_REF, fresh summaries, no ids) planned on the device:
+// one query per distinct popped leader (longest first), the delivery sweeps,
+// emission segments from the sweeps' stops, per-pop totals, one copy back --
+// replay_planned's delivery half for a caller-given stack.  Returns 1 when the
+// bounds do not fit (the caller takes run_deliver), else a DR_* status.
+int deliver_planned(dr_ctx *c, const std::vector<Pop> &pops, uint64_t *pcount, uint64_t *pdigest) {
+  const int WS = c->WS, T = c->nrounds - 1, np = (int)pops.size();
+  std::vector<int> order(np);
+  for (int i = 0; i < np; i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    if (pops[a].round != pops[b].round) return pops[a].round > pops[b].round;
+    return pops[a].source < pops[b].source;
+  });
+  std::vector<dr::SweepQuery> qv;
+  std::vector<int32_t> pq(np), pcur(np);
+  int64_t mw = 0;
+  for (int k = 0; k < np; k++) {
+    const Pop &p = pops[order[k]];
+    if (k == 0 || pops[order[k - 1]].round != p.round || pops[order[k - 1]].source != p.source) {
+      dr::SweepQuery s{};
+      s.top = p.round;
+      s.bottom = 0;
+      s.src0 = (p.source >= 1 && p.source <= c->n) ? p.source - 1 : -1;
+      s.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
+      s.mask_off = mw;
+      s.tgt0 = -1;
+      mw += (int64_t)(p.round + 1) * WS;
+      qv.push_back(s);
+    }
+    pq[order[k]] = (int32_t)qv.size() - 1;
+  }
+  for (int i = 0; i < np; i++) pcur[i] = pops[i].cur_round;
+  const int nq = (int)qv.size();
+  const int64_t rb_cap = (int64_t)np * (T + 1);
+  if (mw > ((int64_t)1 << 29) || rb_cap > ((int64_t)1 << 28)) return 1;
+  // arena: the inputs first (one copy), then device-only scratch
+  Carve cv;
+  int32_t *plan = nullptr, *pop_q, *pop_cur, *dstops, *desc_of_pop;
+  dr::SweepQuery *dq;
+  u64 *dedges, *dwedges, *extra_c, *extra_g, *pedges, *counts, *digest, *outv;
+  int64_t *item_pref;
+  dr::PopDesc *pd;
+  uint32_t *rcnt;
+  size_t in_bytes = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    cv.off = 0;
+    plan = cv.take<int32_t>(dr::PL_N);
+    dq = cv.take<dr::SweepQuery>(nq);
+    pop_q = cv.take<int32_t>(np);
+    pop_cur = cv.take<int32_t>(np);
+    in_bytes = cv.off;
+    dedges = cv.take<u64>(nq);
+    dwedges = cv.take<u64>(nq);
+    dstops = cv.take<int32_t>(nq);
+    desc_of_pop = cv.take<int32_t>(np);
+    extra_c = cv.take<u64>(np);
+    extra_g = cv.take<u64>(np);
+    pedges = cv.take<u64>(np);
+    counts = cv.take<u64>(np);
+    digest = cv.take<u64>(np);
+    outv = cv.take<u64>(2 * (size_t)np);
+    item_pref = cv.take<int64_t>(np + 1 + (size_t)rb_cap / kEmitRPB + np);
+    pd = cv.take<dr::PopDesc>(np);
+    rcnt = cv.take<uint32_t>((size_t)mw / WS);
+    if (pass == 0) {
+      HIPCHK(c, c->plan_arena.ensure(cv.off));
+      cv.base = static_cast<char *>(c->plan_arena.p);
+    }
+  }
+  HIPCHK(c, c->masks.ensure((size_t)mw * 8));
+  {  // inputs, laid out as in the arena
+    std::vector<char> hb(in_bytes, 0);
+    char *db = cv.base;
+    auto at = [&](void *p) { return hb.data() + (static_cast<char *>(p) - db); };
+    int32_t *hp = reinterpret_cast<int32_t *>(at(plan));
+    hp[dr::PL_NPUSH] = np;
+    hp[dr::PL_NQD] = nq;
+    std::memcpy(at(dq), qv.data(), (size_t)nq * sizeof(dr::SweepQuery));
+    std::memcpy(at(pop_q), pq.data(), (size_t)np * 4);
+    std::memcpy(at(pop_cur), pcur.data(), (size_t)np * 4);
+    HIPCHK(c, c->h2d(db, hb.data(), in_bytes));
+  }
+  SweepArgs a{};
+  a.q = dq;
+  a.nq = nq;
+  a.seq = 0;
+  a.masks = c->masks.as<u64>();
+  a.edges = dedges;
+  a.wedges = dwedges;
+  a.stops = dstops;
+  a.rcnt = rcnt;
+  HIPCHK(c, launch_sweep(c, a, dr::SW_WEAK | dr::SW_MERGE));
+  hipLaunchKernelGGL((dr::k_plan_emit<1024>), dim3(1), dim3(1024), 0, c->stream, pop_cur, pop_q, dq, dstops,
+                     c->Cc.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), dedges, kEmitRPB, rb_cap, pd, desc_of_pop,
+                     extra_c, extra_g, pedges, digest, counts, item_pref, plan);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, launch_emit(c, np, 0, pd, nullptr, counts, digest, nullptr, nullptr, nullptr, 0, false,
+                        plan + dr::PL_NDESC, item_pref, dr::PopDesc{}, rcnt));
+  hipLaunchKernelGGL((dr::k_pop_final<256>), dim3(std::max(1, std::min(64, (np + 255) / 256))), dim3(256), 0,
+                     c->stream, plan, desc_of_pop, extra_c, extra_g, counts, digest, outv, outv + np);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, c->d2h(pcount, outv, (size_t)np * 8));
+  HIPCHK(c, c->d2h(pdigest, outv + np, (size_t)np * 8));
+  HIPCHK(c, c->sync());
+  return DR_OK;
+}
 
 // Device-planned replay (memo summaries, DR_DELIVER_REF, no ids): the same
 // phases as the host-planned path below, planned by replay_plan.hpp's kernels,

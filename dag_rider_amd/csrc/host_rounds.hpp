@@ -1,0 +1,47 @@
+// host_rounds.hpp -- the host-side per-round state of a mirror and its builder
+// for pre-packed rounds (dr_append_rounds_packed).  Host code only: compiled by
+// g++ with OpenMP (host_rounds.cpp), used by engine.hip.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace dr_host {
+
+// Host-side state of one mirrored round.  Everything variable-size per round lives
+// here and is flattened to the device from the lowest changed round on
+// (dr_ctx::upload_suffix), so a vertex appended to an old round
+// (process.go:229) rewrites only the rounds from there to the top.
+struct HostRound {
+  std::vector<uint16_t> slots;   // source per slot, insertion order (0 = ghost {0,0})
+  uint64_t deg = 0;              // total strong degree
+  uint64_t nweak = 0;            // weak edges (near + far)
+  std::vector<uint32_t> wc_key;  // weak columns: distinct near targets (delta << 11 | t-1), sorted
+  std::vector<uint64_t> wc_rows; // [key][WS]: the round's sources with that weak edge
+  std::vector<uint64_t> far;     // weak edges with delta > 1023: (own s-1) << 32 | (r' << 11 | t-1)
+};
+
+// k pre-packed rounds r0..r0+k-1 (the dr_append_rounds_packed arrays).
+struct PackedRounds {
+  int n = 0, W = 0, WS = 0, r0 = 0, k = 0;
+  const uint32_t *slot_off = nullptr;
+  const uint16_t *slot_src = nullptr;
+  const uint64_t *strong = nullptr;
+  const uint32_t *weak_off = nullptr;
+  const uint32_t *weak_tgt = nullptr;
+};
+
+struct BuiltRounds {
+  std::vector<HostRound> rounds;  // k
+  std::vector<uint64_t> pres;     // k * WS presence words
+  std::vector<uint16_t> sdeg, wdeg;  // k * n per-vertex strong / weak degrees
+  size_t nfar = 0;
+  int dmax = 1;                   // largest near weak delta seen (>= the caller's)
+};
+
+// Validate and build the host state of every round (rounds in parallel).
+// Returns 0 or a DR_E_* code with `err` set to the message of the first failing
+// round, exactly as a sequential pass over the rounds would report it.
+int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std::string &err);
+
+}  // namespace dr_host

@@ -974,8 +974,9 @@ __global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64
 template <int WS>
 __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K,
                                                uint8_t *__restrict__ good, u64 *__restrict__ CE,
-                                               u64 *__restrict__ RD) {
+                                               u64 *__restrict__ RD, int *__restrict__ rlo, int lo) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
+  if (rlo && blockIdx.x == 0 && threadIdx.x == 0) *rlo = lo;  // k_canon_diff lowers it
   if (r > T) return;
   bool bad = false;
   int cnt = 0;
@@ -1000,6 +1001,23 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
     CE[r] = r == 0 ? 0 : mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
     RD[r] = r == 0 ? 0 : (u64)cnt;
   }
+}
+
+// Incremental canonical emission: the lowest round r < lo whose canonical
+// vertices K_r & P_r differ from the previous cone's (rounds >= lo changed or are
+// new) -> atomicMin(*rlo).  Rounds below *rlo keep their per-round digests, and
+// their positions are unchanged (every count below them is).  One wave per round.
+template <int WS>
+__global__ __launch_bounds__(256) void k_canon_diff(DagView g, int lo, const u64 *__restrict__ K,
+                                                    const u64 *__restrict__ Kprev, int *__restrict__ rlo) {
+  const int r = 1 + blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
+  if (r >= lo) return;
+  bool diff = false;
+  if (w < WS) {
+    const size_t i = (size_t)r * WS + w;
+    diff = ((K[i] ^ Kprev[i]) & g.present[i]) != 0ULL;
+  }
+  if (__ballot(diff) != 0ULL && w == 0) atomicMin(rlo, r);
 }
 
 // ---------------------------------------------------------------------------
@@ -1204,7 +1222,8 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
                                            const uint32_t *__restrict__ rbase, const int64_t *__restrict__ pop_pos,
                                            u64 *__restrict__ digest, u64 *__restrict__ round_out,
                                            int32_t *__restrict__ ids, int64_t ids_cap, u64 *s_dg,
-                                           const uint32_t *__restrict__ rcnt, u64 *__restrict__ pcount) {
+                                           const uint32_t *__restrict__ rcnt, u64 *__restrict__ pcount,
+                                           int skip_below = -1) {
   constexpr int SPL = 16;  // slots per lane per pass: one wave covers 1024 slots with one load latency
   const u64 *img = (d.use_k ? K : masks) + d.mask_off;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1216,6 +1235,7 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
   const int rb = min(d.last + 1, ra + RPB);
   const int64_t pbase = pop_pos ? pop_pos[d.out] : 0;
   for (int r = ra + wid; r < rb; r += NWAVE) {
+    if (r < skip_below) continue;  // wave-uniform (round_out mode: nothing to add up)
     const u64 mw = lane < WS ? img[(int64_t)r * WS + lane] : 0ULL;  // lane w holds mask word w
     u64 pos;
     if (rcnt) {  // the sweep's per-round counts: position = pos0 + counts of rounds first..r-1
@@ -1291,11 +1311,18 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
                                                  u64 *__restrict__ digest, u64 *__restrict__ round_out,
                                                  int32_t *__restrict__ ids, int64_t ids_cap,
                                                  const int64_t *__restrict__ item_pref, const int *__restrict__ ctl,
-                                                 const uint32_t *__restrict__ rcnt, u64 *__restrict__ pcount) {
+                                                 const uint32_t *__restrict__ rcnt, u64 *__restrict__ pcount,
+                                                 const int *__restrict__ skip_below) {
   __shared__ u64 s_dg;
   if (!item_pref) {
-    emit_block<WS, NT, RPB>(g, slot_off, slot_src, pd ? pd[blockIdx.y] : d1, blockIdx.x, masks, K, rbase, pop_pos,
-                            digest, round_out, ids, ids_cap, &s_dg, nullptr, nullptr);
+    const PopDesc d = pd ? pd[blockIdx.y] : d1;
+    int lo = -1;
+    if (skip_below) {  // per-round outputs of rounds >= *skip_below only (incremental canon)
+      lo = *skip_below;
+      if (d.first + ((int)blockIdx.x + 1) * RPB <= lo) return;
+    }
+    emit_block<WS, NT, RPB>(g, slot_off, slot_src, d, blockIdx.x, masks, K, rbase, pop_pos, digest, round_out, ids,
+                            ids_cap, &s_dg, nullptr, nullptr, lo);
     return;
   }
   // item_pref[nd] = item count; item_pref[nd + 1 + it] = the segment owning item it

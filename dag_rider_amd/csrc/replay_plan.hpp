@@ -302,6 +302,21 @@ __global__ __launch_bounds__(NT) void k_plan_emit(const int32_t *__restrict__ po
     for (int64_t it = item_pref[i]; it < item_pref[i + 1]; it++) item_pref[nd + 1 + it] = i;
 }
 
+// orderVertices planned on the device (dr_order_vertices, REF mode): per-pop
+// count and digest = the canonical prefix terms + the pop's own rounds.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pop_final(const int32_t *__restrict__ plan,
+                                                  const int32_t *__restrict__ desc_of_pop,
+                                                  const u64 *__restrict__ extra_c, const u64 *__restrict__ extra_g,
+                                                  const u64 *__restrict__ counts, const u64 *__restrict__ digest,
+                                                  u64 *__restrict__ out_count, u64 *__restrict__ out_digest) {
+  const int64_t np = plan[PL_NPUSH];
+  for (int64_t p = (int64_t)blockIdx.x * NT + threadIdx.x; p < np; p += (int64_t)gridDim.x * NT) {
+    out_count[p] = extra_c[p] + (desc_of_pop[p] >= 0 ? counts[p] : 0);
+    out_digest[p] = extra_g[p] + digest[p];
+  }
+}
+
 // Outputs -> pinned host memory (h_*, every workgroup a share), totals -> hdr (workgroup 0).
 template <int NT>
 __global__ __launch_bounds__(NT) void k_plan_final(int nw, const uint8_t *__restrict__ commit,

@@ -86,6 +86,9 @@ def _check(engines, cur, n, faulty, rng, nq=40):
             ids, cnt, dg = e.order_vertices(stack, top, mode)
             assert ids.tolist() == want.tolist()
             assert cnt.tolist() == wc.tolist() and dg.tolist() == wd.tolist()
+            # counts + digests only: REF mode takes the device-planned path on fresh summaries
+            _, cnt, dg = e.order_vertices(stack, top, mode, cap=0)
+            assert cnt.tolist() == wc.tolist() and dg.tolist() == wd.tolist()
 
 
 @pytest.mark.gpu
@@ -173,3 +176,35 @@ def test_gpu_append_vertices_ghost_and_round0(gpu_device):
                 ids, cnt, dg = e.order_vertices(stack, 2, mode)
                 rc, want, wc, wd = ld.order_vertices(stack, 2, mode)
                 assert ids.tolist() == want.tolist() and dg.tolist() == wd.tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name", ["c2", "c4-small"])
+def test_gpu_wave_loop_matches_replay(gpu_device, cfg_name):
+    """The drop-in loop (append 4 rounds -> waveReady -> orderVertices, counts and
+    digests) equals one full dr_replay on every wave: the canonical cone is
+    rebuilt incrementally between calls (only rounds from the lowest changed one
+    are re-emitted) and pops are planned on the device."""
+    from dag_rider_amd.gen import CONFIGS, GenConfig, generate
+
+    cfg = CONFIGS["c2"] if cfg_name == "c2" else GenConfig("c4-small", 1024, 240, 4, 1.0, 0.02, 0.5, 4, 0.0)
+    d = generate(cfg, nthreads=8)
+    nw = (d.nrounds - 1) // 4
+    with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
+        e.append_packed(d, 0, 1)
+        decided, commit, pushes, pc, pdg = 0, [], [], [], []
+        for w in range(1, nw + 1):
+            e.append_packed(d, 4 * w - 3, 4 * w + 1)
+            cm, vc, pushed = e.wave_ready(w, decided)
+            commit.append(cm)
+            if cm:
+                pushes += pushed
+                _, cnt, dg = e.order_vertices([(4 * (x - 1) + 1, e.wave_leader(x)) for x in pushed], 4 * w,
+                                              L.DR_DELIVER_REF, cap=0)
+                pc += cnt.tolist()
+                pdg += dg.tolist()
+                decided = w
+        ref = e.replay(nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+    assert commit == ref.commit.astype(bool).tolist()
+    assert pushes == ref.push_wave.tolist()
+    assert pc == ref.pop_count.tolist() and pdg == ref.pop_digest.tolist()
