@@ -22,6 +22,7 @@ DR_OPT_DEVICE_PLAN = 2
 DR_OPT_PHASE_TIMING = 3
 DR_LEADER_CONST1, DR_LEADER_SEEDED, DR_LEADER_TABLE = 0, 1, 2
 DR_SHARD_ID_BYTES = 128
+DR_SHARD_OPT_PERSISTENT = 1
 
 P = C.c_void_p
 i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float
@@ -79,6 +80,12 @@ SIGNATURES = {
     "dr_shard_reach_sets": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dr_shard_path_batch": (C.c_int, [P, C.c_int, P, P, C.c_int, P]),
     "dr_shard_stats": (C.c_int, [P, C.POINTER(f32), C.POINTER(u64), C.POINTER(u64)]),
+    "dr_shard_set_option": (C.c_int, [P, C.c_int, C.c_int]),
+    "dr_shard_set_leader_coin": (C.c_int, [P, C.c_int, C.c_uint64, C.c_int, P]),
+    "dr_shard_wave_commit": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "dr_shard_wave_ready": (C.c_int, [P, C.c_int, C.c_int, P, P, P, C.c_int, C.POINTER(C.c_int)]),
+    "dr_shard_order_vertices": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t), P, P]),
+    "dr_shard_replay": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
     # include/dagrider_wire.h
     "dr_wire_check": (C.c_int, [P, C.c_size_t, C.POINTER(i32), C.POINTER(i32)]),
     "dr_wire_append": (C.c_int, [P, P, C.c_size_t]),

@@ -170,9 +170,19 @@ struct dr_ctx {
     }
     return hipSuccess;
   }
+  // H2D segments staged while defer_h2d is set: one k_copy launch for all of them
+  // (an append stages ~a dozen small arrays) at flush_h2d() or the next sync()
+  bool defer_h2d = false;
+  std::vector<dr::CopySeg> h2q;
+  hipError_t flush_h2d() {
+    if (h2q.empty()) return hipSuccess;
+    hipError_t e = launch_copies(h2q.data(), (int)h2q.size());
+    h2q.clear();
+    return e;
+  }
   hipError_t sync() {
-    hipError_t e = hipSuccess;
-    if (!pend.empty()) {
+    hipError_t e = flush_h2d();
+    if (e == hipSuccess && !pend.empty()) {
       std::vector<dr::CopySeg> small;
       for (auto &p : pend) {
         if (p.n >= ((size_t)1 << 22))  // bulk: DMA engine
@@ -233,6 +243,10 @@ struct dr_ctx {
     std::memcpy(p, host, n);
     if (n >= ((size_t)1 << 22)) return hipMemcpyAsync(dev, p, n, hipMemcpyHostToDevice, stream);
     const dr::CopySeg sg{static_cast<const uint8_t *>(p), static_cast<uint8_t *>(dev), n};
+    if (defer_h2d) {
+      h2q.push_back(sg);
+      return hipSuccess;
+    }
     return launch_copies(&sg, 1);
   }
   std::string err;
@@ -363,6 +377,17 @@ struct dr_ctx {
   } while (0)
 
 namespace {
+
+// Scope in which dr_ctx::h2d stages instead of launching; the staged copies go
+// out in one launch at the scope's sync() (or here, on an early error return).
+struct DeferH2D {
+  dr_ctx *c;
+  explicit DeferH2D(dr_ctx *cc) : c(cc) { c->defer_h2d = true; }
+  ~DeferH2D() {
+    c->defer_h2d = false;
+    (void)c->flush_h2d();
+  }
+};
 
 template <int WS>
 constexpr int block_for() {
@@ -801,6 +826,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   const size_t nfar = built.nfar;
   const int dmax = built.dmax;
   // ---- commit: rows and per-vertex degrees, then the flattened per-round arrays ----
+  DeferH2D batch(c);  // every staged copy below goes out in one launch at sync()
   const size_t row_words = (size_t)n * WS;
   if (WS == W && (size_t)k * row_words * 8 <= ((size_t)16 << 20)) {  // per-round appends: pinned staging
     HIPCHK(c, c->h2d(c->strong.as<u64>() + (size_t)r0 * row_words, strong, (size_t)k * row_words * 8));
@@ -874,6 +900,7 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
     }
   }
   // pass 2: apply
+  DeferH2D batch(c);
   if (R > R0) {  // opened rounds start empty: zero rows and degrees
     const size_t a = (size_t)R0 * n, b = (size_t)R * n;
     HIPCHK(c, hipMemsetAsync(c->strong.as<u64>() + a * WS, 0, (b - a) * WS * 8, c->stream));
@@ -932,6 +959,7 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
     HIPCHK(c, c->h2d(b + o_idx, vidx.data(), (size_t)nv * 4));
     HIPCHK(c, c->h2d(b + o_sd, sd.data(), (size_t)nv * 2));
     HIPCHK(c, c->h2d(b + o_wd, wd.data(), (size_t)nv * 2));
+    HIPCHK(c, c->flush_h2d());  // k_put_vertices reads them
     const int blocks = (int)std::min<int64_t>(1024, ((int64_t)nv * WS + 255) / 256);
     hipLaunchKernelGGL(k_put_vertices, dim3(blocks), dim3(256), 0, c->stream, reinterpret_cast<const u64 *>(b),
                        reinterpret_cast<const uint32_t *>(b + o_idx), reinterpret_cast<const uint16_t *>(b + o_sd),

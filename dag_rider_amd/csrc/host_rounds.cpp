@@ -65,8 +65,12 @@ int build_one(const PackedRounds &in, int i, std::vector<int32_t> &tab, BuiltRou
     h.nweak += eb - ea;
     const uint64_t mybit = 1ULL << (s0 & 63);
     const int myword = s0 >> 6;
+    const uint32_t *wt = in.weak_tgt;
+    int32_t *tb = tab.data();
+    uint64_t *rows = h.wc_rows.data();  // re-read after a new column grows it
+    int dm = dmax;
     for (uint32_t e = ea; e < eb; e++) {
-      const uint32_t t = in.weak_tgt[e];
+      const uint32_t t = wt[e];
       const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
       if (ts >= n || tr > r - 2) {
         rc = ts >= n ? failf(err, DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): source > n", r, s0 + 1, tr, ts + 1)
@@ -77,20 +81,22 @@ int build_one(const PackedRounds &in, int i, std::vector<int32_t> &tab, BuiltRou
       const int delta = r - tr;
       if (delta <= 1023) {
         const size_t at = (size_t)delta * n + ts;
-        int32_t col = tab[at];
+        int32_t col = tb[at];
         if (col < 0) {
-          col = tab[at] = (int32_t)h.wc_key.size();
+          col = tb[at] = (int32_t)h.wc_key.size();
           touched.push_back((uint32_t)at);
           h.wc_key.push_back(((uint32_t)delta << 11) | (uint32_t)ts);
           h.wc_rows.resize(h.wc_rows.size() + WS, 0ULL);
+          rows = h.wc_rows.data();
         }
-        h.wc_rows[(size_t)col * WS + myword] |= mybit;
-        dmax = std::max(dmax, delta);
+        rows[(size_t)col * WS + myword] |= mybit;
+        dm = delta > dm ? delta : dm;
       } else {
         h.far.push_back(((uint64_t)s0 << 32) | t);
         nfar++;
       }
     }
+    dmax = dm;
   }
   for (uint32_t at : touched) tab[at] = -1;
   if (rc) return rc;

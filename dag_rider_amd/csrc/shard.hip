@@ -1,30 +1,56 @@
-// shard.hip -- process-column sharded reachability (include/dagrider_shard.h).
+// shard.hip -- process-column sharded reachability, commit and delivery
+// (include/dagrider_shard.h).
 //
 // for a DAG split across the GPUs of one node, GPU g keeps the
 // target columns [g*C, (g+1)*C) of every strong row and the weak edges whose
-// target falls there.  A batch of up to 64 queries sweeps the rounds top-down;
-// the frontier of a round is held TRANSPOSED: FT[s] = u64 mask of the queries
-// that reached source s (so one all-gather of C words per shard per round moves
-// the frontier of all 64 queries).  Per round, one launch of k_shard_round:
+// target falls there; every GPU also keeps the small per-vertex metadata
+// (presence, slot order, strong/weak degrees), so each one can emit the
+// delivered sequences itself once it holds a full frontier.
+//
+// Sweeps (path(), the leader chain of waveReady, the cones of orderVertices).
+// A batch of up to 64 queries sweeps the rounds top-down; the frontier of a
+// round is held TRANSPOSED: FT[s] = u64 mask of the queries that reached source
+// s, so one all-gather of C words per shard per round moves the frontier of all
+// 64 queries.  Per round r:
 //
 //   1. write round r's reach rows (the ballot of bit b over 64 sources is query
 //      b's bitset word -- a 64x64 bit transpose per wave, shard 0 only);
-//   2. strong expansion into the pending frontier of r-1: each wave takes 64
+//   2. chain queries (process.go:341-350) at a leader round: when the wave's
+//      leader is present and in a chain's frontier, push that wave and restart
+//      the chain's frontier at the leader alone -- every shard takes the same
+//      decision from the same full FT_r;
+//   3. strong expansion into the pending frontier of r-1: each wave takes 64
 //      sources; for every (source with a non-empty mask) x (row word) it walks
 //      the active sources with a scalar loop (readlane) and lane j ORs the
 //      source's query mask when the row has target bit j: one atomic per target;
-//   3. weak expansion: the shard's weak edges of round r (sorted by (delta,
-//      target)) OR the source's mask into the pending frontier of r - delta
-//      (wave-uniform destinations collapse to one reduction + one atomic);
-//   4. the last workgroup of the shard (threadfence + counter) drains the
-//      pending frontier of r-1, adds queries that start there, and writes its
-//      columns of FT_{r-1}: straight into the shared frontier buffer (local
-//      mode) or into the send buffer of ncclAllGather (RCCL mode).
+//   4. weak expansion: the shard's weak edges of round r (sorted by (delta,
+//      target)) OR the source's mask into the pending frontier of r - delta;
+//   5. produce: drain the pending frontier of r-1, inject the queries that start
+//      there, publish the shard's columns of FT_{r-1}.
 //
-// Semantics are those of dr_reach_sets / dr_path_batch (process.go:89-148): the
-// reach set is defined over the id space (a dangling target counts as reached,
-// :123,136), an absent vertex has an all-zero row (no edges, :111-116), and the
-// start vertex is in its own set (self path, :91-93).
+// Local mode (all shards in one context, one device) runs a whole batch as ONE
+// cooperative launch (k_shard_sweep): steps 1-4, a grid barrier, step 5 spread
+// over every workgroup, a second barrier, next round -- no per-round launch.
+// RCCL mode launches k_shard_round per round (the last workgroup of the shard
+// produces into the send buffer) followed by ncclAllGather on the same stream.
+//
+// Commit (waveReady's vote, process.go:326-339) for many waves at once: three
+// steps S_k = {v in round 4w-3+k : row(v) & S_{k-1} != 0}; shard g tests its
+// columns of each row against its columns of S_{k-1} and writes a partial hit
+// bitset; the partials of all shards are OR-ed by the next step (RCCL mode: one
+// all-gather of [nwaves][W] words per step).  vcount = |S_3|.
+//
+// Delivery (orderVertices, process.go:404-443): one cone per distinct popped
+// leader (rows for rounds bottom..top), then on every GPU: paper-mode dedup (a
+// per-round scan over the leaders in pop order against the delivered set),
+// per-(leader, round) counts and edge sums, a per-leader scan for positions, and
+// the order-sensitive digest over the round's slots in insertion order.
+//
+// Semantics are those of dagrider_gpu.h (dr_reach_sets, dr_path_batch,
+// dr_wave_commit, dr_wave_ready, dr_order_vertices, dr_replay): the reach set
+// is defined over the id space (a dangling target counts as reached,
+// process.go:123,136), an absent vertex has an all-zero row (no edges,
+// :111-116), and the start vertex is in its own set (self path, :91-93).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -32,17 +58,20 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
 #include "dagrider_gpu.h"
 #include "dagrider_shard.h"
+#include "wave_ops.hpp"
 
 namespace {
 
-typedef unsigned long long u64;
+using dr::u64;
 constexpr int SH_NT = 256;  // threads per workgroup (4 waves)
 constexpr int SH_BATCH = 64;
+enum : int32_t { QF_CHAIN = 1 };
 
 thread_local std::string g_shard_err;
 
@@ -59,6 +88,23 @@ struct SBuf {
     if (e == hipSuccess) cap = c;
     return e;
   }
+  // grow keeping the first `keep` bytes
+  hipError_t grow(size_t bytes, size_t keep, hipStream_t s) {
+    if (bytes <= cap) return hipSuccess;
+    const size_t c = std::max<size_t>({bytes, cap * 2, 4096});
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, c);
+    if (e != hipSuccess) return e;
+    if (p && keep) {
+      e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) { (void)hipFree(q); return e; }
+    }
+    if (p) (void)hipFree(p);
+    p = q;
+    cap = c;
+    return hipSuccess;
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -68,21 +114,31 @@ struct SBuf {
 };
 
 struct QInfo {
-  int32_t top, bottom, src0, pad;  // src0 = 0-based source of `from`, -1 none
-  int64_t obase;                   // word offset of round `bottom` in the batch output
+  int32_t top, bottom, src0, flags;  // src0 = 0-based source of `from`, -1 none; flags QF_*
+  int64_t obase;                     // word offset of round `bottom` in the batch output
+  int32_t push_base;                 // QF_CHAIN: first slot of the query's push list
+  int32_t last;                      // pops: last emitted round, min(p.round, top)
 };
 
 struct ShardArgs {
   const u64 *strong;        // [nlocal][max_rounds][n][WSs]
   const uint32_t *weak;     // per local shard: edges (target col 0-10, source 11-21, delta 22-31)
   const uint64_t *woff;     // [nlocal][max_rounds+1] edge offsets (absolute in weak)
-  const u64 *ft;            // FT_r: [G*C] query masks
-  u64 *ftn;                 // FT_{r-1} destination: full buffer (local) or send buffer (RCCL)
+  const u64 *pres;          // [max_rounds][W] presence (chain restarts)
+  const uint16_t *lead;     // [nlead] chooseLeader(w), 1-based source
+  const uint16_t *sdeg;     // [max_rounds][n] strong degree of the whole row (chain edges)
+  u64 *ftb0, *ftb1;         // FT_r for even / odd r: [G*C] query masks (full width)
+  u64 *send;                // RCCL mode: this shard's columns of FT_{r-1}
   u64 *pend;                // [nlocal][depth][C]
-  unsigned *cnt;            // [nlocal] workgroups done this round
+  unsigned *cnt;            // [nlocal] workgroups done this round (k_shard_round)
+  unsigned *bar;            // grid barrier counter (k_shard_sweep)
+  int32_t *err;             // grid barrier timeout flag
   u64 *out;                 // batch reach rows
   const QInfo *q;           // [nq]
-  int32_t n, W, WSs, C, depth, shard0, local, max_rounds, nq, strong_only;
+  int32_t *push_out;        // chain pushes (waves), query b's list at q[b].push_base
+  int32_t *push_n;          // [64] pushes per chain query
+  u64 *cedges;              // [64] chain edges per query
+  int32_t n, W, WSs, C, depth, shard0, nlocal, local, max_rounds, nq, strong_only, nlead;
   int64_t strong_shard_stride;  // words per local shard of strong
 };
 
@@ -90,42 +146,70 @@ __device__ __forceinline__ u64 shfl_xor64(u64 v, int m) {
   const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
   return ((u64)(uint32_t)hi << 32) | (uint32_t)lo;
 }
-__device__ __forceinline__ u64 rdlane64(u64 x, int l) {
-  return ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
-         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+
+// per-round query masks, one query per lane (wave-uniform results)
+struct RMasks { u64 exp, out, inj, chk; };
+__device__ __forceinline__ RMasks round_masks(const QInfo *q, int nq, int r, int lane) {
+  bool e = false, o = false, i = false, k = false;
+  if (lane < nq) {
+    const QInfo x = q[lane];
+    const bool chain = (x.flags & QF_CHAIN) != 0;
+    e = x.bottom < r && r <= x.top;             // expand round r
+    o = !chain && x.bottom <= r && r <= x.top;  // write round r's reach row
+    i = x.top == r - 1;                         // starts at r-1
+    k = chain && x.bottom <= r && r < x.top;    // leader test at r (chain)
+  }
+  return RMasks{__ballot(e), __ballot(o), __ballot(i), __ballot(k)};
 }
 
-// round r of a batch sweep; see the file comment for the four steps.
-__global__ void __launch_bounds__(SH_NT) k_shard_round(ShardArgs a, int r, u64 expmask, u64 outmask, u64 injmask,
-                                                        int produce) {
-  const int l = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const int nwv = gridDim.x * (SH_NT / 64);
-  const int gw = blockIdx.x * (SH_NT / 64) + (threadIdx.x >> 6);
+// Steps 1-4 of round r for local shard l (see the file comment).  ft = full FT_r.
+// ledges: LDS chain-edge accumulators; writer: the one thread that records pushes.
+__device__ void sweep_round(const ShardArgs &a, const u64 *ft, int r, int l, int gw, int nwv, int lane,
+                            const RMasks &m, u64 chainq, u64 *ledges, bool writer) {
   const int C = a.C;
   u64 *pend = a.pend + (size_t)l * a.depth * C;
-
-  // 1 + 2: reach rows of round r and strong expansion into round r-1.  A wave's
-  // work item is (64-source chunk, target word): nchunks * WSs items spread over
-  // every wave of the grid; the chunk's first word also writes the reach rows.
+  // 2: chain restarts (every thread takes the same decision)
+  u64 rst = 0;
+  int L = -1;
+  if (m.chk && ((r - 1) & 3) == 0) {
+    const int w2 = ((r - 1) >> 2) + 1;
+    L = (w2 < a.nlead ? (int)a.lead[w2] : 1) - 1;
+    if ((a.pres[(size_t)r * a.W + (L >> 6)] >> (L & 63)) & 1ULL) rst = dr::ld_agent(&ft[L]) & m.chk;
+    if (writer)
+      for (u64 x = rst; x; x &= x - 1) {
+        const int b = __builtin_ctzll(x);
+        a.push_out[a.q[b].push_base + a.push_n[b]] = w2;
+        a.push_n[b] += 1;
+      }
+  }
+  // 1 + 3: reach rows and strong expansion.  A wave's work item is (64-source
+  // chunk, target word): nchunks * WSs items spread over every wave of the grid.
   const int nchunks = (a.n + 63) >> 6;
   for (int it = gw; it < nchunks * a.WSs; it += nwv) {
     const int s0 = (it / a.WSs) * 64, tw = it % a.WSs;
     const int s = s0 + lane;
-    const u64 m = s < a.n ? a.ft[s] : 0ULL;
-    if (l == 0 && tw == 0 && outmask) {
-      u64 mine = 0;
-      for (u64 om = outmask; om; om &= om - 1) {
-        const int b = __builtin_ctzll(om);
-        const u64 word = __ballot((m >> b) & 1ULL);
-        if (lane == b) mine = word;
+    u64 mv = s < a.n ? dr::ld_agent(&ft[s]) : 0ULL;
+    if (s != L) mv &= ~rst;
+    if (l == 0 && tw == 0) {
+      if (m.out) {
+        u64 mine = 0;
+        for (u64 om = m.out; om; om &= om - 1) {
+          const int b = __builtin_ctzll(om);
+          const u64 word = __ballot((mv >> b) & 1ULL);
+          if (lane == b) mine = word;
+        }
+        if ((m.out >> lane) & 1ULL) {
+          const QInfo qi = a.q[lane];
+          a.out[qi.obase + (int64_t)(r - qi.bottom) * a.W + (s0 >> 6)] = mine;
+        }
       }
-      if ((outmask >> lane) & 1ULL) {
-        const QInfo qi = a.q[lane];
-        a.out[qi.obase + (int64_t)(r - qi.bottom) * a.W + (s0 >> 6)] = mine;
+      const u64 ce = mv & m.exp & chainq;
+      if (ce && ledges) {
+        const u64 d = a.sdeg[(size_t)r * a.n + s];
+        for (u64 x = ce; x; x &= x - 1) atomicAdd(&ledges[__builtin_ctzll(x)], d);
       }
     }
-    const u64 me = m & expmask;
+    const u64 me = mv & m.exp;
     if (r < 1 || __ballot(me != 0ULL) == 0ULL) continue;
     const u64 row = (me != 0ULL)
                         ? a.strong[(size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.WSs + tw]
@@ -135,42 +219,139 @@ __global__ void __launch_bounds__(SH_NT) k_shard_round(ShardArgs a, int r, u64 e
     while (act) {  // wave-uniform loop over the sources that contribute
       const int src = __builtin_ctzll(act);
       act &= act - 1;
-      const u64 rs = rdlane64(row, src), ms = rdlane64(me, src);
+      const u64 rs = dr::readlane64(row, src), ms = dr::readlane64(me, src);
       if ((rs >> lane) & 1ULL) acc |= ms;
     }
     if (acc) atomicOr(&pend[(size_t)((r - 1) & (a.depth - 1)) * C + tw * 64 + lane], acc);
   }
-
-  // 3: weak expansion
+  // 4: weak expansion
   if (!a.strong_only && r >= 2) {
     const size_t e0 = a.woff[(size_t)l * (a.max_rounds + 1) + r], e1 = a.woff[(size_t)l * (a.max_rounds + 1) + r + 1];
     for (size_t base = e0 + (size_t)gw * 64; base < e1; base += (size_t)nwv * 64) {
       const size_t e = base + lane;
-      u64 m = 0;
+      u64 mv = 0;
       uint32_t key = 0xFFFFFFFFu;
       if (e < e1) {
         const uint32_t w = a.weak[e];
-        m = a.ft[(w >> 11) & 2047u] & expmask;
+        const int src = (int)((w >> 11) & 2047u);
+        mv = dr::ld_agent(&ft[src]) & m.exp;
+        if (src != L) mv &= ~rst;
         const int slot = (r - (int)(w >> 22)) & (a.depth - 1);
         key = (uint32_t)slot * (uint32_t)C + (w & 2047u);
       }
-      const u64 act = __ballot(m != 0ULL);
+      const u64 act = __ballot(mv != 0ULL);
       if (!act) continue;
       const int first = __builtin_ctzll(act);
       const uint32_t kf = (uint32_t)__builtin_amdgcn_readlane((int)key, first);
-      if (__ballot(m != 0ULL && key != kf) == 0ULL) {
-        u64 v = m;
+      if (__ballot(mv != 0ULL && key != kf) == 0ULL) {
+        u64 v = mv;
         for (int d = 32; d; d >>= 1) v |= shfl_xor64(v, d);
         if (lane == first) atomicOr(&pend[kf], v);
-      } else if (m) {
-        atomicOr(&pend[key], m);
+      } else if (mv) {
+        atomicOr(&pend[key], mv);
       }
     }
   }
+}
 
-  // 4: the last workgroup of this shard produces its columns of FT_{r-1}
-  if (!produce) return;
+// step 5 for column t of local shard l: FT_{r1}[col] = pending | starts
+__device__ __forceinline__ u64 produce_col(const ShardArgs &a, const QInfo *q, int l, int t, int r1, u64 inj) {
+  u64 *slotp = a.pend + ((size_t)l * a.depth + (size_t)(r1 & (a.depth - 1))) * a.C;
+  u64 v = atomicExch(&slotp[t], 0ULL);
+  const int col = (a.shard0 + l) * a.C + t;
+  for (u64 im = inj; im; im &= im - 1) {
+    const int b = __builtin_ctzll(im);
+    if (q[b].src0 == col) v |= 1ULL << b;
+  }
+  return v;
+}
+
+// Grid-wide barrier of a cooperative launch: monotone arrival counter.  The
+// wait is bounded (2 s of the 100 MHz real-time clock) and sticky: a timed-out
+// barrier sets *err, every other waiter sees it and the kernel ends instead of
+// hanging (the host reports DR_E_HIP).  Returns false once *err is set.
+__device__ __forceinline__ bool grid_sync(unsigned *bar, unsigned nblk, unsigned &target, int32_t *err) {
+  __shared__ int bad;
+  __syncthreads();
+  target += nblk;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    atomicAdd(bar, 1u);
+    const unsigned long long t0 = wall_clock64();
+    int e = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { e = 1; break; }
+      if (wall_clock64() - t0 > 200000000ULL) {
+        atomicOr(err, 1);
+        e = 1;
+        break;
+      }
+    }
+    __threadfence();
+    bad = e;
+  }
+  __syncthreads();
+  return !bad;
+}
+
+__device__ __forceinline__ void load_queries(const ShardArgs &a, QInfo *qs, u64 *ledges) {
+  if ((int)threadIdx.x < a.nq) qs[threadIdx.x] = a.q[threadIdx.x];
+  if (threadIdx.x < SH_BATCH) ledges[threadIdx.x] = 0;
+  __syncthreads();
+}
+__device__ __forceinline__ void flush_edges(const ShardArgs &a, const u64 *ledges) {
+  __syncthreads();
+  if ((int)threadIdx.x < a.nq && ledges[threadIdx.x]) atomicAdd(&a.cedges[threadIdx.x], ledges[threadIdx.x]);
+}
+
+// Local mode: a whole batch, rounds T..Bm, in one cooperative launch.
+__global__ void __launch_bounds__(SH_NT) k_shard_sweep(ShardArgs a, int T, int Bm) {
+  __shared__ QInfo qs[SH_BATCH];
+  __shared__ u64 ledges[SH_BATCH];
+  load_queries(a, qs, ledges);
+  const int lane = threadIdx.x & 63;
+  const u64 chainq = __ballot(lane < a.nq && (qs[lane].flags & QF_CHAIN));
+  const int l = blockIdx.y;
+  const int nwv = gridDim.x * (SH_NT / 64);
+  const int gw = blockIdx.x * (SH_NT / 64) + (threadIdx.x >> 6);
+  const unsigned nblk = gridDim.x * gridDim.y;
+  const int gthreads = (int)nblk * SH_NT;
+  const int gtid = (int)(blockIdx.y * gridDim.x + blockIdx.x) * SH_NT + (int)threadIdx.x;
+  const bool writer = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+  unsigned target = 0;
+  for (int r = T; r >= Bm; r--) {
+    const RMasks m = round_masks(qs, a.nq, r, lane);
+    sweep_round(a, (r & 1) ? a.ftb1 : a.ftb0, r, l, gw, nwv, lane, m, chainq, ledges, writer);
+    if (r - 1 < Bm) break;
+    if (!grid_sync(a.bar, nblk, target, a.err)) break;
+    u64 *ftn = ((r - 1) & 1) ? a.ftb1 : a.ftb0;
+    for (int t = gtid; t < a.nlocal * a.C; t += gthreads) {
+      const int ll = t / a.C, tc = t - ll * a.C;
+      ftn[(size_t)(a.shard0 + ll) * a.C + tc] = produce_col(a, qs, ll, tc, r - 1, m.inj);
+    }
+    if (!grid_sync(a.bar, nblk, target, a.err)) break;
+  }
+  flush_edges(a, ledges);
+}
+
+// One round per launch (RCCL mode, or local mode without cooperative launch):
+// the last workgroup of each shard produces its columns of FT_{r-1}.
+__global__ void __launch_bounds__(SH_NT) k_shard_round(ShardArgs a, int r, int produce) {
+  __shared__ QInfo qs[SH_BATCH];
+  __shared__ u64 ledges[SH_BATCH];
   __shared__ int last;
+  load_queries(a, qs, ledges);
+  const int lane = threadIdx.x & 63;
+  const u64 chainq = __ballot(lane < a.nq && (qs[lane].flags & QF_CHAIN));
+  const int l = blockIdx.y;
+  const int nwv = gridDim.x * (SH_NT / 64);
+  const int gw = blockIdx.x * (SH_NT / 64) + (threadIdx.x >> 6);
+  const RMasks m = round_masks(qs, a.nq, r, lane);
+  const bool writer = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+  sweep_round(a, (r & 1) ? a.ftb1 : a.ftb0, r, l, gw, nwv, lane, m, chainq, ledges, writer);
+  flush_edges(a, ledges);
+  if (!produce) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
@@ -179,18 +360,168 @@ __global__ void __launch_bounds__(SH_NT) k_shard_round(ShardArgs a, int r, u64 e
   __syncthreads();
   if (!last) return;
   __threadfence();
-  const int g = a.shard0 + l;
-  u64 *slotp = pend + (size_t)((r - 1) & (a.depth - 1)) * C;
-  for (int t = threadIdx.x; t < C; t += SH_NT) {
-    u64 v = atomicExch(&slotp[t], 0ULL);
-    const int col = g * C + t;
-    for (u64 im = injmask; im; im &= im - 1) {
-      const int b = __builtin_ctzll(im);
-      if (a.q[b].src0 == col) v |= 1ULL << b;
-    }
-    a.ftn[(a.local ? (size_t)g * C : 0) + t] = v;
+  u64 *ftn = ((r - 1) & 1) ? a.ftb1 : a.ftb0;
+  for (int t = threadIdx.x; t < a.C; t += SH_NT) {
+    const u64 v = produce_col(a, qs, l, t, r - 1, m.inj);
+    if (a.local) ftn[(size_t)(a.shard0 + l) * a.C + t] = v;
+    else a.send[t] = v;
   }
   if (threadIdx.x == 0) a.cnt[l] = 0;
+}
+
+// Commit step k (1..3) of waves w0..w0+nw-1: partial hits of shard g,
+// P[g][wi][word] bit s <=> row_g(4w-3+k, s) & S_{k-1}[cols of g] != 0.
+// S_0 = S0 (leader bits, [nw][W]); S_{k-1} = OR over the G partials of Pin.
+__global__ void __launch_bounds__(SH_NT) k_shard_vote(ShardArgs a, int w0, int nw, int k, int G, const u64 *S0,
+                                                      const u64 *Pin, u64 *Pout) {
+  __shared__ u64 S[64];
+  const int l = blockIdx.y, g = a.shard0 + l;
+  const int bpw = (a.n + SH_NT - 1) / SH_NT;
+  const int wi = blockIdx.x / bpw, sb = blockIdx.x % bpw;
+  if (wi >= nw) return;
+  const int r = 4 * (w0 + wi - 1) + 1 + k;
+  if ((int)threadIdx.x < a.WSs) {
+    const int cw = g * a.WSs + (int)threadIdx.x;
+    u64 v = 0;
+    if (cw < a.W) {
+      if (k == 1) v = S0[(size_t)wi * a.W + cw];
+      else
+        for (int gg = 0; gg < G; gg++) v |= Pin[((size_t)gg * nw + wi) * a.W + cw];
+    }
+    S[threadIdx.x] = v;
+  }
+  __syncthreads();
+  const int s = sb * SH_NT + (int)threadIdx.x;
+  bool hit = false;
+  if (s < a.n) {
+    const u64 *row = a.strong + (size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.WSs;
+    for (int j = 0; j < a.WSs; j++) hit |= (row[j] & S[j]) != 0ULL;
+  }
+  const u64 b = __ballot(hit);
+  if ((threadIdx.x & 63) == 0 && s < a.n)
+    Pout[((size_t)(a.local ? g : 0) * nw + wi) * a.W + (s >> 6)] = b;
+}
+
+__global__ void k_shard_vcount(const u64 *P, int G, int nw, int W, int32_t *vc) {
+  const int wi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (wi >= nw) return;
+  int c = 0;
+  for (int w = 0; w < W; w++) {
+    u64 v = 0;
+    for (int g = 0; g < G; g++) v |= P[((size_t)g * nw + wi) * W + w];
+    c += __popcll(v);
+  }
+  vc[wi] = c;
+}
+
+// Delivery masks, one wave per round r (lane = word): X = reach & present, and
+// in paper mode & ~delivered, the leaders scanned in pop order (Alg. 3 line 54).
+__global__ void __launch_bounds__(SH_NT) k_shard_dmask(u64 *out, const QInfo *q, int nq, int rmax, int W,
+                                                       const u64 *pres, u64 *D, int paper) {
+  const int r = 1 + (int)(blockIdx.x * (SH_NT / 64) + (threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  if (r > rmax || lane >= W) return;
+  const u64 pw = pres[(size_t)r * W + lane];
+  u64 Dw = paper ? D[(size_t)r * W + lane] : 0ULL;
+  for (int b = 0; b < nq; b++) {
+    const QInfo x = q[b];
+    if (r < x.bottom || r > x.last) continue;
+    u64 *p = &out[x.obase + (int64_t)(r - x.bottom) * W + lane];
+    const u64 v = *p & pw & ~Dw;  // Dw stays 0 in ref mode
+    if (paper) Dw |= v;
+    *p = v;
+  }
+  if (paper) D[(size_t)r * W + lane] = Dw;
+}
+
+// Per (query, round): delivered count and the strong + weak degree sum
+// (rdeg[r] for a round delivered whole).  cnt: [nq][rstride].
+__global__ void __launch_bounds__(SH_NT) k_shard_count(const u64 *out, const QInfo *q, int W, int n, int rstride,
+                                                       const u64 *pres, const uint16_t *sdeg, const uint16_t *wdeg,
+                                                       const u64 *rdeg, uint32_t *cnt, u64 *qedges) {
+  const int b = blockIdx.y;
+  const int r = 1 + (int)(blockIdx.x * (SH_NT / 64) + (threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const QInfo x = q[b];
+  if (r > x.last || r < x.bottom) return;
+  const u64 v = lane < W ? out[x.obase + (int64_t)(r - x.bottom) * W + lane] : 0ULL;
+  const u64 pw = lane < W ? pres[(size_t)r * W + lane] : 0ULL;
+  const uint32_t c = (uint32_t)dr::wave_sum((u64)__popcll(v));
+  u64 e;
+  if (__ballot(v != pw) == 0ULL) {
+    e = rdeg[r];
+  } else {
+    u64 acc = 0;
+    for (u64 y = v; y; y &= y - 1) {
+      const size_t at = (size_t)r * n + lane * 64 + __builtin_ctzll(y);
+      acc += (u64)sdeg[at] + wdeg[at];
+    }
+    e = dr::wave_sum(acc);
+  }
+  if (lane == 0) {
+    cnt[(size_t)b * rstride + r] = c;
+    if (e) atomicAdd(&qedges[b], e);
+  }
+}
+
+// Per query: exclusive scan of the per-round counts -> positions; total count.
+__global__ void __launch_bounds__(SH_NT) k_shard_scan(const QInfo *q, int rstride, uint32_t *cnt, u64 *qcount) {
+  __shared__ u64 part[SH_NT];
+  const int b = blockIdx.x;
+  const QInfo x = q[b];
+  const int lo = std::max(1, x.bottom), hi = x.last;  // rounds lo..hi
+  uint32_t *c = cnt + (size_t)b * rstride;
+  const int span = hi >= lo ? hi - lo + 1 : 0;
+  const int per = (span + SH_NT - 1) / SH_NT;
+  const int a0 = lo + (int)threadIdx.x * per, a1 = std::min(hi + 1, a0 + per);
+  u64 s = 0;
+  for (int r = a0; r < a1; r++) s += c[r];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 run = 0;
+    for (int t = 0; t < SH_NT; t++) {
+      const u64 v = part[t];
+      part[t] = run;
+      run += v;
+    }
+    qcount[b] = run;
+  }
+  __syncthreads();
+  u64 run = part[threadIdx.x];
+  for (int r = a0; r < a1; r++) {  // counts -> exclusive positions, in place (u32: < 2^32 per pop)
+    const uint32_t v = c[r];
+    c[r] = (uint32_t)run;
+    run += v;
+  }
+}
+
+// Per (query, round): sum of digest_term(r, s, k) over the delivered slots of
+// round r in insertion order, k = the query's position.
+__global__ void __launch_bounds__(SH_NT) k_shard_digest(const u64 *out, const QInfo *q, int W, int rstride,
+                                                        const uint32_t *pos, const uint32_t *slot_off,
+                                                        const uint16_t *slot_src, u64 *qdigest) {
+  const int b = blockIdx.y;
+  const int r = 1 + (int)(blockIdx.x * (SH_NT / 64) + (threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const QInfo x = q[b];
+  if (r > x.last || r < x.bottom) return;
+  const u64 xw = lane < W ? out[x.obase + (int64_t)(r - x.bottom) * W + lane] : 0ULL;
+  u64 k = pos[(size_t)b * rstride + r];
+  u64 acc = 0;
+  const uint32_t s0 = slot_off[r], s1 = slot_off[r + 1];
+  for (uint32_t base = s0; base < s1; base += 64) {
+    const uint32_t sl = base + lane;
+    const int s = sl < s1 ? (int)slot_src[sl] : 0;
+    const int wd = s > 0 ? (s - 1) >> 6 : 0;
+    const u64 word = ((u64)(uint32_t)__shfl((int)(xw >> 32), wd, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)xw, wd, 64);
+    const bool in = s > 0 && ((word >> ((s - 1) & 63)) & 1ULL);
+    const u64 bal = __ballot(in);
+    if (in) acc += dr::digest_term((uint32_t)r, (uint32_t)s, k + (u64)__popcll(bal & ((1ULL << lane) - 1ULL)));
+    k += (u64)__popcll(bal);
+  }
+  const u64 t = dr::wave_sum(acc);
+  if (lane == 0 && t) atomicAdd(&qdigest[b], t);
 }
 
 }  // namespace
@@ -198,17 +529,27 @@ __global__ void __launch_bounds__(SH_NT) k_shard_round(ShardArgs a, int r, u64 e
 struct dr_shard {
   int n = 0, f = 0, W = 0, G = 1, shard0 = 0, nlocal = 1, WSs = 1, C = 64, max_rounds = 0, dev = 0;
   bool local = true;
+  int persistent = 1;  // DR_SHARD_OPT_PERSISTENT
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   ncclComm_t comm = nullptr;
   SBuf strong, weak, woff, ft[2], send, pend, cnt, out, qinfo;
+  // per-vertex metadata, full width on every shard
+  SBuf pres, sdeg, wdeg, rdeg, slot_off, slot_src, lead;
+  // per-call scratch
+  SBuf bar, errf, push_out, push_n, cedges, vote_s0, vote_p[2], vote_send, vcount, D, pcnt, qcnt, qedges, qdig;
   std::vector<std::vector<uint32_t>> h_weak;  // per local shard
   std::vector<std::vector<uint64_t>> h_woff;  // per local shard, absolute offsets, size nrounds+1
+  std::vector<u64> h_pres;                    // [nrounds][W]
+  std::vector<uint64_t> h_deg;                // strong degree sum per round
+  std::vector<uint32_t> h_slot_off{0};
+  std::vector<uint16_t> h_lead;
   bool weak_dirty = false;
   float last_ms = 0;
   uint64_t last_rounds = 0, last_xbytes = 0;
+  float ms_vote = 0, ms_sweep = 0, ms_emit = 0;
   std::string err;
   int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -219,12 +560,22 @@ struct dr_shard {
     err = buf;
     return code;
   }
+  int lead_src(int w) const { return (w >= 0 && w < (int)h_lead.size()) ? h_lead[w] : 1; }
+  bool is_present(int r, int s /*1-based*/) const {
+    if (r < 0 || r >= nrounds || s < 1 || s > n) return false;
+    return (h_pres[(size_t)r * W + ((s - 1) >> 6)] >> ((s - 1) & 63)) & 1ULL;
+  }
 };
 
 #define SHCHK(c, x)                                                                                  \
   do {                                                                                               \
     hipError_t e_ = (x);                                                                             \
     if (e_ != hipSuccess) return (c)->fail(DR_E_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+#define SHNCCL(c, x)                                                                                 \
+  do {                                                                                               \
+    ncclResult_t r_ = (x);                                                                           \
+    if (r_ != ncclSuccess) return (c)->fail(DR_E_RCCL, "%s: %s", #x, ncclGetErrorString(r_));        \
   } while (0)
 
 namespace {
@@ -259,97 +610,349 @@ int sync_weak(dr_shard *c) {
   return DR_OK;
 }
 
-// one batch of <= 64 reach-set queries; rows land in host `out` at obase[i]
-int sweep_batch(dr_shard *c, const std::vector<QInfo> &qs, const std::vector<size_t> &hbase, int strong_only,
-                uint64_t *out) {
-  const int nq = (int)qs.size();
-  int T = 0, Bm = 1 << 30;
-  int64_t words = 0;
-  std::vector<QInfo> dq(qs);
-  for (int i = 0; i < nq; i++) {
-    T = std::max(T, qs[i].top);
-    Bm = std::min(Bm, qs[i].bottom);
-    dq[i].obase = words;
-    words += (int64_t)(qs[i].top - qs[i].bottom + 1) * c->W;
-  }
-  const int NT = c->G * c->C;
-  SHCHK(c, c->out.ensure(std::max<int64_t>(words, 1) * 8));
-  SHCHK(c, c->qinfo.ensure(SH_BATCH * sizeof(QInfo)));
-  SHCHK(c, hipMemcpyAsync(c->qinfo.p, dq.data(), nq * sizeof(QInfo), hipMemcpyHostToDevice, c->stream));
-  SHCHK(c, hipMemsetAsync(c->pend.p, 0, (size_t)c->nlocal * c->depth * c->C * 8, c->stream));
-  SHCHK(c, hipMemsetAsync(c->cnt.p, 0, (size_t)c->nlocal * 4, c->stream));
-  std::vector<u64> ft0(NT, 0);
-  for (int i = 0; i < nq; i++)
-    if (qs[i].top == T && qs[i].src0 >= 0) ft0[qs[i].src0] |= 1ULL << i;
-  SHCHK(c, hipMemcpyAsync(c->ft[T & 1].p, ft0.data(), (size_t)NT * 8, hipMemcpyHostToDevice, c->stream));
-
+ShardArgs make_args(dr_shard *c, int nq, int strong_only) {
   ShardArgs a{};
   a.strong = c->strong.as<u64>();
   a.weak = c->weak.as<uint32_t>();
   a.woff = c->woff.as<uint64_t>();
+  a.pres = c->pres.as<u64>();
+  a.lead = c->lead.as<uint16_t>();
+  a.sdeg = c->sdeg.as<uint16_t>();
+  a.ftb0 = c->ft[0].as<u64>();
+  a.ftb1 = c->ft[1].as<u64>();
+  a.send = c->send.as<u64>();
   a.pend = c->pend.as<u64>();
   a.cnt = c->cnt.as<unsigned>();
+  a.bar = c->bar.as<unsigned>();
+  a.err = c->errf.as<int32_t>();
   a.out = c->out.as<u64>();
   a.q = c->qinfo.as<QInfo>();
+  a.push_out = c->push_out.as<int32_t>();
+  a.push_n = c->push_n.as<int32_t>();
+  a.cedges = c->cedges.as<u64>();
   a.n = c->n;
   a.W = c->W;
   a.WSs = c->WSs;
   a.C = c->C;
   a.depth = c->depth;
   a.shard0 = c->shard0;
+  a.nlocal = c->nlocal;
   a.local = c->local ? 1 : 0;
   a.max_rounds = c->max_rounds;
   a.nq = nq;
   a.strong_only = strong_only;
+  a.nlead = (int32_t)c->h_lead.size();
   a.strong_shard_stride = (int64_t)c->max_rounds * c->n * c->WSs;
+  return a;
+}
+
+// One batch of <= 64 sweep queries (rounds max top .. min bottom).  Reach rows
+// land in c->out at dq[i].obase; chain pushes / edges in c->push_* / c->cedges.
+int sweep_batch(dr_shard *c, std::vector<QInfo> &dq, int strong_only) {
+  const int nq = (int)dq.size();
+  int T = 0, Bm = 1 << 30;
+  for (auto &q : dq) {
+    T = std::max(T, q.top);
+    Bm = std::min(Bm, q.bottom);
+  }
+  const int NT = c->G * c->C;
+  SHCHK(c, hipMemcpyAsync(c->qinfo.p, dq.data(), nq * sizeof(QInfo), hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, hipMemsetAsync(c->pend.p, 0, (size_t)c->nlocal * c->depth * c->C * 8, c->stream));
+  SHCHK(c, hipMemsetAsync(c->cnt.p, 0, (size_t)c->nlocal * 4, c->stream));
+  std::vector<u64> ft0(NT, 0);
+  for (int i = 0; i < nq; i++)
+    if (dq[i].top == T && dq[i].src0 >= 0) ft0[dq[i].src0] |= 1ULL << i;
+  SHCHK(c, hipMemcpyAsync(c->ft[T & 1].p, ft0.data(), (size_t)NT * 8, hipMemcpyHostToDevice, c->stream));
+  ShardArgs a = make_args(c, nq, strong_only);
   const int item_waves = (c->n + 63) / 64 * c->WSs;  // (source chunk, target word) items
-  const size_t weak_waves = strong_only ? 0 : (c->max_weak_round + 511) / 512;
-  const int gx = (int)std::max<size_t>((item_waves + 3) / 4, std::min<size_t>(128, (weak_waves + 3) / 4));
+  const size_t weak_waves = strong_only ? 0 : (c->max_weak_round + 63) / 64;
+  int gx = (int)std::max<size_t>((item_waves + 3) / 4, std::min<size_t>(128, (weak_waves + 3) / 4));
+  if (c->local && c->persistent) {
+    // every workgroup must be resident: cap the grid by the occupancy of this device
+    int per_cu = 0, ncu = 0;
+    SHCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_shard_sweep, SH_NT, 0));
+    SHCHK(c, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev));
+    const int cap = std::max(1, per_cu * ncu / std::max(1, c->nlocal));
+    gx = std::max(1, std::min(gx, cap));
+    SHCHK(c, hipMemsetAsync(c->bar.p, 0, 4, c->stream));
+    void *args[] = {&a, &T, &Bm};
+    SHCHK(c, hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_shard_sweep), dim3(gx, c->nlocal),
+                                        dim3(SH_NT), args, 0, c->stream));
+    c->last_rounds += (uint64_t)(T - Bm + 1);
+    return DR_OK;
+  }
   const dim3 grid(gx, c->nlocal), block(SH_NT);
   for (int r = T; r >= Bm; r--) {
-    u64 expm = 0, outm = 0, injm = 0;
-    for (int i = 0; i < nq; i++) {
-      if (qs[i].bottom < r && r <= qs[i].top) expm |= 1ULL << i;
-      if (qs[i].bottom <= r && r <= qs[i].top) outm |= 1ULL << i;
-      if (qs[i].top == r - 1) injm |= 1ULL << i;
-    }
     const int produce = r - 1 >= Bm;
-    a.ft = c->ft[r & 1].as<u64>();
-    a.ftn = c->local ? c->ft[(r - 1) & 1].as<u64>() : c->send.as<u64>();
-    hipLaunchKernelGGL(k_shard_round, grid, block, 0, c->stream, a, r, expm, outm, injm, produce);
+    hipLaunchKernelGGL(k_shard_round, grid, block, 0, c->stream, a, r, produce);
     SHCHK(c, hipGetLastError());
     if (produce && !c->local) {
-      ncclResult_t nr = ncclAllGather(c->send.p, c->ft[(r - 1) & 1].p, (size_t)c->C, ncclUint64, c->comm, c->stream);
-      if (nr != ncclSuccess) return c->fail(DR_E_RCCL, "ncclAllGather: %s", ncclGetErrorString(nr));
+      SHNCCL(c, ncclAllGather(c->send.p, c->ft[(r - 1) & 1].p, (size_t)c->C, ncclUint64, c->comm, c->stream));
       c->last_xbytes += (uint64_t)c->C * 8;
     }
     c->last_rounds++;
   }
-  std::vector<u64> tmp(words);
-  SHCHK(c, hipMemcpyAsync(tmp.data(), c->out.p, words * 8, hipMemcpyDeviceToHost, c->stream));
-  SHCHK(c, hipStreamSynchronize(c->stream));
-  for (int i = 0; i < nq; i++)
-    std::memcpy(out + hbase[i], &tmp[dq[i].obase], (size_t)(qs[i].top - qs[i].bottom + 1) * c->W * 8);
   return DR_OK;
 }
 
-// all queries, in batches of 64, timed with HIP events
+int check_barrier(dr_shard *c) {
+  int32_t e = 0;
+  SHCHK(c, hipMemcpyAsync(&e, c->errf.p, 4, hipMemcpyDeviceToHost, c->stream));
+  SHCHK(c, hipStreamSynchronize(c->stream));
+  if (e) return c->fail(DR_E_HIP, "k_shard_sweep: grid barrier timed out (workgroups not co-resident)");
+  return DR_OK;
+}
+
+int prepare_queries(dr_shard *c, int strong_only) {
+  if (int rc = sync_weak(c)) return rc;
+  (void)strong_only;
+  SHCHK(c, c->qinfo.ensure(SH_BATCH * sizeof(QInfo)));
+  SHCHK(c, c->bar.ensure(64));
+  SHCHK(c, c->errf.ensure(64));
+  SHCHK(c, c->push_n.ensure(SH_BATCH * 4));
+  SHCHK(c, c->cedges.ensure(SH_BATCH * 8));
+  SHCHK(c, hipMemsetAsync(c->errf.p, 0, 4, c->stream));
+  return DR_OK;
+}
+
+// reach-set queries, in batches of 64, timed with HIP events; rows land in host `out` at hbase[i]
 int run_queries(dr_shard *c, const std::vector<QInfo> &qs, const std::vector<size_t> &hbase, int strong_only,
                 uint64_t *out) {
-  if (int rc = sync_weak(c)) return rc;
+  if (int rc = prepare_queries(c, strong_only)) return rc;
   c->last_rounds = 0;
   c->last_xbytes = 0;
   SHCHK(c, hipEventRecord(c->ev0, c->stream));
   for (size_t i0 = 0; i0 < qs.size(); i0 += SH_BATCH) {
     const size_t i1 = std::min(qs.size(), i0 + SH_BATCH);
-    std::vector<QInfo> part(qs.begin() + i0, qs.begin() + i1);
-    std::vector<size_t> hb(hbase.begin() + i0, hbase.begin() + i1);
-    if (int rc = sweep_batch(c, part, hb, strong_only, out)) return rc;
+    std::vector<QInfo> dq(qs.begin() + i0, qs.begin() + i1);
+    int64_t words = 0;
+    for (auto &q : dq) {
+      q.obase = words;
+      words += (int64_t)(q.top - q.bottom + 1) * c->W;
+    }
+    SHCHK(c, c->out.ensure(std::max<int64_t>(words, 1) * 8));
+    if (int rc = sweep_batch(c, dq, strong_only)) return rc;
+    std::vector<u64> tmp(words);
+    SHCHK(c, hipMemcpyAsync(tmp.data(), c->out.p, words * 8, hipMemcpyDeviceToHost, c->stream));
+    SHCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < dq.size(); i++)
+      std::memcpy(out + hbase[i0 + i], &tmp[dq[i].obase], (size_t)(dq[i].top - dq[i].bottom + 1) * c->W * 8);
   }
   SHCHK(c, hipEventRecord(c->ev1, c->stream));
   SHCHK(c, hipEventSynchronize(c->ev1));
   SHCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  return check_barrier(c);
+}
+
+// waveReady's commit decision for waves w0..w1 (all evaluable; see votes())
+int vote_range(dr_shard *c, int w0, int nw, uint8_t *commit, int32_t *vcount) {
+  const int W = c->W, G = c->G;
+  std::vector<u64> s0((size_t)nw * W, 0);
+  std::vector<uint8_t> has(nw, 0);
+  for (int i = 0; i < nw; i++) {
+    const int w = w0 + i, L = c->lead_src(w);
+    if (c->is_present(4 * (w - 1) + 1, L)) {
+      has[i] = 1;
+      s0[(size_t)i * W + ((L - 1) >> 6)] = 1ULL << ((L - 1) & 63);
+    }
+  }
+  const size_t pw = (size_t)G * nw * W * 8;
+  SHCHK(c, c->vote_s0.ensure(s0.size() * 8));
+  SHCHK(c, c->vote_p[0].ensure(pw));
+  SHCHK(c, c->vote_p[1].ensure(pw));
+  SHCHK(c, c->vote_send.ensure((size_t)nw * W * 8));
+  SHCHK(c, c->vcount.ensure((size_t)nw * 4));
+  SHCHK(c, hipMemcpyAsync(c->vote_s0.p, s0.data(), s0.size() * 8, hipMemcpyHostToDevice, c->stream));
+  ShardArgs a = make_args(c, 0, 1);
+  const int bpw = (c->n + SH_NT - 1) / SH_NT;
+  for (int k = 1; k <= 3; k++) {
+    u64 *pin = c->vote_p[(k + 1) & 1].as<u64>(), *pout = c->vote_p[k & 1].as<u64>();
+    u64 *dst = c->local ? pout : c->vote_send.as<u64>();
+    hipLaunchKernelGGL(k_shard_vote, dim3(nw * bpw, c->nlocal), dim3(SH_NT), 0, c->stream, a, w0, nw, k, G,
+                       c->vote_s0.as<u64>(), pin, dst);
+    SHCHK(c, hipGetLastError());
+    if (!c->local) {
+      SHNCCL(c, ncclAllGather(c->vote_send.p, pout, (size_t)nw * W, ncclUint64, c->comm, c->stream));
+      c->last_xbytes += (uint64_t)nw * W * 8;
+    }
+  }
+  hipLaunchKernelGGL(k_shard_vcount, dim3((nw + 255) / 256), dim3(256), 0, c->stream, c->vote_p[1].as<u64>(), G, nw,
+                     W, c->vcount.as<int32_t>());
+  SHCHK(c, hipGetLastError());
+  std::vector<int32_t> vc(nw);
+  SHCHK(c, hipMemcpyAsync(vc.data(), c->vcount.p, (size_t)nw * 4, hipMemcpyDeviceToHost, c->stream));
+  SHCHK(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < nw; i++) {
+    vcount[i] = has[i] ? vc[i] : -1;
+    commit[i] = has[i] && vc[i] >= 2 * c->f + 1;
+  }
   return DR_OK;
+}
+
+// dr_wave_commit semantics (engine.hip commit_range): waves past the DAG panic
+// (Go: index out of range) unless their leader is absent.
+int votes(dr_shard *c, int w0, int w1, uint8_t *commit, int32_t *vcount) {
+  if (w0 < 1 || w1 < w0) return c->fail(DR_E_INVAL, "wave range [%d,%d] invalid (waves are 1-based)", w0, w1);
+  int wk = w0 - 1;
+  while (wk + 1 <= w1 && 4 * (wk + 1) < c->nrounds) wk++;
+  for (int w = wk + 1; w <= w1; w++) {
+    const int r1 = 4 * (w - 1) + 1;
+    if (r1 >= c->nrounds) return c->fail(DR_E_INVAL, "wave %d: leader round %d not in the DAG (Go: index out of range)", w, r1);
+    if (c->is_present(r1, c->lead_src(w))) return c->fail(DR_E_INVAL, "wave %d: round %d not in the DAG (Go: index out of range)", w, 4 * w);
+    commit[w - w0] = 0;
+    vcount[w - w0] = -1;
+  }
+  if (wk < w0) return DR_OK;
+  return vote_range(c, w0, wk - w0 + 1, commit, vcount);
+}
+
+struct ChainTask { int wave, floor; };
+
+// Leader chains (process.go:341-350): pushes[i] = waves pushed by task i, in push order.
+int chains(dr_shard *c, const std::vector<ChainTask> &tasks, std::vector<std::vector<int32_t>> &pushes,
+           uint64_t *edges_total) {
+  pushes.assign(tasks.size(), {});
+  std::vector<QInfo> qv;
+  std::vector<int> qi;
+  for (size_t i = 0; i < tasks.size(); i++) {
+    pushes[i].push_back(tasks[i].wave);
+    if (tasks[i].wave - 1 < tasks[i].floor + 1) continue;
+    if (tasks[i].floor < 0) return c->fail(DR_E_INVAL, "decidedWave %d < 0 (Go: waveRound(0,1) index out of range)", tasks[i].floor);
+    QInfo q{};
+    q.top = 4 * (tasks[i].wave - 1) + 1;
+    q.bottom = 4 * tasks[i].floor + 1;
+    q.src0 = c->lead_src(tasks[i].wave) - 1;
+    q.flags = QF_CHAIN;
+    qv.push_back(q);
+    qi.push_back((int)i);
+  }
+  if (edges_total) *edges_total = 0;
+  if (qv.empty()) return DR_OK;
+  if (int rc = prepare_queries(c, 1)) return rc;
+  for (size_t i0 = 0; i0 < qv.size(); i0 += SH_BATCH) {
+    const size_t i1 = std::min(qv.size(), i0 + SH_BATCH);
+    std::vector<QInfo> dq(qv.begin() + i0, qv.begin() + i1);
+    int32_t off = 0;
+    for (auto &q : dq) {
+      q.push_base = off;
+      off += (q.top - q.bottom) / 4 + 1;
+    }
+    SHCHK(c, c->push_out.ensure((size_t)std::max(off, 1) * 4));
+    SHCHK(c, hipMemsetAsync(c->push_n.p, 0, SH_BATCH * 4, c->stream));
+    SHCHK(c, hipMemsetAsync(c->cedges.p, 0, SH_BATCH * 8, c->stream));
+    if (int rc = sweep_batch(c, dq, 1)) return rc;
+    std::vector<int32_t> pn(dq.size()), po(off);
+    std::vector<u64> ce(dq.size());
+    SHCHK(c, hipMemcpyAsync(pn.data(), c->push_n.p, dq.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    SHCHK(c, hipMemcpyAsync(po.data(), c->push_out.p, (size_t)off * 4, hipMemcpyDeviceToHost, c->stream));
+    SHCHK(c, hipMemcpyAsync(ce.data(), c->cedges.p, dq.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    SHCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t j = 0; j < dq.size(); j++) {
+      auto &p = pushes[qi[i0 + j]];
+      for (int x = 0; x < pn[j]; x++) p.push_back(po[dq[j].push_base + x]);
+      if (edges_total) *edges_total += ce[j];
+    }
+  }
+  return check_barrier(c);
+}
+
+struct Pop { int round, source, cur; };
+
+// orderVertices deliveries of `pops` in pop order: one cone per distinct
+// (round, source), emitted over rounds 1..min(cur, round).
+int deliver(dr_shard *c, const std::vector<Pop> &pops, int mode, uint64_t *pcount, uint64_t *pdigest,
+            uint64_t *pedges) {
+  const int W = c->W;
+  std::map<std::pair<int, int>, int> key;
+  std::vector<int> kidx(pops.size());
+  std::vector<Pop> uniq;
+  std::vector<uint8_t> first(pops.size(), 0);
+  for (size_t i = 0; i < pops.size(); i++) {
+    auto it = key.find({pops[i].round, pops[i].source});
+    if (it == key.end()) {
+      it = key.emplace(std::make_pair(pops[i].round, pops[i].source), (int)uniq.size()).first;
+      uniq.push_back(pops[i]);
+      first[i] = 1;
+    }
+    kidx[i] = it->second;
+  }
+  const int K = (int)uniq.size();
+  std::vector<u64> kc(K), kd(K), ke(K);
+  if (int rc = prepare_queries(c, 0)) return rc;
+  int rmax = 1;
+  for (auto &p : uniq) rmax = std::max(rmax, std::min(p.cur, p.round));
+  const int rstride = c->nrounds + 1;
+  SHCHK(c, c->pcnt.ensure((size_t)SH_BATCH * rstride * 4));
+  SHCHK(c, c->qcnt.ensure(SH_BATCH * 8));
+  SHCHK(c, c->qedges.ensure(SH_BATCH * 8));
+  SHCHK(c, c->qdig.ensure(SH_BATCH * 8));
+  if (mode == DR_DELIVER_PAPER) {
+    SHCHK(c, c->D.ensure((size_t)c->nrounds * W * 8));
+    SHCHK(c, hipMemsetAsync(c->D.p, 0, (size_t)c->nrounds * W * 8, c->stream));
+  }
+  float ms_sw = 0, ms_em = 0;
+  for (int i0 = 0; i0 < K; i0 += SH_BATCH) {
+    const int i1 = std::min(K, i0 + SH_BATCH);
+    std::vector<QInfo> dq;
+    int64_t words = 0;
+    int bmax = 1;
+    for (int i = i0; i < i1; i++) {
+      QInfo q{};
+      q.top = uniq[i].round;
+      q.bottom = std::min(1, q.top);  // round 0 is never delivered nor expanded from
+      q.src0 = (uniq[i].source >= 1 && uniq[i].source <= c->n) ? uniq[i].source - 1 : -1;
+      q.last = std::min(uniq[i].cur, q.top);
+      q.obase = words;
+      words += (int64_t)(q.top - q.bottom + 1) * W;
+      bmax = std::max(bmax, q.last);
+      dq.push_back(q);
+    }
+    const int nq = (int)dq.size();
+    SHCHK(c, c->out.ensure(std::max<int64_t>(words, 1) * 8));
+    SHCHK(c, hipEventRecord(c->ev0, c->stream));
+    if (int rc = sweep_batch(c, dq, 0)) return rc;
+    SHCHK(c, hipEventRecord(c->ev1, c->stream));
+    SHCHK(c, hipMemsetAsync(c->qedges.p, 0, SH_BATCH * 8, c->stream));
+    SHCHK(c, hipMemsetAsync(c->qdig.p, 0, SH_BATCH * 8, c->stream));
+    const int rb = (bmax + 3) / 4;  // 4 rounds (waves) per workgroup
+    const QInfo *qd = c->qinfo.as<QInfo>();
+    hipLaunchKernelGGL(k_shard_dmask, dim3(rb), dim3(SH_NT), 0, c->stream, c->out.as<u64>(), qd, nq, bmax, W,
+                       c->pres.as<u64>(), c->D.as<u64>(), mode == DR_DELIVER_PAPER ? 1 : 0);
+    SHCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(k_shard_count, dim3(rb, nq), dim3(SH_NT), 0, c->stream, c->out.as<u64>(), qd, W, c->n,
+                       rstride, c->pres.as<u64>(), c->sdeg.as<uint16_t>(), c->wdeg.as<uint16_t>(), c->rdeg.as<u64>(),
+                       c->pcnt.as<uint32_t>(), c->qedges.as<u64>());
+    SHCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(k_shard_scan, dim3(nq), dim3(SH_NT), 0, c->stream, qd, rstride, c->pcnt.as<uint32_t>(),
+                       c->qcnt.as<u64>());
+    SHCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(k_shard_digest, dim3(rb, nq), dim3(SH_NT), 0, c->stream, c->out.as<u64>(), qd, W, rstride,
+                       c->pcnt.as<uint32_t>(), c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
+                       c->qdig.as<u64>());
+    SHCHK(c, hipGetLastError());
+    SHCHK(c, hipEventRecord(c->ev2, c->stream));
+    SHCHK(c, hipMemcpyAsync(&kc[i0], c->qcnt.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    SHCHK(c, hipMemcpyAsync(&ke[i0], c->qedges.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    SHCHK(c, hipMemcpyAsync(&kd[i0], c->qdig.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    SHCHK(c, hipStreamSynchronize(c->stream));
+    float a = 0, b = 0;
+    SHCHK(c, hipEventElapsedTime(&a, c->ev0, c->ev1));
+    SHCHK(c, hipEventElapsedTime(&b, c->ev1, c->ev2));
+    ms_sw += a;
+    ms_em += b;
+  }
+  c->ms_sweep = ms_sw;
+  c->ms_emit = ms_em;
+  // a repeated leader in paper mode delivers nothing new (its whole cone is in
+  // the delivered set) and expands nothing (the pruned leader)
+  for (size_t i = 0; i < pops.size(); i++) {
+    const int k = kidx[i];
+    const bool zero = mode == DR_DELIVER_PAPER && !first[i];
+    if (pcount) pcount[i] = zero ? 0 : kc[k];
+    if (pdigest) pdigest[i] = zero ? 0 : kd[k];
+    if (pedges) pedges[i] = zero ? 0 : ke[k];
+  }
+  return check_barrier(c);
 }
 
 }  // namespace
@@ -398,8 +1001,10 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   c->dev = device;
   c->h_weak.resize(c->nlocal);
   c->h_woff.assign(c->nlocal, std::vector<uint64_t>(1, 0));
+  c->h_lead.assign((size_t)max_rounds / 4 + 2, 1);
   if (sh_set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev2) != hipSuccess) {
     g_shard_err = "dr_shard_create: stream/event creation failed";
     dr_shard_destroy(c);
     return DR_E_HIP;
@@ -407,7 +1012,15 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   const size_t NT = (size_t)c->G * c->C;
   if (c->strong.ensure((size_t)c->nlocal * max_rounds * n * c->WSs * 8) != hipSuccess ||
       c->ft[0].ensure(NT * 8) != hipSuccess || c->ft[1].ensure(NT * 8) != hipSuccess ||
-      c->send.ensure((size_t)c->C * 8) != hipSuccess || c->cnt.ensure(c->nlocal * 4) != hipSuccess) {
+      c->send.ensure((size_t)c->C * 8) != hipSuccess || c->cnt.ensure(c->nlocal * 4) != hipSuccess ||
+      c->pres.ensure((size_t)max_rounds * c->W * 8) != hipSuccess ||
+      c->sdeg.ensure((size_t)max_rounds * n * 2) != hipSuccess ||
+      c->wdeg.ensure((size_t)max_rounds * n * 2) != hipSuccess ||
+      c->rdeg.ensure((size_t)max_rounds * 8) != hipSuccess ||
+      c->slot_off.ensure(((size_t)max_rounds + 1) * 4) != hipSuccess ||
+      c->lead.ensure(c->h_lead.size() * 2) != hipSuccess ||
+      hipMemcpy(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->slot_off.p, 0, 4) != hipSuccess) {
     g_shard_err = "dr_shard_create: device allocation failed";
     dr_shard_destroy(c);
     return DR_E_HIP;
@@ -432,10 +1045,13 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out, &c->qinfo})
+  for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out,
+                  &c->qinfo, &c->pres, &c->sdeg, &c->wdeg, &c->rdeg, &c->slot_off, &c->slot_src, &c->lead, &c->bar,
+                  &c->errf, &c->push_out, &c->push_n, &c->cedges, &c->vote_s0, &c->vote_p[0], &c->vote_p[1],
+                  &c->vote_send, &c->vcount, &c->D, &c->pcnt, &c->qcnt, &c->qedges, &c->qdig})
     b->release();
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2})
+    if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -453,6 +1069,37 @@ extern "C" int dr_shard_info(const dr_shard *c, int *nshards, int *shard0, int *
   return DR_OK;
 }
 
+extern "C" int dr_shard_set_option(dr_shard *c, int option, int value) {
+  if (!c) return DR_E_INVAL;
+  if (option == DR_SHARD_OPT_PERSISTENT) {
+    c->persistent = value ? 1 : 0;
+    return DR_OK;
+  }
+  return c->fail(DR_E_INVAL, "unknown option %d", option);
+}
+
+extern "C" int dr_shard_set_leader_coin(dr_shard *c, int mode, uint64_t seed, int k, const int32_t *table) {
+  if (!c) return DR_E_INVAL;
+  if (int rc = sh_set_device(c)) return rc;
+  std::vector<uint16_t> L(c->h_lead.size(), 1);
+  if (mode == DR_LEADER_SEEDED) {
+    for (size_t w = 1; w < L.size(); w++) L[w] = (uint16_t)dr_coin_leader(seed, (int)w, c->n);
+  } else if (mode == DR_LEADER_TABLE) {
+    if (k < 0 || (k > 0 && !table)) return c->fail(DR_E_INVAL, "bad leader table");
+    for (int w = 1; w <= k && w < (int)L.size(); w++) {
+      if (table[w - 1] < 1 || table[w - 1] > c->n)
+        return c->fail(DR_E_INVAL, "leader of wave %d: source %d outside [1, %d]", w, table[w - 1], c->n);
+      L[w] = (uint16_t)table[w - 1];
+    }
+  } else if (mode != DR_LEADER_CONST1) {
+    return c->fail(DR_E_INVAL, "unknown leader coin mode %d", mode);
+  }
+  c->h_lead = std::move(L);
+  SHCHK(c, hipMemcpyAsync(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, hipStreamSynchronize(c->stream));
+  return DR_OK;
+}
+
 extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const uint32_t *slot_off,
                                              const uint16_t *slot_src, const uint64_t *strong,
                                              const uint32_t *weak_off, const uint32_t *weak_tgt) {
@@ -464,31 +1111,34 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
   if (!slot_off || !slot_src || !strong || !weak_off) return c->fail(DR_E_INVAL, "null array");
   const int n = c->n, W = c->W, WSs = c->WSs, C = c->C;
   const u64 lastmask = (n % 64) ? ((1ULL << (n % 64)) - 1ULL) : ~0ULL;
-  std::vector<u64> pres(W);
+  std::vector<u64> pres((size_t)k * W, 0);
   std::vector<u64> rows((size_t)c->nlocal * k * n * WSs, 0);
+  std::vector<uint16_t> sd((size_t)k * n, 0), wd((size_t)k * n, 0);
+  std::vector<u64> rd(k, 0);
+  std::vector<uint64_t> deg(k, 0);
   std::vector<std::vector<uint32_t>> wnew(c->nlocal);
   std::vector<std::vector<uint64_t>> wro(c->nlocal, std::vector<uint64_t>(k + 1, 0));
   int dmax = c->dmax;
   size_t maxw = c->max_weak_round;
   for (int i = 0; i < k; i++) {
     const int r = r0 + i;
-    std::fill(pres.begin(), pres.end(), 0ULL);
+    u64 *P = &pres[(size_t)i * W];
     for (uint32_t sl = slot_off[i]; sl < slot_off[i + 1]; sl++) {
       const int s = slot_src[sl];
       if (s > n) return c->fail(DR_E_CONTRACT, "round %d slot %u: source %d > n=%d", r, sl - slot_off[i], s, n);
       if (s == 0) continue;
       const u64 bit = 1ULL << ((s - 1) & 63);
-      if ((pres[(s - 1) >> 6] & bit) && r >= 1) return c->fail(DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, s);
-      pres[(s - 1) >> 6] |= bit;
+      if ((P[(s - 1) >> 6] & bit) && r >= 1) return c->fail(DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, s);
+      P[(s - 1) >> 6] |= bit;
     }
     for (int l = 0; l < c->nlocal; l++) wro[l][i] = wnew[l].size();
     for (int s0 = 0; s0 < n; s0++) {
-      const bool here = (pres[s0 >> 6] >> (s0 & 63)) & 1ULL;
+      const bool here = (P[s0 >> 6] >> (s0 & 63)) & 1ULL;
       const uint64_t *row = strong + ((size_t)i * n + s0) * W;
-      bool nz = false;
-      for (int w = 0; w < W; w++) nz |= row[w] != 0;
-      if (nz && !here) return c->fail(DR_E_CONTRACT, "round %d: strong edges on absent vertex (%d,%d)", r, r, s0 + 1);
-      if (nz && r == 0) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", s0 + 1);
+      uint64_t d = 0;
+      for (int w = 0; w < W; w++) d += (uint64_t)__builtin_popcountll(row[w]);
+      if (d && !here) return c->fail(DR_E_CONTRACT, "round %d: strong edges on absent vertex (%d,%d)", r, r, s0 + 1);
+      if (d && r == 0) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", s0 + 1);
       if (row[W - 1] & ~lastmask) return c->fail(DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
       for (int l = 0; l < c->nlocal; l++) {
         const int g = c->shard0 + l;
@@ -501,6 +1151,10 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
       const uint32_t ea = weak_off[(size_t)i * n + s0], eb = weak_off[(size_t)i * n + s0 + 1];
       if (eb < ea) return c->fail(DR_E_INVAL, "weak_off not monotone at round %d", r);
       if (eb > ea && !here) return c->fail(DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1);
+      sd[(size_t)i * n + s0] = (uint16_t)d;
+      wd[(size_t)i * n + s0] = (uint16_t)std::min<uint32_t>(eb - ea, 65535u);
+      deg[i] += d;
+      rd[i] += d + (eb - ea);
       for (uint32_t e = ea; e < eb; e++) {
         const uint32_t t = weak_tgt[e];
         const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
@@ -524,6 +1178,23 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
       maxw = std::max<size_t>(maxw, w.size() - wro[l][i]);
     }
   }
+  // per-vertex metadata (every shard holds all of it) and the slot order
+  const uint32_t S0 = c->h_slot_off.back();
+  for (int i = 0; i < k; i++) c->h_slot_off.push_back(S0 + (slot_off[i + 1] - slot_off[0]));
+  const size_t ns = (size_t)(slot_off[k] - slot_off[0]);
+  SHCHK(c, c->slot_src.grow(((size_t)S0 + ns) * 2 + 64, (size_t)S0 * 2, c->stream));
+  if (ns)
+    SHCHK(c, hipMemcpyAsync(c->slot_src.as<uint16_t>() + S0, slot_src + slot_off[0], ns * 2, hipMemcpyHostToDevice,
+                            c->stream));
+  SHCHK(c, hipMemcpyAsync(c->slot_off.as<uint32_t>() + r0 + 1, &c->h_slot_off[r0 + 1], (size_t)k * 4,
+                          hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, hipMemcpyAsync(c->pres.as<u64>() + (size_t)r0 * W, pres.data(), pres.size() * 8, hipMemcpyHostToDevice,
+                          c->stream));
+  SHCHK(c, hipMemcpyAsync(c->sdeg.as<uint16_t>() + (size_t)r0 * n, sd.data(), sd.size() * 2, hipMemcpyHostToDevice,
+                          c->stream));
+  SHCHK(c, hipMemcpyAsync(c->wdeg.as<uint16_t>() + (size_t)r0 * n, wd.data(), wd.size() * 2, hipMemcpyHostToDevice,
+                          c->stream));
+  SHCHK(c, hipMemcpyAsync(c->rdeg.as<u64>() + r0, rd.data(), rd.size() * 8, hipMemcpyHostToDevice, c->stream));
   for (int l = 0; l < c->nlocal; l++) {
     wro[l][k] = wnew[l].size();
     const size_t dst = ((size_t)l * c->max_rounds + r0) * n * WSs;
@@ -534,6 +1205,8 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
     for (int i = 1; i <= k; i++) c->h_woff[l].push_back(base + wro[l][i]);
   }
   SHCHK(c, hipStreamSynchronize(c->stream));
+  c->h_pres.insert(c->h_pres.end(), pres.begin(), pres.end());
+  c->h_deg.insert(c->h_deg.end(), deg.begin(), deg.end());
   c->weak_dirty = true;
   c->dmax = dmax;
   int depth = 2;
@@ -559,7 +1232,7 @@ extern "C" int dr_shard_reach_sets(dr_shard *c, int q, const int32_t *from, cons
     const int fr = from[2 * i], fs = from[2 * i + 1], b = bottom[i];
     if (fr < 0 || fr >= c->nrounds || b < 0 || b > fr)
       return c->fail(DR_E_INVAL, "query %d: rounds [%d,%d] outside the DAG", i, b, fr);
-    qs[i] = QInfo{fr, b, (fs >= 1 && fs <= c->n) ? fs - 1 : -1, 0, 0};
+    qs[i] = QInfo{fr, b, (fs >= 1 && fs <= c->n) ? fs - 1 : -1, 0, 0, 0, fr};
     hb[i] = need;
     need += (size_t)(fr - b + 1) * c->W;
   }
@@ -586,7 +1259,7 @@ extern "C" int dr_shard_path_batch(dr_shard *c, int q, const int32_t *from, cons
     out[i] = 0;
     if (tr < 0 || tr >= fr || ts < 1 || ts > c->n || fs < 1 || fs > c->n) continue;
     // only the row of round tr is needed: a one-round output window
-    qs.push_back(QInfo{fr, tr, fs - 1, 0, 0});
+    qs.push_back(QInfo{fr, tr, fs - 1, 0, 0, 0, fr});
     hb.push_back(need);
     need += (size_t)(fr - tr + 1) * c->W;
     idx.push_back(i);
@@ -598,6 +1271,139 @@ extern "C" int dr_shard_path_batch(dr_shard *c, int q, const int32_t *from, cons
     const int i = idx[k], ts = to[2 * i + 1] - 1;
     out[i] = (sets[hb[k] + (ts >> 6)] >> (ts & 63)) & 1ULL;  // round tr is the first row
   }
+  return DR_OK;
+}
+
+extern "C" int dr_shard_wave_commit(dr_shard *c, int w0, int w1, uint8_t *commit, int32_t *vcount) {
+  if (!c) return DR_E_INVAL;
+  if (!commit || !vcount) return c->fail(DR_E_INVAL, "null output");
+  if (int rc = sh_set_device(c)) return rc;
+  c->last_xbytes = 0;
+  return votes(c, w0, w1, commit, vcount);
+}
+
+extern "C" int dr_shard_wave_ready(dr_shard *c, int wave, int decided_wave, uint8_t *commit, int32_t *vcount,
+                                   int32_t *pushed_waves, int cap, int *n_pushed) {
+  if (!c) return DR_E_INVAL;
+  if (!commit || !vcount || !n_pushed) return c->fail(DR_E_INVAL, "null output");
+  if (int rc = sh_set_device(c)) return rc;
+  *n_pushed = 0;
+  c->last_xbytes = 0;
+  c->last_rounds = 0;
+  if (int rc = votes(c, wave, wave, commit, vcount)) return rc;
+  if (!*commit) return DR_OK;
+  std::vector<std::vector<int32_t>> pushes;
+  if (int rc = chains(c, {ChainTask{wave, decided_wave}}, pushes, nullptr)) return rc;
+  *n_pushed = (int)pushes[0].size();
+  if ((int)pushes[0].size() > cap || (!pushed_waves && !pushes[0].empty()))
+    return c->fail(DR_E_CAPACITY, "%zu pushed leaders, capacity %d", pushes[0].size(), cap);
+  std::copy(pushes[0].begin(), pushes[0].end(), pushed_waves);
+  return DR_OK;
+}
+
+extern "C" int dr_shard_order_vertices(dr_shard *c, const int32_t *stack_rs, int nstack, int cur_round, int mode,
+                                       size_t *out_n, uint64_t *pop_count, uint64_t *pop_digest) {
+  if (!c) return DR_E_INVAL;
+  if (nstack < 0 || (nstack > 0 && !stack_rs)) return c->fail(DR_E_INVAL, "bad stack");
+  if (mode != DR_DELIVER_REF && mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad mode %d", mode);
+  if (int rc = sh_set_device(c)) return rc;
+  if (out_n) *out_n = 0;
+  if (nstack == 0) return DR_OK;
+  if (cur_round >= c->nrounds) return c->fail(DR_E_INVAL, "p.round %d beyond the DAG (Go: index out of range)", cur_round);
+  std::vector<Pop> pops;
+  for (int t = nstack - 1; t >= 0; t--) {  // LIFO (stack/stack.go:23-28)
+    Pop p{stack_rs[2 * t], stack_rs[2 * t + 1], cur_round};
+    if (cur_round >= 1 && (p.round < 0 || p.round >= c->nrounds))
+      return c->fail(DR_E_INVAL, "popped vertex round %d outside the DAG (Go: index out of range)", p.round);
+    if (p.source < 1 || p.source > c->n)
+      return c->fail(DR_E_CONTRACT, "popped vertex (%d,%d): source outside [1,n]", p.round, p.source);
+    if (cur_round < 1) p.round = std::max(0, std::min(p.round, c->nrounds - 1));
+    pops.push_back(p);
+  }
+  std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
+  c->last_xbytes = 0;
+  c->last_rounds = 0;
+  if (int rc = deliver(c, pops, mode, cnt.data(), dg.data(), nullptr)) return rc;
+  uint64_t tot = 0;
+  for (auto x : cnt) tot += x;
+  if (out_n) *out_n = (size_t)tot;
+  if (pop_count) std::copy(cnt.begin(), cnt.end(), pop_count);
+  if (pop_digest) std::copy(dg.begin(), dg.end(), pop_digest);
+  return DR_OK;
+}
+
+extern "C" int dr_shard_replay(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
+  if (!c) return DR_E_INVAL;
+  if (!o || !o->commit || !o->vcount || !o->push_off) return c->fail(DR_E_INVAL, "null output");
+  if (nwaves < 1 || 4 * nwaves >= c->nrounds) return c->fail(DR_E_INVAL, "nwaves %d needs rounds 0..%d mirrored", nwaves, 4 * nwaves);
+  if (chain_mode != DR_CHAIN_LITERAL && chain_mode != DR_CHAIN_PERSISTENT) return c->fail(DR_E_INVAL, "bad chain mode");
+  if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad deliver mode");
+  if (o->ids && o->ids_cap > 0) return c->fail(DR_E_INVAL, "the sharded replay reports counts and digests, not ids");
+  if (int rc = sh_set_device(c)) return rc;
+  o->ms_commit = o->ms_chain = o->ms_deliver = o->ms_emit = o->ms_summary = 0;
+  o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
+  o->n_ids = 0;
+  o->canon_segments = -1;
+  c->last_xbytes = 0;
+  c->last_rounds = 0;
+  hipEvent_t t0 = nullptr, t1 = nullptr, t2 = nullptr;
+  SHCHK(c, hipEventCreate(&t0));
+  SHCHK(c, hipEventCreate(&t1));
+  SHCHK(c, hipEventCreate(&t2));
+  struct EvGuard { hipEvent_t *e[3]; ~EvGuard() { for (auto p : e) if (*p) (void)hipEventDestroy(*p); } } eg{{&t0, &t1, &t2}};
+  SHCHK(c, hipEventRecord(t0, c->stream));
+  // 1. commit decisions of every wave
+  if (int rc = votes(c, 1, nwaves, o->commit, o->vcount)) return rc;
+  SHCHK(c, hipEventRecord(t1, c->stream));
+  uint64_t ce = 0;
+  for (int w = 1; w <= nwaves; w++)
+    if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
+  o->commit_edges = ce;
+  // 2. chains
+  std::vector<ChainTask> tasks;
+  int lastw = 0;
+  for (int w = 1; w <= nwaves; w++)
+    if (o->commit[w - 1]) {
+      tasks.push_back(ChainTask{w, chain_mode == DR_CHAIN_PERSISTENT ? lastw : 0});
+      lastw = w;
+    }
+  std::vector<std::vector<int32_t>> pushes;
+  if (int rc = chains(c, tasks, pushes, &o->chain_edges)) return rc;
+  SHCHK(c, hipEventRecord(t2, c->stream));
+  SHCHK(c, hipEventSynchronize(t2));
+  SHCHK(c, hipEventElapsedTime(&o->ms_commit, t0, t1));
+  SHCHK(c, hipEventElapsedTime(&o->ms_chain, t1, t2));
+  int64_t np = 0;
+  for (auto &p : pushes) np += (int64_t)p.size();
+  o->n_push = np;
+  if (np > o->push_cap || !o->push_wave || !o->pop_count || !o->pop_digest)
+    return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)np, (long long)o->push_cap);
+  // 3. pops (stack order: the oldest pushed leader first)
+  std::vector<Pop> pops;
+  int64_t at = 0;
+  size_t t = 0;
+  for (int w = 1; w <= nwaves; w++) {
+    o->push_off[w - 1] = (uint32_t)at;
+    if (t < tasks.size() && tasks[t].wave == w) {
+      for (int32_t pw : pushes[t]) o->push_wave[at++] = pw;
+      for (auto it = pushes[t].rbegin(); it != pushes[t].rend(); ++it)
+        pops.push_back(Pop{4 * (*it - 1) + 1, c->lead_src(*it), 4 * w});
+      t++;
+    }
+  }
+  o->push_off[nwaves] = (uint32_t)at;
+  std::vector<uint64_t> pe(pops.size());
+  if (!pops.empty())
+    if (int rc = deliver(c, pops, deliver_mode, o->pop_count, o->pop_digest, pe.data())) return rc;
+  o->ms_deliver = c->ms_sweep;
+  o->ms_emit = c->ms_emit;
+  uint64_t de = 0;
+  for (size_t i = 0; i < pops.size(); i++) {
+    de += pe[i];
+    if (o->pop_edges) o->pop_edges[i] = pe[i];
+  }
+  o->deliver_edges = de;
+  o->sweep_count = (uint64_t)pops.size();
   return DR_OK;
 }
 

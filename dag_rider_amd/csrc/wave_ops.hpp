@@ -1,0 +1,62 @@
+// wave_ops.hpp -- wave64 helpers shared by the engine (kernels.hpp) and the
+// column-sharded path (shard.hip): popcount, agent-scope loads, the delivered-
+// sequence digest term and DPP/readlane wave reductions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dr {
+
+typedef unsigned long long u64;
+
+__device__ __forceinline__ int popc64(u64 x) { return __popcll(x); }
+
+__device__ __forceinline__ u64 ld_agent(const u64 *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ u64 mix64(u64 z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ u64 digest_term(uint32_t round, uint32_t source, u64 k) {
+  u64 key = ((u64)round << 32) | source;
+  return mix64(key ^ mix64(k + 0x9E3779B97F4A7C15ULL));
+}
+
+// ---------------------------------------------------------------------------
+// Wave reductions on DPP row operations (rows of 16 lanes) + readlane: no LDS
+// traffic, no ds_bpermute latency chain.  Every lane of the wave must be active.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ u64 dpp64(u64 x) {
+  return ((u64)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | (u64)dpp32<CTRL>((uint32_t)x);
+}
+enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141,
+             DPP_ROW_ROR = 0x120 };
+__device__ __forceinline__ u64 readlane64(u64 x, int l) {
+  return ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+}
+// OR of all 64 lanes (wave-uniform result)
+__device__ __forceinline__ u64 wave_or(u64 x) {
+  x |= dpp64<DPP_QP_1032>(x);
+  x |= dpp64<DPP_QP_2301>(x);
+  x |= dpp64<DPP_ROW_HALF_MIRROR>(x);
+  x |= dpp64<DPP_ROW_MIRROR>(x);
+  return readlane64(x, 0) | readlane64(x, 16) | readlane64(x, 32) | readlane64(x, 48);
+}
+// sum of all 64 lanes (wave-uniform result)
+__device__ __forceinline__ u64 wave_sum(u64 x) {
+  x += dpp64<DPP_QP_1032>(x);
+  x += dpp64<DPP_QP_2301>(x);
+  x += dpp64<DPP_ROW_HALF_MIRROR>(x);
+  x += dpp64<DPP_ROW_MIRROR>(x);
+  return readlane64(x, 0) + readlane64(x, 16) + readlane64(x, 32) + readlane64(x, 48);
+}
+}  // namespace dr

@@ -2,7 +2,8 @@
 
 SURVEY.md s8(e): a DAG split by target column across the GPUs of one node, one
 process per GPU, with one RCCL all-gather of the frontier per round inside the
-library.  ``ShardEngine.from_process_group`` builds the RCCL group from the
+library.  Reach sets and path(), waveReady's commit and chain, orderVertices and
+the whole replay all run on the sharded DAG.  ``ShardEngine.from_process_group`` builds the RCCL group from the
 ``torch.distributed`` default group (rank 0 makes the unique id, a broadcast hands it
 to every rank).  ``ShardEngine(..., nshards=G)`` without an id is local mode: all G
 column shards in one context on one device (same kernels, same split).
@@ -18,6 +19,7 @@ import numpy as np
 
 from . import _lib as L
 from .dag import PackedDag
+from .engine import ReplayResult, _replay_out, _replay_result
 
 
 def shard_unique_id() -> bytes:
@@ -135,3 +137,49 @@ class ShardEngine:
         out = np.zeros(max(q, 1), dtype=np.uint8)
         self._check(self._L.dr_shard_path_batch(self._h, q, L.ptr(fr), L.ptr(to), int(strong_only), L.ptr(out)))
         return out[:q]
+
+    def set_persistent(self, on: bool):
+        """DR_SHARD_OPT_PERSISTENT: one cooperative launch per sweep batch (local mode)."""
+        self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_PERSISTENT, int(on)))
+
+    def set_leader_coin(self, mode: int = L.DR_LEADER_CONST1, seed: int = 0,
+                        table: Optional[Sequence[int]] = None):
+        """chooseLeader (process.go:386-392), as Engine.set_leader_coin."""
+        t = np.asarray(table if table is not None else [1], dtype=np.int32)
+        k = len(table) if table is not None else 0
+        self._check(self._L.dr_shard_set_leader_coin(self._h, mode, seed, k, L.ptr(t)))
+
+    def wave_commit(self, w0: int, w1: int):
+        nw = w1 - w0 + 1
+        cm = np.zeros(max(nw, 1), np.uint8)
+        vc = np.zeros(max(nw, 1), np.int32)
+        self._check(self._L.dr_shard_wave_commit(self._h, w0, w1, L.ptr(cm), L.ptr(vc)))
+        return cm[:nw], vc[:nw]
+
+    def wave_ready(self, wave: int, decided_wave: int):
+        cm = np.zeros(1, np.uint8)
+        vc = np.zeros(1, np.int32)
+        cap = max(wave + 1, 1)
+        pw = np.zeros(cap, np.int32)
+        npush = C.c_int()
+        self._check(self._L.dr_shard_wave_ready(self._h, wave, decided_wave, L.ptr(cm), L.ptr(vc), L.ptr(pw), cap,
+                                                C.byref(npush)))
+        return bool(cm[0]), int(vc[0]), [int(x) for x in pw[:npush.value]]
+
+    def order_vertices(self, stack: Sequence[Tuple[int, int]], cur_round: int, mode: int = L.DR_DELIVER_REF):
+        """Per-pop delivered counts and digests (and the total) of orderVertices."""
+        ns = len(stack)
+        st = np.asarray(stack if ns else [(0, 0)], dtype=np.int32).reshape(-1)
+        out_n = C.c_size_t()
+        pc = np.zeros(max(ns, 1), np.uint64)
+        pd = np.zeros(max(ns, 1), np.uint64)
+        self._check(self._L.dr_shard_order_vertices(self._h, L.ptr(st), ns, cur_round, mode, C.byref(out_n),
+                                                    L.ptr(pc), L.ptr(pd)))
+        return out_n.value, pc[:ns], pd[:ns]
+
+    def replay(self, nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT, deliver_mode: int = L.DR_DELIVER_REF,
+               push_cap: Optional[int] = None) -> ReplayResult:
+        """dr_shard_replay: the whole replay (commit, chains, delivery) on the sharded DAG."""
+        o, keep = _replay_out(nwaves, chain_mode, 0, push_cap)
+        self._check(self._L.dr_shard_replay(self._h, nwaves, chain_mode, deliver_mode, C.byref(o)))
+        return _replay_result(o, keep, 0)

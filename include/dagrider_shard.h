@@ -2,6 +2,7 @@
  * dagrider_shard.h -- process-column sharded reachability.
  *
  * The same path()/reach-set queries as dagrider_gpu.h (process/process.go:89-148),
+ * waveReady's commit and leader chain (:314-354) and orderVertices (:404-443),
  * for a DAG whose edge rows are split by TARGET column across G shards: shard g
  * stores, for every vertex (r, s), the words [g*C, (g+1)*C) of its strong row
  * (C = 64 * ceil(ceil(n/64) / G) target sources per shard) and the weak edges whose
@@ -29,6 +30,8 @@
 #define DAGRIDER_SHARD_H
 #include <stddef.h>
 #include <stdint.h>
+
+#include "dagrider_gpu.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -67,6 +70,36 @@ int dr_shard_reach_sets(dr_shard *ctx, int q, const int32_t *from, const int32_t
 /* dr_path_batch (path(), process.go:89-148) on the sharded DAG. */
 int dr_shard_path_batch(dr_shard *ctx, int q, const int32_t *from, const int32_t *to, int strong_only,
                         uint8_t *out);
+
+/* Options: DR_SHARD_OPT_PERSISTENT (default 1) runs a local-mode sweep batch as
+ * one cooperative launch with grid barriers between rounds; 0 launches one
+ * kernel per round (the RCCL mode's shape).  Results are identical. */
+#define DR_SHARD_OPT_PERSISTENT 1
+int dr_shard_set_option(dr_shard *ctx, int option, int value);
+
+/* chooseLeader (process.go:386-392): dr_set_leader_coin's modes and semantics. */
+int dr_shard_set_leader_coin(dr_shard *ctx, int mode, uint64_t seed, int k, const int32_t *table);
+
+/* dr_wave_commit (waveReady's commit decision, process.go:326-339) on the sharded
+ * DAG: each shard tests its columns of every row of rounds 4w-2..4w against its
+ * columns of the previous step's set; the partial hits are OR-ed across shards
+ * (one all-gather per step in RCCL mode).  Same outputs as dr_wave_commit. */
+int dr_shard_wave_commit(dr_shard *ctx, int w0, int w1, uint8_t *commit, int32_t *vcount);
+
+/* dr_wave_ready (waveReady, process.go:314-354) on the sharded DAG. */
+int dr_shard_wave_ready(dr_shard *ctx, int wave, int decided_wave, uint8_t *commit, int32_t *vcount,
+                        int32_t *pushed_waves, int cap, int *n_pushed);
+
+/* dr_order_vertices (orderVertices, process.go:404-443) on the sharded DAG:
+ * per-pop counts and digests (no id list); *out_n = total delivered. */
+int dr_shard_order_vertices(dr_shard *ctx, const int32_t *stack_rs, int nstack, int cur_round, int mode,
+                            size_t *out_n, uint64_t *pop_count, uint64_t *pop_digest);
+
+/* dr_replay on the sharded DAG: commit, chains and delivery of waves 1..nwaves,
+ * every output of dr_replay_out except the id list (o->ids must be NULL or
+ * ids_cap 0) and the memo statistics.  ms_commit / ms_chain / ms_deliver
+ * (cone sweeps) / ms_emit (dedup, counts, digests) are HIP-event times. */
+int dr_shard_replay(dr_shard *ctx, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o);
 
 /* Last query call: device time (ms, HIP events around the sweeps, exchange
  * included), rounds stepped, and bytes this rank sent through the exchange. */

@@ -10,11 +10,12 @@ import numpy as np
 import pytest
 
 import oracle
+from dag_rider_amd import _lib as L
 from dag_rider_amd.dag import pack_lists
 from dag_rider_amd.engine import Engine
-from dag_rider_amd.gen import generate, small_config
+from dag_rider_amd.gen import CONFIGS, generate, small_config
 from dag_rider_amd.shard import ShardEngine, shard_unique_id
-from dagutil import figure1, random_dag
+from dagutil import dag_fingerprint, figure1, load_large, random_dag
 
 pytestmark = pytest.mark.gpu
 
@@ -120,8 +121,6 @@ def test_shard_rccl_single_rank(gpu_device):
 
 
 def test_shard_errors(gpu_device):
-    from dag_rider_amd import _lib as L
-
     with pytest.raises(L.DrError):
         ShardEngine(10, 3, 8, gpu_device, nshards=0)
     with pytest.raises(L.DrError):
@@ -136,3 +135,107 @@ def test_shard_errors(gpu_device):
         with pytest.raises(L.DrError) as ei:
             se.append_packed(d, 2, 3)  # not contiguous
         assert ei.value.code == L.DR_E_STATE
+
+
+# --------------------------------------------------------------------------- commit + delivery
+MODES = [(cm, dm) for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT) for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER)]
+
+
+def _same_replay(a, b):
+    assert (a.commit == b.commit).all()
+    assert (a.vcount == b.vcount).all()
+    assert (a.push_off == b.push_off).all()
+    assert (a.push_wave == b.push_wave).all()
+    for k in ("pop_count", "pop_digest", "pop_edges"):
+        g, w = getattr(a, k), getattr(b, k)
+        bad = np.nonzero(g != w)[0]
+        assert len(bad) == 0, f"{k}: {len(bad)} pops differ, first at {bad[:5].tolist()}"
+    assert (a.commit_edges, a.chain_edges, a.deliver_edges) == (b.commit_edges, b.chain_edges, b.deliver_edges)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_shard_replay_random_dags(gpu_device, seed):
+    """dr_shard_replay == the bitset oracle (every output, all four chain x deliver modes)
+    on unconstrained random DAGs, at several shard counts, persistent and per-round launches."""
+    rng = np.random.default_rng(3000 + seed)
+    n = int(rng.choice([1, 4, 7, 64, 65, 130, 200, 300]))
+    R = int(rng.integers(8, 41))
+    d = random_dag(rng, n, R, p_present=rng.uniform(0.5, 1), p_s=rng.uniform(0.05, 0.9), p_w=rng.uniform(0, 1),
+                   max_depth=int(rng.integers(2, 20)))
+    f = int(rng.integers(0, (n - 1) // 3 + 2))
+    nw = R // 4
+    bs = oracle.PDag(d)
+    for G in ((1, 2) if seed % 2 else (3, 8)):
+        with ShardEngine(n, f, R + 1, gpu_device, nshards=G) as se:
+            se.append_packed(d)
+            for persistent in (True, False):
+                se.set_persistent(persistent)
+                for cm, dm in MODES:
+                    want = bs.replay(f, nw, cm, dm)
+                    assert want.rc == 0
+                    _same_replay(se.replay(nw, cm, dm), want)
+
+
+def test_shard_commit_chain_order_calls(gpu_device):
+    """The per-call entry points (wave_commit, wave_ready, order_vertices) == the engine's."""
+    rng = np.random.default_rng(77)
+    n, R = 100, 36
+    d = random_dag(rng, n, R, p_present=0.9, p_s=0.7, p_w=0.4, max_depth=6)
+    f = 20
+    with ShardEngine(n, f, R + 1, gpu_device, nshards=4) as se, Engine(n, f, R + 1, gpu_device) as e:
+        se.append_packed(d)
+        e.append_packed(d)
+        nw = R // 4
+        a, b = se.wave_commit(1, nw), e.wave_commit(1, nw)
+        assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
+        for w in range(1, nw + 1):
+            for dec in (0, max(0, w - 3)):
+                assert se.wave_ready(w, dec) == e.wave_ready(w, dec)
+        for cur in (R, 20, 3, 0):
+            stack = [(4 * w - 3, 1) for w in range(1, nw + 1)] + [(9, 5), (9, 5), (30, 17)]
+            for mode in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+                tot, pc, pd = se.order_vertices(stack, cur, mode)
+                _, pc2, pd2 = e.order_vertices(stack, cur, mode, cap=0)
+                assert (pc == pc2).all() and (pd == pd2).all() and tot == int(pc2.sum()), (cur, mode)
+
+
+def test_shard_replay_leader_coin(gpu_device):
+    """A caller's leader table (chooseLeader as a coin) through the sharded commit, chains and pops."""
+    rng = np.random.default_rng(91)
+    n, R = 40, 40
+    d = random_dag(rng, n, R, p_present=0.9, p_s=0.8, p_w=0.3)
+    leaders = [int(x) for x in rng.integers(1, n + 1, size=R // 4 + 1)]
+    bs = oracle.PDag(d, leaders=leaders)
+    with ShardEngine(n, 13, R + 1, gpu_device, nshards=2) as se:
+        se.append_packed(d)
+        se.set_leader_coin(L.DR_LEADER_TABLE, table=leaders)
+        for cm, dm in MODES:
+            _same_replay(se.replay(R // 4, cm, dm), bs.replay(13, R // 4, cm, dm))
+
+
+def test_shard_replay_c4_full(gpu_device):
+    """BASELINE config 4 (n=1024 x 4000 rounds) on the column-sharded DAG at G = 1, 2, 4, 8
+    (local mode): the whole replay equals the committed golden vectors (ref and paper)."""
+    g = load_large()["c4"]
+    cfg = CONFIGS["c4"]
+    d = generate(cfg, nthreads=16)
+    assert dag_fingerprint(d) == g["dag"], "generator drift"
+    for G in (1, 2, 4, 8):
+        with ShardEngine(cfg.n, cfg.faulty, d.nrounds, gpu_device, nshards=G) as se:
+            se.append_packed(d)
+            _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
+            if G in (1, 8):
+                _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_PAPER), g["persistent_paper"])
+
+
+def _check_golden(got, want):
+    assert "".join(str(int(x)) for x in got.commit) == want["commit"]
+    assert got.vcount.tolist() == want["vcount"]
+    assert got.push_off.tolist() == want["push_off"]
+    assert got.push_wave.tolist() == want["push_wave"]
+    for k in ("pop_count", "pop_digest", "pop_edges"):
+        w = np.asarray([int(x) for x in want[k]], dtype=np.uint64)
+        bad = np.nonzero(getattr(got, k) != w)[0]
+        assert len(bad) == 0, f"{k}: {len(bad)} pops differ, first at {bad[:5].tolist()}"
+    assert (got.commit_edges, got.chain_edges, got.deliver_edges) == \
+        (int(want["commit_edges"]), int(want["chain_edges"]), int(want["deliver_edges"]))
