@@ -295,14 +295,18 @@ def commit_split(dist, rank: int, world: int, local: int, want_commit=None, want
 
 
 def colshard_child(args):
-    """One rank of the process-column sharded sweep: every rank
+    """One rank of the process-column sharded path: every rank
     holds 1/N of the target columns; the frontier is all-gathered over RCCL each round.
-    Workload: the full causal-history reach sets (strong + weak, rounds 0..leader) of
-    the 64 newest wave leaders of the C4 DAG -- the sets orderVertices delivers."""
+    Workloads: the full causal-history reach sets (strong + weak, rounds 0..leader) of
+    the 64 newest wave leaders, then the whole replay (dr_shard_replay: waveReady
+    votes and chains, orderVertices cones and emission), both checked on rank 0
+    against the unsharded engine."""
     import numpy as np
 
     from dag_rider_amd.gen import CONFIGS, generate
     from dag_rider_amd.shard import ShardEngine
+
+    from dag_rider_amd import _lib as L
 
     cfg = CONFIGS["c4"]
     d = generate(cfg, nthreads=CPU_THREADS)
@@ -317,7 +321,16 @@ def colshard_child(args):
         got = se.reach_sets(froms, bottoms, False)
         runs.append(se.stats())
     st = min(runs, key=lambda x: x["ms"])
-    out = dict(st, nshards=args.cs_world, queries=len(froms), info=se.info())
+    # the whole replay on the sharded DAG: commit votes (3 all-gathers), chains and
+    # delivery cones (one all-gather per round), emission on every rank
+    t0 = time.perf_counter()
+    rep = se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+    rep_ms = (time.perf_counter() - t0) * 1e3
+    rst = se.stats()
+    out = dict(st, nshards=args.cs_world, queries=len(froms), info=se.info(),
+               replay=dict(ms=rep_ms, phases_ms=rep.ms, sweep_rounds=rst["rounds"],
+                           exchange_bytes=rst["exchange_bytes"], edges=rep.total_edges,
+                           commits=int(rep.commit.sum()), pops=len(rep.pop_count)))
     se.close()
     if args.cs_rank == 0:
         from dag_rider_amd.engine import Engine
@@ -325,8 +338,14 @@ def colshard_child(args):
         with Engine(cfg.n, cfg.faulty, d.nrounds, args.cs_device) as e:
             e.append_packed(d)
             ref = e.reach_sets(froms, bottoms, False)
+            rr = e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
         out["verify_vs_unsharded"] = bool(all((a == b).all() for a, b in zip(got, ref)))
         out["reach_bits"] = int(sum(int(np.unpackbits(a.view(np.uint8)).sum()) for a in got))
+        out["replay"]["verify_vs_unsharded"] = bool(
+            (rep.commit == rr.commit).all() and (rep.vcount == rr.vcount).all()
+            and (rep.push_wave == rr.push_wave).all() and (rep.pop_count == rr.pop_count).all()
+            and (rep.pop_digest == rr.pop_digest).all() and (rep.pop_edges == rr.pop_edges).all()
+            and rep.total_edges == rr.total_edges)
     print(json.dumps(out), flush=True)
 
 

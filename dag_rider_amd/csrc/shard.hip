@@ -162,9 +162,35 @@ __device__ __forceinline__ RMasks round_masks(const QInfo *q, int nq, int r, int
   return RMasks{__ballot(e), __ballot(o), __ballot(i), __ballot(k)};
 }
 
-// Steps 1-4 of round r for local shard l (see the file comment).  ft = full FT_r.
+// The full frontier of round r, read per source.  FtGathered: the FT_r buffer
+// (produced by step 5, or all-gathered).  FtPending (the persistent local-mode
+// kernel): straight from the pending ring slot of round r -- every shard's
+// columns are in this context -- plus the queries that start at r, so a round
+// needs one grid barrier instead of two.
+struct FtGathered {
+  const u64 *ft;
+  __device__ __forceinline__ u64 operator()(int s) const { return dr::ld_agent(&ft[s]); }
+};
+struct FtPending {
+  const u64 *pend;
+  const QInfo *qs;
+  int depth, C, slot;
+  u64 starts;  // queries whose top is r
+  __device__ __forceinline__ u64 operator()(int s) const {
+    const int l = s / C;
+    u64 v = dr::ld_agent(&pend[((size_t)l * depth + slot) * C + (s - l * C)]);
+    for (u64 im = starts; im; im &= im - 1) {
+      const int b = __builtin_ctzll(im);
+      if (qs[b].src0 == s) v |= 1ULL << b;
+    }
+    return v;
+  }
+};
+
+// Steps 1-4 of round r for local shard l (see the file comment).  ft(s) = FT_r[s].
 // ledges: LDS chain-edge accumulators; writer: the one thread that records pushes.
-__device__ void sweep_round(const ShardArgs &a, const u64 *ft, int r, int l, int gw, int nwv, int lane,
+template <class Ft>
+__device__ void sweep_round(const ShardArgs &a, const Ft &ft, int r, int l, int gw, int nwv, int lane,
                             const RMasks &m, u64 chainq, u64 *ledges, bool writer) {
   const int C = a.C;
   u64 *pend = a.pend + (size_t)l * a.depth * C;
@@ -174,7 +200,7 @@ __device__ void sweep_round(const ShardArgs &a, const u64 *ft, int r, int l, int
   if (m.chk && ((r - 1) & 3) == 0) {
     const int w2 = ((r - 1) >> 2) + 1;
     L = (w2 < a.nlead ? (int)a.lead[w2] : 1) - 1;
-    if ((a.pres[(size_t)r * a.W + (L >> 6)] >> (L & 63)) & 1ULL) rst = dr::ld_agent(&ft[L]) & m.chk;
+    if ((a.pres[(size_t)r * a.W + (L >> 6)] >> (L & 63)) & 1ULL) rst = ft(L) & m.chk;
     if (writer)
       for (u64 x = rst; x; x &= x - 1) {
         const int b = __builtin_ctzll(x);
@@ -188,7 +214,7 @@ __device__ void sweep_round(const ShardArgs &a, const u64 *ft, int r, int l, int
   for (int it = gw; it < nchunks * a.WSs; it += nwv) {
     const int s0 = (it / a.WSs) * 64, tw = it % a.WSs;
     const int s = s0 + lane;
-    u64 mv = s < a.n ? dr::ld_agent(&ft[s]) : 0ULL;
+    u64 mv = s < a.n ? ft(s) : 0ULL;
     if (s != L) mv &= ~rst;
     if (l == 0 && tw == 0) {
       if (m.out) {
@@ -234,7 +260,7 @@ __device__ void sweep_round(const ShardArgs &a, const u64 *ft, int r, int l, int
       if (e < e1) {
         const uint32_t w = a.weak[e];
         const int src = (int)((w >> 11) & 2047u);
-        mv = dr::ld_agent(&ft[src]) & m.exp;
+        mv = ft(src) & m.exp;
         if (src != L) mv &= ~rst;
         const int slot = (r - (int)(w >> 22)) & (a.depth - 1);
         key = (uint32_t)slot * (uint32_t)C + (w & 2047u);
@@ -305,7 +331,11 @@ __device__ __forceinline__ void flush_edges(const ShardArgs &a, const u64 *ledge
   if ((int)threadIdx.x < a.nq && ledges[threadIdx.x]) atomicAdd(&a.cedges[threadIdx.x], ledges[threadIdx.x]);
 }
 
-// Local mode: a whole batch, rounds T..Bm, in one cooperative launch.
+// Local mode: a whole batch, rounds T..Bm, in one cooperative launch.  Round r
+// reads its frontier from the pending ring slot of r (FtPending), clears the slot
+// of r+1 that the previous round read (the ring has depth >= dmax + 2, so no
+// expansion of round r or r+1 targets that slot), expands, and ends at one grid
+// barrier.
 __global__ void __launch_bounds__(SH_NT) k_shard_sweep(ShardArgs a, int T, int Bm) {
   __shared__ QInfo qs[SH_BATCH];
   __shared__ u64 ledges[SH_BATCH];
@@ -319,17 +349,20 @@ __global__ void __launch_bounds__(SH_NT) k_shard_sweep(ShardArgs a, int T, int B
   const int gthreads = (int)nblk * SH_NT;
   const int gtid = (int)(blockIdx.y * gridDim.x + blockIdx.x) * SH_NT + (int)threadIdx.x;
   const bool writer = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+  const int dm = a.depth - 1;
   unsigned target = 0;
   for (int r = T; r >= Bm; r--) {
     const RMasks m = round_masks(qs, a.nq, r, lane);
-    sweep_round(a, (r & 1) ? a.ftb1 : a.ftb0, r, l, gw, nwv, lane, m, chainq, ledges, writer);
+    const u64 starts = __ballot(lane < a.nq && qs[lane].top == r);
+    if (r < T)
+      for (int t = gtid; t < a.nlocal * a.C; t += gthreads) {
+        const int ll = t / a.C;
+        __hip_atomic_store(&a.pend[((size_t)ll * a.depth + ((r + 1) & dm)) * a.C + (t - ll * a.C)], 0ULL,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // same coherence point as the ORs
+      }
+    sweep_round(a, FtPending{a.pend, qs, a.depth, a.C, r & dm, starts}, r, l, gw, nwv, lane, m, chainq, ledges,
+                writer);
     if (r - 1 < Bm) break;
-    if (!grid_sync(a.bar, nblk, target, a.err)) break;
-    u64 *ftn = ((r - 1) & 1) ? a.ftb1 : a.ftb0;
-    for (int t = gtid; t < a.nlocal * a.C; t += gthreads) {
-      const int ll = t / a.C, tc = t - ll * a.C;
-      ftn[(size_t)(a.shard0 + ll) * a.C + tc] = produce_col(a, qs, ll, tc, r - 1, m.inj);
-    }
     if (!grid_sync(a.bar, nblk, target, a.err)) break;
   }
   flush_edges(a, ledges);
@@ -349,7 +382,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_round(ShardArgs a, int r, int p
   const int gw = blockIdx.x * (SH_NT / 64) + (threadIdx.x >> 6);
   const RMasks m = round_masks(qs, a.nq, r, lane);
   const bool writer = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
-  sweep_round(a, (r & 1) ? a.ftb1 : a.ftb0, r, l, gw, nwv, lane, m, chainq, ledges, writer);
+  sweep_round(a, FtGathered{(r & 1) ? a.ftb1 : a.ftb0}, r, l, gw, nwv, lane, m, chainq, ledges, writer);
   flush_edges(a, ledges);
   if (!produce) return;
   __syncthreads();
@@ -672,7 +705,9 @@ int sweep_batch(dr_shard *c, std::vector<QInfo> &dq, int strong_only) {
     int per_cu = 0, ncu = 0;
     SHCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_shard_sweep, SH_NT, 0));
     SHCHK(c, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev));
-    const int cap = std::max(1, per_cu * ncu / std::max(1, c->nlocal));
+    // every workgroup arrives at each round's barrier: keep the grid small (the
+    // round's work is a few hundred waves) and resident
+    const int cap = std::max(1, std::min(per_cu * ncu, 128) / std::max(1, c->nlocal));
     gx = std::max(1, std::min(gx, cap));
     SHCHK(c, hipMemsetAsync(c->bar.p, 0, 4, c->stream));
     void *args[] = {&a, &T, &Bm};
@@ -1210,7 +1245,7 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
   c->weak_dirty = true;
   c->dmax = dmax;
   int depth = 2;
-  while (depth <= dmax) depth <<= 1;
+  while (depth < dmax + 2) depth <<= 1;  // k_shard_sweep clears a slot one round after reading it
   if (depth != c->depth || !c->pend.p) {
     SHCHK(c, c->pend.ensure((size_t)c->nlocal * depth * C * 8));
     c->depth = depth;

@@ -277,18 +277,35 @@ int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode, int d
   o->n_push = np;
   uint64_t del_e = 0;
   if (deliver_mode == OR_DELIVER_REF && !o->ids) {
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : del_e)
-    for (int64_t j = 0; j < npop; j++) {
-      int top = 4 * (pops[j].leader_wave - 1) + 1;
+    /* a pop's outputs depend only on its leader (the emission window 1..min(cur,
+     * top) is 1..top in a replay): one cone per distinct leader wave, which keeps
+     * the literal-chain replay (O(w^2) pops) tractable */
+    uint64_t *wc = (uint64_t *)calloc((size_t)nwaves + 1, sizeof(uint64_t));
+    uint64_t *wd = (uint64_t *)calloc((size_t)nwaves + 1, sizeof(uint64_t));
+    uint64_t *we = (uint64_t *)calloc((size_t)nwaves + 1, sizeof(uint64_t));
+    uint8_t *need = (uint8_t *)calloc((size_t)nwaves + 1, 1);
+    for (int64_t j = 0; j < npop; j++) need[pops[j].leader_wave] = 1;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int lw = 1; lw <= nwaves; lw++) {
+      if (!need[lw]) continue;
+      int top = 4 * (lw - 1) + 1;
       uint64_t *m = (uint64_t *)calloc((size_t)(top + 1) * W, sizeof(uint64_t));
-      or_vid from = {top, or_leader(p->leader, p->nleader, pops[j].leader_wave)};
-      uint64_t e = 0;
-      or_bs_cone(p, from, 0, 0, m, &e);
-      emit_pop(p, m, 0, top, pops[j].cur_round, &o->pop_count[j], &o->pop_digest[j], NULL, 0, NULL);
-      o->pop_edges[j] = e;
-      del_e += e;
+      or_vid from = {top, or_leader(p->leader, p->nleader, lw)};
+      or_bs_cone(p, from, 0, 0, m, &we[lw]);
+      emit_pop(p, m, 0, top, top, &wc[lw], &wd[lw], NULL, 0, NULL);
       free(m);
     }
+    for (int64_t j = 0; j < npop; j++) {
+      const int lw = pops[j].leader_wave;
+      o->pop_count[j] = wc[lw];
+      o->pop_digest[j] = wd[lw];
+      o->pop_edges[j] = we[lw];
+      del_e += we[lw];
+    }
+    free(wc);
+    free(wd);
+    free(we);
+    free(need);
   } else {
     /* sequential: needed for the ids list order and for paper-mode dedup */
     uint64_t *D = NULL;
