@@ -12,6 +12,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DR_LIB_VARIANT=timing loads the profiling build (tools/sweep_timing.py only)
 LIB_PATH = os.path.join(_HERE, "libdagrider_gpu_timing.so" if os.environ.get("DR_LIB_VARIANT") == "timing"
                         else "libdagrider_gpu.so")
+# kernel experiments only (never set by tests, smoke or the bench): an alternative build
+LIB_PATH = os.environ.get("DR_LIB_PATH_EXPT", LIB_PATH)
 
 DR_OK, DR_E_INVAL, DR_E_CAPACITY, DR_E_HIP, DR_E_RCCL, DR_E_CONTRACT, DR_E_STATE = 0, -1, -2, -3, -4, -5, -6
 DR_CHAIN_LITERAL, DR_CHAIN_PERSISTENT = 0, 1

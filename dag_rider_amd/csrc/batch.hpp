@@ -221,6 +221,9 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       u64 m = __ballot((qf[i] | qs[i]) != 0ULL);
+#ifdef DR_C5_EXPT_SKIP_Q
+      m = 0;
+#endif
       while (m) {
         const int l = __builtin_ctzll(m);
         m &= m - 1;
@@ -313,6 +316,9 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
       if ((uint32_t)lane < m) SL[lane] = J.slot_src[c0 + lane];
       if ((uint32_t)lane + 64 < m) SL[lane + 64] = J.slot_src[c0 + lane + 64];
       __syncthreads();
+#ifdef DR_C5_EXPT_SKIP_EMIT
+      if (m) continue;
+#endif
       for (uint32_t i = 0; i < m; i++) {
         const int s = SL[i];
         if (s == 0) continue;  // ghost slot {0,0}: never reached

@@ -9,7 +9,7 @@ import pytest
 from dag_rider_amd import _lib as L
 from dag_rider_amd.engine import Engine
 from dag_rider_amd.gen import CONFIGS, generate
-from dagutil import dag_fingerprint, load_large
+from dagutil import dag_fingerprint, load_large, replay_fingerprint
 
 pytestmark = pytest.mark.gpu
 
@@ -41,3 +41,22 @@ def test_large_config_golden(gpu_device, name):
         _check(e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
         e.set_device_plan(True)
         _check(e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_PAPER), g["persistent_paper"])
+
+
+@pytest.mark.parametrize("name", ["c3", "c4"])
+def test_large_config_golden_literal_chain(gpu_device, name):
+    """DR_CHAIN_LITERAL (the reference's Q1: decidedWave never advances, every commit
+    chains down to wave 1, O(w^2) pops) on the full C3 / C4 DAG: replay fingerprint,
+    push count and edge totals equal the bitset oracle's."""
+    g = load_large()[name]
+    cfg = CONFIGS[name]
+    d = generate(cfg, nthreads=16)
+    assert dag_fingerprint(d) == g["dag"], "generator drift"
+    want = g["literal_ref"]
+    with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
+        e.append_packed(d)
+        got = e.replay(cfg.nwaves, L.DR_CHAIN_LITERAL, L.DR_DELIVER_REF)
+    assert len(got.push_wave) == want["n_push"]
+    assert (got.commit_edges, got.chain_edges, got.deliver_edges) == \
+        (int(want["commit_edges"]), int(want["chain_edges"]), int(want["deliver_edges"]))
+    assert replay_fingerprint(got) == want["fingerprint"]

@@ -201,3 +201,15 @@ def test_large_golden_pins_generator_and_oracle():
                             ("literal_ref", oracle.CHAIN_LITERAL, oracle.DELIVER_REF),
                             ("persistent_paper", oracle.CHAIN_PERSISTENT, oracle.DELIVER_PAPER)):
             assert replay_fingerprint(bs.replay(cfg.faulty, cfg.nwaves, cm, dm, nthreads=1)) == c5[key][i]
+
+
+def test_large_golden_pins():
+    """The committed full-size vectors carry the literal-restatement prefix checks made
+    when they were written (8 C3 waves, 4 C4 waves) and the literal-chain fingerprints."""
+    from dagutil import load_large
+
+    g = load_large()
+    assert g["c3"]["literal_prefix_waves"] >= 8 and g["c4"]["literal_prefix_waves"] >= 4
+    for name in ("c3", "c4"):
+        lit = g[name]["literal_ref"]
+        assert len(lit["fingerprint"]) == 32 and lit["n_push"] > len(g[name]["persistent_ref"]["push_wave"])
