@@ -19,12 +19,21 @@
 //      degrees go to a per-DAG scratch.
 //   3. chains (process.go:341-350) from the leaders' Qs: wave w' is pushed
 //      after leader L iff L's bit is in Qs(leader(w')); pops = reverse pushes.
-//   4. bottom-up emission, lane b = leader wave b+1: for each round's slots in
-//      order, vertex v is delivered by b (REF) iff b in Qf(v), or (PAPER) iff
-//      additionally no leader popped before b's first pop is in Qf(v); position
-//      counters give the order-sensitive digest.  Chain edges
-//      come from per-leader prefix sums of strong degrees over Qs at the leader
-//      rounds.
+//   4. bottom-up emission.  Vertex v is delivered by leader b (REF) iff b in
+//      Qf(v), or (PAPER) iff additionally no leader popped before b's first pop
+//      is in Qf(v).  A leader's contribution of a round is computed with lanes =
+//      slots: ballot ranks give the positions, the order-sensitive digest
+//       and edge sums are wave reductions.  REF memo (nw <= 63):
+//      bit 63 of Qf is the canonical cone K (every present vertex of round T);
+//      below the first round where b's cone differs from K, b's prefix equals K's,
+//      so only K and the leaders that already differ (those a few rounds under
+//      their top) are computed per round (the same identity as the
+//      engine's memo).  PAPER computes a leader only in rounds where it delivers
+//      something.  Chain edges: per-leader sums of strong degrees over Qs, only
+//      in the rounds the leader's chain segments cover.
+//   Qs bits are kept only in the rounds the chains can inspect (a leader's bit
+//   dies below its chain's floor round), and sources with an empty Qs skip the
+//   strong-only half of the expansion.
 // Supported: n <= 128, nw <= 64, weak deltas < ring depth (<= 32), no far edges.
 #pragma once
 #include "kernels.hpp"
@@ -62,8 +71,9 @@ constexpr int kSmallMaxPops = 64 * 65 / 2;  // literal chains: wave w pushes up 
 // dynamic LDS of k_replay_small: the weak ring (rsl slots of 128 u64) or the
 // later phases' arrays, whichever is larger
 template <bool PAPER, bool PERSIST>
-constexpr int small_late_bytes() {
-  return 64 * 65 + (((PERSIST ? 64 : kSmallMaxPops) + 255) & ~255) + 64 * (PAPER ? 6 : 3) * 8;
+constexpr int small_late_bytes() {  // coef, pop list, per-leader results, chain sums, paper "before" masks
+  return 64 * 65 + (((PERSIST ? 64 : kSmallMaxPops) + 255) & ~255) + 64 * (PAPER ? 6 : 3) * 8 + 64 * 8 +
+         (PAPER ? 64 * 8 : 0);
 }
 template <bool PAPER, bool PERSIST>
 inline size_t small_lds_bytes(int rsl) {
@@ -83,20 +93,24 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   constexpr int kMaxPops = PERSIST ? 64 : kSmallMaxPops;
   constexpr int RS = PAPER ? 6 : 3;  // per-leader results kept
   constexpr int kCoefB = 64 * 65, kPopB = (kMaxPops + 255) & ~255, kResB = 64 * RS * 8;
-  static_assert(kCoefB + kPopB + kResB == small_late_bytes<PAPER, PERSIST>(), "LDS layout");
-  (void)kResB;
+  static_assert(kCoefB + kPopB + kResB + 64 * 8 + (PAPER ? 64 * 8 : 0) == small_late_bytes<PAPER, PERSIST>(),
+                "LDS layout");
+  // REF memo: bit 63 of Qf carries the canonical cone K (needs a free leader bit)
+  const bool kmemo = !PAPER && nw <= 63;
   extern __shared__ __attribute__((aligned(16))) u64 arena[];                  // small_lds_bytes(rsl)
   u64 *ring = arena;                                                            // [rsl * 128], phase 2
   int8_t *coef = reinterpret_cast<int8_t *>(arena);                             // [64 * 65], phases 3-4
   uint8_t *pop_lead = reinterpret_cast<uint8_t *>(arena) + kCoefB;              // [kSmallMaxPops], 3-5
   u64 *res = reinterpret_cast<u64 *>(reinterpret_cast<char *>(arena) + ((kCoefB + kPopB + 7) & ~7));  // 4-5
-  __shared__ u64 QF[128], QS[128];
+  u64 *CS = res + 64 * RS;   // [64] chain: running strong-degree sums over Qs, phase 4
+  u64 *BEF = CS + 64;        // [64] PAPER: leaders first popped before b, phase 4
+  __shared__ u64 QF[128];
   __shared__ uint32_t DG[128];
   __shared__ u64 QL[64];
   __shared__ int32_t vc_s[64];
   __shared__ int16_t first_pop[64];
+  __shared__ int16_t qs_floor[64];  // lowest round where leader b's strong cone is still inspected
   __shared__ int8_t lst[64];
-  __shared__ uint16_t SL[128];
   const int lane = threadIdx.x;
   const int jb = blockIdx.x;
   if (jb >= njobs) return;
@@ -156,27 +170,47 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
 
   // ---------------- 2. top-down Q pass ----------------
   for (int i = lane; i < rsl * 128; i += 64) ring[i] = 0;
-  u64 qf[2] = {0, 0}, qs[2] = {0, 0};
+  // chains (process.go:341-350) inspect leader b's strong cone only down to the
+  // floor round of the commit whose chain can push b: 4*decidedWave + 1
+  qs_floor[lane] = 0x7fff;
   __syncthreads();
+  if (lane == 0) {
+    int lastc = 0;
+    for (int w = 1; w <= nw; w++)
+      if ((commit_mask >> (w - 1)) & 1ULL) {
+        for (int b = lastc + 1; b <= w; b++) qs_floor[b - 1] = (int16_t)(chain_persistent ? 4 * lastc + 1 : 1);
+        lastc = w;
+      }
+  }
+  __syncthreads();
+  const int my_floor = qs_floor[lane];
+  u64 qf[2] = {0, 0}, qs[2] = {0, 0};
   for (int r = T; r >= 1; r--) {
+    const u64 alive = __ballot(lane < nw && my_floor <= r);
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
       qf[i] |= ring[(r % rsl) * 128 + v];
       ring[(r % rsl) * 128 + v] = 0;
+      qs[i] &= alive;
+    }
+    if (kmemo && r == T) {  // K: every present vertex of the top round
+      if ((pres_word(T, 0) >> lane) & 1ULL) qf[0] |= 1ULL << 63;
+      if ((pres_word(T, 1) >> lane) & 1ULL) qf[1] |= 1ULL << 63;
     }
     if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its bit at the leader's source
       const int w = (r - 1) / 4 + 1;
       const int l = J.lead[w] - 1;
       if ((lead_mask >> (w - 1)) & 1ULL) {
         if (lane == (l & 63)) {  // register arrays: constant indices only
+          const u64 sb = (alive >> (w - 1)) & 1ULL;
           if (l < 64) {
             qf[0] |= 1ULL << (w - 1);
-            qs[0] |= 1ULL << (w - 1);
+            qs[0] |= sb << (w - 1);
             QL[w - 1] = qs[0];
           } else {
             qf[1] |= 1ULL << (w - 1);
-            qs[1] |= 1ULL << (w - 1);
+            qs[1] |= sb << (w - 1);
             QL[w - 1] = qs[1];
           }
         }
@@ -187,9 +221,6 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
     u64 ra[2], rb[2];
     row(r, lane, ra[0], rb[0]);
     row(r, lane + 64, ra[1], rb[1]);
-    QF[lane] = qf[0];
-    QF[lane + 64] = qf[1];
-    __syncthreads();
     // weak columns of round r: Qf of the column's sources into the pending round
     {
       const uint32_t c0 = J.wc_roff[r], c1 = J.wc_roff[r + 1];
@@ -217,23 +248,26 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
       }
     }
     // strong edges: Q of round r-1, lane u owns targets u and u+64
+    // (Qs is a subset of Qf per vertex: the strong-only half runs only for the
+    // sources with a live Qs)
     u64 nf0 = 0, nf1 = 0, ns0 = 0, ns1 = 0;
 #pragma unroll
     for (int i = 0; i < 2; i++) {
-      u64 m = __ballot((qf[i] | qs[i]) != 0ULL);
-#ifdef DR_C5_EXPT_SKIP_Q
-      m = 0;
-#endif
+      u64 m = __ballot(qf[i] != 0ULL);
       while (m) {
         const int l = __builtin_ctzll(m);
         m &= m - 1;
-        const u64 a = readlane64(ra[i], l), b = readlane64(rb[i], l);
-        const u64 f = readlane64(qf[i], l), s = readlane64(qs[i], l);
-        const bool ha = (a >> lane) & 1ULL, hb = (b >> lane) & 1ULL;
-        nf0 |= ha ? f : 0ULL;
-        ns0 |= ha ? s : 0ULL;
-        nf1 |= hb ? f : 0ULL;
-        ns1 |= hb ? s : 0ULL;
+        const u64 a = readlane64(ra[i], l), b = readlane64(rb[i], l), f = readlane64(qf[i], l);
+        nf0 |= ((a >> lane) & 1ULL) ? f : 0ULL;
+        nf1 |= ((b >> lane) & 1ULL) ? f : 0ULL;
+      }
+      u64 ms = __ballot(qs[i] != 0ULL);
+      while (ms) {
+        const int l = __builtin_ctzll(ms);
+        ms &= ms - 1;
+        const u64 a = readlane64(ra[i], l), b = readlane64(rb[i], l), sq = readlane64(qs[i], l);
+        ns0 |= ((a >> lane) & 1ULL) ? sq : 0ULL;
+        ns1 |= ((b >> lane) & 1ULL) ? sq : 0ULL;
       }
     }
     qf[0] = nf0;
@@ -287,70 +321,145 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   if (lane == 0) J.push_off[nw] = (uint32_t)npush;
   __syncthreads();
 
-  // ---------------- 4. bottom-up emission, lane b = leader wave b+1 ----------------
-  const int b = lane;
-  const int myfirst = first_pop[b];
-  u64 before = 0;  // leaders first popped before b (PAPER: they own shared vertices)
-  for (int x = 0; x < 64; x++) {
-    const int fp = first_pop[x];
-    if (fp >= 0 && myfirst >= 0 && fp < myfirst) before |= 1ULL << x;
+  // ---------------- 4. bottom-up emission ----------------
+  // lane b = leader wave b+1 for the per-leader bookkeeping
+  const int myfirst = first_pop[lane];
+  {
+    u64 bef = 0;  // leaders first popped before b (PAPER: they own shared vertices)
+    for (int x = 0; x < 64; x++) {
+      const int fp = first_pop[x];
+      if (fp >= 0 && myfirst >= 0 && fp < myfirst) bef |= 1ULL << x;
+    }
+    if (PAPER) BEF[lane] = bef;
+    CS[lane] = 0;
+    for (int k = 0; k < RS; k++) res[lane * RS + k] = 0;
   }
-  u64 kr = 0, dr_ = 0, er = 0, kp = 0, dp = 0, ep = 0, cs = 0, chain = 0;
+  // chain segments of leader b cover rounds (lo_b, hi_b]
+  int seg_lo = 0x7fff, seg_hi = -1;
+  for (int x = 0; x <= 64; x++)
+    if (coef[lane * 65 + x]) {
+      seg_lo = min(seg_lo, 4 * (x - 1) + 1);
+      seg_hi = max(seg_hi, 4 * (x - 1) + 1);
+    }
+  const u64 popped = __ballot(myfirst >= 0);
+  u64 neq = kmemo ? 0ULL : ~0ULL;   // leaders whose cone differs from K in some round <= r
+  u64 kK = 0, dK = 0, eK = 0;       // K's count, digest, edges through round r-1
+  u64 chain = 0;
+  // one leader's (or K's, b = 63) delivered vertices of round r in slot order,
+  // positions from k0: count, digest, edges (wave-uniform); lanes = slots
+  auto contrib = [&](int r, int b, u64 k0, u64 befb, u64 &cnt, u64 &dg, u64 &ed) {
+    const uint32_t sa = J.slot_off[r], sb = J.slot_off[r + 1];
+    u64 k = k0, dacc = 0, eacc = 0;
+    for (uint32_t c0 = sa; c0 < sb; c0 += 64) {
+      const uint32_t sl = c0 + lane;
+      const int s = sl < sb ? (int)J.slot_src[sl] : 0;  // 0: ghost slot {0,0}, never reached
+      const u64 f = s > 0 ? QF[s - 1] : 0ULL;
+      const bool in = ((f >> b) & 1ULL) && !(f & befb);
+      const u64 bal = __ballot(in);
+      if (in) {
+        dacc += digest_term((uint32_t)r, (uint32_t)s, k + (u64)__popcll(bal & ((1ULL << lane) - 1ULL)));
+        eacc += DG[s - 1] >> 16;
+      }
+      k += (u64)__popcll(bal);
+    }
+    cnt = k - k0;
+    dg = wave_sum(dacc);
+    ed = wave_sum(eacc);
+  };
   for (int r = 1; r <= T; r++) {
     __syncthreads();
+    u64 f2[2] = {0, 0}, s2[2] = {0, 0};
+    uint32_t d2[2] = {0, 0};
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
       if (v < n) {
         const size_t at = (size_t)r * n + v;
-        QF[v] = J.qf[at];
-        QS[v] = J.qs[at];
-        DG[v] = J.deg[at];
+        f2[i] = J.qf[at];
+        s2[i] = J.qs[at];
+        d2[i] = J.deg[at];
+        QF[v] = f2[i];
+        DG[v] = d2[i];
       }
     }
     __syncthreads();
-    const uint32_t sa = J.slot_off[r], sb = J.slot_off[r + 1];
-    for (uint32_t c0 = sa; c0 < sb; c0 += 128) {  // slots staged in LDS, 128 at a time
-      const uint32_t m = min(128u, sb - c0);
+    const u64 active = popped & ~0ULL & __ballot(lane < nw && 4 * lane + 1 >= r);  // leaders whose top >= r
+    if (!PAPER) {
+      if (kmemo) {  // leaders whose cone first differs from K in round r take K's prefix
+        u64 x = 0;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+          if ((pres_word(r, i) >> lane) & 1ULL) x |= f2[i] ^ (((f2[i] >> 63) & 1ULL) ? ~0ULL : 0ULL);
+        const u64 newly = wave_or(x) & active & ~neq;
+        if ((newly >> lane) & 1ULL) {
+          res[lane * RS + 0] = kK;
+          res[lane * RS + 1] = dK;
+          res[lane * RS + 2] = eK;
+        }
+        neq |= newly;
+        u64 c, d, e;
+        contrib(r, 63, kK, 0ULL, c, d, e);
+        kK += c;
+        dK += d;
+        eK += e;
+      }
       __syncthreads();
-      if ((uint32_t)lane < m) SL[lane] = J.slot_src[c0 + lane];
-      if ((uint32_t)lane + 64 < m) SL[lane + 64] = J.slot_src[c0 + lane + 64];
-      __syncthreads();
-#ifdef DR_C5_EXPT_SKIP_EMIT
-      if (m) continue;
-#endif
-      for (uint32_t i = 0; i < m; i++) {
-        const int s = SL[i];
-        if (s == 0) continue;  // ghost slot {0,0}: never reached
-        const u64 f = QF[s - 1], g = QS[s - 1];
-        const uint32_t d = DG[s - 1];
-        if ((g >> b) & 1ULL) cs += d & 0xFFFFu;
-        if ((f >> b) & 1ULL) {
-          const u64 full = d >> 16;
-          dr_ += digest_term((uint32_t)r, (uint32_t)s, kr);
-          kr++;
-          er += full;
-          if (PAPER && !(f & before)) {
-            dp += digest_term((uint32_t)r, (uint32_t)s, kp);
-            kp++;
-            ep += full;
-          }
+      for (u64 m = neq & active; m; m &= m - 1) {
+        const int b = __builtin_ctzll(m);
+        u64 c, d, e;
+        contrib(r, b, res[b * RS + 0], 0ULL, c, d, e);
+        __syncthreads();
+        if (lane == 0) {
+          res[b * RS + 0] += c;
+          res[b * RS + 1] += d;
+          res[b * RS + 2] += e;
+        }
+        __syncthreads();
+      }
+      if (kmemo && ((r - 1) & 3) == 0) {  // a leader equal to K up to its own round: K's prefix
+        const int b = (r - 1) / 4;
+        if (lane == 0 && b < nw && ((popped >> b) & 1ULL) && !((neq >> b) & 1ULL)) {
+          res[b * RS + 0] = kK;
+          res[b * RS + 1] = dK;
+          res[b * RS + 2] = eK;
         }
       }
+    } else {
+      for (u64 m = active; m; m &= m - 1) {
+        const int b = __builtin_ctzll(m);
+        const u64 befb = BEF[b];
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+          any |= ((pres_word(r, i) >> lane) & 1ULL) && ((f2[i] >> b) & 1ULL) && !(f2[i] & befb);
+        if (__ballot(any) == 0ULL) continue;
+        u64 c, d, e;
+        contrib(r, b, res[b * RS + 3], befb, c, d, e);
+        __syncthreads();
+        if (lane == 0) {
+          res[b * RS + 3] += c;
+          res[b * RS + 4] += d;
+          res[b * RS + 5] += e;
+        }
+        __syncthreads();
+      }
     }
+    // chain edges: strong-degree sums over Qs in the leaders' segment rounds
+    for (u64 m = __ballot(lane < nw && seg_lo < r && r <= seg_hi); m; m &= m - 1) {
+      const int b = __builtin_ctzll(m);
+      u64 x = 0;
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+        if ((s2[i] >> b) & 1ULL) x += d2[i] & 0xFFFFu;
+      x = wave_sum(x);
+      if (lane == 0) CS[b] += x;
+    }
+    __syncthreads();
     if (((r - 1) & 3) == 0) {
       const int x = (r - 1) / 4 + 1;
-      const int c = coef[b * 65 + x];
-      if (c) chain += (u64)(int64_t)c * cs;
+      const int c = coef[lane * 65 + x];
+      if (c) chain += (u64)(int64_t)c * CS[lane];
     }
-  }
-  res[b * RS + 0] = kr;
-  res[b * RS + 1] = dr_;
-  res[b * RS + 2] = er;
-  if (PAPER) {
-    res[b * RS + 3] = kp;
-    res[b * RS + 4] = dp;
-    res[b * RS + 5] = ep;
   }
   chain = wave_sum(chain);
   __syncthreads();
