@@ -185,8 +185,32 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   __syncthreads();
   const int my_floor = qs_floor[lane];
   u64 qf[2] = {0, 0}, qs[2] = {0, 0};
+  // software pipeline: round r-1's rows and first 64 weak columns (they do not
+  // depend on the frontier) load while round r is processed
+  u64 nra[2], nrb[2], nw0 = 0, nw1 = 0;
+  uint32_t nkey = 0, nc0 = 0, nc1 = 0;
+  auto prefetch2 = [&](int r) {
+    row(r, lane, nra[0], nrb[0]);
+    row(r, lane + 64, nra[1], nrb[1]);
+    nc0 = J.wc_roff[r];
+    nc1 = J.wc_roff[r + 1];
+    const uint32_t jc = nc0 + lane;
+    nkey = 0;
+    nw0 = nw1 = 0;
+    if (jc < nc1) {
+      nkey = J.wc_key[jc];
+      nw0 = J.wc_rows[(size_t)jc * WS];
+      nw1 = WS > 1 ? J.wc_rows[(size_t)jc * WS + 1] : 0ULL;
+    }
+  };
+  prefetch2(T);
   for (int r = T; r >= 1; r--) {
     const u64 alive = __ballot(lane < nw && my_floor <= r);
+    u64 ra[2] = {nra[0], nra[1]}, rb[2] = {nrb[0], nrb[1]};
+    u64 cw0 = nw0, cw1 = nw1;
+    uint32_t ckey = nkey;
+    const uint32_t c0 = nc0, c1 = nc1;
+    if (r > 1) prefetch2(r - 1);
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
@@ -218,16 +242,23 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
         QL[w - 1] = 0;
       }
     }
-    u64 ra[2], rb[2];
-    row(r, lane, ra[0], rb[0]);
-    row(r, lane + 64, ra[1], rb[1]);
-    // weak columns of round r: Qf of the column's sources into the pending round
-    {
-      const uint32_t c0 = J.wc_roff[r], c1 = J.wc_roff[r + 1];
-      const int WSJ = J.WS;
-      for (uint32_t jc = c0; jc < c1; jc++) {  // wave-uniform
-        const uint32_t key = J.wc_key[jc];
-        const u64 w0 = J.wc_rows[(size_t)jc * WSJ], w1 = WSJ > 1 ? J.wc_rows[(size_t)jc * WSJ + 1] : 0ULL;
+    // weak columns of round r (64 per batch, lane j holding column j; the first
+    // batch was prefetched): Qf of the column's sources into the pending round
+    for (uint32_t cb = c0; cb < c1; cb += 64) {
+      if (cb != c0) {
+        const uint32_t jc = cb + lane;
+        ckey = 0;
+        cw0 = cw1 = 0;
+        if (jc < c1) {
+          ckey = J.wc_key[jc];
+          cw0 = J.wc_rows[(size_t)jc * WS];
+          cw1 = WS > 1 ? J.wc_rows[(size_t)jc * WS + 1] : 0ULL;
+        }
+      }
+      const int m = (int)min(64u, c1 - cb);
+      for (int t = 0; t < m; t++) {  // wave-uniform
+        const u64 w0 = readlane64(cw0, t), w1 = readlane64(cw1, t);
+        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)ckey, t);
         u64 v = ((w0 >> lane) & 1ULL) ? qf[0] : 0ULL;
         v |= ((w1 >> lane) & 1ULL) ? qf[1] : 0ULL;
         v = wave_or(v);
@@ -347,12 +378,13 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   u64 chain = 0;
   // one leader's (or K's, b = 63) delivered vertices of round r in slot order,
   // positions from k0: count, digest, edges (wave-uniform); lanes = slots
-  auto contrib = [&](int r, int b, u64 k0, u64 befb, u64 &cnt, u64 &dg, u64 &ed) {
-    const uint32_t sa = J.slot_off[r], sb = J.slot_off[r + 1];
+  // (sa, sb: the round's slots; slo / shi: its first 128 slot sources, lane-held)
+  auto contrib = [&](int r, int b, u64 k0, u64 befb, uint32_t sa, uint32_t sb, int slo, int shi, u64 &cnt, u64 &dg,
+                     u64 &ed) {
     u64 k = k0, dacc = 0, eacc = 0;
     for (uint32_t c0 = sa; c0 < sb; c0 += 64) {
       const uint32_t sl = c0 + lane;
-      const int s = sl < sb ? (int)J.slot_src[sl] : 0;  // 0: ghost slot {0,0}, never reached
+      const int s = c0 == sa ? slo : c0 == sa + 64 ? shi : (sl < sb ? (int)J.slot_src[sl] : 0);  // 0: ghost / none
       const u64 f = s > 0 ? QF[s - 1] : 0ULL;
       const bool in = ((f >> b) & 1ULL) && !(f & befb);
       const u64 bal = __ballot(in);
@@ -366,22 +398,43 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
     dg = wave_sum(dacc);
     ed = wave_sum(eacc);
   };
-  for (int r = 1; r <= T; r++) {
-    __syncthreads();
-    u64 f2[2] = {0, 0}, s2[2] = {0, 0};
-    uint32_t d2[2] = {0, 0};
+  // software pipeline: round r+1's Q, degrees, presence and slots load while
+  // round r is processed
+  u64 pf[2] = {0, 0}, ps[2] = {0, 0}, pp[2] = {0, 0};
+  uint32_t pd[2] = {0, 0}, psa = 0, psb = 0;
+  int pslo = 0, pshi = 0;
+  auto prefetch4 = [&](int r) {
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
       if (v < n) {
         const size_t at = (size_t)r * n + v;
-        f2[i] = J.qf[at];
-        s2[i] = J.qs[at];
-        d2[i] = J.deg[at];
+        pf[i] = J.qf[at];
+        ps[i] = J.qs[at];
+        pd[i] = J.deg[at];
+      }
+      pp[i] = pres_word(r, i);
+    }
+    psa = J.slot_off[r];
+    psb = J.slot_off[r + 1];
+    pslo = psa + lane < psb ? (int)J.slot_src[psa + lane] : 0;
+    pshi = psa + 64 + lane < psb ? (int)J.slot_src[psa + 64 + lane] : 0;
+  };
+  prefetch4(1);
+  for (int r = 1; r <= T; r++) {
+    __syncthreads();
+    const u64 f2[2] = {pf[0], pf[1]}, s2[2] = {ps[0], ps[1]}, p2[2] = {pp[0], pp[1]};
+    const uint32_t d2[2] = {pd[0], pd[1]}, sa = psa, sb = psb;
+    const int slo = pslo, shi = pshi;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int v = lane + 64 * i;
+      if (v < n) {
         QF[v] = f2[i];
         DG[v] = d2[i];
       }
     }
+    if (r < T) prefetch4(r + 1);
     __syncthreads();
     const u64 active = popped & ~0ULL & __ballot(lane < nw && 4 * lane + 1 >= r);  // leaders whose top >= r
     if (!PAPER) {
@@ -389,7 +442,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
         u64 x = 0;
 #pragma unroll
         for (int i = 0; i < 2; i++)
-          if ((pres_word(r, i) >> lane) & 1ULL) x |= f2[i] ^ (((f2[i] >> 63) & 1ULL) ? ~0ULL : 0ULL);
+          if ((p2[i] >> lane) & 1ULL) x |= f2[i] ^ (((f2[i] >> 63) & 1ULL) ? ~0ULL : 0ULL);
         const u64 newly = wave_or(x) & active & ~neq;
         if ((newly >> lane) & 1ULL) {
           res[lane * RS + 0] = kK;
@@ -398,7 +451,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
         }
         neq |= newly;
         u64 c, d, e;
-        contrib(r, 63, kK, 0ULL, c, d, e);
+        contrib(r, 63, kK, 0ULL, sa, sb, slo, shi, c, d, e);
         kK += c;
         dK += d;
         eK += e;
@@ -407,7 +460,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
       for (u64 m = neq & active; m; m &= m - 1) {
         const int b = __builtin_ctzll(m);
         u64 c, d, e;
-        contrib(r, b, res[b * RS + 0], 0ULL, c, d, e);
+        contrib(r, b, res[b * RS + 0], 0ULL, sa, sb, slo, shi, c, d, e);
         __syncthreads();
         if (lane == 0) {
           res[b * RS + 0] += c;
@@ -431,10 +484,10 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
         bool any = false;
 #pragma unroll
         for (int i = 0; i < 2; i++)
-          any |= ((pres_word(r, i) >> lane) & 1ULL) && ((f2[i] >> b) & 1ULL) && !(f2[i] & befb);
+          any |= ((p2[i] >> lane) & 1ULL) && ((f2[i] >> b) & 1ULL) && !(f2[i] & befb);
         if (__ballot(any) == 0ULL) continue;
         u64 c, d, e;
-        contrib(r, b, res[b * RS + 3], befb, c, d, e);
+        contrib(r, b, res[b * RS + 3], befb, sa, sb, slo, shi, c, d, e);
         __syncthreads();
         if (lane == 0) {
           res[b * RS + 3] += c;
