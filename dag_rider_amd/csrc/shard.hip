@@ -1038,8 +1038,9 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   c->h_woff.assign(c->nlocal, std::vector<uint64_t>(1, 0));
   c->h_lead.assign((size_t)max_rounds / 4 + 2, 1);
   if (sh_set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipEventCreate(&c->ev2) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev0, hipEventReleaseToDevice) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev1, hipEventReleaseToDevice) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev2, hipEventReleaseToDevice) != hipSuccess) {
     g_shard_err = "dr_shard_create: stream/event creation failed";
     dr_shard_destroy(c);
     return DR_E_HIP;
