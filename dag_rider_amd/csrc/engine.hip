@@ -89,6 +89,7 @@ struct dr_ctx {
   hipEvent_t ev[8] = {};
   // device DAG
   DevBuf strong, present, slot_off, slot_src, weak_roff, far, far_roff;
+  DevBuf ppref;  // [round] |P_1| + .. + |P_r| (present vertices, round 0 excluded)
   size_t nfar = 0;
   // weak columns (kernels.hpp DagView::wc_*): one entry per distinct near weak
   // target (delta, t) of a round + the bitset of the round's sources pointing at it
@@ -108,6 +109,7 @@ struct dr_ctx {
   std::vector<HostRound> hr;
   std::vector<u64> h_present;
   std::vector<uint32_t> h_slot_off{0}, h_wc_roff{0}, h_far_roff{0}, h_weak_roff{0};
+  std::vector<u64> h_ppref;
   int up_lo = 0;  // lowest round whose flattened device arrays are stale
   // round summaries (U, SD, WU) per round: sdirty[r] = stale; the canonical cone
   // and its prefixes (K, C, G, E) describe the DAG as of the last canon build
@@ -324,8 +326,13 @@ struct dr_ctx {
     h_wc_roff.resize(R + 1);
     h_far_roff.resize(R + 1);
     h_weak_roff.resize(R + 1);
+    h_ppref.resize(R);
     for (int r = lo; r < R; r++) {
       const HostRound &h = hr[r];
+      u64 np = 0;
+      if (r >= 1)
+        for (uint16_t sl : h.slots) np += sl != 0;
+      h_ppref[r] = (r ? h_ppref[r - 1] : 0) + np;
       h_slot_off[r + 1] = h_slot_off[r] + (uint32_t)h.slots.size();
       h_wc_roff[r + 1] = h_wc_roff[r] + (uint32_t)h.wc_key.size();
       h_far_roff[r + 1] = h_far_roff[r] + (uint32_t)h.far.size();
@@ -358,6 +365,7 @@ struct dr_ctx {
     if ((e = h2d(wc_rows.as<u64>() + k0 * WS, rows.data(), rows.size() * 8)) != hipSuccess) return e;
     if ((e = h2d(far.as<u64>() + f0, ff.data(), ff.size() * 8)) != hipSuccess) return e;
     if ((e = h2d(slot_off.as<uint32_t>() + lo + 1, &h_slot_off[lo + 1], nr * 4)) != hipSuccess) return e;
+    if ((e = h2d(ppref.as<u64>() + lo, &h_ppref[lo], nr * 8)) != hipSuccess) return e;
     if ((e = h2d(wc_roff.as<uint32_t>() + lo + 1, &h_wc_roff[lo + 1], nr * 4)) != hipSuccess) return e;
     if ((e = h2d(far_roff.as<uint32_t>() + lo + 1, &h_far_roff[lo + 1], nr * 4)) != hipSuccess) return e;
     if ((e = h2d(weak_roff.as<uint32_t>() + lo + 1, &h_weak_roff[lo + 1], nr * 4)) != hipSuccess) return e;
@@ -445,6 +453,7 @@ struct SweepArgs {
   u64 *stats;
   const int *nq_dev = nullptr;  // planned replay: query count on the device, nq = grid upper bound
   uint32_t *rcnt = nullptr;     // planned delivery: per-mask-row vertex counts for the emission
+  dr::EmitArgs emit{};          // SW_EMIT: own-round emission outputs
 };
 
 template <int WS, int MODE>
@@ -455,9 +464,11 @@ hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   hipError_t e = hipFuncSetAttribute((const void *)dr::k_sweep<WS, NT, MODE>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(a.seq ? 1 : a.nq), dim3(NT), lds, c->stream,
+  // SW_EMIT: one workgroup more (the canonical prefixes, then the final pass)
+  const int grid = a.seq ? 1 : a.nq + ((MODE & dr::SW_EMIT) ? 1 : 0);
+  hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(grid), dim3(NT), lds, c->stream,
                      c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
-                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt);
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt, a.emit);
   return hipGetLastError();
 }
 template <int WS>
@@ -468,6 +479,8 @@ hipError_t launch_sweep_t(dr_ctx *c, const SweepArgs &a, int mode) {
     case dr::SW_CHAIN: return launch_sweep_m<WS, dr::SW_CHAIN>(c, a);
     case dr::SW_WEAK | dr::SW_PRUNE: return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_PRUNE>(c, a);
     case dr::SW_WEAK | dr::SW_MERGE: return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_MERGE>(c, a);
+    case dr::SW_WEAK | dr::SW_MERGE | dr::SW_EMIT:
+      return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_MERGE | dr::SW_EMIT>(c, a);
   }
   return hipErrorInvalidValue;
 }
@@ -563,12 +576,13 @@ hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc)
   if (e == hipSuccess) e = c->rec(7);  // ms_summary times k_summary_commit alone (the roofline kernel)
   return e;
 }
+// every round's WU, and its speculative canonical digest into RG (k_canon's spec check)
 template <int WS>
 hipError_t launch_weak_union_t(dr_ctx *c, int T, hipStream_t st) {
   const int dd = c->memo_dd();
-  if (dd == 0) return hipSuccess;
   hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, st, c->view(), T, dd, c->WU.as<u64>(),
-                     (const int32_t *)nullptr);
+                     (const int32_t *)nullptr, c->ppref.as<u64>(), c->slot_off.as<uint32_t>(),
+                     c->slot_src.as<uint16_t>(), c->RG.as<u64>());
   return hipGetLastError();
 }
 hipError_t launch_weak_union(dr_ctx *c, int T, hipStream_t st) {
@@ -593,7 +607,8 @@ hipError_t launch_round_summary_t(dr_ctx *c, const int32_t *rounds, int nr) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || mv.dd == 0) return e;
   hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(nr), dim3(256), 0, c->stream, c->view(), c->nrounds - 1,
-                     mv.dd, c->WU.as<u64>(), rounds);
+                     mv.dd, c->WU.as<u64>(), rounds, (const u64 *)nullptr, (const uint32_t *)nullptr,
+                     (const uint16_t *)nullptr, (u64 *)nullptr);
   return hipGetLastError();
 }
 hipError_t launch_round_summary(dr_ctx *c, const int32_t *rounds, int nr) {
@@ -608,12 +623,16 @@ hipError_t launch_round_summary(dr_ctx *c, const int32_t *rounds, int nr) {
   return hipErrorInvalidValue;
 }
 
-// canonical cone: K^cand per round, then the exact cone at the bad rounds
+// canonical cone: K^cand per round, then the exact cone at the bad rounds;
+// spec (a full cone, lo == 1): the round summaries carry every round's
+// speculative canonical digest (k_weak_union), k_canon sets *rlo to the lowest
+// round where it fails, and the canonical emission re-emits from there.
 template <int WS>
-hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo) {
+hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo, bool spec) {
   const dr::MemoView mv = c->memo_view();
   hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
-                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>(), c->rlo.as<int>(), lo);
+                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>(), c->rlo.as<int>(),
+                     spec ? T + 1 : lo);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int dl = c->depth_log2();
@@ -623,21 +642,22 @@ hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((dr::k_canon<WS, NTS>), dim3(1), dim3(NTS), lds, c->stream, c->view(), mv, T, dl,
                      c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>(), c->RD.as<u64>(),
-                     c->Cc.as<u64>(), c->crbase.as<uint32_t>());
+                     c->Cc.as<u64>(), c->crbase.as<uint32_t>(), spec ? c->ppref.as<u64>() : nullptr,
+                     c->rlo.as<int>());
   e = hipGetLastError();
   if (e != hipSuccess || lo <= 1) return e;
   hipLaunchKernelGGL((dr::k_canon_diff<WS>), dim3((lo - 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), lo,
                      c->K.as<u64>(), c->Kprev.as<u64>(), c->rlo.as<int>());
   return hipGetLastError();
 }
-hipError_t launch_canon_cone(dr_ctx *c, int T, int lo) {
+hipError_t launch_canon_cone(dr_ctx *c, int T, int lo, bool spec) {
   switch (c->WS) {
-    case 1: return launch_canon_cone_t<1>(c, T, lo);
-    case 2: return launch_canon_cone_t<2>(c, T, lo);
-    case 4: return launch_canon_cone_t<4>(c, T, lo);
-    case 8: return launch_canon_cone_t<8>(c, T, lo);
-    case 16: return launch_canon_cone_t<16>(c, T, lo);
-    case 32: return launch_canon_cone_t<32>(c, T, lo);
+    case 1: return launch_canon_cone_t<1>(c, T, lo, spec);
+    case 2: return launch_canon_cone_t<2>(c, T, lo, spec);
+    case 4: return launch_canon_cone_t<4>(c, T, lo, spec);
+    case 8: return launch_canon_cone_t<8>(c, T, lo, spec);
+    case 16: return launch_canon_cone_t<16>(c, T, lo, spec);
+    case 32: return launch_canon_cone_t<32>(c, T, lo, spec);
   }
   return hipErrorInvalidValue;
 }
@@ -715,6 +735,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   if (c->strong.ensure(rows) != hipSuccess ||
       c->present.ensure((size_t)max_rounds * c->WS * sizeof(u64)) != hipSuccess ||
       c->slot_off.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
+      c->ppref.ensure((size_t)(max_rounds + 1) * sizeof(u64)) != hipSuccess ||
       c->weak_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->far_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->far.ensure(4096) != hipSuccess ||
@@ -743,7 +764,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)c->sync();
   if (c->pin) (void)hipHostFree(c->pin);
-  DevBuf *bufs[] = {&c->strong,  &c->present, &c->slot_off, &c->slot_src, &c->put_buf,
+  DevBuf *bufs[] = {&c->strong,  &c->present, &c->slot_off, &c->ppref, &c->slot_src, &c->put_buf,
                     &c->weak_roff, &c->far,   &c->far_roff, &c->q_buf,    &c->masks,
                     &c->dlv,     &c->push_out, &c->push_n,  &c->edges,    &c->hits, &c->wedges,
                     &c->commit,  &c->vcount,  &c->popdesc,  &c->rbase,    &c->counts,
@@ -1252,8 +1273,10 @@ int refresh_rounds(dr_ctx *c) {
 // fork): work launched on stream2 first, beside the canonical chain, which then
 // stays on the main stream; ev_join marks its end.  forked: stream2 already
 // waits on an event of the main stream (build_summary's).
+// prefix = false: the caller's emitting sweep computes the G, E prefixes.
+// spec: RG holds every round's speculative digest (build_summary's weak union).
 int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool forked = false,
-                 bool incremental = false) {
+                 bool incremental = false, bool prefix = true, bool spec_rg = false) {
   const int T = c->nrounds - 1;
   // incremental (the per-call path): rounds below the lowest one that changed
   // since the last cone, and whose canonical vertices are unchanged, keep their
@@ -1279,7 +1302,8 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
   Swap sw(c, fork && !side);
   // canonical cone, per-round counts and positions (k_kcand + k_canon), then the
   // per-round digests (emission) and their prefixes
-  HIPCHK(c, launch_canon_cone(c, T, lo));  // *rlo = the lowest round to re-emit
+  const bool spec = spec_rg && lo <= 1;  // a full cone: re-emission from the first non-full round
+  HIPCHK(c, launch_canon_cone(c, T, lo, spec));  // *rlo = the lowest round to re-emit
   dr::PopDesc d{};
   d.mask_off = 0;
   d.rbase_off = 1;  // crbase is indexed by round; rbase_off addresses round `first`
@@ -1290,9 +1314,10 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
   d.use_k = 1;
   HIPCHK(c, launch_emit(c, 1, T, nullptr, c->crbase.as<uint32_t>(), nullptr, nullptr, c->RG.as<u64>(), nullptr,
                         nullptr, 0, false, nullptr, nullptr, d, nullptr,
-                        lo > 1 ? c->rlo.as<int>() : nullptr));  // the descriptor travels by value
-  hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
-                     c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
+                        c->rlo.as<int>()));  // the descriptor travels by value
+  if (prefix)
+    hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
+                       c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
   if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   c->kprev_ok = true;
@@ -1337,7 +1362,8 @@ int refresh_canon(dr_ctx *c) {
 // 1..nwc (host arrays), then the canonical cone and prefixes.  Every replay
 // re-reads the whole DAG; nothing carries over from earlier calls.
 int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
-                  bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr) {
+                  bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr,
+                  bool prefix = true) {
   const int T = c->nrounds - 1;
   if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
   if (int rc = ensure_summary_bufs(c)) return rc;
@@ -1361,7 +1387,7 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   }
   HIPCHK(c, launch_weak_union(c, T, c->stream));
   mark_rounds_clean(c);
-  if (int rc = launch_canon(c, fork, side, early)) return rc;
+  if (int rc = launch_canon(c, fork, side, early, false, prefix, true)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
   if (nwc > 0) {
     HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nwc));
@@ -2244,21 +2270,19 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   const int64_t pbound = persistent ? 2 * (int64_t)nw + 1 : (int64_t)nw * (nw + 1) / 2;
   const int64_t pcap = std::max<int64_t>(1, std::min<int64_t>(o->push_cap, pbound));
   const int64_t chain_slots = persistent ? nw : (int64_t)nw * (nw - 1) / 2;
-  const int64_t rb_cap = pcap * (int64_t)(T + 1);
   size_t mask_words = 0;  // every wave's leader a distinct query: rounds 0..4(w-1)+1
   for (int w = 1; w <= nw; w++) mask_words += (size_t)(4 * (w - 1) + 2) * WS;
-  if (mask_words > ((size_t)1 << 29) || rb_cap > ((int64_t)1 << 28) || chain_slots > INT32_MAX) return 1;
+  if (mask_words > ((size_t)1 << 29) || chain_slots > INT32_MAX) return 1;
   // device arena
   Carve cv;
   int32_t *plan = nullptr, *task_wave, *task_q, *cpush_n, *push_out, *push_wave, *pop_wave, *pop_cur, *pop_q,
-          *desc_of_pop, *qidx, *dstops;
-  int64_t *task_pos, *item_pref;
-  uint32_t *push_off, *rbase, *rcnt;
+          *qidx, *dstops;
+  int64_t *task_pos;
+  uint32_t *push_off;
   uint8_t *seen, *hits;
   dr::SweepQuery *cq, *dq;
-  dr::PopDesc *pd;
-  u64 *cedges, *cwedges, *dedges, *dwedges, *dstats, *extra_c, *extra_g, *pedges, *counts, *digest;
-  int32_t *cstops;
+  u64 *cedges, *cwedges, *dedges, *dwedges, *dstats, *qcount, *qdigest;
+  int32_t *cstops, *qcut;
   for (int pass = 0; pass < 2; pass++) {
     cv.off = 0;
     plan = cv.take<int32_t>(dr::PL_N);
@@ -2277,6 +2301,9 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     dwedges = cv.take<u64>(nw);
     dstops = cv.take<int32_t>(nw);
     dstats = cv.take<u64>(4 * (size_t)nw);
+    qcount = cv.take<u64>(nw);
+    qdigest = cv.take<u64>(nw);
+    qcut = cv.take<int32_t>(nw);
     seen = cv.take<uint8_t>(nw + 1);
     qidx = cv.take<int32_t>(nw + 1);
     push_off = cv.take<uint32_t>(nw + 1);
@@ -2284,23 +2311,13 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     pop_wave = cv.take<int32_t>(pcap);
     pop_cur = cv.take<int32_t>(pcap);
     pop_q = cv.take<int32_t>(pcap);
-    desc_of_pop = cv.take<int32_t>(pcap);
-    extra_c = cv.take<u64>(pcap);
-    extra_g = cv.take<u64>(pcap);
-    pedges = cv.take<u64>(pcap);
-    counts = cv.take<u64>(pcap);
-    digest = cv.take<u64>(pcap);
-    item_pref = cv.take<int64_t>(pcap + 1 + (size_t)rb_cap / kEmitRPB + pcap);  // prefix, then item -> segment
-    pd = cv.take<dr::PopDesc>(pcap);
-    rbase = cv.take<uint32_t>((size_t)rb_cap);
-    rcnt = cv.take<uint32_t>(mask_words / WS);  // one per mask row
     if (pass == 0) {
       HIPCHK(c, c->plan_arena.ensure(cv.off));
       cv.base = static_cast<char *>(c->plan_arena.p);
     }
   }
   HIPCHK(c, c->masks.ensure(mask_words * 8));
-  // outputs: k_plan_final packs them into one device region, which comes back
+  // outputs: the emitting sweep's final pass packs them into one device region, which comes back
   // in one copy (writing them straight into pinned host memory from the kernel
   // took 19.5 us, profiles/r02/v27_timeline.txt)
   const size_t h_bytes = 16 * 8 + (size_t)nw + 4 * (size_t)nw + 4 * ((size_t)nw + 1) + 4 * (size_t)pcap +
@@ -2350,8 +2367,8 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     HIPCHK(c, hipGetLastError());
     return 0;
   };
-  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side)) return rc;
-  // 3. delivery sweeps
+  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false)) return rc;
+  // 3+4. delivery sweeps, each emitting its own rounds (SW_EMIT)
   a.q = dq;
   a.push_out = nullptr;
   a.edges = dedges;
@@ -2359,27 +2376,41 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   a.stops = dstops;
   a.stats = dstats;
   a.nq_dev = plan + dr::PL_NQD;
-  a.rcnt = rcnt;
+  a.rcnt = nullptr;
+  a.emit = dr::EmitArgs{c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), c->Cc.as<u64>(), qcount, qdigest, qcut,
+                        dr::FinalArgs{}};
+  {
+    dr::FinalArgs &f = a.emit.fin;
+    f.T = T;
+    f.nw = nw;
+    f.RG = c->RG.as<u64>();
+    f.CE = c->CE.as<u64>();
+    f.Gc = c->Gc.as<u64>();
+    f.Ec = c->Ec.as<u64>();
+    f.Cc = c->Cc.as<u64>();
+    f.commit = c->commit.as<uint8_t>();
+    f.vcount = c->vcount.as<int32_t>();
+    f.push_off = push_off;
+    f.push_wave = push_wave;
+    f.pop_q = pop_q;
+    f.pop_cur = pop_cur;
+    f.dq = dq;
+    f.stops = dstops;
+    f.dedges = dedges;
+    f.cedges = cedges;
+    f.dstats = dstats;
+    f.nseg = c->nseg.as<int32_t>();
+    f.plan = plan;
+    f.o = dr::FinalOut{h_commit, h_vcount, h_push_off, h_push_wave, h_pc, h_pd, h_pe, h_hdr};
+  }
   dr::SweepQuery probe{};
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
   HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
   HIPCHK(c, c->rec(2));
-  HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
+  HIPCHK(c, launch_sweep(c, a, sweep_mode(probe) | dr::SW_EMIT));
   HIPCHK(c, c->rec(3));
-  // 4. emission
-  hipLaunchKernelGGL((dr::k_plan_emit<1024>), dim3(1), dim3(1024), 0, c->stream, pop_cur, pop_q, dq, dstops,
-                     c->Cc.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), dedges, kEmitRPB, rb_cap, pd, desc_of_pop,
-                     extra_c, extra_g, pedges, digest, counts, item_pref, plan);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, c->rec(4));
-  // positions and pop totals from the sweep's per-round counts (no count pass)
-  HIPCHK(c, launch_emit(c, (int)pcap, 0, pd, rbase, counts, digest, nullptr, nullptr, nullptr, 0, false,
-                        plan + dr::PL_NDESC, item_pref, dr::PopDesc{}, rcnt));
-  HIPCHK(c, c->rec(5));
-  hipLaunchKernelGGL((dr::k_plan_final<256>), dim3(16), dim3(256), 0, c->stream, nw, c->commit.as<uint8_t>(),
-                     c->vcount.as<int32_t>(), push_off, push_wave, desc_of_pop, extra_c, extra_g, pedges, counts,
-                     digest, cedges, dstats, c->nseg.as<int32_t>(), plan, h_commit, h_vcount, h_push_off,
-                     h_push_wave, h_pc, h_pd, h_pe, h_hdr);
+  // 5. per-pop totals and outputs (the canonical prefixes came from the sweep launch's extra workgroup)
+  hipLaunchKernelGGL((dr::k_replay_final<1024>), dim3(1), dim3(1024), 0, c->stream, a.emit);
   HIPCHK(c, hipGetLastError());
   c->plan_host.resize(out_bytes);
   HIPCHK(c, c->d2h(c->plan_host.data(), c->plan_out.p, out_bytes));
@@ -2401,8 +2432,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   if (c->timed(6)) HIPCHK(c, hipEventElapsedTime(&o->ms_summary, c->ev[6], c->ev[7]));
   if (c->timed(0)) {
     HIPCHK(c, hipEventElapsedTime(&o->ms_chain, c->ev[0], c->ev[1]));
-    HIPCHK(c, hipEventElapsedTime(&o->ms_deliver, c->ev[2], c->ev[3]));
-    HIPCHK(c, hipEventElapsedTime(&o->ms_emit, c->ev[4], c->ev[5]));
+    HIPCHK(c, hipEventElapsedTime(&o->ms_deliver, c->ev[2], c->ev[3]));  // sweeps + emission + final pass
   }
   std::memcpy(o->commit, h_commit, (size_t)nw);
   std::memcpy(o->vcount, h_vcount, (size_t)nw * 4);
@@ -2416,6 +2446,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   const int64_t np = (int64_t)h_hdr[dr::PH_NPUSH];
   o->n_push = np;
   if (h_hdr[dr::PH_CAPERR] == 2) return c->fail(DR_E_STATE, "replay planner: segment bound exceeded");
+  if (h_hdr[dr::PH_CAPERR] == 3) return c->fail(DR_E_STATE, "replay planner: a pop below its leader's round");
   if (h_hdr[dr::PH_CAPERR] || np > o->push_cap)
     return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)np, (long long)o->push_cap);
   std::memcpy(o->push_off, h_push_off, ((size_t)nw + 1) * 4);

@@ -28,6 +28,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 
 #include "wave_ops.hpp"
 
@@ -434,12 +435,260 @@ __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWo
 //           F -> ring[r-1] and weak edges of F -> ring[r'].
 // LDS: F[WS] | FE[WS] | ring[depth][WS] | ctl (int[8]) | edges (u64[2]).
 // ---------------------------------------------------------------------------
-enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8 };
+//   SW_EMIT   (with SW_MERGE, planned REF replay) after the sweep, the workgroup
+//             emits the query's own rounds itself (see emit_own_rounds)
+enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8, SW_EMIT = 16 };
+
+// exclusive scan over one workgroup; s = NT/64 scratch slots; every thread calls
+template <int NT, class T>
+__device__ __forceinline__ T block_scan_excl(T v, T *s, T &total) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s[wid] = x;
+  __syncthreads();
+  if (wid == 0) {
+    T t = lane < NW ? s[lane] : T(0);
+#pragma unroll
+    for (int off = 1; off < NW; off <<= 1) {
+      const T y = __shfl_up(t, off);
+      if (lane >= off) t += y;
+    }
+    if (lane < NW) s[lane] = t;
+  }
+  __syncthreads();
+  const T base = wid ? s[wid - 1] : T(0);
+  total = s[NW - 1];
+  __syncthreads();
+  return base + x - v;
+}
+
+template <int NT>
+__device__ __forceinline__ void canon_prefix_block(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                   u64 *__restrict__ A, u64 *__restrict__ B,
+                                                   uint32_t *__restrict__ rbase) {
+  __shared__ u64 s[NT / 64];
+  const int tid = threadIdx.x;
+  const int n = T + 1, per = (n + NT - 1) / NT;
+  const int ra = tid * per, rb = min(n, ra + per);
+  constexpr int MAXP = 16;
+  if (per <= MAXP) {  // block-uniform: every load in flight at once, values kept in registers
+    u64 va[MAXP], vb[MAXP], sa = 0, sb = 0;
+#pragma unroll
+    for (int j = 0; j < MAXP; j++) {
+      const int r = ra + j;
+      const bool in = r >= 1 && r < rb;
+      va[j] = in ? a[r] : 0ULL;
+      vb[j] = in && b ? b[r] : 0ULL;
+      sa += va[j];
+      sb += vb[j];
+    }
+    u64 ta, tb;
+    u64 xa = block_scan_excl<NT>(sa, s, ta);
+    u64 xb = b ? block_scan_excl<NT>(sb, s, tb) : 0ULL;
+#pragma unroll
+    for (int j = 0; j < MAXP; j++) {
+      const int r = ra + j;
+      if (r >= rb) break;
+      if (rbase) rbase[r] = (uint32_t)xa;
+      xa += va[j];
+      xb += vb[j];
+      A[r] = xa;
+      if (b) B[r] = xb;
+    }
+    return;
+  }
+  u64 sa = 0, sb = 0;
+  for (int r = max(ra, 1); r < rb; r++) {
+    sa += a[r];
+    if (b) sb += b[r];
+  }
+  u64 ta, tb;
+  u64 xa = block_scan_excl<NT>(sa, s, ta);
+  u64 xb = b ? block_scan_excl<NT>(sb, s, tb) : 0ULL;  // b is uniform
+  for (int r = ra; r < rb; r++) {
+    if (rbase) rbase[r] = (uint32_t)xa;
+    if (r >= 1) {
+      xa += a[r];
+      if (b) xb += b[r];
+    }
+    A[r] = xa;
+    if (b) B[r] = xb;
+  }
+}
+
+// plan[] slots (int32, device)
+enum : int { PL_NTASK = 0, PL_NQC = 1, PL_NPUSH = 2, PL_CAPERR = 3, PL_NQD = 4, PL_NDESC = 5, PL_N = 8 };
+// header written to host memory by k_plan_final (u64)
+enum : int {
+  PH_NPUSH = 0, PH_CHAIN_E = 1, PH_DELIVER_E = 2, PH_PARTIAL = 3, PH_ROWS = 4, PH_WEAK = 5, PH_SHORT = 6,
+  PH_NQD = 7, PH_NSEG = 8, PH_CAPERR = 9, PH_N = 16
+};
+
+// Host-visible output region of a planned replay (packed, one copy back).
+struct FinalOut {
+  uint8_t *commit;
+  int32_t *vcount;
+  uint32_t *push_off;
+  int32_t *push_wave;
+  u64 *pc, *pd, *pe, *hdr;
+};
+
+// Inputs of the planned replay's last pass (replay_final_block).
+struct FinalArgs {
+  int T, nw;
+  const u64 *RG, *CE;  // canonical per-round digests and edges
+  u64 *Gc, *Ec;        // their prefixes (the extra workgroup of the emitting sweep)
+  const u64 *Cc;
+  const uint8_t *commit;
+  const int32_t *vcount;
+  const uint32_t *push_off;
+  const int32_t *push_wave, *pop_q, *pop_cur;
+  const SweepQuery *dq;
+  const int32_t *stops;
+  const u64 *dedges, *cedges, *dstats;
+  const int32_t *nseg, *plan;
+  FinalOut o;
+};
+
+// SW_EMIT outputs: per query, the count and order-sensitive digest of the
+// vertices of its own rounds (above the merge round), positions starting at
+// C_stop, the number of canonical vertices of rounds 1..stop.
+struct EmitArgs {
+  const uint32_t *slot_off;
+  const uint16_t *slot_src;
+  const u64 *Cc;  // canonical prefix counts (k_canon)
+  u64 *count;     // [query] own-round vertex count
+  u64 *digest;    // [query] own-round digest terms
+  int32_t *cut;   // [query] the canonical rounds are 1..cut (-1: none)
+  FinalArgs fin;
+};
+
+// One wave emits round y: the delivered slots (source bit set in mw, lane w
+// holding word w) in insertion order, vertex k at position pos + rank.  Returns
+// this lane's share of the digest sum.
+// SPL: slots per lane per pass (16 in the sweep would cost it a wave per SIMD of occupancy).
+template <int WS, int SPL = 8>
+__device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot_off,
+                                               const uint16_t *__restrict__ slot_src, int y, u64 mw, u64 pos) {
+  const int lane = threadIdx.x & 63;
+  u64 dg = 0;
+  const uint32_t sa = slot_off[y], sb = slot_off[y + 1];
+  for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPL) {
+    const uint32_t i0 = c0 + (uint32_t)lane * SPL;
+    int src[SPL];
+#pragma unroll
+    for (int j = 0; j < SPL; j++) src[j] = i0 + j < sb ? (int)slot_src[i0 + j] : 0;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < SPL; j++) {
+      const int s = src[j] - 1;
+      const u64 w = __shfl(mw, s >= 0 ? (s >> 6) & (WS - 1) : 0);
+      if (s >= 0 && ((w >> (s & 63)) & 1ULL)) bits |= 1u << j;
+    }
+    const int cnt = __popc(bits);
+    int x = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int yv = __shfl_up(x, off);
+      if (lane >= off) x += yv;
+    }
+    const int total = __shfl(x, 63);
+    u64 k = pos + (u64)(x - cnt);
+#pragma unroll
+    for (int j = 0; j < SPL; j++) {
+      if (!((bits >> j) & 1u)) continue;
+      dg += digest_term((uint32_t)y, (uint32_t)src[j], k);
+      k++;
+    }
+    pos += (u64)total;
+  }
+  return dg;
+}
 
 
+
+// The planned replay's last pass (k_replay_final, after the emitting delivery
+// sweep, SW_EMIT): per pop, the canonical terms at its
+// query's cut (C, G) and merge round (E) plus the query's own-round count,
+// digest and edges (what k_plan_emit + k_emit_ids + k_plan_final did in three
+// launches), the commits and pushes, and the totals, into the packed output
+// region.  Every pop of a replay has cur_round >= top (a leader is popped at a
+// wave's end, above its own round): checked, a violation reports PH_CAPERR = 3.
+template <int NT>
+__device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
+  __shared__ u64 acc[8];
+  __shared__ int s_bad;
+  const int tid = threadIdx.x;
+  if (tid < 8) acc[tid] = 0;
+  if (tid == 0) s_bad = 0;
+  const int caperr = f.plan[PL_CAPERR];
+  const int64_t np = caperr ? 0 : f.plan[PL_NPUSH];
+  const int nqc = f.plan[PL_NQC], nqd = f.plan[PL_NQD];
+  u64 de = 0, ce = 0, st[4] = {0, 0, 0, 0};
+  bool bad = false;
+  // every load of a pop before any store (the stores could alias for the compiler)
+  for (int64_t p = tid; p < np; p += NT) {
+    const int q = f.pop_q[p];
+    const int cur = f.pop_cur[p], pw = f.push_wave[p];
+    const int stop = f.stops[q], cut = ea.cut[q], top = f.dq[q].top;
+    u64 c = ea.count[q], d = ea.digest[q], e = f.dedges[q];
+    if (cut >= 0) {
+      c += f.Cc[cut];
+      d += f.Gc[cut];
+    }
+    if (stop >= 0) e += f.Ec[stop];  // the sweep counted the edges of rounds above stop
+    bad |= cur < top;
+    f.o.push_wave[p] = pw;
+    f.o.pc[p] = c;
+    f.o.pd[p] = d;
+    f.o.pe[p] = e;
+    de += e;
+  }
+  for (int q = tid; q < nqc; q += NT) ce += f.cedges[q];
+  for (int q = tid; q < nqd; q += NT)
+#pragma unroll
+    for (int k = 0; k < 4; k++) st[k] += f.dstats[4 * q + k];
+  for (int w = tid; w < f.nw; w += NT) {
+    const uint8_t cm = f.commit[w];
+    const int32_t vc = f.vcount[w];
+    f.o.commit[w] = cm;
+    f.o.vcount[w] = vc;
+  }
+  if (!caperr)
+    for (int w = tid; w <= f.nw; w += NT) f.o.push_off[w] = f.push_off[w];
+  de = wave_sum(de);
+  ce = wave_sum(ce);
+#pragma unroll
+  for (int k = 0; k < 4; k++) st[k] = wave_sum(st[k]);
+  __syncthreads();  // acc, s_bad initialised
+  if ((tid & 63) == 0) {
+    atomicAdd(&acc[0], de);
+    atomicAdd(&acc[1], ce);
+#pragma unroll
+    for (int k = 0; k < 4; k++) atomicAdd(&acc[2 + k], st[k]);
+  }
+  if (bad) s_bad = 1;
+  __syncthreads();
+  if (tid == 0) {
+    u64 *h = f.o.hdr;
+    h[PH_NPUSH] = (u64)f.plan[PL_NPUSH];
+    h[PH_CHAIN_E] = acc[1];
+    h[PH_DELIVER_E] = acc[0];
+    for (int k = 0; k < 4; k++) h[PH_PARTIAL + k] = acc[2 + k];
+    h[PH_NQD] = (u64)nqd;
+    h[PH_NSEG] = (u64)(int64_t)*f.nseg;
+    h[PH_CAPERR] = (u64)(caperr ? caperr : s_bad ? 3 : 0);
+  }
+}
 
 template <int WS, int NT, int MODE>
-__global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_EMIT) ? 4 : 1))) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
                                               int nq, int seq, int depth_log2,
                                               u64 *__restrict__ masks, u64 *__restrict__ dlv,
                                               int32_t *__restrict__ push_out,
@@ -449,14 +698,20 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
                                               uint8_t *__restrict__ hit_out,
                                               int32_t *__restrict__ stop_out,
                                               u64 *__restrict__ stats_out, const int *__restrict__ nq_dev,
-                                              uint32_t *__restrict__ rcnt) {
+                                              uint32_t *__restrict__ rcnt, const EmitArgs ea) {
+  constexpr bool WEAK = MODE & SW_WEAK, CHAIN = MODE & SW_CHAIN, PRUNE = MODE & SW_PRUNE,
+                 MERGE = MODE & SW_MERGE, EMIT = (MODE & SW_EMIT) && (MODE & SW_MERGE);
+  // EMIT: the grid has one workgroup beyond the query bound, which computes the
+  // canonical prefixes G, E beside the sweeps (k_replay_final reads them)
+  bool work = true;
   if (nq_dev) {  // grid sized by an upper bound, count on the device (planned replay)
     const int m = *nq_dev;
     if (seq) nq = m;
-    else if ((int)blockIdx.x >= m) return;
+    else if ((int)blockIdx.x >= m) {
+      if constexpr (!EMIT) return;
+      work = false;
+    }
   }
-  constexpr bool WEAK = MODE & SW_WEAK, CHAIN = MODE & SW_CHAIN, PRUNE = MODE & SW_PRUNE,
-                 MERGE = MODE & SW_MERGE;
   constexpr u64 WMASK = WS >= 64 ? ~0ULL : ((1ULL << WS) - 1ULL);  // lanes owning a frontier word
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
   u64 *F = smem;                // WS: frontier (reached ids, dangling included)
@@ -472,7 +727,10 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
   const bool act = tid < WS;    // lane w owns frontier word w
 
   const int qa = seq ? 0 : blockIdx.x;
-  const int qb = seq ? nq : blockIdx.x + 1;
+  const int qb = !work ? qa : seq ? nq : blockIdx.x + 1;
+  if constexpr (EMIT) {
+    if (blockIdx.x == gridDim.x - 1) canon_prefix_block<NT>(ea.fin.T, ea.fin.RG, ea.fin.CE, ea.fin.Gc, ea.fin.Ec, nullptr);
+  }
   for (int qi = qa; qi < qb; qi++) {
     const SweepQuery q = qs[qi];
     const bool has_masks = q.flags & Q_MASKS;
@@ -609,6 +867,54 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
       cur = nxt;
       --r;
     }
+    if constexpr (EMIT) {
+      // The query's own rounds (planned REF replay): merged at m =
+      // stop, its delivered sequence is the canonical vertices of rounds 1..m
+      // then rounds m+1..top.  Rounds m..m+dmax-1 equal K (the merge run), so
+      // with cut = m+dmax-1 the positions of rounds m+1..cut are the canonical
+      // ones too: rounds 1..cut are canonical (C_cut, G_cut, added by the final
+      // pass) and only cut+1..top are emitted here; an unmerged sweep owns
+      // every round it reached.  Rounds go NT/64 at a time, one per wave:
+      // counts -> LDS -> each wave's base position.
+      constexpr int NWV = NT / 64;
+      __shared__ u64 s_em[NWV + 1];
+      const int lane = tid & 63, wid = tid >> 6;
+      const int sr = s_ctl[4];
+      const bool mg = s_ctl[3] != 0;
+      const int cut = mg ? sr + mv.dmax - 1 : -1;
+      const int first = mg ? cut + 1 : max(1, sr), last = q.top;
+      const u64 pos0 = mg ? ea.Cc[cut] : 0ULL;
+      u64 run = pos0, dg = 0;
+      if (tid == 0) s_em[NWV] = 0;
+      for (int y0 = first; y0 <= last; y0 += NWV) {  // block-uniform
+        const int y = y0 + wid;
+        const bool on = y <= last;
+        u64 mw = 0;
+        if (on && lane < WS)  // this workgroup's own mask rows (phase A): agent-scope loads
+          mw = ld_agent(masks + q.mask_off + (int64_t)(y - q.bottom) * WS + lane) & g.present[(size_t)y * WS + lane];
+        const u64 cnt = wave_sum((u64)popc64(mw));
+        if (lane == 0) s_em[wid] = cnt;
+        __syncthreads();
+        u64 base = run, tot = 0;
+#pragma unroll
+        for (int i = 0; i < NWV; i++) {
+          const u64 c = s_em[i];
+          base += i < wid ? c : 0ULL;
+          tot += c;
+        }
+        if (on && cnt) dg += wave_emit_round<WS>(ea.slot_off, ea.slot_src, y, mw, base);
+        run += tot;
+        __syncthreads();  // s_em is rewritten by the next rounds
+      }
+      dg = wave_sum(dg);
+      if (lane == 0 && dg) atomicAdd(&s_em[NWV], dg);
+      __syncthreads();
+      if (tid == 0) {
+        ea.count[qi] = run - pos0;
+        ea.digest[qi] = s_em[NWV];
+        ea.cut[qi] = cut;
+      }
+    }
     // results
     DR_TT(tt_end = wall_clock64();)
     my_edges += my_wedges;
@@ -645,6 +951,12 @@ __global__ __launch_bounds__(NT) void k_sweep(DagView g, MemoView mv, const Swee
     }
     __syncthreads();
   }
+}
+
+// The planned replay's final pass (one workgroup), after the emitting sweep.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_replay_final(const EmitArgs ea) {
+  replay_final_block<NT>(ea.fin, ea);
 }
 
 // ---------------------------------------------------------------------------
@@ -902,21 +1214,55 @@ __global__ __launch_bounds__(NT) void k_set_weak(DagView g, int r0, int depth_lo
 
 // WU_r[delta] = the union of round r's weak targets at distance delta, one
 // workgroup per round r = blockIdx.x + 1 (or rounds[blockIdx.x]: incremental).
+//
+// With RG (a full replay): also the speculative canonical digest of round r,
+// assuming every round 1..r full (K_y covers P_y): every present vertex of r
+// (every non-ghost slot, in slot order) delivered at positions from ppref[r-1]
+// = |P_1| + .. + |P_{r-1}|.  k_canon lowers *rlo to the lowest round where that
+// assumption fails; the canonical emission recomputes only rounds >= *rlo.
 template <int WS, int NT>
 __global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64 *__restrict__ WU,
-                                                   const int32_t *__restrict__ rounds) {
+                                                   const int32_t *__restrict__ rounds,
+                                                   const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
+                                                   const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG) {
   __shared__ u64 sWU[16 * WS];
+  __shared__ u64 s_sc[NT / 64], s_rg;
   const int r = rounds ? rounds[blockIdx.x] : blockIdx.x + 1, tid = threadIdx.x;
   if (r > T) return;
   for (int i = tid; i < dd * WS; i += NT) sWU[i] = 0;
+  if (tid == 0) s_rg = 0;
   __syncthreads();
   // every weak-column entry has at least one source: its key alone is the union
   for (uint32_t j = g.wc_roff[r] + tid; j < g.wc_roff[r + 1]; j += NT) {
     const uint32_t key = g.wc_key[j];
     atomicOr(&sWU[((key >> 11) - 2) * WS + ((key & 2047u) >> 6)], 1ULL << (key & 63u));
   }
+  if (RG) {  // block-uniform
+    constexpr int SPT = 4;  // slots per thread per pass
+    const uint32_t sa = slot_off[r], sb = slot_off[r + 1];
+    u64 pos = ppref[r - 1], dg = 0;
+    for (uint32_t c0 = sa; c0 < sb; c0 += NT * SPT) {
+      const uint32_t i0 = c0 + (uint32_t)tid * SPT;
+      uint32_t src[SPT];
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < SPT; j++) {
+        src[j] = i0 + j < sb ? slot_src[i0 + j] : 0u;
+        cnt += src[j] != 0;
+      }
+      u64 tot;
+      u64 k = pos + block_scan_excl<NT>((u64)cnt, s_sc, tot);
+#pragma unroll
+      for (int j = 0; j < SPT; j++)
+        if (src[j]) dg += digest_term((uint32_t)r, src[j], k++);
+      pos += tot;
+    }
+    dg = wave_sum(dg);
+    if ((tid & 63) == 0 && dg) atomicAdd(&s_rg, dg);
+  }
   __syncthreads();
   for (int i = tid; i < dd * WS; i += NT) WU[(size_t)r * dd * WS + i] = sWU[i];
+  if (RG && tid == 0) RG[r] = s_rg;
 }
 
 // K^cand_r = U_{r+1} | OR_d WU_{r+d+2}[d] (the cone of round r when every round
@@ -928,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
                                                uint8_t *__restrict__ good, u64 *__restrict__ CE,
                                                u64 *__restrict__ RD, int *__restrict__ rlo, int lo) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
-  if (rlo && blockIdx.x == 0 && threadIdx.x == 0) *rlo = lo;  // k_canon_diff lowers it
+  if (rlo && blockIdx.x == 0 && threadIdx.x == 0) *rlo = lo;  // k_canon_diff / k_canon lower it
   if (r > T) return;
   bool bad = false;
   int cnt = 0;
@@ -986,7 +1332,8 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
                                               u64 *__restrict__ K, const uint8_t *__restrict__ good,
                                               u64 *__restrict__ CE, int32_t *__restrict__ nseg,
                                               u64 *__restrict__ RD, u64 *__restrict__ Cc,
-                                              uint32_t *__restrict__ crbase) {
+                                              uint32_t *__restrict__ crbase, const u64 *__restrict__ ppref,
+                                              int *__restrict__ rlo) {
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
   u64 *F = smem, *FE = smem + WS, *ring = smem + 2 * WS;
   const int depth = 1 << depth_log2, dmask = depth - 1;
@@ -1097,10 +1444,20 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     __syncthreads();
   }
   u64 run = part[tid] - loc;
+  int bad = INT_MAX;  // ppref: the lowest round whose C differs from the all-full prefix
   for (int x = ra; x < rb; x++) {
     crbase[x] = (uint32_t)run;
     run += RD[x];
     Cc[x] = run;
+    if (ppref && bad == INT_MAX && x >= 1 && run != ppref[x]) bad = x;
+  }
+  if (ppref) {
+    __shared__ int s_bad;
+    if (tid == 0) s_bad = INT_MAX;
+    __syncthreads();
+    if (bad != INT_MAX) atomicMin(&s_bad, bad);
+    __syncthreads();
+    if (tid == 0 && s_bad != INT_MAX) atomicMin(rlo, s_bad);
   }
 }
 
@@ -1295,29 +1652,7 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                      u64 *__restrict__ A, u64 *__restrict__ B,
                                                      uint32_t *__restrict__ rbase) {
-  __shared__ u64 pa[NT], pb[NT];
-  const int tid = threadIdx.x;
-  const int n = T + 1, per = (n + NT - 1) / NT;
-  const int ra = tid * per, rb = min(n, ra + per);
-  u64 sa = 0, sb = 0;
-  for (int r = max(ra, 1); r < rb; r++) { sa += a[r]; if (b) sb += b[r]; }
-  pa[tid] = sa;
-  pb[tid] = sb;
-  __syncthreads();
-  for (int off = 1; off < NT; off <<= 1) {
-    const u64 x = tid >= off ? pa[tid - off] : 0, y = tid >= off ? pb[tid - off] : 0;
-    __syncthreads();
-    pa[tid] += x;
-    pb[tid] += y;
-    __syncthreads();
-  }
-  u64 ra_ = pa[tid] - sa, rb_ = pb[tid] - sb;
-  for (int r = ra; r < rb; r++) {
-    if (rbase) rbase[r] = (uint32_t)ra_;
-    if (r >= 1) { ra_ += a[r]; if (b) rb_ += b[r]; }
-    A[r] = ra_;
-    if (b) B[r] = rb_;
-  }
+  canon_prefix_block<NT>(T, a, b, A, B, rbase);
 }
 
 // Multi-segment copy between device memory and pinned (device-mapped) host

@@ -24,43 +24,6 @@
 
 namespace dr {
 
-// plan[] slots (int32, device)
-enum : int { PL_NTASK = 0, PL_NQC = 1, PL_NPUSH = 2, PL_CAPERR = 3, PL_NQD = 4, PL_NDESC = 5, PL_N = 8 };
-// header written to host memory by k_plan_final (u64)
-enum : int {
-  PH_NPUSH = 0, PH_CHAIN_E = 1, PH_DELIVER_E = 2, PH_PARTIAL = 3, PH_ROWS = 4, PH_WEAK = 5, PH_SHORT = 6,
-  PH_NQD = 7, PH_NSEG = 8, PH_CAPERR = 9, PH_N = 16
-};
-
-// exclusive scan over one workgroup; s = NT/64 scratch slots; every thread calls
-template <int NT, class T>
-__device__ __forceinline__ T block_scan_excl(T v, T *s, T &total) {
-  constexpr int NW = NT / 64;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  T x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const T y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) s[wid] = x;
-  __syncthreads();
-  if (wid == 0) {
-    T t = lane < NW ? s[lane] : T(0);
-#pragma unroll
-    for (int off = 1; off < NW; off <<= 1) {
-      const T y = __shfl_up(t, off);
-      if (lane >= off) t += y;
-    }
-    if (lane < NW) s[lane] = t;
-  }
-  __syncthreads();
-  const T base = wid ? s[wid - 1] : T(0);
-  total = s[NW - 1];
-  __syncthreads();
-  return base + x - v;
-}
-
 // Committed waves -> tasks (wave, floor) -> leader-chain queries.  Persistent
 // decidedWave: floor = the previous committed wave; literal: 0.  A task with
 // wave - floor >= 2 walks rounds 4(w-1)+1 .. 4 floor + 1 and may push up to
