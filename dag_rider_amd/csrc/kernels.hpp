@@ -714,6 +714,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
   }
   constexpr u64 WMASK = WS >= 64 ? ~0ULL : ((1ULL << WS) - 1ULL);  // lanes owning a frontier word
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
+  // EMIT: the delivered words (f & p) and counts of the query's top EMR rounds,
+  // kept by phase A so the own-round emission needs no mask reads or count pass
+  constexpr int EMR = EMIT ? 16 : 1;
+  __shared__ u64 s_emm[EMR * WS];
+  __shared__ uint32_t s_emc[EMR];
   u64 *F = smem;                // WS: frontier (reached ids, dangling included)
   u64 *FE = smem + WS;          // WS: F & present (the vertices that expand)
   u64 *ring = smem + 2 * WS;    // depth * WS
@@ -745,7 +750,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
       ring[(size_t)(q.top & dmask) * WS + (q.src0 >> 6)] = 1ULL << (q.src0 & 63);
     int npush = 0;  // thread 0
     u64 st_partial = 0, st_scan = 0, st_short = 0;  // thread 0: work counters
-    DR_TT(u64 tt0 = wall_clock64(); u64 tt_a = 0, tt_b = 0, tt_pro = 0, tt_ns = 0, tt_np = 0, tt_end = 0;
+    DR_TT(u64 tt0 = wall_clock64(); u64 tt_a = 0, tt_b = 0, tt_pro = 0, tt_ns = 0, tt_np = 0, tt_end = 0, tt_emit = 0;
           u64 tt_sub[4] = {0, 0, 0, 0};)
     int run = 0;    // wave 0: consecutive rounds equal to K
     u64 my_edges = 0, my_wedges = 0, my_rowb = 0;
@@ -816,6 +821,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
             for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
             if (tid == 0) rcnt[q.mask_off / WS + (r - q.bottom)] = (uint32_t)pc;
           }
+          if constexpr (EMIT) {
+            const int e = q.top - r;
+            if (e < EMR) {
+              const u64 fp = act ? f & p : 0ULL;
+              int pc = popc64(fp);
+#pragma unroll
+              for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
+              if (act) s_emm[e * WS + tid] = fp;
+              if (tid == 0) s_emc[e] = (uint32_t)pc;
+            }
+          }
           if (stats_out && tid == 0 && !stop) {
             if (summary) st_short++;
             else { st_partial++; if (WEAK) st_scan += cur.C1 - cur.C0; }
@@ -867,6 +883,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
       cur = nxt;
       --r;
     }
+    DR_TT(const u64 tte = wall_clock64();)
     if constexpr (EMIT) {
       // The query's own rounds (planned REF replay): merged at m =
       // stop, its delivered sequence is the canonical vertices of rounds 1..m
@@ -886,6 +903,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
       const u64 pos0 = mg ? ea.Cc[cut] : 0ULL;
       u64 run = pos0, dg = 0;
       if (tid == 0) s_em[NWV] = 0;
+      if (last - first < EMR) {  // block-uniform: every own round kept by phase A, no count pass
+        for (int y = first + wid; y <= last; y += NWV) {
+          u64 base = pos0;
+          for (int x = first; x < y; x++) base += s_emc[q.top - x];
+          const u64 mw = lane < WS ? s_emm[(q.top - y) * WS + lane] : 0ULL;
+          if (s_emc[q.top - y]) dg += wave_emit_round<WS>(ea.slot_off, ea.slot_src, y, mw, base);
+        }
+        for (int x = first; x <= last; x++) run += s_emc[q.top - x];
+      } else
       for (int y0 = first; y0 <= last; y0 += NWV) {  // block-uniform
         const int y = y0 + wid;
         const bool on = y <= last;
@@ -916,7 +942,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
       }
     }
     // results
-    DR_TT(tt_end = wall_clock64();)
+    DR_TT(tt_end = wall_clock64(); tt_emit = tt_end - tte;)
     my_edges += my_wedges;
     // one LDS atomic per wave and counter (a workgroup of same-address atomics serialises)
     my_edges = wave_sum(my_edges);
@@ -940,6 +966,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
         t[0] = tt_pro; t[1] = tt_a; t[2] = tt_b; t[3] = wall_clock64() - tt0; t[4] = tt_ns; t[5] = tt_np;
         t[6] = (u64)q.top; t[7] = (u64)(int64_t)s_ctl[4];
         t[8] = tt_sub[0]; t[9] = tt_sub[1]; t[10] = tt_sub[2]; t[11] = tt_sub[3]; t[12] = wall_clock64() - tt_end;
+        t[13] = tt0; t[14] = wall_clock64(); t[15] = tt_emit;
       }
 #endif
       if (stats_out) {
@@ -1430,26 +1457,42 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
   if (tid == 0 && nseg) *nseg = segs;
   // canonical positions (the RD writes above are this workgroup's own: visible after the barrier)
   __syncthreads();
-  __shared__ u64 part[NT];
+  __shared__ u64 part[NT / 64];
   const int per = (T + 1 + NT - 1) / NT;
   const int ra = tid * per, rb = min(T + 1, ra + per);
-  u64 loc = 0;
-  for (int x = ra; x < rb; x++) loc += RD[x];
-  part[tid] = loc;
-  __syncthreads();
-  for (int off = 1; off < NT; off <<= 1) {
-    const u64 v = tid >= off ? part[tid - off] : 0;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  u64 run = part[tid] - loc;
   int bad = INT_MAX;  // ppref: the lowest round whose C differs from the all-full prefix
-  for (int x = ra; x < rb; x++) {
-    crbase[x] = (uint32_t)run;
-    run += RD[x];
-    Cc[x] = run;
-    if (ppref && bad == INT_MAX && x >= 1 && run != ppref[x]) bad = x;
+  constexpr int MAXP = 16;
+  if (per <= MAXP) {  // block-uniform: every load in flight at once
+    u64 v[MAXP], pp[MAXP], loc = 0;
+#pragma unroll
+    for (int j = 0; j < MAXP; j++) {
+      const int x = ra + j;
+      v[j] = x < rb ? RD[x] : 0ULL;
+      pp[j] = ppref && x < rb ? ppref[x] : 0ULL;
+      loc += v[j];
+    }
+    u64 tot;
+    u64 run = block_scan_excl<NT>(loc, part, tot);
+#pragma unroll
+    for (int j = 0; j < MAXP; j++) {
+      const int x = ra + j;
+      if (x >= rb) break;
+      crbase[x] = (uint32_t)run;
+      run += v[j];
+      Cc[x] = run;
+      if (ppref && bad == INT_MAX && x >= 1 && run != pp[j]) bad = x;
+    }
+  } else {
+    u64 loc = 0;
+    for (int x = ra; x < rb; x++) loc += RD[x];
+    u64 tot;
+    u64 run = block_scan_excl<NT>(loc, part, tot);
+    for (int x = ra; x < rb; x++) {
+      crbase[x] = (uint32_t)run;
+      run += RD[x];
+      Cc[x] = run;
+      if (ppref && bad == INT_MAX && x >= 1 && run != ppref[x]) bad = x;
+    }
   }
   if (ppref) {
     __shared__ int s_bad;

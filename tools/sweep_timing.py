@@ -37,6 +37,12 @@ for k, name in enumerate(["prologue", "phaseA", "expansion", "total"]):
 for k, name in ((8, "exp_issue"), (9, "exp_rows"), (10, "exp_fold"), (11, "exp_weak"), (12, "results")):
     v = t[:, k] * tick_us
     out[name + "_us"] = dict(mean=float(v.mean()), p50=float(np.median(v)), max=float(v.max()))
+v = t[:, 15] * tick_us
+out["emit_us"] = dict(mean=float(v.mean()), p50=float(np.median(v)), max=float(v.max()))
+st = (t[:, 13] - t[:, 13].min()) * tick_us  # workgroup start offsets within the launch
+en = (t[:, 14] - t[:, 13].min()) * tick_us
+out["start_offset_us"] = dict(p50=float(np.median(st)), p90=float(np.percentile(st, 90)), max=float(st.max()))
+out["end_offset_us"] = dict(p50=float(np.median(en)), p90=float(np.percentile(en, 90)), max=float(en.max()))
 out["summary_rounds"] = float(t[:, 4].mean())
 out["partial_rounds"] = float(t[:, 5].mean())
 out["queries"] = nq
