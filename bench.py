@@ -629,6 +629,7 @@ def main() -> int:
     ap.add_argument("--deliver", default="ref", choices=["ref", "paper"])
     ap.add_argument("--cpu-budget", type=float, default=40.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--phase-timing", type=int, default=1, help=argparse.SUPPRESS)  # 0: no events (experiment)
     ap.add_argument("--loop-waves", type=int, default=0, help="c4-loop: waves to run (0 = all)")
     ap.add_argument("--verify", action="store_true", help="check the replay against the bitset oracle")
     ap.add_argument("--colshard", action="store_true",
@@ -698,7 +699,7 @@ def main() -> int:
 
     # timed steps: HIP events around the summary pass only (the dominant kernel);
     # every other phase is timed by one extra, untimed-by-the-clock replay below
-    eng.set_phase_timing(1)
+    eng.set_phase_timing(args.phase_timing)
     for _ in range(args.warmup):
         step()
     if dist:

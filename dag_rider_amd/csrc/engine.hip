@@ -419,6 +419,9 @@ constexpr int sweep_block() {
 // canonical sweep keep the wide block.  C4: pops 96 -> 75 us.
 template <int WS, int MODE>
 constexpr int sweep_block_m() {
+  // emitting pop sweeps at n = 1024: 3 waves, so every query of a C4 replay is
+  // resident at once at 3 waves per SIMD (168 VGPRs: the emission fits unspilled)
+  if constexpr ((MODE & dr::SW_EMIT) && WS == 16) return 192;
   return (MODE & dr::SW_CHAIN) ? sweep_block<WS>() : WS == 16 ? 256 : sweep_block<WS>();
 }
 

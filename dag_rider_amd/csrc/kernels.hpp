@@ -468,7 +468,7 @@ __device__ __forceinline__ T block_scan_excl(T v, T *s, T &total) {
   return base + x - v;
 }
 
-template <int NT>
+template <int NT, int MAXP = 16>
 __device__ __forceinline__ void canon_prefix_block(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                    u64 *__restrict__ A, u64 *__restrict__ B,
                                                    uint32_t *__restrict__ rbase) {
@@ -476,7 +476,6 @@ __device__ __forceinline__ void canon_prefix_block(int T, const u64 *__restrict_
   const int tid = threadIdx.x;
   const int n = T + 1, per = (n + NT - 1) / NT;
   const int ra = tid * per, rb = min(n, ra + per);
-  constexpr int MAXP = 16;
   if (per <= MAXP) {  // block-uniform: every load in flight at once, values kept in registers
     u64 va[MAXP], vb[MAXP], sa = 0, sb = 0;
 #pragma unroll
@@ -688,7 +687,7 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
 }
 
 template <int WS, int NT, int MODE>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_EMIT) ? 4 : 1))) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_EMIT) ? 3 : 1))) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
                                               int nq, int seq, int depth_log2,
                                               u64 *__restrict__ masks, u64 *__restrict__ dlv,
                                               int32_t *__restrict__ push_out,
@@ -734,7 +733,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
   const int qa = seq ? 0 : blockIdx.x;
   const int qb = !work ? qa : seq ? nq : blockIdx.x + 1;
   if constexpr (EMIT) {
-    if (blockIdx.x == gridDim.x - 1) canon_prefix_block<NT>(ea.fin.T, ea.fin.RG, ea.fin.CE, ea.fin.Gc, ea.fin.Ec, nullptr);
+    if (blockIdx.x == gridDim.x - 1) canon_prefix_block<NT, (4096 + NT - 1) / NT>(ea.fin.T, ea.fin.RG, ea.fin.CE, ea.fin.Gc, ea.fin.Ec, nullptr);
   }
   for (int qi = qa; qi < qb; qi++) {
     const SweepQuery q = qs[qi];
@@ -845,6 +844,43 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
             low = min(low, WEAK ? r - 1 - mv.dd : r - 1);
             if (tid == 0) s_ctl[0] = low;
             DR_TT(tt_ns++;)
+            cur = nxt;
+            --r;
+            continue;
+          }
+          // The query's own top round holds one vertex (its `from`): wave 0 expands
+          // it here -- one row, the round's weak-column words of that source --
+          // instead of a workgroup round (no far edges: merge sweeps run on the
+          // memo path, which has none; strong-only sweeps never read them).
+          if ((!PRUNE && (MERGE || !WEAK)) && !stop && r == q.top && q.src0 >= 0) {
+            const int s0 = q.src0;
+            const bool in = (__shfl(f & p, s0 >> 6) >> (s0 & 63)) & 1ULL;  // FE = {s0}
+            int lowmin = 0x7fffffff;
+            if (in) {
+              if (act) ring[(size_t)((r - 1) & dmask) * WS + tid] |= g.strong[((size_t)r * g.n + s0) * WS + tid];
+              if (tid == 0) {
+                my_edges += g.sdeg[(size_t)r * g.n + s0];
+                my_rowb += WS * 8 + 2;
+              }
+              if constexpr (WEAK) {
+                const uint32_t c0 = (uint32_t)__shfl((int)cur.C0, 0), c1 = (uint32_t)__shfl((int)cur.C1, 0);
+                for (uint32_t jj = c0 + tid; jj < c1; jj += 64) {
+                  if (!((g.wc_rows[(size_t)jj * WS + (s0 >> 6)] >> (s0 & 63)) & 1ULL)) continue;
+                  const uint32_t key = g.wc_key[jj];
+                  const int delta = (int)(key >> 11), ts = (int)(key & 2047u), tr = r - delta;
+                  my_wedges++;
+                  if (tr < q.bottom) continue;
+                  const u64 bit = 1ULL << (ts & 63);
+                  lowmin = min(lowmin, tr);
+                  if (delta < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
+                  else atomicOr(masks + q.mask_off + (int64_t)(tr - q.bottom) * WS + (ts >> 6), bit);
+                }
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) lowmin = min(lowmin, __shfl_xor(lowmin, off));
+              }
+            }
+            low = min(low, min(r - 1, lowmin));
+            if (tid == 0) s_ctl[0] = low;
             cur = nxt;
             --r;
             continue;

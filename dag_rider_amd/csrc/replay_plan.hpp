@@ -6,19 +6,22 @@
 // single-workgroup kernels do that planning on the device, so a whole replay is
 // one stream of launches and one host synchronisation:
 //
-//   k_summary_commit ... canonical prefixes      (round summaries + commits)
+//   k_summary_commit, k_weak_union   round summaries, commits, speculative
+//                                    canonical digests
+//   k_kcand, k_canon, k_emit_ids     canonical cone, re-emission from the first
+//                                    non-full round
 //   k_plan_chains     commit[] -> leader-chain queries   (process.go:341-350)
 //   k_sweep (chains)
 //   k_plan_pops       pushes -> leadersStack pops, distinct-leader queries
 //                     (process.go:404-412: pops run top first)
-//   k_sweep (delivery, merge with the canonical cone)
-//   k_plan_emit       stops -> emission segments + canonical prefix terms
-//   k_emit_count, k_emit_ids (work list)
-//   k_plan_final      outputs -> pinned host memory, totals
+//   k_sweep (delivery, SW_EMIT: merge with the canonical cone, emit the own
+//                     rounds; one extra workgroup: canonical prefixes G, E)
+//   k_replay_final    per-pop totals, outputs (kernels.hpp replay_final_block)
 //
+// (k_plan_emit / k_pop_final serve the per-call dr_order_vertices path.)
 // Every rule here restates the host planner line for line (same floors, same
-// out_off, same query order, same segment bounds), so both paths produce
-// identical replays; tests/test_gpu_parity.py runs both.
+// query order), so both paths produce identical replays;
+// tests/test_gpu_parity.py runs both.
 #pragma once
 #include "kernels.hpp"
 
