@@ -282,6 +282,7 @@ struct dr_ctx {
     v.wc_rows = wc_rows.as<u64>();
     v.wc_roff = wc_roff.as<uint32_t>();
     v.sdeg = sdeg.as<uint16_t>();
+    v.wdeg = wdeg.as<uint16_t>();
     v.lead = lead.as<uint16_t>();
     v.n = n;
     v.nrounds = nrounds;
@@ -419,9 +420,9 @@ constexpr int sweep_block() {
 // canonical sweep keep the wide block.  C4: pops 96 -> 75 us.
 template <int WS, int MODE>
 constexpr int sweep_block_m() {
-  // emitting pop sweeps at n = 1024: 3 waves, so every query of a C4 replay is
+  // merging pop sweeps at n = 1024: 3 waves, so every query of a C4 replay is
   // resident at once at 3 waves per SIMD (168 VGPRs: the emission fits unspilled)
-  if constexpr ((MODE & dr::SW_EMIT) && WS == 16) return 192;
+  if constexpr ((MODE & dr::SW_MERGE) && WS == 16) return 192;
   return (MODE & dr::SW_CHAIN) ? sweep_block<WS>() : WS == 16 ? 256 : sweep_block<WS>();
 }
 
@@ -456,7 +457,6 @@ struct SweepArgs {
   u64 *stats;
   const int *nq_dev = nullptr;  // planned replay: query count on the device, nq = grid upper bound
   uint32_t *rcnt = nullptr;     // planned delivery: per-mask-row vertex counts for the emission
-  dr::EmitArgs emit{};          // SW_EMIT: own-round emission outputs
 };
 
 template <int WS, int MODE>
@@ -467,11 +467,10 @@ hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   hipError_t e = hipFuncSetAttribute((const void *)dr::k_sweep<WS, NT, MODE>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  // SW_EMIT: one workgroup more (the canonical prefixes, then the final pass)
-  const int grid = a.seq ? 1 : a.nq + ((MODE & dr::SW_EMIT) ? 1 : 0);
+  const int grid = a.seq ? 1 : a.nq;
   hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(grid), dim3(NT), lds, c->stream,
                      c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
-                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt, a.emit);
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt);
   return hipGetLastError();
 }
 template <int WS>
@@ -482,8 +481,6 @@ hipError_t launch_sweep_t(dr_ctx *c, const SweepArgs &a, int mode) {
     case dr::SW_CHAIN: return launch_sweep_m<WS, dr::SW_CHAIN>(c, a);
     case dr::SW_WEAK | dr::SW_PRUNE: return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_PRUNE>(c, a);
     case dr::SW_WEAK | dr::SW_MERGE: return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_MERGE>(c, a);
-    case dr::SW_WEAK | dr::SW_MERGE | dr::SW_EMIT:
-      return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_MERGE | dr::SW_EMIT>(c, a);
   }
   return hipErrorInvalidValue;
 }
@@ -2145,6 +2142,49 @@ extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack,
 
 namespace {
 // bump allocator over one device buffer (sizing pass with base == nullptr)
+template <int WS>
+hipError_t launch_paper_emit_t(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq,
+                               const int32_t *firstpop, const int32_t *qcut, const int32_t *qlo,
+                               const uint32_t *firstK, const uint32_t *qr_off, const int32_t *qr_list, u64 *qcount,
+                               u64 *qdigest, u64 *qedges) {
+  hipLaunchKernelGGL((dr::k_paper_emit<WS, 512>), dim3(nw), dim3(512), 0, c->stream, c->view(), c->K.as<u64>(),
+                     c->masks.as<u64>(), plan, dq, firstpop, qcut, qlo, firstK, qr_off, qr_list,
+                     c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), qcount, qdigest, qedges);
+  return hipGetLastError();
+}
+hipError_t launch_paper_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq,
+                             const int32_t *firstpop, const int32_t *qcut, const int32_t *qlo, const uint32_t *firstK,
+                             const uint32_t *qr_off, const int32_t *qr_list, u64 *qcount, u64 *qdigest,
+                             u64 *qedges) {
+  switch (c->WS) {
+#define DR_PE(W) \
+  case W: return launch_paper_emit_t<W>(c, nw, plan, dq, firstpop, qcut, qlo, firstK, qr_off, qr_list, qcount, qdigest, qedges);
+    DR_PE(1) DR_PE(2) DR_PE(4) DR_PE(8) DR_PE(16) DR_PE(32)
+#undef DR_PE
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int WS>
+hipError_t launch_own_emit_t(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
+                             u64 *qcount, u64 *qdigest, int32_t *qcut) {
+  hipLaunchKernelGGL((dr::k_own_emit<WS, 512>), dim3(nw + 1), dim3(512), 0, c->stream, c->view(), c->masks.as<u64>(),
+                     c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(), c->slot_off.as<uint32_t>(),
+                     c->slot_src.as<uint16_t>(), qcount, qdigest, qcut, c->nrounds - 1, c->RG.as<u64>(),
+                     c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>());
+  return hipGetLastError();
+}
+hipError_t launch_own_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
+                           u64 *qcount, u64 *qdigest, int32_t *qcut) {
+  switch (c->WS) {
+#define DR_OE(W) \
+  case W: return launch_own_emit_t<W>(c, nw, plan, dq, stops, qcount, qdigest, qcut);
+    DR_OE(1) DR_OE(2) DR_OE(4) DR_OE(8) DR_OE(16) DR_OE(32)
+#undef DR_OE
+  }
+  return hipErrorInvalidValue;
+}
+
 struct Carve {
   char *base = nullptr;
   size_t off = 0;
@@ -2267,7 +2307,9 @@ int deliver_planned(dr_ctx *c, const std::vector<Pop> &pops, uint64_t *pcount, u
 // phases as the host-planned path below, planned by replay_plan.hpp's kernels,
 // with one host synchronisation.  Returns 1 when the bounds do not fit (the
 // caller then takes the host-planned path), else a DR_* status.
-int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
+// paper: DR_DELIVER_PAPER through the same pipeline, the delivery sweeps' masks
+// turned into first-pop ownership (replay_plan.hpp k_paper_*)
+int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out *o) {
   const int WS = c->WS, T = c->nrounds - 1;
   const bool persistent = chain_mode == DR_CHAIN_PERSISTENT;
   const int64_t pbound = persistent ? 2 * (int64_t)nw + 1 : (int64_t)nw * (nw + 1) / 2;
@@ -2284,8 +2326,9 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   uint32_t *push_off;
   uint8_t *seen, *hits;
   dr::SweepQuery *cq, *dq;
-  u64 *cedges, *cwedges, *dedges, *dwedges, *dstats, *qcount, *qdigest;
-  int32_t *cstops, *qcut;
+  u64 *cedges, *cwedges, *dedges, *dwedges, *dstats, *qcount, *qdigest, *qedges = nullptr;
+  int32_t *cstops, *qcut, *firstpop = nullptr, *qlo = nullptr, *qr_list = nullptr;
+  uint32_t *firstK = nullptr, *qr_cnt = nullptr, *qr_off = nullptr;
   for (int pass = 0; pass < 2; pass++) {
     cv.off = 0;
     plan = cv.take<int32_t>(dr::PL_N);
@@ -2307,6 +2350,16 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     qcount = cv.take<u64>(nw);
     qdigest = cv.take<u64>(nw);
     qcut = cv.take<int32_t>(nw);
+    if (paper) {
+      firstpop = cv.take<int32_t>(nw);
+      qlo = cv.take<int32_t>(nw);
+      qedges = cv.take<u64>(nw);
+      firstK = cv.take<uint32_t>((size_t)T + 2);
+      qr_cnt = cv.take<uint32_t>((size_t)T + 2);
+      qr_off = cv.take<uint32_t>((size_t)T + 3);
+      qr_list = cv.take<int32_t>(3 * (mask_words / WS));  // (owner, mask row offset) per entry: every
+                                                           // query's own range lies in its mask rows
+    }
     seen = cv.take<uint8_t>(nw + 1);
     qidx = cv.take<int32_t>(nw + 1);
     push_off = cv.take<uint32_t>(nw + 1);
@@ -2371,7 +2424,8 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
     return 0;
   };
   if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false)) return rc;
-  // 3+4. delivery sweeps, each emitting its own rounds (SW_EMIT)
+  if (paper) c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
+  // 3+4. delivery sweeps (merging with K), then each query's emission
   a.q = dq;
   a.push_out = nullptr;
   a.edges = dedges;
@@ -2380,10 +2434,10 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   a.stats = dstats;
   a.nq_dev = plan + dr::PL_NQD;
   a.rcnt = nullptr;
-  a.emit = dr::EmitArgs{c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), c->Cc.as<u64>(), qcount, qdigest, qcut,
+  dr::EmitArgs em{c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), c->Cc.as<u64>(), qcount, qdigest, qcut,
                         dr::FinalArgs{}};
   {
-    dr::FinalArgs &f = a.emit.fin;
+    dr::FinalArgs &f = em.fin;
     f.T = T;
     f.nw = nw;
     f.RG = c->RG.as<u64>();
@@ -2410,10 +2464,21 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, dr_replay_out *o) {
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
   HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
   HIPCHK(c, c->rec(2));
-  HIPCHK(c, launch_sweep(c, a, sweep_mode(probe) | dr::SW_EMIT));
+  HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
+  if (paper) {  // first-pop ownership, then each query's delivered rounds
+    hipLaunchKernelGGL((dr::k_paper_plan<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->memo_view().dmax, plan,
+                       pop_q, dq, dstops, firstpop, qcut, qlo, firstK, qr_cnt, qr_off, qr_list);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, launch_paper_emit(c, nw, plan, dq, firstpop, qcut, qlo, firstK, qr_off, qr_list, qcount, qdigest,
+                                qedges));
+    em.fin.firstpop = firstpop;
+    em.fin.qedges = qedges;
+  } else {  // REF: own rounds above the cut; the last workgroup: canonical prefixes G, E
+    HIPCHK(c, launch_own_emit(c, nw, plan, dq, dstops, qcount, qdigest, qcut));
+  }
   HIPCHK(c, c->rec(3));
   // 5. per-pop totals and outputs (the canonical prefixes came from the sweep launch's extra workgroup)
-  hipLaunchKernelGGL((dr::k_replay_final<1024>), dim3(1), dim3(1024), 0, c->stream, a.emit);
+  hipLaunchKernelGGL((dr::k_replay_final<1024>), dim3(1), dim3(1024), 0, c->stream, em);
   HIPCHK(c, hipGetLastError());
   c->plan_host.resize(out_bytes);
   HIPCHK(c, c->d2h(c->plan_host.data(), c->plan_out.p, out_bytes));
@@ -2479,9 +2544,9 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;
   o->canon_segments = -1;
-  if (c->plan_mode != 0 && c->use_memo && c->memo_ok() && deliver_mode == DR_DELIVER_REF &&
-      !(o->ids && o->ids_cap > 0) && o->push_wave && o->pop_count && o->pop_digest) {
-    const int rc = replay_planned(c, nwaves, chain_mode, o);
+  if (c->plan_mode != 0 && c->use_memo && c->memo_ok() && !(o->ids && o->ids_cap > 0) && o->push_wave &&
+      o->pop_count && o->pop_digest) {
+    const int rc = replay_planned(c, nwaves, chain_mode, deliver_mode == DR_DELIVER_PAPER, o);
     if (rc != 1) return rc;
   }
   // 0+1. round summaries + canonical cone, fused with the commit decisions of

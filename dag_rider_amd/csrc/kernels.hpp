@@ -75,6 +75,7 @@ struct DagView {
   const u64 *wc_rows;
   const uint32_t *wc_roff;
   const uint16_t *sdeg;  // [rounds][n] strong degree per vertex
+  const uint16_t *wdeg;  // [rounds][n] weak degree per vertex (far edges included)
   const uint16_t *lead;  // [wave] chooseLeader(w) (process.go:386-392), 1-based source
   int32_t n;
   int32_t nrounds;
@@ -435,9 +436,7 @@ __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWo
 //           F -> ring[r-1] and weak edges of F -> ring[r'].
 // LDS: F[WS] | FE[WS] | ring[depth][WS] | ctl (int[8]) | edges (u64[2]).
 // ---------------------------------------------------------------------------
-//   SW_EMIT   (with SW_MERGE, planned REF replay) after the sweep, the workgroup
-//             emits the query's own rounds itself (see emit_own_rounds)
-enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8, SW_EMIT = 16 };
+enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8 };
 
 // exclusive scan over one workgroup; s = NT/64 scratch slots; every thread calls
 template <int NT, class T>
@@ -542,7 +541,7 @@ struct FinalOut {
 struct FinalArgs {
   int T, nw;
   const u64 *RG, *CE;  // canonical per-round digests and edges
-  u64 *Gc, *Ec;        // their prefixes (the extra workgroup of the emitting sweep)
+  u64 *Gc, *Ec;        // their prefixes (k_own_emit's last workgroup)
   const u64 *Cc;
   const uint8_t *commit;
   const int32_t *vcount;
@@ -552,17 +551,19 @@ struct FinalArgs {
   const int32_t *stops;
   const u64 *dedges, *cedges, *dstats;
   const int32_t *nseg, *plan;
+  const int32_t *firstpop;  // PAPER (k_paper_*): the first pop of each query; later pops deliver nothing
+  const u64 *qedges;        // PAPER: the query's delivered edges
   FinalOut o;
 };
 
-// SW_EMIT outputs: per query, the count and order-sensitive digest of the
-// vertices of its own rounds (above the merge round), positions starting at
-// C_stop, the number of canonical vertices of rounds 1..stop.
+// The planned replay's per-query emission outputs (k_own_emit, k_paper_emit):
+// the count and order-sensitive digest of what each query's first pop delivers
+// beyond the canonical prefix (REF: its own rounds above the cut).
 struct EmitArgs {
   const uint32_t *slot_off;
   const uint16_t *slot_src;
   const u64 *Cc;  // canonical prefix counts (k_canon)
-  u64 *count;     // [query] own-round vertex count
+  u64 *count;     // [query] delivered vertex count (REF: own rounds)
   u64 *digest;    // [query] own-round digest terms
   int32_t *cut;   // [query] the canonical rounds are 1..cut (-1: none)
   FinalArgs fin;
@@ -572,9 +573,14 @@ struct EmitArgs {
 // holding word w) in insertion order, vertex k at position pos + rank.  Returns
 // this lane's share of the digest sum.
 // SPL: slots per lane per pass (16 in the sweep would cost it a wave per SIMD of occupancy).
-template <int WS, int SPL = 8>
+// DEG: also add the strong + weak degrees of the delivered vertices to *edges
+// (this lane's share; sdeg/wdeg indexed [round][source-1], row length n).
+template <int WS, int SPL = 8, bool DEG = false>
 __device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot_off,
-                                               const uint16_t *__restrict__ slot_src, int y, u64 mw, u64 pos) {
+                                               const uint16_t *__restrict__ slot_src, int y, u64 mw, u64 pos,
+                                               const uint16_t *__restrict__ sdeg = nullptr,
+                                               const uint16_t *__restrict__ wdeg = nullptr, int n = 0,
+                                               u64 *edges = nullptr) {
   const int lane = threadIdx.x & 63;
   u64 dg = 0;
   const uint32_t sa = slot_off[y], sb = slot_off[y + 1];
@@ -603,6 +609,10 @@ __device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot
     for (int j = 0; j < SPL; j++) {
       if (!((bits >> j) & 1u)) continue;
       dg += digest_term((uint32_t)y, (uint32_t)src[j], k);
+      if constexpr (DEG) {
+        const size_t at = (size_t)y * n + (src[j] - 1);
+        *edges += (u64)sdeg[at] + wdeg[at];
+      }
       k++;
     }
     pos += (u64)total;
@@ -612,8 +622,8 @@ __device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot
 
 
 
-// The planned replay's last pass (k_replay_final, after the emitting delivery
-// sweep, SW_EMIT): per pop, the canonical terms at its
+// The planned replay's last pass (k_replay_final, after k_own_emit or
+// k_paper_emit): per pop, the canonical terms at its
 // query's cut (C, G) and merge round (E) plus the query's own-round count,
 // digest and edges (what k_plan_emit + k_emit_ids + k_plan_final did in three
 // launches), the commits and pushes, and the totals, into the packed output
@@ -637,11 +647,18 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
     const int cur = f.pop_cur[p], pw = f.push_wave[p];
     const int stop = f.stops[q], cut = ea.cut[q], top = f.dq[q].top;
     u64 c = ea.count[q], d = ea.digest[q], e = f.dedges[q];
-    if (cut >= 0) {
-      c += f.Cc[cut];
-      d += f.Gc[cut];
+    if (f.firstpop) {  // PAPER: everything the query delivers goes to its first pop
+      const bool mine = f.firstpop[q] == (int32_t)p;
+      c = mine ? c : 0ULL;
+      d = mine ? d : 0ULL;
+      e = mine ? f.qedges[q] : 0ULL;
+    } else {
+      if (cut >= 0) {
+        c += f.Cc[cut];
+        d += f.Gc[cut];
+      }
+      if (stop >= 0) e += f.Ec[stop];  // the sweep counted the edges of rounds above stop
     }
-    if (stop >= 0) e += f.Ec[stop];  // the sweep counted the edges of rounds above stop
     bad |= cur < top;
     f.o.push_wave[p] = pw;
     f.o.pc[p] = c;
@@ -687,7 +704,7 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
 }
 
 template <int WS, int NT, int MODE>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_EMIT) ? 3 : 1))) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_MERGE) ? 3 : 1))) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
                                               int nq, int seq, int depth_log2,
                                               u64 *__restrict__ masks, u64 *__restrict__ dlv,
                                               int32_t *__restrict__ push_out,
@@ -697,27 +714,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
                                               uint8_t *__restrict__ hit_out,
                                               int32_t *__restrict__ stop_out,
                                               u64 *__restrict__ stats_out, const int *__restrict__ nq_dev,
-                                              uint32_t *__restrict__ rcnt, const EmitArgs ea) {
-  constexpr bool WEAK = MODE & SW_WEAK, CHAIN = MODE & SW_CHAIN, PRUNE = MODE & SW_PRUNE,
-                 MERGE = MODE & SW_MERGE, EMIT = (MODE & SW_EMIT) && (MODE & SW_MERGE);
-  // EMIT: the grid has one workgroup beyond the query bound, which computes the
-  // canonical prefixes G, E beside the sweeps (k_replay_final reads them)
-  bool work = true;
+                                              uint32_t *__restrict__ rcnt) {
   if (nq_dev) {  // grid sized by an upper bound, count on the device (planned replay)
     const int m = *nq_dev;
     if (seq) nq = m;
-    else if ((int)blockIdx.x >= m) {
-      if constexpr (!EMIT) return;
-      work = false;
-    }
+    else if ((int)blockIdx.x >= m) return;
   }
+  constexpr bool WEAK = MODE & SW_WEAK, CHAIN = MODE & SW_CHAIN, PRUNE = MODE & SW_PRUNE,
+                 MERGE = MODE & SW_MERGE;
   constexpr u64 WMASK = WS >= 64 ? ~0ULL : ((1ULL << WS) - 1ULL);  // lanes owning a frontier word
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
-  // EMIT: the delivered words (f & p) and counts of the query's top EMR rounds,
-  // kept by phase A so the own-round emission needs no mask reads or count pass
-  constexpr int EMR = EMIT ? 16 : 1;
-  __shared__ u64 s_emm[EMR * WS];
-  __shared__ uint32_t s_emc[EMR];
   u64 *F = smem;                // WS: frontier (reached ids, dangling included)
   u64 *FE = smem + WS;          // WS: F & present (the vertices that expand)
   u64 *ring = smem + 2 * WS;    // depth * WS
@@ -731,10 +737,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
   const bool act = tid < WS;    // lane w owns frontier word w
 
   const int qa = seq ? 0 : blockIdx.x;
-  const int qb = !work ? qa : seq ? nq : blockIdx.x + 1;
-  if constexpr (EMIT) {
-    if (blockIdx.x == gridDim.x - 1) canon_prefix_block<NT, (4096 + NT - 1) / NT>(ea.fin.T, ea.fin.RG, ea.fin.CE, ea.fin.Gc, ea.fin.Ec, nullptr);
-  }
+  const int qb = seq ? nq : blockIdx.x + 1;
   for (int qi = qa; qi < qb; qi++) {
     const SweepQuery q = qs[qi];
     const bool has_masks = q.flags & Q_MASKS;
@@ -819,17 +822,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
 #pragma unroll
             for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
             if (tid == 0) rcnt[q.mask_off / WS + (r - q.bottom)] = (uint32_t)pc;
-          }
-          if constexpr (EMIT) {
-            const int e = q.top - r;
-            if (e < EMR) {
-              const u64 fp = act ? f & p : 0ULL;
-              int pc = popc64(fp);
-#pragma unroll
-              for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
-              if (act) s_emm[e * WS + tid] = fp;
-              if (tid == 0) s_emc[e] = (uint32_t)pc;
-            }
           }
           if (stats_out && tid == 0 && !stop) {
             if (summary) st_short++;
@@ -920,63 +912,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_E
       --r;
     }
     DR_TT(const u64 tte = wall_clock64();)
-    if constexpr (EMIT) {
-      // The query's own rounds (planned REF replay): merged at m =
-      // stop, its delivered sequence is the canonical vertices of rounds 1..m
-      // then rounds m+1..top.  Rounds m..m+dmax-1 equal K (the merge run), so
-      // with cut = m+dmax-1 the positions of rounds m+1..cut are the canonical
-      // ones too: rounds 1..cut are canonical (C_cut, G_cut, added by the final
-      // pass) and only cut+1..top are emitted here; an unmerged sweep owns
-      // every round it reached.  Rounds go NT/64 at a time, one per wave:
-      // counts -> LDS -> each wave's base position.
-      constexpr int NWV = NT / 64;
-      __shared__ u64 s_em[NWV + 1];
-      const int lane = tid & 63, wid = tid >> 6;
-      const int sr = s_ctl[4];
-      const bool mg = s_ctl[3] != 0;
-      const int cut = mg ? sr + mv.dmax - 1 : -1;
-      const int first = mg ? cut + 1 : max(1, sr), last = q.top;
-      const u64 pos0 = mg ? ea.Cc[cut] : 0ULL;
-      u64 run = pos0, dg = 0;
-      if (tid == 0) s_em[NWV] = 0;
-      if (last - first < EMR) {  // block-uniform: every own round kept by phase A, no count pass
-        for (int y = first + wid; y <= last; y += NWV) {
-          u64 base = pos0;
-          for (int x = first; x < y; x++) base += s_emc[q.top - x];
-          const u64 mw = lane < WS ? s_emm[(q.top - y) * WS + lane] : 0ULL;
-          if (s_emc[q.top - y]) dg += wave_emit_round<WS>(ea.slot_off, ea.slot_src, y, mw, base);
-        }
-        for (int x = first; x <= last; x++) run += s_emc[q.top - x];
-      } else
-      for (int y0 = first; y0 <= last; y0 += NWV) {  // block-uniform
-        const int y = y0 + wid;
-        const bool on = y <= last;
-        u64 mw = 0;
-        if (on && lane < WS)  // this workgroup's own mask rows (phase A): agent-scope loads
-          mw = ld_agent(masks + q.mask_off + (int64_t)(y - q.bottom) * WS + lane) & g.present[(size_t)y * WS + lane];
-        const u64 cnt = wave_sum((u64)popc64(mw));
-        if (lane == 0) s_em[wid] = cnt;
-        __syncthreads();
-        u64 base = run, tot = 0;
-#pragma unroll
-        for (int i = 0; i < NWV; i++) {
-          const u64 c = s_em[i];
-          base += i < wid ? c : 0ULL;
-          tot += c;
-        }
-        if (on && cnt) dg += wave_emit_round<WS>(ea.slot_off, ea.slot_src, y, mw, base);
-        run += tot;
-        __syncthreads();  // s_em is rewritten by the next rounds
-      }
-      dg = wave_sum(dg);
-      if (lane == 0 && dg) atomicAdd(&s_em[NWV], dg);
-      __syncthreads();
-      if (tid == 0) {
-        ea.count[qi] = run - pos0;
-        ea.digest[qi] = s_em[NWV];
-        ea.cut[qi] = cut;
-      }
-    }
     // results
     DR_TT(tt_end = wall_clock64(); tt_emit = tt_end - tte;)
     my_edges += my_wedges;

@@ -24,6 +24,7 @@
 // tests/test_gpu_parity.py runs both.
 #pragma once
 #include "kernels.hpp"
+#include <climits>
 
 namespace dr {
 
@@ -345,6 +346,263 @@ __global__ __launch_bounds__(NT) void k_plan_final(int nw, const uint8_t *__rest
     h_hdr[PH_NQD] = (u64)nqd;
     h_hdr[PH_NSEG] = (u64)(int64_t)*nseg;
     h_hdr[PH_CAPERR] = (u64)caperr;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// PAPER-mode delivery (DR_DELIVER_PAPER) on the memo path.  Pop p delivers
+// cone(p) minus everything pops 0..p-1 delivered.  That set is downward closed,
+// so the pruned sweep of the oracle delivers exactly cone(p) \ U_{p'<p} cone(p').
+// Every vertex is delivered by the first pop whose cone holds it; only the first
+// pop of each query (distinct leader) can deliver anything.  From the delivery
+// sweeps' masks (SW_MERGE, no emission): query q's cone is K on rounds 1..cut_q
+// (merged: cut = merge round + dmax - 1) and its own mask rows on lo_q..top_q.
+// For round r the candidate owners are the first pop of the queries whose own
+// range holds r, and first_K(r) = the smallest first pop among the merged
+// queries with cut >= r (the first to hold K_r).
+// ---------------------------------------------------------------------------
+
+// One workgroup: first pops, cut / lo per query, first_K (a suffix minimum over
+// rounds), and per round the queries whose own range holds it (CSR: qr_off,
+// qr_list).  Scratch: qr_cnt [T+2].
+template <int NT>
+__global__ __launch_bounds__(NT) void k_paper_plan(int T, int dmax, const int32_t *__restrict__ plan,
+                                                   const int32_t *__restrict__ pop_q, const SweepQuery *__restrict__ dq,
+                                                   const int32_t *__restrict__ stops, int32_t *__restrict__ firstpop,
+                                                   int32_t *__restrict__ qcut, int32_t *__restrict__ qlo,
+                                                   uint32_t *__restrict__ firstK, uint32_t *__restrict__ qr_cnt,
+                                                   uint32_t *__restrict__ qr_off, int32_t *__restrict__ qr_list) {
+  __shared__ uint32_t s[NT / 64];
+  const int tid = threadIdx.x;
+  const int caperr = plan[PL_CAPERR];
+  const int64_t np = caperr ? 0 : plan[PL_NPUSH];
+  const int nq = caperr ? 0 : plan[PL_NQD];
+  for (int q = tid; q < nq; q += NT) firstpop[q] = INT_MAX;
+  for (int r = tid; r <= T + 1; r += NT) {
+    firstK[r] = 0xffffffffu;
+    qr_cnt[r] = 0;
+  }
+  __syncthreads();
+  for (int64_t p = tid; p < np; p += NT) atomicMin(&firstpop[pop_q[p]], (int32_t)p);
+  __syncthreads();
+  for (int q = tid; q < nq; q += NT) {
+    const int stop = stops[q], top = dq[q].top;
+    const int cut = stop >= 0 ? min(stop + dmax - 1, top) : -1;
+    const int lo = stop >= 0 ? cut + 1 : max(1, -1 - stop);
+    qcut[q] = cut;
+    qlo[q] = lo;
+    const uint32_t fp = (uint32_t)__hip_atomic_load(&firstpop[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cut >= 1) atomicMin(&firstK[cut], fp);
+    for (int r = lo; r <= top; r++) atomicAdd(&qr_cnt[r], 1u);
+  }
+  __syncthreads();
+  // first_K(r) = min over c >= r of firstK[c]; qr_off = exclusive prefix of qr_cnt
+  const int n = T + 2, per = (n + NT - 1) / NT;
+  const int ra = tid * per, rb = min(n, ra + per);
+  uint32_t mn = 0xffffffffu, cnt = 0;
+  for (int r = ra; r < rb; r++) {
+    mn = min(mn, __hip_atomic_load(&firstK[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    cnt += __hip_atomic_load(&qr_cnt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  uint32_t tot;
+  uint32_t run = block_scan_excl<NT>(cnt, s, tot);
+  // suffix minimum: the minimum over the threads above (wave shuffles, then the waves above)
+  __shared__ uint32_t smin[NT / 64];
+  const int lane = tid & 63, wid = tid >> 6;
+  uint32_t x = mn;  // inclusive suffix min within the wave
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_down(x, off);
+    if (lane + off < 64) x = min(x, y);
+  }
+  if (lane == 0) smin[wid] = x;
+  __syncthreads();
+  uint32_t above = 0xffffffffu;  // waves above this one
+  for (int i = wid + 1; i < NT / 64; i++) above = min(above, smin[i]);
+  const uint32_t nxt = __shfl_down(x, 1);
+  uint32_t suf = min(above, lane < 63 ? nxt : 0xffffffffu);
+  for (int r = rb - 1; r >= ra; r--) {
+    suf = min(suf, __hip_atomic_load(&firstK[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    firstK[r] = suf;
+  }
+  for (int r = ra; r < rb; r++) {
+    const uint32_t c = __hip_atomic_load(&qr_cnt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qr_off[r] = run;
+    run += c;
+    qr_cnt[r] = 0;  // the fill counter below
+  }
+  if (tid == NT - 1) qr_off[n] = run;
+  __syncthreads();
+  for (int q = tid; q < nq; q += NT) {
+    const int top = dq[q].top, lo = qlo[q];
+    for (int r = lo; r <= top; r++) {
+      const uint32_t at = __hip_atomic_load(&qr_off[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                          atomicAdd(&qr_cnt[r], 1u);
+      // (owner, mask row offset): k_paper_emit needs no further lookup
+      const int64_t mo = dq[q].mask_off;
+      qr_list[3 * (size_t)at] = __hip_atomic_load(&firstpop[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      qr_list[3 * (size_t)at + 1] = (int32_t)(uint32_t)mo;
+      qr_list[3 * (size_t)at + 2] = (int32_t)(mo >> 32);
+    }
+  }
+}
+
+// One workgroup per query q (its first pop p delivers): rounds a..top, a = the
+// first round with first_K = p (merged queries whose K range starts there) or
+// lo_q.  Round r: the base set (K_r when r <= cut_q, else q's mask row) & P_r,
+// minus the base sets of every candidate owner below p at r; positions from the
+// counts of the rounds below (NT/64 rounds at a time, one per wave).
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_paper_emit(DagView g, const u64 *__restrict__ K, const u64 *__restrict__ masks,
+                                                   const int32_t *__restrict__ plan, const SweepQuery *__restrict__ dq,
+                                                   const int32_t *__restrict__ firstpop,
+                                                   const int32_t *__restrict__ qcut, const int32_t *__restrict__ qlo,
+                                                   const uint32_t *__restrict__ firstK,
+                                                   const uint32_t *__restrict__ qr_off,
+                                                   const int32_t *__restrict__ qr_list,
+                                                   const uint32_t *__restrict__ slot_off,
+                                                   const uint16_t *__restrict__ slot_src,
+                                                   u64 *__restrict__ qcount, u64 *__restrict__ qdigest,
+                                                   u64 *__restrict__ qedges) {
+  constexpr int NWV = NT / 64;
+  __shared__ u64 s_c[NWV], s_acc[2];
+  __shared__ int s_a;
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (q >= plan[PL_NQD] || plan[PL_CAPERR]) return;
+  const int p = firstpop[q], cut = qcut[q], lo = qlo[q], top = dq[q].top;
+  const int64_t moff = dq[q].mask_off;
+  // first_K is non-decreasing in r: the first round l in 1..cut with first_K(l) >= p
+  // (a = l when first_K(l) == p, else lo).  The NT rounds below cut are probed at once
+  // (the boundary is usually a few rounds down); a binary search covers the rest.
+  if (tid == 0) {
+    s_acc[0] = s_acc[1] = 0;
+    s_a = cut >= 1 ? 0 : lo;  // 0: not found yet
+  }
+  __syncthreads();
+  if (cut >= 1) {
+    const int r = cut - tid;
+    if (r >= 1) {
+      const bool ge = (int64_t)firstK[r] >= (int64_t)p;
+      const bool below = r == 1 || (int64_t)firstK[r - 1] < (int64_t)p;
+      if (ge && below) s_a = (int64_t)firstK[r] == (int64_t)p ? r : lo;  // the unique boundary
+    }
+    __syncthreads();
+    if (tid == 0 && s_a == 0) {  // the boundary lies more than NT rounds below cut
+      int l = 1, h = max(1, cut - NT + 1);
+      while (l < h) {
+        const int m = (l + h) >> 1;
+        if ((int64_t)firstK[m] >= (int64_t)p) h = m; else l = m + 1;
+      }
+      s_a = (int64_t)firstK[l] == (int64_t)p ? l : lo;
+    }
+  }
+  __syncthreads();
+  const int a = s_a;
+  u64 run = 0, dg = 0, ed = 0;
+  for (int y0 = a; y0 <= top; y0 += NWV) {  // block-uniform
+    const int r = y0 + wid;
+    const bool on = r <= top;
+    u64 mw = 0;
+    if (on && lane < WS) {
+      const u64 pw = g.present[(size_t)r * WS + lane];
+      const uint32_t fk = firstK[r];
+      const u64 kw = K[(size_t)r * WS + lane];
+      u64 base = r <= cut ? kw : masks[moff + (int64_t)r * WS + lane];
+      u64 ex = (int64_t)fk < (int64_t)p ? kw : 0ULL;  // K's owner comes first
+      for (uint32_t i = qr_off[r]; i < qr_off[r + 1]; i++) {
+        const int32_t *e = qr_list + 3 * (size_t)i;
+        if (e[0] < p) {
+          const int64_t mo = (int64_t)(((uint64_t)(uint32_t)e[2] << 32) | (uint32_t)e[1]);
+          ex |= masks[mo + (int64_t)r * WS + lane];
+        }
+      }
+      mw = base & ~ex & pw;
+    }
+    const u64 cnt = wave_sum((u64)popc64(mw));
+    if (lane == 0) s_c[wid] = cnt;
+    __syncthreads();
+    u64 pos = run, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NWV; i++) {
+      const u64 c = s_c[i];
+      pos += i < wid ? c : 0ULL;
+      tot += c;
+    }
+    if (on && cnt)
+      dg += wave_emit_round<WS, 8, true>(slot_off, slot_src, r, mw, pos, g.sdeg, g.wdeg, g.n, &ed);
+    run += tot;
+    __syncthreads();
+  }
+  dg = wave_sum(dg);
+  ed = wave_sum(ed);
+  if (lane == 0) {
+    if (dg) atomicAdd(&s_acc[0], dg);
+    if (ed) atomicAdd(&s_acc[1], ed);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    qcount[q] = run;
+    qdigest[q] = s_acc[0];
+    qedges[q] = s_acc[1];
+  }
+}
+
+// REF delivery, own rounds (after the merging delivery sweeps, SW_MERGE): one
+// workgroup per query, rounds cut+1 .. top (cut = merge round + dmax - 1: the
+// merge run's rounds have the canonical positions too) or, for
+// an unmerged sweep, every round it reached; positions from C_cut on.  NT/64
+// rounds at a time, one per wave.  The grid's last workgroup computes the
+// canonical digest and edge prefixes G, E for k_replay_final.
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restrict__ masks, int dmax,
+                                                 const int32_t *__restrict__ plan, const SweepQuery *__restrict__ dq,
+                                                 const int32_t *__restrict__ stops, const u64 *__restrict__ Cc,
+                                                 const uint32_t *__restrict__ slot_off,
+                                                 const uint16_t *__restrict__ slot_src, u64 *__restrict__ qcount,
+                                                 u64 *__restrict__ qdigest, int32_t *__restrict__ qcut, int T,
+                                                 const u64 *__restrict__ RG, const u64 *__restrict__ CE,
+                                                 u64 *__restrict__ Gc, u64 *__restrict__ Ec) {
+  constexpr int NWV = NT / 64;
+  __shared__ u64 s_c[NWV], s_dg;
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (q == (int)gridDim.x - 1) {
+    canon_prefix_block<NT, (4096 + NT - 1) / NT>(T, RG, CE, Gc, Ec, nullptr);
+    return;
+  }
+  if (q >= plan[PL_NQD] || plan[PL_CAPERR]) return;
+  const int stop = stops[q], top = dq[q].top;
+  const int64_t moff = dq[q].mask_off;
+  const int cut = stop >= 0 ? min(stop + dmax - 1, top) : -1;
+  const int first = stop >= 0 ? cut + 1 : max(1, -1 - stop);
+  const u64 pos0 = cut >= 0 ? Cc[cut] : 0ULL;
+  if (tid == 0) s_dg = 0;
+  u64 run = pos0, dg = 0;
+  for (int y0 = first; y0 <= top; y0 += NWV) {  // block-uniform
+    const int r = y0 + wid;
+    const bool on = r <= top;
+    u64 mw = 0;
+    if (on && lane < WS) mw = masks[moff + (int64_t)r * WS + lane] & g.present[(size_t)r * WS + lane];
+    const u64 cnt = wave_sum((u64)popc64(mw));
+    if (lane == 0) s_c[wid] = cnt;
+    __syncthreads();
+    u64 pos = run, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NWV; i++) {
+      const u64 c = s_c[i];
+      pos += i < wid ? c : 0ULL;
+      tot += c;
+    }
+    if (on && cnt) dg += wave_emit_round<WS>(slot_off, slot_src, r, mw, pos);
+    run += tot;
+    __syncthreads();
+  }
+  dg = wave_sum(dg);
+  if (lane == 0 && dg) atomicAdd(&s_dg, dg);
+  __syncthreads();
+  if (tid == 0) {
+    qcount[q] = run - pos0;
+    qdigest[q] = s_dg;
+    qcut[q] = cut;
   }
 }
 

@@ -234,6 +234,28 @@ def test_device_planned_replay_matches_host_planned(gpu_device, name):
                 assert ei.value.code == L.DR_E_CAPACITY
 
 
+@pytest.mark.parametrize("name", ["c1", "c2", "c5"])
+def test_device_planned_paper_matches_host_planned(gpu_device, name):
+    """PAPER delivery on the device-planned path (first-pop ownership of the merge sweeps'
+    cones, replay_plan.hpp k_paper_*) against the host-planned pruned sweeps and the oracle."""
+    cfg = CONFIGS[name]
+    d = generate(cfg)
+    bs = oracle.PDag(d)
+    with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
+        e.append_packed(d)
+        for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+            e.set_device_plan(True)
+            a = e.replay(cfg.nwaves, cm, L.DR_DELIVER_PAPER)
+            e.set_device_plan(False)
+            b = e.replay(cfg.nwaves, cm, L.DR_DELIVER_PAPER)
+            _compare_replay(a, b, ids=False)
+            _compare_replay(a, bs.replay(cfg.faulty, cfg.nwaves, cm, L.DR_DELIVER_PAPER), ids=False)
+            e.set_device_plan(True)  # twice in a row: arena reuse, cone rebuilt after the PAPER replay
+            _compare_replay(e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF),
+                            bs.replay(cfg.faulty, cfg.nwaves, cm, L.DR_DELIVER_REF), ids=False)
+            _compare_replay(e.replay(cfg.nwaves, cm, L.DR_DELIVER_PAPER), b, ids=False)
+
+
 def test_c1_literal_ids(gpu_device):
     """C1 seeded n=4: full delivered sequence against the literal restatement."""
     cfg = CONFIGS["c1"]
