@@ -142,7 +142,9 @@ struct dr_ctx {
   DevBuf batch_arena;       // dr_replay_batch scratch + outputs (batch.hpp)
   std::vector<char> batch_host;  // dr_replay_batch output region, host side
   // memo needs every weak edge in the dense summary window
-  bool memo_ok() const { return nfar == 0 && dmax_near <= 17; }
+  // memo (round summaries + canonical cone): weak deltas up to 65 (WU holds dd = 64
+  // slots per round; the merge window is dmax rounds), no far edges
+  bool memo_ok() const { return nfar == 0 && dmax_near <= 65; }
   int memo_dd() const { return std::max(0, dmax_near - 1); }
   // scratch
   DevBuf q_buf, masks, dlv, push_out, push_n, edges, wedges, hits, commit, vcount, popdesc, rbase, counts,
@@ -1246,7 +1248,7 @@ void mark_rounds_clean(dr_ctx *c) {
 
 // Incremental round summaries (U, SD, WU) of the rounds appended or changed
 // since they were last built: one workgroup per stale round.  A DAG that left
-// the memo contract (far weak edges, deltas > 17) keeps none.
+// the memo contract (far weak edges, deltas > 65) keeps none.
 int refresh_rounds(dr_ctx *c) {
   if (!(c->use_memo && c->memo_ok())) return DR_OK;
   const int T = c->nrounds - 1;

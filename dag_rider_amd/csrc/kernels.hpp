@@ -1223,7 +1223,7 @@ __global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64
                                                    const int32_t *__restrict__ rounds,
                                                    const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
                                                    const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG) {
-  __shared__ u64 sWU[16 * WS];
+  __shared__ u64 sWU[64 * WS];  // dd <= 64 (dr_ctx::memo_ok)
   __shared__ u64 s_sc[NT / 64], s_rg;
   const int r = rounds ? rounds[blockIdx.x] : blockIdx.x + 1, tid = threadIdx.x;
   if (r > T) return;
