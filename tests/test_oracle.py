@@ -213,3 +213,32 @@ def test_large_golden_pins():
     for name in ("c3", "c4"):
         lit = g[name]["literal_ref"]
         assert len(lit["fingerprint"]) == 32 and lit["n_push"] > len(g[name]["persistent_ref"]["push_wave"])
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_paper_delivery_is_first_cone_owner(seed):
+    """The identity the device PAPER path rests on (replay_plan.hpp k_paper_*): the
+    delivered set is downward closed, so the oracle's pruned sweep delivers exactly
+    cone(p) minus the cones of the pops before p, in (round, slot) order -- every vertex
+    to the first pop whose REF cone holds it."""
+    rng = np.random.default_rng(4000 + seed)
+    n, R = int(rng.integers(4, 24)), int(rng.integers(8, 48))
+    depth = int(rng.integers(2, 12)) if seed % 3 else int(rng.integers(12, 30))
+    d = random_dag(rng, n, R, p_present=rng.uniform(0.5, 1), p_s=rng.uniform(0.05, 0.9), p_w=rng.uniform(0, 1),
+                   max_depth=depth)
+    f = int(rng.integers(0, (n - 1) // 3 + 2))
+    bs = oracle.PDag(d)
+    for cm in (oracle.CHAIN_LITERAL, oracle.CHAIN_PERSISTENT):
+        ref = bs.replay(f, R // 4, cm, oracle.DELIVER_REF, ids_cap=1 << 20)
+        pap = bs.replay(f, R // 4, cm, oracle.DELIVER_PAPER, ids_cap=1 << 20)
+        assert ref.rc == 0 and pap.rc == 0
+        assert (ref.push_wave == pap.push_wave).all()
+        ro = np.concatenate([[0], np.cumsum(ref.pop_count.astype(np.int64))])
+        po = np.concatenate([[0], np.cumsum(pap.pop_count.astype(np.int64))])
+        seen = set()
+        for p in range(len(ref.pop_count)):
+            cone = [tuple(v) for v in ref.ids[ro[p]:ro[p + 1]].tolist()]
+            want = [v for v in cone if v not in seen]
+            assert [tuple(v) for v in pap.ids[po[p]:po[p + 1]].tolist()] == want
+            assert int(pap.pop_digest[p]) == oracle.digest(want)
+            seen.update(cone)
