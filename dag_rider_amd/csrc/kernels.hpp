@@ -575,15 +575,15 @@ struct EmitArgs {
 // SPL: slots per lane per pass (16 in the sweep would cost it a wave per SIMD of occupancy).
 // DEG: also add the strong + weak degrees of the delivered vertices to *edges
 // (this lane's share; sdeg/wdeg indexed [round][source-1], row length n).
+// wave_emit_slots: the same with the round's slot range [sa, sb) already loaded.
 template <int WS, int SPL = 8, bool DEG = false>
-__device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot_off,
-                                               const uint16_t *__restrict__ slot_src, int y, u64 mw, u64 pos,
+__device__ __forceinline__ u64 wave_emit_slots(const uint16_t *__restrict__ slot_src, int y, uint32_t sa,
+                                               uint32_t sb, u64 mw, u64 pos,
                                                const uint16_t *__restrict__ sdeg = nullptr,
                                                const uint16_t *__restrict__ wdeg = nullptr, int n = 0,
                                                u64 *edges = nullptr) {
   const int lane = threadIdx.x & 63;
   u64 dg = 0;
-  const uint32_t sa = slot_off[y], sb = slot_off[y + 1];
   for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPL) {
     const uint32_t i0 = c0 + (uint32_t)lane * SPL;
     int src[SPL];
@@ -618,6 +618,14 @@ __device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot
     pos += (u64)total;
   }
   return dg;
+}
+template <int WS, int SPL = 8, bool DEG = false>
+__device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot_off,
+                                               const uint16_t *__restrict__ slot_src, int y, u64 mw, u64 pos,
+                                               const uint16_t *__restrict__ sdeg = nullptr,
+                                               const uint16_t *__restrict__ wdeg = nullptr, int n = 0,
+                                               u64 *edges = nullptr) {
+  return wave_emit_slots<WS, SPL, DEG>(slot_src, y, slot_off[y], slot_off[y + 1], mw, pos, sdeg, wdeg, n, edges);
 }
 
 

@@ -569,9 +569,11 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
     canon_prefix_block<NT, (4096 + NT - 1) / NT>(T, RG, CE, Gc, Ec, nullptr);
     return;
   }
-  if (q >= plan[PL_NQD] || plan[PL_CAPERR]) return;
+  // the query's fields load with the plan counts (the arena holds every slot below the grid bound)
+  const int nq = plan[PL_NQD], caperr = plan[PL_CAPERR];
   const int stop = stops[q], top = dq[q].top;
   const int64_t moff = dq[q].mask_off;
+  if (q >= nq || caperr) return;
   const int cut = stop >= 0 ? min(stop + dmax - 1, top) : -1;
   const int first = stop >= 0 ? cut + 1 : max(1, -1 - stop);
   const u64 pos0 = cut >= 0 ? Cc[cut] : 0ULL;
@@ -581,7 +583,12 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
     const int r = y0 + wid;
     const bool on = r <= top;
     u64 mw = 0;
-    if (on && lane < WS) mw = masks[moff + (int64_t)r * WS + lane] & g.present[(size_t)r * WS + lane];
+    uint32_t sa = 0, sb = 0;
+    if (on) {  // the slot range loads beside the mask row
+      sa = slot_off[r];
+      sb = slot_off[r + 1];
+      if (lane < WS) mw = masks[moff + (int64_t)r * WS + lane] & g.present[(size_t)r * WS + lane];
+    }
     const u64 cnt = wave_sum((u64)popc64(mw));
     if (lane == 0) s_c[wid] = cnt;
     __syncthreads();
@@ -592,7 +599,7 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
       pos += i < wid ? c : 0ULL;
       tot += c;
     }
-    if (on && cnt) dg += wave_emit_round<WS>(slot_off, slot_src, r, mw, pos);
+    if (on && cnt) dg += wave_emit_slots<WS>(slot_src, r, sa, sb, mw, pos);
     run += tot;
     __syncthreads();
   }
