@@ -1,7 +1,9 @@
 // host_rounds.cpp -- validation and host-state build of pre-packed rounds
-// (dr_append_rounds_packed), one round per OpenMP thread.  The weak-column
-// build is a table lookup per weak edge (C4: ~33 K weak edges per round), which
-// a per-wave append of 4 rounds paid serially.
+// (dr_append_rounds_packed).  The weak-column build is a table lookup per weak
+// edge (C4: ~31 K weak edges per round), so the work is split into (round,
+// source chunk) tasks over the OpenMP threads -- a per-wave append of 4 rounds
+// no longer leaves most cores idle -- and each round's chunk columns are merged
+// by key afterwards.
 #include "host_rounds.hpp"
 
 #include <algorithm>
@@ -26,13 +28,25 @@ int failf(std::string &err, int code, const char *fmt, ...) {
   return code;
 }
 
-// one round; tab is this thread's (delta, t) -> column table, all -1 on entry and exit
-int build_one(const PackedRounds &in, int i, std::vector<int32_t> &tab, BuiltRounds &out, size_t &nfar, int &dmax,
-              std::string &err) {
-  const int n = in.n, W = in.W, WS = in.WS, r = in.r0 + i;
-  const uint64_t lastmask = (n % 64) ? ((1ULL << (n % 64)) - 1ULL) : ~0ULL;
-  uint64_t *P = &out.pres[(size_t)i * WS];
+// One source chunk [s_lo, s_hi) of a round (64-aligned, so its columns cover
+// words [s_lo/64, s_hi/64) of every row): degrees, validation, weak columns.
+struct Chunk {
+  int rc = 0;
+  std::string err;
+  uint64_t deg = 0, nweak = 0;
+  size_t nfar = 0;
+  int dmax = 1;
+  std::vector<uint32_t> key;   // this chunk's distinct near targets, in first-seen order
+  std::vector<uint64_t> rows;  // [key][cw]: the chunk's words of each column
+  std::vector<uint64_t> far;
+};
+
+// The slot pass of round i (insertion order, presence, duplicate ids).
+int build_slots(const PackedRounds &in, int i, BuiltRounds &out, std::string &err) {
+  const int n = in.n, r = in.r0 + i;
+  uint64_t *P = &out.pres[(size_t)i * in.WS];
   HostRound &h = out.rounds[i];
+  h.slots.reserve(in.slot_off[i + 1] - in.slot_off[i]);
   for (uint32_t sl = in.slot_off[i]; sl < in.slot_off[i + 1]; sl++) {
     const int s = in.slot_src[sl];
     if (s > n) return failf(err, DR_E_CONTRACT, "round %d slot %u: source %d > n=%d", r, sl - in.slot_off[i], s, n);
@@ -43,39 +57,49 @@ int build_one(const PackedRounds &in, int i, std::vector<int32_t> &tab, BuiltRou
     if ((wd & bit) && r >= 1) return failf(err, DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, s);
     wd |= bit;
   }
+  return 0;
+}
+
+// tab is this thread's (delta, t) -> local column table, all -1 on entry and exit
+void build_chunk(const PackedRounds &in, int i, int s_lo, int s_hi, std::vector<int32_t> &tab, BuiltRounds &out,
+                 Chunk &ck) {
+  const int n = in.n, W = in.W, r = in.r0 + i;
+  const int w_lo = s_lo >> 6, cw = (s_hi - s_lo + 63) >> 6;
+  const uint64_t lastmask = (n % 64) ? ((1ULL << (n % 64)) - 1ULL) : ~0ULL;
+  const uint64_t *P = &out.pres[(size_t)i * in.WS];
   std::vector<uint32_t> touched;
-  int rc = 0;
-  for (int s0 = 0; s0 < n && !rc; s0++) {
+  int32_t *tb = tab.data();
+  const uint32_t *wt = in.weak_tgt;
+  int dm = ck.dmax;
+  std::string &err = ck.err;
+  for (int s0 = s_lo; s0 < s_hi; s0++) {
     const bool here = (P[s0 >> 6] >> (s0 & 63)) & 1ULL;
     const uint64_t *row = in.strong + ((size_t)i * n + s0) * W;
     uint64_t d = 0, any = 0;
     for (int w = 0; w < W; w++) { d += (uint64_t)__builtin_popcountll(row[w]); any |= row[w]; }
-    if (any && !here) { rc = failf(err, DR_E_CONTRACT, "round %d: strong edges on absent vertex (%d,%d)", r, r, s0 + 1); break; }
-    if (any && r == 0) { rc = failf(err, DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", s0 + 1); break; }
+    if (any && !here) { ck.rc = failf(err, DR_E_CONTRACT, "round %d: strong edges on absent vertex (%d,%d)", r, r, s0 + 1); break; }
+    if (any && r == 0) { ck.rc = failf(err, DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", s0 + 1); break; }
     if (row[W - 1] & ~lastmask) {
-      rc = failf(err, DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
+      ck.rc = failf(err, DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
       break;
     }
-    h.deg += d;
+    ck.deg += d;
     out.sdeg[(size_t)i * n + s0] = (uint16_t)d;
     const uint32_t ea = in.weak_off[(size_t)i * n + s0], eb = in.weak_off[(size_t)i * n + s0 + 1];
-    if (eb < ea) { rc = failf(err, DR_E_INVAL, "weak_off not monotone at round %d", r); break; }
-    if (eb > ea && !here) { rc = failf(err, DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1); break; }
+    if (eb < ea) { ck.rc = failf(err, DR_E_INVAL, "weak_off not monotone at round %d", r); break; }
+    if (eb > ea && !here) { ck.rc = failf(err, DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1); break; }
     out.wdeg[(size_t)i * n + s0] = (uint16_t)std::min<uint32_t>(eb - ea, 65535u);
-    h.nweak += eb - ea;
+    ck.nweak += eb - ea;
     const uint64_t mybit = 1ULL << (s0 & 63);
-    const int myword = s0 >> 6;
-    const uint32_t *wt = in.weak_tgt;
-    int32_t *tb = tab.data();
-    uint64_t *rows = h.wc_rows.data();  // re-read after a new column grows it
-    int dm = dmax;
+    const int myword = (s0 >> 6) - w_lo;
+    uint64_t *rows = ck.rows.data();  // re-read after a new column grows it
     for (uint32_t e = ea; e < eb; e++) {
       const uint32_t t = wt[e];
       const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
       if (ts >= n || tr > r - 2) {
-        rc = ts >= n ? failf(err, DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): source > n", r, s0 + 1, tr, ts + 1)
-                     : failf(err, DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target a round < r-1", r, s0 + 1, tr,
-                             ts + 1);
+        ck.rc = ts >= n ? failf(err, DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): source > n", r, s0 + 1, tr, ts + 1)
+                        : failf(err, DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target a round < r-1", r, s0 + 1,
+                                tr, ts + 1);
         break;
       }
       const int delta = r - tr;
@@ -83,41 +107,47 @@ int build_one(const PackedRounds &in, int i, std::vector<int32_t> &tab, BuiltRou
         const size_t at = (size_t)delta * n + ts;
         int32_t col = tb[at];
         if (col < 0) {
-          col = tb[at] = (int32_t)h.wc_key.size();
+          col = tb[at] = (int32_t)ck.key.size();
           touched.push_back((uint32_t)at);
-          h.wc_key.push_back(((uint32_t)delta << 11) | (uint32_t)ts);
-          h.wc_rows.resize(h.wc_rows.size() + WS, 0ULL);
-          rows = h.wc_rows.data();
+          ck.key.push_back(((uint32_t)delta << 11) | (uint32_t)ts);
+          ck.rows.resize(ck.rows.size() + cw, 0ULL);
+          rows = ck.rows.data();
         }
-        rows[(size_t)col * WS + myword] |= mybit;
+        rows[(size_t)col * cw + myword] |= mybit;
         dm = delta > dm ? delta : dm;
       } else {
-        h.far.push_back(((uint64_t)s0 << 32) | t);
-        nfar++;
+        ck.far.push_back(((uint64_t)s0 << 32) | t);
+        ck.nfar++;
       }
     }
-    dmax = dm;
+    if (ck.rc) break;
   }
+  ck.dmax = dm;
   for (uint32_t at : touched) tab[at] = -1;
-  if (rc) return rc;
-  // columns sorted by key (wc_add's binary search relies on it; no kernel does)
-  const size_t nk = h.wc_key.size();
-  bool sorted = true;
-  for (size_t x = 1; x < nk && sorted; x++) sorted = h.wc_key[x - 1] < h.wc_key[x];
-  if (!sorted) {
-    std::vector<uint32_t> order(nk);
-    for (size_t x = 0; x < nk; x++) order[x] = (uint32_t)x;
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return h.wc_key[a] < h.wc_key[b]; });
-    std::vector<uint32_t> keys(nk);
-    std::vector<uint64_t> rows(nk * WS);
-    for (size_t x = 0; x < nk; x++) {
-      keys[x] = h.wc_key[order[x]];
-      std::memcpy(&rows[x * WS], &h.wc_rows[(size_t)order[x] * WS], (size_t)WS * 8);
+}
+
+// Round i's columns: the union of its chunks' keys, sorted (wc_add's binary
+// search relies on it), each row the chunks' words side by side.
+void merge_round(const PackedRounds &in, int i, const Chunk *ck, int nch, int chunk, BuiltRounds &out) {
+  const int WS = in.WS, n = in.n;
+  HostRound &h = out.rounds[i];
+  std::vector<uint32_t> keys;
+  for (int c = 0; c < nch; c++) keys.insert(keys.end(), ck[c].key.begin(), ck[c].key.end());
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  h.wc_key = keys;
+  h.wc_rows.assign(keys.size() * WS, 0ULL);
+  for (int c = 0; c < nch; c++) {
+    const Chunk &x = ck[c];
+    const int s_lo = c * chunk, w_lo = s_lo >> 6, cw = (std::min(n, s_lo + chunk) - s_lo + 63) >> 6;
+    for (size_t j = 0; j < x.key.size(); j++) {
+      const size_t col = std::lower_bound(keys.begin(), keys.end(), x.key[j]) - keys.begin();
+      std::memcpy(&h.wc_rows[col * WS + w_lo], &x.rows[j * cw], (size_t)cw * 8);
     }
-    h.wc_key.swap(keys);
-    h.wc_rows.swap(rows);
+    h.deg += x.deg;
+    h.nweak += x.nweak;
+    h.far.insert(h.far.end(), x.far.begin(), x.far.end());
   }
-  return 0;
 }
 
 }  // namespace
@@ -128,29 +158,54 @@ int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std
   out.pres.assign((size_t)k * in.WS, 0);
   out.sdeg.assign((size_t)k * n, 0);
   out.wdeg.assign((size_t)k * n, 0);
-  std::vector<int> rc(k, 0), dm(k, dmax0);
-  std::vector<size_t> nf(k, 0);
-  std::vector<std::string> msg(k);
   const uint64_t nweak = in.weak_off[(size_t)k * n] - in.weak_off[0];
-  const bool par = k > 1 && nweak >= 8192;  // thread start-up costs more than tiny rounds
-  const int nth = std::max(1, std::min(k, omp_get_max_threads()));  // no idle team members
+  const bool par = nweak >= 8192;  // thread start-up costs more than tiny appends
+  const int nthr = par ? std::max(1, omp_get_max_threads()) : 1;
+  // source chunks per round: enough (round, chunk) tasks for every thread, 64-aligned
+  const int nwords = (n + 63) / 64;
+  const int nch = std::max(1, std::min(nwords, (nthr + k - 1) / k));
+  const int chunk = ((nwords + nch - 1) / nch) * 64;
+  const int ntask = k * nch;
+  std::vector<int> src(k, 0);
+  std::vector<std::string> smsg(k);
+  std::vector<Chunk> ck((size_t)ntask);
+  for (auto &c : ck) c.dmax = dmax0;
+  const int nth = std::max(1, std::min(ntask, nthr));  // no idle team members
 #pragma omp parallel num_threads(nth) if (par)
   {
     // per thread, kept across calls (all -1 between uses): (delta, t) -> column
     static thread_local std::vector<int32_t> tab;
     if (tab.size() < (size_t)1024 * n) tab.assign((size_t)1024 * n, -1);
+#pragma omp for schedule(static)
+    for (int i = 0; i < k; i++) src[i] = build_slots(in, i, out, smsg[i]);  // presence before the chunks
 #pragma omp for schedule(dynamic, 1)
-    for (int i = 0; i < k; i++) rc[i] = build_one(in, i, tab, out, nf[i], dm[i], msg[i]);
+    for (int t = 0; t < ntask; t++) {
+      const int i = t / nch, c = t % nch;
+      const int s_lo = c * chunk, s_hi = std::min(n, s_lo + chunk);
+      if (src[i] == 0 && s_lo < s_hi) build_chunk(in, i, s_lo, s_hi, tab, out, ck[t]);
+    }
+#pragma omp for schedule(static)
+    for (int i = 0; i < k; i++)
+      if (src[i] == 0) merge_round(in, i, &ck[(size_t)i * nch], nch, chunk, out);
   }
+  // errors as a sequential pass over the rounds reports them: a round's slot pass,
+  // then its sources in order
   out.nfar = 0;
   out.dmax = dmax0;
   for (int i = 0; i < k; i++) {
-    if (rc[i]) {
-      err = msg[i];
-      return rc[i];
+    if (src[i]) {
+      err = smsg[i];
+      return src[i];
     }
-    out.nfar += nf[i];
-    out.dmax = std::max(out.dmax, dm[i]);
+    for (int c = 0; c < nch; c++) {
+      const Chunk &x = ck[(size_t)i * nch + c];
+      if (x.rc) {
+        err = x.err;
+        return x.rc;
+      }
+      out.nfar += x.nfar;
+      out.dmax = std::max(out.dmax, x.dmax);
+    }
   }
   return 0;
 }
