@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdarg>
 #include <cstdio>
@@ -461,13 +462,28 @@ struct SweepArgs {
   uint32_t *rcnt = nullptr;     // planned delivery: per-mask-row vertex counts for the emission
 };
 
+// Raise a kernel's dynamic-LDS limit once per (device, size it has not seen yet):
+// a host call per launch otherwise, and the replay launches sweeps every step.
+constexpr int kLdsDevs = 16;
+inline hipError_t lds_limit(const void *fn, std::atomic<int> *seen, int dev, size_t lds) {
+  std::atomic<int> *sl = dev >= 0 && dev < kLdsDevs ? &seen[dev] : nullptr;
+  if (sl && (int)lds <= sl->load(std::memory_order_relaxed)) return hipSuccess;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess && sl) {
+    int cur = sl->load(std::memory_order_relaxed);
+    while ((int)lds > cur && !sl->compare_exchange_weak(cur, (int)lds)) {
+    }
+  }
+  return e;
+}
+
 template <int WS, int MODE>
 hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   constexpr int NT = sweep_block_m<WS, MODE>();
   const int dl = c->depth_log2();
   const size_t lds = c->sweep_lds(dl);
-  hipError_t e = hipFuncSetAttribute((const void *)dr::k_sweep<WS, NT, MODE>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static std::atomic<int> seen[kLdsDevs] = {};
+  hipError_t e = lds_limit((const void *)dr::k_sweep<WS, NT, MODE>, seen, c->dev, lds);
   if (e != hipSuccess) return e;
   const int grid = a.seq ? 1 : a.nq;
   hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(grid), dim3(NT), lds, c->stream,
@@ -640,7 +656,8 @@ hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo, bool spec) {
   const int dl = c->depth_log2();
   const size_t lds = c->sweep_lds(dl);
   constexpr int NTS = sweep_block<WS>();
-  e = hipFuncSetAttribute((const void *)dr::k_canon<WS, NTS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static std::atomic<int> seen[kLdsDevs] = {};
+  e = lds_limit((const void *)dr::k_canon<WS, NTS>, seen, c->dev, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((dr::k_canon<WS, NTS>), dim3(1), dim3(NTS), lds, c->stream, c->view(), mv, T, dl,
                      c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>(), c->RD.as<u64>(),
