@@ -79,11 +79,13 @@ int dr_coin_leader(uint64_t seed, int wave, int n);
 int dr_wave_leader(const dr_ctx *ctx, int wave);
 
 /* DR_OPT_MEMO (default 1): use round summaries + the canonical cone for
- * orderVertices / path sweeps (identical results; 0 = sweep every cone).
+ * orderVertices / path sweeps (identical results; 0 = sweep every cone).  It
+ * applies while every weak delta is <= 65 and no weak edge spans more than
+ * 1023 rounds.
  * DR_OPT_DEVICE_PLAN (default 1): dr_replay plans its chain, pop and emission
  * phases on the device (one host synchronisation per replay) when summaries
- * are on, deliver_mode is DR_DELIVER_REF and no ids are requested; 0 = plan
- * on the host between phases (identical results).
+ * are on and no ids are requested, in both delivery modes; 0 = plan on the
+ * host between phases (identical results).
  * DR_OPT_PHASE_TIMING (default 2): HIP events time every phase of a
  * device-planned dr_replay (ms_* outputs); 1 = the summary pass only, 0 = none
  * (untimed ms_* are 0).  Each timed event costs the stream a few microseconds. */
