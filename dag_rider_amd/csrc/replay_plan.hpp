@@ -148,13 +148,14 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
     }
   }
   __syncthreads();
-  for (int w = 1 + tid; w <= nw + 1; w += NT) {  // pushes before wave w
-    int lo = 0, hi = ntask;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (task_wave[mid] >= w) hi = mid; else lo = mid + 1;
-    }
-    push_off[w - 1] = (uint32_t)(lo < ntask ? task_pos[lo] : np);
+  // pushes before wave w = the position of the first task with wave >= w (np
+  // past the last): task t owns the waves after its predecessor's, up to its own
+  // (task waves increase), so each writes its range -- no search per wave
+  for (int t = tid; t <= ntask; t += NT) {
+    const int wlo = t == 0 ? 1 : task_wave[t - 1] + 1;
+    const int whi = t < ntask ? task_wave[t] : nw + 1;
+    const uint32_t v = (uint32_t)(t < ntask ? task_pos[t] : np);
+    for (int w = wlo; w <= whi; w++) push_off[w - 1] = v;
   }
   if (tid == 0) c0 = 0;
   __syncthreads();
