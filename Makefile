@@ -39,7 +39,7 @@ $(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/wa
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/engine_timing.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/wave_ops.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DDR_SWEEP_TIMING -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DDR_SWEEP_TIMING -DDR_TUNING -c $< -o $@
 
 $(LIBT): $(BUILD)/engine_timing.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdagrider_gpu_timing.so

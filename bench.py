@@ -10,7 +10,8 @@ one dr_replay of the resident DAG.  Edges are counted by SURVEY.md s8(d)'s formu
 
 Other lines (--config): c3 (n=256 x 10k rounds, weak-heavy: the metric's other
 half), c2, c5 (4096 independent n=128 replays, split across ranks), c4-deep (weak
-edges past the memo window: every pop sweeps its cone), c4-loop (the drop-in call
+edges 80 rounds deep, past the memo window of 65: every pop sweeps its cone),
+c4-deep64 (weak edges 64 deep: memoized at the window's far end), c4-loop (the drop-in call
 pattern: per wave append 4 rounds -> dr_wave_ready -> dr_order_vertices, per-wave
 latency), --deliver paper (dedup across pops).
 
@@ -46,6 +47,17 @@ PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 1024, 2, false>"],
                  "sweep": ["dr::k_sweep<16, 256, 9>"],
                  "batch": ["dr::k_replay_small<8, false, true>"]}
 CPU_THREADS = 16  # the GPU box's host share for one GPU (OMP_NUM_THREADS there)
+
+
+def cpu_threads() -> int:
+    """Host threads the CPU baselines use: this GPU's share of the box.  The GPU box
+    exports OMP_NUM_THREADS=16 per GPU; os.sched_getaffinity there lists every thread
+    of the (shared) host, which the box's rules forbid one GPU's job to take over."""
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", CPU_THREADS))
+    except ValueError:
+        share = CPU_THREADS
+    return max(1, min(share, cpu_info()["affinity"] or 1))
 
 
 def measured_traffic(phase):
@@ -93,15 +105,13 @@ def cpu_literal(cfg, d, budget_s: float, full_edges: int, deliver_mode: int):
     """The oracle's literal restatement of process.go (the reference's algorithm: BFS +
     hash-set visited + linear id scans, one BFS per voter and per orderVertices
     candidate) on a bounded sample: a replay of waves 1..k.  Single thread (the
-    reference is one goroutine) and one thread per core (the independent BFSs of the
-    voter loop and of a pop's candidates in parallel); median of 5 runs each.  The
-    literal cost per wave grows ~ w^2 (every pop BFSes a cone of ~4w rounds for each
-    of 4w*n candidates), so the full replay is extrapolated two ways: per edge at the
-    sample's rate (a lower bound) and by fitting t(w) = a + b w^2 to the measured
-    per-wave times."""
+    reference is one goroutine) and one thread per core of this GPU's host share
+    (the independent BFSs of the voter loop and of a pop's candidates in parallel);
+    median of 5 runs each.  The full replay is extrapolated per edge at the sample's
+    rate (a lower bound) and by the per-wave cost model of literal_wave_model."""
     import oracle
 
-    nt = min(CPU_THREADS, cpu_info()["affinity"] or 1)
+    nt = cpu_threads()
     k, cum = 0, []
     while k < min(cfg.nwaves, 6):
         k += 1
@@ -112,7 +122,6 @@ def cpu_literal(cfg, d, budget_s: float, full_edges: int, deliver_mode: int):
         assert r.rc == 0
         if cum[-1] * 4 > budget_s / 4:
             break
-    per_wave = [cum[0]] + [max(cum[i] - cum[i - 1], 1e-9) for i in range(1, len(cum))]
     ld = oracle.LDag(packed=d, nrounds=4 * k + 1)
     mt_med, mt_ts, r = _median_runs(
         lambda: ld.replay(cfg.faulty, k, oracle.CHAIN_PERSISTENT, deliver_mode, nthreads=nt), 5)
@@ -120,26 +129,79 @@ def cpu_literal(cfg, d, budget_s: float, full_edges: int, deliver_mode: int):
     ld1 = oracle.LDag(packed=d, nrounds=5)
     st_med, st_ts, r1 = _median_runs(lambda: ld1.replay(cfg.faulty, 1, oracle.CHAIN_PERSISTENT, deliver_mode), 5)
     e1 = r1.commit_edges + r1.deliver_edges
-    import numpy as np
-
-    w = np.arange(1, len(per_wave) + 1, dtype=np.float64)
-    if len(per_wave) >= 2:
-        (fa, fb), *_ = np.linalg.lstsq(np.stack([np.ones_like(w), w * w], 1), np.asarray(per_wave), rcond=None)
-        fa, fb = max(float(fa), 0.0), max(float(fb), 0.0)
-    else:
-        fa, fb = per_wave[0], 0.0
-    N = cfg.nwaves
-    full_mt = fa * N + fb * N * (N + 1) * (2 * N + 1) / 6
+    model = literal_wave_model(cfg, d, nt) if cfg.n * cfg.last_round >= 64 * 1000 else None
     return dict(value=e1 / st_med, unit="edges/s", cores=1, kind="port",
                 sample=f"{cfg.name} waves 1..1 (rounds 0..4) literal replay (oracle/ref_literal.c, the reference's "
                        f"algorithm), single thread: {e1} edges, median {st_med:.2f} s of 5 runs",
                 runs_s=st_ts,
                 all_cores=dict(value=edges / mt_med, cores=nt, waves=k, edges=edges, median_s=mt_med, runs_s=mt_ts,
-                               per_wave_s=per_wave),
+                               cum_s=cum),
                 extrapolated_full_s_per_edge=full_edges / (e1 / st_med),
-                extrapolated_full_s_fit_all_cores=full_mt,
-                extrapolated_full_s_fit_single=full_mt * st_med / max(cum[0], 1e-9),
-                fit=dict(model="t(w) = a + b w^2 (all cores)", a=fa, b=fb), host=cpu_info())
+                wave_model=model, host=cpu_info())
+
+
+def literal_wave_model(cfg, d, nt: int, waves=(2, 3, 4, 6, 8, 12, 16), per_wave: int = 64, seed: int = 1):
+    """Per-wave cost of the literal replay, measured on samples and fitted with a free
+    intercept.  orderVertices of wave w's leader runs one path() BFS per slot of rounds
+    1..4w (process.go:414-431); a BFS costs ~ the part of the leader's cone it explores
+    (the whole cone when the slot is unreachable), so its mean time grows ~ linearly in w
+    and the pop costs N_cand(w) x mean(w) ~ w^2.  For each sampled wave: per_wave slots,
+    one in each of per_wave evenly spaced rounds of 1..4w (stratified by round), each
+    BFS timed on its own thread's CPU clock (thread_time, on nt threads).  Fit mean(w) = a + b w (least squares, free intercept,
+    residuals reported); full replay = sum over all waves of the voter time (mean of the
+    samples) + N_cand(w) x (a + b w), single thread.  The voters of waveReady(w)
+    (process.go:330-335) are sampled the same way: per_wave/4 slots of round 4w per wave."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    import oracle
+
+    waves = [w for w in waves if w <= cfg.nwaves]
+    top = 4 * max(waves) + 1
+    ld = oracle.LDag(packed=d, nrounds=top)
+    rng = np.random.default_rng(seed)
+    so = d.slot_off.astype(np.int64)
+    jobs = []
+    for w in waves:
+        rounds = np.unique(np.linspace(1, 4 * w, per_wave).round().astype(np.int64))
+        rounds = np.resize(rounds, per_wave)
+        for r in rounds:
+            if so[r + 1] > so[r]:
+                s = int(d.slot_src[int(rng.integers(so[r], so[r + 1]))])
+                jobs.append(("pop", w, (4 * w - 3, 1), (int(r), s) if s else (0, 0), False))
+        # voters: slots of round 4w, path(v, leader, strong) (process.go:330-335)
+        for i in rng.integers(so[4 * w], so[4 * w + 1], size=per_wave // 4):
+            s = int(d.slot_src[int(i)])
+            jobs.append(("vote", w, (4 * w, s) if s else (0, 0), (4 * w - 3, 1), True))
+
+    def one(job):
+        kind, w, fr, to, strong = job
+        t0 = time.thread_time()
+        ld.path(fr, to, strong)
+        return kind, w, time.thread_time() - t0
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(nt) as ex:
+        res = list(ex.map(one, jobs))
+    wall = time.perf_counter() - t0
+    mean = {w: float(np.mean([t for k, ww, t in res if k == "pop" and ww == w])) for w in waves}
+    vmean = float(np.mean([t for k, _, t in res if k == "vote"]))
+    x = np.asarray(waves, np.float64)
+    y = np.asarray([mean[w] for w in waves])
+    (a, b), *_ = np.linalg.lstsq(np.stack([np.ones_like(x), x], 1), y, rcond=None)
+    pred = a + b * x
+    ncand = lambda w: int(so[min(4 * w, d.nrounds - 1) + 1] - so[1])
+    nvote = lambda w: int(so[4 * w + 1] - so[4 * w])
+    full = sum(nvote(w) * vmean + ncand(w) * max(a + b * w, 0.0) for w in range(1, cfg.nwaves + 1))
+    return dict(model="wave(w) = N_vote(w) x v + N_cand(w) x (a + b w); N_cand(w) = slots of rounds 1..4w, "
+                      "N_vote(w) = slots of round 4w, v = mean voter BFS",
+                waves=waves, bfs_samples_per_wave=per_wave, bfs_mean_s={str(w): mean[w] for w in waves},
+                voter_bfs_mean_s=vmean, voter_samples=len([j for j in jobs if j[0] == "vote"]), a=float(a), b=float(b),
+                residual_rel={str(w): float((yy - pp) / yy) for w, yy, pp in zip(waves, y, pred)},
+                r2=float(1 - ((y - pred) ** 2).sum() / max(((y - y.mean()) ** 2).sum(), 1e-30)),
+                sample_wall_s=wall, threads=nt, extrapolated_full_s_single_thread=full,
+                extrapolated_full_s_all_threads=full / nt)
 
 
 def cpu_bitset(cfg, d, nthreads: int, full_runs: int, deliver_mode: int):
@@ -155,6 +217,17 @@ def cpu_bitset(cfg, d, nthreads: int, full_runs: int, deliver_mode: int):
                 sample=f"{cfg.name} full replay ({cfg.nwaves} waves) bitset restatement (oracle/ref_bitset.c, "
                        f"OpenMP {nthreads} threads): {e} edges, median {med:.3f} s of {full_runs} runs",
                 runs_s=ts), r
+
+
+def same_replay(a, b) -> bool:
+    """Every replay output equal (tests/test_coin.py _same): commits, vote counts, push
+    offsets and pushed waves, per-pop count / digest / edges, and every edge total."""
+    import numpy as np
+
+    arr = ("commit", "vcount", "push_off", "push_wave", "pop_count", "pop_digest", "pop_edges")
+    return bool(all(np.array_equal(np.asarray(getattr(a, k)), np.asarray(getattr(b, k))) for k in arr)
+                and (a.commit_edges, a.chain_edges, a.deliver_edges) == (b.commit_edges, b.chain_edges,
+                                                                         b.deliver_edges))
 
 
 def kernel_bytes(cfg, d, res):
@@ -227,52 +300,18 @@ def reduce_over_ranks(dist, dt: float, edges: int, device: str):
     return float(t.item()), float(e.item())
 
 
-def wave_slice(d, w0: int, w1: int):
-    """The rounds waves w0..w1 read for their commit decisions, as a DAG of its own:
-    round 4(w0-1) .. 4 w1 shifted to 0 .. 4(w1-w0+1) (round 0 keeps presence only; weak
-    edges dropped: the commit rule follows strong edges inside the wave)."""
-    import numpy as np
-
-    from dag_rider_amd.dag import PackedDag
-
-    n, W = d.n, d.W
-    lo, hi = 4 * (w0 - 1), 4 * w1
-    so = d.slot_off[lo:hi + 2].astype(np.int64)
-    strong = d.strong[lo * n * W:(hi + 1) * n * W].copy()
-    strong[:n * W] = 0
-    k = hi - lo + 1
-    return PackedDag(n, k, (so - so[0]).astype(np.uint32), d.slot_src[so[0]:so[-1]].copy(), strong,
-                     np.zeros(k * n + 1, np.uint32), np.zeros(0, np.uint32))
-
-
 def commit_split(dist, rank: int, world: int, local: int, want_commit=None, want_vcount=None, iters: int = 20):
     """the all-waves commit sweep of ONE C4 DAG (seed 4), waves
-    split into contiguous ranges, one per GPU, each GPU holding only its rounds; no
-    exchange.  Returns rank 0's view: max time over ranks, bit-exact check of the
-    gathered commits against the full replay on rank 0."""
+    split into contiguous ranges, one per GPU, each GPU holding only its rounds
+    (dag_rider_amd/split.py); no exchange.  Returns rank 0's view: max time over
+    ranks, bit-exact check of the gathered commits against the full replay on rank 0."""
     import numpy as np
-    import torch
 
-    from dag_rider_amd.engine import Engine
     from dag_rider_amd.gen import CONFIGS, generate
 
     cfg = CONFIGS["c4"]
     d = generate(cfg, nthreads=CPU_THREADS)
-    nw = cfg.nwaves
-    w0, w1 = rank * nw // world + 1, (rank + 1) * nw // world
-    sub = wave_slice(d, w0, w1)
-    with Engine(cfg.n, cfg.faulty, sub.nrounds, local) as e:
-        e.append_packed(sub)
-        cm, vc = e.wave_commit(1, w1 - w0 + 1)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            cm, vc = e.wave_commit(1, w1 - w0 + 1)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / iters
-    mine = dict(rank=rank, w0=w0, w1=w1, commit=cm.tolist(), vcount=vc.tolist(), ms=dt * 1e3)
+    mine = rank_share(cfg, d, rank, world, local, iters, dist)
     allr = [None] * world
     if dist:
         dist.all_gather_object(allr, mine)
@@ -286,12 +325,107 @@ def commit_split(dist, rank: int, world: int, local: int, want_commit=None, want
     if want_commit is not None:
         ok = bool((cmt == want_commit).all() and (vct == want_vcount).all())
     ms = max(r["ms"] for r in allr)
-    n, W = cfg.n, (cfg.n + 63) // 64
-    leaders = int((vct >= 0).sum())
-    alg = leaders * (n * 16 + 2 * n * W * 8)  # k_commit: the leader's chunk of round 4w-2, rounds 4w-1, 4w whole
-    return dict(waves=nw, ranges=[(r["w0"], r["w1"]) for r in allr], ms_max_over_ranks=ms,
-                waves_per_s=nw / (ms / 1e3), algorithmic_bytes=alg, GBps=alg / (ms / 1e3) / 1e9,
-                verify_vs_full_replay=ok, note="dr_wave_commit (k_commit) per rank, wall clock incl. D2H")
+    kms = max(r["kernel_ms"] for r in allr)
+    alg = sum(r["bytes"] for r in allr)
+    return dict(waves=cfg.nwaves, ranges=[(r["w0"], r["w1"]) for r in allr], ms_max_over_ranks=ms,
+                kernel_ms_max_over_ranks=kms, waves_per_s=cfg.nwaves / (ms / 1e3), algorithmic_bytes=alg,
+                per_rank=[{k: r[k] for k in ("rank", "w0", "w1", "ms", "kernel_ms", "bytes", "GBps_kernel")}
+                          for r in allr],
+                verify_vs_full_replay=ok, note="dr_wave_commit (k_commit) per rank: ms = wall clock incl. D2H, "
+                "kernel_ms = HIP events (dr_last_kernel_ms)")
+
+
+def commit_bytes(n: int, W: int, leaders: int) -> int:
+    """k_commit's algorithmic bytes: per wave with a leader, the leader's 16-B chunk of
+    each row of round 4w-2 and rounds 4w-1, 4w whole (bench kernel_bytes 'commit')."""
+    return leaders * (n * 16 + 2 * n * W * 8)
+
+
+def rank_share(cfg, d, rank: int, world: int, local: int, iters: int, dist=None):
+    """One rank's share of the wave-range commit split: its slice of rounds on its own
+    mirror, dr_wave_commit over its waves, timed (wall clock and HIP events)."""
+    import numpy as np
+    import torch
+
+    from dag_rider_amd.engine import Engine
+    from dag_rider_amd.split import wave_ranges, wave_slice
+
+    w0, w1 = wave_ranges(cfg.nwaves, world)[rank]
+    sub = wave_slice(d, w0, w1)
+    with Engine(cfg.n, cfg.faulty, sub.nrounds, local) as e:
+        e.append_packed(sub)
+        cm, vc = e.wave_commit(1, w1 - w0 + 1)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        kms = []
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            cm, vc = e.wave_commit(1, w1 - w0 + 1)
+            kms.append(e.last_kernel_ms())
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
+    km = float(np.median(kms))
+    nb = commit_bytes(cfg.n, (cfg.n + 63) // 64, int((vc >= 0).sum()))
+    return dict(rank=rank, w0=w0, w1=w1, commit=cm.tolist(), vcount=vc.tolist(), ms=dt * 1e3, kernel_ms=km,
+                bytes=nb, GBps_kernel=nb / (km / 1e3) / 1e9 if km > 0 else None)
+
+
+def run_rank_share(args, local: int):
+    """--rank-share N on one GPU: every rank's share of the wave-range commit split of
+    the C4 DAG, decided one after another on this GPU (what each of N GPUs does on its
+    own), checked against the full DAG's decisions; the line reports the slowest share."""
+    import numpy as np
+
+    from dag_rider_amd.engine import Engine
+    from dag_rider_amd.gen import CONFIGS, generate
+
+    cfg = CONFIGS["c4"]
+    d = generate(cfg, nthreads=CPU_THREADS)
+    N = args.rank_share
+    shares = [rank_share(cfg, d, r, N, local, max(args.steps, 1)) for r in range(N)]
+    with Engine(cfg.n, cfg.faulty, d.nrounds, local) as e:
+        e.append_packed(d)
+        fc, fv = e.wave_commit(1, cfg.nwaves)
+        e.wave_commit(1, cfg.nwaves)
+        full_kms = e.last_kernel_ms()
+    cm = np.concatenate([np.asarray(s["commit"], np.uint8) for s in shares])
+    vc = np.concatenate([np.asarray(s["vcount"], np.int32) for s in shares])
+    ok = bool((cm == fc).all() and (vc == fv).all())
+    slow = max(shares, key=lambda s: s["ms"])
+    # commit edges of the slowest share: strong degrees of rounds 4w-2..4w of its waves
+    deg = np.asarray([int(np.unpackbits(d.strong[r * cfg.n * d.W:(r + 1) * cfg.n * d.W].view(np.uint8)).sum())
+                      for r in range(4 * (slow["w0"] - 1), 4 * slow["w1"] + 1)], np.int64)
+    base = 4 * (slow["w0"] - 1)
+    edges = sum(int(deg[4 * w - 2 - base] + deg[4 * w - 1 - base] + deg[4 * w - base])
+                for w in range(slow["w0"], slow["w1"] + 1) if vc[w - 1] >= 0)
+    km = slow["kernel_ms"]
+    return {
+        "metric": "DAG edges traversed/sec (commit sweep, one rank's wave range)",
+        "value": edges / (slow["ms"] / 1e3),
+        "unit": "edges/s",
+        "n_gpus": 1,
+        "steps": max(args.steps, 1),
+        "warmup": 1,
+        "ms_per_step": slow["ms"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded generator, SURVEY.md s8(d) C4 parameters)",
+        "config": {"workload": f"C4 all-waves commit sweep split into {N} wave ranges (SURVEY.md s8(e) row 1): "
+                               f"each share on its own mirror of its rounds, dr_wave_commit; line = slowest share",
+                   "n": cfg.n, "rounds": cfg.last_round, "waves": cfg.nwaves, "parallelism": f"waves{N}"},
+        "roofline": {"bound": "hbm", "achieved": slow["bytes"] / (km / 1e3) / 1e9 if km > 0 else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": slow["bytes"] / (km / 1e3) / 1e9 / HBM_PEAK_GBS if km > 0 else None,
+                     "traffic": None, "kernel": "k_commit (waveReady commit rule)",
+                     "bytes_per_launch": slow["bytes"], "ms_per_launch": km},
+        "cpu_baseline": None,
+        "detail": {"shares": [{k: s[k] for k in ("rank", "w0", "w1", "ms", "kernel_ms", "bytes", "GBps_kernel")}
+                              for s in shares],
+                   "full_dag_kernel_ms": full_kms, "verify_vs_full_dag": ok, "commit_edges_slowest": edges},
+    }
 
 
 def colshard_child(args):
@@ -468,7 +602,7 @@ def cpu_c5(dags, deliver_mode, gpu_res, lit_dags: int = 16, lit_waves: int = 4):
 
     import oracle
 
-    nt = min(CPU_THREADS, cpu_info()["affinity"] or 1)
+    nt = cpu_threads()
     f = (dags[0].n - 1) // 3
     nw = (dags[0].nrounds - 1) // 4
 
@@ -625,12 +759,14 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c4-deep", "c5", "c4-loop"])
+    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c4-deep", "c4-deep64", "c5", "c4-loop"])
     ap.add_argument("--deliver", default="ref", choices=["ref", "paper"])
     ap.add_argument("--cpu-budget", type=float, default=40.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phase-timing", type=int, default=1, help=argparse.SUPPRESS)  # 0: no events (experiment)
     ap.add_argument("--loop-waves", type=int, default=0, help="c4-loop: waves to run (0 = all)")
+    ap.add_argument("--rank-share", type=int, default=0,
+                    help="one GPU: time every rank's share of the C4 wave-range commit split for N ranks")
     ap.add_argument("--verify", action="store_true", help="check the replay against the bitset oracle")
     ap.add_argument("--colshard", action="store_true",
                     help="also run the process-column sharded C4 sweep (default on when N>1)")
@@ -677,6 +813,12 @@ def main() -> int:
             print(json.dumps(out), flush=True)
         if dist:
             dist.destroy_process_group()
+        return 0
+    if args.rank_share:
+        if world > 1 or args.config != "c4":
+            log("[bench] --rank-share is a single-GPU line of the C4 commit split")
+            return 2
+        print(json.dumps(run_rank_share(args, local)), flush=True)
         return 0
     if args.config == "c4-loop":
         if world > 1:
@@ -728,17 +870,14 @@ def main() -> int:
     if rank == 0 and world == 1 and not args.no_cpu:
         runs = 5 if cfg.n * cfg.last_round <= 1024 * 4000 else 3
         cpu2, want = cpu_bitset(cfg, d, CPU_THREADS, runs, args.deliver_mode)
-        verify = bool((want.commit == res.commit).all() and (want.pop_digest == res.pop_digest).all()
-                      and (want.pop_count == res.pop_count).all() and want.deliver_edges == res.deliver_edges
-                      and want.chain_edges == res.chain_edges and want.commit_edges == res.commit_edges)
+        verify = same_replay(res, want)
         cpu = cpu_literal(cfg, d, args.cpu_budget, res.total_edges, args.deliver_mode)
     elif args.verify and rank == 0:
         import oracle
 
         want = oracle.PDag(d).replay(cfg.faulty, cfg.nwaves, oracle.CHAIN_PERSISTENT, args.deliver_mode,
                                      nthreads=CPU_THREADS)
-        verify = bool((want.commit == res.commit).all() and (want.pop_digest == res.pop_digest).all()
-                      and (want.pop_count == res.pop_count).all() and want.deliver_edges == res.deliver_edges)
+        verify = same_replay(res, want)
 
     split = colshard = None
     if world > 1 and args.config == "c4":

@@ -69,7 +69,7 @@ SIGNATURES = {
                                     C.POINTER(C.c_size_t), P, P]),
     "dr_replay": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
     "dr_replay_batch": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
-    "dr_profile_kernel": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(f32)]),
+    "dr_last_kernel_ms": (C.c_int, [P, C.POINTER(f32)]),
     # include/dagrider_shard.h
     "dr_shard_unique_id": (C.c_int, [P]),
     "dr_shard_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.POINTER(P)]),
@@ -103,6 +103,11 @@ SIGNATURES = {
     "dr_gen_weak_tgt": (P, [P]),
 }
 
+# include/dagrider_tuning.h: exported by the profiling build only (DR_LIB_VARIANT=timing)
+TUNING_SIGNATURES = {
+    "dr_profile_kernel": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(f32)]),
+}
+
 _lib = None
 
 
@@ -113,7 +118,10 @@ def lib() -> C.CDLL:
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
                                "there is no CPU fallback")
         L = C.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
+        sigs = dict(SIGNATURES)
+        if LIB_PATH.endswith("_timing.so"):
+            sigs.update(TUNING_SIGNATURES)
+        for name, (res, args) in sigs.items():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

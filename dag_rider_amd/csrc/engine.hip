@@ -109,6 +109,7 @@ struct dr_ctx {
   // host mirror: per-round data, presence [rounds][WS], and the prefix offsets
   // of the flattened device arrays (valid for rounds < up_lo)
   std::vector<HostRound> hr;
+  dr_host::BuildScratch build_scr;  // dr_append_rounds_packed's per-thread column tables
   std::vector<u64> h_present;
   std::vector<uint32_t> h_slot_off{0}, h_wc_roff{0}, h_far_roff{0}, h_weak_roff{0};
   std::vector<u64> h_ppref;
@@ -137,7 +138,8 @@ struct dr_ctx {
   int phase_timing = 2;
   bool timed(int i) const { return phase_timing >= 2 || (phase_timing == 1 && (i == 6 || i == 7)); }
   hipError_t rec(int i) { return timed(i) ? hipEventRecord(ev[i], stream) : hipSuccess; }
-  int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies  // hC/hG/hE mirror Cc/Gc/Ec (fetched lazily after a planned replay)
+  int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies
+  float last_commit_ms = 0;  // dr_last_kernel_ms: the last commit-rule launch (HIP events)
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
   DevBuf plan_out;          // its outputs, packed for one copy back
   std::vector<char> plan_host;
@@ -883,7 +885,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   in.weak_off = weak_off;
   in.weak_tgt = weak_tgt;
   dr_host::BuiltRounds built;
-  if (int rc = dr_host::build_packed_rounds(in, c->dmax_near, built, c->err)) return rc;
+  if (int rc = dr_host::build_packed_rounds(in, c->dmax_near, built, c->err, c->build_scr)) return rc;
   std::vector<HostRound> &nh = built.rounds;
   const size_t nfar = built.nfar;
   const int dmax = built.dmax;
@@ -1510,6 +1512,7 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
   return c->fail(DR_E_INVAL, "unknown option %d", option);
 }
 
+#ifdef DR_TUNING  // tuning build only (libdagrider_gpu_timing.so, include/dagrider_tuning.h)
 namespace {
 // dr_profile_kernel variants of k_summary_commit (WS = 16 geometries; other
 // strides run the shipped one)
@@ -1603,6 +1606,14 @@ extern "C" int dr_profile_kernel(dr_ctx *c, int kernel, int variant, int iters, 
   float ms = 0;
   HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
   *avg_ms = ms / iters;
+  return DR_OK;
+}
+
+#endif  // DR_TUNING
+
+extern "C" int dr_last_kernel_ms(const dr_ctx *c, float *ms) {
+  if (!c || !ms) return DR_E_INVAL;
+  *ms = c->last_commit_ms;
   return DR_OK;
 }
 
@@ -1711,7 +1722,8 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nw));
   HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nw * 4));
   HIPCHK(c, c->sync());
-  if (ms) HIPCHK(c, hipEventElapsedTime(ms, c->ev[4], c->ev[5]));
+  HIPCHK(c, hipEventElapsedTime(&c->last_commit_ms, c->ev[4], c->ev[5]));
+  if (ms) *ms = c->last_commit_ms;
   return DR_OK;
 }
 

@@ -105,6 +105,10 @@ void build_chunk(const PackedRounds &in, int i, int s_lo, int s_hi, std::vector<
       const int delta = r - tr;
       if (delta <= 1023) {
         const size_t at = (size_t)delta * n + ts;
+        if (at >= tab.size()) {  // grow to this delta (+ slack); new entries -1 like the rest
+          tab.resize(std::min<size_t>(1024, (size_t)delta + 9) * n, -1);
+          tb = tab.data();
+        }
         int32_t col = tb[at];
         if (col < 0) {
           col = tb[at] = (int32_t)ck.key.size();
@@ -152,7 +156,7 @@ void merge_round(const PackedRounds &in, int i, const Chunk *ck, int nch, int ch
 
 }  // namespace
 
-int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std::string &err) {
+int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std::string &err, BuildScratch &scr) {
   const int k = in.k, n = in.n;
   out.rounds.assign(k, HostRound{});
   out.pres.assign((size_t)k * in.WS, 0);
@@ -171,11 +175,13 @@ int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std
   std::vector<Chunk> ck((size_t)ntask);
   for (auto &c : ck) c.dmax = dmax0;
   const int nth = std::max(1, std::min(ntask, nthr));  // no idle team members
+  if ((int)scr.tab.size() < nth) scr.tab.resize(nth);
+  for (auto &t : scr.tab)
+    if (!t.empty() && t.size() % n) t.clear();  // sized for another n: start over
 #pragma omp parallel num_threads(nth) if (par)
   {
-    // per thread, kept across calls (all -1 between uses): (delta, t) -> column
-    static thread_local std::vector<int32_t> tab;
-    if (tab.size() < (size_t)1024 * n) tab.assign((size_t)1024 * n, -1);
+    // this thread's table, kept across calls in the context (all -1 between uses)
+    std::vector<int32_t> &tab = scr.tab[par ? omp_get_thread_num() : 0];
 #pragma omp for schedule(static)
     for (int i = 0; i < k; i++) src[i] = build_slots(in, i, out, smsg[i]);  // presence before the chunks
 #pragma omp for schedule(dynamic, 1)

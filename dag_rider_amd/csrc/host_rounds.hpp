@@ -39,9 +39,16 @@ struct BuiltRounds {
   int dmax = 1;                   // largest near weak delta seen (>= the caller's)
 };
 
+// Per-context scratch of the builder: one (delta, t) -> column table per OpenMP
+// thread, all -1 between uses, (largest delta seen + 1) * n entries each.  Owned
+// by the mirror (dr_ctx), so it lives and dies with it.
+struct BuildScratch {
+  std::vector<std::vector<int32_t>> tab;
+};
+
 // Validate and build the host state of every round (rounds in parallel).
 // Returns 0 or a DR_E_* code with `err` set to the message of the first failing
 // round, exactly as a sequential pass over the rounds would report it.
-int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std::string &err);
+int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std::string &err, BuildScratch &scr);
 
 }  // namespace dr_host

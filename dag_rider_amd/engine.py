@@ -95,9 +95,16 @@ class Engine:
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_DEVICE_PLAN, int(on)))
 
     def profile_kernel(self, kernel: int, variant: int = 0, iters: int = 20) -> float:
-        """dr_profile_kernel: average device ms of one kernel variant (tuning hook)."""
+        """dr_profile_kernel: average device ms of one kernel variant (tuning hook of the
+        profiling build: DR_LIB_VARIANT=timing, include/dagrider_tuning.h)."""
         ms = L.f32()
         self._check(self._L.dr_profile_kernel(self._h, kernel, variant, iters, C.byref(ms)))
+        return ms.value
+
+    def last_kernel_ms(self) -> float:
+        """dr_last_kernel_ms: device time of the last commit-rule launch (HIP events)."""
+        ms = L.f32()
+        self._check(self._L.dr_last_kernel_ms(self._h, C.byref(ms)))
         return ms.value
 
     @property

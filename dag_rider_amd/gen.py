@@ -42,9 +42,11 @@ CONFIGS = {
     "c2": GenConfig("c2", 64, 1000, 2, 0.95, 0.05, 0.5, 8, 0.05),
     "c3": GenConfig("c3", 256, 10000, 3, 1.0, 0.3, 0.25, 4, 0.0),
     "c4": GenConfig("c4", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0),
-    # C4 with weak edges up to 24 rounds deep (past the memo window of 17): every
-    # pop sweeps its whole cone (bench.py --config c4-deep)
-    "c4-deep": GenConfig("c4-deep", 1024, 4000, 4, 1.0, 0.02, 0.1, 24, 0.0),
+    # C4 with weak edges up to 80 rounds deep, past the memo window (weak deltas <= 65,
+    # engine.hip memo_ok): every pop sweeps its whole cone (bench.py --config c4-deep)
+    "c4-deep": GenConfig("c4-deep", 1024, 4000, 4, 1.0, 0.02, 0.03, 80, 0.0),
+    # C4 with weak edges up to 64 rounds deep, the memo window's far end (--config c4-deep64)
+    "c4-deep64": GenConfig("c4-deep64", 1024, 4000, 4, 1.0, 0.02, 0.04, 64, 0.0),
     # C5: one of the 4096 independent n=128 replays (seed 5000+i)
     "c5": GenConfig("c5", 128, 128, 5000, 0.9, 0.1, 0.5, 4, 0.05),
 }

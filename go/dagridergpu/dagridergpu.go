@@ -51,7 +51,10 @@ const (
 )
 
 // Mirror is one device copy of a Process's DAG (one dr_ctx).
-type Mirror struct{ ctx *C.dr_ctx }
+type Mirror struct {
+	ctx *C.dr_ctx
+	ids []int32 // OrderVertices' id buffer, reused and grown across calls
+}
 
 // Error is a non-panicking library failure.
 type Error struct {
@@ -231,23 +234,25 @@ func (m *Mirror) WaveReady(wave, decidedWave int) (commit bool, vcount int, push
 // caller forwards each to p.tp.Broadcast as :433-441 does).
 func (m *Mirror) OrderVertices(stack []wire.ID, pRound, mode int) ([]wire.ID, error) {
 	st := idPairs(stack)
+	if len(m.ids) == 0 {
+		m.ids = make([]int32, 2*4096)
+	}
 	var n C.size_t
-	// a first call without an output buffer reports the count (DR_E_CAPACITY)
-	rc := C.dr_order_vertices(m.ctx, i32p(st), C.int(len(stack)), C.int(pRound), C.int(mode), nil, 0, &n, nil, nil)
-	if rc != C.DR_OK && rc != C.DR_E_CAPACITY {
-		return nil, m.must(rc)
+	// one call into the reused buffer; only an undersized buffer (DR_E_CAPACITY,
+	// n = the total) costs a second, exactly sized call
+	rc := C.dr_order_vertices(m.ctx, i32p(st), C.int(len(stack)), C.int(pRound), C.int(mode), i32p(m.ids),
+		C.size_t(len(m.ids)/2), &n, nil, nil)
+	if rc == C.DR_E_CAPACITY {
+		m.ids = make([]int32, 2*int(n))
+		rc = C.dr_order_vertices(m.ctx, i32p(st), C.int(len(stack)), C.int(pRound), C.int(mode), i32p(m.ids),
+			n, &n, nil, nil)
 	}
-	if n == 0 {
-		return nil, nil
-	}
-	ids := make([]int32, 2*int(n))
-	if err := m.must(C.dr_order_vertices(m.ctx, i32p(st), C.int(len(stack)), C.int(pRound), C.int(mode), i32p(ids),
-		n, &n, nil, nil)); err != nil {
+	if err := m.must(rc); err != nil {
 		return nil, err
 	}
 	out := make([]wire.ID, n)
 	for i := range out {
-		out[i] = wire.ID{Round: int(ids[2*i]), Source: int(ids[2*i+1])}
+		out[i] = wire.ID{Round: int(m.ids[2*i]), Source: int(m.ids[2*i+1])}
 	}
 	return out, nil
 }

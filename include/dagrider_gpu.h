@@ -252,12 +252,10 @@ int dr_replay(dr_ctx *ctx, int nwaves, int chain_mode, int deliver_mode, dr_repl
 int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
                     dr_replay_out *outs);
 
-/* Tuning hook (not part of the reference's surface): average device time of
- * `iters` launches of one kernel variant on the resident DAG.  kernel 0 =
- * round-summary + commit pass (variant 0 shipped, 1 rows only, 2 weak edges
- * only, 3 weak unroll 8), 1 = streaming read of the strong rows (variant 0) or
- * rows + weak edges (variant 1), 2 = the replay's whole summary phase. */
-int dr_profile_kernel(dr_ctx *ctx, int kernel, int variant, int iters, float *avg_ms);
+/* Device time (ms, HIP events) of the commit-rule kernel of the last
+ * dr_wave_commit / dr_wave_ready / dr_replay on this context (observability,
+ * like dr_shard_stats; no reference counterpart). */
+int dr_last_kernel_ms(const dr_ctx *ctx, float *ms);
 
 #ifdef __cplusplus
 }

@@ -29,6 +29,18 @@ def test_every_declared_symbol_exported():
     exported = set(re.findall(r" T (dr_\w+)", out))
     assert syms <= exported, syms - exported
     assert set(_lib.SIGNATURES) == syms  # the Python binding binds exactly the header
+    assert "dr_profile_kernel" not in exported  # tuning hook: profiling build only
+
+
+def test_tuning_hook_only_in_profiling_build():
+    timing = os.path.join(ROOT, "dag_rider_amd", "libdagrider_gpu_timing.so")
+    if not os.path.exists(timing):
+        pytest.skip("profiling build not made")
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "dagrider_tuning.h")).read(), flags=re.S)
+    tsyms = set(re.findall(r"\b(dr_[a-z_]+)\s*\(", txt))
+    assert tsyms == set(_lib.TUNING_SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", timing], capture_output=True, text=True, check=True).stdout
+    assert tsyms <= set(re.findall(r" T (dr_\w+)", out))
 
 
 def test_library_loads_and_binds():

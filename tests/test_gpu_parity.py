@@ -177,6 +177,43 @@ def test_memo_on_off_large_n(gpu_device):
                 _compare_replay(e.replay(R // 4, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), want, ids=False)
 
 
+@pytest.mark.parametrize("n", [1024, 1100])
+@pytest.mark.parametrize("depth", [64, 65, 66])
+def test_memo_window_boundary(gpu_device, n, depth):
+    """Weak deltas at the memo window's edge (DR_OPT_MEMO applies up to 65: WU holds 64
+    slots per round; 66 takes the full-sweep path) at row strides 16 (n=1024) and 32
+    (n=1100): every mode, memo and device plan on and off, == the bitset oracle."""
+    from dag_rider_amd.gen import small_config
+
+    cfg = small_config(n, depth + 24, 40 + depth, p_present=0.97, p_late=0.02, p_w=0.05, weak_depth=depth,
+                       p_la=0.1)
+    d = generate(cfg)
+    g = np.repeat(np.arange(d.nrounds * n, dtype=np.int64), np.diff(d.weak_off.astype(np.int64)))
+    assert int((g // n - (d.weak_tgt.astype(np.int64) >> 11)).max()) == depth
+    f, nw = cfg.faulty, cfg.nwaves
+    bs = oracle.PDag(d)
+    with Engine(n, f, d.nrounds, gpu_device) as e:
+        e.append_packed(d)
+        for memo in (True, False):
+            e.set_memo(memo)
+            for plan in ((True, False) if memo else (True,)):
+                e.set_device_plan(plan)
+                for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+                    for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+                        want = bs.replay(f, nw, cm, dm)
+                        assert want.rc == 0
+                        got = e.replay(nw, cm, dm)
+                        _compare_replay(got, want, ids=False)
+                        assert got.chain_edges == want.chain_edges
+        e.set_memo(True)
+        e.set_device_plan(True)
+        stack = [(4 * w - 3, 1) for w in range(1, nw + 1)]
+        for mode in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+            _, cnt_, dg_ = e.order_vertices(stack, d.nrounds - 1, mode, cap=0)
+            rc, _, wc, wd = bs.order_vertices(stack, d.nrounds - 1, mode, cap=1)
+            assert rc == 0 and cnt_.tolist() == wc.tolist() and dg_.tolist() == wd.tolist()
+
+
 def test_list_and_packed_append_agree(gpu_device):
     rng = np.random.default_rng(7)
     d = random_dag(rng, 9, 20, ghosts=0.3)

@@ -8,6 +8,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("DR_LIB_VARIANT", "timing")  # dr_profile_kernel lives in the profiling build only
 from dag_rider_amd.engine import Engine  # noqa: E402
 from dag_rider_amd.gen import CONFIGS, generate  # noqa: E402
 
