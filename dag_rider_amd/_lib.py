@@ -25,6 +25,7 @@ DR_OPT_PHASE_TIMING = 3
 DR_LEADER_CONST1, DR_LEADER_SEEDED, DR_LEADER_TABLE = 0, 1, 2
 DR_SHARD_ID_BYTES = 128
 DR_SHARD_OPT_PERSISTENT = 1
+DR_SHARD_OPT_MEMO = 2
 
 P = C.c_void_p
 i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float

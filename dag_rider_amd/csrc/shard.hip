@@ -64,6 +64,7 @@
 
 #include "dagrider_gpu.h"
 #include "dagrider_shard.h"
+#include "shard_memo.hpp"
 #include "wave_ops.hpp"
 
 namespace {
@@ -121,7 +122,7 @@ struct QInfo {
 };
 
 struct ShardArgs {
-  const u64 *strong;        // [nlocal][max_rounds][n][WSs]
+  const u64 *strong;        // [nlocal][max_rounds][n][SP] (words >= WSs zero)
   const uint32_t *weak;     // per local shard: edges (target col 0-10, source 11-21, delta 22-31)
   const uint64_t *woff;     // [nlocal][max_rounds+1] edge offsets (absolute in weak)
   const u64 *pres;          // [max_rounds][W] presence (chain restarts)
@@ -138,7 +139,7 @@ struct ShardArgs {
   int32_t *push_out;        // chain pushes (waves), query b's list at q[b].push_base
   int32_t *push_n;          // [64] pushes per chain query
   u64 *cedges;              // [64] chain edges per query
-  int32_t n, W, WSs, C, depth, shard0, nlocal, local, max_rounds, nq, strong_only, nlead;
+  int32_t n, W, WSs, SP, C, depth, shard0, nlocal, local, max_rounds, nq, strong_only, nlead;
   int64_t strong_shard_stride;  // words per local shard of strong
 };
 
@@ -238,7 +239,7 @@ __device__ void sweep_round(const ShardArgs &a, const Ft &ft, int r, int l, int 
     const u64 me = mv & m.exp;
     if (r < 1 || __ballot(me != 0ULL) == 0ULL) continue;
     const u64 row = (me != 0ULL)
-                        ? a.strong[(size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.WSs + tw]
+                        ? a.strong[(size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.SP + tw]
                         : 0ULL;
     u64 act = __ballot(row != 0ULL);
     u64 acc = 0;
@@ -427,7 +428,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_vote(ShardArgs a, int w0, int n
   const int s = sb * SH_NT + (int)threadIdx.x;
   bool hit = false;
   if (s < a.n) {
-    const u64 *row = a.strong + (size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.WSs;
+    const u64 *row = a.strong + (size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.SP;
     for (int j = 0; j < a.WSs; j++) hit |= (row[j] & S[j]) != 0ULL;
   }
   const u64 b = __ballot(hit);
@@ -560,9 +561,10 @@ __global__ void __launch_bounds__(SH_NT) k_shard_digest(const u64 *out, const QI
 }  // namespace
 
 struct dr_shard {
-  int n = 0, f = 0, W = 0, G = 1, shard0 = 0, nlocal = 1, WSs = 1, C = 64, max_rounds = 0, dev = 0;
+  int n = 0, f = 0, W = 0, G = 1, shard0 = 0, nlocal = 1, WSs = 1, SP = 1, C = 64, max_rounds = 0, dev = 0;
   bool local = true;
   int persistent = 1;  // DR_SHARD_OPT_PERSISTENT
+  int memo = 1;        // DR_SHARD_OPT_MEMO
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
   hipStream_t stream = nullptr;
@@ -573,8 +575,21 @@ struct dr_shard {
   SBuf pres, sdeg, wdeg, rdeg, slot_off, slot_src, lead;
   // per-call scratch
   SBuf bar, errf, push_out, push_n, cedges, vote_s0, vote_p[2], vote_send, vcount, D, pcnt, qcnt, qedges, qdig;
+  // memoized replay (shard_memo.hpp): strong degree per round, round summaries,
+  // canonical cone and prefixes, the stepped queries' buffers
+  SBuf sdr, mU, mWU, mK, mgood, mRD, mCE, mRG, mC, mE, mG, mksend, mkrecv, mq, mst, mpend, mrecv[2], msend, mmasks,
+      mpush, mqidx, mqout;
+  std::vector<uint64_t> h_sdr;  // strong degree sum per round (host copy)
+  int *alive = nullptr;         // pinned: live queries after the last polled step
   std::vector<std::vector<uint32_t>> h_weak;  // per local shard
   std::vector<std::vector<uint64_t>> h_woff;  // per local shard, absolute offsets, size nrounds+1
+  // weak columns per local shard (the memoized replay, shard_memo.hpp): one entry per
+  // distinct weak target (delta, column) of a round whose column is this shard's, key
+  // delta << 11 | local column, and the W-word bitset of the round's sources with it
+  std::vector<std::vector<uint32_t>> h_wck;
+  std::vector<std::vector<u64>> h_wcr;
+  std::vector<std::vector<uint64_t>> h_wcro;  // per local shard, absolute offsets, size nrounds+1
+  SBuf wck, wcr, wcro;
   std::vector<u64> h_pres;                    // [nrounds][W]
   std::vector<uint64_t> h_deg;                // strong degree sum per round
   std::vector<uint32_t> h_slot_off{0};
@@ -638,6 +653,27 @@ int sync_weak(dr_shard *c) {
     base += w.size();
   }
   SHCHK(c, hipMemcpyAsync(c->woff.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, c->stream));
+  // weak columns, concatenated over the local shards; wcro absolute like woff
+  size_t ncol = 0;
+  for (auto &v : c->h_wck) ncol += v.size();
+  SHCHK(c, c->wck.ensure(std::max<size_t>(ncol, 1) * 4));
+  SHCHK(c, c->wcr.ensure(std::max<size_t>(ncol, 1) * c->W * 8));
+  SHCHK(c, c->wcro.ensure((size_t)c->nlocal * (c->max_rounds + 1) * 8));
+  std::vector<uint64_t> coffs((size_t)c->nlocal * (c->max_rounds + 1), 0);
+  size_t cb = 0;
+  for (int l = 0; l < c->nlocal; l++) {
+    const auto &k = c->h_wck[l];
+    if (!k.empty()) {
+      SHCHK(c, hipMemcpyAsync(c->wck.as<uint32_t>() + cb, k.data(), k.size() * 4, hipMemcpyHostToDevice, c->stream));
+      SHCHK(c, hipMemcpyAsync(c->wcr.as<u64>() + cb * c->W, c->h_wcr[l].data(), k.size() * c->W * 8,
+                              hipMemcpyHostToDevice, c->stream));
+    }
+    uint64_t *o = &coffs[(size_t)l * (c->max_rounds + 1)];
+    for (int r = 0; r <= c->max_rounds; r++)
+      o[r] = cb + c->h_wcro[l][std::min<size_t>(r, c->h_wcro[l].size() - 1)];
+    cb += k.size();
+  }
+  SHCHK(c, hipMemcpyAsync(c->wcro.p, coffs.data(), coffs.size() * 8, hipMemcpyHostToDevice, c->stream));
   SHCHK(c, hipStreamSynchronize(c->stream));
   c->weak_dirty = false;
   return DR_OK;
@@ -666,6 +702,7 @@ ShardArgs make_args(dr_shard *c, int nq, int strong_only) {
   a.n = c->n;
   a.W = c->W;
   a.WSs = c->WSs;
+  a.SP = c->SP;
   a.C = c->C;
   a.depth = c->depth;
   a.shard0 = c->shard0;
@@ -675,7 +712,7 @@ ShardArgs make_args(dr_shard *c, int nq, int strong_only) {
   a.nq = nq;
   a.strong_only = strong_only;
   a.nlead = (int32_t)c->h_lead.size();
-  a.strong_shard_stride = (int64_t)c->max_rounds * c->n * c->WSs;
+  a.strong_shard_stride = (int64_t)c->max_rounds * c->n * c->SP;
   return a;
 }
 
@@ -990,6 +1027,413 @@ int deliver(dr_shard *c, const std::vector<Pop> &pops, int mode, uint64_t *pcoun
   return check_barrier(c);
 }
 
+
+// ---------------------------------------------------------------------------
+// Memoized replay (shard_memo.hpp).  Every shard holds the full canonical cone
+// and every query's full frontier after each exchange, so each one takes the
+// same decisions; only the row work is split by column.
+// ---------------------------------------------------------------------------
+drs::MArgs make_margs(dr_shard *c, int nq) {
+  drs::MArgs a{};
+  a.strong = c->strong.as<u64>();
+  a.strong_stride = (int64_t)c->max_rounds * c->n * c->SP;
+  a.wck = c->wck.as<uint32_t>();
+  a.wcr = c->wcr.as<u64>();
+  a.wcro = c->wcro.as<uint64_t>();
+  a.pres = c->pres.as<u64>();
+  a.sdeg = c->sdeg.as<uint16_t>();
+  a.wdeg = c->wdeg.as<uint16_t>();
+  a.sdr = c->sdr.as<u64>();
+  a.rdeg = c->rdeg.as<u64>();
+  a.lead = c->lead.as<uint16_t>();
+  a.U = c->mU.as<u64>();
+  a.WU = c->mWU.as<u64>();
+  a.K = c->mK.as<u64>();
+  a.q = c->mq.as<drs::MQuery>();
+  a.st0 = c->mst.as<drs::MState>();
+  a.st1 = c->mst.as<drs::MState>() + std::max(nq, 1);
+  a.pend = c->mpend.as<u64>();
+  a.recv0 = c->mrecv[0].as<u64>();
+  a.recv1 = c->mrecv[1].as<u64>();
+  a.send = c->msend.as<u64>();
+  a.masks = c->mmasks.as<u64>();
+  a.push_out = c->mpush.as<int32_t>();
+  a.n = c->n;
+  a.W = c->W;
+  a.WSs = c->WSs;
+  a.SP = c->SP;
+  a.G = c->G;
+  a.shard0 = c->shard0;
+  a.nlocal = c->nlocal;
+  a.local = c->local ? 1 : 0;
+  a.nq = nq;
+  a.depth = c->depth;
+  a.dd = std::max(0, c->dmax - 1);
+  a.dmax = std::max(1, c->dmax);
+  a.summary = 1;
+  a.R = c->max_rounds;
+  a.nlead = (int32_t)c->h_lead.size();
+  return a;
+}
+
+bool memo_applies(const dr_shard *c) { return c->memo && c->dmax <= 65; }
+
+// Step a batch of queries (states in st0, rings clear) until none is live.
+// Returns the number of steps taken (the final states are in st[steps & 1]).
+int run_steps(dr_shard *c, const drs::MArgs &a, int nq, int maxsteps, int *steps) {
+  const dim3 grid(nq, c->nlocal), block(drs::MS_NT);
+  for (int j = 0;; j++) {
+    hipLaunchKernelGGL(drs::k_ms_step, grid, block, 0, c->stream, a, j);
+    SHCHK(c, hipGetLastError());
+    if (!c->local) {
+      SHNCCL(c, ncclAllGather(c->msend.p, c->mrecv[(j + 1) & 1].p, (size_t)nq * c->WSs, ncclUint64, c->comm,
+                              c->stream));
+      c->last_xbytes += (uint64_t)nq * c->WSs * 8;
+    }
+    c->last_rounds++;
+    const int done_steps = j + 1;
+    // poll every 4 steps (each poll is one host round trip)
+    if (done_steps % 4 == 0 || done_steps >= maxsteps) {
+      const drs::MState *st = (done_steps & 1) ? a.st1 : a.st0;
+      hipLaunchKernelGGL(drs::k_ms_alive, dim3(1), block, 0, c->stream, st, nq, c->alive);
+      SHCHK(c, hipGetLastError());
+      SHCHK(c, hipStreamSynchronize(c->stream));
+      if (*c->alive == 0) {
+        *steps = done_steps;
+        return DR_OK;
+      }
+      if (done_steps >= maxsteps)
+        return c->fail(DR_E_HIP, "memo replay: %d queries still live after %d steps", *c->alive, maxsteps);
+    }
+  }
+}
+
+int init_states(dr_shard *c, const std::vector<drs::MQuery> &qs) {
+  const int nq = (int)qs.size();
+  SHCHK(c, c->mq.ensure((size_t)nq * sizeof(drs::MQuery)));
+  SHCHK(c, c->mst.ensure((size_t)2 * nq * sizeof(drs::MState)));
+  std::vector<drs::MState> st(nq);
+  for (int i = 0; i < nq; i++) {
+    st[i] = drs::MState{};
+    st[i].low = qs[i].top;
+  }
+  SHCHK(c, hipMemcpyAsync(c->mq.p, qs.data(), nq * sizeof(drs::MQuery), hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, hipMemcpyAsync(c->mst.p, st.data(), nq * sizeof(drs::MState), hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, c->mpend.ensure((size_t)c->nlocal * nq * c->depth * c->SP * 8));
+  SHCHK(c, c->mrecv[0].ensure((size_t)c->G * nq * c->WSs * 8));
+  SHCHK(c, c->mrecv[1].ensure((size_t)c->G * nq * c->WSs * 8));
+  SHCHK(c, c->msend.ensure((size_t)nq * c->WSs * 8));
+  return DR_OK;
+}
+
+// Round summaries, K^cand, good, the canonical segments and the canonical
+// prefixes C, E, G of the DAG's top round T.
+int build_canon(dr_shard *c, int T, int *nseg) {
+  const int W = c->W, SP = c->SP, nl = c->nlocal, dd = std::max(0, c->dmax - 1);
+  const size_t R = (size_t)c->max_rounds;
+  SHCHK(c, c->mU.ensure((size_t)nl * R * SP * 8));
+  SHCHK(c, c->mWU.ensure(std::max<size_t>((size_t)nl * R * dd * SP, 1) * 8));
+  SHCHK(c, c->mK.ensure((size_t)(T + 1) * W * 8));
+  SHCHK(c, c->mgood.ensure((size_t)T + 8));
+  for (SBuf *b : {&c->mRD, &c->mCE, &c->mRG, &c->mC, &c->mE, &c->mG}) SHCHK(c, b->ensure((size_t)(T + 1) * 8));
+  drs::MArgs a = make_margs(c, 1);
+  if (T >= 1) {
+    hipLaunchKernelGGL(drs::k_ms_summary, dim3(T, nl), dim3(drs::MS_NT), 0, c->stream, a, T, c->mU.as<u64>(),
+                       c->mWU.as<u64>());
+    SHCHK(c, hipGetLastError());
+  }
+  const int rb = (T + 1 + 3) / 4;
+  if (c->local) {
+    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, nl), dim3(drs::MS_NT), 0, c->stream, a, T, (u64 *)nullptr);
+    SHCHK(c, hipGetLastError());
+  } else {
+    SHCHK(c, c->mksend.ensure((size_t)(T + 1) * c->WSs * 8));
+    SHCHK(c, c->mkrecv.ensure((size_t)c->G * (T + 1) * c->WSs * 8));
+    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, nl), dim3(drs::MS_NT), 0, c->stream, a, T, c->mksend.as<u64>());
+    SHCHK(c, hipGetLastError());
+    SHNCCL(c, ncclAllGather(c->mksend.p, c->mkrecv.p, (size_t)(T + 1) * c->WSs, ncclUint64, c->comm, c->stream));
+    c->last_xbytes += (uint64_t)(T + 1) * c->WSs * 8;
+    const size_t tot = (size_t)(T + 1) * W;
+    hipLaunchKernelGGL(drs::k_ms_kunpack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, a, T,
+                       c->mkrecv.as<u64>());
+    SHCHK(c, hipGetLastError());
+  }
+  hipLaunchKernelGGL(drs::k_ms_good, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a, T, c->mgood.as<uint8_t>());
+  SHCHK(c, hipGetLastError());
+  std::vector<uint8_t> good(T + 1);
+  SHCHK(c, hipMemcpyAsync(good.data(), c->mgood.p, T + 1, hipMemcpyDeviceToHost, c->stream));
+  SHCHK(c, hipStreamSynchronize(c->stream));
+  // canonical segments, top down (k_canon, kernels.hpp): from each bad round until
+  // dmax consecutive full rounds restore the regime
+  int pos = T, segs = 0;
+  while (true) {
+    int b = pos - 1;
+    while (b >= 0 && good[b]) b--;
+    if (b < 0) break;
+    segs++;
+    drs::MQuery q{};
+    q.type = drs::MQ_CANON;
+    q.top = b;
+    q.bottom = 0;
+    q.src0 = -1;
+    if (int rc = init_states(c, {q})) return rc;
+    drs::MArgs sa = make_margs(c, 1);
+    hipLaunchKernelGGL(drs::k_ms_canon_init, dim3(nl), dim3(drs::MS_NT), 0, c->stream, sa, b, T);
+    SHCHK(c, hipGetLastError());
+    int steps = 0;
+    if (int rc = run_steps(c, sa, 1, b + 2, &steps)) return rc;
+    drs::MState fin;
+    SHCHK(c, hipMemcpyAsync(&fin, (steps & 1) ? sa.st1 : sa.st0, sizeof fin, hipMemcpyDeviceToHost, c->stream));
+    SHCHK(c, hipStreamSynchronize(c->stream));
+    pos = fin.stop;
+  }
+  *nseg = segs;
+  hipLaunchKernelGGL(drs::k_ms_cstats, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a, T, c->mRD.as<u64>(),
+                     c->mCE.as<u64>());
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, c->mRD.as<u64>(), c->mC.as<u64>(),
+                     c->mCE.as<u64>(), c->mE.as<u64>());
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_rg, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a, T, c->slot_off.as<uint32_t>(),
+                     c->slot_src.as<uint16_t>(), c->mC.as<u64>(), c->mRG.as<u64>());
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, c->mRG.as<u64>(), c->mG.as<u64>(),
+                     (const u64 *)nullptr, (u64 *)nullptr);
+  SHCHK(c, hipGetLastError());
+  (void)dd;
+  return DR_OK;
+}
+
+int paper_emit(dr_shard *c, const drs::MArgs &a, const std::vector<drs::MQuery> &qs,
+               const std::vector<drs::MState> &fin, const std::vector<int> &pop_query, std::vector<uint64_t> &qout,
+               int npop);
+
+// dr_shard_replay on the memo path (REF: k_ms_emit; PAPER: paper_emit).
+int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
+  const bool paper = deliver_mode == DR_DELIVER_PAPER;
+  hipEvent_t ev[5] = {};
+  for (auto &e : ev) SHCHK(c, hipEventCreate(&e));
+  struct EvGuard { hipEvent_t *e; ~EvGuard() { for (int i = 0; i < 5; i++) if (e[i]) (void)hipEventDestroy(e[i]); } } eg{ev};
+  const int T = c->nrounds - 1, W = c->W;
+  if (int rc = prepare_queries(c, 0)) return rc;  // uploads the weak edges and columns
+  SHCHK(c, hipEventRecord(ev[0], c->stream));
+  // 1. commit decisions of every wave (three exchanges)
+  if (int rc = votes(c, 1, nwaves, o->commit, o->vcount)) return rc;
+  SHCHK(c, hipEventRecord(ev[1], c->stream));
+  uint64_t ce = 0;
+  for (int w = 1; w <= nwaves; w++)
+    if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
+  o->commit_edges = ce;
+  // 2. summaries and the canonical cone
+  int nseg = 0;
+  if (int rc = build_canon(c, T, &nseg)) return rc;
+  o->canon_segments = nseg;
+  SHCHK(c, hipEventRecord(ev[2], c->stream));
+  // 3. one batch: a cone for every wave whose leader is present (a superset of the
+  // leaders any chain can push) and the chain of every commit that needs one
+  std::vector<ChainTask> tasks;
+  int lastw = 0;
+  for (int w = 1; w <= nwaves; w++)
+    if (o->commit[w - 1]) {
+      tasks.push_back(ChainTask{w, chain_mode == DR_CHAIN_PERSISTENT ? lastw : 0});
+      lastw = w;
+    }
+  std::vector<drs::MQuery> qs;
+  std::vector<int> popq(nwaves + 1, -1);
+  int64_t moff = 0;
+  for (int w = 1; w <= nwaves; w++) {
+    const int r1 = 4 * (w - 1) + 1, L = c->lead_src(w);
+    if (!c->is_present(r1, L)) continue;
+    drs::MQuery q{};
+    q.type = drs::MQ_POP;
+    q.top = r1;
+    q.bottom = 0;
+    q.src0 = L - 1;
+    q.mask_off = moff;
+    moff += (int64_t)(r1 + 1) * W;
+    popq[w] = (int)qs.size();
+    qs.push_back(q);
+  }
+  const int npop = (int)qs.size();
+  std::vector<int> chainq(tasks.size(), -1);
+  int32_t pbase = 0;
+  int maxsteps = 2;
+  for (auto &q : qs) maxsteps = std::max(maxsteps, q.top - q.bottom + 2);
+  for (size_t i = 0; i < tasks.size(); i++) {
+    if (tasks[i].wave - 1 < tasks[i].floor + 1) continue;
+    if (tasks[i].floor < 0) return c->fail(DR_E_INVAL, "decidedWave %d < 0 (Go: waveRound(0,1) index out of range)", tasks[i].floor);
+    drs::MQuery q{};
+    q.type = drs::MQ_CHAIN;
+    q.top = 4 * (tasks[i].wave - 1) + 1;
+    q.bottom = 4 * tasks[i].floor + 1;
+    q.src0 = c->lead_src(tasks[i].wave) - 1;
+    q.push_base = pbase;
+    pbase += (q.top - q.bottom) / 4 + 1;
+    maxsteps = std::max(maxsteps, q.top - q.bottom + 2);
+    chainq[i] = (int)qs.size();
+    qs.push_back(q);
+  }
+  const int nq = (int)qs.size();
+  int steps = 0;
+  std::vector<drs::MState> fin(nq);
+  std::vector<int32_t> pushes_dev(std::max(pbase, 1));
+  std::vector<uint64_t> qout((size_t)3 * std::max(npop, 1));
+  if (nq > 0) {
+    if (int rc = init_states(c, qs)) return rc;
+    SHCHK(c, c->mmasks.ensure((size_t)std::max<int64_t>(moff, 1) * 8));
+    SHCHK(c, c->mpush.ensure((size_t)std::max(pbase, 1) * 4));
+    SHCHK(c, hipMemsetAsync(c->mpend.p, 0, (size_t)c->nlocal * nq * c->depth * c->SP * 8, c->stream));
+    drs::MArgs a = make_margs(c, nq);
+    if (int rc = run_steps(c, a, nq, maxsteps, &steps)) return rc;
+    SHCHK(c, hipEventRecord(ev[3], c->stream));
+    // 4. emission of every pop query (REF; PAPER needs the pop order, below)
+    if (npop > 0 && !paper) {
+      std::vector<int32_t> qidx(npop);
+      for (int i = 0; i < npop; i++) qidx[i] = i;
+      SHCHK(c, c->mqidx.ensure((size_t)npop * 4));
+      SHCHK(c, c->mqout.ensure((size_t)3 * npop * 8));
+      SHCHK(c, hipMemcpyAsync(c->mqidx.p, qidx.data(), (size_t)npop * 4, hipMemcpyHostToDevice, c->stream));
+      u64 *qo = c->mqout.as<u64>();
+      hipLaunchKernelGGL(drs::k_ms_emit, dim3(npop), dim3(drs::MS_NT), 0, c->stream, a, c->mqidx.as<int32_t>(),
+                         (steps & 1) ? a.st1 : a.st0, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
+                         c->mC.as<u64>(), c->mG.as<u64>(), c->mE.as<u64>(), qo, qo + npop, qo + 2 * npop);
+      SHCHK(c, hipGetLastError());
+      SHCHK(c, hipMemcpyAsync(qout.data(), qo, (size_t)3 * npop * 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    SHCHK(c, hipMemcpyAsync(fin.data(), (steps & 1) ? a.st1 : a.st0, nq * sizeof(drs::MState), hipMemcpyDeviceToHost,
+                            c->stream));
+    if (pbase) SHCHK(c, hipMemcpyAsync(pushes_dev.data(), c->mpush.p, (size_t)pbase * 4, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    SHCHK(c, hipEventRecord(ev[3], c->stream));
+  }
+  SHCHK(c, hipEventRecord(ev[4], c->stream));
+  SHCHK(c, hipEventSynchronize(ev[4]));
+  SHCHK(c, hipEventElapsedTime(&o->ms_commit, ev[0], ev[1]));
+  SHCHK(c, hipEventElapsedTime(&o->ms_summary, ev[1], ev[2]));
+  SHCHK(c, hipEventElapsedTime(&o->ms_deliver, ev[2], ev[3]));
+  SHCHK(c, hipEventElapsedTime(&o->ms_emit, ev[3], ev[4]));
+  o->ms_chain = 0;
+  // 5. assembly: pushes per commit, pops in stack order, each pop = its leader's query
+  std::vector<std::vector<int32_t>> pushes(tasks.size());
+  uint64_t chain_e = 0;
+  for (size_t i = 0; i < tasks.size(); i++) {
+    pushes[i].push_back(tasks[i].wave);
+    if (chainq[i] < 0) continue;
+    const drs::MState &f = fin[chainq[i]];
+    const drs::MQuery &q = qs[chainq[i]];
+    for (int x = 0; x < f.npush; x++) pushes[i].push_back(pushes_dev[q.push_base + x]);
+    chain_e += f.edges;
+  }
+  o->chain_edges = chain_e;
+  int64_t np = 0;
+  for (auto &p : pushes) np += (int64_t)p.size();
+  o->n_push = np;
+  if (np > o->push_cap || !o->push_wave || !o->pop_count || !o->pop_digest)
+    return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)np, (long long)o->push_cap);
+  int64_t at = 0;
+  size_t t = 0;
+  std::vector<int> pop_query;
+  for (int w = 1; w <= nwaves; w++) {
+    o->push_off[w - 1] = (uint32_t)at;
+    if (t < tasks.size() && tasks[t].wave == w) {
+      for (int32_t pw : pushes[t]) o->push_wave[at++] = pw;
+      for (auto it = pushes[t].rbegin(); it != pushes[t].rend(); ++it) {
+        const int q = popq[*it];
+        if (q < 0) return c->fail(DR_E_HIP, "memo replay: pushed wave %d has no cone query", *it);
+        pop_query.push_back(q);
+      }
+      t++;
+    }
+  }
+  o->push_off[nwaves] = (uint32_t)at;
+  if (paper && !pop_query.empty()) {
+    drs::MArgs a = make_margs(c, nq);
+    SHCHK(c, hipEventRecord(ev[3], c->stream));
+    if (int rc = paper_emit(c, a, qs, fin, pop_query, qout, npop)) return rc;
+    SHCHK(c, hipEventRecord(ev[4], c->stream));
+    SHCHK(c, hipEventSynchronize(ev[4]));
+    SHCHK(c, hipEventElapsedTime(&o->ms_emit, ev[3], ev[4]));
+  }
+  uint64_t de = 0;
+  std::vector<uint8_t> seen(paper ? npop : 0, 0);
+  for (size_t pi = 0; pi < pop_query.size(); pi++) {
+    const int q = pop_query[pi];
+    const bool zero = paper && seen[q];  // a repeated leader delivers nothing new (its cone is delivered)
+    if (paper) seen[q] = 1;
+    o->pop_count[pi] = zero ? 0 : qout[q];
+    o->pop_digest[pi] = zero ? 0 : qout[npop + q];
+    const uint64_t e = zero ? 0 : qout[2 * npop + q];
+    if (o->pop_edges) o->pop_edges[pi] = e;
+    de += e;
+  }
+  o->deliver_edges = de;
+  o->sweep_count = (uint64_t)npop;
+  o->sweep_partial = (uint64_t)steps;
+  return DR_OK;
+}
+
+// PAPER on the memo path: the first pop of each distinct leader delivers its cone
+// minus the cones of the pops before it (k_ms_paper).  qout: [count | digest |
+// edges] per query index.
+int paper_emit(dr_shard *c, const drs::MArgs &a, const std::vector<drs::MQuery> &qs,
+               const std::vector<drs::MState> &fin, const std::vector<int> &pop_query, std::vector<uint64_t> &qout,
+               int npop) {
+  std::vector<int> first;
+  std::vector<uint8_t> seen(npop, 0);
+  for (int q : pop_query)
+    if (!seen[q]) {
+      seen[q] = 1;
+      first.push_back(q);
+    }
+  const int m = (int)first.size();
+  std::vector<drs::MPaper> qp(m);
+  int rmax = 1;
+  for (int i = 0; i < m; i++) {
+    const drs::MQuery &Q = qs[first[i]];
+    const drs::MState &S = fin[first[i]];
+    drs::MPaper x{};
+    x.top = Q.top;
+    if (S.merged) {
+      x.cut = std::min(S.stop + a.dmax - 1, Q.top);
+      x.lo = x.cut + 1;
+    } else {
+      x.cut = 0;
+      x.lo = std::max(1, S.stop);
+    }
+    x.mask_off = Q.mask_off;
+    qp[i] = x;
+    rmax = std::max(rmax, Q.top);
+  }
+  const int rstride = rmax + 1;
+  SHCHK(c, c->mqidx.ensure((size_t)m * sizeof(drs::MPaper)));
+  SHCHK(c, c->pcnt.ensure((size_t)m * rstride * 4));
+  SHCHK(c, c->mqout.ensure((size_t)3 * m * 8));
+  u64 *qo = c->mqout.as<u64>();
+  SHCHK(c, hipMemcpyAsync(c->mqidx.p, qp.data(), (size_t)m * sizeof(drs::MPaper), hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, hipMemsetAsync(c->pcnt.p, 0, (size_t)m * rstride * 4, c->stream));
+  SHCHK(c, hipMemsetAsync(qo, 0, (size_t)3 * m * 8, c->stream));
+  const drs::MPaper *dqp = c->mqidx.as<drs::MPaper>();
+  const dim3 grid((rmax + 3) / 4), block(drs::MS_NT);
+  hipLaunchKernelGGL(drs::k_ms_paper<false>, grid, block, 0, c->stream, a, rmax, dqp, m, c->pcnt.as<uint32_t>(),
+                     rstride, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), qo + 2 * m, qo + m);
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_paper_scan, dim3(m), block, 0, c->stream, rmax, c->pcnt.as<uint32_t>(), rstride, qo);
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_paper<true>, grid, block, 0, c->stream, a, rmax, dqp, m, c->pcnt.as<uint32_t>(),
+                     rstride, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), qo + 2 * m, qo + m);
+  SHCHK(c, hipGetLastError());
+  std::vector<uint64_t> h((size_t)3 * m);
+  SHCHK(c, hipMemcpyAsync(h.data(), qo, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  SHCHK(c, hipStreamSynchronize(c->stream));
+  qout.assign((size_t)3 * std::max(npop, 1), 0);
+  for (int i = 0; i < m; i++) {
+    qout[first[i]] = h[i];
+    qout[npop + first[i]] = h[m + i];
+    qout[2 * npop + first[i]] = h[2 * m + i];
+  }
+  return DR_OK;
+}
+
 }  // namespace
 
 extern "C" int dr_shard_unique_id(uint8_t *id) {
@@ -1029,6 +1473,8 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   c->G = nshards;
   c->WSs = (c->W + nshards - 1) / nshards;
   c->C = c->WSs * 64;
+  c->SP = 1;
+  while (c->SP < c->WSs) c->SP <<= 1;  // row stride: a power of two (fixed lane -> column maps)
   c->local = id == nullptr;
   c->shard0 = c->local ? 0 : rank;
   c->nlocal = c->local ? nshards : 1;
@@ -1036,6 +1482,9 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   c->dev = device;
   c->h_weak.resize(c->nlocal);
   c->h_woff.assign(c->nlocal, std::vector<uint64_t>(1, 0));
+  c->h_wck.resize(c->nlocal);
+  c->h_wcr.resize(c->nlocal);
+  c->h_wcro.assign(c->nlocal, std::vector<uint64_t>(1, 0));
   c->h_lead.assign((size_t)max_rounds / 4 + 2, 1);
   if (sh_set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev0, hipEventReleaseToDevice) != hipSuccess ||
@@ -1046,13 +1495,14 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
     return DR_E_HIP;
   }
   const size_t NT = (size_t)c->G * c->C;
-  if (c->strong.ensure((size_t)c->nlocal * max_rounds * n * c->WSs * 8) != hipSuccess ||
+  if (c->strong.ensure((size_t)c->nlocal * max_rounds * n * c->SP * 8) != hipSuccess ||
       c->ft[0].ensure(NT * 8) != hipSuccess || c->ft[1].ensure(NT * 8) != hipSuccess ||
       c->send.ensure((size_t)c->C * 8) != hipSuccess || c->cnt.ensure(c->nlocal * 4) != hipSuccess ||
       c->pres.ensure((size_t)max_rounds * c->W * 8) != hipSuccess ||
       c->sdeg.ensure((size_t)max_rounds * n * 2) != hipSuccess ||
       c->wdeg.ensure((size_t)max_rounds * n * 2) != hipSuccess ||
-      c->rdeg.ensure((size_t)max_rounds * 8) != hipSuccess ||
+      c->rdeg.ensure((size_t)max_rounds * 8) != hipSuccess || c->sdr.ensure((size_t)max_rounds * 8) != hipSuccess ||
+      hipHostMalloc((void **)&c->alive, 64, hipHostMallocDefault) != hipSuccess ||
       c->slot_off.ensure(((size_t)max_rounds + 1) * 4) != hipSuccess ||
       c->lead.ensure(c->h_lead.size() * 2) != hipSuccess ||
       hipMemcpy(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1081,6 +1531,11 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  for (SBuf *b : {&c->wck, &c->wcr, &c->wcro, &c->sdr, &c->mU, &c->mWU, &c->mK, &c->mgood, &c->mRD, &c->mCE, &c->mRG,
+                  &c->mC, &c->mE, &c->mG, &c->mksend, &c->mkrecv, &c->mq, &c->mst, &c->mpend, &c->mrecv[0],
+                  &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout})
+    b->release();
+  if (c->alive) (void)hipHostFree(c->alive);
   for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out,
                   &c->qinfo, &c->pres, &c->sdeg, &c->wdeg, &c->rdeg, &c->slot_off, &c->slot_src, &c->lead, &c->bar,
                   &c->errf, &c->push_out, &c->push_n, &c->cedges, &c->vote_s0, &c->vote_p[0], &c->vote_p[1],
@@ -1109,6 +1564,10 @@ extern "C" int dr_shard_set_option(dr_shard *c, int option, int value) {
   if (!c) return DR_E_INVAL;
   if (option == DR_SHARD_OPT_PERSISTENT) {
     c->persistent = value ? 1 : 0;
+    return DR_OK;
+  }
+  if (option == DR_SHARD_OPT_MEMO) {
+    c->memo = value ? 1 : 0;
     return DR_OK;
   }
   return c->fail(DR_E_INVAL, "unknown option %d", option);
@@ -1145,15 +1604,18 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
   if (k < 0 || r0 + k > c->max_rounds) return c->fail(DR_E_INVAL, "append of %d rounds exceeds max_rounds %d", k, c->max_rounds);
   if (k == 0) return DR_OK;
   if (!slot_off || !slot_src || !strong || !weak_off) return c->fail(DR_E_INVAL, "null array");
-  const int n = c->n, W = c->W, WSs = c->WSs, C = c->C;
+  const int n = c->n, W = c->W, WSs = c->WSs, SP = c->SP, C = c->C;
   const u64 lastmask = (n % 64) ? ((1ULL << (n % 64)) - 1ULL) : ~0ULL;
   std::vector<u64> pres((size_t)k * W, 0);
-  std::vector<u64> rows((size_t)c->nlocal * k * n * WSs, 0);
+  std::vector<u64> rows((size_t)c->nlocal * k * n * SP, 0);
   std::vector<uint16_t> sd((size_t)k * n, 0), wd((size_t)k * n, 0);
   std::vector<u64> rd(k, 0);
   std::vector<uint64_t> deg(k, 0);
   std::vector<std::vector<uint32_t>> wnew(c->nlocal);
   std::vector<std::vector<uint64_t>> wro(c->nlocal, std::vector<uint64_t>(k + 1, 0));
+  std::vector<std::vector<uint32_t>> wck_new(c->nlocal);
+  std::vector<std::vector<u64>> wcr_new(c->nlocal);
+  std::vector<std::vector<uint64_t>> wcro_new(c->nlocal, std::vector<uint64_t>(k + 1, 0));
   int dmax = c->dmax;
   size_t maxw = c->max_weak_round;
   for (int i = 0; i < k; i++) {
@@ -1178,7 +1640,7 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
       if (row[W - 1] & ~lastmask) return c->fail(DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
       for (int l = 0; l < c->nlocal; l++) {
         const int g = c->shard0 + l;
-        u64 *dst = &rows[(((size_t)l * k + i) * n + s0) * WSs];
+        u64 *dst = &rows[(((size_t)l * k + i) * n + s0) * SP];
         for (int w = 0; w < WSs; w++) {
           const int gw = g * WSs + w;
           dst[w] = gw < W ? row[gw] : 0ULL;
@@ -1212,6 +1674,19 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
         return kx < ky;
       });
       maxw = std::max<size_t>(maxw, w.size() - wro[l][i]);
+      // the round's weak columns: runs of equal (delta, target) in the sorted edges
+      auto &ck = wck_new[l];
+      auto &cr = wcr_new[l];
+      wcro_new[l][i] = ck.size();
+      for (size_t e = wro[l][i]; e < w.size(); e++) {
+        const uint32_t key = ((w[e] >> 22) << 11) | (w[e] & 2047u);
+        if (e == wro[l][i] || key != ck.back()) {
+          ck.push_back(key);
+          cr.resize(cr.size() + W, 0ULL);
+        }
+        const uint32_t src = (w[e] >> 11) & 2047u;
+        cr[(ck.size() - 1) * W + (src >> 6)] |= 1ULL << (src & 63);
+      }
     }
   }
   // per-vertex metadata (every shard holds all of it) and the slot order
@@ -1231,14 +1706,20 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
   SHCHK(c, hipMemcpyAsync(c->wdeg.as<uint16_t>() + (size_t)r0 * n, wd.data(), wd.size() * 2, hipMemcpyHostToDevice,
                           c->stream));
   SHCHK(c, hipMemcpyAsync(c->rdeg.as<u64>() + r0, rd.data(), rd.size() * 8, hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, hipMemcpyAsync(c->sdr.as<u64>() + r0, deg.data(), deg.size() * 8, hipMemcpyHostToDevice, c->stream));
   for (int l = 0; l < c->nlocal; l++) {
     wro[l][k] = wnew[l].size();
-    const size_t dst = ((size_t)l * c->max_rounds + r0) * n * WSs;
-    SHCHK(c, hipMemcpyAsync(c->strong.as<u64>() + dst, &rows[(size_t)l * k * n * WSs], (size_t)k * n * WSs * 8,
+    const size_t dst = ((size_t)l * c->max_rounds + r0) * n * SP;
+    SHCHK(c, hipMemcpyAsync(c->strong.as<u64>() + dst, &rows[(size_t)l * k * n * SP], (size_t)k * n * SP * 8,
                             hipMemcpyHostToDevice, c->stream));
     const uint64_t base = c->h_weak[l].size();
     c->h_weak[l].insert(c->h_weak[l].end(), wnew[l].begin(), wnew[l].end());
     for (int i = 1; i <= k; i++) c->h_woff[l].push_back(base + wro[l][i]);
+    wcro_new[l][k] = wck_new[l].size();
+    const uint64_t cbase = c->h_wck[l].size();
+    c->h_wck[l].insert(c->h_wck[l].end(), wck_new[l].begin(), wck_new[l].end());
+    c->h_wcr[l].insert(c->h_wcr[l].end(), wcr_new[l].begin(), wcr_new[l].end());
+    for (int i = 1; i <= k; i++) c->h_wcro[l].push_back(cbase + wcro_new[l][i]);
   }
   SHCHK(c, hipStreamSynchronize(c->stream));
   c->h_pres.insert(c->h_pres.end(), pres.begin(), pres.end());
@@ -1382,6 +1863,7 @@ extern "C" int dr_shard_replay(dr_shard *c, int nwaves, int chain_mode, int deli
   o->canon_segments = -1;
   c->last_xbytes = 0;
   c->last_rounds = 0;
+  if (memo_applies(c)) return replay_memo(c, nwaves, chain_mode, deliver_mode, o);
   hipEvent_t t0 = nullptr, t1 = nullptr, t2 = nullptr;
   SHCHK(c, hipEventCreate(&t0));
   SHCHK(c, hipEventCreate(&t1));

@@ -142,6 +142,10 @@ class ShardEngine:
         """DR_SHARD_OPT_PERSISTENT: one cooperative launch per sweep batch (local mode)."""
         self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_PERSISTENT, int(on)))
 
+    def set_memo(self, on: bool):
+        """DR_SHARD_OPT_MEMO: memoized REF replay (summaries, canonical cone, relative-round steps)."""
+        self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_MEMO, int(on)))
+
     def set_leader_coin(self, mode: int = L.DR_LEADER_CONST1, seed: int = 0,
                         table: Optional[Sequence[int]] = None):
         """chooseLeader (process.go:386-392), as Engine.set_leader_coin."""

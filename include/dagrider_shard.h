@@ -75,6 +75,14 @@ int dr_shard_path_batch(dr_shard *ctx, int q, const int32_t *from, const int32_t
  * one cooperative launch with grid barriers between rounds; 0 launches one
  * kernel per round (the RCCL mode's shape).  Results are identical. */
 #define DR_SHARD_OPT_PERSISTENT 1
+/* DR_SHARD_OPT_MEMO (default 1): dr_shard_replay runs the memoized path when
+ * every weak delta is <= 65 -- per-shard round summaries, the canonical cone,
+ * and every leader chain and delivery cone stepped together by relative round
+ * (a cone stops where its frontier merges with the canonical cone; one exchange
+ * per step for all queries); PAPER delivery assigns each vertex to the first
+ * pop whose cone holds it.  0 = the batched full sweeps.  Results are
+ * identical. */
+#define DR_SHARD_OPT_MEMO 2
 int dr_shard_set_option(dr_shard *ctx, int option, int value);
 
 /* chooseLeader (process.go:386-392): dr_set_leader_coin's modes and semantics. */

@@ -118,6 +118,12 @@ def test_shard_rccl_single_rank(gpu_device):
         _check_reach(se, bs, froms, bottoms)
         st = se.stats()
         assert st["exchange_bytes"] > 0
+        # the whole replay through the all-gathers (memo path: K^cand and every step)
+        f, nw = 66, R // 4
+        for cm, dm in MODES:
+            got = se.replay(nw, cm, dm)
+            _same_replay(got, bs.replay(f, nw, cm, dm))
+            assert got.sweep["canon_segments"] >= 0 and se.stats()["exchange_bytes"] > 0
 
 
 def test_shard_errors(gpu_device):
@@ -168,12 +174,38 @@ def test_shard_replay_random_dags(gpu_device, seed):
     for G in ((1, 2) if seed % 2 else (3, 8)):
         with ShardEngine(n, f, R + 1, gpu_device, nshards=G) as se:
             se.append_packed(d)
-            for persistent in (True, False):
+            for memo, persistent in ((True, True), (False, True), (False, False)):
+                se.set_memo(memo)
                 se.set_persistent(persistent)
                 for cm, dm in MODES:
                     want = bs.replay(f, nw, cm, dm)
                     assert want.rc == 0
                     _same_replay(se.replay(nw, cm, dm), want)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_shard_memo_replay_generated(gpu_device, seed):
+    """The memoized sharded replay (summaries per shard, canonical cone, pops and chains
+    stepped by relative round) == the unsharded engine and the bitset oracle on
+    quorum-shaped DAGs with late vertices, weak edges up to 12 deep and absent leaders,
+    at G = 1, 2, 3, 8, both chain modes, REF and PAPER delivery."""
+    from dag_rider_amd.gen import small_config
+
+    rng = np.random.default_rng(4400 + seed)
+    n = int(rng.choice([64, 100, 256, 700, 1024]))
+    cfg = small_config(n, int(rng.integers(40, 120)), 60 + seed, p_present=float(rng.uniform(0.9, 1)),
+                       p_late=float(rng.uniform(0.02, 0.3)), p_w=float(rng.uniform(0.1, 0.6)),
+                       weak_depth=int(rng.integers(2, 13)), p_la=0.1)
+    d = generate(cfg)
+    bs = oracle.PDag(d)
+    nw = cfg.nwaves
+    for G in (1, 2, 3, 8):
+        with ShardEngine(n, cfg.faulty, d.nrounds, gpu_device, nshards=G) as se:
+            se.append_packed(d)
+            for cm, dm in MODES:
+                got = se.replay(nw, cm, dm)
+                _same_replay(got, bs.replay(cfg.faulty, nw, cm, dm))
+                assert got.sweep["canon_segments"] >= 0  # the memo path ran
 
 
 def test_shard_commit_chain_order_calls(gpu_device):
@@ -223,9 +255,13 @@ def test_shard_replay_c4_full(gpu_device):
     for G in (1, 2, 4, 8):
         with ShardEngine(cfg.n, cfg.faulty, d.nrounds, gpu_device, nshards=G) as se:
             se.append_packed(d)
-            _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
-            if G in (1, 8):
-                _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_PAPER), g["persistent_paper"])
+            got = se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+            _check_golden(got, g["persistent_ref"])
+            assert got.sweep["canon_segments"] >= 0 and se.stats()["rounds"] < 100  # memo: a few dozen steps
+            _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_PAPER), g["persistent_paper"])
+            if G in (1, 8):  # the batched full sweeps (DR_SHARD_OPT_MEMO 0), REF
+                se.set_memo(False)
+                _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
 
 
 def _check_golden(got, want):
