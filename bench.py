@@ -16,12 +16,15 @@ pattern: per wave append 4 rounds -> dr_wave_ready -> dr_order_vertices, per-wav
 latency), --deliver paper (dedup across pops).
 
 --gpus N without torchrun: spawns N ranks (torch.distributed.run) before anything
-touches a GPU; under torchrun WORLD_SIZE must equal N.  Each rank replays its own
-independent C4 DAG (seed 4+rank): independent units, no data-path collective
-("scaling": "weak").  After the timed region N>1 also runs (a) the all-waves commit
-sweep of ONE C4 DAG split into wave ranges, one per GPU (detail.commit_split), and
-(b) the process-column sharded reach sweep with an RCCL all-gather per round
-(detail.colshard).
+touches a GPU; under torchrun WORLD_SIZE must equal N.  For C4 at N > 1 the line
+is BASELINE.json configs[3] as named: ONE C4 DAG (seed 4) with its process columns
+sharded across the N GPUs, the memoized replay with the frontier all-gathered over
+RCCL ("parallelism": "colshardN", "scaling": "strong": the same edges per step at
+every N), timed in one child process per rank (a hung collective is killed, not
+waited for) and checked on rank 0 against the unsharded engine.  detail.replicas
+holds every rank replaying its own unsharded C4 DAG (seed 4+rank, weak scaling),
+detail.commit_split the all-waves commit sweep of the DAG split into wave ranges.
+C5 at N > 1 splits its 4096 DAGs across the ranks.
 
 Prints ONE JSON line on rank 0.
 """
@@ -429,92 +432,131 @@ def run_rank_share(args, local: int):
 
 
 def colshard_child(args):
-    """One rank of the process-column sharded path: every rank
-    holds 1/N of the target columns; the frontier is all-gathered over RCCL each round.
-    Workloads: the full causal-history reach sets (strong + weak, rounds 0..leader) of
-    the 64 newest wave leaders, then the whole replay (dr_shard_replay: waveReady
-    votes and chains, orderVertices cones and emission), both checked on rank 0
-    against the unsharded engine."""
-    import numpy as np
-
-    from dag_rider_amd.gen import CONFIGS, generate
-    from dag_rider_amd.shard import ShardEngine
-
+    """One rank of the process-column sharded C4 replay (BASELINE.json configs[3],
+    SURVEY.md s8(e)): every rank holds 1/N of the target columns of the ONE seed-4 C4
+    DAG; dr_shard_replay runs the memoized replay with the frontier all-gathered over
+    RCCL (shard_memo.hpp).  Warm-up replays, a collective as the start barrier, then
+    exactly --steps timed replays (each returns with its results in host memory).
+    Rank 0 then checks every output against the unsharded engine's dr_replay."""
     from dag_rider_amd import _lib as L
+    from dag_rider_amd.gen import CONFIGS, generate
+    from dag_rider_amd.shard import ShardEngine, ShardReplayer
 
     cfg = CONFIGS["c4"]
     d = generate(cfg, nthreads=CPU_THREADS)
     se = ShardEngine(cfg.n, cfg.faulty, d.nrounds, args.cs_device, args.cs_world, args.cs_rank,
                      bytes.fromhex(args.cs_uid))
     se.append_packed(d)
-    froms = [(4 * w - 3, 1) for w in range(cfg.nwaves, cfg.nwaves - 64, -1)]
-    bottoms = [0] * len(froms)
-    got = se.reach_sets(froms, bottoms, False)  # warm-up
-    runs = []
-    for _ in range(3):
-        got = se.reach_sets(froms, bottoms, False)
-        runs.append(se.stats())
-    st = min(runs, key=lambda x: x["ms"])
-    # the whole replay on the sharded DAG: commit votes (3 all-gathers), chains and
-    # delivery cones (one all-gather per round), emission on every rank
+    step = ShardReplayer(se, cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+    for _ in range(max(args.warmup, 1)):
+        step()
+    se.wave_commit(1, 1)  # a collective: every rank has finished its warm-up
     t0 = time.perf_counter()
-    rep = se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
-    rep_ms = (time.perf_counter() - t0) * 1e3
-    rst = se.stats()
-    out = dict(st, nshards=args.cs_world, queries=len(froms), info=se.info(),
-               replay=dict(ms=rep_ms, phases_ms=rep.ms, sweep_rounds=rst["rounds"],
-                           exchange_bytes=rst["exchange_bytes"], edges=rep.total_edges,
-                           commits=int(rep.commit.sum()), pops=len(rep.pop_count)))
+    for _ in range(args.steps):
+        step()
+    dt = time.perf_counter() - t0
+    rep = step.result()
+    st = se.stats()
+    info = se.info()
+    out = dict(rank=args.cs_rank, ms=dt / args.steps * 1e3, steps=args.steps, phases_ms=rep.ms,
+               sweep_steps=st["rounds"], exchange_bytes=st["exchange_bytes"], edges=rep.total_edges,
+               commits=int(rep.commit.sum()), pops=len(rep.pop_count), canon_segments=rep.sweep["canon_segments"],
+               cols=(info["col0"], info["col1"]), row_bytes=(d.nrounds - 1) * cfg.n * 8 *
+               ((cfg.n + 63) // 64 + args.cs_world - 1) // args.cs_world)
     se.close()
     if args.cs_rank == 0:
         from dag_rider_amd.engine import Engine
 
         with Engine(cfg.n, cfg.faulty, d.nrounds, args.cs_device) as e:
             e.append_packed(d)
-            ref = e.reach_sets(froms, bottoms, False)
             rr = e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
-        out["verify_vs_unsharded"] = bool(all((a == b).all() for a, b in zip(got, ref)))
-        out["reach_bits"] = int(sum(int(np.unpackbits(a.view(np.uint8)).sum()) for a in got))
-        out["replay"]["verify_vs_unsharded"] = bool(
-            (rep.commit == rr.commit).all() and (rep.vcount == rr.vcount).all()
-            and (rep.push_wave == rr.push_wave).all() and (rep.pop_count == rr.pop_count).all()
-            and (rep.pop_digest == rr.pop_digest).all() and (rep.pop_edges == rr.pop_edges).all()
-            and rep.total_edges == rr.total_edges)
+        out["verify_vs_unsharded"] = same_replay(rep, rr)
     print(json.dumps(out), flush=True)
 
 
-def colshard_check(dist, rank: int, world: int, local: int, timeout_s: float = 240.0):
-    """Run colshard_child in one child process per rank (a hung collective can then be
-    killed without losing the headline line); returns rank 0's result + max time."""
+def colshard_run(dist, rank: int, world: int, local: int, steps: int, warmup: int, timeout_s: float = 300.0):
+    """Run colshard_child in one child process per rank (a hung collective is killed
+    by the time limit instead of hanging the job); returns every rank's result (or
+    error) on every rank."""
     import subprocess
 
     from dag_rider_amd.shard import exchange_unique_id
 
-    if dist is not None:
-        uid = exchange_unique_id(dist)
-    else:
-        from dag_rider_amd.shard import shard_unique_id
-
-        uid = shard_unique_id()
+    uid = exchange_unique_id(dist)
     cmd = [sys.executable, os.path.abspath(__file__), "--colshard-child", "--cs-uid", uid.hex(),
-           "--cs-rank", str(rank), "--cs-world", str(world), "--cs-device", str(local)]
-    res = None
+           "--cs-rank", str(rank), "--cs-world", str(world), "--cs-device", str(local),
+           "--steps", str(steps), "--warmup", str(warmup)]
     try:
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
         lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
-        res = json.loads(lines[-1]) if p.returncode == 0 and lines else dict(error=(p.stderr or "")[-400:])
+        res = json.loads(lines[-1]) if p.returncode == 0 and lines else dict(
+            rank=rank, error=f"exit {p.returncode}: " + (p.stderr or "")[-400:])
     except subprocess.TimeoutExpired:
-        res = dict(error=f"timed out after {timeout_s} s")
-    if dist is not None:
-        allr = [None] * world
-        dist.all_gather_object(allr, res)
-    else:
-        allr = [res]
-    ms = [r.get("ms") for r in allr if r and "ms" in r]
-    if rank == 0 and res is not None:
-        res["ms_max_over_ranks"] = max(ms) if len(ms) == world else None
-        res["errors"] = [r.get("error") for r in allr if r and "error" in r] or None
-    return res
+        res = dict(rank=rank, error=f"timed out after {timeout_s} s")
+    allr = [None] * world
+    dist.all_gather_object(allr, res)
+    return allr
+
+
+def c4_multi_line(args, world: int, cs_all, replicas, split):
+    """The N > 1 line of the C4 config: the column-sharded replay of ONE C4 DAG
+    (strong scaling: the same 1.75e12 edges per step whatever N; BASELINE.json
+    configs[3] "process-column sharded across 2/4/8 GPUs with RCCL frontier
+    all-gather"), its slowest rank's time per replay.  The independent-replicas
+    number (every rank its own C4 DAG) goes to detail.replicas.  If any rank's
+    sharded run failed, the line says so and carries the replicas number instead,
+    labelled as such ("parallelism": "replicasN")."""
+    ok = all(r is not None and "error" not in r for r in cs_all)
+    verified = ok and bool(cs_all[0].get("verify_vs_unsharded"))
+    base = {
+        "metric": "DAG edges traversed/sec (commit+delivery)",
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "higher_is_better": True,
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded generator, SURVEY.md s8(d) C4 parameters)",
+        "cpu_baseline": None,
+    }
+    rep_detail = dict(replicas, parallelism=f"replicas{world}", scaling="weak",
+                      note="every rank replays its own C4 DAG (seed 4 + rank), unsharded; value = summed edges / "
+                           "slowest rank")
+    if ok:
+        ms = max(r["ms"] for r in cs_all)
+        edges = cs_all[0]["edges"]
+        r0 = cs_all[0]
+        summ = r0["phases_ms"].get("summary", 0.0)
+        rb = r0["row_bytes"]
+        return dict(base, **{
+            "value": edges / (ms / 1e3),
+            "ms_per_step": ms,
+            "scaling": "strong",
+            "config": {"workload": "C4 full replay of ONE DAG (n=1024 x 4000 rounds, seed 4), process columns sharded "
+                                   f"across {world} GPUs (1/{world} of every strong row and the weak edges targeting "
+                                   "its columns per GPU), frontier all-gathered over RCCL: waveReady (persistent "
+                                   "decidedWave) + orderVertices (ref, full cones), memoized (shard_memo.hpp)",
+                       "n": 1024, "rounds": 4000, "waves": 1000, "parallelism": f"colshard{world}"},
+            "roofline": {"bound": "hbm", "achieved": rb / (summ / 1e3) / 1e9 if summ > 0 else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": rb / (summ / 1e3) / 1e9 / HBM_PEAK_GBS if summ > 0 else None, "traffic": None,
+                         "kernel": "summary phase per rank (k_ms_summary over the rank's columns + K^cand exchange "
+                                   "+ canonical segment), rank 0", "bytes_per_launch": rb, "ms_per_launch": summ},
+            "detail": {"verify_vs_unsharded": verified, "ranks": cs_all, "replicas": rep_detail,
+                       "commit_split": split},
+        })
+    errs = [r.get("error") if r else "no result" for r in cs_all]
+    return dict(base, **{
+        "value": replicas["value"],
+        "ms_per_step": replicas["ms_per_step"],
+        "scaling": "weak",
+        "config": {"workload": f"C4 full replay, independent replicas (seed 4 + rank) -- the column-sharded run "
+                               f"FAILED on this node: {errs}", "n": 1024, "rounds": 4000, "waves": 1000,
+                   "parallelism": f"replicas{world}"},
+        "roofline": replicas.get("roofline"),
+        "detail": {"colshard_errors": errs, "ranks": cs_all, "replicas": rep_detail, "commit_split": split},
+    })
 
 
 def run_c5(args, rank: int, world: int, local: int, dist):
@@ -736,9 +778,12 @@ def spawn_ranks(args) -> int:
     return subprocess.call(cmd)
 
 
-def dist_selftest(rank: int, world: int, local: int) -> int:
+def dist_selftest(rank: int, world: int, local: int, args=None) -> int:
     """The multi-rank plumbing without a GPU (gloo): every rank reports in, the job's
-    line is reduced exactly as the GPU path reduces it (tests/test_dist_gloo.py)."""
+    numbers are reduced exactly as the GPU path reduces them, and the C4 N > 1 line is
+    built by the same code (c4_multi_line) from every rank's sharded-replay result
+    (synthetic here: rank r took 0.25 (r+1) ms; --selftest-fail makes rank 1 fail)
+    (tests/test_dist_gloo.py)."""
     import torch.distributed as dist
 
     dist.init_process_group("gloo", init_method="env://")
@@ -746,9 +791,19 @@ def dist_selftest(rank: int, world: int, local: int) -> int:
         dt, tot = reduce_over_ranks(dist, 0.25 * (rank + 1), 1000 * (rank + 1), "cpu")
         ranks = [None] * world
         dist.all_gather_object(ranks, dict(rank=rank, local_rank=local, pid=os.getpid()))
+        fail = args is not None and args.selftest_fail and rank == 1
+        mine = dict(rank=rank, error="selftest failure") if fail else dict(
+            rank=rank, ms=0.25 * (rank + 1), edges=10 ** 9, verify_vs_unsharded=True, phases_ms={"summary": 0.1},
+            row_bytes=1000)
+        cs_all = [None] * world
+        dist.all_gather_object(cs_all, mine)
         if rank == 0:
-            print(json.dumps({"metric": "dist selftest", "value": tot / dt, "n_gpus": world, "ms_per_step": dt * 1e3,
-                              "ranks": ranks}), flush=True)
+            a = argparse.Namespace(steps=3, warmup=1)
+            reps = dict(value=tot / dt, ms_per_step=dt * 1e3, roofline=None)
+            line = c4_multi_line(a, world, cs_all, reps, None)
+            line.update(metric_selftest="dist selftest", selftest_value=tot / dt, ranks=ranks,
+                        selftest_ms_per_step=dt * 1e3)
+            print(json.dumps(line), flush=True)
     finally:
         dist.destroy_process_group()
     return 0
@@ -772,6 +827,7 @@ def main() -> int:
                     help="also run the process-column sharded C4 sweep (default on when N>1)")
     ap.add_argument("--no-colshard", action="store_true")
     ap.add_argument("--dist-selftest", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--selftest-fail", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--colshard-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cs-uid", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cs-rank", type=int, default=0, help=argparse.SUPPRESS)
@@ -790,7 +846,7 @@ def main() -> int:
         log(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a mislabelled line")
         return 2
     if args.dist_selftest:
-        return dist_selftest(rank, world, local)
+        return dist_selftest(rank, world, local, args)
 
     from dag_rider_amd import _lib as L
 
@@ -880,13 +936,28 @@ def main() -> int:
         verify = same_replay(res, want)
 
     split = colshard = None
+    multi = world > 1 and args.config == "c4" and not args.no_colshard
     if world > 1 and args.config == "c4":
         split = commit_split(dist, rank, world, local, res.commit if rank == 0 else None,
                              res.vcount if rank == 0 else None)
-        if not args.no_colshard:
-            colshard = colshard_check(dist, rank, world, local)
-    elif args.colshard and args.config == "c4":
-        colshard = colshard_check(dist, rank, world, local)
+    if multi or (args.colshard and args.config == "c4"):
+        if dist is None:  # one-rank RCCL group (--colshard at N=1): gloo-free id exchange
+            class _One:
+                @staticmethod
+                def get_rank(group=None):
+                    return 0
+
+                @staticmethod
+                def broadcast_object_list(box, src=0, group=None):
+                    return None
+
+                @staticmethod
+                def all_gather_object(out, obj):
+                    out[0] = obj
+
+            colshard = colshard_run(_One, rank, 1, local, args.steps, args.warmup)
+        else:
+            colshard = colshard_run(dist, rank, world, local, args.steps, args.warmup)
     if rank == 0 and colshard is not None:
         log(f"[colshard] {colshard}")
 
@@ -932,10 +1003,14 @@ def main() -> int:
                    "ms": res.ms, "ms_note": "summary: mean over the timed steps; other phases: one "
                    "profiling replay after them (DR_OPT_PHASE_TIMING=2)",
                    "sweep": res.sweep, "verify_vs_oracle": verify,
-                   "commit_split": split, "colshard": colshard,
+                   "commit_split": split, "colshard": colshard[0] if colshard else None,
                    "kernels": {k: dict(v, GBps=(v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None))
                                for k, v in kb.items()}},
     }
+    if multi:
+        out = c4_multi_line(args, world, colshard, dict(value=out["value"], ms_per_step=ms_per_step,
+                                                        roofline=out["roofline"], edges_per_step=res.total_edges,
+                                                        verify_vs_oracle=verify), split)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

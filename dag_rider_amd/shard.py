@@ -187,3 +187,22 @@ class ShardEngine:
         o, keep = _replay_out(nwaves, chain_mode, 0, push_cap)
         self._check(self._L.dr_shard_replay(self._h, nwaves, chain_mode, deliver_mode, C.byref(o)))
         return _replay_result(o, keep, 0)
+
+
+class ShardReplayer:
+    """dr_shard_replay into output buffers allocated once (the bench's timed steps);
+    result() returns views of those buffers, overwritten by the next call."""
+
+    def __init__(self, se: ShardEngine, nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT,
+                 deliver_mode: int = L.DR_DELIVER_REF):
+        self._se = se
+        self._o, self._keep = _replay_out(nwaves, chain_mode, 0)
+        self._fn, self._args = se._L.dr_shard_replay, (se._h, nwaves, chain_mode, deliver_mode, C.byref(self._o))
+
+    def __call__(self) -> None:
+        rc = self._fn(*self._args)
+        if rc != L.DR_OK:
+            self._se._check(rc)
+
+    def result(self) -> ReplayResult:
+        return _replay_result(self._o, self._keep, 0)

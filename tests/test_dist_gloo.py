@@ -75,7 +75,28 @@ def test_bench_gpus_spawns_ranks():
     assert out["n_gpus"] == 2
     assert sorted(r["rank"] for r in out["ranks"]) == [0, 1]
     assert len({r["pid"] for r in out["ranks"]}) == 2
-    assert out["ms_per_step"] == 500.0 and out["value"] == 3000 / 0.5
+    assert out["selftest_ms_per_step"] == 500.0 and out["selftest_value"] == 3000 / 0.5
+    # the C4 N > 1 line (bench.c4_multi_line): the column-sharded replay of one DAG,
+    # slowest rank (0.5 ms), strong scaling, replicas in detail
+    assert out["config"]["parallelism"] == "colshard2" and out["scaling"] == "strong"
+    assert out["ms_per_step"] == 0.5 and out["value"] == 1e9 / 0.5e-3
+    assert out["detail"]["replicas"]["parallelism"] == "replicas2"
+    assert out["detail"]["verify_vs_unsharded"] is True
+
+
+def test_bench_gpus_colshard_failure_is_labelled():
+    """A rank whose sharded run fails: the line carries the replicas number, says so."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-selftest",
+                        "--selftest-fail"], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
+    assert out["config"]["parallelism"] == "replicas2" and out["scaling"] == "weak"
+    assert "FAILED" in out["config"]["workload"] and out["detail"]["colshard_errors"][1] == "selftest failure"
+    assert out["value"] == 3000 / 0.5
 
 
 def test_bench_world_mismatch_refused():
