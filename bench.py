@@ -571,6 +571,10 @@ def run_c5(args, rank: int, world: int, local: int, dist):
 
     total = 4096
     lo, hi = rank * total // world, (rank + 1) * total // world
+    if args.dags:  # one GPU's share at N = 4096 / dags (e.g. 512 = one rank's share at N = 8)
+        if world > 1:
+            raise SystemExit("--dags is a single-GPU option")
+        lo, hi = 0, min(args.dags, total)
     t0 = time.perf_counter()
     engines, dags, dag_bytes = [], [], 0
     for i in range(lo, hi):
@@ -604,7 +608,7 @@ def run_c5(args, rank: int, world: int, local: int, dist):
         return None
     cpu = None
     if not args.no_cpu and world == 1:
-        cpu = cpu_c5(dags, args.deliver_mode, res)
+        cpu = cpu_c5(dags, args.deliver_mode, res) if not args.dags else None
     ach = dag_bytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
     return {
         "metric": "DAG edges traversed/sec (commit+delivery)",
@@ -619,9 +623,10 @@ def run_c5(args, rank: int, world: int, local: int, dist):
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (seeded generator, SURVEY.md s8(d) C5 parameters, seeds 5000+i)",
-        "config": {"workload": "C5: 4096 independent n=128 x 128-round replays (waveReady + orderVertices "
+        "config": {"workload": f"C5: {total if not args.dags else hi - lo} independent n=128 x 128-round replays "
+                               "(waveReady + orderVertices "
                                f"{'paper' if args.deliver_mode else 'ref'}, persistent decidedWave), split across ranks",
-                   "dags": total, "dags_per_rank": hi - lo, "n": 128, "rounds": 128, "waves": nw,
+                   "dags": total if not args.dags else hi - lo, "dags_per_rank": hi - lo, "n": 128, "rounds": 128, "waves": nw,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "roofline": {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic("batch"),
@@ -814,12 +819,13 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c4-deep", "c4-deep64", "c5", "c4-loop"])
+    ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4-deep", "c4-deep64", "c5", "c4-loop"])
     ap.add_argument("--deliver", default="ref", choices=["ref", "paper"])
     ap.add_argument("--cpu-budget", type=float, default=40.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phase-timing", type=int, default=1, help=argparse.SUPPRESS)  # 0: no events (experiment)
     ap.add_argument("--loop-waves", type=int, default=0, help="c4-loop: waves to run (0 = all)")
+    ap.add_argument("--dags", type=int, default=0, help="c5 on one GPU: replay only the first N DAGs")
     ap.add_argument("--rank-share", type=int, default=0,
                     help="one GPU: time every rank's share of the C4 wave-range commit split for N ranks")
     ap.add_argument("--verify", action="store_true", help="check the replay against the bitset oracle")

@@ -117,6 +117,12 @@ struct dr_ctx {
   // round summaries (U, SD, WU) per round: sdirty[r] = stale; the canonical cone
   // and its prefixes (K, C, G, E) describe the DAG as of the last canon build
   bool use_memo = true;
+  uint64_t version = 0;  // bumped by every change of the DAG or the leader coin
+  // replay_planned's delivery queries (one per wave whose leader is present),
+  // built on the host and cached on the device while the DAG is unchanged
+  DevBuf fixed_q;
+  uint64_t fixed_ver = ~0ULL;
+  int fixed_nw = -1, fixed_nq = 0;
   std::vector<uint8_t> sdirty;
   int sum_dd = -1;            // WU layout the summaries were built with (memo_dd())
   bool canon_ok = false;      // K/C/G/E describe the current DAG
@@ -178,7 +184,7 @@ struct dr_ctx {
   struct Pending { void *dst; void *stage; const void *src; size_t n; };
   std::vector<Pending> pend;
   hipEvent_t ev_sync = nullptr, ev_sync2 = nullptr, ev_fork = nullptr, ev_join = nullptr, ev_start = nullptr,
-            ev_wu = nullptr;
+            ev_wu = nullptr, ev_canon = nullptr;
   hipStream_t stream2 = nullptr;  // second queue: canonical cone beside the leader chains
   hipError_t launch_copies(const dr::CopySeg *sg, int k) {
     for (int i0 = 0; i0 < k; i0 += dr::kCopySegs) {
@@ -332,6 +338,7 @@ struct dr_ctx {
   }
   // a round changed: its summaries are stale, and so is every canonical prefix
   void touch(int r) {
+    version++;
     while ((int)sdirty.size() <= r) { sdirty.push_back(1); ndirty++; }
     if (!sdirty[r]) { sdirty[r] = 1; ndirty++; }
     canon_ok = false;
@@ -765,7 +772,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   // per record.  ev_sync / ev_sync2 order the kernels' writes to pinned host
   // memory before the host reads them, so they keep the system fence.
   for (auto &ev : c->ev) (void)hipEventCreateWithFlags(&ev, hipEventReleaseToDevice);
-  for (hipEvent_t *e : {&c->ev_fork, &c->ev_join, &c->ev_start, &c->ev_wu})
+  for (hipEvent_t *e : {&c->ev_fork, &c->ev_join, &c->ev_start, &c->ev_wu, &c->ev_canon})
     (void)hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice);
   for (hipEvent_t *e : {&c->ev_sync, &c->ev_sync2}) (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
   const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64);
@@ -815,7 +822,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
-  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join, c->ev_start, c->ev_wu})
+  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join, c->ev_start, c->ev_wu, c->ev_canon})
     if (e) (void)hipEventDestroy(e);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1314,7 +1321,7 @@ int refresh_rounds(dr_ctx *c) {
 // prefix = false: the caller's emitting sweep computes the G, E prefixes.
 // spec: RG holds every round's speculative digest (build_summary's weak union).
 int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool forked = false,
-                 bool incremental = false, bool prefix = true, bool spec_rg = false) {
+                 bool incremental = false, bool prefix = true, bool spec_rg = false, bool emit_side = false) {
   const int T = c->nrounds - 1;
   // incremental (the per-call path): rounds below the lowest one that changed
   // since the last cone, and whose canonical vertices are unchanged, keep their
@@ -1332,16 +1339,24 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
   }
+  emit_side = emit_side && fork && side;
   if (fork && side) {
     Swap sw(c, true);
     if (int rc = (*side)()) return rc;
-    HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
+    if (!emit_side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   }
   Swap sw(c, fork && !side);
   // canonical cone, per-round counts and positions (k_kcand + k_canon), then the
   // per-round digests (emission) and their prefixes
   const bool spec = spec_rg && lo <= 1;  // a full cone: re-emission from the first non-full round
   HIPCHK(c, launch_canon_cone(c, T, lo, spec));  // *rlo = the lowest round to re-emit
+  // emit_side: the canonical emission joins stream2's work (side), so the delivery
+  // sweeps can start on the main stream right after the cone; ev_join marks both
+  Swap sw2(c, emit_side);
+  if (emit_side) {
+    HIPCHK(c, hipEventRecord(c->ev_canon, c->stream2));  // c->stream2 is the main stream here
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_canon, 0));
+  }
   dr::PopDesc d{};
   d.mask_off = 0;
   d.rbase_off = 1;  // crbase is indexed by round; rbase_off addresses round `first`
@@ -1357,7 +1372,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
     hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
                        c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
-  if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
+  if ((fork && !side) || emit_side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   c->kprev_ok = true;
   c->canon_dd = c->memo_dd();
   c->canon_lo = INT_MAX;
@@ -1401,7 +1416,7 @@ int refresh_canon(dr_ctx *c) {
 // re-reads the whole DAG; nothing carries over from earlier calls.
 int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
                   bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr,
-                  bool prefix = true) {
+                  bool prefix = true, bool emit_side = false) {
   const int T = c->nrounds - 1;
   if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
   if (int rc = ensure_summary_bufs(c)) return rc;
@@ -1425,7 +1440,7 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   }
   HIPCHK(c, launch_weak_union(c, T, c->stream));
   mark_rounds_clean(c);
-  if (int rc = launch_canon(c, fork, side, early, false, prefix, true)) return rc;
+  if (int rc = launch_canon(c, fork, side, early, false, prefix, true, emit_side)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
   if (nwc > 0) {
     HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nwc));
@@ -1468,6 +1483,7 @@ extern "C" int dr_set_leader_coin(dr_ctx *c, int mode, uint64_t seed, int k, con
     return c->fail(DR_E_INVAL, "unknown leader coin mode %d", mode);
   }
   c->h_lead = std::move(L);
+  c->version++;
   HIPCHK(c, c->h2d(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2));
   HIPCHK(c, c->sync());
   return DR_OK;
@@ -2421,6 +2437,50 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     }
   }
   HIPCHK(c, c->masks.ensure(mask_words * 8));
+  // REF: the delivery queries are fixed in advance -- one per wave whose leader is
+  // present, highest round first (a superset of the leaders any push can pop; a
+  // REF pop depends only on its leader) -- so the delivery sweeps need only the
+  // canonical cone, not the chains; cached while the DAG and coin are unchanged
+  const bool fixedq = !paper;
+  dr::SweepQuery *fq = nullptr;
+  int32_t *fq_idx = nullptr, *fq_plan = nullptr;
+  if (fixedq) {
+    const size_t qb = ((size_t)nw * sizeof(dr::SweepQuery) + 255) & ~(size_t)255;
+    const size_t ib = (((size_t)nw + 1) * 4 + 255) & ~(size_t)255;
+    if (c->fixed_ver != c->version || c->fixed_nw != nw || !c->fixed_q.p) {
+      std::vector<char> hb(qb + ib + dr::PL_N * 4, 0);
+      auto *hq = reinterpret_cast<dr::SweepQuery *>(hb.data());
+      auto *hi = reinterpret_cast<int32_t *>(hb.data() + qb);
+      auto *hp = reinterpret_cast<int32_t *>(hb.data() + qb + ib);
+      int nq = 0;
+      int64_t mo = 0;
+      for (int w = 0; w <= nw; w++) hi[w] = -1;
+      for (int w = nw; w >= 1; w--) {
+        const int top = 4 * (w - 1) + 1;
+        if (!c->is_present(top, c->lead_src(w))) continue;
+        dr::SweepQuery q{};
+        q.top = top;
+        q.bottom = 0;
+        q.src0 = c->lead_src(w) - 1;
+        q.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
+        q.mask_off = mo;
+        q.tgt0 = -1;
+        mo += (int64_t)(top + 1) * WS;
+        hi[w] = nq;
+        hq[nq++] = q;
+      }
+      hp[dr::PL_NQD] = nq;
+      HIPCHK(c, c->fixed_q.ensure(hb.size()));
+      HIPCHK(c, hipMemcpyAsync(c->fixed_q.p, hb.data(), hb.size(), hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      c->fixed_ver = c->version;
+      c->fixed_nw = nw;
+      c->fixed_nq = nq;
+    }
+    fq = c->fixed_q.as<dr::SweepQuery>();
+    fq_idx = reinterpret_cast<int32_t *>(c->fixed_q.as<char>() + qb);
+    fq_plan = reinterpret_cast<int32_t *>(c->fixed_q.as<char>() + qb + ib);
+  }
   // outputs: the emitting sweep's final pass packs them into one device region, which comes back
   // in one copy (writing them straight into pinned host memory from the kernel
   // took 19.5 us, profiles/r02/v27_timeline.txt)
@@ -2467,15 +2527,19 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     // 3. pops
     hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
                        dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave, task_q, cq, cpush_n, push_out, pcap,
-                       task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
+                       task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan, fq_idx,
+                       c->fixed_nq);
     HIPCHK(c, hipGetLastError());
     return 0;
   };
-  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false)) return rc;
+  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false, fixedq)) return rc;
+  if (fixedq) dq = fq;
   if (paper) c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
   // 3+4. delivery sweeps (merging with K), then each query's emission
   a.q = dq;
   a.push_out = nullptr;
+  a.push_n = nullptr;  // the chains' push counts: stream2's pop plan may still read them
+  a.hits = nullptr;
   a.edges = dedges;
   a.wedges = dwedges;
   a.stops = dstops;
@@ -2510,9 +2574,17 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   }
   dr::SweepQuery probe{};
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
-  HIPCHK(c, c->rec(2));
-  HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
+  if (fixedq) {  // the sweeps need only the cone; stream2's chains, pop plan and emission join after them
+    a.nq = c->fixed_nq;
+    a.nq_dev = nullptr;
+    HIPCHK(c, c->rec(2));
+    HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+  } else {
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
+    HIPCHK(c, c->rec(2));
+    HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
+  }
   if (paper) {  // first-pop ownership, then each query's delivered rounds
     hipLaunchKernelGGL((dr::k_paper_plan<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->memo_view().dmax, plan,
                        pop_q, dq, dstops, firstpop, qcut, qlo, firstK, qr_cnt, qr_off, qr_list);
@@ -2522,7 +2594,8 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     em.fin.firstpop = firstpop;
     em.fin.qedges = qedges;
   } else {  // REF: own rounds above the cut; the last workgroup: canonical prefixes G, E
-    HIPCHK(c, launch_own_emit(c, nw, plan, dq, dstops, qcount, qdigest, qcut));
+    HIPCHK(c, launch_own_emit(c, fixedq ? std::max(c->fixed_nq, 1) : nw, fixedq ? fq_plan : plan, dq, dstops, qcount,
+                              qdigest, qcut));
   }
   HIPCHK(c, c->rec(3));
   // 5. per-pop totals and outputs (the canonical prefixes came from the sweep launch's extra workgroup)
@@ -2563,6 +2636,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   o->n_push = np;
   if (h_hdr[dr::PH_CAPERR] == 2) return c->fail(DR_E_STATE, "replay planner: segment bound exceeded");
   if (h_hdr[dr::PH_CAPERR] == 3) return c->fail(DR_E_STATE, "replay planner: a pop below its leader's round");
+  if (h_hdr[dr::PH_CAPERR] == 4) return c->fail(DR_E_STATE, "replay planner: a pushed leader without a query");
   if (h_hdr[dr::PH_CAPERR] || np > o->push_cap)
     return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)np, (long long)o->push_cap);
   std::memcpy(o->push_off, h_push_off, ((size_t)nw + 1) * 4);

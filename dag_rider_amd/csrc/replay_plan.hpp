@@ -106,7 +106,11 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
                                                   int32_t *__restrict__ push_wave, int32_t *__restrict__ pop_wave,
                                                   int32_t *__restrict__ pop_cur, int32_t *__restrict__ pop_q,
                                                   uint8_t *__restrict__ seen, int32_t *__restrict__ qidx,
-                                                  SweepQuery *__restrict__ dq, int32_t *__restrict__ plan) {
+                                                  SweepQuery *__restrict__ dq, int32_t *__restrict__ plan,
+                                                  const int32_t *__restrict__ qfix, int nqfix) {
+  // qfix != nullptr: the delivery queries are fixed in advance (one per wave whose
+  // leader is present, qfix[w] its index; engine.hip replay_planned): only the
+  // pops' query indices are needed here
   __shared__ int64_t s[NT / 64];
   __shared__ int64_t c0, c1;
   const int tid = threadIdx.x;
@@ -156,6 +160,15 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
     const int whi = t < ntask ? task_wave[t] : nw + 1;
     const uint32_t v = (uint32_t)(t < ntask ? task_pos[t] : np);
     for (int w = wlo; w <= whi; w++) push_off[w - 1] = v;
+  }
+  if (qfix) {
+    if (tid == 0) plan[PL_NQD] = nqfix;
+    for (int64_t p = tid; p < np; p += NT) {
+      const int q = qfix[pop_wave[p]];
+      pop_q[p] = q;
+      if (q < 0) plan[PL_CAPERR] = 4;  // a pushed leader that is not present: cannot happen
+    }
+    return;
   }
   if (tid == 0) c0 = 0;
   __syncthreads();
