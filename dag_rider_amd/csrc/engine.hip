@@ -118,11 +118,7 @@ struct dr_ctx {
   // and its prefixes (K, C, G, E) describe the DAG as of the last canon build
   bool use_memo = true;
   uint64_t version = 0;  // bumped by every change of the DAG or the leader coin
-  // replay_planned's delivery queries (one per wave whose leader is present),
-  // built on the host and cached on the device while the DAG is unchanged
-  DevBuf fixed_q;
-  uint64_t fixed_ver = ~0ULL;
-  int fixed_nw = -1, fixed_nq = 0;
+  DevBuf fixed_q;  // replay_planned's delivery queries (k_fixed_queries)
   std::vector<uint8_t> sdirty;
   int sum_dd = -1;            // WU layout the summaries were built with (memo_dd())
   bool canon_ok = false;      // K/C/G/E describe the current DAG
@@ -1416,7 +1412,7 @@ int refresh_canon(dr_ctx *c) {
 // re-reads the whole DAG; nothing carries over from earlier calls.
 int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
                   bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr,
-                  bool prefix = true, bool emit_side = false) {
+                  bool prefix = true, bool emit_side = false, bool wu_side = false) {
   const int T = c->nrounds - 1;
   if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
   if (int rc = ensure_summary_bufs(c)) return rc;
@@ -1438,7 +1434,10 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
       HIPCHK(c, hipEventRecord(fe, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, fe, 0));
   }
-  HIPCHK(c, launch_weak_union(c, T, c->stream));
+  if (wu_side)  // the caller launched the weak unions on stream2 before the row pass (ev_wu marks them)
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_wu, 0));
+  else
+    HIPCHK(c, launch_weak_union(c, T, c->stream));
   mark_rounds_clean(c);
   if (int rc = launch_canon(c, fork, side, early, false, prefix, true, emit_side)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
@@ -2437,49 +2436,34 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     }
   }
   HIPCHK(c, c->masks.ensure(mask_words * 8));
-  // REF: the delivery queries are fixed in advance -- one per wave whose leader is
-  // present, highest round first (a superset of the leaders any push can pop; a
-  // REF pop depends only on its leader) -- so the delivery sweeps need only the
-  // canonical cone, not the chains; cached while the DAG and coin are unchanged
+  // REF: the delivery queries are fixed before the chains run -- one per wave whose
+  // leader is present, highest round first (a superset of the leaders any push can
+  // pop; a REF pop depends only on its leader) -- so the delivery sweeps need only
+  // the canonical cone.  Built on the device by every replay (k_fixed_queries, on
+  // stream2 beside the summary pass); the sweep's grid is the present-leader count,
+  // known on the host from the mirror's presence bits.
   const bool fixedq = !paper;
   dr::SweepQuery *fq = nullptr;
   int32_t *fq_idx = nullptr, *fq_plan = nullptr;
+  int fq_n = 0;
   if (fixedq) {
+    for (int w = 1; w <= nw; w++) fq_n += c->is_present(4 * (w - 1) + 1, c->lead_src(w)) ? 1 : 0;
     const size_t qb = ((size_t)nw * sizeof(dr::SweepQuery) + 255) & ~(size_t)255;
     const size_t ib = (((size_t)nw + 1) * 4 + 255) & ~(size_t)255;
-    if (c->fixed_ver != c->version || c->fixed_nw != nw || !c->fixed_q.p) {
-      std::vector<char> hb(qb + ib + dr::PL_N * 4, 0);
-      auto *hq = reinterpret_cast<dr::SweepQuery *>(hb.data());
-      auto *hi = reinterpret_cast<int32_t *>(hb.data() + qb);
-      auto *hp = reinterpret_cast<int32_t *>(hb.data() + qb + ib);
-      int nq = 0;
-      int64_t mo = 0;
-      for (int w = 0; w <= nw; w++) hi[w] = -1;
-      for (int w = nw; w >= 1; w--) {
-        const int top = 4 * (w - 1) + 1;
-        if (!c->is_present(top, c->lead_src(w))) continue;
-        dr::SweepQuery q{};
-        q.top = top;
-        q.bottom = 0;
-        q.src0 = c->lead_src(w) - 1;
-        q.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
-        q.mask_off = mo;
-        q.tgt0 = -1;
-        mo += (int64_t)(top + 1) * WS;
-        hi[w] = nq;
-        hq[nq++] = q;
-      }
-      hp[dr::PL_NQD] = nq;
-      HIPCHK(c, c->fixed_q.ensure(hb.size()));
-      HIPCHK(c, hipMemcpyAsync(c->fixed_q.p, hb.data(), hb.size(), hipMemcpyHostToDevice, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      c->fixed_ver = c->version;
-      c->fixed_nw = nw;
-      c->fixed_nq = nq;
-    }
+    HIPCHK(c, c->fixed_q.ensure(qb + ib + dr::PL_N * 4));
     fq = c->fixed_q.as<dr::SweepQuery>();
     fq_idx = reinterpret_cast<int32_t *>(c->fixed_q.as<char>() + qb);
     fq_plan = reinterpret_cast<int32_t *>(c->fixed_q.as<char>() + qb + ib);
+    HIPCHK(c, hipEventRecord(c->ev_start, c->stream));  // stream2 joins the replay's stream order here
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+    hipLaunchKernelGGL((dr::k_fixed_queries<1024>), dim3(1), dim3(1024), 0, c->stream2, c->view(), nw, WS,
+                       dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, fq, fq_idx, fq_plan);
+    HIPCHK(c, hipGetLastError());
+    // the weak unions and speculative canonical digests need only the weak-column
+    // keys and slots, not the rows: launched here, they overlap the row pass
+    if (int rc = ensure_summary_bufs(c)) return rc;
+    HIPCHK(c, launch_weak_union(c, T, c->stream2));
+    HIPCHK(c, hipEventRecord(c->ev_wu, c->stream2));  // k_kcand and the pop sweep wait on it
   }
   // outputs: the emitting sweep's final pass packs them into one device region, which comes back
   // in one copy (writing them straight into pinned host memory from the kernel
@@ -2528,11 +2512,11 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
                        dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave, task_q, cq, cpush_n, push_out, pcap,
                        task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan, fq_idx,
-                       c->fixed_nq);
+                       fq_n);
     HIPCHK(c, hipGetLastError());
     return 0;
   };
-  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false, fixedq)) return rc;
+  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false, fixedq, fixedq)) return rc;
   if (fixedq) dq = fq;
   if (paper) c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
   // 3+4. delivery sweeps (merging with K), then each query's emission
@@ -2575,8 +2559,9 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   dr::SweepQuery probe{};
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
   if (fixedq) {  // the sweeps need only the cone; stream2's chains, pop plan and emission join after them
-    a.nq = c->fixed_nq;
+    a.nq = fq_n;
     a.nq_dev = nullptr;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_wu, 0));  // k_fixed_queries
     HIPCHK(c, c->rec(2));
     HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
@@ -2594,7 +2579,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     em.fin.firstpop = firstpop;
     em.fin.qedges = qedges;
   } else {  // REF: own rounds above the cut; the last workgroup: canonical prefixes G, E
-    HIPCHK(c, launch_own_emit(c, fixedq ? std::max(c->fixed_nq, 1) : nw, fixedq ? fq_plan : plan, dq, dstops, qcount,
+    HIPCHK(c, launch_own_emit(c, fixedq ? std::max(fq_n, 1) : nw, fixedq ? fq_plan : plan, dq, dstops, qcount,
                               qdigest, qcut));
   }
   HIPCHK(c, c->rec(3));
