@@ -15,6 +15,7 @@
 #include <cstring>
 #include <string>
 #include <functional>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -105,10 +106,17 @@ struct dr_ctx {
   // (DR_LEADER_CONST1: 1, the reference's constant), mirrored on the device
   DevBuf lead;
   std::vector<uint16_t> h_lead;
+  // repeated ids (DagView::dup_*): slots after the first of their id, per round
+  DevBuf slot_rep, dup_off, dup_src;
+  std::vector<uint32_t> h_dup_off{0};
+  int64_t ndups = 0;  // repeated slots in rounds >= 1 (round 0 may repeat ids: never read)
   int lead_src(int w) const { return (w >= 0 && w < (int)h_lead.size()) ? h_lead[w] : 1; }
   // host mirror: per-round data, presence [rounds][WS], and the prefix offsets
   // of the flattened device arrays (valid for rounds < up_lo)
   std::vector<HostRound> hr;
+  // per vertex [round][n]: strong degree and weak-edge count of the id's current
+  // vertex (its last slot), so a repeated id can take back the one it replaces
+  std::vector<uint16_t> h_sdeg, h_wcnt;
   dr_host::BuildScratch build_scr;  // dr_append_rounds_packed's per-thread column tables
   std::vector<u64> h_present;
   std::vector<uint32_t> h_slot_off{0}, h_wc_roff{0}, h_far_roff{0}, h_weak_roff{0};
@@ -166,6 +174,9 @@ struct dr_ctx {
   // memo (round summaries + canonical cone): weak deltas up to 65 (WU holds dd = 64
   // slots per round; the merge window is dmax rounds), no far edges
   bool memo_ok() const { return nfar == 0 && dmax_near <= 65; }
+  // round summaries and the canonical cone count vertices per id: a mirror with
+  // repeated ids (dups) takes the full sweeps, which count every slot
+  bool memo_on() const { return use_memo && memo_ok() && ndups == 0; }
   int memo_dd() const { return std::max(0, dmax_near - 1); }
   // scratch
   DevBuf q_buf, masks, dlv, push_out, push_n, edges, wedges, hits, commit, vcount, popdesc, rbase, counts,
@@ -307,6 +318,9 @@ struct dr_ctx {
     v.sdeg = sdeg.as<uint16_t>();
     v.wdeg = wdeg.as<uint16_t>();
     v.lead = lead.as<uint16_t>();
+    v.dup_off = ndups ? dup_off.as<uint32_t>() : nullptr;
+    v.dup_src = ndups ? dup_src.as<uint16_t>() : nullptr;
+    v.slot_rep = ndups ? slot_rep.as<uint8_t>() : nullptr;
     v.n = n;
     v.nrounds = nrounds;
     return v;
@@ -348,6 +362,7 @@ struct dr_ctx {
     const int R = nrounds, lo = up_lo;
     if (lo >= R) { up_lo = R; return hipSuccess; }
     h_slot_off.resize(R + 1);
+    h_dup_off.resize(R + 1);
     h_wc_roff.resize(R + 1);
     h_far_roff.resize(R + 1);
     h_weak_roff.resize(R + 1);
@@ -365,7 +380,39 @@ struct dr_ctx {
     }
     const size_t s0 = h_slot_off[lo], s1 = h_slot_off[R], k0 = h_wc_roff[lo], k1 = h_wc_roff[R];
     const size_t f0 = h_far_roff[lo], f1 = h_far_roff[R];
+    // repeated ids: the slots after the first of their id, per round (rounds >= 1)
+    std::vector<uint8_t> rep;
+    std::vector<uint16_t> dsrc;
+    rep.reserve(s1 - s0);
+    {
+      std::vector<u64> seen(WS);
+      for (int r = lo; r < R; r++) {
+        HostRound &h = hr[r];
+        ndups -= h.ndup;
+        h.ndup = 0;
+        std::fill(seen.begin(), seen.end(), 0ULL);
+        for (uint16_t sl : h.slots) {
+          bool again = false;
+          if (sl != 0 && r >= 1) {
+            const u64 bit = 1ULL << ((sl - 1) & 63);
+            again = (seen[(sl - 1) >> 6] & bit) != 0;
+            seen[(sl - 1) >> 6] |= bit;
+          }
+          rep.push_back(again ? 1 : 0);
+          if (again) {
+            dsrc.push_back(sl);
+            h.ndup++;
+          }
+        }
+        ndups += h.ndup;
+        h_dup_off[r + 1] = h_dup_off[r] + h.ndup;
+      }
+    }
+    const size_t d0 = h_dup_off[lo], d1 = h_dup_off[R];
     hipError_t e;
+    if ((e = slot_rep.grow(s1 + 64, s0, stream)) != hipSuccess) return e;
+    if ((e = dup_src.grow(d1 * 2 + 64, d0 * 2, stream)) != hipSuccess) return e;
+    if ((e = dup_off.grow(((size_t)R + 1) * 4 + 64, ((size_t)lo + 1) * 4, stream)) != hipSuccess) return e;
     if ((e = slot_src.grow(s1 * 2 + 64, s0 * 2, stream)) != hipSuccess) return e;
     if ((e = wc_key.grow(k1 * 4 + 64, k0 * 4, stream)) != hipSuccess) return e;
     if ((e = wc_rows.grow(k1 * WS * 8 + 64, k0 * WS * 8, stream)) != hipSuccess) return e;
@@ -386,6 +433,9 @@ struct dr_ctx {
     }
     const size_t nr = (size_t)(R - lo);
     if ((e = h2d(slot_src.as<uint16_t>() + s0, sl.data(), sl.size() * 2)) != hipSuccess) return e;
+    if ((e = h2d(slot_rep.as<uint8_t>() + s0, rep.data(), rep.size())) != hipSuccess) return e;
+    if (d1 > d0 && (e = h2d(dup_src.as<uint16_t>() + d0, dsrc.data(), dsrc.size() * 2)) != hipSuccess) return e;
+    if ((e = h2d(dup_off.as<uint32_t>() + lo, &h_dup_off[lo], (nr + 1) * 4)) != hipSuccess) return e;
     if ((e = h2d(wc_key.as<uint32_t>() + k0, kk.data(), kk.size() * 4)) != hipSuccess) return e;
     if ((e = h2d(wc_rows.as<u64>() + k0 * WS, rows.data(), rows.size() * 8)) != hipSuccess) return e;
     if ((e = h2d(far.as<u64>() + f0, ff.data(), ff.size() * 8)) != hipSuccess) return e;
@@ -911,6 +961,8 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   HIPCHK(c, c->h2d(c->sdeg.as<uint16_t>() + (size_t)r0 * n, built.sdeg.data(), built.sdeg.size() * 2));
   HIPCHK(c, c->h2d(c->wdeg.as<uint16_t>() + (size_t)r0 * n, built.wdeg.data(), built.wdeg.size() * 2));
   for (auto &h : nh) c->hr.push_back(std::move(h));
+  c->h_sdeg.insert(c->h_sdeg.end(), built.sdeg.begin(), built.sdeg.end());
+  c->h_wcnt.insert(c->h_wcnt.end(), built.wdeg.begin(), built.wdeg.end());
   c->h_present.insert(c->h_present.end(), built.pres.begin(), built.pres.end());
   c->nfar += nfar;
   c->dmax_near = dmax;
@@ -933,7 +985,6 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
   // pass 1: validate every vertex against the mirror plus the vertices before it
   // in this call; nothing changes unless all of them are inside the contract
   int R = R0;
-  std::unordered_set<uint64_t> added;
   for (int i = 0; i < k; i++) {
     const int vr = ids[2 * i], vs = ids[2 * i + 1];
     const int r = slot_round ? slot_round[i] : vr;
@@ -952,8 +1003,6 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
     }
     if (vr != r || vs < 1 || vs > n)
       return c->fail(DR_E_CONTRACT, "p.dag[%d]: id (%d,%d) outside the mirrored contract", r, vr, vs);
-    if (r >= 1 && ((r < R0 && c->is_present(r, vs)) || !added.insert(((uint64_t)r << 32) | (uint32_t)vs).second))
-      return c->fail(DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, vs);
     if (r == 0 && sb > sa) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", vs);
     for (uint32_t e = sa; e < sb; e++) {
       const int tr = strong_ids[2 * e], ts = strong_ids[2 * e + 1];
@@ -975,11 +1024,14 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
     HIPCHK(c, hipMemsetAsync(c->wdeg.as<uint16_t>() + a, 0, (b - a) * 2, c->stream));
     c->hr.resize(R);
     c->h_present.resize((size_t)R * WS, 0);
+    c->h_sdeg.resize((size_t)R * n, 0);
+    c->h_wcnt.resize((size_t)R * n, 0);
     c->nrounds = R;
   }
   std::vector<u64> rows((size_t)k * WS, 0);
   std::vector<uint32_t> vidx(k);
   std::vector<uint16_t> sd(k), wd(k);
+  std::unordered_map<uint32_t, int> put_at;  // vertex index -> its entry (a repeated id rewrites it)
   int nv = 0, dmax = c->dmax_near;
   for (int i = 0; i < k; i++) {
     const int vr = ids[2 * i], vs = ids[2 * i + 1];
@@ -991,8 +1043,33 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
       continue;
     }
     h.slots.push_back((uint16_t)vs);
-    c->h_present[(size_t)r * WS + ((vs - 1) >> 6)] |= 1ULL << ((vs - 1) & 63);
-    u64 *row = &rows[(size_t)nv * WS];
+    const size_t vi = (size_t)r * n + vs - 1;
+    u64 &pw = c->h_present[(size_t)r * WS + ((vs - 1) >> 6)];
+    const u64 pbit = 1ULL << ((vs - 1) & 63);
+    if (pw & pbit) {  // the id is already in the round: this vertex replaces it for path()'s
+      // lookup (the last slot, process.go:112-116): take back its degree and weak edges
+      h.deg -= c->h_sdeg[vi];
+      h.nweak -= c->h_wcnt[vi];
+      const int o = vs - 1;
+      for (size_t j = 0; j < h.wc_key.size();) {
+        uint64_t *wr = &h.wc_rows[j * WS];
+        wr[o >> 6] &= ~(1ULL << (o & 63));
+        bool any = false;
+        for (int w = 0; w < WS; w++) any |= wr[w] != 0ULL;
+        if (any) { j++; continue; }
+        h.wc_key.erase(h.wc_key.begin() + (ptrdiff_t)j);
+        h.wc_rows.erase(h.wc_rows.begin() + (ptrdiff_t)(j * WS), h.wc_rows.begin() + (ptrdiff_t)((j + 1) * WS));
+      }
+      const size_t nf = h.far.size();
+      h.far.erase(std::remove_if(h.far.begin(), h.far.end(), [&](uint64_t x) { return (int)(x >> 32) == o; }),
+                  h.far.end());
+      c->nfar -= nf - h.far.size();
+    }
+    pw |= pbit;
+    auto pa = put_at.find((uint32_t)vi);
+    const int slot_nv = pa == put_at.end() ? nv : pa->second;
+    u64 *row = &rows[(size_t)slot_nv * WS];
+    std::fill(row, row + WS, 0ULL);
     for (uint32_t e = strong_off[i]; e < strong_off[i + 1]; e++) {
       const int ts = strong_ids[2 * e + 1] - 1;
       row[ts >> 6] |= 1ULL << (ts & 63);
@@ -1012,10 +1089,12 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
       }
     }
     h.nweak += wb - wa;
-    vidx[nv] = (uint32_t)((size_t)r * n + vs - 1);
-    sd[nv] = (uint16_t)d;
-    wd[nv] = (uint16_t)std::min<uint32_t>(wb - wa, 65535u);
-    nv++;
+    c->h_sdeg[vi] = (uint16_t)d;
+    c->h_wcnt[vi] = (uint16_t)std::min<uint32_t>(wb - wa, 65535u);
+    vidx[slot_nv] = (uint32_t)vi;
+    sd[slot_nv] = (uint16_t)d;
+    wd[slot_nv] = (uint16_t)std::min<uint32_t>(wb - wa, 65535u);
+    if (pa == put_at.end()) put_at.emplace((uint32_t)vi, nv++);
   }
   c->dmax_near = dmax;
   if (nv) {
@@ -1069,6 +1148,10 @@ extern "C" int dr_append_rounds_lists(dr_ctx *c, int r0, int k, const uint32_t *
         return c->fail(DR_E_CONTRACT, "round %d slot %u: id (%d,%d) outside the mirrored contract", r, sl - slot_off[i], vr, vs);
       src[sl - S0] = (uint16_t)vs;
       uint64_t *row = &rows[((size_t)i * n + (vs - 1)) * W];
+      // a repeated id: path()'s lookup takes the last slot (process.go:112-116), so
+      // its edges replace the earlier slot's
+      std::fill(row, row + W, 0ULL);
+      wl[(size_t)i * n + (vs - 1)].clear();
       for (uint32_t e = sa; e < sb; e++) {
         const int tr = strong_ids[2 * e], ts = strong_ids[2 * e + 1];
         if (tr != r - 1 || ts < 1 || ts > n)
@@ -1076,7 +1159,6 @@ extern "C" int dr_append_rounds_lists(dr_ctx *c, int r0, int k, const uint32_t *
         row[(ts - 1) >> 6] |= 1ULL << ((ts - 1) & 63);
       }
       std::vector<uint32_t> &L = wl[(size_t)i * n + (vs - 1)];
-      if (!L.empty() || (wb > wa && false)) {}
       for (uint32_t e = wa; e < wb; e++) {
         const int tr = weak_ids[2 * e], ts = weak_ids[2 * e + 1];
         if (tr < 0 || tr > r - 2 || ts < 1 || ts > n)
@@ -1289,7 +1371,7 @@ void mark_rounds_clean(dr_ctx *c) {
 // since they were last built: one workgroup per stale round.  A DAG that left
 // the memo contract (far weak edges, deltas > 65) keeps none.
 int refresh_rounds(dr_ctx *c) {
-  if (!(c->use_memo && c->memo_ok())) return DR_OK;
+  if (!(c->memo_on())) return DR_OK;
   const int T = c->nrounds - 1;
   if (T < 1) return DR_OK;
   const int dd = c->memo_dd();
@@ -1397,7 +1479,7 @@ int fetch_canon(dr_ctx *c) {
 // Bring the round summaries and the canonical cone up to date with the DAG
 // (the per-call path: only stale rounds are re-read).
 int refresh_canon(dr_ctx *c) {
-  if (!(c->use_memo && c->memo_ok()) || c->nrounds < 2) return DR_OK;
+  if (!(c->memo_on()) || c->nrounds < 2) return DR_OK;
   if (int rc = refresh_rounds(c)) return rc;
   if (!c->canon_ok) {
     if (int rc = ensure_summary_bufs(c)) return rc;
@@ -1459,7 +1541,7 @@ namespace {
 // Round summaries usable for this context's current DAG (Q_SHORTCUT), and the
 // canonical cone too (Q_MERGE).
 bool rounds_fresh(const dr_ctx *c) {
-  return c->use_memo && c->memo_ok() && c->ndirty == 0 && c->sum_dd == c->memo_dd() && c->nrounds >= 2;
+  return c->memo_on() && c->ndirty == 0 && c->sum_dd == c->memo_dd() && c->nrounds >= 2;
 }
 bool summary_fresh(const dr_ctx *c) { return rounds_fresh(c) && c->canon_ok && c->canon_T == c->nrounds - 1; }
 int shortcut_flag(const dr_ctx *c) { return rounds_fresh(c) ? dr::Q_SHORTCUT : 0; }
@@ -1911,6 +1993,7 @@ int run_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *pco
             d.last = last;
             d.out = (int32_t)t;
             d.use_k = 0;
+            d.flags = paper ? dr::PD_FIRST_ONLY : 0;  // PAPER dedups by id (Alg. 3 line 54)
             pd.push_back(d);
           }
         }
@@ -2651,14 +2734,14 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;
   o->canon_segments = -1;
-  if (c->plan_mode != 0 && c->use_memo && c->memo_ok() && !(o->ids && o->ids_cap > 0) && o->push_wave &&
+  if (c->plan_mode != 0 && c->memo_on() && !(o->ids && o->ids_cap > 0) && o->push_wave &&
       o->pop_count && o->pop_digest) {
     const int rc = replay_planned(c, nwaves, chain_mode, deliver_mode == DR_DELIVER_PAPER, o);
     if (rc != 1) return rc;
   }
   // 0+1. round summaries + canonical cone, fused with the commit decisions of
   // every wave (one pass over the DAG per replay); without summaries, k_commit
-  if (c->use_memo && c->memo_ok()) {
+  if (c->memo_on()) {
     if (int rc = build_summary(c, &o->ms_summary, nwaves, o->commit, o->vcount)) return rc;
     o->canon_segments = c->canon_segments;
   } else if (int rc = commit_range(c, 1, nwaves, o->commit, o->vcount, &o->ms_commit)) {
@@ -2724,7 +2807,7 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
 namespace {
 // the fused small-DAG path (batch.hpp) covers this context's DAG
 bool small_ok(const dr_ctx *c, int nwaves) {
-  return c->n <= 128 && nwaves <= 64 && c->nfar == 0 && c->dmax_near < 32;
+  return c->n <= 128 && nwaves <= 64 && c->nfar == 0 && c->dmax_near < 32 && c->ndups == 0;
 }
 
 template <int DEPTH>

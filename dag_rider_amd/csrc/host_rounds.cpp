@@ -41,7 +41,10 @@ struct Chunk {
   std::vector<uint64_t> far;
 };
 
-// The slot pass of round i (insertion order, presence, duplicate ids).
+// The slot pass of round i (insertion order, presence).  An id may repeat (the
+// reference appends whatever uponDeliver / the buffer loop hands it,
+// process.go:158-169, :229): every slot stays, the packed row is the id's one
+// vertex as path()'s lookup sees it (its last slot, :112-116).
 int build_slots(const PackedRounds &in, int i, BuiltRounds &out, std::string &err) {
   const int n = in.n, r = in.r0 + i;
   uint64_t *P = &out.pres[(size_t)i * in.WS];
@@ -52,10 +55,7 @@ int build_slots(const PackedRounds &in, int i, BuiltRounds &out, std::string &er
     if (s > n) return failf(err, DR_E_CONTRACT, "round %d slot %u: source %d > n=%d", r, sl - in.slot_off[i], s, n);
     h.slots.push_back((uint16_t)s);
     if (s == 0) continue;  // ghost slot {0,0}
-    uint64_t &wd = P[(s - 1) >> 6];
-    const uint64_t bit = 1ULL << ((s - 1) & 63);
-    if ((wd & bit) && r >= 1) return failf(err, DR_E_CONTRACT, "round %d: duplicate vertex id (%d,%d)", r, r, s);
-    wd |= bit;
+    P[(s - 1) >> 6] |= 1ULL << ((s - 1) & 63);
   }
   return 0;
 }

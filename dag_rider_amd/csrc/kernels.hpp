@@ -77,9 +77,33 @@ struct DagView {
   const uint16_t *sdeg;  // [rounds][n] strong degree per vertex
   const uint16_t *wdeg;  // [rounds][n] weak degree per vertex (far edges included)
   const uint16_t *lead;  // [wave] chooseLeader(w) (process.go:386-392), 1-based source
+  // repeated ids (uponDeliver / the buffer loop append an id already in the
+  // round, process.go:158-169, :229): null when the mirror has none.  dup_src
+  // lists the source of every slot after the first of its id, per round
+  // (dup_off[r] .. dup_off[r+1]); slot_rep[slot] = 1 for those slots.  Edges
+  // come from the id's last slot (path's lookup, :112-116); vCount and REF
+  // delivery count every slot (:332, :418-429).
+  const uint32_t *dup_off;
+  const uint16_t *dup_src;
+  const uint8_t *slot_rep;
   int32_t n;
   int32_t nrounds;
 };
+
+// repeated slots of round r whose source is in the set X (lane w < WS holds word
+// w of X; every lane of the wave calls it and gets the count)
+template <int WS>
+__device__ __forceinline__ int dup_count(const DagView &g, int r, u64 xw) {
+  if (!g.dup_off) return 0;
+  const uint32_t a = g.dup_off[r], b = g.dup_off[r + 1];
+  int c = 0;
+  for (uint32_t j = a; j < b; j++) {  // wave-uniform
+    const int s = (int)g.dup_src[j] - 1;
+    const u64 w = __shfl(xw, (s >> 6) & (WS - 1));
+    c += (int)((w >> (s & 63)) & 1ULL);
+  }
+  return c;
+}
 
 // OR over the lanes of a row with equal (lane mod C), C a power of two < 16:
 // afterwards lane l of every row holds the OR of its row's class l mod C.
@@ -185,12 +209,15 @@ __global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int qu
     if (tid < WS) { S[tid] = T[tid]; T[tid] = 0; }
     __syncthreads();
   }
-  if (tid == 0) {
-    int vc = 0;
+  if (wid == 0) {  // vCount counts slots (process.go:330-335): repeated ids once per slot
+    const int dc = dup_count<WS>(g, r1 + 3, lane < WS ? S[lane] : 0ULL);
+    if (tid == 0) {
+      int vc = dc;
 #pragma unroll
-    for (int i = 0; i < WS; i++) vc += popc64(S[i]);
-    vcount[bi] = vc;
-    commit[bi] = vc >= quorum ? 1 : 0;
+      for (int i = 0; i < WS; i++) vc += popc64(S[i]);
+      vcount[bi] = vc;
+      commit[bi] = vc >= quorum ? 1 : 0;
+    }
   }
 }
 
@@ -1496,7 +1523,9 @@ struct PopDesc {
   int32_t first, last;
   int32_t out;        // pop index (count / digest / ids slot)
   int32_t use_k;      // mask image: 0 = masks, 1 = canonical K
+  int32_t flags;      // PD_FIRST_ONLY: a repeated id is delivered at its first slot only (PAPER)
 };
+enum : int32_t { PD_FIRST_ONLY = 1 };
 
 // part 1: one workgroup per segment: c_r = |mask_r & present_r|, exclusive scan
 // over the segment's rounds -> rbase, total -> count[seg]
@@ -1513,12 +1542,23 @@ __global__ __launch_bounds__(NT) void k_emit_count(DagView g, const PopDesc *__r
   const int nr = d.last - d.first + 1;
   const int per = nr > 0 ? (nr + NT - 1) / NT : 0;
   const int ra = d.first + tid * per, rb = min(d.last + 1, ra + per);
+  // repeated ids: every slot counts in REF, the first slot only in PAPER
+  const bool reps = g.dup_off && !(d.flags & PD_FIRST_ONLY);
+  auto rep_cnt = [&](int r, const u64 *m) -> uint32_t {
+    uint32_t c = 0;
+    for (uint32_t j = g.dup_off[r]; j < g.dup_off[r + 1]; j++) {
+      const int s = (int)g.dup_src[j] - 1;
+      c += (uint32_t)((m[s >> 6] >> (s & 63)) & 1ULL);
+    }
+    return c;
+  };
   uint32_t loc = 0;
   for (int r = ra; r < rb; r++) {
     const u64 *m = img + (int64_t)r * WS;
     const u64 *p = g.present + (size_t)r * WS;
 #pragma unroll
     for (int w = 0; w < WS; w++) loc += popc64(m[w] & p[w]);
+    if (reps) loc += rep_cnt(r, m);
   }
   part[tid] = loc;
   __syncthreads();
@@ -1536,6 +1576,7 @@ __global__ __launch_bounds__(NT) void k_emit_count(DagView g, const PopDesc *__r
     uint32_t c = 0;
 #pragma unroll
     for (int w = 0; w < WS; w++) c += popc64(m[w] & p[w]);
+    if (reps) c += rep_cnt(r, m);
     run += c;
   }
   if (tid == NT - 1) count[blockIdx.x] = nr > 0 ? part[NT - 1] : 0;
@@ -1585,6 +1626,10 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
       int src[SPL];
 #pragma unroll
       for (int j = 0; j < SPL; j++) src[j] = i0 + j < sb ? (int)slot_src[i0 + j] : 0;
+      if (g.slot_rep && (d.flags & PD_FIRST_ONLY))  // PAPER: a repeated id's later slots deliver nothing
+#pragma unroll
+        for (int j = 0; j < SPL; j++)
+          if (i0 + j < sb && g.slot_rep[i0 + j]) src[j] = 0;
       uint32_t bits = 0;
 #pragma unroll
       for (int j = 0; j < SPL; j++) {

@@ -264,24 +264,12 @@ class Process {
     preds.push_back(0);
     std::vector<uint8_t> admit(buffer.size());
     check(dr_buffer_admit(ctx_, round, (int)buffer.size(), ids.data(), off.data(), preds.data(), admit.data()));
-    // validate every admission before anything moves (Go replaces p.buffer only
-    // after the loop): p.dag[r] in range, and an id the mirror can hold -- Go
-    // would append a second vertex with an id already in the round (path() then
-    // sees the last one), which is outside the mirrored contract
-    std::vector<std::pair<int, int>> seen;
-    for (size_t i = 0; i < buffer.size(); i++) {
-      if (!admit[i]) continue;
-      const vertexID id = buffer[i].id;
-      if (id.round >= (int)dag.size()) throw panic_error("runtime error: index out of range");  // p.dag[r]
-      if (id.round == 0) continue;  // round 0 may repeat ids (genesis)
-      bool dup = std::find(seen.begin(), seen.end(), std::make_pair(id.round, id.source)) != seen.end();
-      for (const vertex &u : dag[id.round]) dup |= u.id == id;
-      if (dup)
-        throw std::runtime_error("dagrider: buffered vertex (" + std::to_string(id.round) + "," +
-                                 std::to_string(id.source) + ") duplicates an id in p.dag[" +
-                                 std::to_string(id.round) + "] (outside the mirrored contract)");
-      seen.emplace_back(id.round, id.source);
-    }
+    // every admission's p.dag[r] must exist before anything moves (Go replaces
+    // p.buffer only after the loop).  A vertex whose id is already in the round is
+    // appended as Go does (path() then sees the last one, process.go:112-116).
+    for (size_t i = 0; i < buffer.size(); i++)
+      if (admit[i] && buffer[i].id.round >= (int)dag.size())
+        throw panic_error("runtime error: index out of range");  // p.dag[r]
     std::vector<vertex> next;
     for (size_t i = 0; i < buffer.size(); i++) {
       if (admit[i]) dag.append(buffer[i].id.round, std::move(buffer[i]));

@@ -97,11 +97,16 @@ int dr_set_option(dr_ctx *ctx, int option, int value);
  *   slot_id    [2*S]   vertex id per slot, in insertion order
  *   strong_off [S+1], strong_ids [2*E]   strongEdges per slot
  *   weak_off   [S+1], weak_ids   [2*E']  weakEdges per slot
- * Contract (else DR_E_CONTRACT): a slot's id is (r, s), 1 <= s <= n, unique in
- * its round (round 0 may repeat ids), or the zero id {0,0} with no edges (the
- * Figure-1 ghost slot, process_internal_test.go:91); strong edges target
- * (r-1, t), weak edges (r', t) with r' < r-1; 1 <= t <= n.  Targets need not
- * exist (a dangling target counts as reached, process.go:123,136). */
+ * Contract (else DR_E_CONTRACT): a slot's id is (r, s), 1 <= s <= n, or the
+ * zero id {0,0} with no edges (the Figure-1 ghost slot,
+ * process_internal_test.go:91); strong edges target (r-1, t), weak edges
+ * (r', t) with r' < r-1; 1 <= t <= n.  Targets need not exist (a dangling
+ * target counts as reached, process.go:123,136).  An id may repeat within a
+ * round, as uponDeliver and the buffer loop let it (process.go:158-169, :229):
+ * every slot is kept, path() sees the id's LAST slot (:112-116), vCount and
+ * REF delivery count every slot (:332, :418-429), PAPER delivers an id once,
+ * at its first slot; edge totals count an id's edges once (its last slot).
+ * Such a mirror replays on the full sweeps (DR_OPT_MEMO does not apply). */
 int dr_append_rounds_lists(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off,
                            const int32_t *slot_id, const uint32_t *strong_off,
                            const int32_t *strong_ids, const uint32_t *weak_off,
@@ -124,8 +129,8 @@ int dr_append_rounds_packed(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off
  * larger r_i: DR_E_INVAL, Go's index out of range).  Its slot follows the
  * round's existing slots.  ids[2i], ids[2i+1] = (round, source); strong edges
  * strong_ids[2e..] for e in [strong_off[i], strong_off[i+1]), weak likewise.
- * Same contract as dr_append_rounds_lists (else DR_E_CONTRACT): id (r_i, s)
- * unique in its round, or the ghost {0,0} with no edges.  All or nothing: on
+ * Same contract as dr_append_rounds_lists (else DR_E_CONTRACT); a vertex whose
+ * id is already in the round becomes the one path() sees (the last slot).  All or nothing: on
  * any error the mirror is unchanged.  Only the rounds touched are re-read when
  * round summaries or the canonical cone are next needed. */
 int dr_append_vertices(dr_ctx *ctx, int k, const int32_t *slot_round, const int32_t *ids,

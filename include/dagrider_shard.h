@@ -59,7 +59,8 @@ int dr_shard_info(const dr_shard *ctx, int *nshards, int *shard0, int *nlocal, i
 
 /* p.dag[r] = append(...) (process.go:229): dr_append_rounds_packed's arguments and
  * contract; the context keeps only its columns.  Weak edges must satisfy
- * r - r' <= 1023 (else DR_E_CONTRACT). */
+ * r - r' <= 1023, and an id may not repeat within a round >= 1 (else
+ * DR_E_CONTRACT; repeated ids replay on the unsharded engine). */
 int dr_shard_append_rounds_packed(dr_shard *ctx, int r0, int k, const uint32_t *slot_off, const uint16_t *slot_src,
                                   const uint64_t *strong, const uint32_t *weak_off, const uint32_t *weak_tgt);
 

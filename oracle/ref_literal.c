@@ -199,6 +199,23 @@ static uint64_t slot_degree(const or_ldag *d, uint32_t i) {
   return (uint64_t)(d->strong_off[i + 1] - d->strong_off[i]) + (d->weak_off[i + 1] - d->weak_off[i]);
 }
 
+/* Repeated ids in a round (uponDeliver / the buffer loop append whatever they are
+ * handed, process.go:158-169, :229).  The edge totals (this
+ * repo's metric) count an id's edges once, those of the vertex path()'s lookup
+ * finds: its LAST slot (:112-116).  slot_first: slot i is its id's first slot in
+ * round r; slot_last: the id's last slot. */
+static int slot_first(const or_ldag *d, int r, uint32_t i) {
+  for (uint32_t j = d->slot_off[r]; j < i; j++)
+    if (vid_eq(d->slot_id[j], d->slot_id[i])) return 0;
+  return 1;
+}
+static uint32_t slot_last(const or_ldag *d, int r, uint32_t i) {
+  uint32_t last = i;
+  for (uint32_t j = i + 1; j < d->slot_off[r + 1]; j++)
+    if (vid_eq(d->slot_id[j], d->slot_id[i])) last = j;
+  return last;
+}
+
 /* process.go:404-443 orderVertices.  One pop per stack entry, top first.
  * mode REF: the delivered filter is a no-op (Q2, :423-427), so each pop
  * delivers its full causal history in rounds 1..cur_round.  mode PAPER:
@@ -234,7 +251,7 @@ static int order_pop(const or_ldag *d, or_vid popped, int cur_round, int mode, h
       if (out && *out_n < out_cap) out[*out_n] = t;
       (*out_n)++;
       dg += or_digest_term(t.round, t.source, k);
-      ed += slot_degree(d, i);
+      if (slot_first(d, r, i)) ed += slot_degree(d, slot_last(d, r, i)); /* an id's edges once */
       k++;
     }
   }
@@ -294,8 +311,11 @@ int or_lit_replay_mt(const or_ldag *d, int faulty, int nwaves, int chain_mode, i
     o->push_off[w - 1] = (uint32_t)npush;
     if (vc >= 0) { /* leader present: the voter loop examined rounds 4w-2..4w */
       for (int r = wave_round(w, 2); r <= wave_round(w, 4); r++)
-        for (uint32_t i = d->slot_off[r]; i < d->slot_off[r + 1]; i++)
-          o->commit_edges += d->strong_off[i + 1] - d->strong_off[i];
+        for (uint32_t i = d->slot_off[r]; i < d->slot_off[r + 1]; i++) {
+          if (!slot_first(d, r, i)) continue; /* an id's row once: its last slot's */
+          const uint32_t j = slot_last(d, r, i);
+          o->commit_edges += d->strong_off[j + 1] - d->strong_off[j];
+        }
     }
     if (!c) continue;
     if (npush + slen > o->push_cap) { rc = OR_PANIC; break; }

@@ -263,16 +263,16 @@ int main() {
   try { p->getWaveVertexLeader(0); } catch (const panic_error &) { panicked = true; }
   REQUIRE(panicked, "getWaveVertexLeader(0)/panics");
 
-  // a duplicate admission is rejected before anything moves: buffer and dag intact
+  // a re-delivered id is appended as Go appends it (process.go:229): p.dag[3] grows
+  // by one slot and path() follows the id's LAST vertex (process.go:112-116)
   {
     p->round = 4;
     const size_t b0 = p->buffer.size(), d3 = p->dag[3].size();
+    REQUIRE(p->path({3, 2}, {2, 2}, true), "processBuffer/before-redelivery");
     p->buffer.push_back(vertex{{3, 2}, {}, E({{2, 1}}), {}});  // (3,2) is already in p.dag[3]
-    bool threw = false;
-    try { p->processBuffer(); } catch (const std::runtime_error &) { threw = true; }
-    REQUIRE(threw && p->buffer.size() == b0 + 1 && p->dag[3].size() == d3 && p->buffer.back().strongEdges.size() == 1,
-            "processBuffer/duplicate-id-rejected-intact");
-    p->buffer.pop_back();
+    p->processBuffer();
+    REQUIRE(p->buffer.size() == b0 && p->dag[3].size() == d3 + 1, "processBuffer/redelivered-appended");
+    REQUIRE(!p->path({3, 2}, {2, 2}, true) && p->path({3, 2}, {2, 1}, true), "path/last-match-after-redelivery");
     REQUIRE(p->path({4, 1}, {2, 4}, false), "processBuffer/mirror-still-usable");
   }
 

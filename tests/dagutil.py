@@ -102,3 +102,27 @@ def load_large():
 
     with gzip.open(os.path.join(GOLDEN, "large_replay.json.gz"), "rt") as f:
         return json.load(f)
+
+
+def with_repeated_ids(rng: np.random.Generator, dag, p_dup=0.3, max_extra=2):
+    """A [][]vertex where some ids of rounds >= 1 repeat in their round, as the
+    reference's uponDeliver / buffer loop append them (process/process.go:158-169,
+    :229): each repeat is a separate slot at a random position, with its own random
+    strong edges (to round r-1) and weak edges (below r-1).  path() follows an id's
+    LAST slot (:112-116); vCount and REF delivery count every slot."""
+    out = [list(r) for r in dag]
+    for r in range(1, len(out)):
+        ids = [v.id for v in out[r] if v.id != VertexID(0, 0)]
+        if not ids:
+            continue
+        prev = [v.id for v in out[r - 1] if v.id != VertexID(0, 0)]
+        below = [v.id for rr in range(max(0, r - 6), r - 1) for v in out[rr] if v.id != VertexID(0, 0)]
+        for vid in ids:
+            if rng.random() >= p_dup:
+                continue
+            for _ in range(int(rng.integers(1, max_extra + 1))):
+                st = [u for u in prev if rng.random() < 0.6]
+                wk = [u for u in below if rng.random() < 0.1]
+                pos = int(rng.integers(0, len(out[r]) + 1))
+                out[r].insert(pos, Vertex(vid, b"", st, wk))
+    return out

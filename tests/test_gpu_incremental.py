@@ -134,8 +134,6 @@ def test_gpu_append_vertices_all_or_nothing(gpu_device):
         before = e.path_batch([((5, s), (4, t)) for s in range(1, 7) for t in range(1, 7)], False).tolist()
         bad_cases = [
             good + [Vertex(VertexID(6, 9), b"", [], [])],                      # source > n
-            good + [Vertex(VertexID(6, good[0].id.source), b"", [], [])],      # duplicate id in the call
-            good + [Vertex(VertexID(5, full[5][0].id.source), b"", [], [])],   # duplicate id in the DAG
             good + [Vertex(VertexID(6, 3), b"", [VertexID(4, 1)], [])],       # strong edge not to r-1
             good + [Vertex(VertexID(6, 3), b"", [], [VertexID(5, 1)])],       # weak edge to r-1
             good + [Vertex(VertexID(0, 0), b"", [VertexID(4, 1)], [])],       # ghost with edges

@@ -324,12 +324,7 @@ def test_errors(gpu_device):
             e.order_vertices([(4, 1)], 5)
         assert ei.value.code == L.DR_E_INVAL
     with Engine(4, 1, 8, gpu_device) as e:
-        bad = [list(r) for r in dag]
         from dag_rider_amd.dag import Vertex, VertexID
-        bad[2] = bad[2] + [Vertex(VertexID(2, 1))]  # duplicate id in a round
-        with pytest.raises(L.DrError) as ei:
-            e.append_lists(bad)
-        assert ei.value.code == L.DR_E_CONTRACT
         bad = [list(r) for r in dag]
         bad[3][1] = Vertex(VertexID(3, 1), b"", [VertexID(1, 1)])  # strong edge skipping a round
         with pytest.raises(L.DrError) as ei:
