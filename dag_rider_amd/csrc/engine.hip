@@ -126,7 +126,6 @@ struct dr_ctx {
   // and its prefixes (K, C, G, E) describe the DAG as of the last canon build
   bool use_memo = true;
   uint64_t version = 0;  // bumped by every change of the DAG or the leader coin
-  DevBuf fixed_q;  // replay_planned's delivery queries (k_fixed_queries)
   std::vector<uint8_t> sdirty;
   int sum_dd = -1;            // WU layout the summaries were built with (memo_dd())
   bool canon_ok = false;      // K/C/G/E describe the current DAG
@@ -191,7 +190,7 @@ struct dr_ctx {
   struct Pending { void *dst; void *stage; const void *src; size_t n; };
   std::vector<Pending> pend;
   hipEvent_t ev_sync = nullptr, ev_sync2 = nullptr, ev_fork = nullptr, ev_join = nullptr, ev_start = nullptr,
-            ev_wu = nullptr, ev_canon = nullptr;
+            ev_wu = nullptr;
   hipStream_t stream2 = nullptr;  // second queue: canonical cone beside the leader chains
   hipError_t launch_copies(const dr::CopySeg *sg, int k) {
     for (int i0 = 0; i0 < k; i0 += dr::kCopySegs) {
@@ -818,7 +817,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   // per record.  ev_sync / ev_sync2 order the kernels' writes to pinned host
   // memory before the host reads them, so they keep the system fence.
   for (auto &ev : c->ev) (void)hipEventCreateWithFlags(&ev, hipEventReleaseToDevice);
-  for (hipEvent_t *e : {&c->ev_fork, &c->ev_join, &c->ev_start, &c->ev_wu, &c->ev_canon})
+  for (hipEvent_t *e : {&c->ev_fork, &c->ev_join, &c->ev_start, &c->ev_wu})
     (void)hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice);
   for (hipEvent_t *e : {&c->ev_sync, &c->ev_sync2}) (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
   const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64);
@@ -868,7 +867,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
-  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join, c->ev_start, c->ev_wu, c->ev_canon})
+  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join, c->ev_start, c->ev_wu})
     if (e) (void)hipEventDestroy(e);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1399,7 +1398,7 @@ int refresh_rounds(dr_ctx *c) {
 // prefix = false: the caller's emitting sweep computes the G, E prefixes.
 // spec: RG holds every round's speculative digest (build_summary's weak union).
 int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool forked = false,
-                 bool incremental = false, bool prefix = true, bool spec_rg = false, bool emit_side = false) {
+                 bool incremental = false, bool prefix = true, bool spec_rg = false) {
   const int T = c->nrounds - 1;
   // incremental (the per-call path): rounds below the lowest one that changed
   // since the last cone, and whose canonical vertices are unchanged, keep their
@@ -1417,24 +1416,16 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
   }
-  emit_side = emit_side && fork && side;
   if (fork && side) {
     Swap sw(c, true);
     if (int rc = (*side)()) return rc;
-    if (!emit_side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
+    HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   }
   Swap sw(c, fork && !side);
   // canonical cone, per-round counts and positions (k_kcand + k_canon), then the
   // per-round digests (emission) and their prefixes
   const bool spec = spec_rg && lo <= 1;  // a full cone: re-emission from the first non-full round
   HIPCHK(c, launch_canon_cone(c, T, lo, spec));  // *rlo = the lowest round to re-emit
-  // emit_side: the canonical emission joins stream2's work (side), so the delivery
-  // sweeps can start on the main stream right after the cone; ev_join marks both
-  Swap sw2(c, emit_side);
-  if (emit_side) {
-    HIPCHK(c, hipEventRecord(c->ev_canon, c->stream2));  // c->stream2 is the main stream here
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_canon, 0));
-  }
   dr::PopDesc d{};
   d.mask_off = 0;
   d.rbase_off = 1;  // crbase is indexed by round; rbase_off addresses round `first`
@@ -1450,7 +1441,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
     hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
                        c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
-  if ((fork && !side) || emit_side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
+  if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   c->kprev_ok = true;
   c->canon_dd = c->memo_dd();
   c->canon_lo = INT_MAX;
@@ -1494,7 +1485,7 @@ int refresh_canon(dr_ctx *c) {
 // re-reads the whole DAG; nothing carries over from earlier calls.
 int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
                   bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr,
-                  bool prefix = true, bool emit_side = false, bool wu_side = false) {
+                  bool prefix = true) {
   const int T = c->nrounds - 1;
   if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
   if (int rc = ensure_summary_bufs(c)) return rc;
@@ -1516,12 +1507,9 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
       HIPCHK(c, hipEventRecord(fe, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, fe, 0));
   }
-  if (wu_side)  // the caller launched the weak unions on stream2 before the row pass (ev_wu marks them)
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_wu, 0));
-  else
-    HIPCHK(c, launch_weak_union(c, T, c->stream));
+  HIPCHK(c, launch_weak_union(c, T, c->stream));
   mark_rounds_clean(c);
-  if (int rc = launch_canon(c, fork, side, early, false, prefix, true, emit_side)) return rc;
+  if (int rc = launch_canon(c, fork, side, early, false, prefix, true)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
   if (nwc > 0) {
     HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nwc));
@@ -2519,35 +2507,6 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     }
   }
   HIPCHK(c, c->masks.ensure(mask_words * 8));
-  // REF: the delivery queries are fixed before the chains run -- one per wave whose
-  // leader is present, highest round first (a superset of the leaders any push can
-  // pop; a REF pop depends only on its leader) -- so the delivery sweeps need only
-  // the canonical cone.  Built on the device by every replay (k_fixed_queries, on
-  // stream2 beside the summary pass); the sweep's grid is the present-leader count,
-  // known on the host from the mirror's presence bits.
-  const bool fixedq = !paper;
-  dr::SweepQuery *fq = nullptr;
-  int32_t *fq_idx = nullptr, *fq_plan = nullptr;
-  int fq_n = 0;
-  if (fixedq) {
-    for (int w = 1; w <= nw; w++) fq_n += c->is_present(4 * (w - 1) + 1, c->lead_src(w)) ? 1 : 0;
-    const size_t qb = ((size_t)nw * sizeof(dr::SweepQuery) + 255) & ~(size_t)255;
-    const size_t ib = (((size_t)nw + 1) * 4 + 255) & ~(size_t)255;
-    HIPCHK(c, c->fixed_q.ensure(qb + ib + dr::PL_N * 4));
-    fq = c->fixed_q.as<dr::SweepQuery>();
-    fq_idx = reinterpret_cast<int32_t *>(c->fixed_q.as<char>() + qb);
-    fq_plan = reinterpret_cast<int32_t *>(c->fixed_q.as<char>() + qb + ib);
-    HIPCHK(c, hipEventRecord(c->ev_start, c->stream));  // stream2 joins the replay's stream order here
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_start, 0));
-    hipLaunchKernelGGL((dr::k_fixed_queries<1024>), dim3(1), dim3(1024), 0, c->stream2, c->view(), nw, WS,
-                       dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, fq, fq_idx, fq_plan);
-    HIPCHK(c, hipGetLastError());
-    // the weak unions and speculative canonical digests need only the weak-column
-    // keys and slots, not the rows: launched here, they overlap the row pass
-    if (int rc = ensure_summary_bufs(c)) return rc;
-    HIPCHK(c, launch_weak_union(c, T, c->stream2));
-    HIPCHK(c, hipEventRecord(c->ev_wu, c->stream2));  // k_kcand and the pop sweep wait on it
-  }
   // outputs: the emitting sweep's final pass packs them into one device region, which comes back
   // in one copy (writing them straight into pinned host memory from the kernel
   // took 19.5 us, profiles/r02/v27_timeline.txt)
@@ -2594,13 +2553,11 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     // 3. pops
     hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
                        dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave, task_q, cq, cpush_n, push_out, pcap,
-                       task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan, fq_idx,
-                       fq_n);
+                       task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
     HIPCHK(c, hipGetLastError());
     return 0;
   };
-  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false, fixedq, fixedq)) return rc;
-  if (fixedq) dq = fq;
+  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false)) return rc;
   if (paper) c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
   // 3+4. delivery sweeps (merging with K), then each query's emission
   a.q = dq;
@@ -2641,18 +2598,9 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   }
   dr::SweepQuery probe{};
   probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
-  if (fixedq) {  // the sweeps need only the cone; stream2's chains, pop plan and emission join after them
-    a.nq = fq_n;
-    a.nq_dev = nullptr;
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_wu, 0));  // k_fixed_queries
-    HIPCHK(c, c->rec(2));
-    HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-  } else {
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
-    HIPCHK(c, c->rec(2));
-    HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
-  }
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
+  HIPCHK(c, c->rec(2));
+  HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
   if (paper) {  // first-pop ownership, then each query's delivered rounds
     hipLaunchKernelGGL((dr::k_paper_plan<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->memo_view().dmax, plan,
                        pop_q, dq, dstops, firstpop, qcut, qlo, firstK, qr_cnt, qr_off, qr_list);
@@ -2662,8 +2610,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     em.fin.firstpop = firstpop;
     em.fin.qedges = qedges;
   } else {  // REF: own rounds above the cut; the last workgroup: canonical prefixes G, E
-    HIPCHK(c, launch_own_emit(c, fixedq ? std::max(fq_n, 1) : nw, fixedq ? fq_plan : plan, dq, dstops, qcount,
-                              qdigest, qcut));
+    HIPCHK(c, launch_own_emit(c, nw, plan, dq, dstops, qcount, qdigest, qcut));
   }
   HIPCHK(c, c->rec(3));
   // 5. per-pop totals and outputs (the canonical prefixes came from the sweep launch's extra workgroup)
@@ -2704,7 +2651,6 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   o->n_push = np;
   if (h_hdr[dr::PH_CAPERR] == 2) return c->fail(DR_E_STATE, "replay planner: segment bound exceeded");
   if (h_hdr[dr::PH_CAPERR] == 3) return c->fail(DR_E_STATE, "replay planner: a pop below its leader's round");
-  if (h_hdr[dr::PH_CAPERR] == 4) return c->fail(DR_E_STATE, "replay planner: a pushed leader without a query");
   if (h_hdr[dr::PH_CAPERR] || np > o->push_cap)
     return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)np, (long long)o->push_cap);
   std::memcpy(o->push_off, h_push_off, ((size_t)nw + 1) * 4);

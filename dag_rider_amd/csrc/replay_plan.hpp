@@ -91,50 +91,6 @@ __global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ 
   }
 }
 
-// REF delivery queries fixed before the chains run: one per wave whose leader is
-// present (a superset of the leaders any push can pop), highest round first,
-// with cumulative mask images (rounds 0..top); qidx[w] = the wave's query or -1;
-// qplan[PL_NQD] = the count.  Rebuilt by every planned replay (engine.hip).
-template <int NT>
-__global__ __launch_bounds__(NT) void k_fixed_queries(DagView g, int nw, int WS, int qflags,
-                                                      SweepQuery *__restrict__ dq, int32_t *__restrict__ qidx,
-                                                      int32_t *__restrict__ qplan) {
-  __shared__ int64_t s[NT / 64];
-  __shared__ int64_t c0, c1;
-  const int tid = threadIdx.x;
-  if (tid == 0) c0 = c1 = 0;
-  if (tid == 0) qidx[0] = -1;
-  __syncthreads();
-  for (int i0 = 0; i0 < nw; i0 += NT) {
-    const int i = i0 + tid, w = nw - i;
-    const int top = 4 * (w - 1) + 1;
-    int l = 0;
-    int64_t f = 0;
-    if (i < nw) {
-      l = g.lead[w] - 1;
-      f = (g.present[(size_t)top * WS + (l >> 6)] >> (l & 63)) & 1ULL;
-    }
-    int64_t tq, tm;
-    const int64_t qi = block_scan_excl<NT>(f, s, tq);
-    const int64_t mo = block_scan_excl<NT>(f ? (int64_t)(top + 1) * WS : int64_t(0), s, tm);
-    if (i < nw) qidx[w] = f ? (int32_t)(c0 + qi) : -1;
-    if (f) {
-      SweepQuery q{};
-      q.top = top;
-      q.bottom = 0;
-      q.src0 = l;
-      q.flags = qflags;
-      q.mask_off = c1 + mo;
-      q.tgt0 = -1;
-      dq[c0 + qi] = q;
-    }
-    __syncthreads();
-    if (tid == 0) { c0 += tq; c1 += tm; }
-    __syncthreads();
-  }
-  if (tid < PL_N) qplan[tid] = tid == PL_NQD ? (int32_t)c0 : 0;
-}
-
 // Pushes (task wave, then its chain's pushes in push order) -> pops in pop
 // order (each task's pushes reversed, process.go:406-412), push_off per wave,
 // and one delivery query per distinct leader, highest round first, with
@@ -150,11 +106,7 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
                                                   int32_t *__restrict__ push_wave, int32_t *__restrict__ pop_wave,
                                                   int32_t *__restrict__ pop_cur, int32_t *__restrict__ pop_q,
                                                   uint8_t *__restrict__ seen, int32_t *__restrict__ qidx,
-                                                  SweepQuery *__restrict__ dq, int32_t *__restrict__ plan,
-                                                  const int32_t *__restrict__ qfix, int nqfix) {
-  // qfix != nullptr: the delivery queries are fixed in advance (one per wave whose
-  // leader is present, qfix[w] its index; engine.hip replay_planned): only the
-  // pops' query indices are needed here
+                                                  SweepQuery *__restrict__ dq, int32_t *__restrict__ plan) {
   __shared__ int64_t s[NT / 64];
   __shared__ int64_t c0, c1;
   const int tid = threadIdx.x;
@@ -204,15 +156,6 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
     const int whi = t < ntask ? task_wave[t] : nw + 1;
     const uint32_t v = (uint32_t)(t < ntask ? task_pos[t] : np);
     for (int w = wlo; w <= whi; w++) push_off[w - 1] = v;
-  }
-  if (qfix) {
-    if (tid == 0) plan[PL_NQD] = nqfix;
-    for (int64_t p = tid; p < np; p += NT) {
-      const int q = qfix[pop_wave[p]];
-      pop_q[p] = q;
-      if (q < 0) plan[PL_CAPERR] = 4;  // a pushed leader that is not present: cannot happen
-    }
-    return;
   }
   if (tid == 0) c0 = 0;
   __syncthreads();

@@ -115,8 +115,11 @@ def with_repeated_ids(rng: np.random.Generator, dag, p_dup=0.3, max_extra=2):
         ids = [v.id for v in out[r] if v.id != VertexID(0, 0)]
         if not ids:
             continue
-        prev = [v.id for v in out[r - 1] if v.id != VertexID(0, 0)]
-        below = [v.id for rr in range(max(0, r - 6), r - 1) for v in out[rr] if v.id != VertexID(0, 0)]
+        # distinct targets: an edge list naming one target twice is a multi-edge, which
+        # the edge totals count once
+        prev = sorted({v.id for v in out[r - 1] if v.id != VertexID(0, 0)}, key=lambda x: (x.round, x.source))
+        below = sorted({v.id for rr in range(max(0, r - 6), r - 1) for v in out[rr] if v.id != VertexID(0, 0)},
+                       key=lambda x: (x.round, x.source))
         for vid in ids:
             if rng.random() >= p_dup:
                 continue

@@ -91,8 +91,9 @@ def test_repeated_ids_appended_one_by_one(gpu_device):
             r = int(rng.integers(1, R + 1))
             ids = [v.id for v in cur[r]]
             vid = ids[int(rng.integers(0, len(ids)))]
-            prev = [v.id for v in cur[r - 1]]
-            below = [v.id for rr in range(max(0, r - 5), r - 1) for v in cur[rr]]
+            prev = sorted({v.id for v in cur[r - 1]}, key=lambda x: (x.round, x.source))  # distinct targets
+            below = sorted({v.id for rr in range(max(0, r - 5), r - 1) for v in cur[rr]},
+                           key=lambda x: (x.round, x.source))
             v = Vertex(vid, b"", [u for u in prev if rng.random() < 0.5], [u for u in below if rng.random() < 0.15])
             e.append_vertices([v])
             cur[r].append(v)

@@ -261,9 +261,7 @@ def test_device_planned_replay_matches_host_planned(gpu_device, name):
             b = e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF)
             _compare_replay(a, b, ids=False)
             assert a.chain_edges == b.chain_edges
-            # REF: the device plan sweeps one cone per present leader (a superset of the
-            # popped ones, fixed before the chains run); the host plan only the popped
-            assert a.sweep["canon_segments"] == b.sweep["canon_segments"] and a.sweep["count"] >= b.sweep["count"]
+            assert a.sweep == b.sweep
             # twice in a row (arena reuse), then with a push capacity that is too small
             e.set_device_plan(True)
             _compare_replay(e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF), b, ids=False)
