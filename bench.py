@@ -44,7 +44,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950
 # correction of MI355X_MICROARCH.md) on this bench: tools/pmc_traffic.py output
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02", "traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "traffic.json")
 # replay phase -> the kernels it launches (names as rocprofv3 reports them)
 PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 1024, 2, false>"],
                  "sweep": ["dr::k_sweep<16, 256, 9>"],
@@ -998,7 +998,7 @@ def main() -> int:
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": ach / HBM_PEAK_GBS,
                      "traffic": measured_traffic(dom) if args.config == "c4" and args.deliver == "ref" else None,
-                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r02/traffic.json)",
+                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r03/traffic.json)",
                      "kernel": kb[dom]["kernel"], "bytes_per_launch": kb[dom]["bytes"],
                      "ms_per_launch": kb[dom]["ms"]},
         "cpu_baseline": cpu,

@@ -581,6 +581,8 @@ struct dr_shard {
       mpush, mqidx, mqout;
   std::vector<uint64_t> h_sdr;  // strong degree sum per round (host copy)
   int *alive = nullptr;         // pinned: live queries after the last polled step
+  int hint_canon = 4, hint_batch = 8;  // steps the last replay's canonical walk / query batch took
+  SBuf mnseg;                   // the canonical walk's final state (its segment count)
   std::vector<std::vector<uint32_t>> h_weak;  // per local shard
   std::vector<std::vector<uint64_t>> h_woff;  // per local shard, absolute offsets, size nrounds+1
   // weak columns per local shard (the memoized replay, shard_memo.hpp): one entry per
@@ -1033,7 +1035,7 @@ int deliver(dr_shard *c, const std::vector<Pop> &pops, int mode, uint64_t *pcoun
 // and every query's full frontier after each exchange, so each one takes the
 // same decisions; only the row work is split by column.
 // ---------------------------------------------------------------------------
-drs::MArgs make_margs(dr_shard *c, int nq) {
+drs::MArgs make_margs(dr_shard *c, int nq, int T = -1) {
   drs::MArgs a{};
   a.strong = c->strong.as<u64>();
   a.strong_stride = (int64_t)c->max_rounds * c->n * c->SP;
@@ -1073,6 +1075,8 @@ drs::MArgs make_margs(dr_shard *c, int nq) {
   a.summary = 1;
   a.R = c->max_rounds;
   a.nlead = (int32_t)c->h_lead.size();
+  a.good = c->mgood.as<uint8_t>();
+  a.T = T >= 0 ? T : c->nrounds - 1;
   return a;
 }
 
@@ -1080,8 +1084,11 @@ bool memo_applies(const dr_shard *c) { return c->memo && c->dmax <= 65; }
 
 // Step a batch of queries (states in st0, rings clear) until none is live.
 // Returns the number of steps taken (the final states are in st[steps & 1]).
-int run_steps(dr_shard *c, const drs::MArgs &a, int nq, int maxsteps, int *steps) {
+int run_steps(dr_shard *c, const drs::MArgs &a, int nq, int maxsteps, int *steps, int hint = 4) {
   const dim3 grid(nq, c->nlocal), block(drs::MS_NT);
+  // the first poll comes after `hint` steps (what the same batch took last time;
+  // extra steps after the last query finished exit at once), then every 2
+  int next_poll = std::max(2, hint);
   for (int j = 0;; j++) {
     hipLaunchKernelGGL(drs::k_ms_step, grid, block, 0, c->stream, a, j);
     SHCHK(c, hipGetLastError());
@@ -1092,8 +1099,9 @@ int run_steps(dr_shard *c, const drs::MArgs &a, int nq, int maxsteps, int *steps
     }
     c->last_rounds++;
     const int done_steps = j + 1;
-    // poll every 4 steps (each poll is one host round trip)
-    if (done_steps % 4 == 0 || done_steps >= maxsteps) {
+    // each poll is one host round trip
+    if (done_steps >= next_poll || done_steps >= maxsteps) {
+      next_poll = done_steps + 2;
       const drs::MState *st = (done_steps & 1) ? a.st1 : a.st0;
       hipLaunchKernelGGL(drs::k_ms_alive, dim3(1), block, 0, c->stream, st, nq, c->alive);
       SHCHK(c, hipGetLastError());
@@ -1116,6 +1124,8 @@ int init_states(dr_shard *c, const std::vector<drs::MQuery> &qs) {
   for (int i = 0; i < nq; i++) {
     st[i] = drs::MState{};
     st[i].low = qs[i].top;
+    st[i].cur = qs[i].top;
+    st[i].fresh = qs[i].type == drs::MQ_CANON ? 1 : 0;
   }
   SHCHK(c, hipMemcpyAsync(c->mq.p, qs.data(), nq * sizeof(drs::MQuery), hipMemcpyHostToDevice, c->stream));
   SHCHK(c, hipMemcpyAsync(c->mst.p, st.data(), nq * sizeof(drs::MState), hipMemcpyHostToDevice, c->stream));
@@ -1128,13 +1138,14 @@ int init_states(dr_shard *c, const std::vector<drs::MQuery> &qs) {
 
 // Round summaries, K^cand, good, the canonical segments and the canonical
 // prefixes C, E, G of the DAG's top round T.
-int build_canon(dr_shard *c, int T, int *nseg) {
+int build_canon(dr_shard *c, int T) {
   const int W = c->W, SP = c->SP, nl = c->nlocal, dd = std::max(0, c->dmax - 1);
   const size_t R = (size_t)c->max_rounds;
   SHCHK(c, c->mU.ensure((size_t)nl * R * SP * 8));
   SHCHK(c, c->mWU.ensure(std::max<size_t>((size_t)nl * R * dd * SP, 1) * 8));
   SHCHK(c, c->mK.ensure((size_t)(T + 1) * W * 8));
   SHCHK(c, c->mgood.ensure((size_t)T + 8));
+  SHCHK(c, c->mnseg.ensure(sizeof(drs::MState)));
   for (SBuf *b : {&c->mRD, &c->mCE, &c->mRG, &c->mC, &c->mE, &c->mG}) SHCHK(c, b->ensure((size_t)(T + 1) * 8));
   drs::MArgs a = make_margs(c, 1);
   if (T >= 1) {
@@ -1160,34 +1171,21 @@ int build_canon(dr_shard *c, int T, int *nseg) {
   }
   hipLaunchKernelGGL(drs::k_ms_good, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a, T, c->mgood.as<uint8_t>());
   SHCHK(c, hipGetLastError());
-  std::vector<uint8_t> good(T + 1);
-  SHCHK(c, hipMemcpyAsync(good.data(), c->mgood.p, T + 1, hipMemcpyDeviceToHost, c->stream));
-  SHCHK(c, hipStreamSynchronize(c->stream));
-  // canonical segments, top down (k_canon, kernels.hpp): from each bad round until
-  // dmax consecutive full rounds restore the regime
-  int pos = T, segs = 0;
-  while (true) {
-    int b = pos - 1;
-    while (b >= 0 && good[b]) b--;
-    if (b < 0) break;
-    segs++;
-    drs::MQuery q{};
-    q.type = drs::MQ_CANON;
-    q.top = b;
-    q.bottom = 0;
-    q.src0 = -1;
-    if (int rc = init_states(c, {q})) return rc;
-    drs::MArgs sa = make_margs(c, 1);
-    hipLaunchKernelGGL(drs::k_ms_canon_init, dim3(nl), dim3(drs::MS_NT), 0, c->stream, sa, b, T);
-    SHCHK(c, hipGetLastError());
-    int steps = 0;
-    if (int rc = run_steps(c, sa, 1, b + 2, &steps)) return rc;
-    drs::MState fin;
-    SHCHK(c, hipMemcpyAsync(&fin, (steps & 1) ? sa.st1 : sa.st0, sizeof fin, hipMemcpyDeviceToHost, c->stream));
-    SHCHK(c, hipStreamSynchronize(c->stream));
-    pos = fin.stop;
-  }
-  *nseg = segs;
+  // the canonical segments, top down (k_canon's walk, kernels.hpp): one MQ_CANON
+  // query finds each bad round on the device (good[]) and sweeps until dmax
+  // consecutive full rounds restore the regime; no host round trip per segment
+  drs::MQuery q{};
+  q.type = drs::MQ_CANON;
+  q.top = T;
+  q.bottom = 0;
+  q.src0 = -1;
+  if (int rc = init_states(c, {q})) return rc;
+  drs::MArgs sa = make_margs(c, 1, T);
+  int steps = 0;
+  if (int rc = run_steps(c, sa, 1, T + 2 * std::max(1, c->nrounds), &steps, c->hint_canon)) return rc;
+  c->hint_canon = steps;
+  SHCHK(c, hipMemcpyAsync(c->mnseg.p, (steps & 1) ? sa.st1 : sa.st0, sizeof(drs::MState), hipMemcpyDeviceToDevice,
+                          c->stream));
   hipLaunchKernelGGL(drs::k_ms_cstats, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a, T, c->mRD.as<u64>(),
                      c->mCE.as<u64>());
   SHCHK(c, hipGetLastError());
@@ -1225,9 +1223,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
   o->commit_edges = ce;
   // 2. summaries and the canonical cone
-  int nseg = 0;
-  if (int rc = build_canon(c, T, &nseg)) return rc;
-  o->canon_segments = nseg;
+  if (int rc = build_canon(c, T)) return rc;
   SHCHK(c, hipEventRecord(ev[2], c->stream));
   // 3. one batch: a cone for every wave whose leader is present (a superset of the
   // leaders any chain can push) and the chain of every commit that needs one
@@ -1276,6 +1272,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   const int nq = (int)qs.size();
   int steps = 0;
   std::vector<drs::MState> fin(nq);
+  drs::MState canon_fin{};
   std::vector<int32_t> pushes_dev(std::max(pbase, 1));
   std::vector<uint64_t> qout((size_t)3 * std::max(npop, 1));
   if (nq > 0) {
@@ -1284,7 +1281,8 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     SHCHK(c, c->mpush.ensure((size_t)std::max(pbase, 1) * 4));
     SHCHK(c, hipMemsetAsync(c->mpend.p, 0, (size_t)c->nlocal * nq * c->depth * c->SP * 8, c->stream));
     drs::MArgs a = make_margs(c, nq);
-    if (int rc = run_steps(c, a, nq, maxsteps, &steps)) return rc;
+    if (int rc = run_steps(c, a, nq, maxsteps, &steps, c->hint_batch)) return rc;
+    c->hint_batch = steps;
     SHCHK(c, hipEventRecord(ev[3], c->stream));
     // 4. emission of every pop query (REF; PAPER needs the pop order, below)
     if (npop > 0 && !paper) {
@@ -1302,9 +1300,11 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     }
     SHCHK(c, hipMemcpyAsync(fin.data(), (steps & 1) ? a.st1 : a.st0, nq * sizeof(drs::MState), hipMemcpyDeviceToHost,
                             c->stream));
+    SHCHK(c, hipMemcpyAsync(&canon_fin, c->mnseg.p, sizeof canon_fin, hipMemcpyDeviceToHost, c->stream));
     if (pbase) SHCHK(c, hipMemcpyAsync(pushes_dev.data(), c->mpush.p, (size_t)pbase * 4, hipMemcpyDeviceToHost, c->stream));
   } else {
     SHCHK(c, hipEventRecord(ev[3], c->stream));
+    SHCHK(c, hipMemcpyAsync(&canon_fin, c->mnseg.p, sizeof canon_fin, hipMemcpyDeviceToHost, c->stream));
   }
   SHCHK(c, hipEventRecord(ev[4], c->stream));
   SHCHK(c, hipEventSynchronize(ev[4]));
@@ -1313,6 +1313,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   SHCHK(c, hipEventElapsedTime(&o->ms_deliver, ev[2], ev[3]));
   SHCHK(c, hipEventElapsedTime(&o->ms_emit, ev[3], ev[4]));
   o->ms_chain = 0;
+  o->canon_segments = canon_fin.npush;
   // 5. assembly: pushes per commit, pops in stack order, each pop = its leader's query
   std::vector<std::vector<int32_t>> pushes(tasks.size());
   uint64_t chain_e = 0;
@@ -1533,7 +1534,7 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (SBuf *b : {&c->wck, &c->wcr, &c->wcro, &c->sdr, &c->mU, &c->mWU, &c->mK, &c->mgood, &c->mRD, &c->mCE, &c->mRG,
                   &c->mC, &c->mE, &c->mG, &c->mksend, &c->mkrecv, &c->mq, &c->mst, &c->mpend, &c->mrecv[0],
-                  &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout})
+                  &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout, &c->mnseg})
     b->release();
   if (c->alive) (void)hipHostFree(c->alive);
   for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out,

@@ -56,7 +56,8 @@ struct MQuery {
 // before step j; the shard-0 workgroup writes the state after it).
 struct MState {
   int32_t done, run, low, stop;  // stop: the round where the query merged / ended
-  int32_t merged, npush;
+  int32_t merged, npush;         // MQ_CANON: npush counts the segments walked
+  int32_t cur, fresh;            // MQ_CANON: its current round; 1 = start the next segment below cur
   u64 edges;                     // MQ_CHAIN: strong degrees of the expanded vertices
 };
 
@@ -82,7 +83,8 @@ struct MArgs {
   u64 *send;                // RCCL mode: [nq][WSs]
   u64 *masks;               // MQ_POP frontier rows
   int32_t *push_out;
-  int32_t n, W, WSs, SP, G, shard0, nlocal, local, nq, depth, dd, dmax, summary, R, nlead;
+  const uint8_t *good;       // [T+1] K^cand_r covers P_r (MQ_CANON: where segments start)
+  int32_t n, W, WSs, SP, G, shard0, nlocal, local, nq, depth, dd, dmax, summary, R, nlead, T;
 };
 
 __device__ __forceinline__ u64 shfl_xor64(u64 v, int m) {
@@ -183,21 +185,38 @@ __global__ __launch_bounds__(MS_NT) void k_ms_good(MArgs a, int T, uint8_t *__re
   if (lane == 0) good[r] = bad ? 0 : 1;
 }
 
-// A canonical segment below bad round b (one MQ_CANON query, index 0): its ring of
-// pending rounds starts with what the full rounds above b put below b (the WU of
-// rounds b+1 .. b+dd+1), exactly as k_canon (kernels.hpp) starts it.
-__global__ __launch_bounds__(MS_NT) void k_ms_canon_init(MArgs a, int b, int T) {
-  const int l = blockIdx.x, tid = threadIdx.x, SP = a.SP, dm = a.depth - 1;
-  u64 *pend = a.pend + (size_t)l * a.nq * a.depth * SP;
+// A canonical segment below bad round b (MQ_CANON): its ring of pending rounds
+// starts with what the full rounds above b put below b (the WU of rounds b+1 ..
+// b+dd+1), exactly as k_canon (kernels.hpp) starts it.  Every thread of the
+// workgroup calls it; the caller synchronises after.
+__device__ __forceinline__ void canon_ring_init(const MArgs &a, u64 *pend, int l, int b) {
+  const int tid = threadIdx.x, SP = a.SP, dm = a.depth - 1;
   for (int i = tid; i < a.depth * SP; i += MS_NT) pend[i] = 0;
   __syncthreads();
   if (tid >= SP) return;
   const size_t ub = (size_t)l * a.R;
   for (int x = b - 1; x >= 0 && x >= b - a.dd; x--) {
     u64 v = 0;
-    for (int y = max(b + 1, x + 2); y <= T && y <= x + a.dd + 1; y++) v |= a.WU[((ub + y) * a.dd + (y - x - 2)) * SP + tid];
+    for (int y = max(b + 1, x + 2); y <= a.T && y <= x + a.dd + 1; y++)
+      v |= a.WU[((ub + y) * a.dd + (y - x - 2)) * SP + tid];
     pend[(size_t)(x & dm) * SP + tid] = v;
   }
+}
+
+// The highest bad round below `below` (-1: none), wave 0 (every lane gets it):
+// 8 rounds per lane per pass, as k_canon's search.
+__device__ __forceinline__ int next_bad(const MArgs &a, int below) {
+  const int lane = threadIdx.x & 63;
+  for (int top = below - 1; top >= 0; top -= 512) {
+    int best = -1;
+    for (int k = 0; k < 8; k++) {
+      const int x = top - 8 * lane - k;
+      if (x >= 0 && !a.good[x]) { best = x; break; }
+    }
+    for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off));
+    if (best >= 0) return best;
+  }
+  return -1;
 }
 
 // One step (see the file comment).  Grid (nq, nlocal).
@@ -212,20 +231,52 @@ __global__ __launch_bounds__(MS_NT) void k_ms_step(MArgs a, int j) {
     return;
   }
   const MQuery Q = a.q[qi];
-  const int r = Q.top - j;
   const int W = a.W, SP = a.SP, dm = a.depth - 1;
   __shared__ u64 sFE[32];
   __shared__ u64 sAcc[32];
   __shared__ int sCtl[2];
+  __shared__ int sStart;
   u64 *pend = a.pend + ((size_t)l * a.nq + qi) * a.depth * SP;
+  // MQ_CANON walks the canonical segments top down on its own (k_canon's walk): at a
+  // segment start it finds the next bad round below its current round, resets its
+  // ring there, and starts from K^cand; it is done when no bad round is left
+  int r = Q.top - j;
+  bool start = false;
+  MState S1 = S;
+  if (Q.type == MQ_CANON) {
+    r = S.cur;
+    if (S.fresh) {
+      if (wv == 0) {
+        const int b = next_bad(a, S.cur);
+        if (lane == 0) sStart = b;
+      }
+      __syncthreads();
+      const int b = sStart;
+      if (b < 0) {
+        if (writer && tid == 0) {
+          S1.done = 1;
+          sn[qi] = S1;
+        }
+        return;
+      }
+      canon_ring_init(a, pend, l, b);
+      __syncthreads();
+      r = b;
+      start = true;
+      S1.run = 0;
+      S1.low = b;
+      S1.npush = S.npush + 1;
+    }
+  }
   if (tid < SP) sAcc[tid] = 0;
   if (wv == 0) {
     const bool act = lane < W;
     u64 f = 0, p = 0;
     if (act) {
-      if (j == 0) {
-        if (Q.type == MQ_CANON) f = a.K[(size_t)r * W + lane];
-        else f = (Q.src0 >= 0 && lane == (Q.src0 >> 6)) ? 1ULL << (Q.src0 & 63) : 0ULL;
+      if (start) {
+        f = a.K[(size_t)r * W + lane];
+      } else if (j == 0) {
+        f = (Q.src0 >= 0 && lane == (Q.src0 >> 6)) ? 1ULL << (Q.src0 & 63) : 0ULL;
       } else {
         const u64 *rv = (j & 1) ? a.recv1 : a.recv0;
         f = rv[((size_t)(lane / a.WSs) * a.nq + qi) * a.WSs + lane % a.WSs];
@@ -248,7 +299,7 @@ __global__ __launch_bounds__(MS_NT) void k_ms_step(MArgs a, int j) {
     const u64 fe = f & p;
     const bool nz = __ballot(act && f != 0ULL) != 0ULL;
     const bool full = __ballot(act && fe != p) == 0ULL;
-    int run = S.run, low = S.low;
+    int run = S1.run, low = S1.low;
     if (nz) low = min(low, r - 1);
     bool merged = false, done;
     if (Q.type == MQ_POP) {
@@ -258,7 +309,7 @@ __global__ __launch_bounds__(MS_NT) void k_ms_step(MArgs a, int j) {
       done = merged || r <= Q.bottom || (!nz && low >= r);
     } else if (Q.type == MQ_CHAIN) {
       done = r <= Q.bottom || (!nz && low >= r);
-    } else {
+    } else {  // MQ_CANON: the segment ends where dmax full rounds restore the regime
       run = full ? run + 1 : 0;
       done = run >= a.dmax || r == 0;
     }
@@ -279,15 +330,20 @@ __global__ __launch_bounds__(MS_NT) void k_ms_step(MArgs a, int j) {
     }
     if (!done && Q.type != MQ_CHAIN && __ballot(act && fe != 0ULL) != 0ULL) low = min(low, r - a.dmax);
     if (writer && lane == 0) {
-      MState o;
+      MState o = S1;
       o.done = done;
       o.run = run;
       o.low = low;
       o.stop = done ? r : 0;
       o.merged = merged;
-      o.npush = S.npush + (restart ? 1 : 0);
+      o.npush = S1.npush + (restart ? 1 : 0);
       o.edges = edges;
-      if (restart) a.push_out[Q.push_base + S.npush] = wvv;
+      if (Q.type == MQ_CANON) {  // a finished segment: look for the next one below r
+        o.done = 0;
+        o.fresh = done ? 1 : 0;
+        o.cur = done ? r : r - 1;
+      }
+      if (restart) a.push_out[Q.push_base + S1.npush] = wvv;
       sn[qi] = o;
     }
     if (act) sFE[lane] = fe;
