@@ -436,16 +436,15 @@ __global__ void __launch_bounds__(SH_NT) k_shard_vote(ShardArgs a, int w0, int n
     Pout[((size_t)(a.local ? g : 0) * nw + wi) * a.W + (s >> 6)] = b;
 }
 
-__global__ void k_shard_vcount(const u64 *P, int G, int nw, int W, int32_t *vc) {
-  const int wi = blockIdx.x * blockDim.x + threadIdx.x;
+// vcount = |S_3|: one wave per wave index, lane = word, the G partials OR-ed
+__global__ __launch_bounds__(SH_NT) void k_shard_vcount(const u64 *P, int G, int nw, int W, int32_t *vc) {
+  const int wi = blockIdx.x * (SH_NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (wi >= nw) return;
-  int c = 0;
-  for (int w = 0; w < W; w++) {
-    u64 v = 0;
-    for (int g = 0; g < G; g++) v |= P[((size_t)g * nw + wi) * W + w];
-    c += __popcll(v);
-  }
-  vc[wi] = c;
+  u64 v = 0;
+  if (lane < W)
+    for (int g = 0; g < G; g++) v |= P[((size_t)g * nw + wi) * W + lane];
+  const u64 c = dr::wave_sum((u64)__popcll(v));
+  if (lane == 0) vc[wi] = (int32_t)c;
 }
 
 // Delivery masks, one wave per round r (lane = word): X = reach & present, and
@@ -582,6 +581,10 @@ struct dr_shard {
   std::vector<uint64_t> h_sdr;  // strong degree sum per round (host copy)
   int *alive = nullptr;         // pinned: live queries after the last polled step
   int hint_canon = 4, hint_batch = 8;  // steps the last replay's canonical walk / query batch took
+  // pinned staging for the memo replay's small transfers (queries in, results out);
+  // reset at each replay's start, grown after a stream sync
+  char *pin = nullptr;
+  size_t pin_cap = 0, pin_used = 0;
   SBuf mnseg;                   // the canonical walk's final state (its segment count)
   std::vector<std::vector<uint32_t>> h_weak;  // per local shard
   std::vector<std::vector<uint64_t>> h_woff;  // per local shard, absolute offsets, size nrounds+1
@@ -850,7 +853,8 @@ int vote_range(dr_shard *c, int w0, int nw, uint8_t *commit, int32_t *vcount) {
       c->last_xbytes += (uint64_t)nw * W * 8;
     }
   }
-  hipLaunchKernelGGL(k_shard_vcount, dim3((nw + 255) / 256), dim3(256), 0, c->stream, c->vote_p[1].as<u64>(), G, nw,
+  hipLaunchKernelGGL(k_shard_vcount, dim3((nw + SH_NT / 64 - 1) / (SH_NT / 64)), dim3(SH_NT), 0, c->stream,
+                     c->vote_p[1].as<u64>(), G, nw,
                      W, c->vcount.as<int32_t>());
   SHCHK(c, hipGetLastError());
   std::vector<int32_t> vc(nw);
@@ -1116,19 +1120,40 @@ int run_steps(dr_shard *c, const drs::MArgs &a, int nq, int maxsteps, int *steps
   }
 }
 
+// n bytes of the pinned staging area (256-B aligned); nullptr on failure
+char *stage(dr_shard *c, size_t n) {
+  const size_t at = (c->pin_used + 255) & ~(size_t)255;
+  if (at + n > c->pin_cap) {
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return nullptr;  // staged copies still in flight
+    const size_t cap = std::max<size_t>({(size_t)4 << 20, 2 * c->pin_cap, 2 * (at + n)});
+    char *q = nullptr;
+    if (hipHostMalloc((void **)&q, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (c->pin) (void)hipHostFree(c->pin);
+    c->pin = q;
+    c->pin_cap = cap;
+    c->pin_used = 0;
+    return stage(c, n);
+  }
+  c->pin_used = at + n;
+  return c->pin + at;
+}
+
 int init_states(dr_shard *c, const std::vector<drs::MQuery> &qs) {
   const int nq = (int)qs.size();
   SHCHK(c, c->mq.ensure((size_t)nq * sizeof(drs::MQuery)));
   SHCHK(c, c->mst.ensure((size_t)2 * nq * sizeof(drs::MState)));
-  std::vector<drs::MState> st(nq);
+  auto *hq = reinterpret_cast<drs::MQuery *>(stage(c, (size_t)nq * sizeof(drs::MQuery)));
+  auto *st = reinterpret_cast<drs::MState *>(stage(c, (size_t)nq * sizeof(drs::MState)));
+  if (!hq || !st) return c->fail(DR_E_HIP, "pinned staging allocation failed");
   for (int i = 0; i < nq; i++) {
+    hq[i] = qs[i];
     st[i] = drs::MState{};
     st[i].low = qs[i].top;
     st[i].cur = qs[i].top;
     st[i].fresh = qs[i].type == drs::MQ_CANON ? 1 : 0;
   }
-  SHCHK(c, hipMemcpyAsync(c->mq.p, qs.data(), nq * sizeof(drs::MQuery), hipMemcpyHostToDevice, c->stream));
-  SHCHK(c, hipMemcpyAsync(c->mst.p, st.data(), nq * sizeof(drs::MState), hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, hipMemcpyAsync(c->mq.p, hq, nq * sizeof(drs::MQuery), hipMemcpyHostToDevice, c->stream));
+  SHCHK(c, hipMemcpyAsync(c->mst.p, st, nq * sizeof(drs::MState), hipMemcpyHostToDevice, c->stream));
   SHCHK(c, c->mpend.ensure((size_t)c->nlocal * nq * c->depth * c->SP * 8));
   SHCHK(c, c->mrecv[0].ensure((size_t)c->G * nq * c->WSs * 8));
   SHCHK(c, c->mrecv[1].ensure((size_t)c->G * nq * c->WSs * 8));
@@ -1214,6 +1239,8 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   struct EvGuard { hipEvent_t *e; ~EvGuard() { for (int i = 0; i < 5; i++) if (e[i]) (void)hipEventDestroy(e[i]); } } eg{ev};
   const int T = c->nrounds - 1, W = c->W;
   if (int rc = prepare_queries(c, 0)) return rc;  // uploads the weak edges and columns
+  SHCHK(c, hipStreamSynchronize(c->stream));
+  c->pin_used = 0;
   SHCHK(c, hipEventRecord(ev[0], c->stream));
   // 1. commit decisions of every wave (three exchanges)
   if (int rc = votes(c, 1, nwaves, o->commit, o->vcount)) return rc;
@@ -1273,6 +1300,9 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   int steps = 0;
   std::vector<drs::MState> fin(nq);
   drs::MState canon_fin{};
+  uint64_t *hq_out = nullptr;
+  drs::MState *hfin = nullptr;
+  int32_t *hpush = nullptr;
   std::vector<int32_t> pushes_dev(std::max(pbase, 1));
   std::vector<uint64_t> qout((size_t)3 * std::max(npop, 1));
   if (nq > 0) {
@@ -1296,18 +1326,26 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
                          (steps & 1) ? a.st1 : a.st0, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
                          c->mC.as<u64>(), c->mG.as<u64>(), c->mE.as<u64>(), qo, qo + npop, qo + 2 * npop);
       SHCHK(c, hipGetLastError());
-      SHCHK(c, hipMemcpyAsync(qout.data(), qo, (size_t)3 * npop * 8, hipMemcpyDeviceToHost, c->stream));
+      hq_out = reinterpret_cast<uint64_t *>(stage(c, (size_t)3 * npop * 8));
+      if (!hq_out) return c->fail(DR_E_HIP, "pinned staging allocation failed");
+      SHCHK(c, hipMemcpyAsync(hq_out, qo, (size_t)3 * npop * 8, hipMemcpyDeviceToHost, c->stream));
     }
-    SHCHK(c, hipMemcpyAsync(fin.data(), (steps & 1) ? a.st1 : a.st0, nq * sizeof(drs::MState), hipMemcpyDeviceToHost,
+    hfin = reinterpret_cast<drs::MState *>(stage(c, nq * sizeof(drs::MState)));
+    hpush = reinterpret_cast<int32_t *>(stage(c, (size_t)std::max(pbase, 1) * 4));
+    if (!hfin || !hpush) return c->fail(DR_E_HIP, "pinned staging allocation failed");
+    SHCHK(c, hipMemcpyAsync(hfin, (steps & 1) ? a.st1 : a.st0, nq * sizeof(drs::MState), hipMemcpyDeviceToHost,
                             c->stream));
     SHCHK(c, hipMemcpyAsync(&canon_fin, c->mnseg.p, sizeof canon_fin, hipMemcpyDeviceToHost, c->stream));
-    if (pbase) SHCHK(c, hipMemcpyAsync(pushes_dev.data(), c->mpush.p, (size_t)pbase * 4, hipMemcpyDeviceToHost, c->stream));
+    if (pbase) SHCHK(c, hipMemcpyAsync(hpush, c->mpush.p, (size_t)pbase * 4, hipMemcpyDeviceToHost, c->stream));
   } else {
     SHCHK(c, hipEventRecord(ev[3], c->stream));
     SHCHK(c, hipMemcpyAsync(&canon_fin, c->mnseg.p, sizeof canon_fin, hipMemcpyDeviceToHost, c->stream));
   }
   SHCHK(c, hipEventRecord(ev[4], c->stream));
   SHCHK(c, hipEventSynchronize(ev[4]));
+  if (hq_out) std::copy(hq_out, hq_out + (size_t)3 * npop, qout.begin());
+  if (hfin) std::copy(hfin, hfin + nq, fin.begin());
+  if (hpush && pbase) std::copy(hpush, hpush + pbase, pushes_dev.begin());
   SHCHK(c, hipEventElapsedTime(&o->ms_commit, ev[0], ev[1]));
   SHCHK(c, hipEventElapsedTime(&o->ms_summary, ev[1], ev[2]));
   SHCHK(c, hipEventElapsedTime(&o->ms_deliver, ev[2], ev[3]));
@@ -1537,6 +1575,7 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
                   &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout, &c->mnseg})
     b->release();
   if (c->alive) (void)hipHostFree(c->alive);
+  if (c->pin) (void)hipHostFree(c->pin);
   for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out,
                   &c->qinfo, &c->pres, &c->sdeg, &c->wdeg, &c->rdeg, &c->slot_off, &c->slot_src, &c->lead, &c->bar,
                   &c->errf, &c->push_out, &c->push_n, &c->cedges, &c->vote_s0, &c->vote_p[0], &c->vote_p[1],

@@ -370,6 +370,10 @@ __global__ __launch_bounds__(MS_NT) void k_ms_step(MArgs a, int j) {
     // strong rows of the frontier: wave wv takes frontier words wv, wv + 4, ...;
     // lane reads words lane + 64 i of the word's 64 rows (column lane mod SP)
     const u64 *rows = a.strong + (size_t)l * a.strong_stride + (size_t)r * a.n * SP;
+    // saturation (as the unsharded sweep's expand_round): once the OR of the rows a
+    // wave has read equals U_r, the union of every row of round r, no further row
+    // can add a bit and the wave stops reading
+    const u64 ur = lane < SP ? a.U[((size_t)l * a.R + r) * SP + lane] : 0ULL;
     u64 acc = 0;
     for (int w = wv; w < W; w += MS_NT / 64) {
       const u64 bits = sFE[w];
@@ -379,6 +383,9 @@ __global__ __launch_bounds__(MS_NT) void k_ms_step(MArgs a, int j) {
         const int k = lane + 64 * i;
         if ((bits >> (k / SP)) & 1ULL) acc |= blk[k];
       }
+      u64 red = acc;
+      for (int off = SP; off < 64; off <<= 1) red |= shfl_xor64(red, off);
+      if (__ballot(lane < SP && red != ur) == 0ULL) break;
     }
     for (int off = SP; off < 64; off <<= 1) acc |= shfl_xor64(acc, off);
     if (lane < SP && acc) atomicOr(&sAcc[lane], acc);
@@ -452,10 +459,31 @@ __global__ __launch_bounds__(MS_NT) void k_ms_cstats(MArgs a, int T, u64 *__rest
   }
 }
 
-// inclusive prefix over rounds 0..T of up to three arrays (one workgroup)
+// exclusive scan over one workgroup of MS_NT threads (wave shuffles + one LDS hop)
+__device__ __forceinline__ u64 ms_block_scan(u64 v, u64 *s, u64 &total) {
+  constexpr int NW = MS_NT / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  u64 x = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const u64 y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s[wid] = x;
+  __syncthreads();
+  u64 base = 0;
+  total = 0;
+  for (int w = 0; w < NW; w++) {
+    if (w < wid) base += s[w];
+    total += s[w];
+  }
+  __syncthreads();
+  return base + x - v;
+}
+
+// inclusive prefix over rounds 0..T of up to two arrays (one workgroup)
 __global__ __launch_bounds__(MS_NT) void k_ms_prefix(int T, const u64 *__restrict__ a0, u64 *__restrict__ b0,
                                                      const u64 *__restrict__ a1, u64 *__restrict__ b1) {
-  __shared__ u64 part[2][MS_NT];
+  __shared__ u64 part[MS_NT / 64];
   const int tid = threadIdx.x, n = T + 1, per = (n + MS_NT - 1) / MS_NT;
   const int ra = tid * per, rb = min(n, ra + per);
   u64 s0 = 0, s1 = 0;
@@ -463,19 +491,9 @@ __global__ __launch_bounds__(MS_NT) void k_ms_prefix(int T, const u64 *__restric
     s0 += a0[r];
     if (a1) s1 += a1[r];
   }
-  part[0][tid] = s0;
-  part[1][tid] = s1;
-  __syncthreads();
-  if (tid < 2) {
-    u64 run = 0;
-    for (int t = 0; t < MS_NT; t++) {
-      const u64 v = part[tid][t];
-      part[tid][t] = run;
-      run += v;
-    }
-  }
-  __syncthreads();
-  u64 x0 = part[0][tid], x1 = part[1][tid];
+  u64 t0, t1;
+  u64 x0 = ms_block_scan(s0, part, t0);
+  u64 x1 = a1 ? ms_block_scan(s1, part, t1) : 0ULL;  // a1 is uniform
   for (int r = ra; r < rb; r++) {
     x0 += a0[r];
     b0[r] = x0;
