@@ -9,31 +9,33 @@
 // Per DAG (T = 4*(nw-1)+1, the highest leader round):
 //   1. commits (waveReady's rule, process.go:326-339), wave by wave: S0 =
 //      {leader}; S_k = ballot(row(v) & S_{k-1} != 0) over rounds 4w-2..4w.
-//   2. one top-down pass over rounds T..1 computing, for every vertex v, the
-//      set of leader waves whose cone contains v: Qs (strong edges only, the
-//      chains' strong_path) and Qf (strong + weak, orderVertices' path(.., false)).
-//      Strong: lane u of round r-1 ORs Q(v) of every v of round r whose row has
-//      bit u (rows broadcast by readlane).  Weak: per weak column (one distinct
-//      weak target of the round), the wave-OR of Qf over the column's sources
-//      goes into a ring of pending rounds (one LDS atomic per column).  Q and
-//      degrees go to a per-DAG scratch.
-//   3. chains (process.go:341-350) from the leaders' Qs: wave w' is pushed
-//      after leader L iff L's bit is in Qs(leader(w')); pops = reverse pushes.
-//   4. bottom-up emission.  Vertex v is delivered by leader b (REF) iff b in
-//      Qf(v), or (PAPER) iff additionally no leader popped before b's first pop
-//      is in Qf(v).  A leader's contribution of a round is computed with lanes =
-//      slots: ballot ranks give the positions, the order-sensitive digest
-//       and edge sums are wave reductions.  REF memo (nw <= 63):
-//      bit 63 of Qf is the canonical cone K (every present vertex of round T);
-//      below the first round where b's cone differs from K, b's prefix equals K's,
-//      so only K and the leaders that already differ (those a few rounds under
-//      their top) are computed per round (the same identity as the
-//      engine's memo).  PAPER computes a leader only in rounds where it delivers
-//      something.  Chain edges: per-leader sums of strong degrees over Qs, only
-//      in the rounds the leader's chain segments cover.
-//   Qs bits are kept only in the rounds the chains can inspect (a leader's bit
-//   dies below its chain's floor round), and sources with an empty Qs skip the
-//   strong-only half of the expansion.
+//   2. one top-down pass over rounds T..1, bit-sliced: lane b holds leader b's
+//      cone in the current round as a vertex set (2 words), F_b with strong and
+//      weak edges (orderVertices' path(.., false)), G_b with strong edges only
+//      (the chains' strong_path, kept while a chain can still inspect it).  Lane
+//      63 is the canonical cone K (every present vertex of round T) and its
+//      strong-only twin.  Round r -> r-1: F_b' = OR of the rows of F_b's members
+//      (one masked wave-OR over lanes = vertices); a weak column (one distinct
+//      weak target of the round) puts its target into b's pending round iff its
+//      sources meet F_b.  A leader whose set equals K's takes K's expansion and
+//      weak targets; only the others (a leader in the few rounds under its top)
+//      are expanded on their own.  F goes to a per-DAG scratch, and per leader
+//      the strong degrees summed over G_b from round T down (the chains' edge
+//      counts, read at the leader rounds).
+//   3. chains (process.go:341-350) from the leaders' strong cones at the leader
+//      vertices (QL): wave w' is pushed after leader L iff L's strong cone holds
+//      leader(w'); pops = reverse pushes.  Chain edges = per segment the strong
+//      degrees summed over its rounds (differences of step 2's suffix sums).
+//   4. bottom-up emission.  Vertex v is delivered by leader b (REF) iff v in F_b,
+//      or (PAPER) iff additionally no leader popped before b's first pop holds v
+//      (the union of their sets: a prefix OR over the leaders in first-pop order).
+//      A leader's contribution of a round is computed with lanes = slots: ballot
+//      ranks give the positions, the order-sensitive digest and
+//      edge sums are wave reductions.  REF memo (nw <= 63): below the first round
+//      where b's cone differs from K, b's prefix equals K's, so only K and the
+//      leaders that already differ (those a few rounds under their top) are
+//      computed per round (the same identity as the engine's
+//      memo).  PAPER computes a leader only in rounds where it delivers something.
 // Supported: n <= 128, nw <= 64, weak deltas < ring depth (<= 32), no far edges.
 #pragma once
 #include "kernels.hpp"
@@ -50,9 +52,10 @@ struct SmallJob {
   const uint32_t *slot_off;
   const uint16_t *slot_src;
   const uint16_t *lead;     // [wave] chooseLeader(w), 1-based source
-  // scratch, rounds 0..T: Qf, Qs, (deg << 16 | strong deg)
-  u64 *qf;
-  u64 *qs;
+  // scratch: cone sets F [T+1][2 words][64 leaders], per-leader strong-degree suffix
+  // sums at the leader rounds [65][64], (deg << 16 | strong deg) [T+1][n]
+  u64 *cone;
+  uint32_t *sufl;
   uint32_t *deg;
   // outputs
   uint8_t *commit;      // [nw]
@@ -71,9 +74,8 @@ constexpr int kSmallMaxPops = 64 * 65 / 2;  // literal chains: wave w pushes up 
 // dynamic LDS of k_replay_small: the weak ring (rsl slots of 128 u64) or the
 // later phases' arrays, whichever is larger
 template <bool PAPER, bool PERSIST>
-constexpr int small_late_bytes() {  // coef, pop list, per-leader results, chain sums, paper "before" masks
-  return 64 * 65 + (((PERSIST ? 64 : kSmallMaxPops) + 255) & ~255) + 64 * (PAPER ? 6 : 3) * 8 + 64 * 8 +
-         (PAPER ? 64 * 8 : 0);
+constexpr int small_late_bytes() {  // coef, pop list, per-leader results
+  return 64 * 65 + (((PERSIST ? 64 : kSmallMaxPops) + 255) & ~255) + 64 * (PAPER ? 6 : 3) * 8;
 }
 template <bool PAPER, bool PERSIST>
 inline size_t small_lds_bytes(int rsl) {
@@ -82,7 +84,8 @@ inline size_t small_lds_bytes(int rsl) {
 }
 
 // rsl = ring slots = largest weak delta + 1 (round x's slot is reused by round
-// x + rsl, which is drained before any contribution to x arrives)
+// x + rsl, which is drained before any contribution to x arrives); a slot holds
+// 2 words per leader lane
 template <int DEPTH, bool PAPER, bool PERSIST>
 __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict__ jobs, int njobs, int nw, int rsl) {
   constexpr bool paper = PAPER;  // REF mode skips the paper-mode digests entirely
@@ -93,24 +96,23 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   constexpr int kMaxPops = PERSIST ? 64 : kSmallMaxPops;
   constexpr int RS = PAPER ? 6 : 3;  // per-leader results kept
   constexpr int kCoefB = 64 * 65, kPopB = (kMaxPops + 255) & ~255, kResB = 64 * RS * 8;
-  static_assert(kCoefB + kPopB + kResB + 64 * 8 + (PAPER ? 64 * 8 : 0) == small_late_bytes<PAPER, PERSIST>(),
-                "LDS layout");
-  // REF memo: bit 63 of Qf carries the canonical cone K (needs a free leader bit)
-  const bool kmemo = !PAPER && nw <= 63;
+  static_assert(kCoefB + kPopB + kResB == small_late_bytes<PAPER, PERSIST>(), "LDS layout");
+  // lane 63 carries the canonical cone K when it is not a leader
+  const bool haveK = nw <= 63;
+  const bool kmemo = !PAPER && haveK;  // REF memo: leaders take K's prefix below their first difference
   extern __shared__ __attribute__((aligned(16))) u64 arena[];                  // small_lds_bytes(rsl)
-  u64 *ring = arena;                                                            // [rsl * 128], phase 2
+  u64 *ring = arena;                                                            // [rsl][2][64], phase 2
   int8_t *coef = reinterpret_cast<int8_t *>(arena);                             // [64 * 65], phases 3-4
   uint8_t *pop_lead = reinterpret_cast<uint8_t *>(arena) + kCoefB;              // [kSmallMaxPops], 3-5
   u64 *res = reinterpret_cast<u64 *>(reinterpret_cast<char *>(arena) + ((kCoefB + kPopB + 7) & ~7));  // 4-5
-  u64 *CS = res + 64 * RS;   // [64] chain: running strong-degree sums over Qs, phase 4
-  u64 *BEF = CS + 64;        // [64] PAPER: leaders first popped before b, phase 4
-  __shared__ u64 QF[128];
+  __shared__ u64 KW[64];            // K's weak targets of the current round, [delta][word]
   __shared__ uint32_t DG[128];
   __shared__ u64 QL[64];
   __shared__ int32_t vc_s[64];
   __shared__ int16_t first_pop[64];
   __shared__ int16_t qs_floor[64];  // lowest round where leader b's strong cone is still inspected
   __shared__ int8_t lst[64];
+  __shared__ int8_t ord[64];        // PAPER: popped leaders in first-pop order
   const int lane = threadIdx.x;
   const int jb = blockIdx.x;
   if (jb >= njobs) return;
@@ -168,8 +170,9 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
     if (vc >= q) commit_mask |= 1ULL << (w - 1);
   }
 
-  // ---------------- 2. top-down Q pass ----------------
+  // ---------------- 2. top-down cone pass (lane b: leader b's sets) ----------------
   for (int i = lane; i < rsl * 128; i += 64) ring[i] = 0;
+  KW[lane] = 0;
   // chains (process.go:341-350) inspect leader b's strong cone only down to the
   // floor round of the commit whose chain can push b: 4*decidedWave + 1
   qs_floor[lane] = 0x7fff;
@@ -184,9 +187,20 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   }
   __syncthreads();
   const int my_floor = qs_floor[lane];
-  u64 qf[2] = {0, 0}, qs[2] = {0, 0};
+  u64 F0 = 0, F1 = 0;  // F_b: round-r vertices in leader b's cone
+  u64 G0 = 0, G1 = 0;  // G_b: the same over strong edges only
+  uint32_t suf = 0;    // strong degrees summed over G_b, rounds r..T
+  // round r's vertices (lanes v, v + 64): rows, strong degrees; b's expansion over its set
+  u64 ra[2], rb[2];
+  uint32_t sd[2];
+  auto expand = [&](u64 s0, u64 s1, u64 &n0, u64 &n1, uint32_t *dsum) {  // s: wave-uniform
+    const bool m0 = (s0 >> lane) & 1ULL, m1 = (s1 >> lane) & 1ULL;
+    n0 = wave_or((m0 ? ra[0] : 0ULL) | (m1 ? ra[1] : 0ULL));
+    n1 = WS > 1 ? wave_or((m0 ? rb[0] : 0ULL) | (m1 ? rb[1] : 0ULL)) : 0ULL;
+    if (dsum) *dsum = (uint32_t)wave_sum((u64)((m0 ? sd[0] : 0u) + (m1 ? sd[1] : 0u)));
+  };
   // software pipeline: round r-1's rows and first 64 weak columns (they do not
-  // depend on the frontier) load while round r is processed
+  // depend on the cones) load while round r is processed
   u64 nra[2], nrb[2], nw0 = 0, nw1 = 0;
   uint32_t nkey = 0, nc0 = 0, nc1 = 0;
   auto prefetch2 = [&](int r) {
@@ -205,45 +219,70 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   };
   prefetch2(T);
   for (int r = T; r >= 1; r--) {
-    const u64 alive = __ballot(lane < nw && my_floor <= r);
-    u64 ra[2] = {nra[0], nra[1]}, rb[2] = {nrb[0], nrb[1]};
+    const bool alive = (lane < nw && my_floor <= r) || (haveK && lane == 63);
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      ra[i] = nra[i];
+      rb[i] = nrb[i];
+      sd[i] = (uint32_t)(__popcll(ra[i]) + __popcll(rb[i]));
+    }
     u64 cw0 = nw0, cw1 = nw1;
     uint32_t ckey = nkey;
     const uint32_t c0 = nc0, c1 = nc1;
     if (r > 1) prefetch2(r - 1);
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const int v = lane + 64 * i;
-      qf[i] |= ring[(r % rsl) * 128 + v];
-      ring[(r % rsl) * 128 + v] = 0;
-      qs[i] &= alive;
+    {  // pending weak targets of round r
+      const int sl = r % rsl;
+      F0 |= ring[(sl * 2) * 64 + lane];
+      F1 |= ring[(sl * 2 + 1) * 64 + lane];
+      ring[(sl * 2) * 64 + lane] = 0;
+      ring[(sl * 2 + 1) * 64 + lane] = 0;
     }
-    if (kmemo && r == T) {  // K: every present vertex of the top round
-      if ((pres_word(T, 0) >> lane) & 1ULL) qf[0] |= 1ULL << 63;
-      if ((pres_word(T, 1) >> lane) & 1ULL) qf[1] |= 1ULL << 63;
+    if (!alive) G0 = G1 = 0;
+    if (haveK && r == T && lane == 63) {  // K: every present vertex of the top round
+      F0 |= pres_word(T, 0);
+      F1 |= pres_word(T, 1);
+      G0 = F0;
+      G1 = F1;
     }
-    if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its bit at the leader's source
+    if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its lane with the leader's vertex
       const int w = (r - 1) / 4 + 1;
       const int l = J.lead[w] - 1;
       if ((lead_mask >> (w - 1)) & 1ULL) {
-        if (lane == (l & 63)) {  // register arrays: constant indices only
-          const u64 sb = (alive >> (w - 1)) & 1ULL;
-          if (l < 64) {
-            qf[0] |= 1ULL << (w - 1);
-            qs[0] |= sb << (w - 1);
-            QL[w - 1] = qs[0];
-          } else {
-            qf[1] |= 1ULL << (w - 1);
-            qs[1] |= sb << (w - 1);
-            QL[w - 1] = qs[1];
-          }
+        const u64 bit = 1ULL << (l & 63);
+        if (lane == w - 1) {
+          if (l < 64) F0 |= bit; else F1 |= bit;
+          if (alive) { if (l < 64) G0 |= bit; else G1 |= bit; }
         }
+        // the leaders whose strong cone holds this leader's vertex (the chains' test)
+        const u64 ql = __ballot(lane < nw && ((((l < 64) ? G0 : G1) >> (l & 63)) & 1ULL));
+        if (lane == 0) QL[w - 1] = ql;
       } else if (lane == 0) {
         QL[w - 1] = 0;
       }
     }
+    J.cone[((size_t)r * 2) * 64 + lane] = F0;
+    J.cone[((size_t)r * 2 + 1) * 64 + lane] = F1;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int v = lane + 64 * i;
+      if (v < n) {
+        const size_t at = (size_t)r * n + v;
+        J.deg[at] = ((sd[i] + J.wdeg[at]) << 16) | sd[i];
+      }
+    }
+    // K (lane 63) and the leaders whose sets differ from it ("solo": expanded on their own)
+    u64 K0 = 0, K1 = 0, KG0 = 0, KG1 = 0;
+    if (haveK) {
+      K0 = readlane64(F0, 63);
+      K1 = readlane64(F1, 63);
+      KG0 = readlane64(G0, 63);
+      KG1 = readlane64(G1, 63);
+    }
+    const bool eqF = haveK && F0 == K0 && F1 == K1, eqG = haveK && G0 == KG0 && G1 == KG1;
+    const u64 soloF = __ballot(!eqF && (F0 | F1) != 0ULL), soloG = __ballot(!eqG && (G0 | G1) != 0ULL);
     // weak columns of round r (64 per batch, lane j holding column j; the first
-    // batch was prefetched): Qf of the column's sources into the pending round
+    // batch was prefetched): a column's target joins b's pending round iff its
+    // sources meet F_b
     for (uint32_t cb = c0; cb < c1; cb += 64) {
       if (cb != c0) {
         const uint32_t jc = cb + lane;
@@ -255,56 +294,58 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
           cw1 = WS > 1 ? J.wc_rows[(size_t)jc * WS + 1] : 0ULL;
         }
       }
-      const int m = (int)min(64u, c1 - cb);
-      for (int t = 0; t < m; t++) {  // wave-uniform
-        const u64 w0 = readlane64(cw0, t), w1 = readlane64(cw1, t);
-        const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)ckey, t);
-        u64 v = ((w0 >> lane) & 1ULL) ? qf[0] : 0ULL;
-        v |= ((w1 >> lane) & 1ULL) ? qf[1] : 0ULL;
-        v = wave_or(v);
-        const int delta = (int)(key >> 11), ts = (int)(key & 2047u);
-        if (lane == 0 && v && r - delta >= 1) atomicOr(&ring[((r - delta) % rsl) * 128 + ts], v);
+      const int delta = (int)(ckey >> 11), ts = (int)(ckey & 2047u);
+      const bool live = (cw0 | cw1) != 0ULL && r - delta >= 1;
+      const u64 tb = 1ULL << (ts & 63);
+      const int tw = ts >> 6, tsl = live ? (r - delta) % rsl : 0;
+      if (haveK && live && ((cw0 & K0) | (cw1 & K1)) != 0ULL) atomicOr(&KW[delta * 2 + tw], tb);
+      for (u64 m = soloF; m; m &= m - 1) {
+        const int b = __builtin_ctzll(m);
+        const u64 s0 = readlane64(F0, b), s1 = readlane64(F1, b);
+        if (live && ((cw0 & s0) | (cw1 & s1)) != 0ULL) atomicOr(&ring[(tsl * 2 + tw) * 64 + b], tb);
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const int v = lane + 64 * i;
-      if (v < n) {
-        const uint32_t sd = (uint32_t)(__popcll(ra[i]) + __popcll(rb[i]));
-        const size_t at = (size_t)r * n + v;
-        J.qf[at] = qf[i];
-        J.qs[at] = qs[i];
-        J.deg[at] = ((sd + J.wdeg[at]) << 16) | sd;
+    if (haveK && c0 < c1) {  // K's weak targets to every lane whose set is K's
+      for (int d = 1; d < rsl && r - d >= 1; d++) {
+        const u64 k0 = KW[d * 2], k1 = KW[d * 2 + 1];
+        if ((k0 | k1) && eqF) {
+          const int tsl = (r - d) % rsl;
+          ring[(tsl * 2) * 64 + lane] |= k0;
+          ring[(tsl * 2 + 1) * 64 + lane] |= k1;
+        }
       }
+      __syncthreads();
+      KW[lane] = 0;
     }
-    // strong edges: Q of round r-1, lane u owns targets u and u+64
-    // (Qs is a subset of Qf per vertex: the strong-only half runs only for the
-    // sources with a live Qs)
-    u64 nf0 = 0, nf1 = 0, ns0 = 0, ns1 = 0;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      u64 m = __ballot(qf[i] != 0ULL);
-      while (m) {
-        const int l = __builtin_ctzll(m);
-        m &= m - 1;
-        const u64 a = readlane64(ra[i], l), b = readlane64(rb[i], l), f = readlane64(qf[i], l);
-        nf0 |= ((a >> lane) & 1ULL) ? f : 0ULL;
-        nf1 |= ((b >> lane) & 1ULL) ? f : 0ULL;
-      }
-      u64 ms = __ballot(qs[i] != 0ULL);
-      while (ms) {
-        const int l = __builtin_ctzll(ms);
-        ms &= ms - 1;
-        const u64 a = readlane64(ra[i], l), b = readlane64(rb[i], l), sq = readlane64(qs[i], l);
-        ns0 |= ((a >> lane) & 1ULL) ? sq : 0ULL;
-        ns1 |= ((b >> lane) & 1ULL) ? sq : 0ULL;
-      }
+    // strong edges: round r-1's sets, and the strong degrees summed over G
+    u64 N0 = 0, N1 = 0, H0 = 0, H1 = 0;
+    if (haveK) {
+      u64 a, b;
+      uint32_t ds;
+      expand(K0, K1, a, b, nullptr);
+      if (eqF) { N0 = a; N1 = b; }
+      expand(KG0, KG1, a, b, &ds);
+      if (eqG) { H0 = a; H1 = b; suf += ds; }
     }
-    qf[0] = nf0;
-    qf[1] = nf1;
-    qs[0] = ns0;
-    qs[1] = ns1;
+    for (u64 m = soloF; m; m &= m - 1) {
+      const int b = __builtin_ctzll(m);
+      u64 x, y;
+      expand(readlane64(F0, b), readlane64(F1, b), x, y, nullptr);
+      if (lane == b) { N0 = x; N1 = y; }
+    }
+    for (u64 m = soloG; m; m &= m - 1) {
+      const int b = __builtin_ctzll(m);
+      u64 x, y;
+      uint32_t ds;
+      expand(readlane64(G0, b), readlane64(G1, b), x, y, &ds);
+      if (lane == b) { H0 = x; H1 = y; suf += ds; }
+    }
+    if (r >= 2 && ((r - 2) & 3) == 0) J.sufl[((r - 2) / 4 + 1) * 64 + lane] = suf;  // Suf_b(4(x-1)+2)
+    F0 = N0;
+    F1 = N1;
+    G0 = H0;
+    G1 = H1;
     __syncthreads();
   }
 
@@ -355,42 +396,41 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   // ---------------- 4. bottom-up emission ----------------
   // lane b = leader wave b+1 for the per-leader bookkeeping
   const int myfirst = first_pop[lane];
-  {
-    u64 bef = 0;  // leaders first popped before b (PAPER: they own shared vertices)
-    for (int x = 0; x < 64; x++) {
-      const int fp = first_pop[x];
-      if (fp >= 0 && myfirst >= 0 && fp < myfirst) bef |= 1ULL << x;
-    }
-    if (PAPER) BEF[lane] = bef;
-    CS[lane] = 0;
-    for (int k = 0; k < RS; k++) res[lane * RS + k] = 0;
+  int myrank = 0;  // PAPER: leaders first popped before b
+  for (int x = 0; x < 64; x++) {
+    const int fp = first_pop[x];
+    myrank += (fp >= 0 && myfirst >= 0 && fp < myfirst) ? 1 : 0;
   }
-  // chain segments of leader b cover rounds (lo_b, hi_b]
-  int seg_lo = 0x7fff, seg_hi = -1;
-  for (int x = 0; x <= 64; x++)
-    if (coef[lane * 65 + x]) {
-      seg_lo = min(seg_lo, 4 * (x - 1) + 1);
-      seg_hi = max(seg_hi, 4 * (x - 1) + 1);
-    }
+  if (PAPER && myfirst >= 0) ord[myrank] = (int8_t)lane;
+  for (int k = 0; k < RS; k++) res[lane * RS + k] = 0;
+  // chain edges: segment sums are differences of the suffix sums at the leader
+  // rounds (every leader's coefficients sum to zero; Suf = 0 above round T)
+  u64 chain = 0;
+  for (int x = 1; x < nw; x++) {
+    const int c = coef[lane * 65 + x];
+    if (c) chain -= (u64)((int64_t)c * (int64_t)J.sufl[x * 64 + lane]);
+  }
+  chain = wave_sum(chain);
   const u64 popped = __ballot(myfirst >= 0);
+  const int npopped = __popcll(popped);
+  __syncthreads();
   u64 neq = kmemo ? 0ULL : ~0ULL;   // leaders whose cone differs from K in some round <= r
   u64 kK = 0, dK = 0, eK = 0;       // K's count, digest, edges through round r-1
-  u64 chain = 0;
-  // one leader's (or K's, b = 63) delivered vertices of round r in slot order,
-  // positions from k0: count, digest, edges (wave-uniform); lanes = slots
-  // (sa, sb: the round's slots; slo / shi: its first 128 slot sources, lane-held)
-  auto contrib = [&](int r, int b, u64 k0, u64 befb, uint32_t sa, uint32_t sb, int slo, int shi, u64 &cnt, u64 &dg,
+  // delivered vertices of round r (the set s0|s1) in slot order, positions from
+  // k0: count, digest, edges (wave-uniform); lanes = slots (sa, sb: the round's
+  // slots; slo / shi: its first 128 slot sources, lane-held)
+  auto contrib = [&](int r, u64 s0, u64 s1, u64 k0, uint32_t sa, uint32_t sb, int slo, int shi, u64 &cnt, u64 &dg,
                      u64 &ed) {
     u64 k = k0, dacc = 0, eacc = 0;
     for (uint32_t c0 = sa; c0 < sb; c0 += 64) {
       const uint32_t sl = c0 + lane;
       const int s = c0 == sa ? slo : c0 == sa + 64 ? shi : (sl < sb ? (int)J.slot_src[sl] : 0);  // 0: ghost / none
-      const u64 f = s > 0 ? QF[s - 1] : 0ULL;
-      const bool in = ((f >> b) & 1ULL) && !(f & befb);
+      const int v = s - 1;
+      const bool in = s > 0 && ((((v < 64) ? s0 : s1) >> (v & 63)) & 1ULL);
       const u64 bal = __ballot(in);
       if (in) {
         dacc += digest_term((uint32_t)r, (uint32_t)s, k + (u64)__popcll(bal & ((1ULL << lane) - 1ULL)));
-        eacc += DG[s - 1] >> 16;
+        eacc += DG[v] >> 16;
       }
       k += (u64)__popcll(bal);
     }
@@ -398,23 +438,21 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
     dg = wave_sum(dacc);
     ed = wave_sum(eacc);
   };
-  // software pipeline: round r+1's Q, degrees, presence and slots load while
+  // software pipeline: round r+1's sets, degrees, presence and slots load while
   // round r is processed
-  u64 pf[2] = {0, 0}, ps[2] = {0, 0}, pp[2] = {0, 0};
+  u64 pf0 = 0, pf1 = 0, pp0 = 0, pp1 = 0;
   uint32_t pd[2] = {0, 0}, psa = 0, psb = 0;
   int pslo = 0, pshi = 0;
   auto prefetch4 = [&](int r) {
+    pf0 = J.cone[((size_t)r * 2) * 64 + lane];
+    pf1 = J.cone[((size_t)r * 2 + 1) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
-      if (v < n) {
-        const size_t at = (size_t)r * n + v;
-        pf[i] = J.qf[at];
-        ps[i] = J.qs[at];
-        pd[i] = J.deg[at];
-      }
-      pp[i] = pres_word(r, i);
+      if (v < n) pd[i] = J.deg[(size_t)r * n + v];
     }
+    pp0 = pres_word(r, 0);
+    pp1 = pres_word(r, 1);
     psa = J.slot_off[r];
     psb = J.slot_off[r + 1];
     pslo = psa + lane < psb ? (int)J.slot_src[psa + lane] : 0;
@@ -423,27 +461,21 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
   prefetch4(1);
   for (int r = 1; r <= T; r++) {
     __syncthreads();
-    const u64 f2[2] = {pf[0], pf[1]}, s2[2] = {ps[0], ps[1]}, p2[2] = {pp[0], pp[1]};
-    const uint32_t d2[2] = {pd[0], pd[1]}, sa = psa, sb = psb;
+    const u64 f0 = pf0, f1 = pf1, P0 = pp0, P1 = pp1;
+    const uint32_t sa = psa, sb = psb;
     const int slo = pslo, shi = pshi;
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
-      if (v < n) {
-        QF[v] = f2[i];
-        DG[v] = d2[i];
-      }
+      if (v < n) DG[v] = pd[i];
     }
     if (r < T) prefetch4(r + 1);
     __syncthreads();
-    const u64 active = popped & ~0ULL & __ballot(lane < nw && 4 * lane + 1 >= r);  // leaders whose top >= r
+    const u64 active = popped & __ballot(lane < nw && 4 * lane + 1 >= r);  // leaders whose top >= r
     if (!PAPER) {
       if (kmemo) {  // leaders whose cone first differs from K in round r take K's prefix
-        u64 x = 0;
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-          if ((p2[i] >> lane) & 1ULL) x |= f2[i] ^ (((f2[i] >> 63) & 1ULL) ? ~0ULL : 0ULL);
-        const u64 newly = wave_or(x) & active & ~neq;
+        const u64 K0 = readlane64(f0, 63), K1 = readlane64(f1, 63);
+        const u64 newly = __ballot((((f0 ^ K0) & P0) | ((f1 ^ K1) & P1)) != 0ULL) & active & ~neq;
         if ((newly >> lane) & 1ULL) {
           res[lane * RS + 0] = kK;
           res[lane * RS + 1] = dK;
@@ -451,7 +483,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
         }
         neq |= newly;
         u64 c, d, e;
-        contrib(r, 63, kK, 0ULL, sa, sb, slo, shi, c, d, e);
+        contrib(r, K0, K1, kK, sa, sb, slo, shi, c, d, e);
         kK += c;
         dK += d;
         eK += e;
@@ -460,7 +492,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
       for (u64 m = neq & active; m; m &= m - 1) {
         const int b = __builtin_ctzll(m);
         u64 c, d, e;
-        contrib(r, b, res[b * RS + 0], 0ULL, sa, sb, slo, shi, c, d, e);
+        contrib(r, readlane64(f0, b), readlane64(f1, b), res[b * RS + 0], sa, sb, slo, shi, c, d, e);
         __syncthreads();
         if (lane == 0) {
           res[b * RS + 0] += c;
@@ -477,17 +509,24 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
           res[b * RS + 2] = eK;
         }
       }
-    } else {
-      for (u64 m = active; m; m &= m - 1) {
-        const int b = __builtin_ctzll(m);
-        const u64 befb = BEF[b];
-        bool any = false;
+    } else if (active) {
+      // what the leaders popped before b hold: exclusive prefix OR over the popped
+      // leaders in first-pop order (lane j = the j-th), read back at b's rank
+      const int src = lane < npopped ? (int)ord[lane] : 0;
+      u64 y0 = shfl64(f0, src), y1 = shfl64(f1, src);
+      if (lane >= npopped) y0 = y1 = 0;
 #pragma unroll
-        for (int i = 0; i < 2; i++)
-          any |= ((p2[i] >> lane) & 1ULL) && ((f2[i] >> b) & 1ULL) && !(f2[i] & befb);
-        if (__ballot(any) == 0ULL) continue;
+      for (int off = 1; off < 64; off <<= 1) {
+        const u64 z0 = shfl_up64(y0, off), z1 = shfl_up64(y1, off);
+        if (lane >= off) { y0 |= z0; y1 |= z1; }
+      }
+      u64 e0 = shfl_up64(y0, 1), e1 = shfl_up64(y1, 1);
+      if (lane == 0) e0 = e1 = 0;
+      const u64 x0 = f0 & ~shfl64(e0, myrank), x1 = f1 & ~shfl64(e1, myrank);
+      for (u64 m = __ballot(((x0 & P0) | (x1 & P1)) != 0ULL) & active; m; m &= m - 1) {
+        const int b = __builtin_ctzll(m);
         u64 c, d, e;
-        contrib(r, b, res[b * RS + 3], befb, sa, sb, slo, shi, c, d, e);
+        contrib(r, readlane64(x0, b), readlane64(x1, b), res[b * RS + 3], sa, sb, slo, shi, c, d, e);
         __syncthreads();
         if (lane == 0) {
           res[b * RS + 3] += c;
@@ -497,24 +536,7 @@ __global__ __launch_bounds__(64) void k_replay_small(const SmallJob *__restrict_
         __syncthreads();
       }
     }
-    // chain edges: strong-degree sums over Qs in the leaders' segment rounds
-    for (u64 m = __ballot(lane < nw && seg_lo < r && r <= seg_hi); m; m &= m - 1) {
-      const int b = __builtin_ctzll(m);
-      u64 x = 0;
-#pragma unroll
-      for (int i = 0; i < 2; i++)
-        if ((s2[i] >> b) & 1ULL) x += d2[i] & 0xFFFFu;
-      x = wave_sum(x);
-      if (lane == 0) CS[b] += x;
-    }
-    __syncthreads();
-    if (((r - 1) & 3) == 0) {
-      const int x = (r - 1) / 4 + 1;
-      const int c = coef[lane * 65 + x];
-      if (c) chain += (u64)(int64_t)c * CS[lane];
-    }
   }
-  chain = wave_sum(chain);
   __syncthreads();
 
   // ---------------- 5. outputs ----------------

@@ -2824,8 +2824,8 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
       dr_ctx *c = ctxs[i];
       dr::SmallJob &J = jobs[i];
       const size_t nv = (size_t)(T + 1) * c->n;
-      J.qf = cv.take<u64>(nv);
-      J.qs = cv.take<u64>(nv);
+      J.cone = cv.take<u64>((size_t)(T + 1) * 128);
+      J.sufl = cv.take<uint32_t>(65 * 64);
       J.deg = cv.take<uint32_t>(nv);
     }
     cv.off = (cv.off + 255) & ~(size_t)255;

@@ -43,6 +43,14 @@ __device__ __forceinline__ u64 readlane64(u64 x, int l) {
   return ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
 }
+// lane l's value (ds_bpermute on both halves); every lane of the wave must be active
+__device__ __forceinline__ u64 shfl64(u64 x, int l) {
+  return ((u64)(uint32_t)__shfl((int)(x >> 32), l) << 32) | (uint32_t)__shfl((int)(uint32_t)x, l);
+}
+// lane (lane - d)'s value, own value for lane < d
+__device__ __forceinline__ u64 shfl_up64(u64 x, int d) {
+  return ((u64)(uint32_t)__shfl_up((int)(x >> 32), d) << 32) | (uint32_t)__shfl_up((int)(uint32_t)x, d);
+}
 // OR of all 64 lanes (wave-uniform result)
 __device__ __forceinline__ u64 wave_or(u64 x) {
   x |= dpp64<DPP_QP_1032>(x);
