@@ -665,11 +665,20 @@ hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc)
   return e;
 }
 // every round's WU, and its speculative canonical digest into RG (k_canon's spec check)
+// one LDS limit per k_weak_union instantiation (both launch sites share it)
+template <int WS>
+hipError_t weak_union_lds(const dr_ctx *c, size_t lds) {
+  static std::atomic<int> seen[kLdsDevs] = {};
+  return lds_limit((const void *)dr::k_weak_union<WS>, seen, c->dev, lds);
+}
 template <int WS>
 hipError_t launch_weak_union_t(dr_ctx *c, int T, hipStream_t st) {
   const int dd = c->memo_dd();
-  hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(T), dim3(256), 0, st, c->view(), T, dd, c->WU.as<u64>(),
-                     (const int32_t *)nullptr, c->ppref.as<u64>(), c->slot_off.as<uint32_t>(),
+  const size_t lds = (size_t)4 * std::max(dd, 1) * WS * 8;
+  hipError_t e = weak_union_lds<WS>(c, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_weak_union<WS>), dim3((T + 3) / 4), dim3(256), lds, st, c->view(), T, 0, dd,
+                     c->WU.as<u64>(), (const int32_t *)nullptr, c->ppref.as<u64>(), c->slot_off.as<uint32_t>(),
                      c->slot_src.as<uint16_t>(), c->RG.as<u64>());
   return hipGetLastError();
 }
@@ -694,9 +703,12 @@ hipError_t launch_round_summary_t(dr_ctx *c, const int32_t *rounds, int nr) {
                      c->U.as<u64>(), c->SD.as<u64>());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || mv.dd == 0) return e;
-  hipLaunchKernelGGL((dr::k_weak_union<WS, 256>), dim3(nr), dim3(256), 0, c->stream, c->view(), c->nrounds - 1,
-                     mv.dd, c->WU.as<u64>(), rounds, (const u64 *)nullptr, (const uint32_t *)nullptr,
-                     (const uint16_t *)nullptr, (u64 *)nullptr);
+  const size_t lds = (size_t)4 * mv.dd * WS * 8;
+  e = weak_union_lds<WS>(c, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_weak_union<WS>), dim3((nr + 3) / 4), dim3(256), lds, c->stream, c->view(),
+                     c->nrounds - 1, nr, mv.dd, c->WU.as<u64>(), rounds, (const u64 *)nullptr,
+                     (const uint32_t *)nullptr, (const uint16_t *)nullptr, (u64 *)nullptr);
   return hipGetLastError();
 }
 hipError_t launch_round_summary(dr_ctx *c, const int32_t *rounds, int nr) {
@@ -1567,6 +1579,11 @@ extern "C" int dr_debug_sweep_timing(uint64_t *out, int nq) {
   if (nq < 0 || nq > dr::kSweepTimingQ) return DR_E_INVAL;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(dr::g_sweep_timing), (size_t)nq * 128, 0, hipMemcpyDeviceToHost) ==
                  hipSuccess ? DR_OK : DR_E_HIP;
+}
+// k_canon's stamps of the last canonical cone (kernels.hpp g_canon_timing, 8 u64)
+extern "C" int dr_debug_canon_timing(uint64_t *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dr::g_canon_timing), 64, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? DR_OK : DR_E_HIP;
 }
 #endif
 
@@ -2756,25 +2773,22 @@ bool small_ok(const dr_ctx *c, int nwaves) {
   return c->n <= 128 && nwaves <= 64 && c->nfar == 0 && c->dmax_near < 32 && c->ndups == 0;
 }
 
-template <int DEPTH>
-hipError_t launch_small(hipStream_t s, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper,
-                        int rsl) {
-  const dim3 g(nj), b(64);
-  const size_t lds_tt = dr::small_lds_bytes<true, true>(rsl), lds_tf = dr::small_lds_bytes<true, false>(rsl);
-  const size_t lds_ft = dr::small_lds_bytes<false, true>(rsl), lds_ff = dr::small_lds_bytes<false, false>(rsl);
-  if (paper && persistent)
-    hipLaunchKernelGGL((dr::k_replay_small<DEPTH, true, true>), g, b, lds_tt, s, jobs,
-                       nj, nw, rsl);
-  else if (paper)
-    hipLaunchKernelGGL((dr::k_replay_small<DEPTH, true, false>), g, b, lds_tf, s,
-                       jobs, nj, nw, rsl);
-  else if (persistent)
-    hipLaunchKernelGGL((dr::k_replay_small<DEPTH, false, true>), g, b, lds_ft, s,
-                       jobs, nj, nw, rsl);
-  else
-    hipLaunchKernelGGL((dr::k_replay_small<DEPTH, false, false>), g, b, lds_ff, s,
-                       jobs, nj, nw, rsl);
+template <bool PAPER, bool PERSIST>
+hipError_t launch_small_t(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int nw, int D) {
+  const size_t lds = dr::small_lds_bytes(D, nw);
+  static std::atomic<int> seen[kLdsDevs] = {};
+  hipError_t e = lds_limit((const void *)dr::k_replay_small<PAPER, PERSIST>, seen, c->dev, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_replay_small<PAPER, PERSIST>), dim3(nj), dim3(dr::kSmallNT), lds, c->stream, jobs, nj,
+                     nw, D);
   return hipGetLastError();
+}
+hipError_t launch_small(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper,
+                        int D) {
+  if (paper) return persistent ? launch_small_t<true, true>(c, jobs, nj, nw, D)
+                               : launch_small_t<true, false>(c, jobs, nj, nw, D);
+  return persistent ? launch_small_t<false, true>(c, jobs, nj, nw, D)
+                    : launch_small_t<false, false>(c, jobs, nj, nw, D);
 }
 }  // namespace
 
@@ -2823,10 +2837,9 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     for (int i = 0; i < nctx; i++) {
       dr_ctx *c = ctxs[i];
       dr::SmallJob &J = jobs[i];
-      const size_t nv = (size_t)(T + 1) * c->n;
       J.cone = cv.take<u64>((size_t)(T + 1) * 128);
       J.sufl = cv.take<uint32_t>(65 * 64);
-      J.deg = cv.take<uint32_t>(nv);
+      J.deg = cv.take<uint32_t>(c->h_slot_off[T + 1]);  // per slot of rounds 0..T
     }
     cv.off = (cv.off + 255) & ~(size_t)255;
     out0 = cv.off;
@@ -2876,12 +2889,8 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     }
     const int persistent = chain_mode == DR_CHAIN_PERSISTENT, paper = deliver_mode == DR_DELIVER_PAPER;
     HIPCHK(c0, hipEventRecord(c0->ev[0], c0->stream));
-    const int need = next_pow2(dmax + 1);
-    const int rsl = dmax + 1;  // ring slots (batch.hpp k_replay_small)
-    hipError_t e = need <= 8    ? launch_small<8>(c0->stream, jt, nctx, nw, persistent, paper, rsl)
-                   : need <= 16 ? launch_small<16>(c0->stream, jt, nctx, nw, persistent, paper, rsl)
-                                : launch_small<32>(c0->stream, jt, nctx, nw, persistent, paper, rsl);
-    HIPCHK(c0, e);
+    const int D = next_pow2(dmax + 1);  // ring slots (batch.hpp k_replay_small): <= 32
+    HIPCHK(c0, launch_small(c0, jt, nctx, nw, persistent, paper, D));
     HIPCHK(c0, hipEventRecord(c0->ev[1], c0->stream));
   }
   // results: one bulk copy of the output region of the arena

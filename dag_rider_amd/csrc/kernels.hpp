@@ -46,6 +46,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // included), the partial rounds' expansion, the total, and the round counts
 constexpr int kSweepTimingQ = 8192;
 __device__ u64 g_sweep_timing[16 * kSweepTimingQ];
+__device__ u64 g_canon_timing[8];  // k_canon: start, segments walked, positions done, segment count, rounds walked
 #define DR_TT(...) __VA_ARGS__
 #else
 #define DR_TT(...)
@@ -1246,56 +1247,70 @@ __global__ __launch_bounds__(NT) void k_set_weak(DagView g, int r0, int depth_lo
 }
 
 // WU_r[delta] = the union of round r's weak targets at distance delta, one
-// workgroup per round r = blockIdx.x + 1 (or rounds[blockIdx.x]: incremental).
+// wavefront per round, four rounds per workgroup: round r = 4 blockIdx.x + wave
+// + 1 <= T (or rounds[4 blockIdx.x + wave] for the first nr entries:
+// incremental).  No workgroup barrier: each wave ORs the round's weak-column keys
+// into its own LDS slice (dynamic LDS, 4 x dd x WS u64).
 //
 // With RG (a full replay): also the speculative canonical digest of round r,
 // assuming every round 1..r full (K_y covers P_y): every present vertex of r
 // (every non-ghost slot, in slot order) delivered at positions from ppref[r-1]
 // = |P_1| + .. + |P_{r-1}|.  k_canon lowers *rlo to the lowest round where that
 // assumption fails; the canonical emission recomputes only rounds >= *rlo.
-template <int WS, int NT>
-__global__ __launch_bounds__(NT) void k_weak_union(DagView g, int T, int dd, u64 *__restrict__ WU,
-                                                   const int32_t *__restrict__ rounds,
-                                                   const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
-                                                   const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG) {
-  __shared__ u64 sWU[64 * WS];  // dd <= 64 (dr_ctx::memo_ok)
-  __shared__ u64 s_sc[NT / 64], s_rg;
-  const int r = rounds ? rounds[blockIdx.x] : blockIdx.x + 1, tid = threadIdx.x;
-  if (r > T) return;
-  for (int i = tid; i < dd * WS; i += NT) sWU[i] = 0;
-  if (tid == 0) s_rg = 0;
-  __syncthreads();
-  // every weak-column entry has at least one source: its key alone is the union
-  for (uint32_t j = g.wc_roff[r] + tid; j < g.wc_roff[r + 1]; j += NT) {
-    const uint32_t key = g.wc_key[j];
-    atomicOr(&sWU[((key >> 11) - 2) * WS + ((key & 2047u) >> 6)], 1ULL << (key & 63u));
+template <int WS>
+__global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, int dd, u64 *__restrict__ WU,
+                                                    const int32_t *__restrict__ rounds,
+                                                    const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
+                                                    const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG) {
+  extern __shared__ __attribute__((aligned(16))) u64 wu_lds[];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + wid;
+  int r;
+  if (rounds) {
+    if (i >= nr) return;
+    r = rounds[i];
+  } else {
+    r = i + 1;
   }
-  if (RG) {  // block-uniform
-    constexpr int SPT = 4;  // slots per thread per pass
+  if (r > T) return;  // wave-uniform: this wave alone
+  u64 *sW = wu_lds + (size_t)wid * dd * WS;
+  for (int k = lane; k < dd * WS; k += 64) sW[k] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // every weak-column entry has at least one source: its key alone is the union
+  for (uint32_t j = g.wc_roff[r] + lane; j < g.wc_roff[r + 1]; j += 64) {
+    const uint32_t key = g.wc_key[j];
+    atomicOr(&sW[((key >> 11) - 2) * WS + ((key & 2047u) >> 6)], 1ULL << (key & 63u));
+  }
+  if (RG) {  // the round's slots in lane-contiguous runs of SPT
+    constexpr int SPT = 8;
     const uint32_t sa = slot_off[r], sb = slot_off[r + 1];
     u64 pos = ppref[r - 1], dg = 0;
-    for (uint32_t c0 = sa; c0 < sb; c0 += NT * SPT) {
-      const uint32_t i0 = c0 + (uint32_t)tid * SPT;
+    for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPT) {
+      const uint32_t i0 = c0 + (uint32_t)lane * SPT;
       uint32_t src[SPT];
-      int cnt = 0;
+      uint32_t cnt = 0;
 #pragma unroll
       for (int j = 0; j < SPT; j++) {
         src[j] = i0 + j < sb ? slot_src[i0 + j] : 0u;
         cnt += src[j] != 0;
       }
-      u64 tot;
-      u64 k = pos + block_scan_excl<NT>((u64)cnt, s_sc, tot);
+      uint32_t inc = cnt;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+      }
+      u64 k = pos + (inc - cnt);
 #pragma unroll
       for (int j = 0; j < SPT; j++)
         if (src[j]) dg += digest_term((uint32_t)r, src[j], k++);
-      pos += tot;
+      pos += __shfl(inc, 63);
     }
     dg = wave_sum(dg);
-    if ((tid & 63) == 0 && dg) atomicAdd(&s_rg, dg);
+    if (lane == 0) RG[r] = dg;
   }
-  __syncthreads();
-  for (int i = tid; i < dd * WS; i += NT) WU[(size_t)r * dd * WS + i] = sWU[i];
-  if (RG && tid == 0) RG[r] = s_rg;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (int k = lane; k < dd * WS; k += 64) WU[(size_t)r * dd * WS + k] = sW[k];
 }
 
 // K^cand_r = U_{r+1} | OR_d WU_{r+d+2}[d] (the cone of round r when every round
@@ -1375,6 +1390,8 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
   const int tid = threadIdx.x;
   int pos = T;  // rounds >= pos are final; the regime holds below pos until the next bad round
   int segs = 0;
+  int lo_w = T + 1;  // the lowest round a segment walk reached (RD below it is the full count)
+  DR_TT(int walked = 0; if (tid == 0) g_canon_timing[0] = wall_clock64();)
   while (true) {
     // next bad round below pos: thread t looks at the 8 rounds of block (pos-1)/8 - t - i*NT
     if (tid == 0) s_ctl[0] = -1;
@@ -1453,19 +1470,36 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
       }
       e += we;
       if (e) atomicAdd(&s_edges[0], e);
+      DR_TT(walked++;)
       __syncthreads();
       if (tid == 0) CE[r] = s_edges[0];
       cur = nxt;
       __syncthreads();
     }
     pos = r;
+    lo_w = min(lo_w, r);
   }
   if (tid == 0 && nseg) *nseg = segs;
+  DR_TT(if (tid == 0) {
+    g_canon_timing[1] = wall_clock64();
+    g_canon_timing[3] = segs;
+    g_canon_timing[4] = walked;
+  })
   // canonical positions (the RD writes above are this workgroup's own: visible after the barrier)
+  // With ppref (a full cone), every round below the lowest walked one holds all its
+  // present vertices (a bad round starts a walk): C there is the presence prefix,
+  // copied; the scan covers the walked region only (C4, C3: the top ~10 rounds).
   __syncthreads();
   __shared__ u64 part[NT / 64];
-  const int per = (T + 1 + NT - 1) / NT;
-  const int ra = tid * per, rb = min(T + 1, ra + per);
+  const int B = ppref ? lo_w : 0;
+#pragma unroll 8
+  for (int x = tid; x < B; x += NT) {
+    Cc[x] = ppref[x];
+    crbase[x] = x >= 1 ? (uint32_t)ppref[x - 1] : 0u;
+  }
+  const u64 base0 = (ppref && B >= 1) ? ppref[B - 1] : 0ULL;
+  const int per = (T + 1 - B + NT - 1) / NT;
+  const int ra = B + tid * per, rb = min(T + 1, ra + per);
   int bad = INT_MAX;  // ppref: the lowest round whose C differs from the all-full prefix
   constexpr int MAXP = 16;
   if (per <= MAXP) {  // block-uniform: every load in flight at once
@@ -1478,7 +1512,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
       loc += v[j];
     }
     u64 tot;
-    u64 run = block_scan_excl<NT>(loc, part, tot);
+    u64 run = base0 + block_scan_excl<NT>(loc, part, tot);
 #pragma unroll
     for (int j = 0; j < MAXP; j++) {
       const int x = ra + j;
@@ -1492,7 +1526,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     u64 loc = 0;
     for (int x = ra; x < rb; x++) loc += RD[x];
     u64 tot;
-    u64 run = block_scan_excl<NT>(loc, part, tot);
+    u64 run = base0 + block_scan_excl<NT>(loc, part, tot);
     for (int x = ra; x < rb; x++) {
       crbase[x] = (uint32_t)run;
       run += RD[x];
@@ -1508,6 +1542,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     __syncthreads();
     if (tid == 0 && s_bad != INT_MAX) atomicMin(rlo, s_bad);
   }
+  DR_TT(if (tid == 0) g_canon_timing[2] = wall_clock64();)
 }
 
 // ---------------------------------------------------------------------------
