@@ -22,6 +22,8 @@ DR_WEAK_LITERAL, DR_WEAK_PAPER = 0, 1
 DR_OPT_MEMO = 1
 DR_OPT_DEVICE_PLAN = 2
 DR_OPT_PHASE_TIMING = 3
+DR_OPT_BATCH_FORM = 4
+DR_BATCH_AUTO, DR_BATCH_WORKGROUP, DR_BATCH_WAVE = 0, 1, 2
 DR_LEADER_CONST1, DR_LEADER_SEEDED, DR_LEADER_TABLE = 0, 1, 2
 DR_SHARD_ID_BYTES = 128
 DR_SHARD_OPT_PERSISTENT = 1

@@ -110,6 +110,7 @@ struct SmallRound {
   u64 p0, p1;          // presence
   u64 cw0, cw1;        // the first 64 weak columns: lane j's source row ...
   uint32_t ckey;       // ... and key
+  uint32_t c0, c1;     // the round's weak columns
 };
 // round r's data for the emission: every lane's set (lane = leader) and the
 // first 128 slots (lane = slot)
@@ -119,9 +120,9 @@ struct EmitRound {
   uint32_t dg[2];
 };
 
-template <bool PAPER, bool PERSIST>
-__global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__restrict__ jobs, int njobs, int nw,
-                                                           int D) {
+template <int D, bool PAPER, bool PERSIST>
+__global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__restrict__ jobs, int njobs, int nw) {
+  static_assert(D >= 2 && D <= 32 && (D & (D - 1)) == 0, "ring slots: a power of two");
   constexpr bool chain_persistent = PERSIST;  // persistent chains push every wave at most once: <= 64 pops
   constexpr int kMaxPops = PERSIST ? 64 : kSmallMaxPops;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__res
   const bool haveK = nw <= 63;         // lane 63 carries K when it is not a leader
   const bool kmemo = !PAPER && haveK;  // REF: leaders take K's prefix below their lowest difference
   extern __shared__ __attribute__((aligned(16))) u64 arena[];
-  const int M = D - 1;                                                         // ring slot = round & M
+  constexpr int M = D - 1;                                                     // ring slot = round & M
   u64 *ring = arena;                                                           // [D][2][64], pass 2F
   u64 *KWt = arena + (size_t)D * 128;                                          // [D][D][2], pass 2F
   uint16_t *cnt = reinterpret_cast<uint16_t *>(KWt + (size_t)D * D * 2);      // [T+1][64]
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__res
   }
   for (int i = tid; i < 64 * 3; i += kSmallNT) res[i] = 0;
   __syncthreads();
+  const int my_lead = lane < nw ? s_lead[lane + 1] - 1 : 0;  // lane w-1: chooseLeader(w), 0-based
 
   auto row2 = [&](int r, int v, u64 &a, u64 &b) {  // row of (r, v+1); zero for v >= n
     a = 0;
@@ -228,7 +230,9 @@ __global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__res
     d.p0 = g_present[(size_t)r * WS];
     d.p1 = WS > 1 ? g_present[(size_t)r * WS + 1] : 0ULL;
     if (weak) {
-      const uint32_t c1 = s_roff[r + 1], jc = s_roff[r] + lane;
+      d.c0 = s_roff[r];
+      d.c1 = s_roff[r + 1];
+      const uint32_t c1 = d.c1, jc = d.c0 + lane;
       const uint32_t jl = jc < c1 ? jc : (c1 > 0 ? c1 - 1 : 0);
       d.ckey = g_wc_key[jl];
       d.cw0 = g_wc_rows[(size_t)jl * WS];
@@ -236,6 +240,7 @@ __global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__res
     } else {
       d.ckey = 0;
       d.cw0 = d.cw1 = 0;
+      d.c0 = d.c1 = 0;
     }
   };
   // OR of the rows of the set (s0, s1) (wave-uniform), and optionally the sum of
@@ -285,22 +290,24 @@ __global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__res
       F1 |= ring[(sl * 2 + 1) * 64 + lane];
       ring[(sl * 2) * 64 + lane] = 0;
       ring[(sl * 2 + 1) * 64 + lane] = 0;
-      if (haveK)  // K's weak targets from rounds r+d, for the lanes whose set was K's there
-        for (int dl = 2; dl < D; dl++) {
-          const u64 *kw = KWt + ((size_t)((r + dl) & M) * D + dl) * 2;
-          const u64 k0 = kw[0], k1 = kw[1];
+      if (haveK) {  // K's weak targets from rounds r+d, for the lanes whose set was K's there
+        u64x2 kw[D];
+#pragma unroll
+        for (int dl = 2; dl < D; dl++) kw[dl] = *reinterpret_cast<const u64x2 *>(KWt + (((r + dl) & M) * D + dl) * 2);
+#pragma unroll
+        for (int dl = 2; dl < D; dl++)
           if ((E >> (dl - 1)) & 1u) {
-            F0 |= k0;
-            F1 |= k1;
+            F0 |= kw[dl].x;
+            F1 |= kw[dl].y;
           }
-        }
+      }
       if (haveK && r == T && lane == 63) {  // K: every present vertex of the top round
         F0 |= d.p0;
         F1 |= d.p1;
       }
       if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its lane with the leader's vertex
         const int w = (r - 1) / 4 + 1;
-        const int l = s_lead[w] - 1;
+        const int l = __builtin_amdgcn_readlane(my_lead, w - 1);
         const bool present = (((l < 64) ? d.p0 : d.p1) >> (l & 63)) & 1ULL;
         if (present && lane == w - 1) {
           if (l < 64) F0 |= 1ULL << l; else F1 |= 1ULL << (l - 64);
@@ -323,7 +330,7 @@ __global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__res
       // weak columns of round r (64 per batch, lane j holding column j; the first
       // batch came with the round): a column's target joins b's pending round iff
       // its sources meet F_b
-      const uint32_t c0 = s_roff[r], c1 = s_roff[r + 1];
+      const uint32_t c0 = d.c0, c1 = d.c1;
       if (lane < 2 * D) KWt[(size_t)sl * D * 2 + lane] = 0;  // round r+D's targets: consumed above r
       wave_lds_fence();
       u64 cw0 = d.cw0, cw1 = d.cw1;
@@ -438,7 +445,7 @@ __global__ __launch_bounds__(kSmallNT) void k_replay_small(const SmallJob *__res
         }
         if (((r - 1) & 3) == 0) {
           const int w = (r - 1) / 4 + 1;
-          const int l = s_lead[w] - 1;
+          const int l = __builtin_amdgcn_readlane(my_lead, w - 1);
           if ((lead_mask >> (w - 1)) & 1ULL) {
             if (lane == w - 1 && alive) {
               if (l < 64) G0 |= 1ULL << l; else G1 |= 1ULL << (l - 64);

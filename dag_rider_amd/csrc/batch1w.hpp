@@ -1,0 +1,533 @@
+// batch1w.hpp -- the throughput form of the fused small-DAG replay: one
+// wavefront per DAG (batch.hpp holds the workgroup-per-DAG form and the job
+// layout).  A wave walks its DAG's phases in order: commits, one bit-sliced
+// top-down cone pass (lane b = leader b, lane 63 = the canonical cone K) for the
+// strong+weak sets F_b and their strong-only twins G_b, chains from the leaders'
+// strong cones, then a bottom-up emission in which a leader equal to K below its
+// top takes K's prefix.  Sixteen DAGs share a CU, so when a
+// batch holds many DAGs per CU (C5 on one GPU: 4096 / 256 CUs) the SIMDs stay
+// busy and the batch's total work bounds it; dr_replay_batch picks this form
+// there and the four-wave form when each CU holds only a few DAGs (one GPU's
+// share at N = 8).  Same semantics and limits as batch.hpp.
+#pragma once
+#include "batch.hpp"
+
+namespace dr {
+
+// dynamic LDS of k_replay_small_1w: the weak ring (rsl slots of 128 u64) or the
+// later phases' arrays, whichever is larger
+template <bool PAPER, bool PERSIST>
+constexpr int small1w_late_bytes() {  // coef, pop list, per-leader results
+  return 64 * 65 + (((PERSIST ? 64 : kSmallMaxPops) + 255) & ~255) + 64 * (PAPER ? 6 : 3) * 8;
+}
+template <bool PAPER, bool PERSIST>
+inline size_t small1w_lds_bytes(int rsl) {
+  const size_t ring = (size_t)rsl * 128 * 8, late = (size_t)small1w_late_bytes<PAPER, PERSIST>();
+  return ring > late ? ring : late;
+}
+
+template <bool PAPER, bool PERSIST>
+__global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restrict__ jobs, int njobs, int nw, int rsl) {
+  constexpr bool paper = PAPER;  // REF mode skips the paper-mode digests entirely
+  constexpr bool chain_persistent = PERSIST;  // persistent chains push every wave at most once: <= 64 pops
+  // LDS is what limits DAGs per CU: the weak ring (phase 2 only) shares its
+  // bytes with the chain coefficients, pop list and per-leader results (phases
+  // 3-5, which start after phase 2's last barrier).
+  constexpr int kMaxPops = PERSIST ? 64 : kSmallMaxPops;
+  constexpr int RS = PAPER ? 6 : 3;  // per-leader results kept
+  constexpr int kCoefB = 64 * 65, kPopB = (kMaxPops + 255) & ~255, kResB = 64 * RS * 8;
+  static_assert(kCoefB + kPopB + kResB == small1w_late_bytes<PAPER, PERSIST>(), "LDS layout");
+  // lane 63 carries the canonical cone K when it is not a leader
+  const bool haveK = nw <= 63;
+  const bool kmemo = !PAPER && haveK;  // REF memo: leaders take K's prefix below their first difference
+  extern __shared__ __attribute__((aligned(16))) u64 arena[];                  // small_lds_bytes(rsl)
+  u64 *ring = arena;                                                            // [rsl][2][64], phase 2
+  int8_t *coef = reinterpret_cast<int8_t *>(arena);                             // [64 * 65], phases 3-4
+  uint8_t *pop_lead = reinterpret_cast<uint8_t *>(arena) + kCoefB;              // [kSmallMaxPops], 3-5
+  u64 *res = reinterpret_cast<u64 *>(reinterpret_cast<char *>(arena) + ((kCoefB + kPopB + 7) & ~7));  // 4-5
+  __shared__ u64 KW[64];            // K's weak targets of the current round, [delta][word]
+  __shared__ uint32_t DG[128];
+  __shared__ u64 QL[64];
+  __shared__ int32_t vc_s[64];
+  __shared__ int16_t first_pop[64];
+  __shared__ int16_t qs_floor[64];  // lowest round where leader b's strong cone is still inspected
+  __shared__ int8_t lst[64];
+  __shared__ int8_t ord[64];        // PAPER: popped leaders in first-pop order
+  const int lane = threadIdx.x;
+  const int jb = blockIdx.x;
+  if (jb >= njobs) return;
+  const SmallJob J = jobs[jb];
+  auto g_strong = as_global(J.strong);
+  auto g_present = as_global(J.present);
+  auto g_wc_key = as_global(J.wc_key);
+  auto g_wc_rows = as_global(J.wc_rows);
+  auto g_wc_roff = as_global(J.wc_roff);
+  auto g_wdeg = as_global(J.wdeg);
+  auto g_slot_off = as_global(J.slot_off);
+  auto g_slot_src = as_global(J.slot_src);
+  auto g_lead = as_global(J.lead);
+  auto g_cone = as_global(J.cone);
+  auto g_sufl = as_global(J.sufl);
+  auto g_deg = as_global(J.deg);
+  auto g_commit = as_global(J.commit);
+  auto g_vcount = as_global(J.vcount);
+  auto g_push_off = as_global(J.push_off);
+  auto g_push_wave = as_global(J.push_wave);
+  auto g_pop_count = as_global(J.pop_count);
+  auto g_pop_digest = as_global(J.pop_digest);
+  auto g_pop_edges = as_global(J.pop_edges);
+  auto g_totals = as_global(J.totals);
+  const int n = J.n, WS = J.WS;
+  const int q = J.quorum;
+  const int T = 4 * (nw - 1) + 1;
+  auto row = [&](int r, int v, u64 &a, u64 &b) {  // row of (r, v+1); zero for v >= n
+    a = 0;
+    b = 0;
+    if (v < n) {
+      const u64 DR_GLOBAL *p = g_strong + ((size_t)r * n + v) * WS;
+      if (WS == 2) {
+        const u64x2 x = *reinterpret_cast<const u64x2 DR_GLOBAL *>(p);
+        a = x.x;
+        b = x.y;
+      } else {
+        a = p[0];
+      }
+    }
+  };
+  auto pres_word = [&](int r, int w) -> u64 { return w < WS ? g_present[(size_t)r * WS + w] : 0ULL; };
+
+  // ---------------- 1. commits ----------------
+  u64 commit_mask = 0, lead_mask = 0, commit_edges = 0;
+  for (int w = 1; w <= nw; w++) {
+    const int r1 = 4 * (w - 1) + 1;
+    const int l = g_lead[w] - 1;  // chooseLeader(w), 0-based (< 128)
+    const bool lead = (pres_word(r1, l >> 6) >> (l & 63)) & 1ULL;
+    if (!lead) {
+      if (lane == 0) vc_s[w - 1] = -1;
+      continue;
+    }
+    lead_mask |= 1ULL << (w - 1);
+    u64 a[3][2], b[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      row(r1 + 1 + k, lane, a[k][0], b[k][0]);
+      row(r1 + 1 + k, lane + 64, a[k][1], b[k][1]);
+    }
+    u64 s0 = l < 64 ? 1ULL << l : 0ULL, s1 = l >= 64 ? 1ULL << (l - 64) : 0ULL, deg = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int r = r1 + 1 + k;
+      const u64 p0 = pres_word(r, 0), p1 = pres_word(r, 1);
+      const bool h0 = ((p0 >> lane) & 1ULL) && (((a[k][0] & s0) | (b[k][0] & s1)) != 0ULL);
+      const bool h1 = ((p1 >> lane) & 1ULL) && (((a[k][1] & s0) | (b[k][1] & s1)) != 0ULL);
+      s0 = __ballot(h0);
+      s1 = __ballot(h1);
+      deg += (u64)(__popcll(a[k][0]) + __popcll(b[k][0]) + __popcll(a[k][1]) + __popcll(b[k][1]));
+    }
+    commit_edges += wave_sum(deg);
+    const int vc = __popcll(s0) + __popcll(s1);
+    if (lane == 0) vc_s[w - 1] = vc;
+    if (vc >= q) commit_mask |= 1ULL << (w - 1);
+  }
+
+  // ---------------- 2. top-down cone pass (lane b: leader b's sets) ----------------
+  for (int i = lane; i < rsl * 128; i += 64) ring[i] = 0;
+  KW[lane] = 0;
+  // chains (process.go:341-350) inspect leader b's strong cone only down to the
+  // floor round of the commit whose chain can push b: 4*decidedWave + 1
+  qs_floor[lane] = 0x7fff;
+  __syncthreads();
+  if (lane == 0) {
+    int lastc = 0;
+    for (int w = 1; w <= nw; w++)
+      if ((commit_mask >> (w - 1)) & 1ULL) {
+        for (int b = lastc + 1; b <= w; b++) qs_floor[b - 1] = (int16_t)(chain_persistent ? 4 * lastc + 1 : 1);
+        lastc = w;
+      }
+  }
+  __syncthreads();
+  const int my_floor = qs_floor[lane];
+  u64 F0 = 0, F1 = 0;  // F_b: round-r vertices in leader b's cone
+  u64 G0 = 0, G1 = 0;  // G_b: the same over strong edges only
+  uint32_t suf = 0;    // strong degrees summed over G_b, rounds r..T
+  // round r's vertices (lanes v, v + 64): rows, strong degrees; b's expansion over its set
+  u64 ra[2], rb[2];
+  uint32_t sd[2];
+  auto expand = [&](u64 s0, u64 s1, u64 &n0, u64 &n1, uint32_t *dsum) {  // s: wave-uniform
+    const bool m0 = (s0 >> lane) & 1ULL, m1 = (s1 >> lane) & 1ULL;
+    n0 = wave_or((m0 ? ra[0] : 0ULL) | (m1 ? ra[1] : 0ULL));
+    n1 = WS > 1 ? wave_or((m0 ? rb[0] : 0ULL) | (m1 ? rb[1] : 0ULL)) : 0ULL;
+    if (dsum) *dsum = (uint32_t)wave_sum((u64)((m0 ? sd[0] : 0u) + (m1 ? sd[1] : 0u)));
+  };
+  // software pipeline: round r-1's rows and first 64 weak columns (they do not
+  // depend on the cones) load while round r is processed
+  u64 nra[2], nrb[2], nw0 = 0, nw1 = 0;
+  uint32_t nkey = 0, nc0 = 0, nc1 = 0;
+  auto prefetch2 = [&](int r) {
+    row(r, lane, nra[0], nrb[0]);
+    row(r, lane + 64, nra[1], nrb[1]);
+    nc0 = g_wc_roff[r];
+    nc1 = g_wc_roff[r + 1];
+    const uint32_t jc = nc0 + lane;
+    nkey = 0;
+    nw0 = nw1 = 0;
+    if (jc < nc1) {
+      nkey = g_wc_key[jc];
+      nw0 = g_wc_rows[(size_t)jc * WS];
+      nw1 = WS > 1 ? g_wc_rows[(size_t)jc * WS + 1] : 0ULL;
+    }
+  };
+  prefetch2(T);
+  for (int r = T; r >= 1; r--) {
+    const bool alive = (lane < nw && my_floor <= r) || (haveK && lane == 63);
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      ra[i] = nra[i];
+      rb[i] = nrb[i];
+      sd[i] = (uint32_t)(__popcll(ra[i]) + __popcll(rb[i]));
+    }
+    u64 cw0 = nw0, cw1 = nw1;
+    uint32_t ckey = nkey;
+    const uint32_t c0 = nc0, c1 = nc1;
+    if (r > 1) prefetch2(r - 1);
+    {  // pending weak targets of round r
+      const int sl = r % rsl;
+      F0 |= ring[(sl * 2) * 64 + lane];
+      F1 |= ring[(sl * 2 + 1) * 64 + lane];
+      ring[(sl * 2) * 64 + lane] = 0;
+      ring[(sl * 2 + 1) * 64 + lane] = 0;
+    }
+    if (!alive) G0 = G1 = 0;
+    if (haveK && r == T && lane == 63) {  // K: every present vertex of the top round
+      F0 |= pres_word(T, 0);
+      F1 |= pres_word(T, 1);
+      G0 = F0;
+      G1 = F1;
+    }
+    if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its lane with the leader's vertex
+      const int w = (r - 1) / 4 + 1;
+      const int l = g_lead[w] - 1;
+      if ((lead_mask >> (w - 1)) & 1ULL) {
+        const u64 bit = 1ULL << (l & 63);
+        if (lane == w - 1) {
+          if (l < 64) F0 |= bit; else F1 |= bit;
+          if (alive) { if (l < 64) G0 |= bit; else G1 |= bit; }
+        }
+        // the leaders whose strong cone holds this leader's vertex (the chains' test)
+        const u64 ql = __ballot(lane < nw && ((((l < 64) ? G0 : G1) >> (l & 63)) & 1ULL));
+        if (lane == 0) QL[w - 1] = ql;
+      } else if (lane == 0) {
+        QL[w - 1] = 0;
+      }
+    }
+    g_cone[((size_t)r * 2) * 64 + lane] = F0;
+    g_cone[((size_t)r * 2 + 1) * 64 + lane] = F1;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int v = lane + 64 * i;
+      if (v < n) {
+        const size_t at = (size_t)r * n + v;
+        g_deg[at] = ((sd[i] + g_wdeg[at]) << 16) | sd[i];
+      }
+    }
+    // K (lane 63) and the leaders whose sets differ from it ("solo": expanded on their own)
+    u64 K0 = 0, K1 = 0, KG0 = 0, KG1 = 0;
+    if (haveK) {
+      K0 = readlane64(F0, 63);
+      K1 = readlane64(F1, 63);
+      KG0 = readlane64(G0, 63);
+      KG1 = readlane64(G1, 63);
+    }
+    const bool eqF = haveK && F0 == K0 && F1 == K1, eqG = haveK && G0 == KG0 && G1 == KG1;
+    const u64 soloF = __ballot(!eqF && (F0 | F1) != 0ULL), soloG = __ballot(!eqG && (G0 | G1) != 0ULL);
+    // weak columns of round r (64 per batch, lane j holding column j; the first
+    // batch was prefetched): a column's target joins b's pending round iff its
+    // sources meet F_b
+    for (uint32_t cb = c0; cb < c1; cb += 64) {
+      if (cb != c0) {
+        const uint32_t jc = cb + lane;
+        ckey = 0;
+        cw0 = cw1 = 0;
+        if (jc < c1) {
+          ckey = g_wc_key[jc];
+          cw0 = g_wc_rows[(size_t)jc * WS];
+          cw1 = WS > 1 ? g_wc_rows[(size_t)jc * WS + 1] : 0ULL;
+        }
+      }
+      const int delta = (int)(ckey >> 11), ts = (int)(ckey & 2047u);
+      const bool live = (cw0 | cw1) != 0ULL && r - delta >= 1;
+      const u64 tb = 1ULL << (ts & 63);
+      const int tw = ts >> 6, tsl = live ? (r - delta) % rsl : 0;
+      if (haveK && live && ((cw0 & K0) | (cw1 & K1)) != 0ULL) atomicOr(&KW[delta * 2 + tw], tb);
+      for (u64 m = soloF; m; m &= m - 1) {
+        const int b = __builtin_ctzll(m);
+        const u64 s0 = readlane64(F0, b), s1 = readlane64(F1, b);
+        if (live && ((cw0 & s0) | (cw1 & s1)) != 0ULL) atomicOr(&ring[(tsl * 2 + tw) * 64 + b], tb);
+      }
+    }
+    __syncthreads();
+    if (haveK && c0 < c1) {  // K's weak targets to every lane whose set is K's
+      for (int d = 1; d < rsl && r - d >= 1; d++) {
+        const u64 k0 = KW[d * 2], k1 = KW[d * 2 + 1];
+        if ((k0 | k1) && eqF) {
+          const int tsl = (r - d) % rsl;
+          ring[(tsl * 2) * 64 + lane] |= k0;
+          ring[(tsl * 2 + 1) * 64 + lane] |= k1;
+        }
+      }
+      __syncthreads();
+      KW[lane] = 0;
+    }
+    // strong edges: round r-1's sets, and the strong degrees summed over G
+    u64 N0 = 0, N1 = 0, H0 = 0, H1 = 0;
+    if (haveK) {
+      u64 a, b;
+      uint32_t ds;
+      expand(K0, K1, a, b, nullptr);
+      if (eqF) { N0 = a; N1 = b; }
+      expand(KG0, KG1, a, b, &ds);
+      if (eqG) { H0 = a; H1 = b; suf += ds; }
+    }
+    for (u64 m = soloF; m; m &= m - 1) {
+      const int b = __builtin_ctzll(m);
+      u64 x, y;
+      expand(readlane64(F0, b), readlane64(F1, b), x, y, nullptr);
+      if (lane == b) { N0 = x; N1 = y; }
+    }
+    for (u64 m = soloG; m; m &= m - 1) {
+      const int b = __builtin_ctzll(m);
+      u64 x, y;
+      uint32_t ds;
+      expand(readlane64(G0, b), readlane64(G1, b), x, y, &ds);
+      if (lane == b) { H0 = x; H1 = y; suf += ds; }
+    }
+    if (r >= 2 && ((r - 2) & 3) == 0) g_sufl[((r - 2) / 4 + 1) * 64 + lane] = suf;  // Suf_b(4(x-1)+2)
+    F0 = N0;
+    F1 = N1;
+    G0 = H0;
+    G1 = H1;
+    __syncthreads();
+  }
+
+  // ---------------- 3. chains and pops (wave-uniform scalar code) ----------------
+  for (int i = lane; i < 64 * 65; i += 64) coef[i] = 0;
+  if (lane < 64) first_pop[lane] = -1;
+  __syncthreads();
+  int npush = 0, npop = 0, last = 0;
+  for (int w = 1; w <= nw; w++) {
+    if (lane == 0) g_push_off[w - 1] = (uint32_t)npush;
+    if (!((commit_mask >> (w - 1)) & 1ULL)) continue;
+    const int floor_w = chain_persistent ? last : 0;
+    // pushed leaders of this commit, push order (every lane writes the same
+    // values to lst: the list stays in LDS, not in per-lane scratch)
+    int k = 0;
+    lst[k++] = (int8_t)w;
+    int L = w;
+    for (int w2 = w - 1; w2 >= floor_w + 1; w2--) {
+      if (((lead_mask >> (w2 - 1)) & 1ULL) && ((QL[w2 - 1] >> (L - 1)) & 1ULL)) {
+        lst[k++] = (int8_t)w2;
+        L = w2;
+      }
+    }
+    __syncthreads();
+    // chain edges: segment i expands leader list[i]'s strong cone over rounds
+    // (round(list[i+1]), round(list[i])], the last one down to round(floor+1)
+    if (lane == 0) {
+      for (int i = 0; i < k; i++) {
+        const int hi = lst[i], lo = i + 1 < k ? lst[i + 1] : floor_w + 1;
+        coef[(lst[i] - 1) * 65 + hi] += 1;
+        coef[(lst[i] - 1) * 65 + lo] -= 1;
+        if (npush + i < J.push_cap) g_push_wave[npush + i] = lst[i];
+      }
+      for (int i = k - 1; i >= 0; i--) {  // pops: reverse push order (stack/stack.go:23-28)
+        const int j = npop + (k - 1 - i);
+        pop_lead[j] = (uint8_t)lst[i];
+        if (first_pop[lst[i] - 1] < 0) first_pop[lst[i] - 1] = (int16_t)j;
+      }
+    }
+    npush += k;
+    npop += k;
+    last = w;
+    __syncthreads();
+  }
+  if (lane == 0) g_push_off[nw] = (uint32_t)npush;
+  __syncthreads();
+
+  // ---------------- 4. bottom-up emission ----------------
+  // lane b = leader wave b+1 for the per-leader bookkeeping
+  const int myfirst = first_pop[lane];
+  int myrank = 0;  // PAPER: leaders first popped before b
+  for (int x = 0; x < 64; x++) {
+    const int fp = first_pop[x];
+    myrank += (fp >= 0 && myfirst >= 0 && fp < myfirst) ? 1 : 0;
+  }
+  if (PAPER && myfirst >= 0) ord[myrank] = (int8_t)lane;
+  for (int k = 0; k < RS; k++) res[lane * RS + k] = 0;
+  // chain edges: segment sums are differences of the suffix sums at the leader
+  // rounds (every leader's coefficients sum to zero; Suf = 0 above round T)
+  u64 chain = 0;
+  for (int x = 1; x < nw; x++) {
+    const int c = coef[lane * 65 + x];
+    if (c) chain -= (u64)((int64_t)c * (int64_t)g_sufl[x * 64 + lane]);
+  }
+  chain = wave_sum(chain);
+  const u64 popped = __ballot(myfirst >= 0);
+  const int npopped = __popcll(popped);
+  __syncthreads();
+  u64 neq = kmemo ? 0ULL : ~0ULL;   // leaders whose cone differs from K in some round <= r
+  u64 kK = 0, dK = 0, eK = 0;       // K's count, digest, edges through round r-1
+  // delivered vertices of round r (the set s0|s1) in slot order, positions from
+  // k0: count, digest, edges (wave-uniform); lanes = slots (sa, sb: the round's
+  // slots; slo / shi: its first 128 slot sources, lane-held)
+  auto contrib = [&](int r, u64 s0, u64 s1, u64 k0, uint32_t sa, uint32_t sb, int slo, int shi, u64 &cnt, u64 &dg,
+                     u64 &ed) {
+    u64 k = k0, dacc = 0, eacc = 0;
+    for (uint32_t c0 = sa; c0 < sb; c0 += 64) {
+      const uint32_t sl = c0 + lane;
+      const int s = c0 == sa ? slo : c0 == sa + 64 ? shi : (sl < sb ? (int)g_slot_src[sl] : 0);  // 0: ghost / none
+      const int v = s - 1;
+      const bool in = s > 0 && ((((v < 64) ? s0 : s1) >> (v & 63)) & 1ULL);
+      const u64 bal = __ballot(in);
+      if (in) {
+        dacc += digest_term((uint32_t)r, (uint32_t)s, k + (u64)__popcll(bal & ((1ULL << lane) - 1ULL)));
+        eacc += DG[v] >> 16;
+      }
+      k += (u64)__popcll(bal);
+    }
+    cnt = k - k0;
+    dg = wave_sum(dacc);
+    ed = wave_sum(eacc);
+  };
+  // software pipeline: round r+1's sets, degrees, presence and slots load while
+  // round r is processed
+  u64 pf0 = 0, pf1 = 0, pp0 = 0, pp1 = 0;
+  uint32_t pd[2] = {0, 0}, psa = 0, psb = 0;
+  int pslo = 0, pshi = 0;
+  auto prefetch4 = [&](int r) {
+    pf0 = g_cone[((size_t)r * 2) * 64 + lane];
+    pf1 = g_cone[((size_t)r * 2 + 1) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int v = lane + 64 * i;
+      if (v < n) pd[i] = g_deg[(size_t)r * n + v];
+    }
+    pp0 = pres_word(r, 0);
+    pp1 = pres_word(r, 1);
+    psa = g_slot_off[r];
+    psb = g_slot_off[r + 1];
+    pslo = psa + lane < psb ? (int)g_slot_src[psa + lane] : 0;
+    pshi = psa + 64 + lane < psb ? (int)g_slot_src[psa + 64 + lane] : 0;
+  };
+  prefetch4(1);
+  for (int r = 1; r <= T; r++) {
+    __syncthreads();
+    const u64 f0 = pf0, f1 = pf1, P0 = pp0, P1 = pp1;
+    const uint32_t sa = psa, sb = psb;
+    const int slo = pslo, shi = pshi;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int v = lane + 64 * i;
+      if (v < n) DG[v] = pd[i];
+    }
+    if (r < T) prefetch4(r + 1);
+    __syncthreads();
+    const u64 active = popped & __ballot(lane < nw && 4 * lane + 1 >= r);  // leaders whose top >= r
+    if (!PAPER) {
+      if (kmemo) {  // leaders whose cone first differs from K in round r take K's prefix
+        const u64 K0 = readlane64(f0, 63), K1 = readlane64(f1, 63);
+        const u64 newly = __ballot((((f0 ^ K0) & P0) | ((f1 ^ K1) & P1)) != 0ULL) & active & ~neq;
+        if ((newly >> lane) & 1ULL) {
+          res[lane * RS + 0] = kK;
+          res[lane * RS + 1] = dK;
+          res[lane * RS + 2] = eK;
+        }
+        neq |= newly;
+        u64 c, d, e;
+        contrib(r, K0, K1, kK, sa, sb, slo, shi, c, d, e);
+        kK += c;
+        dK += d;
+        eK += e;
+      }
+      __syncthreads();
+      for (u64 m = neq & active; m; m &= m - 1) {
+        const int b = __builtin_ctzll(m);
+        u64 c, d, e;
+        contrib(r, readlane64(f0, b), readlane64(f1, b), res[b * RS + 0], sa, sb, slo, shi, c, d, e);
+        __syncthreads();
+        if (lane == 0) {
+          res[b * RS + 0] += c;
+          res[b * RS + 1] += d;
+          res[b * RS + 2] += e;
+        }
+        __syncthreads();
+      }
+      if (kmemo && ((r - 1) & 3) == 0) {  // a leader equal to K up to its own round: K's prefix
+        const int b = (r - 1) / 4;
+        if (lane == 0 && b < nw && ((popped >> b) & 1ULL) && !((neq >> b) & 1ULL)) {
+          res[b * RS + 0] = kK;
+          res[b * RS + 1] = dK;
+          res[b * RS + 2] = eK;
+        }
+      }
+    } else if (active) {
+      // what the leaders popped before b hold: exclusive prefix OR over the popped
+      // leaders in first-pop order (lane j = the j-th), read back at b's rank
+      const int src = lane < npopped ? (int)ord[lane] : 0;
+      u64 y0 = shfl64(f0, src), y1 = shfl64(f1, src);
+      if (lane >= npopped) y0 = y1 = 0;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const u64 z0 = shfl_up64(y0, off), z1 = shfl_up64(y1, off);
+        if (lane >= off) { y0 |= z0; y1 |= z1; }
+      }
+      u64 e0 = shfl_up64(y0, 1), e1 = shfl_up64(y1, 1);
+      if (lane == 0) e0 = e1 = 0;
+      const u64 x0 = f0 & ~shfl64(e0, myrank), x1 = f1 & ~shfl64(e1, myrank);
+      for (u64 m = __ballot(((x0 & P0) | (x1 & P1)) != 0ULL) & active; m; m &= m - 1) {
+        const int b = __builtin_ctzll(m);
+        u64 c, d, e;
+        contrib(r, readlane64(x0, b), readlane64(x1, b), res[b * RS + 3], sa, sb, slo, shi, c, d, e);
+        __syncthreads();
+        if (lane == 0) {
+          res[b * RS + 3] += c;
+          res[b * RS + 4] += d;
+          res[b * RS + 5] += e;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---------------- 5. outputs ----------------
+  u64 dsum = 0;
+  const int np = min(npop, min(J.push_cap, kMaxPops));
+  for (int j = lane; j < np; j += 64) {
+    const int lb = pop_lead[j] - 1;
+    u64 c, d, e;
+    if (!paper) {
+      c = res[lb * RS + 0]; d = res[lb * RS + 1]; e = res[lb * RS + 2];
+    } else if (first_pop[lb] == j) {
+      c = res[lb * RS + (RS - 3)]; d = res[lb * RS + (RS - 2)]; e = res[lb * RS + (RS - 1)];
+    } else {
+      c = 0; d = 0; e = 0;  // the leader's cone was delivered by its first pop
+    }
+    g_pop_count[j] = c;
+    g_pop_digest[j] = d;
+    g_pop_edges[j] = e;
+    dsum += e;
+  }
+  dsum = wave_sum(dsum);
+  if (lane < nw) {
+    g_vcount[lane] = vc_s[lane];
+    g_commit[lane] = (uint8_t)((commit_mask >> lane) & 1ULL);
+  }
+  if (lane == 0) {
+    g_totals[0] = commit_edges;
+    g_totals[1] = chain;
+    g_totals[2] = dsum;
+    g_totals[3] = (u64)npush;
+  }
+}
+
+}  // namespace dr

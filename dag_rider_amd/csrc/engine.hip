@@ -24,6 +24,7 @@
 #include "kernels.hpp"
 #include "replay_plan.hpp"
 #include "batch.hpp"
+#include "batch1w.hpp"
 
 using dr::u64;
 
@@ -148,6 +149,8 @@ struct dr_ctx {
   bool timed(int i) const { return phase_timing >= 2 || (phase_timing == 1 && (i == 6 || i == 7)); }
   hipError_t rec(int i) { return timed(i) ? hipEventRecord(ev[i], stream) : hipSuccess; }
   int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies
+  int batch_form = DR_BATCH_AUTO;  // DR_OPT_BATCH_FORM (dr_replay_batch, first context)
+  int cu_count = 0;         // compute units of the device (dr_replay_batch's form choice)
   float last_commit_ms = 0;  // dr_last_kernel_ms: the last commit-rule launch (HIP events)
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
   DevBuf plan_out;          // its outputs, packed for one copy back
@@ -1606,6 +1609,11 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     c->plan_mode = value != 0;
     return DR_OK;
   }
+  if (option == DR_OPT_BATCH_FORM) {
+    if (value < DR_BATCH_AUTO || value > DR_BATCH_WAVE) return c->fail(DR_E_INVAL, "DR_OPT_BATCH_FORM is 0, 1 or 2");
+    c->batch_form = value;
+    return DR_OK;
+  }
   if (option == DR_OPT_PHASE_TIMING) {
     if (value < 0 || value > 2) return c->fail(DR_E_INVAL, "DR_OPT_PHASE_TIMING is 0, 1 or 2");
     c->phase_timing = value;
@@ -2339,8 +2347,9 @@ hipError_t launch_own_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::Swe
 struct Carve {
   char *base = nullptr;
   size_t off = 0;
+  size_t align = 256;  // a power of two
   template <class T> T *take(size_t n) {
-    off = (off + 255) & ~(size_t)255;
+    off = (off + align - 1) & ~(align - 1);
     T *p = reinterpret_cast<T *>(base + off);
     off += std::max<size_t>(n, 1) * sizeof(T);
     return p;
@@ -2773,22 +2782,49 @@ bool small_ok(const dr_ctx *c, int nwaves) {
   return c->n <= 128 && nwaves <= 64 && c->nfar == 0 && c->dmax_near < 32 && c->ndups == 0;
 }
 
-template <bool PAPER, bool PERSIST>
-hipError_t launch_small_t(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int nw, int D) {
+template <int D, bool PAPER, bool PERSIST>
+hipError_t launch_small_t(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int nw) {
   const size_t lds = dr::small_lds_bytes(D, nw);
   static std::atomic<int> seen[kLdsDevs] = {};
-  hipError_t e = lds_limit((const void *)dr::k_replay_small<PAPER, PERSIST>, seen, c->dev, lds);
+  hipError_t e = lds_limit((const void *)dr::k_replay_small<D, PAPER, PERSIST>, seen, c->dev, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_replay_small<PAPER, PERSIST>), dim3(nj), dim3(dr::kSmallNT), lds, c->stream, jobs, nj,
-                     nw, D);
+  hipLaunchKernelGGL((dr::k_replay_small<D, PAPER, PERSIST>), dim3(nj), dim3(dr::kSmallNT), lds, c->stream, jobs, nj,
+                     nw);
   return hipGetLastError();
 }
+template <int D>
+hipError_t launch_small_d(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper) {
+  if (paper) return persistent ? launch_small_t<D, true, true>(c, jobs, nj, nw)
+                               : launch_small_t<D, true, false>(c, jobs, nj, nw);
+  return persistent ? launch_small_t<D, false, true>(c, jobs, nj, nw)
+                    : launch_small_t<D, false, false>(c, jobs, nj, nw);
+}
+template <bool PAPER, bool PERSIST>
+hipError_t launch_small_1w_t(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int nw, int rsl) {
+  const size_t lds = dr::small1w_lds_bytes<PAPER, PERSIST>(rsl);
+  static std::atomic<int> seen[kLdsDevs] = {};
+  hipError_t e = lds_limit((const void *)dr::k_replay_small_1w<PAPER, PERSIST>, seen, c->dev, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_replay_small_1w<PAPER, PERSIST>), dim3(nj), dim3(64), lds, c->stream, jobs, nj, nw,
+                     rsl);
+  return hipGetLastError();
+}
+// one wavefront per DAG (batch1w.hpp); rsl = ring slots = largest weak delta + 1
+hipError_t launch_small_1w(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper,
+                           int dmax) {
+  const int rsl = dmax + 1;
+  if (paper) return persistent ? launch_small_1w_t<true, true>(c, jobs, nj, nw, rsl)
+                               : launch_small_1w_t<true, false>(c, jobs, nj, nw, rsl);
+  return persistent ? launch_small_1w_t<false, true>(c, jobs, nj, nw, rsl)
+                    : launch_small_1w_t<false, false>(c, jobs, nj, nw, rsl);
+}
+// one workgroup per DAG (batch.hpp); D = ring slots, a power of two above the largest weak delta
 hipError_t launch_small(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int nw, int persistent, int paper,
-                        int D) {
-  if (paper) return persistent ? launch_small_t<true, true>(c, jobs, nj, nw, D)
-                               : launch_small_t<true, false>(c, jobs, nj, nw, D);
-  return persistent ? launch_small_t<false, true>(c, jobs, nj, nw, D)
-                    : launch_small_t<false, false>(c, jobs, nj, nw, D);
+                        int dmax) {
+  const int need = next_pow2(dmax + 1);
+  if (need <= 8) return launch_small_d<8>(c, jobs, nj, nw, persistent, paper);
+  if (need <= 16) return launch_small_d<16>(c, jobs, nj, nw, persistent, paper);
+  return launch_small_d<32>(c, jobs, nj, nw, persistent, paper);
 }
 }  // namespace
 
@@ -2839,10 +2875,12 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
       dr::SmallJob &J = jobs[i];
       J.cone = cv.take<u64>((size_t)(T + 1) * 128);
       J.sufl = cv.take<uint32_t>(65 * 64);
-      J.deg = cv.take<uint32_t>(c->h_slot_off[T + 1]);  // per slot of rounds 0..T
+      // per slot of rounds 0..T (workgroup form) or per (round, vertex) (wave form)
+      J.deg = cv.take<uint32_t>(std::max<size_t>(c->h_slot_off[T + 1], (size_t)(T + 1) * c->n));
     }
     cv.off = (cv.off + 255) & ~(size_t)255;
     out0 = cv.off;
+    cv.align = 16;  // the output region comes back whole: no padding between small arrays
     for (int i = 0; i < nctx; i++) {
       dr::SmallJob &J = jobs[i];
       pcap[i] = std::max<int64_t>(1, std::min<int64_t>(outs[i].push_wave ? outs[i].push_cap : 0, pbound));
@@ -2856,6 +2894,7 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
       J.totals = cv.take<u64>(4);
     }
     out1 = cv.off;
+    cv.align = 256;
     dr::SmallJob *jt = cv.take<dr::SmallJob>(nctx);
     if (pass == 0) {
       HIPCHK(c0, c0->batch_arena.ensure(cv.off));
@@ -2889,8 +2928,18 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     }
     const int persistent = chain_mode == DR_CHAIN_PERSISTENT, paper = deliver_mode == DR_DELIVER_PAPER;
     HIPCHK(c0, hipEventRecord(c0->ev[0], c0->stream));
-    const int D = next_pow2(dmax + 1);  // ring slots (batch.hpp k_replay_small): <= 32
-    HIPCHK(c0, launch_small(c0, jt, nctx, nw, persistent, paper, D));
+    // small_ok: dmax < 32.  The wave form when the CUs each hold many DAGs (throughput),
+    // the workgroup form when they hold few (each DAG's critical path bounds the launch)
+    if (c0->cu_count <= 0) {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c0->dev) != hipSuccess || cus <= 0)
+        cus = 256;
+      c0->cu_count = cus;
+    }
+    const bool wave_form = c0->batch_form == DR_BATCH_WAVE ||
+                           (c0->batch_form == DR_BATCH_AUTO && nctx > 6 * c0->cu_count);
+    HIPCHK(c0, wave_form ? launch_small_1w(c0, jt, nctx, nw, persistent, paper, dmax)
+                         : launch_small(c0, jt, nctx, nw, persistent, paper, dmax));
     HIPCHK(c0, hipEventRecord(c0->ev[1], c0->stream));
   }
   // results: one bulk copy of the output region of the arena

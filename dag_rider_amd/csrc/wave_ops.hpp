@@ -29,9 +29,13 @@ __device__ __forceinline__ u64 digest_term(uint32_t round, uint32_t source, u64 
 // Wave reductions on DPP row operations (rows of 16 lanes) + readlane: no LDS
 // traffic, no ds_bpermute latency chain.  Every lane of the wave must be active.
 // ---------------------------------------------------------------------------
+// every control used here (quad_perm, row_half_mirror, row_mirror) reads a lane of
+// the same row, so no lane is out of bounds: old = x and bound_ctrl leave the
+// destination uninitialised (no v_mov of a zero old value per step) and let the
+// compiler fold the move into the OR / add that consumes it
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp32(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ u64 dpp64(u64 x) {

@@ -94,6 +94,11 @@ class Engine:
         """DR_OPT_DEVICE_PLAN: plan dr_replay's phases on the device (identical results either way)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_DEVICE_PLAN, int(on)))
 
+    def set_batch_form(self, form: int):
+        """DR_OPT_BATCH_FORM (read from a batch's first engine): DR_BATCH_AUTO, DR_BATCH_WORKGROUP
+        (four wavefronts per DAG) or DR_BATCH_WAVE (one wavefront per DAG); identical results."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_BATCH_FORM, int(form)))
+
     def profile_kernel(self, kernel: int, variant: int = 0, iters: int = 20) -> float:
         """dr_profile_kernel: average device ms of one kernel variant (tuning hook of the
         profiling build: DR_LIB_VARIANT=timing, include/dagrider_tuning.h)."""
@@ -274,14 +279,15 @@ def _out_layout(nwaves: int, push_cap: int, ids_cap: int):
     return tuple(out), off + 8
 
 
-def _replay_out(nwaves: int, chain_mode: int, ids_cap: int = 0, push_cap: Optional[int] = None):
+def _replay_out(nwaves: int, chain_mode: int, ids_cap: int = 0, push_cap: Optional[int] = None, buf=None):
     """Output arrays of one dr_replay, carved from a single allocation: a C4 step is
     ~0.25 ms on the GPU, and nine separate arrays plus nine ctypes pointer conversions
-    cost ~45 us of Python per call."""
-    push_cap = push_cap if push_cap is not None else (
-        nwaves * (nwaves + 1) // 2 if chain_mode == L.DR_CHAIN_LITERAL else 2 * nwaves + 1)
+    cost ~45 us of Python per call.  buf: carve from the caller's buffer instead (at
+    least _replay_out_bytes long)."""
+    push_cap = push_cap if push_cap is not None else _default_push_cap(nwaves, chain_mode)
     layout, total = _out_layout(nwaves, push_cap, ids_cap)
-    buf = np.zeros(total, np.uint8)
+    if buf is None:
+        buf = np.zeros(total, np.uint8)
     base = buf.ctypes.data
     keep, a = {"_buf": buf}, {}
     for name, t, off, nb in layout:
@@ -291,6 +297,14 @@ def _replay_out(nwaves: int, chain_mode: int, ids_cap: int = 0, push_cap: Option
         keep["ids"], a["ids"] = None, None
     o = L.ReplayOut(a["cm"], a["vc"], a["po"], a["pw"], push_cap, a["pc"], a["pdg"], a["pe"], a["ids"], ids_cap)
     return o, keep
+
+
+def _default_push_cap(nwaves: int, chain_mode: int) -> int:
+    return nwaves * (nwaves + 1) // 2 if chain_mode == L.DR_CHAIN_LITERAL else 2 * nwaves + 1
+
+
+def _replay_out_bytes(nwaves: int, chain_mode: int, ids_cap: int = 0) -> int:
+    return _out_layout(nwaves, _default_push_cap(nwaves, chain_mode), ids_cap)[1]
 
 
 def _replay_result(o, keep, ids_cap: int = 0) -> ReplayResult:
@@ -342,8 +356,13 @@ class ReplayBatch:
         self._ctxs = (L.P * n)(*[e._h for e in self.engines])
         self._outs = (L.ReplayOut * n)()
         self._keep = []
+        # every context's outputs in one allocation, in context order: dr_replay_batch
+        # unpacks thousands of small result arrays per call (C5: 4096), and contiguous
+        # destinations keep that a sequential write
+        stride = (_replay_out_bytes(nwaves, chain_mode) + 63) // 64 * 64
+        self._buf = np.zeros(max(1, n) * stride, np.uint8)
         for i in range(n):
-            o, keep = _replay_out(nwaves, chain_mode)
+            o, keep = _replay_out(nwaves, chain_mode, buf=self._buf[i * stride:(i + 1) * stride])
             self._outs[i] = o
             self._keep.append(keep)
 

@@ -44,7 +44,8 @@ enum {
   DR_E_STATE = -6     /* call order violated (e.g. append not contiguous) */
 };
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
-enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3 };
+enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3, DR_OPT_BATCH_FORM = 4 };
+enum { DR_BATCH_AUTO = 0, DR_BATCH_WORKGROUP = 1, DR_BATCH_WAVE = 2 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
 enum { DR_WEAK_LITERAL = 0, DR_WEAK_PAPER = 1 };
 
@@ -88,7 +89,13 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * host between phases (identical results).
  * DR_OPT_PHASE_TIMING (default 2): HIP events time every phase of a
  * device-planned dr_replay (ms_* outputs); 1 = the summary pass only, 0 = none
- * (untimed ms_* are 0).  Each timed event costs the stream a few microseconds. */
+ * (untimed ms_* are 0).  Each timed event costs the stream a few microseconds.
+ * DR_OPT_BATCH_FORM (default DR_BATCH_AUTO), read from the first context of a
+ * dr_replay_batch: the fused small-DAG kernel's form.  DR_BATCH_WORKGROUP =
+ * one workgroup of four wavefronts per DAG (shortest time per DAG),
+ * DR_BATCH_WAVE = one wavefront per DAG (most DAGs per CU); AUTO takes the
+ * wave form when the batch holds more than 6 DAGs per CU of the device.
+ * Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 
 /* p.dag[r] = append(p.dag[r], v) (process.go:229) for whole rounds

@@ -17,6 +17,8 @@ from dagutil import dag_fingerprint, load_large, random_dag, replay_fingerprint
 pytestmark = pytest.mark.gpu
 
 MODES = [(cm, dm) for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT) for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER)]
+# the fused kernel's two forms (batch.hpp: a workgroup per DAG, batch1w.hpp: a wavefront per DAG)
+FORMS = [L.DR_BATCH_WORKGROUP, L.DR_BATCH_WAVE]
 
 
 def _same(a, b):
@@ -45,10 +47,12 @@ def _random_batch(dev, seed, count, nw, ns=(1, 4, 7, 33, 64, 65, 100, 128), dept
     return items
 
 
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("cm,dm", MODES)
-def test_batch_random_vs_oracle(gpu_device, cm, dm):
+def test_batch_random_vs_oracle(gpu_device, cm, dm, form):
     nw = 10
     items = _random_batch(gpu_device, 77 + 4 * cm + dm, 24, nw)
+    items[0][2].set_batch_form(form)
     got = replay_batch([e for _, _, e in items], nw, cm, dm)
     for (d, f, e), g in zip(items, got):
         want = oracle.PDag(d).replay(f, nw, cm, dm)
@@ -59,10 +63,12 @@ def test_batch_random_vs_oracle(gpu_device, cm, dm):
         e.close()
 
 
-def test_batch_max_waves(gpu_device):
+@pytest.mark.parametrize("form", FORMS)
+def test_batch_max_waves(gpu_device, form):
     """nw = 64 (the fused path's limit) at n = 128: long literal chains, up to 2080 pops."""
     nw = 64
     items = _random_batch(gpu_device, 5, 3, nw, ns=(128, 100, 64))
+    items[0][2].set_batch_form(form)
     for cm, dm in MODES:
         got = replay_batch([e for _, _, e in items], nw, cm, dm)
         for (d, f, e), g in zip(items, got):
@@ -71,10 +77,12 @@ def test_batch_max_waves(gpu_device):
         e.close()
 
 
-def test_batch_matches_single_replay(gpu_device):
+@pytest.mark.parametrize("form", FORMS)
+def test_batch_matches_single_replay(gpu_device, form):
     """The fused batch and dr_replay context by context agree on everything."""
     nw = 12
-    items = _random_batch(gpu_device, 9, 16, nw)
+    items = _random_batch(gpu_device, 9, 16, nw, depth=(2, 31))
+    items[0][2].set_batch_form(form)
     for cm, dm in MODES:
         got = replay_batch([e for _, _, e in items], nw, cm, dm)
         for (_, _, e), g in zip(items, got):
@@ -120,10 +128,11 @@ def test_batch_errors(gpu_device):
         e.close()
 
 
-def test_c5_batch_golden(gpu_device):
+@pytest.mark.parametrize("form", FORMS)
+def test_c5_batch_golden(gpu_device, form):
     """C5: 4096 independent n=128 x 128-round replays (seeds 5000+i) in one batch,
     bit-exact against the committed fingerprints (PERSISTENT/REF for all, LITERAL/REF and
-    PERSISTENT/PAPER for the first 64)."""
+    PERSISTENT/PAPER for the first 64), in both forms of the fused kernel."""
     g = load_large()["c5"]
     count = g["count"]
     engines = []
@@ -135,6 +144,7 @@ def test_c5_batch_golden(gpu_device):
             e = Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device)
             e.append_packed(d)
             engines.append(e)
+        engines[0].set_batch_form(form)
         nw = c5_config(0).nwaves
         got = replay_batch(engines, nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
         bad = [i for i, r in enumerate(got) if replay_fingerprint(r) != g["persistent_ref"][i]]

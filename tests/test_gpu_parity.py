@@ -146,6 +146,30 @@ def test_random_dag_replay(gpu_device, seed):
                     assert (m == want).all()
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_chains_long_gaps(gpu_device, seed):
+    """Leader chains (process.go:341-350) over long runs of absent or unreachable leaders
+    and frontiers that empty (random_dag with few leaders and sparse strong edges), every
+    replay output against the oracle."""
+    rng = np.random.default_rng(7000 + seed)
+    n = int(rng.choice([4, 16, 64, 100]))
+    R = 4 * int(rng.integers(20, 48)) + int(rng.integers(1, 4))
+    d = random_dag(rng, n, R, p_present=rng.uniform(0.6, 1), p_s=rng.uniform(0.03, 0.7), p_w=rng.uniform(0, 0.5),
+                   max_depth=int(rng.integers(2, 8)), leader_p=float(rng.choice([0.05, 0.2, 0.6])))
+    f = int(rng.integers(0, (n - 1) // 3 + 2))
+    nw = R // 4
+    bs = oracle.PDag(d)
+    with Engine(n, f, R + 1, gpu_device) as e:
+        e.append_packed(d)
+        for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT):
+            for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+                want = bs.replay(f, nw, cm, dm)
+                assert want.rc == 0
+                got = e.replay(nw, cm, dm)
+                _compare_replay(got, want, ids=False)
+                assert got.chain_edges == want.chain_edges
+
+
 def test_far_weak_edges(gpu_device):
     """Weak edges spanning > 1023 rounds use the far format and global frontier rows."""
     rng = np.random.default_rng(77)

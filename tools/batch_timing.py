@@ -1,7 +1,7 @@
 """Where the fused C5 replay's time goes: per-DAG phase timings of k_replay_small
 (batch.hpp) from the profiling build (libdagrider_gpu_timing.so, DR_SWEEP_TIMING).
 
-usage: python tools/batch_timing.py [dags ...]   (default: 512 4096)
+usage: python tools/batch_timing.py [dags ...]   (default: 512 4096); both kernel forms
 One JSON line per batch size: the kernel's HIP-event time and, per phase, the mean /
 p50 / max duration over the DAGs (wall_clock64 ticks, 100 MHz on gfx950).
 """
@@ -19,7 +19,7 @@ from dag_rider_amd import _lib as L  # noqa: E402
 from dag_rider_amd.engine import Engine, ReplayBatch  # noqa: E402
 from dag_rider_amd.gen import c5_config, generate  # noqa: E402
 
-sizes = [int(x) for x in sys.argv[1:]] or [512, 4096]
+sizes = [int(x) for x in sys.argv[1:]] or [512, 1024, 2048, 4096]
 lib = L.lib()
 lib.dr_debug_sweep_timing.restype = C.c_int
 lib.dr_debug_sweep_timing.argtypes = [C.c_void_p, C.c_int]
@@ -34,15 +34,19 @@ for i in range(max(sizes)):
 print(f"loaded {len(engines)} DAGs in {time.perf_counter() - t0:.1f} s", file=sys.stderr)
 nw = c5_config(0).nwaves
 names = ["pass_F", "pass_G_tail", "chains", "emission", "outputs"]
-for nd in sizes:
+for nd, form in [(nd, f) for nd in sizes for f in (L.DR_BATCH_WORKGROUP, L.DR_BATCH_WAVE)]:
+    engines[0].set_batch_form(form)
     b = ReplayBatch(engines[:nd], nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
     for _ in range(3):
         b.run()
     res = b.results()
+    if form == L.DR_BATCH_WAVE:  # no phase stamps in the wave form
+        print(json.dumps({"dags": nd, "form": "wave", "kernel_ms": max(r.ms["deliver"] for r in res)}), flush=True)
+        continue
     buf = np.zeros(16 * nd, np.uint64)
     assert lib.dr_debug_sweep_timing(L.ptr(buf), nd) == 0
     t = buf.reshape(nd, 16)[:, :6].astype(np.float64) * 0.01  # us
-    out = {"dags": nd, "kernel_ms": max(r.ms["deliver"] for r in res)}
+    out = {"dags": nd, "form": "workgroup", "kernel_ms": max(r.ms["deliver"] for r in res)}
     for k, name in enumerate(names):
         v = t[:, k + 1] - t[:, k]
         out[name + "_us"] = dict(mean=round(float(v.mean()), 2), p50=round(float(np.median(v)), 2),
