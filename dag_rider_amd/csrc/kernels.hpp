@@ -821,6 +821,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
             if constexpr (PRUNE) f &= ~ld_agent(dlv + (size_t)r * WS + tid);
             p = cur.P;
           }
+          int single = (r == q.top) ? q.src0 : -1;  // a round whose frontier is one known vertex
           if constexpr (CHAIN) {
             if (r < q.top && ((r - 1) & 3) == 0) {
               const int wv = (r - 1) / 4 + 1, l = g.lead[wv] - 1;  // leader of wave wv, 0-based
@@ -828,6 +829,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
               if (((fl & pl) >> (l & 63)) & 1ULL) {  // v' present, strong_path(leader, v'): push v' (process.go:344-349)
                 f = tid == (l >> 6) ? 1ULL << (l & 63) : 0ULL;
                 if (tid == 0) push_out[q.out_off + npush++] = wv;
+                single = l;  // the chain restarts at v' alone
               }
             }
           }
@@ -876,12 +878,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
             --r;
             continue;
           }
-          // The query's own top round holds one vertex (its `from`): wave 0 expands
-          // it here -- one row, the round's weak-column words of that source --
-          // instead of a workgroup round (no far edges: merge sweeps run on the
-          // memo path, which has none; strong-only sweeps never read them).
-          if ((!PRUNE && (MERGE || !WEAK)) && !stop && r == q.top && q.src0 >= 0) {
-            const int s0 = q.src0;
+          // The query's own top round holds one vertex (its `from`), and so does a
+          // chain's restart round (its pushed leader): wave 0 expands it here -- one
+          // row, the round's weak-column words of that source -- instead of a
+          // workgroup round (no far edges: merge sweeps run on the memo path, which
+          // has none; strong-only sweeps never read them).
+          if ((!PRUNE && (MERGE || !WEAK)) && !stop && single >= 0) {
+            const int s0 = single;
             const bool in = (__shfl(f & p, s0 >> 6) >> (s0 & 63)) & 1ULL;  // FE = {s0}
             int lowmin = 0x7fffffff;
             if (in) {
