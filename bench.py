@@ -635,7 +635,12 @@ def run_c5(args, rank: int, world: int, local: int, dist):
                      "note": "unique DAG bytes (strong rows + weak columns) once per launch"},
         "cpu_baseline": cpu,
         "detail": {"edges_per_step": edges, "commits": int(sum(int(r.commit.sum()) for r in res)),
-                   "pops": int(sum(len(r.pop_count) for r in res))},
+                   "pops": int(sum(len(r.pop_count) for r in res)),
+                   # the last step's phases (dr_replay_batch, first output): host prep before the
+                   # launch, launch -> results on the host, the copy back (device), the unpack
+                   "step_phases_ms": {"host_prep": res[0].ms["commit"], "launch_to_host": res[0].ms["summary"],
+                                      "kernel": kms, "copy_back": res[0].ms["chain"],
+                                      "unpack": res[0].ms["emit"]}},
     }
 
 

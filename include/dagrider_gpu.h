@@ -240,7 +240,10 @@ typedef struct {
   uint64_t commit_edges, chain_edges, deliver_edges;
   /* device time (ms) of each phase of the last call, HIP events (ms_summary: the
    * rows + commit pass k_summary_commit; the weak union that follows it is not
-   * included) */
+   * included).  A fused dr_replay_batch sets ms_deliver = the fused kernel in every
+   * output and, in the first output only, the call's host phases: ms_commit = host
+   * preparation before the launch, ms_summary = launch to results on the host,
+   * ms_chain = the copy back (device), ms_emit = unpacking into the outputs */
   float ms_commit, ms_chain, ms_deliver, ms_emit, ms_summary;
   int32_t canon_segments; /* partial-round segments of the canonical cone (-1: summaries off) */
   /* work done by the delivery sweeps (identical leaders share one sweep):

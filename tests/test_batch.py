@@ -157,3 +157,51 @@ def test_c5_batch_golden(gpu_device, form):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.parametrize("form", FORMS)
+def test_batch_plan_reuse(gpu_device, form):
+    """A repeated batch (same contexts, modes and output buffers) reuses its plan: the
+    checks, job table and output layout of the last call (engine.hip, BatchPlan). Any
+    ABI call that can change a context in between -- appends, the leader coin, an
+    output capacity, create/destroy -- rebuilds it."""
+    nw = 8
+    rng = np.random.default_rng(31)
+    items = []
+    for n in (4, 33, 64, 100, 128, 7):
+        d = random_dag(rng, n, 4 * nw + 8, p_present=0.9, p_s=0.6, p_w=0.5, max_depth=8)
+        f = (n - 1) // 3
+        e = Engine(n, f, d.nrounds, gpu_device)
+        e.append_packed(d, 0, 4 * nw + 1)  # rounds 0..4nw: the batch's waves and no more
+        items.append((d, f, e))
+    engines = [e for _, _, e in items]
+    engines[0].set_batch_form(form)
+    cm, dm = L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF
+    want = [oracle.PDag(d).replay(f, nw, cm, dm) for d, f, _ in items]
+    b = ReplayBatch(engines, nw, cm, dm)
+    for _ in range(3):  # the first call builds the plan, the next ones reuse it
+        for w, g in zip(want, b()):
+            _same(g, w)
+    for e, (d, _, _) in zip(engines[::2], items[::2]):  # appends in between: rebuilt
+        e.append_packed(d)
+    for _ in range(2):
+        for w, g in zip(want, b()):
+            _same(g, w)
+    engines[2].set_leader_coin(L.DR_LEADER_SEEDED, 99)  # a different leader schedule
+    got = b()
+    for i, e in enumerate(engines):
+        _same(got[i], e.replay(nw, cm, dm))
+    engines[2].set_leader_coin()
+    for w, g in zip(want, b()):
+        _same(g, w)
+    for e in engines:
+        e.close()
+    # new contexts (possibly at the old addresses) with new DAGs: rebuilt
+    items = _random_batch(gpu_device, 32, 6, nw)
+    items[0][2].set_batch_form(form)
+    b = ReplayBatch([e for _, _, e in items], nw, cm, dm)
+    for _ in range(2):
+        for (d, f, _), g in zip(items, b()):
+            _same(g, oracle.PDag(d).replay(f, nw, cm, dm))
+    for _, _, e in items:
+        e.close()
