@@ -2359,7 +2359,10 @@ hipError_t launch_paper_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::S
 template <int WS>
 hipError_t launch_own_emit_t(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
                              u64 *qcount, u64 *qdigest, int32_t *qcut) {
-  hipLaunchKernelGGL((dr::k_own_emit<WS, 512>), dim3(nw + 1), dim3(512), 0, c->stream, c->view(), c->masks.as<u64>(),
+  // 256 threads per query at n <= 256 (C3: 41 -> 37 us, more queries resident), 512 above
+  // (C4 at 256: 12.8 -> 18.8 us; profiles/r03/v18_timeline_*_own256.txt)
+  constexpr int NT = WS <= 4 ? 256 : 512;
+  hipLaunchKernelGGL((dr::k_own_emit<WS, NT>), dim3(nw + 1), dim3(NT), 0, c->stream, c->view(), c->masks.as<u64>(),
                      c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(), c->slot_off.as<uint32_t>(),
                      c->slot_src.as<uint16_t>(), qcount, qdigest, qcut, c->nrounds - 1, c->RG.as<u64>(),
                      c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>());

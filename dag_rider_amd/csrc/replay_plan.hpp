@@ -28,6 +28,88 @@
 
 namespace dr {
 
+// Two exclusive scans over one workgroup at once (one set of barriers); s holds
+// 2 * NT/64 slots; every thread calls.
+template <int NT>
+__device__ __forceinline__ void block_scan2_excl(int64_t &a, int64_t &b, int64_t *s, int64_t &ta, int64_t &tb) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t x = a, y = b;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t u = __shfl_up(x, off), v = __shfl_up(y, off);
+    if (lane >= off) {
+      x += u;
+      y += v;
+    }
+  }
+  if (lane == 63) {
+    s[wid] = x;
+    s[NW + wid] = y;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    int64_t t = lane < NW ? s[lane] : 0, z = lane < NW ? s[NW + lane] : 0;
+#pragma unroll
+    for (int off = 1; off < NW; off <<= 1) {
+      const int64_t u = __shfl_up(t, off), v = __shfl_up(z, off);
+      if (lane >= off) {
+        t += u;
+        z += v;
+      }
+    }
+    if (lane < NW) {
+      s[lane] = t;
+      s[NW + lane] = z;
+    }
+  }
+  __syncthreads();
+  ta = s[NW - 1];
+  tb = s[2 * NW - 1];
+  a = (wid ? s[wid - 1] : 0) + x - a;
+  b = (wid ? s[NW + wid - 1] : 0) + y - b;
+  __syncthreads();
+}
+
+// K consecutive items per thread (item tid*K + j of the chunk): their exclusive
+// prefixes in ex[], the chunk total returned.  s: 2 * NT/64 slots.
+template <int NT, int K>
+__device__ __forceinline__ int64_t block_scan_items(const int64_t (&v)[K], int64_t (&ex)[K], int64_t *s) {
+  int64_t sum = 0, zero = 0, tot, tz;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    ex[j] = sum;
+    sum += v[j];
+  }
+  block_scan2_excl<NT>(sum, zero, s, tot, tz);
+#pragma unroll
+  for (int j = 0; j < K; j++) ex[j] += sum;
+  return tot;
+}
+// the same for two item sequences at once
+template <int NT, int K>
+__device__ __forceinline__ void block_scan2_items(const int64_t (&va)[K], const int64_t (&vb)[K], int64_t (&ea)[K],
+                                                  int64_t (&eb)[K], int64_t *s, int64_t &ta, int64_t &tb) {
+  int64_t sa = 0, sb = 0;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    ea[j] = sa;
+    eb[j] = sb;
+    sa += va[j];
+    sb += vb[j];
+  }
+  block_scan2_excl<NT>(sa, sb, s, ta, tb);
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    ea[j] += sa;
+    eb[j] += sb;
+  }
+}
+
+// Planning kernels take kPlanK consecutive items per thread: one pass of
+// barriers covers NT * kPlanK waves (C3's 2500 waves in one pass at NT = 1024).
+constexpr int kPlanK = 4;
+
 // Committed waves -> tasks (wave, floor) -> leader-chain queries.  Persistent
 // decidedWave: floor = the previous committed wave; literal: 0.  A task with
 // wave - floor >= 2 walks rounds 4(w-1)+1 .. 4 floor + 1 and may push up to
@@ -37,50 +119,61 @@ __global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ 
                                                     int nw, int persistent, int qflags, int32_t *__restrict__ task_wave,
                                                     int32_t *__restrict__ task_q, SweepQuery *__restrict__ cq,
                                                     int32_t *__restrict__ plan) {
-  __shared__ int64_t s[NT / 64];
-  __shared__ int64_t c0, c1, c2;
+  constexpr int K = kPlanK, CH = NT * K;
+  __shared__ int64_t s[2 * (NT / 64)];
   const int tid = threadIdx.x;
-  if (tid == 0) c0 = c1 = c2 = 0;
-  __syncthreads();
-  for (int w0 = 0; w0 < nw; w0 += NT) {
-    const int w = w0 + tid;
-    const int64_t f = (w < nw && commit[w]) ? 1 : 0;
-    int64_t tot;
-    const int64_t ex = block_scan_excl<NT>(f, s, tot);
-    if (f) task_wave[c0 + ex] = w + 1;
-    __syncthreads();
-    if (tid == 0) c0 += tot;
-    __syncthreads();
+  int64_t c0 = 0, c1 = 0, c2 = 0;  // running totals (block-uniform)
+  for (int w0 = 0; w0 < nw; w0 += CH) {
+    int64_t f[K], ex[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const int w = w0 + tid * K + j;
+      f[j] = (w < nw && commit[w]) ? 1 : 0;
+    }
+    const int64_t tot = block_scan_items<NT, K>(f, ex, s);
+#pragma unroll
+    for (int j = 0; j < K; j++)
+      if (f[j]) task_wave[c0 + ex[j]] = w0 + tid * K + j + 1;
+    c0 += tot;
   }
+  __syncthreads();  // task_wave written
   const int ntask = (int)c0;
-  for (int t0 = 0; t0 < ntask; t0 += NT) {
-    const int t = t0 + tid;
-    int w = 0, fl = 0;
-    int64_t len = 0, has = 0;
-    if (t < ntask) {
-      w = task_wave[t];
-      fl = (persistent && t > 0) ? task_wave[t - 1] : 0;
-      len = w - fl - 1;
-      has = len >= 1 ? 1 : 0;
+  for (int t0 = 0; t0 < ntask; t0 += CH) {
+    int w[K], fl[K];
+    int64_t len[K], has[K], qi[K], off[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const int t = t0 + tid * K + j;
+      w[j] = fl[j] = 0;
+      len[j] = has[j] = 0;
+      if (t < ntask) {
+        w[j] = task_wave[t];
+        fl[j] = (persistent && t > 0) ? task_wave[t - 1] : 0;
+        len[j] = w[j] - fl[j] - 1;
+        has[j] = len[j] >= 1 ? 1 : 0;
+        if (!has[j]) len[j] = 0;
+      }
     }
     int64_t tq, tl;
-    const int64_t qi = block_scan_excl<NT>(has, s, tq);
-    const int64_t off = block_scan_excl<NT>(has ? len : int64_t(0), s, tl);
-    if (t < ntask) task_q[t] = has ? (int32_t)(c1 + qi) : -1;
-    if (has) {
-      SweepQuery q{};
-      q.top = 4 * (w - 1) + 1;
-      q.bottom = 4 * fl + 1;
-      q.src0 = lead[w] - 1;
-      q.flags = qflags;
-      q.mask_off = 0;
-      q.out_off = (int32_t)(c2 + off);
-      q.tgt0 = -1;
-      cq[c1 + qi] = q;
+    block_scan2_items<NT, K>(has, len, qi, off, s, tq, tl);
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const int t = t0 + tid * K + j;
+      if (t < ntask) task_q[t] = has[j] ? (int32_t)(c1 + qi[j]) : -1;
+      if (has[j]) {
+        SweepQuery q{};
+        q.top = 4 * (w[j] - 1) + 1;
+        q.bottom = 4 * fl[j] + 1;
+        q.src0 = lead[w[j]] - 1;
+        q.flags = qflags;
+        q.mask_off = 0;
+        q.out_off = (int32_t)(c2 + off[j]);
+        q.tgt0 = -1;
+        cq[c1 + qi[j]] = q;
+      }
     }
-    __syncthreads();
-    if (tid == 0) { c1 += tq; c2 += tl; }
-    __syncthreads();
+    c1 += tq;
+    c2 += tl;
   }
   if (tid == 0) {
     plan[PL_NTASK] = ntask;
@@ -107,30 +200,34 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
                                                   int32_t *__restrict__ pop_cur, int32_t *__restrict__ pop_q,
                                                   uint8_t *__restrict__ seen, int32_t *__restrict__ qidx,
                                                   SweepQuery *__restrict__ dq, int32_t *__restrict__ plan) {
-  __shared__ int64_t s[NT / 64];
-  __shared__ int64_t c0, c1;
+  constexpr int K = kPlanK, CH = NT * K;
+  __shared__ int64_t s[2 * (NT / 64)];
   const int tid = threadIdx.x;
   const int ntask = plan[PL_NTASK];
   for (int i = tid; i <= nw; i += NT) seen[i] = 0;
-  if (tid == 0) c0 = c1 = 0;
-  __syncthreads();
-  for (int t0 = 0; t0 < ntask; t0 += NT) {
-    const int t = t0 + tid;
-    int64_t cnt = 0;
-    if (t < ntask) cnt = 1 + (task_q[t] >= 0 ? push_n[task_q[t]] : 0);
-    int64_t tot;
-    const int64_t ex = block_scan_excl<NT>(cnt, s, tot);
-    if (t < ntask) task_pos[t] = c0 + ex;
-    __syncthreads();
-    if (tid == 0) c0 += tot;
-    __syncthreads();
+  int64_t np = 0;  // running total (block-uniform)
+  for (int t0 = 0; t0 < ntask; t0 += CH) {
+    int64_t cnt[K], ex[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const int t = t0 + tid * K + j;
+      const int q = t < ntask ? task_q[t] : -1;
+      cnt[j] = t < ntask ? 1 + (q >= 0 ? push_n[q] : 0) : 0;
+    }
+    const int64_t tot = block_scan_items<NT, K>(cnt, ex, s);
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const int t = t0 + tid * K + j;
+      if (t < ntask) task_pos[t] = np + ex[j];
+    }
+    np += tot;
   }
-  const int64_t np = c0;
   if (tid == 0) plan[PL_NPUSH] = (int32_t)np;
   if (np > pcap) {  // uniform; the host reports DR_E_CAPACITY with n_push = np
     if (tid == 0) plan[PL_CAPERR] = 1;
     return;
   }
+  __syncthreads();  // task_pos written, seen cleared
   for (int t = tid; t < ntask; t += NT) {
     const int w = task_wave[t];
     const int64_t P = task_pos[t];
@@ -147,7 +244,6 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
       seen[pw] = 1;
     }
   }
-  __syncthreads();
   // pushes before wave w = the position of the first task with wave >= w (np
   // past the last): task t owns the waves after its predecessor's, up to its own
   // (task waves increase), so each writes its range -- no search per wave
@@ -157,31 +253,37 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
     const uint32_t v = (uint32_t)(t < ntask ? task_pos[t] : np);
     for (int w = wlo; w <= whi; w++) push_off[w - 1] = v;
   }
-  if (tid == 0) c0 = 0;
-  __syncthreads();
-  for (int i0 = 0; i0 < nw; i0 += NT) {
-    const int i = i0 + tid, w = nw - i;
-    const int64_t f = (i < nw && seen[w]) ? 1 : 0;
-    const int top = 4 * (w - 1) + 1;
+  __syncthreads();  // seen written
+  int64_t c0 = 0, c1 = 0;  // running totals (block-uniform)
+  for (int i0 = 0; i0 < nw; i0 += CH) {
+    int64_t f[K], mw[K], qi[K], mo[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const int i = i0 + tid * K + j, w = nw - i;
+      f[j] = (i < nw && seen[w]) ? 1 : 0;
+      mw[j] = f[j] ? (int64_t)(4 * (w - 1) + 2) * WS : 0;  // rounds 0..top
+    }
     int64_t tq, tm;
-    const int64_t qi = block_scan_excl<NT>(f, s, tq);
-    const int64_t mo = block_scan_excl<NT>(f ? (int64_t)(top + 1) * WS : int64_t(0), s, tm);
-    if (f) {
-      qidx[w] = (int32_t)(c0 + qi);
+    block_scan2_items<NT, K>(f, mw, qi, mo, s, tq, tm);
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      if (!f[j]) continue;
+      const int w = nw - (i0 + tid * K + j);
+      qidx[w] = (int32_t)(c0 + qi[j]);
       SweepQuery q{};
-      q.top = top;
+      q.top = 4 * (w - 1) + 1;
       q.bottom = 0;
       q.src0 = lead[w] - 1;
       q.flags = qflags;
-      q.mask_off = c1 + mo;
+      q.mask_off = c1 + mo[j];
       q.tgt0 = -1;
-      dq[c0 + qi] = q;
+      dq[c0 + qi[j]] = q;
     }
-    __syncthreads();
-    if (tid == 0) { c0 += tq; c1 += tm; }
-    __syncthreads();
+    c0 += tq;
+    c1 += tm;
   }
   if (tid == 0) plan[PL_NQD] = (int32_t)c0;
+  __syncthreads();  // qidx written
   for (int64_t p = tid; p < np; p += NT) pop_q[p] = qidx[pop_wave[p]];
 }
 
@@ -567,7 +669,7 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
   __shared__ u64 s_c[NWV], s_dg;
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (q == (int)gridDim.x - 1) {
-    canon_prefix_block<NT, (4096 + NT - 1) / NT>(T, RG, CE, Gc, Ec, nullptr);
+    canon_prefix_block<NT, 8>(T, RG, CE, Gc, Ec, nullptr);
     return;
   }
   // the query's fields load with the plan counts (the arena holds every slot below the grid bound)
