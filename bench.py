@@ -505,9 +505,14 @@ def c4_multi_line(args, world: int, cs_all, replicas, split):
     all-gather"), its slowest rank's time per replay.  The independent-replicas
     number (every rank its own C4 DAG) goes to detail.replicas.  If any rank's
     sharded run failed, the line says so and carries the replicas number instead,
-    labelled as such ("parallelism": "replicasN")."""
+    labelled as such ("parallelism": "replicasN").  A sharded replay that rank 0 found
+    different from the unsharded engine's counts as failed the same way: its number is
+    never published."""
     ok = all(r is not None and "error" not in r for r in cs_all)
     verified = ok and bool(cs_all[0].get("verify_vs_unsharded"))
+    if ok and not verified:
+        cs_all = [dict(r, error="verify_vs_unsharded failed") if r.get("rank") == 0 else r for r in cs_all]
+        ok = False
     base = {
         "metric": "DAG edges traversed/sec (commit+delivery)",
         "unit": "edges/s",
@@ -523,7 +528,7 @@ def c4_multi_line(args, world: int, cs_all, replicas, split):
     rep_detail = dict(replicas, parallelism=f"replicas{world}", scaling="weak",
                       note="every rank replays its own C4 DAG (seed 4 + rank), unsharded; value = summed edges / "
                            "slowest rank")
-    if ok:
+    if ok and verified:
         ms = max(r["ms"] for r in cs_all)
         edges = cs_all[0]["edges"]
         r0 = cs_all[0]
@@ -638,9 +643,7 @@ def run_c5(args, rank: int, world: int, local: int, dist):
                    "pops": int(sum(len(r.pop_count) for r in res)),
                    # the last step's phases (dr_replay_batch, first output): host prep before the
                    # launch, launch -> results on the host, the copy back (device), the unpack
-                   "step_phases_ms": {"host_prep": res[0].ms["commit"], "launch_to_host": res[0].ms["summary"],
-                                      "kernel": kms, "copy_back": res[0].ms["chain"],
-                                      "unpack": res[0].ms["emit"]}},
+                   "step_phases_ms": dict(b.host_phases(), kernel=kms)},
     }
 
 
@@ -792,7 +795,8 @@ def dist_selftest(rank: int, world: int, local: int, args=None) -> int:
     """The multi-rank plumbing without a GPU (gloo): every rank reports in, the job's
     numbers are reduced exactly as the GPU path reduces them, and the C4 N > 1 line is
     built by the same code (c4_multi_line) from every rank's sharded-replay result
-    (synthetic here: rank r took 0.25 (r+1) ms; --selftest-fail makes rank 1 fail)
+    (synthetic here: rank r took 0.25 (r+1) ms; --selftest-fail makes rank 1 fail,
+    --selftest-wrong makes rank 0's check against the unsharded engine fail)
     (tests/test_dist_gloo.py)."""
     import torch.distributed as dist
 
@@ -802,8 +806,9 @@ def dist_selftest(rank: int, world: int, local: int, args=None) -> int:
         ranks = [None] * world
         dist.all_gather_object(ranks, dict(rank=rank, local_rank=local, pid=os.getpid()))
         fail = args is not None and args.selftest_fail and rank == 1
+        wrong = args is not None and args.selftest_wrong  # rank 0's check against the unsharded engine fails
         mine = dict(rank=rank, error="selftest failure") if fail else dict(
-            rank=rank, ms=0.25 * (rank + 1), edges=10 ** 9, verify_vs_unsharded=True, phases_ms={"summary": 0.1},
+            rank=rank, ms=0.25 * (rank + 1), edges=10 ** 9, verify_vs_unsharded=not wrong, phases_ms={"summary": 0.1},
             row_bytes=1000)
         cs_all = [None] * world
         dist.all_gather_object(cs_all, mine)
@@ -839,6 +844,7 @@ def main() -> int:
     ap.add_argument("--no-colshard", action="store_true")
     ap.add_argument("--dist-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--selftest-fail", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--selftest-wrong", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--colshard-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cs-uid", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cs-rank", type=int, default=0, help=argparse.SUPPRESS)

@@ -23,11 +23,13 @@ DR_OPT_MEMO = 1
 DR_OPT_DEVICE_PLAN = 2
 DR_OPT_PHASE_TIMING = 3
 DR_OPT_BATCH_FORM = 4
+DR_OPT_COMMIT_SPLIT = 5
 DR_BATCH_AUTO, DR_BATCH_WORKGROUP, DR_BATCH_WAVE = 0, 1, 2
 DR_LEADER_CONST1, DR_LEADER_SEEDED, DR_LEADER_TABLE = 0, 1, 2
 DR_SHARD_ID_BYTES = 128
 DR_SHARD_OPT_PERSISTENT = 1
 DR_SHARD_OPT_MEMO = 2
+DR_SHARD_OPT_STEPPED = 3
 
 P = C.c_void_p
 i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float
@@ -73,6 +75,7 @@ SIGNATURES = {
     "dr_replay": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
     "dr_replay_batch": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
     "dr_last_kernel_ms": (C.c_int, [P, C.POINTER(f32)]),
+    "dr_last_batch_phases": (C.c_int, [P, C.POINTER(f32)]),
     # include/dagrider_shard.h
     "dr_shard_unique_id": (C.c_int, [P]),
     "dr_shard_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.POINTER(P)]),

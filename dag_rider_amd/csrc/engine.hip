@@ -33,11 +33,14 @@ namespace {
 
 thread_local std::string g_create_err;
 
-// Bumped by every ABI call that may change a context (appends, options, replays that
-// grow its buffers, create/destroy): a cached dr_replay_batch plan is valid only at the
-// epoch it was built in
-std::atomic<uint64_t> g_ctx_epoch{1};
-void ctx_touched() { g_ctx_epoch.fetch_add(1, std::memory_order_relaxed); }
+// Context generations: every ABI call that may change a context (appends, options,
+// replays that grow its buffers) gives it a new generation from one process-wide
+// counter, and so does dr_create -- a generation is never reused, so a destroyed
+// context whose address comes back in a new one cannot match.  A cached
+// dr_replay_batch plan is valid while every member context keeps the generation it
+// was built at.
+std::atomic<uint64_t> g_ctx_gen{1};
+uint64_t next_gen() { return g_ctx_gen.fetch_add(1, std::memory_order_relaxed) + 1; }
 
 int next_pow2(int x) {
   int p = 1;
@@ -143,6 +146,13 @@ struct dr_ctx {
   // canonical digests, the lowest round to re-emit; canon_lo = lowest round
   // touched since the last cone
   DevBuf Kprev, RG, rlo;
+  // k_commit_split: published S_1 / S_2 words [wave][2][WS], and [wave] barrier
+  // counters | [wave] vote sums | error flag, kept zero between launches
+  DevBuf split_S, split_ctl;
+  size_t split_nw = 0;
+  int split_cap = 0;  // co-resident k_commit_split workgroups on this device (0: not measured)
+  int commit_split = 1;  // DR_OPT_COMMIT_SPLIT
+  int last_split = 0;    // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
   bool kprev_ok = false;
   int ndirty = 0;     // rounds with sdirty set
@@ -159,6 +169,9 @@ struct dr_ctx {
   int batch_form = DR_BATCH_AUTO;  // DR_OPT_BATCH_FORM (dr_replay_batch, first context)
   int cu_count = 0;         // compute units of the device (dr_replay_batch's form choice)
   float last_commit_ms = 0;  // dr_last_kernel_ms: the last commit-rule launch (HIP events)
+  float batch_phases[4] = {};
+  uint64_t gen = 0;  // context generation (g_ctx_gen): bumped by every call that may change the context
+  void touch() { gen = next_gen(); }  // dr_last_batch_phases: host prep, launch -> host, copy back, unpack
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
   DevBuf plan_out;          // its outputs, packed for one copy back
   std::vector<char> plan_host;
@@ -168,12 +181,13 @@ struct dr_ctx {
   std::vector<dr::SmallJob> batch_jobs;  // the job table last uploaded to the arena
   // the last fused batch this context led (dr_replay_batch's first context): a call with
   // the same contexts, modes and output buffers, and no ABI call that could change a
-  // context since (g_ctx_epoch), reuses its checks, job table and output layout
+  // member since (its generation), reuses its checks, job table and output layout
   struct BatchPlan {
-    uint64_t epoch = 0;  // 0: none
+    bool valid = false;
     int nw = 0, chain_mode = 0, deliver_mode = 0, dmax = 0;
     size_t out0 = 0, out1 = 0, jobs_at = 0;  // output region, job table (arena offsets)
     std::vector<dr_ctx *> ctxs;
+    std::vector<uint64_t> gens;  // each member's generation when the plan was built
     std::vector<char> out_keys;  // each output's caller-set prefix (commit .. ids_cap)
   } batch_plan;
   hipError_t batch_host(size_t n, char **out) {
@@ -520,9 +534,57 @@ constexpr int sweep_block_m() {
 }
 
 // ---- kernel launch dispatch over the row stride ----
+constexpr int kSplitNT = 512;
+// A short wave range (fewer than ~half the co-resident workgroups): KS workgroups
+// per wave (k_commit_split).  Returns 1 when the range is too long for it (the
+// caller launches k_commit), else a hipError_t; *split = KS.
+template <int WS>
+int launch_commit_split_t(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc, int *split) {
+  *split = 0;
+  if (WS < 2 || !c->commit_split) return 1;
+  const auto kern = dr::k_commit_split<WS, kSplitNT>;
+  if (c->split_cap == 0) {
+    int per_cu = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kSplitNT, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev) != hipSuccess)
+      return 1;
+    c->split_cap = std::max(1, per_cu * ncu);
+  }
+  const int groups = (nw + 7) / 8;
+  const int ks_min = std::max(2, (c->n + kSplitNT - 1) / kSplitNT);
+  const int KS = std::min(8, c->split_cap / (groups * 8));
+  if (KS < ks_min) return 1;
+  const int RS = ((c->n + KS - 1) / KS + 63) / 64 * 64;
+  if (RS > kSplitNT) return 1;
+  if ((size_t)nw > c->split_nw) {  // counters start at zero; the kernel leaves them at zero
+    hipError_t e;
+    if ((e = c->split_S.ensure((size_t)nw * 2 * WS * 8)) != hipSuccess) return e;
+    if ((e = c->split_ctl.ensure((size_t)nw * 8 + 64)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(c->split_ctl.p, 0, (size_t)nw * 8 + 64, c->stream)) != hipSuccess) return e;
+    c->split_nw = (size_t)nw;
+  }
+  unsigned *cnt = c->split_ctl.as<unsigned>();
+  int32_t *vacc = reinterpret_cast<int32_t *>(cnt + c->split_nw), *err = vacc + c->split_nw;
+  dr::DagView g = c->view();
+  int quorum = 2 * c->f + 1, ks = KS, rs = RS;
+  u64 *S = c->split_S.as<u64>();
+  void *args[] = {&g, &w0, &nw, &ks, &rs, &quorum, &S, &cnt, &vacc, &err, &cm, &vc};
+  hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(kern), dim3(groups * 8 * KS),
+                                            dim3(kSplitNT), args, 0, c->stream);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  *split = KS;
+  return hipSuccess;
+}
+
 template <int WS>
 hipError_t launch_commit_t(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc) {
   constexpr int NT = block_for<WS>();
+  c->last_split = 0;
+  const int rc = launch_commit_split_t<WS>(c, w0, nw, cm, vc, &c->last_split);
+  if (rc != 1) return (hipError_t)rc;
   hipLaunchKernelGGL((dr::k_commit<WS, NT>), dim3(nw), dim3(NT), 0, c->stream, c->view(), w0, nw,
                      2 * c->f + 1, cm, vc);
   return hipGetLastError();
@@ -817,7 +879,6 @@ int h2d(dr_ctx *c, DevBuf &b, const std::vector<T> &v) {
 extern "C" int dr_abi_version(void) { return DR_ABI_VERSION; }
 
 extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx **out) {
-  ctx_touched();
   if (!out) return DR_E_INVAL;
   *out = nullptr;
   if (n < 1 || n > 2048 || faulty < 0 || max_rounds < 1 || max_rounds > (1 << 20) || device < 0) {
@@ -833,6 +894,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
     return DR_E_HIP;
   }
   dr_ctx *c = new dr_ctx();
+  c->touch();
   c->n = n;
   c->f = faulty;
   c->W = (n + 63) / 64;
@@ -882,7 +944,6 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
 }
 
 extern "C" void dr_destroy(dr_ctx *c) {
-  ctx_touched();
   if (!c) return;
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)c->sync();
@@ -897,7 +958,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds, &c->plan_out,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
-                    &c->admit_buf, &c->lead};
+                    &c->admit_buf, &c->lead, &c->split_S, &c->split_ctl};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -951,7 +1012,7 @@ __global__ __launch_bounds__(256) void k_put_vertices(const u64 *__restrict__ ro
 extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t *slot_off,
                                        const uint16_t *slot_src, const uint64_t *strong,
                                        const uint32_t *weak_off, const uint32_t *weak_tgt) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (int rc = set_device(c)) return rc;
   if (r0 != c->nrounds) return c->fail(DR_E_STATE, "append at round %d but %d rounds mirrored", r0, c->nrounds);
@@ -1010,7 +1071,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
 extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, const int32_t *ids,
                                   const uint32_t *strong_off, const int32_t *strong_ids, const uint32_t *weak_off,
                                   const int32_t *weak_ids) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (k < 0) return c->fail(DR_E_INVAL, "negative vertex count");
   if (k == 0) return DR_OK;
@@ -1157,7 +1218,7 @@ extern "C" int dr_append_rounds_lists(dr_ctx *c, int r0, int k, const uint32_t *
                                       const int32_t *slot_id, const uint32_t *strong_off,
                                       const int32_t *strong_ids, const uint32_t *weak_off,
                                       const int32_t *weak_ids) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (k < 0) return c->fail(DR_E_INVAL, "negative round count");
   if (k == 0) return DR_OK;
@@ -1573,7 +1634,7 @@ int shortcut_flag(const dr_ctx *c) { return rounds_fresh(c) ? dr::Q_SHORTCUT : 0
 }  // namespace
 
 extern "C" int dr_set_leader_coin(dr_ctx *c, int mode, uint64_t seed, int k, const int32_t *table) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (int rc = set_device(c)) return rc;
   std::vector<uint16_t> L(c->h_lead.size(), 1);
@@ -1623,7 +1684,7 @@ extern "C" int dr_coin_leader(uint64_t seed, int wave, int n) {
 }
 
 extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (option == DR_OPT_MEMO) {
     c->use_memo = value != 0;
@@ -1631,6 +1692,10 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
   }
   if (option == DR_OPT_DEVICE_PLAN) {
     c->plan_mode = value != 0;
+    return DR_OK;
+  }
+  if (option == DR_OPT_COMMIT_SPLIT) {
+    c->commit_split = value ? 1 : 0;
     return DR_OK;
   }
   if (option == DR_OPT_BATCH_FORM) {
@@ -1688,7 +1753,7 @@ hipError_t launch_sv_t(dr_ctx *c, int T, int variant) {
 // strong rows (variant 0 grid-stride, 2 one block per wave's rows); kernel 2:
 // the whole dr_replay summary phase (k_summary_commit + canonical cone).
 extern "C" int dr_profile_kernel(dr_ctx *c, int kernel, int variant, int iters, float *avg_ms) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c || !avg_ms || iters < 1) return DR_E_INVAL;
   if (int rc = set_device(c)) return rc;
   const int T = c->nrounds - 1;
@@ -1752,9 +1817,15 @@ extern "C" int dr_last_kernel_ms(const dr_ctx *c, float *ms) {
   return DR_OK;
 }
 
+extern "C" int dr_last_batch_phases(const dr_ctx *c, float *ms4) {
+  if (!c || !ms4) return DR_E_INVAL;
+  for (int i = 0; i < 4; i++) ms4[i] = c->batch_phases[i];
+  return DR_OK;
+}
+
 extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_t *to, int strong_only,
                              uint8_t *out) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (q < 0 || (q > 0 && (!from || !to || !out))) return c->fail(DR_E_INVAL, "bad query arrays");
   if (int rc = set_device(c)) return rc;
@@ -1788,7 +1859,7 @@ extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_
 
 extern "C" int dr_reach_sets(dr_ctx *c, int q, const int32_t *from, const int32_t *bottom, int strong_only,
                              uint64_t *out, size_t cap_words, size_t *out_words) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (int rc = set_device(c)) return rc;
   if (int rc = refresh_rounds(c)) return rc;
@@ -1858,7 +1929,15 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
   HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nw));
   HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nw * 4));
+  int32_t split_err = 0;
+  if (c->last_split)
+    HIPCHK(c, c->d2h(&split_err, c->split_ctl.as<char>() + c->split_nw * 8, 4));
   HIPCHK(c, c->sync());
+  if (split_err) {  // a barrier timed out: the counters are left dirty, clear them
+    HIPCHK(c, hipMemsetAsync(c->split_ctl.p, 0, c->split_nw * 8 + 64, c->stream));
+    HIPCHK(c, c->sync());
+    return c->fail(DR_E_HIP, "k_commit_split: a wave's barrier timed out (workgroups not co-resident)");
+  }
   HIPCHK(c, hipEventElapsedTime(&c->last_commit_ms, c->ev[4], c->ev[5]));
   if (ms) *ms = c->last_commit_ms;
   return DR_OK;
@@ -2134,7 +2213,7 @@ __global__ void __launch_bounds__(256) k_buffer_admit(const u64 *__restrict__ pr
 
 extern "C" int dr_buffer_admit(dr_ctx *c, int cur_round, int q, const int32_t *ids, const uint32_t *pred_off,
                                const int32_t *preds, uint8_t *admit) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (q < 0 || (q > 0 && (!ids || !pred_off || !admit))) return c->fail(DR_E_INVAL, "bad buffer arrays");
   if (q == 0) return DR_OK;
@@ -2205,7 +2284,7 @@ extern "C" int dr_buffer_admit(dr_ctx *c, int cur_round, int q, const int32_t *i
 
 extern "C" int dr_set_weak_edges(dr_ctx *c, int round, int nstrong, const int32_t *strong_ids, int mode,
                                  int32_t *out_ids, size_t cap, size_t *out_n) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (out_n) *out_n = 0;
   if (round < 1 || round > c->nrounds)
@@ -2257,7 +2336,7 @@ extern "C" int dr_set_weak_edges(dr_ctx *c, int round, int nstrong, const int32_
 }
 
 extern "C" int dr_wave_commit(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (!commit || !vcount) return c->fail(DR_E_INVAL, "null output");
   if (int rc = set_device(c)) return rc;
@@ -2266,7 +2345,7 @@ extern "C" int dr_wave_commit(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_
 
 extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *commit, int32_t *vcount,
                              int32_t *pushed_waves, int cap, int *n_pushed) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (!commit || !vcount || !n_pushed) return c->fail(DR_E_INVAL, "null output");
   if (int rc = set_device(c)) return rc;
@@ -2290,7 +2369,7 @@ int deliver_planned(dr_ctx *c, const std::vector<Pop> &pops, uint64_t *pcount, u
 extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack, int cur_round, int mode,
                                  int32_t *out_ids, size_t cap, size_t *out_n, uint64_t *pop_count,
                                  uint64_t *pop_digest) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (nstack < 0 || (nstack > 0 && !stack_rs)) return c->fail(DR_E_INVAL, "bad stack");
   if (mode != DR_DELIVER_REF && mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad mode %d", mode);
@@ -2731,7 +2810,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
 }  // namespace
 
 extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
-  ctx_touched();
+  if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (!o || !o->commit || !o->vcount || !o->push_off) return c->fail(DR_E_INVAL, "null output");
   if (nwaves < 1 || 4 * nwaves >= c->nrounds) return c->fail(DR_E_INVAL, "nwaves %d needs rounds 0..%d mirrored", nwaves, 4 * nwaves);
@@ -2874,14 +2953,13 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
   // each output's caller-set fields, commit .. ids_cap
   constexpr size_t kKey = offsetof(dr_replay_out, n_push);
   dr_ctx::BatchPlan &P = c0->batch_plan;
-  bool hit = P.epoch != 0 && P.epoch == g_ctx_epoch.load(std::memory_order_relaxed) && P.nw == nwaves &&
-             P.chain_mode == chain_mode && P.deliver_mode == deliver_mode && P.ctxs.size() == (size_t)nctx &&
-             std::memcmp(P.ctxs.data(), ctxs, sizeof(dr_ctx *) * nctx) == 0;
+  bool hit = P.valid && P.nw == nwaves && P.chain_mode == chain_mode && P.deliver_mode == deliver_mode &&
+             P.ctxs.size() == (size_t)nctx && std::memcmp(P.ctxs.data(), ctxs, sizeof(dr_ctx *) * nctx) == 0;
   for (int i = 0; hit && i < nctx; i++)
-    hit = std::memcmp(P.out_keys.data() + kKey * i, &outs[i], kKey) == 0;
+    hit = P.gens[i] == ctxs[i]->gen && std::memcmp(P.out_keys.data() + kKey * i, &outs[i], kKey) == 0;
   const int nw = nwaves, T = 4 * (nw - 1) + 1;
   if (!hit) {
-    P.epoch = 0;
+    P.valid = false;
     bool fused = true;
     int dmax = 1;
     for (int i = 0; i < nctx; i++) {
@@ -2983,9 +3061,11 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     P.out1 = out1;
     P.jobs_at = (size_t)(reinterpret_cast<char *>(jt) - c0->batch_arena.as<char>());
     P.ctxs.assign(ctxs, ctxs + nctx);
+    P.gens.resize(nctx);
+    for (int i = 0; i < nctx; i++) P.gens[i] = ctxs[i]->gen;
     P.out_keys.resize(kKey * nctx);
     for (int i = 0; i < nctx; i++) std::memcpy(P.out_keys.data() + kKey * i, &outs[i], kKey);
-    P.epoch = g_ctx_epoch.load(std::memory_order_relaxed);
+    P.valid = true;
   } else if (int rc = set_device(c0)) {
     return rc;
   }
@@ -3054,14 +3134,15 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     std::memcpy(o->pop_digest, at(J.pop_digest), 8 * (size_t)np);
     if (o->pop_edges) std::memcpy(o->pop_edges, at(J.pop_edges), 8 * (size_t)np);
   }
-  // the call's host phases, on the first context's output only
+  // the call's host phases (dr_last_batch_phases on the first context; every output's
+  // ms_* fields keep their device meaning: ms_deliver = the fused kernel, the rest 0)
   auto msd = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
     return std::chrono::duration<float, std::milli>(b - a).count();
   };
-  outs[0].ms_commit = msd(h0, h1);
-  outs[0].ms_summary = msd(h1, h2);
-  outs[0].ms_chain = ms_copy;
-  outs[0].ms_emit = msd(h2, std::chrono::steady_clock::now());
+  c0->batch_phases[0] = msd(h0, h1);
+  c0->batch_phases[1] = msd(h1, h2);
+  c0->batch_phases[2] = ms_copy;
+  c0->batch_phases[3] = msd(h2, std::chrono::steady_clock::now());
   if (bad >= 0)
     return c0->fail(DR_E_CAPACITY, "context %d: %lld pushed leaders, capacity %lld", bad, (long long)bad_np,
                     (long long)outs[bad].push_cap);

@@ -223,6 +223,162 @@ __global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int qu
 }
 
 // ---------------------------------------------------------------------------
+// k_commit_split: the same commit rule for a short wave range (a rank's share of
+// the all-waves commit sweep leaves most CUs idle with one workgroup per wave):
+// KS workgroups per wave, co-resident (cooperative launch).  Workgroup j of wave
+// w holds rows [j*RS, (j+1)*RS) of the wave's rounds 2..4 (RS a multiple of 64,
+// RS <= NT) and loads every chunk it needs up front -- none depends on S: round
+// 2 the 16-B chunk holding the leader's bit, rounds 3, 4 whole rows.  It
+// publishes its words of S_1, then of S_2, to Sg (disjoint words, no atomics);
+// the KS workgroups of the wave meet at a counter barrier after each.  |S_3| and
+// its repeated-slot count are summed with atomics; the last workgroup to arrive
+// writes commit / vcount and resets the wave's counters for the next launch.
+// A wave's workgroups sit on one XCD: blockIdx = (group * KS + j) * 8 + xcd,
+// wave = group * 8 + xcd.  A barrier that waits 2 s sets *err and every
+// workgroup ends (the host reports it and clears the counters); none hangs.
+// ---------------------------------------------------------------------------
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_commit_split(DagView g, int w0, int nw, int KS, int RS, int quorum,
+                                                     u64 *__restrict__ Sg, unsigned *__restrict__ cnt,
+                                                     int32_t *__restrict__ vacc, int32_t *__restrict__ err,
+                                                     uint8_t *__restrict__ commit, int32_t *__restrict__ vcount) {
+  using G = Geo<WS, NT>;
+  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP;
+  constexpr int MC = (NT * CPR + NT - 1) / NT;  // chunks per thread per round at RS = NT
+  __shared__ u64 S[WS], Tn[WS];
+  __shared__ int bad;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, grp = slot / KS, j = slot - grp * KS;
+  const int bi = grp * 8 + xcd;
+  if (bi >= nw) return;  // a slot of the last group past the range: no wave
+  const int w = w0 + bi, r1 = 4 * (w - 1) + 1, n = g.n;
+  const int l = g.lead[w] - 1;
+  if (!((g.present[(size_t)r1 * WS + (l >> 6)] >> (l & 63)) & 1ULL)) {  // leader is bottom (process.go:327-329)
+    if (j == 0 && tid == 0) { commit[bi] = 0; vcount[bi] = -1; }
+    return;
+  }
+  const int s0r = j * RS, s1r = min(n, s0r + RS);
+  // every load first: round 2's leader chunk (thread t: row s0r + t), rounds 3, 4 whole rows
+  const int lc = (l >> 6) / CW;  // chunk column of the leader's word
+  u64 a0 = 0, a1 = 0;
+  if (s0r + tid < s1r) {
+    const u64 *p = g.strong + ((size_t)(r1 + 1) * n + s0r + tid) * WS + lc * CW;
+    if constexpr (CW == 2) {
+      const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
+      a0 = x.x;
+      a1 = x.y;
+    } else {
+      a0 = __builtin_nontemporal_load(p);
+    }
+  }
+  const int jj = tid % CPR;
+  u64 v0[2][MC], v1[2][MC];
+#pragma unroll
+  for (int k = 0; k < 2; k++)
+#pragma unroll
+    for (int p = 0; p < MC; p++) {
+      const int s = s0r + tid / CPR + p * RPP;
+      v0[k][p] = 0;
+      v1[k][p] = 0;
+      if (s < s1r) {
+        const u64 *q = g.strong + ((size_t)(r1 + 2 + k) * n + s) * WS + jj * CW;
+        if constexpr (CW == 2) {
+          const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(q));
+          v0[k][p] = x.x;
+          v1[k][p] = x.y;
+        } else {
+          v0[k][p] = __builtin_nontemporal_load(q);
+        }
+      }
+    }
+  u64 *S1 = Sg + (size_t)bi * 2 * WS, *S2 = S1 + WS;
+  unsigned target = 0;
+  auto barrier = [&]() -> bool {  // the KS workgroups of wave bi
+    __syncthreads();
+    target += (unsigned)KS;
+    if (tid == 0) {
+      __threadfence();
+      atomicAdd(&cnt[bi], 1u);
+      const unsigned long long t0 = wall_clock64();
+      int e = 0;
+      while (__hip_atomic_load(&cnt[bi], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { e = 1; break; }
+        if (wall_clock64() - t0 > 200000000ULL) {
+          atomicOr(err, 1);
+          e = 1;
+          break;
+        }
+      }
+      bad = e;
+    }
+    __syncthreads();
+    return !bad;
+  };
+  // S_1 = the rows of round 2 holding the leader's bit: this workgroup's words
+  {
+    const u64 x = (CW == 2 && ((l >> 6) & 1)) ? a1 : a0;
+    const u64 m = __ballot(s0r + tid < s1r && ((x >> (l & 63)) & 1ULL));
+    if (lane == 0 && wid * 64 < RS && s0r + wid * 64 < n) S1[(s0r >> 6) + wid] = m;
+  }
+  if (!barrier()) return;
+  // S_2, S_3: rows of rounds 3, 4 against the published S_1, S_2
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if (tid < WS) {
+      S[tid] = __hip_atomic_load(&(k == 0 ? S1 : S2)[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      Tn[tid] = 0;
+    }
+    __syncthreads();
+    const u64 sa = S[jj * CW], sb = CW == 2 ? S[jj * CW + 1] : 0ULL;
+#pragma unroll
+    for (int p = 0; p < MC; p++) {
+      const int rowbase = s0r + (wid * 64) / CPR + p * RPP;  // first row of this wave's pass
+      if (rowbase >= s1r) break;                             // wave-uniform
+      const bool hit = ((v0[k][p] & sa) | (v1[k][p] & sb)) != 0ULL;
+      u64 m = __ballot(hit);
+      if (lane == 0 && m) {
+        u64 bits;
+        if constexpr (CPR == 1) {
+          bits = m;
+        } else {
+#pragma unroll
+          for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
+          bits = 0;
+#pragma unroll
+          for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
+        }
+        atomicOr(&Tn[rowbase >> 6], bits << (rowbase & 63));
+      }
+    }
+    __syncthreads();
+    if (k == 0) {
+      if (tid < RS / 64 && s0r + tid * 64 < n) S2[(s0r >> 6) + tid] = Tn[(s0r >> 6) + tid];
+      if (!barrier()) return;
+    }
+  }
+  // |S_3| over this workgroup's rows (+ repeated slots, process.go:330-335), summed over the wave
+  if (wid == 0) {
+    const int dc = dup_count<WS>(g, r1 + 3, lane < WS ? Tn[lane] : 0ULL);
+    int c = lane < WS ? popc64(Tn[lane]) : 0;
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if (lane == 0) {
+      atomicAdd(&vacc[bi], c + dc);
+      __threadfence();
+      const unsigned old = atomicAdd(&cnt[bi], 1u);
+      if (old == 3u * (unsigned)KS - 1u) {  // the last of the wave: every sum is in
+        __threadfence();
+        const int vc = __hip_atomic_load(&vacc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vcount[bi] = vc;
+        commit[bi] = vc >= quorum ? 1 : 0;
+        vacc[bi] = 0;
+        cnt[bi] = 0;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Round summaries (memo): per round r, U_r = OR of every strong row, WU_r[d] =
 // union of the weak targets at delta d+2, SD_r = total strong degree.  A sweep
 // whose frontier covers every present vertex of r (a "full" round) expands it

@@ -64,6 +64,7 @@
 
 #include "dagrider_gpu.h"
 #include "dagrider_shard.h"
+#include "shard_fused.hpp"
 #include "shard_memo.hpp"
 #include "wave_ops.hpp"
 
@@ -564,10 +565,12 @@ struct dr_shard {
   bool local = true;
   int persistent = 1;  // DR_SHARD_OPT_PERSISTENT
   int memo = 1;        // DR_SHARD_OPT_MEMO
+  int stepped = 0;     // DR_SHARD_OPT_STEPPED: the memo replay's stepped form even when every column is here
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipEvent_t evs[5] = {};  // the memo replay's phase boundaries
   ncclComm_t comm = nullptr;
   SBuf strong, weak, woff, ft[2], send, pend, cnt, out, qinfo;
   // per-vertex metadata, full width on every shard
@@ -585,7 +588,9 @@ struct dr_shard {
   // reset at each replay's start, grown after a stream sync
   char *pin = nullptr;
   size_t pin_cap = 0, pin_used = 0;
-  SBuf mnseg;                   // the canonical walk's final state (its segment count)
+  SBuf ppref;                   // [round] |P_1| + .. + |P_r| (present vertices, round 0 excluded)
+  std::vector<u64> h_ppref;
+  SBuf mSG, mout;               // speculative canonical digests; the memo replay's output region
   std::vector<std::vector<uint32_t>> h_weak;  // per local shard
   std::vector<std::vector<uint64_t>> h_woff;  // per local shard, absolute offsets, size nrounds+1
   // weak columns per local shard (the memoized replay, shard_memo.hpp): one entry per
@@ -1080,6 +1085,8 @@ drs::MArgs make_margs(dr_shard *c, int nq, int T = -1) {
   a.R = c->max_rounds;
   a.nlead = (int32_t)c->h_lead.size();
   a.good = c->mgood.as<uint8_t>();
+  a.slot_off = c->slot_off.as<uint32_t>();
+  a.slot_src = c->slot_src.as<uint16_t>();
   a.T = T >= 0 ? T : c->nrounds - 1;
   return a;
 }
@@ -1138,22 +1145,29 @@ char *stage(dr_shard *c, size_t n) {
   return c->pin + at;
 }
 
-int init_states(dr_shard *c, const std::vector<drs::MQuery> &qs) {
-  const int nq = (int)qs.size();
-  SHCHK(c, c->mq.ensure((size_t)nq * sizeof(drs::MQuery)));
-  SHCHK(c, c->mst.ensure((size_t)2 * nq * sizeof(drs::MState)));
-  auto *hq = reinterpret_cast<drs::MQuery *>(stage(c, (size_t)nq * sizeof(drs::MQuery)));
-  auto *st = reinterpret_cast<drs::MState *>(stage(c, (size_t)nq * sizeof(drs::MState)));
-  if (!hq || !st) return c->fail(DR_E_HIP, "pinned staging allocation failed");
-  for (int i = 0; i < nq; i++) {
-    hq[i] = qs[i];
-    st[i] = drs::MState{};
-    st[i].low = qs[i].top;
-    st[i].cur = qs[i].top;
-    st[i].fresh = qs[i].type == drs::MQ_CANON ? 1 : 0;
+// States of a stepped batch: queries [0, qs.size()) from the host (rings clear);
+// nq slots in all (k_ms_plan fills the chain slots past them).
+int init_states(dr_shard *c, const std::vector<drs::MQuery> &qs, int nq, bool states = true) {
+  const int nh = (int)qs.size();
+  SHCHK(c, c->mq.ensure((size_t)std::max(nq, 1) * sizeof(drs::MQuery)));
+  SHCHK(c, c->mst.ensure((size_t)2 * std::max(nq, 1) * sizeof(drs::MState)));
+  if (nh > 0) {
+    auto *hq = reinterpret_cast<drs::MQuery *>(stage(c, (size_t)nh * sizeof(drs::MQuery)));
+    auto *st = states ? reinterpret_cast<drs::MState *>(stage(c, (size_t)nh * sizeof(drs::MState))) : nullptr;
+    if (!hq || (states && !st)) return c->fail(DR_E_HIP, "pinned staging allocation failed");
+    std::copy(qs.begin(), qs.end(), hq);
+    SHCHK(c, hipMemcpyAsync(c->mq.p, hq, nh * sizeof(drs::MQuery), hipMemcpyHostToDevice, c->stream));
+    if (states) {
+      for (int i = 0; i < nh; i++) {
+        st[i] = drs::MState{};
+        st[i].low = qs[i].top;
+        st[i].cur = qs[i].top;
+        st[i].fresh = qs[i].type == drs::MQ_CANON ? 1 : 0;
+      }
+      SHCHK(c, hipMemcpyAsync(c->mst.p, st, nh * sizeof(drs::MState), hipMemcpyHostToDevice, c->stream));
+    }
   }
-  SHCHK(c, hipMemcpyAsync(c->mq.p, hq, nq * sizeof(drs::MQuery), hipMemcpyHostToDevice, c->stream));
-  SHCHK(c, hipMemcpyAsync(c->mst.p, st, nq * sizeof(drs::MState), hipMemcpyHostToDevice, c->stream));
+  if (!states) return DR_OK;
   SHCHK(c, c->mpend.ensure((size_t)c->nlocal * nq * c->depth * c->SP * 8));
   SHCHK(c, c->mrecv[0].ensure((size_t)c->G * nq * c->WSs * 8));
   SHCHK(c, c->mrecv[1].ensure((size_t)c->G * nq * c->WSs * 8));
@@ -1161,110 +1175,184 @@ int init_states(dr_shard *c, const std::vector<drs::MQuery> &qs) {
   return DR_OK;
 }
 
-// Round summaries, K^cand, good, the canonical segments and the canonical
-// prefixes C, E, G of the DAG's top round T.
-int build_canon(dr_shard *c, int T) {
-  const int W = c->W, SP = c->SP, nl = c->nlocal, dd = std::max(0, c->dmax - 1);
-  const size_t R = (size_t)c->max_rounds;
-  SHCHK(c, c->mU.ensure((size_t)nl * R * SP * 8));
-  SHCHK(c, c->mWU.ensure(std::max<size_t>((size_t)nl * R * dd * SP, 1) * 8));
-  SHCHK(c, c->mK.ensure((size_t)(T + 1) * W * 8));
-  SHCHK(c, c->mgood.ensure((size_t)T + 8));
-  SHCHK(c, c->mnseg.ensure(sizeof(drs::MState)));
-  for (SBuf *b : {&c->mRD, &c->mCE, &c->mRG, &c->mC, &c->mE, &c->mG}) SHCHK(c, b->ensure((size_t)(T + 1) * 8));
-  drs::MArgs a = make_margs(c, 1);
-  if (T >= 1) {
-    hipLaunchKernelGGL(drs::k_ms_summary, dim3(T, nl), dim3(drs::MS_NT), 0, c->stream, a, T, c->mU.as<u64>(),
-                       c->mWU.as<u64>());
-    SHCHK(c, hipGetLastError());
+// The memo replay's outputs, carved from one device region that comes back in
+// one copy: header, commits, vcounts, every query's final state, the canonical
+// walk's final state (stepped form), chain pushes, per-pop count | digest | edges.
+struct MOut {
+  int32_t *hdr;
+  uint8_t *commit;
+  int32_t *vcount;
+  drs::MState *fin, *canon;
+  int32_t *push;
+  u64 *qout;
+  size_t bytes;
+};
+MOut carve_out(char *base, int nw, int nq, int64_t pcap, int npop) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char *p = base + off;
+    off = (off + bytes + 63) & ~(size_t)63;
+    return p;
+  };
+  MOut m{};
+  m.hdr = reinterpret_cast<int32_t *>(take(drs::FH_N * 4));
+  m.commit = reinterpret_cast<uint8_t *>(take((size_t)nw));
+  m.vcount = reinterpret_cast<int32_t *>(take((size_t)nw * 4));
+  m.fin = reinterpret_cast<drs::MState *>(take((size_t)std::max(nq, 1) * sizeof(drs::MState)));
+  m.canon = reinterpret_cast<drs::MState *>(take(sizeof(drs::MState)));
+  m.push = reinterpret_cast<int32_t *>(take((size_t)std::max<int64_t>(pcap, 1) * 4));
+  m.qout = reinterpret_cast<u64 *>(take((size_t)3 * std::max(npop, 1) * 8));
+  m.bytes = off;
+  return m;
+}
+
+// vcount = |S_3| (the OR of the G partials), commit = vcount >= 2f+1; -1 / no
+// commit where the wave's leader is absent (process.go:327-329).  One wave per wave index.
+__global__ __launch_bounds__(256) void k_ms_vfinal(drs::MArgs a, drs::FArgs f, const u64 *__restrict__ P, int G) {
+  const int wi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wi >= f.nw) return;
+  const int w = wi + 1, r1 = 4 * wi + 1, L = (w < a.nlead ? (int)a.lead[w] : 1) - 1;
+  const bool has = (a.pres[(size_t)r1 * a.W + (L >> 6)] >> (L & 63)) & 1ULL;
+  u64 v = 0;
+  if (lane < a.W)
+    for (int g = 0; g < G; g++) v |= P[((size_t)g * f.nw + wi) * a.W + lane];
+  const int cnt = (int)dr::wave_sum((u64)__popcll(v));
+  if (lane == 0) {
+    f.vcount[wi] = has ? cnt : -1;
+    f.commit[wi] = has && cnt >= f.quorum ? 1 : 0;
   }
-  const int rb = (T + 1 + 3) / 4;
-  if (c->local) {
-    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, nl), dim3(drs::MS_NT), 0, c->stream, a, T, (u64 *)nullptr);
-    SHCHK(c, hipGetLastError());
-  } else {
-    SHCHK(c, c->mksend.ensure((size_t)(T + 1) * c->WSs * 8));
-    SHCHK(c, c->mkrecv.ensure((size_t)c->G * (T + 1) * c->WSs * 8));
-    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, nl), dim3(drs::MS_NT), 0, c->stream, a, T, c->mksend.as<u64>());
-    SHCHK(c, hipGetLastError());
-    SHNCCL(c, ncclAllGather(c->mksend.p, c->mkrecv.p, (size_t)(T + 1) * c->WSs, ncclUint64, c->comm, c->stream));
-    c->last_xbytes += (uint64_t)(T + 1) * c->WSs * 8;
-    const size_t tot = (size_t)(T + 1) * W;
-    hipLaunchKernelGGL(drs::k_ms_kunpack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, a, T,
-                       c->mkrecv.as<u64>());
-    SHCHK(c, hipGetLastError());
-  }
-  hipLaunchKernelGGL(drs::k_ms_good, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a, T, c->mgood.as<uint8_t>());
-  SHCHK(c, hipGetLastError());
-  // the canonical segments, top down (k_canon's walk, kernels.hpp): one MQ_CANON
-  // query finds each bad round on the device (good[]) and sweeps until dmax
-  // consecutive full rounds restore the regime; no host round trip per segment
-  drs::MQuery q{};
-  q.type = drs::MQ_CANON;
-  q.top = T;
-  q.bottom = 0;
-  q.src0 = -1;
-  if (int rc = init_states(c, {q})) return rc;
-  drs::MArgs sa = make_margs(c, 1, T);
-  int steps = 0;
-  if (int rc = run_steps(c, sa, 1, T + 2 * std::max(1, c->nrounds), &steps, c->hint_canon)) return rc;
-  c->hint_canon = steps;
-  SHCHK(c, hipMemcpyAsync(c->mnseg.p, (steps & 1) ? sa.st1 : sa.st0, sizeof(drs::MState), hipMemcpyDeviceToDevice,
-                          c->stream));
-  hipLaunchKernelGGL(drs::k_ms_cstats, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a, T, c->mRD.as<u64>(),
-                     c->mCE.as<u64>());
-  SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, c->mRD.as<u64>(), c->mC.as<u64>(),
-                     c->mCE.as<u64>(), c->mE.as<u64>());
-  SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(drs::k_ms_rg, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a, T, c->slot_off.as<uint32_t>(),
-                     c->slot_src.as<uint16_t>(), c->mC.as<u64>(), c->mRG.as<u64>());
-  SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, c->mRG.as<u64>(), c->mG.as<u64>(),
-                     (const u64 *)nullptr, (u64 *)nullptr);
-  SHCHK(c, hipGetLastError());
-  (void)dd;
-  return DR_OK;
 }
 
 int paper_emit(dr_shard *c, const drs::MArgs &a, const std::vector<drs::MQuery> &qs,
                const std::vector<drs::MState> &fin, const std::vector<int> &pop_query, std::vector<uint64_t> &qout,
                int npop);
 
-// dr_shard_replay on the memo path (REF: k_ms_emit; PAPER: paper_emit).
-int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
-  const bool paper = deliver_mode == DR_DELIVER_PAPER;
-  hipEvent_t ev[5] = {};
-  for (auto &e : ev) SHCHK(c, hipEventCreate(&e));
-  struct EvGuard { hipEvent_t *e; ~EvGuard() { for (int i = 0; i < 5; i++) if (e[i]) (void)hipEventDestroy(e[i]); } } eg{ev};
-  const int T = c->nrounds - 1, W = c->W;
-  if (int rc = prepare_queries(c, 0)) return rc;  // uploads the weak edges and columns
-  SHCHK(c, hipStreamSynchronize(c->stream));
-  c->pin_used = 0;
-  SHCHK(c, hipEventRecord(ev[0], c->stream));
-  // 1. commit decisions of every wave (three exchanges)
-  if (int rc = votes(c, 1, nwaves, o->commit, o->vcount)) return rc;
-  SHCHK(c, hipEventRecord(ev[1], c->stream));
-  uint64_t ce = 0;
-  for (int w = 1; w <= nwaves; w++)
-    if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
-  o->commit_edges = ce;
-  // 2. summaries and the canonical cone
-  if (int rc = build_canon(c, T)) return rc;
-  SHCHK(c, hipEventRecord(ev[2], c->stream));
-  // 3. one batch: a cone for every wave whose leader is present (a superset of the
-  // leaders any chain can push) and the chain of every commit that needs one
-  std::vector<ChainTask> tasks;
-  int lastw = 0;
-  for (int w = 1; w <= nwaves; w++)
-    if (o->commit[w - 1]) {
-      tasks.push_back(ChainTask{w, chain_mode == DR_CHAIN_PERSISTENT ? lastw : 0});
-      lastw = w;
+// The stepped form's device phase (one round of every live query per launch, an
+// exchange between launches; what one rank of an RCCL group of G > 1 runs, and
+// local mode with DR_SHARD_OPT_STEPPED): the pass with this context's partial
+// S_1, vote steps 2 and 3 with their exchanges, K^cand and its exchange, the
+// canonical walk stepped, the canonical prefixes, then every pop and chain
+// stepped together.  Writes m.commit / m.vcount / m.fin / m.canon.
+int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int nq, drs::FArgs f, const MOut &m,
+                  int64_t pcap, int *steps_out) {
+  const int T = c->nrounds - 1, W = c->W, G = c->G, nl = c->nlocal;
+  drs::MArgs a1 = make_margs(c, 1, T);
+  a1.slot_off = c->slot_off.as<uint32_t>();
+  a1.slot_src = c->slot_src.as<uint16_t>();
+  // 1. the pass (U, WU per shard) + this context's partial S_1, then steps 2, 3
+  const size_t pw = (size_t)G * nw * W * 8;
+  SHCHK(c, c->vote_p[0].ensure(pw));
+  SHCHK(c, c->vote_p[1].ensure(pw));
+  SHCHK(c, c->vote_send.ensure((size_t)nw * W * 8));
+  u64 *P1 = c->vote_p[1].as<u64>(), *P0 = c->vote_p[0].as<u64>();
+  if (c->local) SHCHK(c, hipMemsetAsync(P1, 0, pw, c->stream));  // slots 1..G-1: the pass merges every local shard into slot 0
+  {
+    const size_t lds = ((size_t)2 * nl * c->SP + W + (size_t)nl * a1.dd * c->SP) * 8;
+    hipLaunchKernelGGL((drs::k_ms_pass<512, 8>), dim3((T + 3) / 4), dim3(512), lds, c->stream, a1, f, nw,
+                       (int)drs::VOTE_STEP1, c->mU.as<u64>(), c->mWU.as<u64>(), c->local ? P1 : c->vote_send.as<u64>());
+    SHCHK(c, hipGetLastError());
+  }
+  if (!c->local) {
+    SHNCCL(c, ncclAllGather(c->vote_send.p, P1, (size_t)nw * W, ncclUint64, c->comm, c->stream));
+    c->last_xbytes += (uint64_t)nw * W * 8;
+  }
+  ShardArgs sa = make_args(c, 0, 1);
+  const int bpw = (c->n + SH_NT - 1) / SH_NT;
+  for (int k = 2; k <= 3; k++) {
+    u64 *pin = k == 2 ? P1 : P0, *pout = k == 2 ? P0 : P1;
+    hipLaunchKernelGGL(k_shard_vote, dim3(nw * bpw, nl), dim3(SH_NT), 0, c->stream, sa, 1, nw, k, G,
+                       (const u64 *)nullptr, pin, c->local ? pout : c->vote_send.as<u64>());
+    SHCHK(c, hipGetLastError());
+    if (!c->local) {
+      SHNCCL(c, ncclAllGather(c->vote_send.p, pout, (size_t)nw * W, ncclUint64, c->comm, c->stream));
+      c->last_xbytes += (uint64_t)nw * W * 8;
     }
+  }
+  hipLaunchKernelGGL(k_ms_vfinal, dim3((nw + 3) / 4), dim3(256), 0, c->stream, a1, f, (const u64 *)P1, G);
+  SHCHK(c, hipGetLastError());
+  SHCHK(c, hipEventRecord(c->evs[1], c->stream));
+  // 2. K^cand (exchanged), good, the canonical walk, the canonical prefixes
+  const int rb = (T + 1 + 3) / 4;
+  if (c->local) {
+    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, nl), dim3(drs::MS_NT), 0, c->stream, a1, T, (u64 *)nullptr);
+    SHCHK(c, hipGetLastError());
+  } else {
+    SHCHK(c, c->mksend.ensure((size_t)(T + 1) * c->WSs * 8));
+    SHCHK(c, c->mkrecv.ensure((size_t)G * (T + 1) * c->WSs * 8));
+    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, nl), dim3(drs::MS_NT), 0, c->stream, a1, T, c->mksend.as<u64>());
+    SHCHK(c, hipGetLastError());
+    SHNCCL(c, ncclAllGather(c->mksend.p, c->mkrecv.p, (size_t)(T + 1) * c->WSs, ncclUint64, c->comm, c->stream));
+    c->last_xbytes += (uint64_t)(T + 1) * c->WSs * 8;
+    const size_t tot = (size_t)(T + 1) * W;
+    hipLaunchKernelGGL(drs::k_ms_kunpack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, a1, T,
+                       c->mkrecv.as<u64>());
+    SHCHK(c, hipGetLastError());
+  }
+  hipLaunchKernelGGL(drs::k_ms_good, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a1, T, c->mgood.as<uint8_t>());
+  SHCHK(c, hipGetLastError());
+  {
+    drs::MQuery q{};
+    q.type = drs::MQ_CANON;
+    q.top = T;
+    q.bottom = 0;
+    q.src0 = -1;
+    if (int rc = init_states(c, {q}, 1)) return rc;
+    drs::MArgs sa1 = make_margs(c, 1, T);
+    int steps = 0;
+    if (int rc = run_steps(c, sa1, 1, T + 2 * std::max(1, c->nrounds), &steps, c->hint_canon)) return rc;
+    c->hint_canon = steps;
+    SHCHK(c, hipMemcpyAsync(m.canon, (steps & 1) ? sa1.st1 : sa1.st0, sizeof(drs::MState), hipMemcpyDeviceToDevice,
+                            c->stream));
+  }
+  hipLaunchKernelGGL(drs::k_ms_cstats, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a1, T, f.RD, f.CE);
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, (const u64 *)f.RD, f.Cc,
+                     (const u64 *)f.CE, f.Ec);
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_rg, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a1, T, c->slot_off.as<uint32_t>(),
+                     c->slot_src.as<uint16_t>(), (const u64 *)f.Cc, f.RG);
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
+                     (const u64 *)nullptr, (u64 *)nullptr);
+  SHCHK(c, hipGetLastError());
+  SHCHK(c, hipEventRecord(c->evs[2], c->stream));
+  // 3. every pop and every chain (planned on the device from the commits), stepped together
+  if (int rc = init_states(c, pops, nq)) return rc;
+  drs::MArgs a = make_margs(c, nq);
+  a.slot_off = c->slot_off.as<uint32_t>();
+  a.slot_src = c->slot_src.as<uint16_t>();
+  a.push_out = m.push;
+  hipLaunchKernelGGL((drs::k_ms_plan<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
+                     c->mst.as<drs::MState>(), (int)pcap);
+  SHCHK(c, hipGetLastError());
+  SHCHK(c, hipMemsetAsync(c->mpend.p, 0, (size_t)nl * nq * c->depth * c->SP * 8, c->stream));
+  int steps = 0;
+  if (int rc = run_steps(c, a, nq, T + 2, &steps, c->hint_batch)) return rc;
+  c->hint_batch = steps;
+  SHCHK(c, hipMemcpyAsync(m.fin, (steps & 1) ? a.st1 : a.st0, (size_t)nq * sizeof(drs::MState),
+                          hipMemcpyDeviceToDevice, c->stream));
+  *steps_out = steps;
+  return DR_OK;
+}
+
+// dr_shard_replay on the memo path.  Fused form (the context holds every column:
+// local mode, a one-rank group): every kernel reads all columns, so nothing is
+// exchanged and each query runs to its end in one launch -- the pass (U, WU,
+// speculative digests and the complete vote), K^cand, the canonical walk, the
+// canonical digests and prefixes, the chain plan, one sweep launch for every pop
+// and chain, the emission: eight launches and one copy back.  Stepped form:
+// stepped_phase.  REF emission k_ms_emit; PAPER paper_emit after the copy.
+int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
+  const bool paper = deliver_mode == DR_DELIVER_PAPER, persistent = chain_mode == DR_CHAIN_PERSISTENT;
+  const bool fused = c->nlocal == c->G && !c->stepped;
+  const int T = c->nrounds - 1, W = c->W, nw = nwaves;
+  if (int rc = sync_weak(c)) return rc;  // uploads the weak edges and columns after an append
+  c->pin_used = 0;
+  // one cone query per wave whose leader is present (a superset of the leaders any chain can push)
   std::vector<drs::MQuery> qs;
-  std::vector<int> popq(nwaves + 1, -1);
+  std::vector<int> popq(nw + 1, -1);
   int64_t moff = 0;
-  for (int w = 1; w <= nwaves; w++) {
+  for (int w = 1; w <= nw; w++) {
     const int r1 = 4 * (w - 1) + 1, L = c->lead_src(w);
     if (!c->is_present(r1, L)) continue;
     drs::MQuery q{};
@@ -1277,121 +1365,166 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     popq[w] = (int)qs.size();
     qs.push_back(q);
   }
-  const int npop = (int)qs.size();
-  std::vector<int> chainq(tasks.size(), -1);
-  int32_t pbase = 0;
-  int maxsteps = 2;
-  for (auto &q : qs) maxsteps = std::max(maxsteps, q.top - q.bottom + 2);
-  for (size_t i = 0; i < tasks.size(); i++) {
-    if (tasks[i].wave - 1 < tasks[i].floor + 1) continue;
-    if (tasks[i].floor < 0) return c->fail(DR_E_INVAL, "decidedWave %d < 0 (Go: waveRound(0,1) index out of range)", tasks[i].floor);
-    drs::MQuery q{};
-    q.type = drs::MQ_CHAIN;
-    q.top = 4 * (tasks[i].wave - 1) + 1;
-    q.bottom = 4 * tasks[i].floor + 1;
-    q.src0 = c->lead_src(tasks[i].wave) - 1;
-    q.push_base = pbase;
-    pbase += (q.top - q.bottom) / 4 + 1;
-    maxsteps = std::max(maxsteps, q.top - q.bottom + 2);
-    chainq[i] = (int)qs.size();
-    qs.push_back(q);
-  }
-  const int nq = (int)qs.size();
+  const int npop = (int)qs.size(), nq = npop + nw;
+  const int64_t pcap = persistent ? (int64_t)nw : (int64_t)nw * (nw + 1) / 2;
+  if (pcap > ((int64_t)1 << 26)) return c->fail(DR_E_CAPACITY, "literal chains of %d waves: push bound %lld", nw, (long long)pcap);
+  // buffers
+  const size_t R = (size_t)c->max_rounds;
+  const int nl = c->nlocal, dd = std::max(0, c->dmax - 1);
+  SHCHK(c, c->mU.ensure((size_t)nl * R * c->SP * 8));
+  SHCHK(c, c->mWU.ensure(std::max<size_t>((size_t)nl * R * dd * c->SP, 1) * 8));
+  SHCHK(c, c->mK.ensure((size_t)(T + 1) * W * 8));
+  SHCHK(c, c->mgood.ensure((size_t)T + 16));
+  for (SBuf *b : {&c->mRD, &c->mCE, &c->mRG, &c->mC, &c->mE, &c->mG, &c->mSG}) SHCHK(c, b->ensure((size_t)(T + 1) * 8));
+  SHCHK(c, c->mmasks.ensure((size_t)std::max<int64_t>(moff, 1) * 8));
+  MOut m = carve_out(nullptr, nw, nq, pcap, npop);
+  SHCHK(c, c->mout.ensure(m.bytes));
+  m = carve_out(c->mout.as<char>(), nw, nq, pcap, npop);
+  SHCHK(c, hipMemsetAsync(m.hdr, 0, drs::FH_N * 4, c->stream));
+  drs::FArgs f{};
+  f.ppref = c->ppref.as<u64>();
+  f.SG = c->mSG.as<u64>();
+  f.RD = c->mRD.as<u64>();
+  f.CE = c->mCE.as<u64>();
+  f.RG = c->mRG.as<u64>();
+  f.Cc = c->mC.as<u64>();
+  f.Ec = c->mE.as<u64>();
+  f.Gc = c->mG.as<u64>();
+  f.good = c->mgood.as<uint8_t>();
+  f.hdr = m.hdr;
+  f.commit = m.commit;
+  f.vcount = m.vcount;
+  f.fin = m.fin;
+  f.quorum = 2 * c->f + 1;
+  f.nw = nw;
+  f.npop = npop;
+  f.persistent = persistent ? 1 : 0;
+  SHCHK(c, hipEventRecord(c->evs[0], c->stream));
   int steps = 0;
-  std::vector<drs::MState> fin(nq);
-  drs::MState canon_fin{};
-  uint64_t *hq_out = nullptr;
-  drs::MState *hfin = nullptr;
-  int32_t *hpush = nullptr;
-  std::vector<int32_t> pushes_dev(std::max(pbase, 1));
-  std::vector<uint64_t> qout((size_t)3 * std::max(npop, 1));
-  if (nq > 0) {
-    if (int rc = init_states(c, qs)) return rc;
-    SHCHK(c, c->mmasks.ensure((size_t)std::max<int64_t>(moff, 1) * 8));
-    SHCHK(c, c->mpush.ensure((size_t)std::max(pbase, 1) * 4));
-    SHCHK(c, hipMemsetAsync(c->mpend.p, 0, (size_t)c->nlocal * nq * c->depth * c->SP * 8, c->stream));
+  if (fused) {
+    if (int rc = init_states(c, qs, nq, false)) return rc;  // the pop queries; chains are planned on the device
     drs::MArgs a = make_margs(c, nq);
-    if (int rc = run_steps(c, a, nq, maxsteps, &steps, c->hint_batch)) return rc;
-    c->hint_batch = steps;
-    SHCHK(c, hipEventRecord(ev[3], c->stream));
-    // 4. emission of every pop query (REF; PAPER needs the pop order, below)
-    if (npop > 0 && !paper) {
-      std::vector<int32_t> qidx(npop);
-      for (int i = 0; i < npop; i++) qidx[i] = i;
-      SHCHK(c, c->mqidx.ensure((size_t)npop * 4));
-      SHCHK(c, c->mqout.ensure((size_t)3 * npop * 8));
-      SHCHK(c, hipMemcpyAsync(c->mqidx.p, qidx.data(), (size_t)npop * 4, hipMemcpyHostToDevice, c->stream));
-      u64 *qo = c->mqout.as<u64>();
-      hipLaunchKernelGGL(drs::k_ms_emit, dim3(npop), dim3(drs::MS_NT), 0, c->stream, a, c->mqidx.as<int32_t>(),
-                         (steps & 1) ? a.st1 : a.st0, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
-                         c->mC.as<u64>(), c->mG.as<u64>(), c->mE.as<u64>(), qo, qo + npop, qo + 2 * npop);
-      SHCHK(c, hipGetLastError());
-      hq_out = reinterpret_cast<uint64_t *>(stage(c, (size_t)3 * npop * 8));
-      if (!hq_out) return c->fail(DR_E_HIP, "pinned staging allocation failed");
-      SHCHK(c, hipMemcpyAsync(hq_out, qo, (size_t)3 * npop * 8, hipMemcpyDeviceToHost, c->stream));
-    }
-    hfin = reinterpret_cast<drs::MState *>(stage(c, nq * sizeof(drs::MState)));
-    hpush = reinterpret_cast<int32_t *>(stage(c, (size_t)std::max(pbase, 1) * 4));
-    if (!hfin || !hpush) return c->fail(DR_E_HIP, "pinned staging allocation failed");
-    SHCHK(c, hipMemcpyAsync(hfin, (steps & 1) ? a.st1 : a.st0, nq * sizeof(drs::MState), hipMemcpyDeviceToHost,
-                            c->stream));
-    SHCHK(c, hipMemcpyAsync(&canon_fin, c->mnseg.p, sizeof canon_fin, hipMemcpyDeviceToHost, c->stream));
-    if (pbase) SHCHK(c, hipMemcpyAsync(hpush, c->mpush.p, (size_t)pbase * 4, hipMemcpyDeviceToHost, c->stream));
+    a.slot_off = c->slot_off.as<uint32_t>();
+    a.slot_src = c->slot_src.as<uint16_t>();
+    a.good = f.good;
+    a.push_out = m.push;
+    const int rb = (T + 1 + 3) / 4;
+    const size_t lds_pass = ((size_t)2 * nl * c->SP + W + (size_t)nl * dd * c->SP) * 8;
+    hipLaunchKernelGGL((drs::k_ms_pass<512, 8>), dim3((T + 3) / 4), dim3(512), lds_pass, c->stream, a, f, nw,
+                       (int)drs::VOTE_FULL, c->mU.as<u64>(), c->mWU.as<u64>(), (u64 *)nullptr);
+    SHCHK(c, hipGetLastError());
+    SHCHK(c, hipEventRecord(c->evs[1], c->stream));
+    hipLaunchKernelGGL(drs::k_ms_kcand_full, dim3(rb), dim3(256), 0, c->stream, a, f);
+    SHCHK(c, hipGetLastError());
+    const size_t lds_ring = ((size_t)c->depth * W + W) * 8;
+    hipLaunchKernelGGL((drs::k_ms_canon_full<512>), dim3(1), dim3(512), lds_ring, c->stream, a, f);
+    SHCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(drs::k_ms_rg_full, dim3(rb), dim3(256), 0, c->stream, a, f);
+    SHCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
+                       (const u64 *)f.CE, f.Ec);
+    SHCHK(c, hipGetLastError());
+    SHCHK(c, hipEventRecord(c->evs[2], c->stream));
+    hipLaunchKernelGGL((drs::k_ms_plan<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
+                       (drs::MState *)nullptr, (int)pcap);
+    SHCHK(c, hipGetLastError());
+    hipLaunchKernelGGL((drs::k_ms_sweep_full<256>), dim3(nq), dim3(256), lds_ring, c->stream, a, f);
+    SHCHK(c, hipGetLastError());
   } else {
-    SHCHK(c, hipEventRecord(ev[3], c->stream));
-    SHCHK(c, hipMemcpyAsync(&canon_fin, c->mnseg.p, sizeof canon_fin, hipMemcpyDeviceToHost, c->stream));
+    if (int rc = stepped_phase(c, nw, qs, nq, f, m, pcap, &steps)) return rc;
   }
-  SHCHK(c, hipEventRecord(ev[4], c->stream));
-  SHCHK(c, hipEventSynchronize(ev[4]));
-  if (hq_out) std::copy(hq_out, hq_out + (size_t)3 * npop, qout.begin());
-  if (hfin) std::copy(hfin, hfin + nq, fin.begin());
-  if (hpush && pbase) std::copy(hpush, hpush + pbase, pushes_dev.begin());
-  SHCHK(c, hipEventElapsedTime(&o->ms_commit, ev[0], ev[1]));
-  SHCHK(c, hipEventElapsedTime(&o->ms_summary, ev[1], ev[2]));
-  SHCHK(c, hipEventElapsedTime(&o->ms_deliver, ev[2], ev[3]));
-  SHCHK(c, hipEventElapsedTime(&o->ms_emit, ev[3], ev[4]));
+  SHCHK(c, hipEventRecord(c->evs[3], c->stream));
+  drs::MArgs a = make_margs(c, nq);
+  a.slot_off = c->slot_off.as<uint32_t>();
+  a.slot_src = c->slot_src.as<uint16_t>();
+  if (npop > 0 && !paper) {  // REF emission of every pop query (PAPER needs the pop order, below)
+    hipLaunchKernelGGL(drs::k_ms_emit, dim3(npop), dim3(drs::MS_NT), 0, c->stream, a, (const int32_t *)nullptr,
+                       (const drs::MState *)m.fin, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
+                       (const u64 *)f.Cc, (const u64 *)f.Gc, (const u64 *)f.Ec, m.qout, m.qout + npop,
+                       m.qout + 2 * npop);
+    SHCHK(c, hipGetLastError());
+  }
+  SHCHK(c, hipEventRecord(c->evs[4], c->stream));
+  char *hb = stage(c, m.bytes);
+  if (!hb) return c->fail(DR_E_HIP, "pinned staging allocation failed");
+  SHCHK(c, hipMemcpyAsync(hb, c->mout.p, m.bytes, hipMemcpyDeviceToHost, c->stream));
+  SHCHK(c, hipStreamSynchronize(c->stream));
+  const MOut h = carve_out(hb, nw, nq, pcap, npop);
+  SHCHK(c, hipEventElapsedTime(&o->ms_commit, c->evs[0], c->evs[1]));
+  SHCHK(c, hipEventElapsedTime(&o->ms_summary, c->evs[1], c->evs[2]));
+  SHCHK(c, hipEventElapsedTime(&o->ms_deliver, c->evs[2], c->evs[3]));
+  SHCHK(c, hipEventElapsedTime(&o->ms_emit, c->evs[3], c->evs[4]));
   o->ms_chain = 0;
-  o->canon_segments = canon_fin.npush;
-  // 5. assembly: pushes per commit, pops in stack order, each pop = its leader's query
-  std::vector<std::vector<int32_t>> pushes(tasks.size());
+  if (h.hdr[drs::FH_ERR]) return c->fail(DR_E_CAPACITY, "chain pushes exceed the bound %lld", (long long)pcap);
+  std::memcpy(o->commit, h.commit, (size_t)nw);
+  std::memcpy(o->vcount, h.vcount, (size_t)nw * 4);
+  o->canon_segments = fused ? h.hdr[drs::FH_NSEG] : h.canon->npush;
+  uint64_t ce = 0;
+  for (int w = 1; w <= nw; w++)
+    if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
+  o->commit_edges = ce;
+  // the chain tasks k_ms_plan made, in the same order: chain i is query npop + i
+  struct Task { int wave, q; int32_t pbase; };
+  std::vector<Task> tasks;  // every commit, q = -1 without a chain query
+  {
+    int lastw = 0, nch = 0;
+    int32_t pb = 0;
+    for (int w = 1; w <= nw; w++)
+      if (o->commit[w - 1]) {
+        const int fl = persistent ? lastw : 0;
+        Task t{w, -1, 0};
+        if (w - 1 >= fl + 1) {
+          t.q = npop + nch++;
+          t.pbase = pb;
+          pb += w - fl;
+        }
+        tasks.push_back(t);
+        lastw = w;
+      }
+    if (nch != h.hdr[drs::FH_NCHAIN]) return c->fail(DR_E_HIP, "memo replay: %d chains planned on the device, %d on the host", h.hdr[drs::FH_NCHAIN], nch);
+  }
   uint64_t chain_e = 0;
-  for (size_t i = 0; i < tasks.size(); i++) {
-    pushes[i].push_back(tasks[i].wave);
-    if (chainq[i] < 0) continue;
-    const drs::MState &f = fin[chainq[i]];
-    const drs::MQuery &q = qs[chainq[i]];
-    for (int x = 0; x < f.npush; x++) pushes[i].push_back(pushes_dev[q.push_base + x]);
-    chain_e += f.edges;
+  int64_t np = 0;
+  for (const Task &t : tasks) {
+    np += 1 + (t.q >= 0 ? h.fin[t.q].npush : 0);
+    if (t.q >= 0) chain_e += h.fin[t.q].edges;
   }
   o->chain_edges = chain_e;
-  int64_t np = 0;
-  for (auto &p : pushes) np += (int64_t)p.size();
   o->n_push = np;
   if (np > o->push_cap || !o->push_wave || !o->pop_count || !o->pop_digest)
     return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)np, (long long)o->push_cap);
   int64_t at = 0;
-  size_t t = 0;
+  size_t ti = 0;
   std::vector<int> pop_query;
-  for (int w = 1; w <= nwaves; w++) {
+  for (int w = 1; w <= nw; w++) {
     o->push_off[w - 1] = (uint32_t)at;
-    if (t < tasks.size() && tasks[t].wave == w) {
-      for (int32_t pw : pushes[t]) o->push_wave[at++] = pw;
-      for (auto it = pushes[t].rbegin(); it != pushes[t].rend(); ++it) {
-        const int q = popq[*it];
-        if (q < 0) return c->fail(DR_E_HIP, "memo replay: pushed wave %d has no cone query", *it);
+    if (ti < tasks.size() && tasks[ti].wave == w) {
+      const Task &t = tasks[ti];
+      const int64_t a0 = at;
+      o->push_wave[at++] = w;
+      if (t.q >= 0)
+        for (int x = 0; x < h.fin[t.q].npush; x++) o->push_wave[at++] = h.push[t.pbase + x];
+      for (int64_t y = at - 1; y >= a0; y--) {  // pops: the stack's LIFO order
+        const int q = popq[o->push_wave[y]];
+        if (q < 0) return c->fail(DR_E_HIP, "memo replay: pushed wave %d has no cone query", o->push_wave[y]);
         pop_query.push_back(q);
       }
-      t++;
+      ti++;
     }
   }
-  o->push_off[nwaves] = (uint32_t)at;
+  o->push_off[nw] = (uint32_t)at;
+  std::vector<uint64_t> qout(h.qout, h.qout + (size_t)3 * std::max(npop, 1));
+  if (fused) {
+    steps = 0;
+    for (int i = 0; i < npop; i++) steps = std::max(steps, qs[i].top - h.fin[i].stop + 1);
+  }
   if (paper && !pop_query.empty()) {
-    drs::MArgs a = make_margs(c, nq);
-    SHCHK(c, hipEventRecord(ev[3], c->stream));
+    std::vector<drs::MState> fin(h.fin, h.fin + npop);
+    SHCHK(c, hipEventRecord(c->evs[3], c->stream));
     if (int rc = paper_emit(c, a, qs, fin, pop_query, qout, npop)) return rc;
-    SHCHK(c, hipEventRecord(ev[4], c->stream));
-    SHCHK(c, hipEventSynchronize(ev[4]));
-    SHCHK(c, hipEventElapsedTime(&o->ms_emit, ev[3], ev[4]));
+    SHCHK(c, hipEventRecord(c->evs[4], c->stream));
+    SHCHK(c, hipEventSynchronize(c->evs[4]));
+    SHCHK(c, hipEventElapsedTime(&o->ms_emit, c->evs[3], c->evs[4]));
   }
   uint64_t de = 0;
   std::vector<uint8_t> seen(paper ? npop : 0, 0);
@@ -1408,6 +1541,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   o->deliver_edges = de;
   o->sweep_count = (uint64_t)npop;
   o->sweep_partial = (uint64_t)steps;
+  c->last_rounds = (uint64_t)steps;
   return DR_OK;
 }
 
@@ -1528,7 +1662,12 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   if (sh_set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev0, hipEventReleaseToDevice) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev1, hipEventReleaseToDevice) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev2, hipEventReleaseToDevice) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev2, hipEventReleaseToDevice) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evs[0], hipEventReleaseToDevice) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evs[1], hipEventReleaseToDevice) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evs[2], hipEventReleaseToDevice) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evs[3], hipEventReleaseToDevice) != hipSuccess ||
+      hipEventCreateWithFlags(&c->evs[4], hipEventReleaseToDevice) != hipSuccess) {
     g_shard_err = "dr_shard_create: stream/event creation failed";
     dr_shard_destroy(c);
     return DR_E_HIP;
@@ -1541,6 +1680,7 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
       c->sdeg.ensure((size_t)max_rounds * n * 2) != hipSuccess ||
       c->wdeg.ensure((size_t)max_rounds * n * 2) != hipSuccess ||
       c->rdeg.ensure((size_t)max_rounds * 8) != hipSuccess || c->sdr.ensure((size_t)max_rounds * 8) != hipSuccess ||
+      c->ppref.ensure((size_t)max_rounds * 8) != hipSuccess ||
       hipHostMalloc((void **)&c->alive, 64, hipHostMallocDefault) != hipSuccess ||
       c->slot_off.ensure(((size_t)max_rounds + 1) * 4) != hipSuccess ||
       c->lead.ensure(c->h_lead.size() * 2) != hipSuccess ||
@@ -1572,7 +1712,8 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (SBuf *b : {&c->wck, &c->wcr, &c->wcro, &c->sdr, &c->mU, &c->mWU, &c->mK, &c->mgood, &c->mRD, &c->mCE, &c->mRG,
                   &c->mC, &c->mE, &c->mG, &c->mksend, &c->mkrecv, &c->mq, &c->mst, &c->mpend, &c->mrecv[0],
-                  &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout, &c->mnseg})
+                  &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout, &c->ppref, &c->mSG,
+                  &c->mout})
     b->release();
   if (c->alive) (void)hipHostFree(c->alive);
   if (c->pin) (void)hipHostFree(c->pin);
@@ -1581,7 +1722,7 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
                   &c->errf, &c->push_out, &c->push_n, &c->cedges, &c->vote_s0, &c->vote_p[0], &c->vote_p[1],
                   &c->vote_send, &c->vcount, &c->D, &c->pcnt, &c->qcnt, &c->qedges, &c->qdig})
     b->release();
-  for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2})
+  for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->evs[0], c->evs[1], c->evs[2], c->evs[3], c->evs[4]})
     if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1608,6 +1749,10 @@ extern "C" int dr_shard_set_option(dr_shard *c, int option, int value) {
   }
   if (option == DR_SHARD_OPT_MEMO) {
     c->memo = value ? 1 : 0;
+    return DR_OK;
+  }
+  if (option == DR_SHARD_OPT_STEPPED) {
+    c->stepped = value ? 1 : 0;
     return DR_OK;
   }
   return c->fail(DR_E_INVAL, "unknown option %d", option);
@@ -1747,6 +1892,17 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
                           c->stream));
   SHCHK(c, hipMemcpyAsync(c->rdeg.as<u64>() + r0, rd.data(), rd.size() * 8, hipMemcpyHostToDevice, c->stream));
   SHCHK(c, hipMemcpyAsync(c->sdr.as<u64>() + r0, deg.data(), deg.size() * 8, hipMemcpyHostToDevice, c->stream));
+  {  // presence prefix (the canonical positions when every round below is full)
+    const size_t base = c->h_ppref.size();
+    for (int i = 0; i < k; i++) {
+      uint64_t np = 0;
+      for (int w = 0; w < W; w++) np += (uint64_t)__builtin_popcountll(pres[(size_t)i * W + w]);
+      const int r = r0 + i;
+      c->h_ppref.push_back(r == 0 ? 0 : (c->h_ppref.empty() ? 0 : c->h_ppref.back()) + np);
+    }
+    SHCHK(c, hipMemcpyAsync(c->ppref.as<u64>() + r0, c->h_ppref.data() + base, (size_t)k * 8, hipMemcpyHostToDevice,
+                            c->stream));
+  }
   for (int l = 0; l < c->nlocal; l++) {
     wro[l][k] = wnew[l].size();
     const size_t dst = ((size_t)l * c->max_rounds + r0) * n * SP;

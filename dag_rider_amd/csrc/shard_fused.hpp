@@ -1,0 +1,658 @@
+// shard_fused.hpp -- kernels of the column-sharded memoized replay
+// (dr_shard_replay, include/dagrider_shard.h) that read every
+// column a context holds in one workgroup.
+//
+//   k_ms_pass        one workgroup per wave (rounds 4w-3 .. 4w): streams every
+//                    local shard's columns of the wave's strong rows once and
+//                    builds, from that one read, U_r (per shard), WU_r (from the
+//                    weak-column keys), the speculative canonical digest of each
+//                    round, and waveReady's vote (process.go:326-339).  When the
+//                    context holds every column (local mode, a one-rank group:
+//                    "fused") the vote is complete: S_1..S_3, vcount, commit.
+//                    Otherwise (one rank of G > 1) the pass writes this shard's
+//                    partial S_1 for the exchange; steps 2 and 3 follow the
+//                    exchanges (shard.hip k_shard_vote).
+//   k_ms_kcand_full  K^cand_r, good_r and the full-round defaults of RD, CE.
+//   k_ms_canon_full  one workgroup walks the canonical segments below the bad
+//                    rounds (k_canon's walk, kernels.hpp) over the shard arrays,
+//                    then the canonical positions C (the presence prefix below
+//                    the lowest walked round) and the lowest round whose
+//                    speculative digest is stale.
+//   k_ms_rg_full     per-round canonical digests (speculative below that round).
+//   k_ms_plan        waveReady's chain tasks from the device commit flags
+//                    (persistent decidedWave: the previous commit; literal: 0).
+//   k_ms_sweep_full  one workgroup per query (orderVertices cone / leader chain),
+//                    round by round to its end: no exchange is needed when the
+//                    workgroup sees every column, so a query never waits for the
+//                    others (the stepped form, shard_memo.hpp k_ms_step, moves one
+//                    round per launch with an exchange between launches).
+//
+// Semantics are dr_replay's (engine.hip): the same commits, pushes, per-pop
+// counts, digests and edge totals, bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "shard_memo.hpp"
+#include "wave_ops.hpp"
+
+namespace drs {
+
+enum : int { VOTE_FULL = 1, VOTE_STEP1 = 2 };
+
+// extra inputs/outputs of the fused replay (every pointer device memory)
+struct FArgs {
+  const u64 *ppref;    // [R] |P_1| + .. + |P_r| (present vertices, round 0 excluded)
+  u64 *SG;             // [T+1] speculative canonical digest (every round 1..r full)
+  u64 *RD, *CE, *RG;   // [T+1] canonical count, edges, digest of each round
+  u64 *Cc, *Ec, *Gc;   // [T+1] their prefixes
+  uint8_t *good;       // [T+8] K^cand_r covers P_r
+  int32_t *hdr;        // FH_* slots
+  uint8_t *commit;     // [nw]
+  int32_t *vcount;     // [nw]
+  MState *fin;         // [nq] final state of every query
+  int32_t quorum, nw, npop, persistent;
+};
+enum : int { FH_NCHAIN = 0, FH_NSEG = 1, FH_RLO = 2, FH_PUSHES = 3, FH_ERR = 4, FH_N = 8 };
+
+// exclusive scan of v over one workgroup of NT threads (every thread calls it);
+// s: NT/64 slots of LDS; op: 0 sum, 1 max
+template <int NT>
+__device__ __forceinline__ int64_t fblock_scan(int64_t v, int64_t *s, int64_t &total, int op) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t x = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = (int64_t)__shfl_up((long long)x, off);
+    if (lane >= off) x = op ? max(x, y) : x + y;
+  }
+  if (lane == 63) s[wid] = x;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+  for (int w = 0; w < NW; w++) {
+    const int64_t t = s[w];
+    if (w < wid) base = op ? max(base, t) : base + t;
+    tot = op ? max(tot, t) : tot + t;
+  }
+  __syncthreads();
+  total = tot;
+  const int64_t ex = (int64_t)__shfl_up((long long)x, 1);
+  const int64_t lex = lane == 0 ? 0 : ex;
+  return op ? max(base, lex) : base + lex;
+}
+
+// ---------------------------------------------------------------------------
+// k_ms_pass (see the file comment).  Dynamic LDS: sU[NL*SP] | Sp[NL*SP] |
+// Tn[W] | sWU[NL*dd*SP].  Thread t owns chunk column (t mod CPR) of every
+// shard-round (NT is a multiple of CPR), so its OR accumulator holds fixed
+// columns; the rows of the local shards are streamed as one sequence of
+// (shard, pass) elements, GRP 16-B loads in flight.
+// ---------------------------------------------------------------------------
+template <int NT, int GRP>
+__global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int vote_mode, u64 *__restrict__ U,
+                                                u64 *__restrict__ WU, u64 *__restrict__ S1out) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  const int NL = a.nlocal, SP = a.SP, W = a.W, WSs = a.WSs, n = a.n, dd = a.dd, T = a.T;
+  u64 *sU = lds, *Sp = lds + NL * SP, *Tn = Sp + NL * SP, *sWU = Tn + W;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int w = blockIdx.x + 1, r1 = 4 * (w - 1) + 1;
+  const int nr = min(T, r1 + 3) - r1 + 1;
+  const bool do_commit = w <= nwc;
+  const int L = do_commit ? (w < a.nlead ? (int)a.lead[w] : 1) - 1 : 0;
+  const bool leader = do_commit && ((a.pres[(size_t)r1 * W + (L >> 6)] >> (L & 63)) & 1ULL);
+  const int CW = SP >= 2 ? 2 : 1, CPR = SP / CW, CPS = n * CPR, JP = (CPS + NT - 1) / NT, J = NL * JP;
+  const int col = (tid % CPR) * CW;
+  for (int i = tid; i < NL * SP; i += NT) {
+    sU[i] = 0;
+    const int l = i / SP, c = i % SP, gw = (a.shard0 + l) * WSs + c;
+    Sp[i] = (c < WSs && gw == (L >> 6)) ? 1ULL << (L & 63) : 0ULL;
+  }
+  for (int i = tid; i < W; i += NT) Tn[i] = 0;
+  for (int i = tid; i < NL * dd * SP; i += NT) sWU[i] = 0;
+  // speculative canonical digest of round r1 + wid: every present vertex of the
+  // round delivered in slot order at positions from ppref[r-1]
+  if (wid < nr) {
+    constexpr int SPT = 8;
+    const int r = r1 + wid;
+    const uint32_t sa = a.slot_off[r], sb = a.slot_off[r + 1];
+    u64 pos = f.ppref[r - 1], dg = 0;
+    for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPT) {
+      const uint32_t i0 = c0 + (uint32_t)lane * SPT;
+      uint32_t src[SPT];
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int j = 0; j < SPT; j++) {
+        src[j] = i0 + j < sb ? a.slot_src[i0 + j] : 0u;
+        cnt += src[j] != 0;
+      }
+      uint32_t inc = cnt;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+      }
+      u64 k = pos + (inc - cnt);
+#pragma unroll
+      for (int j = 0; j < SPT; j++)
+        if (src[j]) dg += dr::digest_term((uint32_t)r, src[j], k++);
+      pos += __shfl(inc, 63);
+    }
+    dg = dr::wave_sum(dg);
+    if (lane == 0) f.SG[r] = dg;
+  }
+  __syncthreads();
+  for (int k = 0; k < nr; k++) {
+    const int r = r1 + k;
+    const bool test = leader && k >= 1 && (vote_mode == VOTE_FULL || k == 1);
+    // the round's weak targets per shard and delta (every key has a source)
+    for (int l = 0; l < NL; l++) {
+      const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
+      for (uint64_t j = c0 + tid; j < c1; j += NT) {
+        const uint32_t key = a.wck[j];
+        const int d = (int)(key >> 11) - 2, tc = (int)(key & 2047u);
+        atomicOr(&sWU[((size_t)l * dd + d) * SP + (tc >> 6)], 1ULL << (tc & 63));
+      }
+    }
+    u64 a0 = 0, a1 = 0;
+    for (int j0 = 0; j0 < J; j0 += GRP) {
+      u64 x0[GRP], x1[GRP];
+#pragma unroll
+      for (int p = 0; p < GRP; p++) {
+        const int j = j0 + p, l = j / JP, i = j - l * JP, c = tid + i * NT;
+        x0[p] = 0;
+        x1[p] = 0;
+        if (j < J && c < CPS) {
+          const u64 *base = a.strong + (size_t)l * a.strong_stride + (size_t)r * n * SP + (size_t)c * CW;
+          if (CW == 2) {
+            const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(base));
+            x0[p] = v.x;
+            x1[p] = v.y;
+          } else {
+            x0[p] = __builtin_nontemporal_load(base);
+          }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < GRP; p++) {
+        const int j = j0 + p;
+        if (j >= J) break;  // uniform
+        const int l = j / JP, i = j - l * JP;
+        a0 |= x0[p];
+        a1 |= x1[p];
+        if (test) {  // rows of round r reaching S_{k-1} on this shard's columns
+          const u64 s0 = Sp[l * SP + col], s1 = CW == 2 ? Sp[l * SP + col + 1] : 0ULL;
+          const bool hit = ((x0[p] & s0) | (x1[p] & s1)) != 0ULL;
+          u64 m = __ballot(hit);
+          const int cb = wid * 64 + i * NT;  // the wave's first chunk
+          if (lane == 0 && m && cb < CPS) {
+            const int rowbase = cb / CPR;
+            u64 bits = m;
+            if (CPR > 1) {
+              for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
+              bits = 0;
+              for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
+            }
+            atomicOr(&Tn[rowbase >> 6], bits << (rowbase & 63));
+          }
+        }
+        if (i == JP - 1) {  // the shard's columns of round r are done: U
+          for (int off = CPR; off < 64; off <<= 1) {
+            a0 |= shfl_xor64(a0, off);
+            if (CW == 2) a1 |= shfl_xor64(a1, off);
+          }
+          if (lane < CPR) {
+            if (a0) atomicOr(&sU[l * SP + lane * CW], a0);
+            if (CW == 2 && a1) atomicOr(&sU[l * SP + lane * CW + 1], a1);
+          }
+          a0 = a1 = 0;
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < NL * SP; i += NT) {
+      const int l = i / SP, c = i % SP;
+      U[((size_t)l * a.R + r) * SP + c] = sU[i];
+      sU[i] = 0;
+    }
+    for (int i = tid; i < NL * dd * SP; i += NT) {
+      const int l = i / (dd * SP), rest = i - l * dd * SP;
+      WU[((size_t)l * a.R + r) * dd * SP + rest] = sWU[i];
+      sWU[i] = 0;
+    }
+    if (test) {  // S_k: the sources of round r that reach S_{k-1} (this context's shards' columns of it)
+      for (int i = tid; i < W; i += NT) {
+        const u64 v = Tn[i];
+        Tn[i] = 0;
+        const int l = i / WSs - a.shard0, c = i % WSs;
+        if (l >= 0 && l < NL) Sp[l * SP + c] = v;
+        if (vote_mode == VOTE_STEP1 && k == 1 && S1out) S1out[(size_t)(w - 1) * W + i] = v;
+      }
+    }
+    __syncthreads();
+  }
+  if (do_commit && vote_mode == VOTE_STEP1 && !leader && S1out)
+    for (int i = tid; i < W; i += NT) S1out[(size_t)(w - 1) * W + i] = 0;
+  if (do_commit && vote_mode == VOTE_FULL && tid == 0) {
+    if (!leader) {  // leader is bottom (process.go:327-329)
+      f.commit[w - 1] = 0;
+      f.vcount[w - 1] = -1;
+    } else {
+      int vc = 0;
+      for (int i = 0; i < NL * SP; i++) vc += __popcll(Sp[i]);
+      f.vcount[w - 1] = vc;
+      f.commit[w - 1] = vc >= f.quorum ? 1 : 0;
+    }
+  }
+}
+
+// K^cand over the full width (every local shard's U / WU), good_r, and the
+// full-round defaults RD_r = |K^cand_r & P_r|, CE_r = the round's degree sum.
+// One wave per round, lane w < W owns word w (shard w / WSs, column w mod WSs).
+__global__ __launch_bounds__(256) void k_ms_kcand_full(MArgs a, FArgs f) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63, T = a.T;
+  if (r > T) return;
+  bool bad = false;
+  int cnt = 0;
+  if (w < a.W) {
+    const int l = w / a.WSs, cw = w - l * a.WSs;
+    const u64 p = a.pres[(size_t)r * a.W + w];
+    u64 v;
+    if (r == T) {
+      v = p;
+    } else {
+      const size_t ub = (size_t)l * a.R;
+      v = a.U[(ub + r + 1) * a.SP + cw];
+      for (int d = 0; d < a.dd && r + d + 2 <= T; d++) v |= a.WU[((ub + r + d + 2) * a.dd + d) * a.SP + cw];
+    }
+    a.K[(size_t)r * a.W + w] = v;
+    bad = (v & p) != p;
+    cnt = __popcll(v & p);
+  }
+  const bool ok = __ballot(bad) == 0ULL;
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if (w == 0) {
+    f.good[r] = ok;
+    f.RD[r] = r == 0 ? 0 : (u64)cnt;
+    f.CE[r] = r == 0 ? 0 : a.rdeg[r];
+  }
+}
+
+// Full-width expansion of a partial round r of a query held by one workgroup:
+// the frontier FE's strong rows (every local shard's columns) -> ring slot of
+// r-1, and (weak) its weak columns -> the ring slots of their target rounds
+// (>= bottom).  Saturation per shard as in k_ms_step: once the OR of the rows a
+// wave has read equals the shard's U_r, no further row adds a bit.  Every
+// thread calls it; ring / FE are LDS (W words per round slot).
+template <int NT>
+__device__ __forceinline__ void expand_partial_full(const MArgs &a, int r, int bottom, const u64 *FE, u64 *ring,
+                                                    int dm, bool weak) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int SP = a.SP, W = a.W, WSs = a.WSs;
+  u64 *dst = ring + (size_t)((r - 1) & dm) * W;
+  for (int l = 0; l < a.nlocal; l++) {
+    const u64 *rows = a.strong + (size_t)l * a.strong_stride + (size_t)r * a.n * SP;
+    const u64 ur = lane < SP ? a.U[((size_t)l * a.R + r) * SP + lane] : 0ULL;
+    u64 acc = 0;
+    for (int w = wv; w < W; w += NW) {
+      const u64 bits = FE[w];
+      if (!bits) continue;
+      const u64 *blk = rows + (size_t)w * 64 * SP;
+      for (int i = 0; i < SP; i++) {
+        const int k = lane + 64 * i;
+        if ((bits >> (k / SP)) & 1ULL) acc |= blk[k];
+      }
+      u64 red = acc;
+      for (int off = SP; off < 64; off <<= 1) red |= shfl_xor64(red, off);
+      if (__ballot(lane < SP && red != ur) == 0ULL) break;
+    }
+    for (int off = SP; off < 64; off <<= 1) acc |= shfl_xor64(acc, off);
+    if (lane < SP && lane < WSs && acc) atomicOr(&dst[l * WSs + lane], acc);
+  }
+  if (!weak) return;
+  for (int l = 0; l < a.nlocal; l++) {
+    const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
+    for (uint64_t jj = c0 + tid; jj < c1; jj += NT) {
+      const u64 *row = a.wcr + jj * W;
+      u64 hit = 0;
+      for (int w = 0; w < W; w++) hit |= row[w] & FE[w];
+      if (!hit) continue;
+      const uint32_t key = a.wck[jj];
+      const int tr = r - (int)(key >> 11), cg = (a.shard0 + l) * WSs * 64 + (int)(key & 2047u);
+      if (tr < bottom) continue;
+      atomicOr(&ring[(size_t)(tr & dm) * W + (cg >> 6)], 1ULL << (cg & 63));
+    }
+  }
+}
+
+// full round r: ring[r-1] |= U_r, (weak) ring[r-d-2] |= WU_r[d] (>= bottom); lane w < W
+__device__ __forceinline__ void expand_full_round(const MArgs &a, int r, int bottom, u64 *ring, int dm, bool weak,
+                                                  int w) {
+  const int l = w / a.WSs, cw = w - l * a.WSs, W = a.W;
+  const size_t ub = (size_t)l * a.R + r;
+  ring[(size_t)((r - 1) & dm) * W + w] |= a.U[ub * a.SP + cw];
+  if (weak)
+    for (int d = 0; d < a.dd; d++) {
+      const int tr = r - d - 2;
+      if (tr < bottom) break;
+      ring[(size_t)(tr & dm) * W + w] |= a.WU[(ub * a.dd + d) * a.SP + cw];
+    }
+}
+
+// sum over the vertices of FE (LDS, W words) of sdeg (+ wdeg): every thread calls
+// it, thread t takes sources t, t + NT, ...; returns the block total in *out (LDS)
+template <int NT>
+__device__ __forceinline__ void fe_degrees(const MArgs &a, int r, const u64 *FE, bool with_weak, u64 *out) {
+  u64 e = 0;
+  for (int s = threadIdx.x; s < a.n; s += NT)
+    if ((FE[s >> 6] >> (s & 63)) & 1ULL) {
+      const size_t at = (size_t)r * a.n + s;
+      e += a.sdeg[at] + (with_weak ? a.wdeg[at] : 0);
+    }
+  e = dr::wave_sum(e);
+  if ((threadIdx.x & 63) == 0 && e) atomicAdd(out, e);
+}
+
+// ---------------------------------------------------------------------------
+// k_ms_canon_full: one workgroup, the canonical segments top down (k_canon).
+// Dynamic LDS: ring[depth*W] | FE[W].
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_canon_full(MArgs a, FArgs f) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  const int W = a.W, dm = a.depth - 1, T = a.T;
+  u64 *ring = lds, *FE = lds + (size_t)a.depth * W;
+  __shared__ int s_ctl[4];
+  __shared__ u64 s_e;
+  __shared__ int64_t s_scan[NT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int pos = T, segs = 0, lo_w = T + 1;
+  while (true) {
+    if (wv == 0) {
+      const int b = next_bad(a, pos);
+      if (lane == 0) s_ctl[0] = b;
+    }
+    __syncthreads();
+    const int b = s_ctl[0];
+    __syncthreads();
+    if (b < 0) break;
+    segs++;
+    for (int i = tid; i < a.depth * W; i += NT) ring[i] = 0;
+    __syncthreads();
+    if (tid < W) {  // F_b = K^cand_b; pending below b from the full rounds above it
+      ring[(size_t)(b & dm) * W + tid] = a.K[(size_t)b * W + tid];
+      const int l = tid / a.WSs, cw = tid - l * a.WSs;
+      for (int x = b - 1; x >= 0 && x >= b - a.dd; x--) {
+        u64 v = 0;
+        for (int y = max(b + 1, x + 2); y <= T && y <= x + a.dd + 1; y++)
+          v |= a.WU[(((size_t)l * a.R + y) * a.dd + (y - x - 2)) * a.SP + cw];
+        ring[(size_t)(x & dm) * W + tid] |= v;
+      }
+    }
+    __syncthreads();
+    int run = 0, r = b;
+    for (;; --r) {
+      if (wv == 0) {
+        const bool act = lane < W;
+        u64 fw = 0, p = 0;
+        if (act) {
+          u64 *slot = &ring[(size_t)(r & dm) * W + lane];
+          fw = *slot;
+          *slot = 0;
+          p = a.pres[(size_t)r * W + lane];
+          a.K[(size_t)r * W + lane] = fw;
+          FE[lane] = fw & p;
+        }
+        const bool full = __ballot(act && (fw & p) != p) == 0ULL;
+        int cnt = __popcll(fw & p);
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        run = full ? run + 1 : 0;
+        if (lane == 0) {
+          s_ctl[1] = full;
+          s_ctl[2] = run >= a.dmax || r == 0;
+          f.RD[r] = r == 0 ? 0 : (u64)cnt;
+          s_e = 0;
+        }
+      }
+      __syncthreads();
+      if (s_ctl[2]) break;  // regime restored at r (CE_r keeps the full-round total)
+      if (s_ctl[1]) {
+        if (tid < W) expand_full_round(a, r, 0, ring, dm, true, tid);
+      } else {
+        expand_partial_full<NT>(a, r, 0, FE, ring, dm, true);
+        fe_degrees<NT>(a, r, FE, true, &s_e);
+      }
+      __syncthreads();
+      if (tid == 0 && !s_ctl[1]) f.CE[r] = s_e;
+      __syncthreads();
+    }
+    pos = r;
+    lo_w = min(lo_w, r);
+  }
+  // canonical positions: below the lowest walked round every round is full (C
+  // is the presence prefix); the scan covers the walked region only
+  const int B = lo_w;
+  for (int x = tid; x < B && x <= T; x += NT) f.Cc[x] = f.ppref[x];
+  const int span = T + 1 - B, per = span > 0 ? (span + NT - 1) / NT : 0;
+  const int ra = B + tid * per, rb = min(T + 1, ra + per);
+  int64_t loc = 0;
+  for (int x = ra; x < rb; x++) loc += (int64_t)f.RD[x];
+  int64_t tot;
+  u64 run = (B >= 1 ? f.ppref[B - 1] : 0ULL) + (u64)fblock_scan<NT>(loc, s_scan, tot, 0);
+  int bad = INT_MAX;
+  for (int x = ra; x < rb; x++) {
+    run += f.RD[x];
+    f.Cc[x] = run;
+    if (bad == INT_MAX && x >= 1 && run != f.ppref[x]) bad = x;
+  }
+  if (tid == 0) s_ctl[3] = INT_MAX;
+  __syncthreads();
+  if (bad != INT_MAX) atomicMin(&s_ctl[3], bad);
+  __syncthreads();
+  if (tid == 0) {
+    f.hdr[FH_NSEG] = segs;
+    f.hdr[FH_RLO] = s_ctl[3];
+  }
+}
+
+// canonical digest of round r >= 1 (one wave per round): the speculative one
+// below the first round whose position prefix differs from the presence prefix
+__global__ __launch_bounds__(256) void k_ms_rg_full(MArgs a, FArgs f) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r > a.T) return;
+  if (r == 0) {
+    if (lane == 0) f.RG[0] = 0;
+    return;
+  }
+  if (r < f.hdr[FH_RLO]) {
+    if (lane == 0) f.RG[r] = f.SG[r];
+    return;
+  }
+  const u64 mw = lane < a.W ? a.K[(size_t)r * a.W + lane] & a.pres[(size_t)r * a.W + lane] : 0ULL;
+  u64 dg = 0, ed = 0;
+  ms_wave_emit(a.slot_off, a.slot_src, r, mw, f.Cc[r - 1], a.W, nullptr, nullptr, a.n, dg, ed);
+  dg = dr::wave_sum(dg);
+  if (lane == 0) f.RG[r] = dg;
+}
+
+// ---------------------------------------------------------------------------
+// k_ms_plan: waveReady's chain tasks (process.go:341-350) from the device commit
+// flags, one workgroup.  Committed wave w's floor is the previous committed wave
+// (persistent decidedWave) or 0 (Q1 literal); it has a chain query when
+// w - 1 >= floor + 1.  Chain i takes query slot npop + i, its pushes from the
+// exclusive prefix of the chains' push bounds (w - floor each).  Every chain
+// slot's stepped state (st0) is initialised, unused slots as done.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__restrict__ q, MState *__restrict__ st0,
+                                                int push_cap) {
+  __shared__ int64_t s_scan[NT / 64];
+  const int nw = f.nw, tid = threadIdx.x;
+  const int per = (nw + NT - 1) / NT, wa = 1 + tid * per, wb = min(nw + 1, wa + per);
+  // floors: exclusive prefix max of (commit ? w : 0)
+  int64_t m = 0;
+  for (int w = wa; w < wb; w++)
+    if (f.commit[w - 1]) m = w;
+  int64_t tot;
+  int64_t prev = fblock_scan<NT>(m, s_scan, tot, 1);
+  int64_t cnt = 0, pushes = 0;
+  {
+    int64_t pv = prev;
+    for (int w = wa; w < wb; w++)
+      if (f.commit[w - 1]) {
+        const int fl = f.persistent ? (int)pv : 0;
+        if (w - 1 >= fl + 1) {
+          cnt++;
+          pushes += w - fl;
+        }
+        pv = w;
+      }
+  }
+  int64_t ctot, ptot;
+  int64_t ci = fblock_scan<NT>(cnt, s_scan, ctot, 0);
+  int64_t pb = fblock_scan<NT>(pushes, s_scan, ptot, 0);
+  {
+    int64_t pv = prev;
+    for (int w = wa; w < wb; w++)
+      if (f.commit[w - 1]) {
+        const int fl = f.persistent ? (int)pv : 0;
+        if (w - 1 >= fl + 1) {
+          MQuery x{};
+          x.type = MQ_CHAIN;
+          x.top = 4 * (w - 1) + 1;
+          x.bottom = 4 * fl + 1;
+          x.src0 = (w < a.nlead ? (int)a.lead[w] : 1) - 1;
+          x.push_base = (int32_t)pb;
+          const int qi = f.npop + (int)ci;
+          q[qi] = x;
+          if (st0) {
+            MState s{};
+            s.low = x.top;
+            s.cur = x.top;
+            st0[qi] = s;
+          }
+          ci++;
+          pb += w - fl;
+        }
+        pv = w;
+      }
+  }
+  if (st0)
+    for (int i = (int)ctot + tid; i < nw; i += NT) {
+      MState s{};
+      s.done = 1;
+      st0[f.npop + i] = s;
+    }
+  if (tid == 0) {
+    f.hdr[FH_NCHAIN] = (int32_t)ctot;
+    f.hdr[FH_PUSHES] = (int32_t)min<int64_t>(ptot, INT32_MAX);
+    if (ptot > push_cap) f.hdr[FH_ERR] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_ms_sweep_full: one workgroup per query, every round to its end (the same
+// decisions as k_ms_step, shard_memo.hpp).  Grid npop + nw: workgroups past the
+// planned chains exit.  Dynamic LDS: ring[depth*W] | FE[W].
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  const int qi = blockIdx.x;
+  if (qi >= f.npop + f.hdr[FH_NCHAIN]) return;
+  const int W = a.W, dm = a.depth - 1;
+  u64 *ring = lds, *FE = lds + (size_t)a.depth * W;
+  __shared__ int s_ctl[2];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const MQuery Q = a.q[qi];
+  const bool pop = Q.type == MQ_POP, weak = pop;
+  for (int i = tid; i < a.depth * W; i += NT) ring[i] = 0;
+  __syncthreads();
+  if (tid == 0 && Q.src0 >= 0) ring[(size_t)(Q.top & dm) * W + (Q.src0 >> 6)] = 1ULL << (Q.src0 & 63);
+  __syncthreads();
+  int run = 0, low = Q.top, npush = 0;
+  u64 edges = 0;
+  int r = Q.top;
+  bool merged = false;
+  for (;; --r) {
+    if (wv == 0) {
+      const bool act = lane < W;
+      u64 fw = 0, p = 0;
+      if (act) {
+        u64 *slot = &ring[(size_t)(r & dm) * W + lane];
+        fw = *slot;
+        *slot = 0;
+        p = a.pres[(size_t)r * W + lane];
+      }
+      // waveReady's chain (process.go:342-350): a reachable, present leader of
+      // wave wvv is pushed and the chain goes on from it alone
+      bool restart = false;
+      int wvv = 0;
+      if (!pop && r < Q.top && ((r - 1) & 3) == 0) {
+        wvv = ((r - 1) >> 2) + 1;
+        const int L = (wvv < a.nlead ? (int)a.lead[wvv] : 1) - 1;
+        const u64 fl = __shfl(fw & p, L >> 6);
+        if ((fl >> (L & 63)) & 1ULL) {
+          fw = lane == (L >> 6) ? 1ULL << (L & 63) : 0ULL;
+          restart = true;
+        }
+      }
+      const u64 fe = fw & p;
+      const bool nz = __ballot(act && fw != 0ULL) != 0ULL;
+      const bool full = __ballot(act && fe != p) == 0ULL;
+      if (nz) low = min(low, r - 1);
+      bool done;
+      if (pop) {
+        const u64 k = act ? a.K[(size_t)r * W + lane] : 0ULL;
+        run = __ballot(act && fw != k) == 0ULL ? run + 1 : 0;
+        merged = run >= a.dmax;
+        done = merged || r <= Q.bottom || (!nz && low >= r);
+        if (act) a.masks[Q.mask_off + (int64_t)(Q.top - r) * W + lane] = fw;
+      } else {
+        done = r <= Q.bottom || (!nz && low >= r);
+      }
+      const bool summary = !done && full;
+      if (!pop && !done) {
+        if (summary) {
+          edges += a.sdr[r];
+        } else {
+          u64 e = 0;
+          for (u64 x = act ? fe : 0ULL; x; x &= x - 1) e += a.sdeg[(size_t)r * a.n + lane * 64 + __builtin_ctzll(x)];
+          edges += dr::wave_sum(e);
+        }
+      }
+      if (!done && pop && __ballot(act && fe != 0ULL) != 0ULL) low = min(low, r - a.dmax);
+      if (restart) {
+        if (lane == 0) a.push_out[Q.push_base + npush] = wvv;
+        npush++;
+      }
+      if (act) FE[lane] = fe;
+      if (lane == 0) {
+        s_ctl[0] = done;
+        s_ctl[1] = summary;
+      }
+    }
+    __syncthreads();
+    if (s_ctl[0]) break;
+    if (s_ctl[1]) {
+      if (tid < W) expand_full_round(a, r, Q.bottom, ring, dm, weak, tid);
+    } else {
+      expand_partial_full<NT>(a, r, Q.bottom, FE, ring, dm, weak);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    MState o{};
+    o.done = 1;
+    o.run = run;
+    o.low = low;
+    o.stop = r;
+    o.merged = pop && merged;
+    o.npush = npush;
+    o.edges = edges;
+    o.cur = r;
+    f.fin[qi] = o;
+  }
+}
+
+}  // namespace drs

@@ -84,6 +84,8 @@ struct MArgs {
   u64 *masks;               // MQ_POP frontier rows
   int32_t *push_out;
   const uint8_t *good;       // [T+1] K^cand_r covers P_r (MQ_CANON: where segments start)
+  const uint32_t *slot_off;  // [R+1] slot order (insertion order of every round)
+  const uint16_t *slot_src;  // 1-based source per slot (0 = ghost)
   int32_t n, W, WSs, SP, G, shard0, nlocal, local, nq, depth, dd, dmax, summary, R, nlead, T;
 };
 
@@ -548,7 +550,7 @@ __global__ __launch_bounds__(MS_NT) void k_ms_rg(MArgs a, int T, const uint32_t 
   if (lane == 0) RG[r] = dg;
 }
 
-// REF emission, one workgroup per pop query (qidx): the canonical prefix at the
+// REF emission, one workgroup per pop query (qidx; null: query b): the canonical prefix at the
 // cut (C, G, E) plus the query's own rounds cut+1 .. top from its mask rows, 64
 // rounds at a time (counts, exclusive scan, digests and degrees).
 __global__ __launch_bounds__(MS_NT) void k_ms_emit(MArgs a, const int32_t *__restrict__ qidx, const MState *__restrict__ st,
@@ -560,7 +562,7 @@ __global__ __launch_bounds__(MS_NT) void k_ms_emit(MArgs a, const int32_t *__res
   __shared__ uint32_t sCnt[64];
   __shared__ u64 sPos[64];
   __shared__ u64 sTot, sDg, sEd;
-  const int b = blockIdx.x, qi = qidx[b], tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x, qi = qidx ? qidx[b] : b, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const MQuery Q = a.q[qi];
   const MState S = st[qi];
   const int top = Q.top;

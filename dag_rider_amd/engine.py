@@ -94,6 +94,10 @@ class Engine:
         """DR_OPT_DEVICE_PLAN: plan dr_replay's phases on the device (identical results either way)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_DEVICE_PLAN, int(on)))
 
+    def set_commit_split(self, on: bool):
+        """DR_OPT_COMMIT_SPLIT: several workgroups per wave for short wave ranges (identical results)."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_COMMIT_SPLIT, int(on)))
+
     def set_batch_form(self, form: int):
         """DR_OPT_BATCH_FORM (read from a batch's first engine): DR_BATCH_AUTO, DR_BATCH_WORKGROUP
         (four wavefronts per DAG) or DR_BATCH_WAVE (one wavefront per DAG); identical results."""
@@ -379,6 +383,12 @@ class ReplayBatch:
     def __call__(self) -> List[ReplayResult]:
         self.run()
         return self.results()
+
+    def host_phases(self) -> dict:
+        """dr_last_batch_phases of the last run: host prep, launch -> host, copy back, unpack (ms)."""
+        ms = (C.c_float * 4)()
+        L.lib().dr_last_batch_phases(self.engines[0]._h, ms)
+        return dict(host_prep=ms[0], launch_to_host=ms[1], copy_back=ms[2], unpack=ms[3])
 
 
 def replay_batch(engines: Sequence["Engine"], nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT,

@@ -146,6 +146,11 @@ class ShardEngine:
         """DR_SHARD_OPT_MEMO: memoized REF replay (summaries, canonical cone, relative-round steps)."""
         self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_MEMO, int(on)))
 
+    def set_stepped(self, on: bool):
+        """DR_SHARD_OPT_STEPPED: the memo replay's stepped form (one round per launch, columns
+        exchanged between launches) even when this context holds every column."""
+        self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_STEPPED, int(on)))
+
     def set_leader_coin(self, mode: int = L.DR_LEADER_CONST1, seed: int = 0,
                         table: Optional[Sequence[int]] = None):
         """chooseLeader (process.go:386-392), as Engine.set_leader_coin."""

@@ -32,7 +32,10 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 1
+/* 2: dr_last_kernel_ms and dr_last_batch_phases added, dr_profile_kernel moved to the
+ * profiling build (dagrider_tuning.h), repeated ids accepted by every append (Q6),
+ * dr_replay_batch's ms_* fields keep their device meaning */
+#define DR_ABI_VERSION 2
 
 enum {
   DR_OK = 0,
@@ -44,7 +47,7 @@ enum {
   DR_E_STATE = -6     /* call order violated (e.g. append not contiguous) */
 };
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
-enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3, DR_OPT_BATCH_FORM = 4 };
+enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3, DR_OPT_BATCH_FORM = 4, DR_OPT_COMMIT_SPLIT = 5 };
 enum { DR_BATCH_AUTO = 0, DR_BATCH_WORKGROUP = 1, DR_BATCH_WAVE = 2 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
 enum { DR_WEAK_LITERAL = 0, DR_WEAK_PAPER = 1 };
@@ -95,6 +98,10 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * one workgroup of four wavefronts per DAG (shortest time per DAG),
  * DR_BATCH_WAVE = one wavefront per DAG (most DAGs per CU); AUTO takes the
  * wave form when the batch holds more than 6 DAGs per CU of the device.
+ * DR_OPT_COMMIT_SPLIT (default 1): dr_wave_commit / dr_wave_ready on a wave
+ * range too short to fill the device split each wave's vote over several
+ * co-resident workgroups that meet at a barrier after S_1 and S_2; 0 = one
+ * workgroup per wave (identical results).
  * Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 
@@ -261,9 +268,12 @@ int dr_replay(dr_ctx *ctx, int nwaves, int chain_mode, int deliver_mode, dr_repl
  * Contexts must be distinct and on one device; errors name the context.
  * Outputs, semantics and capacities are exactly dr_replay's.  When every
  * context has n <= 128, nwaves <= 64, weak deltas < 32 and no ids are
- * requested, the whole batch runs as one fused kernel (one wavefront per DAG,
- * dag_rider_amd/csrc/batch.hpp; outs[i].ms_deliver = its device time);
- * otherwise the contexts replay one after another through dr_replay. */
+ * requested, the whole batch runs as one fused kernel in one of two forms
+ * (DR_OPT_BATCH_FORM): a workgroup of four wavefronts per DAG
+ * (dag_rider_amd/csrc/batch.hpp) when each CU holds few DAGs, a wavefront per
+ * DAG (batch1w.hpp) when it holds many; outs[i].ms_deliver = the launch's device
+ * time, the other ms_* fields 0.  Otherwise the contexts replay one after
+ * another through dr_replay. */
 int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
                     dr_replay_out *outs);
 
@@ -271,6 +281,12 @@ int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, i
  * dr_wave_commit / dr_wave_ready / dr_replay on this context (observability,
  * like dr_shard_stats; no reference counterpart). */
 int dr_last_kernel_ms(const dr_ctx *ctx, float *ms);
+
+/* Host-side phases (ms, steady clock) of the last fused dr_replay_batch whose
+ * first context is ctx: ms4[0] preparation before the launch (checks, job
+ * table), [1] launch until the results are on the host, [2] the copy back
+ * (device events), [3] unpacking into the callers' outputs (observability). */
+int dr_last_batch_phases(const dr_ctx *ctx, float *ms4);
 
 #ifdef __cplusplus
 }

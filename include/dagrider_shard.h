@@ -84,6 +84,13 @@ int dr_shard_path_batch(dr_shard *ctx, int q, const int32_t *from, const int32_t
  * pop whose cone holds it.  0 = the batched full sweeps.  Results are
  * identical. */
 #define DR_SHARD_OPT_MEMO 2
+/* DR_SHARD_OPT_STEPPED (default 0): when the context holds every column (local
+ * mode, a one-rank group) the memoized replay runs "fused": each kernel reads all
+ * columns, so every query runs to its end in one launch and nothing is
+ * exchanged.  1 runs the stepped form instead -- one round of every live query
+ * per launch with the columns exchanged between launches, what each rank of a
+ * group of G > 1 runs -- so one device can check it.  Results are identical. */
+#define DR_SHARD_OPT_STEPPED 3
 int dr_shard_set_option(dr_shard *ctx, int option, int value);
 
 /* chooseLeader (process.go:386-392): dr_set_leader_coin's modes and semantics. */

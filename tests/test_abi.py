@@ -45,7 +45,7 @@ def test_tuning_hook_only_in_profiling_build():
 
 def test_library_loads_and_binds():
     L = _lib.lib()
-    assert L.dr_abi_version() == 1
+    assert L.dr_abi_version() == 2
 
 
 def test_no_cpu_fallback():

@@ -164,7 +164,8 @@ def test_batch_plan_reuse(gpu_device, form):
     """A repeated batch (same contexts, modes and output buffers) reuses its plan: the
     checks, job table and output layout of the last call (engine.hip, BatchPlan). Any
     ABI call that can change a context in between -- appends, the leader coin, an
-    output capacity, create/destroy -- rebuilds it."""
+    option (the batch form), create/destroy -- and a changed output capacity or chain
+    mode rebuild it."""
     nw = 8
     rng = np.random.default_rng(31)
     items = []
@@ -193,6 +194,35 @@ def test_batch_plan_reuse(gpu_device, form):
         _same(got[i], e.replay(nw, cm, dm))
     engines[2].set_leader_coin()
     for w, g in zip(want, b()):
+        _same(g, w)
+    # a smaller output capacity in between (same buffers): rebuilt, and it must not fit
+    np_max = max(len(w.push_wave) for w in want)
+    i_max = max(range(len(want)), key=lambda i: len(want[i].push_wave))
+    cap0 = b._outs[i_max].push_cap
+    b._outs[i_max].push_cap = np_max - 1
+    with pytest.raises(L.DrError) as ei:
+        b.run()
+    assert ei.value.code == L.DR_E_CAPACITY
+    b._outs[i_max].push_cap = cap0
+    for w, g in zip(want, b()):
+        _same(g, w)
+    # the other batch form on the first context (an option: rebuilt)
+    engines[0].set_batch_form(L.DR_BATCH_WAVE if form != L.DR_BATCH_WAVE else L.DR_BATCH_WORKGROUP)
+    for _ in range(2):
+        for w, g in zip(want, b()):
+            _same(g, w)
+    engines[0].set_batch_form(form)
+    # the other chain mode on the same output buffers: the mode is part of the plan's key
+    bl = ReplayBatch(engines, nw, L.DR_CHAIN_LITERAL, dm)  # literal chains need the larger capacity
+    want_lit = [oracle.PDag(d).replay(f, nw, L.DR_CHAIN_LITERAL, dm) for d, f, _ in items]
+    for w, g in zip(want_lit, bl()):
+        _same(g, w)
+    bl.chain_mode = cm
+    for _ in range(2):
+        for w, g in zip(want, bl()):
+            _same(g, w)
+    bl.chain_mode = L.DR_CHAIN_LITERAL
+    for w, g in zip(want_lit, bl()):
         _same(g, w)
     for e in engines:
         e.close()

@@ -99,6 +99,22 @@ def test_bench_gpus_colshard_failure_is_labelled():
     assert out["value"] == 3000 / 0.5
 
 
+def test_bench_gpus_colshard_wrong_result_not_published():
+    """Rank 0's check of the sharded replay against the unsharded engine fails: the sharded
+    number is not the line's value; the line carries the replicas number and says why."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-selftest",
+                        "--selftest-wrong"], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
+    assert out["config"]["parallelism"] == "replicas2" and out["scaling"] == "weak"
+    assert out["detail"]["colshard_errors"][0] == "verify_vs_unsharded failed"
+    assert out["value"] == 3000 / 0.5
+
+
 def test_bench_world_mismatch_refused():
     """Under torchrun a WORLD_SIZE that disagrees with --gpus exits non-zero, prints nothing."""
     import subprocess

@@ -120,6 +120,11 @@ def test_shard_rccl_single_rank(gpu_device):
         assert st["exchange_bytes"] > 0
         # the whole replay through the all-gathers (memo path: K^cand and every step)
         f, nw = 66, R // 4
+        for cm, dm in MODES:  # one rank holds every column: the fused replay, nothing to exchange
+            got = se.replay(nw, cm, dm)
+            _same_replay(got, bs.replay(f, nw, cm, dm))
+            assert got.sweep["canon_segments"] >= 0
+        se.set_stepped(True)  # the stepped replay through the all-gathers (votes, K^cand, every step)
         for cm, dm in MODES:
             got = se.replay(nw, cm, dm)
             _same_replay(got, bs.replay(f, nw, cm, dm))
@@ -174,9 +179,11 @@ def test_shard_replay_random_dags(gpu_device, seed):
     for G in ((1, 2) if seed % 2 else (3, 8)):
         with ShardEngine(n, f, R + 1, gpu_device, nshards=G) as se:
             se.append_packed(d)
-            for memo, persistent in ((True, True), (False, True), (False, False)):
+            for memo, persistent, stepped in ((True, True, False), (True, True, True), (False, True, False),
+                                              (False, False, False)):
                 se.set_memo(memo)
                 se.set_persistent(persistent)
+                se.set_stepped(stepped)
                 for cm, dm in MODES:
                     want = bs.replay(f, nw, cm, dm)
                     assert want.rc == 0
@@ -185,10 +192,10 @@ def test_shard_replay_random_dags(gpu_device, seed):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_shard_memo_replay_generated(gpu_device, seed):
-    """The memoized sharded replay (summaries per shard, canonical cone, pops and chains
-    stepped by relative round) == the unsharded engine and the bitset oracle on
-    quorum-shaped DAGs with late vertices, weak edges up to 12 deep and absent leaders,
-    at G = 1, 2, 3, 8, both chain modes, REF and PAPER delivery."""
+    """The memoized sharded replay (summaries per shard, canonical cone, pops and chains;
+    fused, and stepped by relative round) == the bitset oracle on quorum-shaped DAGs with
+    late vertices, weak edges up to 12 deep and absent leaders, at G = 1, 2, 3, 8, both
+    chain modes, REF and PAPER delivery."""
     from dag_rider_amd.gen import small_config
 
     rng = np.random.default_rng(4400 + seed)
@@ -202,10 +209,12 @@ def test_shard_memo_replay_generated(gpu_device, seed):
     for G in (1, 2, 3, 8):
         with ShardEngine(n, cfg.faulty, d.nrounds, gpu_device, nshards=G) as se:
             se.append_packed(d)
-            for cm, dm in MODES:
-                got = se.replay(nw, cm, dm)
-                _same_replay(got, bs.replay(cfg.faulty, nw, cm, dm))
-                assert got.sweep["canon_segments"] >= 0  # the memo path ran
+            for stepped in (False, True):
+                se.set_stepped(stepped)
+                for cm, dm in MODES:
+                    got = se.replay(nw, cm, dm)
+                    _same_replay(got, bs.replay(cfg.faulty, nw, cm, dm))
+                    assert got.sweep["canon_segments"] >= 0  # the memo path ran
 
 
 def test_shard_commit_chain_order_calls(gpu_device):
@@ -241,8 +250,10 @@ def test_shard_replay_leader_coin(gpu_device):
     with ShardEngine(n, 13, R + 1, gpu_device, nshards=2) as se:
         se.append_packed(d)
         se.set_leader_coin(L.DR_LEADER_TABLE, table=leaders)
-        for cm, dm in MODES:
-            _same_replay(se.replay(R // 4, cm, dm), bs.replay(13, R // 4, cm, dm))
+        for stepped in (False, True):
+            se.set_stepped(stepped)
+            for cm, dm in MODES:
+                _same_replay(se.replay(R // 4, cm, dm), bs.replay(13, R // 4, cm, dm))
 
 
 def test_shard_replay_c4_full(gpu_device):
@@ -259,6 +270,10 @@ def test_shard_replay_c4_full(gpu_device):
             _check_golden(got, g["persistent_ref"])
             assert got.sweep["canon_segments"] >= 0 and se.stats()["rounds"] < 100  # memo: a few dozen steps
             _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_PAPER), g["persistent_paper"])
+            if G in (2, 8):  # the stepped form (what each rank of a G-rank group runs)
+                se.set_stepped(True)
+                _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
+                se.set_stepped(False)
             if G in (1, 8):  # the batched full sweeps (DR_SHARD_OPT_MEMO 0), REF
                 se.set_memo(False)
                 _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])

@@ -60,3 +60,33 @@ def test_split_random_with_coin(gpu_device, seed):
     for world in (2, 3, 5):
         cm, vc, _ = split_commit(d, f, nw, world, gpu_device, leaders)
         assert (cm == full[0]).all() and (vc == full[1]).all(), (seed, world)
+
+
+@pytest.mark.parametrize("n", [64, 128, 300, 700, 1024, 2048])
+def test_commit_split_kernel(gpu_device, n):
+    """dr_wave_commit on short wave ranges runs each wave's vote on several workgroups
+    (k_commit_split, DR_OPT_COMMIT_SPLIT): the same commits and vCounts as one workgroup
+    per wave (k_commit) and as the whole-DAG commit rule, for every range length, with
+    quorum-shaped DAGs (late vertices, absent leaders) and a seeded leader coin."""
+    from dag_rider_amd.gen import small_config
+
+    cfg = small_config(n, 120, 900 + n, p_present=0.95, p_late=0.1, p_w=0.3, weak_depth=4, p_la=0.1)
+    d = generate(cfg)
+    nw = cfg.nwaves
+    for coin in (False, True):
+        with Engine(n, cfg.faulty, d.nrounds, gpu_device) as e:
+            e.append_packed(d)
+            if coin:
+                e.set_leader_coin(L.DR_LEADER_SEEDED, 5 + n)
+            e.set_commit_split(False)
+            want_c, want_v = e.wave_commit(1, nw)
+            want1 = [e.wave_commit(w, w) for w in range(1, nw + 1)]
+            e.set_commit_split(True)
+            for w0, w1 in ((1, nw), (1, 1), (3, 9), (nw - 4, nw), (2, nw - 1)):
+                for _ in range(2):  # the kernel leaves its barrier counters ready for the next launch
+                    cm, vc = e.wave_commit(w0, w1)
+                    assert (cm == want_c[w0 - 1:w1]).all() and (vc == want_v[w0 - 1:w1]).all(), (w0, w1)
+            for w in range(1, nw + 1):
+                cm, vc = e.wave_commit(w, w)
+                assert cm[0] == want1[w - 1][0][0] and vc[0] == want1[w - 1][1][0], w
+                assert e.wave_ready(w, max(0, w - 3))[:2] == (bool(cm[0]), int(vc[0]))

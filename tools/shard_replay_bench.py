@@ -22,17 +22,19 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c4")
-    ap.add_argument("--runs", type=int, default=5)
+    ap.add_argument("--runs", type=int, default=20)
     ap.add_argument("--shards", default="1,2,4,8")
+    ap.add_argument("--stepped", default="0,1", help="replay forms: 0 fused, 1 stepped (DR_SHARD_OPT_STEPPED)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     d = generate(cfg, nthreads=16)
     with Engine(cfg.n, cfg.faulty, d.nrounds, 0) as e:
         e.append_packed(d)
         rref = e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
-    for G in [int(x) for x in args.shards.split(",")]:
+    for G, stepped in [(int(g), int(s)) for g in args.shards.split(",") for s in args.stepped.split(",")]:
         with ShardEngine(cfg.n, cfg.faulty, d.nrounds, 0, nshards=G) as se:
             se.append_packed(d)
+            se.set_stepped(bool(stepped))
             r = se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)  # warm-up
             walls = []
             for _ in range(args.runs):
@@ -46,7 +48,7 @@ def main():
                       and (r.pop_edges == rref.pop_edges).all()
                       and (r.commit_edges, r.chain_edges, r.deliver_edges)
                       == (rref.commit_edges, rref.chain_edges, rref.deliver_edges))
-            print(json.dumps(dict(config=cfg.name, G=G, memo=True, replay_ok=ok, ms_wall_median=statistics.median(walls),
+            print(json.dumps(dict(config=cfg.name, G=G, memo=True, form="stepped" if stepped else "fused", replay_ok=ok, ms_wall_median=statistics.median(walls),
                                   ms_wall_min=min(walls), runs=walls, phases_ms=r.ms, steps=st["rounds"],
                                   canon_segments=r.sweep["canon_segments"], cones=r.sweep["count"],
                                   edges=r.total_edges)), flush=True)
