@@ -829,7 +829,10 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4-deep", "c4-deep64", "c5", "c4-loop"])
+    ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4-deep", "c4-deep64", "c4-dups", "c5",
+                                                       "c4-loop"])
+    ap.add_argument("--no-memo", action="store_true",
+                    help="DR_OPT_MEMO 0: every cone swept whole (the general full-cone sweep line)")
     ap.add_argument("--deliver", default="ref", choices=["ref", "paper"])
     ap.add_argument("--cpu-budget", type=float, default=40.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -905,6 +908,8 @@ def main() -> int:
     d = generate(cfg, nthreads=CPU_THREADS)
     log(f"[rank {rank}] generated {cfg} in {time.perf_counter() - t0:.1f} s")
     eng = Engine(cfg.n, cfg.faulty, d.nrounds, local)
+    if args.no_memo:
+        eng.set_memo(False)
     t0 = time.perf_counter()
     eng.append_packed(d)
     log(f"[rank {rank}] loaded DAG into HBM in {time.perf_counter() - t0:.1f} s")
@@ -1003,7 +1008,8 @@ def main() -> int:
         "data": f"synthetic (seeded generator, SURVEY.md s8(d) {cfg.name.upper()} parameters)",
         "config": {"workload": f"{cfg.name.upper()} full replay: n={cfg.n} x {cfg.last_round} rounds, {cfg.nwaves} "
                                f"waves, waveReady (persistent decidedWave) + orderVertices ({args.deliver}"
-                               f"{', full cones' if args.deliver == 'ref' else ', dedup'}) per commit",
+                               f"{', full cones' if args.deliver == 'ref' else ', dedup'}) per commit"
+                               + (" -- memo off (DR_OPT_MEMO 0): every cone swept whole" if args.no_memo else ""),
                    "n": cfg.n, "rounds": cfg.last_round, "waves": cfg.nwaves,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -42,6 +42,11 @@ thread_local std::string g_create_err;
 std::atomic<uint64_t> g_ctx_gen{1};
 uint64_t next_gen() { return g_ctx_gen.fetch_add(1, std::memory_order_relaxed) + 1; }
 
+// The memo's weak-delta window: WU holds dmax - 1 unions per
+// round and a merge needs dmax equal rounds, so a deeper window costs every pop
+// sweep more rounds; beyond it the full sweeps run.
+constexpr int kMemoMaxDelta = 255;
+
 int next_pow2(int x) {
   int p = 1;
   while (p < x) p <<= 1;
@@ -203,13 +208,15 @@ struct dr_ctx {
     *out = batch_pin;
     return hipSuccess;
   }
-  // memo needs every weak edge in the dense summary window
-  // memo (round summaries + canonical cone): weak deltas up to 65 (WU holds dd = 64
-  // slots per round; the merge window is dmax rounds), no far edges
-  bool memo_ok() const { return nfar == 0 && dmax_near <= 65; }
-  // round summaries and the canonical cone count vertices per id: a mirror with
-  // repeated ids (dups) takes the full sweeps, which count every slot
-  bool memo_on() const { return use_memo && memo_ok() && ndups == 0; }
+  // memo (round summaries + canonical cone): every weak edge in the dense summary
+  // window -- deltas up to kMemoMaxDelta (WU holds dd = dmax - 1 slots per round, the
+  // merge window is dmax rounds) that the sweeps' LDS ring holds -- and no far edges
+  bool memo_ok() const {
+    return nfar == 0 && dmax_near <= kMemoMaxDelta && (1 << depth_log2()) > dmax_near;
+  }
+  // repeated ids: the summaries' counts and the emission count every slot of a
+  // reached id (REF), PAPER delivers an id at its first slot (slot_rep)
+  bool memo_on() const { return use_memo && memo_ok(); }
   int memo_dd() const { return std::max(0, dmax_near - 1); }
   // scratch
   DevBuf q_buf, masks, dlv, push_out, push_n, edges, wedges, hits, commit, vcount, popdesc, rbase, counts,
@@ -753,13 +760,19 @@ hipError_t weak_union_lds(const dr_ctx *c, size_t lds) {
   static std::atomic<int> seen[kLdsDevs] = {};
   return lds_limit((const void *)dr::k_weak_union<WS>, seen, c->dev, lds);
 }
+// rounds (waves) per k_weak_union workgroup: four, fewer when a deep window's
+// per-wave LDS slice (dd x WS words) would take the workgroup past 64 KiB
+inline int weak_union_waves(int dd, int WS) {
+  const size_t per = (size_t)std::max(dd, 1) * WS * 8;
+  return (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / per));
+}
 template <int WS>
 hipError_t launch_weak_union_t(dr_ctx *c, int T, hipStream_t st) {
-  const int dd = c->memo_dd();
-  const size_t lds = (size_t)4 * std::max(dd, 1) * WS * 8;
+  const int dd = c->memo_dd(), nwv = weak_union_waves(dd, WS);
+  const size_t lds = (size_t)nwv * std::max(dd, 1) * WS * 8;
   hipError_t e = weak_union_lds<WS>(c, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_weak_union<WS>), dim3((T + 3) / 4), dim3(256), lds, st, c->view(), T, 0, dd,
+  hipLaunchKernelGGL((dr::k_weak_union<WS>), dim3((T + nwv - 1) / nwv), dim3(64 * nwv), lds, st, c->view(), T, 0, dd,
                      c->WU.as<u64>(), (const int32_t *)nullptr, c->ppref.as<u64>(), c->slot_off.as<uint32_t>(),
                      c->slot_src.as<uint16_t>(), c->RG.as<u64>());
   return hipGetLastError();
@@ -785,10 +798,11 @@ hipError_t launch_round_summary_t(dr_ctx *c, const int32_t *rounds, int nr) {
                      c->U.as<u64>(), c->SD.as<u64>());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || mv.dd == 0) return e;
-  const size_t lds = (size_t)4 * mv.dd * WS * 8;
+  const int nwv = weak_union_waves(mv.dd, WS);
+  const size_t lds = (size_t)nwv * mv.dd * WS * 8;
   e = weak_union_lds<WS>(c, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_weak_union<WS>), dim3((nr + 3) / 4), dim3(256), lds, c->stream, c->view(),
+  hipLaunchKernelGGL((dr::k_weak_union<WS>), dim3((nr + nwv - 1) / nwv), dim3(64 * nwv), lds, c->stream, c->view(),
                      c->nrounds - 1, nr, mv.dd, c->WU.as<u64>(), rounds, (const u64 *)nullptr,
                      (const uint32_t *)nullptr, (const uint16_t *)nullptr, (u64 *)nullptr);
   return hipGetLastError();

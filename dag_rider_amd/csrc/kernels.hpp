@@ -786,12 +786,13 @@ struct EmitArgs {
 // DEG: also add the strong + weak degrees of the delivered vertices to *edges
 // (this lane's share; sdeg/wdeg indexed [round][source-1], row length n).
 // wave_emit_slots: the same with the round's slot range [sa, sb) already loaded.
+// first_only (PAPER, slot_rep non-null): a repeated id's later slots deliver nothing.
 template <int WS, int SPL = 8, bool DEG = false>
 __device__ __forceinline__ u64 wave_emit_slots(const uint16_t *__restrict__ slot_src, int y, uint32_t sa,
                                                uint32_t sb, u64 mw, u64 pos,
                                                const uint16_t *__restrict__ sdeg = nullptr,
                                                const uint16_t *__restrict__ wdeg = nullptr, int n = 0,
-                                               u64 *edges = nullptr) {
+                                               u64 *edges = nullptr, const uint8_t *__restrict__ first_only = nullptr) {
   const int lane = threadIdx.x & 63;
   u64 dg = 0;
   for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPL) {
@@ -799,6 +800,10 @@ __device__ __forceinline__ u64 wave_emit_slots(const uint16_t *__restrict__ slot
     int src[SPL];
 #pragma unroll
     for (int j = 0; j < SPL; j++) src[j] = i0 + j < sb ? (int)slot_src[i0 + j] : 0;
+    if (first_only)
+#pragma unroll
+      for (int j = 0; j < SPL; j++)
+        if (i0 + j < sb && first_only[i0 + j]) src[j] = 0;
     uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < SPL; j++) {
@@ -834,8 +839,9 @@ __device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot
                                                const uint16_t *__restrict__ slot_src, int y, u64 mw, u64 pos,
                                                const uint16_t *__restrict__ sdeg = nullptr,
                                                const uint16_t *__restrict__ wdeg = nullptr, int n = 0,
-                                               u64 *edges = nullptr) {
-  return wave_emit_slots<WS, SPL, DEG>(slot_src, y, slot_off[y], slot_off[y + 1], mw, pos, sdeg, wdeg, n, edges);
+                                               u64 *edges = nullptr, const uint8_t *__restrict__ first_only = nullptr) {
+  return wave_emit_slots<WS, SPL, DEG>(slot_src, y, slot_off[y], slot_off[y + 1], mw, pos, sdeg, wdeg, n, edges,
+                                       first_only);
 }
 
 
@@ -1041,6 +1047,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
             int pc = act ? popc64(f & p) : 0;
 #pragma unroll
             for (int off = 1; off < WS; off <<= 1) pc += __shfl_xor(pc, off);
+            pc += dup_count<WS>(g, r, act ? f & p : 0ULL);  // REF: every slot of a reached id
             if (tid == 0) rcnt[q.mask_off / WS + (r - q.bottom)] = (uint32_t)pc;
           }
           if (stats_out && tid == 0 && !stop) {
@@ -1321,16 +1328,20 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
       if (gi % NGR == NGR - 1) round_end(gi / NGR);
     }
   }
-  if (do_commit && tid == 0) {
-    if (!leader) {  // leader is bottom (process.go:327-329)
-      commit[w - 1] = 0;
-      vcount[w - 1] = -1;
-    } else {
-      int vc = 0;
+  if (do_commit && wid == 0) {
+    // vCount counts slots (process.go:330-335): repeated ids once per slot
+    const int dc = leader ? dup_count<WS>(g, r1 + 3, lane < WS ? S[lane] : 0ULL) : 0;
+    if (tid == 0) {
+      if (!leader) {  // leader is bottom (process.go:327-329)
+        commit[w - 1] = 0;
+        vcount[w - 1] = -1;
+      } else {
+        int vc = dc;
 #pragma unroll
-      for (int i = 0; i < WS; i++) vc += popc64(S[i]);
-      vcount[w - 1] = vc;
-      commit[w - 1] = vc >= quorum ? 1 : 0;
+        for (int i = 0; i < WS; i++) vc += popc64(S[i]);
+        vcount[w - 1] = vc;
+        commit[w - 1] = vc >= quorum ? 1 : 0;
+      }
     }
   }
 }
@@ -1449,7 +1460,7 @@ __global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, in
                                                     const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG) {
   extern __shared__ __attribute__((aligned(16))) u64 wu_lds[];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + wid;
+  const int i = blockIdx.x * (int)(blockDim.x >> 6) + wid;  // one wave per round
   int r;
   if (rounds) {
     if (i >= nr) return;
@@ -1527,6 +1538,12 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
   const bool ok = __ballot(bad) == 0ULL;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  // REF delivers every slot of a reached id (process.go:418-429): repeated ones count too
+  if (g.dup_off && r >= 1) {
+    u64 kp = 0;
+    if (w < WS) kp = K[(size_t)r * WS + w] & g.present[(size_t)r * WS + w];
+    cnt += dup_count<WS>(g, r, kp);
+  }
   if (w == 0) {
     good[r] = ok;
     CE[r] = r == 0 ? 0 : mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
@@ -1608,10 +1625,16 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     RoundWords cur{}, nxt{};
     if (tid < WS) {
       ring[(size_t)(b & dmask) * WS + tid] = K[(size_t)b * WS + tid];
-      for (int x = b - 1; x >= 0 && x >= b - mv.dd; x--)
-        for (int y = max(b + 1, x + 2); y <= T && y <= x + mv.dd + 1; y++)
-          ring[(size_t)(x & dmask) * WS + tid] |= mv.WU[((size_t)y * mv.dd + (y - x - 2)) * WS + tid];
       load_round<WS, false, true, true>(g, mv, b, cur);
+    }
+    // (round x, word w) pairs over every thread: a deep window has dd^2/2 terms per word
+    for (int it = tid; it < mv.dd * WS; it += NT) {
+      const int x = b - 1 - it / WS, w = it % WS;
+      if (x < 0) continue;
+      u64 v = 0;
+      for (int y = max(b + 1, x + 2); y <= T && y <= x + mv.dd + 1; y++)
+        v |= mv.WU[((size_t)y * mv.dd + (y - x - 2)) * WS + w];
+      ring[(size_t)(x & dmask) * WS + w] = v;
     }
     __syncthreads();
     int run = 0;
@@ -1635,6 +1658,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
         full = __all(full);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if (g.dup_off && r >= 1) cnt += dup_count<WS>(g, r, tid < WS ? FE[tid] : 0ULL);  // every slot (REF)
         run = full ? run + 1 : 0;
         if (tid == 0) {
           s_ctl[1] = full;

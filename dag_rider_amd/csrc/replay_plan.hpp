@@ -631,8 +631,8 @@ __global__ __launch_bounds__(NT) void k_paper_emit(DagView g, const u64 *__restr
       pos += i < wid ? c : 0ULL;
       tot += c;
     }
-    if (on && cnt)
-      dg += wave_emit_round<WS, 8, true>(slot_off, slot_src, r, mw, pos, g.sdeg, g.wdeg, g.n, &ed);
+    if (on && cnt)  // PAPER delivers an id once, at its first slot
+      dg += wave_emit_round<WS, 8, true>(slot_off, slot_src, r, mw, pos, g.sdeg, g.wdeg, g.n, &ed, g.slot_rep);
     run += tot;
     __syncthreads();
   }
@@ -692,7 +692,8 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
       sb = slot_off[r + 1];
       if (lane < WS) mw = masks[moff + (int64_t)r * WS + lane] & g.present[(size_t)r * WS + lane];
     }
-    const u64 cnt = wave_sum((u64)popc64(mw));
+    // REF delivers every slot of a reached id (process.go:418-429): repeated ones count too
+    const u64 cnt = wave_sum((u64)popc64(mw)) + (on && g.dup_off ? (u64)dup_count<WS>(g, r, mw) : 0ULL);
     if (lane == 0) s_c[wid] = cnt;
     __syncthreads();
     u64 pos = run, tot = 0;

@@ -113,7 +113,9 @@ class PackedDag:
 
 
 def pack_lists(dag: Sequence[Sequence[Vertex]], n: int) -> PackedDag:
-    """Pack a contract [][]vertex (ghost slots allowed) into a PackedDag."""
+    """Pack a contract [][]vertex (ghost slots allowed) into a PackedDag.  An id that
+    repeats in its round keeps every slot; its row and weak edges are its LAST slot's,
+    the vertex path()'s lookup sees (process.go:112-116)."""
     W = (n + 63) // 64
     R = len(dag)
     slot_off = [0]
@@ -121,12 +123,17 @@ def pack_lists(dag: Sequence[Sequence[Vertex]], n: int) -> PackedDag:
     strong = np.zeros(R * n * W, dtype=np.uint64)
     weak_lists: List[List[int]] = [[] for _ in range(R * n)]
     for r, rnd in enumerate(dag):
+        seen = set()
         for v in rnd:
             s = v.id.source
             if v.id == VertexID(0, 0):
                 slot_src.append(0)
                 continue
             slot_src.append(s)
+            if s in seen:  # a later slot of the id replaces its edges
+                strong[(r * n + s - 1) * W:(r * n + s) * W] = 0
+                weak_lists[r * n + s - 1] = []
+            seen.add(s)
             for e in v.strong_edges:
                 o = (r * n + s - 1) * W + (e.source - 1) // 64
                 strong[o] |= np.uint64(1 << ((e.source - 1) % 64))

@@ -26,6 +26,10 @@ class GenConfig:
     p_w: float
     weak_depth: int
     p_la: float = 0.0
+    # repeated ids: every id of a round >= 1 gets one more slot
+    # w.p. p_dup, at a random position of its round (uponDeliver / the buffer loop
+    # appending a vertex already in the round, process.go:158-169, :229)
+    p_dup: float = 0.0
 
     @property
     def faulty(self) -> int:
@@ -47,6 +51,8 @@ CONFIGS = {
     "c4-deep": GenConfig("c4-deep", 1024, 4000, 4, 1.0, 0.02, 0.03, 80, 0.0),
     # C4 with weak edges up to 64 rounds deep, the memo window's far end (--config c4-deep64)
     "c4-deep64": GenConfig("c4-deep64", 1024, 4000, 4, 1.0, 0.02, 0.04, 64, 0.0),
+    # C4 with repeated ids: ~1 % of each round's ids delivered twice (--config c4-dups)
+    "c4-dups": GenConfig("c4-dups", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0, 0.01),
     # C5: one of the 4096 independent n=128 replays (seed 5000+i)
     "c5": GenConfig("c5", 128, 128, 5000, 0.9, 0.1, 0.5, 4, 0.05),
 }
@@ -73,14 +79,36 @@ def generate(cfg: GenConfig, nthreads: int = 0) -> PackedDag:
             buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(addr)
             return np.frombuffer(buf, dtype=dtype, count=count).copy()
 
-        return PackedDag(n, nr,
-                         view(lib.dr_gen_slot_off, np.uint32, nr + 1),
-                         view(lib.dr_gen_slot_src, np.uint16, ns),
-                         view(lib.dr_gen_strong, np.uint64, nr * n * W),
-                         view(lib.dr_gen_weak_off, np.uint32, nr * n + 1),
-                         view(lib.dr_gen_weak_tgt, np.uint32, nw))
+        d = PackedDag(n, nr,
+                      view(lib.dr_gen_slot_off, np.uint32, nr + 1),
+                      view(lib.dr_gen_slot_src, np.uint16, ns),
+                      view(lib.dr_gen_strong, np.uint64, nr * n * W),
+                      view(lib.dr_gen_weak_off, np.uint32, nr * n + 1),
+                      view(lib.dr_gen_weak_tgt, np.uint32, nw))
     finally:
         lib.dr_gen_free(h)
+    return with_repeated_slots(d, cfg.p_dup, cfg.seed) if cfg.p_dup > 0 else d
+
+
+def with_repeated_slots(d: PackedDag, p_dup: float, seed: int) -> PackedDag:
+    """Every id of a round >= 1 gets one more slot w.p. p_dup, at a random position of
+    its round.  The packed row is per id (its last slot's, path()'s lookup,
+    process.go:112-116), so only the slot lists change; vCount and REF delivery count
+    the extra slots, PAPER delivers an id at its first."""
+    rng = np.random.default_rng(np.random.SeedSequence([seed, 0x5107]))
+    off = d.slot_off.astype(np.int64)
+    parts, new_off = [], [0]
+    for r in range(d.nrounds):
+        s = d.slot_src[off[r]:off[r + 1]]
+        if r >= 1:
+            ids = s[s != 0]
+            pick = ids[rng.random(len(ids)) < p_dup]
+            if len(pick):
+                s = np.insert(s, np.sort(rng.integers(0, len(s) + 1, size=len(pick))), pick)
+        parts.append(s)
+        new_off.append(new_off[-1] + len(s))
+    return PackedDag(d.n, d.nrounds, np.asarray(new_off, np.uint32), np.concatenate(parts).astype(np.uint16),
+                     d.strong, d.weak_off, d.weak_tgt)
 
 
 def c5_config(i: int) -> GenConfig:

@@ -2,8 +2,11 @@
  * ref_bitset.c -- packed-bitset CPU restatement of the same hot path.
  *
  * TEST INFRASTRUCTURE ONLY (see oracle.h).  Same outputs as ref_literal.c on
- * contract DAGs (strong edges target round r-1, weak edges rounds < r-1,
- * no duplicate ids in a round >= 1), computed by round sweeps:
+ * contract DAGs (strong edges target round r-1, weak edges rounds < r-1),
+ * computed by round sweeps.  An id may repeat in a round (process.go:158-169,
+ * :229): the packed row is its last slot's (path()'s lookup, :112-116), vCount
+ * and REF delivery count every slot (:332, :418-429), PAPER delivers an id at
+ * its first slot, edge totals count an id's edges once.
  *   path(from,to)   process.go:89-148  -> forward sweep from `from`, bit test
  *   waveReady       process.go:314-354 -> backward strong sweep from the
  *                   leader over rounds 4w-2..4w; chain = one forward strong
@@ -116,21 +119,29 @@ static int commit_one(const or_pdag *p, int faulty, int w, uint8_t *commit, int3
   uint64_t S[64], T[64]; /* W <= 32 */
   memset(S, 0, sizeof S);
   S[L >> 6] = 1ULL << (L & 63);
+  uint64_t seen[64];
   for (int r = r1 + 1; r <= r1 + 3; r++) {
     memset(T, 0, sizeof T);
+    memset(seen, 0, sizeof seen);
     for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++) {
       int src = p->slot_src[i];
       if (src == 0) continue;
+      const uint64_t bit = 1ULL << ((src - 1) & 63);
+      if (seen[(src - 1) >> 6] & bit) continue; /* a repeated id: one row, its edges once */
+      seen[(src - 1) >> 6] |= bit;
       const uint64_t *row = row_of(p, r, src - 1);
       int hit = 0;
       for (int k = 0; k < W; k++) { hit |= (row[k] & S[k]) != 0; *edges += (uint64_t)popc(row[k]); }
-      if (hit) T[(src - 1) >> 6] |= 1ULL << ((src - 1) & 63);
+      if (hit) T[(src - 1) >> 6] |= bit;
     }
     memcpy(S, T, sizeof S);
   }
   (void)n;
-  int vc = 0;
-  for (int k = 0; k < W; k++) vc += popc(S[k]);
+  int vc = 0; /* every slot of round 4w whose id reaches the leader (process.go:331-336) */
+  for (uint32_t i = p->slot_off[r1 + 3]; i < p->slot_off[r1 + 4]; i++) {
+    int src = p->slot_src[i];
+    if (src != 0 && ((S[(src - 1) >> 6] >> ((src - 1) & 63)) & 1)) vc++;
+  }
   *vcount = vc;
   *commit = vc >= 2 * faulty + 1;
   return 0;
@@ -196,18 +207,28 @@ static int chain_one(const or_pdag *p, int w, int floor_w, int32_t *out, uint64_
 
 typedef struct { int leader_wave, cur_round, pop_index; } pop_t;
 
+/* first_only (PAPER): a repeated id is delivered at its first slot only; REF
+ * delivers every slot of a reached id */
 static void emit_pop(const or_pdag *p, const uint64_t *masks, int bottom, int top, int cur_round,
-                     uint64_t *count, uint64_t *digest, or_vid *ids, int64_t ids_cap, int64_t *ids_n) {
+                     uint64_t *count, uint64_t *digest, or_vid *ids, int64_t ids_cap, int64_t *ids_n,
+                     int first_only) {
   const int W = p->W;
   uint64_t k = 0, dg = 0;
+  uint64_t seen[64];
   int last = cur_round < top ? cur_round : top;
   for (int r = 1; r <= last; r++) {
     if (r < bottom) continue;
     const uint64_t *F = masks + (size_t)(r - bottom) * W;
+    if (first_only) memset(seen, 0, sizeof seen);
     for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++) {
       int s = p->slot_src[i];
       if (s == 0) continue; /* ghost {0,0}: never reachable (no edge targets source 0) */
       if (!((F[(s - 1) >> 6] >> ((s - 1) & 63)) & 1)) continue;
+      if (first_only) {
+        const uint64_t bit = 1ULL << ((s - 1) & 63);
+        if (seen[(s - 1) >> 6] & bit) continue;
+        seen[(s - 1) >> 6] |= bit;
+      }
       dg += or_digest_term(r, s, k);
       if (ids) {
         if (*ids_n < ids_cap) { ids[*ids_n].round = r; ids[*ids_n].source = s; }
@@ -292,7 +313,7 @@ int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode, int d
       uint64_t *m = (uint64_t *)calloc((size_t)(top + 1) * W, sizeof(uint64_t));
       or_vid from = {top, or_leader(p->leader, p->nleader, lw)};
       or_bs_cone(p, from, 0, 0, m, &we[lw]);
-      emit_pop(p, m, 0, top, top, &wc[lw], &wd[lw], NULL, 0, NULL);
+      emit_pop(p, m, 0, top, top, &wc[lw], &wd[lw], NULL, 0, NULL, 0);
       free(m);
     }
     for (int64_t j = 0; j < npop; j++) {
@@ -317,7 +338,7 @@ int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode, int d
       m[(size_t)top * W + (L >> 6)] |= 1ULL << (L & 63);
       uint64_t e = sweep(p, top, 0, 0, m, D);
       emit_pop(p, m, 0, top, pops[j].cur_round, &o->pop_count[j], &o->pop_digest[j], o->ids,
-               o->ids_cap, &o->n_ids);
+               o->ids_cap, &o->n_ids, deliver_mode == OR_DELIVER_PAPER);
       if (D) { /* delivered := delivered U (new cone restricted to present, rounds 1..cur) */
         int lastr = pops[j].cur_round < top ? pops[j].cur_round : top;
         for (int r = 1; r <= lastr; r++)
@@ -366,7 +387,7 @@ int or_bs_order_vertices(const or_pdag *p, const or_vid *stack, int stack_len, i
     if (v.source >= 1 && v.source <= p->n)
       m[(size_t)top * W + ((v.source - 1) >> 6)] |= 1ULL << ((v.source - 1) & 63);
     sweep(p, top, 0, 0, m, D);
-    emit_pop(p, m, 0, top, cur_round, &pop_count[j], &pop_digest[j], out, out_cap, out_n);
+    emit_pop(p, m, 0, top, cur_round, &pop_count[j], &pop_digest[j], out, out_cap, out_n, mode == OR_DELIVER_PAPER);
     if (D) {
       int lastr = cur_round < top ? cur_round : top;
       for (int r = 1; r <= lastr; r++)

@@ -5,7 +5,9 @@ the buffer loop hands it one (process/process.go:158-169, :229).  path() then fo
 the id's LAST slot (:112-116), waveReady's vCount counts every slot of round 4w (:332),
 orderVertices delivers every slot in REF (the no-op filter, :418-429) and an id once
 in PAPER.  The mirror accepts such DAGs through every append path and replays them on
-the full sweeps; checked here against the literal restatement (oracle/ref_literal.c),
+the memo path (round summaries, canonical cone and emission count every slot of a
+reached id; PAPER skips an id's later slots) and on the full sweeps; checked here
+against the literal restatement (oracle/ref_literal.c),
 which follows process.go line by line, on list-form DAGs whose repeated slots carry
 their own edges."""
 import numpy as np
@@ -49,13 +51,19 @@ def test_repeated_ids_replay_path_order(gpu_device, seed):
         cut = int(rng.integers(1, R + 1))
         e.append_lists(dag, 0, cut)
         e.append_lists(dag, cut, R + 1)
-        for memo in (True, False):  # the memo option is moot: repeated ids take the full sweeps
+        for memo in (True, False):
             e.set_memo(memo)
-            for cm, dm in MODES:
-                want = ld.replay(f, nw, cm, dm, ids_cap=1 << 16)
-                assert want.rc == 0
-                _same(e.replay(nw, cm, dm, ids_cap=1 << 16), want)
-                _same(e.replay(nw, cm, dm), want, ids=False)
+            for plan in ((True, False) if memo else (True,)):
+                e.set_device_plan(plan)
+                for cm, dm in MODES:
+                    want = ld.replay(f, nw, cm, dm, ids_cap=1 << 16)
+                    assert want.rc == 0
+                    _same(e.replay(nw, cm, dm, ids_cap=1 << 16), want)
+                    got = e.replay(nw, cm, dm)
+                    _same(got, want, ids=False)
+                    assert (got.sweep["canon_segments"] >= 0) == memo  # the memo path ran
+        e.set_memo(True)
+        e.set_device_plan(True)
         # waveReady / orderVertices per call, path over a sample of pairs
         for w in range(1, nw + 1):
             rc, vc, st = ld.wave_ready(f, w, max(0, w - 2))
@@ -126,3 +134,35 @@ def test_repeated_ids_in_a_batch(gpu_device):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_repeated_slots_generated_memo(gpu_device, seed):
+    """Quorum-shaped DAGs (the C4 generator's spec) with repeated slots (gen.with_repeated_slots)
+    on the memo path -- round summaries, canonical cone, device-planned and host-planned
+    emission -- == the bitset oracle (oracle/ref_bitset.c, repeated ids: one row per id,
+    vCount / REF count every slot, PAPER the first) in every mode; the memo path ran."""
+    from dag_rider_amd.gen import generate, small_config
+
+    rng = np.random.default_rng(9100 + seed)
+    n = int(rng.choice([64, 130, 256, 1024]))
+    cfg = small_config(n, int(rng.integers(40, 90)), 70 + seed, p_present=0.97, p_late=0.05, p_w=0.4,
+                       weak_depth=int(rng.integers(2, 9)), p_la=0.1, p_dup=float(rng.uniform(0.02, 0.2)))
+    d = generate(cfg)
+    off = d.slot_off
+    reps = sum(int((x := d.slot_src[off[r]:off[r + 1]])[x != 0].size - np.unique(x[x != 0]).size)
+               for r in range(1, d.nrounds))
+    assert reps > 0  # repeated ids present
+    bs = oracle.PDag(d)
+    nw = cfg.nwaves
+    with Engine(n, cfg.faulty, d.nrounds, gpu_device) as e:
+        e.append_packed(d)
+        for plan in (True, False):
+            e.set_device_plan(plan)
+            for cm, dm in MODES:
+                want = bs.replay(cfg.faulty, nw, cm, dm)
+                assert want.rc == 0
+                got = e.replay(nw, cm, dm)
+                _same(got, want, ids=False)
+                assert got.chain_edges == want.chain_edges
+                assert got.sweep["canon_segments"] >= 0

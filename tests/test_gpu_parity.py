@@ -201,12 +201,13 @@ def test_memo_on_off_large_n(gpu_device):
                 _compare_replay(e.replay(R // 4, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), want, ids=False)
 
 
-@pytest.mark.parametrize("n", [1024, 1100])
-@pytest.mark.parametrize("depth", [64, 65, 66])
+@pytest.mark.parametrize("n,depth", [(1024, 64), (1024, 66), (1024, 80), (1024, 255), (1024, 256),
+                                     (1100, 63), (1100, 64), (1100, 66), (300, 150)])
 def test_memo_window_boundary(gpu_device, n, depth):
-    """Weak deltas at the memo window's edge (DR_OPT_MEMO applies up to 65: WU holds 64
-    slots per round; 66 takes the full-sweep path) at row strides 16 (n=1024) and 32
-    (n=1100): every mode, memo and device plan on and off, == the bitset oracle."""
+    """Weak deltas across the memo window (engine.hip kMemoMaxDelta = 255 and the sweeps'
+    LDS ring: 256 rounds at row stride 16 (n=1024), 64 at stride 32 (n=1100), so the memo
+    applies up to 255 / 63; past it the full sweeps run): every mode, memo and device plan
+    on and off, == the bitset oracle, and the memo path really ran where it applies."""
     from dag_rider_amd.gen import small_config
 
     cfg = small_config(n, depth + 24, 40 + depth, p_present=0.97, p_late=0.02, p_w=0.05, weak_depth=depth,
@@ -229,6 +230,8 @@ def test_memo_window_boundary(gpu_device, n, depth):
                         got = e.replay(nw, cm, dm)
                         _compare_replay(got, want, ids=False)
                         assert got.chain_edges == want.chain_edges
+                        limit = 255 if n <= 1024 else 63
+                        assert (got.sweep["canon_segments"] >= 0) == (memo and depth <= limit), got.sweep
         e.set_memo(True)
         e.set_device_plan(True)
         stack = [(4 * w - 3, 1) for w in range(1, nw + 1)]
