@@ -26,6 +26,7 @@
 #include "replay_plan.hpp"
 #include "batch.hpp"
 #include "batch1w.hpp"
+#include "general.hpp"
 
 using dr::u64;
 
@@ -126,6 +127,14 @@ struct dr_ctx {
   DevBuf slot_rep, dup_off, dup_src;
   std::vector<uint32_t> h_dup_off{0};
   int64_t ndups = 0;  // repeated slots in rounds >= 1 (round 0 may repeat ids: never read)
+  // edges outside the round contract (App. A Q8: a strong edge not to r-1, a weak
+  // edge not below r-1): while any is mirrored every query takes the general sweep
+  int64_t nirr = 0;
+  int irr_tmax = 0;  // the highest round an irregular edge targets (the general sweep's row extent)
+  DevBuf irr, irr_roff, gscratch, gquery, gaux;
+  std::vector<uint32_t> h_irr_roff{0};
+  bool general() const { return nirr > 0; }
+  dr::GView gview() const { return dr::GView{irr.as<uint64_t>(), irr_roff.as<uint32_t>()}; }
   int lead_src(int w) const { return (w >= 0 && w < (int)h_lead.size()) ? h_lead[w] : 1; }
   // host mirror: per-round data, presence [rounds][WS], and the prefix offsets
   // of the flattened device arrays (valid for rounds < up_lo)
@@ -212,7 +221,7 @@ struct dr_ctx {
   // window -- deltas up to kMemoMaxDelta (WU holds dd = dmax - 1 slots per round, the
   // merge window is dmax rounds) that the sweeps' LDS ring holds -- and no far edges
   bool memo_ok() const {
-    return nfar == 0 && dmax_near <= kMemoMaxDelta && (1 << depth_log2()) > dmax_near;
+    return nfar == 0 && nirr == 0 && dmax_near <= kMemoMaxDelta && (1 << depth_log2()) > dmax_near;
   }
   // repeated ids: the summaries' counts and the emission count every slot of a
   // reached id (REF), PAPER delivers an id at its first slot (slot_rep)
@@ -405,6 +414,7 @@ struct dr_ctx {
     h_dup_off.resize(R + 1);
     h_wc_roff.resize(R + 1);
     h_far_roff.resize(R + 1);
+    h_irr_roff.resize(R + 1);
     h_weak_roff.resize(R + 1);
     h_ppref.resize(R);
     for (int r = lo; r < R; r++) {
@@ -416,6 +426,7 @@ struct dr_ctx {
       h_slot_off[r + 1] = h_slot_off[r] + (uint32_t)h.slots.size();
       h_wc_roff[r + 1] = h_wc_roff[r] + (uint32_t)h.wc_key.size();
       h_far_roff[r + 1] = h_far_roff[r] + (uint32_t)h.far.size();
+      h_irr_roff[r + 1] = h_irr_roff[r] + (uint32_t)h.irr.size();
       h_weak_roff[r + 1] = h_weak_roff[r] + (uint32_t)h.nweak;
     }
     const size_t s0 = h_slot_off[lo], s1 = h_slot_off[R], k0 = h_wc_roff[lo], k1 = h_wc_roff[R];
@@ -457,19 +468,24 @@ struct dr_ctx {
     if ((e = wc_key.grow(k1 * 4 + 64, k0 * 4, stream)) != hipSuccess) return e;
     if ((e = wc_rows.grow(k1 * WS * 8 + 64, k0 * WS * 8, stream)) != hipSuccess) return e;
     if ((e = far.grow(f1 * 8 + 64, f0 * 8, stream)) != hipSuccess) return e;
+    const size_t i0 = h_irr_roff[lo], i1 = h_irr_roff[R];
+    if ((e = irr.grow(i1 * 8 + 64, i0 * 8, stream)) != hipSuccess) return e;
+    if ((e = irr_roff.grow(((size_t)R + 1) * 4 + 64, ((size_t)lo + 1) * 4, stream)) != hipSuccess) return e;
     std::vector<uint16_t> sl;
     sl.reserve(s1 - s0);
     std::vector<uint32_t> kk;
     kk.reserve(k1 - k0);
-    std::vector<u64> rows, ff;
+    std::vector<u64> rows, ff, ii;
     rows.reserve((k1 - k0) * WS);
     ff.reserve(f1 - f0);
+    ii.reserve(i1 - i0);
     for (int r = lo; r < R; r++) {
       const HostRound &h = hr[r];
       sl.insert(sl.end(), h.slots.begin(), h.slots.end());
       kk.insert(kk.end(), h.wc_key.begin(), h.wc_key.end());
       rows.insert(rows.end(), h.wc_rows.begin(), h.wc_rows.end());
       ff.insert(ff.end(), h.far.begin(), h.far.end());
+      ii.insert(ii.end(), h.irr.begin(), h.irr.end());
     }
     const size_t nr = (size_t)(R - lo);
     if ((e = h2d(slot_src.as<uint16_t>() + s0, sl.data(), sl.size() * 2)) != hipSuccess) return e;
@@ -479,6 +495,8 @@ struct dr_ctx {
     if ((e = h2d(wc_key.as<uint32_t>() + k0, kk.data(), kk.size() * 4)) != hipSuccess) return e;
     if ((e = h2d(wc_rows.as<u64>() + k0 * WS, rows.data(), rows.size() * 8)) != hipSuccess) return e;
     if ((e = h2d(far.as<u64>() + f0, ff.data(), ff.size() * 8)) != hipSuccess) return e;
+    if (i1 > i0 && (e = h2d(irr.as<u64>() + i0, ii.data(), ii.size() * 8)) != hipSuccess) return e;
+    if ((e = h2d(irr_roff.as<uint32_t>() + lo + 1, &h_irr_roff[lo + 1], nr * 4)) != hipSuccess) return e;
     if ((e = h2d(slot_off.as<uint32_t>() + lo + 1, &h_slot_off[lo + 1], nr * 4)) != hipSuccess) return e;
     if ((e = h2d(ppref.as<u64>() + lo, &h_ppref[lo], nr * 8)) != hipSuccess) return e;
     if ((e = h2d(wc_roff.as<uint32_t>() + lo + 1, &h_wc_roff[lo + 1], nr * 4)) != hipSuccess) return e;
@@ -936,7 +954,8 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
       c->ppref.ensure((size_t)(max_rounds + 1) * sizeof(u64)) != hipSuccess ||
       c->weak_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->far_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
-      c->far.ensure(4096) != hipSuccess ||
+      c->far.ensure(4096) != hipSuccess || c->irr.ensure(4096) != hipSuccess ||
+      c->irr_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->wc_roff.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
       c->wc_key.ensure(4096) != hipSuccess || c->wc_rows.ensure(4096) != hipSuccess ||
       c->sdeg.ensure((size_t)max_rounds * n * sizeof(uint16_t)) != hipSuccess ||
@@ -950,6 +969,7 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   (void)hipMemcpy(c->slot_off.p, &zero, 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(c->weak_roff.p, &zero, 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(c->far_roff.p, &zero, 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(c->irr_roff.p, &zero, 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(c->wc_roff.p, &zero, 4, hipMemcpyHostToDevice);
   c->h_lead.assign((size_t)max_rounds / 4 + 2, 1);  // chooseLeader(w) = 1 (process.go:390-392)
   (void)hipMemcpy(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice);
@@ -972,7 +992,8 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds, &c->plan_out,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
-                    &c->admit_buf, &c->lead, &c->split_S, &c->split_ctl};
+                    &c->admit_buf, &c->lead, &c->split_S, &c->split_ctl, &c->irr, &c->irr_roff, &c->gscratch,
+                    &c->gquery, &c->gaux};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1113,16 +1134,19 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
     }
     if (vr != r || vs < 1 || vs > n)
       return c->fail(DR_E_CONTRACT, "p.dag[%d]: id (%d,%d) outside the mirrored contract", r, vr, vs);
-    if (r == 0 && sb > sa) return c->fail(DR_E_CONTRACT, "round 0 vertex (0,%d) has strong edges", vs);
+    // any target id the mirror can hold: edges outside the round contract (App. A Q8)
+    // are kept as irregular edges and answered by the general sweep (general.hpp)
     for (uint32_t e = sa; e < sb; e++) {
       const int tr = strong_ids[2 * e], ts = strong_ids[2 * e + 1];
-      if (tr != r - 1 || ts < 1 || ts > n)
-        return c->fail(DR_E_CONTRACT, "strong edge (%d,%d)->(%d,%d) must target round r-1, source in [1,n]", r, vs, tr, ts);
+      if (tr < 0 || tr >= c->max_rounds || ts < 1 || ts > n)
+        return c->fail(DR_E_CONTRACT, "strong edge (%d,%d)->(%d,%d): target outside rounds [0,%d), sources [1,%d]", r, vs,
+                       tr, ts, c->max_rounds, n);
     }
     for (uint32_t e = wa; e < wb; e++) {
       const int tr = weak_ids[2 * e], ts = weak_ids[2 * e + 1];
-      if (tr < 0 || tr > r - 2 || ts < 1 || ts > n)
-        return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target round < r-1, source in [1,n]", r, vs, tr, ts);
+      if (tr < 0 || tr >= c->max_rounds || ts < 1 || ts > n)
+        return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): target outside rounds [0,%d), sources [1,%d]", r, vs, tr,
+                       ts, c->max_rounds, n);
     }
   }
   // pass 2: apply
@@ -1174,22 +1198,41 @@ extern "C" int dr_append_vertices(dr_ctx *c, int k, const int32_t *slot_round, c
       h.far.erase(std::remove_if(h.far.begin(), h.far.end(), [&](uint64_t x) { return (int)(x >> 32) == o; }),
                   h.far.end());
       c->nfar -= nf - h.far.size();
+      const size_t ni = h.irr.size();
+      h.irr.erase(std::remove_if(h.irr.begin(), h.irr.end(),
+                                 [&](uint64_t x) { return (int)((x >> 32) & 2047u) == o; }),
+                  h.irr.end());
+      c->nirr -= ni - h.irr.size();
     }
     pw |= pbit;
     auto pa = put_at.find((uint32_t)vi);
     const int slot_nv = pa == put_at.end() ? nv : pa->second;
     u64 *row = &rows[(size_t)slot_nv * WS];
     std::fill(row, row + WS, 0ULL);
+    uint64_t nirr_s = 0;  // strong edges outside the round contract (App. A Q8)
     for (uint32_t e = strong_off[i]; e < strong_off[i + 1]; e++) {
-      const int ts = strong_ids[2 * e + 1] - 1;
+      const int tr = strong_ids[2 * e], ts = strong_ids[2 * e + 1] - 1;
+      if (tr != r - 1) {
+        h.irr.push_back(dr::irr_pack(vs - 1, true, tr, ts));
+        c->irr_tmax = std::max(c->irr_tmax, tr);
+        nirr_s++;
+        continue;
+      }
       row[ts >> 6] |= 1ULL << (ts & 63);
     }
-    uint64_t d = 0;
+    c->nirr += (int64_t)nirr_s;
+    uint64_t d = nirr_s;
     for (int w = 0; w < WS; w++) d += (uint64_t)__builtin_popcountll(row[w]);
     h.deg += d;
     const uint32_t wa = weak_off[i], wb = weak_off[i + 1];
     for (uint32_t e = wa; e < wb; e++) {
       const int tr = weak_ids[2 * e], ts = weak_ids[2 * e + 1] - 1, delta = r - tr;
+      if (delta < 2) {  // a weak edge not below r-1 (App. A Q8)
+        h.irr.push_back(dr::irr_pack(vs - 1, false, tr, ts));
+        c->irr_tmax = std::max(c->irr_tmax, tr);
+        c->nirr++;
+        continue;
+      }
       if (delta <= 1023) {
         wc_add(h, WS, ((uint32_t)delta << 11) | (uint32_t)ts, vs - 1);
         dmax = std::max(dmax, delta);
@@ -1243,6 +1286,9 @@ extern "C" int dr_append_rounds_lists(dr_ctx *c, int r0, int k, const uint32_t *
   std::vector<uint16_t> src(std::max<uint32_t>(S1 - S0, 1));
   std::vector<uint64_t> rows((size_t)k * n * W, 0);
   std::vector<std::vector<uint32_t>> wl((size_t)k * n);
+  std::vector<std::vector<uint64_t>> irl((size_t)k * n);  // edges outside the round contract (App. A Q8)
+  if (r0 < 0 || k > c->max_rounds || r0 > c->max_rounds - k)
+    return c->fail(DR_E_INVAL, "append of rounds [%d, %d) exceeds max_rounds %d", r0, r0 + k, c->max_rounds);
   for (int i = 0; i <= k; i++) so[i] = slot_off[i] - S0;
   for (int i = 0; i < k; i++) {
     const int r = r0 + i;
@@ -1263,18 +1309,24 @@ extern "C" int dr_append_rounds_lists(dr_ctx *c, int r0, int k, const uint32_t *
       // its edges replace the earlier slot's
       std::fill(row, row + W, 0ULL);
       wl[(size_t)i * n + (vs - 1)].clear();
+      std::vector<uint64_t> &I = irl[(size_t)i * n + (vs - 1)];
+      I.clear();
       for (uint32_t e = sa; e < sb; e++) {
         const int tr = strong_ids[2 * e], ts = strong_ids[2 * e + 1];
-        if (tr != r - 1 || ts < 1 || ts > n)
-          return c->fail(DR_E_CONTRACT, "strong edge (%d,%d)->(%d,%d) must target round r-1, source in [1,n]", r, vs, tr, ts);
-        row[(ts - 1) >> 6] |= 1ULL << ((ts - 1) & 63);
+        if (tr < 0 || tr >= c->max_rounds || ts < 1 || ts > n)
+          return c->fail(DR_E_CONTRACT, "strong edge (%d,%d)->(%d,%d): target outside rounds [0,%d), sources [1,%d]", r,
+                         vs, tr, ts, c->max_rounds, n);
+        if (tr != r - 1) I.push_back(dr::irr_pack(vs - 1, true, tr, ts - 1));
+        else row[(ts - 1) >> 6] |= 1ULL << ((ts - 1) & 63);
       }
       std::vector<uint32_t> &L = wl[(size_t)i * n + (vs - 1)];
       for (uint32_t e = wa; e < wb; e++) {
         const int tr = weak_ids[2 * e], ts = weak_ids[2 * e + 1];
-        if (tr < 0 || tr > r - 2 || ts < 1 || ts > n)
-          return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target round < r-1, source in [1,n]", r, vs, tr, ts);
-        L.push_back(((uint32_t)tr << 11) | (uint32_t)(ts - 1));
+        if (tr < 0 || tr >= c->max_rounds || ts < 1 || ts > n)
+          return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): target outside rounds [0,%d), sources [1,%d]", r,
+                         vs, tr, ts, c->max_rounds, n);
+        if (tr > r - 2) I.push_back(dr::irr_pack(vs - 1, false, tr, ts - 1));
+        else L.push_back(((uint32_t)tr << 11) | (uint32_t)(ts - 1));
       }
     }
   }
@@ -1285,7 +1337,37 @@ extern "C" int dr_append_rounds_lists(dr_ctx *c, int r0, int k, const uint32_t *
     wt.insert(wt.end(), wl[v].begin(), wl[v].end());
   }
   woff[(size_t)k * n] = (uint32_t)wt.size();
-  return dr_append_rounds_packed(c, r0, k, so.data(), src.data(), rows.data(), woff.data(), wt.data());
+  if (int rc = dr_append_rounds_packed(c, r0, k, so.data(), src.data(), rows.data(), woff.data(), wt.data()))
+    return rc;
+  // the irregular edges of the appended rounds: kept per round, counted in the vertices'
+  // degrees (edge totals count every edge of an id once)
+  bool any = false;
+  for (int i = 0; i < k; i++)
+    for (int s = 0; s < n; s++) {
+      const std::vector<uint64_t> &I = irl[(size_t)i * n + s];
+      if (I.empty()) continue;
+      any = true;
+      HostRound &h = c->hr[r0 + i];
+      uint32_t ns = 0, nwk = 0;
+      for (uint64_t x : I) {
+        ((x >> 31) & 1u) ? ns++ : nwk++;
+        c->irr_tmax = std::max(c->irr_tmax, (int)((x >> 11) & 0xFFFFFu));
+      }
+      h.irr.insert(h.irr.end(), I.begin(), I.end());
+      c->nirr += (int64_t)I.size();
+      const size_t vi = (size_t)(r0 + i) * n + s;
+      c->h_sdeg[vi] = (uint16_t)std::min<uint32_t>(c->h_sdeg[vi] + ns, 65535u);
+      c->h_wcnt[vi] = (uint16_t)std::min<uint32_t>(c->h_wcnt[vi] + nwk, 65535u);
+      h.deg += ns;
+      h.nweak += nwk;
+    }
+  if (!any) return DR_OK;
+  for (int r = r0; r < r0 + k; r++) c->touch(r);
+  HIPCHK(c, c->h2d(c->sdeg.as<uint16_t>() + (size_t)r0 * n, &c->h_sdeg[(size_t)r0 * n], (size_t)k * n * 2));
+  HIPCHK(c, c->h2d(c->wdeg.as<uint16_t>() + (size_t)r0 * n, &c->h_wcnt[(size_t)r0 * n], (size_t)k * n * 2));
+  HIPCHK(c, c->upload_suffix());
+  HIPCHK(c, c->sync());
+  return DR_OK;
 }
 
 // ===========================================================================
@@ -1837,12 +1919,335 @@ extern "C" int dr_last_batch_phases(const dr_ctx *c, float *ms4) {
   return DR_OK;
 }
 
+// one orderVertices pop: the popped leader's id and p.round at its delivery
+struct Pop { int32_t round, source, cur_round; };
+
+// ===========================================================================
+// General graphs: every query of a mirror holding edges
+// outside the round contract, on the general sweep (general.hpp).  One sweep per
+// start vertex gives its whole reach set (every round, cycles included); the
+// reference's functions are then bit tests on it: path() the target's bit,
+// waveReady's vote the leader's bit in the strong sets of round 4w's ids, the
+// chain the first present leader below in the last pushed leader's strong set,
+// orderVertices the set's rows 1..p.round in slot order.
+// ===========================================================================
+namespace {
+
+template <int WS>
+hipError_t launch_gsweep_t(dr_ctx *c, const dr::GQuery *q, int nq, int Tg, u64 *masks, u64 *scratch, uint8_t *hit,
+                           u64 *edges) {
+  hipLaunchKernelGGL((dr::k_gsweep<WS>), dim3(nq), dim3(256), 0, c->stream, c->view(), c->gview(), q, nq, Tg,
+                     c->nrounds, masks, scratch, hit, edges);
+  return hipGetLastError();
+}
+template <int WS>
+hipError_t launch_gdeg_t(dr_ctx *c, const int64_t *moff, const int32_t *first, const int32_t *last, int np, int weak,
+                         u64 *out) {
+  hipLaunchKernelGGL((dr::k_gdeg<WS>), dim3(np), dim3(256), 0, c->stream, c->view(), c->masks.as<u64>(), moff, first,
+                     last, weak, out);
+  return hipGetLastError();
+}
+template <int WS>
+hipError_t launch_gpaper_t(dr_ctx *c, const int64_t *moff, const int32_t *last, int np, int Tg, u64 *D) {
+  hipLaunchKernelGGL((dr::k_gpaper<WS>), dim3(1), dim3(256), 0, c->stream, c->view(), c->masks.as<u64>(), moff, last,
+                     np, Tg, D);
+  return hipGetLastError();
+}
+#define DR_WS_SWITCH(c, call)                         \
+  switch ((c)->WS) {                                  \
+    case 1: { constexpr int WS_ = 1; return call; }   \
+    case 2: { constexpr int WS_ = 2; return call; }   \
+    case 4: { constexpr int WS_ = 4; return call; }   \
+    case 8: { constexpr int WS_ = 8; return call; }   \
+    case 16: { constexpr int WS_ = 16; return call; } \
+    case 32: { constexpr int WS_ = 32; return call; } \
+  }                                                   \
+  return hipErrorInvalidValue
+hipError_t launch_gsweep(dr_ctx *c, const dr::GQuery *q, int nq, int Tg, u64 *m, u64 *s, uint8_t *h, u64 *ed) {
+  DR_WS_SWITCH(c, launch_gsweep_t<WS_>(c, q, nq, Tg, m, s, h, ed));
+}
+hipError_t launch_gdeg(dr_ctx *c, const int64_t *moff, const int32_t *first, const int32_t *last, int np, int weak,
+                       u64 *out) {
+  DR_WS_SWITCH(c, launch_gdeg_t<WS_>(c, moff, first, last, np, weak, out));
+}
+hipError_t launch_gpaper(dr_ctx *c, const int64_t *moff, const int32_t *last, int np, int Tg, u64 *D) {
+  DR_WS_SWITCH(c, launch_gpaper_t<WS_>(c, moff, last, np, Tg, D));
+}
+#undef DR_WS_SWITCH
+
+int gsweep_rows(const dr_ctx *c) { return std::max(c->nrounds - 1, c->irr_tmax) + 1; }
+
+// General sweeps of qv in batches (reach rows of every query at qv[i].mask_off in
+// c->masks, assigned here per batch); hits / edges to the host; on_batch(i0, i1)
+// sees each batch's rows before the next overwrites them.  whole: one batch or
+// DR_E_CAPACITY (callers that keep every query's rows).
+int run_gsweeps(dr_ctx *c, std::vector<dr::GQuery> &qv, std::vector<uint8_t> *hits, std::vector<u64> *edges,
+                const std::function<int(size_t, size_t)> &on_batch, bool whole = false) {
+  const int WS = c->WS, Tg = gsweep_rows(c) - 1;
+  const size_t per = (size_t)(Tg + 1) * WS, budget = (size_t)1 << 27;  // words of rows (and as many of scratch)
+  const size_t bq = std::max<size_t>(1, budget / per);
+  if (whole && qv.size() > bq) return c->fail(DR_E_CAPACITY, "general sweeps: %zu reach sets of %zu words exceed one batch", qv.size(), per);
+  if (hits) hits->assign(qv.size(), 0);
+  if (edges) edges->assign(qv.size(), 0);
+  for (size_t i0 = 0; i0 < qv.size(); i0 += bq) {
+    const size_t i1 = std::min(qv.size(), i0 + bq), nq = i1 - i0;
+    for (size_t i = i0; i < i1; i++) qv[i].mask_off = (int64_t)((i - i0) * per);
+    HIPCHK(c, c->masks.ensure(nq * per * 8));
+    HIPCHK(c, c->gscratch.ensure(nq * per * 8));
+    const size_t o_hit = nq * sizeof(dr::GQuery), o_e = (o_hit + nq + 7) & ~(size_t)7;
+    HIPCHK(c, c->gquery.ensure(o_e + nq * 8));
+    char *qb = c->gquery.as<char>();
+    HIPCHK(c, c->h2d(qb, qv.data() + i0, nq * sizeof(dr::GQuery)));
+    uint8_t *dh = reinterpret_cast<uint8_t *>(qb + o_hit);
+    u64 *de = reinterpret_cast<u64 *>(qb + o_e);
+    HIPCHK(c, launch_gsweep(c, reinterpret_cast<const dr::GQuery *>(qb), (int)nq, Tg, c->masks.as<u64>(),
+                            c->gscratch.as<u64>(), dh, de));
+    if (hits) HIPCHK(c, c->d2h(hits->data() + i0, dh, nq));
+    if (edges) HIPCHK(c, c->d2h(edges->data() + i0, de, nq * 8));
+    HIPCHK(c, c->sync());
+    if (on_batch)
+      if (int rc = on_batch(i0, i1)) return rc;
+  }
+  return DR_OK;
+}
+
+int general_path(dr_ctx *c, int q, const int32_t *from, const int32_t *to, int strong_only, uint8_t *out) {
+  const int Tg = gsweep_rows(c) - 1;
+  std::vector<dr::GQuery> qv;
+  std::vector<int> idx;
+  for (int i = 0; i < q; i++) {
+    const int fr = from[2 * i], fs = from[2 * i + 1], tr = to[2 * i], ts = to[2 * i + 1];
+    if (fr == tr && fs == ts) { out[i] = 1; continue; }  // process.go:91-93
+    if (fr < 0 || fr >= c->nrounds)
+      return c->fail(DR_E_INVAL, "query %d: from round %d outside the DAG (Go: index out of range)", i, fr);
+    out[i] = 0;
+    if (fs < 1 || fs > c->n || tr < 0 || tr > Tg || ts < 1 || ts > c->n) continue;  // no edges / not an id any edge holds
+    qv.push_back(dr::GQuery{fr, fs - 1, strong_only ? 1 : 0, tr, ts - 1, 1, 0, 0});
+    idx.push_back(i);
+  }
+  std::vector<uint8_t> hits;
+  if (int rc = run_gsweeps(c, qv, &hits, nullptr, {})) return rc;
+  for (size_t k = 0; k < idx.size(); k++) out[idx[k]] = hits[k];
+  return DR_OK;
+}
+
+int general_reach(dr_ctx *c, int q, const int32_t *from, const int32_t *bottom, int strong_only, uint64_t *out) {
+  const int W = c->W, WS = c->WS;
+  std::vector<dr::GQuery> qv(q);
+  std::vector<size_t> obase(q);
+  size_t acc = 0;
+  for (int i = 0; i < q; i++) {
+    const int fs = from[2 * i + 1];
+    qv[i] = dr::GQuery{from[2 * i], (fs >= 1 && fs <= c->n) ? fs - 1 : -1, strong_only ? 1 : 0, -1, -1, 1, 0, 0};
+    obase[i] = acc;
+    acc += (size_t)(from[2 * i] - bottom[i] + 1) * W;
+  }
+  std::vector<u64> tmp;
+  return run_gsweeps(c, qv, nullptr, nullptr, [&](size_t i0, size_t i1) -> int {
+    const size_t per = (size_t)gsweep_rows(c) * WS;
+    tmp.resize((i1 - i0) * per);
+    HIPCHK(c, hipMemcpy(tmp.data(), c->masks.p, tmp.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t i = i0; i < i1; i++)
+      for (int r = bottom[i]; r <= from[2 * i]; r++)
+        std::memcpy(out + obase[i] + (size_t)(r - bottom[i]) * W, &tmp[qv[i].mask_off + (size_t)r * WS], (size_t)W * 8);
+    return 0;
+  });
+}
+
+// waveReady's vote (process.go:326-339) for waves w0 .. w0+nw-1, all evaluable:
+// vcount = the slots of round 4w whose id's strong reach set holds the leader.
+int general_votes(dr_ctx *c, int w0, int nw, uint8_t *commit, int32_t *vcount) {
+  const int n = c->n;
+  std::vector<dr::GQuery> qv;
+  std::vector<int32_t> qw;  // wave index of each query
+  for (int i = 0; i < nw; i++) {
+    const int w = w0 + i, r1 = 4 * (w - 1) + 1, L = c->lead_src(w), r4 = 4 * w;
+    commit[i] = 0;
+    vcount[i] = -1;
+    if (!c->is_present(r1, L)) continue;  // leader is bottom (process.go:327-329)
+    vcount[i] = 0;
+    for (int s = 1; s <= n; s++)
+      if (c->is_present(r4, s)) {
+        qv.push_back(dr::GQuery{r4, s - 1, 1, r1, L - 1, 1, 0, 0});
+        qw.push_back(i);
+      }
+  }
+  std::vector<uint8_t> hits;
+  if (int rc = run_gsweeps(c, qv, &hits, nullptr, {})) return rc;
+  std::vector<uint8_t> reach((size_t)nw * (n + 1), 0);  // (wave, source) -> the leader is in its strong set
+  for (size_t k = 0; k < qv.size(); k++) reach[(size_t)qw[k] * (n + 1) + qv[k].s0 + 1] = hits[k];
+  for (int i = 0; i < nw; i++) {
+    if (vcount[i] < 0) continue;
+    int vc = 0;
+    for (uint16_t s : c->hr[4 * (w0 + i)].slots) vc += s != 0 && reach[(size_t)i * (n + 1) + s];  // every slot (:332)
+    vcount[i] = vc;
+    commit[i] = vc >= 2 * c->f + 1 ? 1 : 0;
+  }
+  return DR_OK;
+}
+
+// The leader chain of a commit of wave `wave` (process.go:341-350) above decidedWave
+// `floor`: pushes (task wave first) and the strong degrees of each segment's reach set
+// above the round where the next leader takes over (the last: above round(floor+1,1)).
+int general_chain(dr_ctx *c, int wave, int floor, std::vector<int32_t> &push, uint64_t *edges) {
+  push.assign(1, wave);
+  if (edges) *edges = 0;
+  if (wave - 1 < floor + 1) return DR_OK;
+  if (floor < 0) return c->fail(DR_E_INVAL, "decidedWave %d < 0 (Go: waveRound(0,1) index out of range)", floor);
+  const int WS = c->WS, bottom = 4 * floor + 1, T = c->nrounds - 1;
+  int vr = 4 * (wave - 1) + 1, vs = c->lead_src(wave), cur = wave;
+  std::vector<u64> rows;
+  while (true) {
+    std::vector<dr::GQuery> qv{dr::GQuery{vr, vs - 1, 1, -1, -1, 1, 0, 0}};
+    int next = -1;
+    if (int rc = run_gsweeps(c, qv, nullptr, nullptr, [&](size_t, size_t) -> int {
+          const size_t per = (size_t)gsweep_rows(c) * WS;
+          rows.resize(per);
+          HIPCHK(c, hipMemcpy(rows.data(), c->masks.p, per * 8, hipMemcpyDeviceToHost));
+          for (int w = cur - 1; w >= floor + 1 && next < 0; w--) {  // process.go:342-349
+            const int r = 4 * (w - 1) + 1, L = c->lead_src(w);
+            if (c->is_present(r, L) && ((rows[(size_t)r * WS + ((L - 1) >> 6)] >> ((L - 1) & 63)) & 1ULL)) next = w;
+          }
+          return 0;
+        }))
+      return rc;
+    if (edges) {  // the segment's strong degrees: rows above the round the next leader restarts at
+      const int lo = (next > 0 ? 4 * (next - 1) + 1 : bottom) + 1, hi = T;
+      if (lo <= hi) {
+        HIPCHK(c, c->gaux.ensure(64));
+        int64_t mo = 0;
+        int32_t fl[2] = {lo, hi};
+        char *a = c->gaux.as<char>();
+        HIPCHK(c, c->h2d(a, &mo, 8));
+        HIPCHK(c, c->h2d(a + 8, fl, 8));
+        HIPCHK(c, launch_gdeg(c, reinterpret_cast<const int64_t *>(a), reinterpret_cast<const int32_t *>(a + 8),
+                              reinterpret_cast<const int32_t *>(a + 12), 1, 0, reinterpret_cast<u64 *>(a + 16)));
+        u64 e = 0;
+        HIPCHK(c, c->d2h(&e, a + 16, 8));
+        HIPCHK(c, c->sync());
+        *edges += e;
+      }
+    }
+    if (next < 0) break;
+    push.push_back(next);
+    vr = 4 * (next - 1) + 1;
+    vs = c->lead_src(next);
+    cur = next;
+  }
+  return DR_OK;
+}
+
+// orderVertices (process.go:404-443) for pops in pop order: each pop's reach set
+// (strong + weak) on rounds 1..min(p.round, T) in slot order; PAPER minus what the
+// pops before it delivered (an id once, at its first slot).  counts, digests, edges
+// (strong + weak degrees of the delivered ids) per pop; ids optional.
+int general_deliver(dr_ctx *c, const std::vector<Pop> &pops, int mode, uint64_t *cnt, uint64_t *dg, uint64_t *pe,
+                    int32_t *ids, int64_t ids_cap, int64_t *ids_total) {
+  const int np = (int)pops.size(), WS = c->WS, T = c->nrounds - 1;
+  if (ids_total) *ids_total = 0;
+  if (np == 0) return DR_OK;
+  std::vector<dr::GQuery> qv(np);
+  for (int i = 0; i < np; i++) {
+    const Pop &p = pops[i];
+    const bool ok = p.round >= 0 && p.round <= T && p.source >= 1 && p.source <= c->n;
+    qv[i] = dr::GQuery{ok ? p.round : 0, ok ? p.source - 1 : -1, 0, -1, -1, 1, 0, 0};
+  }
+  if (int rc = run_gsweeps(c, qv, nullptr, nullptr, {}, true)) return rc;  // every pop's rows stay in c->masks
+  std::vector<int64_t> moff(np);
+  std::vector<int32_t> first(np, 1), last(np);
+  for (int i = 0; i < np; i++) {
+    moff[i] = qv[i].mask_off;
+    last[i] = std::min(pops[i].cur_round, T);
+  }
+  HIPCHK(c, c->gaux.ensure((size_t)np * 24 + 64));
+  char *a = c->gaux.as<char>();
+  int64_t *d_moff = reinterpret_cast<int64_t *>(a);
+  int32_t *d_first = reinterpret_cast<int32_t *>(a + (size_t)np * 8), *d_last = d_first + np;
+  u64 *d_e = reinterpret_cast<u64 *>(a + (size_t)np * 16);
+  HIPCHK(c, c->h2d(d_moff, moff.data(), (size_t)np * 8));
+  HIPCHK(c, c->h2d(d_first, first.data(), (size_t)np * 4));
+  HIPCHK(c, c->h2d(d_last, last.data(), (size_t)np * 4));
+  if (mode == DR_DELIVER_PAPER) {  // Alg. 3 line 54: minus the delivered set, pop by pop
+    const size_t dw = (size_t)gsweep_rows(c) * WS;
+    HIPCHK(c, c->dlv.ensure(dw * 8));
+    HIPCHK(c, hipMemsetAsync(c->dlv.p, 0, dw * 8, c->stream));
+    HIPCHK(c, launch_gpaper(c, d_moff, d_last, np, gsweep_rows(c) - 1, c->dlv.as<u64>()));
+  }
+  HIPCHK(c, launch_gdeg(c, d_moff, d_first, d_last, np, 1, d_e));
+  HIPCHK(c, c->d2h(pe, d_e, (size_t)np * 8));
+  HIPCHK(c, c->sync());
+  std::vector<dr::PopDesc> pd;
+  for (int i = 0; i < np; i++) {
+    if (last[i] < 1) continue;
+    dr::PopDesc d{};
+    d.mask_off = moff[i];
+    d.first = 1;
+    d.last = last[i];
+    d.out = i;
+    d.use_k = 0;
+    d.flags = mode == DR_DELIVER_PAPER ? dr::PD_FIRST_ONLY : 0;
+    pd.push_back(d);
+  }
+  return run_emit(c, pd, np, nullptr, cnt, dg, ids, ids_cap, 0, ids_total, nullptr);
+}
+
+int general_replay(dr_ctx *c, int nw, int chain_mode, int deliver_mode, dr_replay_out *o) {
+  if (int rc = general_votes(c, 1, nw, o->commit, o->vcount)) return rc;
+  uint64_t ce = 0;
+  for (int w = 1; w <= nw; w++)
+    if (o->vcount[w - 1] >= 0) ce += c->round_deg(4 * w - 2) + c->round_deg(4 * w - 1) + c->round_deg(4 * w);
+  o->commit_edges = ce;
+  std::vector<Pop> pops;
+  int64_t np = 0;
+  uint64_t chain_e = 0;
+  int last = 0;
+  std::vector<int32_t> push;
+  for (int w = 1; w <= nw; w++) {
+    o->push_off[w - 1] = (uint32_t)np;
+    if (!o->commit[w - 1]) continue;
+    uint64_t e = 0;
+    if (int rc = general_chain(c, w, chain_mode == DR_CHAIN_PERSISTENT ? last : 0, push, &e)) return rc;
+    chain_e += e;
+    last = w;
+    if (np + (int64_t)push.size() > o->push_cap || !o->push_wave)
+      return c->fail(DR_E_CAPACITY, "%lld pushed leaders, capacity %lld", (long long)(np + (int64_t)push.size()),
+                     (long long)o->push_cap);
+    for (int32_t pw : push) o->push_wave[np++] = pw;
+    for (auto it = push.rbegin(); it != push.rend(); ++it)  // the stack's LIFO order
+      pops.push_back(Pop{4 * (*it - 1) + 1, c->lead_src(*it), 4 * w});
+  }
+  o->push_off[nw] = (uint32_t)np;
+  o->n_push = np;
+  o->chain_edges = chain_e;
+  if (!pops.empty() && (!o->pop_count || !o->pop_digest))
+    return c->fail(DR_E_CAPACITY, "%zu pops, no pop outputs", pops.size());
+  std::vector<uint64_t> pe(pops.size());
+  int64_t tot = 0;
+  const bool want_ids = o->ids && o->ids_cap > 0;
+  if (int rc = general_deliver(c, pops, deliver_mode, o->pop_count, o->pop_digest, pe.data(),
+                               want_ids ? o->ids : nullptr, want_ids ? o->ids_cap : 0, &tot))
+    return rc;
+  uint64_t de = 0;
+  for (size_t i = 0; i < pops.size(); i++) {
+    de += pe[i];
+    if (o->pop_edges) o->pop_edges[i] = pe[i];
+  }
+  o->deliver_edges = de;
+  o->n_ids = want_ids ? tot : 0;
+  o->sweep_count = pops.size();
+  if (want_ids && tot > o->ids_cap) return c->fail(DR_E_CAPACITY, "%lld delivered ids, capacity %lld", (long long)tot, (long long)o->ids_cap);
+  return DR_OK;
+}
+
+}  // namespace
+
 extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_t *to, int strong_only,
                              uint8_t *out) {
   if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (q < 0 || (q > 0 && (!from || !to || !out))) return c->fail(DR_E_INVAL, "bad query arrays");
   if (int rc = set_device(c)) return rc;
+  if (c->general()) return general_path(c, q, from, to, strong_only, out);
   if (int rc = refresh_rounds(c)) return rc;
   std::vector<dr::SweepQuery> qv;
   std::vector<int> idx;
@@ -1886,6 +2291,7 @@ extern "C" int dr_reach_sets(dr_ctx *c, int q, const int32_t *from, const int32_
   }
   if (out_words) *out_words = need;
   if (need > cap_words || (!out && need)) return c->fail(DR_E_CAPACITY, "reach sets need %zu words", need);
+  if (c->general()) return general_reach(c, q, from, bottom, strong_only, out);
   std::vector<dr::SweepQuery> qv(q);
   std::vector<size_t> obase(q);
   size_t acc = 0;
@@ -1936,6 +2342,7 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   }
   const int nw = wk - w0 + 1;
   if (nw <= 0) return DR_OK;
+  if (c->general()) return general_votes(c, w0, nw, commit, vcount);
   HIPCHK(c, c->commit.ensure((size_t)nw));
   HIPCHK(c, c->vcount.ensure((size_t)nw * 4));
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
@@ -2007,7 +2414,6 @@ int run_chains(dr_ctx *c, const std::vector<ChainTask> &tasks, std::vector<std::
   return DR_OK;
 }
 
-struct Pop { int32_t round, source, cur_round; };
 struct SweepStats { uint64_t sweeps = 0, partial = 0, rows = 0, weak_scanned = 0, shortcut = 0; };
 
 // Deliver pops (in pop order).
@@ -2305,6 +2711,9 @@ extern "C" int dr_set_weak_edges(dr_ctx *c, int round, int nstrong, const int32_
     return c->fail(DR_E_INVAL, "setWeakEdges: round %d outside [1, %d] (Go: index out of range)", round, c->nrounds);
   if (mode != DR_WEAK_LITERAL && mode != DR_WEAK_PAPER) return c->fail(DR_E_INVAL, "unknown mode %d", mode);
   if (nstrong < 0 || (nstrong > 0 && !strong_ids)) return c->fail(DR_E_INVAL, "bad strong edge array");
+  if (c->general())
+    return c->fail(DR_E_CONTRACT, "setWeakEdges on a mirror with edges outside the round contract (App. A Q8) "
+                                  "is not supported");
   if (int rc = set_device(c)) return rc;
   const int WS = c->WS;
   std::vector<u64> srow(WS, 0);
@@ -2367,8 +2776,12 @@ extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *com
   *n_pushed = 0;
   if (int rc = commit_range(c, wave, wave, commit, vcount, nullptr)) return rc;
   if (!*commit) return DR_OK;
-  std::vector<std::vector<int32_t>> pushes;
-  if (int rc = run_chains(c, {ChainTask{wave, decided_wave}}, pushes, nullptr, nullptr)) return rc;
+  std::vector<std::vector<int32_t>> pushes(1);
+  if (c->general()) {
+    if (int rc = general_chain(c, wave, decided_wave, pushes[0], nullptr)) return rc;
+  } else if (int rc = run_chains(c, {ChainTask{wave, decided_wave}}, pushes, nullptr, nullptr)) {
+    return rc;
+  }
   *n_pushed = (int)pushes[0].size();
   if ((int)pushes[0].size() > cap || (!pushed_waves && !pushes[0].empty()))
     return c->fail(DR_E_CAPACITY, "%zu pushed leaders, capacity %d", pushes[0].size(), cap);
@@ -2401,10 +2814,20 @@ extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack,
     if (cur_round < 1) p.round = std::max(0, std::min(p.round, c->nrounds - 1));
     pops.push_back(p);
   }
-  if (mode == DR_DELIVER_REF)  // stale rounds' summaries + the canonical cone of the current top
-    if (int rc = refresh_canon(c)) return rc;
   std::vector<uint64_t> cnt(pops.size()), dg(pops.size());
   int64_t tot = 0;
+  if (c->general()) {  // edges outside the round contract (App. A Q8): the general sweep
+    std::vector<uint64_t> pe(pops.size());
+    if (int rc = general_deliver(c, pops, mode, cnt.data(), dg.data(), pe.data(), out_ids, (int64_t)cap, &tot))
+      return rc;
+    if (out_n) *out_n = (size_t)tot;
+    if (pop_count) std::copy(cnt.begin(), cnt.end(), pop_count);
+    if (pop_digest) std::copy(dg.begin(), dg.end(), pop_digest);
+    if (out_ids && (size_t)tot > cap) return c->fail(DR_E_CAPACITY, "%lld delivered ids, capacity %zu", (long long)tot, cap);
+    return DR_OK;
+  }
+  if (mode == DR_DELIVER_REF)  // stale rounds' summaries + the canonical cone of the current top
+    if (int rc = refresh_canon(c)) return rc;
   // REF mode on fresh summaries without ids: planned on the device, one copy back
   int rc = 1;
   if (mode == DR_DELIVER_REF && !out_ids && c->plan_mode != 0 && summary_fresh(c))
@@ -2835,6 +3258,7 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;
   o->canon_segments = -1;
+  if (c->general()) return general_replay(c, nwaves, chain_mode, deliver_mode, o);
   if (c->plan_mode != 0 && c->memo_on() && !(o->ids && o->ids_cap > 0) && o->push_wave &&
       o->pop_count && o->pop_digest) {
     const int rc = replay_planned(c, nwaves, chain_mode, deliver_mode == DR_DELIVER_PAPER, o);
@@ -2908,7 +3332,7 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
 namespace {
 // the fused small-DAG path (batch.hpp) covers this context's DAG
 bool small_ok(const dr_ctx *c, int nwaves) {
-  return c->n <= 128 && nwaves <= 64 && c->nfar == 0 && c->dmax_near < 32 && c->ndups == 0;
+  return c->n <= 128 && nwaves <= 64 && c->nfar == 0 && c->dmax_near < 32 && c->ndups == 0 && c->nirr == 0;
 }
 
 template <int D, bool PAPER, bool PERSIST>

@@ -19,6 +19,7 @@ struct HostRound {
   std::vector<uint32_t> wc_key;  // weak columns: distinct near targets (delta << 11 | t-1), sorted
   std::vector<uint64_t> wc_rows; // [key][WS]: the round's sources with that weak edge
   std::vector<uint64_t> far;     // weak edges with delta > 1023: (own s-1) << 32 | (r' << 11 | t-1)
+  std::vector<uint64_t> irr;     // edges outside the round contract (App. A Q8), general.hpp irr_pack
   uint32_t ndup = 0;             // slots repeating an id already in the round (engine.hip upload_suffix)
 };
 

@@ -113,14 +113,20 @@ int dr_set_option(dr_ctx *ctx, int option, int value);
  *   weak_off   [S+1], weak_ids   [2*E']  weakEdges per slot
  * Contract (else DR_E_CONTRACT): a slot's id is (r, s), 1 <= s <= n, or the
  * zero id {0,0} with no edges (the Figure-1 ghost slot,
- * process_internal_test.go:91); strong edges target (r-1, t), weak edges
- * (r', t) with r' < r-1; 1 <= t <= n.  Targets need not exist (a dangling
- * target counts as reached, process.go:123,136).  An id may repeat within a
- * round, as uponDeliver and the buffer loop let it (process.go:158-169, :229):
- * every slot is kept, path() sees the id's LAST slot (:112-116), vCount and
- * REF delivery count every slot (:332, :418-429), PAPER delivers an id once,
- * at its first slot; edge totals count an id's edges once (its last slot).
- * Such a mirror replays on the full sweeps (DR_OPT_MEMO does not apply). */
+ * process_internal_test.go:91); every edge targets an id (r', t) with
+ * 0 <= r' < max_rounds, 1 <= t <= n.  Targets need not exist (a dangling
+ * target counts as reached, process.go:123,136).  Strong edges to (r-1, t) and
+ * weak edges below r-1 are the round contract the reference's own vertices
+ * keep; any other edge (uponDeliver checks only the
+ * strong-edge count, process.go:165 -- a strong edge to another round, a weak
+ * edge to round r-1 or above, even a cycle) is kept too, and while the mirror
+ * holds one every query runs on the general sweep (general.hpp: exact for any
+ * graph, slower; dr_set_weak_edges then returns DR_E_CONTRACT).  An id may
+ * repeat within a round, as uponDeliver and the buffer loop let it
+ * (process.go:158-169, :229): every slot is kept, path() sees the id's LAST
+ * slot (:112-116), vCount and REF delivery count every slot (:332, :418-429),
+ * PAPER delivers an id once, at its first slot; edge totals count an id's
+ * edges once (its last slot). */
 int dr_append_rounds_lists(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off,
                            const int32_t *slot_id, const uint32_t *strong_off,
                            const int32_t *strong_ids, const uint32_t *weak_off,

@@ -129,3 +129,39 @@ def with_repeated_ids(rng: np.random.Generator, dag, p_dup=0.3, max_extra=2):
                 pos = int(rng.integers(0, len(out[r]) + 1))
                 out[r].insert(pos, Vertex(vid, b"", st, wk))
     return out
+
+
+def with_irregular_edges(rng: np.random.Generator, dag, p_irr=0.2, up=True):
+    """A [][]vertex with edges outside the round contract, which
+    uponDeliver admits (it checks only the strong-edge count, process/process.go:165)
+    and path()'s BFS answers (:89-148): some vertices get strong edges to a round other
+    than r-1 and weak edges to round r-1 or above; with `up`, also to the same round or
+    later ones (cycles).  Targets are ids of mirrored rounds (present or not: a
+    dangling target counts as reached), never one the vertex already names."""
+    R = len(dag) - 1
+    out = []
+    for r, rnd in enumerate(dag):
+        row = []
+        for v in rnd:
+            if v.id == VertexID(0, 0) or rng.random() >= p_irr:
+                row.append(v)
+                continue
+            n_src = max(x.id.source for rr in dag for x in rr) or 1
+            have = set(v.strong_edges) | set(v.weak_edges)
+            st, wk = list(v.strong_edges), list(v.weak_edges)
+            for _ in range(int(rng.integers(1, 4))):
+                lo, hi = (0, R) if up else (0, max(0, r - 1))
+                tr = int(rng.integers(lo, hi + 1))
+                t = VertexID(tr, int(rng.integers(1, n_src + 1)))
+                if t in have or t == v.id:
+                    continue
+                strong = rng.random() < 0.5
+                if strong and tr == r - 1 or (not strong and tr <= r - 2):
+                    strong = not strong  # keep it outside the contract
+                if strong and tr == r - 1 or (not strong and tr <= r - 2):
+                    continue
+                (st if strong else wk).append(t)
+                have.add(t)
+            row.append(Vertex(v.id, v.block, st, wk))
+        out.append(row)
+    return out

@@ -132,10 +132,12 @@ def test_gpu_append_vertices_all_or_nothing(gpu_device):
         e.append_lists(full[:6])
         good = full[6][:2]
         before = e.path_batch([((5, s), (4, t)) for s in range(1, 7) for t in range(1, 7)], False).tolist()
+        # (a strong edge not to r-1 or a weak edge not below r-1 is accepted: App. A Q8,
+        # tests/test_gpu_irregular.py)
         bad_cases = [
             good + [Vertex(VertexID(6, 9), b"", [], [])],                      # source > n
-            good + [Vertex(VertexID(6, 3), b"", [VertexID(4, 1)], [])],       # strong edge not to r-1
-            good + [Vertex(VertexID(6, 3), b"", [], [VertexID(5, 1)])],       # weak edge to r-1
+            good + [Vertex(VertexID(6, 3), b"", [VertexID(12, 1)], [])],      # target round >= max_rounds
+            good + [Vertex(VertexID(6, 3), b"", [], [VertexID(5, 7)])],       # target source > n
             good + [Vertex(VertexID(0, 0), b"", [VertexID(4, 1)], [])],       # ghost with edges
         ]
         for verts in bad_cases:

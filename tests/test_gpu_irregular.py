@@ -1,0 +1,139 @@
+"""GPU parity on mirrors holding edges outside the round contract.
+
+uponDeliver admits a vertex whose strong edges do not all target r-1, or whose weak
+edges do not all lie below r-1 (it checks only the strong-edge count,
+process/process.go:165), and path()'s BFS with a visited set answers for any graph
+(:89-148), cycles included.  The mirror keeps such edges beside the packed rows and
+answers every query with the general sweep (dag_rider_amd/csrc/general.hpp); checked
+against the literal restatement (oracle/ref_literal.c), which runs the reference's BFS
+on the same [][]vertex.  Nothing here is refused with DR_E_CONTRACT."""
+import numpy as np
+import pytest
+
+import oracle
+from dag_rider_amd import _lib as L
+from dag_rider_amd.dag import Vertex, VertexID, flatten_lists
+from dag_rider_amd.engine import Engine
+from dagutil import random_dag, with_irregular_edges, with_repeated_ids
+
+pytestmark = pytest.mark.gpu
+
+MODES = [(cm, dm) for cm in (L.DR_CHAIN_LITERAL, L.DR_CHAIN_PERSISTENT) for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER)]
+
+
+def _same(got, want, ids=True):
+    assert got.commit.tolist() == want.commit.tolist()
+    assert got.vcount.tolist() == want.vcount.tolist()
+    assert got.push_off.tolist() == want.push_off.tolist() and got.push_wave.tolist() == want.push_wave.tolist()
+    assert got.pop_count.tolist() == want.pop_count.tolist()
+    assert got.pop_digest.tolist() == want.pop_digest.tolist()
+    assert got.pop_edges.tolist() == want.pop_edges.tolist()
+    assert (got.commit_edges, got.deliver_edges) == (want.commit_edges, want.deliver_edges)
+    if ids:
+        assert got.ids.tolist() == want.ids.tolist()
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_irregular_edges_replay_path_order(gpu_device, seed):
+    rng = np.random.default_rng(5100 + seed)
+    n = int(rng.choice([4, 7, 12, 20, 70]))
+    R = int(rng.integers(8, 21))
+    base = random_dag(rng, n, R, p_present=rng.uniform(0.7, 1), p_s=rng.uniform(0.3, 0.9),
+                      p_w=rng.uniform(0, 0.6), max_depth=int(rng.integers(2, 7))).to_lists()
+    dag = with_irregular_edges(rng, base, p_irr=float(rng.uniform(0.05, 0.3)), up=bool(seed % 3))
+    if seed % 4 == 1:
+        dag = with_repeated_ids(rng, dag, p_dup=0.2)
+    f = int(rng.integers(0, (n - 1) // 3 + 2))
+    nw = R // 4
+    ld = oracle.LDag(arrays=flatten_lists(dag))
+    with Engine(n, f, R + 1, gpu_device) as e:
+        cut = int(rng.integers(1, R + 1))
+        e.append_lists(dag, 0, cut)
+        e.append_lists(dag, cut, R + 1)
+        for cm, dm in MODES:
+            want = ld.replay(f, nw, cm, dm, ids_cap=1 << 16)
+            assert want.rc == 0
+            _same(e.replay(nw, cm, dm, ids_cap=1 << 16), want)
+            _same(e.replay(nw, cm, dm), want, ids=False)
+        for w in range(1, nw + 1):
+            for dec in (0, max(0, w - 2)):
+                rc, vc, stack = ld.wave_ready(f, w, dec)
+                cm_, vc_, pushed = e.wave_ready(w, dec)
+                assert vc_ == vc and cm_ == (rc == 1)
+                if cm_:  # the pushed leaders, as waves
+                    assert pushed == [(r - 1) // 4 + 1 for r, _ in stack]
+        stack = [(int(rng.integers(0, R + 1)), int(rng.integers(1, n + 1))) for _ in range(3)]
+        for cur in (R, int(rng.integers(0, R + 1))):
+            for mode in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+                ids_, cnt_, dg_ = e.order_vertices(stack, cur, mode)
+                rc, want_ids, wc, wd = ld.order_vertices(stack, cur, mode)
+                assert rc == 0
+                assert ids_.tolist() == want_ids.tolist()
+                assert cnt_.tolist() == wc.tolist() and dg_.tolist() == wd.tolist()
+        allids = sorted({(v.id.round, v.id.source) for r in dag for v in r if v.id != VertexID(0, 0)})
+        samp = [allids[i] for i in rng.choice(len(allids), size=min(len(allids), 24), replace=False)]
+        pairs = [(a, b) for a in samp for b in samp]
+        for strong in (True, False):
+            got = e.path_batch(pairs, strong)
+            assert got.tolist() == [ld.path(a, b, strong) for a, b in pairs]
+        # reach sets: the bits of every id of rounds bottom..from
+        froms = samp[:5]
+        bottoms = [int(rng.integers(0, fr[0] + 1)) for fr in froms]
+        for strong in (True, False):
+            sets = e.reach_sets(froms, bottoms, strong)
+            for fr, bt, m in zip(froms, bottoms, sets):
+                for r in range(bt, fr[0] + 1):
+                    for s in range(1, n + 1):
+                        bit = int((int(m[(r - bt) * ((n + 63) // 64) + (s - 1) // 64]) >> ((s - 1) % 64)) & 1)
+                        assert bit == (1 if (r, s) == fr else ld.path(fr, (r, s), strong)), (fr, r, s, strong)
+
+
+def test_irregular_cycle_and_self_round(gpu_device):
+    """A two-vertex cycle across rounds and a same-round edge: path() follows them both
+    ways (the BFS's visited set ends the cycle), waveReady counts a voter that reaches
+    the leader only through an upward edge."""
+    g = [[Vertex(VertexID(0, s)) for s in (1, 2, 3, 4)]]
+    for r in range(1, 9):
+        g.append([Vertex(VertexID(r, s), b"", [VertexID(r - 1, t) for t in (1, 2, 3)], []) for s in (1, 2, 3, 4)])
+    # (4,4) --strong--> (6,2) (upward), (6,2) --weak--> (4,4): a cycle; (5,3) --strong--> (5,1) (same round)
+    g[4][3] = Vertex(VertexID(4, 4), b"", [VertexID(3, 1), VertexID(3, 2), VertexID(3, 3), VertexID(6, 2)], [])
+    g[6][1] = Vertex(VertexID(6, 2), b"", [VertexID(5, 1), VertexID(5, 2), VertexID(5, 3)], [VertexID(4, 4)])
+    g[5][2] = Vertex(VertexID(5, 3), b"", [VertexID(4, 1), VertexID(5, 1)], [])
+    ld = oracle.LDag(arrays=flatten_lists(g))
+    with Engine(4, 1, 9, gpu_device) as e:
+        e.append_lists(g)
+        ids = [(r, s) for r in range(9) for s in range(1, 5)]
+        pairs = [(a, b) for a in ids for b in ids]
+        for strong in (True, False):
+            assert e.path_batch(pairs, strong).tolist() == [ld.path(a, b, strong) for a, b in pairs]
+        for cm, dm in MODES:
+            _same(e.replay(2, cm, dm, ids_cap=1 << 12), ld.replay(1, 2, cm, dm, ids_cap=1 << 12))
+
+
+def test_irregular_vertex_through_buffer_admit(gpu_device):
+    """The buffer loop (process.go:200-234): a vertex whose strong edges skip a round is
+    admitted once its predecessors are present (dr_buffer_admit) and appended
+    (dr_append_vertices); every query then answers as the oracle does."""
+    rng = np.random.default_rng(17)
+    n, R = 6, 12
+    dag = random_dag(rng, n, R, p_present=1.0, p_s=0.8, p_w=0.3, ghosts=0.0).to_lists()
+    with Engine(n, 1, R + 4, gpu_device) as e:
+        e.append_lists(dag)
+        v1 = Vertex(VertexID(R + 1, 1), b"", [VertexID(R, t) for t in (1, 2, 3)], [])
+        e.append_vertices([v1])  # round R+1 opens (p.dag has a slot for it)
+        v = Vertex(VertexID(R + 1, 2), b"", [VertexID(R, 1), VertexID(R, 2), VertexID(R - 2, 3)],
+                   [VertexID(R, 4), VertexID(R - 5, 1)])
+        preds = [(u.round, u.source) for u in v.strong_edges + v.weak_edges]
+        admit = e.buffer_admit(R + 1, [((R + 1, 2), preds)])
+        assert admit.tolist() == [1]
+        e.append_vertices([v])  # not refused: the strong edge to R-2 and the weak one to R are kept
+        dag2 = [list(r) for r in dag] + [[v1, v]]
+        ld = oracle.LDag(arrays=flatten_lists(dag2))
+        ids = [(r, s) for r in range(R + 2) for s in range(1, n + 1)]
+        pairs = [((R + 1, 2), b) for b in ids]
+        for strong in (True, False):
+            assert e.path_batch(pairs, strong).tolist() == [ld.path(a, b, strong) for a, b in pairs]
+        for mode in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+            ids_, cnt_, dg_ = e.order_vertices([(R + 1, 2), (R - 3, 1)], R + 1, mode)
+            rc, want_ids, wc, wd = ld.order_vertices([(R + 1, 2), (R - 3, 1)], R + 1, mode)
+            assert rc == 0 and ids_.tolist() == want_ids.tolist() and dg_.tolist() == wd.tolist()

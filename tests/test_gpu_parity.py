@@ -8,7 +8,7 @@ import pytest
 
 import oracle
 from dag_rider_amd import _lib as L
-from dag_rider_amd.dag import pack_lists
+from dag_rider_amd.dag import flatten_lists, pack_lists
 from dag_rider_amd.engine import Engine
 from dag_rider_amd.gen import CONFIGS, generate
 from dagutil import figure1, random_dag
@@ -351,7 +351,13 @@ def test_errors(gpu_device):
     with Engine(4, 1, 8, gpu_device) as e:
         from dag_rider_amd.dag import Vertex, VertexID
         bad = [list(r) for r in dag]
-        bad[3][1] = Vertex(VertexID(3, 1), b"", [VertexID(1, 1)])  # strong edge skipping a round
+        bad[3][1] = Vertex(VertexID(3, 1), b"", [VertexID(9, 1)])  # a target past max_rounds: no id the mirror holds
         with pytest.raises(L.DrError) as ei:
             e.append_lists(bad)
         assert ei.value.code == L.DR_E_CONTRACT
+        ok = [list(r) for r in dag]
+        ok[3][1] = Vertex(VertexID(3, 1), b"", [VertexID(1, 1)])  # a strong edge skipping a round (App. A Q8): kept
+        e.append_lists(ok)
+        ld = oracle.LDag(arrays=flatten_lists(ok))
+        pairs = [((3, 1), (r, s)) for r in range(4) for s in range(1, 5)]
+        assert e.path_batch(pairs, True).tolist() == [ld.path(a, b, True) for a, b in pairs]
