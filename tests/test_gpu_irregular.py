@@ -82,6 +82,7 @@ def test_irregular_edges_replay_path_order(gpu_device, seed):
         for strong in (True, False):
             sets = e.reach_sets(froms, bottoms, strong)
             for fr, bt, m in zip(froms, bottoms, sets):
+                m = np.asarray(m).reshape(-1)
                 for r in range(bt, fr[0] + 1):
                     for s in range(1, n + 1):
                         bit = int((int(m[(r - bt) * ((n + 63) // 64) + (s - 1) // 64]) >> ((s - 1) % 64)) & 1)

@@ -202,11 +202,11 @@ def test_memo_on_off_large_n(gpu_device):
 
 
 @pytest.mark.parametrize("n,depth", [(1024, 64), (1024, 66), (1024, 80), (1024, 255), (1024, 256),
-                                     (1100, 63), (1100, 64), (1100, 66), (300, 150)])
+                                     (1100, 66), (1100, 127), (1100, 128), (300, 150)])
 def test_memo_window_boundary(gpu_device, n, depth):
     """Weak deltas across the memo window (engine.hip kMemoMaxDelta = 255 and the sweeps'
-    LDS ring: 256 rounds at row stride 16 (n=1024), 64 at stride 32 (n=1100), so the memo
-    applies up to 255 / 63; past it the full sweeps run): every mode, memo and device plan
+    LDS ring: 256 rounds at row stride 16 (n=1024), 128 at stride 32 (n=1100), so the memo
+    applies up to 255 / 127; past it the full sweeps run): every mode, memo and device plan
     on and off, == the bitset oracle, and the memo path really ran where it applies."""
     from dag_rider_amd.gen import small_config
 
@@ -230,7 +230,7 @@ def test_memo_window_boundary(gpu_device, n, depth):
                         got = e.replay(nw, cm, dm)
                         _compare_replay(got, want, ids=False)
                         assert got.chain_edges == want.chain_edges
-                        limit = 255 if n <= 1024 else 63
+                        limit = 255 if n <= 1024 else 127
                         assert (got.sweep["canon_segments"] >= 0) == (memo and depth <= limit), got.sweep
         e.set_memo(True)
         e.set_device_plan(True)
