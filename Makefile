@@ -35,16 +35,22 @@ $(BUILD)/wire.o: $(PKG)/csrc/wire.cpp include/dagrider_wire.h include/dagrider_g
 $(BUILD)/host_rounds.o: $(PKG)/csrc/host_rounds.cpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h | $(BUILD)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(BUILD)/engine.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/wave_ops.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp $(PKG)/csrc/batch1w.hpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h | $(BUILD)
+ENGINE_DEPS := $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/wave_ops.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp $(PKG)/csrc/batch1w.hpp $(PKG)/csrc/general.hpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h
+SHARD_DEPS  := $(PKG)/csrc/shard.hip $(PKG)/csrc/shard_memo.hpp $(PKG)/csrc/shard_fused.hpp $(PKG)/csrc/wave_ops.hpp include/dagrider_shard.h include/dagrider_gpu.h
+
+$(BUILD)/engine.o: $(ENGINE_DEPS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/engine_timing.o: $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/wave_ops.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp $(PKG)/csrc/batch1w.hpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h | $(BUILD)
+$(BUILD)/engine_timing.o: $(ENGINE_DEPS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DDR_SWEEP_TIMING -DDR_TUNING -c $< -o $@
 
-$(LIBT): $(BUILD)/engine_timing.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o
+$(BUILD)/shard_timing.o: $(SHARD_DEPS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DDR_SWEEP_TIMING -c $< -o $@
+
+$(LIBT): $(BUILD)/engine_timing.o $(BUILD)/shard_timing.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdagrider_gpu_timing.so
 
-$(BUILD)/shard.o: $(PKG)/csrc/shard.hip $(PKG)/csrc/shard_memo.hpp $(PKG)/csrc/wave_ops.hpp include/dagrider_shard.h include/dagrider_gpu.h | $(BUILD)
+$(BUILD)/shard.o: $(SHARD_DEPS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(BUILD)/engine.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o

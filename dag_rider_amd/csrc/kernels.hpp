@@ -106,17 +106,6 @@ __device__ __forceinline__ int dup_count(const DagView &g, int r, u64 xw) {
   return c;
 }
 
-// OR over the lanes of a row with equal (lane mod C), C a power of two < 16:
-// afterwards lane l of every row holds the OR of its row's class l mod C.
-template <int C>
-__device__ __forceinline__ u64 row_or_stride(u64 x) {
-  if constexpr (C <= 1) x |= dpp64<DPP_ROW_ROR + 1>(x);
-  if constexpr (C <= 2) x |= dpp64<DPP_ROW_ROR + 2>(x);
-  if constexpr (C <= 4) x |= dpp64<DPP_ROW_ROR + 4>(x);
-  if constexpr (C <= 8) x |= dpp64<DPP_ROW_ROR + 8>(x);
-  return x;
-}
-
 // Geometry per row stride: chunks are 16 B (two words) for WS >= 2, one word for WS == 1.
 template <int WS, int NT>
 struct Geo {

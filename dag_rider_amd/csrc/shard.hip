@@ -569,6 +569,8 @@ struct dr_shard {
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;                       // k_ms_wu beside k_ms_pass (fork / join events)
+  hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   hipEvent_t evs[5] = {};  // the memo replay's phase boundaries
   ncclComm_t comm = nullptr;
@@ -1223,6 +1225,43 @@ __global__ __launch_bounds__(256) void k_ms_vfinal(drs::MArgs a, drs::FArgs f, c
   }
 }
 
+// k_ms_pass at the context's row stride: 1024 threads, two 16-B chunks per
+// thread in flight (k_summary_commit's shipped WS = 16 geometry)
+// (k_ms_wu -- WU and the speculative digests, one workgroup per round, latency
+// bound -- runs beside it on the side stream: the pass keeps one 16-wave
+// workgroup per CU streaming rows, the small workgroups fill the other slots)
+template <int SP>
+hipError_t launch_pass_t(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
+  const int T = c->nrounds - 1, nl = c->nlocal;
+  const size_t lds = ((size_t)2 * nl * SP + c->W) * 8;
+  hipLaunchKernelGGL((drs::k_ms_pass<SP, 1024, 2>), dim3((T + 3) / 4), dim3(1024), lds, c->stream, a, f, nw, mode,
+                     c->mU.as<u64>(), S1);
+  return hipGetLastError();
+}
+hipError_t launch_pass(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
+  const int T = c->nrounds - 1;
+  const bool wu = T >= 1;
+  if (wu) {
+    const size_t lds = std::max<size_t>((size_t)c->nlocal * a.dd * c->SP * 8, 8);
+    if (hipError_t e = hipEventRecord(c->fork, c->stream)) return e;
+    if (hipError_t e = hipStreamWaitEvent(c->side, c->fork, 0)) return e;
+    hipLaunchKernelGGL((drs::k_ms_wu<256>), dim3(T), dim3(256), lds, c->side, a, f, c->mWU.as<u64>());
+    if (hipError_t e = hipGetLastError()) return e;
+    if (hipError_t e = hipEventRecord(c->join, c->side)) return e;
+  }
+  hipError_t e = hipErrorInvalidValue;
+  switch (c->SP) {
+    case 1: e = launch_pass_t<1>(c, a, f, nw, mode, S1); break;
+    case 2: e = launch_pass_t<2>(c, a, f, nw, mode, S1); break;
+    case 4: e = launch_pass_t<4>(c, a, f, nw, mode, S1); break;
+    case 8: e = launch_pass_t<8>(c, a, f, nw, mode, S1); break;
+    case 16: e = launch_pass_t<16>(c, a, f, nw, mode, S1); break;
+    case 32: e = launch_pass_t<32>(c, a, f, nw, mode, S1); break;
+  }
+  if (e == hipSuccess && wu) e = hipStreamWaitEvent(c->stream, c->join, 0);
+  return e;
+}
+
 int paper_emit(dr_shard *c, const drs::MArgs &a, const std::vector<drs::MQuery> &qs,
                const std::vector<drs::MState> &fin, const std::vector<int> &pop_query, std::vector<uint64_t> &qout,
                int npop);
@@ -1247,10 +1286,7 @@ int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int
   u64 *P1 = c->vote_p[1].as<u64>(), *P0 = c->vote_p[0].as<u64>();
   if (c->local) SHCHK(c, hipMemsetAsync(P1, 0, pw, c->stream));  // slots 1..G-1: the pass merges every local shard into slot 0
   {
-    const size_t lds = ((size_t)2 * nl * c->SP + W + (size_t)nl * a1.dd * c->SP) * 8;
-    hipLaunchKernelGGL((drs::k_ms_pass<512, 8>), dim3((T + 3) / 4), dim3(512), lds, c->stream, a1, f, nw,
-                       (int)drs::VOTE_STEP1, c->mU.as<u64>(), c->mWU.as<u64>(), c->local ? P1 : c->vote_send.as<u64>());
-    SHCHK(c, hipGetLastError());
+    SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP1, c->local ? P1 : c->vote_send.as<u64>()));
   }
   if (!c->local) {
     SHNCCL(c, ncclAllGather(c->vote_send.p, P1, (size_t)nw * W, ncclUint64, c->comm, c->stream));
@@ -1306,13 +1342,13 @@ int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int
   }
   hipLaunchKernelGGL(drs::k_ms_cstats, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a1, T, f.RD, f.CE);
   SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, (const u64 *)f.RD, f.Cc,
+  hipLaunchKernelGGL((drs::k_ms_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, (const u64 *)f.RD, f.Cc,
                      (const u64 *)f.CE, f.Ec);
   SHCHK(c, hipGetLastError());
   hipLaunchKernelGGL(drs::k_ms_rg, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a1, T, c->slot_off.as<uint32_t>(),
                      c->slot_src.as<uint16_t>(), (const u64 *)f.Cc, f.RG);
   SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
+  hipLaunchKernelGGL((drs::k_ms_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
                      (const u64 *)nullptr, (u64 *)nullptr);
   SHCHK(c, hipGetLastError());
   SHCHK(c, hipEventRecord(c->evs[2], c->stream));
@@ -1323,7 +1359,7 @@ int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int
   a.slot_src = c->slot_src.as<uint16_t>();
   a.push_out = m.push;
   hipLaunchKernelGGL((drs::k_ms_plan<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
-                     c->mst.as<drs::MState>(), (int)pcap);
+                     c->mst.as<drs::MState>(), (int)pcap, 0);
   SHCHK(c, hipGetLastError());
   SHCHK(c, hipMemsetAsync(c->mpend.p, 0, (size_t)nl * nq * c->depth * c->SP * 8, c->stream));
   int steps = 0;
@@ -1380,7 +1416,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   MOut m = carve_out(nullptr, nw, nq, pcap, npop);
   SHCHK(c, c->mout.ensure(m.bytes));
   m = carve_out(c->mout.as<char>(), nw, nq, pcap, npop);
-  SHCHK(c, hipMemsetAsync(m.hdr, 0, drs::FH_N * 4, c->stream));
+  if (!fused) SHCHK(c, hipMemsetAsync(m.hdr, 0, drs::FH_N * 4, c->stream));  // fused: the kernels write every slot
   drs::FArgs f{};
   f.ppref = c->ppref.as<u64>();
   f.SG = c->mSG.as<u64>();
@@ -1402,17 +1438,14 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   SHCHK(c, hipEventRecord(c->evs[0], c->stream));
   int steps = 0;
   if (fused) {
-    if (int rc = init_states(c, qs, nq, false)) return rc;  // the pop queries; chains are planned on the device
+    SHCHK(c, c->mq.ensure((size_t)std::max(nq, 1) * sizeof(drs::MQuery)));  // pops and chains: k_ms_plan
     drs::MArgs a = make_margs(c, nq);
     a.slot_off = c->slot_off.as<uint32_t>();
     a.slot_src = c->slot_src.as<uint16_t>();
     a.good = f.good;
     a.push_out = m.push;
     const int rb = (T + 1 + 3) / 4;
-    const size_t lds_pass = ((size_t)2 * nl * c->SP + W + (size_t)nl * dd * c->SP) * 8;
-    hipLaunchKernelGGL((drs::k_ms_pass<512, 8>), dim3((T + 3) / 4), dim3(512), lds_pass, c->stream, a, f, nw,
-                       (int)drs::VOTE_FULL, c->mU.as<u64>(), c->mWU.as<u64>(), (u64 *)nullptr);
-    SHCHK(c, hipGetLastError());
+    SHCHK(c, launch_pass(c, a, f, nw, drs::VOTE_FULL, (u64 *)nullptr));
     SHCHK(c, hipEventRecord(c->evs[1], c->stream));
     hipLaunchKernelGGL(drs::k_ms_kcand_full, dim3(rb), dim3(256), 0, c->stream, a, f);
     SHCHK(c, hipGetLastError());
@@ -1421,12 +1454,12 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     SHCHK(c, hipGetLastError());
     hipLaunchKernelGGL(drs::k_ms_rg_full, dim3(rb), dim3(256), 0, c->stream, a, f);
     SHCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(drs::k_ms_prefix, dim3(1), dim3(drs::MS_NT), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
+    hipLaunchKernelGGL((drs::k_ms_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
                        (const u64 *)f.CE, f.Ec);
     SHCHK(c, hipGetLastError());
     SHCHK(c, hipEventRecord(c->evs[2], c->stream));
     hipLaunchKernelGGL((drs::k_ms_plan<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
-                       (drs::MState *)nullptr, (int)pcap);
+                       (drs::MState *)nullptr, (int)pcap, 1);
     SHCHK(c, hipGetLastError());
     hipLaunchKernelGGL((drs::k_ms_sweep_full<256>), dim3(nq), dim3(256), lds_ring, c->stream, a, f);
     SHCHK(c, hipGetLastError());
@@ -1667,7 +1700,10 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
       hipEventCreateWithFlags(&c->evs[1], hipEventReleaseToDevice) != hipSuccess ||
       hipEventCreateWithFlags(&c->evs[2], hipEventReleaseToDevice) != hipSuccess ||
       hipEventCreateWithFlags(&c->evs[3], hipEventReleaseToDevice) != hipSuccess ||
-      hipEventCreateWithFlags(&c->evs[4], hipEventReleaseToDevice) != hipSuccess) {
+      hipEventCreateWithFlags(&c->evs[4], hipEventReleaseToDevice) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) {
     g_shard_err = "dr_shard_create: stream/event creation failed";
     dr_shard_destroy(c);
     return DR_E_HIP;
@@ -1722,8 +1758,9 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
                   &c->errf, &c->push_out, &c->push_n, &c->cedges, &c->vote_s0, &c->vote_p[0], &c->vote_p[1],
                   &c->vote_send, &c->vcount, &c->D, &c->pcnt, &c->qcnt, &c->qedges, &c->qdig})
     b->release();
-  for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->evs[0], c->evs[1], c->evs[2], c->evs[3], c->evs[4]})
+  for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->evs[0], c->evs[1], c->evs[2], c->evs[3], c->evs[4], c->fork, c->join})
     if (ev) (void)hipEventDestroy(ev);
+  if (c->side) (void)hipStreamDestroy(c->side);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -2128,3 +2165,15 @@ extern "C" int dr_shard_stats(const dr_shard *c, float *ms, uint64_t *rounds, ui
   if (exchange_bytes) *exchange_bytes = c->last_xbytes;
   return DR_OK;
 }
+
+#ifdef DR_SWEEP_TIMING
+// profiling build only: the per-query ticks of the last k_ms_sweep_full
+// (shard_fused.hpp g_ms_timing; 8 u64 per query, wall-clock ticks)
+extern "C" int dr_debug_ms_timing(uint64_t *out, int nq) {
+  if (nq < 0 || nq > drs::kMsTimingQ) return DR_E_INVAL;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(drs::g_ms_timing), (size_t)nq * 64, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? DR_OK
+             : DR_E_HIP;
+}
+#endif

@@ -2,11 +2,12 @@
 // (dr_shard_replay, include/dagrider_shard.h) that read every
 // column a context holds in one workgroup.
 //
+//   k_ms_wu          one workgroup per round: WU_r (from the weak-column keys)
+//                    and the round's speculative canonical digest.
 //   k_ms_pass        one workgroup per wave (rounds 4w-3 .. 4w): streams every
 //                    local shard's columns of the wave's strong rows once and
-//                    builds, from that one read, U_r (per shard), WU_r (from the
-//                    weak-column keys), the speculative canonical digest of each
-//                    round, and waveReady's vote (process.go:326-339).  When the
+//                    builds, from that one read, U_r (per shard) and waveReady's
+//                    vote (process.go:326-339).  When the
 //                    context holds every column (local mode, a one-rank group:
 //                    "fused") the vote is complete: S_1..S_3, vcount, commit.
 //                    Otherwise (one rank of G > 1) the pass writes this shard's
@@ -37,6 +38,17 @@
 #include "wave_ops.hpp"
 
 namespace drs {
+
+#ifdef DR_SWEEP_TIMING
+// profiling build only (libdagrider_gpu_timing.so, tools/ms_timing.py): per
+// query of k_ms_sweep_full, wall-clock ticks at start / end, rounds wave 0
+// applied alone, workgroup rounds, ticks inside workgroup rounds, type, top, stop
+constexpr int kMsTimingQ = 8192;
+__device__ u64 g_ms_timing[8 * kMsTimingQ];
+#define DR_MT(...) __VA_ARGS__
+#else
+#define DR_MT(...)
+#endif
 
 enum : int { VOTE_FULL = 1, VOTE_STEP1 = 2 };
 
@@ -82,38 +94,31 @@ __device__ __forceinline__ int64_t fblock_scan(int64_t v, int64_t *s, int64_t &t
 }
 
 // ---------------------------------------------------------------------------
-// k_ms_pass (see the file comment).  Dynamic LDS: sU[NL*SP] | Sp[NL*SP] |
-// Tn[W] | sWU[NL*dd*SP].  Thread t owns chunk column (t mod CPR) of every
-// shard-round (NT is a multiple of CPR), so its OR accumulator holds fixed
-// columns; the rows of the local shards are streamed as one sequence of
-// (shard, pass) elements, GRP 16-B loads in flight.
+// k_ms_wu: one workgroup per round r >= 1: WU_r of every local shard from the
+// round's weak-column keys (LDS atomics, then every word written, zeros
+// included), and wave 0 the speculative canonical digest SG_r (every present
+// vertex of the round delivered in slot order at positions from ppref[r-1]).
+// Dynamic LDS: sWU[NL*dd*SP].  It reads no strong row, so it is kept out of
+// k_ms_pass, whose row stream it would stall at every round.
 // ---------------------------------------------------------------------------
-template <int NT, int GRP>
-__global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int vote_mode, u64 *__restrict__ U,
-                                                u64 *__restrict__ WU, u64 *__restrict__ S1out) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_wu(MArgs a, FArgs f, u64 *__restrict__ WU) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
-  const int NL = a.nlocal, SP = a.SP, W = a.W, WSs = a.WSs, n = a.n, dd = a.dd, T = a.T;
-  u64 *sU = lds, *Sp = lds + NL * SP, *Tn = Sp + NL * SP, *sWU = Tn + W;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int w = blockIdx.x + 1, r1 = 4 * (w - 1) + 1;
-  const int nr = min(T, r1 + 3) - r1 + 1;
-  const bool do_commit = w <= nwc;
-  const int L = do_commit ? (w < a.nlead ? (int)a.lead[w] : 1) - 1 : 0;
-  const bool leader = do_commit && ((a.pres[(size_t)r1 * W + (L >> 6)] >> (L & 63)) & 1ULL);
-  const int CW = SP >= 2 ? 2 : 1, CPR = SP / CW, CPS = n * CPR, JP = (CPS + NT - 1) / NT, J = NL * JP;
-  const int col = (tid % CPR) * CW;
-  for (int i = tid; i < NL * SP; i += NT) {
-    sU[i] = 0;
-    const int l = i / SP, c = i % SP, gw = (a.shard0 + l) * WSs + c;
-    Sp[i] = (c < WSs && gw == (L >> 6)) ? 1ULL << (L & 63) : 0ULL;
-  }
-  for (int i = tid; i < W; i += NT) Tn[i] = 0;
+  const int NL = a.nlocal, SP = a.SP, dd = a.dd;
+  u64 *sWU = lds;
+  const int r = blockIdx.x + 1, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < NL * dd * SP; i += NT) sWU[i] = 0;
-  // speculative canonical digest of round r1 + wid: every present vertex of the
-  // round delivered in slot order at positions from ppref[r-1]
-  if (wid < nr) {
+  __syncthreads();
+  for (int l = 0; l < NL; l++) {  // every key has a source
+    const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
+    for (uint64_t jj = c0 + tid; jj < c1; jj += NT) {
+      const uint32_t key = a.wck[jj];
+      const int d = (int)(key >> 11) - 2, tc = (int)(key & 2047u);
+      atomicOr(&sWU[((size_t)l * dd + d) * SP + (tc >> 6)], 1ULL << (tc & 63));
+    }
+  }
+  if (wid == 0) {
     constexpr int SPT = 8;
-    const int r = r1 + wid;
     const uint32_t sa = a.slot_off[r], sb = a.slot_off[r + 1];
     u64 pos = f.ppref[r - 1], dg = 0;
     for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPT) {
@@ -121,9 +126,9 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
       uint32_t src[SPT];
       uint32_t cnt = 0;
 #pragma unroll
-      for (int j = 0; j < SPT; j++) {
-        src[j] = i0 + j < sb ? a.slot_src[i0 + j] : 0u;
-        cnt += src[j] != 0;
+      for (int q = 0; q < SPT; q++) {
+        src[q] = i0 + q < sb ? a.slot_src[i0 + q] : 0u;
+        cnt += src[q] != 0;
       }
       uint32_t inc = cnt;
 #pragma unroll
@@ -133,78 +138,117 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
       }
       u64 k = pos + (inc - cnt);
 #pragma unroll
-      for (int j = 0; j < SPT; j++)
-        if (src[j]) dg += dr::digest_term((uint32_t)r, src[j], k++);
+      for (int q = 0; q < SPT; q++)
+        if (src[q]) dg += dr::digest_term((uint32_t)r, src[q], k++);
       pos += __shfl(inc, 63);
     }
     dg = dr::wave_sum(dg);
     if (lane == 0) f.SG[r] = dg;
   }
   __syncthreads();
+  for (int i = tid; i < NL * dd * SP; i += NT) {
+    const int l = i / (dd * SP), rest = i - l * dd * SP;
+    WU[((size_t)l * a.R + r) * dd * SP + rest] = sWU[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_ms_pass (see the file comment).  Dynamic LDS: sU[NL*SP] | Sp[NL*SP] |
+// Tn[W].  SP (the row stride) is a template parameter, so the
+// chunk geometry is static: thread t owns 16-B chunk column j = t mod CPR of
+// rows t / CPR + p * RPP of every local shard, and its OR accumulator holds that
+// column.  A round is NL * CPT (shard, pass) elements per thread, loaded GR at a
+// time (nontemporal: each row is read once); a shard's U column is reduced when
+// its last pass is consumed (the pass index is uniform over the workgroup).
+// ---------------------------------------------------------------------------
+template <int SP, int NT, int GR>
+__global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int vote_mode, u64 *__restrict__ U,
+                                                u64 *__restrict__ S1out) {
+  constexpr int CW = SP >= 2 ? 2 : 1, CPR = SP / CW, RPP = NT / CPR;
+  static_assert(NT % 64 == 0 && NT % CPR == 0 && CPR <= 16, "block must tile rows");
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  const int NL = a.nlocal, W = a.W, WSs = a.WSs, n = a.n, T = a.T;
+  u64 *sU = lds, *Sp = lds + NL * SP, *Tn = Sp + NL * SP;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, j = tid % CPR, row0 = tid / CPR;
+  const int w = blockIdx.x + 1, r1 = 4 * (w - 1) + 1;
+  const int nr = min(T, r1 + 3) - r1 + 1;
+  const bool do_commit = w <= nwc;
+  const int L = do_commit ? (w < a.nlead ? (int)a.lead[w] : 1) - 1 : 0;
+  const bool leader = do_commit && ((a.pres[(size_t)r1 * W + (L >> 6)] >> (L & 63)) & 1ULL);
+  const int CPT = (n + RPP - 1) / RPP, E = NL * CPT;
+  for (int i = tid; i < NL * SP; i += NT) {
+    sU[i] = 0;
+    const int l = i / SP, c = i % SP, gw = (a.shard0 + l) * WSs + c;
+    Sp[i] = (c < WSs && gw == (L >> 6)) ? 1ULL << (L & 63) : 0ULL;
+  }
+  for (int i = tid; i < W; i += NT) Tn[i] = 0;
+  __syncthreads();
   for (int k = 0; k < nr; k++) {
     const int r = r1 + k;
     const bool test = leader && k >= 1 && (vote_mode == VOTE_FULL || k == 1);
-    // the round's weak targets per shard and delta (every key has a source)
-    for (int l = 0; l < NL; l++) {
-      const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
-      for (uint64_t j = c0 + tid; j < c1; j += NT) {
-        const uint32_t key = a.wck[j];
-        const int d = (int)(key >> 11) - 2, tc = (int)(key & 2047u);
-        atomicOr(&sWU[((size_t)l * dd + d) * SP + (tc >> 6)], 1ULL << (tc & 63));
-      }
-    }
+    const u64 *rbase = a.strong + (size_t)r * n * SP + (size_t)row0 * SP + j * CW;
     u64 a0 = 0, a1 = 0;
-    for (int j0 = 0; j0 < J; j0 += GRP) {
-      u64 x0[GRP], x1[GRP];
+    for (int e0 = 0; e0 < E; e0 += GR) {
+      u64 x0[GR], x1[GR];
+      {
+        int l = e0 / CPT, p = e0 - l * CPT;
 #pragma unroll
-      for (int p = 0; p < GRP; p++) {
-        const int j = j0 + p, l = j / JP, i = j - l * JP, c = tid + i * NT;
-        x0[p] = 0;
-        x1[p] = 0;
-        if (j < J && c < CPS) {
-          const u64 *base = a.strong + (size_t)l * a.strong_stride + (size_t)r * n * SP + (size_t)c * CW;
-          if (CW == 2) {
-            const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(base));
-            x0[p] = v.x;
-            x1[p] = v.y;
-          } else {
-            x0[p] = __builtin_nontemporal_load(base);
+        for (int q = 0; q < GR; q++) {
+          x0[q] = 0;
+          x1[q] = 0;
+          const int s = row0 + p * RPP;
+          if (e0 + q < E && s < n) {
+            const u64 *src = rbase + (size_t)l * a.strong_stride + (size_t)p * RPP * SP;
+            if constexpr (CW == 2) {
+              const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(src));
+              x0[q] = v.x;
+              x1[q] = v.y;
+            } else {
+              x0[q] = __builtin_nontemporal_load(src);
+            }
+          }
+          if (++p == CPT) {
+            p = 0;
+            l++;
           }
         }
       }
+      int l = e0 / CPT, p = e0 - l * CPT;
 #pragma unroll
-      for (int p = 0; p < GRP; p++) {
-        const int j = j0 + p;
-        if (j >= J) break;  // uniform
-        const int l = j / JP, i = j - l * JP;
-        a0 |= x0[p];
-        a1 |= x1[p];
+      for (int q = 0; q < GR; q++) {
+        if (e0 + q >= E) break;  // uniform
+        a0 |= x0[q];
+        a1 |= x1[q];
         if (test) {  // rows of round r reaching S_{k-1} on this shard's columns
-          const u64 s0 = Sp[l * SP + col], s1 = CW == 2 ? Sp[l * SP + col + 1] : 0ULL;
-          const bool hit = ((x0[p] & s0) | (x1[p] & s1)) != 0ULL;
-          u64 m = __ballot(hit);
-          const int cb = wid * 64 + i * NT;  // the wave's first chunk
-          if (lane == 0 && m && cb < CPS) {
-            const int rowbase = cb / CPR;
+          const u64 s0 = Sp[l * SP + j * CW], s1 = CW == 2 ? Sp[l * SP + j * CW + 1] : 0ULL;
+          u64 m = __ballot(((x0[q] & s0) | (x1[q] & s1)) != 0ULL);
+          const int rowbase = (wid * 64) / CPR + p * RPP;  // the wave's first row
+          if (lane == 0 && m && rowbase < n) {
             u64 bits = m;
-            if (CPR > 1) {
+            if constexpr (CPR > 1) {
+#pragma unroll
               for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
               bits = 0;
+#pragma unroll
               for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
             }
             atomicOr(&Tn[rowbase >> 6], bits << (rowbase & 63));
           }
         }
-        if (i == JP - 1) {  // the shard's columns of round r are done: U
-          for (int off = CPR; off < 64; off <<= 1) {
-            a0 |= shfl_xor64(a0, off);
-            if (CW == 2) a1 |= shfl_xor64(a1, off);
+        if (p == CPT - 1) {  // the shard's columns of round r are done: U
+          if constexpr (CPR < 16) {
+            a0 = dr::row_or_stride<CPR>(a0);
+            if constexpr (CW == 2) a1 = dr::row_or_stride<CPR>(a1);
           }
-          if (lane < CPR) {
-            if (a0) atomicOr(&sU[l * SP + lane * CW], a0);
-            if (CW == 2 && a1) atomicOr(&sU[l * SP + lane * CW + 1], a1);
+          if ((lane & 15) < CPR) {
+            if (a0) atomicOr(&sU[l * SP + (lane & 15) * CW], a0);
+            if (CW == 2 && a1) atomicOr(&sU[l * SP + (lane & 15) * CW + 1], a1);
           }
           a0 = a1 = 0;
+        }
+        if (++p == CPT) {
+          p = 0;
+          l++;
         }
       }
     }
@@ -213,11 +257,6 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
       const int l = i / SP, c = i % SP;
       U[((size_t)l * a.R + r) * SP + c] = sU[i];
       sU[i] = 0;
-    }
-    for (int i = tid; i < NL * dd * SP; i += NT) {
-      const int l = i / (dd * SP), rest = i - l * dd * SP;
-      WU[((size_t)l * a.R + r) * dd * SP + rest] = sWU[i];
-      sWU[i] = 0;
     }
     if (test) {  // S_k: the sources of round r that reach S_{k-1} (this context's shards' columns of it)
       for (int i = tid; i < W; i += NT) {
@@ -280,39 +319,71 @@ __global__ __launch_bounds__(256) void k_ms_kcand_full(MArgs a, FArgs f) {
 // Full-width expansion of a partial round r of a query held by one workgroup:
 // the frontier FE's strong rows (every local shard's columns) -> ring slot of
 // r-1, and (weak) its weak columns -> the ring slots of their target rounds
-// (>= bottom).  Saturation per shard as in k_ms_step: once the OR of the rows a
-// wave has read equals the shard's U_r, no further row adds a bit.  Every
-// thread calls it; ring / FE are LDS (W words per round slot).
+// (>= bottom).  Saturation as in k_ms_step: once the OR of the rows a wave has
+// read equals U_r, no further row adds a bit.  Every thread calls it; ring / FE
+// are LDS (W words per round slot).
+//
+// The local shards' row pieces are read as one row of WP = nlocal * SP words:
+// the 64 rows of frontier word w are 64 * WP words, lane k's i-th load is
+// element k + 64 i (row (k + 64 i) / WP, word (k mod WP)), so with WP dividing
+// 64 a lane always accumulates the same word of the concatenated row, whatever
+// the shard count, and every load of a frontier word is issued before its
+// saturation check.  Other shard counts take the per-shard loop.
 template <int NT>
 __device__ __forceinline__ void expand_partial_full(const MArgs &a, int r, int bottom, const u64 *FE, u64 *ring,
                                                     int dm, bool weak) {
   constexpr int NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int SP = a.SP, W = a.W, WSs = a.WSs;
+  const int SP = a.SP, W = a.W, WSs = a.WSs, NL = a.nlocal, WP = NL * SP;
   u64 *dst = ring + (size_t)((r - 1) & dm) * W;
-  for (int l = 0; l < a.nlocal; l++) {
-    const u64 *rows = a.strong + (size_t)l * a.strong_stride + (size_t)r * a.n * SP;
-    const u64 ur = lane < SP ? a.U[((size_t)l * a.R + r) * SP + lane] : 0ULL;
+  if (WP <= 64 && (64 % WP) == 0) {
+    const int l0 = (lane % WP) / SP, c0 = lane % SP;  // this lane's word of the concatenated row
+    const u64 *base = a.strong + (size_t)l0 * a.strong_stride + (size_t)r * a.n * SP + c0;
+    const u64 ur = lane < WP ? a.U[((size_t)l0 * a.R + r) * SP + c0] : 0ULL;
+    const int RPL = 64 / WP;  // rows per load instruction
     u64 acc = 0;
     for (int w = wv; w < W; w += NW) {
       const u64 bits = FE[w];
       if (!bits) continue;
-      const u64 *blk = rows + (size_t)w * 64 * SP;
-      for (int i = 0; i < SP; i++) {
-        const int k = lane + 64 * i;
-        if ((bits >> (k / SP)) & 1ULL) acc |= blk[k];
+      const int rb = w * 64;
+      for (int i = 0; i < WP; i++) {
+        const int row = i * RPL + lane / WP;
+        if ((bits >> row) & 1ULL) acc |= base[(size_t)(rb + row) * SP];
       }
       u64 red = acc;
-      for (int off = SP; off < 64; off <<= 1) red |= shfl_xor64(red, off);
-      if (__ballot(lane < SP && red != ur) == 0ULL) break;
+      for (int off = WP; off < 64; off <<= 1) red |= shfl_xor64(red, off);
+      if (__ballot(lane < WP && red != ur) == 0ULL) break;
     }
-    for (int off = SP; off < 64; off <<= 1) acc |= shfl_xor64(acc, off);
-    if (lane < SP && lane < WSs && acc) atomicOr(&dst[l * WSs + lane], acc);
+    for (int off = WP; off < 64; off <<= 1) acc |= shfl_xor64(acc, off);
+    if (lane < WP && c0 < WSs && acc) atomicOr(&dst[l0 * WSs + c0], acc);
+  } else {
+    for (int l = 0; l < NL; l++) {
+      const u64 *rows = a.strong + (size_t)l * a.strong_stride + (size_t)r * a.n * SP;
+      const u64 ur = lane < SP ? a.U[((size_t)l * a.R + r) * SP + lane] : 0ULL;
+      u64 acc = 0;
+      for (int w = wv; w < W; w += NW) {
+        const u64 bits = FE[w];
+        if (!bits) continue;
+        const u64 *blk = rows + (size_t)w * 64 * SP;
+        for (int i = 0; i < SP; i++) {
+          const int k = lane + 64 * i;
+          if ((bits >> (k / SP)) & 1ULL) acc |= blk[k];
+        }
+        u64 red = acc;
+        for (int off = SP; off < 64; off <<= 1) red |= shfl_xor64(red, off);
+        if (__ballot(lane < SP && red != ur) == 0ULL) break;
+      }
+      for (int off = SP; off < 64; off <<= 1) acc |= shfl_xor64(acc, off);
+      if (lane < SP && lane < WSs && acc) atomicOr(&dst[l * WSs + lane], acc);
+    }
   }
   if (!weak) return;
-  for (int l = 0; l < a.nlocal; l++) {
+  // weak columns: one wave per local shard when there are as many shards as
+  // waves (their offsets load in parallel), else every thread on each shard
+  const bool per_wave = NL >= NW;
+  for (int l = per_wave ? wv : 0; l < NL; l += per_wave ? NW : 1) {
     const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
-    for (uint64_t jj = c0 + tid; jj < c1; jj += NT) {
+    for (uint64_t jj = c0 + (per_wave ? lane : tid); jj < c1; jj += per_wave ? 64 : NT) {
       const u64 *row = a.wcr + jj * W;
       u64 hit = 0;
       for (int w = 0; w < W; w++) hit |= row[w] & FE[w];
@@ -391,15 +462,17 @@ __global__ __launch_bounds__(NT) void k_ms_canon_full(MArgs a, FArgs f) {
     }
     __syncthreads();
     int run = 0, r = b;
+    const bool act = lane < W;
+    u64 p_nx = (wv == 0 && act) ? a.pres[(size_t)r * W + lane] : 0ULL;  // round r-1's, loaded while r expands
     for (;; --r) {
       if (wv == 0) {
-        const bool act = lane < W;
-        u64 fw = 0, p = 0;
+        u64 fw = 0;
+        const u64 p = p_nx;
         if (act) {
           u64 *slot = &ring[(size_t)(r & dm) * W + lane];
           fw = *slot;
           *slot = 0;
-          p = a.pres[(size_t)r * W + lane];
+          if (r >= 1) p_nx = a.pres[(size_t)(r - 1) * W + lane];
           a.K[(size_t)r * W + lane] = fw;
           FE[lane] = fw & p;
         }
@@ -485,10 +558,43 @@ __global__ __launch_bounds__(256) void k_ms_rg_full(MArgs a, FArgs f) {
 // ---------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__restrict__ q, MState *__restrict__ st0,
-                                                int push_cap) {
+                                                int push_cap, int make_pops) {
   __shared__ int64_t s_scan[NT / 64];
   const int nw = f.nw, tid = threadIdx.x;
   const int per = (nw + NT - 1) / NT, wa = 1 + tid * per, wb = min(nw + 1, wa + per);
+  if (make_pops) {
+    // the pop queries (one per wave whose leader is present, in wave order; mask
+    // rows top..0 each), as the host lists them: no upload before the sweeps
+    auto leader_present = [&](int w, int &L) {
+      const int r1 = 4 * (w - 1) + 1;
+      L = (w < a.nlead ? (int)a.lead[w] : 1) - 1;
+      return ((a.pres[(size_t)r1 * a.W + (L >> 6)] >> (L & 63)) & 1ULL) != 0ULL;
+    };
+    int64_t pc = 0, pm = 0;
+    for (int w = wa; w < wb; w++) {
+      int L;
+      if (leader_present(w, L)) {
+        pc++;
+        pm += (int64_t)(4 * (w - 1) + 2) * a.W;
+      }
+    }
+    int64_t t0, t1;
+    int64_t pi = fblock_scan<NT>(pc, s_scan, t0, 0);
+    int64_t mo = fblock_scan<NT>(pm, s_scan, t1, 0);
+    for (int w = wa; w < wb; w++) {
+      int L;
+      if (leader_present(w, L)) {
+        MQuery x{};
+        x.type = MQ_POP;
+        x.top = 4 * (w - 1) + 1;
+        x.bottom = 0;
+        x.src0 = L;
+        x.mask_off = mo;
+        q[pi++] = x;
+        mo += (int64_t)(x.top + 1) * a.W;
+      }
+    }
+  }
   // floors: exclusive prefix max of (commit ? w : 0)
   int64_t m = 0;
   for (int w = wa; w < wb; w++)
@@ -546,21 +652,46 @@ __global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__rest
   if (tid == 0) {
     f.hdr[FH_NCHAIN] = (int32_t)ctot;
     f.hdr[FH_PUSHES] = (int32_t)min<int64_t>(ptot, INT32_MAX);
-    if (ptot > push_cap) f.hdr[FH_ERR] = 1;
+    f.hdr[FH_ERR] = ptot > push_cap ? 1 : 0;
   }
+}
+
+// Per-round words of lane w < W (global word w = shard w / WSs, column w mod
+// WSs) that do not depend on the frontier, loaded one round ahead by wave 0:
+// presence, canonical row, U and the first FDD weak-summary slots.
+constexpr int FDD = 3;
+struct FRound {
+  u64 P, K, U, WU[FDD];
+};
+__device__ __forceinline__ void fload_round(const MArgs &a, int r, bool pop, int w, FRound &x) {
+  const int l = w / a.WSs, cw = w - l * a.WSs;
+  const size_t ub = (size_t)l * a.R + r;
+  x.P = a.pres[(size_t)r * a.W + w];
+  x.K = pop ? a.K[(size_t)r * a.W + w] : 0ULL;
+  x.U = a.U[ub * a.SP + cw];
+#pragma unroll
+  for (int d = 0; d < FDD; d++) x.WU[d] = (pop && d < a.dd) ? a.WU[(ub * a.dd + d) * a.SP + cw] : 0ULL;
 }
 
 // ---------------------------------------------------------------------------
 // k_ms_sweep_full: one workgroup per query, every round to its end (the same
 // decisions as k_ms_step, shard_memo.hpp).  Grid npop + nw: workgroups past the
 // planned chains exit.  Dynamic LDS: ring[depth*W] | FE[W].
+//
+// Wave 0 decides each round from words it loaded one round ahead and applies,
+// without a workgroup barrier, every round it can expand alone: a full round
+// (ring |= U_r, WU_r from the prefetched words), a round whose frontier is one
+// vertex (the query's top, a chain's restart: that row and its weak columns)
+// and an empty one.  Only a partial round with several vertices is expanded by
+// the whole workgroup (expand_partial_full).
 // ---------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   const int qi = blockIdx.x;
+  DR_MT(const u64 tt0 = wall_clock64(); u64 tt_wg = 0, n_w0 = 0, n_wg = 0;)
   if (qi >= f.npop + f.hdr[FH_NCHAIN]) return;
-  const int W = a.W, dm = a.depth - 1;
+  const int W = a.W, dm = a.depth - 1, WSs = a.WSs;
   u64 *ring = lds, *FE = lds + (size_t)a.depth * W;
   __shared__ int s_ctl[2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -574,72 +705,119 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
   u64 edges = 0;
   int r = Q.top;
   bool merged = false;
-  for (;; --r) {
+  const bool act = lane < W;
+  FRound cur{}, nxt{};
+  if (wv == 0 && act) fload_round(a, r, pop, lane, cur);
+  for (;;) {
     if (wv == 0) {
-      const bool act = lane < W;
-      u64 fw = 0, p = 0;
-      if (act) {
-        u64 *slot = &ring[(size_t)(r & dm) * W + lane];
-        fw = *slot;
-        *slot = 0;
-        p = a.pres[(size_t)r * W + lane];
-      }
-      // waveReady's chain (process.go:342-350): a reachable, present leader of
-      // wave wvv is pushed and the chain goes on from it alone
-      bool restart = false;
-      int wvv = 0;
-      if (!pop && r < Q.top && ((r - 1) & 3) == 0) {
-        wvv = ((r - 1) >> 2) + 1;
-        const int L = (wvv < a.nlead ? (int)a.lead[wvv] : 1) - 1;
-        const u64 fl = __shfl(fw & p, L >> 6);
-        if ((fl >> (L & 63)) & 1ULL) {
-          fw = lane == (L >> 6) ? 1ULL << (L & 63) : 0ULL;
-          restart = true;
+      for (;;) {
+        if (act && r >= 1) fload_round(a, r - 1, pop, lane, nxt);
+        u64 fw = 0;
+        const u64 p = cur.P;
+        if (act) {
+          u64 *slot = &ring[(size_t)(r & dm) * W + lane];
+          fw = *slot;
+          *slot = 0;
         }
-      }
-      const u64 fe = fw & p;
-      const bool nz = __ballot(act && fw != 0ULL) != 0ULL;
-      const bool full = __ballot(act && fe != p) == 0ULL;
-      if (nz) low = min(low, r - 1);
-      bool done;
-      if (pop) {
-        const u64 k = act ? a.K[(size_t)r * W + lane] : 0ULL;
-        run = __ballot(act && fw != k) == 0ULL ? run + 1 : 0;
-        merged = run >= a.dmax;
-        done = merged || r <= Q.bottom || (!nz && low >= r);
-        if (act) a.masks[Q.mask_off + (int64_t)(Q.top - r) * W + lane] = fw;
-      } else {
-        done = r <= Q.bottom || (!nz && low >= r);
-      }
-      const bool summary = !done && full;
-      if (!pop && !done) {
-        if (summary) {
-          edges += a.sdr[r];
+        int single = r == Q.top ? Q.src0 : -1;  // a round whose frontier is one known vertex
+        // waveReady's chain (process.go:342-350): a reachable, present leader of
+        // wave wvv is pushed and the chain goes on from it alone
+        if (!pop && r < Q.top && ((r - 1) & 3) == 0) {
+          const int wvv = ((r - 1) >> 2) + 1;
+          const int L = (wvv < a.nlead ? (int)a.lead[wvv] : 1) - 1;
+          const u64 fl = __shfl(fw & p, L >> 6);
+          if ((fl >> (L & 63)) & 1ULL) {
+            fw = lane == (L >> 6) ? 1ULL << (L & 63) : 0ULL;
+            if (lane == 0) a.push_out[Q.push_base + npush] = wvv;
+            npush++;
+            single = L;
+          }
+        }
+        const u64 fe = fw & p;
+        const bool nz = __ballot(act && fw != 0ULL) != 0ULL;
+        const bool anyfe = __ballot(act && fe != 0ULL) != 0ULL;
+        const bool full = __ballot(act && fe != p) == 0ULL;
+        if (nz) low = min(low, r - 1);
+        bool done;
+        if (pop) {
+          run = __ballot(act && fw != cur.K) == 0ULL ? run + 1 : 0;
+          merged = run >= a.dmax;
+          done = merged || r <= Q.bottom || (!nz && low >= r);
+          if (act) a.masks[Q.mask_off + (int64_t)(Q.top - r) * W + lane] = fw;
         } else {
-          u64 e = 0;
-          for (u64 x = act ? fe : 0ULL; x; x &= x - 1) e += a.sdeg[(size_t)r * a.n + lane * 64 + __builtin_ctzll(x)];
-          edges += dr::wave_sum(e);
+          done = r <= Q.bottom || (!nz && low >= r);
         }
-      }
-      if (!done && pop && __ballot(act && fe != 0ULL) != 0ULL) low = min(low, r - a.dmax);
-      if (restart) {
-        if (lane == 0) a.push_out[Q.push_base + npush] = wvv;
-        npush++;
-      }
-      if (act) FE[lane] = fe;
-      if (lane == 0) {
-        s_ctl[0] = done;
-        s_ctl[1] = summary;
+        const bool summary = !done && full;
+        if (!pop && !done) {
+          if (summary) {
+            edges += a.sdr[r];
+          } else {
+            u64 e = 0;
+            for (u64 x = act ? fe : 0ULL; x; x &= x - 1) e += a.sdeg[(size_t)r * a.n + lane * 64 + __builtin_ctzll(x)];
+            edges += dr::wave_sum(e);
+          }
+        }
+        if (!done && pop && anyfe) low = min(low, r - a.dmax);
+        if (done) {
+          if (lane == 0) {
+            s_ctl[0] = 1;
+            s_ctl[1] = r;
+          }
+          break;
+        }
+        if (summary) {  // ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d]
+          if (act) {
+            ring[(size_t)((r - 1) & dm) * W + lane] |= cur.U;
+            if (weak) {
+              const int l = lane / WSs, cw = lane - l * WSs;
+              for (int d = 0; d < a.dd; d++) {
+                const int tr = r - d - 2;
+                if (tr < Q.bottom) break;
+                ring[(size_t)(tr & dm) * W + lane] |=
+                    d < FDD ? cur.WU[d] : a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw];
+              }
+            }
+          }
+        } else if (anyfe && single >= 0 && ((__shfl(fe, single >> 6) >> (single & 63)) & 1ULL)) {
+          // FE = {single}: its row (every local shard's piece) and its weak columns
+          if (act) {
+            const int l = lane / WSs, cw = lane - l * WSs;
+            ring[(size_t)((r - 1) & dm) * W + lane] |=
+                a.strong[(size_t)l * a.strong_stride + ((size_t)r * a.n + single) * a.SP + cw];
+          }
+          if (weak)
+            for (int l = 0; l < a.nlocal; l++) {
+              const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
+              for (uint64_t jj = c0 + lane; jj < c1; jj += 64) {
+                if (!((a.wcr[jj * W + (single >> 6)] >> (single & 63)) & 1ULL)) continue;
+                const uint32_t key = a.wck[jj];
+                const int tr = r - (int)(key >> 11), cg = (a.shard0 + l) * WSs * 64 + (int)(key & 2047u);
+                if (tr < Q.bottom) continue;
+                atomicOr(&ring[(size_t)(tr & dm) * W + (cg >> 6)], 1ULL << (cg & 63));
+              }
+            }
+        } else if (anyfe) {  // a partial round: the workgroup expands it
+          if (act) FE[lane] = fe;
+          if (lane == 0) {
+            s_ctl[0] = 0;
+            s_ctl[1] = r;
+          }
+          break;
+        }
+        DR_MT(n_w0++;)
+        cur = nxt;
+        --r;
       }
     }
     __syncthreads();
     if (s_ctl[0]) break;
-    if (s_ctl[1]) {
-      if (tid < W) expand_full_round(a, r, Q.bottom, ring, dm, weak, tid);
-    } else {
-      expand_partial_full<NT>(a, r, Q.bottom, FE, ring, dm, weak);
-    }
+    r = s_ctl[1];
+    DR_MT(const u64 tw = wall_clock64();)
+    expand_partial_full<NT>(a, r, Q.bottom, FE, ring, dm, weak);
     __syncthreads();
+    DR_MT(tt_wg += wall_clock64() - tw; n_wg++;)
+    if (wv == 0) cur = nxt;
+    --r;
   }
   if (tid == 0) {
     MState o{};
@@ -652,6 +830,11 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
     o.edges = edges;
     o.cur = r;
     f.fin[qi] = o;
+    DR_MT(if (qi < kMsTimingQ) {
+      u64 *t = g_ms_timing + 8 * (size_t)qi;
+      t[0] = tt0; t[1] = wall_clock64(); t[2] = n_w0; t[3] = n_wg; t[4] = tt_wg;
+      t[5] = (u64)Q.type; t[6] = (u64)Q.top; t[7] = (u64)(int64_t)r;
+    })
   }
 }
 

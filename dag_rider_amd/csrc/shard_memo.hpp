@@ -208,13 +208,19 @@ __device__ __forceinline__ void canon_ring_init(const MArgs &a, u64 *pend, int l
 // The highest bad round below `below` (-1: none), wave 0 (every lane gets it):
 // 8 rounds per lane per pass, as k_canon's search.
 __device__ __forceinline__ int next_bad(const MArgs &a, int below) {
+  constexpr int PL = 16;  // rounds per lane per block: every flag load of a block in flight at once
   const int lane = threadIdx.x & 63;
-  for (int top = below - 1; top >= 0; top -= 512) {
-    int best = -1;
-    for (int k = 0; k < 8; k++) {
-      const int x = top - 8 * lane - k;
-      if (x >= 0 && !a.good[x]) { best = x; break; }
+  for (int top = below - 1; top >= 0; top -= 64 * PL) {
+    uint8_t g[PL];
+#pragma unroll
+    for (int k = 0; k < PL; k++) {
+      const int x = top - PL * lane - k;
+      g[k] = x >= 0 ? a.good[x] : (uint8_t)1;
     }
+    int best = -1;
+#pragma unroll
+    for (int k = PL - 1; k >= 0; k--)
+      if (!g[k]) best = top - PL * lane - k;
     for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off));
     if (best >= 0) return best;
   }
@@ -482,28 +488,51 @@ __device__ __forceinline__ u64 ms_block_scan(u64 v, u64 *s, u64 &total) {
   return base + x - v;
 }
 
-// inclusive prefix over rounds 0..T of up to two arrays (one workgroup)
-__global__ __launch_bounds__(MS_NT) void k_ms_prefix(int T, const u64 *__restrict__ a0, u64 *__restrict__ b0,
-                                                     const u64 *__restrict__ a1, u64 *__restrict__ b1) {
-  __shared__ u64 part[MS_NT / 64];
-  const int tid = threadIdx.x, n = T + 1, per = (n + MS_NT - 1) / MS_NT;
-  const int ra = tid * per, rb = min(n, ra + per);
-  u64 s0 = 0, s1 = 0;
-  for (int r = ra; r < rb; r++) {
-    s0 += a0[r];
-    if (a1) s1 += a1[r];
-  }
-  u64 t0, t1;
-  u64 x0 = ms_block_scan(s0, part, t0);
-  u64 x1 = a1 ? ms_block_scan(s1, part, t1) : 0ULL;  // a1 is uniform
-  for (int r = ra; r < rb; r++) {
-    x0 += a0[r];
-    b0[r] = x0;
-    if (a1) {
-      x1 += a1[r];
-      b1[r] = x1;
+// inclusive prefix over rounds 0..T of up to two arrays, one workgroup of NT
+// threads: tiles of NT * CH rounds, wave v's CH chunks of 64 consecutive rounds
+// loaded together (coalesced, one memory latency per tile), scanned across the
+// lanes with the wave's running carry, then offset by the waves before it
+template <int NT>
+__device__ __forceinline__ void ms_prefix_one(int n, const u64 *__restrict__ a, u64 *__restrict__ b, u64 *part) {
+  constexpr int NW = NT / 64, CH = 8, TILE = NT * CH;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u64 tile_carry = 0;
+  for (int t0 = 0; t0 < n; t0 += TILE) {
+    const int base = t0 + wv * CH * 64 + lane;
+    u64 v[CH];
+#pragma unroll
+    for (int c = 0; c < CH; c++) v[c] = base + c * 64 < n ? a[base + c * 64] : 0ULL;
+    u64 run = 0;
+#pragma unroll
+    for (int c = 0; c < CH; c++) {
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const u64 y = __shfl_up(v[c], off);
+        if (lane >= off) v[c] += y;
+      }
+      v[c] += run;
+      run = __shfl(v[c], 63);
     }
+    if (lane == 0) part[wv] = run;
+    __syncthreads();
+    u64 off = tile_carry, tot = 0;
+    for (int w = 0; w < NW; w++) {
+      if (w < wv) off += part[w];
+      tot += part[w];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < CH; c++)
+      if (base + c * 64 < n) b[base + c * 64] = off + v[c];
+    tile_carry += tot;
   }
+}
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_prefix(int T, const u64 *__restrict__ a0, u64 *__restrict__ b0,
+                                                  const u64 *__restrict__ a1, u64 *__restrict__ b1) {
+  __shared__ u64 part[NT / 64];
+  ms_prefix_one<NT>(T + 1, a0, b0, part);
+  if (a1) ms_prefix_one<NT>(T + 1, a1, b1, part);
 }
 
 // One wave emits round y's slots whose source bit is set in mw (lane w < W holds

@@ -41,8 +41,19 @@ template <int CTRL>
 __device__ __forceinline__ u64 dpp64(u64 x) {
   return ((u64)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | (u64)dpp32<CTRL>((uint32_t)x);
 }
+
 enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141,
              DPP_ROW_ROR = 0x120 };
+// OR over the lanes of a row with equal (lane mod C), C a power of two < 16:
+// afterwards lane l of every row holds the OR of its row's class l mod C.
+template <int C>
+__device__ __forceinline__ u64 row_or_stride(u64 x) {
+  if constexpr (C <= 1) x |= dpp64<DPP_ROW_ROR + 1>(x);
+  if constexpr (C <= 2) x |= dpp64<DPP_ROW_ROR + 2>(x);
+  if constexpr (C <= 4) x |= dpp64<DPP_ROW_ROR + 4>(x);
+  if constexpr (C <= 8) x |= dpp64<DPP_ROW_ROR + 8>(x);
+  return x;
+}
 __device__ __forceinline__ u64 readlane64(u64 x, int l) {
   return ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);

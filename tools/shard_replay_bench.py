@@ -18,7 +18,7 @@ def main():
     from dag_rider_amd import _lib as L
     from dag_rider_amd.engine import Engine
     from dag_rider_amd.gen import CONFIGS, generate
-    from dag_rider_amd.shard import ShardEngine
+    from dag_rider_amd.shard import ShardEngine, ShardReplayer
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c4")
@@ -35,12 +35,14 @@ def main():
         with ShardEngine(cfg.n, cfg.faulty, d.nrounds, 0, nshards=G) as se:
             se.append_packed(d)
             se.set_stepped(bool(stepped))
-            r = se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)  # warm-up
+            rp = ShardReplayer(se, cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)  # outputs allocated once
+            rp()  # warm-up
             walls = []
             for _ in range(args.runs):
                 t0 = time.perf_counter()
-                r = se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+                rp()
                 walls.append((time.perf_counter() - t0) * 1e3)
+            r = rp.result()
             st = se.stats()
             ok = bool((r.commit == rref.commit).all() and (r.vcount == rref.vcount).all()
                       and (r.push_off == rref.push_off).all() and (r.push_wave == rref.push_wave).all()
@@ -49,7 +51,7 @@ def main():
                       and (r.commit_edges, r.chain_edges, r.deliver_edges)
                       == (rref.commit_edges, rref.chain_edges, rref.deliver_edges))
             print(json.dumps(dict(config=cfg.name, G=G, memo=True, form="stepped" if stepped else "fused", replay_ok=ok, ms_wall_median=statistics.median(walls),
-                                  ms_wall_min=min(walls), runs=walls, phases_ms=r.ms, steps=st["rounds"],
+                                  ms_wall_min=min(walls), runs=walls, phases_ms=r.ms, device_ms=sum(r.ms.values()), steps=st["rounds"],
                                   canon_segments=r.sweep["canon_segments"], cones=r.sweep["count"],
                                   edges=r.total_edges)), flush=True)
 
