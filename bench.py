@@ -44,11 +44,24 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950
 # correction of MI355X_MICROARCH.md) on this bench: tools/pmc_traffic.py output
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "traffic.json")
-# replay phase -> the kernels it launches (names as rocprofv3 reports them)
-PHASE_KERNELS = {"summary": ["dr::k_summary_commit<16, 1024, 2, false>"],
-                 "sweep": ["dr::k_sweep<16, 256, 9>"],
-                 "batch": ["dr::k_replay_small<8, false, true>"]}
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r04", "r03")]
+
+
+def phase_kernels(phase: str, W: int = 16):
+    """Replay phase -> candidate lists of the kernels it launches at row stride W, named as
+    rocprofv3 reports them (engine.hip's launch geometry: launch_sc_shipped, sweep_block_m,
+    launch_own_emit_t, the batch forms of DR_OPT_BATCH_FORM).  The first list whose every
+    kernel is in the traffic file is summed."""
+    blk = {1: 64, 2: 128, 4: 256, 8: 512}.get(W, 1024)
+    if phase == "summary":
+        return [[f"dr::k_summary_commit<{W}, 1024, 2, false>" if W == 16 else f"dr::k_summary_commit<{W}, {blk}, 8, false>"]]
+    if phase == "sweep":  # merging pop sweeps (SW_WEAK | SW_MERGE = 9), own-round emission, final pass
+        nt = 192 if W == 16 else min(blk, 512)
+        return [[f"dr::k_sweep<{W}, {nt}, 9>", f"dr::k_own_emit<{W}, {256 if W <= 4 else 512}>",
+                 "dr::k_replay_final<1024>"]]
+    if phase == "batch":  # the wave-per-DAG form (many DAGs per CU) or the workgroup form
+        return [["dr::k_replay_small_1w<false, true>"]] + [[f"dr::k_replay_small<{d}, false, true>"] for d in (4, 8, 16, 32)]
+    return []
 CPU_THREADS = 16  # the GPU box's host share for one GPU (OMP_NUM_THREADS there)
 
 
@@ -63,14 +76,19 @@ def cpu_threads() -> int:
     return max(1, min(share, cpu_info()["affinity"] or 1))
 
 
-def measured_traffic(phase):
-    """PMC-measured HBM bytes per launch of a phase's kernels, or None if not profiled."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            t = json.load(f)
-        return sum(t[k]["traffic_bytes"] for k in PHASE_KERNELS[phase])
-    except (OSError, KeyError, ValueError):
-        return None
+def measured_traffic(phase, W: int = 16):
+    """PMC-measured HBM bytes per launch of a phase's kernels (the newest traffic file that
+    profiled them), with the file it came from; (None, None) if none did."""
+    for path in TRAFFIC_FILES:
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for names in phase_kernels(phase, W):
+            if all(k in t for k in names):
+                return sum(t[k]["traffic_bytes"] for k in names), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def log(*a):
@@ -634,7 +652,8 @@ def run_c5(args, rank: int, world: int, local: int, dist):
                    "dags": total if not args.dags else hi - lo, "dags_per_rank": hi - lo, "n": 128, "rounds": 128, "waves": nw,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "roofline": {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic("batch"),
+                     "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic("batch")[0],
+                     "traffic_unit": f"bytes/launch (rocprofv3 PMC, {measured_traffic('batch')[1]})",
                      "kernel": "k_replay_small (batch.hpp)",
                      "bytes_per_launch": dag_bytes, "ms_per_launch": kms,
                      "note": "unique DAG bytes (strong rows + weak columns) once per launch"},
@@ -992,6 +1011,11 @@ def main() -> int:
     # dominant kernel = the phase with the largest device time (HIP events)
     dom = max(kb, key=lambda k: kb[k]["ms"])
     ach = kb[dom]["bytes"] / (kb[dom]["ms"] / 1e3) / 1e9 if kb[dom]["ms"] > 0 else 0.0
+    # PMC traffic of the dominant phase's kernels for this row stride (REF delivery: the
+    # profiled launch sequence); lines whose dominant kernel moves < 1 % of peak in its time
+    # are latency-bound and say so
+    tr_bytes, tr_file = measured_traffic(dom, (cfg.n + 63) // 64) if args.deliver == "ref" and not args.no_memo else (None, None)
+    bound = "hbm" if ach >= 0.01 * HBM_PEAK_GBS else "latency"
     ms_per_step = dt / args.steps * 1e3
     out = {
         "metric": "DAG edges traversed/sec (commit+delivery)",
@@ -1012,10 +1036,9 @@ def main() -> int:
                                + (" -- memo off (DR_OPT_MEMO 0): every cone swept whole" if args.no_memo else ""),
                    "n": cfg.n, "rounds": cfg.last_round, "waves": cfg.nwaves,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": bound, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": ach / HBM_PEAK_GBS,
-                     "traffic": measured_traffic(dom) if args.config == "c4" and args.deliver == "ref" else None,
-                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r03/traffic.json)",
+                     "traffic": tr_bytes, "traffic_unit": f"bytes/launch (rocprofv3 PMC, {tr_file})",
                      "kernel": kb[dom]["kernel"], "bytes_per_launch": kb[dom]["bytes"],
                      "ms_per_launch": kb[dom]["ms"]},
         "cpu_baseline": cpu,

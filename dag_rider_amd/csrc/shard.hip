@@ -141,7 +141,8 @@ struct ShardArgs {
   int32_t *push_n;          // [64] pushes per chain query
   u64 *cedges;              // [64] chain edges per query
   int32_t n, W, WSs, SP, C, depth, shard0, nlocal, local, max_rounds, nq, strong_only, nlead;
-  int64_t strong_shard_stride;  // words per local shard of strong
+  int64_t strong_shard_stride;  // words between local shards' rows of one round (n * SP)
+  int64_t strong_round_stride;  // words per round, every local shard (nlocal * n * SP)
 };
 
 __device__ __forceinline__ u64 shfl_xor64(u64 v, int m) {
@@ -240,7 +241,7 @@ __device__ void sweep_round(const ShardArgs &a, const Ft &ft, int r, int l, int 
     const u64 me = mv & m.exp;
     if (r < 1 || __ballot(me != 0ULL) == 0ULL) continue;
     const u64 row = (me != 0ULL)
-                        ? a.strong[(size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.SP + tw]
+                        ? a.strong[(size_t)r * a.strong_round_stride + (size_t)l * a.strong_shard_stride + (size_t)s * a.SP + tw]
                         : 0ULL;
     u64 act = __ballot(row != 0ULL);
     u64 acc = 0;
@@ -429,7 +430,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_vote(ShardArgs a, int w0, int n
   const int s = sb * SH_NT + (int)threadIdx.x;
   bool hit = false;
   if (s < a.n) {
-    const u64 *row = a.strong + (size_t)l * a.strong_shard_stride + ((size_t)r * a.n + s) * a.SP;
+    const u64 *row = a.strong + (size_t)r * a.strong_round_stride + (size_t)l * a.strong_shard_stride + (size_t)s * a.SP;
     for (int j = 0; j < a.WSs; j++) hit |= (row[j] & S[j]) != 0ULL;
   }
   const u64 b = __ballot(hit);
@@ -566,6 +567,7 @@ struct dr_shard {
   int persistent = 1;  // DR_SHARD_OPT_PERSISTENT
   int memo = 1;        // DR_SHARD_OPT_MEMO
   int stepped = 0;     // DR_SHARD_OPT_STEPPED: the memo replay's stepped form even when every column is here
+  int pass_geo = 0;    // k_ms_pass geometry (tools/shard_replay_bench.py --pass-geo; DR_SHARD_PASS_GEO)
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
   hipStream_t stream = nullptr;
@@ -593,6 +595,7 @@ struct dr_shard {
   SBuf ppref;                   // [round] |P_1| + .. + |P_r| (present vertices, round 0 excluded)
   std::vector<u64> h_ppref;
   SBuf mSG, mout;               // speculative canonical digests; the memo replay's output region
+  SBuf mctr;                    // last-workgroup counters of k_ms_kcand_canon / k_ms_tail (self-resetting)
   std::vector<std::vector<uint32_t>> h_weak;  // per local shard
   std::vector<std::vector<uint64_t>> h_woff;  // per local shard, absolute offsets, size nrounds+1
   // weak columns per local shard (the memoized replay, shard_memo.hpp): one entry per
@@ -724,7 +727,8 @@ ShardArgs make_args(dr_shard *c, int nq, int strong_only) {
   a.nq = nq;
   a.strong_only = strong_only;
   a.nlead = (int32_t)c->h_lead.size();
-  a.strong_shard_stride = (int64_t)c->max_rounds * c->n * c->SP;
+  a.strong_shard_stride = (int64_t)c->n * c->SP;
+  a.strong_round_stride = (int64_t)c->nlocal * c->n * c->SP;
   return a;
 }
 
@@ -1049,7 +1053,8 @@ int deliver(dr_shard *c, const std::vector<Pop> &pops, int mode, uint64_t *pcoun
 drs::MArgs make_margs(dr_shard *c, int nq, int T = -1) {
   drs::MArgs a{};
   a.strong = c->strong.as<u64>();
-  a.strong_stride = (int64_t)c->max_rounds * c->n * c->SP;
+  a.strong_stride = (int64_t)c->n * c->SP;
+  a.strong_rstride = (int64_t)c->nlocal * c->n * c->SP;
   a.wck = c->wck.as<uint32_t>();
   a.wcr = c->wcr.as<u64>();
   a.wcro = c->wcro.as<uint64_t>();
@@ -1230,13 +1235,24 @@ __global__ __launch_bounds__(256) void k_ms_vfinal(drs::MArgs a, drs::FArgs f, c
 // (k_ms_wu -- WU and the speculative digests, one workgroup per round, latency
 // bound -- runs beside it on the side stream: the pass keeps one 16-wave
 // workgroup per CU streaming rows, the small workgroups fill the other slots)
-template <int SP>
-hipError_t launch_pass_t(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
+template <int SP, int NT, int GR>
+hipError_t launch_pass_g(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
   const int T = c->nrounds - 1, nl = c->nlocal;
   const size_t lds = ((size_t)2 * nl * SP + c->W) * 8;
-  hipLaunchKernelGGL((drs::k_ms_pass<SP, 1024, 2>), dim3((T + 3) / 4), dim3(1024), lds, c->stream, a, f, nw, mode,
+  hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR>), dim3((T + 3) / 4), dim3(NT), lds, c->stream, a, f, nw, mode,
                      c->mU.as<u64>(), S1);
   return hipGetLastError();
+}
+template <int SP>
+hipError_t launch_pass_t(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
+  if constexpr (SP == 2 || SP == 16) {  // the C4 shapes (G = 8, G = 1): geometry variants for tuning
+    switch (c->pass_geo) {
+      case 1: return launch_pass_g<SP, 1024, 4>(c, a, f, nw, mode, S1);
+      case 2: return launch_pass_g<SP, 512, 4>(c, a, f, nw, mode, S1);
+      case 3: return launch_pass_g<SP, 512, 8>(c, a, f, nw, mode, S1);
+    }
+  }
+  return launch_pass_g<SP, 1024, 2>(c, a, f, nw, mode, S1);
 }
 hipError_t launch_pass(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
   const int T = c->nrounds - 1;
@@ -1435,6 +1451,10 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   f.nw = nw;
   f.npop = npop;
   f.persistent = persistent ? 1 : 0;
+  f.qcount = m.qout;
+  f.qdigest = m.qout + npop;
+  f.qedges = m.qout + 2 * npop;
+  f.emit = fused && !paper ? 1 : 0;  // the fused sweep emits each pop itself
   SHCHK(c, hipEventRecord(c->evs[0], c->stream));
   int steps = 0;
   if (fused) {
@@ -1444,23 +1464,19 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     a.slot_src = c->slot_src.as<uint16_t>();
     a.good = f.good;
     a.push_out = m.push;
-    const int rb = (T + 1 + 3) / 4;
     SHCHK(c, launch_pass(c, a, f, nw, drs::VOTE_FULL, (u64 *)nullptr));
     SHCHK(c, hipEventRecord(c->evs[1], c->stream));
-    hipLaunchKernelGGL(drs::k_ms_kcand_full, dim3(rb), dim3(256), 0, c->stream, a, f);
+    // K^cand + the canonical walk (last workgroup); digests + prefixes + plan (last workgroup)
+    const int rb16 = (T + 1 + 15) / 16;
+    const size_t lds_ring = ((size_t)c->depth * W + 2 * W) * 8;
+    hipLaunchKernelGGL((drs::k_ms_kcand_canon<1024>), dim3(rb16), dim3(1024), lds_ring, c->stream, a, f,
+                       c->mctr.as<int>());
     SHCHK(c, hipGetLastError());
-    const size_t lds_ring = ((size_t)c->depth * W + W) * 8;
-    hipLaunchKernelGGL((drs::k_ms_canon_full<512>), dim3(1), dim3(512), lds_ring, c->stream, a, f);
-    SHCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(drs::k_ms_rg_full, dim3(rb), dim3(256), 0, c->stream, a, f);
-    SHCHK(c, hipGetLastError());
-    hipLaunchKernelGGL((drs::k_ms_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
-                       (const u64 *)f.CE, f.Ec);
+    hipLaunchKernelGGL((drs::k_ms_tail<1024>), dim3(rb16), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
+                       (int)pcap, c->mctr.as<int>() + 1);
     SHCHK(c, hipGetLastError());
     SHCHK(c, hipEventRecord(c->evs[2], c->stream));
-    hipLaunchKernelGGL((drs::k_ms_plan<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
-                       (drs::MState *)nullptr, (int)pcap, 1);
-    SHCHK(c, hipGetLastError());
+    // every pop and chain to its end, REF pops emitted by their own workgroup
     hipLaunchKernelGGL((drs::k_ms_sweep_full<256>), dim3(nq), dim3(256), lds_ring, c->stream, a, f);
     SHCHK(c, hipGetLastError());
   } else {
@@ -1470,7 +1486,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   drs::MArgs a = make_margs(c, nq);
   a.slot_off = c->slot_off.as<uint32_t>();
   a.slot_src = c->slot_src.as<uint16_t>();
-  if (npop > 0 && !paper) {  // REF emission of every pop query (PAPER needs the pop order, below)
+  if (npop > 0 && !paper && !f.emit) {  // REF emission of every pop query (PAPER needs the pop order, below)
     hipLaunchKernelGGL(drs::k_ms_emit, dim3(npop), dim3(drs::MS_NT), 0, c->stream, a, (const int32_t *)nullptr,
                        (const drs::MState *)m.fin, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
                        (const u64 *)f.Cc, (const u64 *)f.Gc, (const u64 *)f.Ec, m.qout, m.qout + npop,
@@ -1539,7 +1555,20 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
         for (int x = 0; x < h.fin[t.q].npush; x++) o->push_wave[at++] = h.push[t.pbase + x];
       for (int64_t y = at - 1; y >= a0; y--) {  // pops: the stack's LIFO order
         const int q = popq[o->push_wave[y]];
-        if (q < 0) return c->fail(DR_E_HIP, "memo replay: pushed wave %d has no cone query", o->push_wave[y]);
+        if (q < 0) {
+          if (getenv("DR_DEBUG_PUSH")) {
+            for (const Task &tt : tasks) {
+              fprintf(stderr, "task wave %d q %d pbase %d", tt.wave, tt.q, tt.pbase);
+              if (tt.q >= 0) {
+                const drs::MState &S = h.fin[tt.q];
+                fprintf(stderr, " npush %d stop %d low %d edges %llu pushes:", S.npush, S.stop, S.low, (unsigned long long)S.edges);
+                for (int x = 0; x < S.npush; x++) fprintf(stderr, " %d", h.push[tt.pbase + x]);
+              }
+              fprintf(stderr, "\n");
+            }
+          }
+          return c->fail(DR_E_HIP, "memo replay: pushed wave %d has no cone query", o->push_wave[y]);
+        }
         pop_query.push_back(q);
       }
       ti++;
@@ -1682,6 +1711,7 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   c->SP = 1;
   while (c->SP < c->WSs) c->SP <<= 1;  // row stride: a power of two (fixed lane -> column maps)
   c->local = id == nullptr;
+  if (const char *g = getenv("DR_SHARD_PASS_GEO")) c->pass_geo = atoi(g) & 3;  // tuning only
   c->shard0 = c->local ? 0 : rank;
   c->nlocal = c->local ? nshards : 1;
   c->max_rounds = max_rounds;
@@ -1721,7 +1751,8 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
       c->slot_off.ensure(((size_t)max_rounds + 1) * 4) != hipSuccess ||
       c->lead.ensure(c->h_lead.size() * 2) != hipSuccess ||
       hipMemcpy(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(c->slot_off.p, 0, 4) != hipSuccess) {
+      hipMemset(c->slot_off.p, 0, 4) != hipSuccess || c->mctr.ensure(64) != hipSuccess ||
+      hipMemset(c->mctr.p, 0, 64) != hipSuccess) {
     g_shard_err = "dr_shard_create: device allocation failed";
     dr_shard_destroy(c);
     return DR_E_HIP;
@@ -1862,7 +1893,7 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
       if (row[W - 1] & ~lastmask) return c->fail(DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
       for (int l = 0; l < c->nlocal; l++) {
         const int g = c->shard0 + l;
-        u64 *dst = &rows[(((size_t)l * k + i) * n + s0) * SP];
+        u64 *dst = &rows[(((size_t)i * c->nlocal + l) * n + s0) * SP];
         for (int w = 0; w < WSs; w++) {
           const int gw = g * WSs + w;
           dst[w] = gw < W ? row[gw] : 0ULL;
@@ -1940,11 +1971,12 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
     SHCHK(c, hipMemcpyAsync(c->ppref.as<u64>() + r0, c->h_ppref.data() + base, (size_t)k * 8, hipMemcpyHostToDevice,
                             c->stream));
   }
+  // rows are round-major over the local shards ([round][shard][n][SP]): the k new
+  // rounds are one contiguous block
+  SHCHK(c, hipMemcpyAsync(c->strong.as<u64>() + (size_t)r0 * c->nlocal * n * SP, rows.data(),
+                          (size_t)k * c->nlocal * n * SP * 8, hipMemcpyHostToDevice, c->stream));
   for (int l = 0; l < c->nlocal; l++) {
     wro[l][k] = wnew[l].size();
-    const size_t dst = ((size_t)l * c->max_rounds + r0) * n * SP;
-    SHCHK(c, hipMemcpyAsync(c->strong.as<u64>() + dst, &rows[(size_t)l * k * n * SP], (size_t)k * n * SP * 8,
-                            hipMemcpyHostToDevice, c->stream));
     const uint64_t base = c->h_weak[l].size();
     c->h_weak[l].insert(c->h_weak[l].end(), wnew[l].begin(), wnew[l].end());
     for (int i = 1; i <= k; i++) c->h_woff[l].push_back(base + wro[l][i]);

@@ -63,7 +63,8 @@ struct FArgs {
   uint8_t *commit;     // [nw]
   int32_t *vcount;     // [nw]
   MState *fin;         // [nq] final state of every query
-  int32_t quorum, nw, npop, persistent;
+  u64 *qcount, *qdigest, *qedges;  // [npop] REF emission of each pop (k_ms_sweep_full with emit)
+  int32_t quorum, nw, npop, persistent, emit;
 };
 enum : int { FH_NCHAIN = 0, FH_NSEG = 1, FH_RLO = 2, FH_PUSHES = 3, FH_ERR = 4, FH_N = 8 };
 
@@ -186,12 +187,13 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
   for (int k = 0; k < nr; k++) {
     const int r = r1 + k;
     const bool test = leader && k >= 1 && (vote_mode == VOTE_FULL || k == 1);
-    const u64 *rbase = a.strong + (size_t)r * n * SP + (size_t)row0 * SP + j * CW;
+    const u64 *rbase = a.strong + (size_t)r * a.strong_rstride + (size_t)row0 * SP + j * CW;
     u64 a0 = 0, a1 = 0;
+    int lc = 0, pc = 0;  // (shard, pass) of element e0, carried from group to group
     for (int e0 = 0; e0 < E; e0 += GR) {
       u64 x0[GR], x1[GR];
       {
-        int l = e0 / CPT, p = e0 - l * CPT;
+        int l = lc, p = pc;
 #pragma unroll
         for (int q = 0; q < GR; q++) {
           x0[q] = 0;
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
           }
         }
       }
-      int l = e0 / CPT, p = e0 - l * CPT;
+      int l = lc, p = pc;
 #pragma unroll
       for (int q = 0; q < GR; q++) {
         if (e0 + q >= E) break;  // uniform
@@ -251,6 +253,8 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
           l++;
         }
       }
+      lc = l;
+      pc = p;
     }
     __syncthreads();
     for (int i = tid; i < NL * SP; i += NT) {
@@ -287,8 +291,8 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
 // K^cand over the full width (every local shard's U / WU), good_r, and the
 // full-round defaults RD_r = |K^cand_r & P_r|, CE_r = the round's degree sum.
 // One wave per round, lane w < W owns word w (shard w / WSs, column w mod WSs).
-__global__ __launch_bounds__(256) void k_ms_kcand_full(MArgs a, FArgs f) {
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63, T = a.T;
+__device__ __forceinline__ void kcand_round(const MArgs &a, const FArgs &f, int r) {
+  const int w = threadIdx.x & 63, T = a.T;
   if (r > T) return;
   bool bad = false;
   int cnt = 0;
@@ -315,6 +319,9 @@ __global__ __launch_bounds__(256) void k_ms_kcand_full(MArgs a, FArgs f) {
     f.CE[r] = r == 0 ? 0 : a.rdeg[r];
   }
 }
+__global__ __launch_bounds__(256) void k_ms_kcand_full(MArgs a, FArgs f) {
+  kcand_round(a, f, blockIdx.x * 4 + (threadIdx.x >> 6));
+}
 
 // Full-width expansion of a partial round r of a query held by one workgroup:
 // the frontier FE's strong rows (every local shard's columns) -> ring slot of
@@ -331,15 +338,17 @@ __global__ __launch_bounds__(256) void k_ms_kcand_full(MArgs a, FArgs f) {
 // saturation check.  Other shard counts take the per-shard loop.
 template <int NT>
 __device__ __forceinline__ void expand_partial_full(const MArgs &a, int r, int bottom, const u64 *FE, u64 *ring,
-                                                    int dm, bool weak) {
+                                                    int dm, bool weak, const u64 *Ur = nullptr,
+                                                    int64_t wc0 = -1, int64_t wc1 = -1) {
   constexpr int NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int SP = a.SP, W = a.W, WSs = a.WSs, NL = a.nlocal, WP = NL * SP;
   u64 *dst = ring + (size_t)((r - 1) & dm) * W;
   if (WP <= 64 && (64 % WP) == 0) {
     const int l0 = (lane % WP) / SP, c0 = lane % SP;  // this lane's word of the concatenated row
-    const u64 *base = a.strong + (size_t)l0 * a.strong_stride + (size_t)r * a.n * SP + c0;
-    const u64 ur = lane < WP ? a.U[((size_t)l0 * a.R + r) * SP + c0] : 0ULL;
+    const u64 *base = a.strong + (size_t)r * a.strong_rstride + (size_t)l0 * a.strong_stride + c0;
+    // U_r of this lane's word: from LDS when the caller staged it (W words), else loaded
+    const u64 ur = lane < WP ? (Ur ? (c0 < WSs ? Ur[l0 * WSs + c0] : 0ULL) : a.U[((size_t)l0 * a.R + r) * SP + c0]) : 0ULL;
     const int RPL = 64 / WP;  // rows per load instruction
     u64 acc = 0;
     for (int w = wv; w < W; w += NW) {
@@ -358,7 +367,7 @@ __device__ __forceinline__ void expand_partial_full(const MArgs &a, int r, int b
     if (lane < WP && c0 < WSs && acc) atomicOr(&dst[l0 * WSs + c0], acc);
   } else {
     for (int l = 0; l < NL; l++) {
-      const u64 *rows = a.strong + (size_t)l * a.strong_stride + (size_t)r * a.n * SP;
+      const u64 *rows = a.strong + (size_t)r * a.strong_rstride + (size_t)l * a.strong_stride;
       const u64 ur = lane < SP ? a.U[((size_t)l * a.R + r) * SP + lane] : 0ULL;
       u64 acc = 0;
       for (int w = wv; w < W; w += NW) {
@@ -382,13 +391,15 @@ __device__ __forceinline__ void expand_partial_full(const MArgs &a, int r, int b
   // waves (their offsets load in parallel), else every thread on each shard
   const bool per_wave = NL >= NW;
   for (int l = per_wave ? wv : 0; l < NL; l += per_wave ? NW : 1) {
-    const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
+    // (a prefetched range: one local shard)
+    const uint64_t c0 = wc0 >= 0 ? (uint64_t)wc0 : a.wcro[(size_t)l * (a.R + 1) + r];
+    const uint64_t c1 = wc0 >= 0 ? (uint64_t)wc1 : a.wcro[(size_t)l * (a.R + 1) + r + 1];
     for (uint64_t jj = c0 + (per_wave ? lane : tid); jj < c1; jj += per_wave ? 64 : NT) {
       const u64 *row = a.wcr + jj * W;
+      const uint32_t key = a.wck[jj];  // with the row: one memory latency
       u64 hit = 0;
       for (int w = 0; w < W; w++) hit |= row[w] & FE[w];
       if (!hit) continue;
-      const uint32_t key = a.wck[jj];
       const int tr = r - (int)(key >> 11), cg = (a.shard0 + l) * WSs * 64 + (int)(key & 2047u);
       if (tr < bottom) continue;
       atomicOr(&ring[(size_t)(tr & dm) * W + (cg >> 6)], 1ULL << (cg & 63));
@@ -424,16 +435,48 @@ __device__ __forceinline__ void fe_degrees(const MArgs &a, int r, const u64 *FE,
   if ((threadIdx.x & 63) == 0 && e) atomicAdd(out, e);
 }
 
+// Per-round words of lane w < W (global word w = shard w / WSs, column w mod
+// WSs) that do not depend on the frontier, loaded one round ahead by wave 0:
+// presence, canonical row, U and the first FDD weak-summary slots.
+// Also the leader of the wave whose first round r is (chains), and the round's
+// weak-column range when the context holds one shard (pops).
+constexpr int FDD = 3;
+struct FRound {
+  u64 P, K, U, WU[FDD];
+  uint64_t C0, C1;
+  u64 SD;  // chains: the round's strong-degree sum
+  int L;
+};
+// Every lane of wave 0 calls it (lanes >= W load nothing), so no part of the
+// record is assigned under a lane-divergent branch.
+__device__ __forceinline__ void fload_round(const MArgs &a, int r, bool pop, int w, FRound &x, bool wantK = true) {
+  const bool on = w < a.W;
+  const int l = on ? w / a.WSs : 0, cw = on ? w - l * a.WSs : 0;
+  const size_t ub = (size_t)l * a.R + r;
+  x.P = on ? a.pres[(size_t)r * a.W + w] : 0ULL;
+  x.K = (on && pop && wantK) ? a.K[(size_t)r * a.W + w] : 0ULL;
+  x.U = on ? a.U[ub * a.SP + cw] : 0ULL;
+#pragma unroll
+  for (int d = 0; d < FDD; d++) x.WU[d] = (on && pop && d < a.dd) ? a.WU[(ub * a.dd + d) * a.SP + cw] : 0ULL;
+  x.C0 = (pop && a.nlocal == 1) ? a.wcro[r] : 0;
+  x.C1 = (pop && a.nlocal == 1) ? a.wcro[r + 1] : 0;
+  x.SD = pop ? 0ULL : a.sdr[r];
+  const int wvv = ((r - 1) >> 2) + 1;
+  x.L = (!pop && r >= 1 && ((r - 1) & 3) == 0) ? (wvv < a.nlead ? (int)a.lead[wvv] : 1) - 1 : -1;
+}
+
 // ---------------------------------------------------------------------------
 // k_ms_canon_full: one workgroup, the canonical segments top down (k_canon).
-// Dynamic LDS: ring[depth*W] | FE[W].
+// Dynamic LDS: ring[depth*W] | FE[W] | Ur[W].  As in k_ms_sweep_full, wave 0
+// walks with the round words loaded three rounds ahead and applies full rounds
+// alone; partial rounds take the workgroup (degrees loaded before the rows).
 // ---------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(NT) void k_ms_canon_full(MArgs a, FArgs f) {
-  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+__device__ __forceinline__ void canon_walk(const MArgs &a, const FArgs &f, u64 *lds) {
   const int W = a.W, dm = a.depth - 1, T = a.T;
-  u64 *ring = lds, *FE = lds + (size_t)a.depth * W;
+  u64 *ring = lds, *FE = lds + (size_t)a.depth * W, *Ur = FE + W;
   __shared__ int s_ctl[4];
+  __shared__ int64_t s_wc[2];
   __shared__ u64 s_e;
   __shared__ int64_t s_scan[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -463,42 +506,96 @@ __global__ __launch_bounds__(NT) void k_ms_canon_full(MArgs a, FArgs f) {
     __syncthreads();
     int run = 0, r = b;
     const bool act = lane < W;
-    u64 p_nx = (wv == 0 && act) ? a.pres[(size_t)r * W + lane] : 0ULL;  // round r-1's, loaded while r expands
-    for (;; --r) {
-      if (wv == 0) {
-        u64 fw = 0;
-        const u64 p = p_nx;
-        if (act) {
-          u64 *slot = &ring[(size_t)(r & dm) * W + lane];
-          fw = *slot;
-          *slot = 0;
-          if (r >= 1) p_nx = a.pres[(size_t)(r - 1) * W + lane];
-          a.K[(size_t)r * W + lane] = fw;
-          FE[lane] = fw & p;
-        }
-        const bool full = __ballot(act && (fw & p) != p) == 0ULL;
-        int cnt = __popcll(fw & p);
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-        run = full ? run + 1 : 0;
-        if (lane == 0) {
-          s_ctl[1] = full;
-          s_ctl[2] = run >= a.dmax || r == 0;
-          f.RD[r] = r == 0 ? 0 : (u64)cnt;
-          s_e = 0;
-        }
-      }
-      __syncthreads();
-      if (s_ctl[2]) break;  // regime restored at r (CE_r keeps the full-round total)
-      if (s_ctl[1]) {
-        if (tid < W) expand_full_round(a, r, 0, ring, dm, true, tid);
-      } else {
-        expand_partial_full<NT>(a, r, 0, FE, ring, dm, true);
-        fe_degrees<NT>(a, r, FE, true, &s_e);
-      }
-      __syncthreads();
-      if (tid == 0 && !s_ctl[1]) f.CE[r] = s_e;
-      __syncthreads();
+    // wave 0: the round words three rounds ahead; full rounds applied alone
+    FRound c0{}, c1{}, c2{}, c3{};
+    if (wv == 0) {
+      fload_round(a, r, true, lane, c0, false);
+      if (r >= 1) fload_round(a, r - 1, true, lane, c1, false);
+      if (r >= 2) fload_round(a, r - 2, true, lane, c2, false);
     }
+    for (;;) {
+      if (wv == 0) {
+        for (;;) {
+          if (r >= 3) fload_round(a, r - 3, true, lane, c3, false);
+          u64 fw = 0;
+          const u64 p = c0.P;
+          if (act) {
+            u64 *slot = &ring[(size_t)(r & dm) * W + lane];
+            fw = *slot;
+            *slot = 0;
+            a.K[(size_t)r * W + lane] = fw;
+          }
+          const u64 fe = fw & p;
+          const bool full = __ballot(act && fe != p) == 0ULL;
+          int cnt = __popcll(fe);
+          for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+          run = full ? run + 1 : 0;
+          if (lane == 0) f.RD[r] = r == 0 ? 0 : (u64)cnt;
+          if (run >= a.dmax || r == 0) {  // regime restored at r (CE_r keeps the full-round total)
+            if (lane == 0) s_ctl[1] = 1;
+            break;
+          }
+          if (!full) {  // partial: the workgroup expands it
+            if (act) {
+              FE[lane] = fe;
+              Ur[lane] = c0.U;
+            }
+            if (lane == 0) {
+              s_ctl[1] = 0;
+              s_ctl[2] = r;
+              s_wc[0] = a.nlocal == 1 ? (int64_t)c0.C0 : -1;
+              s_wc[1] = (int64_t)c0.C1;
+              s_e = 0;
+            }
+            break;
+          }
+          if (act) {  // full: ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d]
+            ring[(size_t)((r - 1) & dm) * W + lane] |= c0.U;
+            const int l = lane / a.WSs, cw = lane - l * a.WSs;
+            for (int d = 0; d < a.dd; d++) {
+              const int tr = r - d - 2;
+              if (tr < 0) break;
+              ring[(size_t)(tr & dm) * W + lane] |=
+                  d < FDD ? c0.WU[d] : a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw];
+            }
+          }
+          c0 = c1;
+          c1 = c2;
+          c2 = c3;
+          --r;
+        }
+      }
+      __syncthreads();
+      if (s_ctl[1]) break;
+      r = s_ctl[2];
+      // the partial round's strong + weak degrees (loaded before the rows) and expansion
+      constexpr int KS = 2048 / NT;
+      uint32_t dg[KS];
+#pragma unroll
+      for (int k = 0; k < KS; k++) {
+        const int sv = tid + k * NT;
+        const size_t at = (size_t)r * a.n + sv;
+        dg[k] = (sv < a.n && ((FE[sv >> 6] >> (sv & 63)) & 1ULL)) ? (uint32_t)a.sdeg[at] + a.wdeg[at] : 0u;
+      }
+      expand_partial_full<NT>(a, r, 0, FE, ring, dm, true, Ur, s_wc[0], s_wc[1]);
+      u64 e = 0;
+#pragma unroll
+      for (int k = 0; k < KS; k++) e += dg[k];
+      e = dr::wave_sum(e);
+      if (lane == 0 && e) atomicAdd(&s_e, e);
+      __syncthreads();
+      if (tid == 0) f.CE[r] = s_e;
+      if (wv == 0) {
+        c0 = c1;
+        c1 = c2;
+        c2 = c3;
+      }
+      --r;
+    }
+    if (tid == 0) s_ctl[3] = r;  // wave 0's stop round
+    __syncthreads();
+    r = s_ctl[3];
+    __syncthreads();
     pos = r;
     lo_w = min(lo_w, r);
   }
@@ -527,11 +624,41 @@ __global__ __launch_bounds__(NT) void k_ms_canon_full(MArgs a, FArgs f) {
     f.hdr[FH_RLO] = s_ctl[3];
   }
 }
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_canon_full(MArgs a, FArgs f) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  canon_walk<NT>(a, f, lds);
+}
+
+// The last workgroup to finish (counter, self-resetting) of a parallel phase
+// runs the serial step after it: every other workgroup's writes are visible to it
+// after the agent-scope acquire.
+__device__ __forceinline__ bool last_block(int *counter) {
+  __shared__ int s_last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(counter, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return false;
+  __threadfence();
+  if (threadIdx.x == 0) *counter = 0;
+  return true;
+}
+
+// K^cand of every round (one wave per round), then the canonical walk in the
+// last workgroup: one launch for k_ms_kcand_full + k_ms_canon_full.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_kcand_canon(MArgs a, FArgs f, int *counter) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  kcand_round(a, f, blockIdx.x * (NT / 64) + (threadIdx.x >> 6));
+  if (!last_block(counter)) return;
+  canon_walk<NT>(a, f, lds);
+}
 
 // canonical digest of round r >= 1 (one wave per round): the speculative one
 // below the first round whose position prefix differs from the presence prefix
-__global__ __launch_bounds__(256) void k_ms_rg_full(MArgs a, FArgs f) {
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+__device__ __forceinline__ void rg_round(const MArgs &a, const FArgs &f, int r) {
+  const int lane = threadIdx.x & 63;
   if (r > a.T) return;
   if (r == 0) {
     if (lane == 0) f.RG[0] = 0;
@@ -547,6 +674,9 @@ __global__ __launch_bounds__(256) void k_ms_rg_full(MArgs a, FArgs f) {
   dg = dr::wave_sum(dg);
   if (lane == 0) f.RG[r] = dg;
 }
+__global__ __launch_bounds__(256) void k_ms_rg_full(MArgs a, FArgs f) {
+  rg_round(a, f, blockIdx.x * 4 + (threadIdx.x >> 6));
+}
 
 // ---------------------------------------------------------------------------
 // k_ms_plan: waveReady's chain tasks (process.go:341-350) from the device commit
@@ -557,8 +687,8 @@ __global__ __launch_bounds__(256) void k_ms_rg_full(MArgs a, FArgs f) {
 // slot's stepped state (st0) is initialised, unused slots as done.
 // ---------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__restrict__ q, MState *__restrict__ st0,
-                                                int push_cap, int make_pops) {
+__device__ __forceinline__ void plan_body(const MArgs &a, const FArgs &f, MQuery *__restrict__ q,
+                                          MState *__restrict__ st0, int push_cap, int make_pops) {
   __shared__ int64_t s_scan[NT / 64];
   const int nw = f.nw, tid = threadIdx.x;
   const int per = (nw + NT - 1) / NT, wa = 1 + tid * per, wb = min(nw + 1, wa + per);
@@ -655,35 +785,38 @@ __global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__rest
     f.hdr[FH_ERR] = ptot > push_cap ? 1 : 0;
   }
 }
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__restrict__ q, MState *__restrict__ st0,
+                                                int push_cap, int make_pops) {
+  plan_body<NT>(a, f, q, st0, push_cap, make_pops);
+}
 
-// Per-round words of lane w < W (global word w = shard w / WSs, column w mod
-// WSs) that do not depend on the frontier, loaded one round ahead by wave 0:
-// presence, canonical row, U and the first FDD weak-summary slots.
-constexpr int FDD = 3;
-struct FRound {
-  u64 P, K, U, WU[FDD];
-};
-__device__ __forceinline__ void fload_round(const MArgs &a, int r, bool pop, int w, FRound &x) {
-  const int l = w / a.WSs, cw = w - l * a.WSs;
-  const size_t ub = (size_t)l * a.R + r;
-  x.P = a.pres[(size_t)r * a.W + w];
-  x.K = pop ? a.K[(size_t)r * a.W + w] : 0ULL;
-  x.U = a.U[ub * a.SP + cw];
-#pragma unroll
-  for (int d = 0; d < FDD; d++) x.WU[d] = (pop && d < a.dd) ? a.WU[(ub * a.dd + d) * a.SP + cw] : 0ULL;
+// The canonical digest of every round (one wave per round), then in the last
+// workgroup the prefixes G, E and the plan (pops and chains): one launch for
+// k_ms_rg_full + k_ms_prefix + k_ms_plan.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_tail(MArgs a, FArgs f, MQuery *__restrict__ q, int push_cap, int *counter) {
+  __shared__ u64 part[NT / 64];
+  rg_round(a, f, blockIdx.x * (NT / 64) + (threadIdx.x >> 6));
+  if (!last_block(counter)) return;
+  ms_prefix_one<NT>(a.T + 1, f.RG, f.Gc, part);
+  ms_prefix_one<NT>(a.T + 1, f.CE, f.Ec, part);
+  __syncthreads();
+  plan_body<NT>(a, f, q, (MState *)nullptr, push_cap, 1);
 }
 
 // ---------------------------------------------------------------------------
 // k_ms_sweep_full: one workgroup per query, every round to its end (the same
 // decisions as k_ms_step, shard_memo.hpp).  Grid npop + nw: workgroups past the
-// planned chains exit.  Dynamic LDS: ring[depth*W] | FE[W].
+// planned chains exit.  Dynamic LDS: ring[depth*W] | FE[W] | Ur[W].
 //
-// Wave 0 decides each round from words it loaded one round ahead and applies,
-// without a workgroup barrier, every round it can expand alone: a full round
-// (ring |= U_r, WU_r from the prefetched words), a round whose frontier is one
-// vertex (the query's top, a chain's restart: that row and its weak columns)
-// and an empty one.  Only a partial round with several vertices is expanded by
-// the whole workgroup (expand_partial_full).
+// Wave 0 decides each round from words it loaded three rounds ahead and
+// applies, without a workgroup barrier, every round it can expand alone: a full
+// round (ring |= U_r, WU_r from the prefetched words), a round whose frontier is
+// one vertex (the query's top, a chain's restart: that row and its weak
+// columns) and an empty one.  Only a partial round with several vertices is
+// expanded by the whole workgroup (expand_partial_full, U_r staged in LDS; a
+// chain's degree loads issued before the rows).
 // ---------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
@@ -692,8 +825,10 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
   DR_MT(const u64 tt0 = wall_clock64(); u64 tt_wg = 0, n_w0 = 0, n_wg = 0;)
   if (qi >= f.npop + f.hdr[FH_NCHAIN]) return;
   const int W = a.W, dm = a.depth - 1, WSs = a.WSs;
-  u64 *ring = lds, *FE = lds + (size_t)a.depth * W;
+  u64 *ring = lds, *FE = lds + (size_t)a.depth * W, *Ur = FE + W;
   __shared__ int s_ctl[2];
+  __shared__ int64_t s_wc[2];
+  __shared__ u64 s_e;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const MQuery Q = a.q[qi];
   const bool pop = Q.type == MQ_POP, weak = pop;
@@ -706,14 +841,14 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
   int r = Q.top;
   bool merged = false;
   const bool act = lane < W;
-  FRound cur{}, nxt{};
-  if (wv == 0 && act) fload_round(a, r, pop, lane, cur);
+  FRound c0{}, c1{};  // rounds r (wave 0) and r-1, issued at round r
+  if (wv == 0) fload_round(a, r, pop, lane, c0);
   for (;;) {
     if (wv == 0) {
       for (;;) {
-        if (act && r >= 1) fload_round(a, r - 1, pop, lane, nxt);
+        if (r >= 1) fload_round(a, r - 1, pop, lane, c1);
         u64 fw = 0;
-        const u64 p = cur.P;
+        const u64 p = c0.P;
         if (act) {
           u64 *slot = &ring[(size_t)(r & dm) * W + lane];
           fw = *slot;
@@ -722,15 +857,14 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
         int single = r == Q.top ? Q.src0 : -1;  // a round whose frontier is one known vertex
         // waveReady's chain (process.go:342-350): a reachable, present leader of
         // wave wvv is pushed and the chain goes on from it alone
-        if (!pop && r < Q.top && ((r - 1) & 3) == 0) {
-          const int wvv = ((r - 1) >> 2) + 1;
-          const int L = (wvv < a.nlead ? (int)a.lead[wvv] : 1) - 1;
-          const u64 fl = __shfl(fw & p, L >> 6);
-          if ((fl >> (L & 63)) & 1ULL) {
-            fw = lane == (L >> 6) ? 1ULL << (L & 63) : 0ULL;
-            if (lane == 0) a.push_out[Q.push_base + npush] = wvv;
+        const int Lr = c0.L;  // uniform
+        if (!pop && r < Q.top && Lr >= 0) {
+          const u64 fl = __shfl(fw & p, Lr >> 6);
+          if ((fl >> (Lr & 63)) & 1ULL) {
+            fw = lane == (Lr >> 6) ? 1ULL << (Lr & 63) : 0ULL;
+            if (lane == 0) a.push_out[Q.push_base + npush] = ((r - 1) >> 2) + 1;
             npush++;
-            single = L;
+            single = Lr;
           }
         }
         const u64 fe = fw & p;
@@ -740,7 +874,7 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
         if (nz) low = min(low, r - 1);
         bool done;
         if (pop) {
-          run = __ballot(act && fw != cur.K) == 0ULL ? run + 1 : 0;
+          run = __ballot(act && fw != c0.K) == 0ULL ? run + 1 : 0;
           merged = run >= a.dmax;
           done = merged || r <= Q.bottom || (!nz && low >= r);
           if (act) a.masks[Q.mask_off + (int64_t)(Q.top - r) * W + lane] = fw;
@@ -748,15 +882,6 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
           done = r <= Q.bottom || (!nz && low >= r);
         }
         const bool summary = !done && full;
-        if (!pop && !done) {
-          if (summary) {
-            edges += a.sdr[r];
-          } else {
-            u64 e = 0;
-            for (u64 x = act ? fe : 0ULL; x; x &= x - 1) e += a.sdeg[(size_t)r * a.n + lane * 64 + __builtin_ctzll(x)];
-            edges += dr::wave_sum(e);
-          }
-        }
         if (!done && pop && anyfe) low = min(low, r - a.dmax);
         if (done) {
           if (lane == 0) {
@@ -765,47 +890,57 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
           }
           break;
         }
+        const bool one = !summary && anyfe && single >= 0 && ((__shfl(fe, single >> 6) >> (single & 63)) & 1ULL);
         if (summary) {  // ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d]
+          if (!pop) edges += __shfl(c0.SD, 0);
           if (act) {
-            ring[(size_t)((r - 1) & dm) * W + lane] |= cur.U;
+            ring[(size_t)((r - 1) & dm) * W + lane] |= c0.U;
             if (weak) {
               const int l = lane / WSs, cw = lane - l * WSs;
               for (int d = 0; d < a.dd; d++) {
                 const int tr = r - d - 2;
                 if (tr < Q.bottom) break;
                 ring[(size_t)(tr & dm) * W + lane] |=
-                    d < FDD ? cur.WU[d] : a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw];
+                    d < FDD ? c0.WU[d] : a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw];
               }
             }
           }
-        } else if (anyfe && single >= 0 && ((__shfl(fe, single >> 6) >> (single & 63)) & 1ULL)) {
-          // FE = {single}: its row (every local shard's piece) and its weak columns
+        } else if (one) {  // FE = {single}: its row (every local shard's piece) and its weak columns
+          if (!pop) edges += a.sdeg[(size_t)r * a.n + single];
           if (act) {
             const int l = lane / WSs, cw = lane - l * WSs;
             ring[(size_t)((r - 1) & dm) * W + lane] |=
-                a.strong[(size_t)l * a.strong_stride + ((size_t)r * a.n + single) * a.SP + cw];
+                a.strong[(size_t)r * a.strong_rstride + (size_t)l * a.strong_stride + (size_t)single * a.SP + cw];
           }
           if (weak)
             for (int l = 0; l < a.nlocal; l++) {
-              const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
-              for (uint64_t jj = c0 + lane; jj < c1; jj += 64) {
-                if (!((a.wcr[jj * W + (single >> 6)] >> (single & 63)) & 1ULL)) continue;
+              const uint64_t wa = a.nlocal == 1 ? c0.C0 : a.wcro[(size_t)l * (a.R + 1) + r];
+              const uint64_t wb = a.nlocal == 1 ? c0.C1 : a.wcro[(size_t)l * (a.R + 1) + r + 1];
+              const uint64_t ja = __shfl((long long)wa, 0), jb = __shfl((long long)wb, 0);
+              for (uint64_t jj = ja + lane; jj < jb; jj += 64) {
                 const uint32_t key = a.wck[jj];
+                if (!((a.wcr[jj * W + (single >> 6)] >> (single & 63)) & 1ULL)) continue;
                 const int tr = r - (int)(key >> 11), cg = (a.shard0 + l) * WSs * 64 + (int)(key & 2047u);
                 if (tr < Q.bottom) continue;
                 atomicOr(&ring[(size_t)(tr & dm) * W + (cg >> 6)], 1ULL << (cg & 63));
               }
             }
         } else if (anyfe) {  // a partial round: the workgroup expands it
-          if (act) FE[lane] = fe;
+          if (act) {
+            FE[lane] = fe;
+            Ur[lane] = c0.U;
+          }
           if (lane == 0) {
             s_ctl[0] = 0;
             s_ctl[1] = r;
+            s_wc[0] = a.nlocal == 1 ? (int64_t)c0.C0 : -1;
+            s_wc[1] = (int64_t)c0.C1;
+            s_e = 0;
           }
           break;
         }
         DR_MT(n_w0++;)
-        cur = nxt;
+        c0 = c1;
         --r;
       }
     }
@@ -813,12 +948,32 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
     if (s_ctl[0]) break;
     r = s_ctl[1];
     DR_MT(const u64 tw = wall_clock64();)
-    expand_partial_full<NT>(a, r, Q.bottom, FE, ring, dm, weak);
+    constexpr int KS = 2048 / NT;  // sources per thread (n <= 2048)
+    uint16_t dg[KS];
+    if (!pop) {  // the chain's strong degrees of FE, loaded before the rows
+#pragma unroll
+      for (int k = 0; k < KS; k++) {
+        const int sv = tid + k * NT;
+        dg[k] = (sv < a.n && ((FE[sv >> 6] >> (sv & 63)) & 1ULL)) ? a.sdeg[(size_t)r * a.n + sv] : (uint16_t)0;
+      }
+    }
+    expand_partial_full<NT>(a, r, Q.bottom, FE, ring, dm, weak, Ur, s_wc[0], s_wc[1]);
+    if (!pop) {
+      u64 e = 0;
+#pragma unroll
+      for (int k = 0; k < KS; k++) e += dg[k];
+      e = dr::wave_sum(e);
+      if (lane == 0 && e) atomicAdd(&s_e, e);
+    }
     __syncthreads();
     DR_MT(tt_wg += wall_clock64() - tw; n_wg++;)
-    if (wv == 0) cur = nxt;
+    if (wv == 0) {
+      if (!pop) edges += s_e;
+      c0 = c1;
+    }
     --r;
   }
+  __shared__ MState s_fin;
   if (tid == 0) {
     MState o{};
     o.done = 1;
@@ -830,11 +985,19 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
     o.edges = edges;
     o.cur = r;
     f.fin[qi] = o;
+    s_fin = o;
     DR_MT(if (qi < kMsTimingQ) {
       u64 *t = g_ms_timing + 8 * (size_t)qi;
       t[0] = tt0; t[1] = wall_clock64(); t[2] = n_w0; t[3] = n_wg; t[4] = tt_wg;
       t[5] = (u64)Q.type; t[6] = (u64)Q.top; t[7] = (u64)(int64_t)r;
     })
+  }
+  if (pop && f.emit) {  // REF emission of this pop here: wave 0's mask rows are at agent scope first
+    static_assert(NT == MS_NT, "ms_emit_query assumes MS_NT threads");
+    if (wv == 0) __threadfence();
+    __syncthreads();
+    const MState S = s_fin;
+    ms_emit_query(a, Q, S, a.slot_off, a.slot_src, f.Cc, f.Gc, f.Ec, qi, f.qcount, f.qdigest, f.qedges);
   }
 }
 

@@ -62,8 +62,9 @@ struct MState {
 };
 
 struct MArgs {
-  const u64 *strong;        // [nlocal][max_rounds][n][SP]
-  int64_t strong_stride;    // words per local shard
+  const u64 *strong;        // [max_rounds][nlocal][n][SP]: round-major over the local shards
+  int64_t strong_stride;    // words between local shards' rows of one round (n * SP)
+  int64_t strong_rstride;   // words per round (nlocal * n * SP)
   const uint32_t *wck;      // weak columns: key delta << 11 | local column
   const u64 *wcr;           // [column][W] sources with that weak edge
   const uint64_t *wcro;     // [nlocal][R+1] absolute column offsets per round
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(MS_NT) void k_ms_summary(MArgs a, int T, u64 *__res
   if (tid < SP) sU[tid] = 0;
   for (int i = tid; i < a.dd * SP; i += MS_NT) sWU[i] = 0;
   __syncthreads();
-  const u64 *rows = a.strong + (size_t)l * a.strong_stride + (size_t)r * a.n * SP;
+  const u64 *rows = a.strong + (size_t)r * a.strong_rstride + (size_t)l * a.strong_stride;
   const size_t nw = (size_t)a.n * SP;
   if (SP >= 2) {
     const u64x2 *p = reinterpret_cast<const u64x2 *>(rows);
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(MS_NT) void k_ms_step(MArgs a, int j) {
   } else {
     // strong rows of the frontier: wave wv takes frontier words wv, wv + 4, ...;
     // lane reads words lane + 64 i of the word's 64 rows (column lane mod SP)
-    const u64 *rows = a.strong + (size_t)l * a.strong_stride + (size_t)r * a.n * SP;
+    const u64 *rows = a.strong + (size_t)r * a.strong_rstride + (size_t)l * a.strong_stride;
     // saturation (as the unsharded sweep's expand_round): once the OR of the rows a
     // wave has read equals U_r, the union of every row of round r, no further row
     // can add a bit and the wave stops reading
@@ -579,21 +580,21 @@ __global__ __launch_bounds__(MS_NT) void k_ms_rg(MArgs a, int T, const uint32_t 
   if (lane == 0) RG[r] = dg;
 }
 
-// REF emission, one workgroup per pop query (qidx; null: query b): the canonical prefix at the
-// cut (C, G, E) plus the query's own rounds cut+1 .. top from its mask rows, 64
-// rounds at a time (counts, exclusive scan, digests and degrees).
-__global__ __launch_bounds__(MS_NT) void k_ms_emit(MArgs a, const int32_t *__restrict__ qidx, const MState *__restrict__ st,
-                                                   const uint32_t *__restrict__ slot_off,
-                                                   const uint16_t *__restrict__ slot_src, const u64 *__restrict__ Cc,
-                                                   const u64 *__restrict__ Gc, const u64 *__restrict__ Ec,
-                                                   u64 *__restrict__ qcount, u64 *__restrict__ qdigest,
-                                                   u64 *__restrict__ qedges) {
+// REF emission of one pop query by one workgroup of MS_NT threads (every thread
+// calls it): the canonical prefix at the cut (C, G, E) plus the query's own
+// rounds cut+1 .. top from its mask rows, 64 rounds at a time (counts, exclusive
+// scan, digests and degrees).  Mask rows are read at agent scope: the fused
+// sweep calls it right after its own wave 0 wrote them.
+__device__ __forceinline__ void ms_emit_query(const MArgs &a, const MQuery &Q, const MState &S,
+                                              const uint32_t *__restrict__ slot_off,
+                                              const uint16_t *__restrict__ slot_src, const u64 *__restrict__ Cc,
+                                              const u64 *__restrict__ Gc, const u64 *__restrict__ Ec, int b,
+                                              u64 *__restrict__ qcount, u64 *__restrict__ qdigest,
+                                              u64 *__restrict__ qedges) {
   __shared__ uint32_t sCnt[64];
   __shared__ u64 sPos[64];
   __shared__ u64 sTot, sDg, sEd;
-  const int b = blockIdx.x, qi = qidx ? qidx[b] : b, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const MQuery Q = a.q[qi];
-  const MState S = st[qi];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int top = Q.top;
   int cut, lo;
   if (S.merged) {
@@ -607,14 +608,17 @@ __global__ __launch_bounds__(MS_NT) void k_ms_emit(MArgs a, const int32_t *__res
     sDg = 0;
     sEd = 0;
   }
+  auto mask_word = [&](int y) -> u64 {
+    if (lane >= a.W) return 0ULL;
+    const u64 m = __hip_atomic_load(a.masks + Q.mask_off + (int64_t)(top - y) * a.W + lane, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+    return m & a.pres[(size_t)y * a.W + lane];
+  };
   u64 run = Cc[cut];
   for (int y0 = lo; y0 <= top; y0 += 64) {
     const int ny = min(64, top - y0 + 1);
     for (int i = wv; i < ny; i += MS_NT / 64) {
-      const int y = y0 + i;
-      const u64 mw = lane < a.W ? a.masks[Q.mask_off + (int64_t)(top - y) * a.W + lane] & a.pres[(size_t)y * a.W + lane]
-                                : 0ULL;
-      const u64 c = dr::wave_sum((u64)__popcll(mw));
+      const u64 c = dr::wave_sum((u64)__popcll(mask_word(y0 + i)));
       if (lane == 0) sCnt[i] = (uint32_t)c;
     }
     __syncthreads();
@@ -632,9 +636,7 @@ __global__ __launch_bounds__(MS_NT) void k_ms_emit(MArgs a, const int32_t *__res
     u64 dg = 0, ed = 0;
     for (int i = wv; i < ny; i += MS_NT / 64) {
       const int y = y0 + i;
-      const u64 mw = lane < a.W ? a.masks[Q.mask_off + (int64_t)(top - y) * a.W + lane] & a.pres[(size_t)y * a.W + lane]
-                                : 0ULL;
-      ms_wave_emit(slot_off, slot_src, y, mw, sPos[i], a.W, a.sdeg, a.wdeg, a.n, dg, ed);
+      ms_wave_emit(slot_off, slot_src, y, mask_word(y), sPos[i], a.W, a.sdeg, a.wdeg, a.n, dg, ed);
     }
     dg = dr::wave_sum(dg);
     ed = dr::wave_sum(ed);
@@ -652,6 +654,16 @@ __global__ __launch_bounds__(MS_NT) void k_ms_emit(MArgs a, const int32_t *__res
   }
 }
 
+// REF emission, one workgroup per pop query (qidx; null: query b)
+__global__ __launch_bounds__(MS_NT) void k_ms_emit(MArgs a, const int32_t *__restrict__ qidx, const MState *__restrict__ st,
+                                                   const uint32_t *__restrict__ slot_off,
+                                                   const uint16_t *__restrict__ slot_src, const u64 *__restrict__ Cc,
+                                                   const u64 *__restrict__ Gc, const u64 *__restrict__ Ec,
+                                                   u64 *__restrict__ qcount, u64 *__restrict__ qdigest,
+                                                   u64 *__restrict__ qedges) {
+  const int b = blockIdx.x, qi = qidx ? qidx[b] : b;
+  ms_emit_query(a, a.q[qi], st[qi], slot_off, slot_src, Cc, Gc, Ec, b, qcount, qdigest, qedges);
+}
 
 // ---------------------------------------------------------------------------
 // PAPER delivery (Alg. 3 line 54: a pop delivers its cone minus everything
