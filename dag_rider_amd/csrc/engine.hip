@@ -160,11 +160,10 @@ struct dr_ctx {
   // canonical digests, the lowest round to re-emit; canon_lo = lowest round
   // touched since the last cone
   DevBuf Kprev, RG, rlo;
-  // k_commit_split: published S_1 / S_2 words [wave][2][WS], and [wave] barrier
-  // counters | [wave] vote sums | error flag, kept zero between launches
-  DevBuf split_S, split_ctl;
+  // k_commit_split: [wave] arrivals << 32 | |S_3| sum, kept zero between launches
+  DevBuf split_ctl;
   size_t split_nw = 0;
-  int split_cap = 0;  // co-resident k_commit_split workgroups on this device (0: not measured)
+  int split_cap = 0;  // CUs of this device (0: not read yet): ranges shorter than this split
   int commit_split = 1;  // DR_OPT_COMMIT_SPLIT
   int last_split = 0;    // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
@@ -559,49 +558,36 @@ constexpr int sweep_block_m() {
 }
 
 // ---- kernel launch dispatch over the row stride ----
-constexpr int kSplitNT = 512;
-// A short wave range (fewer than ~half the co-resident workgroups): KS workgroups
-// per wave (k_commit_split).  Returns 1 when the range is too long for it (the
-// caller launches k_commit), else a hipError_t; *split = KS.
+constexpr int kSplitNT = 512, kSplitP3 = 2;
+// A short wave range (fewer waves than CUs): KS workgroups per wave
+// (k_commit_split), each deciding S_1, S_2 in full and a share of S_3.  Returns
+// 1 when the range is long enough for one workgroup per wave (the caller
+// launches k_commit), else a hipError_t; *split = KS.
 template <int WS>
 int launch_commit_split_t(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc, int *split) {
   *split = 0;
   if (WS < 2 || !c->commit_split) return 1;
-  const auto kern = dr::k_commit_split<WS, kSplitNT>;
   if (c->split_cap == 0) {
-    int per_cu = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kSplitNT, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev) != hipSuccess)
-      return 1;
-    c->split_cap = std::max(1, per_cu * ncu);
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev) != hipSuccess) return 1;
+    c->split_cap = std::max(1, ncu);
   }
-  const int groups = (nw + 7) / 8;
-  const int ks_min = std::max(2, (c->n + kSplitNT - 1) / kSplitNT);
-  const int KS = std::min(8, c->split_cap / (groups * 8));
-  if (KS < ks_min) return 1;
-  const int RS = ((c->n + KS - 1) / KS + 63) / 64 * 64;
-  if (RS > kSplitNT) return 1;
+  if (nw >= c->split_cap) return 1;
+  using G = dr::Geo<WS, kSplitNT>;
+  const int RS = G::RPP * kSplitP3;  // rows of round 4 per workgroup
+  const int KS = (c->n + RS - 1) / RS;
+  if (KS < 2) return 1;
   if ((size_t)nw > c->split_nw) {  // counters start at zero; the kernel leaves them at zero
     hipError_t e;
-    if ((e = c->split_S.ensure((size_t)nw * 2 * WS * 8)) != hipSuccess) return e;
     if ((e = c->split_ctl.ensure((size_t)nw * 8 + 64)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(c->split_ctl.p, 0, (size_t)nw * 8 + 64, c->stream)) != hipSuccess) return e;
     c->split_nw = (size_t)nw;
   }
-  unsigned *cnt = c->split_ctl.as<unsigned>();
-  int32_t *vacc = reinterpret_cast<int32_t *>(cnt + c->split_nw), *err = vacc + c->split_nw;
-  dr::DagView g = c->view();
-  int quorum = 2 * c->f + 1, ks = KS, rs = RS;
-  u64 *S = c->split_S.as<u64>();
-  void *args[] = {&g, &w0, &nw, &ks, &rs, &quorum, &S, &cnt, &vacc, &err, &cm, &vc};
-  hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(kern), dim3(groups * 8 * KS),
-                                            dim3(kSplitNT), args, 0, c->stream);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return 1;
-  }
+  const int groups = (nw + 7) / 8;
+  hipLaunchKernelGGL((dr::k_commit_split<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0, c->stream,
+                     c->view(), w0, nw, KS, 2 * c->f + 1, c->split_ctl.as<unsigned long long>(), cm, vc);
   *split = KS;
-  return hipSuccess;
+  return hipGetLastError();
 }
 
 template <int WS>
@@ -992,7 +978,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds, &c->plan_out,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
-                    &c->admit_buf, &c->lead, &c->split_S, &c->split_ctl, &c->irr, &c->irr_roff, &c->gscratch,
+                    &c->admit_buf, &c->lead, &c->split_ctl, &c->irr, &c->irr_roff, &c->gscratch,
                     &c->gquery, &c->gaux};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
@@ -2350,15 +2336,7 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
   HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nw));
   HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nw * 4));
-  int32_t split_err = 0;
-  if (c->last_split)
-    HIPCHK(c, c->d2h(&split_err, c->split_ctl.as<char>() + c->split_nw * 8, 4));
   HIPCHK(c, c->sync());
-  if (split_err) {  // a barrier timed out: the counters are left dirty, clear them
-    HIPCHK(c, hipMemsetAsync(c->split_ctl.p, 0, c->split_nw * 8 + 64, c->stream));
-    HIPCHK(c, c->sync());
-    return c->fail(DR_E_HIP, "k_commit_split: a wave's barrier timed out (workgroups not co-resident)");
-  }
   HIPCHK(c, hipEventElapsedTime(&c->last_commit_ms, c->ev[4], c->ev[5]));
   if (ms) *ms = c->last_commit_ms;
   return DR_OK;

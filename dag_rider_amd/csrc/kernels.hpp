@@ -214,28 +214,27 @@ __global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int qu
 // ---------------------------------------------------------------------------
 // k_commit_split: the same commit rule for a short wave range (a rank's share of
 // the all-waves commit sweep leaves most CUs idle with one workgroup per wave):
-// KS workgroups per wave, co-resident (cooperative launch).  Workgroup j of wave
-// w holds rows [j*RS, (j+1)*RS) of the wave's rounds 2..4 (RS a multiple of 64,
-// RS <= NT) and loads every chunk it needs up front -- none depends on S: round
-// 2 the 16-B chunk holding the leader's bit, rounds 3, 4 whole rows.  It
-// publishes its words of S_1, then of S_2, to Sg (disjoint words, no atomics);
-// the KS workgroups of the wave meet at a counter barrier after each.  |S_3| and
-// its repeated-slot count are summed with atomics; the last workgroup to arrive
-// writes commit / vcount and resets the wave's counters for the next launch.
-// A wave's workgroups sit on one XCD: blockIdx = (group * KS + j) * 8 + xcd,
-// wave = group * 8 + xcd.  A barrier that waits 2 s sets *err and every
-// workgroup ends (the host reports it and clears the counters); none hangs.
+// KS workgroups per wave, no barrier between them.  Every workgroup of wave w
+// computes S_1 (the rows of round 2 holding the leader's bit: one 16-B chunk per
+// row) and S_2 (rows of round 3 reaching S_1: the whole round) itself, then its
+// own share of S_3 -- rows [j*RS, (j+1)*RS) of round 4, RS = P3 passes of rows --
+// and adds |S_3 share| (+ its repeated slots) to the wave's sum.  Count and sum
+// share one 64-bit word (arrivals << 32 | votes) added by one atomic, so the
+// last workgroup to arrive holds the complete sum with no fence (an agent-scope
+// release per workgroup would write back the XCD's L2); it writes commit /
+// vcount and zeroes the word.  Every load goes out before the first ballot (none
+// depends on S).
+// The KS workgroups of a wave sit on one XCD (blockIdx = (group*KS + j)*8 + xcd,
+// wave = group*8 + xcd), so the rounds they all read come from one L2.
 // ---------------------------------------------------------------------------
-template <int WS, int NT>
-__global__ __launch_bounds__(NT) void k_commit_split(DagView g, int w0, int nw, int KS, int RS, int quorum,
-                                                     u64 *__restrict__ Sg, unsigned *__restrict__ cnt,
-                                                     int32_t *__restrict__ vacc, int32_t *__restrict__ err,
+template <int WS, int NT, int P3>
+__global__ __launch_bounds__(NT) void k_commit_split(DagView g, int w0, int nw, int KS, int quorum,
+                                                     unsigned long long *__restrict__ acc,
                                                      uint8_t *__restrict__ commit, int32_t *__restrict__ vcount) {
   using G = Geo<WS, NT>;
-  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP;
-  constexpr int MC = (NT * CPR + NT - 1) / NT;  // chunks per thread per round at RS = NT
-  __shared__ u64 S[WS], Tn[WS];
-  __shared__ int bad;
+  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT, NMAX = G::NMAX;
+  constexpr int L1 = (NMAX + NT - 1) / NT;  // round-2 rows per thread
+  __shared__ u64 S1[WS], S2[WS], S3[WS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, grp = slot / KS, j = slot - grp * KS;
   const int bi = grp * 8 + xcd;
@@ -246,122 +245,105 @@ __global__ __launch_bounds__(NT) void k_commit_split(DagView g, int w0, int nw, 
     if (j == 0 && tid == 0) { commit[bi] = 0; vcount[bi] = -1; }
     return;
   }
-  const int s0r = j * RS, s1r = min(n, s0r + RS);
-  // every load first: round 2's leader chunk (thread t: row s0r + t), rounds 3, 4 whole rows
-  const int lc = (l >> 6) / CW;  // chunk column of the leader's word
-  u64 a0 = 0, a1 = 0;
-  if (s0r + tid < s1r) {
-    const u64 *p = g.strong + ((size_t)(r1 + 1) * n + s0r + tid) * WS + lc * CW;
-    if constexpr (CW == 2) {
-      const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
-      a0 = x.x;
-      a1 = x.y;
-    } else {
-      a0 = __builtin_nontemporal_load(p);
-    }
+  // every load first: round 2's leader word of each row, round 3 whole, round 4's share
+  u64 a[L1];
+  const u64 *rows2 = g.strong + (size_t)(r1 + 1) * n * WS + (l >> 6);
+#pragma unroll
+  for (int k = 0; k < L1; k++) {
+    const int s = tid + k * NT;
+    a[k] = s < n ? __builtin_nontemporal_load(rows2 + (size_t)s * WS) : 0ULL;
   }
   const int jj = tid % CPR;
-  u64 v0[2][MC], v1[2][MC];
+  u64 v0[CPT], v1[CPT];
+  const u64 *rows3 = g.strong + (size_t)(r1 + 2) * n * WS;
 #pragma unroll
-  for (int k = 0; k < 2; k++)
-#pragma unroll
-    for (int p = 0; p < MC; p++) {
-      const int s = s0r + tid / CPR + p * RPP;
-      v0[k][p] = 0;
-      v1[k][p] = 0;
-      if (s < s1r) {
-        const u64 *q = g.strong + ((size_t)(r1 + 2 + k) * n + s) * WS + jj * CW;
-        if constexpr (CW == 2) {
-          const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(q));
-          v0[k][p] = x.x;
-          v1[k][p] = x.y;
-        } else {
-          v0[k][p] = __builtin_nontemporal_load(q);
-        }
+  for (int p = 0; p < CPT; p++) {
+    const int s = tid / CPR + p * RPP;
+    v0[p] = 0;
+    v1[p] = 0;
+    if (s < n) {
+      const u64 *q = rows3 + (size_t)s * WS + jj * CW;
+      if constexpr (CW == 2) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(q));
+        v0[p] = x.x;
+        v1[p] = x.y;
+      } else {
+        v0[p] = __builtin_nontemporal_load(q);
       }
     }
-  u64 *S1 = Sg + (size_t)bi * 2 * WS, *S2 = S1 + WS;
-  unsigned target = 0;
-  auto barrier = [&]() -> bool {  // the KS workgroups of wave bi
-    __syncthreads();
-    target += (unsigned)KS;
-    if (tid == 0) {
-      __threadfence();
-      atomicAdd(&cnt[bi], 1u);
-      const unsigned long long t0 = wall_clock64();
-      int e = 0;
-      while (__hip_atomic_load(&cnt[bi], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { e = 1; break; }
-        if (wall_clock64() - t0 > 200000000ULL) {
-          atomicOr(err, 1);
-          e = 1;
-          break;
-        }
-      }
-      bad = e;
-    }
-    __syncthreads();
-    return !bad;
-  };
-  // S_1 = the rows of round 2 holding the leader's bit: this workgroup's words
-  {
-    const u64 x = (CW == 2 && ((l >> 6) & 1)) ? a1 : a0;
-    const u64 m = __ballot(s0r + tid < s1r && ((x >> (l & 63)) & 1ULL));
-    if (lane == 0 && wid * 64 < RS && s0r + wid * 64 < n) S1[(s0r >> 6) + wid] = m;
   }
-  if (!barrier()) return;
-  // S_2, S_3: rows of rounds 3, 4 against the published S_1, S_2
+  u64 u0[P3], u1[P3];
+  const u64 *rows4 = g.strong + (size_t)(r1 + 3) * n * WS;
 #pragma unroll
-  for (int k = 0; k < 2; k++) {
-    if (tid < WS) {
-      S[tid] = __hip_atomic_load(&(k == 0 ? S1 : S2)[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      Tn[tid] = 0;
+  for (int p = 0; p < P3; p++) {
+    const int s = j * P3 * RPP + tid / CPR + p * RPP;
+    u0[p] = 0;
+    u1[p] = 0;
+    if (s < n) {
+      const u64 *q = rows4 + (size_t)s * WS + jj * CW;
+      if constexpr (CW == 2) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(q));
+        u0[p] = x.x;
+        u1[p] = x.y;
+      } else {
+        u0[p] = __builtin_nontemporal_load(q);
+      }
     }
-    __syncthreads();
+  }
+  if (tid < WS) {
+    S1[tid] = 0;
+    S2[tid] = 0;
+    S3[tid] = 0;
+  }
+  __syncthreads();
+  // S_1: a wave's ballot is one word of rows
+#pragma unroll
+  for (int k = 0; k < L1; k++) {
+    const int s0 = wid * 64 + k * NT;
+    const u64 m = __ballot(tid + k * NT < n && ((a[k] >> (l & 63)) & 1ULL));
+    if (lane == 0 && s0 < n && m) S1[s0 >> 6] = m;
+  }
+  __syncthreads();
+  // the rows of a pass that reach S (ballot of CPR-lane groups -> one bit per row)
+  auto pass_bits = [&](u64 x0, u64 x1, const u64 *S) -> u64 {
     const u64 sa = S[jj * CW], sb = CW == 2 ? S[jj * CW + 1] : 0ULL;
+    u64 m = __ballot(((x0 & sa) | (x1 & sb)) != 0ULL);
+    if constexpr (CPR == 1) return m;
+    u64 bits = 0;
 #pragma unroll
-    for (int p = 0; p < MC; p++) {
-      const int rowbase = s0r + (wid * 64) / CPR + p * RPP;  // first row of this wave's pass
-      if (rowbase >= s1r) break;                             // wave-uniform
-      const bool hit = ((v0[k][p] & sa) | (v1[k][p] & sb)) != 0ULL;
-      u64 m = __ballot(hit);
-      if (lane == 0 && m) {
-        u64 bits;
-        if constexpr (CPR == 1) {
-          bits = m;
-        } else {
+    for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
 #pragma unroll
-          for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
-          bits = 0;
+    for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
+    return bits;
+  };
 #pragma unroll
-          for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
-        }
-        atomicOr(&Tn[rowbase >> 6], bits << (rowbase & 63));
-      }
-    }
-    __syncthreads();
-    if (k == 0) {
-      if (tid < RS / 64 && s0r + tid * 64 < n) S2[(s0r >> 6) + tid] = Tn[(s0r >> 6) + tid];
-      if (!barrier()) return;
-    }
+  for (int p = 0; p < CPT; p++) {
+    const int rowbase = (wid * 64) / CPR + p * RPP;  // first row of this wave's pass
+    if (rowbase >= n) break;                         // wave-uniform
+    const u64 bits = pass_bits(v0[p], v1[p], S1);
+    if (lane == 0 && bits) atomicOr(&S2[rowbase >> 6], bits << (rowbase & 63));
   }
-  // |S_3| over this workgroup's rows (+ repeated slots, process.go:330-335), summed over the wave
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < P3; p++) {
+    const int rowbase = j * P3 * RPP + (wid * 64) / CPR + p * RPP;
+    if (rowbase >= n) break;
+    const u64 bits = pass_bits(u0[p], u1[p], S2);
+    if (lane == 0 && bits) atomicOr(&S3[rowbase >> 6], bits << (rowbase & 63));
+  }
+  __syncthreads();
+  // |S_3 share| (+ its repeated slots, process.go:330-335) into the wave's sum
   if (wid == 0) {
-    const int dc = dup_count<WS>(g, r1 + 3, lane < WS ? Tn[lane] : 0ULL);
-    int c = lane < WS ? popc64(Tn[lane]) : 0;
+    const int dc = dup_count<WS>(g, r1 + 3, lane < WS ? S3[lane] : 0ULL);
+    int c = lane < WS ? popc64(S3[lane]) : 0;
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
     if (lane == 0) {
-      atomicAdd(&vacc[bi], c + dc);
-      __threadfence();
-      const unsigned old = atomicAdd(&cnt[bi], 1u);
-      if (old == 3u * (unsigned)KS - 1u) {  // the last of the wave: every sum is in
-        __threadfence();
-        const int vc = __hip_atomic_load(&vacc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long old = atomicAdd(&acc[bi], (1ULL << 32) | (unsigned long long)(c + dc));
+      if ((old >> 32) == (unsigned long long)KS - 1ULL) {  // the last of the wave: every share is in
+        const int vc = (int)(uint32_t)old + c + dc;
         vcount[bi] = vc;
         commit[bi] = vc >= quorum ? 1 : 0;
-        vacc[bi] = 0;
-        cnt[bi] = 0;
+        acc[bi] = 0;
       }
     }
   }

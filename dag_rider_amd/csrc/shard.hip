@@ -567,7 +567,9 @@ struct dr_shard {
   int persistent = 1;  // DR_SHARD_OPT_PERSISTENT
   int memo = 1;        // DR_SHARD_OPT_MEMO
   int stepped = 0;     // DR_SHARD_OPT_STEPPED: the memo replay's stepped form even when every column is here
-  int pass_geo = 0;    // k_ms_pass geometry (tools/shard_replay_bench.py --pass-geo; DR_SHARD_PASS_GEO)
+  int pass_geo = 0;    // k_ms_pass geometry (tuning: DR_SHARD_PASS_GEO)
+  int wu_side = 1;     // k_ms_wu on the side stream beside the pass (tuning: DR_SHARD_WU_SIDE=0 runs it before)
+  int emit_fused = 0;  // REF emission inside the fused sweep (tuning: DR_SHARD_EMIT_FUSED=1)
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
   hipStream_t stream = nullptr;
@@ -595,7 +597,6 @@ struct dr_shard {
   SBuf ppref;                   // [round] |P_1| + .. + |P_r| (present vertices, round 0 excluded)
   std::vector<u64> h_ppref;
   SBuf mSG, mout;               // speculative canonical digests; the memo replay's output region
-  SBuf mctr;                    // last-workgroup counters of k_ms_kcand_canon / k_ms_tail (self-resetting)
   std::vector<std::vector<uint32_t>> h_weak;  // per local shard
   std::vector<std::vector<uint64_t>> h_woff;  // per local shard, absolute offsets, size nrounds+1
   // weak columns per local shard (the memoized replay, shard_memo.hpp): one entry per
@@ -1230,8 +1231,7 @@ __global__ __launch_bounds__(256) void k_ms_vfinal(drs::MArgs a, drs::FArgs f, c
   }
 }
 
-// k_ms_pass at the context's row stride: 1024 threads, two 16-B chunks per
-// thread in flight (k_summary_commit's shipped WS = 16 geometry)
+// k_ms_pass at the context's row stride
 // (k_ms_wu -- WU and the speculative digests, one workgroup per round, latency
 // bound -- runs beside it on the side stream: the pass keeps one 16-wave
 // workgroup per CU streaming rows, the small workgroups fill the other slots)
@@ -1245,25 +1245,32 @@ hipError_t launch_pass_g(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, 
 }
 template <int SP>
 hipError_t launch_pass_t(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
-  if constexpr (SP == 2 || SP == 16) {  // the C4 shapes (G = 8, G = 1): geometry variants for tuning
+  // 512 threads, 8 chunks in flight: at C4, G = 8 (SP 2) 147 us vs 179 us at 1024 x 2,
+  // G = 1 (SP 16) the same (profiles/r04/ pass geometries)
+  if constexpr (SP == 2 || SP == 16) {  // the C4 shapes: the other geometries, for tuning
     switch (c->pass_geo) {
       case 1: return launch_pass_g<SP, 1024, 4>(c, a, f, nw, mode, S1);
       case 2: return launch_pass_g<SP, 512, 4>(c, a, f, nw, mode, S1);
-      case 3: return launch_pass_g<SP, 512, 8>(c, a, f, nw, mode, S1);
+      case 3: return launch_pass_g<SP, 1024, 2>(c, a, f, nw, mode, S1);
     }
   }
-  return launch_pass_g<SP, 1024, 2>(c, a, f, nw, mode, S1);
+  return launch_pass_g<SP, 512, 8>(c, a, f, nw, mode, S1);
 }
 hipError_t launch_pass(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
   const int T = c->nrounds - 1;
   const bool wu = T >= 1;
+  const bool side = wu && c->wu_side;
   if (wu) {
     const size_t lds = std::max<size_t>((size_t)c->nlocal * a.dd * c->SP * 8, 8);
-    if (hipError_t e = hipEventRecord(c->fork, c->stream)) return e;
-    if (hipError_t e = hipStreamWaitEvent(c->side, c->fork, 0)) return e;
-    hipLaunchKernelGGL((drs::k_ms_wu<256>), dim3(T), dim3(256), lds, c->side, a, f, c->mWU.as<u64>());
+    if (side) {
+      if (hipError_t e = hipEventRecord(c->fork, c->stream)) return e;
+      if (hipError_t e = hipStreamWaitEvent(c->side, c->fork, 0)) return e;
+    }
+    hipLaunchKernelGGL((drs::k_ms_wu<256>), dim3(T), dim3(256), lds, side ? c->side : c->stream, a, f,
+                       c->mWU.as<u64>());
     if (hipError_t e = hipGetLastError()) return e;
-    if (hipError_t e = hipEventRecord(c->join, c->side)) return e;
+    if (side)
+      if (hipError_t e = hipEventRecord(c->join, c->side)) return e;
   }
   hipError_t e = hipErrorInvalidValue;
   switch (c->SP) {
@@ -1274,7 +1281,7 @@ hipError_t launch_pass(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, in
     case 16: e = launch_pass_t<16>(c, a, f, nw, mode, S1); break;
     case 32: e = launch_pass_t<32>(c, a, f, nw, mode, S1); break;
   }
-  if (e == hipSuccess && wu) e = hipStreamWaitEvent(c->stream, c->join, 0);
+  if (e == hipSuccess && side) e = hipStreamWaitEvent(c->stream, c->join, 0);
   return e;
 }
 
@@ -1454,7 +1461,9 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   f.qcount = m.qout;
   f.qdigest = m.qout + npop;
   f.qedges = m.qout + 2 * npop;
-  f.emit = fused && !paper ? 1 : 0;  // the fused sweep emits each pop itself
+  // the fused sweep emitting each pop itself (DR_SHARD_EMIT_FUSED=1, tuning): 101 us against
+  // 68 + 22 us as two launches at C4 G = 1 (profiles/r04/)
+  f.emit = fused && !paper && c->emit_fused ? 1 : 0;
   SHCHK(c, hipEventRecord(c->evs[0], c->stream));
   int steps = 0;
   if (fused) {
@@ -1466,14 +1475,20 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     a.push_out = m.push;
     SHCHK(c, launch_pass(c, a, f, nw, drs::VOTE_FULL, (u64 *)nullptr));
     SHCHK(c, hipEventRecord(c->evs[1], c->stream));
-    // K^cand + the canonical walk (last workgroup); digests + prefixes + plan (last workgroup)
-    const int rb16 = (T + 1 + 15) / 16;
+    // K^cand, the canonical walk, the canonical digests and prefixes, the plan (pops and chains).
+    // (As one workgroup's tail of the parallel launch before it -- a done counter behind an
+    // agent-scope fence per workgroup -- these took 108 + 92 us against 40 + 33 us apart:
+    // every fence writes back the XCD's L2; profiles/r04/.)
+    const int rb = (T + 1 + 3) / 4;
     const size_t lds_ring = ((size_t)c->depth * W + 2 * W) * 8;
-    hipLaunchKernelGGL((drs::k_ms_kcand_canon<1024>), dim3(rb16), dim3(1024), lds_ring, c->stream, a, f,
-                       c->mctr.as<int>());
+    hipLaunchKernelGGL(drs::k_ms_kcand_full, dim3(rb), dim3(256), 0, c->stream, a, f);
     SHCHK(c, hipGetLastError());
-    hipLaunchKernelGGL((drs::k_ms_tail<1024>), dim3(rb16), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
-                       (int)pcap, c->mctr.as<int>() + 1);
+    hipLaunchKernelGGL((drs::k_ms_canon_full<512>), dim3(1), dim3(512), lds_ring, c->stream, a, f);
+    SHCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(drs::k_ms_rg_full, dim3(rb), dim3(256), 0, c->stream, a, f);
+    SHCHK(c, hipGetLastError());
+    hipLaunchKernelGGL((drs::k_ms_prefix_plan<1024>), dim3(1), dim3(1024), 0, c->stream, a, f,
+                       c->mq.as<drs::MQuery>(), (int)pcap);
     SHCHK(c, hipGetLastError());
     SHCHK(c, hipEventRecord(c->evs[2], c->stream));
     // every pop and chain to its end, REF pops emitted by their own workgroup
@@ -1712,6 +1727,8 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   while (c->SP < c->WSs) c->SP <<= 1;  // row stride: a power of two (fixed lane -> column maps)
   c->local = id == nullptr;
   if (const char *g = getenv("DR_SHARD_PASS_GEO")) c->pass_geo = atoi(g) & 3;  // tuning only
+  if (const char *g = getenv("DR_SHARD_WU_SIDE")) c->wu_side = atoi(g) != 0;
+  if (const char *g = getenv("DR_SHARD_EMIT_FUSED")) c->emit_fused = atoi(g) != 0;
   c->shard0 = c->local ? 0 : rank;
   c->nlocal = c->local ? nshards : 1;
   c->max_rounds = max_rounds;
@@ -1751,8 +1768,7 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
       c->slot_off.ensure(((size_t)max_rounds + 1) * 4) != hipSuccess ||
       c->lead.ensure(c->h_lead.size() * 2) != hipSuccess ||
       hipMemcpy(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(c->slot_off.p, 0, 4) != hipSuccess || c->mctr.ensure(64) != hipSuccess ||
-      hipMemset(c->mctr.p, 0, 64) != hipSuccess) {
+      hipMemset(c->slot_off.p, 0, 4) != hipSuccess) {
     g_shard_err = "dr_shard_create: device allocation failed";
     dr_shard_destroy(c);
     return DR_E_HIP;

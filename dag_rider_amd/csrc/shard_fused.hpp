@@ -630,30 +630,6 @@ __global__ __launch_bounds__(NT) void k_ms_canon_full(MArgs a, FArgs f) {
   canon_walk<NT>(a, f, lds);
 }
 
-// The last workgroup to finish (counter, self-resetting) of a parallel phase
-// runs the serial step after it: every other workgroup's writes are visible to it
-// after the agent-scope acquire.
-__device__ __forceinline__ bool last_block(int *counter) {
-  __shared__ int s_last;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(counter, 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return false;
-  __threadfence();
-  if (threadIdx.x == 0) *counter = 0;
-  return true;
-}
-
-// K^cand of every round (one wave per round), then the canonical walk in the
-// last workgroup: one launch for k_ms_kcand_full + k_ms_canon_full.
-template <int NT>
-__global__ __launch_bounds__(NT) void k_ms_kcand_canon(MArgs a, FArgs f, int *counter) {
-  extern __shared__ __attribute__((aligned(16))) u64 lds[];
-  kcand_round(a, f, blockIdx.x * (NT / 64) + (threadIdx.x >> 6));
-  if (!last_block(counter)) return;
-  canon_walk<NT>(a, f, lds);
-}
 
 // canonical digest of round r >= 1 (one wave per round): the speculative one
 // below the first round whose position prefix differs from the presence prefix
@@ -791,32 +767,29 @@ __global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__rest
   plan_body<NT>(a, f, q, st0, push_cap, make_pops);
 }
 
-// The canonical digest of every round (one wave per round), then in the last
-// workgroup the prefixes G, E and the plan (pops and chains): one launch for
-// k_ms_rg_full + k_ms_prefix + k_ms_plan.
+// The canonical prefixes G, E (RG, CE -> Gc, Ec) and the plan (pops and chains)
+// in one single-workgroup launch (the fused form: both read only what earlier
+// launches wrote)
 template <int NT>
-__global__ __launch_bounds__(NT) void k_ms_tail(MArgs a, FArgs f, MQuery *__restrict__ q, int push_cap, int *counter) {
+__global__ __launch_bounds__(NT) void k_ms_prefix_plan(MArgs a, FArgs f, MQuery *__restrict__ q, int push_cap) {
   __shared__ u64 part[NT / 64];
-  rg_round(a, f, blockIdx.x * (NT / 64) + (threadIdx.x >> 6));
-  if (!last_block(counter)) return;
   ms_prefix_one<NT>(a.T + 1, f.RG, f.Gc, part);
   ms_prefix_one<NT>(a.T + 1, f.CE, f.Ec, part);
-  __syncthreads();
   plan_body<NT>(a, f, q, (MState *)nullptr, push_cap, 1);
 }
+
 
 // ---------------------------------------------------------------------------
 // k_ms_sweep_full: one workgroup per query, every round to its end (the same
 // decisions as k_ms_step, shard_memo.hpp).  Grid npop + nw: workgroups past the
-// planned chains exit.  Dynamic LDS: ring[depth*W] | FE[W] | Ur[W].
+// planned chains exit.  Dynamic LDS: ring[depth*W] | FE[W].
 //
-// Wave 0 decides each round from words it loaded three rounds ahead and
-// applies, without a workgroup barrier, every round it can expand alone: a full
-// round (ring |= U_r, WU_r from the prefetched words), a round whose frontier is
-// one vertex (the query's top, a chain's restart: that row and its weak
-// columns) and an empty one.  Only a partial round with several vertices is
-// expanded by the whole workgroup (expand_partial_full, U_r staged in LDS; a
-// chain's degree loads issued before the rows).
+// Wave 0 decides each round from words it loaded one round ahead and applies,
+// without a workgroup barrier, every round it can expand alone: a full round
+// (ring |= U_r, WU_r from the prefetched words), a round whose frontier is one
+// vertex (the query's top, a chain's restart: that row and its weak columns)
+// and an empty one.  Only a partial round with several vertices is expanded by
+// the whole workgroup (expand_partial_full).
 // ---------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
@@ -825,9 +798,8 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
   DR_MT(const u64 tt0 = wall_clock64(); u64 tt_wg = 0, n_w0 = 0, n_wg = 0;)
   if (qi >= f.npop + f.hdr[FH_NCHAIN]) return;
   const int W = a.W, dm = a.depth - 1, WSs = a.WSs;
-  u64 *ring = lds, *FE = lds + (size_t)a.depth * W, *Ur = FE + W;
+  u64 *ring = lds, *FE = lds + (size_t)a.depth * W;
   __shared__ int s_ctl[2];
-  __shared__ int64_t s_wc[2];
   __shared__ u64 s_e;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const MQuery Q = a.q[qi];
@@ -841,14 +813,14 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
   int r = Q.top;
   bool merged = false;
   const bool act = lane < W;
-  FRound c0{}, c1{};  // rounds r (wave 0) and r-1, issued at round r
-  if (wv == 0) fload_round(a, r, pop, lane, c0);
+  FRound cur{}, nxt{};
+  if (wv == 0 && act) fload_round(a, r, pop, lane, cur);
   for (;;) {
     if (wv == 0) {
       for (;;) {
-        if (r >= 1) fload_round(a, r - 1, pop, lane, c1);
+        if (act && r >= 1) fload_round(a, r - 1, pop, lane, nxt);
         u64 fw = 0;
-        const u64 p = c0.P;
+        const u64 p = cur.P;
         if (act) {
           u64 *slot = &ring[(size_t)(r & dm) * W + lane];
           fw = *slot;
@@ -857,14 +829,15 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
         int single = r == Q.top ? Q.src0 : -1;  // a round whose frontier is one known vertex
         // waveReady's chain (process.go:342-350): a reachable, present leader of
         // wave wvv is pushed and the chain goes on from it alone
-        const int Lr = c0.L;  // uniform
-        if (!pop && r < Q.top && Lr >= 0) {
-          const u64 fl = __shfl(fw & p, Lr >> 6);
-          if ((fl >> (Lr & 63)) & 1ULL) {
-            fw = lane == (Lr >> 6) ? 1ULL << (Lr & 63) : 0ULL;
-            if (lane == 0) a.push_out[Q.push_base + npush] = ((r - 1) >> 2) + 1;
+        if (!pop && r < Q.top && ((r - 1) & 3) == 0) {
+          const int wvv = ((r - 1) >> 2) + 1;
+          const int L = (wvv < a.nlead ? (int)a.lead[wvv] : 1) - 1;
+          const u64 fl = __shfl(fw & p, L >> 6);
+          if ((fl >> (L & 63)) & 1ULL) {
+            fw = lane == (L >> 6) ? 1ULL << (L & 63) : 0ULL;
+            if (lane == 0) a.push_out[Q.push_base + npush] = wvv;
             npush++;
-            single = Lr;
+            single = L;
           }
         }
         const u64 fe = fw & p;
@@ -874,7 +847,7 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
         if (nz) low = min(low, r - 1);
         bool done;
         if (pop) {
-          run = __ballot(act && fw != c0.K) == 0ULL ? run + 1 : 0;
+          run = __ballot(act && fw != cur.K) == 0ULL ? run + 1 : 0;
           merged = run >= a.dmax;
           done = merged || r <= Q.bottom || (!nz && low >= r);
           if (act) a.masks[Q.mask_off + (int64_t)(Q.top - r) * W + lane] = fw;
@@ -882,6 +855,7 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
           done = r <= Q.bottom || (!nz && low >= r);
         }
         const bool summary = !done && full;
+        if (!pop && !done && summary) edges += a.sdr[r];
         if (!done && pop && anyfe) low = min(low, r - a.dmax);
         if (done) {
           if (lane == 0) {
@@ -890,22 +864,21 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
           }
           break;
         }
-        const bool one = !summary && anyfe && single >= 0 && ((__shfl(fe, single >> 6) >> (single & 63)) & 1ULL);
         if (summary) {  // ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d]
-          if (!pop) edges += __shfl(c0.SD, 0);
           if (act) {
-            ring[(size_t)((r - 1) & dm) * W + lane] |= c0.U;
+            ring[(size_t)((r - 1) & dm) * W + lane] |= cur.U;
             if (weak) {
               const int l = lane / WSs, cw = lane - l * WSs;
               for (int d = 0; d < a.dd; d++) {
                 const int tr = r - d - 2;
                 if (tr < Q.bottom) break;
                 ring[(size_t)(tr & dm) * W + lane] |=
-                    d < FDD ? c0.WU[d] : a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw];
+                    d < FDD ? cur.WU[d] : a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw];
               }
             }
           }
-        } else if (one) {  // FE = {single}: its row (every local shard's piece) and its weak columns
+        } else if (anyfe && single >= 0 && ((__shfl(fe, single >> 6) >> (single & 63)) & 1ULL)) {
+          // FE = {single}: its row (every local shard's piece) and its weak columns
           if (!pop) edges += a.sdeg[(size_t)r * a.n + single];
           if (act) {
             const int l = lane / WSs, cw = lane - l * WSs;
@@ -914,33 +887,26 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
           }
           if (weak)
             for (int l = 0; l < a.nlocal; l++) {
-              const uint64_t wa = a.nlocal == 1 ? c0.C0 : a.wcro[(size_t)l * (a.R + 1) + r];
-              const uint64_t wb = a.nlocal == 1 ? c0.C1 : a.wcro[(size_t)l * (a.R + 1) + r + 1];
-              const uint64_t ja = __shfl((long long)wa, 0), jb = __shfl((long long)wb, 0);
-              for (uint64_t jj = ja + lane; jj < jb; jj += 64) {
-                const uint32_t key = a.wck[jj];
+              const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
+              for (uint64_t jj = c0 + lane; jj < c1; jj += 64) {
                 if (!((a.wcr[jj * W + (single >> 6)] >> (single & 63)) & 1ULL)) continue;
+                const uint32_t key = a.wck[jj];
                 const int tr = r - (int)(key >> 11), cg = (a.shard0 + l) * WSs * 64 + (int)(key & 2047u);
                 if (tr < Q.bottom) continue;
                 atomicOr(&ring[(size_t)(tr & dm) * W + (cg >> 6)], 1ULL << (cg & 63));
               }
             }
         } else if (anyfe) {  // a partial round: the workgroup expands it
-          if (act) {
-            FE[lane] = fe;
-            Ur[lane] = c0.U;
-          }
+          if (act) FE[lane] = fe;
           if (lane == 0) {
             s_ctl[0] = 0;
             s_ctl[1] = r;
-            s_wc[0] = a.nlocal == 1 ? (int64_t)c0.C0 : -1;
-            s_wc[1] = (int64_t)c0.C1;
             s_e = 0;
           }
           break;
         }
         DR_MT(n_w0++;)
-        c0 = c1;
+        cur = nxt;
         --r;
       }
     }
@@ -950,14 +916,14 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
     DR_MT(const u64 tw = wall_clock64();)
     constexpr int KS = 2048 / NT;  // sources per thread (n <= 2048)
     uint16_t dg[KS];
-    if (!pop) {  // the chain's strong degrees of FE, loaded before the rows
+    if (!pop) {  // a chain's strong degrees of FE (the edges it traverses), loaded before the rows
 #pragma unroll
       for (int k = 0; k < KS; k++) {
         const int sv = tid + k * NT;
         dg[k] = (sv < a.n && ((FE[sv >> 6] >> (sv & 63)) & 1ULL)) ? a.sdeg[(size_t)r * a.n + sv] : (uint16_t)0;
       }
     }
-    expand_partial_full<NT>(a, r, Q.bottom, FE, ring, dm, weak, Ur, s_wc[0], s_wc[1]);
+    expand_partial_full<NT>(a, r, Q.bottom, FE, ring, dm, weak);
     if (!pop) {
       u64 e = 0;
 #pragma unroll
@@ -969,7 +935,7 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
     DR_MT(tt_wg += wall_clock64() - tw; n_wg++;)
     if (wv == 0) {
       if (!pop) edges += s_e;
-      c0 = c1;
+      cur = nxt;
     }
     --r;
   }
@@ -992,9 +958,8 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
       t[5] = (u64)Q.type; t[6] = (u64)Q.top; t[7] = (u64)(int64_t)r;
     })
   }
-  if (pop && f.emit) {  // REF emission of this pop here: wave 0's mask rows are at agent scope first
+  if (pop && f.emit) {  // REF emission of this pop here (wave 0's mask rows: same CU, after the barrier)
     static_assert(NT == MS_NT, "ms_emit_query assumes MS_NT threads");
-    if (wv == 0) __threadfence();
     __syncthreads();
     const MState S = s_fin;
     ms_emit_query(a, Q, S, a.slot_off, a.slot_src, f.Cc, f.Gc, f.Ec, qi, f.qcount, f.qdigest, f.qedges);

@@ -583,8 +583,9 @@ __global__ __launch_bounds__(MS_NT) void k_ms_rg(MArgs a, int T, const uint32_t 
 // REF emission of one pop query by one workgroup of MS_NT threads (every thread
 // calls it): the canonical prefix at the cut (C, G, E) plus the query's own
 // rounds cut+1 .. top from its mask rows, 64 rounds at a time (counts, exclusive
-// scan, digests and degrees).  Mask rows are read at agent scope: the fused
-// sweep calls it right after its own wave 0 wrote them.
+// scan, digests and degrees).  The fused sweep calls it right after its own
+// wave 0 wrote the mask rows: a workgroup barrier orders them (one CU, its L1
+// writes through).
 __device__ __forceinline__ void ms_emit_query(const MArgs &a, const MQuery &Q, const MState &S,
                                               const uint32_t *__restrict__ slot_off,
                                               const uint16_t *__restrict__ slot_src, const u64 *__restrict__ Cc,
@@ -610,9 +611,7 @@ __device__ __forceinline__ void ms_emit_query(const MArgs &a, const MQuery &Q, c
   }
   auto mask_word = [&](int y) -> u64 {
     if (lane >= a.W) return 0ULL;
-    const u64 m = __hip_atomic_load(a.masks + Q.mask_off + (int64_t)(top - y) * a.W + lane, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-    return m & a.pres[(size_t)y * a.W + lane];
+    return a.masks[Q.mask_off + (int64_t)(top - y) * a.W + lane] & a.pres[(size_t)y * a.W + lane];
   };
   u64 run = Cc[cut];
   for (int y0 = lo; y0 <= top; y0 += 64) {
