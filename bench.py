@@ -375,8 +375,8 @@ def rank_share(cfg, d, rank: int, world: int, local: int, iters: int, dist=None)
     sub = wave_slice(d, w0, w1)
     with Engine(cfg.n, cfg.faulty, sub.nrounds, local) as e:
         e.append_packed(sub)
-        if os.environ.get("DR_BENCH_COMMIT_SPLIT") == "0":  # tuning: k_commit, one workgroup per wave
-            e.set_commit_split(False)
+        if os.environ.get("DR_BENCH_COMMIT_SPLIT"):  # tuning: 0 k_commit, 1 one launch, 2 two launches
+            e.set_commit_split(int(os.environ["DR_BENCH_COMMIT_SPLIT"]))
         cm, vc = e.wave_commit(1, w1 - w0 + 1)
         torch.cuda.synchronize()
         if dist:

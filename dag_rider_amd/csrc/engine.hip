@@ -161,7 +161,7 @@ struct dr_ctx {
   // touched since the last cone
   DevBuf Kprev, RG, rlo;
   // k_commit_split: [wave] arrivals << 32 | |S_3| sum, kept zero between launches
-  DevBuf split_ctl;
+  DevBuf split_ctl, split_S2;  // split_S2: [wave][WS] S_2 of the two-launch form
   size_t split_nw = 0;
   int split_cap = 0;  // CUs of this device (0: not read yet): ranges shorter than this split
   int commit_split = 1;  // DR_OPT_COMMIT_SPLIT
@@ -584,8 +584,18 @@ int launch_commit_split_t(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc, i
     c->split_nw = (size_t)nw;
   }
   const int groups = (nw + 7) / 8;
-  hipLaunchKernelGGL((dr::k_commit_split<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0, c->stream,
-                     c->view(), w0, nw, KS, 2 * c->f + 1, c->split_ctl.as<unsigned long long>(), cm, vc);
+  if (c->commit_split == 2) {  // two launches: S_2 shares to memory, then S_3 shares (tuning)
+    if (hipError_t e = c->split_S2.ensure((size_t)nw * WS * 8)) return e;
+    hipLaunchKernelGGL((dr::k_commit_s2<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0, c->stream,
+                       c->view(), w0, nw, KS, c->split_S2.as<u64>(), cm, vc);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL((dr::k_commit_s3<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0, c->stream,
+                       c->view(), w0, nw, KS, 2 * c->f + 1, (const u64 *)c->split_S2.as<u64>(),
+                       c->split_ctl.as<unsigned long long>(), cm, vc);
+  } else {
+    hipLaunchKernelGGL((dr::k_commit_split<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0,
+                       c->stream, c->view(), w0, nw, KS, 2 * c->f + 1, c->split_ctl.as<unsigned long long>(), cm, vc);
+  }
   *split = KS;
   return hipGetLastError();
 }
@@ -978,7 +988,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds, &c->plan_out,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
-                    &c->admit_buf, &c->lead, &c->split_ctl, &c->irr, &c->irr_roff, &c->gscratch,
+                    &c->admit_buf, &c->lead, &c->split_ctl, &c->split_S2, &c->irr, &c->irr_roff, &c->gscratch,
                     &c->gquery, &c->gaux};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
@@ -1777,7 +1787,8 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     return DR_OK;
   }
   if (option == DR_OPT_COMMIT_SPLIT) {
-    c->commit_split = value ? 1 : 0;
+    if (value < 0 || value > 2) return c->fail(DR_E_INVAL, "DR_OPT_COMMIT_SPLIT is 0, 1 or 2");
+    c->commit_split = value;
     return DR_OK;
   }
   if (option == DR_OPT_BATCH_FORM) {

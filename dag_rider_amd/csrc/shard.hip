@@ -1239,8 +1239,12 @@ template <int SP, int NT, int GR>
 hipError_t launch_pass_g(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
   const int T = c->nrounds - 1, nl = c->nlocal;
   const size_t lds = ((size_t)2 * nl * SP + c->W) * 8;
-  hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR>), dim3((T + 3) / 4), dim3(NT), lds, c->stream, a, f, nw, mode,
-                     c->mU.as<u64>(), S1);
+  if (nl == 1)
+    hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR, true>), dim3((T + 3) / 4), dim3(NT), lds, c->stream, a, f, nw, mode,
+                       c->mU.as<u64>(), S1);
+  else
+    hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR, false>), dim3((T + 3) / 4), dim3(NT), lds, c->stream, a, f, nw,
+                       mode, c->mU.as<u64>(), S1);
   return hipGetLastError();
 }
 template <int SP>

@@ -162,13 +162,16 @@ __global__ __launch_bounds__(NT) void k_ms_wu(MArgs a, FArgs f, u64 *__restrict_
 // time (nontemporal: each row is read once); a shard's U column is reduced when
 // its last pass is consumed (the pass index is uniform over the workgroup).
 // ---------------------------------------------------------------------------
-template <int SP, int NT, int GR>
+// ONE: the context holds one shard (G = 1 fused, or one rank of an RCCL group):
+// the element index is the pass, and the S chunk a thread tests is read once per
+// round.
+template <int SP, int NT, int GR, bool ONE>
 __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int vote_mode, u64 *__restrict__ U,
                                                 u64 *__restrict__ S1out) {
   constexpr int CW = SP >= 2 ? 2 : 1, CPR = SP / CW, RPP = NT / CPR;
   static_assert(NT % 64 == 0 && NT % CPR == 0 && CPR <= 16, "block must tile rows");
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
-  const int NL = a.nlocal, W = a.W, WSs = a.WSs, n = a.n, T = a.T;
+  const int NL = ONE ? 1 : a.nlocal, W = a.W, WSs = a.WSs, n = a.n, T = a.T;
   u64 *sU = lds, *Sp = lds + NL * SP, *Tn = Sp + NL * SP;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, j = tid % CPR, row0 = tid / CPR;
   const int w = blockIdx.x + 1, r1 = 4 * (w - 1) + 1;
@@ -189,6 +192,11 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
     const bool test = leader && k >= 1 && (vote_mode == VOTE_FULL || k == 1);
     const u64 *rbase = a.strong + (size_t)r * a.strong_rstride + (size_t)row0 * SP + j * CW;
     u64 a0 = 0, a1 = 0;
+    u64 t0 = 0, t1 = 0;  // ONE: this thread's chunk of S_{k-1}
+    if (ONE && test) {
+      t0 = Sp[j * CW];
+      t1 = CW == 2 ? Sp[j * CW + 1] : 0ULL;
+    }
     int lc = 0, pc = 0;  // (shard, pass) of element e0, carried from group to group
     for (int e0 = 0; e0 < E; e0 += GR) {
       u64 x0[GR], x1[GR];
@@ -222,7 +230,7 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
         a0 |= x0[q];
         a1 |= x1[q];
         if (test) {  // rows of round r reaching S_{k-1} on this shard's columns
-          const u64 s0 = Sp[l * SP + j * CW], s1 = CW == 2 ? Sp[l * SP + j * CW + 1] : 0ULL;
+          const u64 s0 = ONE ? t0 : Sp[l * SP + j * CW], s1 = ONE ? t1 : (CW == 2 ? Sp[l * SP + j * CW + 1] : 0ULL);
           u64 m = __ballot(((x0[q] & s0) | (x1[q] & s1)) != 0ULL);
           const int rowbase = (wid * 64) / CPR + p * RPP;  // the wave's first row
           if (lane == 0 && m && rowbase < n) {

@@ -94,9 +94,10 @@ class Engine:
         """DR_OPT_DEVICE_PLAN: plan dr_replay's phases on the device (identical results either way)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_DEVICE_PLAN, int(on)))
 
-    def set_commit_split(self, on: bool):
-        """DR_OPT_COMMIT_SPLIT: several workgroups per wave for short wave ranges (identical results)."""
-        self._check(self._L.dr_set_option(self._h, L.DR_OPT_COMMIT_SPLIT, int(on)))
+    def set_commit_split(self, mode: int):
+        """DR_OPT_COMMIT_SPLIT: several workgroups per wave for short wave ranges (0 off, 1 one
+        launch, 2 two launches; identical results)."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_COMMIT_SPLIT, int(mode)))
 
     def set_batch_form(self, form: int):
         """DR_OPT_BATCH_FORM (read from a batch's first engine): DR_BATCH_AUTO, DR_BATCH_WORKGROUP

@@ -99,9 +99,10 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * DR_BATCH_WAVE = one wavefront per DAG (most DAGs per CU); AUTO takes the
  * wave form when the batch holds more than 6 DAGs per CU of the device.
  * DR_OPT_COMMIT_SPLIT (default 1): dr_wave_commit / dr_wave_ready on a wave
- * range too short to fill the device split each wave's vote over several
- * co-resident workgroups that meet at a barrier after S_1 and S_2; 0 = one
- * workgroup per wave (identical results).
+ * range shorter than the device's CU count split each wave's vote over several
+ * workgroups: 1 = one launch (each computes S_1, S_2 whole and a share of S_3),
+ * 2 = two launches (S_2 shares to memory, then S_3 shares); 0 = one workgroup
+ * per wave.  Identical results.
  * Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 

@@ -78,15 +78,16 @@ def test_commit_split_kernel(gpu_device, n):
             e.append_packed(d)
             if coin:
                 e.set_leader_coin(L.DR_LEADER_SEEDED, 5 + n)
-            e.set_commit_split(False)
+            e.set_commit_split(0)
             want_c, want_v = e.wave_commit(1, nw)
             want1 = [e.wave_commit(w, w) for w in range(1, nw + 1)]
-            e.set_commit_split(True)
-            for w0, w1 in ((1, nw), (1, 1), (3, 9), (nw - 4, nw), (2, nw - 1)):
-                for _ in range(2):  # the kernel leaves its barrier counters ready for the next launch
-                    cm, vc = e.wave_commit(w0, w1)
-                    assert (cm == want_c[w0 - 1:w1]).all() and (vc == want_v[w0 - 1:w1]).all(), (w0, w1)
-            for w in range(1, nw + 1):
-                cm, vc = e.wave_commit(w, w)
-                assert cm[0] == want1[w - 1][0][0] and vc[0] == want1[w - 1][1][0], w
-                assert e.wave_ready(w, max(0, w - 3))[:2] == (bool(cm[0]), int(vc[0]))
+            for mode in (1, 2):  # one launch; two launches (S_2 shares through memory)
+                e.set_commit_split(mode)
+                for w0, w1 in ((1, nw), (1, 1), (3, 9), (nw - 4, nw), (2, nw - 1)):
+                    for _ in range(2):  # the kernel leaves its arrival counters zero for the next launch
+                        cm, vc = e.wave_commit(w0, w1)
+                        assert (cm == want_c[w0 - 1:w1]).all() and (vc == want_v[w0 - 1:w1]).all(), (mode, w0, w1)
+                for w in range(1, nw + 1):
+                    cm, vc = e.wave_commit(w, w)
+                    assert cm[0] == want1[w - 1][0][0] and vc[0] == want1[w - 1][1][0], (mode, w)
+                    assert e.wave_ready(w, max(0, w - 3))[:2] == (bool(cm[0]), int(vc[0]))
