@@ -375,7 +375,7 @@ def rank_share(cfg, d, rank: int, world: int, local: int, iters: int, dist=None)
     sub = wave_slice(d, w0, w1)
     with Engine(cfg.n, cfg.faulty, sub.nrounds, local) as e:
         e.append_packed(sub)
-        if os.environ.get("DR_BENCH_COMMIT_SPLIT"):  # tuning: 0 k_commit, 1 one launch, 2 two launches
+        if os.environ.get("DR_BENCH_COMMIT_SPLIT"):  # tuning: 1 = k_commit_split (default 0, k_commit)
             e.set_commit_split(int(os.environ["DR_BENCH_COMMIT_SPLIT"]))
         cm, vc = e.wave_commit(1, w1 - w0 + 1)
         torch.cuda.synchronize()

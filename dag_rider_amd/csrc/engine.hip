@@ -161,10 +161,12 @@ struct dr_ctx {
   // touched since the last cone
   DevBuf Kprev, RG, rlo;
   // k_commit_split: [wave] arrivals << 32 | |S_3| sum, kept zero between launches
-  DevBuf split_ctl, split_S2;  // split_S2: [wave][WS] S_2 of the two-launch form
+  DevBuf split_ctl;
   size_t split_nw = 0;
   int split_cap = 0;  // CUs of this device (0: not read yet): ranges shorter than this split
-  int commit_split = 1;  // DR_OPT_COMMIT_SPLIT
+  // DR_OPT_COMMIT_SPLIT: off by default -- at C4's N = 8 share (125 waves) k_commit_split
+  // took 29 us against 22 us for k_commit, one workgroup per wave (profiles/r04/)
+  int commit_split = 0;
   int last_split = 0;    // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
   bool kprev_ok = false;
@@ -584,18 +586,8 @@ int launch_commit_split_t(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc, i
     c->split_nw = (size_t)nw;
   }
   const int groups = (nw + 7) / 8;
-  if (c->commit_split == 2) {  // two launches: S_2 shares to memory, then S_3 shares (tuning)
-    if (hipError_t e = c->split_S2.ensure((size_t)nw * WS * 8)) return e;
-    hipLaunchKernelGGL((dr::k_commit_s2<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0, c->stream,
-                       c->view(), w0, nw, KS, c->split_S2.as<u64>(), cm, vc);
-    if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL((dr::k_commit_s3<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0, c->stream,
-                       c->view(), w0, nw, KS, 2 * c->f + 1, (const u64 *)c->split_S2.as<u64>(),
-                       c->split_ctl.as<unsigned long long>(), cm, vc);
-  } else {
-    hipLaunchKernelGGL((dr::k_commit_split<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0,
-                       c->stream, c->view(), w0, nw, KS, 2 * c->f + 1, c->split_ctl.as<unsigned long long>(), cm, vc);
-  }
+  hipLaunchKernelGGL((dr::k_commit_split<WS, kSplitNT, kSplitP3>), dim3(groups * 8 * KS), dim3(kSplitNT), 0,
+                     c->stream, c->view(), w0, nw, KS, 2 * c->f + 1, c->split_ctl.as<unsigned long long>(), cm, vc);
   *split = KS;
   return hipGetLastError();
 }
@@ -988,7 +980,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
                     &c->Cc,      &c->Gc,      &c->Ec,       &c->crbase,   &c->ccount,
                     &c->nseg,    &c->stops,   &c->qstats, &c->plan_arena, &c->batch_arena, &c->srounds, &c->plan_out,
                     &c->wc_key,  &c->wc_rows, &c->wc_roff, &c->sdeg, &c->setweak, &c->wdeg,
-                    &c->admit_buf, &c->lead, &c->split_ctl, &c->split_S2, &c->irr, &c->irr_roff, &c->gscratch,
+                    &c->admit_buf, &c->lead, &c->split_ctl, &c->irr, &c->irr_roff, &c->gscratch,
                     &c->gquery, &c->gaux};
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
@@ -1787,8 +1779,7 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     return DR_OK;
   }
   if (option == DR_OPT_COMMIT_SPLIT) {
-    if (value < 0 || value > 2) return c->fail(DR_E_INVAL, "DR_OPT_COMMIT_SPLIT is 0, 1 or 2");
-    c->commit_split = value;
+    c->commit_split = value ? 1 : 0;
     return DR_OK;
   }
   if (option == DR_OPT_BATCH_FORM) {

@@ -349,165 +349,6 @@ __global__ __launch_bounds__(NT) void k_commit_split(DagView g, int w0, int nw, 
   }
 }
 
-// The commit rule for a short wave range in two launches, no row read twice:
-// k_commit_s2 -- KS workgroups per wave (XCD-grouped as k_commit_split), each
-// computing S_1 whole (one 16-B chunk per row of round 2) and S_2 for its share
-// of round 3's rows (P3 passes of 64 rows: whole words), written to S2g; then
-// k_commit_s3 -- the same workgroups, S_3 for their share of round 4 against
-// the S_2 words of the first launch, summed as in k_commit_split.
-template <int WS, int NT, int P3>
-__global__ __launch_bounds__(NT) void k_commit_s2(DagView g, int w0, int nw, int KS, u64 *__restrict__ S2g,
-                                                  uint8_t *__restrict__ commit, int32_t *__restrict__ vcount) {
-  using G = Geo<WS, NT>;
-  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, NMAX = G::NMAX;
-  constexpr int L1 = (NMAX + NT - 1) / NT;
-  static_assert((P3 * RPP) % 64 == 0, "a share is whole words of rows");
-  __shared__ u64 S1[WS], T2[WS];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, grp = slot / KS, j = slot - grp * KS;
-  const int bi = grp * 8 + xcd;
-  if (bi >= nw) return;
-  const int w = w0 + bi, r1 = 4 * (w - 1) + 1, n = g.n;
-  const int l = g.lead[w] - 1;
-  if (!((g.present[(size_t)r1 * WS + (l >> 6)] >> (l & 63)) & 1ULL)) {  // leader is bottom (process.go:327-329)
-    if (j == 0 && tid == 0) { commit[bi] = 0; vcount[bi] = -1; }
-    return;
-  }
-  u64 a[L1];
-  const u64 *rows2 = g.strong + (size_t)(r1 + 1) * n * WS + (l >> 6);
-#pragma unroll
-  for (int k = 0; k < L1; k++) {
-    const int s = tid + k * NT;
-    a[k] = s < n ? __builtin_nontemporal_load(rows2 + (size_t)s * WS) : 0ULL;
-  }
-  const int jj = tid % CPR;
-  u64 v0[P3], v1[P3];
-  const u64 *rows3 = g.strong + (size_t)(r1 + 2) * n * WS;
-#pragma unroll
-  for (int p = 0; p < P3; p++) {
-    const int s = j * P3 * RPP + tid / CPR + p * RPP;
-    v0[p] = 0;
-    v1[p] = 0;
-    if (s < n) {
-      const u64 *q = rows3 + (size_t)s * WS + jj * CW;
-      if constexpr (CW == 2) {
-        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(q));
-        v0[p] = x.x;
-        v1[p] = x.y;
-      } else {
-        v0[p] = __builtin_nontemporal_load(q);
-      }
-    }
-  }
-  if (tid < WS) {
-    S1[tid] = 0;
-    T2[tid] = 0;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < L1; k++) {
-    const int s0 = wid * 64 + k * NT;
-    const u64 m = __ballot(tid + k * NT < n && ((a[k] >> (l & 63)) & 1ULL));
-    if (lane == 0 && s0 < n && m) S1[s0 >> 6] = m;
-  }
-  __syncthreads();
-  const u64 sa = S1[jj * CW], sb = CW == 2 ? S1[jj * CW + 1] : 0ULL;
-#pragma unroll
-  for (int p = 0; p < P3; p++) {
-    const int rowbase = j * P3 * RPP + (wid * 64) / CPR + p * RPP;
-    if (rowbase >= n) break;
-    u64 m = __ballot(((v0[p] & sa) | (v1[p] & sb)) != 0ULL);
-    if (lane == 0 && m) {
-      u64 bits = m;
-      if constexpr (CPR > 1) {
-#pragma unroll
-        for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
-        bits = 0;
-#pragma unroll
-        for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
-      }
-      atomicOr(&T2[rowbase >> 6], bits << (rowbase & 63));
-    }
-  }
-  __syncthreads();
-  // this share's words of S_2 (rows j*P3*RPP ..): whole words, no other workgroup writes them
-  const int wa = j * P3 * RPP / 64, wb = min(WS, (j + 1) * P3 * RPP / 64);
-  if (tid < wb - wa) S2g[(size_t)bi * WS + wa + tid] = T2[wa + tid];
-}
-
-template <int WS, int NT, int P3>
-__global__ __launch_bounds__(NT) void k_commit_s3(DagView g, int w0, int nw, int KS, int quorum,
-                                                  const u64 *__restrict__ S2g, unsigned long long *__restrict__ acc,
-                                                  uint8_t *__restrict__ commit, int32_t *__restrict__ vcount) {
-  using G = Geo<WS, NT>;
-  constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP;
-  __shared__ u64 S2[WS], S3[WS];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, grp = slot / KS, j = slot - grp * KS;
-  const int bi = grp * 8 + xcd;
-  if (bi >= nw) return;
-  const int w = w0 + bi, r1 = 4 * (w - 1) + 1, n = g.n;
-  const int l = g.lead[w] - 1;
-  if (!((g.present[(size_t)r1 * WS + (l >> 6)] >> (l & 63)) & 1ULL)) return;  // decided by k_commit_s2
-  const int jj = tid % CPR;
-  u64 u0[P3], u1[P3];
-  const u64 *rows4 = g.strong + (size_t)(r1 + 3) * n * WS;
-#pragma unroll
-  for (int p = 0; p < P3; p++) {
-    const int s = j * P3 * RPP + tid / CPR + p * RPP;
-    u0[p] = 0;
-    u1[p] = 0;
-    if (s < n) {
-      const u64 *q = rows4 + (size_t)s * WS + jj * CW;
-      if constexpr (CW == 2) {
-        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(q));
-        u0[p] = x.x;
-        u1[p] = x.y;
-      } else {
-        u0[p] = __builtin_nontemporal_load(q);
-      }
-    }
-  }
-  if (tid < WS) {
-    S2[tid] = S2g[(size_t)bi * WS + tid];
-    S3[tid] = 0;
-  }
-  __syncthreads();
-  const u64 sa = S2[jj * CW], sb = CW == 2 ? S2[jj * CW + 1] : 0ULL;
-#pragma unroll
-  for (int p = 0; p < P3; p++) {
-    const int rowbase = j * P3 * RPP + (wid * 64) / CPR + p * RPP;
-    if (rowbase >= n) break;
-    u64 m = __ballot(((u0[p] & sa) | (u1[p] & sb)) != 0ULL);
-    if (lane == 0 && m) {
-      u64 bits = m;
-      if constexpr (CPR > 1) {
-#pragma unroll
-        for (int sh = 1; sh < CPR; sh <<= 1) m |= m >> sh;
-        bits = 0;
-#pragma unroll
-        for (int gI = 0; gI < 64 / CPR; gI++) bits |= ((m >> (gI * CPR)) & 1ULL) << gI;
-      }
-      atomicOr(&S3[rowbase >> 6], bits << (rowbase & 63));
-    }
-  }
-  __syncthreads();
-  if (wid == 0) {
-    const int dc = dup_count<WS>(g, r1 + 3, lane < WS ? S3[lane] : 0ULL);
-    int c = lane < WS ? popc64(S3[lane]) : 0;
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-    if (lane == 0) {
-      const unsigned long long old = atomicAdd(&acc[bi], (1ULL << 32) | (unsigned long long)(c + dc));
-      if ((old >> 32) == (unsigned long long)KS - 1ULL) {
-        const int vc = (int)(uint32_t)old + c + dc;
-        vcount[bi] = vc;
-        commit[bi] = vc >= quorum ? 1 : 0;
-        acc[bi] = 0;
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Round summaries (memo): per round r, U_r = OR of every strong row, WU_r[d] =
 // union of the weak targets at delta d+2, SD_r = total strong degree.  A sweep

@@ -55,6 +55,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -568,7 +569,10 @@ struct dr_shard {
   int memo = 1;        // DR_SHARD_OPT_MEMO
   int stepped = 0;     // DR_SHARD_OPT_STEPPED: the memo replay's stepped form even when every column is here
   int pass_geo = 0;    // k_ms_pass geometry (tuning: DR_SHARD_PASS_GEO)
-  int wu_side = 1;     // k_ms_wu on the side stream beside the pass (tuning: DR_SHARD_WU_SIDE=0 runs it before)
+  // k_ms_wu on the side stream beside the pass (tuning: DR_SHARD_WU_SIDE=1); by default
+  // before it on the main stream: C4 G = 1 0.348 vs 0.358 ms, G = 8 0.380 vs 0.398 ms, the
+  // pass's workgroups queue behind the side stream's (profiles/r04/)
+  int wu_side = 0;
   int emit_fused = 0;  // REF emission inside the fused sweep (tuning: DR_SHARD_EMIT_FUSED=1)
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
@@ -1406,6 +1410,9 @@ int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int
 // and chain, the emission: eight launches and one copy back.  Stepped form:
 // stepped_phase.  REF emission k_ms_emit; PAPER paper_emit after the copy.
 int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
+  const auto th0 = std::chrono::steady_clock::now();
+  static const bool th_on = getenv("DR_SHARD_HOST_TIMING") != nullptr;  // investigation only
+  std::chrono::steady_clock::time_point th1 = th0, th2 = th0, th3 = th0;
   const bool paper = deliver_mode == DR_DELIVER_PAPER, persistent = chain_mode == DR_CHAIN_PERSISTENT;
   const bool fused = c->nlocal == c->G && !c->stepped;
   const int T = c->nrounds - 1, W = c->W, nw = nwaves;
@@ -1469,6 +1476,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   // 68 + 22 us as two launches at C4 G = 1 (profiles/r04/)
   f.emit = fused && !paper && c->emit_fused ? 1 : 0;
   SHCHK(c, hipEventRecord(c->evs[0], c->stream));
+  th1 = std::chrono::steady_clock::now();
   int steps = 0;
   if (fused) {
     SHCHK(c, c->mq.ensure((size_t)std::max(nq, 1) * sizeof(drs::MQuery)));  // pops and chains: k_ms_plan
@@ -1516,7 +1524,9 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   char *hb = stage(c, m.bytes);
   if (!hb) return c->fail(DR_E_HIP, "pinned staging allocation failed");
   SHCHK(c, hipMemcpyAsync(hb, c->mout.p, m.bytes, hipMemcpyDeviceToHost, c->stream));
+  th2 = std::chrono::steady_clock::now();
   SHCHK(c, hipStreamSynchronize(c->stream));
+  th3 = std::chrono::steady_clock::now();
   const MOut h = carve_out(hb, nw, nq, pcap, npop);
   SHCHK(c, hipEventElapsedTime(&o->ms_commit, c->evs[0], c->evs[1]));
   SHCHK(c, hipEventElapsedTime(&o->ms_summary, c->evs[1], c->evs[2]));
@@ -1623,6 +1633,13 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   o->sweep_count = (uint64_t)npop;
   o->sweep_partial = (uint64_t)steps;
   c->last_rounds = (uint64_t)steps;
+  if (th_on) {
+    auto us = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
+      return std::chrono::duration<double, std::micro>(y - x).count();
+    };
+    fprintf(stderr, "[shard host] prep %.1f us, enqueue %.1f us, wait %.1f us, assemble %.1f us, %zu B back\n",
+            us(th0, th1), us(th1, th2), us(th2, th3), us(th3, std::chrono::steady_clock::now()), m.bytes);
+  }
   return DR_OK;
 }
 

@@ -352,6 +352,12 @@ __device__ __forceinline__ void expand_partial_full(const MArgs &a, int r, int b
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int SP = a.SP, W = a.W, WSs = a.WSs, NL = a.nlocal, WP = NL * SP;
   u64 *dst = ring + (size_t)((r - 1) & dm) * W;
+  // one local shard: its weak-column range goes out with the U word and the rows
+  // (the columns' loads then wait on one memory latency, not two)
+  if (weak && NL == 1 && wc0 < 0) {
+    wc0 = (int64_t)a.wcro[r];
+    wc1 = (int64_t)a.wcro[r + 1];
+  }
   if (WP <= 64 && (64 % WP) == 0) {
     const int l0 = (lane % WP) / SP, c0 = lane % SP;  // this lane's word of the concatenated row
     const u64 *base = a.strong + (size_t)r * a.strong_rstride + (size_t)l0 * a.strong_stride + c0;
@@ -457,6 +463,8 @@ struct FRound {
 };
 // Every lane of wave 0 calls it (lanes >= W load nothing), so no part of the
 // record is assigned under a lane-divergent branch.
+// EXTRA: also the weak range, SD and the wave leader (the canonical walk uses the range).
+template <bool EXTRA = true>
 __device__ __forceinline__ void fload_round(const MArgs &a, int r, bool pop, int w, FRound &x, bool wantK = true) {
   const bool on = w < a.W;
   const int l = on ? w / a.WSs : 0, cw = on ? w - l * a.WSs : 0;
@@ -466,11 +474,13 @@ __device__ __forceinline__ void fload_round(const MArgs &a, int r, bool pop, int
   x.U = on ? a.U[ub * a.SP + cw] : 0ULL;
 #pragma unroll
   for (int d = 0; d < FDD; d++) x.WU[d] = (on && pop && d < a.dd) ? a.WU[(ub * a.dd + d) * a.SP + cw] : 0ULL;
-  x.C0 = (pop && a.nlocal == 1) ? a.wcro[r] : 0;
-  x.C1 = (pop && a.nlocal == 1) ? a.wcro[r + 1] : 0;
-  x.SD = pop ? 0ULL : a.sdr[r];
-  const int wvv = ((r - 1) >> 2) + 1;
-  x.L = (!pop && r >= 1 && ((r - 1) & 3) == 0) ? (wvv < a.nlead ? (int)a.lead[wvv] : 1) - 1 : -1;
+  if constexpr (EXTRA) {
+    x.C0 = (pop && a.nlocal == 1) ? a.wcro[r] : 0;
+    x.C1 = (pop && a.nlocal == 1) ? a.wcro[r + 1] : 0;
+    x.SD = pop ? 0ULL : a.sdr[r];
+    const int wvv = ((r - 1) >> 2) + 1;
+    x.L = (!pop && r >= 1 && ((r - 1) & 3) == 0) ? (wvv < a.nlead ? (int)a.lead[wvv] : 1) - 1 : -1;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -799,8 +809,10 @@ __global__ __launch_bounds__(NT) void k_ms_prefix_plan(MArgs a, FArgs f, MQuery 
 // and an empty one.  Only a partial round with several vertices is expanded by
 // the whole workgroup (expand_partial_full).
 // ---------------------------------------------------------------------------
+// (4 waves per SIMD: every C4 query resident at once -- at 130 VGPRs, 3 per SIMD, the
+// last quarter of the pops started after the first had finished, profiles/r04/)
 template <int NT>
-__global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_ms_sweep_full(MArgs a, FArgs f) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   const int qi = blockIdx.x;
   DR_MT(const u64 tt0 = wall_clock64(); u64 tt_wg = 0, n_w0 = 0, n_wg = 0;)
@@ -821,12 +833,15 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
   int r = Q.top;
   bool merged = false;
   const bool act = lane < W;
-  FRound cur{}, nxt{};
-  if (wv == 0 && act) fload_round(a, r, pop, lane, cur);
+  FRound cur{}, nxt{}, nx2{};  // wave 0: rounds r, r-1 (loaded), r-2 (issued at round r)
+  if (wv == 0 && act) {
+    fload_round<false>(a, r, pop, lane, cur);
+    if (r >= 1) fload_round<false>(a, r - 1, pop, lane, nxt);
+  }
   for (;;) {
     if (wv == 0) {
       for (;;) {
-        if (act && r >= 1) fload_round(a, r - 1, pop, lane, nxt);
+        if (act && r >= 2) fload_round<false>(a, r - 2, pop, lane, nx2);
         u64 fw = 0;
         const u64 p = cur.P;
         if (act) {
@@ -915,6 +930,7 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
         }
         DR_MT(n_w0++;)
         cur = nxt;
+        nxt = nx2;
         --r;
       }
     }
@@ -944,6 +960,7 @@ __global__ __launch_bounds__(NT) void k_ms_sweep_full(MArgs a, FArgs f) {
     if (wv == 0) {
       if (!pop) edges += s_e;
       cur = nxt;
+      nxt = nx2;
     }
     --r;
   }

@@ -95,8 +95,8 @@ class Engine:
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_DEVICE_PLAN, int(on)))
 
     def set_commit_split(self, mode: int):
-        """DR_OPT_COMMIT_SPLIT: several workgroups per wave for short wave ranges (0 off, 1 one
-        launch, 2 two launches; identical results)."""
+        """DR_OPT_COMMIT_SPLIT: several workgroups per wave for short wave ranges (1; 0 = one
+        workgroup per wave, the default; identical results)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_COMMIT_SPLIT, int(mode)))
 
     def set_batch_form(self, form: int):

@@ -98,11 +98,11 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * one workgroup of four wavefronts per DAG (shortest time per DAG),
  * DR_BATCH_WAVE = one wavefront per DAG (most DAGs per CU); AUTO takes the
  * wave form when the batch holds more than 6 DAGs per CU of the device.
- * DR_OPT_COMMIT_SPLIT (default 1): dr_wave_commit / dr_wave_ready on a wave
- * range shorter than the device's CU count split each wave's vote over several
- * workgroups: 1 = one launch (each computes S_1, S_2 whole and a share of S_3),
- * 2 = two launches (S_2 shares to memory, then S_3 shares); 0 = one workgroup
- * per wave.  Identical results.
+ * DR_OPT_COMMIT_SPLIT (default 0): 1 = dr_wave_commit / dr_wave_ready on a
+ * wave range shorter than the device's CU count split each wave's vote over
+ * several workgroups (each computes S_1, S_2 whole and a share of S_3); 0 = one
+ * workgroup per wave, the faster on MI355X at C4.  Identical
+ * results.
  * Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 
