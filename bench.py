@@ -471,10 +471,13 @@ def colshard_child(args):
     for _ in range(max(args.warmup, 1)):
         step()
     se.wave_commit(1, 1)  # a collective: every rank has finished its warm-up
+    se.set_phase_timing(False)  # the timed replays record no phase events
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     dt = time.perf_counter() - t0
+    se.set_phase_timing(True)
+    step()  # one more replay (every rank) for the per-phase device times
     rep = step.result()
     st = se.stats()
     info = se.info()

@@ -30,6 +30,7 @@ DR_SHARD_ID_BYTES = 128
 DR_SHARD_OPT_PERSISTENT = 1
 DR_SHARD_OPT_MEMO = 2
 DR_SHARD_OPT_STEPPED = 3
+DR_SHARD_OPT_PHASE_TIMING = 4
 
 P = C.c_void_p
 i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float

@@ -568,6 +568,9 @@ struct dr_shard {
   int persistent = 1;  // DR_SHARD_OPT_PERSISTENT
   int memo = 1;        // DR_SHARD_OPT_MEMO
   int stepped = 0;     // DR_SHARD_OPT_STEPPED: the memo replay's stepped form even when every column is here
+  int phase_timing = 1;  // DR_SHARD_OPT_PHASE_TIMING
+  // a phase boundary of the memo replay (recorded only with phase timing)
+  hipError_t mark(int k) { return phase_timing ? hipEventRecord(evs[k], stream) : hipSuccess; }
   int pass_geo = 0;    // k_ms_pass geometry (tuning: DR_SHARD_PASS_GEO)
   // k_ms_wu on the side stream beside the pass (tuning: DR_SHARD_WU_SIDE=1); by default
   // before it on the main stream: C4 G = 1 0.348 vs 0.358 ms, G = 8 0.380 vs 0.398 ms, the
@@ -1269,12 +1272,12 @@ hipError_t launch_pass(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, in
   const bool wu = T >= 1;
   const bool side = wu && c->wu_side;
   if (wu) {
-    const size_t lds = std::max<size_t>((size_t)c->nlocal * a.dd * c->SP * 8, 8);
+    const size_t lds = std::max<size_t>((size_t)4 * c->nlocal * a.dd * c->SP * 8, 8);
     if (side) {
       if (hipError_t e = hipEventRecord(c->fork, c->stream)) return e;
       if (hipError_t e = hipStreamWaitEvent(c->side, c->fork, 0)) return e;
     }
-    hipLaunchKernelGGL((drs::k_ms_wu<256>), dim3(T), dim3(256), lds, side ? c->side : c->stream, a, f,
+    hipLaunchKernelGGL((drs::k_ms_wu<256>), dim3((T + 3) / 4), dim3(256), lds, side ? c->side : c->stream, a, f,
                        c->mWU.as<u64>());
     if (hipError_t e = hipGetLastError()) return e;
     if (side)
@@ -1337,7 +1340,7 @@ int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int
   }
   hipLaunchKernelGGL(k_ms_vfinal, dim3((nw + 3) / 4), dim3(256), 0, c->stream, a1, f, (const u64 *)P1, G);
   SHCHK(c, hipGetLastError());
-  SHCHK(c, hipEventRecord(c->evs[1], c->stream));
+  SHCHK(c, c->mark(1));
   // 2. K^cand (exchanged), good, the canonical walk, the canonical prefixes
   const int rb = (T + 1 + 3) / 4;
   if (c->local) {
@@ -1382,7 +1385,7 @@ int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int
   hipLaunchKernelGGL((drs::k_ms_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
                      (const u64 *)nullptr, (u64 *)nullptr);
   SHCHK(c, hipGetLastError());
-  SHCHK(c, hipEventRecord(c->evs[2], c->stream));
+  SHCHK(c, c->mark(2));
   // 3. every pop and every chain (planned on the device from the commits), stepped together
   if (int rc = init_states(c, pops, nq)) return rc;
   drs::MArgs a = make_margs(c, nq);
@@ -1475,7 +1478,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   // the fused sweep emitting each pop itself (DR_SHARD_EMIT_FUSED=1, tuning): 101 us against
   // 68 + 22 us as two launches at C4 G = 1 (profiles/r04/)
   f.emit = fused && !paper && c->emit_fused ? 1 : 0;
-  SHCHK(c, hipEventRecord(c->evs[0], c->stream));
+  SHCHK(c, c->mark(0));
   th1 = std::chrono::steady_clock::now();
   int steps = 0;
   if (fused) {
@@ -1486,7 +1489,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     a.good = f.good;
     a.push_out = m.push;
     SHCHK(c, launch_pass(c, a, f, nw, drs::VOTE_FULL, (u64 *)nullptr));
-    SHCHK(c, hipEventRecord(c->evs[1], c->stream));
+    SHCHK(c, c->mark(1));
     // K^cand, the canonical walk, the canonical digests and prefixes, the plan (pops and chains).
     // (As one workgroup's tail of the parallel launch before it -- a done counter behind an
     // agent-scope fence per workgroup -- these took 108 + 92 us against 40 + 33 us apart:
@@ -1502,14 +1505,14 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     hipLaunchKernelGGL((drs::k_ms_prefix_plan<1024>), dim3(1), dim3(1024), 0, c->stream, a, f,
                        c->mq.as<drs::MQuery>(), (int)pcap);
     SHCHK(c, hipGetLastError());
-    SHCHK(c, hipEventRecord(c->evs[2], c->stream));
+    SHCHK(c, c->mark(2));
     // every pop and chain to its end, REF pops emitted by their own workgroup
     hipLaunchKernelGGL((drs::k_ms_sweep_full<256>), dim3(nq), dim3(256), lds_ring, c->stream, a, f);
     SHCHK(c, hipGetLastError());
   } else {
     if (int rc = stepped_phase(c, nw, qs, nq, f, m, pcap, &steps)) return rc;
   }
-  SHCHK(c, hipEventRecord(c->evs[3], c->stream));
+  SHCHK(c, c->mark(3));
   drs::MArgs a = make_margs(c, nq);
   a.slot_off = c->slot_off.as<uint32_t>();
   a.slot_src = c->slot_src.as<uint16_t>();
@@ -1520,7 +1523,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
                        m.qout + 2 * npop);
     SHCHK(c, hipGetLastError());
   }
-  SHCHK(c, hipEventRecord(c->evs[4], c->stream));
+  SHCHK(c, c->mark(4));
   char *hb = stage(c, m.bytes);
   if (!hb) return c->fail(DR_E_HIP, "pinned staging allocation failed");
   SHCHK(c, hipMemcpyAsync(hb, c->mout.p, m.bytes, hipMemcpyDeviceToHost, c->stream));
@@ -1528,10 +1531,12 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   SHCHK(c, hipStreamSynchronize(c->stream));
   th3 = std::chrono::steady_clock::now();
   const MOut h = carve_out(hb, nw, nq, pcap, npop);
-  SHCHK(c, hipEventElapsedTime(&o->ms_commit, c->evs[0], c->evs[1]));
-  SHCHK(c, hipEventElapsedTime(&o->ms_summary, c->evs[1], c->evs[2]));
-  SHCHK(c, hipEventElapsedTime(&o->ms_deliver, c->evs[2], c->evs[3]));
-  SHCHK(c, hipEventElapsedTime(&o->ms_emit, c->evs[3], c->evs[4]));
+  if (c->phase_timing) {
+    SHCHK(c, hipEventElapsedTime(&o->ms_commit, c->evs[0], c->evs[1]));
+    SHCHK(c, hipEventElapsedTime(&o->ms_summary, c->evs[1], c->evs[2]));
+    SHCHK(c, hipEventElapsedTime(&o->ms_deliver, c->evs[2], c->evs[3]));
+    SHCHK(c, hipEventElapsedTime(&o->ms_emit, c->evs[3], c->evs[4]));
+  }
   o->ms_chain = 0;
   if (h.hdr[drs::FH_ERR]) return c->fail(DR_E_CAPACITY, "chain pushes exceed the bound %lld", (long long)pcap);
   std::memcpy(o->commit, h.commit, (size_t)nw);
@@ -1604,18 +1609,23 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     }
   }
   o->push_off[nw] = (uint32_t)at;
-  std::vector<uint64_t> qout(h.qout, h.qout + (size_t)3 * std::max(npop, 1));
+  std::vector<uint64_t> qout;  // PAPER: paper_emit's counts; REF reads the copied region
+  const uint64_t *qo = reinterpret_cast<const uint64_t *>(h.qout);
   if (fused) {
     steps = 0;
     for (int i = 0; i < npop; i++) steps = std::max(steps, qs[i].top - h.fin[i].stop + 1);
   }
   if (paper && !pop_query.empty()) {
     std::vector<drs::MState> fin(h.fin, h.fin + npop);
-    SHCHK(c, hipEventRecord(c->evs[3], c->stream));
+    SHCHK(c, c->mark(3));
+    qout.assign(qo, qo + (size_t)3 * std::max(npop, 1));
     if (int rc = paper_emit(c, a, qs, fin, pop_query, qout, npop)) return rc;
-    SHCHK(c, hipEventRecord(c->evs[4], c->stream));
-    SHCHK(c, hipEventSynchronize(c->evs[4]));
-    SHCHK(c, hipEventElapsedTime(&o->ms_emit, c->evs[3], c->evs[4]));
+    qo = qout.data();
+    SHCHK(c, c->mark(4));
+    if (c->phase_timing) {
+      SHCHK(c, hipEventSynchronize(c->evs[4]));
+      SHCHK(c, hipEventElapsedTime(&o->ms_emit, c->evs[3], c->evs[4]));
+    }
   }
   uint64_t de = 0;
   std::vector<uint8_t> seen(paper ? npop : 0, 0);
@@ -1623,9 +1633,9 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     const int q = pop_query[pi];
     const bool zero = paper && seen[q];  // a repeated leader delivers nothing new (its cone is delivered)
     if (paper) seen[q] = 1;
-    o->pop_count[pi] = zero ? 0 : qout[q];
-    o->pop_digest[pi] = zero ? 0 : qout[npop + q];
-    const uint64_t e = zero ? 0 : qout[2 * npop + q];
+    o->pop_count[pi] = zero ? 0 : qo[q];
+    o->pop_digest[pi] = zero ? 0 : qo[npop + q];
+    const uint64_t e = zero ? 0 : qo[2 * npop + q];
     if (o->pop_edges) o->pop_edges[pi] = e;
     de += e;
   }
@@ -1858,6 +1868,10 @@ extern "C" int dr_shard_set_option(dr_shard *c, int option, int value) {
   }
   if (option == DR_SHARD_OPT_STEPPED) {
     c->stepped = value ? 1 : 0;
+    return DR_OK;
+  }
+  if (option == DR_SHARD_OPT_PHASE_TIMING) {
+    c->phase_timing = value ? 1 : 0;
     return DR_OK;
   }
   return c->fail(DR_E_INVAL, "unknown option %d", option);

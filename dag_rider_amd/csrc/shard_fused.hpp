@@ -95,30 +95,31 @@ __device__ __forceinline__ int64_t fblock_scan(int64_t v, int64_t *s, int64_t &t
 }
 
 // ---------------------------------------------------------------------------
-// k_ms_wu: one workgroup per round r >= 1: WU_r of every local shard from the
-// round's weak-column keys (LDS atomics, then every word written, zeros
-// included), and wave 0 the speculative canonical digest SG_r (every present
-// vertex of the round delivered in slot order at positions from ppref[r-1]).
-// Dynamic LDS: sWU[NL*dd*SP].  It reads no strong row, so it is kept out of
+// k_ms_wu: one wave per round r >= 1 (NT/64 rounds per workgroup): WU_r of every
+// local shard from the round's weak-column keys (LDS atomics, then every word
+// written, zeros included), and the speculative canonical digest SG_r (every
+// present vertex of the round delivered in slot order at positions from
+// ppref[r-1]).  Dynamic LDS: sWU[NT/64][NL*dd*SP].  It reads no strong row, so it is kept out of
 // k_ms_pass, whose row stream it would stall at every round.
 // ---------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_wu(MArgs a, FArgs f, u64 *__restrict__ WU) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
-  const int NL = a.nlocal, SP = a.SP, dd = a.dd;
-  u64 *sWU = lds;
-  const int r = blockIdx.x + 1, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int i = tid; i < NL * dd * SP; i += NT) sWU[i] = 0;
-  __syncthreads();
+  constexpr int NW = NT / 64;
+  const int NL = a.nlocal, SP = a.SP, dd = a.dd, words = NL * dd * SP;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, r = blockIdx.x * NW + wid + 1;
+  u64 *sWU = lds + (size_t)wid * words;  // this wave's round
+  for (int i = lane; i < words; i += 64) sWU[i] = 0;
+  if (r > a.T) return;  // (wave-uniform; no workgroup barrier below)
   for (int l = 0; l < NL; l++) {  // every key has a source
     const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
-    for (uint64_t jj = c0 + tid; jj < c1; jj += NT) {
+    for (uint64_t jj = c0 + lane; jj < c1; jj += 64) {
       const uint32_t key = a.wck[jj];
       const int d = (int)(key >> 11) - 2, tc = (int)(key & 2047u);
       atomicOr(&sWU[((size_t)l * dd + d) * SP + (tc >> 6)], 1ULL << (tc & 63));
     }
   }
-  if (wid == 0) {
+  {  // speculative canonical digest of round r
     constexpr int SPT = 8;
     const uint32_t sa = a.slot_off[r], sb = a.slot_off[r + 1];
     u64 pos = f.ppref[r - 1], dg = 0;
@@ -146,8 +147,7 @@ __global__ __launch_bounds__(NT) void k_ms_wu(MArgs a, FArgs f, u64 *__restrict_
     dg = dr::wave_sum(dg);
     if (lane == 0) f.SG[r] = dg;
   }
-  __syncthreads();
-  for (int i = tid; i < NL * dd * SP; i += NT) {
+  for (int i = lane; i < words; i += 64) {  // (LDS ops of one wave complete in order)
     const int l = i / (dd * SP), rest = i - l * dd * SP;
     WU[((size_t)l * a.R + r) * dd * SP + rest] = sWU[i];
   }

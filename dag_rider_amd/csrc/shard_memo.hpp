@@ -538,27 +538,55 @@ __global__ __launch_bounds__(NT) void k_ms_prefix(int T, const u64 *__restrict__
 
 // One wave emits round y's slots whose source bit is set in mw (lane w < W holds
 // word w) in insertion order from position pos: digest terms and, with sdeg, the
-// strong + weak degrees (this lane's shares).
+// strong + weak degrees (this lane's shares).  Lane l takes SPT consecutive slots
+// of each 64*SPT block: every slot and degree load of a block goes out at once
+// (three memory latencies per round, not two per 64 slots), and an exclusive scan
+// of the lanes' hit counts keeps the slot order.
 __device__ __forceinline__ void ms_wave_emit(const uint32_t *__restrict__ slot_off, const uint16_t *__restrict__ slot_src,
                                              int y, u64 mw, u64 pos, int W, const uint16_t *sdeg, const uint16_t *wdeg,
                                              int n, u64 &dg, u64 &ed) {
+  constexpr int SPT = 16;
   const int lane = threadIdx.x & 63;
   const uint32_t s0 = slot_off[y], s1 = slot_off[y + 1];
-  for (uint32_t base = s0; base < s1; base += 64) {
-    const uint32_t sl = base + lane;
-    const int s = sl < s1 ? (int)slot_src[sl] : 0;
-    const int wd = s > 0 ? (s - 1) >> 6 : 0;
-    const u64 word = ((u64)(uint32_t)__shfl((int)(mw >> 32), wd, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)mw, wd, 64);
-    const bool in = s > 0 && ((word >> ((s - 1) & 63)) & 1ULL);
-    const u64 bal = __ballot(in);
-    if (in) {
-      dg += dr::digest_term((uint32_t)y, (uint32_t)s, pos + (u64)__popcll(bal & ((1ULL << lane) - 1ULL)));
-      if (sdeg) {
-        const size_t at = (size_t)y * n + (s - 1);
-        ed += (u64)sdeg[at] + wdeg[at];
+  const uint32_t hi32 = (uint32_t)(mw >> 32), lo32 = (uint32_t)mw;
+  for (uint32_t c0 = s0; c0 < s1; c0 += 64 * SPT) {
+    const uint32_t i0 = c0 + (uint32_t)lane * SPT;
+    int src[SPT];
+#pragma unroll
+    for (int q = 0; q < SPT; q++) src[q] = i0 + q < s1 ? (int)slot_src[i0 + q] : 0;
+    uint32_t inm = 0;  // bit q: slot i0 + q is delivered
+#pragma unroll
+    for (int q = 0; q < SPT; q++) {
+      const int sv = src[q];
+      const int wd = sv > 0 ? (sv - 1) >> 6 : 0;
+      const u64 word = ((u64)(uint32_t)__shfl((int)hi32, wd, 64) << 32) | (uint32_t)__shfl((int)lo32, wd, 64);
+      inm |= (sv > 0 && ((word >> ((sv - 1) & 63)) & 1ULL)) ? 1u << q : 0u;
+    }
+    uint16_t d1[SPT], d2[SPT];
+    if (sdeg) {
+#pragma unroll
+      for (int q = 0; q < SPT; q++) {
+        const size_t at = (size_t)y * n + (src[q] > 0 ? src[q] - 1 : 0);
+        d1[q] = (inm >> q) & 1u ? sdeg[at] : (uint16_t)0;
+        d2[q] = (inm >> q) & 1u ? wdeg[at] : (uint16_t)0;
       }
     }
-    pos += (u64)__popcll(bal);
+    const uint32_t cnt = (uint32_t)__popc(inm);
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = __shfl_up(inc, off);
+      if (lane >= off) inc += t;
+    }
+    u64 k = pos + (inc - cnt);
+#pragma unroll
+    for (int q = 0; q < SPT; q++)
+      if ((inm >> q) & 1u) dg += dr::digest_term((uint32_t)y, (uint32_t)src[q], k++);
+    if (sdeg) {
+#pragma unroll
+      for (int q = 0; q < SPT; q++) ed += (u64)d1[q] + d2[q];
+    }
+    pos += __shfl(inc, 63);
   }
   (void)W;
 }

@@ -151,6 +151,10 @@ class ShardEngine:
         exchanged between launches) even when this context holds every column."""
         self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_STEPPED, int(on)))
 
+    def set_phase_timing(self, on: bool):
+        """DR_SHARD_OPT_PHASE_TIMING: per-phase device times in the replay's ms_* (default on)."""
+        self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_PHASE_TIMING, int(on)))
+
     def set_leader_coin(self, mode: int = L.DR_LEADER_CONST1, seed: int = 0,
                         table: Optional[Sequence[int]] = None):
         """chooseLeader (process.go:386-392), as Engine.set_leader_coin."""

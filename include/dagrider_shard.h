@@ -91,6 +91,10 @@ int dr_shard_path_batch(dr_shard *ctx, int q, const int32_t *from, const int32_t
  * per launch with the columns exchanged between launches, what each rank of a
  * group of G > 1 runs -- so one device can check it.  Results are identical. */
 #define DR_SHARD_OPT_STEPPED 3
+/* DR_SHARD_OPT_PHASE_TIMING (default 1): the memoized replay records HIP events
+ * between its phases and reports them in dr_replay_out.ms_*; 0 leaves them 0
+ * (reading the events back costs the host ~20 us per replay). */
+#define DR_SHARD_OPT_PHASE_TIMING 4
 int dr_shard_set_option(dr_shard *ctx, int option, int value);
 
 /* chooseLeader (process.go:386-392): dr_set_leader_coin's modes and semantics. */

@@ -37,11 +37,14 @@ def main():
             se.set_stepped(bool(stepped))
             rp = ShardReplayer(se, cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)  # outputs allocated once
             rp()  # warm-up
+            se.set_phase_timing(False)  # timed replays: no phase events
             walls = []
             for _ in range(args.runs):
                 t0 = time.perf_counter()
                 rp()
                 walls.append((time.perf_counter() - t0) * 1e3)
+            se.set_phase_timing(True)
+            rp()  # one more replay for the per-phase device times
             r = rp.result()
             st = se.stats()
             ok = bool((r.commit == rref.commit).all() and (r.vcount == rref.vcount).all()
