@@ -51,6 +51,12 @@ class ReplayOut(C.Structure):
                 ("sweep_partial", u64), ("sweep_row_bytes", u64), ("sweep_weak_scanned", u64), ("sweep_shortcut", u64)]
 
 
+class ReplayView(C.Structure):
+    _fields_ = [("commit", P), ("vcount", P), ("push_off", P), ("push_wave", P), ("pop_count", P),
+                ("pop_digest", P), ("pop_edges", P), ("n_push", i64), ("commit_edges", u64), ("chain_edges", u64),
+                ("deliver_edges", u64), ("ms_deliver", f32)]
+
+
 # symbol -> (restype, argtypes); every symbol declared in include/*.h
 SIGNATURES = {
     "dr_abi_version": (C.c_int, []),
@@ -75,6 +81,8 @@ SIGNATURES = {
                                     C.POINTER(C.c_size_t), P, P]),
     "dr_replay": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
     "dr_replay_batch": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(ReplayOut)]),
+    "dr_replay_batch_view": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.c_int, i64,
+                                       C.POINTER(ReplayView)]),
     "dr_last_kernel_ms": (C.c_int, [P, C.POINTER(f32)]),
     "dr_last_batch_phases": (C.c_int, [P, C.POINTER(f32)]),
     # include/dagrider_shard.h

@@ -185,6 +185,7 @@ struct dr_ctx {
   int cu_count = 0;         // compute units of the device (dr_replay_batch's form choice)
   float last_commit_ms = 0;  // dr_last_kernel_ms: the last commit-rule launch (HIP events)
   float batch_phases[4] = {};
+  std::vector<dr_replay_out> view_outs;  // dr_replay_batch_view's capacities (this context first)
   uint64_t gen = 0;  // context generation (g_ctx_gen): bumped by every call that may change the context
   void touch() { gen = next_gen(); }  // dr_last_batch_phases: host prep, launch -> host, copy back, unpack
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
@@ -3361,8 +3362,11 @@ hipError_t launch_small(const dr_ctx *c, const dr::SmallJob *jobs, int nj, int n
 }
 }  // namespace
 
-extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
-                               dr_replay_out *outs) {
+namespace {
+// dr_replay_batch (views == nullptr: results copied into outs) and dr_replay_batch_view
+// (views: pointers into the copied-back region; outs holds only the capacities)
+int replay_batch_impl(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
+                      dr_replay_out *outs, dr_replay_view *views) {
   if (!ctxs || nctx < 1 || !outs) return DR_E_INVAL;
   for (int i = 0; i < nctx; i++)
     if (!ctxs[i]) return DR_E_INVAL;
@@ -3396,6 +3400,7 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
       return c0->fail(DR_E_INVAL, "bad chain mode");
     if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER)
       return c0->fail(DR_E_INVAL, "bad deliver mode");
+    if (!fused && views) return c0->fail(DR_E_INVAL, "dr_replay_batch_view: the batch does not run fused");
     if (!fused) {  // general shapes: one dr_replay per context (all on the GPU)
       for (int i = 0; i < nctx; i++)
         if (int rc = dr_replay(ctxs[i], nwaves, chain_mode, deliver_mode, &outs[i])) {
@@ -3528,6 +3533,26 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     dr_replay_out *o = &outs[i];
     const u64 *tot = reinterpret_cast<const u64 *>(at(J.totals));
     const int64_t np = (int64_t)tot[3];
+    if (views) {  // in place: pointers into the copied-back region
+      dr_replay_view &v = views[i];
+      v.commit = reinterpret_cast<const uint8_t *>(at(J.commit));
+      v.vcount = reinterpret_cast<const int32_t *>(at(J.vcount));
+      v.push_off = reinterpret_cast<const uint32_t *>(at(J.push_off));
+      v.push_wave = reinterpret_cast<const int32_t *>(at(J.push_wave));
+      v.pop_count = reinterpret_cast<const uint64_t *>(at(J.pop_count));
+      v.pop_digest = reinterpret_cast<const uint64_t *>(at(J.pop_digest));
+      v.pop_edges = reinterpret_cast<const uint64_t *>(at(J.pop_edges));
+      v.n_push = np;
+      v.commit_edges = tot[0];
+      v.chain_edges = tot[1];
+      v.deliver_edges = tot[2];
+      v.ms_deliver = ms;
+      if (np > o->push_cap && bad < 0) {
+        bad = i;
+        bad_np = np;
+      }
+      continue;
+    }
     std::memcpy(o->commit, at(J.commit), nw);
     std::memcpy(o->vcount, at(J.vcount), 4 * (size_t)nw);
     std::memcpy(o->push_off, at(J.push_off), 4 * (size_t)(nw + 1));
@@ -3565,4 +3590,31 @@ extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int ch
     return c0->fail(DR_E_CAPACITY, "context %d: %lld pushed leaders, capacity %lld", bad, (long long)bad_np,
                     (long long)outs[bad].push_cap);
   return DR_OK;
+}
+}  // namespace
+
+extern "C" int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
+                               dr_replay_out *outs) {
+  return replay_batch_impl(ctxs, nctx, nwaves, chain_mode, deliver_mode, outs, nullptr);
+}
+
+extern "C" int dr_replay_batch_view(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
+                                    int64_t push_cap, dr_replay_view *views) {
+  if (!ctxs || nctx < 1 || !views || push_cap < 1 || !ctxs[0]) return DR_E_INVAL;
+  // capacities only: the outputs' pointers are never written in view mode (a stable
+  // array per first context, so a repeated batch reuses its plan)
+  std::vector<dr_replay_out> &outs = ctxs[0]->view_outs;
+  static uint8_t dummy[8];
+  if (outs.size() != (size_t)nctx) outs.assign(nctx, dr_replay_out{});
+  for (dr_replay_out &o : outs) {
+    o.commit = dummy;
+    o.vcount = reinterpret_cast<int32_t *>(dummy);
+    o.push_off = reinterpret_cast<uint32_t *>(dummy);
+    o.push_wave = reinterpret_cast<int32_t *>(dummy);
+    o.pop_count = reinterpret_cast<uint64_t *>(dummy);
+    o.pop_digest = reinterpret_cast<uint64_t *>(dummy);
+    o.pop_edges = reinterpret_cast<uint64_t *>(dummy);
+    o.push_cap = push_cap;
+  }
+  return replay_batch_impl(ctxs, nctx, nwaves, chain_mode, deliver_mode, outs.data(), views);
 }

@@ -557,20 +557,40 @@ __device__ __forceinline__ void load_round(const DagView &g, const MemoView &mv,
 
 // full round r: ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d] (lane w < WS owns word w)
 template <int WS, bool WEAK>
+// Every lane of wave 0 calls it (x is lane w's prefetched words for w < WS).
 __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWords &x, int r, int bottom,
                                                u64 *ring, int dmask) {
-  const int w = threadIdx.x;
-  ring[(size_t)((r - 1) & dmask) * WS + w] |= x.U;
-  if constexpr (!WEAK) return;
+  const int lane = threadIdx.x;
+  if (lane < WS) {
+    ring[(size_t)((r - 1) & dmask) * WS + lane] |= x.U;
+    if constexpr (WEAK) {
 #pragma unroll
-  for (int d = 0; d < DDR; d++) {
-    const int tr = r - d - 2;
-    if (d < mv.dd && tr >= bottom) ring[(size_t)(tr & dmask) * WS + w] |= x.WU[d];
+      for (int d = 0; d < DDR; d++) {
+        const int tr = r - d - 2;
+        if (d < mv.dd && tr >= bottom) ring[(size_t)(tr & dmask) * WS + lane] |= x.WU[d];
+      }
+    }
   }
-  for (int d = DDR; d < mv.dd; d++) {
-    const int tr = r - d - 2;
-    if (tr < bottom) break;
-    ring[(size_t)(tr & dmask) * WS + w] |= mv.WU[((size_t)r * mv.dd + d) * WS + w];
+  if constexpr (!WEAK) return;
+  // deeper slots (a deep window: dd up to 254) over all 64 lanes -- 64/WS lanes per
+  // word, each taking every (64/WS)-th slot -- 8 loads in flight per lane, then
+  // their ORs (every (slot, word) is its own ring word)
+  constexpr int LPW = WS >= 64 ? 1 : 64 / WS;
+  const int w = lane % WS, j = lane / WS;
+  const int dlim = min(mv.dd, r - 1 - bottom);  // tr = r - d - 2 >= bottom
+  if (j >= LPW) return;
+  for (int d0 = DDR + j; d0 < dlim; d0 += 8 * LPW) {
+    u64 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int d = d0 + q * LPW;
+      v[q] = d < dlim ? mv.WU[((size_t)r * mv.dd + d) * WS + w] : 0ULL;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int d = d0 + q * LPW;
+      if (d < dlim) ring[(size_t)((r - d - 2) & dmask) * WS + w] |= v[q];
+    }
   }
 }
 
@@ -1026,7 +1046,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
             else { st_partial++; if (WEAK) st_scan += cur.C1 - cur.C0; }
           }
           if (summary) {  // the round is the union of its rows: apply the summaries, stay in wave 0
-            if (act) expand_summary<WS, WEAK>(mv, cur, r, q.bottom, ring, dmask);
+            expand_summary<WS, WEAK>(mv, cur, r, q.bottom, ring, dmask);  // every lane of wave 0
             if (tid == 0) {
               my_edges += cur.SD;
               if (WEAK) my_wedges += cur.NW;
@@ -1500,6 +1520,7 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
       k = p;
     } else {
       k = mv.U[(size_t)(r + 1) * WS + w];
+#pragma unroll 8
       for (int d = 0; d < mv.dd && r + d + 2 <= T; d++) k |= mv.WU[((size_t)(r + d + 2) * mv.dd + d) * WS + w];
     }
     K[(size_t)r * WS + w] = k;
@@ -1603,6 +1624,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
       const int x = b - 1 - it / WS, w = it % WS;
       if (x < 0) continue;
       u64 v = 0;
+#pragma unroll 8
       for (int y = max(b + 1, x + 2); y <= T && y <= x + mv.dd + 1; y++)
         v |= mv.WU[((size_t)y * mv.dd + (y - x - 2)) * WS + w];
       ring[(size_t)(x & dmask) * WS + w] = v;
@@ -1642,7 +1664,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
       if (s_ctl[2]) break;  // regime restored at r (or bottom reached): CE_r stays the full total
       u64 e = 0, we = 0;
       if (s_ctl[1]) {
-        if (tid < WS) expand_summary<WS, true>(mv, cur, r, 0, ring, dmask);
+        if (tid < 64) expand_summary<WS, true>(mv, cur, r, 0, ring, dmask);  // wave 0
         if (tid == 0) e = mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
       } else {
         u64 rb = 0;

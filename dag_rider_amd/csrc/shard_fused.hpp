@@ -483,6 +483,37 @@ __device__ __forceinline__ void fload_round(const MArgs &a, int r, bool pop, int
   }
 }
 
+// A full round's weak summaries: ring[r-d-2] |= WU_r[d] for d < dd and r-d-2 >=
+// bottom.  Every lane of wave 0 calls it: lane w < W applies the FDD prefetched
+// slots (pre) of word w; the deeper slots are spread over all 64 lanes (64/W per
+// word, each every (64/W)-th slot), 8 loads in flight per lane before their ORs.
+__device__ __forceinline__ void full_weak_round(const MArgs &a, int r, int bottom, u64 *ring, int dm, const u64 *pre,
+                                                int lane) {
+  const int W = a.W, dlim = min(a.dd, r - 1 - bottom);
+  if (lane < W) {
+#pragma unroll
+    for (int d = 0; d < FDD; d++)
+      if (d < dlim) ring[(size_t)((r - d - 2) & dm) * W + lane] |= pre[d];
+  }
+  const int LPW = (W <= 64 && 64 % W == 0) ? 64 / W : 1;
+  const int w = lane % W, j = lane / W;
+  if (j >= LPW) return;
+  const int l = w / a.WSs, cw = w - l * a.WSs;
+  for (int d0 = FDD + j; d0 < dlim; d0 += 8 * LPW) {
+    u64 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int d = d0 + q * LPW;
+      v[q] = d < dlim ? a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw] : 0ULL;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int d = d0 + q * LPW;
+      if (d < dlim) ring[(size_t)((r - d - 2) & dm) * W + w] |= v[q];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_ms_canon_full: one workgroup, the canonical segments top down (k_canon).
 // Dynamic LDS: ring[depth*W] | FE[W] | Ur[W].  As in k_ms_sweep_full, wave 0
@@ -567,16 +598,9 @@ __device__ __forceinline__ void canon_walk(const MArgs &a, const FArgs &f, u64 *
             }
             break;
           }
-          if (act) {  // full: ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d]
-            ring[(size_t)((r - 1) & dm) * W + lane] |= c0.U;
-            const int l = lane / a.WSs, cw = lane - l * a.WSs;
-            for (int d = 0; d < a.dd; d++) {
-              const int tr = r - d - 2;
-              if (tr < 0) break;
-              ring[(size_t)(tr & dm) * W + lane] |=
-                  d < FDD ? c0.WU[d] : a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw];
-            }
-          }
+          // full: ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d]
+          if (act) ring[(size_t)((r - 1) & dm) * W + lane] |= c0.U;
+          full_weak_round(a, r, 0, ring, dm, c0.WU, lane);
           c0 = c1;
           c1 = c2;
           c2 = c3;
@@ -888,18 +912,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
           break;
         }
         if (summary) {  // ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d]
-          if (act) {
-            ring[(size_t)((r - 1) & dm) * W + lane] |= cur.U;
-            if (weak) {
-              const int l = lane / WSs, cw = lane - l * WSs;
-              for (int d = 0; d < a.dd; d++) {
-                const int tr = r - d - 2;
-                if (tr < Q.bottom) break;
-                ring[(size_t)(tr & dm) * W + lane] |=
-                    d < FDD ? cur.WU[d] : a.WU[(((size_t)l * a.R + r) * a.dd + d) * a.SP + cw];
-              }
-            }
-          }
+          if (act) ring[(size_t)((r - 1) & dm) * W + lane] |= cur.U;
+          if (weak) full_weak_round(a, r, Q.bottom, ring, dm, cur.WU, lane);  // every lane of wave 0
         } else if (anyfe && single >= 0 && ((__shfl(fe, single >> 6) >> (single & 63)) & 1ULL)) {
           // FE = {single}: its row (every local shard's piece) and its weak columns
           if (!pop) edges += a.sdeg[(size_t)r * a.n + single];

@@ -392,6 +392,52 @@ class ReplayBatch:
         return dict(host_prep=ms[0], launch_to_host=ms[1], copy_back=ms[2], unpack=ms[3])
 
 
+class ReplayBatchView:
+    """dr_replay_batch_view over a fixed list of engines: each call leaves every context's
+    results where the batch's single copy back put them (no per-context copies);
+    results() wraps them as numpy views, valid until the next call."""
+
+    def __init__(self, engines: Sequence["Engine"], nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT,
+                 deliver_mode: int = L.DR_DELIVER_REF, push_cap: Optional[int] = None):
+        self.engines = list(engines)
+        self.nwaves, self.chain_mode, self.deliver_mode = nwaves, chain_mode, deliver_mode
+        n = len(self.engines)
+        self._ctxs = (L.P * n)(*[e._h for e in self.engines])
+        self._views = (L.ReplayView * n)()
+        if push_cap is None:
+            push_cap = nwaves if chain_mode == L.DR_CHAIN_PERSISTENT else nwaves * (nwaves + 1) // 2
+        self.push_cap = push_cap
+
+    def run(self) -> None:
+        L0 = L.lib()
+        rc = L0.dr_replay_batch_view(self._ctxs, len(self.engines), self.nwaves, self.chain_mode,
+                                     self.deliver_mode, self.push_cap, self._views)
+        if rc != L.DR_OK:
+            raise L.DrError(rc, L0.dr_last_error(self.engines[0]._h).decode())
+
+    def results(self) -> List[ReplayResult]:
+        nw, out = self.nwaves, []
+        for v in self._views:
+            k = int(v.n_push)
+
+            def arr(p, dt, m):
+                return np.ctypeslib.as_array(C.cast(p, C.POINTER(dt)), shape=(max(m, 1),))[:m]
+            out.append(ReplayResult(arr(v.commit, C.c_uint8, nw), arr(v.vcount, C.c_int32, nw),
+                                    arr(v.push_off, C.c_uint32, nw + 1), arr(v.push_wave, C.c_int32, k),
+                                    arr(v.pop_count, C.c_uint64, k), arr(v.pop_digest, C.c_uint64, k),
+                                    arr(v.pop_edges, C.c_uint64, k), None, v.commit_edges, v.chain_edges,
+                                    v.deliver_edges, dict(commit=0.0, chain=0.0, deliver=v.ms_deliver, emit=0.0,
+                                                          summary=0.0),
+                                    {}))
+        return out
+
+    def host_phases(self) -> dict:
+        """dr_last_batch_phases of the last run: host prep, launch -> host, copy back, unpack (ms)."""
+        ms = (C.c_float * 4)()
+        L.lib().dr_last_batch_phases(self.engines[0]._h, ms)
+        return dict(host_prep=ms[0], launch_to_host=ms[1], copy_back=ms[2], unpack=ms[3])
+
+
 def replay_batch(engines: Sequence["Engine"], nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT,
                  deliver_mode: int = L.DR_DELIVER_REF) -> List[ReplayResult]:
     """dr_replay_batch: every engine's dr_replay, as one fused launch when the DAGs are small."""

@@ -284,6 +284,28 @@ int dr_replay(dr_ctx *ctx, int nwaves, int chain_mode, int deliver_mode, dr_repl
 int dr_replay_batch(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
                     dr_replay_out *outs);
 
+/* The results of one context of a fused dr_replay_batch_view, in place: every
+ * pointer is into one host region owned by the batch's first context, valid until
+ * the next dr_replay_batch / dr_replay_batch_view on it or its destruction. */
+typedef struct dr_replay_view {
+  const uint8_t *commit;     /* [nwaves], as dr_replay_out.commit */
+  const int32_t *vcount;     /* [nwaves] */
+  const uint32_t *push_off;  /* [nwaves + 1] */
+  const int32_t *push_wave;  /* [n_push] */
+  const uint64_t *pop_count, *pop_digest, *pop_edges;  /* [n_push] */
+  int64_t n_push;
+  uint64_t commit_edges, chain_edges, deliver_edges;
+  float ms_deliver;  /* the fused launch's device time (HIP events), as dr_replay_out.ms_deliver */
+} dr_replay_view;
+
+/* dr_replay_batch without copying each context's results out: views[i] points at
+ * context i's results where the batch's single copy back left them (C5: 4096
+ * contexts, ~0.3 ms of per-context copies saved).  Only for a batch that runs
+ * fused (see dr_replay_batch; DR_E_INVAL otherwise); push_cap bounds each
+ * context's pushes, as dr_replay_out.push_cap. */
+int dr_replay_batch_view(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode, int deliver_mode,
+                         int64_t push_cap, dr_replay_view *views);
+
 /* Device time (ms, HIP events) of the commit-rule kernel of the last
  * dr_wave_commit / dr_wave_ready / dr_replay on this context (observability,
  * like dr_shard_stats; no reference counterpart). */

@@ -235,3 +235,47 @@ def test_batch_plan_reuse(gpu_device, form):
             _same(g, oracle.PDag(d).replay(f, nw, cm, dm))
     for _, _, e in items:
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", [L.DR_BATCH_WORKGROUP, L.DR_BATCH_WAVE])
+def test_batch_view_in_place(gpu_device, form):
+    """dr_replay_batch_view: every context's results read in place from the batch's one
+    copy back equal the oracle's and dr_replay_batch's, in all four chain x delivery
+    modes, on repeated calls (the plan is reused) and across a rebuild (an append);
+    a capacity below a context's pushes is DR_E_CAPACITY."""
+    from dag_rider_amd.engine import ReplayBatchView
+
+    nw = 6
+    rng = np.random.default_rng(77)
+    items = []
+    for n in (4, 33, 64, 100, 128):
+        d = random_dag(rng, n, 4 * nw + 6, p_present=0.9, p_s=0.6, p_w=0.5, max_depth=8)
+        f = (n - 1) // 3
+        e = Engine(n, f, d.nrounds, gpu_device)
+        e.append_packed(d, 0, 4 * nw + 1)
+        items.append((d, f, e))
+    engines = [e for _, _, e in items]
+    engines[0].set_batch_form(form)
+    for cm in (L.DR_CHAIN_PERSISTENT, L.DR_CHAIN_LITERAL):
+        for dm in (L.DR_DELIVER_REF, L.DR_DELIVER_PAPER):
+            want = [oracle.PDag(d).replay(f, nw, cm, dm) for d, f, _ in items]
+            bv = ReplayBatchView(engines, nw, cm, dm)
+            for _ in range(2):
+                bv.run()
+                for w, g in zip(want, bv.results()):
+                    _same(g, w)
+            copied = ReplayBatch(engines, nw, cm, dm)()
+            bv.run()
+            for c, g in zip(copied, bv.results()):
+                _same(g, c)
+    items[1][2].append_packed(items[1][0])  # the rest of one DAG: the plan is rebuilt
+    bv = ReplayBatchView(engines, nw)
+    bv.run()
+    for (d, f, _), g in zip(items, bv.results()):
+        _same(g, oracle.PDag(d).replay(f, nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF))
+    np_max = max(len(g.push_wave) for g in bv.results())
+    small = ReplayBatchView(engines, nw, push_cap=np_max - 1)
+    with pytest.raises(L.DrError) as ex:
+        small.run()
+    assert ex.value.code == L.DR_E_CAPACITY
