@@ -556,10 +556,11 @@ __device__ __forceinline__ void load_round(const DagView &g, const MemoView &mv,
 }
 
 // full round r: ring[r-1] |= U_r, ring[r-d-2] |= WU_r[d] (lane w < WS owns word w)
-template <int WS, bool WEAK>
-// Every lane of wave 0 calls it (x is lane w's prefetched words for w < WS).
-__device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWords &x, int r, int bottom,
-                                               u64 *ring, int dmask) {
+// Threads 0 .. NTH-1 call it (wave 0: NTH = 64; a whole workgroup: NTH = its size);
+// x is thread w's prefetched words for w < WS.
+template <int WS, bool WEAK, int NTH = 64>
+__device__ __forceinline__ void expand_summary_t(const MemoView &mv, const RoundWords &x, int r, int bottom,
+                                                 u64 *ring, int dmask) {
   const int lane = threadIdx.x;
   if (lane < WS) {
     ring[(size_t)((r - 1) & dmask) * WS + lane] |= x.U;
@@ -572,10 +573,10 @@ __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWo
     }
   }
   if constexpr (!WEAK) return;
-  // deeper slots (a deep window: dd up to 254) over all 64 lanes -- 64/WS lanes per
-  // word, each taking every (64/WS)-th slot -- 8 loads in flight per lane, then
+  // deeper slots (a deep window: dd up to 254) over all NTH threads -- NTH/WS per
+  // word, each taking every (NTH/WS)-th slot -- 8 loads in flight per thread, then
   // their ORs (every (slot, word) is its own ring word)
-  constexpr int LPW = WS >= 64 ? 1 : 64 / WS;
+  constexpr int LPW = WS >= NTH ? 1 : NTH / WS;
   const int w = lane % WS, j = lane / WS;
   const int dlim = min(mv.dd, r - 1 - bottom);  // tr = r - d - 2 >= bottom
   if (j >= LPW) return;
@@ -592,6 +593,11 @@ __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWo
       if (d < dlim) ring[(size_t)((r - d - 2) & dmask) * WS + w] |= v[q];
     }
   }
+}
+template <int WS, bool WEAK>
+__device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWords &x, int r, int bottom, u64 *ring,
+                                               int dmask) {
+  expand_summary_t<WS, WEAK, 64>(mv, x, r, bottom, ring, dmask);
 }
 
 // ---------------------------------------------------------------------------
@@ -1664,7 +1670,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
       if (s_ctl[2]) break;  // regime restored at r (or bottom reached): CE_r stays the full total
       u64 e = 0, we = 0;
       if (s_ctl[1]) {
-        if (tid < 64) expand_summary<WS, true>(mv, cur, r, 0, ring, dmask);  // wave 0
+        expand_summary_t<WS, true, NT>(mv, cur, r, 0, ring, dmask);  // the whole workgroup
         if (tid == 0) e = mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
       } else {
         u64 rb = 0;
