@@ -76,15 +76,18 @@ def cpu_threads() -> int:
     return max(1, min(share, cpu_info()["affinity"] or 1))
 
 
-def measured_traffic(phase, W: int = 16):
+def measured_traffic(phase, W: int = 16, config: str = "c4"):
     """PMC-measured HBM bytes per launch of a phase's kernels (the newest traffic file that
-    profiled them), with the file it came from; (None, None) if none did."""
+    profiled them on this config), with the file it came from; (None, None) if none did."""
     for path in TRAFFIC_FILES:
         try:
             with open(path) as f:
                 t = json.load(f)
         except (OSError, ValueError):
             continue
+        # per config since round 4 ({config: {kernel: ...}}); round 3's file is C4's kernels
+        t = t.get(config, {}) if any(isinstance(v, dict) and "traffic_bytes" not in v for v in t.values()) else (
+            t if config == "c4" else {})
         for names in phase_kernels(phase, W):
             if all(k in t for k in names):
                 return sum(t[k]["traffic_bytes"] for k in names), os.path.relpath(path, ROOT)
@@ -659,8 +662,8 @@ def run_c5(args, rank: int, world: int, local: int, dist):
                    "dags": total if not args.dags else hi - lo, "dags_per_rank": hi - lo, "n": 128, "rounds": 128, "waves": nw,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "roofline": {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic("batch")[0],
-                     "traffic_unit": f"bytes/launch (rocprofv3 PMC, {measured_traffic('batch')[1]})",
+                     "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic("batch", 2, "c5")[0] if total == 4096 and not args.dags else None,
+                     "traffic_unit": f"bytes/launch (rocprofv3 PMC, {measured_traffic('batch', 2, 'c5')[1]})",
                      "kernel": "k_replay_small (batch.hpp)",
                      "bytes_per_launch": dag_bytes, "ms_per_launch": kms,
                      "note": "unique DAG bytes (strong rows + weak columns) once per launch"},
@@ -1021,7 +1024,8 @@ def main() -> int:
     # PMC traffic of the dominant phase's kernels for this row stride (REF delivery: the
     # profiled launch sequence); lines whose dominant kernel moves < 1 % of peak in its time
     # are latency-bound and say so
-    tr_bytes, tr_file = measured_traffic(dom, (cfg.n + 63) // 64) if args.deliver == "ref" and not args.no_memo else (None, None)
+    tr_bytes, tr_file = (measured_traffic(dom, (cfg.n + 63) // 64, cfg.name) if args.deliver == "ref" and not args.no_memo
+                         else (None, None))
     bound = "hbm" if ach >= 0.01 * HBM_PEAK_GBS else "latency"
     ms_per_step = dt / args.steps * 1e3
     out = {
