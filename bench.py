@@ -860,6 +860,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4-deep", "c4-deep64", "c4-dups", "c5",
                                                        "c4-loop"])
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the captured hipGraph of the launch sequence (DR_OPT_REPLAY_GRAPH)")
     ap.add_argument("--no-memo", action="store_true",
                     help="DR_OPT_MEMO 0: every cone swept whole (the general full-cone sweep line)")
     ap.add_argument("--deliver", default="ref", choices=["ref", "paper"])
@@ -939,6 +941,8 @@ def main() -> int:
     eng = Engine(cfg.n, cfg.faulty, d.nrounds, local)
     if args.no_memo:
         eng.set_memo(False)
+    if args.graph:
+        eng.set_replay_graph(True)
     t0 = time.perf_counter()
     eng.append_packed(d)
     log(f"[rank {rank}] loaded DAG into HBM in {time.perf_counter() - t0:.1f} s")
@@ -963,6 +967,7 @@ def main() -> int:
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0  # the timed region ends here
+    graph_state = eng.replay_graph_state()  # 1: the timed steps launched the captured hipGraph
     res = step.result()
     res = dataclasses.replace(res, **{k: getattr(res, k).copy() for k in
                                       ("commit", "vcount", "push_off", "push_wave", "pop_count", "pop_digest",
@@ -1041,6 +1046,7 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "u64",
         "data": f"synthetic (seeded generator, SURVEY.md s8(d) {cfg.name.upper()} parameters)",
+        "replay_form": {1: "hipGraph", 0: "launches", -1: "launches (capture failed)"}[graph_state],
         "config": {"workload": f"{cfg.name.upper()} full replay: n={cfg.n} x {cfg.last_round} rounds, {cfg.nwaves} "
                                f"waves, waveReady (persistent decidedWave) + orderVertices ({args.deliver}"
                                f"{', full cones' if args.deliver == 'ref' else ', dedup'}) per commit"

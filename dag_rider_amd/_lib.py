@@ -24,6 +24,7 @@ DR_OPT_DEVICE_PLAN = 2
 DR_OPT_PHASE_TIMING = 3
 DR_OPT_BATCH_FORM = 4
 DR_OPT_COMMIT_SPLIT = 5
+DR_OPT_REPLAY_GRAPH = 6
 DR_BATCH_AUTO, DR_BATCH_WORKGROUP, DR_BATCH_WAVE = 0, 1, 2
 DR_LEADER_CONST1, DR_LEADER_SEEDED, DR_LEADER_TABLE = 0, 1, 2
 DR_SHARD_ID_BYTES = 128
@@ -68,6 +69,7 @@ SIGNATURES = {
     "dr_set_leader_coin": (C.c_int, [P, C.c_int, C.c_uint64, C.c_int, P]),
     "dr_coin_leader": (C.c_int, [C.c_uint64, C.c_int, C.c_int]),
     "dr_wave_leader": (C.c_int, [P, C.c_int]),
+    "dr_replay_graph_state": (C.c_int, [P]),
     "dr_append_rounds_lists": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
     "dr_append_rounds_packed": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "dr_append_vertices": (C.c_int, [P, C.c_int, P, P, P, P, P, P]),

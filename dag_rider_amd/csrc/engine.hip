@@ -180,6 +180,20 @@ struct dr_ctx {
   int phase_timing = 2;
   bool timed(int i) const { return phase_timing >= 2 || (phase_timing == 1 && (i == 6 || i == 7)); }
   hipError_t rec(int i) { return timed(i) ? hipEventRecord(ev[i], stream) : hipSuccess; }
+  // DR_OPT_REPLAY_GRAPH (default 0): a device-planned dr_replay whose configuration
+  // (graph_key) matches the previous call's is captured once as a hipGraph --
+  // every launch, both streams, the copy of the outputs into pinned memory -- and
+  // later calls with the same key launch that graph.  The summary pass stays outside the
+  // graph, between its timing events (an event record inside a capture needs
+  // hipEventRecordExternal, which the HIP runtime torch loads refuses).  Off by default:
+  // C4 0.220 ms per step with the graph, 0.214 without; C3 0.272 / 0.270
+  // (profiles/r04/v6_graph_*) -- the device-side gaps between dependent kernels stay
+  int replay_graph = 0;
+  int graph_fail = 0;      // a capture or instantiation failed: eager launches from then on
+  int graph_state = 0;     // dr_replay_graph_state: the last dr_replay's form
+  uint64_t cfg_gen = 0;    // bumped by dr_set_option
+  std::vector<uint64_t> last_key, rg_key;
+  hipGraphExec_t rg_exec = nullptr;
   int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies
   int batch_form = DR_BATCH_AUTO;  // DR_OPT_BATCH_FORM (dr_replay_batch, first context)
   int cu_count = 0;         // compute units of the device (dr_replay_batch's form choice)
@@ -988,6 +1002,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
     if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join, c->ev_start, c->ev_wu})
     if (e) (void)hipEventDestroy(e);
+  if (c->rg_exec) (void)hipGraphExecDestroy(c->rg_exec);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1666,25 +1681,30 @@ int refresh_canon(dr_ctx *c) {
 // k_summary_commit, which with nwc > 0 also decides the commits of waves
 // 1..nwc (host arrays), then the canonical cone and prefixes.  Every replay
 // re-reads the whole DAG; nothing carries over from earlier calls.
+// parts: 1 = the row pass (k_summary_commit between its timing events), 2 = the rest
+// (a replay graph holds part 2 alone), 3 = both.
 int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
                   bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr,
-                  bool prefix = true) {
+                  bool prefix = true, int parts = 3) {
   const int T = c->nrounds - 1;
   if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
-  if (int rc = ensure_summary_bufs(c)) return rc;
-  HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
-  HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
-  // rows + commits, then the weak unions from the weak-column keys (on a second
-  // stream beside the row pass they only queued behind its workgroups and paid a
-  // cross-stream join: profiles/r02/v30_timeline.txt)
-  HIPCHK(c, c->rec(6));
-  HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
+  if (parts & 1) {
+    if (int rc = ensure_summary_bufs(c)) return rc;
+    HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
+    HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
+    // rows + commits, then the weak unions from the weak-column keys (on a second
+    // stream beside the row pass they only queued behind its workgroups and paid a
+    // cross-stream join: profiles/r02/v30_timeline.txt)
+    HIPCHK(c, c->rec(6));
+    HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
+  }
+  if (!(parts & 2)) return DR_OK;
   const bool early = fork && side;
   if (early) {  // stream2's work (side) needs only the rows' summaries and commits: fork here,
     // on the summary's end event when it is recorded anyway (each event costs the
     // stream ~7 us: profiles/r02/v34_timeline.txt)
     hipEvent_t fe = c->ev_fork;
-    if (c->timed(7))
+    if (c->timed(7) && (parts & 1))  // (a capture forks on an event of its own)
       fe = c->ev[7];
     else
       HIPCHK(c, hipEventRecord(fe, c->stream));
@@ -1743,6 +1763,7 @@ extern "C" int dr_set_leader_coin(dr_ctx *c, int mode, uint64_t seed, int k, con
 }
 
 extern "C" int dr_wave_leader(const dr_ctx *c, int wave) { return c ? c->lead_src(wave) : -1; }
+extern "C" int dr_replay_graph_state(const dr_ctx *c) { return c ? c->graph_state : 0; }
 
 #ifdef DR_SWEEP_TIMING
 // profiling build only: the per-query phase timings of the last k_sweep launch
@@ -1771,6 +1792,12 @@ extern "C" int dr_coin_leader(uint64_t seed, int wave, int n) {
 extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
   if (c) c->touch();
   if (!c) return DR_E_INVAL;
+  c->cfg_gen++;
+  if (option == DR_OPT_REPLAY_GRAPH) {
+    c->replay_graph = value != 0;
+    c->graph_fail = 0;
+    return DR_OK;
+  }
   if (option == DR_OPT_MEMO) {
     c->use_memo = value != 0;
     return DR_OK;
@@ -3001,6 +3028,18 @@ int deliver_planned(dr_ctx *c, const std::vector<Pop> &pops, uint64_t *pcount, u
 // caller then takes the host-planned path), else a DR_* status.
 // paper: DR_DELIVER_PAPER through the same pipeline, the delivery sweeps' masks
 // turned into first-pop ownership (replay_plan.hpp k_paper_*)
+// Everything dr_replay's device-planned launch sequence depends on besides the
+// DAG's contents (version): options, sizes, and the buffers it names.
+std::vector<uint64_t> graph_key(const dr_ctx *c, int nw, int chain_mode, bool paper, int64_t pcap) {
+  auto P = [](const void *p) { return (uint64_t)reinterpret_cast<uintptr_t>(p); };
+  return {c->version,          c->cfg_gen,         (uint64_t)c->nrounds, (uint64_t)nw,          (uint64_t)chain_mode,
+          (uint64_t)paper,     (uint64_t)pcap,     (uint64_t)c->phase_timing, (uint64_t)c->dmax_near,
+          (uint64_t)c->use_memo, (uint64_t)c->kprev_ok, (uint64_t)c->pin_cap, P(c->pin),  P(c->K.p), P(c->Kprev.p),
+          P(c->plan_arena.p), P(c->plan_out.p),   P(c->masks.p),       P(c->U.p),    P(c->WU.p),  P(c->SD.p),
+          P(c->commit.p),      P(c->vcount.p),     P(c->strong.p),       P(c->RG.p),   P(c->slot_src.p),
+          P(c->ppref.p)};
+}
+
 int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out *o) {
   const int WS = c->WS, T = c->nrounds - 1;
   const bool persistent = chain_mode == DR_CHAIN_PERSISTENT;
@@ -3081,104 +3120,178 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   u64 *h_pc = hv.take<u64>(pcap), *h_pd = hv.take<u64>(pcap), *h_pe = hv.take<u64>(pcap);
   const size_t out_bytes = hv.off;
 
-  // 0+1. summaries + commits; then the leader chains and pop planning on stream2
-  // beside the canonical cone on the main stream (the cone takes longer, so the
-  // join before the delivery sweeps finds stream2 done)
-  const int sc = dr::Q_SHORTCUT;
-  SweepArgs a;
-  std::function<int()> side = [&]() -> int {
-    // 2. leader chains
-    hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(),
-                       c->lead.as<uint16_t>(), nw,
-                       persistent ? 1 : 0, dr::Q_CHAIN | dr::Q_STRONG_ONLY | sc, task_wave, task_q, cq, plan);
-    HIPCHK(c, hipGetLastError());
-    a.q = cq;
-    a.nq = nw;
-    a.seq = 0;
-    a.masks = c->masks.as<u64>();
-    a.dlv = nullptr;
-    a.push_out = push_out;
-    a.push_n = cpush_n;
-    a.edges = cedges;
-    a.wedges = cwedges;
-    a.hits = hits;
-    a.stops = cstops;
-    a.stats = nullptr;
-    a.nq_dev = plan + dr::PL_NQC;
-    HIPCHK(c, c->rec(0));
-    HIPCHK(c, launch_sweep(c, a, dr::SW_CHAIN));
-    HIPCHK(c, c->rec(1));
-    // 3. pops
-    hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
-                       dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave, task_q, cq, cpush_n, push_out, pcap,
-                       task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
-    HIPCHK(c, hipGetLastError());
-    return 0;
-  };
-  if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false)) return rc;
-  if (paper) c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
-  // 3+4. delivery sweeps (merging with K), then each query's emission
-  a.q = dq;
-  a.push_out = nullptr;
-  a.push_n = nullptr;  // the chains' push counts: stream2's pop plan may still read them
-  a.hits = nullptr;
-  a.edges = dedges;
-  a.wedges = dwedges;
-  a.stops = dstops;
-  a.stats = dstats;
-  a.nq_dev = plan + dr::PL_NQD;
-  a.rcnt = nullptr;
-  dr::EmitArgs em{c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), c->Cc.as<u64>(), qcount, qdigest, qcut,
-                        dr::FinalArgs{}};
-  {
-    dr::FinalArgs &f = em.fin;
-    f.T = T;
-    f.nw = nw;
-    f.RG = c->RG.as<u64>();
-    f.CE = c->CE.as<u64>();
-    f.Gc = c->Gc.as<u64>();
-    f.Ec = c->Ec.as<u64>();
-    f.Cc = c->Cc.as<u64>();
-    f.commit = c->commit.as<uint8_t>();
-    f.vcount = c->vcount.as<int32_t>();
-    f.push_off = push_off;
-    f.push_wave = push_wave;
-    f.pop_q = pop_q;
-    f.pop_cur = pop_cur;
-    f.dq = dq;
-    f.stops = dstops;
-    f.dedges = dedges;
-    f.cedges = cedges;
-    f.dstats = dstats;
-    f.nseg = c->nseg.as<int32_t>();
-    f.plan = plan;
-    f.o = dr::FinalOut{h_commit, h_vcount, h_push_off, h_push_wave, h_pc, h_pd, h_pe, h_hdr};
+  // graph form (DR_OPT_REPLAY_GRAPH): launch the captured graph when nothing the
+  // launch sequence depends on changed since it was captured; capture when this
+  // call's configuration matches the previous call's (every buffer is sized then)
+  enum { EAGER, CAPTURE, LAUNCH } form = EAGER;
+  if (c->replay_graph && !c->graph_fail && c->phase_timing <= 1) {
+    if (c->pin_used || !c->pend.empty() || !c->h2q.empty()) HIPCHK(c, c->sync());  // the stage starts at pin
+    const std::vector<uint64_t> key = graph_key(c, nw, chain_mode, paper, pcap);
+    if (c->rg_exec && key == c->rg_key)
+      form = LAUNCH;
+    else if (key == c->last_key && c->pin_cap >= out_bytes)
+      form = CAPTURE;
   }
-  dr::SweepQuery probe{};
-  probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
-  HIPCHK(c, c->rec(2));
-  HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
-  if (paper) {  // first-pop ownership, then each query's delivered rounds
-    hipLaunchKernelGGL((dr::k_paper_plan<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->memo_view().dmax, plan,
-                       pop_q, dq, dstops, firstpop, qcut, qlo, firstK, qr_cnt, qr_off, qr_list);
+  auto enqueue = [&](char *stage, int parts) -> int {
+    // 0+1. summaries + commits; then the leader chains and pop planning on stream2
+    // beside the canonical cone on the main stream (the cone takes longer, so the
+    // join before the delivery sweeps finds stream2 done)
+    const int sc = dr::Q_SHORTCUT;
+    SweepArgs a;
+    std::function<int()> side = [&]() -> int {
+      // 2. leader chains
+      hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(),
+                         c->lead.as<uint16_t>(), nw,
+                         persistent ? 1 : 0, dr::Q_CHAIN | dr::Q_STRONG_ONLY | sc, task_wave, task_q, cq, plan);
+      HIPCHK(c, hipGetLastError());
+      a.q = cq;
+      a.nq = nw;
+      a.seq = 0;
+      a.masks = c->masks.as<u64>();
+      a.dlv = nullptr;
+      a.push_out = push_out;
+      a.push_n = cpush_n;
+      a.edges = cedges;
+      a.wedges = cwedges;
+      a.hits = hits;
+      a.stops = cstops;
+      a.stats = nullptr;
+      a.nq_dev = plan + dr::PL_NQC;
+      HIPCHK(c, c->rec(0));
+      HIPCHK(c, launch_sweep(c, a, dr::SW_CHAIN));
+      HIPCHK(c, c->rec(1));
+      // 3. pops
+      hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
+                         dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave, task_q, cq, cpush_n, push_out, pcap,
+                         task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
+      HIPCHK(c, hipGetLastError());
+      return 0;
+    };
+    if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false, parts)) return rc;
+    if (paper) c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
+    // 3+4. delivery sweeps (merging with K), then each query's emission
+    a.q = dq;
+    a.push_out = nullptr;
+    a.push_n = nullptr;  // the chains' push counts: stream2's pop plan may still read them
+    a.hits = nullptr;
+    a.edges = dedges;
+    a.wedges = dwedges;
+    a.stops = dstops;
+    a.stats = dstats;
+    a.nq_dev = plan + dr::PL_NQD;
+    a.rcnt = nullptr;
+    dr::EmitArgs em{c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), c->Cc.as<u64>(), qcount, qdigest, qcut,
+                          dr::FinalArgs{}};
+    {
+      dr::FinalArgs &f = em.fin;
+      f.T = T;
+      f.nw = nw;
+      f.RG = c->RG.as<u64>();
+      f.CE = c->CE.as<u64>();
+      f.Gc = c->Gc.as<u64>();
+      f.Ec = c->Ec.as<u64>();
+      f.Cc = c->Cc.as<u64>();
+      f.commit = c->commit.as<uint8_t>();
+      f.vcount = c->vcount.as<int32_t>();
+      f.push_off = push_off;
+      f.push_wave = push_wave;
+      f.pop_q = pop_q;
+      f.pop_cur = pop_cur;
+      f.dq = dq;
+      f.stops = dstops;
+      f.dedges = dedges;
+      f.cedges = cedges;
+      f.dstats = dstats;
+      f.nseg = c->nseg.as<int32_t>();
+      f.plan = plan;
+      f.o = dr::FinalOut{h_commit, h_vcount, h_push_off, h_push_wave, h_pc, h_pd, h_pe, h_hdr};
+    }
+    dr::SweepQuery probe{};
+    probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
+    HIPCHK(c, c->rec(2));
+    HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
+    if (paper) {  // first-pop ownership, then each query's delivered rounds
+      hipLaunchKernelGGL((dr::k_paper_plan<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->memo_view().dmax, plan,
+                         pop_q, dq, dstops, firstpop, qcut, qlo, firstK, qr_cnt, qr_off, qr_list);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, launch_paper_emit(c, nw, plan, dq, firstpop, qcut, qlo, firstK, qr_off, qr_list, qcount, qdigest,
+                                  qedges));
+      em.fin.firstpop = firstpop;
+      em.fin.qedges = qedges;
+    } else {  // REF: own rounds above the cut; the last workgroup: canonical prefixes G, E
+      HIPCHK(c, launch_own_emit(c, nw, plan, dq, dstops, qcount, qdigest, qcut));
+    }
+    HIPCHK(c, c->rec(3));
+    // 5. per-pop totals and outputs (the canonical prefixes came from the sweep launch's extra workgroup)
+    hipLaunchKernelGGL((dr::k_replay_final<1024>), dim3(1), dim3(1024), 0, c->stream, em);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, launch_paper_emit(c, nw, plan, dq, firstpop, qcut, qlo, firstK, qr_off, qr_list, qcount, qdigest,
-                                qedges));
-    em.fin.firstpop = firstpop;
-    em.fin.qedges = qedges;
-  } else {  // REF: own rounds above the cut; the last workgroup: canonical prefixes G, E
-    HIPCHK(c, launch_own_emit(c, nw, plan, dq, dstops, qcount, qdigest, qcut));
+    if (stage) {  // graph: the outputs into pinned memory inside the graph
+      const dr::CopySeg sg{c->plan_out.as<uint8_t>(), reinterpret_cast<uint8_t *>(stage), out_bytes};
+      HIPCHK(c, c->launch_copies(&sg, 1));
+    }
+    return DR_OK;
+  };  // enqueue
+  char *hb = nullptr;
+  bool enqueued = false;
+  if (form != EAGER)  // the row pass, timed, ahead of the graph
+    if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, nullptr, false, 1)) return rc;
+  if (form == CAPTURE) {
+    hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed);
+    int rc = e == hipSuccess ? enqueue(c->pin, 2) : DR_E_HIP;
+    hipGraph_t g = nullptr;
+    if (e == hipSuccess) {
+      const hipError_t e2 = hipStreamEndCapture(c->stream, &g);
+      if (e2 != hipSuccess) e = e2;
+    }
+    hipGraphExec_t x = nullptr;
+    if (rc == DR_OK && e == hipSuccess && g) e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    if (rc != DR_OK || e != hipSuccess || !x) {  // eager from here on, this call included
+      std::fprintf(stderr, "dagrider: replay graph capture failed (%s; %s); launching kernel by kernel\n",
+                   hipGetErrorString(e), rc != DR_OK ? c->err.c_str() : "launch sequence ok");
+      (void)hipGetLastError();
+      if (x) (void)hipGraphExecDestroy(x);
+      c->graph_fail = 1;
+      if (int rc2 = enqueue(nullptr, 2)) return rc2;  // after the row pass already launched
+      enqueued = true;
+      form = EAGER;
+    } else {
+      if (c->rg_exec) (void)hipGraphExecDestroy(c->rg_exec);
+      c->rg_exec = x;
+      c->rg_key = graph_key(c, nw, chain_mode, paper, pcap);  // after the capture's own K <-> Kprev swap
+      form = LAUNCH;
+    }
+  } else if (form == LAUNCH) {  // the host state a captured replay leaves behind
+    mark_rounds_clean(c);
+    c->kprev_ok = true;
+    c->canon_dd = c->memo_dd();
+    c->canon_lo = INT_MAX;
+    c->canon_T = T;
+    c->canon_host = false;
+    c->canon_ok = !paper;
   }
-  HIPCHK(c, c->rec(3));
-  // 5. per-pop totals and outputs (the canonical prefixes came from the sweep launch's extra workgroup)
-  hipLaunchKernelGGL((dr::k_replay_final<1024>), dim3(1), dim3(1024), 0, c->stream, em);
-  HIPCHK(c, hipGetLastError());
-  c->plan_host.resize(out_bytes);
-  HIPCHK(c, c->d2h(c->plan_host.data(), c->plan_out.p, out_bytes));
-  HIPCHK(c, c->sync());
+  if (form == LAUNCH) {
+    HIPCHK(c, hipGraphLaunch(c->rg_exec, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_sync, c->stream));
+    hipError_t e;
+    while ((e = hipEventQuery(c->ev_sync)) == hipErrorNotReady) {
+    }
+    HIPCHK(c, e);
+    hb = c->pin;
+    c->graph_state = 1;
+  } else {
+    if (!enqueued)
+      if (int rc = enqueue(nullptr, 3)) return rc;
+    c->plan_host.resize(out_bytes);
+    HIPCHK(c, c->d2h(c->plan_host.data(), c->plan_out.p, out_bytes));
+    HIPCHK(c, c->sync());
+    hb = c->plan_host.data();
+    c->graph_state = c->graph_fail ? -1 : 0;
+  }
+  c->last_key = graph_key(c, nw, chain_mode, paper, pcap);
   {  // device addresses -> the same offsets in the host copy
-    char *hb = c->plan_host.data(), *db = c->plan_out.as<char>();
+    char *db = c->plan_out.as<char>();
     auto H = [&](auto *p) { return reinterpret_cast<decltype(p)>(hb + (reinterpret_cast<char *>(p) - db)); };
     h_hdr = H(h_hdr);
     h_commit = H(h_commit);

@@ -99,6 +99,15 @@ class Engine:
         workgroup per wave, the default; identical results)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_COMMIT_SPLIT, int(mode)))
 
+    def set_replay_graph(self, on: bool):
+        """DR_OPT_REPLAY_GRAPH: replay a repeated device-planned dr_replay as one captured
+        hipGraph (default off; identical results)."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_REPLAY_GRAPH, int(on)))
+
+    def replay_graph_state(self) -> int:
+        """The last replay's form: 1 graph launch, 0 kernel by kernel, -1 after a failed capture."""
+        return int(self._L.dr_replay_graph_state(self._h))
+
     def set_batch_form(self, form: int):
         """DR_OPT_BATCH_FORM (read from a batch's first engine): DR_BATCH_AUTO, DR_BATCH_WORKGROUP
         (four wavefronts per DAG) or DR_BATCH_WAVE (one wavefront per DAG); identical results."""

@@ -47,7 +47,8 @@ enum {
   DR_E_STATE = -6     /* call order violated (e.g. append not contiguous) */
 };
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
-enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3, DR_OPT_BATCH_FORM = 4, DR_OPT_COMMIT_SPLIT = 5 };
+enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3, DR_OPT_BATCH_FORM = 4, DR_OPT_COMMIT_SPLIT = 5,
+       DR_OPT_REPLAY_GRAPH = 6 };
 enum { DR_BATCH_AUTO = 0, DR_BATCH_WORKGROUP = 1, DR_BATCH_WAVE = 2 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
 enum { DR_WEAK_LITERAL = 0, DR_WEAK_PAPER = 1 };
@@ -103,8 +104,17 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * several workgroups (each computes S_1, S_2 whole and a share of S_3); 0 = one
  * workgroup per wave, the faster on MI355X at C4.  Identical
  * results.
- * Identical results. */
+ * DR_OPT_REPLAY_GRAPH (default 0): 1 = a device-planned dr_replay called again
+ * with the same DAG version, options, wave count, modes and push capacity is
+ * captured once as a hipGraph (both streams' launches after the summary pass
+ * and the copy of the outputs into pinned memory) and later such calls launch
+ * the graph (with DR_OPT_PHASE_TIMING <= 1).  0 = launch every kernel per call,
+ * as fast on MI355X at C3/C4.  Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
+/* The form of the context's last dr_replay: 1 = a captured graph was launched,
+ * 0 = kernels launched one by one, -1 = one by one after a failed capture
+ * (DR_OPT_REPLAY_GRAPH then stays off until set again). */
+int dr_replay_graph_state(const dr_ctx *ctx);
 
 /* p.dag[r] = append(p.dag[r], v) (process.go:229) for whole rounds
  * [r0, r0+k), r0 == dr_num_rounds(ctx): the flattened [][]vertex.
