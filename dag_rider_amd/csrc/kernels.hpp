@@ -500,9 +500,22 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
 #pragma unroll
   for (int p = 0; p < WPF; p++)
     if (c0 + (uint32_t)(p * EPP) < c1) column(wv[p], wk[p]);  // wave-uniform
-  for (uint32_t j0 = c0 + (uint32_t)(WPF * EPP); j0 < c1; j0 += EPP) {
-    const uint32_t jj = j0 + (uint32_t)(tid / WS);
-    column(jj < c1 ? g.wc_rows[(size_t)jj * WS + w] : 0ULL, jj < c1 ? g.wc_key[jj] : 0u);
+  // the rest CB passes at a time: their loads in flight together (a deep window's
+  // round holds ~1000 columns: one load latency per pass had made the weak columns
+  // ~90 us of each partial round at c4-deep)
+  constexpr int CB = 8;
+  for (uint32_t j0 = c0 + (uint32_t)(WPF * EPP); j0 < c1; j0 += CB * EPP) {
+    u64 rv[CB];
+    uint32_t kv[CB];
+#pragma unroll
+    for (int q = 0; q < CB; q++) {
+      const uint32_t jj = j0 + (uint32_t)(q * EPP) + (uint32_t)(tid / WS);
+      rv[q] = jj < c1 ? g.wc_rows[(size_t)jj * WS + w] : 0ULL;
+      kv[q] = jj < c1 ? g.wc_key[jj] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < CB; q++)
+      if (j0 + (uint32_t)(q * EPP) < c1) column(rv[q], kv[q]);  // wave-uniform
   }
   const uint32_t f0 = g.far_roff[r], f1 = g.far_roff[r + 1];
   for (uint32_t e = f0 + tid; e < f1; e += NT) {
@@ -530,7 +543,9 @@ struct RoundWords {
   u64 P, K, U, WU[DDR];
   uint32_t C0, C1;  // the round's weak-column range
   u64 SD;           // the round's strong-degree sum (summary rounds' edge count)
-  uint32_t NW;      // the round's weak edges
+  uint32_t NW0, NW1;  // weak_roff[r], weak_roff[r+1]: the round's weak edges = NW1 - NW0, subtracted where
+                      // used (a subtraction here waits on every load in flight, prefetches included)
+  __device__ __forceinline__ uint32_t NW() const { return NW1 - NW0; }
 };
 
 template <int WS, bool MERGE, bool SUMMARY, bool WEAK>
@@ -545,7 +560,10 @@ __device__ __forceinline__ void load_round(const DagView &g, const MemoView &mv,
   if constexpr (SUMMARY) {
     if (w == 0) {
       x.SD = mv.SD[r];
-      if constexpr (WEAK) x.NW = g.weak_roff[r + 1] - g.weak_roff[r];
+      if constexpr (WEAK) {
+        x.NW0 = g.weak_roff[r];
+        x.NW1 = g.weak_roff[r + 1];
+      }
     }
     x.U = mv.U[(size_t)r * WS + w];
     if constexpr (WEAK) {
@@ -574,25 +592,65 @@ __device__ __forceinline__ void expand_summary_t(const MemoView &mv, const Round
   }
   if constexpr (!WEAK) return;
   // deeper slots (a deep window: dd up to 254) over all NTH threads -- NTH/WS per
-  // word, each taking every (NTH/WS)-th slot -- 8 loads in flight per thread, then
-  // their ORs (every (slot, word) is its own ring word)
+  // word, each taking every (NTH/WS)-th slot -- B loads in flight per thread, then
+  // their ORs (every (slot, word) is its own ring word).  Wave 0 alone (NTH = 64):
+  // B = 24, one round trip per round up to dd = 99 at WS = 16 (8 took three at dd = 79)
   constexpr int LPW = WS >= NTH ? 1 : NTH / WS;
+  constexpr int B = NTH == 64 ? 24 : 8;
   const int w = lane % WS, j = lane / WS;
   const int dlim = min(mv.dd, r - 1 - bottom);  // tr = r - d - 2 >= bottom
   if (j >= LPW) return;
-  for (int d0 = DDR + j; d0 < dlim; d0 += 8 * LPW) {
-    u64 v[8];
+  for (int d0 = DDR + j; d0 < dlim; d0 += B * LPW) {
+    u64 v[B];
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
+    for (int q = 0; q < B; q++) {
       const int d = d0 + q * LPW;
       v[q] = d < dlim ? mv.WU[((size_t)r * mv.dd + d) * WS + w] : 0ULL;
     }
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
+    for (int q = 0; q < B; q++) {
       const int d = d0 + q * LPW;
       if (d < dlim) ring[(size_t)((r - d - 2) & dmask) * WS + w] |= v[q];
     }
   }
+}
+// The deep slots of a full round preloaded one round ahead (k_canon's walk): thread
+// t holds slots DDR + t/WS + q*LPW, q < PF, of word t % WS (PF = 4 covers dd <= 66 at
+// WS = 16, NT = 512); later slots load when used.  Threads 0 .. NTH-1 call both.
+template <int WS, int NTH, int PF>
+__device__ __forceinline__ void deep_slots_load(const MemoView &mv, int r, int bottom, u64 (&v)[PF]) {
+  constexpr int LPW = WS >= NTH ? 1 : NTH / WS;
+  const int w = threadIdx.x % WS, j = threadIdx.x / WS;
+  const int dlim = min(mv.dd, r - 1 - bottom);
+#pragma unroll
+  for (int q = 0; q < PF; q++) {
+    const int d = DDR + j + q * LPW;
+    v[q] = (j < LPW && d < dlim) ? mv.WU[((size_t)r * mv.dd + d) * WS + w] : 0ULL;
+  }
+}
+template <int WS, int NTH, int PF>
+__device__ __forceinline__ void expand_summary_pre(const MemoView &mv, const RoundWords &x, int r, int bottom,
+                                                   u64 *ring, int dmask, const u64 (&v)[PF]) {
+  const int lane = threadIdx.x;
+  if (lane < WS) {
+    ring[(size_t)((r - 1) & dmask) * WS + lane] |= x.U;
+#pragma unroll
+    for (int d = 0; d < DDR; d++) {
+      const int tr = r - d - 2;
+      if (d < mv.dd && tr >= bottom) ring[(size_t)(tr & dmask) * WS + lane] |= x.WU[d];
+    }
+  }
+  constexpr int LPW = WS >= NTH ? 1 : NTH / WS;
+  const int w = lane % WS, j = lane / WS;
+  if (j >= LPW) return;
+  const int dlim = min(mv.dd, r - 1 - bottom);
+#pragma unroll
+  for (int q = 0; q < PF; q++) {
+    const int d = DDR + j + q * LPW;
+    if (d < dlim) ring[(size_t)((r - d - 2) & dmask) * WS + w] |= v[q];
+  }
+  for (int d = DDR + j + PF * LPW; d < dlim; d += LPW)  // beyond the preloaded slots
+    ring[(size_t)((r - d - 2) & dmask) * WS + w] |= mv.WU[((size_t)r * mv.dd + d) * WS + w];
 }
 template <int WS, bool WEAK>
 __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWords &x, int r, int bottom, u64 *ring,
@@ -1055,7 +1113,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
             expand_summary<WS, WEAK>(mv, cur, r, q.bottom, ring, dmask);  // every lane of wave 0
             if (tid == 0) {
               my_edges += cur.SD;
-              if (WEAK) my_wedges += cur.NW;
+              if (WEAK) my_wedges += cur.NW();
             }
             low = min(low, WEAK ? r - 1 - mv.dd : r - 1);
             if (tid == 0) s_ctl[0] = low;
@@ -1467,7 +1525,13 @@ __global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, in
   }
   if (r > T) return;  // wave-uniform: this wave alone
   u64 *sW = wu_lds + (size_t)wid * dd * WS;
-  for (int k = lane; k < dd * WS; k += 64) sW[k] = 0;
+  // 16-B LDS and HBM accesses when every row is 16-B aligned (WS even)
+  typedef u64 u64v2 __attribute__((ext_vector_type(2)));
+  if constexpr (WS % 2 == 0) {
+    for (int k = lane; k < dd * WS / 2; k += 64) reinterpret_cast<u64v2 *>(sW)[k] = u64v2{0, 0};
+  } else {
+    for (int k = lane; k < dd * WS; k += 64) sW[k] = 0;
+  }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   // every weak-column entry has at least one source: its key alone is the union
   for (uint32_t j = g.wc_roff[r] + lane; j < g.wc_roff[r + 1]; j += 64) {
@@ -1503,32 +1567,42 @@ __global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, in
     if (lane == 0) RG[r] = dg;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  for (int k = lane; k < dd * WS; k += 64) WU[(size_t)r * dd * WS + k] = sW[k];
+  if constexpr (WS % 2 == 0) {
+    u64v2 *dst = reinterpret_cast<u64v2 *>(WU + (size_t)r * dd * WS);
+    for (int k = lane; k < dd * WS / 2; k += 64) dst[k] = reinterpret_cast<const u64v2 *>(sW)[k];
+  } else {
+    for (int k = lane; k < dd * WS; k += 64) WU[(size_t)r * dd * WS + k] = sW[k];
+  }
 }
 
 // K^cand_r = U_{r+1} | OR_d WU_{r+d+2}[d] (the cone of round r when every round
 // above it is full); K^cand_T = P_T.  good_r = K^cand_r covers P_r.  CE_r (the
 // canonical round's edges) defaults to the full-round total, RD_r (its vertex
-// count |K_r & P_r|) to K^cand's.  One wave per round, lane w < WS owns word w.
+// count |K_r & P_r|) to K^cand's.  One wave per round, lane w < WS owns word w;
+// the window's WU terms are spread over all 64 lanes (64/WS classes of delta d,
+// OR-reduced across lanes): a deep window (dd = 79) has 79 terms per word.
 template <int WS>
 __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K,
                                                uint8_t *__restrict__ good, u64 *__restrict__ CE,
                                                u64 *__restrict__ RD, int *__restrict__ rlo, int lo) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
   if (rlo && blockIdx.x == 0 && threadIdx.x == 0) *rlo = lo;  // k_canon_diff / k_canon lower it
-  if (r > T) return;
+  if (r > T) return;  // wave-uniform
+  constexpr int G = WS >= 64 ? 1 : 64 / WS;  // delta classes
+  const int wl = w % WS, cls = w / WS;
+  u64 k = 0;
+  if (r < T && cls < G) {
+    if (cls == 0) k = mv.U[(size_t)(r + 1) * WS + wl];
+#pragma unroll 4
+    for (int d = cls; d < mv.dd && r + d + 2 <= T; d += G) k |= mv.WU[((size_t)(r + d + 2) * mv.dd + d) * WS + wl];
+  }
+#pragma unroll
+  for (int m = WS; m < 64; m <<= 1) k |= shfl_xor64(k, m);
   bool bad = false;
   int cnt = 0;
   if (w < WS) {
     const u64 p = g.present[(size_t)r * WS + w];
-    u64 k;
-    if (r == T) {
-      k = p;
-    } else {
-      k = mv.U[(size_t)(r + 1) * WS + w];
-#pragma unroll 8
-      for (int d = 0; d < mv.dd && r + d + 2 <= T; d++) k |= mv.WU[((size_t)(r + d + 2) * mv.dd + d) * WS + w];
-    }
+    if (r == T) k = p;
     K[(size_t)r * WS + w] = k;
     bad = (k & p) != p;
     cnt = popc64(k & p);
@@ -1591,7 +1665,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
   int pos = T;  // rounds >= pos are final; the regime holds below pos until the next bad round
   int segs = 0;
   int lo_w = T + 1;  // the lowest round a segment walk reached (RD below it is the full count)
-  DR_TT(int walked = 0; if (tid == 0) g_canon_timing[0] = wall_clock64();)
+  DR_TT(int walked = 0; if (tid == 0) { g_canon_timing[0] = wall_clock64(); g_canon_timing[5] = 0; })
   while (true) {
     // next bad round below pos: thread t looks at the 8 rounds of block (pos-1)/8 - t - i*NT
     if (tid == 0) s_ctl[0] = -1;
@@ -1617,13 +1691,24 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     __syncthreads();
     if (b < 0) break;
     segs++;
+    DR_TT(const u64 t_init = wall_clock64();)
     // state at b: F_b = K^cand_b; pending for rounds below from the full rounds above b
     for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
     __syncthreads();
-    RoundWords cur{}, nxt{};
+    // the walk's per-round words three rounds ahead, in four register sets that the
+    // unrolled loop below uses in turn (one round ahead, every round paid a load
+    // latency: ~2.2 us a round at c4-deep; rotating the sets through moves waits for the
+    // loads in flight, so the sets keep their registers and the rounds take turns).  The
+    // walk's threads share the round through LDS only: its barriers order LDS alone and
+    // leave the prefetches in flight (lds_barrier).
+    constexpr int PF = 4;
+    RoundWords rw[4] = {};
+    u64 dv[4][PF];
     if (tid < WS) {
       ring[(size_t)(b & dmask) * WS + tid] = K[(size_t)b * WS + tid];
-      load_round<WS, false, true, true>(g, mv, b, cur);
+      load_round<WS, false, true, true>(g, mv, b, rw[0]);
+      if (b >= 1) load_round<WS, false, true, true>(g, mv, b - 1, rw[1]);
+      if (b >= 2) load_round<WS, false, true, true>(g, mv, b - 2, rw[2]);
     }
     // (round x, word w) pairs over every thread: a deep window has dd^2/2 terms per word
     for (int it = tid; it < mv.dd * WS; it += NT) {
@@ -1638,51 +1723,66 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     __syncthreads();
     int run = 0;
     int r = b;
-    for (;; --r) {
-      if (tid < 64) {
-        int cnt = 0;
-        bool full = true;
-        if (tid < WS) {
-          if (r > 0) load_round<WS, false, true, true>(g, mv, r - 1, nxt);
-          const int slot = (r & dmask) * WS + tid;
-          const u64 f = ring[slot];
-          ring[slot] = 0;
-          const u64 p = cur.P;
-          F[tid] = f;
-          FE[tid] = f & p;
-          K[(size_t)r * WS + tid] = f;
-          full = (f & p) == p;
-          cnt = popc64(f & p);
-        }
-        full = __all(full);
+    deep_slots_load<WS, NT, PF>(mv, b, 0, dv[0]);
+    deep_slots_load<WS, NT, PF>(mv, max(b - 1, 0), 0, dv[1]);
+    deep_slots_load<WS, NT, PF>(mv, max(b - 2, 0), 0, dv[2]);
+    DR_TT(if (tid == 0) g_canon_timing[5] += wall_clock64() - t_init;)
+    bool done = false;
+    while (!done) {
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-        if (g.dup_off && r >= 1) cnt += dup_count<WS>(g, r, tid < WS ? FE[tid] : 0ULL);  // every slot (REF)
-        run = full ? run + 1 : 0;
-        if (tid == 0) {
-          s_ctl[1] = full;
-          s_ctl[2] = (run >= mv.dmax) || r == 0;
-          s_edges[0] = 0;
-          RD[r] = r == 0 ? 0 : (u64)cnt;
+      for (int k = 0; k < 4; k++) {
+        const RoundWords &cur = rw[k];
+        if (r >= 3) {  // round r-3's words, in flight
+          deep_slots_load<WS, NT, PF>(mv, r - 3, 0, dv[(k + 3) & 3]);
+          if (tid < WS) load_round<WS, false, true, true>(g, mv, r - 3, rw[(k + 3) & 3]);
         }
+        if (tid < 64) {
+          int cnt = 0;
+          bool full = true;
+          if (tid < WS) {
+            const int slot = (r & dmask) * WS + tid;
+            const u64 f = ring[slot];
+            ring[slot] = 0;
+            const u64 p = cur.P;
+            F[tid] = f;
+            FE[tid] = f & p;
+            K[(size_t)r * WS + tid] = f;
+            full = (f & p) == p;
+            cnt = popc64(f & p);
+          }
+          full = __all(full);
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+          if (g.dup_off && r >= 1) cnt += dup_count<WS>(g, r, tid < WS ? FE[tid] : 0ULL);  // every slot (REF)
+          run = full ? run + 1 : 0;
+          if (tid == 0) {
+            s_ctl[1] = full;
+            s_ctl[2] = (run >= mv.dmax) || r == 0;
+            s_edges[0] = 0;
+            RD[r] = r == 0 ? 0 : (u64)cnt;
+          }
+        }
+        lds_barrier();
+        if (s_ctl[2]) {  // regime restored at r (or bottom reached): CE_r stays the full total
+          done = true;
+          break;
+        }
+        u64 e = 0, we = 0;
+        if (s_ctl[1]) {
+          expand_summary_pre<WS, NT, PF>(mv, cur, r, 0, ring, dmask, dv[k]);  // the whole workgroup
+          if (tid == 0) e = cur.SD + cur.NW();  // prefetched with the round's words
+        } else {
+          u64 rb = 0;
+          expand_round<WS, NT, true>(g, r, 0, FE, ring, depth, K, mv.U + (size_t)r * WS, e, we, rb);
+        }
+        e += we;
+        if (e) atomicAdd(&s_edges[0], e);
+        DR_TT(walked++;)
+        lds_barrier();
+        if (tid == 0) CE[r] = s_edges[0];
+        --r;
+        lds_barrier();
       }
-      __syncthreads();
-      if (s_ctl[2]) break;  // regime restored at r (or bottom reached): CE_r stays the full total
-      u64 e = 0, we = 0;
-      if (s_ctl[1]) {
-        expand_summary_t<WS, true, NT>(mv, cur, r, 0, ring, dmask);  // the whole workgroup
-        if (tid == 0) e = mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
-      } else {
-        u64 rb = 0;
-        expand_round<WS, NT, true>(g, r, 0, FE, ring, depth, K, mv.U + (size_t)r * WS, e, we, rb);
-      }
-      e += we;
-      if (e) atomicAdd(&s_edges[0], e);
-      DR_TT(walked++;)
-      __syncthreads();
-      if (tid == 0) CE[r] = s_edges[0];
-      cur = nxt;
-      __syncthreads();
     }
     pos = r;
     lo_w = min(lo_w, r);

@@ -40,6 +40,7 @@
 namespace drs {
 
 using dr::u64;
+using dr::shfl_xor64;
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int MS_NT = 256;  // threads per workgroup (4 waves)
@@ -89,11 +90,6 @@ struct MArgs {
   const uint16_t *slot_src;  // 1-based source per slot (0 = ghost)
   int32_t n, W, WSs, SP, G, shard0, nlocal, local, nq, depth, dd, dmax, summary, R, nlead, T;
 };
-
-__device__ __forceinline__ u64 shfl_xor64(u64 v, int m) {
-  const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-  return ((u64)(uint32_t)hi << 32) | (uint32_t)lo;
-}
 
 // Round summaries of one shard: one workgroup per (round, local shard).  Thread t's
 // 16-B chunks hold columns (2t) mod SP and (2t+1) mod SP of every row it reads

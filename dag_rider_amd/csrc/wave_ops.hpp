@@ -62,6 +62,19 @@ __device__ __forceinline__ u64 readlane64(u64 x, int l) {
 __device__ __forceinline__ u64 shfl64(u64 x, int l) {
   return ((u64)(uint32_t)__shfl((int)(x >> 32), l) << 32) | (uint32_t)__shfl((int)(uint32_t)x, l);
 }
+// Workgroup barrier that orders LDS only: the release waits for this thread's LDS
+// accesses (lgkmcnt), not for its global loads in flight, so loads prefetched ahead of a
+// barrier stay in flight across it (__syncthreads waits for every vmcnt event).  For
+// loops whose threads share data through LDS alone.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// lane (lane ^ m)'s value; every lane of the wave must be active
+__device__ __forceinline__ u64 shfl_xor64(u64 x, int m) {
+  return ((u64)(uint32_t)__shfl_xor((int)(x >> 32), m) << 32) | (uint32_t)__shfl_xor((int)(uint32_t)x, m);
+}
 // lane (lane - d)'s value, own value for lane < d
 __device__ __forceinline__ u64 shfl_up64(u64 x, int d) {
   return ((u64)(uint32_t)__shfl_up((int)(x >> 32), d) << 32) | (uint32_t)__shfl_up((int)(uint32_t)x, d);

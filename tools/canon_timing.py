@@ -31,4 +31,5 @@ for name in sys.argv[1:] or ["c4", "c3"]:
         assert lib.dr_debug_canon_timing(L.ptr(buf)) == 0
     t = buf.astype(np.float64)
     print(json.dumps({"config": name, "segments_us": (t[1] - t[0]) * 0.01, "positions_us": (t[2] - t[1]) * 0.01,
-                      "segments": int(buf[3]), "rounds_walked": int(buf[4])}), flush=True)
+                      "segments": int(buf[3]), "rounds_walked": int(buf[4]),
+                      "segment_init_us": float(t[5]) * 0.01}), flush=True)
