@@ -596,7 +596,7 @@ __device__ __forceinline__ void expand_summary_t(const MemoView &mv, const Round
   // their ORs (every (slot, word) is its own ring word).  Wave 0 alone (NTH = 64):
   // B = 24, one round trip per round up to dd = 99 at WS = 16 (8 took three at dd = 79)
   constexpr int LPW = WS >= NTH ? 1 : NTH / WS;
-  constexpr int B = NTH == 64 ? 24 : 8;
+  constexpr int B = (NTH == 64 && WS >= 16) ? 24 : 8;  // (24 at WS = 4 took the WS = 4 sweeps from 4 to 3 waves/SIMD)
   const int w = lane % WS, j = lane / WS;
   const int dlim = min(mv.dd, r - 1 - bottom);  // tr = r - d - 2 >= bottom
   if (j >= LPW) return;
