@@ -211,6 +211,11 @@ func (m *Mirror) SetLeaderCoin(mode int, seed uint64, table []int) error {
 // of getWaveVertexLeader (process.go:357-371) is (round(wave,1), WaveLeader).
 func (m *Mirror) WaveLeader(wave int) int { return int(C.dr_wave_leader(m.ctx, C.int(wave))) }
 
+// ReplayGraphState is the form of the mirror's last Replay (dr_replay_graph_state): 1 = the
+// captured hipGraph was launched (DR_OPT_REPLAY_GRAPH), 0 = kernel by kernel, -1 = kernel by
+// kernel after a failed capture.
+func (m *Mirror) ReplayGraphState() int { return int(C.dr_replay_graph_state(m.ctx)) }
+
 // WaveReady is waveReady(wave) (process.go:314-354) given decidedWave: the
 // commit decision, the vote count (-1: no leader vertex) and on commit the
 // waves whose leaders are pushed onto leadersStack, in push order.
