@@ -36,7 +36,7 @@ $(BUILD)/host_rounds.o: $(PKG)/csrc/host_rounds.cpp $(PKG)/csrc/host_rounds.hpp 
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
 ENGINE_DEPS := $(PKG)/csrc/engine.hip $(PKG)/csrc/kernels.hpp $(PKG)/csrc/wave_ops.hpp $(PKG)/csrc/replay_plan.hpp $(PKG)/csrc/batch.hpp $(PKG)/csrc/batch1w.hpp $(PKG)/csrc/general.hpp $(PKG)/csrc/host_rounds.hpp include/dagrider_gpu.h
-SHARD_DEPS  := $(PKG)/csrc/shard.hip $(PKG)/csrc/shard_memo.hpp $(PKG)/csrc/shard_fused.hpp $(PKG)/csrc/wave_ops.hpp include/dagrider_shard.h include/dagrider_gpu.h
+SHARD_DEPS  := $(PKG)/csrc/shard.hip $(PKG)/csrc/shard_memo.hpp $(PKG)/csrc/shard_fused.hpp $(PKG)/csrc/shard_step.hpp $(PKG)/csrc/wave_ops.hpp include/dagrider_shard.h include/dagrider_gpu.h
 
 $(BUILD)/engine.o: $(ENGINE_DEPS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

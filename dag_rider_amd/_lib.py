@@ -99,6 +99,7 @@ SIGNATURES = {
     "dr_shard_reach_sets": (C.c_int, [P, C.c_int, P, P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dr_shard_path_batch": (C.c_int, [P, C.c_int, P, P, C.c_int, P]),
     "dr_shard_stats": (C.c_int, [P, C.POINTER(f32), C.POINTER(u64), C.POINTER(u64)]),
+    "dr_shard_host_syncs": (C.c_int, [P, C.POINTER(u64)]),
     "dr_shard_set_option": (C.c_int, [P, C.c_int, C.c_int]),
     "dr_shard_set_leader_coin": (C.c_int, [P, C.c_int, C.c_uint64, C.c_int, P]),
     "dr_shard_wave_commit": (C.c_int, [P, C.c_int, C.c_int, P, P]),

@@ -101,7 +101,10 @@ __global__ __launch_bounds__(256) void k_gsweep(DagView g, GView gv, const GQuer
         }
       }
       __syncthreads();
-      if (!s_any) {
+      const int any = s_any;
+      // every wave has read s_any before wave 0 rewrites it (and NEW) for the next round
+      __syncthreads();
+      if (!any) {
         r--;
         continue;
       }

@@ -67,6 +67,7 @@
 #include "dagrider_shard.h"
 #include "shard_fused.hpp"
 #include "shard_memo.hpp"
+#include "shard_step.hpp"
 #include "wave_ops.hpp"
 
 namespace {
@@ -594,9 +595,14 @@ struct dr_shard {
   // canonical cone and prefixes, the stepped queries' buffers
   SBuf sdr, mU, mWU, mK, mgood, mRD, mCE, mRG, mC, mE, mG, mksend, mkrecv, mq, mst, mpend, mrecv[2], msend, mmasks,
       mpush, mqidx, mqout;
+  // stepped form: the canonical walk's query; S_1 per wave (k_ms_lcol; RCCL mode: the
+  // exchanged partials, lcol_g slots of lcol_nw waves), valid until an append or a coin change
+  SBuf mcq, mlcol, mlcolp;
+  bool lcol_ok = false;
+  int lcol_nw = 1, lcol_g = 1;
+  uint64_t syncs = 0;  // host waits of the last query call (dr_shard_host_syncs)
   std::vector<uint64_t> h_sdr;  // strong degree sum per round (host copy)
-  int *alive = nullptr;         // pinned: live queries after the last polled step
-  int hint_canon = 4, hint_batch = 8;  // steps the last replay's canonical walk / query batch took
+  int hint_canon = 8, hint_batch = 12;  // steps the last replay's canonical walk / query batch took
   // pinned staging for the memo replay's small transfers (queries in, results out);
   // reset at each replay's start, grown after a stream sync
   char *pin = nullptr;
@@ -697,6 +703,7 @@ int sync_weak(dr_shard *c) {
     cb += k.size();
   }
   SHCHK(c, hipMemcpyAsync(c->wcro.p, coffs.data(), coffs.size() * 8, hipMemcpyHostToDevice, c->stream));
+  c->syncs++;
   SHCHK(c, hipStreamSynchronize(c->stream));
   c->weak_dirty = false;
   return DR_OK;
@@ -1108,45 +1115,17 @@ drs::MArgs make_margs(dr_shard *c, int nq, int T = -1) {
 
 bool memo_applies(const dr_shard *c) { return c->memo && c->dmax <= 65; }
 
-// Step a batch of queries (states in st0, rings clear) until none is live.
-// Returns the number of steps taken (the final states are in st[steps & 1]).
-int run_steps(dr_shard *c, const drs::MArgs &a, int nq, int maxsteps, int *steps, int hint = 4) {
-  const dim3 grid(nq, c->nlocal), block(drs::MS_NT);
-  // the first poll comes after `hint` steps (what the same batch took last time;
-  // extra steps after the last query finished exit at once), then every 2
-  int next_poll = std::max(2, hint);
-  for (int j = 0;; j++) {
-    hipLaunchKernelGGL(drs::k_ms_step, grid, block, 0, c->stream, a, j);
-    SHCHK(c, hipGetLastError());
-    if (!c->local) {
-      SHNCCL(c, ncclAllGather(c->msend.p, c->mrecv[(j + 1) & 1].p, (size_t)nq * c->WSs, ncclUint64, c->comm,
-                              c->stream));
-      c->last_xbytes += (uint64_t)nq * c->WSs * 8;
-    }
-    c->last_rounds++;
-    const int done_steps = j + 1;
-    // each poll is one host round trip
-    if (done_steps >= next_poll || done_steps >= maxsteps) {
-      next_poll = done_steps + 2;
-      const drs::MState *st = (done_steps & 1) ? a.st1 : a.st0;
-      hipLaunchKernelGGL(drs::k_ms_alive, dim3(1), block, 0, c->stream, st, nq, c->alive);
-      SHCHK(c, hipGetLastError());
-      SHCHK(c, hipStreamSynchronize(c->stream));
-      if (*c->alive == 0) {
-        *steps = done_steps;
-        return DR_OK;
-      }
-      if (done_steps >= maxsteps)
-        return c->fail(DR_E_HIP, "memo replay: %d queries still live after %d steps", *c->alive, maxsteps);
-    }
-  }
+// every host wait of a query call goes through here (dr_shard_host_syncs counts them)
+hipError_t host_sync(dr_shard *c) {
+  c->syncs++;
+  return hipStreamSynchronize(c->stream);
 }
 
 // n bytes of the pinned staging area (256-B aligned); nullptr on failure
 char *stage(dr_shard *c, size_t n) {
   const size_t at = (c->pin_used + 255) & ~(size_t)255;
   if (at + n > c->pin_cap) {
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return nullptr;  // staged copies still in flight
+    if (host_sync(c) != hipSuccess) return nullptr;  // staged copies still in flight
     const size_t cap = std::max<size_t>({(size_t)4 << 20, 2 * c->pin_cap, 2 * (at + n)});
     char *q = nullptr;
     if (hipHostMalloc((void **)&q, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
@@ -1160,39 +1139,10 @@ char *stage(dr_shard *c, size_t n) {
   return c->pin + at;
 }
 
-// States of a stepped batch: queries [0, qs.size()) from the host (rings clear);
-// nq slots in all (k_ms_plan fills the chain slots past them).
-int init_states(dr_shard *c, const std::vector<drs::MQuery> &qs, int nq, bool states = true) {
-  const int nh = (int)qs.size();
-  SHCHK(c, c->mq.ensure((size_t)std::max(nq, 1) * sizeof(drs::MQuery)));
-  SHCHK(c, c->mst.ensure((size_t)2 * std::max(nq, 1) * sizeof(drs::MState)));
-  if (nh > 0) {
-    auto *hq = reinterpret_cast<drs::MQuery *>(stage(c, (size_t)nh * sizeof(drs::MQuery)));
-    auto *st = states ? reinterpret_cast<drs::MState *>(stage(c, (size_t)nh * sizeof(drs::MState))) : nullptr;
-    if (!hq || (states && !st)) return c->fail(DR_E_HIP, "pinned staging allocation failed");
-    std::copy(qs.begin(), qs.end(), hq);
-    SHCHK(c, hipMemcpyAsync(c->mq.p, hq, nh * sizeof(drs::MQuery), hipMemcpyHostToDevice, c->stream));
-    if (states) {
-      for (int i = 0; i < nh; i++) {
-        st[i] = drs::MState{};
-        st[i].low = qs[i].top;
-        st[i].cur = qs[i].top;
-        st[i].fresh = qs[i].type == drs::MQ_CANON ? 1 : 0;
-      }
-      SHCHK(c, hipMemcpyAsync(c->mst.p, st, nh * sizeof(drs::MState), hipMemcpyHostToDevice, c->stream));
-    }
-  }
-  if (!states) return DR_OK;
-  SHCHK(c, c->mpend.ensure((size_t)c->nlocal * nq * c->depth * c->SP * 8));
-  SHCHK(c, c->mrecv[0].ensure((size_t)c->G * nq * c->WSs * 8));
-  SHCHK(c, c->mrecv[1].ensure((size_t)c->G * nq * c->WSs * 8));
-  SHCHK(c, c->msend.ensure((size_t)nq * c->WSs * 8));
-  return DR_OK;
-}
-
 // The memo replay's outputs, carved from one device region that comes back in
-// one copy: header, commits, vcounts, every query's final state, the canonical
-// walk's final state (stepped form), chain pushes, per-pop count | digest | edges.
+// one copy: header, commits, vcounts, every query's state (the stepped form
+// steps them in place), the canonical walk's state (stepped form), chain pushes,
+// per-pop count | digest | edges.
 struct MOut {
   int32_t *hdr;
   uint8_t *commit;
@@ -1221,55 +1171,45 @@ MOut carve_out(char *base, int nw, int nq, int64_t pcap, int npop) {
   return m;
 }
 
-// vcount = |S_3| (the OR of the G partials), commit = vcount >= 2f+1; -1 / no
-// commit where the wave's leader is absent (process.go:327-329).  One wave per wave index.
-__global__ __launch_bounds__(256) void k_ms_vfinal(drs::MArgs a, drs::FArgs f, const u64 *__restrict__ P, int G) {
-  const int wi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (wi >= f.nw) return;
-  const int w = wi + 1, r1 = 4 * wi + 1, L = (w < a.nlead ? (int)a.lead[w] : 1) - 1;
-  const bool has = (a.pres[(size_t)r1 * a.W + (L >> 6)] >> (L & 63)) & 1ULL;
-  u64 v = 0;
-  if (lane < a.W)
-    for (int g = 0; g < G; g++) v |= P[((size_t)g * f.nw + wi) * a.W + lane];
-  const int cnt = (int)dr::wave_sum((u64)__popcll(v));
-  if (lane == 0) {
-    f.vcount[wi] = has ? cnt : -1;
-    f.commit[wi] = has && cnt >= f.quorum ? 1 : 0;
-  }
-}
-
-// k_ms_pass at the context's row stride
-// (k_ms_wu -- WU and the speculative digests, one workgroup per round, latency
-// bound -- runs beside it on the side stream: the pass keeps one 16-wave
-// workgroup per CU streaming rows, the small workgroups fill the other slots)
+// k_ms_pass at the context's row stride.  Vote modes: VOTE_FULL (fused), VOTE_STEP2 /
+// VOTE_STEP3 (stepped: Sout = this context's partial of the tested round's set, Sin =
+// Gin exchanged slots of [sin_nw][W] it is tested against)
+struct PassIO {
+  u64 *Sout = nullptr;
+  const u64 *Sin = nullptr;
+  int Gin = 0, sin_nw = 0;
+};
 template <int SP, int NT, int GR>
-hipError_t launch_pass_g(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
+hipError_t launch_pass_g(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, const PassIO &io) {
   const int T = c->nrounds - 1, nl = c->nlocal;
   const size_t lds = ((size_t)2 * nl * SP + c->W) * 8;
   if (nl == 1)
     hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR, true>), dim3((T + 3) / 4), dim3(NT), lds, c->stream, a, f, nw, mode,
-                       c->mU.as<u64>(), S1);
+                       c->mU.as<u64>(), io.Sout, io.Sin, io.Gin, io.sin_nw);
   else
     hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR, false>), dim3((T + 3) / 4), dim3(NT), lds, c->stream, a, f, nw,
-                       mode, c->mU.as<u64>(), S1);
+                       mode, c->mU.as<u64>(), io.Sout, io.Sin, io.Gin, io.sin_nw);
   return hipGetLastError();
 }
 template <int SP>
-hipError_t launch_pass_t(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
+hipError_t launch_pass_t(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, const PassIO &io) {
   // 512 threads, 8 chunks in flight: at C4, G = 8 (SP 2) 147 us vs 179 us at 1024 x 2,
   // G = 1 (SP 16) the same (profiles/r04/ pass geometries)
   if constexpr (SP == 2 || SP == 16) {  // the C4 shapes: the other geometries, for tuning
     switch (c->pass_geo) {
-      case 1: return launch_pass_g<SP, 1024, 4>(c, a, f, nw, mode, S1);
-      case 2: return launch_pass_g<SP, 512, 4>(c, a, f, nw, mode, S1);
-      case 3: return launch_pass_g<SP, 1024, 2>(c, a, f, nw, mode, S1);
+      case 1: return launch_pass_g<SP, 1024, 4>(c, a, f, nw, mode, io);
+      case 2: return launch_pass_g<SP, 512, 4>(c, a, f, nw, mode, io);
+      case 3: return launch_pass_g<SP, 1024, 2>(c, a, f, nw, mode, io);
     }
   }
-  return launch_pass_g<SP, 512, 8>(c, a, f, nw, mode, S1);
+  return launch_pass_g<SP, 512, 8>(c, a, f, nw, mode, io);
 }
-hipError_t launch_pass(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, u64 *S1) {
+// the pass, after k_ms_wu (with_wu: WU and the speculative digests; the third vote
+// step reads no summary)
+hipError_t launch_pass(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, const PassIO &io,
+                       bool with_wu = true) {
   const int T = c->nrounds - 1;
-  const bool wu = T >= 1;
+  const bool wu = with_wu && T >= 1;
   const bool side = wu && c->wu_side;
   if (wu) {
     const size_t lds = std::max<size_t>((size_t)4 * c->nlocal * a.dd * c->SP * 8, 8);
@@ -1285,12 +1225,12 @@ hipError_t launch_pass(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, in
   }
   hipError_t e = hipErrorInvalidValue;
   switch (c->SP) {
-    case 1: e = launch_pass_t<1>(c, a, f, nw, mode, S1); break;
-    case 2: e = launch_pass_t<2>(c, a, f, nw, mode, S1); break;
-    case 4: e = launch_pass_t<4>(c, a, f, nw, mode, S1); break;
-    case 8: e = launch_pass_t<8>(c, a, f, nw, mode, S1); break;
-    case 16: e = launch_pass_t<16>(c, a, f, nw, mode, S1); break;
-    case 32: e = launch_pass_t<32>(c, a, f, nw, mode, S1); break;
+    case 1: e = launch_pass_t<1>(c, a, f, nw, mode, io); break;
+    case 2: e = launch_pass_t<2>(c, a, f, nw, mode, io); break;
+    case 4: e = launch_pass_t<4>(c, a, f, nw, mode, io); break;
+    case 8: e = launch_pass_t<8>(c, a, f, nw, mode, io); break;
+    case 16: e = launch_pass_t<16>(c, a, f, nw, mode, io); break;
+    case 32: e = launch_pass_t<32>(c, a, f, nw, mode, io); break;
   }
   if (e == hipSuccess && side) e = hipStreamWaitEvent(c->stream, c->join, 0);
   return e;
@@ -1300,108 +1240,129 @@ int paper_emit(dr_shard *c, const drs::MArgs &a, const std::vector<drs::MQuery> 
                const std::vector<drs::MState> &fin, const std::vector<int> &pop_query, std::vector<uint64_t> &qout,
                int npop);
 
-// The stepped form's device phase (one round of every live query per launch, an
-// exchange between launches; what one rank of an RCCL group of G > 1 runs, and
-// local mode with DR_SHARD_OPT_STEPPED): the pass with this context's partial
-// S_1, vote steps 2 and 3 with their exchanges, K^cand and its exchange, the
-// canonical walk stepped, the canonical prefixes, then every pop and chain
-// stepped together.  Writes m.commit / m.vcount / m.fin / m.canon.
-int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int nq, drs::FArgs f, const MOut &m,
-                  int64_t pcap, int *steps_out) {
-  const int T = c->nrounds - 1, W = c->W, G = c->G, nl = c->nlocal;
-  drs::MArgs a1 = make_margs(c, 1, T);
-  a1.slot_off = c->slot_off.as<uint32_t>();
-  a1.slot_src = c->slot_src.as<uint16_t>();
-  // 1. the pass (U, WU per shard) + this context's partial S_1, then steps 2, 3
-  const size_t pw = (size_t)G * nw * W * 8;
-  SHCHK(c, c->vote_p[0].ensure(pw));
-  SHCHK(c, c->vote_p[1].ensure(pw));
-  SHCHK(c, c->vote_send.ensure((size_t)nw * W * 8));
-  u64 *P1 = c->vote_p[1].as<u64>(), *P0 = c->vote_p[0].as<u64>();
-  if (c->local) SHCHK(c, hipMemsetAsync(P1, 0, pw, c->stream));  // slots 1..G-1: the pass merges every local shard into slot 0
-  {
-    SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP1, c->local ? P1 : c->vote_send.as<u64>()));
-  }
-  if (!c->local) {
-    SHNCCL(c, ncclAllGather(c->vote_send.p, P1, (size_t)nw * W, ncclUint64, c->comm, c->stream));
-    c->last_xbytes += (uint64_t)nw * W * 8;
-  }
-  ShardArgs sa = make_args(c, 0, 1);
-  const int bpw = (c->n + SH_NT - 1) / SH_NT;
-  for (int k = 2; k <= 3; k++) {
-    u64 *pin = k == 2 ? P1 : P0, *pout = k == 2 ? P0 : P1;
-    hipLaunchKernelGGL(k_shard_vote, dim3(nw * bpw, nl), dim3(SH_NT), 0, c->stream, sa, 1, nw, k, G,
-                       (const u64 *)nullptr, pin, c->local ? pout : c->vote_send.as<u64>());
-    SHCHK(c, hipGetLastError());
-    if (!c->local) {
-      SHNCCL(c, ncclAllGather(c->vote_send.p, pout, (size_t)nw * W, ncclUint64, c->comm, c->stream));
-      c->last_xbytes += (uint64_t)nw * W * 8;
+// ---------------------------------------------------------------------------
+// The stepped form (shard_step.hpp).  Every launch goes out on the context's
+// stream (RCCL mode: each exchange on it too); the host waits once, for the
+// results.
+// ---------------------------------------------------------------------------
+// S_1 of every mirrored wave (k_ms_lcol), after an append or a coin change: the
+// rank holding the leader's column finds it, one exchange gives it to every rank
+int ensure_lcol(dr_shard *c) {
+  const int T = c->nrounds - 1, nwl = std::max(0, (T + 2) / 4);
+  if (c->lcol_ok) return DR_OK;
+  drs::MArgs a = make_margs(c, 1, T);
+  const size_t words = (size_t)std::max(nwl, 1) * c->W;
+  SHCHK(c, c->mlcol.ensure((size_t)(c->local ? 1 : c->G) * words * 8));
+  if (nwl > 0) {
+    if (c->local) {
+      hipLaunchKernelGGL(drs::k_ms_lcol, dim3((nwl + 3) / 4), dim3(256), 0, c->stream, a, nwl, c->mlcol.as<u64>());
+      SHCHK(c, hipGetLastError());
+    } else {
+      SHCHK(c, c->mlcolp.ensure(words * 8));
+      hipLaunchKernelGGL(drs::k_ms_lcol, dim3((nwl + 3) / 4), dim3(256), 0, c->stream, a, nwl, c->mlcolp.as<u64>());
+      SHCHK(c, hipGetLastError());
+      SHNCCL(c, ncclAllGather(c->mlcolp.p, c->mlcol.p, words, ncclUint64, c->comm, c->stream));
+      c->last_xbytes += words * 8;
     }
   }
-  hipLaunchKernelGGL(k_ms_vfinal, dim3((nw + 3) / 4), dim3(256), 0, c->stream, a1, f, (const u64 *)P1, G);
-  SHCHK(c, hipGetLastError());
-  SHCHK(c, c->mark(1));
-  // 2. K^cand (exchanged), good, the canonical walk, the canonical prefixes
-  const int rb = (T + 1 + 3) / 4;
+  c->lcol_nw = std::max(nwl, 1);
+  c->lcol_g = c->local ? 1 : c->G;
+  c->lcol_ok = true;
+  return DR_OK;
+}
+
+// Launch steps [j0, j1) of a batch of nq queries (states st, in place), each
+// followed by its exchange in RCCL mode.
+int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MState *st, int nq, int j0, int j1) {
+  const int WL = c->nlocal * c->WSs;
+  const size_t lds = ((size_t)c->depth * WL + c->W) * 8;
+  SHCHK(c, c->mpend.ensure((size_t)std::max(nq, 1) * c->depth * WL * 8));
+  SHCHK(c, c->mrecv[0].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
+  SHCHK(c, c->mrecv[1].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
+  SHCHK(c, c->msend.ensure((size_t)std::max(nq, 1) * c->WSs * 8));
+  drs::MArgs b = a;
+  b.pend = c->mpend.as<u64>();
+  for (int j = j0; j < j1; j++) {
+    u64 *rin = c->mrecv[j & 1].as<u64>();
+    u64 *rout = c->local ? c->mrecv[(j + 1) & 1].as<u64>() : c->msend.as<u64>();
+    hipLaunchKernelGGL((drs::k_ms_step2<drs::MS_NT>), dim3(nq), dim3(drs::MS_NT), lds, c->stream, b, f, j, st,
+                       (const u64 *)rin, rout);
+    SHCHK(c, hipGetLastError());
+    if (!c->local) {
+      SHNCCL(c, ncclAllGather(c->msend.p, c->mrecv[(j + 1) & 1].p, (size_t)nq * c->WSs, ncclUint64, c->comm,
+                              c->stream));
+      c->last_xbytes += (uint64_t)nq * c->WSs * 8;
+    }
+    c->last_rounds++;
+  }
+  return DR_OK;
+}
+
+// The stepped commit phase: S_1 (cached), the pass with the partial S_2, the S_2
+// exchange, the third vote step (with K^cand in RCCL mode: one exchange for both),
+// then k_ms_kfin: K, good, the RD / CE defaults, vcount / commit, the walk's query.
+int stepped_commit(dr_shard *c, int nw, const drs::FArgs &f, const MOut &m) {
+  const int T = c->nrounds - 1, W = c->W, G = c->G;
+  drs::MArgs a1 = make_margs(c, 1, T);
+  if (int rc = ensure_lcol(c)) return rc;
+  const size_t pw = (size_t)std::max(nw, 1) * W * 8;
+  SHCHK(c, c->vote_p[0].ensure((c->local ? 1 : G) * pw));  // S_2 partials, exchanged
+  SHCHK(c, c->vote_p[1].ensure(pw));                        // local: S_3; RCCL: this rank's S_2
+  u64 *S2 = c->vote_p[0].as<u64>();
+  PassIO p2;
+  p2.Sout = c->local ? S2 : c->vote_p[1].as<u64>();
+  p2.Sin = c->mlcol.as<u64>();
+  p2.Gin = c->lcol_g;
+  p2.sin_nw = c->lcol_nw;
+  SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP2, p2));
+  if (!c->local) {
+    SHNCCL(c, ncclAllGather(c->vote_p[1].p, S2, (size_t)nw * W, ncclUint64, c->comm, c->stream));
+    c->last_xbytes += (uint64_t)nw * W * 8;
+  }
+  PassIO p3;
+  p3.Sin = S2;
+  p3.Gin = c->local ? 1 : G;
+  p3.sin_nw = nw;
+  const int rb = (T + 1 + 3) / 4, nb = rb + (nw + 3) / 4;
   if (c->local) {
-    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, nl), dim3(drs::MS_NT), 0, c->stream, a1, T, (u64 *)nullptr);
+    p3.Sout = c->vote_p[1].as<u64>();
+    SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP3, p3, false));
+    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(nb), dim3(256), 0, c->stream, a1, f, (const u64 *)nullptr, (int64_t)0,
+                       (const u64 *)p3.Sout, 1, c->mcq.as<drs::MQuery>(), m.canon);
     SHCHK(c, hipGetLastError());
   } else {
-    SHCHK(c, c->mksend.ensure((size_t)(T + 1) * c->WSs * 8));
-    SHCHK(c, c->mkrecv.ensure((size_t)G * (T + 1) * c->WSs * 8));
-    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, nl), dim3(drs::MS_NT), 0, c->stream, a1, T, c->mksend.as<u64>());
+    // one send buffer: this rank's K^cand columns [(T+1) * WSs], then its partial S_3 [nw * W]
+    const int64_t ks = (int64_t)(T + 1) * c->WSs + (int64_t)nw * W;
+    SHCHK(c, c->mksend.ensure((size_t)ks * 8));
+    SHCHK(c, c->mkrecv.ensure((size_t)G * ks * 8));
+    hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, c->nlocal), dim3(drs::MS_NT), 0, c->stream, a1, T,
+                       c->mksend.as<u64>());
     SHCHK(c, hipGetLastError());
-    SHNCCL(c, ncclAllGather(c->mksend.p, c->mkrecv.p, (size_t)(T + 1) * c->WSs, ncclUint64, c->comm, c->stream));
-    c->last_xbytes += (uint64_t)(T + 1) * c->WSs * 8;
-    const size_t tot = (size_t)(T + 1) * W;
-    hipLaunchKernelGGL(drs::k_ms_kunpack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, a1, T,
-                       c->mkrecv.as<u64>());
+    p3.Sout = c->mksend.as<u64>() + (size_t)(T + 1) * c->WSs;
+    SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP3, p3, false));
+    SHNCCL(c, ncclAllGather(c->mksend.p, c->mkrecv.p, (size_t)ks, ncclUint64, c->comm, c->stream));
+    c->last_xbytes += (uint64_t)ks * 8;
+    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(nb), dim3(256), 0, c->stream, a1, f, (const u64 *)c->mkrecv.as<u64>(), ks,
+                       (const u64 *)nullptr, G, c->mcq.as<drs::MQuery>(), m.canon);
     SHCHK(c, hipGetLastError());
   }
-  hipLaunchKernelGGL(drs::k_ms_good, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a1, T, c->mgood.as<uint8_t>());
+  return DR_OK;
+}
+
+// What follows the canonical walk: its positions, the canonical digests, the G / E
+// prefixes and the plan of the batch (pops and chains with their initial states).
+int stepped_canon_tail(dr_shard *c, const drs::FArgs &f, const MOut &m, int nq, int64_t pcap) {
+  const int T = c->nrounds - 1, rb = (T + 1 + 3) / 4;
+  drs::MArgs a1 = make_margs(c, 1, T);
+  hipLaunchKernelGGL((drs::k_ms_cpos<1024>), dim3(1), dim3(1024), 0, c->stream, a1, f, (const drs::MState *)m.canon);
   SHCHK(c, hipGetLastError());
-  {
-    drs::MQuery q{};
-    q.type = drs::MQ_CANON;
-    q.top = T;
-    q.bottom = 0;
-    q.src0 = -1;
-    if (int rc = init_states(c, {q}, 1)) return rc;
-    drs::MArgs sa1 = make_margs(c, 1, T);
-    int steps = 0;
-    if (int rc = run_steps(c, sa1, 1, T + 2 * std::max(1, c->nrounds), &steps, c->hint_canon)) return rc;
-    c->hint_canon = steps;
-    SHCHK(c, hipMemcpyAsync(m.canon, (steps & 1) ? sa1.st1 : sa1.st0, sizeof(drs::MState), hipMemcpyDeviceToDevice,
-                            c->stream));
-  }
-  hipLaunchKernelGGL(drs::k_ms_cstats, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a1, T, f.RD, f.CE);
+  hipLaunchKernelGGL(drs::k_ms_rg_full, dim3(rb), dim3(256), 0, c->stream, a1, f);
   SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL((drs::k_ms_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, (const u64 *)f.RD, f.Cc,
-                     (const u64 *)f.CE, f.Ec);
-  SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(drs::k_ms_rg, dim3(rb), dim3(drs::MS_NT), 0, c->stream, a1, T, c->slot_off.as<uint32_t>(),
-                     c->slot_src.as<uint16_t>(), (const u64 *)f.Cc, f.RG);
-  SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL((drs::k_ms_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, (const u64 *)f.RG, f.Gc,
-                     (const u64 *)nullptr, (u64 *)nullptr);
-  SHCHK(c, hipGetLastError());
-  SHCHK(c, c->mark(2));
-  // 3. every pop and every chain (planned on the device from the commits), stepped together
-  if (int rc = init_states(c, pops, nq)) return rc;
   drs::MArgs a = make_margs(c, nq);
-  a.slot_off = c->slot_off.as<uint32_t>();
-  a.slot_src = c->slot_src.as<uint16_t>();
   a.push_out = m.push;
-  hipLaunchKernelGGL((drs::k_ms_plan<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
-                     c->mst.as<drs::MState>(), (int)pcap, 0);
+  hipLaunchKernelGGL((drs::k_ms_plan_steps<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
+                     m.fin, (int)pcap);
   SHCHK(c, hipGetLastError());
-  SHCHK(c, hipMemsetAsync(c->mpend.p, 0, (size_t)nl * nq * c->depth * c->SP * 8, c->stream));
-  int steps = 0;
-  if (int rc = run_steps(c, a, nq, T + 2, &steps, c->hint_batch)) return rc;
-  c->hint_batch = steps;
-  SHCHK(c, hipMemcpyAsync(m.fin, (steps & 1) ? a.st1 : a.st0, (size_t)nq * sizeof(drs::MState),
-                          hipMemcpyDeviceToDevice, c->stream));
-  *steps_out = steps;
   return DR_OK;
 }
 
@@ -1410,8 +1371,10 @@ int stepped_phase(dr_shard *c, int nw, const std::vector<drs::MQuery> &pops, int
 // exchanged and each query runs to its end in one launch -- the pass (U, WU,
 // speculative digests and the complete vote), K^cand, the canonical walk, the
 // canonical digests and prefixes, the chain plan, one sweep launch for every pop
-// and chain, the emission: eight launches and one copy back.  Stepped form:
-// stepped_phase.  REF emission k_ms_emit; PAPER paper_emit after the copy.
+// and chain, the emission: eight launches and one copy back.  Stepped form
+// (shard_step.hpp): the launches of each phase back to back, as many steps as the
+// last replay took, one copy back; more steps only if a query was still live.
+// REF emission k_ms_emit; PAPER paper_emit after the copy.
 int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_replay_out *o) {
   const auto th0 = std::chrono::steady_clock::now();
   static const bool th_on = getenv("DR_SHARD_HOST_TIMING") != nullptr;  // investigation only
@@ -1419,6 +1382,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   const bool paper = deliver_mode == DR_DELIVER_PAPER, persistent = chain_mode == DR_CHAIN_PERSISTENT;
   const bool fused = c->nlocal == c->G && !c->stepped;
   const int T = c->nrounds - 1, W = c->W, nw = nwaves;
+  c->syncs = 0;
   if (int rc = sync_weak(c)) return rc;  // uploads the weak edges and columns after an append
   c->pin_used = 0;
   // one cone query per wave whose leader is present (a superset of the leaders any chain can push)
@@ -1450,10 +1414,11 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   SHCHK(c, c->mgood.ensure((size_t)T + 16));
   for (SBuf *b : {&c->mRD, &c->mCE, &c->mRG, &c->mC, &c->mE, &c->mG, &c->mSG}) SHCHK(c, b->ensure((size_t)(T + 1) * 8));
   SHCHK(c, c->mmasks.ensure((size_t)std::max<int64_t>(moff, 1) * 8));
+  SHCHK(c, c->mq.ensure((size_t)std::max(nq, 1) * sizeof(drs::MQuery)));  // pops and chains: planned on the device
+  SHCHK(c, c->mcq.ensure(sizeof(drs::MQuery)));                           // the stepped canonical walk
   MOut m = carve_out(nullptr, nw, nq, pcap, npop);
   SHCHK(c, c->mout.ensure(m.bytes));
   m = carve_out(c->mout.as<char>(), nw, nq, pcap, npop);
-  if (!fused) SHCHK(c, hipMemsetAsync(m.hdr, 0, drs::FH_N * 4, c->stream));  // fused: the kernels write every slot
   drs::FArgs f{};
   f.ppref = c->ppref.as<u64>();
   f.SG = c->mSG.as<u64>();
@@ -1480,15 +1445,25 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   f.emit = fused && !paper && c->emit_fused ? 1 : 0;
   SHCHK(c, c->mark(0));
   th1 = std::chrono::steady_clock::now();
-  int steps = 0;
+  c->last_rounds = 0;
+  drs::MArgs a = make_margs(c, nq);
+  a.push_out = m.push;
+  drs::MArgs ac = make_margs(c, 1, T);  // the stepped canonical walk: one query
+  ac.q = c->mcq.as<drs::MQuery>();
+  auto emit = [&]() -> int {  // REF emission of every pop query (PAPER needs the pop order, below)
+    if (npop > 0 && !paper && !f.emit) {
+      hipLaunchKernelGGL(drs::k_ms_emit, dim3(npop), dim3(drs::MS_NT), 0, c->stream, a, (const int32_t *)nullptr,
+                         (const drs::MState *)m.fin, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
+                         (const u64 *)f.Cc, (const u64 *)f.Gc, (const u64 *)f.Ec, m.qout, m.qout + npop,
+                         m.qout + 2 * npop);
+      SHCHK(c, hipGetLastError());
+    }
+    return DR_OK;
+  };
+  int jc = 0, jb = 0;  // stepped form: canonical walk / batch steps launched
   if (fused) {
-    SHCHK(c, c->mq.ensure((size_t)std::max(nq, 1) * sizeof(drs::MQuery)));  // pops and chains: k_ms_plan
-    drs::MArgs a = make_margs(c, nq);
-    a.slot_off = c->slot_off.as<uint32_t>();
-    a.slot_src = c->slot_src.as<uint16_t>();
     a.good = f.good;
-    a.push_out = m.push;
-    SHCHK(c, launch_pass(c, a, f, nw, drs::VOTE_FULL, (u64 *)nullptr));
+    SHCHK(c, launch_pass(c, a, f, nw, drs::VOTE_FULL, PassIO{}));
     SHCHK(c, c->mark(1));
     // K^cand, the canonical walk, the canonical digests and prefixes, the plan (pops and chains).
     // (As one workgroup's tail of the parallel launch before it -- a done counter behind an
@@ -1510,27 +1485,57 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     hipLaunchKernelGGL((drs::k_ms_sweep_full<256>), dim3(nq), dim3(256), lds_ring, c->stream, a, f);
     SHCHK(c, hipGetLastError());
   } else {
-    if (int rc = stepped_phase(c, nw, qs, nq, f, m, pcap, &steps)) return rc;
+    if (int rc = stepped_commit(c, nw, f, m)) return rc;
+    SHCHK(c, c->mark(1));
+    jc = std::max(1, c->hint_canon);
+    if (int rc = launch_steps(c, ac, f, m.canon, 1, 0, jc)) return rc;
+    if (int rc = stepped_canon_tail(c, f, m, nq, pcap)) return rc;
+    SHCHK(c, c->mark(2));
+    jb = std::max(1, c->hint_batch);
+    if (int rc = launch_steps(c, a, f, m.fin, nq, 0, jb)) return rc;
   }
   SHCHK(c, c->mark(3));
-  drs::MArgs a = make_margs(c, nq);
-  a.slot_off = c->slot_off.as<uint32_t>();
-  a.slot_src = c->slot_src.as<uint16_t>();
-  if (npop > 0 && !paper && !f.emit) {  // REF emission of every pop query (PAPER needs the pop order, below)
-    hipLaunchKernelGGL(drs::k_ms_emit, dim3(npop), dim3(drs::MS_NT), 0, c->stream, a, (const int32_t *)nullptr,
-                       (const drs::MState *)m.fin, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
-                       (const u64 *)f.Cc, (const u64 *)f.Gc, (const u64 *)f.Ec, m.qout, m.qout + npop,
-                       m.qout + 2 * npop);
-    SHCHK(c, hipGetLastError());
-  }
+  if (int rc = emit()) return rc;
   SHCHK(c, c->mark(4));
   char *hb = stage(c, m.bytes);
   if (!hb) return c->fail(DR_E_HIP, "pinned staging allocation failed");
   SHCHK(c, hipMemcpyAsync(hb, c->mout.p, m.bytes, hipMemcpyDeviceToHost, c->stream));
   th2 = std::chrono::steady_clock::now();
-  SHCHK(c, hipStreamSynchronize(c->stream));
+  SHCHK(c, host_sync(c));
   th3 = std::chrono::steady_clock::now();
   const MOut h = carve_out(hb, nw, nq, pcap, npop);
+  if (!fused) {
+    // a query still live after the launched steps (the DAG changed since the step
+    // counts were taken): step on from where it is, then everything that reads it again
+    const int bound = T + 2 * std::max(1, c->nrounds) + 8;
+    for (;;) {
+      const bool cdone = h.canon->done != 0;
+      bool bdone = cdone;
+      for (int i = 0; bdone && i < nq; i++) bdone = h.fin[i].done != 0;
+      if (cdone && bdone) break;
+      if (!cdone) {
+        const int more = std::max(4, jc);
+        if (jc + more > bound) return c->fail(DR_E_HIP, "memo replay: the canonical walk is live after %d steps", jc);
+        if (int rc = launch_steps(c, ac, f, m.canon, 1, jc, jc + more)) return rc;
+        jc += more;
+        if (int rc = stepped_canon_tail(c, f, m, nq, pcap)) return rc;
+        jb = std::max(1, c->hint_batch);
+        if (int rc = launch_steps(c, a, f, m.fin, nq, 0, jb)) return rc;
+      } else {
+        const int more = std::max(4, jb);
+        if (jb + more > bound) return c->fail(DR_E_HIP, "memo replay: queries live after %d steps", jb);
+        if (int rc = launch_steps(c, a, f, m.fin, nq, jb, jb + more)) return rc;
+        jb += more;
+      }
+      if (int rc = emit()) return rc;
+      SHCHK(c, hipMemcpyAsync(hb, c->mout.p, m.bytes, hipMemcpyDeviceToHost, c->stream));
+      SHCHK(c, host_sync(c));
+    }
+    c->hint_canon = std::max(1, h.canon->steps);
+    int need = 1;
+    for (int i = 0; i < nq; i++) need = std::max(need, h.fin[i].steps);
+    c->hint_batch = need;
+  }
   if (c->phase_timing) {
     SHCHK(c, hipEventElapsedTime(&o->ms_commit, c->evs[0], c->evs[1]));
     SHCHK(c, hipEventElapsedTime(&o->ms_summary, c->evs[1], c->evs[2]));
@@ -1541,7 +1546,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   if (h.hdr[drs::FH_ERR]) return c->fail(DR_E_CAPACITY, "chain pushes exceed the bound %lld", (long long)pcap);
   std::memcpy(o->commit, h.commit, (size_t)nw);
   std::memcpy(o->vcount, h.vcount, (size_t)nw * 4);
-  o->canon_segments = fused ? h.hdr[drs::FH_NSEG] : h.canon->npush;
+  o->canon_segments = h.hdr[drs::FH_NSEG];
   uint64_t ce = 0;
   for (int w = 1; w <= nw; w++)
     if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
@@ -1589,20 +1594,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
         for (int x = 0; x < h.fin[t.q].npush; x++) o->push_wave[at++] = h.push[t.pbase + x];
       for (int64_t y = at - 1; y >= a0; y--) {  // pops: the stack's LIFO order
         const int q = popq[o->push_wave[y]];
-        if (q < 0) {
-          if (getenv("DR_DEBUG_PUSH")) {
-            for (const Task &tt : tasks) {
-              fprintf(stderr, "task wave %d q %d pbase %d", tt.wave, tt.q, tt.pbase);
-              if (tt.q >= 0) {
-                const drs::MState &S = h.fin[tt.q];
-                fprintf(stderr, " npush %d stop %d low %d edges %llu pushes:", S.npush, S.stop, S.low, (unsigned long long)S.edges);
-                for (int x = 0; x < S.npush; x++) fprintf(stderr, " %d", h.push[tt.pbase + x]);
-              }
-              fprintf(stderr, "\n");
-            }
-          }
-          return c->fail(DR_E_HIP, "memo replay: pushed wave %d has no cone query", o->push_wave[y]);
-        }
+        if (q < 0) return c->fail(DR_E_HIP, "memo replay: pushed wave %d has no cone query", o->push_wave[y]);
         pop_query.push_back(q);
       }
       ti++;
@@ -1611,6 +1603,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   o->push_off[nw] = (uint32_t)at;
   std::vector<uint64_t> qout;  // PAPER: paper_emit's counts; REF reads the copied region
   const uint64_t *qo = reinterpret_cast<const uint64_t *>(h.qout);
+  int steps = c->hint_batch;
   if (fused) {
     steps = 0;
     for (int i = 0; i < npop; i++) steps = std::max(steps, qs[i].top - h.fin[i].stop + 1);
@@ -1795,7 +1788,6 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
       c->wdeg.ensure((size_t)max_rounds * n * 2) != hipSuccess ||
       c->rdeg.ensure((size_t)max_rounds * 8) != hipSuccess || c->sdr.ensure((size_t)max_rounds * 8) != hipSuccess ||
       c->ppref.ensure((size_t)max_rounds * 8) != hipSuccess ||
-      hipHostMalloc((void **)&c->alive, 64, hipHostMallocDefault) != hipSuccess ||
       c->slot_off.ensure(((size_t)max_rounds + 1) * 4) != hipSuccess ||
       c->lead.ensure(c->h_lead.size() * 2) != hipSuccess ||
       hipMemcpy(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1827,9 +1819,8 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
   for (SBuf *b : {&c->wck, &c->wcr, &c->wcro, &c->sdr, &c->mU, &c->mWU, &c->mK, &c->mgood, &c->mRD, &c->mCE, &c->mRG,
                   &c->mC, &c->mE, &c->mG, &c->mksend, &c->mkrecv, &c->mq, &c->mst, &c->mpend, &c->mrecv[0],
                   &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout, &c->ppref, &c->mSG,
-                  &c->mout})
+                  &c->mout, &c->mcq, &c->mlcol, &c->mlcolp})
     b->release();
-  if (c->alive) (void)hipHostFree(c->alive);
   if (c->pin) (void)hipHostFree(c->pin);
   for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out,
                   &c->qinfo, &c->pres, &c->sdeg, &c->wdeg, &c->rdeg, &c->slot_off, &c->slot_src, &c->lead, &c->bar,
@@ -1894,6 +1885,7 @@ extern "C" int dr_shard_set_leader_coin(dr_shard *c, int mode, uint64_t seed, in
     return c->fail(DR_E_INVAL, "unknown leader coin mode %d", mode);
   }
   c->h_lead = std::move(L);
+  c->lcol_ok = false;  // the stepped vote's S_1 follows the leaders
   SHCHK(c, hipMemcpyAsync(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice, c->stream));
   SHCHK(c, hipStreamSynchronize(c->stream));
   return DR_OK;
@@ -2041,6 +2033,7 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
   c->h_pres.insert(c->h_pres.end(), pres.begin(), pres.end());
   c->h_deg.insert(c->h_deg.end(), deg.begin(), deg.end());
   c->weak_dirty = true;
+  c->lcol_ok = false;
   c->dmax = dmax;
   int depth = 2;
   while (depth < dmax + 2) depth <<= 1;  // k_shard_sweep clears a slot one round after reading it
@@ -2246,6 +2239,12 @@ extern "C" int dr_shard_stats(const dr_shard *c, float *ms, uint64_t *rounds, ui
   if (ms) *ms = c->last_ms;
   if (rounds) *rounds = c->last_rounds;
   if (exchange_bytes) *exchange_bytes = c->last_xbytes;
+  return DR_OK;
+}
+
+extern "C" int dr_shard_host_syncs(const dr_shard *c, uint64_t *syncs) {
+  if (!c || !syncs) return DR_E_INVAL;
+  *syncs = c->syncs;
   return DR_OK;
 }
 

@@ -50,7 +50,11 @@ __device__ u64 g_ms_timing[8 * kMsTimingQ];
 #define DR_MT(...)
 #endif
 
-enum : int { VOTE_FULL = 1, VOTE_STEP1 = 2 };
+// k_ms_pass vote modes: VOTE_FULL every step of the vote (the context holds every
+// column); VOTE_STEP2 this context's partial S_2 from the replicated S_1 (one rank
+// of G > 1, or the stepped form on one device); VOTE_STEP3 round 4w's rows only,
+// against S_2: the partial S_3
+enum : int { VOTE_FULL = 1, VOTE_STEP2 = 2, VOTE_STEP3 = 3 };
 
 // extra inputs/outputs of the fused replay (every pointer device memory)
 struct FArgs {
@@ -165,9 +169,13 @@ __global__ __launch_bounds__(NT) void k_ms_wu(MArgs a, FArgs f, u64 *__restrict_
 // ONE: the context holds one shard (G = 1 fused, or one rank of an RCCL group):
 // the element index is the pass, and the S chunk a thread tests is read once per
 // round.
+// Sin (VOTE_STEP2 / 3): the set the tested round is checked against, Gin slots of
+// [sin_nw][W] OR-ed (the exchanged partials); Sout: this context's partial of the
+// tested round's set, [nwc][W].
 template <int SP, int NT, int GR, bool ONE>
 __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int vote_mode, u64 *__restrict__ U,
-                                                u64 *__restrict__ S1out) {
+                                                u64 *__restrict__ Sout, const u64 *__restrict__ Sin, int Gin,
+                                                int sin_nw) {
   constexpr int CW = SP >= 2 ? 2 : 1, CPR = SP / CW, RPP = NT / CPR;
   static_assert(NT % 64 == 0 && NT % CPR == 0 && CPR <= 16, "block must tile rows");
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
@@ -180,16 +188,28 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
   const int L = do_commit ? (w < a.nlead ? (int)a.lead[w] : 1) - 1 : 0;
   const bool leader = do_commit && ((a.pres[(size_t)r1 * W + (L >> 6)] >> (L & 63)) & 1ULL);
   const int CPT = (n + RPP - 1) / RPP, E = NL * CPT;
+  const int ktest = vote_mode == VOTE_STEP2 ? 2 : 3;  // the stepped modes test one round
+  if (vote_mode == VOTE_STEP3 && !(leader && nr == 4)) {  // no vote: nothing to read
+    if (do_commit)
+      for (int i = tid; i < W; i += NT) Sout[(size_t)(w - 1) * W + i] = 0;
+    return;
+  }
   for (int i = tid; i < NL * SP; i += NT) {
     sU[i] = 0;
     const int l = i / SP, c = i % SP, gw = (a.shard0 + l) * WSs + c;
-    Sp[i] = (c < WSs && gw == (L >> 6)) ? 1ULL << (L & 63) : 0ULL;
+    u64 v = 0;
+    if (vote_mode == VOTE_FULL) {
+      v = (c < WSs && gw == (L >> 6)) ? 1ULL << (L & 63) : 0ULL;
+    } else if (leader && c < WSs && gw < W) {
+      for (int g = 0; g < Gin; g++) v |= Sin[((size_t)g * sin_nw + (w - 1)) * W + gw];
+    }
+    Sp[i] = v;
   }
   for (int i = tid; i < W; i += NT) Tn[i] = 0;
   __syncthreads();
-  for (int k = 0; k < nr; k++) {
+  for (int k = vote_mode == VOTE_STEP3 ? 3 : 0; k < nr; k++) {
     const int r = r1 + k;
-    const bool test = leader && k >= 1 && (vote_mode == VOTE_FULL || k == 1);
+    const bool test = leader && (vote_mode == VOTE_FULL ? k >= 1 : k == ktest);
     const u64 *rbase = a.strong + (size_t)r * a.strong_rstride + (size_t)row0 * SP + j * CW;
     u64 a0 = 0, a1 = 0;
     u64 t0 = 0, t1 = 0;  // ONE: this thread's chunk of S_{k-1}
@@ -265,24 +285,25 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
       pc = p;
     }
     __syncthreads();
-    for (int i = tid; i < NL * SP; i += NT) {
-      const int l = i / SP, c = i % SP;
-      U[((size_t)l * a.R + r) * SP + c] = sU[i];
-      sU[i] = 0;
-    }
+    if (vote_mode != VOTE_STEP3)
+      for (int i = tid; i < NL * SP; i += NT) {
+        const int l = i / SP, c = i % SP;
+        U[((size_t)l * a.R + r) * SP + c] = sU[i];
+        sU[i] = 0;
+      }
     if (test) {  // S_k: the sources of round r that reach S_{k-1} (this context's shards' columns of it)
       for (int i = tid; i < W; i += NT) {
         const u64 v = Tn[i];
         Tn[i] = 0;
         const int l = i / WSs - a.shard0, c = i % WSs;
         if (l >= 0 && l < NL) Sp[l * SP + c] = v;
-        if (vote_mode == VOTE_STEP1 && k == 1 && S1out) S1out[(size_t)(w - 1) * W + i] = v;
+        if (vote_mode != VOTE_FULL && Sout) Sout[(size_t)(w - 1) * W + i] = v;
       }
     }
     __syncthreads();
   }
-  if (do_commit && vote_mode == VOTE_STEP1 && !leader && S1out)
-    for (int i = tid; i < W; i += NT) S1out[(size_t)(w - 1) * W + i] = 0;
+  if (do_commit && vote_mode == VOTE_STEP2 && !(leader && nr >= 3) && Sout)
+    for (int i = tid; i < W; i += NT) Sout[(size_t)(w - 1) * W + i] = 0;
   if (do_commit && vote_mode == VOTE_FULL && tid == 0) {
     if (!leader) {  // leader is bottom (process.go:327-329)
       f.commit[w - 1] = 0;
@@ -514,6 +535,38 @@ __device__ __forceinline__ void full_weak_round(const MArgs &a, int r, int botto
   }
 }
 
+// canonical positions C: the presence prefix below the lowest walked round B, a
+// scan of RD over [B, T] above it; FH_RLO = the first round whose prefix differs
+// from the presence prefix (the speculative digests are exact below it), FH_NSEG.
+// Shared by the fused walk (canon_walk's tail) and the stepped one.
+template <int NT>
+__device__ __forceinline__ void canon_positions(const MArgs &a, const FArgs &f, int B, int segs) {
+  __shared__ int64_t s_scan[NT / 64];
+  __shared__ int s_bad;
+  const int tid = threadIdx.x, T = a.T;
+  for (int x = tid; x < B && x <= T; x += NT) f.Cc[x] = f.ppref[x];
+  const int span = T + 1 - B, per = span > 0 ? (span + NT - 1) / NT : 0;
+  const int ra = B + tid * per, rb = min(T + 1, ra + per);
+  int64_t loc = 0;
+  for (int x = ra; x < rb; x++) loc += (int64_t)f.RD[x];
+  int64_t tot;
+  u64 run = (B >= 1 ? f.ppref[B - 1] : 0ULL) + (u64)fblock_scan<NT>(loc, s_scan, tot, 0);
+  int bad = INT_MAX;
+  for (int x = ra; x < rb; x++) {
+    run += f.RD[x];
+    f.Cc[x] = run;
+    if (bad == INT_MAX && x >= 1 && run != f.ppref[x]) bad = x;
+  }
+  if (tid == 0) s_bad = INT_MAX;
+  __syncthreads();
+  if (bad != INT_MAX) atomicMin(&s_bad, bad);
+  __syncthreads();
+  if (tid == 0) {
+    f.hdr[FH_NSEG] = segs;
+    f.hdr[FH_RLO] = s_bad;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_ms_canon_full: one workgroup, the canonical segments top down (k_canon).
 // Dynamic LDS: ring[depth*W] | FE[W] | Ur[W].  As in k_ms_sweep_full, wave 0
@@ -527,7 +580,6 @@ __device__ __forceinline__ void canon_walk(const MArgs &a, const FArgs &f, u64 *
   __shared__ int s_ctl[4];
   __shared__ int64_t s_wc[2];
   __shared__ u64 s_e;
-  __shared__ int64_t s_scan[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int pos = T, segs = 0, lo_w = T + 1;
   while (true) {
@@ -643,28 +695,7 @@ __device__ __forceinline__ void canon_walk(const MArgs &a, const FArgs &f, u64 *
   }
   // canonical positions: below the lowest walked round every round is full (C
   // is the presence prefix); the scan covers the walked region only
-  const int B = lo_w;
-  for (int x = tid; x < B && x <= T; x += NT) f.Cc[x] = f.ppref[x];
-  const int span = T + 1 - B, per = span > 0 ? (span + NT - 1) / NT : 0;
-  const int ra = B + tid * per, rb = min(T + 1, ra + per);
-  int64_t loc = 0;
-  for (int x = ra; x < rb; x++) loc += (int64_t)f.RD[x];
-  int64_t tot;
-  u64 run = (B >= 1 ? f.ppref[B - 1] : 0ULL) + (u64)fblock_scan<NT>(loc, s_scan, tot, 0);
-  int bad = INT_MAX;
-  for (int x = ra; x < rb; x++) {
-    run += f.RD[x];
-    f.Cc[x] = run;
-    if (bad == INT_MAX && x >= 1 && run != f.ppref[x]) bad = x;
-  }
-  if (tid == 0) s_ctl[3] = INT_MAX;
-  __syncthreads();
-  if (bad != INT_MAX) atomicMin(&s_ctl[3], bad);
-  __syncthreads();
-  if (tid == 0) {
-    f.hdr[FH_NSEG] = segs;
-    f.hdr[FH_RLO] = s_ctl[3];
-  }
+  canon_positions<NT>(a, f, lo_w, segs);
 }
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_canon_full(MArgs a, FArgs f) {
@@ -738,6 +769,12 @@ __device__ __forceinline__ void plan_body(const MArgs &a, const FArgs &f, MQuery
         x.bottom = 0;
         x.src0 = L;
         x.mask_off = mo;
+        if (st0) {  // the stepped batch's initial state
+          MState s{};
+          s.low = x.top;
+          s.cur = x.top;
+          st0[pi] = s;
+        }
         q[pi++] = x;
         mo += (int64_t)(x.top + 1) * a.W;
       }

@@ -59,6 +59,7 @@ struct MState {
   int32_t done, run, low, stop;  // stop: the round where the query merged / ended
   int32_t merged, npush;         // MQ_CANON: npush counts the segments walked
   int32_t cur, fresh;            // MQ_CANON: its current round; 1 = start the next segment below cur
+  int32_t steps, pad;            // stepped form: launches the query was live in
   u64 edges;                     // MQ_CHAIN: strong degrees of the expanded vertices
 };
 

@@ -100,7 +100,9 @@ class ShardEngine:
     def stats(self) -> dict:
         ms, rounds, xb = L.f32(), L.u64(), L.u64()
         self._check(self._L.dr_shard_stats(self._h, C.byref(ms), C.byref(rounds), C.byref(xb)))
-        return dict(ms=ms.value, rounds=rounds.value, exchange_bytes=xb.value)
+        sy = L.u64()
+        self._check(self._L.dr_shard_host_syncs(self._h, C.byref(sy)))
+        return dict(ms=ms.value, rounds=rounds.value, exchange_bytes=xb.value, host_syncs=sy.value)
 
     def append_packed(self, d: PackedDag, r0: Optional[int] = None, r1: Optional[int] = None):
         r0 = self.num_rounds if r0 is None else r0

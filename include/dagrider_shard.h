@@ -125,6 +125,12 @@ int dr_shard_replay(dr_shard *ctx, int nwaves, int chain_mode, int deliver_mode,
  * included), rounds stepped, and bytes this rank sent through the exchange. */
 int dr_shard_stats(const dr_shard *ctx, float *ms, uint64_t *rounds, uint64_t *exchange_bytes);
 
+/* Host waits (stream synchronisations) of the last dr_shard_replay on the memoized
+ * path: 1 when every launch of the replay went out back to back and the host
+ * waited once, for the results (more after an append, whose weak columns upload
+ * first, or when a query was still live after the launched steps). */
+int dr_shard_host_syncs(const dr_shard *ctx, uint64_t *syncs);
+
 #ifdef __cplusplus
 }
 #endif

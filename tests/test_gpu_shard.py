@@ -240,6 +240,36 @@ def test_shard_commit_chain_order_calls(gpu_device):
                 assert (pc == pc2).all() and (pd == pd2).all() and tot == int(pc2.sum()), (cur, mode)
 
 
+def test_shard_stepped_steps_on_after_append(gpu_device):
+    """The stepped replay launches as many steps as the last replay took; after an append
+    (longer chains and cones) or a coin change it must step on until every query ends, and
+    still equal the oracle.  Then a repeated replay waits on the host once."""
+    from dag_rider_amd.gen import small_config
+
+    cfg = small_config(130, 120, 71, p_present=0.95, p_late=0.2, p_w=0.4, weak_depth=6, p_la=0.3)
+    d = generate(cfg)
+    f = cfg.faulty
+    rng = np.random.default_rng(5)
+    for G in (1, 3):
+        with ShardEngine(cfg.n, f, d.nrounds, gpu_device, nshards=G) as se:
+            se.set_stepped(True)
+            se.append_packed(d, 0, 41)
+            bs = oracle.PDag(d)  # waves 1..10 read rounds <= 40 only
+            for cm, dm in MODES:
+                _same_replay(se.replay(10, cm, dm), bs.replay(f, 10, cm, dm))
+            se.append_packed(d, 41, d.nrounds)
+            for cm, dm in MODES:
+                _same_replay(se.replay(cfg.nwaves, cm, dm), bs.replay(f, cfg.nwaves, cm, dm))
+            _same_replay(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF),
+                         bs.replay(f, cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF))
+            assert se.stats()["host_syncs"] == 1
+            leaders = [int(x) for x in rng.integers(1, cfg.n + 1, size=cfg.nwaves + 1)]
+            se.set_leader_coin(L.DR_LEADER_TABLE, table=leaders)
+            bl = oracle.PDag(d, leaders=leaders)
+            for cm, dm in MODES:
+                _same_replay(se.replay(cfg.nwaves, cm, dm), bl.replay(f, cfg.nwaves, cm, dm))
+
+
 def test_shard_replay_leader_coin(gpu_device):
     """A caller's leader table (chooseLeader as a coin) through the sharded commit, chains and pops."""
     rng = np.random.default_rng(91)
@@ -273,6 +303,9 @@ def test_shard_replay_c4_full(gpu_device):
             if G in (2, 8):  # the stepped form (what each rank of a G-rank group runs)
                 se.set_stepped(True)
                 _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
+                # again with the step counts the first replay took: every launch back to back, one host wait
+                _check_golden(se.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
+                assert se.stats()["host_syncs"] == 1
                 se.set_stepped(False)
             if G in (1, 8):  # the batched full sweeps (DR_SHARD_OPT_MEMO 0), REF
                 se.set_memo(False)

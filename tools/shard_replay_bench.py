@@ -54,7 +54,7 @@ def main():
                       and (r.commit_edges, r.chain_edges, r.deliver_edges)
                       == (rref.commit_edges, rref.chain_edges, rref.deliver_edges))
             print(json.dumps(dict(config=cfg.name, G=G, memo=True, form="stepped" if stepped else "fused", replay_ok=ok, ms_wall_median=statistics.median(walls),
-                                  ms_wall_min=min(walls), runs=walls, phases_ms=r.ms, device_ms=sum(r.ms.values()), steps=st["rounds"],
+                                  ms_wall_min=min(walls), runs=walls, phases_ms=r.ms, device_ms=sum(r.ms.values()), steps=st["rounds"], host_syncs=st["host_syncs"],
                                   canon_segments=r.sweep["canon_segments"], cones=r.sweep["count"],
                                   edges=r.total_edges)), flush=True)
 

@@ -1,6 +1,7 @@
 """Print the last replay step's kernel/copy timeline (with gaps) from rocprofv3 CSVs.
 
 usage: python tools/timeline.py <dir containing *_kernel_trace.csv [*_memory_copy_trace.csv]>
+       [--last] [--start KERNEL_SUBSTRING]   (default start marker: k_summary_commit)
 """
 import csv
 import glob
@@ -18,7 +19,8 @@ for f in glob.glob(os.path.join(d, "**", "*memory_copy_trace.csv"), recursive=Tr
 ev.sort()
 # bench.py's last replay is a profiling one (every phase bracketed by HIP events);
 # the last TIMED step starts at the second-to-last k_summary_commit (--last: the last)
-starts = [i for i, e in enumerate(ev) if "k_summary_commit" in e[2]]
+mark = sys.argv[sys.argv.index("--start") + 1] if "--start" in sys.argv else "k_summary_commit"
+starts = [i for i, e in enumerate(ev) if mark in e[2]]
 pick = -1 if "--last" in sys.argv or len(starts) < 2 else -2
 i0 = starts[pick] if starts else max(0, len(ev) - 60)
 i1 = starts[pick + 1] if pick == -2 else len(ev)
