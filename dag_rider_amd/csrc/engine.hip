@@ -3037,7 +3037,11 @@ std::vector<uint64_t> graph_key(const dr_ctx *c, int nw, int chain_mode, bool pa
           (uint64_t)c->use_memo, (uint64_t)c->kprev_ok, (uint64_t)c->pin_cap, P(c->pin),  P(c->K.p), P(c->Kprev.p),
           P(c->plan_arena.p), P(c->plan_out.p),   P(c->masks.p),       P(c->U.p),    P(c->WU.p),  P(c->SD.p),
           P(c->commit.p),      P(c->vcount.p),     P(c->strong.p),       P(c->RG.p),   P(c->slot_src.p),
-          P(c->ppref.p)};
+          P(c->ppref.p),       P(c->present.p),    P(c->wc_rows.p),      P(c->wc_key.p), P(c->wc_roff.p),
+          P(c->weak_roff.p),   P(c->far.p),        P(c->far_roff.p),     P(c->sdeg.p), P(c->wdeg.p),
+          P(c->lead.p),        P(c->slot_off.p),   P(c->dup_off.p),      P(c->dup_src.p), P(c->slot_rep.p),
+          P(c->Cc.p),          P(c->CE.p),         P(c->RD.p),           P(c->Gc.p),   P(c->Ec.p),
+          P(c->good.p),        P(c->nseg.p),       P(c->crbase.p),       P(c->rlo.p),  (uint64_t)c->ndups};
 }
 
 int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out *o) {
@@ -3274,10 +3278,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   if (form == LAUNCH) {
     HIPCHK(c, hipGraphLaunch(c->rg_exec, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_sync, c->stream));
-    hipError_t e;
-    while ((e = hipEventQuery(c->ev_sync)) == hipErrorNotReady) {
-    }
-    HIPCHK(c, e);
+    HIPCHK(c, hipEventSynchronize(c->ev_sync));  // (a blocking wait: no host core spinning while the graph runs)
     hb = c->pin;
     c->graph_state = 1;
   } else {

@@ -578,6 +578,8 @@ struct dr_shard {
   // pass's workgroups queue behind the side stream's (profiles/r04/)
   int wu_side = 0;
   int emit_fused = 0;  // REF emission inside the fused sweep (tuning: DR_SHARD_EMIT_FUSED=1)
+  int keep4 = 1;       // stepped pass: round 4w's rows with cached loads, re-read by the third vote step (off: DR_SHARD_KEEP4=0)
+  int step_nt = 256;   // k_ms_step2 threads per query (tuning: DR_SHARD_STEP_NT=128)
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
   hipStream_t stream = nullptr;
@@ -597,9 +599,11 @@ struct dr_shard {
       mpush, mqidx, mqout;
   // stepped form: the canonical walk's query; S_1 per wave (k_ms_lcol; RCCL mode: the
   // exchanged partials, lcol_g slots of lcol_nw waves), valid until an append or a coin change
-  SBuf mcq, mlcol, mlcolp;
+  SBuf mcq, mlcol, mlcolp, vote_s3;
   bool lcol_ok = false;
   int lcol_nw = 1, lcol_g = 1;
+  uint64_t lead_version = 0;  // bumped by every coin change
+  uint64_t pops_key[4] = {};  // what the device's pop query table was built for (upload_pops)
   uint64_t syncs = 0;  // host waits of the last query call (dr_shard_host_syncs)
   std::vector<uint64_t> h_sdr;  // strong degree sum per round (host copy)
   int hint_canon = 8, hint_batch = 12;  // steps the last replay's canonical walk / query batch took
@@ -1178,17 +1182,19 @@ struct PassIO {
   u64 *Sout = nullptr;
   const u64 *Sin = nullptr;
   int Gin = 0, sin_nw = 0;
+  hipStream_t st = nullptr;  // the context's stream if null
 };
 template <int SP, int NT, int GR>
 hipError_t launch_pass_g(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, int nw, int mode, const PassIO &io) {
   const int T = c->nrounds - 1, nl = c->nlocal;
   const size_t lds = ((size_t)2 * nl * SP + c->W) * 8;
+  hipStream_t st = io.st ? io.st : c->stream;
   if (nl == 1)
-    hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR, true>), dim3((T + 3) / 4), dim3(NT), lds, c->stream, a, f, nw, mode,
+    hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR, true>), dim3((T + 3) / 4), dim3(NT), lds, st, a, f, nw, mode,
                        c->mU.as<u64>(), io.Sout, io.Sin, io.Gin, io.sin_nw);
   else
-    hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR, false>), dim3((T + 3) / 4), dim3(NT), lds, c->stream, a, f, nw,
-                       mode, c->mU.as<u64>(), io.Sout, io.Sin, io.Gin, io.sin_nw);
+    hipLaunchKernelGGL((drs::k_ms_pass<SP, NT, GR, false>), dim3((T + 3) / 4), dim3(NT), lds, st, a, f, nw, mode,
+                       c->mU.as<u64>(), io.Sout, io.Sin, io.Gin, io.sin_nw);
   return hipGetLastError();
 }
 template <int SP>
@@ -1273,9 +1279,10 @@ int ensure_lcol(dr_shard *c) {
 
 // Launch steps [j0, j1) of a batch of nq queries (states st, in place), each
 // followed by its exchange in RCCL mode.
-int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MState *st, int nq, int j0, int j1) {
+int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MState *st, int nq, int j0, int j1,
+                 int batch) {
   const int WL = c->nlocal * c->WSs;
-  const size_t lds = ((size_t)c->depth * WL + c->W) * 8;
+  const size_t lds = std::max<size_t>(((size_t)c->depth * WL + c->W) * 8, 2 * 256 / 64 * 8);  // (the G prefix's scan)
   SHCHK(c, c->mpend.ensure((size_t)std::max(nq, 1) * c->depth * WL * 8));
   SHCHK(c, c->mrecv[0].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
   SHCHK(c, c->mrecv[1].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
@@ -1285,8 +1292,13 @@ int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MSt
   for (int j = j0; j < j1; j++) {
     u64 *rin = c->mrecv[j & 1].as<u64>();
     u64 *rout = c->local ? c->mrecv[(j + 1) & 1].as<u64>() : c->msend.as<u64>();
-    hipLaunchKernelGGL((drs::k_ms_step2<drs::MS_NT>), dim3(nq), dim3(drs::MS_NT), lds, c->stream, b, f, j, st,
-                       (const u64 *)rin, rout);
+    const int nb = nq + (batch && j == 0 ? 1 : 0);  // + the G prefix
+    if (c->step_nt == 128)
+      hipLaunchKernelGGL((drs::k_ms_step2<128>), dim3(nb), dim3(128), lds, c->stream, b, f, j, st, (const u64 *)rin,
+                         rout, batch);
+    else
+      hipLaunchKernelGGL((drs::k_ms_step2<256>), dim3(nb), dim3(256), lds, c->stream, b, f, j, st, (const u64 *)rin,
+                         rout, batch);
     SHCHK(c, hipGetLastError());
     if (!c->local) {
       SHNCCL(c, ncclAllGather(c->msend.p, c->mrecv[(j + 1) & 1].p, (size_t)nq * c->WSs, ncclUint64, c->comm,
@@ -1298,16 +1310,19 @@ int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MSt
   return DR_OK;
 }
 
-// The stepped commit phase: S_1 (cached), the pass with the partial S_2, the S_2
-// exchange, the third vote step (with K^cand in RCCL mode: one exchange for both),
-// then k_ms_kfin: K, good, the RD / CE defaults, vcount / commit, the walk's query.
+// The stepped commit phase: S_1 (cached), the pass with the partial S_2 and the S_2
+// exchange; the third vote step (partial S_3) forks to the second stream, beside the
+// canonical walk; K^cand (RCCL mode: its exchange), then k_ms_kfin: K, good, the
+// RD / CE defaults, the walk's query.  The S_3 partials are joined (and exchanged)
+// after the walk (stepped_join_votes), and k_ms_cpos counts the votes.
 int stepped_commit(dr_shard *c, int nw, const drs::FArgs &f, const MOut &m) {
   const int T = c->nrounds - 1, W = c->W, G = c->G;
   drs::MArgs a1 = make_margs(c, 1, T);
   if (int rc = ensure_lcol(c)) return rc;
   const size_t pw = (size_t)std::max(nw, 1) * W * 8;
   SHCHK(c, c->vote_p[0].ensure((c->local ? 1 : G) * pw));  // S_2 partials, exchanged
-  SHCHK(c, c->vote_p[1].ensure(pw));                        // local: S_3; RCCL: this rank's S_2
+  SHCHK(c, c->vote_p[1].ensure(pw));                        // this rank's S_2 (RCCL send), then its S_3
+  SHCHK(c, c->vote_s3.ensure((c->local ? 1 : G) * pw));    // RCCL: the exchanged S_3 partials
   u64 *S2 = c->vote_p[0].as<u64>();
   PassIO p2;
   p2.Sout = c->local ? S2 : c->vote_p[1].as<u64>();
@@ -1319,50 +1334,77 @@ int stepped_commit(dr_shard *c, int nw, const drs::FArgs &f, const MOut &m) {
     SHNCCL(c, ncclAllGather(c->vote_p[1].p, S2, (size_t)nw * W, ncclUint64, c->comm, c->stream));
     c->last_xbytes += (uint64_t)nw * W * 8;
   }
+  // the third vote step on the second stream
+  SHCHK(c, hipEventRecord(c->fork, c->stream));
+  SHCHK(c, hipStreamWaitEvent(c->side, c->fork, 0));
   PassIO p3;
   p3.Sin = S2;
   p3.Gin = c->local ? 1 : G;
   p3.sin_nw = nw;
-  const int rb = (T + 1 + 3) / 4, nb = rb + (nw + 3) / 4;
+  p3.Sout = c->vote_p[1].as<u64>();
+  p3.st = c->side;
+  SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP3, p3, false));
+  SHCHK(c, hipEventRecord(c->join, c->side));
+  const int rb = (T + 1 + 3) / 4;
   if (c->local) {
-    p3.Sout = c->vote_p[1].as<u64>();
-    SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP3, p3, false));
-    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(nb), dim3(256), 0, c->stream, a1, f, (const u64 *)nullptr, (int64_t)0,
-                       (const u64 *)p3.Sout, 1, c->mcq.as<drs::MQuery>(), m.canon);
+    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(rb), dim3(256), 0, c->stream, a1, f, (const u64 *)nullptr, (int64_t)0,
+                       c->mcq.as<drs::MQuery>(), m.canon);
     SHCHK(c, hipGetLastError());
   } else {
-    // one send buffer: this rank's K^cand columns [(T+1) * WSs], then its partial S_3 [nw * W]
-    const int64_t ks = (int64_t)(T + 1) * c->WSs + (int64_t)nw * W;
+    const int64_t ks = (int64_t)(T + 1) * c->WSs;
     SHCHK(c, c->mksend.ensure((size_t)ks * 8));
     SHCHK(c, c->mkrecv.ensure((size_t)G * ks * 8));
     hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, c->nlocal), dim3(drs::MS_NT), 0, c->stream, a1, T,
                        c->mksend.as<u64>());
     SHCHK(c, hipGetLastError());
-    p3.Sout = c->mksend.as<u64>() + (size_t)(T + 1) * c->WSs;
-    SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP3, p3, false));
     SHNCCL(c, ncclAllGather(c->mksend.p, c->mkrecv.p, (size_t)ks, ncclUint64, c->comm, c->stream));
     c->last_xbytes += (uint64_t)ks * 8;
-    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(nb), dim3(256), 0, c->stream, a1, f, (const u64 *)c->mkrecv.as<u64>(), ks,
-                       (const u64 *)nullptr, G, c->mcq.as<drs::MQuery>(), m.canon);
+    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(rb), dim3(256), 0, c->stream, a1, f, (const u64 *)c->mkrecv.as<u64>(), ks,
+                       c->mcq.as<drs::MQuery>(), m.canon);
     SHCHK(c, hipGetLastError());
   }
   return DR_OK;
 }
 
-// What follows the canonical walk: its positions, the canonical digests, the G / E
-// prefixes and the plan of the batch (pops and chains with their initial states).
-int stepped_canon_tail(dr_shard *c, const drs::FArgs &f, const MOut &m, int nq, int64_t pcap) {
+// the S_3 partials into the main stream (RCCL mode: exchanged); returns the OR's input
+int stepped_join_votes(dr_shard *c, int nw, const u64 **P3, int *Gp) {
+  SHCHK(c, hipStreamWaitEvent(c->stream, c->join, 0));
+  if (c->local) {
+    *P3 = c->vote_p[1].as<u64>();
+    *Gp = 1;
+    return DR_OK;
+  }
+  SHNCCL(c, ncclAllGather(c->vote_p[1].p, c->vote_s3.p, (size_t)nw * c->W, ncclUint64, c->comm, c->stream));
+  c->last_xbytes += (uint64_t)nw * c->W * 8;
+  *P3 = c->vote_s3.as<u64>();
+  *Gp = c->G;
+  return DR_OK;
+}
+
+// What follows the canonical walk: its positions, the E prefix and the chain plan
+// (k_ms_cpos), the canonical digests (the G prefix: the first batch step).
+int stepped_canon_tail(dr_shard *c, const drs::FArgs &f, const MOut &m, int nq, int64_t pcap, const u64 *P3, int Gp) {
   const int T = c->nrounds - 1, rb = (T + 1 + 3) / 4;
-  drs::MArgs a1 = make_margs(c, 1, T);
-  hipLaunchKernelGGL((drs::k_ms_cpos<1024>), dim3(1), dim3(1024), 0, c->stream, a1, f, (const drs::MState *)m.canon);
-  SHCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(drs::k_ms_rg_full, dim3(rb), dim3(256), 0, c->stream, a1, f);
-  SHCHK(c, hipGetLastError());
-  drs::MArgs a = make_margs(c, nq);
+  drs::MArgs a = make_margs(c, nq, T);
   a.push_out = m.push;
-  hipLaunchKernelGGL((drs::k_ms_plan_steps<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, c->mq.as<drs::MQuery>(),
-                     m.fin, (int)pcap);
+  hipLaunchKernelGGL((drs::k_ms_cpos<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, (const drs::MState *)m.canon,
+                     c->mq.as<drs::MQuery>(), (int)pcap, P3, Gp);
   SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(drs::k_ms_rg_full, dim3(rb), dim3(256), 0, c->stream, a, f);
+  SHCHK(c, hipGetLastError());
+  return DR_OK;
+}
+
+// The pop queries of a stepped replay (one per wave whose leader is present, mask rows
+// laid out in wave order): uploaded when the DAG, the leaders or the wave count changed.
+int upload_pops(dr_shard *c, const std::vector<drs::MQuery> &qs, int nw) {
+  const uint64_t key[4] = {(uint64_t)c->nrounds, c->lead_version, (uint64_t)nw, (uint64_t)(uintptr_t)c->mq.p};
+  if (std::equal(key, key + 4, c->pops_key) || qs.empty()) return DR_OK;
+  auto *hq = reinterpret_cast<drs::MQuery *>(stage(c, qs.size() * sizeof(drs::MQuery)));
+  if (!hq) return c->fail(DR_E_HIP, "pinned staging allocation failed");
+  std::copy(qs.begin(), qs.end(), hq);
+  SHCHK(c, hipMemcpyAsync(c->mq.p, hq, qs.size() * sizeof(drs::MQuery), hipMemcpyHostToDevice, c->stream));
+  std::copy(key, key + 4, c->pops_key);
   return DR_OK;
 }
 
@@ -1443,6 +1485,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   // the fused sweep emitting each pop itself (DR_SHARD_EMIT_FUSED=1, tuning): 101 us against
   // 68 + 22 us as two launches at C4 G = 1 (profiles/r04/)
   f.emit = fused && !paper && c->emit_fused ? 1 : 0;
+  f.keep4 = c->keep4;
   SHCHK(c, c->mark(0));
   th1 = std::chrono::steady_clock::now();
   c->last_rounds = 0;
@@ -1461,6 +1504,8 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     return DR_OK;
   };
   int jc = 0, jb = 0;  // stepped form: canonical walk / batch steps launched
+  const u64 *P3 = nullptr;  // stepped form: the S_3 partials (Gp slots)
+  int Gp = 1;
   if (fused) {
     a.good = f.good;
     SHCHK(c, launch_pass(c, a, f, nw, drs::VOTE_FULL, PassIO{}));
@@ -1487,12 +1532,14 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   } else {
     if (int rc = stepped_commit(c, nw, f, m)) return rc;
     SHCHK(c, c->mark(1));
+    if (int rc = upload_pops(c, qs, nw)) return rc;
     jc = std::max(1, c->hint_canon);
-    if (int rc = launch_steps(c, ac, f, m.canon, 1, 0, jc)) return rc;
-    if (int rc = stepped_canon_tail(c, f, m, nq, pcap)) return rc;
+    if (int rc = launch_steps(c, ac, f, m.canon, 1, 0, jc, 0)) return rc;
+    if (int rc = stepped_join_votes(c, nw, &P3, &Gp)) return rc;
+    if (int rc = stepped_canon_tail(c, f, m, nq, pcap, P3, Gp)) return rc;
     SHCHK(c, c->mark(2));
     jb = std::max(1, c->hint_batch);
-    if (int rc = launch_steps(c, a, f, m.fin, nq, 0, jb)) return rc;
+    if (int rc = launch_steps(c, a, f, m.fin, nq, 0, jb, 1)) return rc;
   }
   SHCHK(c, c->mark(3));
   if (int rc = emit()) return rc;
@@ -1516,15 +1563,15 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
       if (!cdone) {
         const int more = std::max(4, jc);
         if (jc + more > bound) return c->fail(DR_E_HIP, "memo replay: the canonical walk is live after %d steps", jc);
-        if (int rc = launch_steps(c, ac, f, m.canon, 1, jc, jc + more)) return rc;
+        if (int rc = launch_steps(c, ac, f, m.canon, 1, jc, jc + more, 0)) return rc;
         jc += more;
-        if (int rc = stepped_canon_tail(c, f, m, nq, pcap)) return rc;
+        if (int rc = stepped_canon_tail(c, f, m, nq, pcap, P3, Gp)) return rc;
         jb = std::max(1, c->hint_batch);
-        if (int rc = launch_steps(c, a, f, m.fin, nq, 0, jb)) return rc;
+        if (int rc = launch_steps(c, a, f, m.fin, nq, 0, jb, 1)) return rc;
       } else {
         const int more = std::max(4, jb);
         if (jb + more > bound) return c->fail(DR_E_HIP, "memo replay: queries live after %d steps", jb);
-        if (int rc = launch_steps(c, a, f, m.fin, nq, jb, jb + more)) return rc;
+        if (int rc = launch_steps(c, a, f, m.fin, nq, jb, jb + more, 1)) return rc;
         jb += more;
       }
       if (int rc = emit()) return rc;
@@ -1753,6 +1800,8 @@ extern "C" int dr_shard_create(int n, int faulty, int max_rounds, int device, in
   if (const char *g = getenv("DR_SHARD_PASS_GEO")) c->pass_geo = atoi(g) & 3;  // tuning only
   if (const char *g = getenv("DR_SHARD_WU_SIDE")) c->wu_side = atoi(g) != 0;
   if (const char *g = getenv("DR_SHARD_EMIT_FUSED")) c->emit_fused = atoi(g) != 0;
+  if (const char *g = getenv("DR_SHARD_KEEP4")) c->keep4 = atoi(g) != 0;
+  if (const char *g = getenv("DR_SHARD_STEP_NT")) c->step_nt = atoi(g) == 128 ? 128 : 256;
   c->shard0 = c->local ? 0 : rank;
   c->nlocal = c->local ? nshards : 1;
   c->max_rounds = max_rounds;
@@ -1819,7 +1868,7 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
   for (SBuf *b : {&c->wck, &c->wcr, &c->wcro, &c->sdr, &c->mU, &c->mWU, &c->mK, &c->mgood, &c->mRD, &c->mCE, &c->mRG,
                   &c->mC, &c->mE, &c->mG, &c->mksend, &c->mkrecv, &c->mq, &c->mst, &c->mpend, &c->mrecv[0],
                   &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout, &c->ppref, &c->mSG,
-                  &c->mout, &c->mcq, &c->mlcol, &c->mlcolp})
+                  &c->mout, &c->mcq, &c->mlcol, &c->mlcolp, &c->vote_s3})
     b->release();
   if (c->pin) (void)hipHostFree(c->pin);
   for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out,
@@ -1886,6 +1935,7 @@ extern "C" int dr_shard_set_leader_coin(dr_shard *c, int mode, uint64_t seed, in
   }
   c->h_lead = std::move(L);
   c->lcol_ok = false;  // the stepped vote's S_1 follows the leaders
+  c->lead_version++;
   SHCHK(c, hipMemcpyAsync(c->lead.p, c->h_lead.data(), c->h_lead.size() * 2, hipMemcpyHostToDevice, c->stream));
   SHCHK(c, hipStreamSynchronize(c->stream));
   return DR_OK;

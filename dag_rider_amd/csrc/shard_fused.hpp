@@ -69,6 +69,7 @@ struct FArgs {
   MState *fin;         // [nq] final state of every query
   u64 *qcount, *qdigest, *qedges;  // [npop] REF emission of each pop (k_ms_sweep_full with emit)
   int32_t quorum, nw, npop, persistent, emit;
+  int32_t keep4;  // VOTE_STEP2: round 4w's rows with cached loads (read again by VOTE_STEP3; tuning)
 };
 enum : int { FH_NCHAIN = 0, FH_NSEG = 1, FH_RLO = 2, FH_PUSHES = 3, FH_ERR = 4, FH_N = 8 };
 
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
   for (int k = vote_mode == VOTE_STEP3 ? 3 : 0; k < nr; k++) {
     const int r = r1 + k;
     const bool test = leader && (vote_mode == VOTE_FULL ? k >= 1 : k == ktest);
+    const bool keep = f.keep4 && vote_mode == VOTE_STEP2 && k == 3;
     const u64 *rbase = a.strong + (size_t)r * a.strong_rstride + (size_t)row0 * SP + j * CW;
     u64 a0 = 0, a1 = 0;
     u64 t0 = 0, t1 = 0;  // ONE: this thread's chunk of S_{k-1}
@@ -230,11 +232,12 @@ __global__ __launch_bounds__(NT) void k_ms_pass(MArgs a, FArgs f, int nwc, int v
           if (e0 + q < E && s < n) {
             const u64 *src = rbase + (size_t)l * a.strong_stride + (size_t)p * RPP * SP;
             if constexpr (CW == 2) {
-              const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(src));
+              const u64x2 v = keep ? *reinterpret_cast<const u64x2 *>(src)
+                                   : __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(src));
               x0[q] = v.x;
               x1[q] = v.y;
             } else {
-              x0[q] = __builtin_nontemporal_load(src);
+              x0[q] = keep ? *src : __builtin_nontemporal_load(src);
             }
           }
           if (++p == CPT) {
@@ -851,9 +854,8 @@ __global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__rest
 // launches wrote)
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_prefix_plan(MArgs a, FArgs f, MQuery *__restrict__ q, int push_cap) {
-  __shared__ u64 part[NT / 64];
-  ms_prefix_one<NT>(a.T + 1, f.RG, f.Gc, part);
-  ms_prefix_one<NT>(a.T + 1, f.CE, f.Ec, part);
+  __shared__ u64 part[2 * NT / 64];
+  ms_prefix_two<NT>(a.T + 1, f.RG, f.Gc, f.CE, f.Ec, part);
   plan_body<NT>(a, f, q, (MState *)nullptr, push_cap, 1);
 }
 

@@ -203,22 +203,32 @@ __device__ __forceinline__ void canon_ring_init(const MArgs &a, u64 *pend, int l
   }
 }
 
-// The highest bad round below `below` (-1: none), wave 0 (every lane gets it):
-// 8 rounds per lane per pass, as k_canon's search.
+// The highest bad round below `below` (-1: none), one wave (every lane gets it).
+// The 0/1 flags are read 8 at a time (u64 words, a byte != 1 is a bad round), 16
+// words per lane in flight: one pass covers 8192 rounds.
 __device__ __forceinline__ int next_bad(const MArgs &a, int below) {
-  constexpr int PL = 16;  // rounds per lane per block: every flag load of a block in flight at once
+  constexpr int PL = 16;
+  constexpr uint64_t ONES = 0x0101010101010101ULL;
   const int lane = threadIdx.x & 63;
-  for (int top = below - 1; top >= 0; top -= 64 * PL) {
-    uint8_t g[PL];
+  if (below <= 0) return -1;
+  const uint64_t *g = reinterpret_cast<const uint64_t *>(a.good);
+  const int wtop = (below - 1) >> 3, nb = below - 8 * wtop;  // rounds of word wtop below `below`: its low nb bytes
+  const uint64_t topmask = nb >= 8 ? ~0ULL : (1ULL << (8 * nb)) - 1ULL;
+  for (int top = wtop; top >= 0; top -= 64 * PL) {
+    uint64_t v[PL];
 #pragma unroll
     for (int k = 0; k < PL; k++) {
       const int x = top - PL * lane - k;
-      g[k] = x >= 0 ? a.good[x] : (uint8_t)1;
+      v[k] = x >= 0 ? g[x] : ONES;
     }
     int best = -1;
 #pragma unroll
-    for (int k = PL - 1; k >= 0; k--)
-      if (!g[k]) best = top - PL * lane - k;
+    for (int k = PL - 1; k >= 0; k--) {
+      const int x = top - PL * lane - k;
+      uint64_t bad = v[k] ^ ONES;
+      if (x == wtop) bad &= topmask;
+      if (bad) best = 8 * x + (63 - __clzll(bad)) / 8;
+    }
     for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off));
     if (best >= 0) return best;
   }
@@ -523,6 +533,67 @@ __device__ __forceinline__ void ms_prefix_one(int n, const u64 *__restrict__ a, 
     for (int c = 0; c < CH; c++)
       if (base + c * 64 < n) b[base + c * 64] = off + v[c];
     tile_carry += tot;
+  }
+}
+// inclusive prefixes of two arrays (a1 may be null) over 0..n-1 in one pass of one
+// workgroup of NT threads: tiles of NT * CH elements, thread t owns CH consecutive
+// elements (serial sums), one wave scan of the threads' totals for both arrays, one
+// LDS hop for the waves' totals.  part: 2 * NT / 64 words of LDS.
+template <int NT, int CH = 4>
+__device__ __forceinline__ void ms_prefix_two(int n, const u64 *__restrict__ a0, u64 *__restrict__ b0,
+                                              const u64 *__restrict__ a1, u64 *__restrict__ b1, u64 *part) {
+  constexpr int NW = NT / 64, TILE = NT * CH;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u64 cx = 0, cy = 0;  // carries from the tiles before
+  for (int t0 = 0; t0 < n; t0 += TILE) {
+    const int base = t0 + (int)threadIdx.x * CH;
+    u64 x[CH], y[CH];
+#pragma unroll
+    for (int c = 0; c < CH; c++) {
+      x[c] = base + c < n ? a0[base + c] : 0ULL;
+      y[c] = (a1 && base + c < n) ? a1[base + c] : 0ULL;
+    }
+#pragma unroll
+    for (int c = 1; c < CH; c++) {
+      x[c] += x[c - 1];
+      y[c] += y[c - 1];
+    }
+    const u64 sx = x[CH - 1], sy = y[CH - 1];
+    u64 ix = sx, iy = sy;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const u64 tx = dr::shfl_up64(ix, off), ty = dr::shfl_up64(iy, off);
+      if (lane >= off) {
+        ix += tx;
+        iy += ty;
+      }
+    }
+    if (lane == 63) {
+      part[wv] = ix;
+      part[NW + wv] = iy;
+    }
+    __syncthreads();
+    u64 ox = cx, oy = cy, tx = 0, ty = 0;
+    for (int w = 0; w < NW; w++) {
+      const u64 px = part[w], py = part[NW + w];
+      if (w < wv) {
+        ox += px;
+        oy += py;
+      }
+      tx += px;
+      ty += py;
+    }
+    __syncthreads();
+    ox += ix - sx;
+    oy += iy - sy;
+#pragma unroll
+    for (int c = 0; c < CH; c++)
+      if (base + c < n) {
+        b0[base + c] = ox + x[c];
+        if (b1) b1[base + c] = oy + y[c];
+      }
+    cx += tx;
+    cy += ty;
   }
 }
 template <int NT>

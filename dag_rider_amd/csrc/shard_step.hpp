@@ -15,17 +15,20 @@
 //   k_ms_wu, k_ms_pass (VOTE_STEP2)   one read of the rank's columns of every
 //                   strong row: U per round and, from the replicated S_1, this
 //                   rank's partial S_2 (process.go:326-339) -> exchange.
-//   k_ms_pass (VOTE_STEP3)   round 4w's rows against S_2 only: partial S_3,
-//                   exchanged together with K^cand (k_ms_kcand) in RCCL mode.
-//   k_ms_kfin       K (= K^cand), good_r, the full-round defaults of RD / CE, the
-//                   vote count and commit of every wave, the canonical walk's
-//                   query and state.
+//   k_ms_pass (VOTE_STEP3)   round 4w's rows against S_2 only: partial S_3, on
+//                   the second stream, beside the canonical walk (one workgroup
+//                   per launch: the GPU is nearly idle under it); its exchange
+//                   after the walk.
+//   k_ms_kfin       K (= K^cand; RCCL mode: after the K^cand exchange), good_r,
+//                   the full-round defaults of RD / CE, the walk's query and state.
 //   k_ms_step2 x s  the canonical walk (one query), one round per launch.
-//   k_ms_cpos       the canonical positions C over the walked rounds.
-//   k_ms_rg_full, k_ms_plan_steps   canonical digests, the G / E prefixes, and
-//                   every pop and leader chain planned on the device from the
-//                   commit flags, with their initial states.
-//   k_ms_step2 x s  every pop and chain, one round per launch.
+//   k_ms_cpos       vcount / commit of every wave, the canonical positions C over
+//                   the walked rounds, the E prefix, and the leader chains planned
+//                   on the device from the commit flags (the pop queries are a
+//                   cached table).
+//   k_ms_rg_full    the canonical digests.
+//   k_ms_step2 x s  every pop and chain, one round per launch (the first one also
+//                   computes the G prefix in one more workgroup).
 //   k_ms_emit       REF emission; one copy back, one host sync.
 //
 // k_ms_step2 is one workgroup per query (every local shard's columns in the same
@@ -63,90 +66,78 @@ __global__ __launch_bounds__(256) void k_ms_lcol(MArgs a, int nwl, u64 *__restri
 
 // Local-mode K^cand over every local shard (kcand_round), good_r, the RD / CE
 // defaults; RCCL mode: the same from the all-gathered K^cand columns (krecv:
-// [G][stride] with this layout: [(T+1) * WSs] K^cand words, then [nw * W] partial
-// S_3).  Extra workgroups: vcount / commit of every wave from the S_3 partials
-// (P3: [Gp][nw][W] in local mode, inside krecv in RCCL mode); block 0 also
-// writes the canonical walk's query and initial state.
+// [G][kstride], [(T+1) * WSs] K^cand words per rank).  Block 0 also writes the
+// canonical walk's query and initial state.
 __global__ __launch_bounds__(256) void k_ms_kfin(MArgs a, FArgs f, const u64 *__restrict__ krecv, int64_t kstride,
-                                                 const u64 *__restrict__ P3, int Gp, MQuery *__restrict__ cq,
-                                                 MState *__restrict__ cst) {
-  const int rb = (a.T + 1 + 3) / 4, lane = threadIdx.x & 63;
-  if ((int)blockIdx.x < rb) {
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      MQuery q{};
-      q.type = MQ_CANON;
-      q.top = a.T;
-      q.bottom = 0;
-      q.src0 = -1;
-      *cq = q;
-      MState s{};
-      s.cur = a.T;
-      s.fresh = 1;
-      s.stop = a.T + 1;  // lowest round a segment stopped at (T + 1: none)
-      *cst = s;
-    }
-    if (!krecv) {
-      kcand_round(a, f, r);
-      return;
-    }
-    if (r > a.T) return;
-    bool bad = false;
-    int cnt = 0;
-    if (lane < a.W) {
-      const u64 p = a.pres[(size_t)r * a.W + lane];
-      const int g = lane / a.WSs, cw = lane - g * a.WSs;
-      const u64 v = krecv[(size_t)g * kstride + (size_t)r * a.WSs + cw];
-      a.K[(size_t)r * a.W + lane] = v;
-      bad = (v & p) != p;
-      cnt = __popcll(v & p);
-    }
-    const bool ok = __ballot(bad) == 0ULL;
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-    if (lane == 0) {
-      f.good[r] = ok;
-      f.RD[r] = r == 0 ? 0 : (u64)cnt;
-      f.CE[r] = r == 0 ? 0 : a.rdeg[r];
-    }
+                                                 MQuery *__restrict__ cq, MState *__restrict__ cst) {
+  const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    MQuery q{};
+    q.type = MQ_CANON;
+    q.top = a.T;
+    q.bottom = 0;
+    q.src0 = -1;
+    *cq = q;
+    MState s{};
+    s.cur = a.T;
+    s.fresh = 1;
+    s.stop = a.T + 1;  // lowest round a segment stopped at (T + 1: none)
+    *cst = s;
+  }
+  if (!krecv) {
+    kcand_round(a, f, r);
     return;
   }
-  // vcount = |S_3| (OR of the partials), commit = vcount >= 2f+1; -1 / no commit
-  // where the wave's leader is absent (process.go:327-329)
-  const int wi = (blockIdx.x - rb) * 4 + (threadIdx.x >> 6);
-  if (wi >= f.nw) return;
-  const int w = wi + 1, r1 = 4 * wi + 1, L = (w < a.nlead ? (int)a.lead[w] : 1) - 1;
-  const bool has = (a.pres[(size_t)r1 * a.W + (L >> 6)] >> (L & 63)) & 1ULL;
-  u64 v = 0;
+  if (r > a.T) return;
+  bool bad = false;
+  int cnt = 0;
   if (lane < a.W) {
-    if (krecv) {
-      for (int g = 0; g < a.G; g++) v |= krecv[(size_t)g * kstride + (size_t)(a.T + 1) * a.WSs + (size_t)wi * a.W + lane];
-    } else {
+    const u64 p = a.pres[(size_t)r * a.W + lane];
+    const int g = lane / a.WSs, cw = lane - g * a.WSs;
+    const u64 v = krecv[(size_t)g * kstride + (size_t)r * a.WSs + cw];
+    a.K[(size_t)r * a.W + lane] = v;
+    bad = (v & p) != p;
+    cnt = __popcll(v & p);
+  }
+  const bool ok = __ballot(bad) == 0ULL;
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if (lane == 0) {
+    f.good[r] = ok;
+    f.RD[r] = r == 0 ? 0 : (u64)cnt;
+    f.CE[r] = r == 0 ? 0 : a.rdeg[r];
+  }
+}
+
+// After the stepped walk (one workgroup): vcount / commit of every wave from the
+// partial S_3 sets (P3: [Gp][nw][W], OR-ed; -1 / no commit where the leader is
+// absent, process.go:327-329), the canonical positions C (B = the walk's lowest stop
+// round), the E prefix (CE is final), and the chain tasks of the batch from the
+// commit flags (plan_body; the pop queries are the context's cached table and start
+// from their initial state in the first step).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_cpos(MArgs a, FArgs f, const MState *__restrict__ cst,
+                                                MQuery *__restrict__ q, int push_cap, const u64 *__restrict__ P3,
+                                                int Gp) {
+  __shared__ u64 part[2 * NT / 64];
+  const int lane = threadIdx.x & 63;
+  for (int wi0 = 0; wi0 < f.nw; wi0 += NT / 64) {  // one wave per wave index
+    const int wi = wi0 + (int)(threadIdx.x >> 6);
+    if (wi >= f.nw) break;  // wave-uniform
+    const int w = wi + 1, r1 = 4 * wi + 1, L = (w < a.nlead ? (int)a.lead[w] : 1) - 1;
+    const bool has = (a.pres[(size_t)r1 * a.W + (L >> 6)] >> (L & 63)) & 1ULL;
+    u64 v = 0;
+    if (lane < a.W)
       for (int g = 0; g < Gp; g++) v |= P3[((size_t)g * f.nw + wi) * a.W + lane];
+    const int c = (int)dr::wave_sum((u64)__popcll(v));
+    if (lane == 0) {
+      f.vcount[wi] = has ? c : -1;
+      f.commit[wi] = has && c >= f.quorum ? 1 : 0;
     }
   }
-  const int c = (int)dr::wave_sum((u64)__popcll(v));
-  if (lane == 0) {
-    f.vcount[wi] = has ? c : -1;
-    f.commit[wi] = has && c >= f.quorum ? 1 : 0;
-  }
-}
-
-// the stepped walk's positions (one workgroup): B = its lowest stop round
-template <int NT>
-__global__ __launch_bounds__(NT) void k_ms_cpos(MArgs a, FArgs f, const MState *__restrict__ cst) {
   const MState S = *cst;
-  canon_positions<NT>(a, f, min(S.stop, a.T + 1), S.npush);
-}
-
-// the G, E prefixes and the plan of the stepped batch: the pop queries and the
-// chain tasks with their initial states (one workgroup)
-template <int NT>
-__global__ __launch_bounds__(NT) void k_ms_plan_steps(MArgs a, FArgs f, MQuery *__restrict__ q, MState *__restrict__ st,
-                                                      int push_cap) {
-  __shared__ u64 part[NT / 64];
-  ms_prefix_one<NT>(a.T + 1, f.RG, f.Gc, part);
-  ms_prefix_one<NT>(a.T + 1, f.CE, f.Ec, part);
-  plan_body<NT>(a, f, q, st, push_cap, 1);
+  canon_positions<NT>(a, f, min(S.stop, a.T + 1), S.npush);  // (its barriers order the commit writes)
+  ms_prefix_two<NT>(a.T + 1, f.CE, f.Ec, nullptr, nullptr, part);
+  plan_body<NT>(a, f, q, nullptr, push_cap, 0);
 }
 
 // Partial round r of one query (every local shard's columns): the frontier FE's
@@ -155,14 +146,16 @@ __global__ __launch_bounds__(NT) void k_ms_plan_steps(MArgs a, FArgs f, MQuery *
 // (word l * WSs + c = column word c of local shard l).  Saturation as in the fused
 // sweep: once the OR of the rows a wave has read equals U_r on its words, no
 // further row adds a bit.  Every thread calls it.
+// strong = false: the rows are done (wave 0 saturated on the first word, k_ms_step2).
 template <int NT>
 __device__ __forceinline__ void expand_partial_local(const MArgs &a, int r, int bottom, const u64 *FE, u64 *ring, int WL,
-                                                     int dm, bool weak) {
+                                                     int dm, bool weak, bool strong) {
   constexpr int NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int SP = a.SP, W = a.W, WSs = a.WSs, NL = a.nlocal, WP = NL * SP;
   u64 *dst = ring + (size_t)((r - 1) & dm) * WL;
-  if (WP <= 64 && (64 % WP) == 0) {
+  if (!strong) {
+  } else if (WP <= 64 && (64 % WP) == 0) {
     const int l0 = (lane % WP) / SP, c0 = lane % SP;  // this lane's word of the concatenated row
     const u64 *base = a.strong + (size_t)r * a.strong_rstride + (size_t)l0 * a.strong_stride + c0;
     const u64 ur = lane < WP ? a.U[((size_t)l0 * a.R + r) * SP + c0] : 0ULL;
@@ -226,19 +219,41 @@ __device__ __forceinline__ void expand_partial_local(const MArgs &a, int r, int 
 // this step's rounds; rout: local mode the same layout for the next step (this
 // context's shards), RCCL mode [nq][WSs] (the send buffer).  Dynamic LDS:
 // ring[depth][WL] | FE[W].
+// batch: the pops and chains (their first step starts them from their query; chain
+// slots past the planned chains end there), else the canonical walk.  The first
+// batch step has one more workgroup: the G prefix (RG is final), read only by the
+// emission after the last step.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_step2(MArgs a, FArgs f, int j, MState *__restrict__ st,
-                                                 const u64 *__restrict__ rin, u64 *__restrict__ rout) {
+                                                 const u64 *__restrict__ rin, u64 *__restrict__ rout, int batch) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const MState S = st[qi];
-  if (S.done) return;
+  if (batch && j == 0 && qi == a.nq) {
+    ms_prefix_two<NT, 16>(a.T + 1, f.RG, f.Gc, nullptr, nullptr, lds);
+    return;
+  }
   const MQuery Q = a.q[qi];
+  MState S = st[qi];
+  if (batch && j == 0) {
+    if (qi >= f.npop + f.hdr[FH_NCHAIN]) {  // an unused chain slot
+      if (tid == 0) {
+        MState d{};
+        d.done = 1;
+        st[qi] = d;
+      }
+      return;
+    }
+    S = MState{};
+    S.low = Q.top;
+    S.cur = Q.top;
+  }
+  if (S.done) return;
   const int W = a.W, WSs = a.WSs, WL = a.nlocal * WSs, dm = a.depth - 1, D = a.depth, SP = a.SP;
   u64 *ring = lds, *FE = lds + (size_t)D * WL;
-  __shared__ int s_ctl[2];
+  __shared__ int s_ctl[3];
   __shared__ u64 s_e;
   __shared__ MState s_st;
+  __shared__ u64 sAcc[64];  // wave 0's rows of the first frontier word, local words of slot r-1
   u64 *gring = a.pend + (size_t)qi * D * WL;
   const bool pop = Q.type == MQ_POP, chain = Q.type == MQ_CHAIN, canon = Q.type == MQ_CANON;
   int r = canon ? S.cur : Q.top - j;
@@ -334,6 +349,27 @@ __global__ __launch_bounds__(NT) void k_ms_step2(MArgs a, FArgs f, int j, MState
       if (lane == 0) f.RD[r] = r == 0 ? 0 : (u64)cnt;
     }
     const bool summary = !done && full;
+    // A partial round's rows, first frontier word, by wave 0 alone: in a quorum DAG the
+    // OR of 64 rows is already U_r, the OR of every row of the round (saturation), and
+    // the other waves then read no row at all (they would each read a word of their own)
+    const int WP = a.nlocal * SP;
+    int sat = 0;
+    if (lane < WL) sAcc[lane] = 0;
+    if (!done && !summary && anyfe && WP <= 64 && (64 % WP) == 0) {
+      const int l0 = (lane % WP) / SP, c0 = lane % SP, RPL = 64 / WP;
+      const u64 *base = a.strong + (size_t)r * a.strong_rstride + (size_t)l0 * a.strong_stride + c0;
+      const u64 ur = lane < WP ? a.U[((size_t)l0 * a.R + r) * SP + c0] : 0ULL;
+      const int w0 = __ffsll((long long)__ballot(act && fe != 0ULL)) - 1;
+      const u64 bits = dr::shfl64(fe, w0);
+      u64 acc = 0;
+      for (int i = 0; i < WP; i++) {
+        const int row = i * RPL + lane / WP;
+        if ((bits >> row) & 1ULL) acc |= base[(size_t)(w0 * 64 + row) * SP];
+      }
+      for (int off = WP; off < 64; off <<= 1) acc |= shfl_xor64(acc, off);
+      sat = __ballot(lane < WP && acc != ur) == 0ULL;
+      if (lane < WP && c0 < WSs) sAcc[l0 * WSs + c0] = acc;
+    }
     u64 edges = S.edges;
     if (chain && summary) edges += a.sdr[r];
     if (!done && !chain && anyfe) low = min(low, r - a.dmax);
@@ -357,6 +393,7 @@ __global__ __launch_bounds__(NT) void k_ms_step2(MArgs a, FArgs f, int j, MState
       s_st = o;
       s_ctl[0] = done;
       s_ctl[1] = summary;
+      s_ctl[2] = sat;
       s_e = 0;
     }
   }
@@ -391,16 +428,17 @@ __global__ __launch_bounds__(NT) void k_ms_step2(MArgs a, FArgs f, int j, MState
       e = dr::wave_sum(e);
       if (lane == 0 && e) atomicAdd(&s_e, e);
     }
-    expand_partial_local<NT>(a, r, Q.bottom, FE, ring, WL, dm, weak);
+    expand_partial_local<NT>(a, r, Q.bottom, FE, ring, WL, dm, weak, !s_ctl[2]);
   }
   __syncthreads();
   // the ring goes back to global memory; slot r-1 (complete: every contribution
   // from the rounds above is in) leaves it for the exchange
   const int so = ((r - 1) & dm) * WL;
   for (int i = tid; i < D * WL; i += NT) {
-    const u64 v = ring[i];
+    u64 v = ring[i];
     if (i >= so && i < so + WL) {
       const int lw = i - so, l = lw / WSs, cw = lw - l * WSs;
+      v |= sAcc[lw];
       if (a.local) rout[((size_t)(a.shard0 + l) * a.nq + qi) * WSs + cw] = v;
       else rout[(size_t)qi * WSs + cw] = v;
       gring[i] = 0;

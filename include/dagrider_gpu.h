@@ -41,7 +41,8 @@ enum {
   DR_OK = 0,
   DR_E_INVAL = -1,    /* bad argument / reference would panic */
   DR_E_CAPACITY = -2, /* output buffer too small; required size reported */
-  DR_E_HIP = -3,      /* device / runtime failure */
+  DR_E_HIP = -3,      /* device / runtime failure: the call may have stopped part-way (e.g. an append
+                         whose rounds are mirrored without their irregular edges); destroy the context */
   DR_E_RCCL = -4,     /* collective failure */
   DR_E_CONTRACT = -5, /* DAG outside the mirrored contract (see dr_append_rounds_lists) */
   DR_E_STATE = -6     /* call order violated (e.g. append not contiguous) */
@@ -163,7 +164,12 @@ int dr_append_rounds_packed(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off
  * Same contract as dr_append_rounds_lists (else DR_E_CONTRACT); a vertex whose
  * id is already in the round becomes the one path() sees (the last slot).  All or nothing: on
  * any error the mirror is unchanged.  Only the rounds touched are re-read when
- * round summaries or the canonical cone are next needed. */
+ * round summaries or the canonical cone are next needed.  An edge may target
+ * any round below max_rounds, also one not mirrored yet: such a target is a
+ * dangling id (reached, never expanded), where Go's path() would index past
+ * p.dag and panic once its BFS dequeued it (process.go:111) -- whether it does
+ * depends on the BFS order, so this case answers instead of failing (parity
+ * unpinned for it). */
 int dr_append_vertices(dr_ctx *ctx, int k, const int32_t *slot_round, const int32_t *ids,
                        const uint32_t *strong_off, const int32_t *strong_ids, const uint32_t *weak_off,
                        const int32_t *weak_ids);

@@ -1,0 +1,21 @@
+# round 5 (d): stepped replay -- chain plan in k_ms_cpos, cached pop table, u64 bad-round search; variants
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r5d
+mkdir -p $O
+timeout -k 10 500 python3 -u -m pytest tests/test_gpu_shard.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+summ() { python3 -c "
+import json,sys
+for l in open('$1'):
+    d=json.loads(l); print('$2', d['G'], d['form'], round(d['ms_wall_median'],4), d['replay_ok'], d['steps'], d.get('host_syncs'), {k: round(v,4) for k,v in d['phases_ms'].items()})
+"; }
+timeout -k 10 300 python3 -u tools/shard_replay_bench.py --runs 20 > $O/shard.jsonl 2>&1
+summ $O/shard.jsonl base
+DR_SHARD_KEEP4=1 timeout -k 10 300 python3 -u tools/shard_replay_bench.py --runs 20 --stepped 1 > $O/shard_keep4.jsonl 2>&1
+summ $O/shard_keep4.jsonl keep4
+DR_SHARD_HOST_TIMING=1 timeout -k 10 300 python3 -u tools/shard_replay_bench.py --runs 5 --shards 1 > $O/host_timing.jsonl 2> $O/host_timing.err
+tail -4 $O/host_timing.err
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/shard_replay_bench.py --runs 3 --shards 1,8 --stepped 1 > $O/prof.jsonl 2>&1
+echo done
