@@ -167,6 +167,9 @@ struct dr_ctx {
   // DR_OPT_COMMIT_SPLIT: off by default -- at C4's N = 8 share (125 waves) k_commit_split
   // took 29 us against 22 us for k_commit, one workgroup per wave (profiles/r04/)
   int commit_split = 0;
+  // the planned replay's leader chains on one register-resident wavefront each at n <= 256
+  // (k_chain_reg; DR_CHAIN_REG=0: k_sweep's chain mode)
+  int chain_reg = getenv("DR_CHAIN_REG") ? atoi(getenv("DR_CHAIN_REG")) : 1;
   int last_split = 0;    // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
   bool kprev_ok = false;
@@ -690,6 +693,26 @@ int sweep_mode(const dr::SweepQuery &q) {
   if (q.flags & dr::Q_PRUNE) m |= dr::SW_PRUNE;
   if (q.flags & dr::Q_MERGE) m |= dr::SW_MERGE;
   return m;
+}
+// The planned replay's leader chains (a device-counted batch): n <= 256 on one
+// wavefront per chain with every round in registers (k_chain_reg), else k_sweep.
+template <int WS, int PF>
+hipError_t launch_chain_reg(dr_ctx *c, const SweepArgs &a) {
+  hipLaunchKernelGGL((dr::k_chain_reg<WS, PF>), dim3((a.nq + 3) / 4), dim3(256), 0, c->stream, c->view(), a.q,
+                     a.nq_dev, a.push_out, a.push_n, a.edges, a.wedges, a.hits, a.stops);
+  return hipGetLastError();
+}
+hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode);
+hipError_t launch_chains(dr_ctx *c, const SweepArgs &a) {
+  if (a.nq <= 0) return hipSuccess;
+  if (a.nq_dev && !a.seq && c->chain_reg) {
+    switch (c->WS) {
+      case 1: return launch_chain_reg<1, 4>(c, a);
+      case 2: return launch_chain_reg<2, 4>(c, a);
+      case 4: return launch_chain_reg<4, 3>(c, a);
+    }
+  }
+  return launch_sweep(c, a, dr::SW_CHAIN);
 }
 hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode) {
   if (a.nq <= 0) return hipSuccess;
@@ -2880,16 +2903,25 @@ hipError_t launch_paper_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::S
   return hipErrorInvalidValue;
 }
 
+// The canonical prefixes G, E of a REF replay: in k_own_emit's last workgroup when
+// one pass of its threads covers the rounds (C4: 4001 rounds, 512 threads, off the
+// critical path beside the pops' emission); a longer DAG (C3: 10 001 rounds, two
+// passes of 40 rounds a thread, ~20 us at the end of k_own_emit) takes k_canon_prefix
+// (1024 threads, one pass) on the canonical chain instead.
+bool own_emit_prefix(const dr_ctx *c, int own_nt) { return c->nrounds <= 8 * own_nt; }
+inline int own_emit_nt(const dr_ctx *c) { return c->WS <= 4 ? 256 : 512; }
+
 template <int WS>
 hipError_t launch_own_emit_t(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
                              u64 *qcount, u64 *qdigest, int32_t *qcut) {
   // 256 threads per query at n <= 256 (C3: 41 -> 37 us, more queries resident), 512 above
   // (C4 at 256: 12.8 -> 18.8 us; profiles/r03/v18_timeline_*_own256.txt)
   constexpr int NT = WS <= 4 ? 256 : 512;
-  hipLaunchKernelGGL((dr::k_own_emit<WS, NT>), dim3(nw + 1), dim3(NT), 0, c->stream, c->view(), c->masks.as<u64>(),
-                     c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(), c->slot_off.as<uint32_t>(),
-                     c->slot_src.as<uint16_t>(), qcount, qdigest, qcut, c->nrounds - 1, c->RG.as<u64>(),
-                     c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>());
+  const bool pre = own_emit_prefix(c, NT);  // else k_canon_prefix ran on the canonical chain
+  hipLaunchKernelGGL((dr::k_own_emit<WS, NT>), dim3(nw + (pre ? 1 : 0)), dim3(NT), 0, c->stream, c->view(),
+                     c->masks.as<u64>(), c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(),
+                     c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), qcount, qdigest, qcut, c->nrounds - 1,
+                     c->RG.as<u64>(), c->CE.as<u64>(), pre ? c->Gc.as<u64>() : nullptr, c->Ec.as<u64>());
   return hipGetLastError();
 }
 hipError_t launch_own_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
@@ -3162,7 +3194,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       a.stats = nullptr;
       a.nq_dev = plan + dr::PL_NQC;
       HIPCHK(c, c->rec(0));
-      HIPCHK(c, launch_sweep(c, a, dr::SW_CHAIN));
+      HIPCHK(c, launch_chains(c, a));
       HIPCHK(c, c->rec(1));
       // 3. pops
       hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
@@ -3171,7 +3203,9 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       HIPCHK(c, hipGetLastError());
       return 0;
     };
-    if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false, parts)) return rc;
+    // (REF: the canonical prefixes in k_own_emit's last workgroup unless the DAG is too long)
+    const bool canon_prefix = !paper && !own_emit_prefix(c, own_emit_nt(c));
+    if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, canon_prefix, parts)) return rc;
     if (paper) c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
     // 3+4. delivery sweeps (merging with K), then each query's emission
     a.q = dq;

@@ -1234,6 +1234,112 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
   }
 }
 
+// Leader chains (SW_CHAIN: strong only, process.go:341-350) for n <= 64 * WS, WS <=
+// 4, one wavefront per chain and every round in registers: lane l holds the WS rows
+// of sources l*WS .. l*WS + WS-1 (WS * WS contiguous words), loaded PF rounds ahead
+// with the round's presence and the lane's strong degrees.  A round is the OR of the
+// lane's rows whose source is in F & P and one OR across the wave of WS words; a
+// strong-only frontier has nothing pending below r-1, so there is no ring, no LDS and
+// no barrier.  The chain sweep of k_sweep walks a long leader gap round by round in
+// wave 0 with two workgroup barriers and a row read per round (C3: ~2 us a round, one
+// chain the critical path of the replay).  Same outputs as k_sweep's chain mode:
+// pushes, push count, edges (strong degrees of every expanded vertex), hits (no
+// target: 0), stop (-1 - the round the sweep ended at).  Four chains per workgroup.
+template <int WS, int PF>
+__global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *__restrict__ qs,
+                                                   const int *__restrict__ nq_dev, int32_t *__restrict__ push_out,
+                                                   int32_t *__restrict__ push_n, u64 *__restrict__ edges_out,
+                                                   u64 *__restrict__ wedges_out, uint8_t *__restrict__ hit_out,
+                                                   int32_t *__restrict__ stop_out) {
+  static_assert(WS >= 1 && WS <= 4 && PF >= 2, "register-resident rounds");
+  constexpr int RW = WS * WS;  // words of the lane's rows per round
+  const int lane = threadIdx.x & 63, qi = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (qi >= *nq_dev) return;  // wave-uniform
+  const SweepQuery q = qs[qi];
+  const int n = g.n, s0 = lane * WS, wd = s0 >> 6, sh = s0 & 63;  // a lane's WS sources share a word
+  const int lo = max(q.bottom, 0);
+  u64 rows[PF][RW], P[PF][WS];
+  uint32_t dg[PF][WS];
+  auto load = [&](u64 (&rw)[RW], u64 (&pw)[WS], uint32_t (&dd)[WS], int r) {
+    const u64 *src = g.strong + ((size_t)r * n + (size_t)min(s0, n - 1)) * WS;
+#pragma unroll
+    for (int i = 0; i < RW; i++) rw[i] = s0 + i / WS < n ? src[i] : 0ULL;
+#pragma unroll
+    for (int w = 0; w < WS; w++) pw[w] = g.present[(size_t)r * WS + w];
+#pragma unroll
+    for (int k = 0; k < WS; k++) dd[k] = s0 + k < n ? g.sdeg[(size_t)r * n + s0 + k] : 0u;
+  };
+  u64 F[WS];
+#pragma unroll
+  for (int w = 0; w < WS; w++) F[w] = (q.src0 >= 0 && w == (q.src0 >> 6)) ? 1ULL << (q.src0 & 63) : 0ULL;
+  int r = q.top;
+#pragma unroll
+  for (int k = 0; k < PF; k++)
+    if (r - k >= lo) load(rows[k], P[k], dg[k], r - k);
+  int npush = 0, stop_r = q.bottom;
+  u64 e = 0;
+  bool ended = false;
+  while (!ended) {
+#pragma unroll
+    for (int k = 0; k < PF; k++) {  // round r is in slot k
+      // waveReady's chain: a reachable, present leader of wave wv is pushed and the
+      // chain goes on from it alone (also at the bottom round, before the sweep stops)
+      if (r < q.top && ((r - 1) & 3) == 0) {
+        const int wv = (r - 1) / 4 + 1, L = g.lead[wv] - 1;
+        u64 fl = 0;
+#pragma unroll
+        for (int w = 0; w < WS; w++)
+          if (w == (L >> 6)) fl = F[w] & P[k][w];
+        if ((fl >> (L & 63)) & 1ULL) {
+#pragma unroll
+          for (int w = 0; w < WS; w++) F[w] = w == (L >> 6) ? 1ULL << (L & 63) : 0ULL;
+          if (lane == 0) push_out[q.out_off + npush] = wv;
+          npush++;
+        }
+      }
+      if (r <= q.bottom) {
+        ended = true;
+        break;
+      }
+      u64 any = 0;
+#pragma unroll
+      for (int w = 0; w < WS; w++) any |= F[w];
+      if (!any) {  // nothing reached in round r: nothing below either
+        stop_r = r;
+        ended = true;
+        break;
+      }
+      u64 fw = 0;
+#pragma unroll
+      for (int w = 0; w < WS; w++)
+        if (w == wd) fw = F[w] & P[k][w];
+      const uint32_t fe = (uint32_t)(fw >> sh);
+      u64 acc[WS];
+#pragma unroll
+      for (int w = 0; w < WS; w++) acc[w] = 0;
+#pragma unroll
+      for (int j = 0; j < WS; j++)
+        if ((fe >> j) & 1u) {
+          e += dg[k][j];
+#pragma unroll
+          for (int w = 0; w < WS; w++) acc[w] |= rows[k][j * WS + w];
+        }
+#pragma unroll
+      for (int w = 0; w < WS; w++) F[w] = wave_or(acc[w]);
+      if (r - PF >= lo) load(rows[k], P[k], dg[k], r - PF);  // slot k is free: round r - PF
+      --r;
+    }
+  }
+  e = wave_sum(e);
+  if (lane == 0) {
+    if (push_n) push_n[qi] = npush;
+    if (edges_out) edges_out[qi] = e;
+    if (wedges_out) wedges_out[qi] = 0;
+    if (hit_out) hit_out[qi] = 0;
+    if (stop_out) stop_out[qi] = -1 - stop_r;
+  }
+}
+
 // The planned replay's final pass (one workgroup), after the emitting sweep.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_replay_final(const EmitArgs ea) {

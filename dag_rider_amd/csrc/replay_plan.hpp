@@ -654,8 +654,9 @@ __global__ __launch_bounds__(NT) void k_paper_emit(DagView g, const u64 *__restr
 // workgroup per query, rounds cut+1 .. top (cut = merge round + dmax - 1: the
 // merge run's rounds have the canonical positions too) or, for
 // an unmerged sweep, every round it reached; positions from C_cut on.  NT/64
-// rounds at a time, one per wave.  The grid's last workgroup computes the
-// canonical digest and edge prefixes G, E for k_replay_final.
+// rounds at a time, one per wave.  With Gc, the grid's last workgroup computes the
+// canonical digest and edge prefixes G, E for k_replay_final (one pass of its
+// threads: T + 1 <= 8 NT; a longer DAG's prefixes come from k_canon_prefix).
 template <int WS, int NT>
 __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restrict__ masks, int dmax,
                                                  const int32_t *__restrict__ plan, const SweepQuery *__restrict__ dq,
@@ -668,7 +669,7 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
   constexpr int NWV = NT / 64;
   __shared__ u64 s_c[NWV], s_dg;
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (q == (int)gridDim.x - 1) {
+  if (Gc && q == (int)gridDim.x - 1) {  // (Gc null: k_canon_prefix computed them)
     canon_prefix_block<NT, 8>(T, RG, CE, Gc, Ec, nullptr);
     return;
   }

@@ -578,8 +578,8 @@ struct dr_shard {
   // pass's workgroups queue behind the side stream's (profiles/r04/)
   int wu_side = 0;
   int emit_fused = 0;  // REF emission inside the fused sweep (tuning: DR_SHARD_EMIT_FUSED=1)
-  int keep4 = 1;       // stepped pass: round 4w's rows with cached loads, re-read by the third vote step (off: DR_SHARD_KEEP4=0)
   int step_nt = 256;   // k_ms_step2 threads per query (tuning: DR_SHARD_STEP_NT=128)
+  int keep4 = 1;       // stepped pass: round 4w's rows with cached loads, re-read by the third vote step (off: DR_SHARD_KEEP4=0)
   int nrounds = 0, dmax = 1, depth = 2;
   size_t max_weak_round = 0;
   hipStream_t stream = nullptr;
@@ -595,11 +595,11 @@ struct dr_shard {
   SBuf bar, errf, push_out, push_n, cedges, vote_s0, vote_p[2], vote_send, vcount, D, pcnt, qcnt, qedges, qdig;
   // memoized replay (shard_memo.hpp): strong degree per round, round summaries,
   // canonical cone and prefixes, the stepped queries' buffers
-  SBuf sdr, mU, mWU, mK, mgood, mRD, mCE, mRG, mC, mE, mG, mksend, mkrecv, mq, mst, mpend, mrecv[2], msend, mmasks,
+  SBuf sdr, mU, mWU, mK, mgood, mRD, mCE, mRG, mC, mE, mG, mksend, mkrecv, mq, mpend, mrecv[2], msend, mmasks,
       mpush, mqidx, mqout;
   // stepped form: the canonical walk's query; S_1 per wave (k_ms_lcol; RCCL mode: the
   // exchanged partials, lcol_g slots of lcol_nw waves), valid until an append or a coin change
-  SBuf mcq, mlcol, mlcolp, vote_s3;
+  SBuf mcq, mlcol, mlcolp;
   bool lcol_ok = false;
   int lcol_nw = 1, lcol_g = 1;
   uint64_t lead_version = 0;  // bumped by every coin change
@@ -1087,12 +1087,7 @@ drs::MArgs make_margs(dr_shard *c, int nq, int T = -1) {
   a.WU = c->mWU.as<u64>();
   a.K = c->mK.as<u64>();
   a.q = c->mq.as<drs::MQuery>();
-  a.st0 = c->mst.as<drs::MState>();
-  a.st1 = c->mst.as<drs::MState>() + std::max(nq, 1);
   a.pend = c->mpend.as<u64>();
-  a.recv0 = c->mrecv[0].as<u64>();
-  a.recv1 = c->mrecv[1].as<u64>();
-  a.send = c->msend.as<u64>();
   a.masks = c->mmasks.as<u64>();
   a.push_out = c->mpush.as<int32_t>();
   a.n = c->n;
@@ -1282,7 +1277,7 @@ int ensure_lcol(dr_shard *c) {
 int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MState *st, int nq, int j0, int j1,
                  int batch) {
   const int WL = c->nlocal * c->WSs;
-  const size_t lds = std::max<size_t>(((size_t)c->depth * WL + c->W) * 8, 2 * 256 / 64 * 8);  // (the G prefix's scan)
+  const size_t lds = ((size_t)c->depth * WL + c->W) * 8;
   SHCHK(c, c->mpend.ensure((size_t)std::max(nq, 1) * c->depth * WL * 8));
   SHCHK(c, c->mrecv[0].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
   SHCHK(c, c->mrecv[1].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
@@ -1292,12 +1287,11 @@ int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MSt
   for (int j = j0; j < j1; j++) {
     u64 *rin = c->mrecv[j & 1].as<u64>();
     u64 *rout = c->local ? c->mrecv[(j + 1) & 1].as<u64>() : c->msend.as<u64>();
-    const int nb = nq + (batch && j == 0 ? 1 : 0);  // + the G prefix
     if (c->step_nt == 128)
-      hipLaunchKernelGGL((drs::k_ms_step2<128>), dim3(nb), dim3(128), lds, c->stream, b, f, j, st, (const u64 *)rin,
+      hipLaunchKernelGGL((drs::k_ms_step2<128>), dim3(nq), dim3(128), lds, c->stream, b, f, j, st, (const u64 *)rin,
                          rout, batch);
     else
-      hipLaunchKernelGGL((drs::k_ms_step2<256>), dim3(nb), dim3(256), lds, c->stream, b, f, j, st, (const u64 *)rin,
+      hipLaunchKernelGGL((drs::k_ms_step2<256>), dim3(nq), dim3(256), lds, c->stream, b, f, j, st, (const u64 *)rin,
                          rout, batch);
     SHCHK(c, hipGetLastError());
     if (!c->local) {
@@ -1310,19 +1304,16 @@ int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MSt
   return DR_OK;
 }
 
-// The stepped commit phase: S_1 (cached), the pass with the partial S_2 and the S_2
-// exchange; the third vote step (partial S_3) forks to the second stream, beside the
-// canonical walk; K^cand (RCCL mode: its exchange), then k_ms_kfin: K, good, the
-// RD / CE defaults, the walk's query.  The S_3 partials are joined (and exchanged)
-// after the walk (stepped_join_votes), and k_ms_cpos counts the votes.
+// The stepped commit phase: S_1 (cached), the pass with the partial S_2, the S_2
+// exchange, the third vote step (with K^cand in RCCL mode: one exchange for both),
+// then k_ms_kfin: K, good, the RD / CE defaults, vcount / commit, the walk's query.
 int stepped_commit(dr_shard *c, int nw, const drs::FArgs &f, const MOut &m) {
   const int T = c->nrounds - 1, W = c->W, G = c->G;
   drs::MArgs a1 = make_margs(c, 1, T);
   if (int rc = ensure_lcol(c)) return rc;
   const size_t pw = (size_t)std::max(nw, 1) * W * 8;
   SHCHK(c, c->vote_p[0].ensure((c->local ? 1 : G) * pw));  // S_2 partials, exchanged
-  SHCHK(c, c->vote_p[1].ensure(pw));                        // this rank's S_2 (RCCL send), then its S_3
-  SHCHK(c, c->vote_s3.ensure((c->local ? 1 : G) * pw));    // RCCL: the exchanged S_3 partials
+  SHCHK(c, c->vote_p[1].ensure(pw));                        // local: S_3; RCCL: this rank's S_2
   u64 *S2 = c->vote_p[0].as<u64>();
   PassIO p2;
   p2.Sout = c->local ? S2 : c->vote_p[1].as<u64>();
@@ -1334,63 +1325,48 @@ int stepped_commit(dr_shard *c, int nw, const drs::FArgs &f, const MOut &m) {
     SHNCCL(c, ncclAllGather(c->vote_p[1].p, S2, (size_t)nw * W, ncclUint64, c->comm, c->stream));
     c->last_xbytes += (uint64_t)nw * W * 8;
   }
-  // the third vote step on the second stream
-  SHCHK(c, hipEventRecord(c->fork, c->stream));
-  SHCHK(c, hipStreamWaitEvent(c->side, c->fork, 0));
   PassIO p3;
   p3.Sin = S2;
   p3.Gin = c->local ? 1 : G;
   p3.sin_nw = nw;
-  p3.Sout = c->vote_p[1].as<u64>();
-  p3.st = c->side;
-  SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP3, p3, false));
-  SHCHK(c, hipEventRecord(c->join, c->side));
-  const int rb = (T + 1 + 3) / 4;
+  const int rb = (T + 1 + 3) / 4, nb = rb + (nw + 3) / 4;
   if (c->local) {
-    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(rb), dim3(256), 0, c->stream, a1, f, (const u64 *)nullptr, (int64_t)0,
-                       c->mcq.as<drs::MQuery>(), m.canon);
+    p3.Sout = c->vote_p[1].as<u64>();
+    SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP3, p3, false));
+    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(nb), dim3(256), 0, c->stream, a1, f, (const u64 *)nullptr, (int64_t)0,
+                       (const u64 *)p3.Sout, 1, c->mcq.as<drs::MQuery>(), m.canon);
     SHCHK(c, hipGetLastError());
   } else {
-    const int64_t ks = (int64_t)(T + 1) * c->WSs;
+    // one send buffer: this rank's K^cand columns [(T+1) * WSs], then its partial S_3 [nw * W]
+    const int64_t ks = (int64_t)(T + 1) * c->WSs + (int64_t)nw * W;
     SHCHK(c, c->mksend.ensure((size_t)ks * 8));
     SHCHK(c, c->mkrecv.ensure((size_t)G * ks * 8));
     hipLaunchKernelGGL(drs::k_ms_kcand, dim3(rb, c->nlocal), dim3(drs::MS_NT), 0, c->stream, a1, T,
                        c->mksend.as<u64>());
     SHCHK(c, hipGetLastError());
+    p3.Sout = c->mksend.as<u64>() + (size_t)(T + 1) * c->WSs;
+    SHCHK(c, launch_pass(c, a1, f, nw, drs::VOTE_STEP3, p3, false));
     SHNCCL(c, ncclAllGather(c->mksend.p, c->mkrecv.p, (size_t)ks, ncclUint64, c->comm, c->stream));
     c->last_xbytes += (uint64_t)ks * 8;
-    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(rb), dim3(256), 0, c->stream, a1, f, (const u64 *)c->mkrecv.as<u64>(), ks,
-                       c->mcq.as<drs::MQuery>(), m.canon);
+    hipLaunchKernelGGL(drs::k_ms_kfin, dim3(nb), dim3(256), 0, c->stream, a1, f, (const u64 *)c->mkrecv.as<u64>(), ks,
+                       (const u64 *)nullptr, G, c->mcq.as<drs::MQuery>(), m.canon);
     SHCHK(c, hipGetLastError());
   }
   return DR_OK;
 }
 
-// the S_3 partials into the main stream (RCCL mode: exchanged); returns the OR's input
-int stepped_join_votes(dr_shard *c, int nw, const u64 **P3, int *Gp) {
-  SHCHK(c, hipStreamWaitEvent(c->stream, c->join, 0));
-  if (c->local) {
-    *P3 = c->vote_p[1].as<u64>();
-    *Gp = 1;
-    return DR_OK;
-  }
-  SHNCCL(c, ncclAllGather(c->vote_p[1].p, c->vote_s3.p, (size_t)nw * c->W, ncclUint64, c->comm, c->stream));
-  c->last_xbytes += (uint64_t)nw * c->W * 8;
-  *P3 = c->vote_s3.as<u64>();
-  *Gp = c->G;
-  return DR_OK;
-}
-
-// What follows the canonical walk: its positions, the E prefix and the chain plan
-// (k_ms_cpos), the canonical digests (the G prefix: the first batch step).
-int stepped_canon_tail(dr_shard *c, const drs::FArgs &f, const MOut &m, int nq, int64_t pcap, const u64 *P3, int Gp) {
+// What follows the canonical walk: the vote counts, its positions, the E prefix and
+// the chain plan (k_ms_cpos), the canonical digests and their G prefix.
+int stepped_canon_tail(dr_shard *c, const drs::FArgs &f, const MOut &m, int nq, int64_t pcap) {
   const int T = c->nrounds - 1, rb = (T + 1 + 3) / 4;
   drs::MArgs a = make_margs(c, nq, T);
   a.push_out = m.push;
   hipLaunchKernelGGL((drs::k_ms_cpos<1024>), dim3(1), dim3(1024), 0, c->stream, a, f, (const drs::MState *)m.canon,
-                     c->mq.as<drs::MQuery>(), (int)pcap, P3, Gp);
+                     c->mq.as<drs::MQuery>(), (int)pcap);
   SHCHK(c, hipGetLastError());
   hipLaunchKernelGGL(drs::k_ms_rg_full, dim3(rb), dim3(256), 0, c->stream, a, f);
+  SHCHK(c, hipGetLastError());
+  hipLaunchKernelGGL((drs::k_ms_gprefix<1024>), dim3(1), dim3(1024), 0, c->stream, a, f);
   SHCHK(c, hipGetLastError());
   return DR_OK;
 }
@@ -1504,8 +1480,6 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     return DR_OK;
   };
   int jc = 0, jb = 0;  // stepped form: canonical walk / batch steps launched
-  const u64 *P3 = nullptr;  // stepped form: the S_3 partials (Gp slots)
-  int Gp = 1;
   if (fused) {
     a.good = f.good;
     SHCHK(c, launch_pass(c, a, f, nw, drs::VOTE_FULL, PassIO{}));
@@ -1535,8 +1509,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
     if (int rc = upload_pops(c, qs, nw)) return rc;
     jc = std::max(1, c->hint_canon);
     if (int rc = launch_steps(c, ac, f, m.canon, 1, 0, jc, 0)) return rc;
-    if (int rc = stepped_join_votes(c, nw, &P3, &Gp)) return rc;
-    if (int rc = stepped_canon_tail(c, f, m, nq, pcap, P3, Gp)) return rc;
+    if (int rc = stepped_canon_tail(c, f, m, nq, pcap)) return rc;
     SHCHK(c, c->mark(2));
     jb = std::max(1, c->hint_batch);
     if (int rc = launch_steps(c, a, f, m.fin, nq, 0, jb, 1)) return rc;
@@ -1565,7 +1538,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
         if (jc + more > bound) return c->fail(DR_E_HIP, "memo replay: the canonical walk is live after %d steps", jc);
         if (int rc = launch_steps(c, ac, f, m.canon, 1, jc, jc + more, 0)) return rc;
         jc += more;
-        if (int rc = stepped_canon_tail(c, f, m, nq, pcap, P3, Gp)) return rc;
+        if (int rc = stepped_canon_tail(c, f, m, nq, pcap)) return rc;
         jb = std::max(1, c->hint_batch);
         if (int rc = launch_steps(c, a, f, m.fin, nq, 0, jb, 1)) return rc;
       } else {
@@ -1598,7 +1571,7 @@ int replay_memo(dr_shard *c, int nwaves, int chain_mode, int deliver_mode, dr_re
   for (int w = 1; w <= nw; w++)
     if (o->vcount[w - 1] >= 0) ce += c->h_deg[4 * w - 2] + c->h_deg[4 * w - 1] + c->h_deg[4 * w];
   o->commit_edges = ce;
-  // the chain tasks k_ms_plan made, in the same order: chain i is query npop + i
+  // the chain tasks plan_body made (k_ms_prefix_plan, k_ms_cpos), in the same order: chain i is query npop + i
   struct Task { int wave, q; int32_t pbase; };
   std::vector<Task> tasks;  // every commit, q = -1 without a chain query
   {
@@ -1866,9 +1839,9 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (SBuf *b : {&c->wck, &c->wcr, &c->wcro, &c->sdr, &c->mU, &c->mWU, &c->mK, &c->mgood, &c->mRD, &c->mCE, &c->mRG,
-                  &c->mC, &c->mE, &c->mG, &c->mksend, &c->mkrecv, &c->mq, &c->mst, &c->mpend, &c->mrecv[0],
+                  &c->mC, &c->mE, &c->mG, &c->mksend, &c->mkrecv, &c->mq, &c->mpend, &c->mrecv[0],
                   &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout, &c->ppref, &c->mSG,
-                  &c->mout, &c->mcq, &c->mlcol, &c->mlcolp, &c->vote_s3})
+                  &c->mout, &c->mcq, &c->mlcol, &c->mlcolp})
     b->release();
   if (c->pin) (void)hipHostFree(c->pin);
   for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out,

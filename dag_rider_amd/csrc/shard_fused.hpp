@@ -20,8 +20,9 @@
 //                    the lowest walked round) and the lowest round whose
 //                    speculative digest is stale.
 //   k_ms_rg_full     per-round canonical digests (speculative below that round).
-//   k_ms_plan        waveReady's chain tasks from the device commit flags
-//                    (persistent decidedWave: the previous commit; literal: 0).
+//   k_ms_prefix_plan the G, E prefixes and waveReady's chain tasks from the device
+//                    commit flags (persistent decidedWave: the previous commit;
+//                    literal: 0), plan_body.
 //   k_ms_sweep_full  one workgroup per query (orderVertices cone / leader chain),
 //                    round by round to its end: no exchange is needed when the
 //                    workgroup sees every column, so a query never waits for the
@@ -731,16 +732,16 @@ __global__ __launch_bounds__(256) void k_ms_rg_full(MArgs a, FArgs f) {
 }
 
 // ---------------------------------------------------------------------------
-// k_ms_plan: waveReady's chain tasks (process.go:341-350) from the device commit
-// flags, one workgroup.  Committed wave w's floor is the previous committed wave
-// (persistent decidedWave) or 0 (Q1 literal); it has a chain query when
-// w - 1 >= floor + 1.  Chain i takes query slot npop + i, its pushes from the
-// exclusive prefix of the chains' push bounds (w - floor each).  Every chain
-// slot's stepped state (st0) is initialised, unused slots as done.
+// plan_body: waveReady's chain tasks (process.go:341-350) from the device commit
+// flags, one workgroup (k_ms_prefix_plan, k_ms_cpos).  Committed wave w's floor is
+// the previous committed wave (persistent decidedWave) or 0 (Q1 literal); it has a
+// chain query when w - 1 >= floor + 1.  Chain i takes query slot npop + i, its
+// pushes from the exclusive prefix of the chains' push bounds (w - floor each).
+// make_pops: also the pop queries (the fused form).
 // ---------------------------------------------------------------------------
 template <int NT>
-__device__ __forceinline__ void plan_body(const MArgs &a, const FArgs &f, MQuery *__restrict__ q,
-                                          MState *__restrict__ st0, int push_cap, int make_pops) {
+__device__ __forceinline__ void plan_body(const MArgs &a, const FArgs &f, MQuery *__restrict__ q, int push_cap,
+                                          int make_pops) {
   __shared__ int64_t s_scan[NT / 64];
   const int nw = f.nw, tid = threadIdx.x;
   const int per = (nw + NT - 1) / NT, wa = 1 + tid * per, wb = min(nw + 1, wa + per);
@@ -772,12 +773,6 @@ __device__ __forceinline__ void plan_body(const MArgs &a, const FArgs &f, MQuery
         x.bottom = 0;
         x.src0 = L;
         x.mask_off = mo;
-        if (st0) {  // the stepped batch's initial state
-          MState s{};
-          s.low = x.top;
-          s.cur = x.top;
-          st0[pi] = s;
-        }
         q[pi++] = x;
         mo += (int64_t)(x.top + 1) * a.W;
       }
@@ -819,34 +814,17 @@ __device__ __forceinline__ void plan_body(const MArgs &a, const FArgs &f, MQuery
           x.push_base = (int32_t)pb;
           const int qi = f.npop + (int)ci;
           q[qi] = x;
-          if (st0) {
-            MState s{};
-            s.low = x.top;
-            s.cur = x.top;
-            st0[qi] = s;
-          }
           ci++;
           pb += w - fl;
         }
         pv = w;
       }
   }
-  if (st0)
-    for (int i = (int)ctot + tid; i < nw; i += NT) {
-      MState s{};
-      s.done = 1;
-      st0[f.npop + i] = s;
-    }
   if (tid == 0) {
     f.hdr[FH_NCHAIN] = (int32_t)ctot;
     f.hdr[FH_PUSHES] = (int32_t)min<int64_t>(ptot, INT32_MAX);
     f.hdr[FH_ERR] = ptot > push_cap ? 1 : 0;
   }
-}
-template <int NT>
-__global__ __launch_bounds__(NT) void k_ms_plan(MArgs a, FArgs f, MQuery *__restrict__ q, MState *__restrict__ st0,
-                                                int push_cap, int make_pops) {
-  plan_body<NT>(a, f, q, st0, push_cap, make_pops);
 }
 
 // The canonical prefixes G, E (RG, CE -> Gc, Ec) and the plan (pops and chains)
@@ -856,7 +834,7 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_prefix_plan(MArgs a, FArgs f, MQuery *__restrict__ q, int push_cap) {
   __shared__ u64 part[2 * NT / 64];
   ms_prefix_two<NT>(a.T + 1, f.RG, f.Gc, f.CE, f.Ec, part);
-  plan_body<NT>(a, f, q, (MState *)nullptr, push_cap, 1);
+  plan_body<NT>(a, f, q, push_cap, 1);
 }
 
 

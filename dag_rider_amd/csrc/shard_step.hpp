@@ -15,21 +15,23 @@
 //   k_ms_wu, k_ms_pass (VOTE_STEP2)   one read of the rank's columns of every
 //                   strong row: U per round and, from the replicated S_1, this
 //                   rank's partial S_2 (process.go:326-339) -> exchange.
-//   k_ms_pass (VOTE_STEP3)   round 4w's rows against S_2 only: partial S_3, on
-//                   the second stream, beside the canonical walk (one workgroup
-//                   per launch: the GPU is nearly idle under it); its exchange
-//                   after the walk.
-//   k_ms_kfin       K (= K^cand; RCCL mode: after the K^cand exchange), good_r,
-//                   the full-round defaults of RD / CE, the walk's query and state.
+//   k_ms_pass (VOTE_STEP3)   round 4w's rows against S_2 only: partial S_3,
+//                   exchanged together with K^cand (k_ms_kcand) in RCCL mode.
+//   k_ms_kfin       K (= K^cand), good_r, the full-round defaults of RD / CE, the
+//                   vote count and commit of every wave, the walk's query and state.
 //   k_ms_step2 x s  the canonical walk (one query), one round per launch.
-//   k_ms_cpos       vcount / commit of every wave, the canonical positions C over
-//                   the walked rounds, the E prefix, and the leader chains planned
-//                   on the device from the commit flags (the pop queries are a
-//                   cached table).
-//   k_ms_rg_full    the canonical digests.
-//   k_ms_step2 x s  every pop and chain, one round per launch (the first one also
-//                   computes the G prefix in one more workgroup).
+//   k_ms_cpos       the canonical positions C over the walked rounds, the E
+//                   prefix, and the leader chains planned on the device from the
+//                   commit flags (the pop queries are a cached table).
+//   k_ms_rg_full, k_ms_gprefix   the canonical digests and their prefix G.
+//   k_ms_step2 x s  every pop and chain, one round per launch.
 //   k_ms_emit       REF emission; one copy back, one host sync.
+//
+// Tried and not kept (profiles/r05/): the third vote step on a second stream beside
+// the canonical walk (the walk's one-workgroup launches queued behind its
+// workgroups: summary phase 0.062 -> 0.146 ms at G = 1), and each REF pop emitting
+// in the step where it ends (every such step grew by the slowest emission: deliver
+// + emit 0.101 -> 0.122 ms); 64 threads per query (0.43 -> 0.51 ms).
 //
 // k_ms_step2 is one workgroup per query (every local shard's columns in the same
 // workgroup): the query's pending ring of rounds below lives in LDS during the
@@ -66,78 +68,92 @@ __global__ __launch_bounds__(256) void k_ms_lcol(MArgs a, int nwl, u64 *__restri
 
 // Local-mode K^cand over every local shard (kcand_round), good_r, the RD / CE
 // defaults; RCCL mode: the same from the all-gathered K^cand columns (krecv:
-// [G][kstride], [(T+1) * WSs] K^cand words per rank).  Block 0 also writes the
-// canonical walk's query and initial state.
+// [G][kstride], each rank's [(T+1) * WSs] K^cand words then its [nw * W] partial
+// S_3).  Extra workgroups: vcount / commit of every wave from the S_3 partials (P3:
+// [Gp][nw][W] in local mode, inside krecv in RCCL mode; -1 / no commit where the
+// leader is absent, process.go:327-329); block 0 also writes the canonical walk's
+// query and initial state.
 __global__ __launch_bounds__(256) void k_ms_kfin(MArgs a, FArgs f, const u64 *__restrict__ krecv, int64_t kstride,
-                                                 MQuery *__restrict__ cq, MState *__restrict__ cst) {
-  const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    MQuery q{};
-    q.type = MQ_CANON;
-    q.top = a.T;
-    q.bottom = 0;
-    q.src0 = -1;
-    *cq = q;
-    MState s{};
-    s.cur = a.T;
-    s.fresh = 1;
-    s.stop = a.T + 1;  // lowest round a segment stopped at (T + 1: none)
-    *cst = s;
-  }
-  if (!krecv) {
-    kcand_round(a, f, r);
+                                                 const u64 *__restrict__ P3, int Gp, MQuery *__restrict__ cq,
+                                                 MState *__restrict__ cst) {
+  const int rb = (a.T + 1 + 3) / 4, lane = threadIdx.x & 63;
+  if ((int)blockIdx.x < rb) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      MQuery q{};
+      q.type = MQ_CANON;
+      q.top = a.T;
+      q.bottom = 0;
+      q.src0 = -1;
+      *cq = q;
+      MState s{};
+      s.cur = a.T;
+      s.fresh = 1;
+      s.stop = a.T + 1;  // lowest round a segment stopped at (T + 1: none)
+      *cst = s;
+    }
+    if (!krecv) {
+      kcand_round(a, f, r);
+      return;
+    }
+    if (r > a.T) return;
+    bool bad = false;
+    int cnt = 0;
+    if (lane < a.W) {
+      const u64 p = a.pres[(size_t)r * a.W + lane];
+      const int g = lane / a.WSs, cw = lane - g * a.WSs;
+      const u64 v = krecv[(size_t)g * kstride + (size_t)r * a.WSs + cw];
+      a.K[(size_t)r * a.W + lane] = v;
+      bad = (v & p) != p;
+      cnt = __popcll(v & p);
+    }
+    const bool ok = __ballot(bad) == 0ULL;
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if (lane == 0) {
+      f.good[r] = ok;
+      f.RD[r] = r == 0 ? 0 : (u64)cnt;
+      f.CE[r] = r == 0 ? 0 : a.rdeg[r];
+    }
     return;
   }
-  if (r > a.T) return;
-  bool bad = false;
-  int cnt = 0;
+  const int wi = (blockIdx.x - rb) * 4 + (threadIdx.x >> 6);
+  if (wi >= f.nw) return;
+  const int w = wi + 1, r1 = 4 * wi + 1, L = (w < a.nlead ? (int)a.lead[w] : 1) - 1;
+  const bool has = (a.pres[(size_t)r1 * a.W + (L >> 6)] >> (L & 63)) & 1ULL;
+  u64 v = 0;
   if (lane < a.W) {
-    const u64 p = a.pres[(size_t)r * a.W + lane];
-    const int g = lane / a.WSs, cw = lane - g * a.WSs;
-    const u64 v = krecv[(size_t)g * kstride + (size_t)r * a.WSs + cw];
-    a.K[(size_t)r * a.W + lane] = v;
-    bad = (v & p) != p;
-    cnt = __popcll(v & p);
+    if (krecv) {
+      for (int g = 0; g < a.G; g++) v |= krecv[(size_t)g * kstride + (size_t)(a.T + 1) * a.WSs + (size_t)wi * a.W + lane];
+    } else {
+      for (int g = 0; g < Gp; g++) v |= P3[((size_t)g * f.nw + wi) * a.W + lane];
+    }
   }
-  const bool ok = __ballot(bad) == 0ULL;
-  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  const int c = (int)dr::wave_sum((u64)__popcll(v));
   if (lane == 0) {
-    f.good[r] = ok;
-    f.RD[r] = r == 0 ? 0 : (u64)cnt;
-    f.CE[r] = r == 0 ? 0 : a.rdeg[r];
+    f.vcount[wi] = has ? c : -1;
+    f.commit[wi] = has && c >= f.quorum ? 1 : 0;
   }
 }
 
-// After the stepped walk (one workgroup): vcount / commit of every wave from the
-// partial S_3 sets (P3: [Gp][nw][W], OR-ed; -1 / no commit where the leader is
-// absent, process.go:327-329), the canonical positions C (B = the walk's lowest stop
-// round), the E prefix (CE is final), and the chain tasks of the batch from the
+// After the stepped walk (one workgroup): the canonical positions C (B = its lowest
+// stop round), the E prefix (CE is final), and the chain tasks of the batch from the
 // commit flags (plan_body; the pop queries are the context's cached table and start
 // from their initial state in the first step).
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_cpos(MArgs a, FArgs f, const MState *__restrict__ cst,
-                                                MQuery *__restrict__ q, int push_cap, const u64 *__restrict__ P3,
-                                                int Gp) {
+                                                MQuery *__restrict__ q, int push_cap) {
   __shared__ u64 part[2 * NT / 64];
-  const int lane = threadIdx.x & 63;
-  for (int wi0 = 0; wi0 < f.nw; wi0 += NT / 64) {  // one wave per wave index
-    const int wi = wi0 + (int)(threadIdx.x >> 6);
-    if (wi >= f.nw) break;  // wave-uniform
-    const int w = wi + 1, r1 = 4 * wi + 1, L = (w < a.nlead ? (int)a.lead[w] : 1) - 1;
-    const bool has = (a.pres[(size_t)r1 * a.W + (L >> 6)] >> (L & 63)) & 1ULL;
-    u64 v = 0;
-    if (lane < a.W)
-      for (int g = 0; g < Gp; g++) v |= P3[((size_t)g * f.nw + wi) * a.W + lane];
-    const int c = (int)dr::wave_sum((u64)__popcll(v));
-    if (lane == 0) {
-      f.vcount[wi] = has ? c : -1;
-      f.commit[wi] = has && c >= f.quorum ? 1 : 0;
-    }
-  }
   const MState S = *cst;
-  canon_positions<NT>(a, f, min(S.stop, a.T + 1), S.npush);  // (its barriers order the commit writes)
+  canon_positions<NT>(a, f, min(S.stop, a.T + 1), S.npush);
   ms_prefix_two<NT>(a.T + 1, f.CE, f.Ec, nullptr, nullptr, part);
-  plan_body<NT>(a, f, q, nullptr, push_cap, 0);
+  plan_body<NT>(a, f, q, push_cap, 0);
+}
+
+// the G prefix of the canonical digests (one workgroup; RG is final)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ms_gprefix(MArgs a, FArgs f) {
+  __shared__ u64 part[2 * NT / 64];
+  ms_prefix_two<NT>(a.T + 1, f.RG, f.Gc, nullptr, nullptr, part);
 }
 
 // Partial round r of one query (every local shard's columns): the frontier FE's
@@ -220,18 +236,12 @@ __device__ __forceinline__ void expand_partial_local(const MArgs &a, int r, int 
 // context's shards), RCCL mode [nq][WSs] (the send buffer).  Dynamic LDS:
 // ring[depth][WL] | FE[W].
 // batch: the pops and chains (their first step starts them from their query; chain
-// slots past the planned chains end there), else the canonical walk.  The first
-// batch step has one more workgroup: the G prefix (RG is final), read only by the
-// emission after the last step.
+// slots past the planned chains end there), else the canonical walk.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_ms_step2(MArgs a, FArgs f, int j, MState *__restrict__ st,
                                                  const u64 *__restrict__ rin, u64 *__restrict__ rout, int batch) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (batch && j == 0 && qi == a.nq) {
-    ms_prefix_two<NT, 16>(a.T + 1, f.RG, f.Gc, nullptr, nullptr, lds);
-    return;
-  }
   const MQuery Q = a.q[qi];
   MState S = st[qi];
   if (batch && j == 0) {
