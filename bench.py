@@ -13,7 +13,9 @@ half), c2, c5 (4096 independent n=128 replays, split across ranks), c4-deep (wea
 edges 80 rounds deep, past the memo window of 65: every pop sweeps its cone),
 c4-deep64 (weak edges 64 deep: memoized at the window's far end), c4-loop (the drop-in call
 pattern: per wave append 4 rounds -> dr_wave_ready -> dr_order_vertices, per-wave
-latency), --deliver paper (dedup across pops).
+latency), c4-far / c4-q8 (C4 + one weak edge 600 rounds deep / one strong edge to round
+r-3: exceptions to the regular graph, tested once and found benign, so the memo stays on),
+--deliver paper (dedup across pops).
 
 --gpus N without torchrun: spawns N ranks (torch.distributed.run) before anything
 touches a GPU; under torchrun WORLD_SIZE must equal N.  For C4 at N > 1 the line
@@ -859,7 +861,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4-deep", "c4-deep64", "c4-dups", "c5",
-                                                       "c4-loop"])
+                                                       "c4-loop", "c4-far", "c4-q8"])
     ap.add_argument("--graph", action="store_true",
                     help="replay the captured hipGraph of the launch sequence (DR_OPT_REPLAY_GRAPH)")
     ap.add_argument("--no-memo", action="store_true",
@@ -1065,7 +1067,7 @@ def main() -> int:
                    "commits": int(res.commit.sum()), "pops": int(len(res.pop_count)),
                    "ms": res.ms, "ms_note": "summary: mean over the timed steps; other phases: one "
                    "profiling replay after them (DR_OPT_PHASE_TIMING=2)",
-                   "sweep": res.sweep, "verify_vs_oracle": verify,
+                   "sweep": res.sweep, "verify_vs_oracle": verify, "exceptions": eng.exception_stats(),
                    "commit_split": split, "colshard": colshard[0] if colshard else None,
                    "kernels": {k: dict(v, GBps=(v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None))
                                for k, v in kb.items()}},

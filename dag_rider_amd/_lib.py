@@ -86,6 +86,7 @@ SIGNATURES = {
     "dr_replay_batch_view": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.c_int, i64,
                                        C.POINTER(ReplayView)]),
     "dr_last_kernel_ms": (C.c_int, [P, C.POINTER(f32)]),
+    "dr_exception_stats": (C.c_int, [P, P]),
     "dr_last_batch_phases": (C.c_int, [P, C.POINTER(f32)]),
     # include/dagrider_shard.h
     "dr_shard_unique_id": (C.c_int, [P]),

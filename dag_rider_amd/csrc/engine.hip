@@ -133,7 +133,33 @@ struct dr_ctx {
   int irr_tmax = 0;  // the highest round an irregular edge targets (the general sweep's row extent)
   DevBuf irr, irr_roff, gscratch, gquery, gaux;
   std::vector<uint32_t> h_irr_roff{0};
-  bool general() const { return nirr > 0; }
+  // Exceptions: the regular graph G_reg holds the strong rows and the weak
+  // columns of delta <= reg_max(); every other edge below its round -- a weak column past
+  // the window, a far weak edge, an irregular edge to a lower round -- is an exception.
+  // An exception u -> v with v in u's G_reg cone (its strong cone for a strong edge) is
+  // benign: it changes no cone, so every query may run on G_reg's summaries and canonical
+  // cone.  ensure_exceptions tests the exceptions of the rounds touched since its last
+  // test, one sweep each; an irregular edge to the same or a later round (irr_up) always
+  // takes the general sweep.  Per round (upload_suffix): the largest regular delta, the
+  // exception count, the irr_up count; per round (ensure_exceptions): exceptions found
+  // not benign.
+  std::vector<int32_t> h_rdreg, h_rexc, h_rup, h_rbad;
+  std::vector<uint32_t> h_sdx;  // [round] strong edges outside the rows (DagView::sdx)
+  DevBuf sdx;
+  int dreg = 1;            // largest regular weak delta (1: none)
+  int64_t nexc = 0, nirr_up = 0, nirr_down = 0, nbad = 0;
+  int exc_lo = 0;          // lowest round touched since the last exception test
+  uint64_t exc_sweeps = 0; // exception sweeps run (dr_exception_stats)
+  int depth_cap() const {
+    const int cap_words = (65536 - 64) / 8 - 2 * WS;
+    int cap = 1;
+    while (cap * 2 * WS <= cap_words) cap *= 2;
+    return cap;
+  }
+  int reg_max() const { return std::min(kMemoMaxDelta, depth_cap() - 1); }
+  // every exception known benign (the last test covers every round)
+  bool exc_clear() const { return nexc == 0 || (exc_lo >= nrounds && nbad == 0); }
+  bool general() const { return nirr_up > 0 || (nirr_down > 0 && !exc_clear()); }
   dr::GView gview() const { return dr::GView{irr.as<uint64_t>(), irr_roff.as<uint32_t>()}; }
   int lead_src(int w) const { return (w >= 0 && w < (int)h_lead.size()) ? h_lead[w] : 1; }
   // host mirror: per-round data, presence [rounds][WS], and the prefix offsets
@@ -236,16 +262,15 @@ struct dr_ctx {
     *out = batch_pin;
     return hipSuccess;
   }
-  // memo (round summaries + canonical cone): every weak edge in the dense summary
-  // window -- deltas up to kMemoMaxDelta (WU holds dd = dmax - 1 slots per round, the
-  // merge window is dmax rounds) that the sweeps' LDS ring holds -- and no far edges
-  bool memo_ok() const {
-    return nfar == 0 && nirr == 0 && dmax_near <= kMemoMaxDelta && (1 << depth_log2()) > dmax_near;
-  }
+  // memo (round summaries + canonical cone) over the regular graph: weak deltas up to
+  // reg_max() (WU holds dd = dreg - 1 slots per round, the merge window is dreg rounds,
+  // the sweeps' LDS ring holds them), every exception benign, no irregular edge upward
+  bool memo_struct_ok() const { return nirr_up == 0; }
+  bool memo_ok() const { return memo_struct_ok() && exc_clear(); }
   // repeated ids: the summaries' counts and the emission count every slot of a
   // reached id (REF), PAPER delivers an id at its first slot (slot_rep)
   bool memo_on() const { return use_memo && memo_ok(); }
-  int memo_dd() const { return std::max(0, dmax_near - 1); }
+  int memo_dd() const { return std::max(0, dreg - 1); }
   // scratch
   DevBuf q_buf, masks, dlv, push_out, push_n, edges, wedges, hits, commit, vcount, popdesc, rbase, counts,
       digest, pop_pos, ids;
@@ -370,7 +395,9 @@ struct dr_ctx {
     m.SD = SD.as<u64>();
     m.K = K.as<u64>();
     m.dd = memo_dd();
-    m.dmax = std::max(1, dmax_near);
+    m.dmax = std::max(1, dreg);
+    // exceptions present: the canonical walk and Q_REGULAR sweeps follow G_reg alone
+    m.dreg = nexc > 0 ? dreg : 0x7fffffff;
     return m;
   }
   dr::DagView view() const {
@@ -389,6 +416,7 @@ struct dr_ctx {
     v.dup_off = ndups ? dup_off.as<uint32_t>() : nullptr;
     v.dup_src = ndups ? dup_src.as<uint16_t>() : nullptr;
     v.slot_rep = ndups ? slot_rep.as<uint8_t>() : nullptr;
+    v.sdx = nirr > 0 ? sdx.as<uint32_t>() : nullptr;
     v.n = n;
     v.nrounds = nrounds;
     return v;
@@ -422,6 +450,27 @@ struct dr_ctx {
     canon_ok = false;
     canon_lo = std::min(canon_lo, r);
     up_lo = std::min(up_lo, r);
+    exc_lo = std::min(exc_lo, r);
+  }
+  // round r's regular window, exceptions and upward irregular edges (upload_suffix)
+  void round_exceptions(int r) {
+    const HostRound &h = hr[r];
+    const int X = reg_max();
+    int d = 1, ex = (int)h.far.size(), up = 0;
+    for (size_t j = 0; j < h.wc_key.size(); j++) {
+      const int delta = (int)(h.wc_key[j] >> 11);
+      if (delta <= X) { d = std::max(d, delta); continue; }
+      for (int w = 0; w < WS; w++) ex += __builtin_popcountll(h.wc_rows[j * WS + w]);
+    }
+    uint32_t sx = 0;
+    for (uint64_t x : h.irr) {
+      ((int)((x >> 11) & 0xFFFFFu) >= r) ? up++ : ex++;
+      sx += (uint32_t)((x >> 31) & 1u);
+    }
+    h_sdx[r] = sx;
+    h_rdreg[r] = d;
+    h_rexc[r] = ex;
+    h_rup[r] = up;
   }
   // Flatten rounds [up_lo, nrounds) of the variable-size per-round arrays
   // (slots, weak columns, far edges, weak counts, presence) and copy them to
@@ -448,6 +497,20 @@ struct dr_ctx {
       h_irr_roff[r + 1] = h_irr_roff[r] + (uint32_t)h.irr.size();
       h_weak_roff[r + 1] = h_weak_roff[r] + (uint32_t)h.nweak;
     }
+    h_rdreg.resize(R, 1);
+    h_rexc.resize(R, 0);
+    h_rup.resize(R, 0);
+    h_rbad.resize(R, 0);
+    h_sdx.resize(R, 0);
+    for (int r = lo; r < R; r++) round_exceptions(r);
+    dreg = 1;
+    nexc = nirr_up = 0;
+    for (int r = 0; r < R; r++) {
+      dreg = std::max(dreg, h_rdreg[r]);
+      nexc += h_rexc[r];
+      nirr_up += h_rup[r];
+    }
+    nirr_down = nirr - nirr_up;
     const size_t s0 = h_slot_off[lo], s1 = h_slot_off[R], k0 = h_wc_roff[lo], k1 = h_wc_roff[R];
     const size_t f0 = h_far_roff[lo], f1 = h_far_roff[R];
     // repeated ids: the slots after the first of their id, per round (rounds >= 1)
@@ -523,6 +586,10 @@ struct dr_ctx {
     if ((e = h2d(weak_roff.as<uint32_t>() + lo + 1, &h_weak_roff[lo + 1], nr * 4)) != hipSuccess) return e;
     if ((e = h2d(present.as<u64>() + (size_t)lo * WS, &h_present[(size_t)lo * WS], nr * WS * 8)) != hipSuccess)
       return e;
+    if (nirr > 0) {
+      if ((e = sdx.ensure(((size_t)max_rounds + 1) * 4)) != hipSuccess) return e;
+      if ((e = h2d(sdx.as<uint32_t>(), h_sdx.data(), (size_t)R * 4)) != hipSuccess) return e;  // every round: small
+    }
     up_lo = R;
     return hipSuccess;
   }
@@ -1089,6 +1156,7 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   in.WS = WS;
   in.r0 = r0;
   in.k = k;
+  in.max_rounds = c->max_rounds;
   in.slot_off = slot_off;
   in.slot_src = slot_src;
   in.strong = strong;
@@ -1122,6 +1190,8 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   c->h_wcnt.insert(c->h_wcnt.end(), built.wdeg.begin(), built.wdeg.end());
   c->h_present.insert(c->h_present.end(), built.pres.begin(), built.pres.end());
   c->nfar += nfar;
+  c->nirr += (int64_t)built.nirr;
+  if (built.nirr) c->irr_tmax = std::max(c->irr_tmax, built.irr_tmax);
   c->dmax_near = dmax;
   c->nrounds += k;
   for (int r = r0; r < r0 + k; r++) c->touch(r);
@@ -1591,7 +1661,7 @@ void mark_rounds_clean(dr_ctx *c) {
 // since they were last built: one workgroup per stale round.  A DAG that left
 // the memo contract (far weak edges, deltas > 65) keeps none.
 int refresh_rounds(dr_ctx *c) {
-  if (!(c->memo_on())) return DR_OK;
+  if (!c->use_memo || !c->memo_struct_ok()) return DR_OK;  // G_reg's summaries: exceptions tested or not
   const int T = c->nrounds - 1;
   if (T < 1) return DR_OK;
   const int dd = c->memo_dd();
@@ -1607,6 +1677,82 @@ int refresh_rounds(dr_ctx *c) {
   }
   mark_rounds_clean(c);
   return DR_OK;
+}
+
+// The exception test: every exception u -> v of a round touched since
+// the last test is benign iff v is in u's cone over G_reg (strong cone for a strong
+// edge): one sweep from u down to v's round per exception, Q_REGULAR (weak columns of
+// delta <= dreg, no far edge), on G_reg's round summaries (Q_SHORTCUT).  A test covers a
+// round for good: later rounds cannot change the cone of u below u's round, and an
+// append or replacement in round r re-tests rounds >= r (touch).  Nothing to do with
+// no exceptions, or with an upward irregular edge (the general sweep serves everything).
+int ensure_exceptions(dr_ctx *c) {
+  const int R = c->nrounds;
+  if (c->exc_lo >= R) return DR_OK;
+  if (c->nexc == 0 || c->nirr_up > 0) {
+    c->exc_lo = c->nexc == 0 ? INT_MAX : c->exc_lo;
+    return DR_OK;
+  }
+  const int lo = std::max(0, c->exc_lo), WS = c->WS, X = c->reg_max();
+  std::vector<dr::SweepQuery> qs, qw;  // strong-only, weak
+  std::vector<int32_t> rs, rw;         // each query's round
+  auto add = [&](int r, int src0, int tr, int ts0, bool strong) {
+    dr::SweepQuery q{};
+    q.top = r;
+    q.bottom = tr;
+    q.src0 = src0;
+    q.tgt0 = ts0;
+    q.flags = strong ? dr::Q_STRONG_ONLY : dr::Q_REGULAR;
+    (strong ? qs : qw).push_back(q);
+    (strong ? rs : rw).push_back(r);
+  };
+  for (int r = lo; r < R; r++) {
+    c->nbad -= c->h_rbad[r];
+    c->h_rbad[r] = 0;
+    if (!c->h_rexc[r]) continue;
+    const HostRound &h = c->hr[r];
+    for (size_t j = 0; j < h.wc_key.size(); j++) {
+      const int delta = (int)(h.wc_key[j] >> 11), ts = (int)(h.wc_key[j] & 2047u);
+      if (delta <= X) continue;
+      for (int w = 0; w < WS; w++)
+        for (u64 x = h.wc_rows[j * WS + w]; x; x &= x - 1) add(r, w * 64 + __builtin_ctzll(x), r - delta, ts, false);
+    }
+    for (uint64_t x : h.far) {
+      const uint32_t t = (uint32_t)x;
+      add(r, (int)(x >> 32), (int)(t >> 11), (int)(t & 2047u), false);
+    }
+    for (uint64_t x : h.irr) {
+      const int tr = (int)((x >> 11) & 0xFFFFFu);
+      if (tr < r) add(r, (int)((x >> 32) & 2047u), tr, (int)(x & 2047u), ((x >> 31) & 1u) != 0);
+    }
+  }
+  if (int rc = refresh_rounds(c)) return rc;
+  const int sc = (c->use_memo && c->ndirty == 0 && c->sum_dd == c->memo_dd() && R >= 2) ? dr::Q_SHORTCUT : 0;
+  for (int pass = 0; pass < 2; pass++) {
+    std::vector<dr::SweepQuery> &qv = pass ? qw : qs;
+    const std::vector<int32_t> &rv = pass ? rw : rs;
+    if (qv.empty()) continue;
+    for (auto &q : qv) q.flags |= sc;
+    std::vector<uint8_t> hits;
+    int rc = run_sweeps(c, qv, false, nullptr, nullptr, &hits, nullptr, nullptr, nullptr,
+                        [](size_t, size_t) { return 0; }, nullptr);
+    if (rc) return rc;
+    c->exc_sweeps += qv.size();
+    for (size_t i = 0; i < qv.size(); i++)
+      if (!hits[i]) {
+        c->h_rbad[rv[i]]++;
+        c->nbad++;
+      }
+  }
+  c->exc_lo = INT_MAX;
+  return DR_OK;
+}
+
+// every query entry point: the device, then the exception test of the rounds changed
+// since the last one (general() and memo_on() read its verdict)
+int prep_query(dr_ctx *c) {
+  if (int rc = set_device(c)) return rc;
+  return ensure_exceptions(c);
 }
 
 // Canonical cone K of the current top round + canonical prefixes C, G, E
@@ -1945,6 +2091,17 @@ extern "C" int dr_profile_kernel(dr_ctx *c, int kernel, int variant, int iters, 
 }
 
 #endif  // DR_TUNING
+
+extern "C" int dr_exception_stats(const dr_ctx *c, int64_t *out) {
+  if (!c || !out) return DR_E_INVAL;
+  out[0] = c->nexc;
+  out[1] = c->nbad;
+  out[2] = (int64_t)c->exc_sweeps;
+  out[3] = c->dreg;
+  out[4] = c->nirr_up;
+  out[5] = c->memo_on() ? 1 : 0;
+  return DR_OK;
+}
 
 extern "C" int dr_last_kernel_ms(const dr_ctx *c, float *ms) {
   if (!c || !ms) return DR_E_INVAL;
@@ -2285,7 +2442,7 @@ extern "C" int dr_path_batch(dr_ctx *c, int q, const int32_t *from, const int32_
   if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (q < 0 || (q > 0 && (!from || !to || !out))) return c->fail(DR_E_INVAL, "bad query arrays");
-  if (int rc = set_device(c)) return rc;
+  if (int rc = prep_query(c)) return rc;
   if (c->general()) return general_path(c, q, from, to, strong_only, out);
   if (int rc = refresh_rounds(c)) return rc;
   std::vector<dr::SweepQuery> qv;
@@ -2319,7 +2476,7 @@ extern "C" int dr_reach_sets(dr_ctx *c, int q, const int32_t *from, const int32_
                              uint64_t *out, size_t cap_words, size_t *out_words) {
   if (c) c->touch();
   if (!c) return DR_E_INVAL;
-  if (int rc = set_device(c)) return rc;
+  if (int rc = prep_query(c)) return rc;
   if (int rc = refresh_rounds(c)) return rc;
   size_t need = 0;
   for (int i = 0; i < q; i++) {
@@ -2681,7 +2838,7 @@ extern "C" int dr_buffer_admit(dr_ctx *c, int cur_round, int q, const int32_t *i
   }
   std::fill(admit, admit + q, 0);
   if (rhi < 0) return DR_OK;  // every buffered vertex is ahead of the current round
-  if (int rc = set_device(c)) return rc;
+  if (int rc = prep_query(c)) return rc;
   int ghost_round = INT32_MAX;
   for (int r = 0; r < c->nrounds && ghost_round == INT32_MAX; r++)
     if (c->has_ghost(r)) ghost_round = r;
@@ -2742,10 +2899,10 @@ extern "C" int dr_set_weak_edges(dr_ctx *c, int round, int nstrong, const int32_
     return c->fail(DR_E_INVAL, "setWeakEdges: round %d outside [1, %d] (Go: index out of range)", round, c->nrounds);
   if (mode != DR_WEAK_LITERAL && mode != DR_WEAK_PAPER) return c->fail(DR_E_INVAL, "unknown mode %d", mode);
   if (nstrong < 0 || (nstrong > 0 && !strong_ids)) return c->fail(DR_E_INVAL, "bad strong edge array");
+  if (int rc = prep_query(c)) return rc;
   if (c->general())
     return c->fail(DR_E_CONTRACT, "setWeakEdges on a mirror with edges outside the round contract (App. A Q8) "
                                   "is not supported");
-  if (int rc = set_device(c)) return rc;
   const int WS = c->WS;
   std::vector<u64> srow(WS, 0);
   for (int i = 0; i < nstrong; i++) {
@@ -2793,7 +2950,7 @@ extern "C" int dr_wave_commit(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_
   if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (!commit || !vcount) return c->fail(DR_E_INVAL, "null output");
-  if (int rc = set_device(c)) return rc;
+  if (int rc = prep_query(c)) return rc;
   return commit_range(c, w0, w1, commit, vcount, nullptr);
 }
 
@@ -2802,7 +2959,7 @@ extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *com
   if (c) c->touch();
   if (!c) return DR_E_INVAL;
   if (!commit || !vcount || !n_pushed) return c->fail(DR_E_INVAL, "null output");
-  if (int rc = set_device(c)) return rc;
+  if (int rc = prep_query(c)) return rc;
   if (int rc = refresh_rounds(c)) return rc;
   *n_pushed = 0;
   if (int rc = commit_range(c, wave, wave, commit, vcount, nullptr)) return rc;
@@ -2831,7 +2988,7 @@ extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack,
   if (!c) return DR_E_INVAL;
   if (nstack < 0 || (nstack > 0 && !stack_rs)) return c->fail(DR_E_INVAL, "bad stack");
   if (mode != DR_DELIVER_REF && mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad mode %d", mode);
-  if (int rc = set_device(c)) return rc;
+  if (int rc = prep_query(c)) return rc;
   if (out_n) *out_n = 0;
   if (nstack == 0) return DR_OK;
   if (cur_round >= c->nrounds) return c->fail(DR_E_INVAL, "p.round %d beyond the DAG (Go: index out of range)", cur_round);
@@ -3073,7 +3230,8 @@ std::vector<uint64_t> graph_key(const dr_ctx *c, int nw, int chain_mode, bool pa
           P(c->weak_roff.p),   P(c->far.p),        P(c->far_roff.p),     P(c->sdeg.p), P(c->wdeg.p),
           P(c->lead.p),        P(c->slot_off.p),   P(c->dup_off.p),      P(c->dup_src.p), P(c->slot_rep.p),
           P(c->Cc.p),          P(c->CE.p),         P(c->RD.p),           P(c->Gc.p),   P(c->Ec.p),
-          P(c->good.p),        P(c->nseg.p),       P(c->crbase.p),       P(c->rlo.p),  (uint64_t)c->ndups};
+          P(c->good.p),        P(c->nseg.p),       P(c->crbase.p),       P(c->rlo.p),  (uint64_t)c->ndups,
+          P(c->view().sdx),    (uint64_t)c->dreg,  (uint64_t)c->nexc};
 }
 
 int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out *o) {
@@ -3382,7 +3540,7 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   if (nwaves < 1 || 4 * nwaves >= c->nrounds) return c->fail(DR_E_INVAL, "nwaves %d needs rounds 0..%d mirrored", nwaves, 4 * nwaves);
   if (chain_mode != DR_CHAIN_LITERAL && chain_mode != DR_CHAIN_PERSISTENT) return c->fail(DR_E_INVAL, "bad chain mode");
   if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad deliver mode");
-  if (int rc = set_device(c)) return rc;
+  if (int rc = prep_query(c)) return rc;
   o->ms_commit = o->ms_chain = o->ms_deliver = o->ms_emit = o->ms_summary = 0;
   o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;

@@ -35,10 +35,11 @@ struct Chunk {
   std::string err;
   uint64_t deg = 0, nweak = 0;
   size_t nfar = 0;
-  int dmax = 1;
+  int dmax = 1, irr_tmax = 0;
   std::vector<uint32_t> key;   // this chunk's distinct near targets, in first-seen order
   std::vector<uint64_t> rows;  // [key][cw]: the chunk's words of each column
   std::vector<uint64_t> far;
+  std::vector<uint64_t> irr;  // edges outside the round contract (general.hpp irr_pack)
 };
 
 // The slot pass of round i (insertion order, presence).  An id may repeat (the
@@ -83,24 +84,30 @@ void build_chunk(const PackedRounds &in, int i, int s_lo, int s_hi, std::vector<
       ck.rc = failf(err, DR_E_CONTRACT, "round %d vertex (%d,%d): strong target source > n", r, r, s0 + 1);
       break;
     }
-    ck.deg += d;
-    out.sdeg[(size_t)i * n + s0] = (uint16_t)d;
     const uint32_t ea = in.weak_off[(size_t)i * n + s0], eb = in.weak_off[(size_t)i * n + s0 + 1];
     if (eb < ea) { ck.rc = failf(err, DR_E_INVAL, "weak_off not monotone at round %d", r); break; }
     if (eb > ea && !here) { ck.rc = failf(err, DR_E_CONTRACT, "round %d: weak edges on absent vertex (%d,%d)", r, r, s0 + 1); break; }
-    out.wdeg[(size_t)i * n + s0] = (uint16_t)std::min<uint32_t>(eb - ea, 65535u);
-    ck.nweak += eb - ea;
     const uint64_t mybit = 1ULL << (s0 & 63);
     const int myword = (s0 >> 6) - w_lo;
     uint64_t *rows = ck.rows.data();  // re-read after a new column grows it
+    uint32_t nsx = 0;  // strong edges outside the row (bit 31)
     for (uint32_t e = ea; e < eb; e++) {
       const uint32_t t = wt[e];
-      const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
-      if (ts >= n || tr > r - 2) {
-        ck.rc = ts >= n ? failf(err, DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): source > n", r, s0 + 1, tr, ts + 1)
-                        : failf(err, DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target a round < r-1", r, s0 + 1,
-                                tr, ts + 1);
+      const bool sx = (t >> 31) != 0;
+      const int tr = (int)((t >> 11) & 0xFFFFFu), ts = (int)(t & 2047u);
+      if (ts >= n || tr >= in.max_rounds || (sx && tr == r - 1)) {
+        ck.rc = ts >= n          ? failf(err, DR_E_CONTRACT, "edge (%d,%d)->(%d,%d): source > n", r, s0 + 1, tr, ts + 1)
+                : !sx || tr != r - 1 ? failf(err, DR_E_CONTRACT, "edge (%d,%d)->(%d,%d): round >= max_rounds %d", r,
+                                             s0 + 1, tr, ts + 1, in.max_rounds)
+                                     : failf(err, DR_E_CONTRACT, "strong edge (%d,%d)->(%d,%d) belongs in the row", r,
+                                             s0 + 1, tr, ts + 1);
         break;
+      }
+      if (sx || tr > r - 2) {  // outside the round contract (App. A Q8): kept for the general sweep / exception test
+        ck.irr.push_back(((uint64_t)s0 << 32) | ((uint64_t)(sx ? 1u : 0u) << 31) | ((uint64_t)tr << 11) | (uint64_t)ts);
+        ck.irr_tmax = tr > ck.irr_tmax ? tr : ck.irr_tmax;
+        nsx += sx ? 1u : 0u;
+        continue;
       }
       const int delta = r - tr;
       if (delta <= 1023) {
@@ -125,6 +132,11 @@ void build_chunk(const PackedRounds &in, int i, int s_lo, int s_hi, std::vector<
       }
     }
     if (ck.rc) break;
+    d += nsx;  // a vertex's strong degree counts every strong edge
+    ck.deg += d;
+    out.sdeg[(size_t)i * n + s0] = (uint16_t)std::min<uint64_t>(d, 65535u);
+    out.wdeg[(size_t)i * n + s0] = (uint16_t)std::min<uint32_t>(eb - ea - nsx, 65535u);
+    ck.nweak += eb - ea - nsx;
   }
   ck.dmax = dm;
   for (uint32_t at : touched) tab[at] = -1;
@@ -151,6 +163,7 @@ void merge_round(const PackedRounds &in, int i, const Chunk *ck, int nch, int ch
     h.deg += x.deg;
     h.nweak += x.nweak;
     h.far.insert(h.far.end(), x.far.begin(), x.far.end());
+    h.irr.insert(h.irr.end(), x.irr.begin(), x.irr.end());
   }
 }
 
@@ -210,6 +223,8 @@ int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std
         return x.rc;
       }
       out.nfar += x.nfar;
+      out.nirr += x.irr.size();
+      out.irr_tmax = std::max(out.irr_tmax, x.irr_tmax);
       out.dmax = std::max(out.dmax, x.dmax);
     }
   }

@@ -25,12 +25,12 @@ struct HostRound {
 
 // k pre-packed rounds r0..r0+k-1 (the dr_append_rounds_packed arrays).
 struct PackedRounds {
-  int n = 0, W = 0, WS = 0, r0 = 0, k = 0;
+  int n = 0, W = 0, WS = 0, r0 = 0, k = 0, max_rounds = 0;
   const uint32_t *slot_off = nullptr;
   const uint16_t *slot_src = nullptr;
   const uint64_t *strong = nullptr;
   const uint32_t *weak_off = nullptr;
-  const uint32_t *weak_tgt = nullptr;
+  const uint32_t *weak_tgt = nullptr;  // (r' << 11) | t-1; bit 31: a strong edge outside r-1 (App. A Q8)
 };
 
 struct BuiltRounds {
@@ -38,6 +38,8 @@ struct BuiltRounds {
   std::vector<uint64_t> pres;     // k * WS presence words
   std::vector<uint16_t> sdeg, wdeg;  // k * n per-vertex strong / weak degrees
   size_t nfar = 0;
+  size_t nirr = 0;                // edges outside the round contract (HostRound::irr)
+  int irr_tmax = 0;               // the highest round one of them targets
   int dmax = 1;                   // largest near weak delta seen (>= the caller's)
 };
 

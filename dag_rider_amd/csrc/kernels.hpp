@@ -52,7 +52,9 @@ __device__ u64 g_canon_timing[8];  // k_canon: start, segments walked, positions
 #define DR_TT(...)
 #endif
 
-enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8, Q_SHORTCUT = 16, Q_MERGE = 32 };
+// Q_REGULAR: follow only the regular graph -- strong rows and weak columns of delta
+// <= MemoView::dreg, no far edge (the exception test, engine.hip ensure_exceptions)
+enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8, Q_SHORTCUT = 16, Q_MERGE = 32, Q_REGULAR = 64 };
 
 struct SweepQuery {
   int32_t top;       // start round (the `from` vertex's round)
@@ -87,6 +89,10 @@ struct DagView {
   const uint32_t *dup_off;
   const uint16_t *dup_src;
   const uint8_t *slot_rep;
+  // [round] strong edges kept beside the rows (App. A Q8: to a round other than r-1),
+  // counted in sdeg but not in the rows' popcount: the round summaries' SD adds them.
+  // Null when the mirror has none.
+  const uint32_t *sdx;
   int32_t n;
   int32_t nrounds;
 };
@@ -364,7 +370,8 @@ struct MemoView {
   const u64 *SD;
   const u64 *K;
   int32_t dd;    // dense weak slots (deltas 2 .. dd+1); 0 with no weak edges
-  int32_t dmax;  // merge window = max(1, largest weak delta)
+  int32_t dmax;  // merge window = max(1, largest regular weak delta)
+  int32_t dreg;  // the regular window: weak columns of larger delta (and far edges) are exceptions
 };
 
 // One partial round r of a sweep: the frontier FE's strong rows -> ring slot of
@@ -379,10 +386,14 @@ struct MemoView {
 // summaries) a wave stops loading rows once the OR of what it has read equals Ur
 // -- no further row can add a bit.  wc0/wc1: the round's weak-column range when
 // the caller prefetched it (-1: read it here).  row_bytes counts bytes read.
+// dreg: weak columns of larger delta and far edges are not followed (Q_REGULAR); the
+// weak edges counted are every weak edge of the frontier's vertices (their weak degree,
+// exceptions included: the edge totals are the reference's).
 template <int WS, int NT, bool WEAK>
 __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom, const u64 *FE, u64 *ring, int depth,
                                             u64 *mask_bottom, const u64 *Ur, u64 &my_edges, u64 &my_wedges,
-                                            u64 &row_bytes, int64_t wc0 = -1, int64_t wc1 = -1, u64 *tsub = nullptr) {
+                                            u64 &row_bytes, int64_t wc0 = -1, int64_t wc1 = -1, u64 *tsub = nullptr,
+                                            int dreg = 0x7fffffff) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT, NMAX = G::NMAX;
   constexpr int GRP = CPT < 4 ? CPT : 4;  // 4 x RPP rows per step: a C4 frontier saturates in one
@@ -409,7 +420,8 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
     }
   }
   const uint16_t *deg = g.sdeg + (size_t)r * n;
-  uint16_t dg[SPT];  // loaded now, used after the rows: no wait here
+  const uint16_t *wdg = g.wdeg + (size_t)r * n;
+  uint16_t dg[SPT], dw[SPT];  // loaded now, used after the rows: no wait here
   uint32_t din = 0;  // bit k: source tid*SPT+k is in the frontier
 #pragma unroll
   for (int k = 0; k < SPT; k++) {
@@ -417,6 +429,7 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
     const bool in = s < n && ((FE[s >> 6] >> (s & 63)) & 1ULL);
     din |= (in ? 1u : 0u) << k;
     dg[k] = in ? deg[s] : (uint16_t)0;
+    dw[k] = (WEAK && in) ? wdg[s] : (uint16_t)0;
   }
   const u64 *rows = g.strong + (size_t)r * n * WS;
   u64 a0 = 0, a1 = 0;
@@ -474,7 +487,10 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
     if (CW == 2 && a1) atomicOr(dst + 1, a1);
   }
 #pragma unroll
-  for (int k = 0; k < SPT; k++) my_edges += dg[k];
+  for (int k = 0; k < SPT; k++) {
+    my_edges += dg[k];
+    if constexpr (WEAK) my_wedges += dw[k];
+  }
   row_bytes += 2 * (u64)__popc(din);
   DR_TT(if (tsub && tid == 0) { const u64 t = wall_clock64(); tsub[2] += t - t0; t0 = t; })
   if constexpr (!WEAK) return lowmin;
@@ -485,9 +501,8 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
   const u64 gm = WS >= 64 ? ~0ULL : (((1ULL << WS) - 1ULL) << gbase);
   auto column = [&](u64 row, uint32_t key) {
     const u64 v = row & fe;
-    my_wedges += (u64)popc64(v);
     const u64 bal = __ballot(v != 0ULL);
-    if (w == 0 && (bal & gm)) {
+    if (w == 0 && (bal & gm) && (int)(key >> 11) <= dreg) {
       const int delta = (int)(key >> 11), ts = (int)(key & 2047u), tr = r - delta;
       if (tr >= bottom) {
         const u64 bit = 1ULL << (ts & 63);
@@ -517,13 +532,12 @@ __device__ __forceinline__ int expand_round(const DagView &g, int r, int bottom,
     for (int q = 0; q < CB; q++)
       if (j0 + (uint32_t)(q * EPP) < c1) column(rv[q], kv[q]);  // wave-uniform
   }
-  const uint32_t f0 = g.far_roff[r], f1 = g.far_roff[r + 1];
+  const uint32_t f0 = g.far_roff[r], f1 = dreg > 1023 ? g.far_roff[r + 1] : f0;
   for (uint32_t e = f0 + tid; e < f1; e += NT) {
     const u64 y = g.far[e];
     const int own = (int)(y >> 32);
     const uint32_t t = (uint32_t)y;
     if (!((FE[own >> 6] >> (own & 63)) & 1ULL)) continue;
-    my_wedges++;
     const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
     if (tr < bottom) continue;
     const u64 bit = 1ULL << (ts & 63);
@@ -785,6 +799,83 @@ __device__ __forceinline__ void canon_prefix_block(int T, const u64 *__restrict_
   }
 }
 
+// The same prefixes without rbase (A, B over rounds 0..T, round 0 counted as 0), thread
+// t owning CH consecutive rounds of each tile of NT * CH (16-B loads, every load of a
+// tile in flight at once), one scan of the threads' totals per tile.  C3's 10 001
+// rounds are one tile at NT = 1024 (canon_prefix_block: 17 us, lanes 80 B apart).
+template <int NT, int CH = 16>
+__device__ __forceinline__ void canon_prefix_tiles(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                   u64 *__restrict__ A, u64 *__restrict__ B) {
+  constexpr int NW = NT / 64, TILE = NT * CH;
+  static_assert(CH % 2 == 0, "pairs of rounds per load");
+  __shared__ u64 part[2 * NW];
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, n = T + 1;
+  u64 cx = 0, cy = 0;
+  for (int t0 = 0; t0 < n; t0 += TILE) {
+    const int base = t0 + (int)threadIdx.x * CH;
+    u64 x[CH], y[CH];
+#pragma unroll
+    for (int c = 0; c < CH; c += 2) {
+      const int r = base + c;
+      if (r + 1 < n) {
+        const u64x2 va = *reinterpret_cast<const u64x2 *>(a + r), vb = b ? *reinterpret_cast<const u64x2 *>(b + r) : u64x2{0, 0};
+        x[c] = va.x;
+        x[c + 1] = va.y;
+        y[c] = vb.x;
+        y[c + 1] = vb.y;
+      } else {
+        x[c] = r < n ? a[r] : 0ULL;
+        y[c] = (r < n && b) ? b[r] : 0ULL;
+        x[c + 1] = y[c + 1] = 0;
+      }
+      if (r == 0) x[0] = y[0] = 0;  // round 0 is never delivered
+    }
+#pragma unroll
+    for (int c = 1; c < CH; c++) {
+      x[c] += x[c - 1];
+      y[c] += y[c - 1];
+    }
+    const u64 sx = x[CH - 1], sy = y[CH - 1];
+    u64 ix = sx, iy = sy;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const u64 tx = shfl_up64(ix, off), ty = shfl_up64(iy, off);
+      if (lane >= off) {
+        ix += tx;
+        iy += ty;
+      }
+    }
+    if (lane == 63) {
+      part[wv] = ix;
+      part[NW + wv] = iy;
+    }
+    __syncthreads();
+    u64 ox = cx, oy = cy, tx = 0, ty = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      const u64 px = part[w], py = part[NW + w];
+      if (w < wv) {
+        ox += px;
+        oy += py;
+      }
+      tx += px;
+      ty += py;
+    }
+    __syncthreads();
+    ox += ix - sx;
+    oy += iy - sy;
+#pragma unroll
+    for (int c = 0; c < CH; c++)
+      if (base + c < n) {
+        A[base + c] = ox + x[c];
+        if (b) B[base + c] = oy + y[c];
+      }
+    cx += tx;
+    cy += ty;
+  }
+}
+
 // plan[] slots (int32, device)
 enum : int { PL_NTASK = 0, PL_NQC = 1, PL_NPUSH = 2, PL_CAPERR = 3, PL_NQD = 4, PL_NDESC = 5, PL_N = 8 };
 // header written to host memory by k_plan_final (u64)
@@ -1021,6 +1112,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
     const SweepQuery q = qs[qi];
     const bool has_masks = q.flags & Q_MASKS;
     const bool shortcut = q.flags & Q_SHORTCUT;
+    const int dreg = (q.flags & Q_REGULAR) ? mv.dreg : 0x7fffffff;
     for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
     if (tid == 0) {
       s_ctl[0] = q.top; s_ctl[1] = q.top; s_ctl[2] = 0; s_ctl[3] = 0; s_ctl[4] = q.bottom;
@@ -1138,13 +1230,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
                 my_rowb += WS * 8 + 2;
               }
               if constexpr (WEAK) {
+                if (tid == 0) my_wedges += g.wdeg[(size_t)r * g.n + s0];  // every weak edge of the vertex
                 const uint32_t c0 = (uint32_t)__shfl((int)cur.C0, 0), c1 = (uint32_t)__shfl((int)cur.C1, 0);
                 for (uint32_t jj = c0 + tid; jj < c1; jj += 64) {
                   if (!((g.wc_rows[(size_t)jj * WS + (s0 >> 6)] >> (s0 & 63)) & 1ULL)) continue;
                   const uint32_t key = g.wc_key[jj];
                   const int delta = (int)(key >> 11), ts = (int)(key & 2047u), tr = r - delta;
-                  my_wedges++;
-                  if (tr < q.bottom) continue;
+                  if (tr < q.bottom || delta > dreg) continue;
                   const u64 bit = 1ULL << (ts & 63);
                   lowmin = min(lowmin, tr);
                   if (delta < depth) atomicOr(ring + (size_t)(tr & dmask) * WS + (ts >> 6), bit);
@@ -1182,11 +1274,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
       if (s_ctl[0] < r || true) {
         const int lowmin = expand_round<WS, NT, WEAK>(g, r, q.bottom, FE, ring, depth, masks + q.mask_off,
                                                       shortcut ? mv.U + (size_t)r * WS : nullptr, my_edges,
-                                                      my_wedges, my_rowb, WEAK ? s_ctl[5] : -1, WEAK ? s_ctl[6] : -1
+                                                      my_wedges, my_rowb, WEAK ? s_ctl[5] : -1, WEAK ? s_ctl[6] : -1,
 #ifdef DR_SWEEP_TIMING
-                                                      , tt_sub
+                                                      tt_sub,
+#else
+                                                      nullptr,
 #endif
-        );
+                                                      dreg);
         if (WEAK && lowmin != 0x7fffffff) atomicMin(&s_ctl[0], lowmin);
       }
       __syncthreads();
@@ -1464,7 +1558,7 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
       if (test) { S[tid] = Tn[tid]; Tn[tid] = 0; }
       if (k + 1 < nr) P[tid] = g.present[(size_t)(r + 1) * WS + tid];
     }
-    if (tid == 0) { SD[r] = sSD; sSD = 0; }
+    if (tid == 0) { SD[r] = sSD + (g.sdx ? g.sdx[r] : 0u); sSD = 0; }
     __syncthreads();
     round_begin(k + 1);
   };
@@ -1552,7 +1646,7 @@ __global__ __launch_bounds__(NT) void k_round_summary(DagView g, const int32_t *
   if (lane == 0 && deg) atomicAdd(&sSD, deg);
   __syncthreads();
   if (tid < WS) U[(size_t)r * WS + tid] = sU[tid];
-  if (tid == 0) SD[r] = sSD;
+  if (tid == 0) SD[r] = sSD + (g.sdx ? g.sdx[r] : 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1642,7 +1736,8 @@ __global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, in
   // every weak-column entry has at least one source: its key alone is the union
   for (uint32_t j = g.wc_roff[r] + lane; j < g.wc_roff[r + 1]; j += 64) {
     const uint32_t key = g.wc_key[j];
-    atomicOr(&sW[((key >> 11) - 2) * WS + ((key & 2047u) >> 6)], 1ULL << (key & 63u));
+    const uint32_t d = (key >> 11) - 2;  // keys beyond the regular window are exceptions (no slot)
+    if (d < (uint32_t)dd) atomicOr(&sW[d * WS + ((key & 2047u) >> 6)], 1ULL << (key & 63u));
   }
   if (RG) {  // the round's slots in lane-contiguous runs of SPT
     constexpr int SPT = 8;
@@ -1879,7 +1974,8 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
           if (tid == 0) e = cur.SD + cur.NW();  // prefetched with the round's words
         } else {
           u64 rb = 0;
-          expand_round<WS, NT, true>(g, r, 0, FE, ring, depth, K, mv.U + (size_t)r * WS, e, we, rb);
+          expand_round<WS, NT, true>(g, r, 0, FE, ring, depth, K, mv.U + (size_t)r * WS, e, we, rb, -1, -1, nullptr,
+                                     mv.dreg);  // G_reg: exceptions are benign (engine.hip ensure_exceptions)
         }
         e += we;
         if (e) atomicAdd(&s_edges[0], e);
@@ -2168,7 +2264,8 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                      u64 *__restrict__ A, u64 *__restrict__ B,
                                                      uint32_t *__restrict__ rbase) {
-  canon_prefix_block<NT>(T, a, b, A, B, rbase);
+  if (rbase) canon_prefix_block<NT>(T, a, b, A, B, rbase);
+  else canon_prefix_tiles<NT>(T, a, b, A, B);
 }
 
 // Multi-segment copy between device memory and pinned (device-mapped) host

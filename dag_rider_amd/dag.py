@@ -62,7 +62,8 @@ def flatten_lists(dag: Sequence[Sequence[Vertex]], r0: int = 0, r1: int | None =
 @dataclass
 class PackedDag:
     """Packed DAG: strong rows by (round, source-1), W=ceil(n/64) words; weak CSR by
-    vertex index r*n+s-1, targets (round << 11) | (source-1); slot_src 0 = ghost."""
+    vertex index r*n+s-1, targets (round << 11) | (source-1), bit 31 set for a strong
+    edge outside round r-1 (App. A Q8); slot_src 0 = ghost."""
 
     n: int
     nrounds: int
@@ -105,8 +106,10 @@ class PackedDag:
                 strong = [VertexID(r - 1, w * 64 + b + 1) for w in range(self.W) for b in range(64)
                           if (int(row[w]) >> b) & 1]
                 g = r * self.n + s - 1
-                weak = [VertexID(int(t) >> 11, (int(t) & 2047) + 1)
-                        for t in self.weak_tgt[self.weak_off[g]:self.weak_off[g + 1]]]
+                ts = [int(t) for t in self.weak_tgt[self.weak_off[g]:self.weak_off[g + 1]]]
+                # bit 31: a strong edge outside the row's round r-1 (App. A Q8)
+                strong += [VertexID((t >> 11) & 0xFFFFF, (t & 2047) + 1) for t in ts if t >> 31]
+                weak = [VertexID(t >> 11, (t & 2047) + 1) for t in ts if not t >> 31]
                 rnd.append(Vertex(VertexID(r, s), b"", strong, weak))
             dag.append(rnd)
         return dag

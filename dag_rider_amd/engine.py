@@ -126,6 +126,14 @@ class Engine:
         self._check(self._L.dr_last_kernel_ms(self._h, C.byref(ms)))
         return ms.value
 
+    def exception_stats(self) -> dict:
+        """dr_exception_stats: the exceptions to the regular graph and the test's verdict
+        (include/dagrider_gpu.h)."""
+        out = np.zeros(6, np.int64)
+        self._check(self._L.dr_exception_stats(self._h, out.ctypes.data))
+        keys = ("exceptions", "changing", "sweeps", "regular_delta", "upward", "memo")
+        return {k: int(v) for k, v in zip(keys, out)}
+
     @property
     def num_rounds(self) -> int:
         return self._L.dr_num_rounds(self._h)

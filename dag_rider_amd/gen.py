@@ -30,6 +30,10 @@ class GenConfig:
     # w.p. p_dup, at a random position of its round (uponDeliver / the buffer loop
     # appending a vertex already in the round, process.go:158-169, :229)
     p_dup: float = 0.0
+    # single edges added after generation, (round, source, target round, target source,
+    # strong): a weak edge past the memo window or a strong edge skipping rounds (App. A
+    # Q8) -- exceptions to the regular graph (engine.hip ensure_exceptions)
+    extra: tuple = ()
 
     @property
     def faulty(self) -> int:
@@ -53,6 +57,11 @@ CONFIGS = {
     "c4-deep64": GenConfig("c4-deep64", 1024, 4000, 4, 1.0, 0.02, 0.04, 64, 0.0),
     # C4 with repeated ids: ~1 % of each round's ids delivered twice (--config c4-dups)
     "c4-dups": GenConfig("c4-dups", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0, 0.01),
+    # C4 + one weak edge 600 rounds deep (past the regular window): an exception whose
+    # target is in its source's regular cone, so the memo stays on (--config c4-far)
+    "c4-far": GenConfig("c4-far", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0, extra=((2002, 17, 1402, 5, False),)),
+    # C4 + one strong edge to round r-3 (--config c4-q8)
+    "c4-q8": GenConfig("c4-q8", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0, extra=((2001, 17, 1998, 5, True),)),
     # C5: one of the 4096 independent n=128 replays (seed 5000+i)
     "c5": GenConfig("c5", 128, 128, 5000, 0.9, 0.1, 0.5, 4, 0.05),
 }
@@ -87,7 +96,28 @@ def generate(cfg: GenConfig, nthreads: int = 0) -> PackedDag:
                       view(lib.dr_gen_weak_tgt, np.uint32, nw))
     finally:
         lib.dr_gen_free(h)
-    return with_repeated_slots(d, cfg.p_dup, cfg.seed) if cfg.p_dup > 0 else d
+    if cfg.p_dup > 0:
+        d = with_repeated_slots(d, cfg.p_dup, cfg.seed)
+    return with_extra_edges(d, cfg.extra) if cfg.extra else d
+
+
+def with_extra_edges(d: PackedDag, extra) -> PackedDag:
+    """Append single edges to their vertices' weak_tgt lists: (r, s, tr, ts, strong) adds
+    (r, s) -> (tr, ts), a strong one with bit 31 set (include/dagrider_gpu.h,
+    dr_append_rounds_packed).  Each source must be present in its round."""
+    n = d.n
+    off = d.weak_off.astype(np.int64)
+    tgt = d.weak_tgt
+    at, val = [], []
+    for r, s, tr, ts, strong in sorted(extra):
+        g = r * n + s - 1
+        at.append(off[g + 1])
+        val.append((tr << 11) | (ts - 1) | ((1 << 31) if strong else 0))
+    tgt = np.insert(tgt, at, np.asarray(val, np.uint32)).astype(np.uint32)
+    add = np.zeros(len(off), np.int64)
+    for r, s, *_ in extra:
+        add[r * n + s:] += 1  # every offset after the vertex's own list start
+    return PackedDag(n, d.nrounds, d.slot_off, d.slot_src, d.strong, (off + add).astype(np.uint32), tgt)
 
 
 def with_repeated_slots(d: PackedDag, p_dup: float, seed: int) -> PackedDag:

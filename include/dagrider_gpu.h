@@ -131,9 +131,15 @@ int dr_replay_graph_state(const dr_ctx *ctx);
  * weak edges below r-1 are the round contract the reference's own vertices
  * keep; any other edge (uponDeliver checks only the
  * strong-edge count, process.go:165 -- a strong edge to another round, a weak
- * edge to round r-1 or above, even a cycle) is kept too, and while the mirror
- * holds one every query runs on the general sweep (general.hpp: exact for any
- * graph, slower; dr_set_weak_edges then returns DR_E_CONTRACT).  An id may
+ * edge to round r-1 or above, even a cycle) is kept too.  One that targets a
+ * lower round is an exception (as are weak edges past the memo window and far
+ * weak edges): the next query tests each new exception u -> v with one sweep
+ * (is v in u's cone without the exceptions? then the edge changes no cone) and
+ * the memoized path stays on while every one is (dr_exception_stats).  While
+ * the mirror holds an edge to the same or a later round, or an exception
+ * that changes a cone, every query runs on the general sweep (general.hpp:
+ * exact for any graph, slower; dr_set_weak_edges then returns
+ * DR_E_CONTRACT).  An id may
  * repeat within a round, as uponDeliver and the buffer loop let it
  * (process.go:158-169, :229): every slot is kept, path() sees the id's LAST
  * slot (:112-116), vCount and REF delivery count every slot (:332, :418-429),
@@ -148,7 +154,10 @@ int dr_append_rounds_lists(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off,
  *   slot_src [slot_off[k]] source per slot (0 = ghost)
  *   strong   [k*n*W]  row of (r0+i, s) at (i*n + s-1)*W, zero for absent s
  *   weak_off [k*n+1]  relative offsets into weak_tgt (weak_off[0] may be != 0)
- *   weak_tgt          (round << 11) | (source-1) */
+ *   weak_tgt          (round << 11) | (source-1): a weak edge; with bit 31 set, a
+ *                     strong edge outside the row's round r-1 (App. A Q8).  A weak
+ *                     edge to round r-1 or above is one too (dr_append_rounds_lists'
+ *                     contract). */
 int dr_append_rounds_packed(dr_ctx *ctx, int r0, int k, const uint32_t *slot_off,
                             const uint16_t *slot_src, const uint64_t *strong,
                             const uint32_t *weak_off, const uint32_t *weak_tgt);
@@ -326,6 +335,12 @@ int dr_replay_batch_view(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mo
  * dr_wave_commit / dr_wave_ready / dr_replay on this context (observability,
  * like dr_shard_stats; no reference counterpart). */
 int dr_last_kernel_ms(const dr_ctx *ctx, float *ms);
+/* The exception test's state (dr_append_rounds_lists): out[0] exceptions mirrored,
+ * out[1] of them found to change a cone at the last test, out[2] exception sweeps
+ * run so far, out[3] the regular weak window (largest delta kept in the memo's
+ * summaries), out[4] edges to the same or a later round, out[5] 1 while the
+ * memoized path serves queries (every exception tested and benign, none upward). */
+int dr_exception_stats(const dr_ctx *ctx, int64_t *out6);
 
 /* Host-side phases (ms, steady clock) of the last fused dr_replay_batch whose
  * first context is ctx: ms4[0] preparation before the launch (checks, job

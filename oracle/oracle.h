@@ -16,7 +16,7 @@
  *             `visited`, last-match linear id lookup per dequeue, one BFS per
  *             (leader, candidate) in orderVertices.  General graphs.
  *   bs_*   -- packed-bitset round sweeps (OpenMP over independent units).
- *             Contract DAGs only (strong edges to r-1, weak edges to < r-1).
+ *             Edges to lower rounds only (rows: strong edges to r-1; weak_tgt: the rest).
  * They are cross-checked on thousands of seeded DAGs (tests/test_oracle.py).
  */
 #ifndef DAGRIDER_ORACLE_H
@@ -50,6 +50,8 @@ typedef struct {
 /* Packed DAG: strong rows indexed by (round, source-1), W = ceil(n/64) u64
  * words, bit (t-1) <=> strong edge to (round-1, t).  weak CSR indexed by the
  * vertex index r*n + (s-1); each weak target packed (round << 11) | (source-1).
+ * With bit 31 set an entry is a strong edge to a round < r-1 (App. A Q8; the
+ * bitset restatement takes those and weak edges to r-1, no edge upward).
  * slot_src holds the source of each slot (0 = ghost slot, id {0,0}). */
 typedef struct {
   int32_t n, W, nrounds;

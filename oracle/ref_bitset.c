@@ -14,6 +14,10 @@
  *   orderVertices   process.go:404-443 -> forward strong+weak cone sweep per
  *                   pop, then (round asc, slot asc) emission
  * OpenMP parallelises over independent waves / chains / pops.
+ * Edges outside the round contract that target a lower
+ * round ride in weak_tgt: a weak edge to r-1, and with bit 31 set a strong edge
+ * to a round < r-1 (oracle.h).  Edges to the same or a later round are the
+ * literal restatement's alone.
  */
 #include "oracle.h"
 
@@ -32,6 +36,15 @@ static inline int present(const or_pdag *p, int r, int src) {
   return 0;
 }
 static inline int popc(uint64_t x) { return __builtin_popcountll(x); }
+/* weak_tgt entry: target round, and bit 31 = a strong edge outside the row (App. A Q8) */
+static inline int tgt_round(uint32_t t) { return (int)((t >> 11) & 0xFFFFFu); }
+static inline int tgt_strong(uint32_t t) { return (int)(t >> 31); }
+static int has_strong_extras(const or_pdag *p) {
+  const uint32_t ne = p->weak_off[(size_t)p->nrounds * p->n];
+  for (uint32_t e = p->weak_off[0]; e < ne; e++)
+    if (tgt_strong(p->weak_tgt[e])) return 1;
+  return 0;
+}
 
 /* Forward sweep from (top, src0) down to `bottom`.  masks: (top-bottom+1)*W
  * words, round r at (r-bottom)*W, caller-zeroed, bit src0 seeded by caller.
@@ -58,15 +71,14 @@ static uint64_t sweep(const or_pdag *p, int top, int bottom, int strong_only, ui
         if (s0 >= n) continue;
         const uint64_t *row = row_of(p, r, s0);
         for (int k = 0; k < W; k++) { N[k] |= row[k]; edges += (uint64_t)popc(row[k]); }
-        if (!strong_only) {
-          size_t g = (size_t)r * n + s0;
-          for (uint32_t e = p->weak_off[g]; e < p->weak_off[g + 1]; e++) {
-            uint32_t t = p->weak_tgt[e];
-            int tr = (int)(t >> 11), ts = (int)(t & 2047u);
-            edges++;
-            if (tr < bottom) continue;
-            masks[(size_t)(tr - bottom) * W + (ts >> 6)] |= 1ULL << (ts & 63);
-          }
+        size_t g = (size_t)r * n + s0;
+        for (uint32_t e = p->weak_off[g]; e < p->weak_off[g + 1]; e++) {
+          uint32_t t = p->weak_tgt[e];
+          if (strong_only && !tgt_strong(t)) continue;
+          int tr = tgt_round(t), ts = (int)(t & 2047u);
+          edges++;
+          if (tr < bottom) continue;
+          masks[(size_t)(tr - bottom) * W + (ts >> 6)] |= 1ULL << (ts & 63);
         }
       }
     }
@@ -116,12 +128,13 @@ static int commit_one(const or_pdag *p, int faulty, int w, uint8_t *commit, int3
   *edges = 0;
   const int L = or_leader(p->leader, p->nleader, w) - 1; /* chooseLeader(w), 0-based */
   if (!present(p, r1, L + 1)) { *commit = 0; *vcount = -1; return 0; }
-  uint64_t S[64], T[64]; /* W <= 32 */
+  /* S[k]: the ids of round r1+k with a strong path to the leader (W <= 32) */
+  uint64_t S[4][64];
   memset(S, 0, sizeof S);
-  S[L >> 6] = 1ULL << (L & 63);
+  S[0][L >> 6] = 1ULL << (L & 63);
   uint64_t seen[64];
   for (int r = r1 + 1; r <= r1 + 3; r++) {
-    memset(T, 0, sizeof T);
+    uint64_t *T = S[r - r1];
     memset(seen, 0, sizeof seen);
     for (uint32_t i = p->slot_off[r]; i < p->slot_off[r + 1]; i++) {
       int src = p->slot_src[i];
@@ -131,16 +144,23 @@ static int commit_one(const or_pdag *p, int faulty, int w, uint8_t *commit, int3
       seen[(src - 1) >> 6] |= bit;
       const uint64_t *row = row_of(p, r, src - 1);
       int hit = 0;
-      for (int k = 0; k < W; k++) { hit |= (row[k] & S[k]) != 0; *edges += (uint64_t)popc(row[k]); }
+      for (int k = 0; k < W; k++) { hit |= (row[k] & S[r - r1 - 1][k]) != 0; *edges += (uint64_t)popc(row[k]); }
+      const size_t g = (size_t)r * n + (src - 1);
+      for (uint32_t e = p->weak_off[g]; e < p->weak_off[g + 1]; e++) { /* strong edges skipping rounds */
+        const uint32_t t = p->weak_tgt[e];
+        if (!tgt_strong(t)) continue;
+        const int tr = tgt_round(t), ts = (int)(t & 2047u);
+        (*edges)++;
+        if (tr >= r1 && tr < r - 1) hit |= (int)((S[tr - r1][ts >> 6] >> (ts & 63)) & 1);
+      }
       if (hit) T[(src - 1) >> 6] |= bit;
     }
-    memcpy(S, T, sizeof S);
   }
-  (void)n;
+  const uint64_t *Sv = S[3];
   int vc = 0; /* every slot of round 4w whose id reaches the leader (process.go:331-336) */
   for (uint32_t i = p->slot_off[r1 + 3]; i < p->slot_off[r1 + 4]; i++) {
     int src = p->slot_src[i];
-    if (src != 0 && ((S[(src - 1) >> 6] >> ((src - 1) & 63)) & 1)) vc++;
+    if (src != 0 && ((Sv[(src - 1) >> 6] >> ((src - 1) & 63)) & 1)) vc++;
   }
   *vcount = vc;
   *commit = vc >= 2 * faulty + 1;
@@ -164,6 +184,55 @@ int or_bs_commit_sweep(const or_pdag *p, int faulty, int w0, int w1, uint8_t *co
 /* Leader chain of a commit at wave w (process.go:341-350): one forward strong
  * sweep from round 4w-3 down to round(floor+1, 1), restarting the frontier at
  * every leader it reaches.  Writes pushed waves (push order) to out. */
+/* The same with strong edges that skip rounds (extras): the frontier of every round
+ * below the current one is pending in M (rounds bottom..top); a restart drops it. */
+static int chain_one_x(const or_pdag *p, int w, int floor_w, int32_t *out, uint64_t *edges) {
+  const int W = p->W, n = p->n;
+  int top = 4 * (w - 1) + 1, bottom = 4 * floor_w + 1;
+  int np = 0;
+  out[np++] = w;
+  uint64_t *M = (uint64_t *)calloc((size_t)(top - bottom + 1) * W, sizeof(uint64_t));
+  const int L0 = or_leader(p->leader, p->nleader, w) - 1;
+  M[(size_t)(top - bottom) * W + (L0 >> 6)] = 1ULL << (L0 & 63);
+  uint64_t e = 0;
+  for (int r = top;; r--) {
+    uint64_t *F = M + (size_t)(r - bottom) * W;
+    if (r < top && ((r - 1) & 3) == 0) {
+      int w2 = (r - 1) / 4 + 1;
+      const int L2 = or_leader(p->leader, p->nleader, w2) - 1;
+      if (((F[L2 >> 6] >> (L2 & 63)) & 1) && present(p, r, L2 + 1)) {
+        out[np++] = w2;
+        memset(M, 0, (size_t)(r - bottom + 1) * W * sizeof(uint64_t));
+        F[L2 >> 6] = 1ULL << (L2 & 63);
+      }
+    }
+    if (r <= bottom) break;
+    uint64_t *N = F - W;
+    for (int k = 0; k < W; k++) {
+      uint64_t x = F[k];
+      while (x) {
+        int b = __builtin_ctzll(x);
+        x &= x - 1;
+        int s0 = k * 64 + b;
+        if (s0 >= n) continue;
+        const uint64_t *row = row_of(p, r, s0);
+        for (int j = 0; j < W; j++) { N[j] |= row[j]; e += (uint64_t)popc(row[j]); }
+        const size_t g = (size_t)r * n + s0;
+        for (uint32_t q = p->weak_off[g]; q < p->weak_off[g + 1]; q++) {
+          const uint32_t t = p->weak_tgt[q];
+          if (!tgt_strong(t)) continue;
+          const int tr = tgt_round(t), ts = (int)(t & 2047u);
+          e++;
+          if (tr >= bottom) M[(size_t)(tr - bottom) * W + (ts >> 6)] |= 1ULL << (ts & 63);
+        }
+      }
+    }
+  }
+  free(M);
+  *edges = e;
+  return np;
+}
+
 static int chain_one(const or_pdag *p, int w, int floor_w, int32_t *out, uint64_t *edges) {
   const int W = p->W, n = p->n;
   int top = 4 * (w - 1) + 1, bottom = 4 * floor_w + 1;
@@ -267,10 +336,11 @@ int or_bs_replay(const or_pdag *p, int faulty, int nwaves, int chain_mode, int d
   int32_t *pushbuf = (int32_t *)malloc((size_t)nc * (nwaves + 1) * sizeof(int32_t) + 4);
   int *npush = (int *)calloc((size_t)nc + 1, sizeof(int));
   uint64_t chain_e = 0;
+  const int sx = has_strong_extras(p);
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : chain_e)
   for (int c = 0; c < nc; c++) {
     uint64_t e = 0;
-    npush[c] = chain_one(p, cw[c], cfloor[c], pushbuf + (size_t)c * (nwaves + 1), &e);
+    npush[c] = (sx ? chain_one_x : chain_one)(p, cw[c], cfloor[c], pushbuf + (size_t)c * (nwaves + 1), &e);
     chain_e += e;
   }
   o->chain_edges = chain_e;

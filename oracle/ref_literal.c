@@ -359,7 +359,8 @@ int or_ldag_from_packed(const or_pdag *p, int nrounds, or_ldag *out) {
       const uint64_t *row = p->strong + ((size_t)r * p->n + (s - 1)) * p->W;
       for (int w = 0; w < p->W; w++) ns += (uint64_t)__builtin_popcountll(row[w]);
       size_t g = (size_t)r * p->n + (s - 1);
-      nw += p->weak_off[g + 1] - p->weak_off[g];
+      for (uint32_t k = p->weak_off[g]; k < p->weak_off[g + 1]; k++) /* bit 31: a strong edge off r-1 */
+        (p->weak_tgt[k] >> 31) ? ns++ : nw++;
     }
   so[nslots] = (uint32_t)ns;
   wo[nslots] = (uint32_t)nw;
@@ -385,9 +386,9 @@ int or_ldag_from_packed(const or_pdag *p, int nrounds, or_ldag *out) {
       uint32_t f = wo[i];
       for (uint32_t k = p->weak_off[g]; k < p->weak_off[g + 1]; k++) {
         uint32_t t = p->weak_tgt[k];
-        wid[f].round = (int32_t)(t >> 11);
-        wid[f].source = (int32_t)(t & 2047u) + 1;
-        f++;
+        or_vid *dst = (t >> 31) ? &sid[e++] : &wid[f++];
+        dst->round = (int32_t)((t >> 11) & 0xFFFFFu);
+        dst->source = (int32_t)(t & 2047u) + 1;
       }
     }
   out->nrounds = nrounds;

@@ -111,6 +111,41 @@ def test_literal_vs_bitset_random(seed):
                 assert lit.path(a, b, strong) == bs.path(a, b, strong)
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_literal_vs_bitset_extra_edges(seed):
+    """Edges below their round outside the row/column shape (strong
+    edges skipping rounds, weak edges to r-1; weak edges of any depth) ride in the packed
+    weak_tgt, bit 31 marking a strong one: the bitset restatement answers as the literal
+    BFS does on the same [][]vertex (or_ldag_from_packed)."""
+    from dag_rider_amd.gen import with_extra_edges
+
+    rng = np.random.default_rng(900 + seed)
+    n = int(rng.integers(1, 40))
+    R = int(rng.integers(6, 32))
+    base = random_dag(rng, n, R, p_present=rng.uniform(0.6, 1), p_s=rng.uniform(0.2, 0.9), p_w=rng.uniform(0, 0.6),
+                      max_depth=int(rng.integers(2, 10)))
+    extra = []
+    for _ in range(int(rng.integers(1, 8))):
+        r = int(rng.integers(2, R + 1))
+        srcs = [int(x) for x in base.slot_src[base.slot_off[r]:base.slot_off[r + 1]] if x]
+        if not srcs:
+            continue
+        strong = bool(rng.random() < 0.5)
+        tr = int(rng.integers(0, r - 1)) if strong else int(rng.integers(0, r))
+        extra.append((r, int(rng.choice(srcs)), tr, int(rng.integers(1, n + 1)), strong))
+    d = with_extra_edges(base, tuple(extra)) if extra else base
+    f = int(rng.integers(0, (n - 1) // 3 + 2))
+    lit, bs = oracle.LDag(packed=d), oracle.PDag(d)
+    for cm in (oracle.CHAIN_LITERAL, oracle.CHAIN_PERSISTENT):
+        for dm in (oracle.DELIVER_REF, oracle.DELIVER_PAPER):
+            _same(lit.replay(f, R // 4, cm, dm, ids_cap=1 << 16), bs.replay(f, R // 4, cm, dm, ids_cap=1 << 16))
+    ids = [(r, s) for r in range(R + 1) for s in range(1, n + 1)]
+    for strong in (0, 1):
+        for a in ids[::23]:
+            for b in ids[::11]:
+                assert lit.path(a, b, strong) == bs.path(a, b, strong)
+
+
 @pytest.mark.parametrize("seed", range(20))
 def test_literal_vs_bitset_generator(seed):
     rng = np.random.default_rng(100 + seed)
@@ -189,7 +224,7 @@ def test_large_golden_pins_generator_and_oracle():
     g = load_large()
     for name in ("c3", "c4"):
         cfg = dict(CONFIGS[name].__dict__)
-        assert cfg.pop("p_dup") == 0.0  # (a field added after the vectors were written)
+        assert cfg.pop("p_dup") == 0.0 and cfg.pop("extra") == ()  # (fields added after the vectors were written)
         assert g[name]["config"] == cfg
         assert len(g[name]["persistent_ref"]["pop_digest"]) == len(g[name]["persistent_ref"]["push_wave"])
     c5 = g["c5"]
