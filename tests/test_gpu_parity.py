@@ -204,10 +204,11 @@ def test_memo_on_off_large_n(gpu_device):
 @pytest.mark.parametrize("n,depth", [(1024, 64), (1024, 66), (1024, 80), (1024, 255), (1024, 256),
                                      (1100, 66), (1100, 127), (1100, 128), (300, 150)])
 def test_memo_window_boundary(gpu_device, n, depth):
-    """Weak deltas across the memo window (engine.hip kMemoMaxDelta = 255 and the sweeps'
-    LDS ring: 256 rounds at row stride 16 (n=1024), 128 at stride 32 (n=1100), so the memo
-    applies up to 255 / 127; past it the full sweeps run): every mode, memo and device plan
-    on and off, == the bitset oracle, and the memo path really ran where it applies."""
+    """Weak deltas across the regular window (engine.hip kMemoMaxDelta = 255 and the sweeps'
+    LDS ring: 256 rounds at row stride 16 (n=1024), 128 at stride 32 (n=1100), so the
+    summaries hold deltas up to 255 / 127; deeper weak edges are exceptions, tested once,
+    and the memo stays on while every one is benign -- here, every one): every mode, memo
+    and device plan on and off, == the bitset oracle, and the memo path really ran."""
     from dag_rider_amd.gen import small_config
 
     cfg = small_config(n, depth + 24, 40 + depth, p_present=0.97, p_late=0.02, p_w=0.05, weak_depth=depth,
@@ -231,7 +232,10 @@ def test_memo_window_boundary(gpu_device, n, depth):
                         _compare_replay(got, want, ids=False)
                         assert got.chain_edges == want.chain_edges
                         limit = 255 if n <= 1024 else 127
-                        assert (got.sweep["canon_segments"] >= 0) == (memo and depth <= limit), got.sweep
+                        st = e.exception_stats()
+                        assert (st["exceptions"] > 0) == (depth > limit) and st["regular_delta"] <= limit, st
+                        assert st["changing"] == 0, st
+                        assert (got.sweep["canon_segments"] >= 0) == memo, (got.sweep, st)
         e.set_memo(True)
         e.set_device_plan(True)
         stack = [(4 * w - 3, 1) for w in range(1, nw + 1)]
