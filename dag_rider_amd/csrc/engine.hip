@@ -196,6 +196,9 @@ struct dr_ctx {
   // the planned replay's leader chains on one register-resident wavefront each at n <= 256
   // (k_chain_reg; DR_CHAIN_REG=0: k_sweep's chain mode)
   int chain_reg = getenv("DR_CHAIN_REG") ? atoi(getenv("DR_CHAIN_REG")) : 1;
+  // k_canon_prefix over 16-round tiles with vector loads (DR_CANON_TILES=0: the per-thread
+  // run form of canon_prefix_block)
+  int canon_tiles = getenv("DR_CANON_TILES") ? atoi(getenv("DR_CANON_TILES")) : 1;
   int last_split = 0;    // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
   bool kprev_ok = false;
@@ -1806,7 +1809,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
                         c->rlo.as<int>()));  // the descriptor travels by value
   if (prefix)
     hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
-                       c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
+                       c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr, c->canon_tiles);
   HIPCHK(c, hipGetLastError());
   if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   c->kprev_ok = true;

@@ -799,56 +799,39 @@ __device__ __forceinline__ void canon_prefix_block(int T, const u64 *__restrict_
   }
 }
 
-// The same prefixes without rbase (A, B over rounds 0..T, round 0 counted as 0), thread
-// t owning CH consecutive rounds of each tile of NT * CH (16-B loads, every load of a
-// tile in flight at once), one scan of the threads' totals per tile.  C3's 10 001
-// rounds are one tile at NT = 1024 (canon_prefix_block: 17 us, lanes 80 B apart).
-template <int NT, int CH = 16>
-__device__ __forceinline__ void canon_prefix_tiles(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
+// The same prefixes without rbase (A, B over rounds 0..T, round 0 counted as 0).  Wave
+// w of a tile owns 64 K consecutive rounds, lane l rounds l, 64 + l, ...: every load and
+// store is coalesced and all 2 K loads of a lane are in flight at once.  The wave totals
+// go through LDS once per tile; each 64-round step is a wave scan plus the running carry.
+// C3's 10 001 rounds are one tile at NT = 1024 (canon_prefix_block: 18 us, lanes 80 B
+// apart; a thread-per-16-rounds tile form: 31 us, profiles/r05/).
+template <int NT, int K = 16>
+__device__ __forceinline__ void canon_prefix_waves(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                    u64 *__restrict__ A, u64 *__restrict__ B) {
-  constexpr int NW = NT / 64, TILE = NT * CH;
-  static_assert(CH % 2 == 0, "pairs of rounds per load");
+  constexpr int NW = NT / 64;
   __shared__ u64 part[2 * NW];
-  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, n = T + 1;
-  u64 cx = 0, cy = 0;
-  for (int t0 = 0; t0 < n; t0 += TILE) {
-    const int base = t0 + (int)threadIdx.x * CH;
-    u64 x[CH], y[CH];
+  u64 cx = 0, cy = 0;  // the tiles below
+  for (int t0 = 0; t0 < n; t0 += NT * K) {
+    const int wbase = t0 + wv * 64 * K + lane;
+    u64 x[K], y[K], sx = 0, sy = 0;
 #pragma unroll
-    for (int c = 0; c < CH; c += 2) {
-      const int r = base + c;
-      if (r + 1 < n) {
-        const u64x2 va = *reinterpret_cast<const u64x2 *>(a + r), vb = b ? *reinterpret_cast<const u64x2 *>(b + r) : u64x2{0, 0};
-        x[c] = va.x;
-        x[c + 1] = va.y;
-        y[c] = vb.x;
-        y[c + 1] = vb.y;
-      } else {
-        x[c] = r < n ? a[r] : 0ULL;
-        y[c] = (r < n && b) ? b[r] : 0ULL;
-        x[c + 1] = y[c + 1] = 0;
-      }
-      if (r == 0) x[0] = y[0] = 0;  // round 0 is never delivered
+    for (int k = 0; k < K; k++) {
+      const int r = wbase + 64 * k;
+      const bool in = r >= 1 && r < n;  // round 0 is never delivered
+      x[k] = in ? a[r] : 0ULL;
+      y[k] = (in && b) ? b[r] : 0ULL;
     }
 #pragma unroll
-    for (int c = 1; c < CH; c++) {
-      x[c] += x[c - 1];
-      y[c] += y[c - 1];
+    for (int k = 0; k < K; k++) {
+      sx += x[k];
+      sy += y[k];
     }
-    const u64 sx = x[CH - 1], sy = y[CH - 1];
-    u64 ix = sx, iy = sy;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const u64 tx = shfl_up64(ix, off), ty = shfl_up64(iy, off);
-      if (lane >= off) {
-        ix += tx;
-        iy += ty;
-      }
-    }
-    if (lane == 63) {
-      part[wv] = ix;
-      part[NW + wv] = iy;
+    sx = wave_sum(sx);
+    sy = wave_sum(sy);
+    if (lane == 0) {
+      part[wv] = sx;
+      part[NW + wv] = sy;
     }
     __syncthreads();
     u64 ox = cx, oy = cy, tx = 0, ty = 0;
@@ -863,14 +846,27 @@ __device__ __forceinline__ void canon_prefix_tiles(int T, const u64 *__restrict_
       ty += py;
     }
     __syncthreads();
-    ox += ix - sx;
-    oy += iy - sy;
 #pragma unroll
-    for (int c = 0; c < CH; c++)
-      if (base + c < n) {
-        A[base + c] = ox + x[c];
-        if (b) B[base + c] = oy + y[c];
+    for (int k = 0; k < K; k++) {  // K independent wave scans; only the carry chains them
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const u64 ux = shfl_up64(x[k], off), uy = shfl_up64(y[k], off);
+        if (lane >= off) {
+          x[k] += ux;
+          y[k] += uy;
+        }
       }
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const int r = wbase + 64 * k;
+      if (r < n) {
+        A[r] = ox + x[k];
+        if (b) B[r] = oy + y[k];
+      }
+      ox += __shfl(x[k], 63);
+      oy += __shfl(y[k], 63);
+    }
     cx += tx;
     cy += ty;
   }
@@ -2263,9 +2259,9 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
 template <int NT>
 __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                      u64 *__restrict__ A, u64 *__restrict__ B,
-                                                     uint32_t *__restrict__ rbase) {
-  if (rbase) canon_prefix_block<NT>(T, a, b, A, B, rbase);
-  else canon_prefix_tiles<NT>(T, a, b, A, B);
+                                                     uint32_t *__restrict__ rbase, int tiles = 1) {
+  if (rbase || !tiles) canon_prefix_block<NT>(T, a, b, A, B, rbase);
+  else canon_prefix_waves<NT>(T, a, b, A, B);
 }
 
 // Multi-segment copy between device memory and pinned (device-mapped) host
