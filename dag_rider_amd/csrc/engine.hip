@@ -196,9 +196,6 @@ struct dr_ctx {
   // the planned replay's leader chains on one register-resident wavefront each at n <= 256
   // (k_chain_reg; DR_CHAIN_REG=0: k_sweep's chain mode)
   int chain_reg = getenv("DR_CHAIN_REG") ? atoi(getenv("DR_CHAIN_REG")) : 1;
-  // k_canon_prefix over 16-round tiles with vector loads (DR_CANON_TILES=0: the per-thread
-  // run form of canon_prefix_block)
-  int canon_tiles = getenv("DR_CANON_TILES") ? atoi(getenv("DR_CANON_TILES")) : 1;
   int last_split = 0;    // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
   bool kprev_ok = false;
@@ -860,7 +857,9 @@ hipError_t launch_sc_shipped(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc
 }
 
 // rows + commit decisions (U, SD); the weak-edge unions (WU) come from the
-// weak-column keys alone (launch_weak_union), beside it or after it
+// weak-column keys alone (launch_weak_union), after it.  (Inside the row pass's
+// workgroups, one wave per round after the rows, they lengthened the pass by as much as
+// the separate launch took: C4 89 -> 105 us, profiles/r05/v7_*.)
 template <int WS>
 hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
   hipError_t e = launch_sc_shipped<WS>(c, T, nwc, cm, vc);
@@ -1043,7 +1042,9 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   for (hipEvent_t *e : {&c->ev_fork, &c->ev_join, &c->ev_start, &c->ev_wu})
     (void)hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice);
   for (hipEvent_t *e : {&c->ev_sync, &c->ev_sync2}) (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
-  const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64);
+  // (+ a lane's WS rows of slack: k_chain_reg reads each lane's WS rows whole, past n
+  // in the last round when WS does not divide n)
+  const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64) + (size_t)c->WS * c->WS * sizeof(u64);
   if (c->strong.ensure(rows) != hipSuccess ||
       c->present.ensure((size_t)max_rounds * c->WS * sizeof(u64)) != hipSuccess ||
       c->slot_off.ensure((size_t)(max_rounds + 1) * sizeof(uint32_t)) != hipSuccess ||
@@ -1809,7 +1810,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
                         c->rlo.as<int>()));  // the descriptor travels by value
   if (prefix)
     hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
-                       c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr, c->canon_tiles);
+                       c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
   HIPCHK(c, hipGetLastError());
   if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   c->kprev_ok = true;

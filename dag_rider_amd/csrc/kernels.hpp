@@ -799,79 +799,6 @@ __device__ __forceinline__ void canon_prefix_block(int T, const u64 *__restrict_
   }
 }
 
-// The same prefixes without rbase (A, B over rounds 0..T, round 0 counted as 0).  Wave
-// w of a tile owns 64 K consecutive rounds, lane l rounds l, 64 + l, ...: every load and
-// store is coalesced and all 2 K loads of a lane are in flight at once.  The wave totals
-// go through LDS once per tile; each 64-round step is a wave scan plus the running carry.
-// C3's 10 001 rounds are one tile at NT = 1024 (canon_prefix_block: 18 us, lanes 80 B
-// apart; a thread-per-16-rounds tile form: 31 us, profiles/r05/).
-template <int NT, int K = 16>
-__device__ __forceinline__ void canon_prefix_waves(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
-                                                   u64 *__restrict__ A, u64 *__restrict__ B) {
-  constexpr int NW = NT / 64;
-  __shared__ u64 part[2 * NW];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, n = T + 1;
-  u64 cx = 0, cy = 0;  // the tiles below
-  for (int t0 = 0; t0 < n; t0 += NT * K) {
-    const int wbase = t0 + wv * 64 * K + lane;
-    u64 x[K], y[K], sx = 0, sy = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const int r = wbase + 64 * k;
-      const bool in = r >= 1 && r < n;  // round 0 is never delivered
-      x[k] = in ? a[r] : 0ULL;
-      y[k] = (in && b) ? b[r] : 0ULL;
-    }
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      sx += x[k];
-      sy += y[k];
-    }
-    sx = wave_sum(sx);
-    sy = wave_sum(sy);
-    if (lane == 0) {
-      part[wv] = sx;
-      part[NW + wv] = sy;
-    }
-    __syncthreads();
-    u64 ox = cx, oy = cy, tx = 0, ty = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-      const u64 px = part[w], py = part[NW + w];
-      if (w < wv) {
-        ox += px;
-        oy += py;
-      }
-      tx += px;
-      ty += py;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; k++) {  // K independent wave scans; only the carry chains them
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const u64 ux = shfl_up64(x[k], off), uy = shfl_up64(y[k], off);
-        if (lane >= off) {
-          x[k] += ux;
-          y[k] += uy;
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const int r = wbase + 64 * k;
-      if (r < n) {
-        A[r] = ox + x[k];
-        if (b) B[r] = oy + y[k];
-      }
-      ox += __shfl(x[k], 63);
-      oy += __shfl(y[k], 63);
-    }
-    cx += tx;
-    cy += ty;
-  }
-}
-
 // plan[] slots (int32, device)
 enum : int { PL_NTASK = 0, PL_NQC = 1, PL_NPUSH = 2, PL_CAPERR = 3, PL_NQD = 4, PL_NDESC = 5, PL_N = 8 };
 // header written to host memory by k_plan_final (u64)
@@ -1346,26 +1273,49 @@ __global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *
   const int lane = threadIdx.x & 63, qi = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   if (qi >= *nq_dev) return;  // wave-uniform
   const SweepQuery q = qs[qi];
+  constexpr int PB = 64;  // pushes buffered per chain
+  __shared__ int32_t s_push[4][PB];
+  int32_t *pbuf = s_push[threadIdx.x >> 6];
   const int n = g.n, s0 = lane * WS, wd = s0 >> 6, sh = s0 & 63;  // a lane's WS sources share a word
-  const int lo = max(q.bottom, 0);
   u64 rows[PF][RW], P[PF][WS];
   uint32_t dg[PF][WS];
-  auto load = [&](u64 (&rw)[RW], u64 (&pw)[WS], uint32_t (&dd)[WS], int r) {
-    const u64 *src = g.strong + ((size_t)r * n + (size_t)min(s0, n - 1)) * WS;
+  int LD[PF];
+  // Every load unconditional and unmasked: branch-free loads whose values are not
+  // touched until their round lets the compiler count them (s_waitcnt vmcnt(k)) instead of
+  // draining the queue (vmcnt(0)) before each round -- conditional loads, a select right
+  // after each load and the wave leader read inside the loop had made every round a full
+  // memory latency (C3: 46 us for the longest chain, 36 rounds).  A lane past n reads row
+  // 0 and a source past n is never in F & P, so neither value is ever used.  The leader of
+  // the wave starting at round r travels with the round (every lane loads it: a wave-wide
+  // value must not come from a lane-divergent load).
+  const int s_safe = s0 < n ? s0 : 0;
+  auto load = [&](u64 (&rw)[RW], u64 (&pw)[WS], uint32_t (&dd)[WS], int &ld, int r) {
+    r = max(r, 0);
+    const u64 *src = g.strong + ((size_t)r * n + (size_t)s_safe) * WS;
+    if constexpr (RW % 2 == 0) {
+      typedef u64 u64v2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int i = 0; i < RW; i++) rw[i] = s0 + i / WS < n ? src[i] : 0ULL;
+      for (int i = 0; i < RW; i += 2) {
+        const u64v2 x = *reinterpret_cast<const u64v2 *>(src + i);
+        rw[i] = x.x;
+        rw[i + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < RW; i++) rw[i] = src[i];
+    }
 #pragma unroll
     for (int w = 0; w < WS; w++) pw[w] = g.present[(size_t)r * WS + w];
 #pragma unroll
-    for (int k = 0; k < WS; k++) dd[k] = s0 + k < n ? g.sdeg[(size_t)r * n + s0 + k] : 0u;
+    for (int k = 0; k < WS; k++) dd[k] = g.sdeg[(size_t)r * n + min(s_safe + k, n - 1)];
+    ld = g.lead[((r - 1) >> 2) + 1];  // (used only when r starts a wave)
   };
   u64 F[WS];
 #pragma unroll
   for (int w = 0; w < WS; w++) F[w] = (q.src0 >= 0 && w == (q.src0 >> 6)) ? 1ULL << (q.src0 & 63) : 0ULL;
   int r = q.top;
 #pragma unroll
-  for (int k = 0; k < PF; k++)
-    if (r - k >= lo) load(rows[k], P[k], dg[k], r - k);
+  for (int k = 0; k < PF; k++) load(rows[k], P[k], dg[k], LD[k], r - k);  // (rounds below lo: loaded, never used)
   int npush = 0, stop_r = q.bottom;
   u64 e = 0;
   bool ended = false;
@@ -1374,17 +1324,25 @@ __global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *
     for (int k = 0; k < PF; k++) {  // round r is in slot k
       // waveReady's chain: a reachable, present leader of wave wv is pushed and the
       // chain goes on from it alone (also at the bottom round, before the sweep stops)
-      if (r < q.top && ((r - 1) & 3) == 0) {
-        const int wv = (r - 1) / 4 + 1, L = g.lead[wv] - 1;
-        u64 fl = 0;
+      // (every loaded value is consumed every round, through selects: a value a branch
+      // may skip leaves its load's register in doubt, and the compiler then drains the
+      // whole queue before reusing it)
+      const int L = LD[k] - 1;
+      u64 fl = 0;
 #pragma unroll
-        for (int w = 0; w < WS; w++)
-          if (w == (L >> 6)) fl = F[w] & P[k][w];
+      for (int w = 0; w < WS; w++) fl = w == (L >> 6) ? F[w] & P[k][w] : fl;
+      if (r < q.top && ((r - 1) & 3) == 0) {
+        const int wv = (r - 1) / 4 + 1;
         if ((fl >> (L & 63)) & 1ULL) {
 #pragma unroll
           for (int w = 0; w < WS; w++) F[w] = w == (L >> 6) ? 1ULL << (L & 63) : 0ULL;
-          if (lane == 0) push_out[q.out_off + npush] = wv;
+          // pushes collect in LDS (no global store inside the loop: stores count in vmcnt
+          // too, and a conditional one defeats the compiler's count of the loads in flight)
+          if (lane == 0) pbuf[npush & (PB - 1)] = wv;
           npush++;
+          if ((npush & (PB - 1)) == 0) {  // (a chain of more than PB pushes: flush)
+            if (lane < PB) push_out[q.out_off + npush - PB + lane] = pbuf[lane];
+          }
         }
       }
       if (r <= q.bottom) {
@@ -1401,24 +1359,27 @@ __global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *
       }
       u64 fw = 0;
 #pragma unroll
-      for (int w = 0; w < WS; w++)
-        if (w == wd) fw = F[w] & P[k][w];
+      for (int w = 0; w < WS; w++) fw = w == wd ? F[w] & P[k][w] : fw;
       const uint32_t fe = (uint32_t)(fw >> sh);
       u64 acc[WS];
 #pragma unroll
       for (int w = 0; w < WS; w++) acc[w] = 0;
 #pragma unroll
-      for (int j = 0; j < WS; j++)
-        if ((fe >> j) & 1u) {
-          e += dg[k][j];
+      for (int j = 0; j < WS; j++) {
+        const u64 m = 0ULL - (u64)((fe >> j) & 1u);
+        e += dg[k][j] & (uint32_t)m;
 #pragma unroll
-          for (int w = 0; w < WS; w++) acc[w] |= rows[k][j * WS + w];
-        }
+        for (int w = 0; w < WS; w++) acc[w] |= rows[k][j * WS + w] & m;
+      }
 #pragma unroll
       for (int w = 0; w < WS; w++) F[w] = wave_or(acc[w]);
-      if (r - PF >= lo) load(rows[k], P[k], dg[k], r - PF);  // slot k is free: round r - PF
+      load(rows[k], P[k], dg[k], LD[k], r - PF);  // slot k is free: round r - PF
       --r;
     }
+  }
+  {
+    const int left = npush & (PB - 1);
+    if (lane < left) push_out[q.out_off + npush - left + lane] = pbuf[lane];
   }
   e = wave_sum(e);
   if (lane == 0) {
@@ -1704,23 +1665,13 @@ __global__ __launch_bounds__(NT) void k_set_weak(DagView g, int r0, int depth_lo
 // (every non-ghost slot, in slot order) delivered at positions from ppref[r-1]
 // = |P_1| + .. + |P_{r-1}|.  k_canon lowers *rlo to the lowest round where that
 // assumption fails; the canonical emission recomputes only rounds >= *rlo.
+// One round's WU_r and speculative digest RG[r] on one wavefront, in the wave's LDS
+// slice sW (dd x WS words).  No workgroup barrier.
 template <int WS>
-__global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, int dd, u64 *__restrict__ WU,
-                                                    const int32_t *__restrict__ rounds,
-                                                    const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
-                                                    const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG) {
-  extern __shared__ __attribute__((aligned(16))) u64 wu_lds[];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = blockIdx.x * (int)(blockDim.x >> 6) + wid;  // one wave per round
-  int r;
-  if (rounds) {
-    if (i >= nr) return;
-    r = rounds[i];
-  } else {
-    r = i + 1;
-  }
-  if (r > T) return;  // wave-uniform: this wave alone
-  u64 *sW = wu_lds + (size_t)wid * dd * WS;
+__device__ __forceinline__ void weak_union_round(const DagView &g, int r, int dd, u64 *__restrict__ WU, u64 *sW,
+                                                 const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
+                                                 const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG,
+                                                 int lane) {
   // 16-B LDS and HBM accesses when every row is 16-B aligned (WS even)
   typedef u64 u64v2 __attribute__((ext_vector_type(2)));
   if constexpr (WS % 2 == 0) {
@@ -1770,6 +1721,25 @@ __global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, in
   } else {
     for (int k = lane; k < dd * WS; k += 64) WU[(size_t)r * dd * WS + k] = sW[k];
   }
+}
+
+template <int WS>
+__global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, int dd, u64 *__restrict__ WU,
+                                                    const int32_t *__restrict__ rounds,
+                                                    const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
+                                                    const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG) {
+  extern __shared__ __attribute__((aligned(16))) u64 wu_lds[];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * (int)(blockDim.x >> 6) + wid;  // one wave per round
+  int r;
+  if (rounds) {
+    if (i >= nr) return;
+    r = rounds[i];
+  } else {
+    r = i + 1;
+  }
+  if (r > T) return;  // wave-uniform: this wave alone
+  weak_union_round<WS>(g, r, dd, WU, wu_lds + (size_t)wid * dd * WS, ppref, slot_off, slot_src, RG, lane);
 }
 
 // K^cand_r = U_{r+1} | OR_d WU_{r+d+2}[d] (the cone of round r when every round
@@ -2259,9 +2229,8 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
 template <int NT>
 __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                      u64 *__restrict__ A, u64 *__restrict__ B,
-                                                     uint32_t *__restrict__ rbase, int tiles = 1) {
-  if (rbase || !tiles) canon_prefix_block<NT>(T, a, b, A, B, rbase);
-  else canon_prefix_waves<NT>(T, a, b, A, B);
+                                                     uint32_t *__restrict__ rbase) {
+  canon_prefix_block<NT>(T, a, b, A, B, rbase);
 }
 
 // Multi-segment copy between device memory and pinned (device-mapped) host
