@@ -15,6 +15,8 @@ c4-deep64 (weak edges 64 deep: memoized at the window's far end), c4-loop (the d
 pattern: per wave append 4 rounds -> dr_wave_ready -> dr_order_vertices, per-wave
 latency), c4-far / c4-q8 (C4 + one weak edge 600 rounds deep / one strong edge to round
 r-3: exceptions to the regular graph, tested once and found benign, so the memo stays on),
+c4-up (C4 + one weak edge to its own round: the general sweep serves every query; no oracle
+takes such an edge at this size, the general sweep's parity is tests/test_gpu_irregular.py's),
 --deliver paper (dedup across pops).
 
 --gpus N without torchrun: spawns N ranks (torch.distributed.run) before anything
@@ -46,7 +48,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950
 # correction of MI355X_MICROARCH.md) on this bench: tools/pmc_traffic.py output
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r04", "r03")]
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r05", "r04", "r03")]
 
 
 def phase_kernels(phase: str, W: int = 16):
@@ -61,8 +63,10 @@ def phase_kernels(phase: str, W: int = 16):
         nt = 192 if W == 16 else min(blk, 512)
         return [[f"dr::k_sweep<{W}, {nt}, 9>", f"dr::k_own_emit<{W}, {256 if W <= 4 else 512}>",
                  "dr::k_replay_final<1024>"]]
-    if phase == "batch":  # the wave-per-DAG form (many DAGs per CU) or the workgroup form
-        return [["dr::k_replay_small_1w<false, true>"]] + [[f"dr::k_replay_small<{d}, false, true>"] for d in (4, 8, 16, 32)]
+    if phase == "batch_k_replay_small_1w":  # the wave-per-DAG form (many DAGs per CU)
+        return [["dr::k_replay_small_1w<false, true>"]]
+    if phase == "batch_k_replay_small":  # the workgroup form (a ring depth per launch)
+        return [[f"dr::k_replay_small<{d}, false, true>"] for d in (4, 8, 16, 32)]
     return []
 CPU_THREADS = 16  # the GPU box's host share for one GPU (OMP_NUM_THREADS there)
 
@@ -256,11 +260,12 @@ def same_replay(a, b) -> bool:
                                                                          b.deliver_edges))
 
 
-def kernel_bytes(cfg, d, res):
-    """Algorithmic bytes per launch of each replay phase."""
+def kernel_bytes(cfg, d, res, dreg=None):
+    """Algorithmic bytes per launch of each replay phase.  dreg: the engine's
+    regular weak window (the summaries' depth; deeper weak edges are exceptions, s3.5)."""
     n, W, T = cfg.n, (cfg.n + 63) // 64, d.nrounds - 1
     leaders = int((res.vcount >= 0).sum())
-    dd = max(0, weak_depth(d) - 1)
+    dd = max(0, (dreg if dreg else weak_depth(d)) - 1)
     sw = res.sweep
     return {
         # k_summary_commit: every strong row of rounds 1..T read once; U and SD written
@@ -289,8 +294,8 @@ def weak_columns(d):
         return 0
     r = g // n
     t = d.weak_tgt.astype(np.int64)
-    delta = r - (t >> 11)
-    near = delta <= 1023
+    delta = r - ((t >> 11) & 0xFFFFF)
+    near = (delta >= 2) & (delta <= 1023) & ((t >> 31) == 0)  # (bit 31 / delta < 2: App. A Q8 edges, no column)
     return int(len(np.unique((r[near] << 22) | (delta[near] << 11) | (t[near] & 2047))))
 
 
@@ -302,7 +307,9 @@ def weak_depth(d):
     g = np.repeat(np.arange(d.nrounds * n, dtype=np.int64), np.diff(d.weak_off.astype(np.int64)))
     if len(g) == 0:
         return 1
-    return int((g // n - (d.weak_tgt.astype(np.int64) >> 11)).max())
+    t = d.weak_tgt.astype(np.int64)
+    weak = (t >> 31) == 0  # (bit 31: a strong edge outside the rows)
+    return int((g[weak] // n - (t[weak] >> 11)).max()) if weak.any() else 1
 
 
 def rank_config(cfg, rank: int, world: int):
@@ -645,6 +652,14 @@ def run_c5(args, rank: int, world: int, local: int, dist):
     if not args.no_cpu and world == 1:
         cpu = cpu_c5(dags, args.deliver_mode, res) if not args.dags else None
     ach = dag_bytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+    form = b.form()  # the fused kernel that ran (AUTO: the wave form above 6 DAGs per CU)
+    # PMC traffic of this form at this batch size, when the traffic file holds it; the bound
+    # from the measured bytes' rate: >= 25 % of peak reads as HBM-bound, else latency-bound
+    tr_bytes = tr_file = None
+    if not args.dags or args.dags >= total:
+        tr_bytes, tr_file = measured_traffic("batch_" + form, 2, "c5")
+    tr_rate = tr_bytes / (kms / 1e3) / 1e9 if tr_bytes and kms > 0 else None
+    bound = "hbm" if max(ach, tr_rate or 0.0) >= 0.25 * HBM_PEAK_GBS else "latency"
     return {
         "metric": "DAG edges traversed/sec (commit+delivery)",
         "value": total_edges * args.steps / dt,
@@ -663,12 +678,14 @@ def run_c5(args, rank: int, world: int, local: int, dist):
                                f"{'paper' if args.deliver_mode else 'ref'}, persistent decidedWave), split across ranks",
                    "dags": total if not args.dags else hi - lo, "dags_per_rank": hi - lo, "n": 128, "rounds": 128, "waves": nw,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
-        "roofline": {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBS, "traffic": measured_traffic("batch", 2, "c5")[0] if total == 4096 and not args.dags else None,
-                     "traffic_unit": f"bytes/launch (rocprofv3 PMC, {measured_traffic('batch', 2, 'c5')[1]})",
-                     "kernel": "k_replay_small (batch.hpp)",
+        "roofline": {"bound": bound, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": ach / HBM_PEAK_GBS, "traffic": tr_bytes,
+                     "traffic_unit": f"bytes/launch (rocprofv3 PMC, {tr_file})",
+                     "traffic_rate_GBps": tr_rate,
+                     "kernel": f"{form} ({'batch1w.hpp' if form.endswith('1w') else 'batch.hpp'})",
                      "bytes_per_launch": dag_bytes, "ms_per_launch": kms,
-                     "note": "unique DAG bytes (strong rows + weak columns) once per launch"},
+                     "note": "unique DAG bytes (strong rows + weak columns) once per launch; bound from the "
+                             "larger of the algorithmic and the measured rate"},
         "cpu_baseline": cpu,
         "detail": {"edges_per_step": edges, "commits": int(sum(int(r.commit.sum()) for r in res)),
                    "pops": int(sum(len(r.pop_count) for r in res)),
@@ -743,6 +760,7 @@ def run_loop(args, local: int):
         e.append_packed(d, 0, 1)
         decided = 0
         lat = {"append": [], "wave_ready": [], "order_vertices": [], "wave": []}
+        aph = {k: [] for k in ("build", "stage_rows", "stage_rounds", "copy_wait")}
         commit, vcount, pushes, pc, pdg = [], [], [], [], []
         torch.cuda.synchronize()
         t_start = time.perf_counter()
@@ -750,6 +768,8 @@ def run_loop(args, local: int):
             t0 = time.perf_counter()
             e.append_packed(d, 4 * w - 3, 4 * w + 1)
             t1 = time.perf_counter()
+            for k, v in e.append_phases().items():
+                aph[k].append(v * 1e-3)
             cm, vc, pushed = e.wave_ready(w, decided)
             t2 = time.perf_counter()
             commit.append(cm)
@@ -767,6 +787,7 @@ def run_loop(args, local: int):
             lat["order_vertices"].append(t3 - t2)
             lat["wave"].append(t3 - t0)
         total = time.perf_counter() - t_start
+        lat.update({"append." + k: v for k, v in aph.items()})
         return total, lat, (np.asarray(commit, np.uint8), np.asarray(vcount, np.int32), pushes, pc, pdg)
 
     # warm-up pass (first-call costs), then the measured pass on a fresh mirror
@@ -861,7 +882,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4-deep", "c4-deep64", "c4-dups", "c5",
-                                                       "c4-loop", "c4-far", "c4-q8"])
+                                                       "c4-loop", "c4-far", "c4-q8", "c4-up"])
     ap.add_argument("--graph", action="store_true",
                     help="replay the captured hipGraph of the launch sequence (DR_OPT_REPLAY_GRAPH)")
     ap.add_argument("--no-memo", action="store_true",
@@ -1024,7 +1045,8 @@ def main() -> int:
             dist.destroy_process_group()
         return 0
 
-    kb = kernel_bytes(cfg, d, res)
+    exc = eng.exception_stats()
+    kb = kernel_bytes(cfg, d, res, exc["regular_delta"])
     # dominant kernel = the phase with the largest device time (HIP events)
     dom = max(kb, key=lambda k: kb[k]["ms"])
     ach = kb[dom]["bytes"] / (kb[dom]["ms"] / 1e3) / 1e9 if kb[dom]["ms"] > 0 else 0.0
@@ -1067,7 +1089,7 @@ def main() -> int:
                    "commits": int(res.commit.sum()), "pops": int(len(res.pop_count)),
                    "ms": res.ms, "ms_note": "summary: mean over the timed steps; other phases: one "
                    "profiling replay after them (DR_OPT_PHASE_TIMING=2)",
-                   "sweep": res.sweep, "verify_vs_oracle": verify, "exceptions": eng.exception_stats(),
+                   "sweep": res.sweep, "verify_vs_oracle": verify, "exceptions": exc,
                    "commit_split": split, "colshard": colshard[0] if colshard else None,
                    "kernels": {k: dict(v, GBps=(v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None))
                                for k, v in kb.items()}},

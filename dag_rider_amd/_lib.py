@@ -88,6 +88,8 @@ SIGNATURES = {
     "dr_last_kernel_ms": (C.c_int, [P, C.POINTER(f32)]),
     "dr_exception_stats": (C.c_int, [P, P]),
     "dr_last_batch_phases": (C.c_int, [P, C.POINTER(f32)]),
+    "dr_last_batch_form": (C.c_int, [P]),
+    "dr_last_append_phases": (C.c_int, [P, C.POINTER(f32)]),
     # include/dagrider_shard.h
     "dr_shard_unique_id": (C.c_int, [P]),
     "dr_shard_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.POINTER(P)]),

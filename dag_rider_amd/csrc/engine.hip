@@ -225,6 +225,8 @@ struct dr_ctx {
   hipGraphExec_t rg_exec = nullptr;
   int plan_mode = 1;        // DR_OPT_DEVICE_PLAN: dr_replay planned on the device when it applies
   int batch_form = DR_BATCH_AUTO;  // DR_OPT_BATCH_FORM (dr_replay_batch, first context)
+  int last_batch_form = 0;         // dr_last_batch_form: the fused form this context's last batch ran
+  float append_phases[4] = {};     // dr_last_append_phases: the last dr_append_rounds_packed (host ms)
   int cu_count = 0;         // compute units of the device (dr_replay_batch's form choice)
   float last_commit_ms = 0;  // dr_last_kernel_ms: the last commit-rule launch (HIP events)
   float batch_phases[4] = {};
@@ -1167,7 +1169,9 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   in.weak_off = weak_off;
   in.weak_tgt = weak_tgt;
   dr_host::BuiltRounds built;
+  const auto ta0 = std::chrono::steady_clock::now();
   if (int rc = dr_host::build_packed_rounds(in, c->dmax_near, built, c->err, c->build_scr)) return rc;
+  const auto ta1 = std::chrono::steady_clock::now();
   std::vector<HostRound> &nh = built.rounds;
   const size_t nfar = built.nfar;
   const int dmax = built.dmax;
@@ -1199,8 +1203,16 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   c->dmax_near = dmax;
   c->nrounds += k;
   for (int r = r0; r < r0 + k; r++) c->touch(r);
+  const auto ta2 = std::chrono::steady_clock::now();
   HIPCHK(c, c->upload_suffix());
+  const auto ta3 = std::chrono::steady_clock::now();
   HIPCHK(c, c->sync());
+  const auto ta4 = std::chrono::steady_clock::now();
+  auto ms = [](auto a, auto b) { return std::chrono::duration<float, std::milli>(b - a).count(); };
+  c->append_phases[0] = ms(ta0, ta1);  // validation + host rounds (weak columns)
+  c->append_phases[1] = ms(ta1, ta2);  // rows and degrees staged
+  c->append_phases[2] = ms(ta2, ta3);  // flattened per-round arrays staged
+  c->append_phases[3] = ms(ta3, ta4);  // one copy launch, wait for the device
   return DR_OK;
 }
 
@@ -2110,6 +2122,14 @@ extern "C" int dr_exception_stats(const dr_ctx *c, int64_t *out) {
 extern "C" int dr_last_kernel_ms(const dr_ctx *c, float *ms) {
   if (!c || !ms) return DR_E_INVAL;
   *ms = c->last_commit_ms;
+  return DR_OK;
+}
+
+extern "C" int dr_last_batch_form(const dr_ctx *c) { return c ? c->last_batch_form : DR_E_INVAL; }
+
+extern "C" int dr_last_append_phases(const dr_ctx *c, float *ms4) {
+  if (!c || !ms4) return DR_E_INVAL;
+  std::memcpy(ms4, c->append_phases, sizeof c->append_phases);
   return DR_OK;
 }
 
@@ -3818,6 +3838,7 @@ int replay_batch_impl(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode,
   }
   const bool wave_form = c0->batch_form == DR_BATCH_WAVE ||
                          (c0->batch_form == DR_BATCH_AUTO && nctx > 6 * c0->cu_count);
+  c0->last_batch_form = wave_form ? DR_BATCH_WAVE : DR_BATCH_WORKGROUP;
   HIPCHK(c0, wave_form ? launch_small_1w(c0, jt, nctx, nw, persistent, paper, P.dmax)
                        : launch_small(c0, jt, nctx, nw, persistent, paper, P.dmax));
   HIPCHK(c0, hipEventRecord(c0->ev[1], c0->stream));

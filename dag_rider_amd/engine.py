@@ -126,6 +126,12 @@ class Engine:
         self._check(self._L.dr_last_kernel_ms(self._h, C.byref(ms)))
         return ms.value
 
+    def append_phases(self) -> dict:
+        """dr_last_append_phases: host ms of the last packed append by phase."""
+        ms = (C.c_float * 4)()
+        self._check(self._L.dr_last_append_phases(self._h, ms))
+        return dict(build=ms[0], stage_rows=ms[1], stage_rounds=ms[2], copy_wait=ms[3])
+
     def exception_stats(self) -> dict:
         """dr_exception_stats: the exceptions to the regular graph and the test's verdict
         (include/dagrider_gpu.h)."""
@@ -408,6 +414,11 @@ class ReplayBatch:
         L.lib().dr_last_batch_phases(self.engines[0]._h, ms)
         return dict(host_prep=ms[0], launch_to_host=ms[1], copy_back=ms[2], unpack=ms[3])
 
+    def form(self) -> str:
+        """dr_last_batch_form of the last run: the fused kernel that ran ("" when none did)."""
+        f = L.lib().dr_last_batch_form(self.engines[0]._h)
+        return {L.DR_BATCH_WORKGROUP: "k_replay_small", L.DR_BATCH_WAVE: "k_replay_small_1w"}.get(f, "")
+
 
 class ReplayBatchView:
     """dr_replay_batch_view over a fixed list of engines: each call leaves every context's
@@ -453,6 +464,11 @@ class ReplayBatchView:
         ms = (C.c_float * 4)()
         L.lib().dr_last_batch_phases(self.engines[0]._h, ms)
         return dict(host_prep=ms[0], launch_to_host=ms[1], copy_back=ms[2], unpack=ms[3])
+
+    def form(self) -> str:
+        """dr_last_batch_form of the last run: the fused kernel that ran ("" when none did)."""
+        f = L.lib().dr_last_batch_form(self.engines[0]._h)
+        return {L.DR_BATCH_WORKGROUP: "k_replay_small", L.DR_BATCH_WAVE: "k_replay_small_1w"}.get(f, "")
 
 
 def replay_batch(engines: Sequence["Engine"], nwaves: int, chain_mode: int = L.DR_CHAIN_PERSISTENT,

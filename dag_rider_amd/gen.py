@@ -62,6 +62,9 @@ CONFIGS = {
     "c4-far": GenConfig("c4-far", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0, extra=((2002, 17, 1402, 5, False),)),
     # C4 + one strong edge to round r-3 (--config c4-q8)
     "c4-q8": GenConfig("c4-q8", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0, extra=((2001, 17, 1998, 5, True),)),
+    # C4 + one weak edge to its own round (App. A Q8, not below the source: no exception
+    # test applies): every query takes the general sweep (--config c4-up, k_gsweep at scale)
+    "c4-up": GenConfig("c4-up", 1024, 4000, 4, 1.0, 0.02, 0.5, 4, 0.0, extra=((2002, 17, 2002, 5, False),)),
     # C5: one of the 4096 independent n=128 replays (seed 5000+i)
     "c5": GenConfig("c5", 128, 128, 5000, 0.9, 0.1, 0.5, 4, 0.05),
 }

@@ -347,6 +347,14 @@ int dr_exception_stats(const dr_ctx *ctx, int64_t *out6);
  * table), [1] launch until the results are on the host, [2] the copy back
  * (device events), [3] unpacking into the callers' outputs (observability). */
 int dr_last_batch_phases(const dr_ctx *ctx, float *ms4);
+/* The fused form the last dr_replay_batch led by ctx ran: DR_BATCH_WORKGROUP
+ * (k_replay_small) or DR_BATCH_WAVE (k_replay_small_1w); 0 when its shapes took one
+ * dr_replay per context (or none ran yet). */
+int dr_last_batch_form(const dr_ctx *ctx);
+/* Host time of the last dr_append_rounds_packed (ms): ms4[0] validation and the rounds'
+ * host state (weak columns), [1] rows and degrees staged, [2] the flattened per-round
+ * arrays staged, [3] the copy launch and the wait for the device. */
+int dr_last_append_phases(const dr_ctx *ctx, float *ms4);
 
 #ifdef __cplusplus
 }
