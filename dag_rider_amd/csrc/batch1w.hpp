@@ -50,7 +50,6 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
   __shared__ u64 QL[64];
   __shared__ int32_t vc_s[64];
   __shared__ int16_t first_pop[64];
-  __shared__ int16_t qs_floor[64];  // lowest round where leader b's strong cone is still inspected
   __shared__ int8_t lst[64];
   __shared__ int8_t ord[64];        // PAPER: popped leaders in first-pop order
   const int lane = threadIdx.x;
@@ -96,57 +95,38 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
   };
   auto pres_word = [&](int r, int w) -> u64 { return w < WS ? g_present[(size_t)r * WS + w] : 0ULL; };
 
-  // ---------------- 1. commits ----------------
-  u64 commit_mask = 0, lead_mask = 0, commit_edges = 0;
-  for (int w = 1; w <= nw; w++) {
-    const int r1 = 4 * (w - 1) + 1;
-    const int l = g_lead[w] - 1;  // chooseLeader(w), 0-based (< 128)
-    const bool lead = (pres_word(r1, l >> 6) >> (l & 63)) & 1ULL;
-    if (!lead) {
-      if (lane == 0) vc_s[w - 1] = -1;
-      continue;
+  // ---------------- 1. leaders ----------------
+  // (the commit rule runs inside the cone pass below, on the rows it reads anyway: a
+  // separate pass had re-read three of every four rounds, profiles/r05/)
+  u64 commit_mask = 0, commit_edges = 0;
+  u64 lead_mask;
+  {
+    bool lp = false;
+    if (lane < nw) {
+      const int l = g_lead[lane + 1] - 1;  // chooseLeader(w), 0-based (< 128)
+      lp = (pres_word(4 * lane + 1, l >> 6) >> (l & 63)) & 1ULL;
     }
-    lead_mask |= 1ULL << (w - 1);
-    u64 a[3][2], b[3][2];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      row(r1 + 1 + k, lane, a[k][0], b[k][0]);
-      row(r1 + 1 + k, lane + 64, a[k][1], b[k][1]);
-    }
-    u64 s0 = l < 64 ? 1ULL << l : 0ULL, s1 = l >= 64 ? 1ULL << (l - 64) : 0ULL, deg = 0;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int r = r1 + 1 + k;
-      const u64 p0 = pres_word(r, 0), p1 = pres_word(r, 1);
-      const bool h0 = ((p0 >> lane) & 1ULL) && (((a[k][0] & s0) | (b[k][0] & s1)) != 0ULL);
-      const bool h1 = ((p1 >> lane) & 1ULL) && (((a[k][1] & s0) | (b[k][1] & s1)) != 0ULL);
-      s0 = __ballot(h0);
-      s1 = __ballot(h1);
-      deg += (u64)(__popcll(a[k][0]) + __popcll(b[k][0]) + __popcll(a[k][1]) + __popcll(b[k][1]));
-    }
-    commit_edges += wave_sum(deg);
-    const int vc = __popcll(s0) + __popcll(s1);
-    if (lane == 0) vc_s[w - 1] = vc;
-    if (vc >= q) commit_mask |= 1ULL << (w - 1);
+    lead_mask = __ballot(lp);
+    if (lane < nw && !lp) vc_s[lane] = -1;
   }
 
   // ---------------- 2. top-down cone pass (lane b: leader b's sets) ----------------
   for (int i = lane; i < rsl * 128; i += 64) ring[i] = 0;
   KW[lane] = 0;
-  // chains (process.go:341-350) inspect leader b's strong cone only down to the
-  // floor round of the commit whose chain can push b: 4*decidedWave + 1
-  qs_floor[lane] = 0x7fff;
   __syncthreads();
-  if (lane == 0) {
-    int lastc = 0;
-    for (int w = 1; w <= nw; w++)
-      if ((commit_mask >> (w - 1)) & 1ULL) {
-        for (int b = lastc + 1; b <= w; b++) qs_floor[b - 1] = (int16_t)(chain_persistent ? 4 * lastc + 1 : 1);
-        lastc = w;
-      }
+  // leader b's strong cone is followed to round 1 (the chains read its degree sums only
+  // from their floor up; the commits, which would set the floors, are decided in this pass)
+  const bool alive = lane < nw || (haveK && lane == 63);
+  // the commit rule (process.go:326-339) of the wave whose leader round is r: rows and
+  // presence of rounds r+1 .. r+3, kept from the iterations above (lanes v, v + 64)
+  u64 ha[3][2], hb[3][2], hp[3][2];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {  // rounds T+1 .. T+3 (the top wave's; the DAG holds 4 nw + 1 rounds)
+    row(T + 1 + k, lane, ha[k][0], hb[k][0]);
+    row(T + 1 + k, lane + 64, ha[k][1], hb[k][1]);
+    hp[k][0] = pres_word(T + 1 + k, 0);
+    hp[k][1] = pres_word(T + 1 + k, 1);
   }
-  __syncthreads();
-  const int my_floor = qs_floor[lane];
   u64 F0 = 0, F1 = 0;  // F_b: round-r vertices in leader b's cone
   u64 G0 = 0, G1 = 0;  // G_b: the same over strong edges only
   uint32_t suf = 0;    // strong degrees summed over G_b, rounds r..T
@@ -179,13 +159,44 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
   };
   prefetch2(T);
   for (int r = T; r >= 1; r--) {
-    const bool alive = (lane < nw && my_floor <= r) || (haveK && lane == 63);
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       ra[i] = nra[i];
       rb[i] = nrb[i];
       sd[i] = (uint32_t)(__popcll(ra[i]) + __popcll(rb[i]));
     }
+    if (((r - 1) & 3) == 0) {  // leader round of wave w: its vote from rounds r+1 .. r+3
+      const int w = (r - 1) / 4 + 1;
+      if ((lead_mask >> (w - 1)) & 1ULL) {
+        const int l = g_lead[w] - 1;
+        u64 s0 = l < 64 ? 1ULL << l : 0ULL, s1 = l >= 64 ? 1ULL << (l - 64) : 0ULL, deg = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const bool h0 = ((hp[k][0] >> lane) & 1ULL) && (((ha[k][0] & s0) | (hb[k][0] & s1)) != 0ULL);
+          const bool h1 = ((hp[k][1] >> lane) & 1ULL) && (((ha[k][1] & s0) | (hb[k][1] & s1)) != 0ULL);
+          s0 = __ballot(h0);
+          s1 = __ballot(h1);
+          deg += (u64)(__popcll(ha[k][0]) + __popcll(hb[k][0]) + __popcll(ha[k][1]) + __popcll(hb[k][1]));
+        }
+        commit_edges += wave_sum(deg);
+        const int vc = __popcll(s0) + __popcll(s1);
+        if (lane == 0) vc_s[w - 1] = vc;
+        if (vc >= q) commit_mask |= 1ULL << (w - 1);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {  // round r joins the history (r+1 .. r+3 for the next leader round)
+      ha[2][i] = ha[1][i];
+      hb[2][i] = hb[1][i];
+      hp[2][i] = hp[1][i];
+      ha[1][i] = ha[0][i];
+      hb[1][i] = hb[0][i];
+      hp[1][i] = hp[0][i];
+      ha[0][i] = ra[i];
+      hb[0][i] = rb[i];
+    }
+    hp[0][0] = pres_word(r, 0);
+    hp[0][1] = pres_word(r, 1);
     u64 cw0 = nw0, cw1 = nw1;
     uint32_t ckey = nkey;
     const uint32_t c0 = nc0, c1 = nc1;

@@ -190,9 +190,12 @@ struct dr_ctx {
   DevBuf split_ctl;
   size_t split_nw = 0;
   int split_cap = 0;  // CUs of this device (0: not read yet): ranges shorter than this split
-  // DR_OPT_COMMIT_SPLIT: off by default -- at C4's N = 8 share (125 waves) k_commit_split
-  // took 29 us against 22 us for k_commit, one workgroup per wave (profiles/r04/)
-  int commit_split = 0;
+  // DR_OPT_COMMIT_SPLIT: 2 (default) splits ranges of at most kSplitAuto waves -- the
+  // per-call waveReady's single wave: k_commit's one workgroup reads its three rounds
+  // alone (C4: 16 us, profiles/r05/v10_timeline_loop.txt); at C4's N = 8 share (125 waves)
+  // k_commit_split took 29 us against 22 us for k_commit (profiles/r04/); 1 = every range
+  // shorter than the CU count, 0 = never
+  int commit_split = 2;
   // the planned replay's leader chains on one register-resident wavefront each at n <= 256
   // (k_chain_reg; DR_CHAIN_REG=0: k_sweep's chain mode)
   int chain_reg = getenv("DR_CHAIN_REG") ? atoi(getenv("DR_CHAIN_REG")) : 1;
@@ -647,7 +650,7 @@ constexpr int sweep_block_m() {
 }
 
 // ---- kernel launch dispatch over the row stride ----
-constexpr int kSplitNT = 512, kSplitP3 = 2;
+constexpr int kSplitNT = 512, kSplitP3 = 2, kSplitAuto = 4;
 // A short wave range (fewer waves than CUs): KS workgroups per wave
 // (k_commit_split), each deciding S_1, S_2 in full and a share of S_3.  Returns
 // 1 when the range is long enough for one workgroup per wave (the caller
@@ -655,7 +658,7 @@ constexpr int kSplitNT = 512, kSplitP3 = 2;
 template <int WS>
 int launch_commit_split_t(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc, int *split) {
   *split = 0;
-  if (WS < 2 || !c->commit_split) return 1;
+  if (WS < 2 || !c->commit_split || (c->commit_split == 2 && nw > kSplitAuto)) return 1;
   if (c->split_cap == 0) {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev) != hipSuccess) return 1;
@@ -1992,7 +1995,8 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     return DR_OK;
   }
   if (option == DR_OPT_COMMIT_SPLIT) {
-    c->commit_split = value ? 1 : 0;
+    if (value < 0 || value > 2) return c->fail(DR_E_INVAL, "DR_OPT_COMMIT_SPLIT is 0, 1 or 2");
+    c->commit_split = value;
     return DR_OK;
   }
   if (option == DR_OPT_BATCH_FORM) {

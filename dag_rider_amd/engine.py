@@ -95,8 +95,9 @@ class Engine:
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_DEVICE_PLAN, int(on)))
 
     def set_commit_split(self, mode: int):
-        """DR_OPT_COMMIT_SPLIT: several workgroups per wave for short wave ranges (1; 0 = one
-        workgroup per wave, the default; identical results)."""
+        """DR_OPT_COMMIT_SPLIT: several workgroups per wave for short wave ranges (1: every range
+        shorter than the CU count, 2: ranges of at most 4 waves, the default; 0 = one workgroup
+        per wave; identical results)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_COMMIT_SPLIT, int(mode)))
 
     def set_replay_graph(self, on: bool):

@@ -100,10 +100,11 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * one workgroup of four wavefronts per DAG (shortest time per DAG),
  * DR_BATCH_WAVE = one wavefront per DAG (most DAGs per CU); AUTO takes the
  * wave form when the batch holds more than 6 DAGs per CU of the device.
- * DR_OPT_COMMIT_SPLIT (default 0): 1 = dr_wave_commit / dr_wave_ready on a
+ * DR_OPT_COMMIT_SPLIT (default 2): 1 = dr_wave_commit / dr_wave_ready on a
  * wave range shorter than the device's CU count split each wave's vote over
  * several workgroups (each computes S_1, S_2 whole and a share of S_3); 0 = one
- * workgroup per wave, the faster on MI355X at C4.  Identical
+ * workgroup per wave, the faster on MI355X at C4's 125-wave shares (DESIGN.md
+ * s7); 2 = split ranges of at most 4 waves (the per-call waveReady).  Identical
  * results.
  * DR_OPT_REPLAY_GRAPH (default 0): 1 = a device-planned dr_replay called again
  * with the same DAG version, options, wave count, modes and push capacity is

@@ -81,7 +81,7 @@ def test_commit_split_kernel(gpu_device, n):
             e.set_commit_split(0)
             want_c, want_v = e.wave_commit(1, nw)
             want1 = [e.wave_commit(w, w) for w in range(1, nw + 1)]
-            for mode in (1,):  # several workgroups per wave
+            for mode in (1, 2):  # several workgroups per wave: every short range / ranges of <= 4 waves
                 e.set_commit_split(mode)
                 for w0, w1 in ((1, nw), (1, 1), (3, 9), (nw - 4, nw), (2, nw - 1)):
                     for _ in range(2):  # the kernel leaves its arrival counters zero for the next launch
