@@ -946,7 +946,8 @@ hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo, bool spec) {
   const dr::MemoView mv = c->memo_view();
   hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
                      c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>(), c->rlo.as<int>(),
-                     spec ? T + 1 : lo);
+                     spec ? T + 1 : lo, spec ? c->ppref.as<u64>() : nullptr, c->Cc.as<u64>(),
+                     c->crbase.as<uint32_t>());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int dl = c->depth_log2();
@@ -1654,7 +1655,7 @@ int ensure_summary_bufs(dr_ctx *c) {
   HIPCHK(c, c->WU.ensure(std::max<size_t>(R * dd * WS, 1) * 8));
   HIPCHK(c, c->SD.ensure(R * 8));
   HIPCHK(c, c->K.ensure(R * WS * 8));
-  HIPCHK(c, c->good.ensure(R + 8));  // k_canon reads good[] 8 rounds at a time
+  HIPCHK(c, c->good.ensure(R + 64));  // k_canon reads good[] 64 rounds at a time
   HIPCHK(c, c->CE.ensure(R * 8));
   HIPCHK(c, c->RD.ensure(R * 8));
   HIPCHK(c, c->Kprev.ensure(R * WS * 8));

@@ -1751,7 +1751,9 @@ __global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, in
 template <int WS>
 __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K,
                                                uint8_t *__restrict__ good, u64 *__restrict__ CE,
-                                               u64 *__restrict__ RD, int *__restrict__ rlo, int lo) {
+                                               u64 *__restrict__ RD, int *__restrict__ rlo, int lo,
+                                               const u64 *__restrict__ ppref, u64 *__restrict__ Cc,
+                                               uint32_t *__restrict__ crbase) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
   if (rlo && blockIdx.x == 0 && threadIdx.x == 0) *rlo = lo;  // k_canon_diff / k_canon lower it
   if (r > T) return;  // wave-uniform
@@ -1787,6 +1789,11 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
     good[r] = ok;
     CE[r] = r == 0 ? 0 : mv.SD[r] + (g.weak_roff[r + 1] - g.weak_roff[r]);
     RD[r] = r == 0 ? 0 : (u64)cnt;
+  }
+  if (ppref && w == 1) {  // a full cone: positions default to the presence prefix (k_canon
+    // rewrites the rounds from its lowest walked round up)
+    Cc[r] = ppref[r];
+    crbase[r] = r >= 1 ? (uint32_t)ppref[r - 1] : 0u;
   }
 }
 
@@ -1834,21 +1841,33 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
   int lo_w = T + 1;  // the lowest round a segment walk reached (RD below it is the full count)
   DR_TT(int walked = 0; if (tid == 0) { g_canon_timing[0] = wall_clock64(); g_canon_timing[5] = 0; })
   while (true) {
-    // next bad round below pos: thread t looks at the 8 rounds of block (pos-1)/8 - t - i*NT
+    // next bad round below pos: thread t looks at the 64 rounds of block (pos-1)/64 - t -
+    // i*NT (four 16-B loads of good[], one pass over C3's 10 001 rounds; 8 rounds a
+    // thread took five dependent passes there)
     if (tid == 0) s_ctl[0] = -1;
     __syncthreads();
-    for (int b0 = (pos - 1) >> 3; b0 >= 0; b0 -= NT) {
+    for (int b0 = (pos - 1) >> 6; b0 >= 0; b0 -= NT) {
       const int b = b0 - tid;
       if (b >= 0) {
-        const u64 v = *reinterpret_cast<const u64 *>(good + 8 * (size_t)b);
+        typedef u64 u64v2 __attribute__((ext_vector_type(2)));
+        const u64v2 *gp = reinterpret_cast<const u64v2 *>(good + 64 * (size_t)b);
+        u64 v[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const u64v2 x = gp[k];
+          v[2 * k] = x.x;
+          v[2 * k + 1] = x.y;
+        }
+        int hit = -1;  // the highest round x < pos of the block with good[x] == 0
 #pragma unroll
         for (int k = 7; k >= 0; k--) {
-          const int x = 8 * b + k;
-          if (x < pos && !((v >> (8 * k)) & 0xffULL)) {
-            atomicMax(&s_ctl[0], x);
-            break;
-          }
+          const int x0 = 64 * b + 8 * k;  // rounds x0 .. x0+7, one byte (0 or 1) each
+          u64 m = ~v[k] & 0x0101010101010101ULL;  // bit 8j: round x0 + j is bad
+          const int lim = pos - x0;              // rounds below pos only
+          if (lim < 8) m &= lim <= 0 ? 0ULL : (1ULL << (8 * lim)) - 1ULL;
+          if (hit < 0 && m) hit = x0 + (63 - __clzll(m)) / 8;
         }
+        if (hit >= 0) atomicMax(&s_ctl[0], hit);
       }
       __syncthreads();
       if (s_ctl[0] >= 0) break;
@@ -1967,12 +1986,7 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
   // copied; the scan covers the walked region only (C4, C3: the top ~10 rounds).
   __syncthreads();
   __shared__ u64 part[NT / 64];
-  const int B = ppref ? lo_w : 0;
-#pragma unroll 8
-  for (int x = tid; x < B; x += NT) {
-    Cc[x] = ppref[x];
-    crbase[x] = x >= 1 ? (uint32_t)ppref[x - 1] : 0u;
-  }
+  const int B = ppref ? lo_w : 0;  // (rounds below B: k_kcand wrote the presence prefix)
   const u64 base0 = (ppref && B >= 1) ? ppref[B - 1] : 0ULL;
   const int per = (T + 1 - B + NT - 1) / NT;
   const int ra = B + tid * per, rb = min(T + 1, ra + per);
