@@ -1826,7 +1826,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
                         c->rlo.as<int>()));  // the descriptor travels by value
   if (prefix)
     hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
-                       c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), (uint32_t *)nullptr);
+                       c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>());
   HIPCHK(c, hipGetLastError());
   if (fork && !side) HIPCHK(c, hipEventRecord(c->ev_join, c->stream));  // c->stream is stream2 here
   c->kprev_ok = true;

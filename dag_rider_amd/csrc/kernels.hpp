@@ -2240,11 +2240,67 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
 // Inclusive prefix over rounds 0..T of up to three per-round arrays (one
 // workgroup; rounds >= 1 only).  With rbase != nullptr, also the exclusive
 // prefix of a (positions of round r's first canonical vertex).
+// The same prefixes without rbase (A, B over rounds 0..T, round 0 counted as 0) through
+// LDS: tiles of NT * PT rounds loaded and stored lane-consecutively (coalesced), each
+// thread scanning PT contiguous rounds out of LDS, one block scan per tile and array.
+// C3's 10 001 rounds: 16.9 us against 18.8 us for canon_prefix_block, whose lanes read
+// and write 80 B apart (profiles/r05/v10_prefix_bench.txt; a single-CU pass either way).
+template <int NT, int PT = 4>
+__device__ __forceinline__ void canon_prefix_lds(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                 u64 *__restrict__ A, u64 *__restrict__ B) {
+  constexpr int TILE = NT * PT;
+  __shared__ u64 sa[TILE], sb[TILE];
+  __shared__ u64 part[NT / 64];
+  const int tid = threadIdx.x, n = T + 1;
+  u64 ca = 0, cb = 0;
+  for (int t0 = 0; t0 < n; t0 += TILE) {
+#pragma unroll
+    for (int j = 0; j < PT; j++) {
+      const int r = t0 + j * NT + tid;
+      const bool in = r >= 1 && r < n;  // round 0 is never delivered
+      const int rc = in ? r : 0;
+      const u64 x = a[rc], y = b[rc];
+      sa[j * NT + tid] = in ? x : 0ULL;
+      sb[j * NT + tid] = in ? y : 0ULL;
+    }
+    __syncthreads();
+    u64 xa[PT], xb[PT], la = 0, lb = 0;
+#pragma unroll
+    for (int j = 0; j < PT; j++) {
+      xa[j] = sa[tid * PT + j];
+      xb[j] = sb[tid * PT + j];
+      la += xa[j];
+      lb += xb[j];
+    }
+    u64 ta, tb;
+    u64 ea = ca + block_scan_excl<NT>(la, part, ta);
+    u64 eb = cb + block_scan_excl<NT>(lb, part, tb);
+#pragma unroll
+    for (int j = 0; j < PT; j++) {
+      ea += xa[j];
+      eb += xb[j];
+      sa[tid * PT + j] = ea;
+      sb[tid * PT + j] = eb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PT; j++) {
+      const int r = t0 + j * NT + tid;
+      if (r < n) {
+        A[r] = sa[j * NT + tid];
+        B[r] = sb[j * NT + tid];
+      }
+    }
+    ca += ta;
+    cb += tb;
+    __syncthreads();
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
-                                                     u64 *__restrict__ A, u64 *__restrict__ B,
-                                                     uint32_t *__restrict__ rbase) {
-  canon_prefix_block<NT>(T, a, b, A, B, rbase);
+                                                     u64 *__restrict__ A, u64 *__restrict__ B) {
+  canon_prefix_lds<NT>(T, a, b, A, B);
 }
 
 // Multi-segment copy between device memory and pinned (device-mapped) host
