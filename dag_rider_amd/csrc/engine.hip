@@ -146,6 +146,7 @@ struct dr_ctx {
   std::vector<int32_t> h_rdreg, h_rexc, h_rup, h_rbad;
   std::vector<uint32_t> h_sdx;  // [round] strong edges outside the rows (DagView::sdx)
   DevBuf sdx;
+  bool sdx_valid = false;       // the device copy holds every mirrored round's h_sdx
   int dreg = 1;            // largest regular weak delta (1: none)
   int64_t nexc = 0, nirr_up = 0, nirr_down = 0, nbad = 0;
   int exc_lo = 0;          // lowest round touched since the last exception test
@@ -314,7 +315,9 @@ struct dr_ctx {
     h2q.clear();
     return e;
   }
+  bool async_pending = false;  // an append returned before its copies ran (dr_replay_batch waits)
   hipError_t sync() {
+    async_pending = false;
     hipError_t e = flush_h2d();
     if (e == hipSuccess && !pend.empty()) {
       std::vector<dr::CopySeg> small;
@@ -502,20 +505,34 @@ struct dr_ctx {
       h_irr_roff[r + 1] = h_irr_roff[r] + (uint32_t)h.irr.size();
       h_weak_roff[r + 1] = h_weak_roff[r] + (uint32_t)h.nweak;
     }
-    h_rdreg.resize(R, 1);
-    h_rexc.resize(R, 0);
-    h_rup.resize(R, 0);
-    h_rbad.resize(R, 0);
-    h_sdx.resize(R, 0);
-    for (int r = lo; r < R; r++) round_exceptions(r);
-    dreg = 1;
-    nexc = nirr_up = 0;
-    for (int r = 0; r < R; r++) {
-      dreg = std::max(dreg, h_rdreg[r]);
-      nexc += h_rexc[r];
-      nirr_up += h_rup[r];
+    {  // the exception counters of rounds [lo, R), the totals updated in place (an append at
+       // the top touches only its rounds; the largest regular delta is recomputed whole only
+       // when a round that held it changed)
+      const int Rold = (int)h_rexc.size();
+      bool dreg_drop = false;
+      for (int r = lo; r < std::min(Rold, R); r++) {
+        nexc -= h_rexc[r];
+        nirr_up -= h_rup[r];
+        dreg_drop |= h_rdreg[r] == dreg;
+      }
+      h_rdreg.resize(R, 1);
+      h_rexc.resize(R, 0);
+      h_rup.resize(R, 0);
+      h_rbad.resize(R, 0);
+      h_sdx.resize(R, 0);
+      for (int r = lo; r < R; r++) {
+        round_exceptions(r);
+        nexc += h_rexc[r];
+        nirr_up += h_rup[r];
+      }
+      if (dreg_drop) {
+        dreg = 1;
+        for (int r = 0; r < R; r++) dreg = std::max(dreg, h_rdreg[r]);
+      } else {
+        for (int r = lo; r < R; r++) dreg = std::max(dreg, h_rdreg[r]);
+      }
+      nirr_down = nirr - nirr_up;
     }
-    nirr_down = nirr - nirr_up;
     const size_t s0 = h_slot_off[lo], s1 = h_slot_off[R], k0 = h_wc_roff[lo], k1 = h_wc_roff[R];
     const size_t f0 = h_far_roff[lo], f1 = h_far_roff[R];
     // repeated ids: the slots after the first of their id, per round (rounds >= 1)
@@ -591,9 +608,13 @@ struct dr_ctx {
     if ((e = h2d(weak_roff.as<uint32_t>() + lo + 1, &h_weak_roff[lo + 1], nr * 4)) != hipSuccess) return e;
     if ((e = h2d(present.as<u64>() + (size_t)lo * WS, &h_present[(size_t)lo * WS], nr * WS * 8)) != hipSuccess)
       return e;
-    if (nirr > 0) {
+    if (nirr > 0) {  // the rounds from lo, or every round when the device copy is not current
       if ((e = sdx.ensure(((size_t)max_rounds + 1) * 4)) != hipSuccess) return e;
-      if ((e = h2d(sdx.as<uint32_t>(), h_sdx.data(), (size_t)R * 4)) != hipSuccess) return e;  // every round: small
+      const int x0 = sdx_valid ? lo : 0;
+      if ((e = h2d(sdx.as<uint32_t>() + x0, h_sdx.data() + x0, (size_t)(R - x0) * 4)) != hipSuccess) return e;
+      sdx_valid = true;
+    } else {
+      sdx_valid = false;
     }
     up_lo = R;
     return hipSuccess;
@@ -1182,7 +1203,8 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   // ---- commit: rows and per-vertex degrees, then the flattened per-round arrays ----
   DeferH2D batch(c);  // every staged copy below goes out in one launch at sync()
   const size_t row_words = (size_t)n * WS;
-  if (WS == W && (size_t)k * row_words * 8 <= ((size_t)16 << 20)) {  // per-round appends: pinned staging
+  const bool staged = WS == W && (size_t)k * row_words * 8 <= ((size_t)16 << 20);
+  if (staged) {  // per-round appends: pinned staging
     HIPCHK(c, c->h2d(c->strong.as<u64>() + (size_t)r0 * row_words, strong, (size_t)k * row_words * 8));
   } else if (WS == W) {  // bulk loads: straight from the caller's memory
     HIPCHK(c, hipMemcpyAsync(c->strong.as<u64>() + (size_t)r0 * row_words, strong,
@@ -1210,13 +1232,18 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   const auto ta2 = std::chrono::steady_clock::now();
   HIPCHK(c, c->upload_suffix());
   const auto ta3 = std::chrono::steady_clock::now();
-  HIPCHK(c, c->sync());
+  // one copy launch for everything staged, no wait: every later call of this context runs
+  // behind it on the same stream, the caller's arrays were copied into pinned staging
+  // memory (kept until the next wait), and a copy error surfaces at the next call.  (A bulk
+  // load's rows went straight from the caller's memory: wait for them.)
+  HIPCHK(c, staged ? c->flush_h2d() : c->sync());
+  c->async_pending = staged;
   const auto ta4 = std::chrono::steady_clock::now();
   auto ms = [](auto a, auto b) { return std::chrono::duration<float, std::milli>(b - a).count(); };
   c->append_phases[0] = ms(ta0, ta1);  // validation + host rounds (weak columns)
   c->append_phases[1] = ms(ta1, ta2);  // rows and degrees staged
   c->append_phases[2] = ms(ta2, ta3);  // flattened per-round arrays staged
-  c->append_phases[3] = ms(ta3, ta4);  // one copy launch, wait for the device
+  c->append_phases[3] = ms(ta3, ta4);  // one copy launch (no wait)
   return DR_OK;
 }
 
@@ -3706,6 +3733,13 @@ int replay_batch_impl(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode,
   for (int i = 0; i < nctx; i++)
     if (!ctxs[i]) return DR_E_INVAL;
   dr_ctx *c0 = ctxs[0];
+  // the fused launch reads every member's mirror on the first context's stream: appends
+  // still in flight on a member's own stream finish first
+  for (int i = 0; i < nctx; i++)
+    if (ctxs[i]->async_pending) {
+      if (int rc = set_device(ctxs[i])) return rc;
+      HIPCHK(ctxs[i], ctxs[i]->sync());
+    }
   const auto h0 = std::chrono::steady_clock::now();
   // each output's caller-set fields, commit .. ids_cap
   constexpr size_t kKey = offsetof(dr_replay_out, n_push);

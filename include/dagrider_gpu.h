@@ -354,7 +354,8 @@ int dr_last_batch_phases(const dr_ctx *ctx, float *ms4);
 int dr_last_batch_form(const dr_ctx *ctx);
 /* Host time of the last dr_append_rounds_packed (ms): ms4[0] validation and the rounds'
  * host state (weak columns), [1] rows and degrees staged, [2] the flattened per-round
- * arrays staged, [3] the copy launch and the wait for the device. */
+ * arrays staged, [3] the copy launch (the call does not wait for the device: later
+ * calls of the context run behind the copy on its stream). */
 int dr_last_append_phases(const dr_ctx *ctx, float *ms4);
 
 #ifdef __cplusplus
