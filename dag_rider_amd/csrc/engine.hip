@@ -158,6 +158,16 @@ struct dr_ctx {
     return cap;
   }
   int reg_max() const { return std::min(kMemoMaxDelta, depth_cap() - 1); }
+  // the lowest round holding an edge to the same or a later round (INT_MAX: none): a
+  // general sweep toward a target in round t never needs the rounds below t unless some
+  // path climbs back from there, which only such an edge below t allows
+  int min_up_round() const {
+    if (nirr_up == 0) return INT_MAX;
+    for (int r = 0; r < (int)h_rup.size(); r++)
+      if (h_rup[r]) return r;
+    return INT_MAX;
+  }
+  int gsweep_bottom(int t) const { return (t >= 0 && min_up_round() >= t) ? t : 0; }
   // every exception known benign (the last test covers every round)
   bool exc_clear() const { return nexc == 0 || (exc_lo >= nrounds && nbad == 0); }
   bool general() const { return nirr_up > 0 || (nirr_down > 0 && !exc_clear()); }
@@ -1707,8 +1717,9 @@ void mark_rounds_clean(dr_ctx *c) {
 // Incremental round summaries (U, SD, WU) of the rounds appended or changed
 // since they were last built: one workgroup per stale round.  A DAG that left
 // the memo contract (far weak edges, deltas > 65) keeps none.
-int refresh_rounds(dr_ctx *c) {
-  if (!c->use_memo || !c->memo_struct_ok()) return DR_OK;  // G_reg's summaries: exceptions tested or not
+int refresh_rounds(dr_ctx *c, bool any = false) {
+  // G_reg's summaries, exceptions tested or not (any: also with edges upward, for k_gsweep)
+  if (!c->use_memo || (!any && !c->memo_struct_ok())) return DR_OK;
   const int T = c->nrounds - 1;
   if (T < 1) return DR_OK;
   const int dd = c->memo_dd();
@@ -2187,9 +2198,9 @@ namespace {
 
 template <int WS>
 hipError_t launch_gsweep_t(dr_ctx *c, const dr::GQuery *q, int nq, int Tg, u64 *masks, u64 *scratch, uint8_t *hit,
-                           u64 *edges) {
+                           u64 *edges, const u64 *U) {
   hipLaunchKernelGGL((dr::k_gsweep<WS>), dim3(nq), dim3(256), 0, c->stream, c->view(), c->gview(), q, nq, Tg,
-                     c->nrounds, masks, scratch, hit, edges);
+                     c->nrounds, masks, scratch, hit, edges, U);
   return hipGetLastError();
 }
 template <int WS>
@@ -2215,8 +2226,9 @@ hipError_t launch_gpaper_t(dr_ctx *c, const int64_t *moff, const int32_t *last, 
     case 32: { constexpr int WS_ = 32; return call; } \
   }                                                   \
   return hipErrorInvalidValue
-hipError_t launch_gsweep(dr_ctx *c, const dr::GQuery *q, int nq, int Tg, u64 *m, u64 *s, uint8_t *h, u64 *ed) {
-  DR_WS_SWITCH(c, launch_gsweep_t<WS_>(c, q, nq, Tg, m, s, h, ed));
+hipError_t launch_gsweep(dr_ctx *c, const dr::GQuery *q, int nq, int Tg, u64 *m, u64 *s, uint8_t *h, u64 *ed,
+                         const u64 *U) {
+  DR_WS_SWITCH(c, launch_gsweep_t<WS_>(c, q, nq, Tg, m, s, h, ed, U));
 }
 hipError_t launch_gdeg(dr_ctx *c, const int64_t *moff, const int32_t *first, const int32_t *last, int np, int weak,
                        u64 *out) {
@@ -2241,6 +2253,13 @@ int run_gsweeps(dr_ctx *c, std::vector<dr::GQuery> &qv, std::vector<uint8_t> *hi
   if (whole && qv.size() > bq) return c->fail(DR_E_CAPACITY, "general sweeps: %zu reach sets of %zu words exceed one batch", qv.size(), per);
   if (hits) hits->assign(qv.size(), 0);
   if (edges) edges->assign(qv.size(), 0);
+  // the rows' unions U_r (valid whatever irregular edges the mirror holds): full rounds
+  // skip their rows
+  const u64 *U = nullptr;
+  if (c->use_memo && c->nrounds >= 2) {
+    if (int rc = refresh_rounds(c, true)) return rc;
+    if (c->ndirty == 0 && c->sum_dd == c->memo_dd()) U = c->U.as<u64>();
+  }
   for (size_t i0 = 0; i0 < qv.size(); i0 += bq) {
     const size_t i1 = std::min(qv.size(), i0 + bq), nq = i1 - i0;
     for (size_t i = i0; i < i1; i++) qv[i].mask_off = (int64_t)((i - i0) * per);
@@ -2253,7 +2272,7 @@ int run_gsweeps(dr_ctx *c, std::vector<dr::GQuery> &qv, std::vector<uint8_t> *hi
     uint8_t *dh = reinterpret_cast<uint8_t *>(qb + o_hit);
     u64 *de = reinterpret_cast<u64 *>(qb + o_e);
     HIPCHK(c, launch_gsweep(c, reinterpret_cast<const dr::GQuery *>(qb), (int)nq, Tg, c->masks.as<u64>(),
-                            c->gscratch.as<u64>(), dh, de));
+                            c->gscratch.as<u64>(), dh, de, U));
     if (hits) HIPCHK(c, c->d2h(hits->data() + i0, dh, nq));
     if (edges) HIPCHK(c, c->d2h(edges->data() + i0, de, nq * 8));
     HIPCHK(c, c->sync());
@@ -2274,7 +2293,7 @@ int general_path(dr_ctx *c, int q, const int32_t *from, const int32_t *to, int s
       return c->fail(DR_E_INVAL, "query %d: from round %d outside the DAG (Go: index out of range)", i, fr);
     out[i] = 0;
     if (fs < 1 || fs > c->n || tr < 0 || tr > Tg || ts < 1 || ts > c->n) continue;  // no edges / not an id any edge holds
-    qv.push_back(dr::GQuery{fr, fs - 1, strong_only ? 1 : 0, tr, ts - 1, 1, 0, 0});
+    qv.push_back(dr::GQuery{fr, fs - 1, strong_only ? 1 : 0, tr, ts - 1, 1, 0, 0, c->gsweep_bottom(tr), 0});
     idx.push_back(i);
   }
   std::vector<uint8_t> hits;
@@ -2320,7 +2339,7 @@ int general_votes(dr_ctx *c, int w0, int nw, uint8_t *commit, int32_t *vcount) {
     vcount[i] = 0;
     for (int s = 1; s <= n; s++)
       if (c->is_present(r4, s)) {
-        qv.push_back(dr::GQuery{r4, s - 1, 1, r1, L - 1, 1, 0, 0});
+        qv.push_back(dr::GQuery{r4, s - 1, 1, r1, L - 1, 1, 0, 0, c->gsweep_bottom(r1), 0});
         qw.push_back(i);
       }
   }
@@ -2350,7 +2369,7 @@ int general_chain(dr_ctx *c, int wave, int floor, std::vector<int32_t> &push, ui
   int vr = 4 * (wave - 1) + 1, vs = c->lead_src(wave), cur = wave;
   std::vector<u64> rows;
   while (true) {
-    std::vector<dr::GQuery> qv{dr::GQuery{vr, vs - 1, 1, -1, -1, 1, 0, 0}};
+    std::vector<dr::GQuery> qv{dr::GQuery{vr, vs - 1, 1, -1, -1, 1, 0, 0, c->gsweep_bottom(bottom), 0}};
     int next = -1;
     if (int rc = run_gsweeps(c, qv, nullptr, nullptr, [&](size_t, size_t) -> int {
           const size_t per = (size_t)gsweep_rows(c) * WS;

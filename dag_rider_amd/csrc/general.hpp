@@ -48,28 +48,39 @@ struct GQuery {
   int32_t tr, ts;       // tested target (0-based source), -1: none
   int32_t elo, ehi;     // degree sum over expanded present vertices of rounds [elo, ehi]
   int64_t mask_off;     // word offset of this query's F rows [0..T] in masks
+  int32_t bot;          // lowest round expanded (rows below stay empty; 0: every round)
+  int32_t pad;
 };
 
 // T: the last round the reach rows cover (irregular edges may target rounds past
 // the mirrored ones, NR: those hold no vertex).
+// U (optional): the rounds' strong-row unions (k_summary_commit / k_round_summary, valid
+// for the rows whatever irregular edges the mirror holds): a round whose present vertices
+// are all newly expanded sends U_r to round r-1 instead of its rows.  Strong rows are
+// ORed in registers and reduced through LDS (one global OR per word and round); every F
+// row belongs to this workgroup alone, so the weak and irregular scatters' atomics are
+// ordered by the round's barriers (no device-scope fence per round: round 4 had one, and
+// a global atomic per row word -- C4 scale: ~160 us a round, profiles/r05/v13_*).
 template <int WS>
 __global__ __launch_bounds__(256) void k_gsweep(DagView g, GView gv, const GQuery *__restrict__ qs, int nq, int T,
                                                 int NR, u64 *__restrict__ masks, u64 *__restrict__ scratch,
-                                                uint8_t *__restrict__ hit, u64 *__restrict__ edges) {
+                                                uint8_t *__restrict__ hit, u64 *__restrict__ edges,
+                                                const u64 *__restrict__ U) {
   constexpr int NT = 256;
   const int qi = blockIdx.x;
   if (qi >= nq) return;
   const GQuery q = qs[qi];
   const int tid = threadIdx.x, lane = tid & 63;
   u64 *F = masks + q.mask_off, *E = scratch + (size_t)qi * (T + 1) * WS;
-  __shared__ u64 NEW[WS];
-  __shared__ int s_any, s_same, s_up;
+  __shared__ u64 NEW[WS], ACC[WS];
+  __shared__ int s_any, s_same, s_up, s_full;
   __shared__ u64 s_e;
   for (size_t i = tid; i < (size_t)(T + 1) * WS; i += NT) {
     F[i] = 0;
     E[i] = 0;
   }
   if (tid == 0) s_e = 0;
+  if (tid < WS) ACC[tid] = 0;
   __syncthreads();
   if (q.s0 < 0 || q.r0 < 0 || q.r0 > T) {
     if (tid == 0) {
@@ -80,22 +91,26 @@ __global__ __launch_bounds__(256) void k_gsweep(DagView g, GView gv, const GQuer
   }
   if (tid == 0) atomicOr(&F[(size_t)q.r0 * WS + (q.s0 >> 6)], 1ULL << (q.s0 & 63));
   __syncthreads();
+  const int bot = max(q.bot, 0);
   int hi = q.r0;
-  while (hi >= 0) {
+  while (hi >= bot) {
     int up = -1;
     int r = hi;
-    while (r >= 0) {
+    while (r >= bot) {
       if (tid < 64) {
-        u64 nw = 0;
+        u64 nw = 0, p = 0;
         if (lane < WS) {
-          const u64 f = ld_agent(&F[(size_t)r * WS + lane]), p = r < NR ? g.present[(size_t)r * WS + lane] : 0ULL;
+          const u64 f = ld_agent(&F[(size_t)r * WS + lane]);
+          p = r < NR ? g.present[(size_t)r * WS + lane] : 0ULL;
           nw = f & p & ~E[(size_t)r * WS + lane];
           E[(size_t)r * WS + lane] |= nw;
           NEW[lane] = nw;
         }
         const bool any = __ballot(nw != 0ULL) != 0ULL;
+        const bool full = __ballot(lane < WS && nw != p) == 0ULL;  // every present vertex new
         if (lane == 0) {
           s_any = any;
+          s_full = full;
           s_same = 0;
           s_up = -1;
         }
@@ -120,13 +135,32 @@ __global__ __launch_bounds__(256) void k_gsweep(DagView g, GView gv, const GQuer
         if (lane == 0 && e) atomicAdd(&s_e, e);
       }
       // strong rows -> round r-1
-      if (r >= 1) {
-        const u64 *rows = g.strong + (size_t)r * g.n * WS;
-        for (int s = tid; s < g.n; s += NT) {
-          if (!((NEW[s >> 6] >> (s & 63)) & 1ULL)) continue;
+      if (r >= 1 && r - 1 >= bot) {
+        if (U && s_full) {  // block-uniform
+          if (tid < WS) {
+            const u64 x = U[(size_t)r * WS + tid];
+            if (x) atomicOr(&F[(size_t)(r - 1) * WS + tid], x);
+          }
+        } else {
+          const u64 *rows = g.strong + (size_t)r * g.n * WS;
+          u64 acc[WS];
+#pragma unroll
+          for (int w = 0; w < WS; w++) acc[w] = 0;
+          for (int s = tid; s < g.n; s += NT) {
+            if (!((NEW[s >> 6] >> (s & 63)) & 1ULL)) continue;
+#pragma unroll
+            for (int w = 0; w < WS; w++) acc[w] |= rows[(size_t)s * WS + w];
+          }
+#pragma unroll
           for (int w = 0; w < WS; w++) {
-            const u64 x = rows[(size_t)s * WS + w];
-            if (x) atomicOr(&F[(size_t)(r - 1) * WS + w], x);
+            const u64 v = wave_or(acc[w]);
+            if (lane == 0 && v) atomicOr(&ACC[w], v);
+          }
+          __syncthreads();
+          if (tid < WS) {
+            const u64 x = ACC[tid];
+            ACC[tid] = 0;
+            if (x) atomicOr(&F[(size_t)(r - 1) * WS + tid], x);
           }
         }
       }
@@ -139,13 +173,13 @@ __global__ __launch_bounds__(256) void k_gsweep(DagView g, GView gv, const GQuer
           if (!h) continue;
           const uint32_t key = g.wc_key[j];
           const int tr = r - (int)(key >> 11), ts = (int)(key & 2047u);
-          atomicOr(&F[(size_t)tr * WS + (ts >> 6)], 1ULL << (ts & 63));
+          if (tr >= bot) atomicOr(&F[(size_t)tr * WS + (ts >> 6)], 1ULL << (ts & 63));
         }
         // far weak edges (delta > 1023): own source - 1 << 32 | target round << 11 | target source - 1
         for (uint32_t j = g.far_roff[r] + tid; j < g.far_roff[r + 1]; j += NT) {
           const u64 x = g.far[j];
           const int own = (int)(x >> 32), tr = (int)((x >> 11) & 0x1FFFFFu), ts = (int)(x & 2047u);
-          if (!((NEW[own >> 6] >> (own & 63)) & 1ULL)) continue;
+          if (!((NEW[own >> 6] >> (own & 63)) & 1ULL) || tr < bot) continue;
           atomicOr(&F[(size_t)tr * WS + (ts >> 6)], 1ULL << (ts & 63));
         }
       }
@@ -155,7 +189,7 @@ __global__ __launch_bounds__(256) void k_gsweep(DagView g, GView gv, const GQuer
         const int own = (int)((x >> 32) & 2047u), tr = (int)((x >> 11) & 0xFFFFFu), ts = (int)(x & 2047u);
         const bool strong = (x >> 31) & 1u;
         if (q.strong_only && !strong) continue;
-        if (!((NEW[own >> 6] >> (own & 63)) & 1ULL)) continue;
+        if (!((NEW[own >> 6] >> (own & 63)) & 1ULL) || tr < bot) continue;
         const u64 bit = 1ULL << (ts & 63);
         const u64 old = atomicOr(&F[(size_t)tr * WS + (ts >> 6)], bit);
         if (!(old & bit) && tr >= r) {
@@ -163,8 +197,7 @@ __global__ __launch_bounds__(256) void k_gsweep(DagView g, GView gv, const GQuer
           else atomicMax(&s_up, tr);
         }
       }
-      __threadfence();  // the atomics are in L2 before wave 0 reads F at agent scope
-      __syncthreads();
+      __syncthreads();  // (waits for this workgroup's atomics: wave 0 reads F from L2 next)
       if (s_up > up) up = s_up;
       if (!s_same) r--;  // a new bit in round r itself: expand r again
       __syncthreads();

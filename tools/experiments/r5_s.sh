@@ -12,3 +12,6 @@ for rep in 1 2; do
   python3 -c "import json; d=json.loads(open('$O/loop_$rep.json').read()); print({k: round(v['p50'],1) for k, v in d['detail']['latency_us'].items()}, d['detail']['verify_vs_replay'])"
 done
 echo done
+timeout -k 10 240 python3 -u tools/gsweep_bench.py 256 > $O/gsweep.jsonl 2> $O/gsweep.err || echo "gsweep bench ended rc=$?"
+cat $O/gsweep.jsonl
+echo done2
