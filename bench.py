@@ -636,12 +636,15 @@ def run_c5(args, rank: int, world: int, local: int, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    step_ends = []
     for _ in range(args.steps):
-        b.run()
+        b.run()  # synchronous: the step ends with every DAG's results on the host
+        step_ends.append(time.perf_counter())
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0  # the timed region ends here: reading the results back is not a step
+    step_ms = [(b1 - b0) * 1e3 for b0, b1 in zip([t0] + step_ends[:-1], step_ends)]
     res = b.results()
     edges = sum(r.total_edges for r in res)
     kms = max(r.ms["deliver"] for r in res)  # the fused launch's device time (HIP events)
@@ -691,7 +694,8 @@ def run_c5(args, rank: int, world: int, local: int, dist):
                    "pops": int(sum(len(r.pop_count) for r in res)),
                    # the last step's phases (dr_replay_batch, first output): host prep before the
                    # launch, launch -> results on the host, the copy back (device), the unpack
-                   "step_phases_ms": dict(b.host_phases(), kernel=kms)},
+                   "step_phases_ms": dict(b.host_phases(), kernel=kms),
+                   "step_ms": step_ms},
     }
 
 
