@@ -59,10 +59,12 @@ struct DevBuf {
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
+    // a buffer that grows (per-call paths on a growing DAG: masks, plan arena, summaries)
+    // takes 1.5x, so that it is not freed every call: hipFree waits for the device
+    const size_t c = std::max<size_t>({bytes, cap ? cap + cap / 2 : 0, 4096});
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    size_t c = std::max<size_t>(bytes, 4096);
     hipError_t e = hipMalloc(&p, c);
     if (e == hipSuccess) cap = c;
     return e;
