@@ -2237,70 +2237,88 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
   }
 }
 
-// Inclusive prefix over rounds 0..T of up to three per-round arrays (one
-// workgroup; rounds >= 1 only).  With rbase != nullptr, also the exclusive
-// prefix of a (positions of round r's first canonical vertex).
-// The same prefixes without rbase (A, B over rounds 0..T, round 0 counted as 0) through
-// LDS: tiles of NT * PT rounds loaded and stored lane-consecutively (coalesced), each
-// thread scanning PT contiguous rounds out of LDS, one block scan per tile and array.
-// C3's 10 001 rounds: 16.9 us against 18.8 us for canon_prefix_block, whose lanes read
-// and write 80 B apart (profiles/r05/v10_prefix_bench.txt; a single-CU pass either way).
-template <int NT, int PT = 4>
-__device__ __forceinline__ void canon_prefix_lds(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
-                                                 u64 *__restrict__ A, u64 *__restrict__ B) {
-  constexpr int TILE = NT * PT;
-  __shared__ u64 sa[TILE], sb[TILE];
-  __shared__ u64 part[NT / 64];
-  const int tid = threadIdx.x, n = T + 1;
+// The canonical prefixes A, B of two per-round arrays over rounds 0..T (round 0 counted
+// as 0), one workgroup, every round of a chunk of J * NT in registers: column j of the
+// chunk (NT rounds) is loaded lane-consecutively (coalesced, all 2J loads in flight at
+// once), each wave scans its 64 rounds of every column by DPP (no LDS, no barrier), and
+// wave 0 turns the J * NT/64 wave totals into offsets through LDS: two LDS-only barriers
+// per chunk, one memory round trip.  C3 (10 001 rounds, J = 10): one chunk, 11.4 us against
+// 16.8 us for an LDS-tiled form and 18.8 us for canon_prefix_block's per-thread runs
+// (profiles/r05/v15_prefix_bench.txt; a single-CU pass either way).
+template <int NT, int J>
+__device__ __forceinline__ void canon_prefix_regs(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                  u64 *__restrict__ A, u64 *__restrict__ B) {
+  constexpr int NW = NT / 64, E = J * NW, PL = (E + 63) / 64;
+  __shared__ u64 oa[E + 1], ob[E + 1];  // wave totals -> exclusive offsets; [E] = the chunk total
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, n = T + 1;
   u64 ca = 0, cb = 0;
-  for (int t0 = 0; t0 < n; t0 += TILE) {
+  for (int c0 = 0; c0 < n; c0 += J * NT) {
+    u64 xa[J], xb[J];
 #pragma unroll
-    for (int j = 0; j < PT; j++) {
-      const int r = t0 + j * NT + tid;
+    for (int j = 0; j < J; j++) {  // clamped addresses: unconditional loads, all in flight
+      const int r = c0 + j * NT + tid;
+      const int rc = (r >= 1 && r < n) ? r : 0;
+      xa[j] = a[rc];
+      xb[j] = b[rc];
+    }
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const int r = c0 + j * NT + tid;
       const bool in = r >= 1 && r < n;  // round 0 is never delivered
-      const int rc = in ? r : 0;
-      const u64 x = a[rc], y = b[rc];
-      sa[j * NT + tid] = in ? x : 0ULL;
-      sb[j * NT + tid] = in ? y : 0ULL;
-    }
-    __syncthreads();
-    u64 xa[PT], xb[PT], la = 0, lb = 0;
-#pragma unroll
-    for (int j = 0; j < PT; j++) {
-      xa[j] = sa[tid * PT + j];
-      xb[j] = sb[tid * PT + j];
-      la += xa[j];
-      lb += xb[j];
-    }
-    u64 ta, tb;
-    u64 ea = ca + block_scan_excl<NT>(la, part, ta);
-    u64 eb = cb + block_scan_excl<NT>(lb, part, tb);
-#pragma unroll
-    for (int j = 0; j < PT; j++) {
-      ea += xa[j];
-      eb += xb[j];
-      sa[tid * PT + j] = ea;
-      sb[tid * PT + j] = eb;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PT; j++) {
-      const int r = t0 + j * NT + tid;
-      if (r < n) {
-        A[r] = sa[j * NT + tid];
-        B[r] = sb[j * NT + tid];
+      xa[j] = wave_scan_incl(in ? xa[j] : 0ULL);
+      xb[j] = wave_scan_incl(in ? xb[j] : 0ULL);
+      if (lane == 63) {
+        oa[j * NW + wid] = xa[j];
+        ob[j * NW + wid] = xb[j];
       }
     }
-    ca += ta;
-    cb += tb;
-    __syncthreads();
+    lds_barrier();
+    if (wid == 0) {  // exclusive offsets of the E (column, wave) totals, in round order
+      u64 va[PL], vb[PL], sa = 0, sb = 0;
+#pragma unroll
+      for (int k = 0; k < PL; k++) {
+        const int e = lane * PL + k;
+        va[k] = e < E ? oa[e] : 0ULL;
+        vb[k] = e < E ? ob[e] : 0ULL;
+        sa += va[k];
+        sb += vb[k];
+      }
+      const u64 ia = wave_scan_incl(sa), ib = wave_scan_incl(sb);
+      u64 pa = ia - sa, pb = ib - sb;
+#pragma unroll
+      for (int k = 0; k < PL; k++) {
+        const int e = lane * PL + k;
+        if (e < E) {
+          oa[e] = pa;
+          ob[e] = pb;
+        }
+        pa += va[k];
+        pb += vb[k];
+      }
+      if (lane == 63) {
+        oa[E] = ia;
+        ob[E] = ib;
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const int r = c0 + j * NT + tid;
+      if (r < n) {
+        A[r] = ca + oa[j * NW + wid] + xa[j];
+        B[r] = cb + ob[j * NW + wid] + xb[j];
+      }
+    }
+    ca += oa[E];
+    cb += ob[E];
+    lds_barrier();  // the offsets are rewritten by the next chunk
   }
 }
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                      u64 *__restrict__ A, u64 *__restrict__ B) {
-  canon_prefix_lds<NT>(T, a, b, A, B);
+  canon_prefix_regs<NT, 10>(T, a, b, A, B);
 }
 
 // Multi-segment copy between device memory and pinned (device-mapped) host

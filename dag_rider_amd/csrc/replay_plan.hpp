@@ -670,7 +670,7 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
   __shared__ u64 s_c[NWV], s_dg;
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (Gc && q == (int)gridDim.x - 1) {  // (Gc null: k_canon_prefix computed them)
-    canon_prefix_block<NT, 8>(T, RG, CE, Gc, Ec, nullptr);
+    canon_prefix_regs<NT, 8>(T, RG, CE, Gc, Ec);
     return;
   }
   // the query's fields load with the plan counts (the arena holds every slot below the grid bound)

@@ -87,6 +87,26 @@ __device__ __forceinline__ u64 wave_or(u64 x) {
   x |= dpp64<DPP_ROW_MIRROR>(x);
   return readlane64(x, 0) | readlane64(x, 16) | readlane64(x, 32) | readlane64(x, 48);
 }
+// 64-bit DPP move with zero where the source lane is out of the row or the row is masked
+// off (old = 0, bound_ctrl off)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ u64 dpp64z(u64 x) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, ROWS, 0xF, false);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, ROWS, 0xF, false);
+  return ((u64)hi << 32) | lo;
+}
+// inclusive prefix sum over the 64 lanes: row_shr 1, 2, 4, 8 inside each row of 16, then
+// row_bcast:15 (rows 1, 3 add the last lane of the row below) and row_bcast:31 (rows 2, 3
+// add lane 31); every lane of the wave must be active
+__device__ __forceinline__ u64 wave_scan_incl(u64 x) {
+  x += dpp64z<0x111, 0xF>(x);
+  x += dpp64z<0x112, 0xF>(x);
+  x += dpp64z<0x114, 0xF>(x);
+  x += dpp64z<0x118, 0xF>(x);
+  x += dpp64z<0x142, 0xA>(x);
+  x += dpp64z<0x143, 0xC>(x);
+  return x;
+}
 // sum of all 64 lanes (wave-uniform result)
 __device__ __forceinline__ u64 wave_sum(u64 x) {
   x += dpp64<DPP_QP_1032>(x);

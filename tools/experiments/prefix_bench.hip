@@ -1,9 +1,11 @@
 // prefix_bench.hip -- k_canon_prefix's one-workgroup prefix over T+1 rounds of two
 // u64 arrays (C3: 10 001 rounds), three forms timed with HIP events (round 5 experiment):
-//   0  canon_prefix_block<1024> (the shipped run form: thread t owns rounds t*per ..)
-//   1  an LDS-transposed tile form: coalesced loads into LDS, each thread scans 4
+//   0  canon_prefix_block<1024> (the run form shipped to round 4: thread t owns rounds t*per ..)
+//   1  an LDS-transposed tile form (shipped in round 5 up to v14): coalesced loads into LDS, each thread scans 4
 //      contiguous rounds out of LDS, one block scan per tile, coalesced stores
 //   2  canon_prefix_block<256>
+//   3  k_canon_prefix<1024> as shipped since round 5's v14 (canon_prefix_regs: every round
+//      of the chunk in registers, DPP wave scans, two LDS-only barriers)
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../dag_rider_amd/csrc prefix_bench.hip -o prefix_bench
 #include <cstdio>
 #include <cstdlib>
@@ -84,7 +86,7 @@ int main(int argc, char **argv) {
   std::vector<u64> wantA(n), wantB(n);
   u64 sa = 0, sb = 0;
   for (int i = 0; i < n; i++) { if (i >= 1) { sa += ha[i]; sb += hb[i]; } wantA[i] = sa; wantB[i] = sb; }
-  for (int form = 0; form < 3; form++) {
+  for (int form = 0; form < 4; form++) {
     float best = 1e9;
     for (int it = 0; it < 50; it++) {
       hipMemset(A, 0, n * 8);
@@ -92,6 +94,7 @@ int main(int argc, char **argv) {
       if (form == 0) hipLaunchKernelGGL((k_prefix_block<1024>), dim3(1), dim3(1024), 0, 0, T, a, b, A, B);
       if (form == 1) hipLaunchKernelGGL((k_prefix_lds<1024>), dim3(1), dim3(1024), 0, 0, T, a, b, A, B);
       if (form == 2) hipLaunchKernelGGL((k_prefix_block<256>), dim3(1), dim3(256), 0, 0, T, a, b, A, B);
+      if (form == 3) hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, 0, T, a, b, A, B);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms = 0;
