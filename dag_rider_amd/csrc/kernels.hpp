@@ -125,9 +125,13 @@ struct Geo {
 
 // ---------------------------------------------------------------------------
 // k_commit: one workgroup per wave.  S0 = {leader}; S_{k+1} = {v in round
-// r1+k+1 : row(v) & S_k != 0}; vcount = |S_3|.  Row loads of round r1+1 are
-// restricted to the chunk holding the leader's bit; rounds r1+2, r1+3 are
-// prefetched whole (they do not depend on S) when the registers allow.
+// r1+k+1 : row(v) & S_k != 0}; vcount = |S_3|.  Every row load of the wave goes out
+// before the first is used: round r1+1 as the word holding the leader's bit of each
+// row (one source per thread), rounds r1+2, r1+3 whole (16-B chunks; they do not
+// depend on S).  An absent vertex's row is zero (the append rejects strong edges on
+// one), so no presence test is needed.  (Round by round, each round's loads waited
+// for the previous round's S: three memory round trips a wave, 21 us for a rank's
+// 125-wave share at N = 8, 0.20 of peak, profiles/r05/final_bench_share8.json.)
 // ---------------------------------------------------------------------------
 template <int WS, int NT>
 __global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int quorum,
@@ -135,9 +139,9 @@ __global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int qu
                                                int32_t *__restrict__ vcount) {
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
+  constexpr int NS = (64 * WS + NT - 1) / NT;  // passes over the sources of round r1+1
   __shared__ u64 S[WS];
   __shared__ u64 T[WS];
-  __shared__ u64 P[3][WS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int bi = blockIdx.x;
   if (bi >= nw) return;
@@ -149,43 +153,58 @@ __global__ __launch_bounds__(NT) void k_commit(DagView g, int w0, int nw, int qu
     if (tid == 0) { commit[bi] = 0; vcount[bi] = -1; }
     return;
   }
-  if (tid < WS) {
-    S[tid] = tid == (l >> 6) ? 1ULL << (l & 63) : 0ULL;
-    T[tid] = 0;
+  const int j = tid % CPR;  // this thread's chunk column in rounds r1+2, r1+3
+  const u64 *rows1 = g.strong + (size_t)(r1 + 1) * n * WS;
+  u64 x1[NS];
 #pragma unroll
-    for (int k = 0; k < 3; k++) P[k][tid] = g.present[(size_t)(r1 + 1 + k) * WS + tid];
+  for (int i = 0; i < NS; i++) {
+    const int s = i * NT + tid;
+    x1[i] = rows1[(size_t)(s < n ? s : 0) * WS + (l >> 6)];
   }
-  __syncthreads();
-  const int j = tid % CPR;  // this thread's chunk column
-#pragma unroll
-  for (int k = 1; k <= 3; k++) {
-    const int r = r1 + k;
-    const u64 *rows = g.strong + (size_t)r * n * WS;
-    const u64 *pres = P[k - 1];
-    // S chunk this thread ANDs with
-    u64 s0 = S[j * CW], s1 = CW == 2 ? S[j * CW + 1] : 0ULL;
-    const bool need = (s0 | s1) != 0ULL;
-    u64 v0[CPT], v1[CPT];
+  // both rounds in registers when they fit (n = 2048: 16 chunks a round, round r1+3 then
+  // loads once round r1+2 is consumed)
+  constexpr int PRE = CPT <= 8 ? 2 : 1;
+  u64 v0[PRE][CPT], v1[PRE][CPT];
+  auto load = [&](int k, int slot) {
+    const u64 *rows = g.strong + (size_t)(r1 + 2 + k) * n * WS;
 #pragma unroll
     for (int p = 0; p < CPT; p++) {
       const int s = tid / CPR + p * RPP;
-      v0[p] = 0;
-      v1[p] = 0;
-      if (need && s < n && ((pres[s >> 6] >> (s & 63)) & 1ULL)) {
-        if constexpr (CW == 2) {
-          const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(rows + (size_t)s * WS + 2 * j);
-          v0[p] = x.x;
-          v1[p] = x.y;
-        } else {
-          v0[p] = rows[s];
-        }
+      const size_t at = (size_t)(s < n ? s : 0) * WS;  // clamped: unconditional loads
+      if constexpr (CW == 2) {
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(rows + at + 2 * j);
+        v0[slot][p] = x.x;
+        v1[slot][p] = x.y;
+      } else {
+        v0[slot][p] = rows[at];
+        v1[slot][p] = 0;
       }
     }
+  };
+#pragma unroll
+  for (int k = 0; k < PRE; k++) load(k, k);
+  if (tid < WS) T[tid] = 0;
+  // S_1: the sources of round r1+1 whose row holds the leader (wave = 64 sources)
+#pragma unroll
+  for (int i = 0; i < NS; i++) {
+    const int s = i * NT + tid;
+    const u64 m = __ballot(s < n && ((x1[i] >> (l & 63)) & 1ULL));
+    const int word = (i * NT) / 64 + wid;
+    if (lane == 0 && word < WS) S[word] = m;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int kk = PRE == 2 ? k : 0;
+    if (PRE == 1 && k == 1) load(1, 0);
+    // S chunk this thread ANDs with
+    const u64 s0 = S[j * CW], s1 = CW == 2 ? S[j * CW + 1] : 0ULL;
 #pragma unroll
     for (int p = 0; p < CPT; p++) {
       const int rowbase = (wid * 64) / CPR + p * RPP;  // first row of this wave's pass
       if (rowbase >= n) break;                         // wave-uniform
-      const bool hit = ((v0[p] & s0) | (v1[p] & s1)) != 0ULL;
+      const int s = tid / CPR + p * RPP;
+      const bool hit = s < n && ((v0[kk][p] & s0) | (v1[kk][p] & s1)) != 0ULL;
       u64 m = __ballot(hit);
       if (lane == 0 && m) {
         u64 bits;
