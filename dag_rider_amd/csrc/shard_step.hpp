@@ -213,6 +213,10 @@ __device__ __forceinline__ void expand_partial_local(const MArgs &a, int r, int 
     }
   }
   if (!weak) return;
+  // the frontier's nonzero words: a column's source words are read only there (a query's
+  // first step has one source, one word of W)
+  u64 fm = 0;
+  for (int w = 0; w < W; w++) fm |= FE[w] ? 1ULL << w : 0ULL;
   const bool per_wave = NL >= NW;
   for (int l = per_wave ? wv : 0; l < NL; l += per_wave ? NW : 1) {
     const uint64_t c0 = a.wcro[(size_t)l * (a.R + 1) + r], c1 = a.wcro[(size_t)l * (a.R + 1) + r + 1];
@@ -220,7 +224,10 @@ __device__ __forceinline__ void expand_partial_local(const MArgs &a, int r, int 
       const u64 *row = a.wcr + jj * W;
       const uint32_t key = a.wck[jj];
       u64 hit = 0;
-      for (int w = 0; w < W; w++) hit |= row[w] & FE[w];
+      for (u64 m = fm; m; m &= m - 1) {
+        const int w = __builtin_ctzll(m);
+        hit |= row[w] & FE[w];
+      }
       if (!hit) continue;
       const int tr = r - (int)(key >> 11), cb = l * WSs * 64 + (int)(key & 2047u);  // local bit
       if (tr < bottom) continue;
@@ -270,6 +277,16 @@ __global__ __launch_bounds__(NT) void k_ms_step2(MArgs a, FArgs f, int j, MState
   bool start = false;
   MState S1 = S;
   S1.steps = S.steps + 1;
+  // wave 0's words of round r go out before the ring copy below (which waits for its own
+  // loads before it writes LDS), unless a canonical segment starts (its round is found first)
+  const bool early = !(canon && S.fresh);
+  u64 e_fw = 0, e_p = 0, e_k = 0;
+  if (early && wv == 0 && lane < a.W) {
+    if (j == 0 && !canon) e_fw = (Q.src0 >= 0 && lane == (Q.src0 >> 6)) ? 1ULL << (Q.src0 & 63) : 0ULL;
+    else e_fw = rin[((size_t)(lane / a.WSs) * a.nq + qi) * a.WSs + lane % a.WSs];
+    e_p = a.pres[(size_t)r * a.W + lane];
+    if (pop) e_k = a.K[(size_t)r * a.W + lane];
+  }
   if (canon && S.fresh) {
     // the next canonical segment: the highest bad round below cur; its ring starts
     // with what the full rounds above it put below it (canon_ring_init)
@@ -313,11 +330,14 @@ __global__ __launch_bounds__(NT) void k_ms_step2(MArgs a, FArgs f, int j, MState
     const bool act = lane < W;
     u64 fw = 0, p = 0, k = 0;
     if (act) {
-      if (start) fw = a.K[(size_t)r * W + lane];
-      else if (j == 0 && !canon) fw = (Q.src0 >= 0 && lane == (Q.src0 >> 6)) ? 1ULL << (Q.src0 & 63) : 0ULL;
-      else fw = rin[((size_t)(lane / WSs) * a.nq + qi) * WSs + lane % WSs];
-      p = a.pres[(size_t)r * W + lane];
-      if (pop) k = a.K[(size_t)r * W + lane];
+      if (start) {
+        fw = a.K[(size_t)r * W + lane];
+        p = a.pres[(size_t)r * W + lane];
+      } else {
+        fw = e_fw;
+        p = e_p;
+        k = e_k;
+      }
     }
     // waveReady's chain (process.go:342-350): a reachable, present leader of wave
     // wvv is pushed and the chain goes on from it alone
