@@ -14,6 +14,12 @@
 
 namespace dr {
 
+// Materialise a value here: an empty asm that reads it keeps the compiler from sinking its
+// computation (and the wait for the load it came from) below the next round's prefetch,
+// where the wait's in-order count then covered the prefetch's loads too.
+__device__ __forceinline__ void pin_vgpr(u64 x) { asm volatile("" : : "v"(x)); }
+__device__ __forceinline__ void pin_vgpr(uint32_t x) { asm volatile("" : : "v"(x)); }
+
 // dynamic LDS of k_replay_small_1w: the weak ring (rsl slots of 128 u64) or the
 // later phases' arrays, whichever is larger
 template <bool PAPER, bool PERSIST>
@@ -27,7 +33,7 @@ inline size_t small1w_lds_bytes(int rsl) {
 }
 
 template <bool PAPER, bool PERSIST>
-__global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restrict__ jobs, int njobs, int nw, int rsl) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_replay_small_1w(const SmallJob *__restrict__ jobs, int njobs, int nw, int rsl) {
   constexpr bool paper = PAPER;  // REF mode skips the paper-mode digests entirely
   constexpr bool chain_persistent = PERSIST;  // persistent chains push every wave at most once: <= 64 pops
   // LDS is what limits DAGs per CU: the weak ring (phase 2 only) shares its
@@ -55,6 +61,11 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
   const int lane = threadIdx.x;
   const int jb = blockIdx.x;
   if (jb >= njobs) return;
+  // profiling build: wall-clock stamps at the phase boundaries, cycle counts of the cone
+  // pass's parts (tools/batch_timing.py)
+  DR_TT(u64 *tt = jb < kSweepTimingQ ? g_sweep_timing + (size_t)jb * 16 : nullptr;
+        auto stamp = [&](int k) { if (tt && lane == 0) tt[k] = wall_clock64(); };
+        stamp(0);)
   const SmallJob J = jobs[jb];
   auto g_strong = as_global(J.strong);
   auto g_present = as_global(J.present);
@@ -94,6 +105,31 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
     }
   };
   auto pres_word = [&](int r, int w) -> u64 { return w < WS ? g_present[(size_t)r * WS + w] : 0ULL; };
+  // The per-round weak-column and slot offsets (rounds 0..T+1 <= 254) and the leaders
+  // (waves 0..nw <= 64) in registers -- lane l holds entries l, 64+l, 128+l, 192+l --
+  // read by wave-uniform readlane.  The prefetches of the passes below take their
+  // addresses from them: an address that came from a load just issued made the wave
+  // wait for that load, and for every load issued before it, so each round had paid a
+  // full memory latency (profiles/r05/v20_batch_timing.jsonl).
+  uint32_t roffv[4], soffv[4], leadv[2];  // (soffv: loaded for the emission, phase 4)
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = 64 * k + lane, ic = i <= T + 1 ? i : T + 1;
+    roffv[k] = g_wc_roff[ic];
+  }
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int i = 64 * k + lane;
+    leadv[k] = g_lead[i <= nw ? i : nw];
+  }
+  auto tab4 = [&](const uint32_t (&v)[4], int i) -> uint32_t {  // i wave-uniform
+    const int k = i >> 6;
+    const uint32_t x = k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, i & 63);
+  };
+  auto lead_of = [&](int w) -> int {  // chooseLeader(w), 1-based source
+    return __builtin_amdgcn_readlane((int)(w < 64 ? leadv[0] : leadv[1]), w & 63);
+  };
 
   // ---------------- 1. leaders ----------------
   // (the commit rule runs inside the cone pass below, on the rows it reads anyway: a
@@ -109,6 +145,8 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
     lead_mask = __ballot(lp);
     if (lane < nw && !lp) vc_s[lane] = -1;
   }
+  DR_TT(stamp(1); u64 cyc[6] = {0, 0, 0, 0, 0, 0}; u64 tc = __builtin_readcyclecounter();
+        auto tick = [&](int k) { const u64 x = __builtin_readcyclecounter(); cyc[k] += x - tc; tc = x; };)
 
   // ---------------- 2. top-down cone pass (lane b: leader b's sets) ----------------
   for (int i = lane; i < rsl * 128; i += 64) ring[i] = 0;
@@ -119,13 +157,17 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
   const bool alive = lane < nw || (haveK && lane == 63);
   // the commit rule (process.go:326-339) of the wave whose leader round is r: rows and
   // presence of rounds r+1 .. r+3, kept from the iterations above (lanes v, v + 64)
-  u64 ha[3][2], hb[3][2], hp[3][2];
+  // hp[k]: bit i = vertex lane + 64 i present (two bits instead of two presence words)
+  u64 ha[3][2], hb[3][2];
+  uint32_t hp[3];
+  auto pbits = [&](u64 p0, u64 p1) -> uint32_t {
+    return (uint32_t)((p0 >> lane) & 1ULL) | ((uint32_t)((p1 >> lane) & 1ULL) << 1);
+  };
 #pragma unroll
   for (int k = 0; k < 3; k++) {  // rounds T+1 .. T+3 (the top wave's; the DAG holds 4 nw + 1 rounds)
     row(T + 1 + k, lane, ha[k][0], hb[k][0]);
     row(T + 1 + k, lane + 64, ha[k][1], hb[k][1]);
-    hp[k][0] = pres_word(T + 1 + k, 0);
-    hp[k][1] = pres_word(T + 1 + k, 1);
+    hp[k] = pbits(pres_word(T + 1 + k, 0), pres_word(T + 1 + k, 1));
   }
   u64 F0 = 0, F1 = 0;  // F_b: round-r vertices in leader b's cone
   u64 G0 = 0, G1 = 0;  // G_b: the same over strong edges only
@@ -139,41 +181,62 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
     n1 = WS > 1 ? wave_or((m0 ? rb[0] : 0ULL) | (m1 ? rb[1] : 0ULL)) : 0ULL;
     if (dsum) *dsum = (uint32_t)wave_sum((u64)((m0 ? sd[0] : 0u) + (m1 ? sd[1] : 0u)));
   };
-  // software pipeline: round r-1's rows and first 64 weak columns (they do not
-  // depend on the cones) load while round r is processed
-  u64 nra[2], nrb[2], nw0 = 0, nw1 = 0;
-  uint32_t nkey = 0, nc0 = 0, nc1 = 0;
-  auto prefetch2 = [&](int r) {
-    row(r, lane, nra[0], nrb[0]);
-    row(r, lane + 64, nra[1], nrb[1]);
-    nc0 = g_wc_roff[r];
-    nc1 = g_wc_roff[r + 1];
-    const uint32_t jc = nc0 + lane;
-    nkey = 0;
-    nw0 = nw1 = 0;
-    if (jc < nc1) {
-      nkey = g_wc_key[jc];
-      nw0 = g_wc_rows[(size_t)jc * WS];
-      nw1 = WS > 1 ? g_wc_rows[(size_t)jc * WS + 1] : 0ULL;
-    }
+  // software pipeline: round r-1's rows, presence, weak degrees and first 64 weak
+  // columns (they do not depend on the cones) load while round r is processed, into
+  // one of two register sets that the 2x unrolled loop below uses in turn (one set
+  // rotated through moves at the loop's back edge made the wave wait there for the
+  // loads it had just issued; the offsets come from registers, tab4)
+  struct Pf {
+    u64 ra[2], rb[2], w0, w1;
+    uint32_t pr[2];  // the 32-bit half of each presence word that holds this lane's bit
+    uint32_t key, c0, c1;
+    uint16_t wd[2];  // (kept 16-bit: a widening right after the load made the wave wait for it)
   };
-  prefetch2(T);
-  for (int r = T; r >= 1; r--) {
+  // Every load unconditional, at a clamped address, its value masked only where the round
+  // uses it (cone_round): a conditional load, or a select right after a load, made the
+  // wave wait for the loads just issued.  A row is one 16-B load (WS = 1: the second word
+  // is the next row's, masked; the mirror's strong buffer has a row of slack); a column
+  // index past the round's columns reads column 0 (the key buffers hold >= 4 KiB).
+  auto prefetch2 = [&](int r, Pf &p) {
+    p.c0 = tab4(roffv, r);
+    p.c1 = tab4(roffv, r + 1);
+    const uint32_t jc = p.c0 + lane, jcc = jc < p.c1 ? jc : 0u;
+    p.key = g_wc_key[jcc];
+    p.w0 = g_wc_rows[(size_t)jcc * WS];
+    p.w1 = g_wc_rows[(size_t)jcc * WS + (WS > 1 ? 1 : 0)];
 #pragma unroll
     for (int i = 0; i < 2; i++) {
-      ra[i] = nra[i];
-      rb[i] = nrb[i];
-      sd[i] = (uint32_t)(__popcll(ra[i]) + __popcll(rb[i]));
+      const int v = lane + 64 * i, vc = v < n ? v : 0;
+      const u64x2 x = *reinterpret_cast<const u64x2 DR_GLOBAL *>(g_strong + ((size_t)r * n + vc) * WS);
+      p.ra[i] = x.x;
+      p.rb[i] = x.y;
+      p.wd[i] = g_wdeg[(size_t)r * n + vc];
     }
+    const uint32_t DR_GLOBAL *ph = reinterpret_cast<const uint32_t DR_GLOBAL *>(g_present + (size_t)r * WS);
+    p.pr[0] = ph[lane >> 5];
+    p.pr[1] = ph[(WS > 1 ? 2 : 0) + (lane >> 5)];
+  };
+  auto cone_round = [&](int r, const Pf &cur, Pf &nxt) {
+    DR_TT(tick(0);)  // the loop and the round's loads
+    uint16_t cwd[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {  // the prefetched words, masked (prefetch2)
+      const bool in = lane + 64 * i < n;
+      ra[i] = in ? cur.ra[i] : 0ULL;
+      rb[i] = in && WS > 1 ? cur.rb[i] : 0ULL;
+      sd[i] = (uint32_t)(__popcll(ra[i]) + __popcll(rb[i]));
+      cwd[i] = cur.wd[i];
+    }
+    const uint32_t cpb = ((cur.pr[0] >> (lane & 31)) & 1u) | (WS > 1 ? ((cur.pr[1] >> (lane & 31)) & 1u) << 1 : 0u);
     if (((r - 1) & 3) == 0) {  // leader round of wave w: its vote from rounds r+1 .. r+3
       const int w = (r - 1) / 4 + 1;
       if ((lead_mask >> (w - 1)) & 1ULL) {
-        const int l = g_lead[w] - 1;
+        const int l = lead_of(w) - 1;
         u64 s0 = l < 64 ? 1ULL << l : 0ULL, s1 = l >= 64 ? 1ULL << (l - 64) : 0ULL, deg = 0;
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-          const bool h0 = ((hp[k][0] >> lane) & 1ULL) && (((ha[k][0] & s0) | (hb[k][0] & s1)) != 0ULL);
-          const bool h1 = ((hp[k][1] >> lane) & 1ULL) && (((ha[k][1] & s0) | (hb[k][1] & s1)) != 0ULL);
+          const bool h0 = (hp[k] & 1u) && (((ha[k][0] & s0) | (hb[k][0] & s1)) != 0ULL);
+          const bool h1 = (hp[k] & 2u) && (((ha[k][1] & s0) | (hb[k][1] & s1)) != 0ULL);
           s0 = __ballot(h0);
           s1 = __ballot(h1);
           deg += (u64)(__popcll(ha[k][0]) + __popcll(hb[k][0]) + __popcll(ha[k][1]) + __popcll(hb[k][1]));
@@ -184,23 +247,35 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
         if (vc >= q) commit_mask |= 1ULL << (w - 1);
       }
     }
+    DR_TT(tick(1);)  // the commit rule
 #pragma unroll
     for (int i = 0; i < 2; i++) {  // round r joins the history (r+1 .. r+3 for the next leader round)
       ha[2][i] = ha[1][i];
       hb[2][i] = hb[1][i];
-      hp[2][i] = hp[1][i];
       ha[1][i] = ha[0][i];
       hb[1][i] = hb[0][i];
-      hp[1][i] = hp[0][i];
       ha[0][i] = ra[i];
       hb[0][i] = rb[i];
     }
-    hp[0][0] = pres_word(r, 0);
-    hp[0][1] = pres_word(r, 1);
-    u64 cw0 = nw0, cw1 = nw1;
-    uint32_t ckey = nkey;
-    const uint32_t c0 = nc0, c1 = nc1;
-    if (r > 1) prefetch2(r - 1);
+    hp[2] = hp[1];
+    hp[1] = hp[0];
+    hp[0] = cpb;
+    const bool cin = cur.c0 + lane < cur.c1;
+    u64 cw0 = cin ? cur.w0 : 0ULL, cw1 = cin && WS > 1 ? cur.w1 : 0ULL;
+    uint32_t ckey = cin ? cur.key : 0u;
+    const uint32_t c0 = cur.c0, c1 = cur.c1;
+    // this round's words are in before the next round's loads go out
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      pin_vgpr(ra[i]);
+      pin_vgpr(rb[i]);
+      pin_vgpr(sd[i]);
+      pin_vgpr((uint32_t)cwd[i]);
+    }
+    pin_vgpr(cw0);
+    pin_vgpr(cw1);
+    pin_vgpr(ckey);
+    if (r > 1) prefetch2(r - 1, nxt);
     {  // pending weak targets of round r
       const int sl = r % rsl;
       F0 |= ring[(sl * 2) * 64 + lane];
@@ -217,7 +292,7 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
     }
     if (((r - 1) & 3) == 0) {  // leader round of wave w: seed its lane with the leader's vertex
       const int w = (r - 1) / 4 + 1;
-      const int l = g_lead[w] - 1;
+      const int l = lead_of(w) - 1;
       if ((lead_mask >> (w - 1)) & 1ULL) {
         const u64 bit = 1ULL << (l & 63);
         if (lane == w - 1) {
@@ -238,7 +313,7 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
       const int v = lane + 64 * i;
       if (v < n) {
         const size_t at = (size_t)r * n + v;
-        g_deg[at] = ((sd[i] + g_wdeg[at]) << 16) | sd[i];
+        g_deg[at] = ((sd[i] + (uint32_t)cwd[i]) << 16) | sd[i];
       }
     }
     // K (lane 63) and the leaders whose sets differ from it ("solo": expanded on their own)
@@ -251,6 +326,7 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
     }
     const bool eqF = haveK && F0 == K0 && F1 == K1, eqG = haveK && G0 == KG0 && G1 == KG1;
     const u64 soloF = __ballot(!eqF && (F0 | F1) != 0ULL), soloG = __ballot(!eqG && (G0 | G1) != 0ULL);
+    DR_TT(tick(2);)  // ring, seeds, cone and degree stores, solo ballots
     // weak columns of round r (64 per batch, lane j holding column j; the first
     // batch was prefetched): a column's target joins b's pending round iff its
     // sources meet F_b
@@ -289,6 +365,7 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
       __syncthreads();
       KW[lane] = 0;
     }
+    DR_TT(tick(3);)  // weak columns, K's weak targets spread
     // strong edges: round r-1's sets, and the strong degrees summed over G
     u64 N0 = 0, N1 = 0, H0 = 0, H1 = 0;
     if (haveK) {
@@ -299,6 +376,7 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
       expand(KG0, KG1, a, b, &ds);
       if (eqG) { H0 = a; H1 = b; suf += ds; }
     }
+    DR_TT(tick(4);)  // K's two expansions
     for (u64 m = soloF; m; m &= m - 1) {
       const int b = __builtin_ctzll(m);
       u64 x, y;
@@ -318,7 +396,15 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
     G0 = H0;
     G1 = H1;
     __syncthreads();
+    DR_TT(tick(5);)  // the leaders' own expansions
+  };
+  Pf pa, pb;
+  prefetch2(T, pa);
+  for (int r = T; r >= 1; r -= 2) {
+    cone_round(r, pa, pb);
+    if (r >= 2) cone_round(r - 1, pb, pa);
   }
+  DR_TT(stamp(2); if (tt && lane == 0) for (int k = 0; k < 6; k++) tt[8 + k] = cyc[k];)
 
   // ---------------- 3. chains and pops (wave-uniform scalar code) ----------------
   for (int i = lane; i < 64 * 65; i += 64) coef[i] = 0;
@@ -363,8 +449,14 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
   }
   if (lane == 0) g_push_off[nw] = (uint32_t)npush;
   __syncthreads();
+  DR_TT(stamp(3);)
 
   // ---------------- 4. bottom-up emission ----------------
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = 64 * k + lane, ic = i <= T + 1 ? i : T + 1;
+    soffv[k] = g_slot_off[ic];
+  }
   // lane b = leader wave b+1 for the per-leader bookkeeping
   const int myfirst = first_pop[lane];
   int myrank = 0;  // PAPER: leaders first popped before b
@@ -420,12 +512,12 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
-      if (v < n) pd[i] = g_deg[(size_t)r * n + v];
+      pd[i] = g_deg[(size_t)r * n + (v < n ? v : 0)];  // (a lane past n: never read)
     }
     pp0 = pres_word(r, 0);
     pp1 = pres_word(r, 1);
-    psa = g_slot_off[r];
-    psb = g_slot_off[r + 1];
+    psa = tab4(soffv, r);
+    psb = tab4(soffv, r + 1);
     pslo = psa + lane < psb ? (int)g_slot_src[psa + lane] : 0;
     pshi = psa + 64 + lane < psb ? (int)g_slot_src[psa + 64 + lane] : 0;
   };
@@ -509,6 +601,7 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
     }
   }
   __syncthreads();
+  DR_TT(stamp(4);)
 
   // ---------------- 5. outputs ----------------
   u64 dsum = 0;
@@ -539,6 +632,7 @@ __global__ __launch_bounds__(64) void k_replay_small_1w(const SmallJob *__restri
     g_totals[2] = dsum;
     g_totals[3] = (u64)npush;
   }
+  DR_TT(stamp(5);)
 }
 
 }  // namespace dr
