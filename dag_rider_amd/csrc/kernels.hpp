@@ -1985,9 +1985,11 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
         if (e) atomicAdd(&s_edges[0], e);
         DR_TT(walked++;)
         lds_barrier();
+        // (no barrier before the next round: every thread read this round's s_ctl before
+        // the one above, the ring's contributions are in, and s_edges is read and reset
+        // by thread 0 alone)
         if (tid == 0) CE[r] = s_edges[0];
         --r;
-        lds_barrier();
       }
     }
     pos = r;
