@@ -60,6 +60,7 @@ struct SmallJob {
   const u64 *wc_rows;
   const uint32_t *wc_roff;
   const uint16_t *wdeg;     // [rounds][n] weak degree per vertex
+  const uint16_t *sdeg;     // [rounds][n] strong degree per vertex (the wave form's emission)
   const uint32_t *slot_off;
   const uint16_t *slot_src;
   const uint16_t *lead;     // [wave] chooseLeader(w), 1-based source

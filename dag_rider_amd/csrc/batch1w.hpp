@@ -73,12 +73,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   auto g_wc_rows = as_global(J.wc_rows);
   auto g_wc_roff = as_global(J.wc_roff);
   auto g_wdeg = as_global(J.wdeg);
+  auto g_sdeg = as_global(J.sdeg);
   auto g_slot_off = as_global(J.slot_off);
   auto g_slot_src = as_global(J.slot_src);
   auto g_lead = as_global(J.lead);
   auto g_cone = as_global(J.cone);
   auto g_sufl = as_global(J.sufl);
-  auto g_deg = as_global(J.deg);
   auto g_commit = as_global(J.commit);
   auto g_vcount = as_global(J.vcount);
   auto g_push_off = as_global(J.push_off);
@@ -190,7 +190,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     u64 ra[2], rb[2], w0, w1;
     uint32_t pr[2];  // the 32-bit half of each presence word that holds this lane's bit
     uint32_t key, c0, c1;
-    uint16_t wd[2];  // (kept 16-bit: a widening right after the load made the wave wait for it)
   };
   // Every load unconditional, at a clamped address, its value masked only where the round
   // uses it (cone_round): a conditional load, or a select right after a load, made the
@@ -210,7 +209,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
       const u64x2 x = *reinterpret_cast<const u64x2 DR_GLOBAL *>(g_strong + ((size_t)r * n + vc) * WS);
       p.ra[i] = x.x;
       p.rb[i] = x.y;
-      p.wd[i] = g_wdeg[(size_t)r * n + vc];
     }
     const uint32_t DR_GLOBAL *ph = reinterpret_cast<const uint32_t DR_GLOBAL *>(g_present + (size_t)r * WS);
     p.pr[0] = ph[lane >> 5];
@@ -218,14 +216,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   };
   auto cone_round = [&](int r, const Pf &cur, Pf &nxt) {
     DR_TT(tick(0);)  // the loop and the round's loads
-    uint16_t cwd[2];
 #pragma unroll
     for (int i = 0; i < 2; i++) {  // the prefetched words, masked (prefetch2)
       const bool in = lane + 64 * i < n;
       ra[i] = in ? cur.ra[i] : 0ULL;
       rb[i] = in && WS > 1 ? cur.rb[i] : 0ULL;
       sd[i] = (uint32_t)(__popcll(ra[i]) + __popcll(rb[i]));
-      cwd[i] = cur.wd[i];
     }
     const uint32_t cpb = ((cur.pr[0] >> (lane & 31)) & 1u) | (WS > 1 ? ((cur.pr[1] >> (lane & 31)) & 1u) << 1 : 0u);
     if (((r - 1) & 3) == 0) {  // leader round of wave w: its vote from rounds r+1 .. r+3
@@ -270,7 +266,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
       pin_vgpr(ra[i]);
       pin_vgpr(rb[i]);
       pin_vgpr(sd[i]);
-      pin_vgpr((uint32_t)cwd[i]);
     }
     pin_vgpr(cw0);
     pin_vgpr(cw1);
@@ -308,14 +303,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     g_cone[((size_t)r * 2) * 64 + lane] = F0;
     g_cone[((size_t)r * 2 + 1) * 64 + lane] = F1;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const int v = lane + 64 * i;
-      if (v < n) {
-        const size_t at = (size_t)r * n + v;
-        g_deg[at] = ((sd[i] + (uint32_t)cwd[i]) << 16) | sd[i];
-      }
-    }
     // K (lane 63) and the leaders whose sets differ from it ("solo": expanded on their own)
     u64 K0 = 0, K1 = 0, KG0 = 0, KG1 = 0;
     if (haveK) {
@@ -493,7 +480,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
       const u64 bal = __ballot(in);
       if (in) {
         dacc += digest_term((uint32_t)r, (uint32_t)s, k + (u64)__popcll(bal & ((1ULL << lane) - 1ULL)));
-        eacc += DG[v] >> 16;
+        eacc += DG[v];
       }
       k += (u64)__popcll(bal);
     }
@@ -504,7 +491,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // software pipeline: round r+1's sets, degrees, presence and slots load while
   // round r is processed
   u64 pf0 = 0, pf1 = 0, pp0 = 0, pp1 = 0;
-  uint32_t pd[2] = {0, 0}, psa = 0, psb = 0;
+  uint16_t psd[2] = {0, 0}, pwd[2] = {0, 0};  // (16-bit: no widening right after the loads)
+  uint32_t psa = 0, psb = 0;
   int pslo = 0, pshi = 0;
   auto prefetch4 = [&](int r) {
     pf0 = g_cone[((size_t)r * 2) * 64 + lane];
@@ -512,7 +500,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
-      pd[i] = g_deg[(size_t)r * n + (v < n ? v : 0)];  // (a lane past n: never read)
+      const size_t at = (size_t)r * n + (v < n ? v : 0);  // (a lane past n: never read)
+      psd[i] = g_sdeg[at];
+      pwd[i] = g_wdeg[at];
     }
     pp0 = pres_word(r, 0);
     pp1 = pres_word(r, 1);
@@ -530,7 +520,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
-      if (v < n) DG[v] = pd[i];
+      if (v < n) DG[v] = (uint32_t)psd[i] + (uint32_t)pwd[i];  // strong + weak degree
     }
     if (r < T) prefetch4(r + 1);
     __syncthreads();

@@ -3851,6 +3851,7 @@ int replay_batch_impl(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode,
       J.wc_rows = c->wc_rows.as<u64>();
       J.wc_roff = c->wc_roff.as<uint32_t>();
       J.wdeg = c->wdeg.as<uint16_t>();
+      J.sdeg = c->sdeg.as<uint16_t>();
       J.slot_off = c->slot_off.as<uint32_t>();
       J.slot_src = c->slot_src.as<uint16_t>();
       J.lead = c->lead.as<uint16_t>();
