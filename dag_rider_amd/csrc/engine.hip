@@ -1067,8 +1067,10 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   c->WS = next_pow2(c->W);
   c->max_rounds = max_rounds;
   c->dev = device;
-  if (set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+  // (stream2 is created at the first fork, ensure_stream2: a context that never forks --
+  // one DAG of a C5 batch -- keeps one HIP stream, and a device-wide synchronize walks
+  // every stream of the process: 4096 contexts x 2 streams cost it ~2.7 ms)
+  if (set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     g_create_err = "dr_create: stream creation failed";
     delete c;
     return DR_E_HIP;
@@ -1824,6 +1826,11 @@ int prep_query(dr_ctx *c) {
 // waits on an event of the main stream (build_summary's).
 // prefix = false: the caller's emitting sweep computes the G, E prefixes.
 // spec: RG holds every round's speculative digest (build_summary's weak union).
+// the second stream, created at the first fork (dr_create)
+inline hipError_t ensure_stream2(dr_ctx *c) {
+  return c->stream2 ? hipSuccess : hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+}
+
 int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool forked = false,
                  bool incremental = false, bool prefix = true, bool spec_rg = false) {
   const int T = c->nrounds - 1;
@@ -1839,6 +1846,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
     Swap(dr_ctx *c_, bool on_) : c(c_), on(on_) { if (on) std::swap(c->stream, c->stream2); }
     ~Swap() { if (on) std::swap(c->stream, c->stream2); }
   };
+  if (fork) HIPCHK(c, ensure_stream2(c));
   if (fork && !forked) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
@@ -1929,6 +1937,7 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
   }
   if (!(parts & 2)) return DR_OK;
   const bool early = fork && side;
+  if (early) HIPCHK(c, ensure_stream2(c));
   if (early) {  // stream2's work (side) needs only the rows' summaries and commits: fork here,
     // on the summary's end event when it is recorded anyway (each event costs the
     // stream ~7 us: profiles/r02/v34_timeline.txt)
