@@ -16,7 +16,7 @@ LIBT      := $(PKG)/libdagrider_gpu_timing.so
 ORACLE    := oracle/liboracle.so
 BUILD     := build
 
-.PHONY: all lib oracle clean tests-cpp timing
+.PHONY: all lib oracle clean tests-cpp timing FORCE
 all: lib oracle tests-cpp timing
 timing: $(LIBT)
 
@@ -47,13 +47,26 @@ $(BUILD)/engine_timing.o: $(ENGINE_DEPS) | $(BUILD)
 $(BUILD)/shard_timing.o: $(SHARD_DEPS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DDR_SWEEP_TIMING -c $< -o $@
 
-$(LIBT): $(BUILD)/engine_timing.o $(BUILD)/shard_timing.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o
+$(LIBT): $(BUILD)/engine_timing.o $(BUILD)/shard_timing.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o $(BUILD)/build_id.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdagrider_gpu_timing.so
 
 $(BUILD)/shard.o: $(SHARD_DEPS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/engine.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o
+# provenance: dr_build_id() returns the sha256 (first 16 hex digits) of every source
+# the library is built from, in byte order of their paths -- the same hash
+# dag_rider_amd/_lib.py source_hash() computes from a tree, so a prebuilt library can be
+# matched to the sources it claims.  build_id.c is rewritten only when the hash changes.
+ID_SRCS  := $(sort $(wildcard $(PKG)/csrc/*.hip $(PKG)/csrc/*.hpp $(PKG)/csrc/*.cpp include/*.h))
+BUILD_ID := $(shell cat $(ID_SRCS) | sha256sum | cut -c1-16)
+$(BUILD)/build_id.c: FORCE | $(BUILD)
+	@echo 'const char *dr_build_id(void) { return "$(BUILD_ID)"; }' > $@.tmp
+	@if cmp -s $@.tmp $@; then rm -f $@.tmp; else mv $@.tmp $@; fi
+$(BUILD)/build_id.o: $(BUILD)/build_id.c
+	$(CC) -O2 -fPIC -c $< -o $@
+FORCE:
+
+$(LIB): $(BUILD)/engine.o $(BUILD)/shard.o $(BUILD)/dag_gen.o $(BUILD)/wire.o $(BUILD)/host_rounds.o $(BUILD)/build_id.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lgomp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdagrider_gpu.so
 
 $(ORACLE): oracle/ref_literal.c oracle/ref_bitset.c oracle/oracle.h

@@ -100,6 +100,15 @@ def measured_traffic(phase, W: int = 16, config: str = "c4"):
     return None, None
 
 
+def emit_line(out: dict) -> None:
+    """Print a bench line with the library's provenance (dr_build_id next to this tree's
+    source hash: a prebuilt library must match the sources it is reported against)."""
+    from dag_rider_amd import _lib as L
+
+    out.setdefault("provenance", L.provenance())
+    print(json.dumps(out), flush=True)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -944,7 +953,7 @@ def main() -> int:
     if args.config == "c5":
         out = run_c5(args, rank, world, local, dist)
         if out is not None:
-            print(json.dumps(out), flush=True)
+            emit_line(out)
         if dist:
             dist.destroy_process_group()
         return 0
@@ -952,13 +961,13 @@ def main() -> int:
         if world > 1 or args.config != "c4":
             log("[bench] --rank-share is a single-GPU line of the C4 commit split")
             return 2
-        print(json.dumps(run_rank_share(args, local)), flush=True)
+        emit_line(run_rank_share(args, local))
         return 0
     if args.config == "c4-loop":
         if world > 1:
             log("[bench] c4-loop is a single-GPU latency line")
             return 2
-        print(json.dumps(run_loop(args, local)), flush=True)
+        emit_line(run_loop(args, local))
         return 0
 
     cfg = rank_config(CONFIGS[args.config], rank, world)
@@ -1102,7 +1111,7 @@ def main() -> int:
         out = c4_multi_line(args, world, colshard, dict(value=out["value"], ms_per_step=ms_per_step,
                                                         roofline=out["roofline"], edges_per_step=res.total_edges,
                                                         verify_vs_oracle=verify), split)
-    print(json.dumps(out), flush=True)
+    emit_line(out)
     if dist:
         dist.destroy_process_group()
     return 0

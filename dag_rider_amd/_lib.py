@@ -32,6 +32,7 @@ DR_SHARD_OPT_PERSISTENT = 1
 DR_SHARD_OPT_MEMO = 2
 DR_SHARD_OPT_STEPPED = 3
 DR_SHARD_OPT_PHASE_TIMING = 4
+DR_SHARD_OPT_STEP_HINTS = 5
 
 P = C.c_void_p
 i32, u32, i64, u64, f32 = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_float
@@ -61,6 +62,7 @@ class ReplayView(C.Structure):
 # symbol -> (restype, argtypes); every symbol declared in include/*.h
 SIGNATURES = {
     "dr_abi_version": (C.c_int, []),
+    "dr_build_id": (C.c_char_p, []),
     "dr_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)]),
     "dr_destroy": (None, [P]),
     "dr_last_error": (C.c_char_p, [P]),
@@ -148,6 +150,36 @@ def lib() -> C.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def source_hash(root: str | None = None) -> str:
+    """The hash the Makefile stamps into dr_build_id(): sha256 (first 16 hex digits) of
+    dag_rider_amd/csrc/*.{hip,hpp,cpp} and include/*.h, concatenated in byte order of
+    their paths.  Equal to build_id() when the library was built from this tree."""
+    import glob
+    import hashlib
+
+    root = root or os.path.dirname(_HERE)
+    paths = []
+    for pat in ("dag_rider_amd/csrc/*.hip", "dag_rider_amd/csrc/*.hpp", "dag_rider_amd/csrc/*.cpp", "include/*.h"):
+        paths += glob.glob(pat, root_dir=root)
+    h = hashlib.sha256()
+    for p in sorted(paths):
+        with open(os.path.join(root, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    """dr_build_id(): the source hash the library was built from."""
+    return lib().dr_build_id().decode()
+
+
+def provenance() -> dict:
+    """The loaded library's build id next to this tree's source hash (a prebuilt library
+    pushed to the GPU box must match the sources it runs beside)."""
+    b, s = build_id(), source_hash()
+    return {"build_id": b, "source_hash": s, "match": b == s, "lib": LIB_PATH}
 
 
 class DrError(RuntimeError):

@@ -163,12 +163,9 @@ struct dr_ctx {
   // the lowest round holding an edge to the same or a later round (INT_MAX: none): a
   // general sweep toward a target in round t never needs the rounds below t unless some
   // path climbs back from there, which only such an edge below t allows
-  int min_up_round() const {
-    if (nirr_up == 0) return INT_MAX;
-    for (int r = 0; r < (int)h_rup.size(); r++)
-      if (h_rup[r]) return r;
-    return INT_MAX;
-  }
+  // (cached in up_min: upload_suffix recomputes it from the lowest round it rewrote)
+  int up_min = INT_MAX;
+  int min_up_round() const { return nirr_up == 0 ? INT_MAX : up_min; }
   int gsweep_bottom(int t) const { return (t >= 0 && min_up_round() >= t) ? t : 0; }
   // every exception known benign (the last test covers every round)
   bool exc_clear() const { return nexc == 0 || (exc_lo >= nrounds && nbad == 0); }
@@ -328,6 +325,22 @@ struct dr_ctx {
     return e;
   }
   bool async_pending = false;  // an append returned before its copies ran (dr_replay_batch waits)
+  // A host wait: poll the event for up to kSpinUs (a per-call query's results are
+  // usually back within tens of microseconds, and an interrupt round trip costs more),
+  // then block in hipEventSynchronize, so a long wait does not hold a host core.
+  static constexpr int kSpinUs = 200;
+  static hipError_t wait_event(hipEvent_t ev) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipEventQuery(ev);
+      if (e != hipErrorNotReady) return e;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) return hipEventSynchronize(ev);
+      std::this_thread::yield();
+    }
+  }
+  // the append whose copies may still be in flight (a HIP error before the next completed
+  // wait names it: fail() appends it to the message)
+  std::string async_what;
   hipError_t sync() {
     async_pending = false;
     hipError_t e = flush_h2d();
@@ -344,16 +357,12 @@ struct dr_ctx {
     }
     if (e == hipSuccess) e = hipEventRecord(ev_sync, stream);
     if (e == hipSuccess && stream2) e = hipEventRecord(ev_sync2, stream2);
+    if (e == hipSuccess) e = wait_event(ev_sync);
+    if (e == hipSuccess && stream2) e = wait_event(ev_sync2);
     if (e == hipSuccess) {
-      while ((e = hipEventQuery(ev_sync)) == hipErrorNotReady) {
-      }
-    }
-    if (e == hipSuccess && stream2) {
-      while ((e = hipEventQuery(ev_sync2)) == hipErrorNotReady) {
-      }
-    }
-    if (e == hipSuccess)
       for (auto &p : pend) std::memcpy(p.dst, p.stage, p.n);
+      async_what.clear();
+    }
     pend.clear();
     pin_used = 0;
     return e;
@@ -406,6 +415,7 @@ struct dr_ctx {
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
     err = buf;
+    if (code == DR_E_HIP && !async_what.empty()) err += " (pending before this call: " + async_what + ")";
     return code;
   }
   dr::MemoView memo_view() const {
@@ -544,6 +554,14 @@ struct dr_ctx {
         for (int r = lo; r < R; r++) dreg = std::max(dreg, h_rdreg[r]);
       }
       nirr_down = nirr - nirr_up;
+      if (up_min >= lo) {  // rounds below lo kept their counts
+        up_min = INT_MAX;
+        for (int r = lo; r < R; r++)
+          if (h_rup[r]) {
+            up_min = r;
+            break;
+          }
+      }
     }
     const size_t s0 = h_slot_off[lo], s1 = h_slot_off[R], k0 = h_wc_roff[lo], k1 = h_wc_roff[R];
     const size_t f0 = h_far_roff[lo], f1 = h_far_roff[R];
@@ -1252,6 +1270,11 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   // load's rows went straight from the caller's memory: wait for them.)
   HIPCHK(c, staged ? c->flush_h2d() : c->sync());
   c->async_pending = staged;
+  if (staged) {
+    char what[96];
+    std::snprintf(what, sizeof what, "the copies of dr_append_rounds_packed rounds %d..%d", r0, r0 + k - 1);
+    c->async_what = what;
+  }
   const auto ta4 = std::chrono::steady_clock::now();
   auto ms = [](auto a, auto b) { return std::chrono::duration<float, std::milli>(b - a).count(); };
   c->append_phases[0] = ms(ta0, ta1);  // validation + host rounds (weak columns)

@@ -600,6 +600,9 @@ struct dr_shard {
   // stepped form: the canonical walk's query; S_1 per wave (k_ms_lcol; RCCL mode: the
   // exchanged partials, lcol_g slots of lcol_nw waves), valid until an append or a coin change
   SBuf mcq, mlcol, mlcolp;
+  // the stepped canonical walk's own pending ring and exchanged frontiers: a walk resumed
+  // after the batch steps ran (a continuation, replay_memo) finds them as it left them
+  SBuf cpend, crecv[2], csend;
   bool lcol_ok = false;
   int lcol_nw = 1, lcol_g = 1;
   uint64_t lead_version = 0;  // bumped by every coin change
@@ -1278,15 +1281,18 @@ int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MSt
                  int batch) {
   const int WL = c->nlocal * c->WSs;
   const size_t lds = ((size_t)c->depth * WL + c->W) * 8;
-  SHCHK(c, c->mpend.ensure((size_t)std::max(nq, 1) * c->depth * WL * 8));
-  SHCHK(c, c->mrecv[0].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
-  SHCHK(c, c->mrecv[1].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
-  SHCHK(c, c->msend.ensure((size_t)std::max(nq, 1) * c->WSs * 8));
+  // the canonical walk (batch 0, one query) and the batch steps keep separate buffers
+  SBuf &pend = batch ? c->mpend : c->cpend, &send = batch ? c->msend : c->csend;
+  SBuf *recv = batch ? c->mrecv : c->crecv;
+  SHCHK(c, pend.ensure((size_t)std::max(nq, 1) * c->depth * WL * 8));
+  SHCHK(c, recv[0].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
+  SHCHK(c, recv[1].ensure((size_t)c->G * std::max(nq, 1) * c->WSs * 8));
+  SHCHK(c, send.ensure((size_t)std::max(nq, 1) * c->WSs * 8));
   drs::MArgs b = a;
-  b.pend = c->mpend.as<u64>();
+  b.pend = pend.as<u64>();
   for (int j = j0; j < j1; j++) {
-    u64 *rin = c->mrecv[j & 1].as<u64>();
-    u64 *rout = c->local ? c->mrecv[(j + 1) & 1].as<u64>() : c->msend.as<u64>();
+    u64 *rin = recv[j & 1].as<u64>();
+    u64 *rout = c->local ? recv[(j + 1) & 1].as<u64>() : send.as<u64>();
     if (c->step_nt == 128)
       hipLaunchKernelGGL((drs::k_ms_step2<128>), dim3(nq), dim3(128), lds, c->stream, b, f, j, st, (const u64 *)rin,
                          rout, batch);
@@ -1295,8 +1301,7 @@ int launch_steps(dr_shard *c, const drs::MArgs &a, const drs::FArgs &f, drs::MSt
                          rout, batch);
     SHCHK(c, hipGetLastError());
     if (!c->local) {
-      SHNCCL(c, ncclAllGather(c->msend.p, c->mrecv[(j + 1) & 1].p, (size_t)nq * c->WSs, ncclUint64, c->comm,
-                              c->stream));
+      SHNCCL(c, ncclAllGather(send.p, recv[(j + 1) & 1].p, (size_t)nq * c->WSs, ncclUint64, c->comm, c->stream));
       c->last_xbytes += (uint64_t)nq * c->WSs * 8;
     }
     c->last_rounds++;
@@ -1841,7 +1846,7 @@ extern "C" void dr_shard_destroy(dr_shard *c) {
   for (SBuf *b : {&c->wck, &c->wcr, &c->wcro, &c->sdr, &c->mU, &c->mWU, &c->mK, &c->mgood, &c->mRD, &c->mCE, &c->mRG,
                   &c->mC, &c->mE, &c->mG, &c->mksend, &c->mkrecv, &c->mq, &c->mpend, &c->mrecv[0],
                   &c->mrecv[1], &c->msend, &c->mmasks, &c->mpush, &c->mqidx, &c->mqout, &c->ppref, &c->mSG,
-                  &c->mout, &c->mcq, &c->mlcol, &c->mlcolp})
+                  &c->mout, &c->mcq, &c->mlcol, &c->mlcolp, &c->cpend, &c->crecv[0], &c->crecv[1], &c->csend})
     b->release();
   if (c->pin) (void)hipHostFree(c->pin);
   for (SBuf *b : {&c->strong, &c->weak, &c->woff, &c->ft[0], &c->ft[1], &c->send, &c->pend, &c->cnt, &c->out,
@@ -1885,6 +1890,11 @@ extern "C" int dr_shard_set_option(dr_shard *c, int option, int value) {
   }
   if (option == DR_SHARD_OPT_PHASE_TIMING) {
     c->phase_timing = value ? 1 : 0;
+    return DR_OK;
+  }
+  if (option == DR_SHARD_OPT_STEP_HINTS) {
+    if (value < 1) return c->fail(DR_E_INVAL, "step hint %d < 1", value);
+    c->hint_canon = c->hint_batch = value;
     return DR_OK;
   }
   return c->fail(DR_E_INVAL, "unknown option %d", option);
@@ -1974,7 +1984,10 @@ extern "C" int dr_shard_append_rounds_packed(dr_shard *c, int r0, int k, const u
       rd[i] += d + (eb - ea);
       for (uint32_t e = ea; e < eb; e++) {
         const uint32_t t = weak_tgt[e];
-        const int tr = (int)(t >> 11), ts = (int)(t & 2047u);
+        const int tr = (int)((t >> 11) & 0xFFFFFu), ts = (int)(t & 2047u);
+        if (t >> 31)  // dagrider_gpu.h: bit 31 marks a strong edge outside r-1 (App. A Q8)
+          return c->fail(DR_E_CONTRACT, "strong edge (%d,%d)->(%d,%d) outside r-1: not supported by dr_shard", r,
+                         s0 + 1, tr, ts + 1);
         if (ts >= n) return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d): source > n", r, s0 + 1, tr, ts + 1);
         if (tr > r - 2) return c->fail(DR_E_CONTRACT, "weak edge (%d,%d)->(%d,%d) must target a round < r-1", r, s0 + 1, tr, ts + 1);
         const int delta = r - tr;

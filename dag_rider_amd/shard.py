@@ -157,6 +157,11 @@ class ShardEngine:
         """DR_SHARD_OPT_PHASE_TIMING: per-phase device times in the replay's ms_* (default on)."""
         self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_PHASE_TIMING, int(on)))
 
+    def set_step_hints(self, steps: int):
+        """DR_SHARD_OPT_STEP_HINTS: the stepped form's initial step counts (1 forces every
+        continuation of a live canonical walk or query)."""
+        self._check(self._L.dr_shard_set_option(self._h, L.DR_SHARD_OPT_STEP_HINTS, int(steps)))
+
     def set_leader_coin(self, mode: int = L.DR_LEADER_CONST1, seed: int = 0,
                         table: Optional[Sequence[int]] = None):
         """chooseLeader (process.go:386-392), as Engine.set_leader_coin."""

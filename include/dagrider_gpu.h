@@ -66,6 +66,10 @@ int dr_abi_version(void);
 int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx **out);
 void dr_destroy(dr_ctx *ctx);
 const char *dr_last_error(const dr_ctx *ctx);
+/* Provenance: the sha256 (first 16 hex digits) of the sources this library was built
+ * from (dag_rider_amd/csrc/{*.hip,*.hpp,*.cpp} and include/{*.h}, concatenated in byte
+ * order of their paths), stamped by the Makefile.  Static string, never NULL. */
+const char *dr_build_id(void);
 /* number of rounds currently mirrored (len(p.dag)) */
 int dr_num_rounds(const dr_ctx *ctx);
 /* chooseLeader(w) (process.go:386-392): "a global perfect coin"; the

@@ -59,8 +59,11 @@ int dr_shard_info(const dr_shard *ctx, int *nshards, int *shard0, int *nlocal, i
 
 /* p.dag[r] = append(...) (process.go:229): dr_append_rounds_packed's arguments and
  * contract; the context keeps only its columns.  Weak edges must satisfy
- * r - r' <= 1023, and an id may not repeat within a round >= 1 (else
- * DR_E_CONTRACT; repeated ids replay on the unsharded engine). */
+ * 2 <= r - r' <= 1023, and an id may not repeat within a round >= 1 (else
+ * DR_E_CONTRACT; repeated ids replay on the unsharded engine).  The packed
+ * format's irregular entries -- bit 31 of weak_tgt, a strong edge outside r-1,
+ * and weak edges to r-1 or above (App. A Q8) -- are not supported here either
+ * (DR_E_CONTRACT naming the edge); dr_append_rounds_packed takes them. */
 int dr_shard_append_rounds_packed(dr_shard *ctx, int r0, int k, const uint32_t *slot_off, const uint16_t *slot_src,
                                   const uint64_t *strong, const uint32_t *weak_off, const uint32_t *weak_tgt);
 
@@ -95,6 +98,12 @@ int dr_shard_path_batch(dr_shard *ctx, int q, const int32_t *from, const int32_t
  * between its phases and reports them in dr_replay_out.ms_*; 0 leaves them 0
  * (reading the events back costs the host ~20 us per replay). */
 #define DR_SHARD_OPT_PHASE_TIMING 4
+/* DR_SHARD_OPT_STEP_HINTS (tuning and tests): the stepped form launches as many
+ * steps of the canonical walk and of the query batch as the last replay needed
+ * (8 and 12 before the first) and continues a query still live after them; value
+ * (>= 1) resets both counts, e.g. 1 forces every continuation path.  Results are
+ * identical. */
+#define DR_SHARD_OPT_STEP_HINTS 5
 int dr_shard_set_option(dr_shard *ctx, int option, int value);
 
 /* chooseLeader (process.go:386-392): dr_set_leader_coin's modes and semantics. */

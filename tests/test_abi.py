@@ -73,3 +73,11 @@ def test_oracle_not_linked_by_product():
             if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
                 txt = open(os.path.join(root, f)).read()
                 assert "import oracle" not in txt and "from oracle" not in txt and "oracle.h" not in txt, f
+
+
+def test_build_id_matches_tree():
+    """dr_build_id() (the source hash the Makefile stamps) equals the hash of this tree's
+    sources: the library under test was built from them, not left over from other ones."""
+    p = _lib.provenance()
+    assert len(p["build_id"]) == 16 and int(p["build_id"], 16) >= 0
+    assert p["match"], p

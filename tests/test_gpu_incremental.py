@@ -208,3 +208,39 @@ def test_gpu_wave_loop_matches_replay(gpu_device, cfg_name):
     assert commit == ref.commit.astype(bool).tolist()
     assert pushes == ref.push_wave.tolist()
     assert pc == ref.pop_count.tolist() and pdg == ref.pop_digest.tolist()
+
+
+@pytest.mark.gpu
+def test_staged_packed_append_then_queries(gpu_device):
+    """A per-round packed append returns before its copies run: the next call
+    on the context -- path, waveReady, orderVertices, or destroy -- runs behind them on the
+    same stream.  Appends of 4 rounds at a time, each followed at once by queries against
+    the literal oracle on the prefix; the last append is followed by destroy alone."""
+    from dag_rider_amd.gen import generate, small_config
+
+    cfg = small_config(100, 48, 77, p_present=0.95, p_late=0.2, p_w=0.4, weak_depth=6)
+    d = generate(cfg)
+    rng = np.random.default_rng(13)
+    with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
+        e.append_packed(d, 0, 1)
+        r1 = 1
+        while r1 + 4 <= d.nrounds - 4:
+            e.append_packed(d, r1, r1 + 4)
+            r1 += 4
+            ld = oracle.LDag(packed=d, nrounds=r1)
+            pairs = []
+            for _ in range(16):
+                ra = int(rng.integers(1, r1))
+                srcs = d.slot_src[d.slot_off[ra]:d.slot_off[ra + 1]]
+                srcs = srcs[srcs != 0]
+                if len(srcs):
+                    a = (ra, int(srcs[int(rng.integers(0, len(srcs)))]))
+                    pairs.append((a, (int(rng.integers(0, ra + 1)), int(rng.integers(1, cfg.n + 1)))))
+            assert e.path_batch(pairs, False).tolist() == [ld.path(a, b, False) for a, b in pairs]
+            w = (r1 - 1) // 4
+            if w >= 1:
+                rc, vc, st = ld.wave_ready(cfg.faulty, w, 0)
+                assert rc == 0
+                commit, vcount, pushed = e.wave_ready(w, 0)
+                assert vcount == vc and commit == (len(st) > 0)
+        e.append_packed(d, r1, d.nrounds)  # then destroy with the copies possibly in flight

@@ -146,6 +146,14 @@ def test_shard_errors(gpu_device):
         with pytest.raises(L.DrError) as ei:
             se.append_packed(d, 2, 3)  # not contiguous
         assert ei.value.code == L.DR_E_STATE
+    # a strong edge outside r-1 (bit 31 of weak_tgt) is named as unsupported, with its round
+    from dag_rider_amd.gen import with_extra_edges
+    d2 = with_extra_edges(d, [(4, 1, 1, 2, True)])
+    with ShardEngine(g["n"], g["faulty"], 8, gpu_device, nshards=2) as se:
+        with pytest.raises(L.DrError) as ei:
+            se.append_packed(d2)
+        assert ei.value.code == L.DR_E_CONTRACT
+        assert "strong edge (4,1)->(1,2) outside r-1" in str(ei.value)
 
 
 # --------------------------------------------------------------------------- commit + delivery
@@ -268,6 +276,31 @@ def test_shard_stepped_steps_on_after_append(gpu_device):
             bl = oracle.PDag(d, leaders=leaders)
             for cm, dm in MODES:
                 _same_replay(se.replay(cfg.nwaves, cm, dm), bl.replay(f, cfg.nwaves, cm, dm))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_shard_stepped_canon_continuation(gpu_device, seed):
+    """A canonical walk still live after the launched steps resumes after the batch steps
+    ran (the walk and the batch shared their pending ring and frontier buffers).
+    Step hints of 1 force the continuation on a first replay whose walk has several
+    segments; every mode against the bitset oracle at G = 1 and 3."""
+    rng = np.random.default_rng(6100 + seed)
+    n, R = int(rng.choice([64, 130, 200])), 60
+    d = random_dag(rng, n, R, p_present=0.85, p_s=0.35, p_w=0.5, max_depth=8)
+    f = (n - 1) // 3
+    nw = R // 4
+    bs = oracle.PDag(d)
+    segs = 0
+    for G in (1, 3):
+        for cm, dm in MODES:
+            with ShardEngine(n, f, R + 1, gpu_device, nshards=G) as se:
+                se.append_packed(d)
+                se.set_stepped(True)
+                se.set_step_hints(1)
+                got = se.replay(nw, cm, dm)
+                _same_replay(got, bs.replay(f, nw, cm, dm))
+                segs = max(segs, got.sweep["canon_segments"])
+    assert segs >= 2  # the walk had more than one segment to continue through
 
 
 def test_shard_replay_leader_coin(gpu_device):
