@@ -472,6 +472,165 @@ def run_rank_share(args, local: int):
     }
 
 
+def wsplit_share_bytes(p, n: int, W: int) -> int:
+    """Algorithmic bytes of one slice's row pass (k_summary_commit): every strong row of
+    slice rounds 1..top once, plus U and SD (bench kernel_bytes 'summary')."""
+    T = p.nrounds - 1
+    return T * n * W * 8 + T * W * 8 + 8 * T
+
+
+def run_wave_split_shares(args, local: int):
+    """--wave-split N on one GPU: the whole C4 replay split into N wave ranges
+    (dag_rider_amd/split.py), every rank's slice on its own mirror, timed one after another
+    on this GPU (what each of N GPUs runs), combined with the exchange done in memory and
+    checked against the unsharded replay; the line reports the slowest share."""
+    import numpy as np
+    import torch
+
+    from dag_rider_amd import _lib as L
+    from dag_rider_amd.engine import Engine
+    from dag_rider_amd.gen import CONFIGS, generate
+    from dag_rider_amd.split import (SliceRank, check_and_offsets, combine_slices, owned_part, presence_prefix,
+                                     slice_plans)
+
+    cfg = CONFIGS["c4"]
+    d = generate(cfg, nthreads=CPU_THREADS)
+    N = args.wave_split
+    plans = slice_plans(d, cfg.nwaves, N, halo=args.halo)
+    gp = presence_prefix(d)
+    ranks = [SliceRank(d, p, cfg.faulty, local, None, gp) for p in plans]
+    shares, outs = [], []
+    steps = max(args.steps, 1)
+    for sr in ranks:
+        sr.eng.set_phase_timing(1)
+        for _ in range(max(args.warmup, 1)):
+            sr.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ms_sum = 0.0
+        for _ in range(steps):
+            sr.step()
+            ms_sum += sr.step.ms_summary
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        res, sres = sr.step.result(), sr.eng.slice_result()
+        res = dataclasses.replace(res, **{k: getattr(res, k).copy() for k in
+                                          ("commit", "vcount", "push_off", "push_wave", "pop_count", "pop_digest",
+                                           "pop_edges")})
+        outs.append((res, sres))
+        p = sr.p
+        nb = wsplit_share_bytes(p, cfg.n, d.W)
+        km = ms_sum / steps
+        shares.append(dict(rank=p.rank, w0=p.w0, w1=p.w1, wf=p.wf, rounds=[p.off, p.top], seeded=p.seeded,
+                           ms=dt * 1e3, summary_kernel_ms=km, row_bytes=nb,
+                           GBps_summary=nb / (km / 1e3) / 1e9 if km > 0 else None,
+                           pops_own=int(res.push_off[p.nwaves]) - int(res.push_off[p.own_w0 - 1])))
+    summ = np.stack([sr.summary(*o) for sr, o in zip(ranks, outs)])
+    offs, redo = check_and_offsets(plans, summ)
+    for k, base in redo.items():  # (C4: never -- its canonical cone is full below the top)
+        ranks[k].rebase(base)
+        ranks[k].step()
+        outs[k] = (ranks[k].step.result(), ranks[k].eng.slice_result())
+        summ[k] = ranks[k].summary(*outs[k])
+    if redo:
+        offs, _ = check_and_offsets(plans, summ)
+    got = combine_slices([owned_part(p, o[0], *off) for p, o, off in zip(plans, outs, offs)], summ)
+    for sr in ranks:
+        sr.close()
+    with Engine(cfg.n, cfg.faulty, d.nrounds, local) as e:
+        e.append_packed(d)
+        want = e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+    ok = same_replay(got, want)
+    slow = max(shares, key=lambda x: x["ms"])
+    # the slowest share's edges: its owned commits, chains and pops
+    k = slow["rank"]
+    S = summ[k]
+    from dag_rider_amd.split import SUMMARY_FIELDS as F
+
+    pa, pb = int(got.push_off[plans[k].w0 - 1]), int(got.push_off[plans[k].w1])
+    share_edges = int(S[F.index("commit_edges")]) + int(S[F.index("own_chain_edges")]) + \
+        int(np.asarray(got.pop_edges[pa:pb], np.uint64).sum(dtype=np.uint64))
+    km = slow["summary_kernel_ms"]
+    return {
+        "metric": "DAG edges traversed/sec (commit+delivery, one rank's wave range of the whole replay)",
+        "value": share_edges / (slow["ms"] / 1e3),
+        "unit": "edges/s",
+        "n_gpus": 1,
+        "steps": steps,
+        "warmup": max(args.warmup, 1),
+        "ms_per_step": slow["ms"],
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded generator, SURVEY.md s8(d) C4 parameters)",
+        "config": {"workload": f"C4 full replay (waveReady persistent + orderVertices REF) split into {N} wave "
+                               f"ranges (dag_rider_amd/split.py): each share on its own mirror of its rounds "
+                               f"({args.halo}-wave halo below, dmax rounds above, seeded full); line = slowest "
+                               f"share, exchange excluded (one all-gather of 13 words + the gather of the pops "
+                               f"per replay in the N-GPU line)",
+                   "n": cfg.n, "rounds": cfg.last_round, "waves": cfg.nwaves, "parallelism": f"wavesplit{N}"},
+        "roofline": {"bound": "hbm", "achieved": slow["row_bytes"] / (km / 1e3) / 1e9 if km > 0 else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": slow["row_bytes"] / (km / 1e3) / 1e9 / HBM_PEAK_GBS if km > 0 else None,
+                     "traffic": None, "kernel": "k_summary_commit over the slowest share's slice",
+                     "bytes_per_launch": slow["row_bytes"], "ms_per_launch": km},
+        "cpu_baseline": None,
+        "detail": {"shares": shares, "verify_vs_unsharded": ok, "share_edges_slowest": share_edges,
+                   "whole_replay_edges": int(got.commit_edges + got.chain_edges + got.deliver_edges),
+                   "rebased_ranks": sorted(redo), "ms_max_over_shares": slow["ms"]},
+    }
+
+
+def wsplit_run(dist, rank: int, world: int, local: int, steps: int, warmup: int, halo: int):
+    """The N-GPU wave-split replay of the ONE seed-4 C4 DAG: this rank's slice mirror,
+    warm-up steps, a barrier, then exactly `steps` timed steps of dist_split_step (the
+    slice replay, the 13-word all-gather over RCCL, offsets, the gather of the owned
+    pops); rank 0 checks the combined replay against the unsharded engine.  Returns
+    rank 0's view (None elsewhere); errors are reported, not raised."""
+    import torch
+
+    from dag_rider_amd import _lib as L
+    from dag_rider_amd.gen import CONFIGS, generate
+    from dag_rider_amd.split import SliceError, SliceRank, dist_split_step, presence_prefix, slice_plans
+
+    cfg = CONFIGS["c4"]
+    d = generate(cfg, nthreads=CPU_THREADS)
+    dev = torch.device("cuda", local)
+    err = None
+    try:
+        plans = slice_plans(d, cfg.nwaves, world, halo=halo)
+        sr = SliceRank(d, plans[rank], cfg.faulty, local, None, presence_prefix(d))
+        sr.eng.set_phase_timing(0)
+        for _ in range(max(warmup, 1)):
+            got, summ = dist_split_step(dist, sr, plans, dev)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            got, summ = dist_split_step(dist, sr, plans, dev)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        sr.close()
+    except SliceError as ex:
+        err, dt = f"SliceError: {ex}", 0.0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank != 0:
+        return None
+    if err:
+        return dict(error=err)
+    from dag_rider_amd.engine import Engine
+
+    with Engine(cfg.n, cfg.faulty, d.nrounds, local) as e:
+        e.append_packed(d)
+        want = e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+    ms = float(t.item()) / steps * 1e3
+    edges = int(got.commit_edges + got.chain_edges + got.deliver_edges)
+    return dict(ms=ms, edges=edges, verify_vs_unsharded=same_replay(got, want), world=world, halo=halo,
+                ranges=[(p.w0, p.w1) for p in plans])
+
+
 def colshard_child(args):
     """One rank of the process-column sharded C4 replay (BASELINE.json configs[3],
     SURVEY.md s8(e)): every rank holds 1/N of the target columns of the ONE seed-4 C4
@@ -542,7 +701,7 @@ def colshard_run(dist, rank: int, world: int, local: int, steps: int, warmup: in
     return allr
 
 
-def c4_multi_line(args, world: int, cs_all, replicas, split):
+def c4_multi_line(args, world: int, cs_all, replicas, split, wsplit=None):
     """The N > 1 line of the C4 config: the column-sharded replay of ONE C4 DAG
     (strong scaling: the same 1.75e12 edges per step whatever N; BASELINE.json
     configs[3] "process-column sharded across 2/4/8 GPUs with RCCL frontier
@@ -572,6 +731,27 @@ def c4_multi_line(args, world: int, cs_all, replicas, split):
     rep_detail = dict(replicas, parallelism=f"replicas{world}", scaling="weak",
                       note="every rank replays its own C4 DAG (seed 4 + rank), unsharded; value = summed edges / "
                            "slowest rank")
+    cs_detail = dict(ok=ok and verified, ranks=cs_all,
+                     ms=max(r["ms"] for r in cs_all) if ok and verified else None)
+    if wsplit is not None and "error" not in wsplit and wsplit.get("verify_vs_unsharded"):
+        ms = wsplit["ms"]
+        return dict(base, **{
+            "value": wsplit["edges"] / (ms / 1e3),
+            "ms_per_step": ms,
+            "scaling": "strong",
+            "config": {"workload": "C4 full replay of ONE DAG (n=1024 x 4000 rounds, seed 4) split into "
+                                   f"{world} wave ranges, one per GPU (dag_rider_amd/split.py): each GPU mirrors "
+                                   f"its waves' rounds plus a {wsplit['halo']}-wave halo below and the dmax rounds "
+                                   "above, replays waveReady (persistent decidedWave) + orderVertices (ref) for its "
+                                   "waves, then one RCCL all-gather of 13 words per rank (canonical prefixes, "
+                                   "checks) and one of the owned pops; value = the whole replay's edges / the "
+                                   "slowest rank's time per step",
+                       "n": 1024, "rounds": 4000, "waves": 1000, "parallelism": f"wavesplit{world}"},
+            "roofline": replicas.get("roofline"),
+            "detail": {"verify_vs_unsharded": True, "wsplit": wsplit, "colshard": cs_detail, "replicas": rep_detail,
+                       "commit_split": split,
+                       "roofline_note": "roofline: rank 0's unsharded replica replay (same kernels, whole DAG)"},
+        })
     if ok and verified:
         ms = max(r["ms"] for r in cs_all)
         edges = cs_all[0]["edges"]
@@ -593,7 +773,7 @@ def c4_multi_line(args, world: int, cs_all, replicas, split):
                          "kernel": "summary phase per rank (k_ms_summary over the rank's columns + K^cand exchange "
                                    "+ canonical segment), rank 0", "bytes_per_launch": rb, "ms_per_launch": summ},
             "detail": {"verify_vs_unsharded": verified, "ranks": cs_all, "replicas": rep_detail,
-                       "commit_split": split},
+                       "commit_split": split, "wsplit": wsplit},
         })
     errs = [r.get("error") if r else "no result" for r in cs_all]
     return dict(base, **{
@@ -604,7 +784,8 @@ def c4_multi_line(args, world: int, cs_all, replicas, split):
                                f"FAILED on this node: {errs}", "n": 1024, "rounds": 4000, "waves": 1000,
                    "parallelism": f"replicas{world}"},
         "roofline": replicas.get("roofline"),
-        "detail": {"colshard_errors": errs, "ranks": cs_all, "replicas": rep_detail, "commit_split": split},
+        "detail": {"colshard_errors": errs, "ranks": cs_all, "replicas": rep_detail, "commit_split": split,
+                   "wsplit": wsplit},
     })
 
 
@@ -908,6 +1089,10 @@ def main() -> int:
     ap.add_argument("--dags", type=int, default=0, help="c5 on one GPU: replay only the first N DAGs")
     ap.add_argument("--rank-share", type=int, default=0,
                     help="one GPU: time every rank's share of the C4 wave-range commit split for N ranks")
+    ap.add_argument("--wave-split", type=int, default=0,
+                    help="one GPU: time every rank's share of the C4 replay split into N wave ranges")
+    ap.add_argument("--halo", type=int, default=8, help="wave split: waves below each rank's range it mirrors")
+    ap.add_argument("--no-wsplit", action="store_true", help="N>1: skip the wave-split replay")
     ap.add_argument("--verify", action="store_true", help="check the replay against the bitset oracle")
     ap.add_argument("--colshard", action="store_true",
                     help="also run the process-column sharded C4 sweep (default on when N>1)")
@@ -962,6 +1147,12 @@ def main() -> int:
             log("[bench] --rank-share is a single-GPU line of the C4 commit split")
             return 2
         emit_line(run_rank_share(args, local))
+        return 0
+    if args.wave_split:
+        if world > 1 or args.config != "c4":
+            log("[bench] --wave-split is a single-GPU line of the C4 replay's wave split")
+            return 2
+        emit_line(run_wave_split_shares(args, local))
         return 0
     if args.config == "c4-loop":
         if world > 1:
@@ -1052,6 +1243,11 @@ def main() -> int:
             colshard = colshard_run(dist, rank, world, local, args.steps, args.warmup)
     if rank == 0 and colshard is not None:
         log(f"[colshard] {colshard}")
+    wsplit = None
+    if world > 1 and args.config == "c4" and not args.no_wsplit:
+        wsplit = wsplit_run(dist, rank, world, local, args.steps, args.warmup, args.halo)
+        if rank == 0:
+            log(f"[wsplit] {wsplit}")
 
     if rank != 0:
         if dist:
@@ -1110,7 +1306,7 @@ def main() -> int:
     if multi:
         out = c4_multi_line(args, world, colshard, dict(value=out["value"], ms_per_step=ms_per_step,
                                                         roofline=out["roofline"], edges_per_step=res.total_edges,
-                                                        verify_vs_oracle=verify), split)
+                                                        verify_vs_oracle=verify), split, wsplit)
     emit_line(out)
     if dist:
         dist.destroy_process_group()

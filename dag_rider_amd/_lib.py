@@ -59,6 +59,16 @@ class ReplayView(C.Structure):
                 ("deliver_edges", u64), ("ms_deliver", f32)]
 
 
+class SliceCfg(C.Structure):
+    _fields_ = [("round_offset", i32), ("seeded_top", i32), ("pos_base", u64), ("own_w0", i32), ("nprobe", i32),
+                ("probe", i32 * 8)]
+
+
+class SliceOut(C.Structure):
+    _fields_ = [("C", u64 * 8), ("G", u64 * 8), ("E", u64 * 8), ("min_stop", i32), ("pad_", i32),
+                ("own_chain_edges", u64)]
+
+
 # symbol -> (restype, argtypes); every symbol declared in include/*.h
 SIGNATURES = {
     "dr_abi_version": (C.c_int, []),
@@ -92,6 +102,8 @@ SIGNATURES = {
     "dr_last_batch_phases": (C.c_int, [P, C.POINTER(f32)]),
     "dr_last_batch_form": (C.c_int, [P]),
     "dr_last_append_phases": (C.c_int, [P, C.POINTER(f32)]),
+    "dr_set_slice": (C.c_int, [P, C.POINTER(SliceCfg)]),
+    "dr_slice_result": (C.c_int, [P, C.POINTER(SliceOut)]),
     # include/dagrider_shard.h
     "dr_shard_unique_id": (C.c_int, [P]),
     "dr_shard_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.POINTER(P)]),

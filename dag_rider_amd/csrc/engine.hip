@@ -163,6 +163,10 @@ struct dr_ctx {
   // the lowest round holding an edge to the same or a later round (INT_MAX: none): a
   // general sweep toward a target in round t never needs the rounds below t unless some
   // path climbs back from there, which only such an edge below t allows
+  // wave-range slice (dr_set_slice): dr_replay only, REF + persistent on the memo path
+  bool slice_on = false;
+  dr_slice_cfg slice{};
+  dr_slice_out slice_res{};
   // (cached in up_min: upload_suffix recomputes it from the lowest round it rewrote)
   int up_min = INT_MAX;
   int min_up_round() const { return nirr_up == 0 ? INT_MAX : up_min; }
@@ -328,8 +332,9 @@ struct dr_ctx {
   // A host wait: poll the event for up to kSpinUs (a per-call query's results are
   // usually back within tens of microseconds, and an interrupt round trip costs more),
   // then block in hipEventSynchronize, so a long wait does not hold a host core.
-  static constexpr int kSpinUs = 200;
+  // (DR_WAIT_SPIN_US overrides the bound: measurement only)
   static hipError_t wait_event(hipEvent_t ev) {
+    static const int kSpinUs = getenv("DR_WAIT_SPIN_US") ? atoi(getenv("DR_WAIT_SPIN_US")) : 200;
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
       const hipError_t e = hipEventQuery(ev);
@@ -449,6 +454,8 @@ struct dr_ctx {
     v.sdx = nirr > 0 ? sdx.as<uint32_t>() : nullptr;
     v.n = n;
     v.nrounds = nrounds;
+    v.roff = slice_on ? slice.round_offset : 0;
+    v.seed_lo = slice_on && slice.seeded_top > 0 ? nrounds - slice.seeded_top : INT_MAX;
     return v;
   }
   bool is_present(int r, int s /*1-based*/) const {
@@ -520,7 +527,7 @@ struct dr_ctx {
       u64 np = 0;
       if (r >= 1)
         for (uint16_t sl : h.slots) np += sl != 0;
-      h_ppref[r] = (r ? h_ppref[r - 1] : 0) + np;
+      h_ppref[r] = (r ? h_ppref[r - 1] : (slice_on ? slice.pos_base : 0)) + np;
       h_slot_off[r + 1] = h_slot_off[r] + (uint32_t)h.slots.size();
       h_wc_roff[r + 1] = h_wc_roff[r] + (uint32_t)h.wc_key.size();
       h_far_roff[r + 1] = h_far_roff[r] + (uint32_t)h.far.size();
@@ -1835,7 +1842,9 @@ int ensure_exceptions(dr_ctx *c) {
 
 // every query entry point: the device, then the exception test of the rounds changed
 // since the last one (general() and memo_on() read its verdict)
-int prep_query(dr_ctx *c) {
+int prep_query(dr_ctx *c, bool slice_ok = false) {
+  if (c->slice_on && !slice_ok)
+    return c->fail(DR_E_STATE, "a sliced context (dr_set_slice) answers dr_replay only");
   if (int rc = set_device(c)) return rc;
   return ensure_exceptions(c);
 }
@@ -3410,7 +3419,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   // outputs: the emitting sweep's final pass packs them into one device region, which comes back
   // in one copy (writing them straight into pinned host memory from the kernel
   // took 19.5 us, profiles/r02/v27_timeline.txt)
-  const size_t h_bytes = 16 * 8 + (size_t)nw + 4 * (size_t)nw + 4 * ((size_t)nw + 1) + 4 * (size_t)pcap +
+  const size_t h_bytes = dr::PH_N * 8 + (size_t)nw + 4 * (size_t)nw + 4 * ((size_t)nw + 1) + 4 * (size_t)pcap +
                          3 * 8 * (size_t)pcap + 8 * 256;
   HIPCHK(c, c->plan_out.ensure(h_bytes));
   Carve hv;
@@ -3510,6 +3519,11 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       f.nseg = c->nseg.as<int32_t>();
       f.plan = plan;
       f.o = dr::FinalOut{h_commit, h_vcount, h_push_off, h_push_wave, h_pc, h_pd, h_pe, h_hdr};
+      f.task_wave = task_wave;
+      f.task_q = task_q;
+      f.own_w0 = c->slice_on ? c->slice.own_w0 : 0;
+      f.nprobe = c->slice_on ? c->slice.nprobe : 0;
+      for (int i = 0; i < dr::kMaxProbe; i++) f.probe[i] = c->slice_on && i < c->slice.nprobe ? c->slice.probe[i] : 0;
     }
     dr::SweepQuery probe{};
     probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
@@ -3638,6 +3652,18 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   o->sweep_weak_scanned = h_hdr[dr::PH_WEAK];
   o->sweep_shortcut = h_hdr[dr::PH_SHORT];
   o->n_ids = 0;
+  if (c->slice_on) {
+    dr_slice_out &so = c->slice_res;
+    so = dr_slice_out{};
+    for (int i = 0; i < c->slice.nprobe; i++) {
+      so.C[i] = h_hdr[dr::PH_PROBE + i];
+      so.G[i] = h_hdr[dr::PH_PROBE + dr::kMaxProbe + i];
+      so.E[i] = h_hdr[dr::PH_PROBE + 2 * dr::kMaxProbe + i];
+    }
+    const int64_t ms = (int64_t)h_hdr[dr::PH_MINSTOP];
+    so.min_stop = ms >= INT_MAX ? INT_MAX : (int32_t)ms;
+    so.own_chain_edges = h_hdr[dr::PH_OWN_CE];
+  }
   return DR_OK;
 }
 }  // namespace
@@ -3649,7 +3675,17 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   if (nwaves < 1 || 4 * nwaves >= c->nrounds) return c->fail(DR_E_INVAL, "nwaves %d needs rounds 0..%d mirrored", nwaves, 4 * nwaves);
   if (chain_mode != DR_CHAIN_LITERAL && chain_mode != DR_CHAIN_PERSISTENT) return c->fail(DR_E_INVAL, "bad chain mode");
   if (deliver_mode != DR_DELIVER_REF && deliver_mode != DR_DELIVER_PAPER) return c->fail(DR_E_INVAL, "bad deliver mode");
-  if (int rc = prep_query(c)) return rc;
+  if (int rc = prep_query(c, true)) return rc;
+  if (c->slice_on) {  // a slice replays on the device-planned memo path alone (its outputs come from there)
+    if (chain_mode != DR_CHAIN_PERSISTENT || deliver_mode != DR_DELIVER_REF)
+      return c->fail(DR_E_STATE, "a sliced context replays persistent chains with REF delivery only");
+    if (c->general() || !c->memo_on() || c->plan_mode == 0 || (o->ids && o->ids_cap > 0) || !o->push_wave ||
+        !o->pop_count || !o->pop_digest)
+      return c->fail(DR_E_STATE, "a sliced context needs the memoized device-planned replay (no ids, every output)");
+    if (c->slice.own_w0 > nwaves) return c->fail(DR_E_INVAL, "slice: own_w0 %d > nwaves %d", c->slice.own_w0, nwaves);
+    for (int i = 0; i < c->slice.nprobe; i++)
+      if (c->slice.probe[i] >= c->nrounds) return c->fail(DR_E_INVAL, "slice: probe round %d beyond the mirror", c->slice.probe[i]);
+  }
   o->ms_commit = o->ms_chain = o->ms_deliver = o->ms_emit = o->ms_summary = 0;
   o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;
@@ -3785,6 +3821,8 @@ int replay_batch_impl(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode,
   if (!ctxs || nctx < 1 || !outs) return DR_E_INVAL;
   for (int i = 0; i < nctx; i++)
     if (!ctxs[i]) return DR_E_INVAL;
+  for (int i = 0; i < nctx; i++)
+    if (ctxs[i]->slice_on) return ctxs[0]->fail(DR_E_STATE, "context %d is sliced (dr_set_slice): dr_replay only", i);
   dr_ctx *c0 = ctxs[0];
   // the fused launch reads every member's mirror on the first context's stream: appends
   // still in flight on a member's own stream finish first
@@ -4041,4 +4079,41 @@ extern "C" int dr_replay_batch_view(dr_ctx *const *ctxs, int nctx, int nwaves, i
     o.push_cap = push_cap;
   }
   return replay_batch_impl(ctxs, nctx, nwaves, chain_mode, deliver_mode, outs.data(), views);
+}
+
+extern "C" int dr_set_slice(dr_ctx *c, const dr_slice_cfg *cfg) {
+  if (c) c->touch();
+  if (!c) return DR_E_INVAL;
+  if (int rc = set_device(c)) return rc;
+  const uint64_t old_base = c->slice_on ? c->slice.pos_base : 0;
+  if (!cfg) {
+    c->slice_on = false;
+    c->slice = dr_slice_cfg{};
+  } else {
+    if (cfg->round_offset < 0 || cfg->seeded_top < 0 || cfg->seeded_top >= std::max(1, c->nrounds) ||
+        cfg->own_w0 < 0 || cfg->nprobe < 0 || cfg->nprobe > dr::kMaxProbe)
+      return c->fail(DR_E_INVAL, "bad slice configuration");
+    for (int i = 0; i < cfg->nprobe; i++)
+      if (cfg->probe[i] < 0) return c->fail(DR_E_INVAL, "slice probe %d: negative round", i);
+    c->slice_on = true;
+    c->slice = *cfg;
+  }
+  c->slice_res = dr_slice_out{};
+  c->cfg_gen++;          // a captured replay graph is stale
+  c->canon_ok = false;   // positions and digests change with the base and the key offset
+  c->kprev_ok = false;
+  const uint64_t base = c->slice_on ? c->slice.pos_base : 0;
+  if (base != old_base && !c->h_ppref.empty()) {  // positions start at the new base: every round's prefix
+    for (u64 &x : c->h_ppref) x = x - old_base + base;
+    HIPCHK(c, c->h2d(c->ppref.as<u64>(), c->h_ppref.data(), c->h_ppref.size() * 8));
+    HIPCHK(c, c->sync());
+  }
+  return DR_OK;
+}
+
+extern "C" int dr_slice_result(const dr_ctx *c, dr_slice_out *out) {
+  if (!c || !out) return DR_E_INVAL;
+  if (!c->slice_on) return DR_E_STATE;
+  *out = c->slice_res;
+  return DR_OK;
 }

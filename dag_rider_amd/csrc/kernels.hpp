@@ -95,6 +95,10 @@ struct DagView {
   const uint32_t *sdx;
   int32_t n;
   int32_t nrounds;
+  // wave-range slice (dr_set_slice): digest keys use global rounds (round + roff);
+  // rounds >= seed_lo are taken as full canonical rounds (K covers P; INT_MAX: none)
+  int32_t roff;
+  int32_t seed_lo;
 };
 
 // repeated slots of round r whose source is in the set X (lane w < WS holds word
@@ -821,10 +825,12 @@ __device__ __forceinline__ void canon_prefix_block(int T, const u64 *__restrict_
 // plan[] slots (int32, device)
 enum : int { PL_NTASK = 0, PL_NQC = 1, PL_NPUSH = 2, PL_CAPERR = 3, PL_NQD = 4, PL_NDESC = 5, PL_N = 8 };
 // header written to host memory by k_plan_final (u64)
+// (PH_MINSTOP .. PH_PROBE + 23: a sliced context's outputs, dr_slice_result)
 enum : int {
   PH_NPUSH = 0, PH_CHAIN_E = 1, PH_DELIVER_E = 2, PH_PARTIAL = 3, PH_ROWS = 4, PH_WEAK = 5, PH_SHORT = 6,
-  PH_NQD = 7, PH_NSEG = 8, PH_CAPERR = 9, PH_N = 16
+  PH_NQD = 7, PH_NSEG = 8, PH_CAPERR = 9, PH_MINSTOP = 10, PH_OWN_CE = 11, PH_PROBE = 16, PH_N = 40
 };
+constexpr int kMaxProbe = 8;
 
 // Host-visible output region of a planned replay (packed, one copy back).
 struct FinalOut {
@@ -852,6 +858,11 @@ struct FinalArgs {
   const int32_t *firstpop;  // PAPER (k_paper_*): the first pop of each query; later pops deliver nothing
   const u64 *qedges;        // PAPER: the query's delivered edges
   FinalOut o;
+  // a sliced context (dr_set_slice; own_w0 = 0: none): the owned commits' min pop stop
+  // and chain edges (task_wave / task_q: k_plan_chains' tasks), C, G, E at the probes
+  const int32_t *task_wave, *task_q;
+  int32_t own_w0, nprobe;
+  int32_t probe[kMaxProbe];
 };
 
 // The planned replay's per-query emission outputs (k_own_emit, k_paper_emit):
@@ -880,7 +891,8 @@ __device__ __forceinline__ u64 wave_emit_slots(const uint16_t *__restrict__ slot
                                                uint32_t sb, u64 mw, u64 pos,
                                                const uint16_t *__restrict__ sdeg = nullptr,
                                                const uint16_t *__restrict__ wdeg = nullptr, int n = 0,
-                                               u64 *edges = nullptr, const uint8_t *__restrict__ first_only = nullptr) {
+                                               u64 *edges = nullptr, const uint8_t *__restrict__ first_only = nullptr,
+                                               int koff = 0) {
   const int lane = threadIdx.x & 63;
   u64 dg = 0;
   for (uint32_t c0 = sa; c0 < sb; c0 += 64 * SPL) {
@@ -911,7 +923,7 @@ __device__ __forceinline__ u64 wave_emit_slots(const uint16_t *__restrict__ slot
 #pragma unroll
     for (int j = 0; j < SPL; j++) {
       if (!((bits >> j) & 1u)) continue;
-      dg += digest_term((uint32_t)y, (uint32_t)src[j], k);
+      dg += digest_term((uint32_t)(y + koff), (uint32_t)src[j], k);
       if constexpr (DEG) {
         const size_t at = (size_t)y * n + (src[j] - 1);
         *edges += (u64)sdeg[at] + wdeg[at];
@@ -927,9 +939,10 @@ __device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot
                                                const uint16_t *__restrict__ slot_src, int y, u64 mw, u64 pos,
                                                const uint16_t *__restrict__ sdeg = nullptr,
                                                const uint16_t *__restrict__ wdeg = nullptr, int n = 0,
-                                               u64 *edges = nullptr, const uint8_t *__restrict__ first_only = nullptr) {
+                                               u64 *edges = nullptr, const uint8_t *__restrict__ first_only = nullptr,
+                                               int koff = 0) {
   return wave_emit_slots<WS, SPL, DEG>(slot_src, y, slot_off[y], slot_off[y + 1], mw, pos, sdeg, wdeg, n, edges,
-                                       first_only);
+                                       first_only, koff);
 }
 
 
@@ -953,6 +966,15 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
   const int nqc = f.plan[PL_NQC], nqd = f.plan[PL_NQD];
   u64 de = 0, ce = 0, st[4] = {0, 0, 0, 0};
   bool bad = false;
+  __shared__ int s_minstop;
+  __shared__ u64 s_owce;
+  if (tid == 0) {
+    s_minstop = INT_MAX;
+    s_owce = 0;
+  }
+  // a slice: the pops of owned commits start at push_off[own_w0 - 1]
+  const int64_t pown = f.own_w0 > 0 && !caperr ? (int64_t)f.push_off[f.own_w0 - 1] : INT64_MAX;
+  int minstop = INT_MAX;
   // every load of a pop before any store (the stores could alias for the compiler)
   for (int64_t p = tid; p < np; p += NT) {
     const int q = f.pop_q[p];
@@ -972,6 +994,7 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
       if (stop >= 0) e += f.Ec[stop];  // the sweep counted the edges of rounds above stop
     }
     bad |= cur < top;
+    if (p >= pown) minstop = min(minstop, stop);
     f.o.push_wave[p] = pw;
     f.o.pc[p] = c;
     f.o.pd[p] = d;
@@ -979,6 +1002,14 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
     de += e;
   }
   for (int q = tid; q < nqc; q += NT) ce += f.cedges[q];
+  u64 owce = 0;
+  if (f.own_w0 > 0) {
+    const int ntask = f.plan[PL_NTASK];
+    for (int t = tid; t < ntask; t += NT) {
+      const int q = f.task_q[t];
+      if (q >= 0 && f.task_wave[t] >= f.own_w0) owce += f.cedges[q];
+    }
+  }
   for (int q = tid; q < nqd; q += NT)
 #pragma unroll
     for (int k = 0; k < 4; k++) st[k] += f.dstats[4 * q + k];
@@ -1002,9 +1033,22 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
     for (int k = 0; k < 4; k++) atomicAdd(&acc[2 + k], st[k]);
   }
   if (bad) s_bad = 1;
+  if (f.own_w0 > 0) {
+    owce = wave_sum(owce);
+    if ((tid & 63) == 0 && owce) atomicAdd(&s_owce, owce);
+    if (minstop != INT_MAX) atomicMin(&s_minstop, minstop);
+  }
+  if (tid < f.nprobe) {
+    const int r = f.probe[tid];
+    f.o.hdr[PH_PROBE + tid] = f.Cc[r];
+    f.o.hdr[PH_PROBE + kMaxProbe + tid] = f.Gc[r];
+    f.o.hdr[PH_PROBE + 2 * kMaxProbe + tid] = f.Ec[r];
+  }
   __syncthreads();
   if (tid == 0) {
     u64 *h = f.o.hdr;
+    h[PH_MINSTOP] = (u64)(int64_t)s_minstop;
+    h[PH_OWN_CE] = s_owce;
     h[PH_NPUSH] = (u64)f.plan[PL_NPUSH];
     h[PH_CHAIN_E] = acc[1];
     h[PH_DELIVER_E] = acc[0];
@@ -1727,7 +1771,7 @@ __device__ __forceinline__ void weak_union_round(const DagView &g, int r, int dd
       u64 k = pos + (inc - cnt);
 #pragma unroll
       for (int j = 0; j < SPT; j++)
-        if (src[j]) dg += digest_term((uint32_t)r, src[j], k++);
+        if (src[j]) dg += digest_term((uint32_t)(r + g.roff), src[j], k++);
       pos += __shfl(inc, 63);
     }
     dg = wave_sum(dg);
@@ -1791,6 +1835,7 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
   if (w < WS) {
     const u64 p = g.present[(size_t)r * WS + w];
     if (r == T) k = p;
+    else if (r >= g.seed_lo) k |= p;  // a seeded slice top: the rank above reports these rounds full
     K[(size_t)r * WS + w] = k;
     bad = (k & p) != p;
     cnt = popc64(k & p);
@@ -2008,7 +2053,8 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
   __syncthreads();
   __shared__ u64 part[NT / 64];
   const int B = ppref ? lo_w : 0;  // (rounds below B: k_kcand wrote the presence prefix)
-  const u64 base0 = (ppref && B >= 1) ? ppref[B - 1] : 0ULL;
+  // (ppref[0]: the slice's position base, 0 for a whole DAG; round 0 is never delivered)
+  const u64 base0 = ppref ? ppref[B >= 1 ? B - 1 : 0] : 0ULL;
   const int per = (T + 1 - B + NT - 1) / NT;
   const int ra = B + tid * per, rb = min(T + 1, ra + per);
   int bad = INT_MAX;  // ppref: the lowest round whose C differs from the all-full prefix
@@ -2195,10 +2241,10 @@ __device__ __forceinline__ void emit_block(const DagView &g, const uint32_t *__r
 #pragma unroll
       for (int j = 0; j < SPL; j++) {
         if (!((bits >> j) & 1u)) continue;
-        rdg += digest_term((uint32_t)r, (uint32_t)src[j], k);
+        rdg += digest_term((uint32_t)(r + g.roff), (uint32_t)src[j], k);
         if (ids) {
           const int64_t at = pbase + (int64_t)k;
-          if (at < ids_cap) { ids[2 * at] = r; ids[2 * at + 1] = src[j]; }
+          if (at < ids_cap) { ids[2 * at] = r + g.roff; ids[2 * at + 1] = src[j]; }
         }
         k++;
       }

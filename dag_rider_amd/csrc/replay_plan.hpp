@@ -632,7 +632,7 @@ __global__ __launch_bounds__(NT) void k_paper_emit(DagView g, const u64 *__restr
       tot += c;
     }
     if (on && cnt)  // PAPER delivers an id once, at its first slot
-      dg += wave_emit_round<WS, 8, true>(slot_off, slot_src, r, mw, pos, g.sdeg, g.wdeg, g.n, &ed, g.slot_rep);
+      dg += wave_emit_round<WS, 8, true>(slot_off, slot_src, r, mw, pos, g.sdeg, g.wdeg, g.n, &ed, g.slot_rep, g.roff);
     run += tot;
     __syncthreads();
   }
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
       pos += i < wid ? c : 0ULL;
       tot += c;
     }
-    if (on && cnt) dg += wave_emit_slots<WS>(slot_src, r, sa, sb, mw, pos);
+    if (on && cnt) dg += wave_emit_slots<WS>(slot_src, r, sa, sb, mw, pos, nullptr, nullptr, 0, nullptr, nullptr, g.roff);
     run += tot;
     __syncthreads();
   }

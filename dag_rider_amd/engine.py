@@ -141,6 +141,28 @@ class Engine:
         keys = ("exceptions", "changing", "sweeps", "regular_delta", "upward", "memo")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def set_slice(self, round_offset: int = 0, pos_base: int = 0, seeded_top: int = 0, own_w0: int = 0,
+                  probes: Sequence[int] = (), clear: bool = False):
+        """dr_set_slice: this mirror is global rounds [round_offset, ...) of a bigger DAG
+        (dag_rider_amd/split.py, include/dagrider_gpu.h); clear=True drops it."""
+        if clear:
+            self._check(self._L.dr_set_slice(self._h, None))
+            return
+        if len(probes) > 8:
+            raise ValueError("at most 8 probe rounds")
+        cfg = L.SliceCfg(round_offset, seeded_top, pos_base, own_w0, len(probes))
+        for i, r in enumerate(probes):
+            cfg.probe[i] = int(r)
+        self._check(self._L.dr_set_slice(self._h, C.byref(cfg)))
+
+    def slice_result(self) -> dict:
+        """dr_slice_result: C, G, E at the probes, the owned pops' lowest merge round and the
+        owned commits' chain edges from the last dr_replay."""
+        o = L.SliceOut()
+        self._check(self._L.dr_slice_result(self._h, C.byref(o)))
+        return dict(C=[int(x) for x in o.C], G=[int(x) for x in o.G], E=[int(x) for x in o.E],
+                    min_stop=int(o.min_stop), own_chain_edges=int(o.own_chain_edges))
+
     @property
     def num_rounds(self) -> int:
         return self._L.dr_num_rounds(self._h)

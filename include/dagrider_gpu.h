@@ -362,6 +362,45 @@ int dr_last_batch_form(const dr_ctx *ctx);
  * calls of the context run behind the copy on its stream). */
 int dr_last_append_phases(const dr_ctx *ctx, float *ms4);
 
+/* Wave-range slice of one DAG (SURVEY.md s8(e) row 1 widened to the whole replay:
+ * waveReady :314-354 and orderVertices :404-443 of a contiguous wave range on the GPU
+ * that holds only those rounds; dag_rider_amd/split.py).  The context mirrors global
+ * rounds [round_offset, round_offset + nrounds) as its rounds 0.. (weak edges below
+ * round_offset dropped, round 0's rows empty) and dr_replay then reports what the
+ * whole DAG's replay reports for the slice's waves, up to additive offsets that the
+ * ranks' dr_slice_out exchange supplies:
+ *   - digest keys use global rounds (slice round + round_offset);
+ *   - canonical positions start at pos_base, the canonical vertices of global rounds
+ *     1..round_offset (so pop counts are global);
+ *   - seeded_top > 0: the top seeded_top rounds are taken as full canonical rounds
+ *     (K covers every present vertex) -- the rounds above a lower rank's waves, whose
+ *     canonical cone the rank above reports (its C probes);
+ *   - own_w0: the first slice wave this rank owns (1-based, slice numbering): the
+ *     replay's min pop stop and owned chain edges count the commits from it on;
+ *   - probes: the canonical prefixes C (count, from pos_base), G (digest, from 0) and
+ *     E (edges, from 0) at up to 8 slice rounds.
+ * Only dr_replay (REF delivery, persistent chains, memo path) runs on a sliced
+ * context; the other query calls return DR_E_STATE while a slice is set.  NULL
+ * clears it. */
+typedef struct dr_slice_cfg {
+  int32_t round_offset;
+  int32_t seeded_top;
+  uint64_t pos_base;
+  int32_t own_w0;
+  int32_t nprobe;
+  int32_t probe[8];
+} dr_slice_cfg;
+typedef struct dr_slice_out {
+  uint64_t C[8], G[8], E[8];   /* the canonical prefixes at cfg.probe[] */
+  int32_t min_stop;            /* lowest merge round (slice numbering) of the pops of owned
+                                  commits; < 0: one did not merge inside the slice */
+  int32_t pad_;
+  uint64_t own_chain_edges;    /* chain edges of the owned commits */
+} dr_slice_out;
+int dr_set_slice(dr_ctx *ctx, const dr_slice_cfg *cfg);
+/* the slice outputs of the last dr_replay on a sliced context */
+int dr_slice_result(const dr_ctx *ctx, dr_slice_out *out);
+
 #ifdef __cplusplus
 }
 #endif
