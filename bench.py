@@ -1085,6 +1085,9 @@ def main() -> int:
     ap.add_argument("--cpu-budget", type=float, default=40.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phase-timing", type=int, default=1, help=argparse.SUPPRESS)  # 0: no events (experiment)
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="bracket the summary pass with HIP events on every k-th timed step (each event "
+                         "record costs the stream ~4 us: tools/experiments/launch_probe.hip)")
     ap.add_argument("--loop-waves", type=int, default=0, help="c4-loop: waves to run (0 = all)")
     ap.add_argument("--dags", type=int, default=0, help="c5 on one GPU: replay only the first N DAGs")
     ap.add_argument("--rank-share", type=int, default=0,
@@ -1094,6 +1097,9 @@ def main() -> int:
     ap.add_argument("--halo", type=int, default=8, help="wave split: waves below each rank's range it mirrors")
     ap.add_argument("--no-wsplit", action="store_true", help="N>1: skip the wave-split replay")
     ap.add_argument("--verify", action="store_true", help="check the replay against the bitset oracle")
+    ap.add_argument("--verify-general", action="store_true",
+                    help="check the replay against the general sweep's (memo off) on the GPU (c4-up: no CPU oracle "
+                         "takes edges to the same round at this size)")
     ap.add_argument("--colshard", action="store_true",
                     help="also run the process-column sharded C4 sweep (default on when N>1)")
     ap.add_argument("--no-colshard", action="store_true")
@@ -1186,10 +1192,15 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ms_summary = 0.0
-    for _ in range(args.steps):
+    ms_summary, n_ev = 0.0, 0
+    every = max(1, args.event_every) if args.phase_timing == 1 else 1
+    for i in range(args.steps):
+        if every > 1:  # (a host-side option: no device work)
+            eng.set_phase_timing(1 if i % every == 0 else 0)
         step()
-        ms_summary += step.ms_summary
+        if i % every == 0:
+            ms_summary += step.ms_summary
+            n_ev += 1
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -1202,7 +1213,7 @@ def main() -> int:
     dt, total_edges = reduce_over_ranks(dist, wall, res.total_edges, "cuda")
     eng.set_phase_timing(2)
     prof = eng.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, args.deliver_mode)  # per-phase HIP event times
-    res.ms = dict(prof.ms, summary=ms_summary / args.steps)
+    res.ms = dict(prof.ms, summary=ms_summary / max(n_ev, 1))
 
     verify = None
     cpu = cpu2 = None
@@ -1211,6 +1222,15 @@ def main() -> int:
         cpu2, want = cpu_bitset(cfg, d, CPU_THREADS, runs, args.deliver_mode)
         verify = same_replay(res, want)
         cpu = cpu_literal(cfg, d, args.cpu_budget, res.total_edges, args.deliver_mode)
+    elif args.verify_general and rank == 0:
+        with Engine(cfg.n, cfg.faulty, d.nrounds, local) as eg:
+            eg.append_packed(d)
+            eg.set_memo(False)
+            t0 = time.perf_counter()
+            wantg = eg.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, args.deliver_mode)
+            log(f"[rank 0] general-sweep replay (memo off) in {time.perf_counter() - t0:.1f} s, path "
+                f"{eg.last_replay_path()}")
+        verify = same_replay(res, wantg)
     elif args.verify and rank == 0:
         import oracle
 
@@ -1296,9 +1316,13 @@ def main() -> int:
         "detail": {"edges_per_step": res.total_edges, "commit_edges": res.commit_edges,
                    "chain_edges": res.chain_edges, "deliver_edges": res.deliver_edges,
                    "commits": int(res.commit.sum()), "pops": int(len(res.pop_count)),
-                   "ms": res.ms, "ms_note": "summary: mean over the timed steps; other phases: one "
+                   "ms": res.ms, "ms_note": f"summary: mean over the {n_ev} timed steps whose summary pass HIP events "
+                   f"bracket (every {every}th: each record costs the stream ~4 us); other phases: one "
                    "profiling replay after them (DR_OPT_PHASE_TIMING=2)",
                    "sweep": res.sweep, "verify_vs_oracle": verify, "exceptions": exc,
+                   "replay_path": {0: "memo", 1: "memo, upward weak edges verified (k_verify_up)",
+                                   2: "general sweep (an upward edge changes a cone)", 3: "general sweep",
+                                   -1: "none"}.get(eng.last_replay_path(), "?"),
                    "commit_split": split, "colshard": colshard[0] if colshard else None,
                    "kernels": {k: dict(v, GBps=(v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None))
                                for k, v in kb.items()}},

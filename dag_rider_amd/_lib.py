@@ -103,6 +103,7 @@ SIGNATURES = {
     "dr_last_batch_form": (C.c_int, [P]),
     "dr_last_append_phases": (C.c_int, [P, C.POINTER(f32)]),
     "dr_set_slice": (C.c_int, [P, C.POINTER(SliceCfg)]),
+    "dr_last_replay_path": (C.c_int, [P]),
     "dr_slice_result": (C.c_int, [P, C.POINTER(SliceOut)]),
     # include/dagrider_shard.h
     "dr_shard_unique_id": (C.c_int, [P]),

@@ -146,6 +146,15 @@ struct dr_ctx {
   // exception count, the irr_up count; per round (ensure_exceptions): exceptions found
   // not benign.
   std::vector<int32_t> h_rdreg, h_rexc, h_rup, h_rbad;
+  // upward irregular edges that are strong ones (h_rups): a weak-only upward set may take
+  // the verified memo replay (dr_replay: up_verify, replay_plan.hpp k_verify_up)
+  std::vector<int32_t> h_rups;
+  int64_t nirr_ups = 0;
+  bool up_verify = false;
+  DevBuf upe, upbad;            // the upward weak edges (ru, su0, rv, tv0), the violation count
+  std::vector<uint64_t> upe_key;
+  int upe_n = 0;
+  int last_path = -1;           // dr_last_replay_path
   std::vector<uint32_t> h_sdx;  // [round] strong edges outside the rows (DagView::sdx)
   DevBuf sdx;
   bool sdx_valid = false;       // the device copy holds every mirrored round's h_sdx
@@ -173,7 +182,15 @@ struct dr_ctx {
   int gsweep_bottom(int t) const { return (t >= 0 && min_up_round() >= t) ? t : 0; }
   // every exception known benign (the last test covers every round)
   bool exc_clear() const { return nexc == 0 || (exc_lo >= nrounds && nbad == 0); }
-  bool general() const { return nirr_up > 0 || (nirr_down > 0 && !exc_clear()); }
+  bool general() const { return (nirr_up > 0 && !up_verify) || (nirr_down > 0 && !exc_clear()); }
+  // dr_replay may take the memo path with a per-replay check of the upward edges: weak ones
+  // only, a bounded number of them, every downward exception benign
+  static constexpr int64_t kMaxUpVerify = 1 << 14;
+  // (the downward exceptions are worth testing: a verified replay can use the memo)
+  bool up_verifiable_structure() const { return nirr_ups == 0 && nirr_up <= kMaxUpVerify; }
+  bool up_verifiable() const {
+    return nirr_up > 0 && nirr_ups == 0 && nirr_up <= kMaxUpVerify && (nirr_down == 0 || exc_clear());
+  }
   dr::GView gview() const { return dr::GView{irr.as<uint64_t>(), irr_roff.as<uint32_t>()}; }
   int lead_src(int w) const { return (w >= 0 && w < (int)h_lead.size()) ? h_lead[w] : 1; }
   // host mirror: per-round data, presence [rounds][WS], and the prefix offsets
@@ -250,6 +267,15 @@ struct dr_ctx {
   std::vector<dr_replay_out> view_outs;  // dr_replay_batch_view's capacities (this context first)
   uint64_t gen = 0;  // context generation (g_ctx_gen): bumped by every call that may change the context
   void touch() { gen = next_gen(); }  // dr_last_batch_phases: host prep, launch -> host, copy back, unpack
+  // REF planned replay: the static delivery-query table, one query per wave whose leader
+  // is present (highest wave first, masks of rounds 0..top each), wave -> query index, and
+  // a constant plan header {PL_NQD = count, PL_CAPERR = 0} for the launches that must not
+  // read the chain planner's (it runs on the second stream)
+  DevBuf sdq, sqidx, splan;
+  DevBuf pushed;            // [wave] the replay stamp of a chain push (dr::PopMark)
+  int32_t pop_epoch = 0;
+  std::vector<uint64_t> sdq_key;
+  int sdq_n = 0;
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
   DevBuf plan_out;          // its outputs, packed for one copy back
   std::vector<char> plan_host;
@@ -284,7 +310,7 @@ struct dr_ctx {
   // memo (round summaries + canonical cone) over the regular graph: weak deltas up to
   // reg_max() (WU holds dd = dreg - 1 slots per round, the merge window is dreg rounds,
   // the sweeps' LDS ring holds them), every exception benign, no irregular edge upward
-  bool memo_struct_ok() const { return nirr_up == 0; }
+  bool memo_struct_ok() const { return nirr_up == 0 || up_verify; }
   bool memo_ok() const { return memo_struct_ok() && exc_clear(); }
   // repeated ids: the summaries' counts and the emission count every slot of a
   // reached id (REF), PAPER delivers an id at its first slot (slot_rep)
@@ -493,7 +519,7 @@ struct dr_ctx {
   void round_exceptions(int r) {
     const HostRound &h = hr[r];
     const int X = reg_max();
-    int d = 1, ex = (int)h.far.size(), up = 0;
+    int d = 1, ex = (int)h.far.size(), up = 0, ups = 0;
     for (size_t j = 0; j < h.wc_key.size(); j++) {
       const int delta = (int)(h.wc_key[j] >> 11);
       if (delta <= X) { d = std::max(d, delta); continue; }
@@ -501,13 +527,16 @@ struct dr_ctx {
     }
     uint32_t sx = 0;
     for (uint64_t x : h.irr) {
-      ((int)((x >> 11) & 0xFFFFFu) >= r) ? up++ : ex++;
+      const bool upw = (int)((x >> 11) & 0xFFFFFu) >= r;
+      upw ? up++ : ex++;
+      if (upw && ((x >> 31) & 1u)) ups++;
       sx += (uint32_t)((x >> 31) & 1u);
     }
     h_sdx[r] = sx;
     h_rdreg[r] = d;
     h_rexc[r] = ex;
     h_rup[r] = up;
+    h_rups[r] = ups;
   }
   // Flatten rounds [up_lo, nrounds) of the variable-size per-round arrays
   // (slots, weak columns, far edges, weak counts, presence) and copy them to
@@ -542,17 +571,20 @@ struct dr_ctx {
       for (int r = lo; r < std::min(Rold, R); r++) {
         nexc -= h_rexc[r];
         nirr_up -= h_rup[r];
+        nirr_ups -= h_rups[r];
         dreg_drop |= h_rdreg[r] == dreg;
       }
       h_rdreg.resize(R, 1);
       h_rexc.resize(R, 0);
       h_rup.resize(R, 0);
+      h_rups.resize(R, 0);
       h_rbad.resize(R, 0);
       h_sdx.resize(R, 0);
       for (int r = lo; r < R; r++) {
         round_exceptions(r);
         nexc += h_rexc[r];
         nirr_up += h_rup[r];
+        nirr_ups += h_rups[r];
       }
       if (dreg_drop) {
         dreg = 1;
@@ -762,17 +794,24 @@ hipError_t launch_commit(dr_ctx *c, int w0, int nw, uint8_t *cm, int32_t *vc) {
   return hipErrorInvalidValue;
 }
 
-struct SweepArgs {
-  const dr::SweepQuery *q;
-  int nq, seq;
-  u64 *masks, *dlv;
-  int32_t *push_out, *push_n;
-  u64 *edges, *wedges;
-  uint8_t *hits;
-  int32_t *stops;
-  u64 *stats;
+struct SweepArgs {  // (every field initialised: a launch never reads a stale pointer)
+  const dr::SweepQuery *q = nullptr;
+  int nq = 0, seq = 0;
+  u64 *masks = nullptr, *dlv = nullptr;
+  int32_t *push_out = nullptr, *push_n = nullptr;
+  u64 *edges = nullptr, *wedges = nullptr;
+  uint8_t *hits = nullptr;
+  int32_t *stops = nullptr;
+  u64 *stats = nullptr;
   const int *nq_dev = nullptr;  // planned replay: query count on the device, nq = grid upper bound
   uint32_t *rcnt = nullptr;     // planned delivery: per-mask-row vertex counts for the emission
+  dr::PopMark pm{};             // REF planned replay: live delivery queries / chain stamps
+};
+// The REF replay's leader chains inside the single-stream launches: the chain plan in the
+// weak-union launch (k_wu_plan), the chain sweeps beside the canonical walk (k_canon_chains)
+struct ChainFuse {
+  dr::ChainPlanArgs pa;
+  dr::ChainArgs xa;
 };
 
 // Raise a kernel's dynamic-LDS limit once per (device, size it has not seen yet):
@@ -801,7 +840,7 @@ hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   const int grid = a.seq ? 1 : a.nq;
   hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(grid), dim3(NT), lds, c->stream,
                      c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
-                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt);
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt, a.pm);
   return hipGetLastError();
 }
 template <int WS>
@@ -829,7 +868,7 @@ int sweep_mode(const dr::SweepQuery &q) {
 template <int WS, int PF>
 hipError_t launch_chain_reg(dr_ctx *c, const SweepArgs &a) {
   hipLaunchKernelGGL((dr::k_chain_reg<WS, PF>), dim3((a.nq + 3) / 4), dim3(256), 0, c->stream, c->view(), a.q,
-                     a.nq_dev, a.push_out, a.push_n, a.edges, a.wedges, a.hits, a.stops);
+                     a.nq_dev, a.push_out, a.push_n, a.edges, a.wedges, a.hits, a.stops, a.pm);
   return hipGetLastError();
 }
 hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode);
@@ -913,9 +952,19 @@ hipError_t launch_sc(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
 // WS = 16 (n = 1024): 1024 threads, 2 chunks per thread per group: 80.8 us
 // for C4's 524.8 MB (6.5 TB/s), faster than a bare blocked streaming read of
 // the same rows (profiles/r02/v29_tune.txt: 82.5 us)
+// A short DAG (fewer waves than CUs: a wave-split rank's slice, 134 waves at N = 8) leaves
+// most CUs idle, and a CU's bandwidth is its bytes in flight over the latency: each thread
+// then keeps all 8 of its chunks of a round in flight (GRP 8).
 template <int WS>
 hipError_t launch_sc_shipped(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
-  if constexpr (WS == 16) return launch_sc<WS, 1024, 2, false>(c, T, nwc, cm, vc);
+  if constexpr (WS == 16) {
+    if (c->cu_count <= 0) {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev) == hipSuccess) c->cu_count = cus;
+    }
+    if ((T + 3) / 4 < c->cu_count) return launch_sc<WS, 1024, 8, false>(c, T, nwc, cm, vc);
+    return launch_sc<WS, 1024, 2, false>(c, T, nwc, cm, vc);
+  }
   return launch_sc<WS, summary_block<WS>(), 8, false>(c, T, nwc, cm, vc);
 }
 
@@ -953,14 +1002,34 @@ hipError_t launch_weak_union_t(dr_ctx *c, int T, hipStream_t st) {
                      c->slot_src.as<uint16_t>(), c->RG.as<u64>());
   return hipGetLastError();
 }
-hipError_t launch_weak_union(dr_ctx *c, int T, hipStream_t st) {
+// ... and with cf (the REF replay): the chain plan as the launch's last workgroup
+// (k_wu_plan; a deep window's smaller workgroups take a separate k_plan_chains)
+template <int WS>
+hipError_t launch_wu_plan_t(dr_ctx *c, int T, const ChainFuse &cf) {
+  const int dd = c->memo_dd(), nwv = weak_union_waves(dd, WS);
+  if (nwv != 4) {
+    hipError_t e = launch_weak_union_t<WS>(c, T, c->stream);
+    if (e != hipSuccess) return e;
+    const dr::ChainPlanArgs &pa = cf.pa;
+    hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, pa.commit, pa.lead, pa.nw,
+                       pa.persistent, pa.qflags, pa.task_wave, pa.task_q, pa.cq, pa.plan);
+    return hipGetLastError();
+  }
+  const size_t lds = (size_t)4 * std::max(dd, 1) * WS * 8;
+  static std::atomic<int> seen[kLdsDevs] = {};
+  hipError_t e = lds_limit((const void *)dr::k_wu_plan<WS>, seen, c->dev, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_wu_plan<WS>), dim3((T + 3) / 4 + 1), dim3(256), lds, c->stream, c->view(), T, dd,
+                     c->WU.as<u64>(), c->ppref.as<u64>(), c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
+                     c->RG.as<u64>(), cf.pa);
+  return hipGetLastError();
+}
+hipError_t launch_weak_union(dr_ctx *c, int T, hipStream_t st, const ChainFuse *cf = nullptr) {
   switch (c->WS) {
-    case 1: return launch_weak_union_t<1>(c, T, st);
-    case 2: return launch_weak_union_t<2>(c, T, st);
-    case 4: return launch_weak_union_t<4>(c, T, st);
-    case 8: return launch_weak_union_t<8>(c, T, st);
-    case 16: return launch_weak_union_t<16>(c, T, st);
-    case 32: return launch_weak_union_t<32>(c, T, st);
+#define DR_WU(W) \
+  case W: return cf ? launch_wu_plan_t<W>(c, T, *cf) : launch_weak_union_t<W>(c, T, st);
+    DR_WU(1) DR_WU(2) DR_WU(4) DR_WU(8) DR_WU(16) DR_WU(32)
+#undef DR_WU
   }
   return hipErrorInvalidValue;
 }
@@ -1000,7 +1069,7 @@ hipError_t launch_round_summary(dr_ctx *c, const int32_t *rounds, int nr) {
 // speculative canonical digest (k_weak_union), k_canon sets *rlo to the lowest
 // round where it fails, and the canonical emission re-emits from there.
 template <int WS>
-hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo, bool spec) {
+hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo, bool spec, const ChainFuse *cf = nullptr) {
   const dr::MemoView mv = c->memo_view();
   hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
                      c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>(), c->rlo.as<int>(),
@@ -1011,27 +1080,53 @@ hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo, bool spec) {
   const int dl = c->depth_log2();
   const size_t lds = c->sweep_lds(dl);
   constexpr int NTS = sweep_block<WS>();
-  static std::atomic<int> seen[kLdsDevs] = {};
-  e = lds_limit((const void *)dr::k_canon<WS, NTS>, seen, c->dev, lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_canon<WS, NTS>), dim3(1), dim3(NTS), lds, c->stream, c->view(), mv, T, dl,
-                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>(), c->RD.as<u64>(),
-                     c->Cc.as<u64>(), c->crbase.as<uint32_t>(), spec ? c->ppref.as<u64>() : nullptr,
-                     c->rlo.as<int>());
+  if (cf) {  // workgroup 0 walks the canonical cone, the others sweep the leader chains
+    const dr::CanonArgs ca{T, dl, c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>(),
+                           c->RD.as<u64>(), c->Cc.as<u64>(), c->crbase.as<uint32_t>(),
+                           spec ? c->ppref.as<u64>() : nullptr, c->rlo.as<int>()};
+    const int nq = std::max(cf->pa.nw, 1);
+    bool creg = false;
+    if constexpr (WS == 4) creg = c->chain_reg != 0;
+    if (creg) {
+      if constexpr (WS == 4) {
+        static std::atomic<int> seen_r[kLdsDevs] = {};
+        e = lds_limit((const void *)dr::k_canon_chains<WS, NTS, true>, seen_r, c->dev, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((dr::k_canon_chains<WS, NTS, true>), dim3(1 + (nq + 3) / 4), dim3(NTS), lds, c->stream,
+                           c->view(), mv, ca, cf->xa);
+      }
+    } else {
+      static std::atomic<int> seen_s[kLdsDevs] = {};
+      e = lds_limit((const void *)dr::k_canon_chains<WS, NTS, false>, seen_s, c->dev, lds);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL((dr::k_canon_chains<WS, NTS, false>), dim3(1 + nq), dim3(NTS), lds, c->stream, c->view(),
+                         mv, ca, cf->xa);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess || lo <= 1) return e;
+  } else {
+    static std::atomic<int> seen[kLdsDevs] = {};
+    e = lds_limit((const void *)dr::k_canon<WS, NTS>, seen, c->dev, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((dr::k_canon<WS, NTS>), dim3(1), dim3(NTS), lds, c->stream, c->view(), mv, T, dl,
+                       c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->nseg.as<int32_t>(), c->RD.as<u64>(),
+                       c->Cc.as<u64>(), c->crbase.as<uint32_t>(), spec ? c->ppref.as<u64>() : nullptr,
+                       c->rlo.as<int>());
+  }
   e = hipGetLastError();
   if (e != hipSuccess || lo <= 1) return e;
   hipLaunchKernelGGL((dr::k_canon_diff<WS>), dim3((lo - 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), lo,
                      c->K.as<u64>(), c->Kprev.as<u64>(), c->rlo.as<int>());
   return hipGetLastError();
 }
-hipError_t launch_canon_cone(dr_ctx *c, int T, int lo, bool spec) {
+hipError_t launch_canon_cone(dr_ctx *c, int T, int lo, bool spec, const ChainFuse *cf = nullptr) {
   switch (c->WS) {
-    case 1: return launch_canon_cone_t<1>(c, T, lo, spec);
-    case 2: return launch_canon_cone_t<2>(c, T, lo, spec);
-    case 4: return launch_canon_cone_t<4>(c, T, lo, spec);
-    case 8: return launch_canon_cone_t<8>(c, T, lo, spec);
-    case 16: return launch_canon_cone_t<16>(c, T, lo, spec);
-    case 32: return launch_canon_cone_t<32>(c, T, lo, spec);
+    case 1: return launch_canon_cone_t<1>(c, T, lo, spec, cf);
+    case 2: return launch_canon_cone_t<2>(c, T, lo, spec, cf);
+    case 4: return launch_canon_cone_t<4>(c, T, lo, spec, cf);
+    case 8: return launch_canon_cone_t<8>(c, T, lo, spec, cf);
+    case 16: return launch_canon_cone_t<16>(c, T, lo, spec, cf);
+    case 32: return launch_canon_cone_t<32>(c, T, lo, spec, cf);
   }
   return hipErrorInvalidValue;
 }
@@ -1781,7 +1876,7 @@ int refresh_rounds(dr_ctx *c, bool any = false) {
 int ensure_exceptions(dr_ctx *c) {
   const int R = c->nrounds;
   if (c->exc_lo >= R) return DR_OK;
-  if (c->nexc == 0 || c->nirr_up > 0) {
+  if (c->nexc == 0 || (c->nirr_up > 0 && !c->up_verifiable_structure())) {
     c->exc_lo = c->nexc == 0 ? INT_MAX : c->exc_lo;
     return DR_OK;
   }
@@ -1864,7 +1959,7 @@ inline hipError_t ensure_stream2(dr_ctx *c) {
 }
 
 int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool forked = false,
-                 bool incremental = false, bool prefix = true, bool spec_rg = false) {
+                 bool incremental = false, bool prefix = true, bool spec_rg = false, const ChainFuse *cf = nullptr) {
   const int T = c->nrounds - 1;
   // incremental (the per-call path): rounds below the lowest one that changed
   // since the last cone, and whose canonical vertices are unchanged, keep their
@@ -1892,7 +1987,7 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
   // canonical cone, per-round counts and positions (k_kcand + k_canon), then the
   // per-round digests (emission) and their prefixes
   const bool spec = spec_rg && lo <= 1;  // a full cone: re-emission from the first non-full round
-  HIPCHK(c, launch_canon_cone(c, T, lo, spec));  // *rlo = the lowest round to re-emit
+  HIPCHK(c, launch_canon_cone(c, T, lo, spec, cf));  // *rlo = the lowest round to re-emit
   dr::PopDesc d{};
   d.mask_off = 0;
   d.rbase_off = 1;  // crbase is indexed by round; rbase_off addresses round `first`
@@ -1954,7 +2049,7 @@ int refresh_canon(dr_ctx *c) {
 // (a replay graph holds part 2 alone), 3 = both.
 int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = nullptr, int32_t *vcount = nullptr,
                   bool host_out = true, bool fork = false, const std::function<int()> *side = nullptr,
-                  bool prefix = true, int parts = 3) {
+                  bool prefix = true, int parts = 3, const ChainFuse *cf = nullptr) {
   const int T = c->nrounds - 1;
   if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
   if (parts & 1) {
@@ -1980,9 +2075,9 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
       HIPCHK(c, hipEventRecord(fe, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, fe, 0));
   }
-  HIPCHK(c, launch_weak_union(c, T, c->stream));
+  HIPCHK(c, launch_weak_union(c, T, c->stream, cf));
   mark_rounds_clean(c);
-  if (int rc = launch_canon(c, fork, side, early, false, prefix, true)) return rc;
+  if (int rc = launch_canon(c, fork, side, early, false, prefix, true, cf)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
   if (nwc > 0) {
     HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nwc));
@@ -3178,32 +3273,28 @@ hipError_t launch_paper_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::S
   return hipErrorInvalidValue;
 }
 
-// The canonical prefixes G, E of a REF replay: in k_own_emit's last workgroup when
-// one pass of its threads covers the rounds (C4: 4001 rounds, 512 threads, off the
-// critical path beside the pops' emission); a longer DAG (C3: 10 001 rounds, two
-// passes of 40 rounds a thread, ~20 us at the end of k_own_emit) takes k_canon_prefix
-// (1024 threads, one pass) on the canonical chain instead.
-bool own_emit_prefix(const dr_ctx *c, int own_nt) { return c->nrounds <= 8 * own_nt; }
-inline int own_emit_nt(const dr_ctx *c) { return c->WS <= 4 ? 256 : 512; }
 
 template <int WS>
-hipError_t launch_own_emit_t(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
-                             u64 *qcount, u64 *qdigest, int32_t *qcut) {
+hipError_t launch_own_emit_t(dr_ctx *c, int nq, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
+                             u64 *qcount, u64 *qdigest, int32_t *qcut, const dr::PopMark &pm,
+                             const dr::PopPlanArgs &pp) {
   // 256 threads per query at n <= 256 (C3: 41 -> 37 us, more queries resident), 512 above
-  // (C4 at 256: 12.8 -> 18.8 us; profiles/r03/v18_timeline_*_own256.txt)
+  // (C4 at 256: 12.8 -> 18.8 us; profiles/r03/v18_timeline_*_own256.txt).  Workgroup 0: the
+  // canonical prefixes G, E (every DAG length: canon_prefix_regs walks chunks); the last,
+  // with pp.active: the pop plan.
   constexpr int NT = WS <= 4 ? 256 : 512;
-  const bool pre = own_emit_prefix(c, NT);  // else k_canon_prefix ran on the canonical chain
-  hipLaunchKernelGGL((dr::k_own_emit<WS, NT>), dim3(nw + (pre ? 1 : 0)), dim3(NT), 0, c->stream, c->view(),
-                     c->masks.as<u64>(), c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(),
+  hipLaunchKernelGGL((dr::k_own_emit<WS, NT>), dim3(1 + nq + (pp.active ? 1 : 0)), dim3(NT), 0, c->stream,
+                     c->view(), c->masks.as<u64>(), c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(),
                      c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), qcount, qdigest, qcut, c->nrounds - 1,
-                     c->RG.as<u64>(), c->CE.as<u64>(), pre ? c->Gc.as<u64>() : nullptr, c->Ec.as<u64>());
+                     c->RG.as<u64>(), c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), pm, pp);
   return hipGetLastError();
 }
-hipError_t launch_own_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
-                           u64 *qcount, u64 *qdigest, int32_t *qcut) {
+hipError_t launch_own_emit(dr_ctx *c, int nq, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
+                           u64 *qcount, u64 *qdigest, int32_t *qcut, const dr::PopMark &pm,
+                           const dr::PopPlanArgs &pp) {
   switch (c->WS) {
 #define DR_OE(W) \
-  case W: return launch_own_emit_t<W>(c, nw, plan, dq, stops, qcount, qdigest, qcut);
+  case W: return launch_own_emit_t<W>(c, nq, plan, dq, stops, qcount, qdigest, qcut, pm, pp);
     DR_OE(1) DR_OE(2) DR_OE(4) DR_OE(8) DR_OE(16) DR_OE(32)
 #undef DR_OE
   }
@@ -3352,6 +3443,86 @@ std::vector<uint64_t> graph_key(const dr_ctx *c, int nw, int chain_mode, bool pa
           P(c->view().sdx),    (uint64_t)c->dreg,  (uint64_t)c->nexc};
 }
 
+// The static delivery-query table of an nw-wave REF replay (rebuilt when the DAG, the
+// leader coin or the wave count changed): pops no longer wait for the leader chains --
+// a pop's cone depends on its leader alone, and every pushed leader is a present one.
+int ensure_static_pops(dr_ctx *c, int nw) {
+  const std::vector<uint64_t> key{c->version, (uint64_t)nw, (uint64_t)c->WS, (uint64_t)(uintptr_t)c->sdq.p};
+  if (key == c->sdq_key) return DR_OK;
+  std::vector<dr::SweepQuery> q;
+  std::vector<int32_t> qi((size_t)nw + 1, -1);
+  int64_t moff = 0;
+  for (int w = nw; w >= 1; w--) {
+    const int top = 4 * (w - 1) + 1, L = c->lead_src(w);
+    if (!c->is_present(top, L)) continue;
+    dr::SweepQuery x{};
+    x.top = top;
+    x.bottom = 0;
+    x.src0 = L - 1;
+    x.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
+    x.mask_off = moff;
+    x.tgt0 = -1;
+    moff += (int64_t)(top + 1) * c->WS;
+    qi[w] = (int32_t)q.size();
+    q.push_back(x);
+  }
+  HIPCHK(c, c->sdq.ensure(std::max<size_t>(q.size(), 1) * sizeof(dr::SweepQuery)));
+  HIPCHK(c, c->sqidx.ensure(qi.size() * 4));
+  HIPCHK(c, c->splan.ensure(dr::PL_N * 4));
+  std::vector<int32_t> sp(dr::PL_N, 0);
+  sp[dr::PL_NQD] = (int32_t)q.size();
+  if (!q.empty()) HIPCHK(c, c->h2d(c->sdq.p, q.data(), q.size() * sizeof(dr::SweepQuery)));
+  HIPCHK(c, c->h2d(c->sqidx.p, qi.data(), qi.size() * 4));
+  HIPCHK(c, c->h2d(c->splan.p, sp.data(), sp.size() * 4));
+  HIPCHK(c, c->flush_h2d());
+  c->sdq_n = (int)q.size();
+  c->sdq_key = {c->version, (uint64_t)nw, (uint64_t)c->WS, (uint64_t)(uintptr_t)c->sdq.p};
+  return DR_OK;
+}
+
+// The upward weak edges (ru, su0, rv, tv0) for k_verify_up (rebuilt when the DAG changed).
+int ensure_up_edges(dr_ctx *c) {
+  const std::vector<uint64_t> key{c->version, (uint64_t)(uintptr_t)c->upe.p};
+  if (key == c->upe_key) return DR_OK;
+  std::vector<int32_t> e;
+  for (int r = 0; r < c->nrounds; r++)
+    for (uint64_t x : c->hr[r].irr) {
+      const int tr = (int)((x >> 11) & 0xFFFFFu);
+      if (tr < r || ((x >> 31) & 1u)) continue;
+      e.insert(e.end(), {r, (int32_t)((x >> 32) & 2047u), tr, (int32_t)(x & 2047u)});
+    }
+  HIPCHK(c, c->upe.ensure(std::max<size_t>(e.size(), 4) * 4));
+  HIPCHK(c, c->upbad.ensure(64));
+  if (!e.empty()) HIPCHK(c, c->h2d(c->upe.p, e.data(), e.size() * 4));
+  HIPCHK(c, c->flush_h2d());
+  c->upe_n = (int)(e.size() / 4);
+  c->upe_key = {c->version, (uint64_t)(uintptr_t)c->upe.p};
+  return DR_OK;
+}
+
+template <int WS>
+hipError_t launch_verify_up_t(dr_ctx *c, const int32_t *stops, const int32_t *qcut, const dr::PopMark &pm) {
+  const int64_t n = (int64_t)c->upe_n * (c->sdq_n + 1);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 255) / 256));
+  hipError_t e = hipMemsetAsync(c->upbad.p, 0, 4, c->stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((dr::k_verify_up<WS>), dim3(grid), dim3(256), 0, c->stream, c->K.as<u64>(), c->masks.as<u64>(),
+                     c->sdq.as<dr::SweepQuery>(), c->sdq_n, stops, qcut, c->upe.as<int4>(), c->upe_n,
+                     c->upbad.as<int32_t>(), pm);
+  return hipGetLastError();
+}
+hipError_t launch_verify_up(dr_ctx *c, const int32_t *stops, const int32_t *qcut, const dr::PopMark &pm) {
+  switch (c->WS) {
+    case 1: return launch_verify_up_t<1>(c, stops, qcut, pm);
+    case 2: return launch_verify_up_t<2>(c, stops, qcut, pm);
+    case 4: return launch_verify_up_t<4>(c, stops, qcut, pm);
+    case 8: return launch_verify_up_t<8>(c, stops, qcut, pm);
+    case 16: return launch_verify_up_t<16>(c, stops, qcut, pm);
+    case 32: return launch_verify_up_t<32>(c, stops, qcut, pm);
+  }
+  return hipErrorInvalidValue;
+}
+
 int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out *o) {
   const int WS = c->WS, T = c->nrounds - 1;
   const bool persistent = chain_mode == DR_CHAIN_PERSISTENT;
@@ -3432,6 +3603,12 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   u64 *h_pc = hv.take<u64>(pcap), *h_pd = hv.take<u64>(pcap), *h_pe = hv.take<u64>(pcap);
   const size_t out_bytes = hv.off;
 
+  // REF: the delivery sweeps run from the static per-wave query table, beside the chains
+  const bool stat = !paper;
+  if (stat)
+    if (int rc = ensure_static_pops(c, nw)) return rc;
+  dr::SweepQuery *sdq = c->sdq.as<dr::SweepQuery>();
+  const int32_t *splan = c->splan.as<int32_t>();
   // graph form (DR_OPT_REPLAY_GRAPH): launch the captured graph when nothing the
   // launch sequence depends on changed since it was captured; capture when this
   // call's configuration matches the previous call's (every buffer is sized then)
@@ -3444,12 +3621,38 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     else if (key == c->last_key && c->pin_cap >= out_bytes)
       form = CAPTURE;
   }
+  // REF (stat): one stream.  The chain plan rides in the weak-union launch and the chain
+  // sweeps beside the canonical walk (k_wu_plan, k_canon_chains); the delivery sweeps run
+  // from the static table at once, a query live when its wave committed or a chain pushed
+  // its leader (dr::PopMark); the pop plan and the canonical prefixes G, E ride in the
+  // emission launch (k_own_emit).  A second stream would cost a fork and a join, ~18 us on
+  // MI355X even when the other stream's work is long done (launch_probe.hip).
+  // PAPER: the chains and the pop plan on stream2 beside the canonical cone, as before.
+  int32_t *pushed = nullptr;
+  // the commit flags' buffer before any pointer to it is taken below (build_summary would
+  // size it, but the chain plan's and the pop filter's arguments are built first: on a
+  // context's first replay the buffer did not exist yet)
+  HIPCHK(c, c->commit.ensure((size_t)std::max(nw, 1)));
+  HIPCHK(c, c->vcount.ensure((size_t)std::max(nw, 1) * 4));
+  if (stat) {
+    const size_t need = ((size_t)nw + 2) * 4;
+    if (c->pushed.cap < need) {
+      HIPCHK(c, c->pushed.ensure(need));
+      HIPCHK(c, hipMemsetAsync(c->pushed.p, 0, c->pushed.cap, c->stream));
+    }
+    pushed = c->pushed.as<int32_t>();
+    if (++c->pop_epoch <= 0) c->pop_epoch = 1;
+  }
+  const dr::PopMark pmark{stat ? c->commit.as<uint8_t>() : nullptr, pushed, c->pop_epoch};
   auto enqueue = [&](char *stage, int parts) -> int {
-    // 0+1. summaries + commits; then the leader chains and pop planning on stream2
-    // beside the canonical cone on the main stream (the cone takes longer, so the
-    // join before the delivery sweeps finds stream2 done)
     const int sc = dr::Q_SHORTCUT;
     SweepArgs a;
+    ChainFuse cf{};
+    if (stat) {
+      cf.pa = dr::ChainPlanArgs{c->commit.as<uint8_t>(), c->lead.as<uint16_t>(), nw, persistent ? 1 : 0,
+                                dr::Q_CHAIN | dr::Q_STRONG_ONLY | sc, task_wave, task_q, cq, plan};
+      cf.xa = dr::ChainArgs{cq, plan + dr::PL_NQC, push_out, cpush_n, cedges, cwedges, hits, cstops, pmark};
+    }
     std::function<int()> side = [&]() -> int {
       // 2. leader chains
       hipLaunchKernelGGL((dr::k_plan_chains<1024>), dim3(1), dim3(1024), 0, c->stream, c->commit.as<uint8_t>(),
@@ -3475,16 +3678,25 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       // 3. pops
       hipLaunchKernelGGL((dr::k_plan_pops<1024>), dim3(1), dim3(1024), 0, c->stream, nw, WS,
                          dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave, task_q, cq, cpush_n, push_out, pcap,
-                         task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan);
+                         task_pos, push_off, push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan,
+                         (const int32_t *)nullptr, 0);
       HIPCHK(c, hipGetLastError());
       return 0;
     };
-    // (REF: the canonical prefixes in k_own_emit's last workgroup unless the DAG is too long)
-    const bool canon_prefix = !paper && !own_emit_prefix(c, own_emit_nt(c));
-    if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, canon_prefix, parts)) return rc;
-    if (paper) c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
-    // 3+4. delivery sweeps (merging with K), then each query's emission
-    a.q = dq;
+    // PAPER computes no canonical prefixes G, E; REF's come from k_own_emit's workgroup 0
+    if (stat) {
+      if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, false, nullptr, false, parts, &cf)) return rc;
+    } else {
+      if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, true, &side, false, parts)) return rc;
+      c->canon_ok = false;  // no canonical prefixes G, E from this replay: a later call rebuilds the cone
+    }
+    // 3+4. delivery sweeps (merging with K), then each query's emission (every field: the
+    // side lambda that used to fill some of them runs for PAPER only)
+    a.seq = 0;
+    a.masks = c->masks.as<u64>();
+    a.dlv = nullptr;
+    a.nq = nw;
+    a.q = stat ? sdq : dq;
     a.push_out = nullptr;
     a.push_n = nullptr;  // the chains' push counts: stream2's pop plan may still read them
     a.hits = nullptr;
@@ -3492,8 +3704,10 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     a.wedges = dwedges;
     a.stops = dstops;
     a.stats = dstats;
-    a.nq_dev = plan + dr::PL_NQD;
+    a.nq_dev = stat ? nullptr : plan + dr::PL_NQD;  // (static: the table's count)
+    if (stat) a.nq = c->sdq_n;
     a.rcnt = nullptr;
+    a.pm = pmark;
     dr::EmitArgs em{c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), c->Cc.as<u64>(), qcount, qdigest, qcut,
                           dr::FinalArgs{}};
     {
@@ -3511,7 +3725,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       f.push_wave = push_wave;
       f.pop_q = pop_q;
       f.pop_cur = pop_cur;
-      f.dq = dq;
+      f.dq = stat ? sdq : dq;
       f.stops = dstops;
       f.dedges = dedges;
       f.cedges = cedges;
@@ -3521,13 +3735,14 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       f.o = dr::FinalOut{h_commit, h_vcount, h_push_off, h_push_wave, h_pc, h_pd, h_pe, h_hdr};
       f.task_wave = task_wave;
       f.task_q = task_q;
+      f.upbad = c->up_verify ? c->upbad.as<int32_t>() : nullptr;
       f.own_w0 = c->slice_on ? c->slice.own_w0 : 0;
       f.nprobe = c->slice_on ? c->slice.nprobe : 0;
       for (int i = 0; i < dr::kMaxProbe; i++) f.probe[i] = c->slice_on && i < c->slice.nprobe ? c->slice.probe[i] : 0;
     }
     dr::SweepQuery probe{};
     probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // the pops planned on stream2
+    if (!stat) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // PAPER: the pops planned on stream2
     HIPCHK(c, c->rec(2));
     HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));
     if (paper) {  // first-pop ownership, then each query's delivered rounds
@@ -3538,8 +3753,12 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
                                   qedges));
       em.fin.firstpop = firstpop;
       em.fin.qedges = qedges;
-    } else {  // REF: own rounds above the cut; the last workgroup: canonical prefixes G, E
-      HIPCHK(c, launch_own_emit(c, nw, plan, dq, dstops, qcount, qdigest, qcut));
+    } else {  // REF: own rounds above the cut; workgroup 0 the canonical prefixes G, E, the last the pop plan
+      const dr::PopPlanArgs pp{1, nw, WS, dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave,
+                               task_q, cq, cpush_n, push_out, pcap, task_pos, push_off, push_wave, pop_wave, pop_cur,
+                               pop_q, seen, qidx, dq, plan, c->sqidx.as<int32_t>(), c->sdq_n};
+      HIPCHK(c, launch_own_emit(c, c->sdq_n, splan, sdq, dstops, qcount, qdigest, qcut, pmark, pp));
+      if (c->up_verify) HIPCHK(c, launch_verify_up(c, dstops, qcut, pmark));  // the upward edges against the cones
     }
     HIPCHK(c, c->rec(3));
     // 5. per-pop totals and outputs (the canonical prefixes came from the sweep launch's extra workgroup)
@@ -3621,8 +3840,8 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   // outputs
   o->ms_summary = o->ms_chain = o->ms_deliver = o->ms_emit = 0;
   if (c->timed(6)) HIPCHK(c, hipEventElapsedTime(&o->ms_summary, c->ev[6], c->ev[7]));
-  if (c->timed(0)) {
-    HIPCHK(c, hipEventElapsedTime(&o->ms_chain, c->ev[0], c->ev[1]));
+  if (c->timed(0)) {  // (REF: the chains run inside the canonical walk's launch, not timed apart)
+    if (!stat) HIPCHK(c, hipEventElapsedTime(&o->ms_chain, c->ev[0], c->ev[1]));
     HIPCHK(c, hipEventElapsedTime(&o->ms_deliver, c->ev[2], c->ev[3]));  // sweeps + emission + final pass
   }
   std::memcpy(o->commit, h_commit, (size_t)nw);
@@ -3652,6 +3871,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   o->sweep_weak_scanned = h_hdr[dr::PH_WEAK];
   o->sweep_shortcut = h_hdr[dr::PH_SHORT];
   o->n_ids = 0;
+  if (c->up_verify && h_hdr[dr::PH_UPBAD] > 0) return 2;  // an upward edge changes a cone: the general sweep
   if (c->slice_on) {
     dr_slice_out &so = c->slice_res;
     so = dr_slice_out{};
@@ -3690,7 +3910,28 @@ extern "C" int dr_replay(dr_ctx *c, int nwaves, int chain_mode, int deliver_mode
   o->sweep_count = o->sweep_partial = o->sweep_row_bytes = o->sweep_weak_scanned = o->sweep_shortcut = 0;
   o->n_ids = 0;
   o->canon_segments = -1;
-  if (c->general()) return general_replay(c, nwaves, chain_mode, deliver_mode, o);
+  if (c->general()) {
+    // weak edges to the same or a later round (App. A Q8): the memo replay on the regular
+    // graph, then a check that no such edge changes a cone it computed (k_verify_up)
+    if (c->up_verifiable() && deliver_mode == DR_DELIVER_REF && c->use_memo && c->plan_mode != 0 &&
+        !(o->ids && o->ids_cap > 0) && o->push_wave && o->pop_count && o->pop_digest) {
+      c->up_verify = true;
+      int rc = ensure_up_edges(c);
+      if (rc == DR_OK) rc = replay_planned(c, nwaves, chain_mode, false, o);
+      c->up_verify = false;
+      c->canon_ok = false;  // (the cone is the regular graph's: the general paths never read it)
+      if (rc == DR_OK) {
+        c->last_path = 1;
+        return DR_OK;
+      }
+      if (rc != 1 && rc != 2) return rc;
+      c->last_path = rc == 2 ? 2 : 3;
+    } else {
+      c->last_path = 3;
+    }
+    return general_replay(c, nwaves, chain_mode, deliver_mode, o);
+  }
+  c->last_path = 0;
   if (c->plan_mode != 0 && c->memo_on() && !(o->ids && o->ids_cap > 0) && o->push_wave &&
       o->pop_count && o->pop_digest) {
     const int rc = replay_planned(c, nwaves, chain_mode, deliver_mode == DR_DELIVER_PAPER, o);
@@ -4117,3 +4358,5 @@ extern "C" int dr_slice_result(const dr_ctx *c, dr_slice_out *out) {
   *out = c->slice_res;
   return DR_OK;
 }
+
+extern "C" int dr_last_replay_path(const dr_ctx *c) { return c ? c->last_path : DR_E_INVAL; }

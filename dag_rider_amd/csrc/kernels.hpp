@@ -68,6 +68,21 @@ struct SweepQuery {
   int32_t pad;
 };
 
+// The single-stream REF replay (engine.hip replay_planned): the delivery sweeps run from
+// the static per-wave query table before the leader chains are known, so a query is live
+// when its wave committed or a chain pushed its leader (pushed[w] == epoch, the replay's
+// stamp: no clearing between replays).  Chain sweeps stamp pushed[]; delivery sweeps,
+// their emission and the upward-edge check skip a query that is not live.
+struct PopMark {
+  const uint8_t *commit;  // [wave-1]; null: no filter / no stamping
+  int32_t *pushed;        // [wave]
+  int32_t epoch;
+  __device__ bool live(int top) const {
+    const int w = (top - 1) / 4 + 1;
+    return commit[w - 1] || pushed[w] == epoch;
+  }
+};
+
 struct DagView {
   const u64 *strong;
   const u64 *present;
@@ -828,7 +843,7 @@ enum : int { PL_NTASK = 0, PL_NQC = 1, PL_NPUSH = 2, PL_CAPERR = 3, PL_NQD = 4, 
 // (PH_MINSTOP .. PH_PROBE + 23: a sliced context's outputs, dr_slice_result)
 enum : int {
   PH_NPUSH = 0, PH_CHAIN_E = 1, PH_DELIVER_E = 2, PH_PARTIAL = 3, PH_ROWS = 4, PH_WEAK = 5, PH_SHORT = 6,
-  PH_NQD = 7, PH_NSEG = 8, PH_CAPERR = 9, PH_MINSTOP = 10, PH_OWN_CE = 11, PH_PROBE = 16, PH_N = 40
+  PH_NQD = 7, PH_NSEG = 8, PH_CAPERR = 9, PH_MINSTOP = 10, PH_OWN_CE = 11, PH_UPBAD = 12, PH_PROBE = 16, PH_N = 40
 };
 constexpr int kMaxProbe = 8;
 
@@ -861,6 +876,7 @@ struct FinalArgs {
   // a sliced context (dr_set_slice; own_w0 = 0: none): the owned commits' min pop stop
   // and chain edges (task_wave / task_q: k_plan_chains' tasks), C, G, E at the probes
   const int32_t *task_wave, *task_q;
+  const int32_t *upbad;  // k_verify_up's count (null: no upward edges checked)
   int32_t own_w0, nprobe;
   int32_t probe[kMaxProbe];
 };
@@ -1048,6 +1064,7 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
   if (tid == 0) {
     u64 *h = f.o.hdr;
     h[PH_MINSTOP] = (u64)(int64_t)s_minstop;
+    h[PH_UPBAD] = f.upbad ? (u64)*f.upbad : 0ULL;
     h[PH_OWN_CE] = s_owce;
     h[PH_NPUSH] = (u64)f.plan[PL_NPUSH];
     h[PH_CHAIN_E] = acc[1];
@@ -1059,22 +1076,24 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
   }
 }
 
+// The sweep of query bidx (seq: every query in turn), the body of k_sweep and of the
+// fused canonical-walk + chains launch (k_canon_chains).
 template <int WS, int NT, int MODE>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_MERGE) ? 3 : 1))) void k_sweep(DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
-                                              int nq, int seq, int depth_log2,
-                                              u64 *__restrict__ masks, u64 *__restrict__ dlv,
-                                              int32_t *__restrict__ push_out,
-                                              int32_t *__restrict__ push_n,
-                                              u64 *__restrict__ edges_out,
-                                              u64 *__restrict__ wedges_out,
-                                              uint8_t *__restrict__ hit_out,
-                                              int32_t *__restrict__ stop_out,
-                                              u64 *__restrict__ stats_out, const int *__restrict__ nq_dev,
-                                              uint32_t *__restrict__ rcnt) {
+__device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView mv, const SweepQuery *__restrict__ qs,
+                                           int nq, int seq, int depth_log2,
+                                           u64 *__restrict__ masks, u64 *__restrict__ dlv,
+                                           int32_t *__restrict__ push_out,
+                                           int32_t *__restrict__ push_n,
+                                           u64 *__restrict__ edges_out,
+                                           u64 *__restrict__ wedges_out,
+                                           uint8_t *__restrict__ hit_out,
+                                           int32_t *__restrict__ stop_out,
+                                           u64 *__restrict__ stats_out, const int *__restrict__ nq_dev,
+                                           uint32_t *__restrict__ rcnt, const PopMark pm) {
   if (nq_dev) {  // grid sized by an upper bound, count on the device (planned replay)
     const int m = *nq_dev;
     if (seq) nq = m;
-    else if ((int)blockIdx.x >= m) return;
+    else if (bidx >= m) return;
   }
   constexpr bool WEAK = MODE & SW_WEAK, CHAIN = MODE & SW_CHAIN, PRUNE = MODE & SW_PRUNE,
                  MERGE = MODE & SW_MERGE;
@@ -1092,10 +1111,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
   const bool w0 = tid < 64;     // wave 0 runs phase A and every summary round
   const bool act = tid < WS;    // lane w owns frontier word w
 
-  const int qa = seq ? 0 : blockIdx.x;
-  const int qb = seq ? nq : blockIdx.x + 1;
+  const int qa = seq ? 0 : bidx;
+  const int qb = seq ? nq : bidx + 1;
   for (int qi = qa; qi < qb; qi++) {
     const SweepQuery q = qs[qi];
+    if (!CHAIN && pm.commit && !pm.live(q.top)) {  // (block-uniform) a wave nobody pops
+      if (stats_out && threadIdx.x < 4) stats_out[4 * qi + threadIdx.x] = 0;
+      continue;
+    }
     const bool has_masks = q.flags & Q_MASKS;
     const bool shortcut = q.flags & Q_SHORTCUT;
     const int dreg = (q.flags & Q_REGULAR) ? mv.dreg : 0x7fffffff;
@@ -1149,7 +1172,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
               const u64 fl = __shfl(f, l >> 6), pl = __shfl(p, l >> 6);
               if (((fl & pl) >> (l & 63)) & 1ULL) {  // v' present, strong_path(leader, v'): push v' (process.go:344-349)
                 f = tid == (l >> 6) ? 1ULL << (l & 63) : 0ULL;
-                if (tid == 0) push_out[q.out_off + npush++] = wv;
+                if (tid == 0) {
+                  push_out[q.out_off + npush++] = wv;
+                  if (pm.pushed) pm.pushed[wv] = pm.epoch;  // (a delivery query of wave wv is live)
+                }
                 single = l;  // the chain restarts at v' alone
               }
             }
@@ -1314,6 +1340,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
   }
 }
 
+template <int WS, int NT, int MODE>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_MERGE) ? 3 : 1))) void k_sweep(
+    DagView g, MemoView mv, const SweepQuery *__restrict__ qs, int nq, int seq, int depth_log2, u64 *__restrict__ masks,
+    u64 *__restrict__ dlv, int32_t *__restrict__ push_out, int32_t *__restrict__ push_n, u64 *__restrict__ edges_out,
+    u64 *__restrict__ wedges_out, uint8_t *__restrict__ hit_out, int32_t *__restrict__ stop_out,
+    u64 *__restrict__ stats_out, const int *__restrict__ nq_dev, uint32_t *__restrict__ rcnt, const PopMark pm) {
+  sweep_body<WS, NT, MODE>((int)blockIdx.x, g, mv, qs, nq, seq, depth_log2, masks, dlv, push_out, push_n, edges_out,
+                           wedges_out, hit_out, stop_out, stats_out, nq_dev, rcnt, pm);
+}
+
 // Leader chains (SW_CHAIN: strong only, process.go:341-350) for n <= 64 * WS, WS <=
 // 4, one wavefront per chain and every round in registers: lane l holds the WS rows
 // of sources l*WS .. l*WS + WS-1 (WS * WS contiguous words), loaded PF rounds ahead
@@ -1326,14 +1362,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
 // pushes, push count, edges (strong degrees of every expanded vertex), hits (no
 // target: 0), stop (-1 - the round the sweep ended at).  Four chains per workgroup.
 template <int WS, int PF>
-__global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *__restrict__ qs,
-                                                   const int *__restrict__ nq_dev, int32_t *__restrict__ push_out,
-                                                   int32_t *__restrict__ push_n, u64 *__restrict__ edges_out,
-                                                   u64 *__restrict__ wedges_out, uint8_t *__restrict__ hit_out,
-                                                   int32_t *__restrict__ stop_out) {
+__device__ __forceinline__ void chain_reg_body(const int bidx, DagView g, const SweepQuery *__restrict__ qs,
+                                               const int *__restrict__ nq_dev, int32_t *__restrict__ push_out,
+                                               int32_t *__restrict__ push_n, u64 *__restrict__ edges_out,
+                                               u64 *__restrict__ wedges_out, uint8_t *__restrict__ hit_out,
+                                               int32_t *__restrict__ stop_out, const PopMark pm) {
   static_assert(WS >= 1 && WS <= 4 && PF >= 2, "register-resident rounds");
   constexpr int RW = WS * WS;  // words of the lane's rows per round
-  const int lane = threadIdx.x & 63, qi = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, qi = bidx * 4 + (int)(threadIdx.x >> 6);
   if (qi >= *nq_dev) return;  // wave-uniform
   const SweepQuery q = qs[qi];
   constexpr int PB = 64;  // pushes buffered per chain
@@ -1404,7 +1440,10 @@ __global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *
           if (lane == 0) pbuf[npush & (PB - 1)] = wv;
           npush++;
           if ((npush & (PB - 1)) == 0) {  // (a chain of more than PB pushes: flush)
-            if (lane < PB) push_out[q.out_off + npush - PB + lane] = pbuf[lane];
+            if (lane < PB) {
+              push_out[q.out_off + npush - PB + lane] = pbuf[lane];
+              if (pm.pushed) pm.pushed[pbuf[lane]] = pm.epoch;
+            }
           }
         }
       }
@@ -1442,7 +1481,10 @@ __global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *
   }
   {
     const int left = npush & (PB - 1);
-    if (lane < left) push_out[q.out_off + npush - left + lane] = pbuf[lane];
+    if (lane < left) {
+      push_out[q.out_off + npush - left + lane] = pbuf[lane];
+      if (pm.pushed) pm.pushed[pbuf[lane]] = pm.epoch;  // (a delivery query of that wave is live)
+    }
   }
   e = wave_sum(e);
   if (lane == 0) {
@@ -1452,6 +1494,16 @@ __global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *
     if (hit_out) hit_out[qi] = 0;
     if (stop_out) stop_out[qi] = -1 - stop_r;
   }
+}
+
+template <int WS, int PF>
+__global__ __launch_bounds__(256) void k_chain_reg(DagView g, const SweepQuery *__restrict__ qs,
+                                                   const int *__restrict__ nq_dev, int32_t *__restrict__ push_out,
+                                                   int32_t *__restrict__ push_n, u64 *__restrict__ edges_out,
+                                                   u64 *__restrict__ wedges_out, uint8_t *__restrict__ hit_out,
+                                                   int32_t *__restrict__ stop_out, const PopMark pm) {
+  chain_reg_body<WS, PF>((int)blockIdx.x, g, qs, nq_dev, push_out, push_n, edges_out, wedges_out, hit_out, stop_out,
+                         pm);
 }
 
 // The planned replay's final pass (one workgroup), after the emitting sweep.
@@ -1888,12 +1940,12 @@ __global__ __launch_bounds__(256) void k_canon_diff(DagView g, int lo, const u64
 // C_{r-1} (k_kcand's counts, rewritten here for the segment rounds).
 // ---------------------------------------------------------------------------
 template <int WS, int NT>
-__global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int depth_log2,
-                                              u64 *__restrict__ K, const uint8_t *__restrict__ good,
-                                              u64 *__restrict__ CE, int32_t *__restrict__ nseg,
-                                              u64 *__restrict__ RD, u64 *__restrict__ Cc,
-                                              uint32_t *__restrict__ crbase, const u64 *__restrict__ ppref,
-                                              int *__restrict__ rlo) {
+__device__ __forceinline__ void canon_body(DagView g, MemoView mv, int T, int depth_log2,
+                                           u64 *__restrict__ K, const uint8_t *__restrict__ good,
+                                           u64 *__restrict__ CE, int32_t *__restrict__ nseg,
+                                           u64 *__restrict__ RD, u64 *__restrict__ Cc,
+                                           uint32_t *__restrict__ crbase, const u64 *__restrict__ ppref,
+                                           int *__restrict__ rlo) {
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
   u64 *F = smem, *FE = smem + WS, *ring = smem + 2 * WS;
   const int depth = 1 << depth_log2, dmask = depth - 1;
@@ -2100,6 +2152,58 @@ __global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int
     if (tid == 0 && s_bad != INT_MAX) atomicMin(rlo, s_bad);
   }
   DR_TT(if (tid == 0) g_canon_timing[2] = wall_clock64();)
+}
+
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_canon(DagView g, MemoView mv, int T, int depth_log2,
+                                              u64 *__restrict__ K, const uint8_t *__restrict__ good,
+                                              u64 *__restrict__ CE, int32_t *__restrict__ nseg,
+                                              u64 *__restrict__ RD, u64 *__restrict__ Cc,
+                                              uint32_t *__restrict__ crbase, const u64 *__restrict__ ppref,
+                                              int *__restrict__ rlo) {
+  canon_body<WS, NT>(g, mv, T, depth_log2, K, good, CE, nseg, RD, Cc, crbase, ppref, rlo);
+}
+
+// The canonical walk (workgroup 0) and the leader chains (every other workgroup) in one
+// launch: the chains need only the commits and the rows, the walk only the summaries, so
+// neither waits for the other and no second stream (no fork or join event, ~18 us on
+// MI355X, tools/experiments/launch_probe.hip) is needed.  CREG: the chains on one
+// wavefront each (chain_reg_body, NT = 256), else k_sweep's chain mode.
+struct CanonArgs {
+  int T, depth_log2;
+  u64 *K;
+  const uint8_t *good;
+  u64 *CE;
+  int32_t *nseg;
+  u64 *RD, *Cc;
+  uint32_t *crbase;
+  const u64 *ppref;
+  int *rlo;
+};
+struct ChainArgs {
+  const SweepQuery *q;
+  const int *nq_dev;
+  int32_t *push_out, *push_n;
+  u64 *edges, *wedges;
+  uint8_t *hits;
+  int32_t *stops;
+  PopMark pm;
+};
+template <int WS, int NT, bool CREG>
+__global__ __launch_bounds__(NT) void k_canon_chains(DagView g, MemoView mv, const CanonArgs ca, const ChainArgs xa) {
+  if (blockIdx.x == 0) {
+    canon_body<WS, NT>(g, mv, ca.T, ca.depth_log2, ca.K, ca.good, ca.CE, ca.nseg, ca.RD, ca.Cc, ca.crbase, ca.ppref,
+                       ca.rlo);
+    return;
+  }
+  if constexpr (CREG) {
+    chain_reg_body<WS, 3>((int)blockIdx.x - 1, g, xa.q, xa.nq_dev, xa.push_out, xa.push_n, xa.edges, xa.wedges,
+                          xa.hits, xa.stops, xa.pm);
+  } else {
+    sweep_body<WS, NT, SW_CHAIN>((int)blockIdx.x - 1, g, mv, xa.q, 0, 0, ca.depth_log2, nullptr, nullptr, xa.push_out,
+                                 xa.push_n, xa.edges, xa.wedges, xa.hits, xa.stops, nullptr, xa.nq_dev, nullptr,
+                                 xa.pm);
+  }
 }
 
 // ---------------------------------------------------------------------------

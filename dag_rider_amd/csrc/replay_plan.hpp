@@ -115,10 +115,10 @@ constexpr int kPlanK = 4;
 // wave - floor >= 2 walks rounds 4(w-1)+1 .. 4 floor + 1 and may push up to
 // wave - floor - 1 leaders at out_off.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ commit, const uint16_t *__restrict__ lead,
-                                                    int nw, int persistent, int qflags, int32_t *__restrict__ task_wave,
-                                                    int32_t *__restrict__ task_q, SweepQuery *__restrict__ cq,
-                                                    int32_t *__restrict__ plan) {
+__device__ __forceinline__ void plan_chains_body(const uint8_t *__restrict__ commit, const uint16_t *__restrict__ lead,
+                                                 int nw, int persistent, int qflags, int32_t *__restrict__ task_wave,
+                                                 int32_t *__restrict__ task_q, SweepQuery *__restrict__ cq,
+                                                 int32_t *__restrict__ plan) {
   constexpr int K = kPlanK, CH = NT * K;
   __shared__ int64_t s[2 * (NT / 64)];
   const int tid = threadIdx.x;
@@ -184,12 +184,50 @@ __global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ 
   }
 }
 
+template <int NT>
+__global__ __launch_bounds__(NT) void k_plan_chains(const uint8_t *__restrict__ commit, const uint16_t *__restrict__ lead,
+                                                    int nw, int persistent, int qflags, int32_t *__restrict__ task_wave,
+                                                    int32_t *__restrict__ task_q, SweepQuery *__restrict__ cq,
+                                                    int32_t *__restrict__ plan) {
+  plan_chains_body<NT>(commit, lead, nw, persistent, qflags, task_wave, task_q, cq, plan);
+}
+
+// The round summaries' weak unions and speculative digests (k_weak_union, four rounds a
+// workgroup) and, in the grid's last workgroup, the leader-chain plan (plan_chains_body):
+// the chains' queries need only the commits, so they are ready when the canonical walk's
+// launch starts its chain workgroups (k_canon_chains).
+struct ChainPlanArgs {
+  const uint8_t *commit;
+  const uint16_t *lead;
+  int nw, persistent, qflags;
+  int32_t *task_wave, *task_q;
+  SweepQuery *cq;
+  int32_t *plan;
+};
+template <int WS>
+__global__ __launch_bounds__(256) void k_wu_plan(DagView g, int T, int dd, u64 *__restrict__ WU,
+                                                 const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
+                                                 const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG,
+                                                 const ChainPlanArgs pa) {
+  if (blockIdx.x == gridDim.x - 1) {
+    plan_chains_body<256>(pa.commit, pa.lead, pa.nw, pa.persistent, pa.qflags, pa.task_wave, pa.task_q, pa.cq, pa.plan);
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) u64 wu_lds[];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = (int)blockIdx.x * 4 + wid + 1;  // one wave per round
+  if (r > T) return;  // wave-uniform
+  weak_union_round<WS>(g, r, dd, WU, wu_lds + (size_t)wid * dd * WS, ppref, slot_off, slot_src, RG, lane);
+}
+
 // Pushes (task wave, then its chain's pushes in push order) -> pops in pop
 // order (each task's pushes reversed, process.go:406-412), push_off per wave,
 // and one delivery query per distinct leader, highest round first, with
-// cumulative mask images (rounds 0..top).
+// cumulative mask images (rounds 0..top).  qidx_static (REF): the delivery
+// queries were swept already from the static table of every wave whose leader is
+// present (no dependence on the chains); a pop takes its leader wave's entry.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, const uint16_t *__restrict__ lead,
+__device__ __forceinline__ void plan_pops_body(int nw, int WS, int qflags, const uint16_t *__restrict__ lead,
                                                   const int32_t *__restrict__ task_wave,
                                                   const int32_t *__restrict__ task_q,
                                                   const SweepQuery *__restrict__ cq,
@@ -199,7 +237,9 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
                                                   int32_t *__restrict__ push_wave, int32_t *__restrict__ pop_wave,
                                                   int32_t *__restrict__ pop_cur, int32_t *__restrict__ pop_q,
                                                   uint8_t *__restrict__ seen, int32_t *__restrict__ qidx,
-                                                  SweepQuery *__restrict__ dq, int32_t *__restrict__ plan) {
+                                                  SweepQuery *__restrict__ dq, int32_t *__restrict__ plan,
+                                                  const int32_t *__restrict__ qidx_static,
+                                                  int nqd_static) {
   constexpr int K = kPlanK, CH = NT * K;
   __shared__ int64_t s[2 * (NT / 64)];
   const int tid = threadIdx.x;
@@ -253,6 +293,12 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
     const uint32_t v = (uint32_t)(t < ntask ? task_pos[t] : np);
     for (int w = wlo; w <= whi; w++) push_off[w - 1] = v;
   }
+  if (qidx_static) {  // the delivery queries are the static per-wave table (one per present leader)
+    __syncthreads();  // pop_wave written (block-uniform branch: a kernel argument)
+    if (tid == 0) plan[PL_NQD] = nqd_static;
+    for (int64_t p = tid; p < np; p += NT) pop_q[p] = qidx_static[pop_wave[p]];
+    return;
+  }
   __syncthreads();  // seen written
   int64_t c0 = 0, c1 = 0;  // running totals (block-uniform)
   for (int i0 = 0; i0 < nw; i0 += CH) {
@@ -286,6 +332,42 @@ __global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, co
   __syncthreads();  // qidx written
   for (int64_t p = tid; p < np; p += NT) pop_q[p] = qidx[pop_wave[p]];
 }
+template <int NT>
+__global__ __launch_bounds__(NT) void k_plan_pops(int nw, int WS, int qflags, const uint16_t *__restrict__ lead,
+                                                  const int32_t *__restrict__ task_wave,
+                                                  const int32_t *__restrict__ task_q,
+                                                  const SweepQuery *__restrict__ cq,
+                                                  const int32_t *__restrict__ push_n,
+                                                  const int32_t *__restrict__ push_out, int64_t pcap,
+                                                  int64_t *__restrict__ task_pos, uint32_t *__restrict__ push_off,
+                                                  int32_t *__restrict__ push_wave, int32_t *__restrict__ pop_wave,
+                                                  int32_t *__restrict__ pop_cur, int32_t *__restrict__ pop_q,
+                                                  uint8_t *__restrict__ seen, int32_t *__restrict__ qidx,
+                                                  SweepQuery *__restrict__ dq, int32_t *__restrict__ plan,
+                                                  const int32_t *__restrict__ qidx_static = nullptr,
+                                                  int nqd_static = 0) {
+  plan_pops_body<NT>(nw, WS, qflags, lead, task_wave, task_q, cq, push_n, push_out, pcap, task_pos, push_off,
+                     push_wave, pop_wave, pop_cur, pop_q, seen, qidx, dq, plan, qidx_static, nqd_static);
+}
+// plan_pops_body's arguments, for the workgroup of k_own_emit that runs it
+struct PopPlanArgs {
+  int active;  // 0: no plan workgroup
+  int nw, WS, qflags;
+  const uint16_t *lead;
+  const int32_t *task_wave, *task_q;
+  const SweepQuery *cq;
+  const int32_t *push_n, *push_out;
+  int64_t pcap;
+  int64_t *task_pos;
+  uint32_t *push_off;
+  int32_t *push_wave, *pop_wave, *pop_cur, *pop_q;
+  uint8_t *seen;
+  int32_t *qidx;
+  SweepQuery *dq;
+  int32_t *plan;
+  const int32_t *qidx_static;
+  int nqd_static;
+};
 
 // Stops -> per-pop emission segment + canonical terms (run_deliver's on_batch):
 // merged at m = stop: rounds 1..min(m, cur) are canonical (prefixes C, G, E),
@@ -665,19 +747,31 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
                                                  const uint16_t *__restrict__ slot_src, u64 *__restrict__ qcount,
                                                  u64 *__restrict__ qdigest, int32_t *__restrict__ qcut, int T,
                                                  const u64 *__restrict__ RG, const u64 *__restrict__ CE,
-                                                 u64 *__restrict__ Gc, u64 *__restrict__ Ec) {
+                                                 u64 *__restrict__ Gc, u64 *__restrict__ Ec, const PopMark pm,
+                                                 const PopPlanArgs pp) {
   constexpr int NWV = NT / 64;
   __shared__ u64 s_c[NWV], s_dg;
-  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (Gc && q == (int)gridDim.x - 1) {  // (Gc null: k_canon_prefix computed them)
+  // workgroup 0 (with Gc): the canonical prefixes G, E -- the longest workgroup, so it
+  // starts first; the last (pp.active): the pop plan (plan_pops_body), which needs only the
+  // chains' pushes (the launch before this one)
+  const int pre = Gc ? 1 : 0, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (pre && blockIdx.x == 0) {  // (Gc null: k_canon_prefix computed them)
     canon_prefix_regs<NT, 8>(T, RG, CE, Gc, Ec);
     return;
   }
+  if (pp.active && blockIdx.x == gridDim.x - 1) {
+    plan_pops_body<NT>(pp.nw, pp.WS, pp.qflags, pp.lead, pp.task_wave, pp.task_q, pp.cq, pp.push_n, pp.push_out,
+                       pp.pcap, pp.task_pos, pp.push_off, pp.push_wave, pp.pop_wave, pp.pop_cur, pp.pop_q, pp.seen,
+                       pp.qidx, pp.dq, pp.plan, pp.qidx_static, pp.nqd_static);
+    return;
+  }
+  const int q = (int)blockIdx.x - pre;
   // the query's fields load with the plan counts (the arena holds every slot below the grid bound)
   const int nq = plan[PL_NQD], caperr = plan[PL_CAPERR];
   const int stop = stops[q], top = dq[q].top;
   const int64_t moff = dq[q].mask_off;
   if (q >= nq || caperr) return;
+  if (pm.commit && !pm.live(top)) return;  // a wave nobody pops: its sweep did not run
   const int cut = stop >= 0 ? min(stop + dmax - 1, top) : -1;
   const int first = stop >= 0 ? cut + 1 : max(1, -1 - stop);
   const u64 pos0 = cut >= 0 ? Cc[cut] : 0ULL;
@@ -716,6 +810,47 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
     qdigest[q] = s_dg;
     qcut[q] = cut;
   }
+}
+
+// Upward weak edges (App. A Q8: to the same or a later round) on the memo path
+// (engine.hip dr_replay, up_verify).  The replay ran on the regular graph G_reg; an
+// edge u -> v changes no cone C computed there when u in C implies v in C (C is then
+// closed under the edge, so the least closed set holding the query is still C).  One
+// thread per (edge, cone) pair -- the canonical cone K (q = -1) and every delivery
+// query of the static table, whose cone is K at and below its cut and its own mask
+// rows above (an unmerged query: its rows down to where it ended) -- counts the pairs
+// where u is reached and v is not.  Any count sends dr_replay to the general sweep.
+template <int WS>
+__global__ __launch_bounds__(256) void k_verify_up(const u64 *__restrict__ K, const u64 *__restrict__ masks,
+                                                   const SweepQuery *__restrict__ dq, int nq,
+                                                   const int32_t *__restrict__ stops, const int32_t *__restrict__ qcut,
+                                                   const int4 *__restrict__ up, int ne, int32_t *__restrict__ bad,
+                                                   const PopMark pm) {
+  const int64_t n = (int64_t)ne * (nq + 1);
+  int cnt = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(i / (nq + 1)), q = (int)(i % (nq + 1)) - 1;
+    const int4 E = up[e];  // (ru, su0, rv, tv0)
+    auto bitK = [&](int r, int s) { return ((K[(size_t)r * WS + (s >> 6)] >> (s & 63)) & 1ULL) != 0; };
+    bool in_u, in_v;
+    if (q < 0) {
+      in_u = bitK(E.x, E.y);
+      in_v = bitK(E.z, E.w);
+    } else {
+      const SweepQuery Q = dq[q];
+      if (pm.commit && !pm.live(Q.top)) continue;  // a wave nobody pops (its sweep did not run)
+      const int stop = stops[q], cut = qcut[q], lo = stop >= 0 ? 0 : -1 - stop;
+      auto in = [&](int r, int s) -> bool {
+        if (r > Q.top || r < lo) return false;
+        if (r <= cut) return bitK(r, s);
+        return ((masks[Q.mask_off + (int64_t)r * WS + (s >> 6)] >> (s & 63)) & 1ULL) != 0;
+      };
+      in_u = in(E.x, E.y);
+      in_v = in(E.z, E.w);
+    }
+    cnt += in_u && !in_v;
+  }
+  if (cnt) atomicAdd(bad, cnt);
 }
 
 }  // namespace dr

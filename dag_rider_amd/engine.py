@@ -155,6 +155,11 @@ class Engine:
             cfg.probe[i] = int(r)
         self._check(self._L.dr_set_slice(self._h, C.byref(cfg)))
 
+    def last_replay_path(self) -> int:
+        """dr_last_replay_path: 0 memo, 1 memo with the upward edges verified, 2 general after a
+        failed check, 3 general."""
+        return int(self._L.dr_last_replay_path(self._h))
+
     def slice_result(self) -> dict:
         """dr_slice_result: C, G, E at the probes, the owned pops' lowest merge round and the
         owned commits' chain edges from the last dr_replay."""

@@ -287,7 +287,9 @@ typedef struct {
    * included).  A fused dr_replay_batch sets ms_deliver = the fused kernel in every
    * output and, in the first output only, the call's host phases: ms_commit = host
    * preparation before the launch, ms_summary = launch to results on the host,
-   * ms_chain = the copy back (device), ms_emit = unpacking into the outputs */
+   * ms_chain = the copy back (device), ms_emit = unpacking into the outputs.  A
+   * device-planned REF dr_replay runs its leader chains inside the canonical walk's
+   * launch and reports ms_chain = 0 */
   float ms_commit, ms_chain, ms_deliver, ms_emit, ms_summary;
   int32_t canon_segments; /* partial-round segments of the canonical cone (-1: summaries off) */
   /* work done by the delivery sweeps (identical leaders share one sweep):
@@ -361,6 +363,14 @@ int dr_last_batch_form(const dr_ctx *ctx);
  * arrays staged, [3] the copy launch (the call does not wait for the device: later
  * calls of the context run behind the copy on its stream). */
 int dr_last_append_phases(const dr_ctx *ctx, float *ms4);
+
+/* The path the last dr_replay took: 0 the memoized (or full-cone) replay on the
+ * regular graph; 1 the same with weak edges to the same or a later round (App. A
+ * Q8) checked against every cone it computed and found not to change one
+ * (k_verify_up); 2 the general sweep after that check found a cone they change; 3 the
+ * general sweep (strong edges upward, too many such edges, or PAPER delivery); -1
+ * none yet. */
+int dr_last_replay_path(const dr_ctx *ctx);
 
 /* Wave-range slice of one DAG (SURVEY.md s8(e) row 1 widened to the whole replay:
  * waveReady :314-354 and orderVertices :404-443 of a contiguous wave range on the GPU

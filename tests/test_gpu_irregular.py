@@ -138,3 +138,44 @@ def test_irregular_vertex_through_buffer_admit(gpu_device):
             ids_, cnt_, dg_ = e.order_vertices([(R + 1, 2), (R - 3, 1)], R + 1, mode)
             rc, want_ids, wc, wd = ld.order_vertices([(R + 1, 2), (R - 3, 1)], R + 1, mode)
             assert rc == 0 and ids_.tolist() == want_ids.tolist() and dg_.tolist() == wd.tolist()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_upward_weak_edges_verified_memo(gpu_device, seed):
+    """Weak edges to the same or a later round on quorum-shaped DAGs:
+    dr_replay (REF, no ids) runs the memo replay on the regular graph and checks every
+    such edge against every cone it computed (k_verify_up).  Edges inside the canonical
+    regime change no cone -> the memo path answers (dr_last_replay_path 1); an edge from a
+    low vertex up to a late one nobody reaches does -> the general sweep (2).  Both equal
+    the literal restatement's BFS, in both chain modes."""
+    from dag_rider_amd.gen import generate, small_config, with_extra_edges
+
+    rng = np.random.default_rng(5600 + seed)
+    n = int(rng.choice([16, 64, 130]))
+    cfg = small_config(n, 4 * int(rng.integers(10, 25)), 5600 + seed, p_present=1.0, p_late=0.05, p_w=0.4,
+                       weak_depth=4)
+    d = generate(cfg)
+    R = d.nrounds - 1
+    present = lambda r: [int(s) for s in d.slot_src[d.slot_off[r]:d.slot_off[r + 1]] if s]  # noqa: E731
+    benign = []
+    for _ in range(3):  # same-round and one-round-up edges in the middle (full canonical rounds)
+        r = int(rng.integers(R // 3, 2 * R // 3))
+        a, b = rng.choice(present(r), size=2, replace=False)
+        benign.append((r, int(a), r, int(b), False))
+        up = present(r + 1)
+        benign.append((r, int(a), r + 1, int(up[int(rng.integers(0, len(up)))]), False))
+    # from a round-2 vertex up to the top round: the top round's vertices are reached by no
+    # lower pop, so the cones holding the round-2 vertex grow
+    bad = [(2, present(2)[0], R, present(R)[-1], False)]
+    for extra, want_path in ((benign, 1), (benign + bad, 2)):
+        dx = with_extra_edges(d, extra)
+        ld = oracle.LDag(packed=dx)
+        with Engine(n, cfg.faulty, dx.nrounds, gpu_device) as e:
+            e.append_packed(dx)
+            assert e.exception_stats()["upward"] == len(extra)
+            for cm in (L.DR_CHAIN_PERSISTENT, L.DR_CHAIN_LITERAL):
+                want = ld.replay(cfg.faulty, cfg.nwaves, cm, L.DR_DELIVER_REF)
+                assert want.rc == 0
+                got = e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF)
+                _same(got, want, ids=False)
+                assert e.last_replay_path() == want_path, (cm, e.last_replay_path())
