@@ -810,7 +810,7 @@ def run_c5(args, rank: int, world: int, local: int, dist):
     for i in range(lo, hi):
         cfg = c5_config(i)
         d = generate(cfg)
-        e = Engine(cfg.n, cfg.faulty, d.nrounds, local)
+        e = Engine(cfg.n, cfg.faulty, d.nrounds, local, shared_stream=True)  # one HIP stream for the batch
         e.append_packed(d)
         engines.append(e)
         dags.append(d)

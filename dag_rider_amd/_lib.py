@@ -25,6 +25,8 @@ DR_OPT_PHASE_TIMING = 3
 DR_OPT_BATCH_FORM = 4
 DR_OPT_COMMIT_SPLIT = 5
 DR_OPT_REPLAY_GRAPH = 6
+DR_OPT_FUSE = 7
+DR_CREATE_SHARED_STREAM = 1
 DR_BATCH_AUTO, DR_BATCH_WORKGROUP, DR_BATCH_WAVE = 0, 1, 2
 DR_LEADER_CONST1, DR_LEADER_SEEDED, DR_LEADER_TABLE = 0, 1, 2
 DR_SHARD_ID_BYTES = 128
@@ -74,6 +76,7 @@ SIGNATURES = {
     "dr_abi_version": (C.c_int, []),
     "dr_build_id": (C.c_char_p, []),
     "dr_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)]),
+    "dr_create_ex": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)]),
     "dr_destroy": (None, [P]),
     "dr_last_error": (C.c_char_p, [P]),
     "dr_num_rounds": (C.c_int, [P]),

@@ -84,6 +84,9 @@ struct SmallJob {
 constexpr int kSmallMaxPops = 64 * 65 / 2;  // literal chains: wave w pushes up to w leaders
 constexpr int kSmallNT = 256;               // four wavefronts per DAG
 constexpr int kSmallPF = 4;                 // rounds loaded ahead by the cone passes
+// u64 words of a job's cone scratch per round: the workgroup form's dense [2][64] sets, or
+// the wave form's record (K, mask, up to 64 lanes' sets: 3 + 128 words)
+constexpr int kConeRecWords = 131;
 
 // dynamic LDS of k_replay_small (D = ring slots, a power of two above the
 // largest weak delta): pass 2F's weak ring [D][2][64] u64 and K's weak targets

@@ -169,6 +169,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     row(T + 1 + k, lane + 64, ha[k][1], hb[k][1]);
     hp[k] = pbits(pres_word(T + 1 + k, 0), pres_word(T + 1 + k, 1));
   }
+  uint32_t crec = (uint32_t)(T + 1) * kConeRecWords;  // the cone records (below)
   u64 F0 = 0, F1 = 0;  // F_b: round-r vertices in leader b's cone
   u64 G0 = 0, G1 = 0;  // G_b: the same over strong edges only
   uint32_t suf = 0;    // strong degrees summed over G_b, rounds r..T
@@ -301,8 +302,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         QL[w - 1] = 0;
       }
     }
-    g_cone[((size_t)r * 2) * 64 + lane] = F0;
-    g_cone[((size_t)r * 2 + 1) * 64 + lane] = F1;
     // K (lane 63) and the leaders whose sets differ from it ("solo": expanded on their own)
     u64 K0 = 0, K1 = 0, KG0 = 0, KG1 = 0;
     if (haveK) {
@@ -310,6 +309,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
       K1 = readlane64(F1, 63);
       KG0 = readlane64(G0, 63);
       KG1 = readlane64(G1, 63);
+    }
+    {  // round r's cone record for the emission: K, the lanes whose set differs from K, their sets
+      const u64 dm = __ballot(F0 != K0 || F1 != K1);
+      crec -= 3u + 2u * (uint32_t)__popcll(dm);
+      u64 DR_GLOBAL *rec = g_cone + crec;
+      if (lane == 0) {
+        rec[0] = K0;
+        rec[1] = K1;
+        rec[2] = dm;
+      }
+      if ((dm >> lane) & 1ULL) {
+        const uint32_t at = 3u + 2u * (uint32_t)__popcll(dm & ((1ULL << lane) - 1ULL));
+        rec[at] = F0;
+        rec[at + 1] = F1;
+      }
     }
     const bool eqF = haveK && F0 == K0 && F1 == K1, eqG = haveK && G0 == KG0 && G1 == KG1;
     const u64 soloF = __ballot(!eqF && (F0 | F1) != 0ULL), soloG = __ballot(!eqG && (G0 | G1) != 0ULL);
@@ -385,6 +399,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     __syncthreads();
     DR_TT(tick(5);)  // the leaders' own expansions
   };
+  // crec: the cone records, written top down from the end of the job's scratch (round T's
+  // highest): round 1's is the lowest, and each round's follows the one below it, so the
+  // bottom-up emission reads them in address order.  A record is K (2 words), the mask of
+  // the lanes whose set differs from K, and those lanes' sets in lane order: C5's leaders
+  // equal K below their top few rounds, so this is ~1/10 of all 64 lanes' sets per round
+  // (the dense [round][2][64] image was ~35 % of the kernel's HBM traffic)
   Pf pa, pb;
   prefetch2(T, pa);
   for (int r = T; r >= 1; r -= 2) {
@@ -490,13 +510,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   };
   // software pipeline: round r+1's sets, degrees, presence and slots load while
   // round r is processed
+  // the cone records in two stages: round r+1's header (K, mask) was loaded a round ago,
+  // its lanes' sets load now, and round r+2's header, whose address follows from r+1's mask
   u64 pf0 = 0, pf1 = 0, pp0 = 0, pp1 = 0;
+  u64 pk0 = 0, pk1 = 0, pm = 0;  // the header of the round whose sets pf0 / pf1 hold
+  u64 hk0 = 0, hk1 = 0, hm = 0;  // the next round's header
+  uint32_t hat = crec;           // the next round's record
+  auto load_hdr = [&](uint32_t at) {
+    hk0 = g_cone[at];
+    hk1 = g_cone[at + 1];
+    hm = g_cone[at + 2];
+  };
+  auto load_sets = [&]() {  // the sets of the round whose header is in hk / hm: unconditional loads
+    pk0 = hk0;
+    pk1 = hk1;
+    pm = hm;
+    const bool in = (pm >> lane) & 1ULL;
+    const uint32_t at = in ? hat + 3u + 2u * (uint32_t)__popcll(pm & ((1ULL << lane) - 1ULL)) : hat;
+    pf0 = g_cone[at];
+    pf1 = g_cone[at + 1];
+    hat += 3u + 2u * (uint32_t)__popcll(pm);
+  };
   uint16_t psd[2] = {0, 0}, pwd[2] = {0, 0};  // (16-bit: no widening right after the loads)
   uint32_t psa = 0, psb = 0;
   int pslo = 0, pshi = 0;
   auto prefetch4 = [&](int r) {
-    pf0 = g_cone[((size_t)r * 2) * 64 + lane];
-    pf1 = g_cone[((size_t)r * 2 + 1) * 64 + lane];
+    load_sets();
+    if (r < T) load_hdr(hat);
 #pragma unroll
     for (int i = 0; i < 2; i++) {
       const int v = lane + 64 * i;
@@ -511,10 +551,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     pslo = psa + lane < psb ? (int)g_slot_src[psa + lane] : 0;
     pshi = psa + 64 + lane < psb ? (int)g_slot_src[psa + 64 + lane] : 0;
   };
+  load_hdr(hat);
   prefetch4(1);
   for (int r = 1; r <= T; r++) {
     __syncthreads();
-    const u64 f0 = pf0, f1 = pf1, P0 = pp0, P1 = pp1;
+    const bool own = (pm >> lane) & 1ULL;  // this lane's set differs from K in round r
+    const u64 f0 = own ? pf0 : pk0, f1 = own ? pf1 : pk1, P0 = pp0, P1 = pp1;
     const uint32_t sa = psa, sb = psb;
     const int slo = pslo, shi = pshi;
 #pragma unroll

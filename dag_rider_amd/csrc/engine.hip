@@ -16,6 +16,7 @@
 #include <cstring>
 #include <string>
 #include <functional>
+#include <mutex>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -108,6 +109,7 @@ struct dr_ctx {
   int nrounds = 0;
   int dmax_near = 1;  // largest weak delta stored in the near format
   hipStream_t stream = nullptr;
+  bool shared_stream = false;  // DR_CREATE_SHARED_STREAM: stream is the device's shared one
   hipEvent_t ev[8] = {};
   // device DAG
   DevBuf strong, present, slot_off, slot_src, weak_roff, far, far_roff;
@@ -230,7 +232,12 @@ struct dr_ctx {
   // the planned replay's leader chains on one register-resident wavefront each at n <= 256
   // (k_chain_reg; DR_CHAIN_REG=0: k_sweep's chain mode)
   int chain_reg = getenv("DR_CHAIN_REG") ? atoi(getenv("DR_CHAIN_REG")) : 1;
-  int last_split = 0;    // workgroups per wave of the last commit launch (0: k_commit)
+  // DR_OPT_FUSE: bit 0 = a full replay's weak unions ride in the row pass's launch
+  // (dr::WUArgs, the chain plan then in k_kcand_plan); bit 1 = the canonical re-emission
+  // rides in the delivery sweeps' launch; bit 2 = the speculative G, E prefixes beside the
+  // canonical walk (k_canon_chains) and the pop plan beside the delivery sweeps
+  int fuse = getenv("DR_FUSE") ? atoi(getenv("DR_FUSE")) : 7;
+  int last_split = 0;   // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
   bool kprev_ok = false;
   int ndirty = 0;     // rounds with sdirty set
@@ -806,12 +813,17 @@ struct SweepArgs {  // (every field initialised: a launch never reads a stale po
   const int *nq_dev = nullptr;  // planned replay: query count on the device, nq = grid upper bound
   uint32_t *rcnt = nullptr;     // planned delivery: per-mask-row vertex counts for the emission
   dr::PopMark pm{};             // REF planned replay: live delivery queries / chain stamps
+  dr::CanonEmit ce{};           // merge sweeps: the canonical re-emission's workgroups (first in the grid)
+  dr::PopPlanArgs pp{};         // merge sweeps: the pop plan's workgroup (last in the grid; pp.active)
 };
 // The REF replay's leader chains inside the single-stream launches: the chain plan in the
 // weak-union launch (k_wu_plan), the chain sweeps beside the canonical walk (k_canon_chains)
 struct ChainFuse {
   dr::ChainPlanArgs pa;
   dr::ChainArgs xa;
+  bool plan_in_kcand = false;  // the weak unions rode in the row pass: the plan rides in k_kcand_plan
+  bool emit_in_sweep = false;  // the canonical re-emission rides in the delivery sweeps' launch
+  dr::SpecPrefix sp{};         // the speculative G, E prefixes beside the canonical walk (last workgroup)
 };
 
 // Raise a kernel's dynamic-LDS limit once per (device, size it has not seen yet):
@@ -837,10 +849,16 @@ hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   static std::atomic<int> seen[kLdsDevs] = {};
   hipError_t e = lds_limit((const void *)dr::k_sweep<WS, NT, MODE>, seen, c->dev, lds);
   if (e != hipSuccess) return e;
-  const int grid = a.seq ? 1 : a.nq;
+  const int ne = (MODE & dr::SW_MERGE) ? a.ce.nblk : 0;
+  const int np = (MODE & dr::SW_MERGE) && a.pp.active ? 1 : 0;
+  const int grid = (a.seq ? 1 : a.nq) + ne + np;
+  dr::CanonEmit ce = a.ce;
+  ce.nblk = ne;
+  dr::PopPlanArgs pp = a.pp;
+  pp.active = np;
   hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(grid), dim3(NT), lds, c->stream,
                      c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
-                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt, a.pm);
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt, a.pm, ce, pp);
   return hipGetLastError();
 }
 template <int WS>
@@ -897,6 +915,9 @@ hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode) {
 }
 
 constexpr int kEmitRPB = 4;  // rounds per emit workgroup: one per wave
+// workgroups of the delivery sweeps' launch that re-emit the canonical rounds (C4: a
+// top segment of a few dozen rounds, a wave each)
+constexpr int kCanonEmitBlocks = 16;
 
 // Planned mode (plan != nullptr, device-planned replay): the count pass runs
 // ndesc = an upper bound of workgroups and reads the true count from plan[0];
@@ -943,10 +964,33 @@ hipError_t launch_emit(dr_ctx *c, int ndesc, int span, const dr::PopDesc *pd, ui
 
 // k_summary_commit geometry (block, chunks in flight per thread, software
 // pipelining); dr_profile_kernel's variants time the alternatives.
+// rounds (waves) per k_weak_union workgroup: four, fewer when a deep window's
+// per-wave LDS slice (dd x WS words) would take the workgroup past 64 KiB
+inline int weak_union_waves(int dd, int WS, int cap = 4) {
+  const size_t per = (size_t)std::max(dd, 1) * WS * 8;
+  return (int)std::max<size_t>(1, std::min<size_t>(cap, 65536 / per));
+}
+// wu: the weak unions and speculative digests ride in the same launch (dr::WUArgs)
 template <int WS, int NT, int GRP, bool PIPE>
-hipError_t launch_sc(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
-  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, GRP, PIPE>), dim3((T + 3) / 4), dim3(NT), 0, c->stream,
-                     c->view(), T, nwc, 2 * c->f + 1, c->U.as<u64>(), c->SD.as<u64>(), cm, vc);
+hipError_t launch_sc(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc, bool wu = false) {
+  dr::WUArgs wa{};
+  const int nsum = (T + 3) / 4;
+  int grid = nsum;
+  size_t lds = 0;
+  if (wu) {
+    wa.nsum = nsum;
+    wa.dd = c->memo_dd();
+    wa.nwv = weak_union_waves(wa.dd, WS, NT / 64);
+    wa.WU = c->WU.as<u64>();
+    wa.ppref = c->ppref.as<u64>();
+    wa.slot_off = c->slot_off.as<uint32_t>();
+    wa.slot_src = c->slot_src.as<uint16_t>();
+    wa.RG = c->RG.as<u64>();
+    grid += (T + wa.nwv - 1) / wa.nwv;
+    lds = (size_t)wa.nwv * std::max(wa.dd, 1) * WS * 8;  // <= 64 KiB: no attribute needed
+  }
+  hipLaunchKernelGGL((dr::k_summary_commit<WS, NT, GRP, PIPE>), dim3(grid), dim3(NT), lds, c->stream, c->view(), T,
+                     nwc, 2 * c->f + 1, c->U.as<u64>(), c->SD.as<u64>(), cm, vc, wa);
   return hipGetLastError();
 }
 // WS = 16 (n = 1024): 1024 threads, 2 chunks per thread per group: 80.8 us
@@ -956,25 +1000,27 @@ hipError_t launch_sc(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
 // most CUs idle, and a CU's bandwidth is its bytes in flight over the latency: each thread
 // then keeps all 8 of its chunks of a round in flight (GRP 8).
 template <int WS>
-hipError_t launch_sc_shipped(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
+hipError_t launch_sc_shipped(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc, bool wu = false) {
   if constexpr (WS == 16) {
     if (c->cu_count <= 0) {
       int cus = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->dev) == hipSuccess) c->cu_count = cus;
     }
-    if ((T + 3) / 4 < c->cu_count) return launch_sc<WS, 1024, 8, false>(c, T, nwc, cm, vc);
-    return launch_sc<WS, 1024, 2, false>(c, T, nwc, cm, vc);
+    if ((T + 3) / 4 < c->cu_count) return launch_sc<WS, 1024, 8, false>(c, T, nwc, cm, vc, wu);
+    return launch_sc<WS, 1024, 2, false>(c, T, nwc, cm, vc, wu);
   }
-  return launch_sc<WS, summary_block<WS>(), 8, false>(c, T, nwc, cm, vc);
+  return launch_sc<WS, summary_block<WS>(), 8, false>(c, T, nwc, cm, vc, wu);
 }
 
 // rows + commit decisions (U, SD); the weak-edge unions (WU) come from the
-// weak-column keys alone (launch_weak_union), after it.  (Inside the row pass's
-// workgroups, one wave per round after the rows, they lengthened the pass by as much as
-// the separate launch took: C4 89 -> 105 us, profiles/r05/v7_*.)
+// weak-column keys alone: with wu, as extra workgroups after the row workgroups of the
+// same launch (they take the CUs the pass's last workgroups leave idle), else
+// launch_weak_union after it.  (Inside the row pass's workgroups, one wave per round
+// after the rows, they lengthened the pass by as much as the separate launch took:
+// C4 89 -> 105 us, profiles/r05/v7_*.)
 template <int WS>
-hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
-  hipError_t e = launch_sc_shipped<WS>(c, T, nwc, cm, vc);
+hipError_t launch_summary_t(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc, bool wu) {
+  hipError_t e = launch_sc_shipped<WS>(c, T, nwc, cm, vc, wu);
   if (e == hipSuccess) e = c->rec(7);  // ms_summary times k_summary_commit alone (the roofline kernel)
   return e;
 }
@@ -984,12 +1030,6 @@ template <int WS>
 hipError_t weak_union_lds(const dr_ctx *c, size_t lds) {
   static std::atomic<int> seen[kLdsDevs] = {};
   return lds_limit((const void *)dr::k_weak_union<WS>, seen, c->dev, lds);
-}
-// rounds (waves) per k_weak_union workgroup: four, fewer when a deep window's
-// per-wave LDS slice (dd x WS words) would take the workgroup past 64 KiB
-inline int weak_union_waves(int dd, int WS) {
-  const size_t per = (size_t)std::max(dd, 1) * WS * 8;
-  return (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / per));
 }
 template <int WS>
 hipError_t launch_weak_union_t(dr_ctx *c, int T, hipStream_t st) {
@@ -1071,10 +1111,16 @@ hipError_t launch_round_summary(dr_ctx *c, const int32_t *rounds, int nr) {
 template <int WS>
 hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo, bool spec, const ChainFuse *cf = nullptr) {
   const dr::MemoView mv = c->memo_view();
-  hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
-                     c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>(), c->rlo.as<int>(),
-                     spec ? T + 1 : lo, spec ? c->ppref.as<u64>() : nullptr, c->Cc.as<u64>(),
-                     c->crbase.as<uint32_t>());
+  if (cf && cf->plan_in_kcand)
+    hipLaunchKernelGGL((dr::k_kcand_plan<WS>), dim3((T + 1 + 3) / 4 + 1), dim3(256), 0, c->stream, c->view(), mv, T,
+                       c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>(), c->rlo.as<int>(),
+                       spec ? T + 1 : lo, spec ? c->ppref.as<u64>() : nullptr, c->Cc.as<u64>(),
+                       c->crbase.as<uint32_t>(), cf->pa);
+  else
+    hipLaunchKernelGGL((dr::k_kcand<WS>), dim3((T + 1 + 3) / 4), dim3(256), 0, c->stream, c->view(), mv, T,
+                       c->K.as<u64>(), c->good.as<uint8_t>(), c->CE.as<u64>(), c->RD.as<u64>(), c->rlo.as<int>(),
+                       spec ? T + 1 : lo, spec ? c->ppref.as<u64>() : nullptr, c->Cc.as<u64>(),
+                       c->crbase.as<uint32_t>());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int dl = c->depth_log2();
@@ -1092,15 +1138,15 @@ hipError_t launch_canon_cone_t(dr_ctx *c, int T, int lo, bool spec, const ChainF
         static std::atomic<int> seen_r[kLdsDevs] = {};
         e = lds_limit((const void *)dr::k_canon_chains<WS, NTS, true>, seen_r, c->dev, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((dr::k_canon_chains<WS, NTS, true>), dim3(1 + (nq + 3) / 4), dim3(NTS), lds, c->stream,
-                           c->view(), mv, ca, cf->xa);
+        hipLaunchKernelGGL((dr::k_canon_chains<WS, NTS, true>), dim3(1 + (nq + 3) / 4 + (cf->sp.on ? 1 : 0)),
+                           dim3(NTS), lds, c->stream, c->view(), mv, ca, cf->xa, cf->sp);
       }
     } else {
       static std::atomic<int> seen_s[kLdsDevs] = {};
       e = lds_limit((const void *)dr::k_canon_chains<WS, NTS, false>, seen_s, c->dev, lds);
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL((dr::k_canon_chains<WS, NTS, false>), dim3(1 + nq), dim3(NTS), lds, c->stream, c->view(),
-                         mv, ca, cf->xa);
+      hipLaunchKernelGGL((dr::k_canon_chains<WS, NTS, false>), dim3(1 + nq + (cf->sp.on ? 1 : 0)), dim3(NTS), lds,
+                         c->stream, c->view(), mv, ca, cf->xa, cf->sp);
     }
     e = hipGetLastError();
     if (e != hipSuccess || lo <= 1) return e;
@@ -1131,14 +1177,14 @@ hipError_t launch_canon_cone(dr_ctx *c, int T, int lo, bool spec, const ChainFus
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_summary(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc) {
+hipError_t launch_summary(dr_ctx *c, int T, int nwc, uint8_t *cm, int32_t *vc, bool wu = false) {
   switch (c->WS) {
-    case 1: return launch_summary_t<1>(c, T, nwc, cm, vc);
-    case 2: return launch_summary_t<2>(c, T, nwc, cm, vc);
-    case 4: return launch_summary_t<4>(c, T, nwc, cm, vc);
-    case 8: return launch_summary_t<8>(c, T, nwc, cm, vc);
-    case 16: return launch_summary_t<16>(c, T, nwc, cm, vc);
-    case 32: return launch_summary_t<32>(c, T, nwc, cm, vc);
+    case 1: return launch_summary_t<1>(c, T, nwc, cm, vc, wu);
+    case 2: return launch_summary_t<2>(c, T, nwc, cm, vc, wu);
+    case 4: return launch_summary_t<4>(c, T, nwc, cm, vc, wu);
+    case 8: return launch_summary_t<8>(c, T, nwc, cm, vc, wu);
+    case 16: return launch_summary_t<16>(c, T, nwc, cm, vc, wu);
+    case 32: return launch_summary_t<32>(c, T, nwc, cm, vc, wu);
   }
   return hipErrorInvalidValue;
 }
@@ -1164,7 +1210,43 @@ int h2d(dr_ctx *c, DevBuf &b, const std::vector<T> &v) {
 // ===========================================================================
 extern "C" int dr_abi_version(void) { return DR_ABI_VERSION; }
 
+// DR_CREATE_SHARED_STREAM: one HIP stream per device shared by every such context
+// (reference-counted, created with the first): a batch of thousands of small contexts
+// (C5) otherwise holds thousands of streams, and a device-wide synchronize walks each
+namespace {
+struct SharedStream {
+  hipStream_t s = nullptr;
+  int refs = 0;
+};
+std::mutex g_ss_mu;
+SharedStream g_ss[kLdsDevs];
+hipError_t shared_stream_get(int dev, hipStream_t *out) {
+  if (dev < 0 || dev >= kLdsDevs) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(g_ss_mu);
+  SharedStream &x = g_ss[dev];
+  if (!x.s) {
+    hipError_t e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+  }
+  x.refs++;
+  *out = x.s;
+  return hipSuccess;
+}
+void shared_stream_put(int dev) {
+  std::lock_guard<std::mutex> lk(g_ss_mu);
+  SharedStream &x = g_ss[dev];
+  if (--x.refs == 0) {
+    (void)hipStreamDestroy(x.s);
+    x.s = nullptr;
+  }
+}
+}  // namespace
+
 extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx **out) {
+  return dr_create_ex(n, faulty, max_rounds, device, 0, out);
+}
+
+extern "C" int dr_create_ex(int n, int faulty, int max_rounds, int device, int flags, dr_ctx **out) {
   if (!out) return DR_E_INVAL;
   *out = nullptr;
   if (n < 1 || n > 2048 || faulty < 0 || max_rounds < 1 || max_rounds > (1 << 20) || device < 0) {
@@ -1190,8 +1272,18 @@ extern "C" int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx *
   // (stream2 is created at the first fork, ensure_stream2: a context that never forks --
   // one DAG of a C5 batch -- keeps one HIP stream, and a device-wide synchronize walks
   // every stream of the process: 4096 contexts x 2 streams cost it ~2.7 ms)
-  if (set_device(c) != DR_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if ((flags & ~DR_CREATE_SHARED_STREAM) != 0) {
+    g_create_err = "dr_create_ex: unknown flags";
+    delete c;
+    return DR_E_INVAL;
+  }
+  c->shared_stream = (flags & DR_CREATE_SHARED_STREAM) != 0;
+  if (set_device(c) != DR_OK ||
+      (c->shared_stream ? shared_stream_get(device, &c->stream)
+                        : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
     g_create_err = "dr_create: stream creation failed";
+    c->shared_stream = false;
+    c->stream = nullptr;
     delete c;
     return DR_E_HIP;
   }
@@ -1259,7 +1351,10 @@ extern "C" void dr_destroy(dr_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   if (c->rg_exec) (void)hipGraphExecDestroy(c->rg_exec);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream) {
+    if (c->shared_stream) shared_stream_put(c->dev);
+    else (void)hipStreamDestroy(c->stream);
+  }
   delete c;
 }
 
@@ -1996,9 +2091,10 @@ int launch_canon(dr_ctx *c, bool fork, const std::function<int()> *side, bool fo
   d.last = T;
   d.out = 0;
   d.use_k = 1;
-  HIPCHK(c, launch_emit(c, 1, T, nullptr, c->crbase.as<uint32_t>(), nullptr, nullptr, c->RG.as<u64>(), nullptr,
-                        nullptr, 0, false, nullptr, nullptr, d, nullptr,
-                        c->rlo.as<int>()));  // the descriptor travels by value
+  if (!(cf && cf->emit_in_sweep && spec))  // (else the delivery sweeps' launch re-emits, dr::CanonEmit)
+    HIPCHK(c, launch_emit(c, 1, T, nullptr, c->crbase.as<uint32_t>(), nullptr, nullptr, c->RG.as<u64>(), nullptr,
+                          nullptr, 0, false, nullptr, nullptr, d, nullptr,
+                          c->rlo.as<int>()));  // the descriptor travels by value
   if (prefix)
     hipLaunchKernelGGL((dr::k_canon_prefix<1024>), dim3(1), dim3(1024), 0, c->stream, T, c->RG.as<u64>(),
                        c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>());
@@ -2052,17 +2148,25 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
                   bool prefix = true, int parts = 3, const ChainFuse *cf = nullptr) {
   const int T = c->nrounds - 1;
   if (T < 1) return c->fail(DR_E_STATE, "summary needs rounds 0..1 at least");
+  const bool wu_fused = (c->fuse & 1) != 0;  // (the same for both parts of one replay)
   if (parts & 1) {
     if (int rc = ensure_summary_bufs(c)) return rc;
     HIPCHK(c, c->commit.ensure((size_t)std::max(nwc, 1)));
     HIPCHK(c, c->vcount.ensure((size_t)std::max(nwc, 1) * 4));
-    // rows + commits, then the weak unions from the weak-column keys (on a second
-    // stream beside the row pass they only queued behind its workgroups and paid a
-    // cross-stream join: profiles/r02/v30_timeline.txt)
+    // rows + commits and the weak unions from the weak-column keys, as the same launch's
+    // last workgroups or a launch after it (on a second stream beside the row pass they
+    // only queued behind its workgroups and paid a cross-stream join:
+    // profiles/r02/v30_timeline.txt)
     HIPCHK(c, c->rec(6));
-    HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));  // records ev[7]
+    HIPCHK(c, launch_summary(c, T, nwc, c->commit.as<uint8_t>(), c->vcount.as<int32_t>(), wu_fused));  // records ev[7]
   }
   if (!(parts & 2)) return DR_OK;
+  ChainFuse cfk;
+  if (cf && wu_fused) {  // the chain plan rides in K^cand's launch instead of the weak unions'
+    cfk = *cf;
+    cfk.plan_in_kcand = true;
+    cf = &cfk;
+  }
   const bool early = fork && side;
   if (early) HIPCHK(c, ensure_stream2(c));
   if (early) {  // stream2's work (side) needs only the rows' summaries and commits: fork here,
@@ -2075,7 +2179,7 @@ int build_summary(dr_ctx *c, float *ms_summary, int nwc = 0, uint8_t *commit = n
       HIPCHK(c, hipEventRecord(fe, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, fe, 0));
   }
-  HIPCHK(c, launch_weak_union(c, T, c->stream, cf));
+  if (!wu_fused) HIPCHK(c, launch_weak_union(c, T, c->stream, cf));
   mark_rounds_clean(c);
   if (int rc = launch_canon(c, fork, side, early, false, prefix, true, cf)) return rc;
   if (!host_out) return DR_OK;  // planned replay: results stay on the device
@@ -2165,6 +2269,11 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
   }
   if (option == DR_OPT_MEMO) {
     c->use_memo = value != 0;
+    return DR_OK;
+  }
+  if (option == DR_OPT_FUSE) {
+    if (value < 0 || value > 7) return c->fail(DR_E_INVAL, "DR_OPT_FUSE is a mask of bits 1, 2, 4");
+    c->fuse = value;
     return DR_OK;
   }
   if (option == DR_OPT_DEVICE_PLAN) {
@@ -3277,7 +3386,7 @@ hipError_t launch_paper_emit(dr_ctx *c, int nw, const int32_t *plan, const dr::S
 template <int WS>
 hipError_t launch_own_emit_t(dr_ctx *c, int nq, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
                              u64 *qcount, u64 *qdigest, int32_t *qcut, const dr::PopMark &pm,
-                             const dr::PopPlanArgs &pp) {
+                             const dr::PopPlanArgs &pp, const int *lo_w) {
   // 256 threads per query at n <= 256 (C3: 41 -> 37 us, more queries resident), 512 above
   // (C4 at 256: 12.8 -> 18.8 us; profiles/r03/v18_timeline_*_own256.txt).  Workgroup 0: the
   // canonical prefixes G, E (every DAG length: canon_prefix_regs walks chunks); the last,
@@ -3286,15 +3395,15 @@ hipError_t launch_own_emit_t(dr_ctx *c, int nq, const int32_t *plan, const dr::S
   hipLaunchKernelGGL((dr::k_own_emit<WS, NT>), dim3(1 + nq + (pp.active ? 1 : 0)), dim3(NT), 0, c->stream,
                      c->view(), c->masks.as<u64>(), c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(),
                      c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), qcount, qdigest, qcut, c->nrounds - 1,
-                     c->RG.as<u64>(), c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), pm, pp);
+                     c->RG.as<u64>(), c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), pm, pp, lo_w);
   return hipGetLastError();
 }
 hipError_t launch_own_emit(dr_ctx *c, int nq, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
                            u64 *qcount, u64 *qdigest, int32_t *qcut, const dr::PopMark &pm,
-                           const dr::PopPlanArgs &pp) {
+                           const dr::PopPlanArgs &pp, const int *lo_w) {
   switch (c->WS) {
 #define DR_OE(W) \
-  case W: return launch_own_emit_t<W>(c, nq, plan, dq, stops, qcount, qdigest, qcut, pm, pp);
+  case W: return launch_own_emit_t<W>(c, nq, plan, dq, stops, qcount, qdigest, qcut, pm, pp, lo_w);
     DR_OE(1) DR_OE(2) DR_OE(4) DR_OE(8) DR_OE(16) DR_OE(32)
 #undef DR_OE
   }
@@ -3390,6 +3499,7 @@ int deliver_planned(dr_ctx *c, const std::vector<Pop> &pops, uint64_t *pcount, u
     int32_t *hp = reinterpret_cast<int32_t *>(at(plan));
     hp[dr::PL_NPUSH] = np;
     hp[dr::PL_NQD] = nq;
+    hp[dr::PL_NLIVE] = nq;
     std::memcpy(at(dq), qv.data(), (size_t)nq * sizeof(dr::SweepQuery));
     std::memcpy(at(pop_q), pq.data(), (size_t)np * 4);
     std::memcpy(at(pop_cur), pcur.data(), (size_t)np * 4);
@@ -3613,7 +3723,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   // launch sequence depends on changed since it was captured; capture when this
   // call's configuration matches the previous call's (every buffer is sized then)
   enum { EAGER, CAPTURE, LAUNCH } form = EAGER;
-  if (c->replay_graph && !c->graph_fail && c->phase_timing <= 1) {
+  if (c->replay_graph && !c->graph_fail && c->phase_timing <= 1 && !c->shared_stream) {
     if (c->pin_used || !c->pend.empty() || !c->h2q.empty()) HIPCHK(c, c->sync());  // the stage starts at pin
     const std::vector<uint64_t> key = graph_key(c, nw, chain_mode, paper, pcap);
     if (c->rg_exec && key == c->rg_key)
@@ -3652,6 +3762,10 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       cf.pa = dr::ChainPlanArgs{c->commit.as<uint8_t>(), c->lead.as<uint16_t>(), nw, persistent ? 1 : 0,
                                 dr::Q_CHAIN | dr::Q_STRONG_ONLY | sc, task_wave, task_q, cq, plan};
       cf.xa = dr::ChainArgs{cq, plan + dr::PL_NQC, push_out, cpush_n, cedges, cwedges, hits, cstops, pmark};
+      cf.emit_in_sweep = (c->fuse & 2) != 0;
+      if (c->fuse & 4)  // the speculative prefixes beside the walk; k_own_emit rescans from its lowest round
+        cf.sp = dr::SpecPrefix{1, c->RG.as<u64>(), c->SD.as<u64>(), c->weak_roff.as<uint32_t>(), c->Gc.as<u64>(),
+                               c->Ec.as<u64>()};
     }
     std::function<int()> side = [&]() -> int {
       // 2. leader chains
@@ -3708,6 +3822,13 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     if (stat) a.nq = c->sdq_n;
     a.rcnt = nullptr;
     a.pm = pmark;
+    if (stat && cf.emit_in_sweep)  // the canonical re-emission beside the delivery sweeps
+      a.ce = dr::CanonEmit{kCanonEmitBlocks, T, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
+                           c->K.as<u64>(), c->crbase.as<uint32_t>(), c->RG.as<u64>(), c->rlo.as<int>()};
+    if (stat && cf.sp.on)  // the pop plan (the chains' pushes, the launch before) beside the delivery sweeps
+      a.pp = dr::PopPlanArgs{1, nw, WS, dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave,
+                             task_q, cq, cpush_n, push_out, pcap, task_pos, push_off, push_wave, pop_wave, pop_cur,
+                             pop_q, seen, qidx, dq, plan, c->sqidx.as<int32_t>(), c->sdq_n};
     dr::EmitArgs em{c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), c->Cc.as<u64>(), qcount, qdigest, qcut,
                           dr::FinalArgs{}};
     {
@@ -3754,10 +3875,12 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       em.fin.firstpop = firstpop;
       em.fin.qedges = qedges;
     } else {  // REF: own rounds above the cut; workgroup 0 the canonical prefixes G, E, the last the pop plan
-      const dr::PopPlanArgs pp{1, nw, WS, dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave,
-                               task_q, cq, cpush_n, push_out, pcap, task_pos, push_off, push_wave, pop_wave, pop_cur,
-                               pop_q, seen, qidx, dq, plan, c->sqidx.as<int32_t>(), c->sdq_n};
-      HIPCHK(c, launch_own_emit(c, c->sdq_n, splan, sdq, dstops, qcount, qdigest, qcut, pmark, pp));
+      dr::PopPlanArgs pp{1, nw, WS, dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave,
+                         task_q, cq, cpush_n, push_out, pcap, task_pos, push_off, push_wave, pop_wave, pop_cur,
+                         pop_q, seen, qidx, dq, plan, c->sqidx.as<int32_t>(), c->sdq_n};
+      if (cf.sp.on) pp.active = 0;  // (the delivery sweeps' launch planned the pops)
+      HIPCHK(c, launch_own_emit(c, c->sdq_n, splan, sdq, dstops, qcount, qdigest, qcut, pmark, pp,
+                                cf.sp.on ? c->nseg.as<int32_t>() + 1 : nullptr));
       if (c->up_verify) HIPCHK(c, launch_verify_up(c, dstops, qcut, pmark));  // the upward edges against the cones
     }
     HIPCHK(c, c->rec(3));
@@ -4124,7 +4247,7 @@ int replay_batch_impl(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode,
       for (int i = 0; i < nctx; i++) {
         dr_ctx *c = ctxs[i];
         dr::SmallJob &J = jobs[i];
-        J.cone = cv.take<u64>((size_t)(T + 1) * 128);
+        J.cone = cv.take<u64>((size_t)(T + 1) * dr::kConeRecWords);
         J.sufl = cv.take<uint32_t>(65 * 64);
         // per slot of rounds 0..T (workgroup form) or per (round, vertex) (wave form)
         J.deg = cv.take<uint32_t>(std::max<size_t>(c->h_slot_off[T + 1], (size_t)(T + 1) * c->n));

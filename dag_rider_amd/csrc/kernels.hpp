@@ -838,7 +838,9 @@ __device__ __forceinline__ void canon_prefix_block(int T, const u64 *__restrict_
 }
 
 // plan[] slots (int32, device)
-enum : int { PL_NTASK = 0, PL_NQC = 1, PL_NPUSH = 2, PL_CAPERR = 3, PL_NQD = 4, PL_NDESC = 5, PL_N = 8 };
+// (PL_NLIVE: the delivery queries a replay swept -- the static table's live ones -- for the
+// sweep statistics; PL_NQD counts the launched table)
+enum : int { PL_NTASK = 0, PL_NQC = 1, PL_NPUSH = 2, PL_CAPERR = 3, PL_NQD = 4, PL_NDESC = 5, PL_NLIVE = 6, PL_N = 8 };
 // header written to host memory by k_plan_final (u64)
 // (PH_MINSTOP .. PH_PROBE + 23: a sliced context's outputs, dr_slice_result)
 enum : int {
@@ -1070,7 +1072,7 @@ __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
     h[PH_CHAIN_E] = acc[1];
     h[PH_DELIVER_E] = acc[0];
     for (int k = 0; k < 4; k++) h[PH_PARTIAL + k] = acc[2 + k];
-    h[PH_NQD] = (u64)nqd;
+    h[PH_NQD] = (u64)f.plan[PL_NLIVE];
     h[PH_NSEG] = (u64)(int64_t)*f.nseg;
     h[PH_CAPERR] = (u64)(caperr ? caperr : s_bad ? 3 : 0);
   }
@@ -1340,16 +1342,6 @@ __device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView m
   }
 }
 
-template <int WS, int NT, int MODE>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_MERGE) ? 3 : 1))) void k_sweep(
-    DagView g, MemoView mv, const SweepQuery *__restrict__ qs, int nq, int seq, int depth_log2, u64 *__restrict__ masks,
-    u64 *__restrict__ dlv, int32_t *__restrict__ push_out, int32_t *__restrict__ push_n, u64 *__restrict__ edges_out,
-    u64 *__restrict__ wedges_out, uint8_t *__restrict__ hit_out, int32_t *__restrict__ stop_out,
-    u64 *__restrict__ stats_out, const int *__restrict__ nq_dev, uint32_t *__restrict__ rcnt, const PopMark pm) {
-  sweep_body<WS, NT, MODE>((int)blockIdx.x, g, mv, qs, nq, seq, depth_log2, masks, dlv, push_out, push_n, edges_out,
-                           wedges_out, hit_out, stop_out, stats_out, nq_dev, rcnt, pm);
-}
-
 // Leader chains (SW_CHAIN: strong only, process.go:341-350) for n <= 64 * WS, WS <=
 // 4, one wavefront per chain and every round in registers: lane l holds the WS rows
 // of sources l*WS .. l*WS + WS-1 (WS * WS contiguous words), loaded PF rounds ahead
@@ -1524,10 +1516,40 @@ __global__ __launch_bounds__(NT) void k_replay_final(const EmitArgs ea) {
 // -- are issued before the current group is consumed, so the two barriers that
 // publish a round's U, SD and S overlap the next round's loads.
 // ---------------------------------------------------------------------------
+template <int WS>
+__device__ __forceinline__ void weak_union_round(const DagView &g, int r, int dd, u64 *__restrict__ WU, u64 *sW,
+                                                 const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
+                                                 const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG,
+                                                 int lane);
+
+// The weak unions and speculative digests (weak_union_round) in the row pass's launch:
+// workgroups nsum .. nsum + nwug - 1 of the grid, after every row workgroup, take the
+// rounds nwv at a time (one wave each, the other waves idle).  They depend on the
+// weak-column keys and the slot lists alone, so they fill the CUs the row pass's last
+// workgroups leave idle instead of a launch of their own after it (C4: 12 us).
+struct WUArgs {
+  int nsum;  // row-pass workgroups ((T + 3) / 4); 0: no weak-union workgroups
+  int dd, nwv;
+  u64 *WU;
+  const u64 *ppref;
+  const uint32_t *slot_off;
+  const uint16_t *slot_src;
+  u64 *RG;
+};
+
 template <int WS, int NT, int GRP, bool PIPE>
 __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc, int quorum, u64 *__restrict__ U,
                                                        u64 *__restrict__ SD, uint8_t *__restrict__ commit,
-                                                       int32_t *__restrict__ vcount) {
+                                                       int32_t *__restrict__ vcount, const WUArgs wa) {
+  if (wa.nsum > 0 && (int)blockIdx.x >= wa.nsum) {  // (block-uniform) a weak-union workgroup
+    extern __shared__ __attribute__((aligned(16))) u64 wu_lds[];
+    const int wid = threadIdx.x >> 6;
+    const int r = ((int)blockIdx.x - wa.nsum) * wa.nwv + wid + 1;
+    if (wid >= wa.nwv || r > T) return;  // wave-uniform
+    weak_union_round<WS>(g, r, wa.dd, wa.WU, wu_lds + (size_t)wid * wa.dd * WS, wa.ppref, wa.slot_off, wa.slot_src,
+                         wa.RG, threadIdx.x & 63);
+    return;
+  }
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
   constexpr int GR = CPT < GRP ? CPT : GRP;  // chunks per group
@@ -1787,6 +1809,7 @@ __device__ __forceinline__ void weak_union_round(const DagView &g, int r, int dd
                                                  const u64 *__restrict__ ppref, const uint32_t *__restrict__ slot_off,
                                                  const uint16_t *__restrict__ slot_src, u64 *__restrict__ RG,
                                                  int lane) {
+  if (dd <= 0 && !RG) return;
   // 16-B LDS and HBM accesses when every row is 16-B aligned (WS even)
   typedef u64 u64v2 __attribute__((ext_vector_type(2)));
   if constexpr (WS % 2 == 0) {
@@ -1864,11 +1887,11 @@ __global__ __launch_bounds__(256) void k_weak_union(DagView g, int T, int nr, in
 // the window's WU terms are spread over all 64 lanes (64/WS classes of delta d,
 // OR-reduced across lanes): a deep window (dd = 79) has 79 terms per word.
 template <int WS>
-__global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K,
-                                               uint8_t *__restrict__ good, u64 *__restrict__ CE,
-                                               u64 *__restrict__ RD, int *__restrict__ rlo, int lo,
-                                               const u64 *__restrict__ ppref, u64 *__restrict__ Cc,
-                                               uint32_t *__restrict__ crbase) {
+__device__ __forceinline__ void kcand_body(DagView g, MemoView mv, int T, u64 *__restrict__ K,
+                                           uint8_t *__restrict__ good, u64 *__restrict__ CE,
+                                           u64 *__restrict__ RD, int *__restrict__ rlo, int lo,
+                                           const u64 *__restrict__ ppref, u64 *__restrict__ Cc,
+                                           uint32_t *__restrict__ crbase) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), w = threadIdx.x & 63;
   if (rlo && blockIdx.x == 0 && threadIdx.x == 0) *rlo = lo;  // k_canon_diff / k_canon lower it
   if (r > T) return;  // wave-uniform
@@ -1911,6 +1934,14 @@ __global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u6
     Cc[r] = ppref[r];
     crbase[r] = r >= 1 ? (uint32_t)ppref[r - 1] : 0u;
   }
+}
+template <int WS>
+__global__ __launch_bounds__(256) void k_kcand(DagView g, MemoView mv, int T, u64 *__restrict__ K,
+                                               uint8_t *__restrict__ good, u64 *__restrict__ CE,
+                                               u64 *__restrict__ RD, int *__restrict__ rlo, int lo,
+                                               const u64 *__restrict__ ppref, u64 *__restrict__ Cc,
+                                               uint32_t *__restrict__ crbase) {
+  kcand_body<WS>(g, mv, T, K, good, CE, RD, rlo, lo, ppref, Cc, crbase);
 }
 
 // Incremental canonical emission: the lowest round r < lo whose canonical
@@ -2092,7 +2123,10 @@ __device__ __forceinline__ void canon_body(DagView g, MemoView mv, int T, int de
     pos = r;
     lo_w = min(lo_w, r);
   }
-  if (tid == 0 && nseg) *nseg = segs;
+  if (tid == 0 && nseg) {
+    nseg[0] = segs;
+    nseg[1] = lo_w;  // (T + 1: no walk) below it K is K^cand, every round full, CE the full total
+  }
   DR_TT(if (tid == 0) {
     g_canon_timing[1] = wall_clock64();
     g_canon_timing[3] = segs;
@@ -2189,8 +2223,109 @@ struct ChainArgs {
   int32_t *stops;
   PopMark pm;
 };
+// The canonical prefixes A, B of two per-round arrays over rounds 0..T (round 0 counted
+// as 0), one workgroup, every round of a chunk of J * NT in registers: column j of the
+// chunk (NT rounds) is loaded lane-consecutively (coalesced, all 2J loads in flight at
+// once), each wave scans its 64 rounds of every column by DPP (no LDS, no barrier), and
+// wave 0 turns the J * NT/64 wave totals into offsets through LDS: two LDS-only barriers
+// per chunk, one memory round trip.  C3 (10 001 rounds, J = 10): one chunk, 11.4 us against
+// 16.8 us for an LDS-tiled form and 18.8 us for canon_prefix_block's per-thread runs
+// (profiles/r05/v15_prefix_bench.txt; a single-CU pass either way).
+template <int NT, int J, class LA, class LB>
+__device__ __forceinline__ void canon_prefix_gen(int r0, int T, u64 ca, u64 cb, LA la, LB lb, u64 *__restrict__ A,
+                                                 u64 *__restrict__ B) {
+  constexpr int NW = NT / 64, E = J * NW, PL = (E + 63) / 64;
+  __shared__ u64 oa[E + 1], ob[E + 1];  // wave totals -> exclusive offsets; [E] = the chunk total
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, n = T + 1, lo = r0 > 1 ? r0 : 1;
+  for (int c0 = r0; c0 < n; c0 += J * NT) {
+    u64 xa[J], xb[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {  // clamped addresses: unconditional loads, all in flight
+      const int r = c0 + j * NT + tid;
+      const int rc = (r >= lo && r < n) ? r : lo;
+      xa[j] = la(rc);
+      xb[j] = lb(rc);
+    }
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const int r = c0 + j * NT + tid;
+      const bool in = r >= lo && r < n;  // round 0 is never delivered
+      xa[j] = wave_scan_incl(in ? xa[j] : 0ULL);
+      xb[j] = wave_scan_incl(in ? xb[j] : 0ULL);
+      if (lane == 63) {
+        oa[j * NW + wid] = xa[j];
+        ob[j * NW + wid] = xb[j];
+      }
+    }
+    lds_barrier();
+    if (wid == 0) {  // exclusive offsets of the E (column, wave) totals, in round order
+      u64 va[PL], vb[PL], sa = 0, sb = 0;
+#pragma unroll
+      for (int k = 0; k < PL; k++) {
+        const int e = lane * PL + k;
+        va[k] = e < E ? oa[e] : 0ULL;
+        vb[k] = e < E ? ob[e] : 0ULL;
+        sa += va[k];
+        sb += vb[k];
+      }
+      const u64 ia = wave_scan_incl(sa), ib = wave_scan_incl(sb);
+      u64 pa = ia - sa, pb = ib - sb;
+#pragma unroll
+      for (int k = 0; k < PL; k++) {
+        const int e = lane * PL + k;
+        if (e < E) {
+          oa[e] = pa;
+          ob[e] = pb;
+        }
+        pa += va[k];
+        pb += vb[k];
+      }
+      if (lane == 63) {
+        oa[E] = ia;
+        ob[E] = ib;
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const int r = c0 + j * NT + tid;
+      if (r < n) {
+        A[r] = ca + oa[j * NW + wid] + xa[j];
+        B[r] = cb + ob[j * NW + wid] + xb[j];
+      }
+    }
+    ca += oa[E];
+    cb += ob[E];
+    lds_barrier();  // the offsets are rewritten by the next chunk
+  }
+}
+template <int NT, int J>
+__device__ __forceinline__ void canon_prefix_regs(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                  u64 *__restrict__ A, u64 *__restrict__ B) {
+  canon_prefix_gen<NT, J>(0, T, 0ULL, 0ULL, [&](int r) { return a[r]; }, [&](int r) { return b[r]; }, A, B);
+}
+
+// The speculative canonical prefixes (the grid's last workgroup of k_canon_chains when
+// on): G, E over every round as if every round were full -- the weak-union launch's
+// per-round digests RG and the full-round edge totals SD + weak counts (k_kcand's CE
+// default) -- exact below the canonical walk's lowest round; k_own_emit's workgroup 0
+// then rescans only the rounds from there up (C3: 10 001 rounds, five chunks of one
+// workgroup, off the critical path).
+struct SpecPrefix {
+  int on;
+  const u64 *RG, *SD;
+  const uint32_t *weak_roff;
+  u64 *Gc, *Ec;
+};
 template <int WS, int NT, bool CREG>
-__global__ __launch_bounds__(NT) void k_canon_chains(DagView g, MemoView mv, const CanonArgs ca, const ChainArgs xa) {
+__global__ __launch_bounds__(NT) void k_canon_chains(DagView g, MemoView mv, const CanonArgs ca, const ChainArgs xa,
+                                                     const SpecPrefix sp) {
+  if (sp.on && blockIdx.x == gridDim.x - 1) {
+    canon_prefix_gen<NT, 8>(
+        0, ca.T, 0ULL, 0ULL, [&](int r) { return sp.RG[r]; },
+        [&](int r) { return sp.SD[r] + (u64)(sp.weak_roff[r + 1] - sp.weak_roff[r]); }, sp.Gc, sp.Ec);
+    return;
+  }
   if (blockIdx.x == 0) {
     canon_body<WS, NT>(g, mv, ca.T, ca.depth_log2, ca.K, ca.good, ca.CE, ca.nseg, ca.RD, ca.Cc, ca.crbase, ca.ppref,
                        ca.rlo);
@@ -2408,83 +2543,7 @@ __global__ __launch_bounds__(NT) void k_emit_ids(DagView g, const uint32_t *__re
   }
 }
 
-// The canonical prefixes A, B of two per-round arrays over rounds 0..T (round 0 counted
-// as 0), one workgroup, every round of a chunk of J * NT in registers: column j of the
-// chunk (NT rounds) is loaded lane-consecutively (coalesced, all 2J loads in flight at
-// once), each wave scans its 64 rounds of every column by DPP (no LDS, no barrier), and
-// wave 0 turns the J * NT/64 wave totals into offsets through LDS: two LDS-only barriers
-// per chunk, one memory round trip.  C3 (10 001 rounds, J = 10): one chunk, 11.4 us against
-// 16.8 us for an LDS-tiled form and 18.8 us for canon_prefix_block's per-thread runs
-// (profiles/r05/v15_prefix_bench.txt; a single-CU pass either way).
-template <int NT, int J>
-__device__ __forceinline__ void canon_prefix_regs(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,
-                                                  u64 *__restrict__ A, u64 *__restrict__ B) {
-  constexpr int NW = NT / 64, E = J * NW, PL = (E + 63) / 64;
-  __shared__ u64 oa[E + 1], ob[E + 1];  // wave totals -> exclusive offsets; [E] = the chunk total
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, n = T + 1;
-  u64 ca = 0, cb = 0;
-  for (int c0 = 0; c0 < n; c0 += J * NT) {
-    u64 xa[J], xb[J];
-#pragma unroll
-    for (int j = 0; j < J; j++) {  // clamped addresses: unconditional loads, all in flight
-      const int r = c0 + j * NT + tid;
-      const int rc = (r >= 1 && r < n) ? r : 0;
-      xa[j] = a[rc];
-      xb[j] = b[rc];
-    }
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-      const int r = c0 + j * NT + tid;
-      const bool in = r >= 1 && r < n;  // round 0 is never delivered
-      xa[j] = wave_scan_incl(in ? xa[j] : 0ULL);
-      xb[j] = wave_scan_incl(in ? xb[j] : 0ULL);
-      if (lane == 63) {
-        oa[j * NW + wid] = xa[j];
-        ob[j * NW + wid] = xb[j];
-      }
-    }
-    lds_barrier();
-    if (wid == 0) {  // exclusive offsets of the E (column, wave) totals, in round order
-      u64 va[PL], vb[PL], sa = 0, sb = 0;
-#pragma unroll
-      for (int k = 0; k < PL; k++) {
-        const int e = lane * PL + k;
-        va[k] = e < E ? oa[e] : 0ULL;
-        vb[k] = e < E ? ob[e] : 0ULL;
-        sa += va[k];
-        sb += vb[k];
-      }
-      const u64 ia = wave_scan_incl(sa), ib = wave_scan_incl(sb);
-      u64 pa = ia - sa, pb = ib - sb;
-#pragma unroll
-      for (int k = 0; k < PL; k++) {
-        const int e = lane * PL + k;
-        if (e < E) {
-          oa[e] = pa;
-          ob[e] = pb;
-        }
-        pa += va[k];
-        pb += vb[k];
-      }
-      if (lane == 63) {
-        oa[E] = ia;
-        ob[E] = ib;
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-      const int r = c0 + j * NT + tid;
-      if (r < n) {
-        A[r] = ca + oa[j * NW + wid] + xa[j];
-        B[r] = cb + ob[j * NW + wid] + xb[j];
-      }
-    }
-    ca += oa[E];
-    cb += ob[E];
-    lds_barrier();  // the offsets are rewritten by the next chunk
-  }
-}
+
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_canon_prefix(int T, const u64 *__restrict__ a, const u64 *__restrict__ b,

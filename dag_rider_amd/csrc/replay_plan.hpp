@@ -180,6 +180,7 @@ __device__ __forceinline__ void plan_chains_body(const uint8_t *__restrict__ com
     plan[PL_NQC] = (int32_t)c1;
     plan[PL_CAPERR] = 0;
     plan[PL_NQD] = 0;
+    plan[PL_NLIVE] = 0;
     plan[PL_NDESC] = 0;
   }
 }
@@ -218,6 +219,22 @@ __global__ __launch_bounds__(256) void k_wu_plan(DagView g, int T, int dd, u64 *
   const int r = (int)blockIdx.x * 4 + wid + 1;  // one wave per round
   if (r > T) return;  // wave-uniform
   weak_union_round<WS>(g, r, dd, WU, wu_lds + (size_t)wid * dd * WS, ppref, slot_off, slot_src, RG, lane);
+}
+
+// K^cand (kcand_body, one wave per round) and, in the grid's last workgroup, the
+// leader-chain plan: with the weak unions inside the row pass's launch (WUArgs), the
+// commits are final when this launch starts.
+template <int WS>
+__global__ __launch_bounds__(256) void k_kcand_plan(DagView g, MemoView mv, int T, u64 *__restrict__ K,
+                                                    uint8_t *__restrict__ good, u64 *__restrict__ CE,
+                                                    u64 *__restrict__ RD, int *__restrict__ rlo, int lo,
+                                                    const u64 *__restrict__ ppref, u64 *__restrict__ Cc,
+                                                    uint32_t *__restrict__ crbase, const ChainPlanArgs pa) {
+  if (blockIdx.x == gridDim.x - 1) {
+    plan_chains_body<256>(pa.commit, pa.lead, pa.nw, pa.persistent, pa.qflags, pa.task_wave, pa.task_q, pa.cq, pa.plan);
+    return;
+  }
+  kcand_body<WS>(g, mv, T, K, good, CE, RD, rlo, lo, ppref, Cc, crbase);
 }
 
 // Pushes (task wave, then its chain's pushes in push order) -> pops in pop
@@ -294,9 +311,13 @@ __device__ __forceinline__ void plan_pops_body(int nw, int WS, int qflags, const
     for (int w = wlo; w <= whi; w++) push_off[w - 1] = v;
   }
   if (qidx_static) {  // the delivery queries are the static per-wave table (one per present leader)
-    __syncthreads();  // pop_wave written (block-uniform branch: a kernel argument)
+    __syncthreads();  // pop_wave written, seen set (block-uniform branch: a kernel argument)
     if (tid == 0) plan[PL_NQD] = nqd_static;
     for (int64_t p = tid; p < np; p += NT) pop_q[p] = qidx_static[pop_wave[p]];
+    int64_t live = 0, zero = 0, tl, tz;  // the distinct popped leaders: the table's queries that swept
+    for (int w = 1 + tid; w <= nw; w += NT) live += seen[w];
+    block_scan2_excl<NT>(live, zero, s, tl, tz);
+    if (tid == 0) plan[PL_NLIVE] = (int32_t)tl;
     return;
   }
   __syncthreads();  // seen written
@@ -328,7 +349,10 @@ __device__ __forceinline__ void plan_pops_body(int nw, int WS, int qflags, const
     c0 += tq;
     c1 += tm;
   }
-  if (tid == 0) plan[PL_NQD] = (int32_t)c0;
+  if (tid == 0) {
+    plan[PL_NQD] = (int32_t)c0;
+    plan[PL_NLIVE] = (int32_t)c0;
+  }
   __syncthreads();  // qidx written
   for (int64_t p = tid; p < np; p += NT) pop_q[p] = qidx[pop_wave[p]];
 }
@@ -748,7 +772,7 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
                                                  u64 *__restrict__ qdigest, int32_t *__restrict__ qcut, int T,
                                                  const u64 *__restrict__ RG, const u64 *__restrict__ CE,
                                                  u64 *__restrict__ Gc, u64 *__restrict__ Ec, const PopMark pm,
-                                                 const PopPlanArgs pp) {
+                                                 const PopPlanArgs pp, const int *__restrict__ lo_w) {
   constexpr int NWV = NT / 64;
   __shared__ u64 s_c[NWV], s_dg;
   // workgroup 0 (with Gc): the canonical prefixes G, E -- the longest workgroup, so it
@@ -756,7 +780,15 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
   // chains' pushes (the launch before this one)
   const int pre = Gc ? 1 : 0, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (pre && blockIdx.x == 0) {  // (Gc null: k_canon_prefix computed them)
-    canon_prefix_regs<NT, 8>(T, RG, CE, Gc, Ec);
+    if (lo_w) {  // the speculative prefixes are exact below the walk's lowest round: rescan from there
+      const int lw = *lo_w;
+      if (lw <= T)
+        canon_prefix_gen<NT, 8>(
+            lw, T, lw >= 1 ? Gc[lw - 1] : 0ULL, lw >= 1 ? Ec[lw - 1] : 0ULL, [&](int r) { return RG[r]; },
+            [&](int r) { return CE[r]; }, Gc, Ec);
+    } else {
+      canon_prefix_regs<NT, 8>(T, RG, CE, Gc, Ec);
+    }
     return;
   }
   if (pp.active && blockIdx.x == gridDim.x - 1) {
@@ -851,6 +883,68 @@ __global__ __launch_bounds__(256) void k_verify_up(const u64 *__restrict__ K, co
     cnt += in_u && !in_v;
   }
   if (cnt) atomicAdd(bad, cnt);
+}
+
+// The canonical re-emission (per-round digests RG of rounds >= *rlo, positions from
+// crbase: launch_canon's k_emit_ids) as the first nblk workgroups of the delivery sweeps'
+// launch: it needs the canonical walk's K and positions, the sweeps need K alone, so the
+// two run side by side instead of one launch after the other (C4: 6.6 us).  A workgroup
+// takes round blocks of NT/64 rounds (a wave each) from the top down, nblk apart.
+struct CanonEmit {
+  int nblk;  // 0: none
+  int T;
+  const uint32_t *slot_off;
+  const uint16_t *slot_src;
+  const u64 *K;
+  const uint32_t *crbase;
+  u64 *RG;
+  const int *rlo;
+};
+template <int WS, int NT>
+__device__ __forceinline__ void canon_emit_blocks(const DagView &g, const CanonEmit &ce, int b) {
+  constexpr int RPB = NT / 64;
+  __shared__ u64 s_dg;
+  PopDesc d{};
+  d.mask_off = 0;
+  d.rbase_off = 1;  // crbase is indexed by round; rbase_off addresses round `first`
+  d.pos0 = 0;
+  d.first = 1;
+  d.last = ce.T;
+  d.out = 0;
+  d.use_k = 1;
+  const int lo = *ce.rlo;
+  const int nb = (ce.T + RPB - 1) / RPB;
+  const int blo = lo > 1 ? (lo - 1) / RPB : 0;  // the block holding round lo
+  for (int blk = nb - 1 - b; blk >= blo; blk -= ce.nblk)  // (block-uniform)
+    emit_block<WS, NT, RPB>(g, ce.slot_off, ce.slot_src, d, blk, nullptr, ce.K, ce.crbase, nullptr, nullptr, ce.RG,
+                            nullptr, 0, &s_dg, nullptr, nullptr, lo);
+}
+
+template <int WS, int NT, int MODE>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_MERGE) ? 3 : 1))) void k_sweep(
+    DagView g, MemoView mv, const SweepQuery *__restrict__ qs, int nq, int seq, int depth_log2, u64 *__restrict__ masks,
+    u64 *__restrict__ dlv, int32_t *__restrict__ push_out, int32_t *__restrict__ push_n, u64 *__restrict__ edges_out,
+    u64 *__restrict__ wedges_out, uint8_t *__restrict__ hit_out, int32_t *__restrict__ stop_out,
+    u64 *__restrict__ stats_out, const int *__restrict__ nq_dev, uint32_t *__restrict__ rcnt, const PopMark pm,
+    const CanonEmit ce, const PopPlanArgs pp) {
+  int bidx = (int)blockIdx.x;
+  if constexpr ((MODE & SW_MERGE) != 0) {
+    if (ce.nblk > 0) {  // (block-uniform) the first nblk workgroups re-emit canonical rounds
+      if (bidx < ce.nblk) {
+        canon_emit_blocks<WS, NT>(g, ce, bidx);
+        return;
+      }
+      bidx -= ce.nblk;
+    }
+    if (pp.active && (int)blockIdx.x == (int)gridDim.x - 1) {  // the last: the pop plan (plan_pops_body)
+      plan_pops_body<NT>(pp.nw, pp.WS, pp.qflags, pp.lead, pp.task_wave, pp.task_q, pp.cq, pp.push_n, pp.push_out,
+                         pp.pcap, pp.task_pos, pp.push_off, pp.push_wave, pp.pop_wave, pp.pop_cur, pp.pop_q, pp.seen,
+                         pp.qidx, pp.dq, pp.plan, pp.qidx_static, pp.nqd_static);
+      return;
+    }
+  }
+  sweep_body<WS, NT, MODE>(bidx, g, mv, qs, nq, seq, depth_log2, masks, dlv, push_out, push_n, edges_out, wedges_out,
+                           hit_out, stop_out, stats_out, nq_dev, rcnt, pm);
 }
 
 }  // namespace dr

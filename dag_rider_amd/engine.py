@@ -41,10 +41,13 @@ class ReplayResult:
 class Engine:
     """One Process.dag mirror on a GPU (dr_create ... dr_destroy)."""
 
-    def __init__(self, n: int, faulty: int, max_rounds: int, device: int = 0):
+    def __init__(self, n: int, faulty: int, max_rounds: int, device: int = 0, shared_stream: bool = False):
         self._L = L.lib()
         h = L.P()
-        rc = self._L.dr_create(n, faulty, max_rounds, device, C.byref(h))
+        # shared_stream: DR_CREATE_SHARED_STREAM (one stream for every such context of the
+        # device: the members of a large dr_replay_batch)
+        rc = self._L.dr_create_ex(n, faulty, max_rounds, device, L.DR_CREATE_SHARED_STREAM if shared_stream else 0,
+                                  C.byref(h))
         if rc != L.DR_OK:
             raise L.DrError(rc, self._L.dr_last_error(None).decode())
         self._h = h
@@ -108,6 +111,10 @@ class Engine:
     def replay_graph_state(self) -> int:
         """The last replay's form: 1 graph launch, 0 kernel by kernel, -1 after a failed capture."""
         return int(self._L.dr_replay_graph_state(self._h))
+
+    def set_fuse(self, mask: int):
+        """DR_OPT_FUSE: which independent replay phases share a launch (7 = all, 0 = none)."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_FUSE, int(mask)))
 
     def set_batch_form(self, form: int):
         """DR_OPT_BATCH_FORM (read from a batch's first engine): DR_BATCH_AUTO, DR_BATCH_WORKGROUP

@@ -49,7 +49,7 @@ enum {
 };
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
 enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3, DR_OPT_BATCH_FORM = 4, DR_OPT_COMMIT_SPLIT = 5,
-       DR_OPT_REPLAY_GRAPH = 6 };
+       DR_OPT_REPLAY_GRAPH = 6, DR_OPT_FUSE = 7 };
 enum { DR_BATCH_AUTO = 0, DR_BATCH_WORKGROUP = 1, DR_BATCH_WAVE = 2 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
 enum { DR_WEAK_LITERAL = 0, DR_WEAK_PAPER = 1 };
@@ -64,6 +64,15 @@ int dr_abi_version(void);
  * max_rounds bounds the rounds that may be appended (device memory is sized
  * from it).  device >= 0 is a HIP ordinal. */
 int dr_create(int n, int faulty, int max_rounds, int device, dr_ctx **out);
+/* dr_create with flags.  DR_CREATE_SHARED_STREAM: the context enqueues on one HIP
+ * stream shared by every such context of the device (created with the first, destroyed
+ * with the last) instead of a stream of its own -- for batches of many small mirrors
+ * (dr_replay_batch over thousands of contexts), where a device-wide synchronize walks
+ * every stream of the process.  Calls on such contexts still return when their own work
+ * is done; they may also wait for work other shared-stream contexts queued before it.
+ * DR_OPT_REPLAY_GRAPH does not capture on a shared stream. */
+enum { DR_CREATE_SHARED_STREAM = 1 };
+int dr_create_ex(int n, int faulty, int max_rounds, int device, int flags, dr_ctx **out);
 void dr_destroy(dr_ctx *ctx);
 const char *dr_last_error(const dr_ctx *ctx);
 /* Provenance: the sha256 (first 16 hex digits) of the sources this library was built
@@ -115,7 +124,12 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * captured once as a hipGraph (both streams' launches after the summary pass
  * and the copy of the outputs into pinned memory) and later such calls launch
  * the graph (with DR_OPT_PHASE_TIMING <= 1).  0 = launch every kernel per call,
- * as fast on MI355X at C3/C4.  Identical results. */
+ * as fast on MI355X at C3/C4.  Identical results.
+ * DR_OPT_FUSE (default 7, bits): which independent phases of a device-planned REF
+ * dr_replay share a launch with the phase beside them: 1 = the weak unions with the row
+ * pass, 2 = the canonical re-emission with the delivery sweeps, 4 = the speculative
+ * canonical prefixes with the canonical walk and the pop plan with the delivery sweeps;
+ * 0 = each phase its own launch.  Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 /* The form of the context's last dr_replay: 1 = a captured graph was launched,
  * 0 = kernels launched one by one, -1 = one by one after a failed capture

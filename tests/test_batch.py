@@ -279,3 +279,44 @@ def test_batch_view_in_place(gpu_device, form):
     with pytest.raises(L.DrError) as ex:
         small.run()
     assert ex.value.code == L.DR_E_CAPACITY
+
+
+@pytest.mark.parametrize("form", FORMS)
+def test_batch_shared_stream(gpu_device, form):
+    """DR_CREATE_SHARED_STREAM: contexts on the device's one shared stream (the C5 bench's
+    batch members) replay alone and in a batch exactly as contexts with streams of their own,
+    through appends in flight, destroys in any order and a new shared context after the
+    last one went."""
+    nw = 8
+    rng = np.random.default_rng(515)
+    dags = []
+    for _ in range(6):
+        n = int(rng.choice((7, 64, 100, 128)))
+        d = random_dag(rng, n, 4 * nw + 2, p_present=0.9, p_s=0.5, p_w=0.5, max_depth=6)
+        dags.append((d, int(rng.integers(0, (n - 1) // 3 + 1))))
+    shared = []
+    for d, f in dags:
+        e = Engine(d.n, f, d.nrounds, gpu_device, shared_stream=True)
+        e.append_packed(d)  # (the copies may still run when the next context appends)
+        shared.append(e)
+    shared[0].set_batch_form(form)
+    for cm, dm in MODES:
+        got = replay_batch(shared, nw, cm, dm)
+        for (d, f), e, g in zip(dags, shared, got):
+            want = oracle.PDag(d).replay(f, nw, cm, dm)
+            _same(g, want)
+            _same(e.replay(nw, cm, dm), want)
+    for i in (3, 0, 5):  # destroy out of order; the others keep the stream
+        shared[i].close()
+    rest = [e for i, e in enumerate(shared) if i not in (3, 0, 5)]
+    rest[0].set_batch_form(form)
+    got = replay_batch(rest, nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF)
+    for (d, f), g in zip([x for i, x in enumerate(dags) if i not in (3, 0, 5)], got):
+        _same(g, oracle.PDag(d).replay(f, nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF))
+    for e in rest:
+        e.close()
+    d, f = dags[1]
+    with Engine(d.n, f, d.nrounds, gpu_device, shared_stream=True) as e:  # the stream is created again
+        e.append_packed(d)
+        _same(e.replay(nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF),
+              oracle.PDag(d).replay(f, nw, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF))
