@@ -235,7 +235,8 @@ struct dr_ctx {
   // DR_OPT_FUSE: bit 0 = a full replay's weak unions ride in the row pass's launch
   // (dr::WUArgs, the chain plan then in k_kcand_plan); bit 1 = the canonical re-emission
   // rides in the delivery sweeps' launch; bit 2 = the speculative G, E prefixes beside the
-  // canonical walk (k_canon_chains) and the pop plan beside the delivery sweeps
+  // canonical walk (k_canon_chains) and the pop plan beside the delivery sweeps; bit 3 = the
+  // delivery sweeps' queries grouped by XCD (dr::CanonEmit::xcd)
   int fuse = getenv("DR_FUSE") ? atoi(getenv("DR_FUSE")) : 7;
   int last_split = 0;   // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
@@ -849,7 +850,7 @@ hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   static std::atomic<int> seen[kLdsDevs] = {};
   hipError_t e = lds_limit((const void *)dr::k_sweep<WS, NT, MODE>, seen, c->dev, lds);
   if (e != hipSuccess) return e;
-  const int ne = (MODE & dr::SW_MERGE) ? a.ce.nblk : 0;
+  const int ne = (MODE & dr::SW_MERGE) ? a.ce.nblk : 0;  // (a multiple of 8, CanonEmit::xcd)
   const int np = (MODE & dr::SW_MERGE) && a.pp.active ? 1 : 0;
   const int grid = (a.seq ? 1 : a.nq) + ne + np;
   dr::CanonEmit ce = a.ce;
@@ -2272,7 +2273,7 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     return DR_OK;
   }
   if (option == DR_OPT_FUSE) {
-    if (value < 0 || value > 7) return c->fail(DR_E_INVAL, "DR_OPT_FUSE is a mask of bits 1, 2, 4");
+    if (value < 0 || value > 15) return c->fail(DR_E_INVAL, "DR_OPT_FUSE is a mask of bits 1, 2, 4, 8");
     c->fuse = value;
     return DR_OK;
   }
@@ -3744,6 +3745,9 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   // context's first replay the buffer did not exist yet)
   HIPCHK(c, c->commit.ensure((size_t)std::max(nw, 1)));
   HIPCHK(c, c->vcount.ensure((size_t)std::max(nw, 1) * 4));
+  // ... and the summaries' and prefixes' buffers (the speculative prefixes' arguments hold
+  // RG, SD, Gc, Ec before build_summary runs)
+  if (int rc = ensure_summary_bufs(c)) return rc;
   if (stat) {
     const size_t need = ((size_t)nw + 2) * 4;
     if (c->pushed.cap < need) {
@@ -3823,8 +3827,9 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     a.rcnt = nullptr;
     a.pm = pmark;
     if (stat && cf.emit_in_sweep)  // the canonical re-emission beside the delivery sweeps
-      a.ce = dr::CanonEmit{kCanonEmitBlocks, T, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
+      a.ce = dr::CanonEmit{kCanonEmitBlocks, 0, T, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
                            c->K.as<u64>(), c->crbase.as<uint32_t>(), c->RG.as<u64>(), c->rlo.as<int>()};
+    if (stat) a.ce.xcd = (c->fuse & 8) ? 1 : 0;
     if (stat && cf.sp.on)  // the pop plan (the chains' pushes, the launch before) beside the delivery sweeps
       a.pp = dr::PopPlanArgs{1, nw, WS, dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave,
                              task_q, cq, cpush_n, push_out, pcap, task_pos, push_off, push_wave, pop_wave, pop_cur,

@@ -892,6 +892,10 @@ __global__ __launch_bounds__(256) void k_verify_up(const u64 *__restrict__ K, co
 // takes round blocks of NT/64 rounds (a wave each) from the top down, nblk apart.
 struct CanonEmit {
   int nblk;  // 0: none
+  // the delivery queries grouped by XCD: blocks b and b + 8 share an XCD's L2 (round-robin
+  // dispatch, MI355X_MICROARCH.md), so each XCD takes a contiguous run of the table --
+  // adjacent waves' queries read the same rounds' words
+  int xcd;
   int T;
   const uint32_t *slot_off;
   const uint16_t *slot_src;
@@ -935,6 +939,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
         return;
       }
       bidx -= ce.nblk;
+    }
+    if (ce.xcd && !seq && !nq_dev && bidx < nq) {  // (nblk is a multiple of 8: b % 8 still names the XCD)
+      const int x = bidx & 7, k = bidx >> 3;
+      bidx = x * (nq >> 3) + min(x, nq & 7) + k;
     }
     if (pp.active && (int)blockIdx.x == (int)gridDim.x - 1) {  // the last: the pop plan (plan_pops_body)
       plan_pops_body<NT>(pp.nw, pp.WS, pp.qflags, pp.lead, pp.task_wave, pp.task_q, pp.cq, pp.push_n, pp.push_out,

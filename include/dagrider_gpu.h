@@ -129,7 +129,8 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * dr_replay share a launch with the phase beside them: 1 = the weak unions with the row
  * pass, 2 = the canonical re-emission with the delivery sweeps, 4 = the speculative
  * canonical prefixes with the canonical walk and the pop plan with the delivery sweeps;
- * 0 = each phase its own launch.  Identical results. */
+ * 0 = each phase its own launch; + 8 = the delivery sweeps' queries
+ * grouped by XCD (adjacent waves on one L2).  Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 /* The form of the context's last dr_replay: 1 = a captured graph was launched,
  * 0 = kernels launched one by one, -1 = one by one after a failed capture

@@ -23,7 +23,7 @@ step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4 -o c
 step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 bench.py --config c3 --no-cpu --steps 5 --warmup 2 > $O/prof_c3.json 2> $O/prof_c3.err || exit 1
 step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o c5 -- python3 bench.py --config c5 --no-cpu --steps 5 --warmup 2 > $O/prof_c5.json 2> $O/prof_c5.err || exit 1
 step 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof_swt -o swt -- python3 tools/sweep_timing.py c4 > $O/swt_c4.json 2> $O/swt_c4.err || exit 1
-for f in 0 3 5; do
+for f in 0 3 15; do
   DR_FUSE=$f step 400 python3 -u bench.py --no-cpu --steps 50 --warmup 5 > $O/bench_c4_fuse$f.json 2> $O/bench_c4_fuse$f.err || exit 1
   python3 -c "import json; d=json.loads(open('$O/bench_c4_fuse$f.json').read()); print('fuse$f', round(d['ms_per_step'],4))"
 done
