@@ -48,7 +48,12 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950
 # correction of MI355X_MICROARCH.md) on this bench: tools/pmc_traffic.py output
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r05", "r04", "r03")]
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r06", "r05", "r04", "r03")]
+
+
+def fuse_mask() -> int:
+    """The engine's DR_OPT_FUSE mask for this process (DR_FUSE overrides the default 7)."""
+    return int(os.environ.get("DR_FUSE", "7"))
 
 
 def phase_kernels(phase: str, W: int = 16):
@@ -269,18 +274,25 @@ def same_replay(a, b) -> bool:
                                                                          b.deliver_edges))
 
 
-def kernel_bytes(cfg, d, res, dreg=None):
+def kernel_bytes(cfg, d, res, dreg=None, mstat=None, wu_fused=True):
     """Algorithmic bytes per launch of each replay phase.  dreg: the engine's
-    regular weak window (the summaries' depth; deeper weak edges are exceptions, s3.5)."""
+    regular weak window (the summaries' depth; deeper weak edges are exceptions, s3.5).
+    mstat (Engine.mirror_stats) with wu_fused: the row pass's launch also carries the weak
+    unions and speculative digests (DR_OPT_FUSE bit 1): the weak-column keys (4 B each), the
+    slot sources (2 B each), slot offsets, column offsets and presence prefixes (16 B per round)
+    read, WU and RG written."""
     n, W, T = cfg.n, (cfg.n + 63) // 64, d.nrounds - 1
     leaders = int((res.vcount >= 0).sum())
     dd = max(0, (dreg if dreg else weak_depth(d)) - 1)
     sw = res.sweep
+    wu = (4 * mstat["weak_columns"] + 2 * mstat["slots"] + 16 * T + T * dd * W * 8 + 8 * T) if (mstat and wu_fused) \
+        else 0
     return {
-        # k_summary_commit: every strong row of rounds 1..T read once; U and SD written
-        # (the weak-column keys -> WU pass, k_weak_union, runs after it, ~4 us, untimed here)
-        "summary": dict(kernel="k_summary_commit (rows -> U, SD + waveReady commit rule)", ms=res.ms["summary"],
-                        bytes=T * n * W * 8 + T * W * 8 + T * 8),
+        # k_summary_commit: every strong row of rounds 1..T read once; U and SD written; with
+        # the weak unions in the same launch, their bytes too
+        "summary": dict(kernel="k_summary_commit (rows -> U, SD + waveReady commit rule"
+                               + (" + weak unions, speculative digests)" if wu else ")"), ms=res.ms["summary"],
+                        bytes=T * n * W * 8 + T * W * 8 + T * 8 + wu),
         # round 4w-2: the word holding the leader bit; rounds 4w-1, 4w: whole rows
         "commit": dict(kernel="k_commit (waveReady commit rule)", ms=res.ms["commit"],
                        bytes=leaders * (n * 8 + 2 * n * W * 8)),
@@ -1275,7 +1287,7 @@ def main() -> int:
         return 0
 
     exc = eng.exception_stats()
-    kb = kernel_bytes(cfg, d, res, exc["regular_delta"])
+    kb = kernel_bytes(cfg, d, res, exc["regular_delta"], eng.mirror_stats(), (fuse_mask() & 1) != 0)
     # dominant kernel = the phase with the largest device time (HIP events)
     dom = max(kb, key=lambda k: kb[k]["ms"])
     ach = kb[dom]["bytes"] / (kb[dom]["ms"] / 1e3) / 1e9 if kb[dom]["ms"] > 0 else 0.0

@@ -76,6 +76,7 @@ SIGNATURES = {
     "dr_abi_version": (C.c_int, []),
     "dr_build_id": (C.c_char_p, []),
     "dr_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)]),
+    "dr_mirror_stats": (C.c_int, [P, C.c_void_p, C.c_int]),
     "dr_create_ex": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)]),
     "dr_destroy": (None, [P]),
     "dr_last_error": (C.c_char_p, [P]),

@@ -311,7 +311,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
       KG1 = readlane64(G1, 63);
     }
     {  // round r's cone record for the emission: K, the lanes whose set differs from K, their sets
-      const u64 dm = __ballot(F0 != K0 || F1 != K1);
+      // (a leader's lane above its own round holds nothing, and a lane past the leaders is
+      // empty: the emission knows both, so neither is stored)
+      const bool own = (lane < nw && r <= 4 * lane + 1) || (haveK && lane == 63);
+      const u64 dm = __ballot(own && (F0 != K0 || F1 != K1));
       crec -= 3u + 2u * (uint32_t)__popcll(dm);
       u64 DR_GLOBAL *rec = g_cone + crec;
       if (lane == 0) {
@@ -556,7 +559,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (int r = 1; r <= T; r++) {
     __syncthreads();
     const bool own = (pm >> lane) & 1ULL;  // this lane's set differs from K in round r
-    const u64 f0 = own ? pf0 : pk0, f1 = own ? pf1 : pk1, P0 = pp0, P1 = pp1;
+    const bool held = (lane < nw && r <= 4 * lane + 1) || (haveK && lane == 63);  // else empty
+    const u64 f0 = own ? pf0 : held ? pk0 : 0ULL, f1 = own ? pf1 : held ? pk1 : 0ULL, P0 = pp0, P1 = pp1;
     const uint32_t sa = psa, sb = psb;
     const int slo = pslo, shi = pshi;
 #pragma unroll

@@ -903,7 +903,8 @@ hipError_t launch_chains(dr_ctx *c, const SweepArgs &a) {
   return launch_sweep(c, a, dr::SW_CHAIN);
 }
 hipError_t launch_sweep(dr_ctx *c, const SweepArgs &a, int mode) {
-  if (a.nq <= 0) return hipSuccess;
+  // (with no query, the launch still runs the canonical re-emission and pop plan riding in it)
+  if (a.nq <= 0 && !((mode & dr::SW_MERGE) && (a.ce.nblk > 0 || a.pp.active))) return hipSuccess;
   switch (c->WS) {
     case 1: return launch_sweep_t<1>(c, a, mode);
     case 2: return launch_sweep_t<2>(c, a, mode);
@@ -2410,6 +2411,14 @@ extern "C" int dr_exception_stats(const dr_ctx *c, int64_t *out) {
   return DR_OK;
 }
 
+extern "C" int dr_mirror_stats(const dr_ctx *c, int64_t *out, int k) {
+  if (!c || !out || k < 0) return DR_E_INVAL;
+  const int64_t v[4] = {c->nrounds, (int64_t)c->h_slot_off.back(), (int64_t)c->h_wc_roff.back(),
+                        (int64_t)c->h_weak_roff.back()};
+  for (int i = 0; i < k && i < 4; i++) out[i] = v[i];
+  return DR_OK;
+}
+
 extern "C" int dr_last_kernel_ms(const dr_ctx *c, float *ms) {
   if (!c || !ms) return DR_E_INVAL;
   *ms = c->last_commit_ms;
@@ -3392,6 +3401,15 @@ hipError_t launch_own_emit_t(dr_ctx *c, int nq, const int32_t *plan, const dr::S
   // (C4 at 256: 12.8 -> 18.8 us; profiles/r03/v18_timeline_*_own256.txt).  Workgroup 0: the
   // canonical prefixes G, E (every DAG length: canon_prefix_regs walks chunks); the last,
   // with pp.active: the pop plan.
+  // (DR_OWN_NT=512 / 256: the experiment's override at WS > 4)
+  static const int own_nt = getenv("DR_OWN_NT") ? atoi(getenv("DR_OWN_NT")) : 512;
+  if (WS > 4 && own_nt == 256) {
+    hipLaunchKernelGGL((dr::k_own_emit<WS, 256>), dim3(1 + nq + (pp.active ? 1 : 0)), dim3(256), 0, c->stream,
+                       c->view(), c->masks.as<u64>(), c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(),
+                       c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), qcount, qdigest, qcut, c->nrounds - 1,
+                       c->RG.as<u64>(), c->CE.as<u64>(), c->Gc.as<u64>(), c->Ec.as<u64>(), pm, pp, lo_w);
+    return hipGetLastError();
+  }
   constexpr int NT = WS <= 4 ? 256 : 512;
   hipLaunchKernelGGL((dr::k_own_emit<WS, NT>), dim3(1 + nq + (pp.active ? 1 : 0)), dim3(NT), 0, c->stream,
                      c->view(), c->masks.as<u64>(), c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(),

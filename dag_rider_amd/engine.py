@@ -148,6 +148,12 @@ class Engine:
         keys = ("exceptions", "changing", "sweeps", "regular_delta", "upward", "memo")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def mirror_stats(self) -> dict:
+        """dr_mirror_stats: rounds, slots, weak-column entries and weak edges of the mirror."""
+        out = np.zeros(4, np.int64)
+        self._check(self._L.dr_mirror_stats(self._h, out.ctypes.data, 4))
+        return {k: int(v) for k, v in zip(("rounds", "slots", "weak_columns", "weak_edges"), out)}
+
     def set_slice(self, round_offset: int = 0, pos_base: int = 0, seeded_top: int = 0, own_w0: int = 0,
                   probes: Sequence[int] = (), clear: bool = False):
         """dr_set_slice: this mirror is global rounds [round_offset, ...) of a bigger DAG

@@ -363,6 +363,10 @@ int dr_last_kernel_ms(const dr_ctx *ctx, float *ms);
  * summaries), out[4] edges to the same or a later round, out[5] 1 while the
  * memoized path serves queries (every exception tested and benign, none upward). */
 int dr_exception_stats(const dr_ctx *ctx, int64_t *out6);
+/* The mirror's sizes (the bench's algorithmic byte counts): out[0] rounds, out[1] slots,
+ * out[2] weak-column entries (distinct near weak targets per round), out[3] weak edges;
+ * the first min(k, 4) are written. */
+int dr_mirror_stats(const dr_ctx *ctx, int64_t *out, int k);
 
 /* Host-side phases (ms, steady clock) of the last fused dr_replay_batch whose
  * first context is ctx: ms4[0] preparation before the launch (checks, job

@@ -182,9 +182,37 @@ def test_upward_weak_edges_verified_memo(gpu_device, seed):
             assert e.exception_stats()["upward"] == len(extra)
             for cm in (L.DR_CHAIN_PERSISTENT, L.DR_CHAIN_LITERAL):
                 got = e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF)
-                assert e.last_replay_path() == want_path, (cm, e.last_replay_path())
                 _same(got, eg.replay(cfg.nwaves, cm, L.DR_DELIVER_REF), ids=False)
+                # (at n <= 130 a pop's cone is partial for several rounds below its top, so a
+                # middle round's edge may well change one: the check may send even the "benign"
+                # set to the general sweep -- test_upward_edge_memo_path_at_n1024 pins path 1)
+                path = e.last_replay_path()
+                assert path == want_path or path == 2, (cm, path)
                 if ld is not None:
                     want = ld.replay(cfg.faulty, cfg.nwaves, cm, L.DR_DELIVER_REF)
                     assert want.rc == 0
                     _same(got, want, ids=False)
+
+
+def test_upward_edge_memo_path_at_n1024(gpu_device):
+    """A same-round and a next-round weak edge in the middle of a C4-shaped DAG (n = 1024,
+    quorum strong edges): every cone that reaches their source is full there, so the verified
+    memo replay keeps the memo path (dr_last_replay_path 1, the c4-up bench line's case) and
+    equals the general sweep."""
+    from dag_rider_amd.gen import generate, small_config, with_extra_edges
+
+    cfg = small_config(1024, 48, 5700, p_present=1.0, p_late=0.02, p_w=0.5, weak_depth=4)
+    d = generate(cfg)
+    present = lambda r: [int(s) for s in d.slot_src[d.slot_off[r]:d.slot_off[r + 1]] if s]  # noqa: E731
+    extra = [(26, present(26)[3], 26, present(26)[9], False), (26, present(26)[5], 27, present(27)[11], False)]
+    dx = with_extra_edges(d, extra)
+    with Engine(cfg.n, cfg.faulty, dx.nrounds, gpu_device) as e, \
+            Engine(cfg.n, cfg.faulty, dx.nrounds, gpu_device) as eg:
+        e.append_packed(dx)
+        eg.append_packed(dx)
+        eg.set_memo(False)
+        assert e.exception_stats()["upward"] == 2
+        for cm in (L.DR_CHAIN_PERSISTENT, L.DR_CHAIN_LITERAL):
+            got = e.replay(cfg.nwaves, cm, L.DR_DELIVER_REF)
+            assert e.last_replay_path() == 1
+            _same(got, eg.replay(cfg.nwaves, cm, L.DR_DELIVER_REF), ids=False)
