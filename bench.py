@@ -66,7 +66,7 @@ def phase_kernels(phase: str, W: int = 16):
         return [[f"dr::k_summary_commit<{W}, 1024, 2, false>" if W == 16 else f"dr::k_summary_commit<{W}, {blk}, 8, false>"]]
     if phase == "sweep":  # merging pop sweeps (SW_WEAK | SW_MERGE = 9), own-round emission, final pass
         nt = 192 if W == 16 else min(blk, 512)
-        return [[f"dr::k_sweep<{W}, {nt}, 9>", f"dr::k_own_emit<{W}, {256 if W <= 4 else 512}>",
+        return [[f"dr::k_sweep<{W}, {nt}, 9>", f"dr::k_own_emit<{W}, 256>",
                  "dr::k_replay_final<1024>"]]
     if phase == "batch_k_replay_small_1w":  # the wave-per-DAG form (many DAGs per CU)
         return [["dr::k_replay_small_1w<false, true>"]]

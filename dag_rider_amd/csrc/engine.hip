@@ -3397,12 +3397,15 @@ template <int WS>
 hipError_t launch_own_emit_t(dr_ctx *c, int nq, const int32_t *plan, const dr::SweepQuery *dq, const int32_t *stops,
                              u64 *qcount, u64 *qdigest, int32_t *qcut, const dr::PopMark &pm,
                              const dr::PopPlanArgs &pp, const int *lo_w) {
-  // 256 threads per query at n <= 256 (C3: 41 -> 37 us, more queries resident), 512 above
-  // (C4 at 256: 12.8 -> 18.8 us; profiles/r03/v18_timeline_*_own256.txt).  Workgroup 0: the
+  // 256 threads per query at n <= 256 (C3: 41 -> 37 us, more queries resident); above it
+  // see own_nt below (round 3: C4 at 256 12.8 -> 18.8 us, when the own ranges were longer,
+  // profiles/r03/v18_timeline_*_own256.txt).  Workgroup 0: the
   // canonical prefixes G, E (every DAG length: canon_prefix_regs walks chunks); the last,
   // with pp.active: the pop plan.
-  // (DR_OWN_NT=512 / 256: the experiment's override at WS > 4)
-  static const int own_nt = getenv("DR_OWN_NT") ? atoi(getenv("DR_OWN_NT")) : 512;
+  // At WS > 4 256 threads too (round 6: a query's own range is the few rounds above its cut,
+  // and at 512 threads, 90 VGPRs, C4's 977 queries took two passes over the CUs: 17.0 ->
+  // 14.8 us, profiles/r06/i_timeline_c4_own256.txt).  DR_OWN_NT=512: the wide block.
+  static const int own_nt = getenv("DR_OWN_NT") ? atoi(getenv("DR_OWN_NT")) : 256;
   if (WS > 4 && own_nt == 256) {
     hipLaunchKernelGGL((dr::k_own_emit<WS, 256>), dim3(1 + nq + (pp.active ? 1 : 0)), dim3(256), 0, c->stream,
                        c->view(), c->masks.as<u64>(), c->memo_view().dmax, plan, dq, stops, c->Cc.as<u64>(),
@@ -3661,6 +3664,15 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
   size_t mask_words = 0;  // every wave's leader a distinct query: rounds 0..4(w-1)+1
   for (int w = 1; w <= nw; w++) mask_words += (size_t)(4 * (w - 1) + 2) * WS;
   if (mask_words > ((size_t)1 << 29) || chain_slots > INT32_MAX) return 1;
+  // A replay that launches kernel by kernel starts the row pass first: the host's planning
+  // below (arena, static query table, launch arguments) then runs beside it instead of
+  // before it (the row pass needs only the summary buffers and the commit flags)
+  const bool early = !(c->replay_graph && !c->graph_fail && c->phase_timing <= 1 && !c->shared_stream);
+  if (early) {
+    HIPCHK(c, c->commit.ensure((size_t)std::max(nw, 1)));
+    HIPCHK(c, c->vcount.ensure((size_t)std::max(nw, 1) * 4));
+    if (int rc = build_summary(c, nullptr, nw, nullptr, nullptr, false, false, nullptr, false, 1)) return rc;
+  }
   // device arena
   Carve cv;
   int32_t *plan = nullptr, *task_wave, *task_q, *cpush_n, *push_out, *push_wave, *pop_wave, *pop_cur, *pop_q,
@@ -3963,7 +3975,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
     c->graph_state = 1;
   } else {
     if (!enqueued)
-      if (int rc = enqueue(nullptr, 3)) return rc;
+      if (int rc = enqueue(nullptr, early ? 2 : 3)) return rc;
     c->plan_host.resize(out_bytes);
     HIPCHK(c, c->d2h(c->plan_host.data(), c->plan_out.p, out_bytes));
     HIPCHK(c, c->sync());
