@@ -52,8 +52,8 @@ TRAFFIC_FILES = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r0
 
 
 def fuse_mask() -> int:
-    """The engine's DR_OPT_FUSE mask for this process (DR_FUSE overrides the default 7)."""
-    return int(os.environ.get("DR_FUSE", "7"))
+    """The engine's DR_OPT_FUSE mask for this process (DR_FUSE overrides the default 23)."""
+    return int(os.environ.get("DR_FUSE", "23"))
 
 
 def phase_kernels(phase: str, W: int = 16):

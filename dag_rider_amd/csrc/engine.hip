@@ -236,8 +236,9 @@ struct dr_ctx {
   // (dr::WUArgs, the chain plan then in k_kcand_plan); bit 1 = the canonical re-emission
   // rides in the delivery sweeps' launch; bit 2 = the speculative G, E prefixes beside the
   // canonical walk (k_canon_chains) and the pop plan beside the delivery sweeps; bit 3 = the
-  // delivery sweeps' queries grouped by XCD (dr::CanonEmit::xcd)
-  int fuse = getenv("DR_FUSE") ? atoi(getenv("DR_FUSE")) : 7;
+  // delivery sweeps' queries grouped by XCD (dr::CanonEmit::xcd); bit 4 = the static delivery queries merge
+  // fast (dr::Q_FAST)
+  int fuse = getenv("DR_FUSE") ? atoi(getenv("DR_FUSE")) : 23;
   int last_split = 0;   // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
   bool kprev_ok = false;
@@ -284,6 +285,7 @@ struct dr_ctx {
   int32_t pop_epoch = 0;
   std::vector<uint64_t> sdq_key;
   int sdq_n = 0;
+  bool sdq_fast = false;  // the static table's queries carry Q_FAST
   DevBuf plan_arena;        // device-planned replay (replay_plan.hpp)
   DevBuf plan_out;          // its outputs, packed for one copy back
   std::vector<char> plan_host;
@@ -467,6 +469,7 @@ struct dr_ctx {
     m.dmax = std::max(1, dreg);
     // exceptions present: the canonical walk and Q_REGULAR sweeps follow G_reg alone
     m.dreg = nexc > 0 ? dreg : 0x7fffffff;
+    m.CE = CE.as<u64>();
     return m;
   }
   dr::DagView view() const {
@@ -506,7 +509,8 @@ struct dr_ctx {
     while ((1 << l) < d) l++;
     return l;
   }
-  size_t sweep_lds(int dl) const { return (size_t)(2 * WS + (1 << dl) * WS) * 8 + 64; }
+  // (+ a second ring for Q_FAST merge sweeps: kring, kernels.hpp sweep_body)
+  size_t sweep_lds(int dl, bool fast = false) const { return (size_t)((2 + (fast ? 2 : 1) * (1 << dl)) * WS) * 8 + 64; }
   uint64_t round_deg(int r) const { return hr[r].deg; }
   bool has_ghost(int r) const {
     for (uint16_t s : hr[r].slots)
@@ -816,6 +820,7 @@ struct SweepArgs {  // (every field initialised: a launch never reads a stale po
   dr::PopMark pm{};             // REF planned replay: live delivery queries / chain stamps
   dr::CanonEmit ce{};           // merge sweeps: the canonical re-emission's workgroups (first in the grid)
   dr::PopPlanArgs pp{};         // merge sweeps: the pop plan's workgroup (last in the grid; pp.active)
+  bool fast = false;            // some query has Q_FAST: the second ring in LDS
 };
 // The REF replay's leader chains inside the single-stream launches: the chain plan in the
 // weak-union launch (k_wu_plan), the chain sweeps beside the canonical walk (k_canon_chains)
@@ -846,7 +851,7 @@ template <int WS, int MODE>
 hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   constexpr int NT = sweep_block_m<WS, MODE>();
   const int dl = c->depth_log2();
-  const size_t lds = c->sweep_lds(dl);
+  const size_t lds = c->sweep_lds(dl, a.fast);
   static std::atomic<int> seen[kLdsDevs] = {};
   hipError_t e = lds_limit((const void *)dr::k_sweep<WS, NT, MODE>, seen, c->dev, lds);
   if (e != hipSuccess) return e;
@@ -870,6 +875,8 @@ hipError_t launch_sweep_t(dr_ctx *c, const SweepArgs &a, int mode) {
     case dr::SW_CHAIN: return launch_sweep_m<WS, dr::SW_CHAIN>(c, a);
     case dr::SW_WEAK | dr::SW_PRUNE: return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_PRUNE>(c, a);
     case dr::SW_WEAK | dr::SW_MERGE: return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_MERGE>(c, a);
+    case dr::SW_WEAK | dr::SW_MERGE | dr::SW_FAST:
+      return launch_sweep_m<WS, dr::SW_WEAK | dr::SW_MERGE | dr::SW_FAST>(c, a);
   }
   return hipErrorInvalidValue;
 }
@@ -880,6 +887,7 @@ int sweep_mode(const dr::SweepQuery &q) {
   if (q.flags & dr::Q_CHAIN) m |= dr::SW_CHAIN;
   if (q.flags & dr::Q_PRUNE) m |= dr::SW_PRUNE;
   if (q.flags & dr::Q_MERGE) m |= dr::SW_MERGE;
+  if ((q.flags & dr::Q_FAST) && (m & dr::SW_MERGE) && (m & dr::SW_WEAK)) m |= dr::SW_FAST;
   return m;
 }
 // The planned replay's leader chains (a device-counted batch): n <= 256 on one
@@ -2274,7 +2282,7 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     return DR_OK;
   }
   if (option == DR_OPT_FUSE) {
-    if (value < 0 || value > 15) return c->fail(DR_E_INVAL, "DR_OPT_FUSE is a mask of bits 1, 2, 4, 8");
+    if (value < 0 || value > 31) return c->fail(DR_E_INVAL, "DR_OPT_FUSE is a mask of bits 1, 2, 4, 8, 16");
     c->fuse = value;
     return DR_OK;
   }
@@ -3579,7 +3587,13 @@ std::vector<uint64_t> graph_key(const dr_ctx *c, int nw, int chain_mode, bool pa
 // leader coin or the wave count changed): pops no longer wait for the leader chains --
 // a pop's cone depends on its leader alone, and every pushed leader is a present one.
 int ensure_static_pops(dr_ctx *c, int nw) {
-  const std::vector<uint64_t> key{c->version, (uint64_t)nw, (uint64_t)c->WS, (uint64_t)(uintptr_t)c->sdq.p};
+  // DR_OPT_FUSE bit 16: the fast merge (Q_FAST) where every weak slot rides in the sweep's
+  // round words (dd <= DDR), at n > 512: the SW_FAST sweep's second ring costs registers
+  // (C4, WS 16: 156 -> 161 VGPRs, 3 waves/SIMD either way, pop sweep 32.7 -> 29.3 us; C3, WS 4:
+  // 126 -> 141, 4 -> 3 waves/SIMD, 50.6 -> 63.6 us: profiles/r06/j_*)
+  const bool fast = (c->fuse & 16) && c->memo_dd() <= dr::DDR && c->WS >= 16;
+  const std::vector<uint64_t> key{c->version, (uint64_t)nw, (uint64_t)c->WS, (uint64_t)(uintptr_t)c->sdq.p,
+                                  (uint64_t)fast, (uint64_t)c->memo_dd()};
   if (key == c->sdq_key) return DR_OK;
   std::vector<dr::SweepQuery> q;
   std::vector<int32_t> qi((size_t)nw + 1, -1);
@@ -3591,7 +3605,7 @@ int ensure_static_pops(dr_ctx *c, int nw) {
     x.top = top;
     x.bottom = 0;
     x.src0 = L - 1;
-    x.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
+    x.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE | (fast ? dr::Q_FAST : 0);
     x.mask_off = moff;
     x.tgt0 = -1;
     moff += (int64_t)(top + 1) * c->WS;
@@ -3608,7 +3622,9 @@ int ensure_static_pops(dr_ctx *c, int nw) {
   HIPCHK(c, c->h2d(c->splan.p, sp.data(), sp.size() * 4));
   HIPCHK(c, c->flush_h2d());
   c->sdq_n = (int)q.size();
-  c->sdq_key = {c->version, (uint64_t)nw, (uint64_t)c->WS, (uint64_t)(uintptr_t)c->sdq.p};
+  c->sdq_fast = fast;
+  c->sdq_key = {c->version, (uint64_t)nw, (uint64_t)c->WS, (uint64_t)(uintptr_t)c->sdq.p, (uint64_t)fast,
+                (uint64_t)c->memo_dd()};
   return DR_OK;
 }
 
@@ -3860,6 +3876,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       a.ce = dr::CanonEmit{kCanonEmitBlocks, 0, T, c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(),
                            c->K.as<u64>(), c->crbase.as<uint32_t>(), c->RG.as<u64>(), c->rlo.as<int>()};
     if (stat) a.ce.xcd = (c->fuse & 8) ? 1 : 0;
+    a.fast = stat && c->sdq_fast;
     if (stat && cf.sp.on)  // the pop plan (the chains' pushes, the launch before) beside the delivery sweeps
       a.pp = dr::PopPlanArgs{1, nw, WS, dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave,
                              task_q, cq, cpush_n, push_out, pcap, task_pos, push_off, push_wave, pop_wave, pop_cur,
@@ -3897,7 +3914,7 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
       for (int i = 0; i < dr::kMaxProbe; i++) f.probe[i] = c->slice_on && i < c->slice.nprobe ? c->slice.probe[i] : 0;
     }
     dr::SweepQuery probe{};
-    probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE;
+    probe.flags = dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE | (stat && c->sdq_fast ? dr::Q_FAST : 0);
     if (!stat) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));  // PAPER: the pops planned on stream2
     HIPCHK(c, c->rec(2));
     HIPCHK(c, launch_sweep(c, a, sweep_mode(probe)));

@@ -54,7 +54,11 @@ __device__ u64 g_canon_timing[8];  // k_canon: start, segments walked, positions
 
 // Q_REGULAR: follow only the regular graph -- strong rows and weak columns of delta
 // <= MemoView::dreg, no far edge (the exception test, engine.hip ensure_exceptions)
-enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8, Q_SHORTCUT = 16, Q_MERGE = 32, Q_REGULAR = 64 };
+// Q_FAST (merge sweeps with summaries, dd <= DDR): also stop at the first round r whose
+// frontier equals K_r while the pending ring equals K's pending contributions from the
+// rounds above (sweep_body: kring); the cut is then r itself
+enum : int32_t { Q_STRONG_ONLY = 1, Q_CHAIN = 2, Q_MASKS = 4, Q_PRUNE = 8, Q_SHORTCUT = 16, Q_MERGE = 32, Q_REGULAR = 64,
+                 Q_FAST = 128 };
 
 struct SweepQuery {
   int32_t top;       // start round (the `from` vertex's round)
@@ -410,6 +414,7 @@ struct MemoView {
   int32_t dd;    // dense weak slots (deltas 2 .. dd+1); 0 with no weak edges
   int32_t dmax;  // merge window = max(1, largest regular weak delta)
   int32_t dreg;  // the regular window: weak columns of larger delta (and far edges) are exceptions
+  const u64 *CE;  // the canonical rounds' edges (Q_FAST: the rounds a fast merge skips)
 };
 
 // One partial round r of a sweep: the frontier FE's strong rows -> ring slot of
@@ -727,7 +732,9 @@ __device__ __forceinline__ void expand_summary(const MemoView &mv, const RoundWo
 //           F -> ring[r-1] and weak edges of F -> ring[r'].
 // LDS: F[WS] | FE[WS] | ring[depth][WS] | ctl (int[8]) | edges (u64[2]).
 // ---------------------------------------------------------------------------
-enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8 };
+// SW_FAST (with SW_WEAK | SW_MERGE): the fast merge of Q_FAST queries compiled in (its second
+// ring costs registers: a launch of queries without Q_FAST keeps the plain merge sweep)
+enum : int { SW_WEAK = 1, SW_CHAIN = 2, SW_PRUNE = 4, SW_MERGE = 8, SW_FAST = 16 };
 
 // exclusive scan over one workgroup; s = NT/64 scratch slots; every thread calls
 template <int NT, class T>
@@ -1098,7 +1105,7 @@ __device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView m
     else if (bidx >= m) return;
   }
   constexpr bool WEAK = MODE & SW_WEAK, CHAIN = MODE & SW_CHAIN, PRUNE = MODE & SW_PRUNE,
-                 MERGE = MODE & SW_MERGE;
+                 MERGE = MODE & SW_MERGE, FASTM = (MODE & SW_FAST) && WEAK && MERGE;
   constexpr u64 WMASK = WS >= 64 ? ~0ULL : ((1ULL << WS) - 1ULL);  // lanes owning a frontier word
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
   u64 *F = smem;                // WS: frontier (reached ids, dangling included)
@@ -1109,6 +1116,9 @@ __device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView m
   //      [5] [6] the partial round's weak-column range
   int *s_ctl = reinterpret_cast<int *>(ring + (size_t)depth * WS);
   u64 *s_edges = reinterpret_cast<u64 *>(s_ctl + 8);  // [0] all edges, [1] weak edges, [2] row bytes
+  // Q_FAST: K's contributions pending for the rounds below, from the rounds the sweep has
+  // passed (depth x WS, after the control words: sweep_lds(dl, true))
+  u64 *kring = reinterpret_cast<u64 *>(reinterpret_cast<char *>(smem) + (size_t)(2 * WS + depth * WS) * 8 + 64);
   const int tid = threadIdx.x;
   const bool w0 = tid < 64;     // wave 0 runs phase A and every summary round
   const bool act = tid < WS;    // lane w owns frontier word w
@@ -1124,7 +1134,11 @@ __device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView m
     const bool has_masks = q.flags & Q_MASKS;
     const bool shortcut = q.flags & Q_SHORTCUT;
     const int dreg = (q.flags & Q_REGULAR) ? mv.dreg : 0x7fffffff;
-    for (int i = tid; i < depth * WS; i += NT) ring[i] = 0;
+    const bool fast = FASTM && shortcut && (q.flags & Q_FAST) && mv.dd <= DDR;
+    for (int i = tid; i < depth * WS; i += NT) {
+      ring[i] = 0;
+      if (FASTM && fast) kring[i] = 0;
+    }
     if (tid == 0) {
       s_ctl[0] = q.top; s_ctl[1] = q.top; s_ctl[2] = 0; s_ctl[3] = 0; s_ctl[4] = q.bottom;
       s_edges[0] = 0; s_edges[1] = 0; s_edges[2] = 0;
@@ -1137,6 +1151,7 @@ __device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView m
     DR_TT(u64 tt0 = wall_clock64(); u64 tt_a = 0, tt_b = 0, tt_pro = 0, tt_ns = 0, tt_np = 0, tt_end = 0, tt_emit = 0;
           u64 tt_sub[4] = {0, 0, 0, 0};)
     int run = 0;    // wave 0: consecutive rounds equal to K
+    int kfrun = 0;  // wave 0 (Q_FAST): consecutive rounds passed whose K covers the round
     u64 my_edges = 0, my_wedges = 0, my_rowb = 0;
     RoundWords cur{}, nxt{};
     if (act) {
@@ -1160,6 +1175,7 @@ __device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView m
             const int slot = (r & dmask) * WS + tid;
             f = ring[slot];
             ring[slot] = 0;
+            if (FASTM && fast) kring[slot] = 0;
             u64 *mrow = has_masks ? masks + q.mask_off + (int64_t)(r - q.bottom) * WS : nullptr;
             if constexpr (WEAK && !MERGE) {
               if (has_masks) f |= ld_agent(mrow + tid);  // far weak scatters
@@ -1195,11 +1211,43 @@ __device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView m
           }
           const bool nz = (__ballot(act && f != 0ULL) & WMASK) != 0;
           const bool full = (__ballot(act && (f & p) != p) & WMASK) == 0;
+          bool eq = false;
           if constexpr (MERGE) {
-            const bool eq = (__ballot(act && f != cur.K) & WMASK) == 0;
+            eq = (__ballot(act && f != cur.K) & WMASK) == 0;
             run = eq ? run + 1 : 0;
           }
-          const bool merged = MERGE && run >= mv.dmax;
+          // Q_FAST: F_r = K_r and the ring's pending words for r-1 .. r-dmax+1 equal K's
+          // (the contributions of rounds r+1 .. r+dmax-1, every one covered by K: WU) -- the
+          // sweep's state at r is K's, so its cone below r+1 is K's
+          bool fastm = false;
+          if constexpr (FASTM) {
+            if (fast) {
+              const bool kf = (__ballot(act && (cur.K & p) != p) & WMASK) == 0;
+              if (eq && kfrun >= mv.dmax - 1 && r - mv.dmax + 1 >= max(q.bottom, 0)) {
+                bool diff = false;
+                if (act)
+                  for (int j = 1; j < mv.dmax; j++) {
+                    const size_t sl = (size_t)((r - j) & dmask) * WS + tid;
+                    diff |= ring[sl] != kring[sl];
+                  }
+                fastm = (__ballot(diff) & WMASK) == 0;
+              }
+              if (kf && act)  // K_r covers the round: its contributions below are WU_r
+#pragma unroll
+                for (int d = 0; d < DDR; d++) {
+                  const int tr = r - d - 2;
+                  if (d < mv.dd && tr >= q.bottom) kring[(size_t)(tr & dmask) * WS + tid] |= cur.WU[d];
+                }
+              kfrun = kf ? kfrun + 1 : 0;
+            }
+          }
+          const bool merged = MERGE && (run >= mv.dmax || fastm);
+          if (FASTM && fastm && run < mv.dmax) {  // the cut is r: the canonical edges of r - dmax + 2 .. r
+            u64 ce = 0;
+            if (tid < mv.dmax - 1) ce = mv.CE[r - tid];
+            ce = wave_sum(ce);
+            if (tid == 0) my_edges += ce;
+          }
           int low = s_ctl[0];
           if (nz && r - 1 < low) low = r - 1;
           const bool stop = merged || r <= q.bottom || (!nz && low >= r);
@@ -1271,7 +1319,7 @@ __device__ __forceinline__ void sweep_body(const int bidx, DagView g, MemoView m
             s_ctl[1] = r;
             s_ctl[2] = stop ? 1 : 0;
             s_ctl[3] = merged ? 1 : 0;
-            if (stop && (merged || r > q.bottom)) s_ctl[4] = r;
+            if (stop && (merged || r > q.bottom)) s_ctl[4] = (FASTM && fastm && run < mv.dmax) ? r - mv.dmax + 1 : r;
             if constexpr (WEAK) {  // the round's weak-column range, prefetched with its words
               s_ctl[5] = (int)cur.C0;
               s_ctl[6] = (int)cur.C1;

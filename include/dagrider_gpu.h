@@ -125,12 +125,13 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * and the copy of the outputs into pinned memory) and later such calls launch
  * the graph (with DR_OPT_PHASE_TIMING <= 1).  0 = launch every kernel per call,
  * as fast on MI355X at C3/C4.  Identical results.
- * DR_OPT_FUSE (default 7, bits): which independent phases of a device-planned REF
+ * DR_OPT_FUSE (default 23, bits): which independent phases of a device-planned REF
  * dr_replay share a launch with the phase beside them: 1 = the weak unions with the row
  * pass, 2 = the canonical re-emission with the delivery sweeps, 4 = the speculative
  * canonical prefixes with the canonical walk and the pop plan with the delivery sweeps;
  * 0 = each phase its own launch; + 8 = the delivery sweeps' queries
- * grouped by XCD (adjacent waves on one L2).  Identical results. */
+ * grouped by XCD (adjacent waves on one L2); + 16 = the delivery sweeps stop at the first
+ * round whose state equals the canonical cone's (n > 512).  Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 /* The form of the context's last dr_replay: 1 = a captured graph was launched,
  * 0 = kernels launched one by one, -1 = one by one after a failed capture
