@@ -237,7 +237,7 @@ struct dr_ctx {
   // rides in the delivery sweeps' launch; bit 2 = the speculative G, E prefixes beside the
   // canonical walk (k_canon_chains) and the pop plan beside the delivery sweeps; bit 3 = the
   // delivery sweeps' queries grouped by XCD (dr::CanonEmit::xcd); bit 4 = the static delivery queries merge
-  // fast (dr::Q_FAST)
+  // fast (dr::Q_FAST); bit 5 = each query's own rounds emitted by its sweep workgroup (dr::OwnEmit)
   int fuse = getenv("DR_FUSE") ? atoi(getenv("DR_FUSE")) : 23;
   int last_split = 0;   // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
@@ -821,6 +821,7 @@ struct SweepArgs {  // (every field initialised: a launch never reads a stale po
   dr::CanonEmit ce{};           // merge sweeps: the canonical re-emission's workgroups (first in the grid)
   dr::PopPlanArgs pp{};         // merge sweeps: the pop plan's workgroup (last in the grid; pp.active)
   bool fast = false;            // some query has Q_FAST: the second ring in LDS
+  dr::OwnEmit oe{};             // merge sweeps: each query's own-round emission after its sweep
 };
 // The REF replay's leader chains inside the single-stream launches: the chain plan in the
 // weak-union launch (k_wu_plan), the chain sweeps beside the canonical walk (k_canon_chains)
@@ -864,7 +865,8 @@ hipError_t launch_sweep_m(dr_ctx *c, const SweepArgs &a) {
   pp.active = np;
   hipLaunchKernelGGL((dr::k_sweep<WS, NT, MODE>), dim3(grid), dim3(NT), lds, c->stream,
                      c->view(), c->memo_view(), a.q, a.nq, a.seq, dl, a.masks, a.dlv, a.push_out,
-                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt, a.pm, ce, pp);
+                     a.push_n, a.edges, a.wedges, a.hits, a.stops, a.stats, a.nq_dev, a.rcnt, a.pm, ce, pp,
+                     (MODE & dr::SW_MERGE) ? a.oe : dr::OwnEmit{});
   return hipGetLastError();
 }
 template <int WS>
@@ -2282,7 +2284,7 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
     return DR_OK;
   }
   if (option == DR_OPT_FUSE) {
-    if (value < 0 || value > 31) return c->fail(DR_E_INVAL, "DR_OPT_FUSE is a mask of bits 1, 2, 4, 8, 16");
+    if (value < 0 || value > 63) return c->fail(DR_E_INVAL, "DR_OPT_FUSE is a mask of bits 1, 2, 4, 8, 16, 32");
     c->fuse = value;
     return DR_OK;
   }
@@ -3877,6 +3879,12 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
                            c->K.as<u64>(), c->crbase.as<uint32_t>(), c->RG.as<u64>(), c->rlo.as<int>()};
     if (stat) a.ce.xcd = (c->fuse & 8) ? 1 : 0;
     a.fast = stat && c->sdq_fast;
+    // DR_OPT_FUSE bit 32 (with the speculative prefixes): the own rounds emitted by each query's
+    // sweep workgroup, the G, E rescan in the final pass; no k_own_emit launch
+    const bool own_in_sweep = stat && cf.sp.on && (c->fuse & 32);
+    if (own_in_sweep)
+      a.oe = dr::OwnEmit{1, c->Cc.as<u64>(), c->slot_off.as<uint32_t>(), c->slot_src.as<uint16_t>(), qcount, qdigest,
+                         qcut};
     if (stat && cf.sp.on)  // the pop plan (the chains' pushes, the launch before) beside the delivery sweeps
       a.pp = dr::PopPlanArgs{1, nw, WS, dr::Q_MASKS | dr::Q_SHORTCUT | dr::Q_MERGE, c->lead.as<uint16_t>(), task_wave,
                              task_q, cq, cpush_n, push_out, pcap, task_pos, push_off, push_wave, pop_wave, pop_cur,
@@ -3931,8 +3939,11 @@ int replay_planned(dr_ctx *c, int nw, int chain_mode, bool paper, dr_replay_out 
                          task_q, cq, cpush_n, push_out, pcap, task_pos, push_off, push_wave, pop_wave, pop_cur,
                          pop_q, seen, qidx, dq, plan, c->sqidx.as<int32_t>(), c->sdq_n};
       if (cf.sp.on) pp.active = 0;  // (the delivery sweeps' launch planned the pops)
-      HIPCHK(c, launch_own_emit(c, c->sdq_n, splan, sdq, dstops, qcount, qdigest, qcut, pmark, pp,
-                                cf.sp.on ? c->nseg.as<int32_t>() + 1 : nullptr));
+      if (!own_in_sweep)
+        HIPCHK(c, launch_own_emit(c, c->sdq_n, splan, sdq, dstops, qcount, qdigest, qcut, pmark, pp,
+                                  cf.sp.on ? c->nseg.as<int32_t>() + 1 : nullptr));
+      else
+        em.fin.lo_w = c->nseg.as<int32_t>() + 1;
       if (c->up_verify) HIPCHK(c, launch_verify_up(c, dstops, qcut, pmark));  // the upward edges against the cones
     }
     HIPCHK(c, c->rec(3));

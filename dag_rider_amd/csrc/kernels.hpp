@@ -888,6 +888,9 @@ struct FinalArgs {
   const int32_t *upbad;  // k_verify_up's count (null: no upward edges checked)
   int32_t own_w0, nprobe;
   int32_t probe[kMaxProbe];
+  // the canonical walk's lowest round (nseg + 1): the final pass first rescans the G, E
+  // prefixes from there (the speculative prefixes are exact below it; null: no rescan here)
+  const int32_t *lo_w;
 };
 
 // The planned replay's per-query emission outputs (k_own_emit, k_paper_emit):
@@ -979,11 +982,22 @@ __device__ __forceinline__ u64 wave_emit_round(const uint32_t *__restrict__ slot
 // launches), the commits and pushes, and the totals, into the packed output
 // region.  Every pop of a replay has cur_round >= top (a leader is popped at a
 // wave's end, above its own round): checked, a violation reports PH_CAPERR = 3.
+template <int NT, int J, class LA, class LB>
+__device__ __forceinline__ void canon_prefix_gen(int r0, int T, u64 ca, u64 cb, LA la, LB lb, u64 *__restrict__ A,
+                                                 u64 *__restrict__ B);
 template <int NT>
 __device__ void replay_final_block(const FinalArgs &f, const EmitArgs &ea) {
   __shared__ u64 acc[8];
   __shared__ int s_bad;
   const int tid = threadIdx.x;
+  if (f.lo_w) {  // (block-uniform) G, E from the walk's lowest round up (DR_OPT_FUSE bit 32)
+    const int lw = *f.lo_w;
+    if (lw <= f.T)
+      canon_prefix_gen<NT, 8>(
+          lw, f.T, lw >= 1 ? f.Gc[lw - 1] : 0ULL, lw >= 1 ? f.Ec[lw - 1] : 0ULL, [&](int r) { return f.RG[r]; },
+          [&](int r) { return f.CE[r]; }, f.Gc, f.Ec);
+    __syncthreads();
+  }
   if (tid < 8) acc[tid] = 0;
   if (tid == 0) s_bad = 0;
   const int caperr = f.plan[PL_CAPERR];

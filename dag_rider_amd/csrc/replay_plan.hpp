@@ -756,54 +756,17 @@ __global__ __launch_bounds__(NT) void k_paper_emit(DagView g, const u64 *__restr
   }
 }
 
-// REF delivery, own rounds (after the merging delivery sweeps, SW_MERGE): one
-// workgroup per query, rounds cut+1 .. top (cut = merge round + dmax - 1: the
-// merge run's rounds have the canonical positions too, DESIGN.md s3.2) or, for
-// an unmerged sweep, every round it reached; positions from C_cut on.  NT/64
-// rounds at a time, one per wave.  With Gc, the grid's last workgroup computes the
-// canonical digest and edge prefixes G, E for k_replay_final (one pass of its
-// threads: T + 1 <= 8 NT; a longer DAG's prefixes come from k_canon_prefix).
+// One query's own-round emission (k_own_emit, or the delivery sweep's workgroup right after
+// its sweep: dr::OwnEmit): rounds cut+1 .. top from its mask rows, positions from C_cut.
 template <int WS, int NT>
-__global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restrict__ masks, int dmax,
-                                                 const int32_t *__restrict__ plan, const SweepQuery *__restrict__ dq,
-                                                 const int32_t *__restrict__ stops, const u64 *__restrict__ Cc,
-                                                 const uint32_t *__restrict__ slot_off,
-                                                 const uint16_t *__restrict__ slot_src, u64 *__restrict__ qcount,
-                                                 u64 *__restrict__ qdigest, int32_t *__restrict__ qcut, int T,
-                                                 const u64 *__restrict__ RG, const u64 *__restrict__ CE,
-                                                 u64 *__restrict__ Gc, u64 *__restrict__ Ec, const PopMark pm,
-                                                 const PopPlanArgs pp, const int *__restrict__ lo_w) {
+__device__ __forceinline__ void own_emit_query(const DagView &g, const u64 *__restrict__ masks, int dmax, int q,
+                                               int stop, int top, int64_t moff, const u64 *__restrict__ Cc,
+                                               const uint32_t *__restrict__ slot_off,
+                                               const uint16_t *__restrict__ slot_src, u64 *__restrict__ qcount,
+                                               u64 *__restrict__ qdigest, int32_t *__restrict__ qcut) {
   constexpr int NWV = NT / 64;
   __shared__ u64 s_c[NWV], s_dg;
-  // workgroup 0 (with Gc): the canonical prefixes G, E -- the longest workgroup, so it
-  // starts first; the last (pp.active): the pop plan (plan_pops_body), which needs only the
-  // chains' pushes (the launch before this one)
-  const int pre = Gc ? 1 : 0, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (pre && blockIdx.x == 0) {  // (Gc null: k_canon_prefix computed them)
-    if (lo_w) {  // the speculative prefixes are exact below the walk's lowest round: rescan from there
-      const int lw = *lo_w;
-      if (lw <= T)
-        canon_prefix_gen<NT, 8>(
-            lw, T, lw >= 1 ? Gc[lw - 1] : 0ULL, lw >= 1 ? Ec[lw - 1] : 0ULL, [&](int r) { return RG[r]; },
-            [&](int r) { return CE[r]; }, Gc, Ec);
-    } else {
-      canon_prefix_regs<NT, 8>(T, RG, CE, Gc, Ec);
-    }
-    return;
-  }
-  if (pp.active && blockIdx.x == gridDim.x - 1) {
-    plan_pops_body<NT>(pp.nw, pp.WS, pp.qflags, pp.lead, pp.task_wave, pp.task_q, pp.cq, pp.push_n, pp.push_out,
-                       pp.pcap, pp.task_pos, pp.push_off, pp.push_wave, pp.pop_wave, pp.pop_cur, pp.pop_q, pp.seen,
-                       pp.qidx, pp.dq, pp.plan, pp.qidx_static, pp.nqd_static);
-    return;
-  }
-  const int q = (int)blockIdx.x - pre;
-  // the query's fields load with the plan counts (the arena holds every slot below the grid bound)
-  const int nq = plan[PL_NQD], caperr = plan[PL_CAPERR];
-  const int stop = stops[q], top = dq[q].top;
-  const int64_t moff = dq[q].mask_off;
-  if (q >= nq || caperr) return;
-  if (pm.commit && !pm.live(top)) return;  // a wave nobody pops: its sweep did not run
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int cut = stop >= 0 ? min(stop + dmax - 1, top) : -1;
   const int first = stop >= 0 ? cut + 1 : max(1, -1 - stop);
   const u64 pos0 = cut >= 0 ? Cc[cut] : 0ULL;
@@ -843,6 +806,56 @@ __global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restric
     qcut[q] = cut;
   }
 }
+
+// REF delivery, own rounds (after the merging delivery sweeps, SW_MERGE): one
+// workgroup per query, rounds cut+1 .. top (cut = merge round + dmax - 1: the
+// merge run's rounds have the canonical positions too, DESIGN.md s3.2) or, for
+// an unmerged sweep, every round it reached; positions from C_cut on.  NT/64
+// rounds at a time, one per wave.  With Gc, the grid's last workgroup computes the
+// canonical digest and edge prefixes G, E for k_replay_final (one pass of its
+// threads: T + 1 <= 8 NT; a longer DAG's prefixes come from k_canon_prefix).
+template <int WS, int NT>
+__global__ __launch_bounds__(NT) void k_own_emit(DagView g, const u64 *__restrict__ masks, int dmax,
+                                                 const int32_t *__restrict__ plan, const SweepQuery *__restrict__ dq,
+                                                 const int32_t *__restrict__ stops, const u64 *__restrict__ Cc,
+                                                 const uint32_t *__restrict__ slot_off,
+                                                 const uint16_t *__restrict__ slot_src, u64 *__restrict__ qcount,
+                                                 u64 *__restrict__ qdigest, int32_t *__restrict__ qcut, int T,
+                                                 const u64 *__restrict__ RG, const u64 *__restrict__ CE,
+                                                 u64 *__restrict__ Gc, u64 *__restrict__ Ec, const PopMark pm,
+                                                 const PopPlanArgs pp, const int *__restrict__ lo_w) {
+  // workgroup 0 (with Gc): the canonical prefixes G, E -- the longest workgroup, so it
+  // starts first; the last (pp.active): the pop plan (plan_pops_body), which needs only the
+  // chains' pushes (the launch before this one)
+  const int pre = Gc ? 1 : 0;
+  if (pre && blockIdx.x == 0) {  // (Gc null: k_canon_prefix computed them)
+    if (lo_w) {  // the speculative prefixes are exact below the walk's lowest round: rescan from there
+      const int lw = *lo_w;
+      if (lw <= T)
+        canon_prefix_gen<NT, 8>(
+            lw, T, lw >= 1 ? Gc[lw - 1] : 0ULL, lw >= 1 ? Ec[lw - 1] : 0ULL, [&](int r) { return RG[r]; },
+            [&](int r) { return CE[r]; }, Gc, Ec);
+    } else {
+      canon_prefix_regs<NT, 8>(T, RG, CE, Gc, Ec);
+    }
+    return;
+  }
+  if (pp.active && blockIdx.x == gridDim.x - 1) {
+    plan_pops_body<NT>(pp.nw, pp.WS, pp.qflags, pp.lead, pp.task_wave, pp.task_q, pp.cq, pp.push_n, pp.push_out,
+                       pp.pcap, pp.task_pos, pp.push_off, pp.push_wave, pp.pop_wave, pp.pop_cur, pp.pop_q, pp.seen,
+                       pp.qidx, pp.dq, pp.plan, pp.qidx_static, pp.nqd_static);
+    return;
+  }
+  const int q = (int)blockIdx.x - pre;
+  // the query's fields load with the plan counts (the arena holds every slot below the grid bound)
+  const int nq = plan[PL_NQD], caperr = plan[PL_CAPERR];
+  const int stop = stops[q], top = dq[q].top;
+  const int64_t moff = dq[q].mask_off;
+  if (q >= nq || caperr) return;
+  if (pm.commit && !pm.live(top)) return;  // a wave nobody pops: its sweep did not run
+  own_emit_query<WS, NT>(g, masks, dmax, q, stop, top, moff, Cc, slot_off, slot_src, qcount, qdigest, qcut);
+}
+
 
 // Upward weak edges (App. A Q8: to the same or a later round) on the memo path
 // (engine.hip dr_replay, up_verify).  The replay ran on the regular graph G_reg; an
@@ -924,13 +937,24 @@ __device__ __forceinline__ void canon_emit_blocks(const DagView &g, const CanonE
                             nullptr, 0, &s_dg, nullptr, nullptr, lo);
 }
 
+// The own-round emission inside the delivery sweeps' launch (DR_OPT_FUSE bit 32): each query's
+// workgroup emits its rounds above the cut as soon as its sweep stops, instead of a launch of
+// its own after every sweep (k_own_emit)
+struct OwnEmit {
+  int on;
+  const u64 *Cc;
+  const uint32_t *slot_off;
+  const uint16_t *slot_src;
+  u64 *qcount, *qdigest;
+  int32_t *qcut;
+};
 template <int WS, int NT, int MODE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_MERGE) ? 3 : 1))) void k_sweep(
     DagView g, MemoView mv, const SweepQuery *__restrict__ qs, int nq, int seq, int depth_log2, u64 *__restrict__ masks,
     u64 *__restrict__ dlv, int32_t *__restrict__ push_out, int32_t *__restrict__ push_n, u64 *__restrict__ edges_out,
     u64 *__restrict__ wedges_out, uint8_t *__restrict__ hit_out, int32_t *__restrict__ stop_out,
     u64 *__restrict__ stats_out, const int *__restrict__ nq_dev, uint32_t *__restrict__ rcnt, const PopMark pm,
-    const CanonEmit ce, const PopPlanArgs pp) {
+    const CanonEmit ce, const PopPlanArgs pp, const OwnEmit oe) {
   int bidx = (int)blockIdx.x;
   if constexpr ((MODE & SW_MERGE) != 0) {
     if (ce.nblk > 0) {  // (block-uniform) the first nblk workgroups re-emit canonical rounds
@@ -953,6 +977,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((MODE & SW_M
   }
   sweep_body<WS, NT, MODE>(bidx, g, mv, qs, nq, seq, depth_log2, masks, dlv, push_out, push_n, edges_out, wedges_out,
                            hit_out, stop_out, stats_out, nq_dev, rcnt, pm);
+  if constexpr ((MODE & SW_MERGE) != 0) {
+    if (oe.on && !seq && !nq_dev && bidx < nq) {  // (block-uniform)
+      const SweepQuery q = qs[bidx];
+      if (pm.commit && !pm.live(q.top)) return;  // a wave nobody pops: no sweep, no emission
+      // (sweep_body ended with a barrier after thread 0 wrote the stop and the mask rows)
+      own_emit_query<WS, NT>(g, masks, mv.dmax, bidx, stop_out[bidx], q.top, q.mask_off, oe.Cc, oe.slot_off,
+                             oe.slot_src, oe.qcount, oe.qdigest, oe.qcut);
+    }
+  }
 }
 
 }  // namespace dr

@@ -37,7 +37,7 @@ def test_large_config_golden(gpu_device, name):
     with Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) as e:
         e.append_packed(d)
         _check(e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
-        for mask in (0, 1, 2, 4, 7, 15, 23, 31):  # DR_OPT_FUSE: the launch groupings give the same replay
+        for mask in (0, 1, 2, 4, 7, 15, 23, 31, 39, 55, 63):  # DR_OPT_FUSE: the launch groupings give the same replay
             e.set_fuse(mask)
             _check(e.replay(cfg.nwaves, L.DR_CHAIN_PERSISTENT, L.DR_DELIVER_REF), g["persistent_ref"])
         e.set_device_plan(False)  # the host-planned phases give the same replay

@@ -101,7 +101,7 @@ def test_random_dag_replay(gpu_device, seed):
     bs = oracle.PDag(d)
     with Engine(n, f, R + 1, gpu_device) as e:
         if seed % 2:  # DR_OPT_FUSE: every launch grouping plus the fast merge (Q_FAST)
-            e.set_fuse(31)
+            e.set_fuse(63)
         # append in two chunks: exercises the append-only mirror
         cut = int(rng.integers(1, R + 1))
         e.append_packed(d, 0, cut)
