@@ -26,6 +26,7 @@ DR_OPT_BATCH_FORM = 4
 DR_OPT_COMMIT_SPLIT = 5
 DR_OPT_REPLAY_GRAPH = 6
 DR_OPT_FUSE = 7
+DR_OPT_CALL_OVERLAP = 8
 DR_CREATE_SHARED_STREAM = 1
 DR_BATCH_AUTO, DR_BATCH_WORKGROUP, DR_BATCH_WAVE = 0, 1, 2
 DR_LEADER_CONST1, DR_LEADER_SEEDED, DR_LEADER_TABLE = 0, 1, 2

@@ -239,6 +239,12 @@ struct dr_ctx {
   // delivery sweeps' queries grouped by XCD (dr::CanonEmit::xcd); bit 4 = the static delivery queries merge
   // fast (dr::Q_FAST); bit 5 = each query's own rounds emitted by its sweep workgroup (dr::OwnEmit)
   int fuse = getenv("DR_FUSE") ? atoi(getenv("DR_FUSE")) : 23;
+  // DR_OPT_CALL_OVERLAP: once a REF orderVertices was answered, dr_wave_ready starts the
+  // canonical cone of the new top on stream2 beside the commit rule (the next
+  // dr_order_vertices merges with it); s2_detached: that work is in flight, the waits
+  // inside dr_wave_ready skip stream2 and its end joins it on the device (ev_join)
+  int call_overlap = getenv("DR_CALL_OVERLAP") ? atoi(getenv("DR_CALL_OVERLAP")) : 1;
+  bool ref_seen = false, s2_detached = false;
   int last_split = 0;   // workgroups per wave of the last commit launch (0: k_commit)
   int canon_lo = 0, canon_dd = -1;
   bool kprev_ok = false;
@@ -397,9 +403,9 @@ struct dr_ctx {
       if (e == hipSuccess && !small.empty()) e = launch_copies(small.data(), (int)small.size());
     }
     if (e == hipSuccess) e = hipEventRecord(ev_sync, stream);
-    if (e == hipSuccess && stream2) e = hipEventRecord(ev_sync2, stream2);
+    if (e == hipSuccess && stream2 && !s2_detached) e = hipEventRecord(ev_sync2, stream2);
     if (e == hipSuccess) e = wait_event(ev_sync);
-    if (e == hipSuccess && stream2) e = wait_event(ev_sync2);
+    if (e == hipSuccess && stream2 && !s2_detached) e = wait_event(ev_sync2);
     if (e == hipSuccess) {
       for (auto &p : pend) std::memcpy(p.dst, p.stage, p.n);
       async_what.clear();
@@ -1088,30 +1094,25 @@ hipError_t launch_weak_union(dr_ctx *c, int T, hipStream_t st, const ChainFuse *
 
 // incremental summaries of the listed rounds (device list of nr rounds)
 template <int WS>
-hipError_t launch_round_summary_t(dr_ctx *c, const int32_t *rounds, int nr) {
+hipError_t launch_round_summary_t(dr_ctx *c, const dr::RoundList &rl) {
   constexpr int NT = block_for<WS>() < 256 ? 256 : block_for<WS>();
   const dr::MemoView mv = c->memo_view();
-  hipLaunchKernelGGL((dr::k_round_summary<WS, NT>), dim3(nr), dim3(NT), 0, c->stream, c->view(), rounds,
-                     c->U.as<u64>(), c->SD.as<u64>());
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || mv.dd == 0) return e;
-  const int nwv = weak_union_waves(mv.dd, WS);
-  const size_t lds = (size_t)nwv * mv.dd * WS * 8;
-  e = weak_union_lds<WS>(c, lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((dr::k_weak_union<WS>), dim3((nr + nwv - 1) / nwv), dim3(64 * nwv), lds, c->stream, c->view(),
-                     c->nrounds - 1, nr, mv.dd, c->WU.as<u64>(), rounds, (const u64 *)nullptr,
-                     (const uint32_t *)nullptr, (const uint16_t *)nullptr, (u64 *)nullptr);
+  // the weak unions in the same launch: nwv rounds per workgroup within 64 KB of LDS
+  const int nwv = mv.dd > 0 ? weak_union_waves(mv.dd, WS, NT / 64) : 1;
+  const int nwu = mv.dd > 0 ? (rl.n + nwv - 1) / nwv : 0;
+  const size_t lds = mv.dd > 0 ? (size_t)nwv * mv.dd * WS * 8 : 0;
+  hipLaunchKernelGGL((dr::k_round_summary<WS, NT>), dim3(rl.n + nwu), dim3(NT), lds, c->stream, c->view(), rl,
+                     c->U.as<u64>(), c->SD.as<u64>(), mv.dd, nwv, c->WU.as<u64>());
   return hipGetLastError();
 }
-hipError_t launch_round_summary(dr_ctx *c, const int32_t *rounds, int nr) {
+hipError_t launch_round_summary(dr_ctx *c, const dr::RoundList &rounds) {
   switch (c->WS) {
-    case 1: return launch_round_summary_t<1>(c, rounds, nr);
-    case 2: return launch_round_summary_t<2>(c, rounds, nr);
-    case 4: return launch_round_summary_t<4>(c, rounds, nr);
-    case 8: return launch_round_summary_t<8>(c, rounds, nr);
-    case 16: return launch_round_summary_t<16>(c, rounds, nr);
-    case 32: return launch_round_summary_t<32>(c, rounds, nr);
+    case 1: return launch_round_summary_t<1>(c, rounds);
+    case 2: return launch_round_summary_t<2>(c, rounds);
+    case 4: return launch_round_summary_t<4>(c, rounds);
+    case 8: return launch_round_summary_t<8>(c, rounds);
+    case 16: return launch_round_summary_t<16>(c, rounds);
+    case 32: return launch_round_summary_t<32>(c, rounds);
   }
   return hipErrorInvalidValue;
 }
@@ -1966,8 +1967,15 @@ int refresh_rounds(dr_ctx *c, bool any = false) {
   for (int r = 1; r <= T; r++)
     if (all || c->sdirty[r]) list.push_back(r);
   if (!list.empty()) {
-    HIPCHK(c, c->h2d(c->srounds.p, list.data(), list.size() * 4));
-    HIPCHK(c, launch_round_summary(c, c->srounds.as<int32_t>(), (int)list.size()));
+    dr::RoundList rl{};
+    rl.n = (int)list.size();
+    if (rl.n <= dr::kRoundListMax) {  // in the launch's arguments
+      std::copy(list.begin(), list.end(), rl.r);
+    } else {
+      HIPCHK(c, c->h2d(c->srounds.p, list.data(), list.size() * 4));
+      rl.ext = c->srounds.as<int32_t>();
+    }
+    HIPCHK(c, launch_round_summary(c, rl));
   }
   mark_rounds_clean(c);
   return DR_OK;
@@ -2286,6 +2294,11 @@ extern "C" int dr_set_option(dr_ctx *c, int option, int value) {
   if (option == DR_OPT_FUSE) {
     if (value < 0 || value > 63) return c->fail(DR_E_INVAL, "DR_OPT_FUSE is a mask of bits 1, 2, 4, 8, 16, 32");
     c->fuse = value;
+    return DR_OK;
+  }
+  if (option == DR_OPT_CALL_OVERLAP) {
+    if (value < 0 || value > 2) return c->fail(DR_E_INVAL, "DR_OPT_CALL_OVERLAP is 0, 1 or 2");
+    c->call_overlap = value;
     return DR_OK;
   }
   if (option == DR_OPT_DEVICE_PLAN) {
@@ -2867,7 +2880,8 @@ namespace {
 
 // Commit decisions for waves [w0, w1] (host handles waves whose round(w,4) is
 // not mirrored: legal only when their leader is bottom).
-int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, float *ms) {
+int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, float *ms,
+                 const std::function<int()> *pre_sync = nullptr) {
   if (w0 < 1 || w1 < w0) return c->fail(DR_E_INVAL, "wave range [%d,%d] invalid (waves are 1-based)", w0, w1);
   int wk = w0 - 1;  // last wave the kernel can evaluate
   while (wk + 1 <= w1 && 4 * (wk + 1) < c->nrounds) wk++;
@@ -2888,6 +2902,8 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
   HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nw));
   HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nw * 4));
+  if (pre_sync)  // launches the host queues while the commit rule runs
+    if (int rc = (*pre_sync)()) return rc;
   HIPCHK(c, c->sync());
   HIPCHK(c, hipEventElapsedTime(&c->last_commit_ms, c->ev[4], c->ev[5]));
   if (ms) *ms = c->last_commit_ms;
@@ -3304,7 +3320,30 @@ extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *com
   if (int rc = prep_query(c)) return rc;
   if (int rc = refresh_rounds(c)) return rc;
   *n_pushed = 0;
-  if (int rc = commit_range(c, wave, wave, commit, vcount, nullptr)) return rc;
+  // DR_OPT_CALL_OVERLAP: the canonical cone of the new top (what the next REF
+  // dr_order_vertices merges with, refresh_canon) on stream2, forked after the round
+  // summaries and launched while the commit rule runs; every later launch on the main
+  // stream waits for it on the device (the join below), none on the host
+  const bool spec = c->call_overlap == 2 && c->ref_seen && c->memo_on() && c->nrounds >= 2 && !c->canon_ok;
+  std::function<int()> fork = [c]() -> int {
+    c->s2_detached = true;
+    return launch_canon(c, true, nullptr, true, true);
+  };
+  if (spec) {
+    if (int rc = ensure_summary_bufs(c)) return rc;
+    HIPCHK(c, ensure_stream2(c));
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+  }
+  struct Join {  // (on every return below)
+    dr_ctx *c;
+    ~Join() {
+      if (!c->s2_detached) return;
+      c->s2_detached = false;
+      (void)hipStreamWaitEvent(c->stream, c->ev_join, 0);
+    }
+  } join{c};
+  if (int rc = commit_range(c, wave, wave, commit, vcount, nullptr, spec ? &fork : nullptr)) return rc;
   if (!*commit) return DR_OK;
   std::vector<std::vector<int32_t>> pushes(1);
   if (c->general()) {
@@ -3316,6 +3355,12 @@ extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *com
   if ((int)pushes[0].size() > cap || (!pushed_waves && !pushes[0].empty()))
     return c->fail(DR_E_CAPACITY, "%zu pushed leaders, capacity %d", pushes[0].size(), cap);
   std::copy(pushes[0].begin(), pushes[0].end(), pushed_waves);
+  // DR_OPT_CALL_OVERLAP 1: a commit, so orderVertices follows -- its canonical cone runs on
+  // the device while the caller prepares the pops (no wait here)
+  if (c->call_overlap == 1 && c->ref_seen && c->memo_on() && c->nrounds >= 2 && !c->canon_ok) {
+    if (int rc = ensure_summary_bufs(c)) return rc;
+    if (int rc = launch_canon(c, false, nullptr, false, true)) return rc;
+  }
   return DR_OK;
 }
 
@@ -3356,8 +3401,10 @@ extern "C" int dr_order_vertices(dr_ctx *c, const int32_t *stack_rs, int nstack,
     if (out_ids && (size_t)tot > cap) return c->fail(DR_E_CAPACITY, "%lld delivered ids, capacity %zu", (long long)tot, cap);
     return DR_OK;
   }
-  if (mode == DR_DELIVER_REF)  // stale rounds' summaries + the canonical cone of the current top
+  if (mode == DR_DELIVER_REF) {  // stale rounds' summaries + the canonical cone of the current top
+    c->ref_seen = true;
     if (int rc = refresh_canon(c)) return rc;
+  }
   // REF mode on fresh summaries without ids: planned on the device, one copy back
   int rc = 1;
   if (mode == DR_DELIVER_REF && !out_ids && c->plan_mode != 0 && summary_fresh(c))

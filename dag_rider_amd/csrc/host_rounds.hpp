@@ -48,6 +48,8 @@ struct BuiltRounds {
 // by the mirror (dr_ctx), so it lives and dies with it.
 struct BuildScratch {
   std::vector<std::vector<int32_t>> tab;
+  std::vector<std::vector<uint64_t>> bm;    // merge_round's key bitmap, per thread
+  std::vector<std::vector<uint32_t>> rank;  // and its running popcount per word
 };
 
 // Validate and build the host state of every round (rounds in parallel).

@@ -1757,18 +1757,42 @@ __global__ __launch_bounds__(NT) void k_summary_commit(DagView g, int T, int nwc
   }
 }
 
+// The rounds an append touched: up to kRoundListMax of them travel in the launch's
+// arguments (the per-call waveReady's four: no copy before the launch), more in
+// device memory (ext).
+constexpr int kRoundListMax = 16;
+struct RoundList {
+  int n;
+  int32_t r[kRoundListMax];
+  const int32_t *ext;
+};
+__device__ __forceinline__ int round_at(const RoundList &l, int i) { return l.ext ? l.ext[i] : l.r[i]; }
+
 // U_r and SD_r of the listed rounds (the incremental summaries of rounds an
 // append touched): one workgroup per round, the row stream of k_summary_commit
-// without the commit rule.
+// without the commit rule.  With dd > 0 the workgroups after the first rl.n take
+// the listed rounds' weak unions WU_r, nwv rounds each (one wave per round, the
+// others idle; dynamic LDS nwv x dd x WS words): they read the weak-column keys
+// alone, so they run beside the row workgroups instead of in a launch after them.
 template <int WS, int NT>
-__global__ __launch_bounds__(NT) void k_round_summary(DagView g, const int32_t *__restrict__ rounds,
-                                                      u64 *__restrict__ U, u64 *__restrict__ SD) {
+__global__ __launch_bounds__(NT) void k_round_summary(DagView g, const RoundList rl, u64 *__restrict__ U,
+                                                      u64 *__restrict__ SD, int dd, int nwv,
+                                                      u64 *__restrict__ WU) {
+  if ((int)blockIdx.x >= rl.n) {  // (block-uniform) a weak-union workgroup
+    extern __shared__ __attribute__((aligned(16))) u64 wu_lds[];
+    const int wid = threadIdx.x >> 6;
+    const int i = ((int)blockIdx.x - rl.n) * nwv + wid;
+    if (wid >= nwv || i >= rl.n) return;  // wave-uniform
+    weak_union_round<WS>(g, round_at(rl, i), dd, WU, wu_lds + (size_t)wid * dd * WS, nullptr, nullptr, nullptr,
+                         nullptr, threadIdx.x & 63);
+    return;
+  }
   using G = Geo<WS, NT>;
   constexpr int CW = G::CW, CPR = G::CPR, RPP = G::RPP, CPT = G::CPT;
   __shared__ u64 sU[WS];
   __shared__ u64 sSD;
   const int tid = threadIdx.x, lane = tid & 63, j = tid % CPR, n = g.n;
-  const int r = rounds[blockIdx.x];
+  const int r = round_at(rl, blockIdx.x);
   if (tid < WS) sU[tid] = 0;
   if (tid == 0) sSD = 0;
   __syncthreads();

@@ -116,6 +116,12 @@ class Engine:
         """DR_OPT_FUSE: which independent replay phases share a launch (7 = all, 0 = none)."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_FUSE, int(mask)))
 
+    def set_call_overlap(self, mode: int):
+        """DR_OPT_CALL_OVERLAP: after a REF orderVertices, waveReady launches the canonical cone of
+        the new top once it knows of a commit (1, the default) or on a second stream beside the
+        commit rule (2); 0 = orderVertices computes it.  Identical results."""
+        self._check(self._L.dr_set_option(self._h, L.DR_OPT_CALL_OVERLAP, int(mode)))
+
     def set_batch_form(self, form: int):
         """DR_OPT_BATCH_FORM (read from a batch's first engine): DR_BATCH_AUTO, DR_BATCH_WORKGROUP
         (four wavefronts per DAG) or DR_BATCH_WAVE (one wavefront per DAG); identical results."""

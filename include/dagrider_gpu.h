@@ -49,7 +49,7 @@ enum {
 };
 enum { DR_CHAIN_LITERAL = 0, DR_CHAIN_PERSISTENT = 1 };
 enum { DR_OPT_MEMO = 1, DR_OPT_DEVICE_PLAN = 2, DR_OPT_PHASE_TIMING = 3, DR_OPT_BATCH_FORM = 4, DR_OPT_COMMIT_SPLIT = 5,
-       DR_OPT_REPLAY_GRAPH = 6, DR_OPT_FUSE = 7 };
+       DR_OPT_REPLAY_GRAPH = 6, DR_OPT_FUSE = 7, DR_OPT_CALL_OVERLAP = 8 };
 enum { DR_BATCH_AUTO = 0, DR_BATCH_WORKGROUP = 1, DR_BATCH_WAVE = 2 };
 enum { DR_DELIVER_REF = 0, DR_DELIVER_PAPER = 1 };
 enum { DR_WEAK_LITERAL = 0, DR_WEAK_PAPER = 1 };
@@ -131,7 +131,11 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * canonical prefixes with the canonical walk and the pop plan with the delivery sweeps;
  * 0 = each phase its own launch; + 8 = the delivery sweeps' queries
  * grouped by XCD (adjacent waves on one L2); + 16 = the delivery sweeps stop at the first
- * round whose state equals the canonical cone's (n > 512).  Identical results. */
+ * round whose state equals the canonical cone's (n > 512).  Identical results.
+ * DR_OPT_CALL_OVERLAP (default 1): once the context answered a DR_DELIVER_REF
+ * dr_order_vertices, dr_wave_ready computes the canonical cone of the new top round on a
+ * second stream beside the commit rule (the next REF dr_order_vertices merges with it);
+ * 0 = dr_order_vertices computes it.  Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 /* The form of the context's last dr_replay: 1 = a captured graph was launched,
  * 0 = kernels launched one by one, -1 = one by one after a failed capture

@@ -246,3 +246,54 @@ def test_staged_packed_append_then_queries(gpu_device):
                 if commit:
                     assert [(4 * (x - 1) + 1, e.wave_leader(x)) for x in pushed] == list(st)
         e.append_packed(d, r1, d.nrounds)  # then destroy with the copies possibly in flight
+
+
+@pytest.mark.gpu
+def test_gpu_wave_loop_call_overlap_interleaved(gpu_device):
+    """DR_OPT_CALL_OVERLAP: after a REF orderVertices, waveReady launches the canonical cone of
+    the new top once a commit is known (1) or on a second stream while the commit rule runs (2).  The loop below skips
+    orderVertices on some commits, answers others in PAPER mode (with ids) or REF mode (ids,
+    or counts + digests on the device-planned path), and asks path() between calls; every
+    answer equals a context with the overlap off doing the same calls."""
+    from dag_rider_amd.gen import GenConfig, generate
+
+    cfg = GenConfig("c4-small", 1024, 160, 4, 1.0, 0.02, 0.5, 4, 0.0)
+    d = generate(cfg, nthreads=8)
+    nw = (d.nrounds - 1) // 4
+    rng = np.random.default_rng(31)
+    engines = [Engine(cfg.n, cfg.faulty, d.nrounds, gpu_device) for _ in range(3)]
+    for e, ov in zip(engines, (1, 2, 0)):
+        e.set_call_overlap(ov)
+    try:
+        for e in engines:
+            e.append_packed(d, 0, 1)
+        decided = 0
+        for w in range(1, nw + 1):
+            out = []
+            for e in engines:
+                e.append_packed(d, 4 * w - 3, 4 * w + 1)
+                out.append(e.wave_ready(w, decided))
+            assert out[0] == out[1] == out[2]
+            cm, _, pushed = out[0]
+            pairs = [((4 * w, int(rng.integers(1, cfg.n + 1))), (int(rng.integers(0, 4 * w)),
+                                                                  int(rng.integers(1, cfg.n + 1))))
+                     for _ in range(8)]
+            want = engines[2].path_batch(pairs, False).tolist()
+            assert all(e.path_batch(pairs, False).tolist() == want for e in engines[:2])
+            if not cm:
+                continue
+            stack = [(4 * (x - 1) + 1, engines[0].wave_leader(x)) for x in pushed]
+            k = w % 4
+            if k == 1:
+                continue  # committed, not delivered: the next waveReady forks again
+            mode = L.DR_DELIVER_PAPER if k == 2 else L.DR_DELIVER_REF
+            cap = 0 if k == 3 else None
+            res = [e.order_vertices(stack, 4 * w, mode, cap=cap) if cap is not None
+                   else e.order_vertices(stack, 4 * w, mode) for e in engines]
+            for r in res[:2]:
+                for a, b in zip(r, res[2]):
+                    assert np.asarray(a).tolist() == np.asarray(b).tolist()
+            decided = w
+    finally:
+        for e in engines:
+            e.close()
