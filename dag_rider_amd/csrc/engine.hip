@@ -446,6 +446,10 @@ struct dr_ctx {
     hipError_t e = stage(n, &p);
     if (e != hipSuccess) return e;
     std::memcpy(p, host, n);
+    return h2d_staged(dev, p, n);
+  }
+  // the copy of n bytes the caller already wrote at p (from stage())
+  hipError_t h2d_staged(void *dev, void *p, size_t n) {
     if (n >= ((size_t)1 << 22)) return hipMemcpyAsync(dev, p, n, hipMemcpyHostToDevice, stream);
     const dr::CopySeg sg{static_cast<const uint8_t *>(p), static_cast<uint8_t *>(dev), n};
     if (defer_h2d) {
@@ -1436,7 +1440,14 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   in.weak_off = weak_off;
   in.weak_tgt = weak_tgt;
   dr_host::BuiltRounds built;
+  const size_t row_words = (size_t)n * WS;
+  const bool staged = WS == W && (size_t)k * row_words * 8 <= ((size_t)16 << 20);
+  void *row_stage = nullptr;  // per-round appends: the build's chunk tasks copy the rows into pinned staging
   const auto ta0 = std::chrono::steady_clock::now();
+  if (staged) {
+    HIPCHK(c, c->stage((size_t)k * row_words * 8, &row_stage));
+    in.strong_stage = static_cast<uint64_t *>(row_stage);
+  }
   if (int rc = dr_host::build_packed_rounds(in, c->dmax_near, built, c->err, c->build_scr)) return rc;
   const auto ta1 = std::chrono::steady_clock::now();
   std::vector<HostRound> &nh = built.rounds;
@@ -1444,10 +1455,8 @@ extern "C" int dr_append_rounds_packed(dr_ctx *c, int r0, int k, const uint32_t 
   const int dmax = built.dmax;
   // ---- commit: rows and per-vertex degrees, then the flattened per-round arrays ----
   DeferH2D batch(c);  // every staged copy below goes out in one launch at sync()
-  const size_t row_words = (size_t)n * WS;
-  const bool staged = WS == W && (size_t)k * row_words * 8 <= ((size_t)16 << 20);
-  if (staged) {  // per-round appends: pinned staging
-    HIPCHK(c, c->h2d(c->strong.as<u64>() + (size_t)r0 * row_words, strong, (size_t)k * row_words * 8));
+  if (staged) {  // per-round appends: pinned staging, written by the build
+    HIPCHK(c, c->h2d_staged(c->strong.as<u64>() + (size_t)r0 * row_words, row_stage, (size_t)k * row_words * 8));
   } else if (WS == W) {  // bulk loads: straight from the caller's memory
     HIPCHK(c, hipMemcpyAsync(c->strong.as<u64>() + (size_t)r0 * row_words, strong,
                              (size_t)k * row_words * 8, hipMemcpyHostToDevice, c->stream));

@@ -31,6 +31,7 @@ struct PackedRounds {
   const uint64_t *strong = nullptr;
   const uint32_t *weak_off = nullptr;
   const uint32_t *weak_tgt = nullptr;  // (r' << 11) | t-1; bit 31: a strong edge outside r-1 (App. A Q8)
+  uint64_t *strong_stage = nullptr;    // optional: the rows are copied here too (each chunk task its own)
 };
 
 struct BuiltRounds {

@@ -5,6 +5,7 @@
 // no longer leaves most cores idle -- and each round's chunk columns are merged
 // by key afterwards.
 #include "host_rounds.hpp"
+namespace dr_host_old { using dr_host::PackedRounds; using dr_host::BuiltRounds; using dr_host::BuildScratch; using dr_host::HostRound; }
 
 #include <algorithm>
 #include <cstdarg>
@@ -15,7 +16,7 @@
 
 #include "dagrider_gpu.h"
 
-namespace dr_host {
+namespace dr_host_old {
 namespace {
 
 int failf(std::string &err, int code, const char *fmt, ...) {
@@ -42,26 +43,20 @@ struct Chunk {
   std::vector<uint64_t> irr;  // edges outside the round contract (general.hpp irr_pack)
 };
 
-// The slot pass of round i (insertion order, presence) for the sources [s_lo, s_hi)
-// of one chunk: its words of the presence row (the chunks' words are disjoint); the
-// chunk at s_lo == 0 also keeps the slot list and reports a bad source.  An id may
-// repeat (the reference appends whatever uponDeliver / the buffer loop hands it,
-// process.go:158-169, :229): every slot stays, the packed row is the id's one vertex
-// as path()'s lookup sees it (its last slot, :112-116).
-int build_slots(const PackedRounds &in, int i, int s_lo, int s_hi, BuiltRounds &out, std::string &err) {
+// The slot pass of round i (insertion order, presence).  An id may repeat (the
+// reference appends whatever uponDeliver / the buffer loop hands it,
+// process.go:158-169, :229): every slot stays, the packed row is the id's one
+// vertex as path()'s lookup sees it (its last slot, :112-116).
+int build_slots(const PackedRounds &in, int i, BuiltRounds &out, std::string &err) {
   const int n = in.n, r = in.r0 + i;
   uint64_t *P = &out.pres[(size_t)i * in.WS];
-  const bool first = s_lo == 0;
   HostRound &h = out.rounds[i];
-  if (first) h.slots.reserve(in.slot_off[i + 1] - in.slot_off[i]);
+  h.slots.reserve(in.slot_off[i + 1] - in.slot_off[i]);
   for (uint32_t sl = in.slot_off[i]; sl < in.slot_off[i + 1]; sl++) {
     const int s = in.slot_src[sl];
-    if (s > n) {
-      if (first) return failf(err, DR_E_CONTRACT, "round %d slot %u: source %d > n=%d", r, sl - in.slot_off[i], s, n);
-      continue;
-    }
-    if (first) h.slots.push_back((uint16_t)s);
-    if (s == 0 || s - 1 < s_lo || s - 1 >= s_hi) continue;  // ghost slot {0,0}, or another chunk's
+    if (s > n) return failf(err, DR_E_CONTRACT, "round %d slot %u: source %d > n=%d", r, sl - in.slot_off[i], s, n);
+    h.slots.push_back((uint16_t)s);
+    if (s == 0) continue;  // ghost slot {0,0}
     P[(s - 1) >> 6] |= 1ULL << ((s - 1) & 63);
   }
   return 0;
@@ -150,36 +145,20 @@ void build_chunk(const PackedRounds &in, int i, int s_lo, int s_hi, std::vector<
 
 // Round i's columns: the union of its chunks' keys, sorted (wc_add's binary
 // search relies on it), each row the chunks' words side by side.
-// The keys (delta << 11 | t-1) as a bitmap over (delta, t) -- delta <= 1023, t < 2048
-// -- whose running popcount is each key's column.
-void merge_round(const PackedRounds &in, int i, const Chunk *ck, int nch, int chunk, BuiltRounds &out,
-                 std::vector<uint64_t> &bm, std::vector<uint32_t> &rank) {
+void merge_round(const PackedRounds &in, int i, const Chunk *ck, int nch, int chunk, BuiltRounds &out) {
   const int WS = in.WS, n = in.n;
   HostRound &h = out.rounds[i];
-  int dm = 0;
-  for (int c = 0; c < nch; c++)
-    for (uint32_t k : ck[c].key) dm = std::max(dm, (int)(k >> 11));
-  const size_t nword = (size_t)(dm + 1) * 32;  // 2048 bits per delta
-  if (bm.size() < nword) bm.resize(nword);
-  std::fill(bm.begin(), bm.begin() + (ptrdiff_t)nword, 0ULL);
-  for (int c = 0; c < nch; c++)
-    for (uint32_t k : ck[c].key) bm[k >> 6] |= 1ULL << (k & 63);
-  if (rank.size() < nword) rank.resize(nword);
-  uint32_t nk = 0;
-  for (size_t w = 0; w < nword; w++) {
-    rank[w] = nk;
-    nk += (uint32_t)__builtin_popcountll(bm[w]);
-  }
-  h.wc_key.resize(nk);
-  for (size_t w = 0, j = 0; w < nword; w++)
-    for (uint64_t x = bm[w]; x; x &= x - 1) h.wc_key[j++] = (uint32_t)(w * 64 + (size_t)__builtin_ctzll(x));
-  h.wc_rows.assign((size_t)nk * WS, 0ULL);
+  std::vector<uint32_t> keys;
+  for (int c = 0; c < nch; c++) keys.insert(keys.end(), ck[c].key.begin(), ck[c].key.end());
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  h.wc_key = keys;
+  h.wc_rows.assign(keys.size() * WS, 0ULL);
   for (int c = 0; c < nch; c++) {
     const Chunk &x = ck[c];
     const int s_lo = c * chunk, w_lo = s_lo >> 6, cw = (std::min(n, s_lo + chunk) - s_lo + 63) >> 6;
     for (size_t j = 0; j < x.key.size(); j++) {
-      const uint32_t k = x.key[j];
-      const size_t col = rank[k >> 6] + (size_t)__builtin_popcountll(bm[k >> 6] & ((1ULL << (k & 63)) - 1ULL));
+      const size_t col = std::lower_bound(keys.begin(), keys.end(), x.key[j]) - keys.begin();
       std::memcpy(&h.wc_rows[col * WS + w_lo], &x.rows[j * cw], (size_t)cw * 8);
     }
     h.deg += x.deg;
@@ -205,40 +184,29 @@ int build_packed_rounds(const PackedRounds &in, int dmax0, BuiltRounds &out, std
   const int nch = std::max(1, std::min(nwords, (nthr + k - 1) / k));
   const int chunk = ((nwords + nch - 1) / nch) * 64;
   const int ntask = k * nch;
-  std::vector<int> src(k, 0);  // a round's slot pass status (its chunk at source 0)
+  std::vector<int> src(k, 0);
   std::vector<std::string> smsg(k);
   std::vector<Chunk> ck((size_t)ntask);
   for (auto &c : ck) c.dmax = dmax0;
   const int nth = std::max(1, std::min(ntask, nthr));  // no idle team members
   if ((int)scr.tab.size() < nth) scr.tab.resize(nth);
-  if ((int)scr.bm.size() < nth) scr.bm.resize(nth);
-  if ((int)scr.rank.size() < nth) scr.rank.resize(nth);
   for (auto &t : scr.tab)
     if (!t.empty() && t.size() % n) t.clear();  // sized for another n: start over
 #pragma omp parallel num_threads(nth) if (par)
   {
-    // this thread's scratch, kept across calls in the context (tab all -1 between uses)
-    const int th = par ? omp_get_thread_num() : 0;
-    std::vector<int32_t> &tab = scr.tab[th];
+    // this thread's table, kept across calls in the context (all -1 between uses)
+    std::vector<int32_t> &tab = scr.tab[par ? omp_get_thread_num() : 0];
+#pragma omp for schedule(static)
+    for (int i = 0; i < k; i++) src[i] = build_slots(in, i, out, smsg[i]);  // presence before the chunks
 #pragma omp for schedule(dynamic, 1)
-    for (int t = 0; t < ntask; t++) {  // each chunk its own presence words, then its sources
+    for (int t = 0; t < ntask; t++) {
       const int i = t / nch, c = t % nch;
       const int s_lo = c * chunk, s_hi = std::min(n, s_lo + chunk);
-      if (in.strong_stage && s_lo < s_hi)  // the caller's staging copy of the rows, chunk by chunk
-        std::memcpy(in.strong_stage + ((size_t)i * n + s_lo) * in.W, in.strong + ((size_t)i * n + s_lo) * in.W,
-                    (size_t)(s_hi - s_lo) * in.W * 8);
-      std::string msg;
-      const int rc = build_slots(in, i, s_lo, s_hi, out, msg);
-      if (rc) {
-        src[i] = rc;
-        smsg[i] = msg;
-      } else if (s_lo < s_hi) {
-        build_chunk(in, i, s_lo, s_hi, tab, out, ck[t]);
-      }
+      if (src[i] == 0 && s_lo < s_hi) build_chunk(in, i, s_lo, s_hi, tab, out, ck[t]);
     }
 #pragma omp for schedule(static)
     for (int i = 0; i < k; i++)
-      if (src[i] == 0) merge_round(in, i, &ck[(size_t)i * nch], nch, chunk, out, scr.bm[th], scr.rank[th]);
+      if (src[i] == 0) merge_round(in, i, &ck[(size_t)i * nch], nch, chunk, out);
   }
   // errors as a sequential pass over the rounds reports them: a round's slot pass,
   // then its sources in order
