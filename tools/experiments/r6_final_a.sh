@@ -2,7 +2,7 @@
 # verified, c4-up against the general sweep, the per-call loop, the wave-split shares
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r6fa
+O=${O:-gpurun_out/r6fa}
 mkdir -p $O
 step() { local t=$1; shift; echo "[step] $*" >&2; timeout -k 10 $t "$@"; }
 step 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1

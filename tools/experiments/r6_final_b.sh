@@ -2,7 +2,7 @@
 # traffic passes of C4 and C3 (and C4 with the XCD-grouped delivery queries, DR_FUSE=31)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r6fb
+O=${O:-gpurun_out/r6fb}
 mkdir -p $O
 step() { local t=$1; shift; echo "[step] $*" >&2; timeout -k 10 $t "$@"; }
 for cfg in c4 c3 c5; do
