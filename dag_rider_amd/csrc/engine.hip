@@ -316,7 +316,7 @@ struct dr_ctx {
       batch_pin = nullptr;
       batch_pin_cap = 0;
       const size_t cap = std::max<size_t>(n, (size_t)1 << 20);
-      hipError_t e = hipHostMalloc((void **)&batch_pin, cap, hipHostMallocDefault);
+      hipError_t e = hipHostMalloc((void **)&batch_pin, cap, hipHostMallocMapped);
       if (e != hipSuccess) return e;
       batch_pin_cap = cap;
     }
@@ -4459,7 +4459,15 @@ int replay_batch_impl(dr_ctx *const *ctxs, int nctx, int nwaves, int chain_mode,
   // results: one bulk copy of the output region of the arena
   char *host = nullptr;
   HIPCHK(c0, c0->batch_host(out1 - out0, &host));
-  HIPCHK(c0, hipMemcpyAsync(host, c0->batch_arena.as<char>() + out0, out1 - out0, hipMemcpyDeviceToHost, c0->stream));
+  // (DR_BATCH_COPY=dma: the DMA engine; default: k_copy's workgroups write the pinned, device-mapped region)
+  static const bool dma = getenv("DR_BATCH_COPY") && std::strcmp(getenv("DR_BATCH_COPY"), "dma") == 0;
+  if (dma) {
+    HIPCHK(c0, hipMemcpyAsync(host, c0->batch_arena.as<char>() + out0, out1 - out0, hipMemcpyDeviceToHost, c0->stream));
+  } else {
+    const dr::CopySeg sg{reinterpret_cast<const uint8_t *>(c0->batch_arena.as<char>() + out0),
+                         reinterpret_cast<uint8_t *>(host), out1 - out0};
+    HIPCHK(c0, c0->launch_copies(&sg, 1));
+  }
   HIPCHK(c0, hipEventRecord(c0->ev[2], c0->stream));
   HIPCHK(c0, hipStreamSynchronize(c0->stream));
   const auto h2 = std::chrono::steady_clock::now();
