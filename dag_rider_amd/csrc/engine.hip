@@ -2904,16 +2904,21 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   const int nw = wk - w0 + 1;
   if (nw <= 0) return DR_OK;
   if (c->general()) return general_votes(c, w0, nw, commit, vcount);
-  HIPCHK(c, c->commit.ensure((size_t)nw));
-  HIPCHK(c, c->vcount.ensure((size_t)nw * 4));
+  // the flags and counts straight into pinned, device-mapped staging: no copy launch
+  // after the commit rule (the per-call waveReady waits on this one kernel)
+  // (one stage call: a second could sync and reuse the first's space)
+  const size_t hv_off = ((size_t)nw + 15) & ~(size_t)15;
+  void *hc = nullptr;
+  HIPCHK(c, c->stage(hv_off + (size_t)nw * 4, &hc));
+  void *hv = static_cast<char *>(hc) + hv_off;
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
-  HIPCHK(c, launch_commit(c, w0, nw, c->commit.as<uint8_t>(), c->vcount.as<int32_t>()));
+  HIPCHK(c, launch_commit(c, w0, nw, static_cast<uint8_t *>(hc), static_cast<int32_t *>(hv)));
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
-  HIPCHK(c, c->d2h(commit, c->commit.p, (size_t)nw));
-  HIPCHK(c, c->d2h(vcount, c->vcount.p, (size_t)nw * 4));
   if (pre_sync)  // launches the host queues while the commit rule runs
     if (int rc = (*pre_sync)()) return rc;
   HIPCHK(c, c->sync());
+  std::memcpy(commit, hc, (size_t)nw);
+  std::memcpy(vcount, hv, (size_t)nw * 4);
   HIPCHK(c, hipEventElapsedTime(&c->last_commit_ms, c->ev[4], c->ev[5]));
   if (ms) *ms = c->last_commit_ms;
   return DR_OK;
@@ -3609,12 +3614,17 @@ int deliver_planned(dr_ctx *c, const std::vector<Pop> &pops, uint64_t *pcount, u
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, launch_emit(c, np, 0, pd, nullptr, counts, digest, nullptr, nullptr, nullptr, 0, false,
                         plan + dr::PL_NDESC, item_pref, dr::PopDesc{}, rcnt));
+  // the per-pop totals straight into pinned, device-mapped staging (no copy launch)
+  void *ho = nullptr;
+  HIPCHK(c, c->stage((size_t)np * 16, &ho));
+  u64 *hout = static_cast<u64 *>(ho);
   hipLaunchKernelGGL((dr::k_pop_final<256>), dim3(std::max(1, std::min(64, (np + 255) / 256))), dim3(256), 0,
-                     c->stream, plan, desc_of_pop, extra_c, extra_g, counts, digest, outv, outv + np);
+                     c->stream, plan, desc_of_pop, extra_c, extra_g, counts, digest, hout, hout + np);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, c->d2h(pcount, outv, (size_t)np * 8));
-  HIPCHK(c, c->d2h(pdigest, outv + np, (size_t)np * 8));
   HIPCHK(c, c->sync());
+  std::memcpy(pcount, hout, (size_t)np * 8);
+  std::memcpy(pdigest, hout + np, (size_t)np * 8);
+  (void)outv;
   return DR_OK;
 }
 
