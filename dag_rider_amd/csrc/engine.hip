@@ -345,7 +345,7 @@ struct dr_ctx {
   struct Pending { void *dst; void *stage; const void *src; size_t n; };
   std::vector<Pending> pend;
   hipEvent_t ev_sync = nullptr, ev_sync2 = nullptr, ev_fork = nullptr, ev_join = nullptr, ev_start = nullptr,
-            ev_wu = nullptr;
+            ev_wu = nullptr, ev_commit = nullptr;  // ev_commit: system fence (commit_range's early wait)
   hipStream_t stream2 = nullptr;  // second queue: canonical cone beside the leader chains
   hipError_t launch_copies(const dr::CopySeg *sg, int k) {
     for (int i0 = 0; i0 < k; i0 += dr::kCopySegs) {
@@ -1311,7 +1311,7 @@ extern "C" int dr_create_ex(int n, int faulty, int max_rounds, int device, int f
   for (auto &ev : c->ev) (void)hipEventCreateWithFlags(&ev, hipEventReleaseToDevice);
   for (hipEvent_t *e : {&c->ev_fork, &c->ev_join, &c->ev_start, &c->ev_wu})
     (void)hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice);
-  for (hipEvent_t *e : {&c->ev_sync, &c->ev_sync2}) (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
+  for (hipEvent_t *e : {&c->ev_sync, &c->ev_sync2, &c->ev_commit}) (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
   // (+ a lane's WS rows of slack: k_chain_reg reads each lane's WS rows whole, past n
   // in the last round when WS does not divide n)
   const size_t rows = (size_t)max_rounds * n * c->WS * sizeof(u64) + (size_t)c->WS * c->WS * sizeof(u64);
@@ -1364,7 +1364,7 @@ extern "C" void dr_destroy(dr_ctx *c) {
   for (DevBuf *b : bufs) b->release();
   for (auto &ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
-  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join, c->ev_start, c->ev_wu})
+  for (hipEvent_t e : {c->ev_sync, c->ev_sync2, c->ev_fork, c->ev_join, c->ev_start, c->ev_wu, c->ev_commit})
     if (e) (void)hipEventDestroy(e);
   if (c->rg_exec) (void)hipGraphExecDestroy(c->rg_exec);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -2889,8 +2889,10 @@ namespace {
 
 // Commit decisions for waves [w0, w1] (host handles waves whose round(w,4) is
 // not mirrored: legal only when their leader is bottom).
+// pre_sync: launches queued while the commit rule runs; behind (on the same stream): the
+// host waits for the commit rule alone (ev_commit), not for them
 int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, float *ms,
-                 const std::function<int()> *pre_sync = nullptr) {
+                 const std::function<int()> *pre_sync = nullptr, const std::function<int()> *behind = nullptr) {
   if (w0 < 1 || w1 < w0) return c->fail(DR_E_INVAL, "wave range [%d,%d] invalid (waves are 1-based)", w0, w1);
   int wk = w0 - 1;  // last wave the kernel can evaluate
   while (wk + 1 <= w1 && 4 * (wk + 1) < c->nrounds) wk++;
@@ -2916,7 +2918,13 @@ int commit_range(dr_ctx *c, int w0, int w1, uint8_t *commit, int32_t *vcount, fl
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
   if (pre_sync)  // launches the host queues while the commit rule runs
     if (int rc = (*pre_sync)()) return rc;
-  HIPCHK(c, c->sync());
+  if (behind && c->pend.empty() && c->h2q.empty()) {
+    HIPCHK(c, hipEventRecord(c->ev_commit, c->stream));
+    if (int rc = (*behind)()) return rc;
+    HIPCHK(c, dr_ctx::wait_event(c->ev_commit));
+  } else {
+    HIPCHK(c, c->sync());
+  }
   std::memcpy(commit, hc, (size_t)nw);
   std::memcpy(vcount, hv, (size_t)nw * 4);
   HIPCHK(c, hipEventElapsedTime(&c->last_commit_ms, c->ev[4], c->ev[5]));
@@ -3357,7 +3365,17 @@ extern "C" int dr_wave_ready(dr_ctx *c, int wave, int decided_wave, uint8_t *com
       (void)hipStreamWaitEvent(c->stream, c->ev_join, 0);
     }
   } join{c};
-  if (int rc = commit_range(c, wave, wave, commit, vcount, nullptr, spec ? &fork : nullptr)) return rc;
+  // DR_OPT_CALL_OVERLAP 1, when no leader chain can follow (the previous wave is decided):
+  // the canonical cone goes in behind the commit rule before it is known whether the wave
+  // commits -- its launches overlap the commit rule, and the host waits for the rule alone
+  const bool behind = c->call_overlap == 1 && decided_wave >= wave - 1 && c->ref_seen && c->memo_on() &&
+                      c->nrounds >= 2 && !c->canon_ok;
+  std::function<int()> canon_behind = [c]() -> int { return launch_canon(c, false, nullptr, false, true); };
+  if (behind)
+    if (int rc = ensure_summary_bufs(c)) return rc;
+  if (int rc = commit_range(c, wave, wave, commit, vcount, nullptr, spec ? &fork : nullptr,
+                            behind ? &canon_behind : nullptr))
+    return rc;
   if (!*commit) return DR_OK;
   std::vector<std::vector<int32_t>> pushes(1);
   if (c->general()) {

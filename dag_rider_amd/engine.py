@@ -118,8 +118,9 @@ class Engine:
 
     def set_call_overlap(self, mode: int):
         """DR_OPT_CALL_OVERLAP: after a REF orderVertices, waveReady launches the canonical cone of
-        the new top once it knows of a commit (1, the default) or on a second stream beside the
-        commit rule (2); 0 = orderVertices computes it.  Identical results."""
+        the new top without waiting for it (1, the default: behind the commit rule when no leader
+        chain can follow, else once it knows of a commit; 2: on a second stream beside the commit
+        rule); 0 = orderVertices computes it.  Identical results."""
         self._check(self._L.dr_set_option(self._h, L.DR_OPT_CALL_OVERLAP, int(mode)))
 
     def set_batch_form(self, form: int):

@@ -133,9 +133,11 @@ int dr_wave_leader(const dr_ctx *ctx, int wave);
  * grouped by XCD (adjacent waves on one L2); + 16 = the delivery sweeps stop at the first
  * round whose state equals the canonical cone's (n > 512).  Identical results.
  * DR_OPT_CALL_OVERLAP (default 1): once the context answered a DR_DELIVER_REF
- * dr_order_vertices, dr_wave_ready computes the canonical cone of the new top round on a
- * second stream beside the commit rule (the next REF dr_order_vertices merges with it);
- * 0 = dr_order_vertices computes it.  Identical results. */
+ * dr_order_vertices, dr_wave_ready launches the canonical cone of the new top round (what
+ * the next REF dr_order_vertices merges with) without waiting for it: 1 = behind the
+ * commit rule on the context's stream when no leader chain can follow (decided_wave >=
+ * wave - 1), else after the wave's commit is known; 2 = on a second stream beside the
+ * commit rule; 0 = dr_order_vertices computes it.  Identical results. */
 int dr_set_option(dr_ctx *ctx, int option, int value);
 /* The form of the context's last dr_replay: 1 = a captured graph was launched,
  * 0 = kernels launched one by one, -1 = one by one after a failed capture
