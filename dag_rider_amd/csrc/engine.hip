@@ -353,7 +353,10 @@ struct dr_ctx {
       const int m = std::min(dr::kCopySegs, k - i0);
       uint64_t mx = 1;
       for (int i = 0; i < m; i++) { L.s[i] = sg[i0 + i]; mx = std::max<uint64_t>(mx, sg[i0 + i].n); }
-      const unsigned bx = (unsigned)std::min<uint64_t>(256, (mx + 4095) / 4096);
+      // bytes per workgroup (DR_COPY_BLK, measurement only: 512-4096 B moved nothing on the
+      // per-call loop, profiles/r06/cb_loop_*.json)
+      static const uint64_t blk = getenv("DR_COPY_BLK") ? std::max(256, atoi(getenv("DR_COPY_BLK"))) : 4096;
+      const unsigned bx = (unsigned)std::min<uint64_t>(256, (mx + blk - 1) / blk);
       hipLaunchKernelGGL(dr::k_copy, dim3(bx, m), dim3(256), 0, stream, L);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
